@@ -1,0 +1,124 @@
+/*
+ * mums.h -- C ABI of the MI355X-native multi-MUM seed finder (libmums_hip.so).
+ *
+ * This is the drop-in boundary for libMems' MemHash / MaskedMemHash hot path
+ * (koadman/libMems 1.6.1).  Each entry point names the reference interface it
+ * replaces (paths relative to /root/reference/libMems/).  Plain pointers and
+ * sizes only; no C++ exceptions cross this boundary: every call returns a
+ * status code (MUMS_OK == 0) and mums_last_error() carries the message that
+ * the reference would have thrown or printed.
+ *
+ * Threading (MemHash.h:38, Aligner.h:198 TLS<MemHash>): a context is used by
+ * one host thread at a time; distinct contexts are independent and may be
+ * used concurrently from different host threads.
+ *
+ * Coordinates (AbstractMatch.h:27, MemHash.cpp:176-177): match starts are
+ * 1-based, signed (negative = reverse complement relative to the first
+ * present genome), 0 = NO_MATCH.  Result order is the reference's
+ * bucket-major MatchList order (MemHash.h:182-203).
+ */
+#ifndef MUMS_H
+#define MUMS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MUMS_ABI_VERSION 1
+
+enum mums_status {
+    MUMS_OK = 0,
+    MUMS_E_INVALID = -1,      /* bad argument / inconsistent state (gnException InvalidData)        */
+    MUMS_E_NOMEM = -2,        /* device allocation failed                                           */
+    MUMS_E_HIP = -3,          /* HIP runtime error                                                  */
+    MUMS_E_GAP = -4,          /* '-' in a genome: SortedMerList.cpp:433-437 throws "Gap in genome"  */
+    MUMS_E_UNSUPPORTED = -5,  /* a feature outside the implemented scope (see mums_last_error)      */
+    MUMS_E_NODEVICE = -6      /* no HIP device: the product path never falls back to the CPU        */
+};
+
+/* Run stages for mums_find_stage(). */
+enum mums_stage {
+    MUMS_STAGE_SEEDS = 1,     /* pack + keys + sort + merge/accept + probe build ("sorted+matched") */
+    MUMS_STAGE_ALL = 2        /* + extension, bucket replay, MatchList materialisation (FindMatches)*/
+};
+
+typedef struct mums_ctx mums_ctx;
+
+typedef struct mums_stats {
+    uint64_t seedmers;          /* N = sum over genomes of SMLLength (SortedMerList.cpp:288-295)     */
+    uint64_t groups;            /* distinct masked keys                                               */
+    uint64_t probes;            /* accepted seed probes handed to AddHashEntry                        */
+    uint64_t mem_count;         /* MemHash::MemCount()  (MemHash.h:94)                                */
+    uint64_t collision_count;   /* MemHash::MemCollisionCount() (MemHash.h:97)                        */
+    uint64_t repeat_limit_groups; /* groups larger than MER_REPEAT_LIMIT (MatchFinder.cpp:166)        */
+    uint64_t nonempty_buckets;  /* hash buckets holding >= 1 entry                                    */
+    double   ms_keys;           /* device time per phase of the last run (HIP events)                 */
+    double   ms_sort;
+    double   ms_groups;
+    double   ms_buckets;
+    double   ms_replay;
+    double   ms_output;
+    double   ms_total;
+} mums_stats;
+
+/* MemHash::MemHash (MemHash.cpp:33-49); device = HIP ordinal. */
+int  mums_ctx_create(int device, mums_ctx** out);
+/* MemHash::~MemHash */
+int  mums_ctx_destroy(mums_ctx* ctx);
+/* Optional: run on a caller-provided hipStream_t (default: a private stream). */
+int  mums_set_stream(mums_ctx* ctx, void* hip_stream);
+
+/* Seed pattern (SeedMasks.h getSeed, SortedMerList::Create seed argument,
+ * SortedMerList.cpp:786-824).  0 = choose getDefaultSeedWeight() from the
+ * mean genome length at find time (MatchList.h:351-357). */
+int  mums_set_seed(mums_ctx* ctx, uint64_t pattern);
+/* MemHash::SetRepeatTolerance / SetEnumerationTolerance (MemHash.h:125-144)
+ * and MemHash::SetTableSize (MemHash.cpp:95-102). */
+int  mums_set_params(mums_ctx* ctx, uint32_t repeat_tol, uint32_t enum_tol, uint32_t table_size);
+/* MaskedMemHash (MaskedMemHash.h:25-40): masked=1 selects MaskedMemHash::HashMatch
+ * semantics; seq_mask = MaskedMemHash::SetMask (genome 0 = most significant bit). */
+int  mums_set_mask(mums_ctx* ctx, int masked, uint64_t seq_mask);
+
+/* MatchFinder::AddSequence (MatchFinder.cpp:59-87) for a host ASCII genome
+ * (copied to HBM).  Genome ids are assigned in call order. */
+int  mums_add_genome(mums_ctx* ctx, const char* ascii, uint64_t n);
+/* Same for a device-resident ASCII genome (not copied; must outlive the find). */
+int  mums_add_genome_device(mums_ctx* ctx, const void* d_ascii, uint64_t n);
+/* MemHash::Clear / ClearSequences (MemHash.cpp:80-93): drops genomes and results. */
+int  mums_clear(mums_ctx* ctx);
+
+/* MemHash::FindMatches(MatchList&) (MemHash.cpp:109-115) / CreateMatches (:104-107). */
+int  mums_find(mums_ctx* ctx);
+/* Run only up to a stage (benchmarks); MUMS_STAGE_ALL == mums_find. */
+int  mums_find_stage(mums_ctx* ctx, int stage);
+
+/* MemHash::GetMatchList (MemHash.h:182-203): number of matches and genomes. */
+int  mums_result_count(mums_ctx* ctx, uint64_t* count, uint32_t* seq_count);
+/* lengths[count]; starts[count * seq_count] row-major (match-major). */
+int  mums_result_copy(mums_ctx* ctx, uint64_t* lengths, int64_t* starts);
+
+/* MemCount / MemCollisionCount (MemHash.h:94-97) + per-phase device timings. */
+int  mums_get_stats(mums_ctx* ctx, mums_stats* out);
+/* Message of the last failing call on this context ("" if none). */
+const char* mums_last_error(mums_ctx* ctx);
+
+/* ---- row A1-A5 helpers (seed table, keys, SortedMerList) ------------------ */
+/* getSeed(weight, rank) (SeedMasks.h:298-321); SOLID_SEED == INT32_MAX. */
+int64_t  mums_get_seed(int weight, int seed_rank);
+/* getDefaultSeedWeight (SeedMasks.h:389-401). */
+uint32_t mums_default_seed_weight(uint64_t avg_len);
+/* GetDnaSeedMer for every position of genome g after mums_find_stage(>=SEEDS):
+ * out[p] = canonical key (SortedMerList.cpp:764-769, 64-bit left-aligned form). */
+int  mums_copy_seed_keys(mums_ctx* ctx, uint32_t genome, uint64_t* out, uint64_t cap);
+/* MemorySML::Create (MemorySML.cpp:45-60): SML positions of genome g sorted by
+ * full key, ties by ascending position. */
+int  mums_build_sml(mums_ctx* ctx, uint32_t genome, uint32_t* positions, uint64_t cap);
+
+int  mums_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MUMS_H */

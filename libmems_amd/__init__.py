@@ -1,0 +1,310 @@
+"""libmems_amd -- MI355X-native multi-MUM seed finder (libMems MemHash hot path).
+
+Python mirror of the reference's MemHash / MaskedMemHash interface
+(koadman/libMems 1.6.1, libMems/MemHash.h:38-175, MaskedMemHash.h:25-40) over
+the C ABI in include/mums.h (libmums_hip.so, built in-tree by `make -C
+libmems_amd`).  All compute runs in hand-written HIP kernels for gfx950; there
+is no CPU fallback: if the shared library or a HIP device is missing, the
+calls raise instead of computing anything on the host.
+
+Method names follow the reference (AddSequence, FindMatches, GetMatchList,
+SetRepeatTolerance, SetEnumerationTolerance, SetTableSize, MemCount,
+MemCollisionCount, Clear, SetMask) so parity tests read like the reference's
+usage in Aligner.cpp:1181-1207.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmums_hip.so")
+
+MUMS_OK = 0
+MUMS_E_INVALID = -1
+MUMS_E_NOMEM = -2
+MUMS_E_HIP = -3
+MUMS_E_GAP = -4
+MUMS_E_UNSUPPORTED = -5
+MUMS_E_NODEVICE = -6
+
+STAGE_SEEDS = 1
+STAGE_ALL = 2
+
+DEFAULT_MEM_TABLE_SIZE = 40000       # MemHash.h:30
+DEFAULT_REPEAT_TOLERANCE = 0         # MemHash.h:31
+DEFAULT_ENUMERATION_TOLERANCE = 1    # MemHash.h:32
+SOLID_SEED = 2147483647              # SeedMasks.h:263
+
+
+class MumsError(RuntimeError):
+    """A non-zero status from the C ABI (the reference would have thrown)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"mums error {code}: {msg}")
+        self.code = code
+
+
+class GapInSequence(MumsError):
+    """SortedMerList.cpp:433-437 throws "Gap in genome sequence"."""
+
+
+class _Stats(ctypes.Structure):
+    _fields_ = [
+        ("seedmers", ctypes.c_uint64),
+        ("groups", ctypes.c_uint64),
+        ("probes", ctypes.c_uint64),
+        ("mem_count", ctypes.c_uint64),
+        ("collision_count", ctypes.c_uint64),
+        ("repeat_limit_groups", ctypes.c_uint64),
+        ("nonempty_buckets", ctypes.c_uint64),
+        ("ms_keys", ctypes.c_double),
+        ("ms_sort", ctypes.c_double),
+        ("ms_groups", ctypes.c_double),
+        ("ms_buckets", ctypes.c_double),
+        ("ms_replay", ctypes.c_double),
+        ("ms_output", ctypes.c_double),
+        ("ms_total", ctypes.c_double),
+    ]
+
+
+EXPORTED_SYMBOLS = [
+    "mums_abi_version", "mums_ctx_create", "mums_ctx_destroy", "mums_set_stream", "mums_set_seed",
+    "mums_set_params", "mums_set_mask", "mums_add_genome", "mums_add_genome_device", "mums_clear",
+    "mums_find", "mums_find_stage", "mums_result_count", "mums_result_copy", "mums_get_stats",
+    "mums_last_error", "mums_get_seed", "mums_default_seed_weight", "mums_copy_seed_keys",
+    "mums_build_sml",
+]
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libmums_hip.so (raises if it was not built: no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(f"{path} not built: run `make -C {_HERE}` (hipcc --offload-arch=gfx950)")
+    lib = ctypes.CDLL(path)
+    vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    lib.mums_abi_version.restype = i32
+    lib.mums_ctx_create.argtypes = [i32, ctypes.POINTER(vp)]
+    lib.mums_ctx_destroy.argtypes = [vp]
+    lib.mums_set_stream.argtypes = [vp, vp]
+    lib.mums_set_seed.argtypes = [vp, u64]
+    lib.mums_set_params.argtypes = [vp, u32, u32, u32]
+    lib.mums_set_mask.argtypes = [vp, i32, u64]
+    lib.mums_add_genome.argtypes = [vp, ctypes.c_char_p, u64]
+    lib.mums_add_genome_device.argtypes = [vp, vp, u64]
+    lib.mums_clear.argtypes = [vp]
+    lib.mums_find.argtypes = [vp]
+    lib.mums_find_stage.argtypes = [vp, i32]
+    lib.mums_result_count.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u32)]
+    lib.mums_result_copy.argtypes = [vp, vp, vp]
+    lib.mums_get_stats.argtypes = [vp, ctypes.POINTER(_Stats)]
+    lib.mums_last_error.argtypes = [vp]
+    lib.mums_last_error.restype = ctypes.c_char_p
+    lib.mums_get_seed.argtypes = [i32, i32]
+    lib.mums_get_seed.restype = ctypes.c_int64
+    lib.mums_default_seed_weight.argtypes = [u64]
+    lib.mums_default_seed_weight.restype = u32
+    lib.mums_copy_seed_keys.argtypes = [vp, u32, vp, u64]
+    lib.mums_build_sml.argtypes = [vp, u32, vp, u64]
+    _lib = lib
+    return lib
+
+
+def getSeed(weight: int, seed_rank: int = 0) -> int:
+    """SeedMasks.h:298-321."""
+    return int(load_library().mums_get_seed(weight, seed_rank)) & 0xFFFFFFFFFFFFFFFF
+
+
+def getSeedLength(seed: int) -> int:
+    """SeedMasks.h:335-350."""
+    if seed == 0:
+        return 0
+    s = seed & 0xFFFFFFFFFFFFFFFF
+    lo = (s & -s).bit_length() - 1
+    return s.bit_length() - lo
+
+
+def getSeedWeight(seed: int) -> int:
+    """SeedMasks.h:363-373."""
+    return bin(seed & 0xFFFFFFFFFFFFFFFF).count("1")
+
+
+def getDefaultSeedWeight(avg_len: int) -> int:
+    """SeedMasks.h:389-401."""
+    return int(load_library().mums_default_seed_weight(avg_len))
+
+
+@dataclass
+class MatchList:
+    """GetMatchList output (MemHash.h:182-203): lengths[M], starts[M, G] (1-based, signed, 0 = NO_MATCH)."""
+
+    lengths: np.ndarray
+    starts: np.ndarray
+
+    def __len__(self) -> int:
+        return int(self.lengths.shape[0])
+
+    def text(self) -> str:
+        """`len\\ts0\\t...` per match (UngappedLocalAlignment.h:200-206)."""
+        if len(self) == 0:
+            return ""
+        cols = [self.lengths.astype(np.int64)[:, None], self.starts]
+        arr = np.concatenate(cols, axis=1)
+        return "".join("\t".join(map(str, row)) + "\n" for row in arr.tolist())
+
+
+class MemHash:
+    """MemHash (MemHash.h:38) on one MI355X; genomes are added in order as in AddSequence."""
+
+    _masked = 0
+
+    def __init__(self, device: int = 0):
+        self._lib = load_library()
+        self._ctx = ctypes.c_void_p()
+        rc = self._lib.mums_ctx_create(device, ctypes.byref(self._ctx))
+        if rc != MUMS_OK:
+            raise MumsError(rc, "mums_ctx_create failed (no HIP device? the GPU path has no CPU fallback)")
+        self._seq_mask = 0
+        self._keepalive: List[object] = []
+        self.SetTableSize(DEFAULT_MEM_TABLE_SIZE)
+        self._rt = DEFAULT_REPEAT_TOLERANCE
+        self._et = DEFAULT_ENUMERATION_TOLERANCE
+        self._ts = DEFAULT_MEM_TABLE_SIZE
+        self._lib.mums_set_mask(self._ctx, self._masked, 0)
+
+    # ---- lifetime ------------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_ctx", None) and self._ctx.value:
+            self._lib.mums_ctx_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc: int) -> None:
+        if rc != MUMS_OK:
+            msg = self._lib.mums_last_error(self._ctx).decode(errors="replace")
+            if rc == MUMS_E_GAP:
+                raise GapInSequence(rc, msg)
+            raise MumsError(rc, msg)
+
+    # ---- configuration (MemHash.h:72, 125-144; MaskedMemHash.h:32) ------------
+    def SetTableSize(self, n: int) -> None:
+        self._ts = n
+        self._check(self._lib.mums_set_params(self._ctx, getattr(self, "_rt", 0), getattr(self, "_et", 1), n))
+
+    def SetRepeatTolerance(self, t: int) -> None:
+        self._rt = t
+        self._check(self._lib.mums_set_params(self._ctx, t, self._et, self._ts))
+
+    def SetEnumerationTolerance(self, t: int) -> None:
+        self._et = t
+        self._check(self._lib.mums_set_params(self._ctx, self._rt, t, self._ts))
+
+    def SetSeed(self, pattern: int) -> None:
+        """Seed pattern the SortedMerLists are built with (0 = default weight for the genome lengths)."""
+        self._check(self._lib.mums_set_seed(self._ctx, pattern))
+
+    # ---- input -------------------------------------------------------------------
+    def AddSequence(self, seq) -> None:
+        """MatchFinder::AddSequence (MatchFinder.cpp:59-87).  `seq` is bytes/str (host) or a
+        torch uint8 CUDA tensor (device-resident, not copied)."""
+        if hasattr(seq, "data_ptr") and getattr(seq, "is_cuda", False):
+            self._keepalive.append(seq)
+            self._check(self._lib.mums_add_genome_device(self._ctx, ctypes.c_void_p(seq.data_ptr()), seq.numel()))
+            return
+        if isinstance(seq, str):
+            seq = seq.encode()
+        b = bytes(seq)
+        self._check(self._lib.mums_add_genome(self._ctx, b, len(b)))
+
+    def Clear(self) -> None:
+        """MemHash::Clear (MemHash.cpp:80-93)."""
+        self._keepalive.clear()
+        self._check(self._lib.mums_clear(self._ctx))
+
+    ClearSequences = Clear
+
+    # ---- compute -----------------------------------------------------------------
+    def FindMatches(self, sequences: Optional[Sequence] = None) -> MatchList:
+        """MemHash::FindMatches (MemHash.cpp:109-115): optionally AddSequence each, then find."""
+        if sequences is not None:
+            for s in sequences:
+                self.AddSequence(s)
+        self._check(self._lib.mums_find(self._ctx))
+        return self.GetMatchList()
+
+    def CreateMatches(self) -> bool:
+        """MemHash::CreateMatches (MemHash.cpp:104-107)."""
+        self._check(self._lib.mums_find(self._ctx))
+        return True
+
+    def FindStage(self, stage: int) -> None:
+        self._check(self._lib.mums_find_stage(self._ctx, stage))
+
+    def GetMatchList(self) -> MatchList:
+        cnt = ctypes.c_uint64()
+        g = ctypes.c_uint32()
+        self._check(self._lib.mums_result_count(self._ctx, ctypes.byref(cnt), ctypes.byref(g)))
+        lengths = np.zeros(cnt.value, dtype=np.uint64)
+        starts = np.zeros((cnt.value, g.value), dtype=np.int64)
+        if cnt.value:
+            self._check(self._lib.mums_result_copy(self._ctx, lengths.ctypes.data, starts.ctypes.data))
+        return MatchList(lengths, starts)
+
+    # ---- metrics (MemHash.h:94-105) -------------------------------------------------
+    def stats(self) -> dict:
+        s = _Stats()
+        self._check(self._lib.mums_get_stats(self._ctx, ctypes.byref(s)))
+        return {name: getattr(s, name) for name, _ in _Stats._fields_}
+
+    def MemCount(self) -> int:
+        return int(self.stats()["mem_count"])
+
+    def MemCollisionCount(self) -> int:
+        return int(self.stats()["collision_count"])
+
+    # ---- SortedMerList helpers (rows A3-A5) ------------------------------------------
+    def SeedKeys(self, genome: int, m: int) -> np.ndarray:
+        out = np.zeros(max(m, 1), dtype=np.uint64)
+        self._check(self._lib.mums_copy_seed_keys(self._ctx, genome, out.ctypes.data, m))
+        return out[:m]
+
+    def SortedMerList(self, genome: int, m: int) -> np.ndarray:
+        out = np.zeros(max(m, 1), dtype=np.uint32)
+        self._check(self._lib.mums_build_sml(self._ctx, genome, out.ctypes.data, m))
+        return out[:m]
+
+
+class MaskedMemHash(MemHash):
+    """MaskedMemHash (MaskedMemHash.h:25-40): hash only seeds whose genome-presence bitmap equals the mask."""
+
+    _masked = 1
+
+    def SetMask(self, seq_mask: int) -> None:
+        self._seq_mask = seq_mask
+        self._check(self._lib.mums_set_mask(self._ctx, 1, seq_mask))
+
+
+__all__ = [
+    "MemHash", "MaskedMemHash", "MatchList", "MumsError", "GapInSequence", "getSeed", "getSeedLength",
+    "getSeedWeight", "getDefaultSeedWeight", "load_library", "EXPORTED_SYMBOLS", "STAGE_SEEDS", "STAGE_ALL",
+]

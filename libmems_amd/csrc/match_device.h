@@ -1,0 +1,204 @@
+// match_device.h -- MatchHashEntry arithmetic on gfx950 registers (rows A8-A10).
+//
+// A match lives in registers as {len, offset, mersize, s[MG]} with MG a
+// compile-time bound (all loops fully unrolled: no runtime-indexed register
+// arrays, which would spill to scratch).  Genomes G..MG-1 hold 0 (NO_MATCH),
+// which is neutral for every function below.
+#pragma once
+
+#include "mums_internal.h"
+
+namespace mums {
+
+template <int MG>
+struct Mhe {
+    int64_t len;
+    int64_t offset;
+    int64_t mersize;  // L for probes (MemHash.cpp:172), 0 for stored entries (MatchHashEntry.cpp:122)
+    int64_t s[MG];    // signed 1-based starts, 0 = NO_MATCH
+};
+
+// FirstStart (HybridAbstractMatch.h:121-129)
+template <int MG>
+__device__ __forceinline__ int first_start(const Mhe<MG>& m) {
+    int f = MG;
+    #pragma unroll
+    for (int g = MG - 1; g >= 0; --g) f = (m.s[g] != 0) ? g : f;
+    return f;
+}
+
+template <int MG>
+__device__ __forceinline__ int64_t start_at(const Mhe<MG>& m, int i) {
+    int64_t v = 0;
+    #pragma unroll
+    for (int g = 0; g < MG; ++g) v = (g == i) ? m.s[g] : v;
+    return v;
+}
+
+// Contains: does a contain b (MatchHashEntry.cpp:164-200)
+template <int MG>
+__device__ __forceinline__ bool mhe_contains(const Mhe<MG>& a, const Mhe<MG>& b) {
+    if (a.offset != b.offset) return false;
+    const int i = first_start(b);
+    const int64_t ai = start_at(a, i), bi = start_at(b, i);
+    if (ai == 0) return false;
+    const int64_t diff = bi - ai;
+    if (diff < 0 || (uint64_t)a.len < (uint64_t)(b.len + diff)) return false;
+    const int64_t diff_rc = b.len - a.len + diff;
+    bool ok = true;
+    #pragma unroll
+    for (int g = 0; g < MG; ++g) {
+        if (g <= i) continue;
+        const int64_t di = b.s[g] - a.s[g];
+        if (b.s[g] == 0 && a.s[g] == 0) continue;
+        if (b.s[g] < 0 && diff_rc == di) continue;
+        if (diff != di) ok = false;
+    }
+    return ok;
+}
+
+// strict_start_lessthan_ptr (MatchHashEntry.cpp:48-69)
+template <int MG>
+__device__ __forceinline__ bool mhe_strict_lt(const Mhe<MG>& a, const Mhe<MG>& b) {
+    const int start_diff = first_start(a) - first_start(b);
+    if (start_diff == 0) {
+        int res = -1;  // -1 undecided, 0 false, 1 true
+        #pragma unroll
+        for (int g = 0; g < MG; ++g) {
+            int64_t as = a.s[g], bs = b.s[g];
+            if (as < 0) as = -as + a.len - a.mersize;
+            if (bs < 0) bs = -bs + b.len - b.mersize;
+            const int64_t d = as - bs;
+            if (res < 0 && d != 0) res = d < 0 ? 1 : 0;
+        }
+        if (res >= 0) return res == 1;
+    }
+    return start_diff < 0;
+}
+
+// MheCompare (MatchHashEntry.h:121-143)
+template <int MG>
+__device__ __forceinline__ bool mhe_less(const Mhe<MG>& a, const Mhe<MG>& b) {
+    const int fa = first_start(a), fb = first_start(b);
+    if (fa > fb) return true;
+    if (fa != fb) return false;
+    int res = -1;
+    #pragma unroll
+    for (int g = 0; g < MG; ++g) {
+        const bool az = a.s[g] == 0, bz = b.s[g] == 0;
+        if (res < 0 && az && !bz) res = 1;
+        if (res < 0 && !az && bz) res = 0;
+    }
+    if (res >= 0) return res == 1;
+    if (mhe_contains(a, b) || mhe_contains(b, a)) return false;
+    return mhe_strict_lt(a, b);
+}
+
+// stored entry layout in the pool: int64 [len, offset, s_0 .. s_{G-1}]
+template <int MG>
+__device__ __forceinline__ void load_entry(const int64_t* __restrict__ pool, uint32_t id, int G, Mhe<MG>& e) {
+    const int64_t* p = pool + (uint64_t)id * (uint64_t)(G + 2);
+    e.len = p[0];
+    e.offset = p[1];
+    e.mersize = 0;
+    #pragma unroll
+    for (int g = 0; g < MG; ++g) e.s[g] = (g < G) ? p[2 + g] : 0;
+}
+
+// std::lower_bound over table ids[0..t) (libstdc++: half = len >> 1, middle = first + half)
+template <int MG>
+__device__ __forceinline__ uint32_t lower_bound_tbl(const uint32_t* tbl, uint32_t t, const int64_t* __restrict__ pool,
+                                                   int G, const Mhe<MG>& val) {
+    uint32_t first = 0, len = t;
+    Mhe<MG> e;
+    while (len > 0) {
+        const uint32_t half = len >> 1, mid = first + half;
+        load_entry(pool, tbl[mid], G, e);
+        if (mhe_less(e, val)) {
+            first = mid + 1;
+            len = len - half - 1;
+        } else {
+            len = half;
+        }
+    }
+    return first;
+}
+
+// Build the seed probe of a masked-key group whose first sorted record is h.
+// MemHash::EnumerateMatches (MemHash.cpp:139-162) acceptance with enum_tol == 1,
+// HashMatch (:167-187) / MaskedMemHash::HashMatch (MaskedMemHash.cpp:38-63),
+// SetDirection (:189-203), CalculateOffset (MatchHashEntry.cpp:141-160).
+// Returns false when the group yields no AddHashEntry call.
+// *gsize receives the group size (counted up to kRepeatLimit + 1).
+template <int MG, typename K>
+__device__ __forceinline__ bool build_probe(const K* __restrict__ skey, const uint32_t* __restrict__ sidx, uint64_t N,
+                                            uint64_t h, const GenomeTable& gt, const MatchParams& mp, int L,
+                                            Mhe<MG>& P, uint32_t* gsize) {
+    const K v0 = skey[h] >> 1;
+    const uint32_t maxc = (uint32_t)gt.G * (mp.repeat_tol + 1u);
+    uint32_t tally[MG];
+    int64_t pos1[MG];
+    uint32_t par[MG];
+    #pragma unroll
+    for (int g = 0; g < MG; ++g) { tally[g] = 0; pos1[g] = 0; par[g] = 0; }
+    uint32_t cnt = 0, nh = 0;
+    bool reject = false;
+    for (uint64_t i = h; i < N; ++i) {
+        const K k = skey[i];
+        if ((k >> 1) != v0) break;
+        ++cnt;
+        if (cnt > maxc) {
+            // some genome exceeds repeat_tol+1 occurrences: rejected.  Keep
+            // counting only to report groups above MER_REPEAT_LIMIT.
+            reject = true;
+            if (cnt > (uint32_t)kRepeatLimit) break;
+            continue;
+        }
+        if (reject) continue;
+        const uint64_t gi = sidx[i];
+        const int g = genome_of(gt, gi);
+        const int64_t p = (int64_t)(gi - gt.base[g]);
+        #pragma unroll
+        for (int q = 0; q < MG; ++q) {
+            if (q != g) continue;
+            if (tally[q] < mp.enum_tol) { pos1[q] = p + 1; par[q] = (uint32_t)(k & 1); ++nh; }
+            if (tally[q] > mp.repeat_tol) reject = true;
+            ++tally[q];
+        }
+    }
+    *gsize = cnt;
+    if (reject || cnt < 2 || nh < 2) return false;
+    P.len = L;
+    P.mersize = L;
+    #pragma unroll
+    for (int g = 0; g < MG; ++g) P.s[g] = pos1[g];
+    const int ref = first_start(P);
+    uint32_t ref_par = 0;
+    #pragma unroll
+    for (int g = 0; g < MG; ++g) ref_par = (g == ref) ? par[g] : ref_par;
+    #pragma unroll
+    for (int g = 0; g < MG; ++g)
+        if (g > ref && P.s[g] != 0 && par[g] != ref_par) P.s[g] = -P.s[g];
+    const int64_t sref = start_at(P, ref);
+    int64_t off = 0;
+    uint64_t match_number = 0;
+    int mult = 0;
+    #pragma unroll
+    for (int g = 0; g < MG; ++g) {
+        if (g > ref && P.s[g] != 0) off += P.s[g] - sref - (P.s[g] < 0 ? (int64_t)L : 0);
+        if (g < gt.G) {
+            match_number = (match_number << 1) | (P.s[g] != 0 ? 1ull : 0ull);
+            mult += P.s[g] != 0;
+        }
+    }
+    P.offset = off;
+    if (mp.masked) return mp.seq_mask == 0 || match_number == mp.seq_mask;
+    return mult >= 2;
+}
+
+__device__ __forceinline__ uint32_t bucket_of(int64_t offset, uint32_t table_size) {
+    const int64_t T = (int64_t)table_size;
+    return (uint32_t)(((offset % T) + T) % T);  // MemHash.cpp:213
+}
+
+}  // namespace mums

@@ -1,0 +1,526 @@
+// mums_capi.hip -- C ABI (include/mums.h) over the gfx950 multi-MUM pipeline.
+//
+// One context = one MemHash instance (MemHash.h:38).  mums_find runs, on the
+// context's HIP stream:
+//   keys     seed_keys_kernel            ASCII -> ckey[N]             (A2-A4)
+//   sort     radix_sort<K>               (ckey, idx) stable, 2w+1 bits  (A5-A7)
+//   groups   probe_pass x2 + scan        accepted probes in key order (A8-A9)
+//   buckets  radix_sort<u32> on bucket   probes grouped per bucket    (A10)
+//   replay   replay_kernel               AddHashEntry + ExtendMatch   (A10-A11)
+//   output   scan + emit_kernel          bucket-major MatchList       (A12)
+// There is no CPU fallback: without a HIP device every call that would compute
+// returns MUMS_E_NODEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mums.h"
+#include "mums_internal.h"
+
+using namespace mums;
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
+        size_t want = bytes + (bytes >> 4) + 4096;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        else p = nullptr;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <typename T> T* as() const { return (T*)p; }
+};
+
+struct GenomeIn {
+    const char* d_ptr;
+    uint64_t n;
+    bool owned;
+};
+
+enum { EV_START, EV_KEYS, EV_SORT, EV_GROUPS, EV_BUCKETS, EV_REPLAY, EV_OUTPUT, EV_COUNT };
+
+}  // namespace
+
+struct mums_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    uint64_t seed = 0;
+    uint32_t repeat_tol = 0, enum_tol = 1, table_size = 40000;
+    int masked = 0;
+    uint64_t seq_mask = 0;
+    std::vector<GenomeIn> genomes;
+    std::string err;
+
+    DevBuf ckey, kA, kB, vA, vB, tmp, partials, counters;
+    DevBuf bstart, bend, tsize, obase, pool, tbl, out_len, out_s;
+    hipEvent_t ev[EV_COUNT] = {};
+
+    // state of the last run
+    int stage_done = 0;
+    bool key64 = false;
+    int L = 0, w = 0;
+    uint64_t pattern = 0, N = 0, P = 0, M = 0;
+    int sorted_buf = 0;
+    GenomeTable gt{};
+    DevCounters hc{};
+    mums_stats st{};
+    const uint32_t* sorted_heads = nullptr;
+    const uint32_t* sorted_buckets = nullptr;
+};
+
+namespace {
+
+int fail(mums_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+int hipfail(mums_ctx* c, hipError_t e, const char* where) {
+    return fail(c, e == hipErrorOutOfMemory ? MUMS_E_NOMEM : MUMS_E_HIP,
+                std::string(where) + ": " + hipGetErrorString(e));
+}
+
+#define HIPCHK(expr)                                               \
+    do {                                                           \
+        hipError_t e_ = (expr);                                    \
+        if (e_ != hipSuccess) return hipfail(ctx, e_, #expr);      \
+    } while (0)
+
+bool have_device() {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess && n > 0;
+}
+
+SeedSpec make_seed_spec(uint64_t pattern, int L, int w) {
+    SeedSpec ss{};
+    ss.pattern = pattern;
+    ss.L = L;
+    ss.w = w;
+    int cum = 0, r = -1;
+    bool prev = false;
+    for (int k = 0; k < L; ++k) {
+        const bool care = (pattern >> (L - 1 - k)) & 1;
+        if (care) {
+            if (!prev) {
+                ++r;
+                ss.run_start[r] = k;
+                ss.run_len[r] = 0;
+            }
+            ss.run_len[r]++;
+        }
+        prev = care;
+    }
+    ss.nruns = r + 1;
+    for (int i = 0; i < ss.nruns; ++i) {
+        cum += ss.run_len[i];
+        ss.run_dst[i] = 2 * (w - cum);
+    }
+    return ss;
+}
+
+int seed_len(uint64_t s) {
+    if (!s) return 0;
+    int lo = __builtin_ctzll(s), hi = 63 - __builtin_clzll(s);
+    return hi - lo + 1;
+}
+
+template <int MG, typename K>
+int run_groups(mums_ctx* ctx, const K* skey, const uint32_t* sidx, const MatchParams& mp, uint32_t* probe_head,
+               uint32_t* probe_bucket, hipStream_t st) {
+    const uint64_t nt = group_tiles(ctx->N);
+    uint32_t* partials = ctx->partials.as<uint32_t>();
+    DevCounters* dc = ctx->counters.as<DevCounters>();
+    HIPCHK((launch_probe_pass<MG, K>(skey, sidx, ctx->N, ctx->gt, mp, ctx->L, partials, probe_head, probe_bucket, dc,
+                                     false, st)));
+    HIPCHK(exclusive_scan_u32(partials, nt, ctx->tmp.p, &dc->nprobes, st));
+    HIPCHK((launch_probe_pass<MG, K>(skey, sidx, ctx->N, ctx->gt, mp, ctx->L, partials, probe_head, probe_bucket, dc,
+                                     true, st)));
+    return MUMS_OK;
+}
+
+template <int MG, typename K>
+int run_replay(mums_ctx* ctx, const K* skey, const uint32_t* sidx, const MatchParams& mp, hipStream_t st) {
+    HIPCHK((launch_replay<MG, K>(skey, sidx, ctx->N, ctx->gt, mp, ctx->L, ctx->sorted_heads, ctx->bstart.as<uint32_t>(),
+                                 ctx->bend.as<uint32_t>(), ctx->tbl.as<uint32_t>(), ctx->pool.as<int64_t>(),
+                                 ctx->ckey.as<K>(), ctx->tsize.as<uint32_t>(), ctx->counters.p, st)));
+    return MUMS_OK;
+}
+
+template <typename K>
+int run_pipeline(mums_ctx* ctx, int stage) {
+    hipStream_t st = ctx->stream;
+    const int G = (int)ctx->genomes.size();
+    const uint64_t N = ctx->N;
+    MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, ctx->masked, ctx->seq_mask};
+
+    // workspace (grow-only; no allocation in steady state)
+    HIPCHK(ctx->ckey.ensure(N * sizeof(K) + 64));
+    HIPCHK(ctx->kA.ensure(N * sizeof(K) + 64));
+    HIPCHK(ctx->kB.ensure(N * sizeof(K) + 64));
+    HIPCHK(ctx->vA.ensure(N * 4 + 64));
+    HIPCHK(ctx->vB.ensure(N * 4 + 64));
+    size_t tmpb = std::max(radix_tmp_bytes(N), scan_tmp_bytes(N));
+    tmpb = std::max(tmpb, radix_tmp_bytes(N / 2 + 1));
+    tmpb = std::max(tmpb, scan_tmp_bytes((uint64_t)ctx->table_size));
+    HIPCHK(ctx->tmp.ensure(tmpb));
+    HIPCHK(ctx->partials.ensure((group_tiles(N) + 64) * 4));
+    HIPCHK(ctx->counters.ensure(sizeof(DevCounters)));
+    DevCounters* dc = ctx->counters.as<DevCounters>();
+
+    HIPCHK(hipEventRecord(ctx->ev[EV_START], st));
+    HIPCHK(hipMemsetAsync(dc, 0, sizeof(DevCounters), st));
+
+    // keys
+    std::vector<const char*> ptrs(G);
+    for (int g = 0; g < G; ++g) ptrs[g] = ctx->genomes[g].d_ptr;
+    SeedSpec ss = make_seed_spec(ctx->pattern, ctx->L, ctx->w);
+    HIPCHK(launch_seed_keys(ss, ctx->gt, ptrs.data(), ctx->ckey.p, sizeof(K) == 8, &dc->err, st));
+    HIPCHK(hipEventRecord(ctx->ev[EV_KEYS], st));
+
+    // sort: the G SortedMerLists, merged
+    int buf = 0;
+    HIPCHK(radix_sort<K>(ctx->ckey.as<K>(), nullptr, N, 2 * ctx->w + 1, ctx->kA.as<K>(), ctx->vA.as<uint32_t>(),
+                         ctx->kB.as<K>(), ctx->vB.as<uint32_t>(), ctx->tmp.p, &buf, st));
+    ctx->sorted_buf = buf;
+    const K* skey = buf ? ctx->kB.as<K>() : ctx->kA.as<K>();
+    const uint32_t* sidx = buf ? ctx->vB.as<uint32_t>() : ctx->vA.as<uint32_t>();
+    char* fk = buf ? (char*)ctx->kA.p : (char*)ctx->kB.p;       // free pair for probes
+    char* fv = buf ? (char*)ctx->vA.p : (char*)ctx->vB.p;
+    HIPCHK(hipEventRecord(ctx->ev[EV_SORT], st));
+
+    // groups -> probes (P <= N/2: both free buffers hold two P-long uint32 arrays)
+    const uint64_t pcap = N / 2 + 1;
+    uint32_t* bucketA = (uint32_t*)fk;
+    uint32_t* bucketB = bucketA + pcap;
+    uint32_t* headA = (uint32_t*)fv;
+    uint32_t* headB = headA + pcap;
+    int rc;
+    if (G <= 4) rc = run_groups<4, K>(ctx, skey, sidx, mp, headA, bucketA, st);
+    else if (G <= 8) rc = run_groups<8, K>(ctx, skey, sidx, mp, headA, bucketA, st);
+    else if (G <= 16) rc = run_groups<16, K>(ctx, skey, sidx, mp, headA, bucketA, st);
+    else rc = run_groups<32, K>(ctx, skey, sidx, mp, headA, bucketA, st);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (ctx->hc.err & 1u) return fail(ctx, MUMS_E_GAP, "Gap in genome sequence ('-' encountered)");
+    ctx->P = ctx->hc.nprobes;
+    HIPCHK(hipEventRecord(ctx->ev[EV_GROUPS], st));
+
+    // probes grouped by hash bucket, key order kept (stable)
+    int tbits = 1;
+    while (tbits < 32 && ((uint64_t)1 << tbits) < (uint64_t)ctx->table_size) ++tbits;
+    int pbuf = 0;
+    HIPCHK(radix_sort<uint32_t>(bucketA, headA, ctx->P, tbits, bucketB, headB, bucketA, headA, ctx->tmp.p, &pbuf,
+                                st));
+    ctx->sorted_buckets = pbuf ? bucketA : bucketB;
+    ctx->sorted_heads = pbuf ? headA : headB;
+    HIPCHK(hipEventRecord(ctx->ev[EV_BUCKETS], st));
+    ctx->stage_done = MUMS_STAGE_SEEDS;
+
+    if (stage >= MUMS_STAGE_ALL) {
+        const uint32_t T = ctx->table_size;
+        HIPCHK(ctx->bstart.ensure((size_t)T * 4));
+        HIPCHK(ctx->bend.ensure((size_t)T * 4));
+        HIPCHK(ctx->tsize.ensure((size_t)T * 4));
+        HIPCHK(ctx->obase.ensure((size_t)T * 4 + 64));
+        HIPCHK(ctx->pool.ensure((ctx->P + 1) * (size_t)(G + 2) * 8));
+        HIPCHK(ctx->tbl.ensure((ctx->P + 1) * 4));
+        HIPCHK(hipMemsetAsync(ctx->bstart.p, 0, (size_t)T * 4, st));
+        HIPCHK(hipMemsetAsync(ctx->bend.p, 0, (size_t)T * 4, st));
+        HIPCHK(hipMemsetAsync(ctx->tsize.p, 0, (size_t)T * 4, st));
+        HIPCHK(launch_bucket_ranges(ctx->sorted_buckets, ctx->P, ctx->bstart.as<uint32_t>(), ctx->bend.as<uint32_t>(),
+                                    st));
+        if (ctx->P > 0) {
+            if (G <= 4) rc = run_replay<4, K>(ctx, skey, sidx, mp, st);
+            else if (G <= 8) rc = run_replay<8, K>(ctx, skey, sidx, mp, st);
+            else if (G <= 16) rc = run_replay<16, K>(ctx, skey, sidx, mp, st);
+            else rc = run_replay<32, K>(ctx, skey, sidx, mp, st);
+            if (rc) return rc;
+        }
+        HIPCHK(hipEventRecord(ctx->ev[EV_REPLAY], st));
+        HIPCHK(hipMemcpyAsync(ctx->obase.p, ctx->tsize.p, (size_t)T * 4, hipMemcpyDeviceToDevice, st));
+        HIPCHK(exclusive_scan_u32(ctx->obase.as<uint32_t>(), T, ctx->tmp.p, &dc->nmatches, st));
+        HIPCHK(hipMemcpyAsync(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        ctx->M = ctx->hc.nmatches;
+        HIPCHK(ctx->out_len.ensure((ctx->M + 1) * 8));
+        HIPCHK(ctx->out_s.ensure((ctx->M + 1) * (size_t)G * 8));
+        HIPCHK(launch_emit(ctx->tsize.as<uint32_t>(), ctx->obase.as<uint32_t>(), ctx->bstart.as<uint32_t>(),
+                           ctx->tbl.as<uint32_t>(), ctx->pool.as<int64_t>(), G, T, ctx->out_len.as<uint64_t>(),
+                           ctx->out_s.as<int64_t>(), st));
+        HIPCHK(hipEventRecord(ctx->ev[EV_OUTPUT], st));
+        ctx->stage_done = MUMS_STAGE_ALL;
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipMemcpy(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost));
+
+    // stats
+    mums_stats& s = ctx->st;
+    s = mums_stats{};
+    s.seedmers = N;
+    s.groups = ctx->hc.groups;
+    s.probes = ctx->P;
+    s.repeat_limit_groups = ctx->hc.repeat_limit;
+    auto el = [&](int a, int b) {
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, ctx->ev[a], ctx->ev[b]);
+        return (double)ms;
+    };
+    s.ms_keys = el(EV_START, EV_KEYS);
+    s.ms_sort = el(EV_KEYS, EV_SORT);
+    s.ms_groups = el(EV_SORT, EV_GROUPS);
+    s.ms_buckets = el(EV_GROUPS, EV_BUCKETS);
+    if (ctx->stage_done >= MUMS_STAGE_ALL) {
+        s.mem_count = ctx->hc.entries;
+        s.collision_count = ctx->hc.collisions;
+        s.ms_replay = el(EV_BUCKETS, EV_REPLAY);
+        s.ms_output = el(EV_REPLAY, EV_OUTPUT);
+        s.ms_total = el(EV_START, EV_OUTPUT);
+    } else {
+        s.ms_total = el(EV_START, EV_BUCKETS);
+    }
+    return MUMS_OK;
+}
+
+int check_ctx(mums_ctx* ctx) {
+    if (!ctx) return MUMS_E_INVALID;
+    ctx->err.clear();
+    return MUMS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mums_abi_version(void) { return MUMS_ABI_VERSION; }
+
+int mums_ctx_create(int device, mums_ctx** out) {
+    if (!out) return MUMS_E_INVALID;
+    *out = nullptr;
+    if (!have_device()) return MUMS_E_NODEVICE;
+    mums_ctx* ctx = new mums_ctx();
+    ctx->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) { delete ctx; return MUMS_E_HIP; }
+    e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) { delete ctx; return MUMS_E_HIP; }
+    ctx->own_stream = true;
+    for (int i = 0; i < EV_COUNT; ++i) (void)hipEventCreate(&ctx->ev[i]);
+    *out = ctx;
+    return MUMS_OK;
+}
+
+int mums_ctx_destroy(mums_ctx* ctx) {
+    if (!ctx) return MUMS_E_INVALID;
+    (void)hipSetDevice(ctx->device);
+    mums_clear(ctx);
+    DevBuf* bufs[] = {&ctx->ckey, &ctx->kA, &ctx->kB, &ctx->vA, &ctx->vB, &ctx->tmp, &ctx->partials,
+                      &ctx->counters, &ctx->bstart, &ctx->bend, &ctx->tsize, &ctx->obase, &ctx->pool,
+                      &ctx->tbl, &ctx->out_len, &ctx->out_s};
+    for (DevBuf* b : bufs) b->release();
+    for (int i = 0; i < EV_COUNT; ++i)
+        if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
+    if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return MUMS_OK;
+}
+
+int mums_set_stream(mums_ctx* ctx, void* s) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (!s) return fail(ctx, MUMS_E_INVALID, "null stream");
+    if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    ctx->stream = (hipStream_t)s;
+    ctx->own_stream = false;
+    return MUMS_OK;
+}
+
+int mums_set_seed(mums_ctx* ctx, uint64_t pattern) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    ctx->seed = pattern;
+    return MUMS_OK;
+}
+
+int mums_set_params(mums_ctx* ctx, uint32_t repeat_tol, uint32_t enum_tol, uint32_t table_size) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (table_size == 0) return fail(ctx, MUMS_E_INVALID, "table size must be > 0");
+    ctx->repeat_tol = repeat_tol;
+    ctx->enum_tol = enum_tol;
+    ctx->table_size = table_size;
+    return MUMS_OK;
+}
+
+int mums_set_mask(mums_ctx* ctx, int masked, uint64_t seq_mask) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    ctx->masked = masked ? 1 : 0;
+    ctx->seq_mask = seq_mask;
+    return MUMS_OK;
+}
+
+int mums_add_genome(mums_ctx* ctx, const char* ascii, uint64_t n) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (!ascii && n) return fail(ctx, MUMS_E_INVALID, "Null gnSequence pointer");  // MatchFinder.cpp:63-65
+    if (ctx->genomes.size() >= (size_t)kMaxG)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "more than 32 genomes per context");
+    HIPCHK(hipSetDevice(ctx->device));
+    char* d = nullptr;
+    HIPCHK(hipMalloc(&d, n + 16));
+    if (n) HIPCHK(hipMemcpy(d, ascii, n, hipMemcpyHostToDevice));
+    ctx->genomes.push_back({d, n, true});
+    ctx->stage_done = 0;
+    return MUMS_OK;
+}
+
+int mums_add_genome_device(mums_ctx* ctx, const void* d_ascii, uint64_t n) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (!d_ascii && n) return fail(ctx, MUMS_E_INVALID, "Null gnSequence pointer");
+    if (ctx->genomes.size() >= (size_t)kMaxG)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "more than 32 genomes per context");
+    ctx->genomes.push_back({(const char*)d_ascii, n, false});
+    ctx->stage_done = 0;
+    return MUMS_OK;
+}
+
+int mums_clear(mums_ctx* ctx) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    (void)hipSetDevice(ctx->device);
+    for (auto& g : ctx->genomes)
+        if (g.owned && g.d_ptr) (void)hipFree((void*)g.d_ptr);
+    ctx->genomes.clear();
+    ctx->stage_done = 0;
+    ctx->M = ctx->P = ctx->N = 0;
+    ctx->st = mums_stats{};
+    return MUMS_OK;
+}
+
+int mums_find_stage(mums_ctx* ctx, int stage) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (!have_device()) return fail(ctx, MUMS_E_NODEVICE, "no HIP device");
+    HIPCHK(hipSetDevice(ctx->device));
+    ctx->stage_done = 0;
+    ctx->M = ctx->P = 0;
+    const int G = (int)ctx->genomes.size();
+    if (ctx->enum_tol > 1)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "enumeration tolerance > 1 (MatchFinder::EnumerateMatches) not implemented");
+    // seed (MatchList.h:351-357 default, SortedMerList::Create checks :788-798)
+    uint64_t total = 0;
+    for (auto& g : ctx->genomes) total += g.n;
+    uint64_t pat = ctx->seed;
+    if (pat == 0) {
+        uint32_t wdef = mums_default_seed_weight(G ? total / (uint64_t)G : 0);
+        pat = (uint64_t)mums_get_seed((int)wdef, 0);
+    }
+    const int L = seed_len(pat), w = __builtin_popcountll(pat);
+    if (L == 0) return fail(ctx, MUMS_E_INVALID, "Can't have 0 seed length");
+    if (L > 32) return fail(ctx, MUMS_E_INVALID, "Mer size is too large");
+    if (w > 31) return fail(ctx, MUMS_E_UNSUPPORTED, "seed weight 32 not supported");
+    ctx->pattern = pat;
+    ctx->L = L;
+    ctx->w = w;
+    ctx->key64 = (2 * w + 1) > 32;
+    GenomeTable& gt = ctx->gt;
+    gt = GenomeTable{};
+    gt.G = G;
+    uint64_t N = 0;
+    for (int g = 0; g < G; ++g) {
+        gt.n[g] = ctx->genomes[g].n;
+        gt.m[g] = gt.n[g] < (uint64_t)L ? 0 : gt.n[g] - L + 1;
+        gt.base[g] = N;
+        N += gt.m[g];
+    }
+    gt.base[G] = N;
+    for (int g = G + 1; g <= kMaxG; ++g) gt.base[g] = N;
+    if (N >= 0xFFFFFFF0ull)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed-mers per context (chunked mode not implemented)");
+    ctx->N = N;
+    if (G == 0) {
+        ctx->stage_done = MUMS_STAGE_ALL;
+        ctx->st = mums_stats{};
+        return MUMS_OK;
+    }
+    int rc = ctx->key64 ? run_pipeline<uint64_t>(ctx, stage) : run_pipeline<uint32_t>(ctx, stage);
+    return rc;
+}
+
+int mums_find(mums_ctx* ctx) { return mums_find_stage(ctx, MUMS_STAGE_ALL); }
+
+int mums_result_count(mums_ctx* ctx, uint64_t* count, uint32_t* seq_count) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (ctx->stage_done < MUMS_STAGE_ALL) return fail(ctx, MUMS_E_INVALID, "no completed FindMatches on this context");
+    if (count) *count = ctx->M;
+    if (seq_count) *seq_count = (uint32_t)ctx->genomes.size();
+    return MUMS_OK;
+}
+
+int mums_result_copy(mums_ctx* ctx, uint64_t* lengths, int64_t* starts) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (ctx->stage_done < MUMS_STAGE_ALL) return fail(ctx, MUMS_E_INVALID, "no completed FindMatches on this context");
+    if (ctx->M == 0) return MUMS_OK;
+    HIPCHK(hipSetDevice(ctx->device));
+    const size_t G = ctx->genomes.size();
+    if (lengths) HIPCHK(hipMemcpy(lengths, ctx->out_len.p, ctx->M * 8, hipMemcpyDeviceToHost));
+    if (starts) HIPCHK(hipMemcpy(starts, ctx->out_s.p, ctx->M * G * 8, hipMemcpyDeviceToHost));
+    return MUMS_OK;
+}
+
+int mums_get_stats(mums_ctx* ctx, mums_stats* out) {
+    if (check_ctx(ctx) || !out) return MUMS_E_INVALID;
+    *out = ctx->st;
+    return MUMS_OK;
+}
+
+const char* mums_last_error(mums_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int mums_copy_seed_keys(mums_ctx* ctx, uint32_t genome, uint64_t* out, uint64_t cap) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (ctx->stage_done < MUMS_STAGE_SEEDS) return fail(ctx, MUMS_E_INVALID, "keys not computed yet");
+    if (genome >= ctx->genomes.size()) return fail(ctx, MUMS_E_INVALID, "genome index out of range");
+    const uint64_t m = ctx->gt.m[genome];
+    if (cap < m) return fail(ctx, MUMS_E_INVALID, "output buffer too small");
+    HIPCHK(hipSetDevice(ctx->device));
+    const int sh = 64 - 2 * ctx->w;
+    if (ctx->key64) {
+        std::vector<uint64_t> h(m);
+        if (m) HIPCHK(hipMemcpy(h.data(), ctx->ckey.as<uint64_t>() + ctx->gt.base[genome], m * 8, hipMemcpyDeviceToHost));
+        for (uint64_t p = 0; p < m; ++p) out[p] = ((h[p] >> 1) << sh) | (h[p] & 1);
+    } else {
+        std::vector<uint32_t> h(m);
+        if (m) HIPCHK(hipMemcpy(h.data(), ctx->ckey.as<uint32_t>() + ctx->gt.base[genome], m * 4, hipMemcpyDeviceToHost));
+        for (uint64_t p = 0; p < m; ++p) out[p] = (((uint64_t)h[p] >> 1) << sh) | (h[p] & 1);
+    }
+    return MUMS_OK;
+}
+
+int mums_build_sml(mums_ctx* ctx, uint32_t genome, uint32_t* positions, uint64_t cap) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (ctx->stage_done < MUMS_STAGE_SEEDS) return fail(ctx, MUMS_E_INVALID, "keys not sorted yet");
+    if (genome >= ctx->genomes.size()) return fail(ctx, MUMS_E_INVALID, "genome index out of range");
+    const uint64_t m = ctx->gt.m[genome];
+    if (cap < m) return fail(ctx, MUMS_E_INVALID, "output buffer too small");
+    HIPCHK(hipSetDevice(ctx->device));
+    // the merged sorted stream restricted to one genome is that genome's SML
+    std::vector<uint32_t> idx(ctx->N);
+    const uint32_t* sidx = ctx->sorted_buf ? ctx->vB.as<uint32_t>() : ctx->vA.as<uint32_t>();
+    if (ctx->N) HIPCHK(hipMemcpy(idx.data(), sidx, ctx->N * 4, hipMemcpyDeviceToHost));
+    const uint64_t lo = ctx->gt.base[genome], hi = ctx->gt.base[genome + 1];
+    uint64_t o = 0;
+    for (uint64_t i = 0; i < ctx->N; ++i)
+        if (idx[i] >= lo && idx[i] < hi) positions[o++] = (uint32_t)(idx[i] - lo);
+    return MUMS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,712 @@
+/*
+ * mums_oracle.c -- TEST INFRASTRUCTURE ONLY (parity checker; see mums_oracle.h).
+ *
+ * Plain-C restatement of the libMems 1.6.1 MemHash hot path.  Every function
+ * names the reference file:line it follows (paths relative to libMems/).
+ * Nothing here is shipped in, linked into, or called by the product path.
+ */
+#include "mums_oracle.h"
+
+#include <limits.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------- */
+/* Seed pattern table: SeedMasks.h:44-260 (low words; the high words are 0). */
+/* Rows are weights 0..31, columns seed ranks 0..5; 0 = "no seed".           */
+/* ------------------------------------------------------------------------- */
+static const uint32_t k_seed_table[32][6] = {
+    {0}, {0}, {0},
+    {0xb, 0, 0, 0, 0, 0},                                   /* w3  */
+    {0x3b, 0, 0, 0, 0, 0},                                  /* w4  */
+    {0x6b, 0x139, 0x193, 0x6b, 0, 0},                       /* w5  */
+    {0x58D, 0x653, 0x1AB, 0xdb, 0, 0},                      /* w6  */
+    {0x1953, 0x588d, 0x688b, 0x17d, 0x164d, 0},             /* w7  */
+    {0x3927, 0x1CA7, 0x6553, 0xb6d, 0, 0},                  /* w8  */
+    {0x7497, 0x1c927, 0x72a7, 0x6fb, 0x16ed, 0},            /* w9  */
+    {0x1d297, 0x3A497, 0xE997, 0x6D5B, 0, 0},               /* w10 */
+    {0x7954f, 0x75257, 0x1c9527, 0x5bed, 0x5b26d, 0},       /* w11 */
+    {0x7954f, 0x3D32F, 0x768B7, 0x5B56D, 0, 0},             /* w12 */
+    {0x792a4f, 0x1d64d7, 0x1d3597, 0x1b7db, 0x75ad7, 0},    /* w13 */
+    {0x1e6acf, 0xF59AF, 0x3D4CAF, 0x35AD6B, 0, 0},          /* w14 */
+    {0x7ac9af, 0x7b2a6f, 0x79aacf, 0x16df6d, 0x6b5d6b, 0},  /* w15 */
+    {0xf599af, 0xEE5A77, 0x7CD59F, 0xEB5AD7, 0, 0},         /* w16 */
+    {0x6dbedb, 0, 0, 0, 0, 0},                              /* w17 */
+    {0x3E6B59F, 0x3EB335F, 0x7B3566F, 0, 0, 0},             /* w18 */
+    {0x7b974ef, 0x7d6735f, 0x1edd74f, 0, 0, 0},             /* w19 */
+    {0x1F59B35F, 0x3EDCEDF, 0xFAE675F, 0, 0, 0},            /* w20 */
+    {0x7ddaddf, 0xaeb3f, 0x7eb76bf, 0, 0, 0},               /* w21 */
+    {0x003fffff, 0, 0, 0, 0, 0},                            /* w22 */
+    {0x007fffff, 0, 0, 0, 0, 0},
+    {0x00ffffff, 0, 0, 0, 0, 0},
+    {0x01ffffff, 0, 0, 0, 0, 0},
+    {0x03ffffff, 0, 0, 0, 0, 0},
+    {0x07ffffff, 0, 0, 0, 0, 0},
+    {0x0fffffff, 0, 0, 0, 0, 0},
+    {0x1fffffff, 0, 0, 0, 0, 0},
+    {0x3fffffff, 0, 0, 0, 0, 0},
+    {0x7fffffff, 0, 0, 0, 0, 0},                            /* w31 */
+};
+
+/* getSolidSeed: SeedMasks.h:270-281 */
+static int64_t solid_seed(int weight) { return (int64_t)((((uint64_t)1) << weight) - 1); }
+
+/* getSeed: SeedMasks.h:298-321 (SOLID_SEED == INT_MAX, :263) */
+int64_t oracle_get_seed(int weight, int seed_rank) {
+    if (seed_rank == INT_MAX) return solid_seed(weight);
+    if (weight > 31) return solid_seed(32);
+    if (seed_rank > 5) return solid_seed(weight);
+    if (weight < 0 || k_seed_table[weight][seed_rank] == 0) return solid_seed(weight);
+    return (int64_t)k_seed_table[weight][seed_rank];
+}
+
+/* getSeedLength: SeedMasks.h:335-350 */
+int oracle_seed_length(int64_t seed) {
+    int right = -1, left = -1;
+    uint64_t s = (uint64_t)seed;
+    for (int b = 0; b < 64; ++b, s >>= 1)
+        if (s & 1) { left = b; if (right == -1) right = b; }
+    return left != -1 ? left - right + 1 : 0;
+}
+
+/* getSeedWeight: SeedMasks.h:363-373 */
+int oracle_seed_weight(int64_t seed) {
+    int w = 0;
+    uint64_t s = (uint64_t)seed;
+    for (int b = 0; b < 64; ++b, s >>= 1) w += (int)(s & 1);
+    return w;
+}
+
+/* getDefaultSeedWeight: SeedMasks.h:389-401 */
+unsigned oracle_default_seed_weight(uint64_t avg_len) {
+    unsigned m = (unsigned)ceil((log((double)avg_len) / log(2.0)) / 1.5);
+    if (!(m & 1)) ++m;
+    m = m < 5 ? 0 : m;
+    if (avg_len == 0) m = 0;
+    return m > 31 ? 31 : m;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Encoding: BasicDNATable SortedMerList.cpp:29-47, translate32 :425-460,     */
+/* SetSequence :306-317 (ceil(2n/32) + 2 words; pad words zeroed here, they   */
+/* are uninitialised in the reference but always masked off).                */
+/* ------------------------------------------------------------------------- */
+static uint8_t dna_code(unsigned char c) {
+    switch (c) {
+    case 'c': case 'C': case 'b': case 'B': case 'y': case 'Y': return 1;
+    case 'g': case 'G': case 's': case 'S': case 'k': case 'K': return 2;
+    case 't': case 'T': return 3;
+    default: return 0;
+    }
+}
+
+static uint64_t packed_words(uint64_t n) { return (2 * n) / 32 + (((2 * n) % 32) ? 1 : 0) + 2; }
+
+int64_t oracle_pack(const char* seq, uint64_t n, uint32_t* out) {
+    uint64_t nw = packed_words(n);
+    memset(out, 0, nw * sizeof(uint32_t));
+    for (uint64_t i = 0; i < n; ++i) {
+        if (seq[i] == '-') return -1;  /* SortedMerList.cpp:433-437 throws */
+        out[i / 16] |= (uint32_t)dna_code((unsigned char)seq[i]) << (30 - 2 * (i % 16));
+    }
+    return (int64_t)nw;
+}
+
+typedef struct sml_ctx {
+    const uint32_t* words;
+    uint64_t n;          /* sequence length                 */
+    uint64_t seed;       /* pattern                         */
+    int L, w;            /* seed length / weight            */
+    uint64_t mer_mask;   /* top 2L bits  (SetMerMaskSize)   */
+    uint64_t seed_mask;  /* top 2w bits                     */
+} sml_ctx;
+
+static uint64_t top_mask(int chars) {  /* SetMerMaskSize: SortedMerList.cpp:271-282 */
+    return chars >= 32 ? ~(uint64_t)0 : (~(uint64_t)0) << (64 - 2 * chars);
+}
+
+/* GetMer: SortedMerList.cpp:321-342 */
+static uint64_t get_mer(const sml_ctx* c, uint64_t pos) {
+    uint64_t wi = (pos * 2) / 32, bit = (pos * 2) % 32;
+    uint64_t m = ((uint64_t)c->words[wi] << 32) | c->words[wi + 1];
+    if (bit > 0) m = (m << bit) | (c->words[wi + 2] >> (32 - bit));
+    return m & c->mer_mask;
+}
+
+/* GetSeedMer: SortedMerList.cpp:726-762 (mer_transition at :744 never fires, L<=32) */
+static uint64_t get_seed_mer(const sml_ctx* c, uint64_t pos) {
+    uint64_t mer = get_mer(c, pos), sm = 0;
+    for (int k = 0; k < c->L; ++k) {
+        if (c->seed & ((uint64_t)1 << (c->L - 1 - k)))
+            sm = (sm << 2) | ((mer >> (62 - 2 * k)) & 3);
+    }
+    return c->w >= 32 ? sm : sm << (64 - 2 * c->w);
+}
+
+/* RevCompMer: SortedMerList.cpp:597-614 (literal restatement) */
+static uint64_t revcomp_mer(uint64_t a, int len) {
+    uint64_t b = ~a, r = 0;
+    for (int i = 0; i < 64; i += 2) {
+        r |= b & 3;
+        b >>= 2;
+        r <<= 2;
+    }
+    int sh = 64 - 2 * (len + 1);
+    r = sh >= 0 ? r << sh : r >> (-sh);
+    return r | 1;
+}
+
+/* GetDnaSeedMer: SortedMerList.cpp:764-769 */
+static uint64_t get_dna_seed_mer(const sml_ctx* c, uint64_t pos) {
+    uint64_t s = get_seed_mer(c, pos);
+    uint64_t r = revcomp_mer(s, c->w);
+    return s < r ? s : r;
+}
+
+static int sml_init(sml_ctx* c, const char* seq, uint64_t n, uint64_t seed, uint32_t** words_out) {
+    uint32_t* words = (uint32_t*)malloc(packed_words(n) * sizeof(uint32_t) + 16);
+    if (!words) return -2;
+    if (oracle_pack(seq, n, words) < 0) { free(words); return -1; }
+    c->words = words;
+    c->n = n;
+    c->seed = seed;
+    c->L = oracle_seed_length((int64_t)seed);
+    c->w = oracle_seed_weight((int64_t)seed);
+    c->mer_mask = top_mask(c->L);
+    c->seed_mask = top_mask(c->w);
+    *words_out = words;
+    return 0;
+}
+
+/* SMLLength: SortedMerList.cpp:288-295 (linear sequences only) */
+static uint64_t sml_length(uint64_t n, int L) { return n < (uint64_t)L ? 0 : n - L + 1; }
+
+int oracle_seed_keys(const char* seq, uint64_t n, uint64_t seed, uint64_t* out) {
+    sml_ctx c; uint32_t* w;
+    int rc = sml_init(&c, seq, n, seed, &w);
+    if (rc) return rc;
+    uint64_t m = sml_length(n, c.L);
+    for (uint64_t p = 0; p < m; ++p) out[p] = get_dna_seed_mer(&c, p);
+    free(w);
+    return 0;
+}
+
+/* MemorySML::Create: MemorySML.cpp:45-60 (std::sort by key, unstable; here   */
+/* ties are broken by position so the order is deterministic).               */
+typedef struct { uint64_t key; uint32_t pos; } bmer_t;
+
+static int bmer_cmp(const void* a, const void* b) {
+    const bmer_t* x = (const bmer_t*)a; const bmer_t* y = (const bmer_t*)b;
+    if (x->key != y->key) return x->key < y->key ? -1 : 1;
+    return x->pos < y->pos ? -1 : (x->pos > y->pos);
+}
+
+static bmer_t* build_sml(const sml_ctx* c, const uint64_t* keys, uint64_t m) {
+    bmer_t* v = (bmer_t*)malloc((m ? m : 1) * sizeof(bmer_t));
+    for (uint64_t p = 0; p < m; ++p) { v[p].key = keys[p]; v[p].pos = (uint32_t)p; }
+    qsort(v, m, sizeof(bmer_t), bmer_cmp);
+    (void)c;
+    return v;
+}
+
+int oracle_build_sml(const char* seq, uint64_t n, uint64_t seed, uint32_t* out_pos) {
+    sml_ctx c; uint32_t* w;
+    int rc = sml_init(&c, seq, n, seed, &w);
+    if (rc) return rc;
+    uint64_t m = sml_length(n, c.L);
+    uint64_t* keys = (uint64_t*)malloc((m ? m : 1) * sizeof(uint64_t));
+    for (uint64_t p = 0; p < m; ++p) keys[p] = get_dna_seed_mer(&c, p);
+    bmer_t* v = build_sml(&c, keys, m);
+    for (uint64_t i = 0; i < m; ++i) out_pos[i] = v[i].pos;
+    free(v); free(keys); free(w);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------- */
+/* MatchHashEntry (MatchHashEntry.h:30-103, MatchHashEntry.cpp).              */
+/* A match = one length + G signed 1-based starts (0 = NO_MATCH,             */
+/* AbstractMatch.h:27); m_mersize is L for probes (HashMatch, MemHash.cpp:172)*/
+/* and 0 for stored copies (operator=, MatchHashEntry.cpp:122).              */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+    int64_t len;
+    int64_t offset;
+    int64_t mersize;
+    int64_t* s;   /* G starts */
+} mhe_t;
+
+typedef struct {
+    int G, L;
+    uint64_t seed_mask;
+    const uint64_t** keys;   /* keys[g][p] = GetDnaSeedMer(p) of genome g */
+    const uint64_t* n;       /* genome lengths                            */
+    int64_t gnseqi_end;      /* value of (int64)GNSEQI_END                */
+} ext_ctx;
+
+/* FirstStart: HybridAbstractMatch.h:121-129 (lowest genome with a start) */
+static int first_start(const mhe_t* m, int G) {
+    for (int i = 0; i < G; ++i) if (m->s[i] != 0) return i;
+    return INT_MAX;
+}
+
+/* CalculateOffset: MatchHashEntry.cpp:141-160 */
+static void calc_offset(mhe_t* m, int G) {
+    int r = first_start(m, G);
+    int64_t off = 0;
+    for (int i = r + 1; i < G; ++i) {
+        if (m->s[i] != 0) {
+            int64_t t = m->s[i] - m->s[r];
+            if (m->s[i] < 0) t -= m->len;
+            off += t;
+        }
+    }
+    m->offset = off;
+}
+
+/* Contains: MatchHashEntry.cpp:164-200  (does a contain b) */
+static int contains(const mhe_t* a, const mhe_t* b, int G) {
+    if (a->offset != b->offset) return 0;
+    int i = first_start(b, G);
+    int64_t diff = b->s[i] - a->s[i];
+    if (a->s[i] == 0) return 0;
+    if (diff < 0 || a->len < b->len + diff) return 0;
+    int64_t diff_rc = b->len - a->len + diff;
+    for (++i; i < G; ++i) {
+        int64_t di = b->s[i] - a->s[i];
+        if (b->s[i] == 0 && a->s[i] == 0) continue;
+        else if (b->s[i] < 0 && diff_rc == di) continue;
+        else if (diff != di) return 0;
+    }
+    return 1;
+}
+
+/* strict_start_lessthan_ptr: MatchHashEntry.cpp:48-69 */
+static int strict_start_lt(const mhe_t* a, const mhe_t* b, int G) {
+    int start_diff = first_start(a, G) - first_start(b, G);
+    if (start_diff == 0) {
+        for (int i = 0; i < G; ++i) {
+            int64_t as = a->s[i], bs = b->s[i];
+            if (as < 0) as = -as + a->len - a->mersize;
+            if (bs < 0) bs = -bs + b->len - b->mersize;
+            int64_t d = as - bs;
+            if (d == 0) continue;
+            return d < 0;
+        }
+    }
+    return start_diff < 0;
+}
+
+/* MheCompare: MatchHashEntry.h:121-143 */
+static int mhe_less(const mhe_t* a, const mhe_t* b, int G) {
+    int fa = first_start(a, G), fb = first_start(b, G);
+    if (fa > fb) return 1;
+    if (fa == fb) {
+        for (int i = fa; i < G; ++i) {
+            if (a->s[i] == 0 && b->s[i] != 0) return 1;
+            if (a->s[i] != 0 && b->s[i] == 0) return 0;
+        }
+        if (contains(a, b, G) || contains(b, a, G)) return 0;
+        return strict_start_lt(a, b, G);
+    }
+    return 0;
+}
+
+/* oriented seed test used by ExtendMatch: MatchFinder.h:265-293 */
+static void seed_at(const ext_ctx* x, int g, const mhe_t* m, uint64_t* key, int* parity) {
+    int64_t mt = m->s[g];
+    if (mt < 0) mt = -mt + m->len - x->L;
+    uint64_t k = x->keys[g][mt - 1];
+    *parity = m->s[g] < 0 ? (int)(k & 1) : !(k & 1);
+    *key = k & x->seed_mask;
+}
+
+/* ExtendMatch: MatchFinder.h:218-374 (literal restatement of the control   */
+/* flow; circular sequences are out of scope).                               */
+static void extend_match(const ext_ctx* x, mhe_t* m) {
+    int G = x->G, L = x->L;
+    int cur[64]; int used = 0;
+    for (int g = 0; g < G; ++g) if (m->s[g] != 0) cur[used++] = g;
+    int jump = L;
+    int extend_again = 0;
+    for (int dir = 0; dir < 4; ++dir) {
+        int64_t maxlen;
+        if (dir == 0 || dir == 1) maxlen = x->gnseqi_end;   /* max_backward / max_forward defaults */
+        else maxlen = L;
+        for (int q = 0; q < used; ++q) {
+            int g = cur[q];
+            if (m->s[g] < 0) {
+                int64_t rc_len = (int64_t)x->n[g] - m->len + m->s[g] + 1;
+                if (rc_len < maxlen) maxlen = rc_len;
+            } else if (m->s[g] - 1 < maxlen) {
+                maxlen = m->s[g] - 1;
+            }
+        }
+        int j = 0, i = used;
+        uint64_t extend_limit = 0, extend_attempts = 0;
+        while (maxlen - jump >= 0) {
+            m->len += jump;
+            maxlen -= jump;
+            for (j = 0; j < used; ++j) {
+                int g = cur[j];
+                if (m->s[g] > 0) {
+                    m->s[g] -= jump;
+                    if (m->s[g] <= 0) m->s[g] += (int64_t)x->n[g];
+                }
+            }
+            uint64_t k0; int p0;
+            seed_at(x, cur[0], m, &k0, &p0);
+            for (i = 1; i < used; ++i) {
+                uint64_t ki; int pi;
+                seed_at(x, cur[i], m, &ki, &pi);
+                if (k0 != ki || p0 != pi) {
+                    if (dir < 2) maxlen = 0;
+                    break;
+                }
+            }
+            extend_attempts += (uint64_t)jump;
+            if (i == used) extend_limit = extend_attempts;
+            if (dir > 1 && extend_attempts == (uint64_t)L) break;
+        }
+        if (i < used) {
+            m->len -= jump;
+            for (; j > 0; j--)
+                if (m->s[cur[j - 1]] >= 0) m->s[cur[j - 1]] += jump;
+        }
+        if (dir > 1 && extend_attempts > 0) {
+            if (extend_limit > 0) extend_again = 1;
+            int64_t unmatched = (int64_t)(extend_attempts - extend_limit);
+            if (i < used) unmatched -= jump;
+            m->len -= unmatched;
+            for (j = 0; j < used; ++j) {
+                int g = cur[j];
+                if (m->s[g] > 0) {
+                    m->s[g] += unmatched;
+                    if (m->s[g] > (int64_t)x->n[g]) m->s[g] -= (int64_t)x->n[g];
+                }
+            }
+        }
+        for (int g = 0; g < G; ++g) m->s[g] = -m->s[g];   /* Invert: HybridAbstractMatch.h:206-213 */
+        if (dir >= 1) jump = 1;
+        if (dir == 3 && extend_again) { dir = -1; jump = L; extend_again = 0; }
+    }
+}
+
+/* ------------------------------------------------------------------------- */
+/* MemHash table (MemHash.cpp:209-251) and driver                             */
+/* ------------------------------------------------------------------------- */
+typedef struct { uint32_t* v; uint32_t n, cap; } bucket_t;
+
+struct oracle_result {
+    int G;
+    uint64_t count;
+    uint64_t* lengths;
+    int64_t* starts;
+    uint64_t mem_count, collision_count, max_group, probes, seedmers;
+};
+
+typedef struct {
+    ext_ctx x;
+    uint32_t table_size;
+    bucket_t* buckets;
+    mhe_t* pool; uint64_t pool_n, pool_cap;
+    int64_t* spool; uint64_t spool_n, spool_cap;
+    uint64_t mem_count, collisions, probes;
+} memhash_t;
+
+static uint32_t pool_add(memhash_t* h, const mhe_t* src) {
+    int G = h->x.G;
+    if (h->pool_n == h->pool_cap) {
+        h->pool_cap = h->pool_cap ? h->pool_cap * 2 : 1024;
+        h->pool = (mhe_t*)realloc(h->pool, h->pool_cap * sizeof(mhe_t));
+    }
+    if (h->spool_n + (uint64_t)G > h->spool_cap) {
+        /* starts live in a separate pool; re-point entries after growth */
+        uint64_t ncap = h->spool_cap ? h->spool_cap * 2 : 1024 * (uint64_t)G;
+        while (ncap < h->spool_n + (uint64_t)G) ncap *= 2;
+        int64_t* ns = (int64_t*)realloc(h->spool, ncap * sizeof(int64_t));
+        for (uint64_t e = 0; e < h->pool_n; ++e) h->pool[e].s = ns + (h->pool[e].s - h->spool);
+        h->spool = ns; h->spool_cap = ncap;
+    }
+    mhe_t* e = &h->pool[h->pool_n];
+    e->len = src->len; e->offset = src->offset;
+    e->mersize = 0;   /* operator=: MatchHashEntry.cpp:118-126 */
+    e->s = h->spool + h->spool_n;
+    memcpy(e->s, src->s, (size_t)G * sizeof(int64_t));
+    h->spool_n += (uint64_t)G;
+    return (uint32_t)h->pool_n++;
+}
+
+/* std::lower_bound (libstdc++ __lower_bound: halve len, middle = first+half) */
+static uint32_t lower_bound_mhe(memhash_t* h, const bucket_t* b, const mhe_t* val) {
+    uint32_t first = 0, len = b->n;
+    while (len > 0) {
+        uint32_t half = len >> 1, mid = first + half;
+        if (mhe_less(&h->pool[b->v[mid]], val, h->x.G)) { first = mid + 1; len = len - half - 1; }
+        else len = half;
+    }
+    return first;
+}
+
+/* MemHash::AddHashEntry: MemHash.cpp:209-251 */
+static void add_hash_entry(memhash_t* h, mhe_t* p) {
+    int64_t T = (int64_t)h->table_size;
+    uint32_t bi = (uint32_t)(((p->offset % T) + T) % T);
+    bucket_t* b = &h->buckets[bi];
+    ++h->probes;
+    uint32_t it = lower_bound_mhe(h, b, p);
+    if (it != b->n) {
+        const mhe_t* e = &h->pool[b->v[it]];
+        if (!mhe_less(e, p, h->x.G) && !mhe_less(p, e, h->x.G)) { ++h->collisions; return; }
+    }
+    extend_match(&h->x, p);
+    uint32_t id = pool_add(h, p);
+    uint32_t ins = lower_bound_mhe(h, b, &h->pool[id]);
+    if (b->n == b->cap) {
+        b->cap = b->cap ? b->cap * 2 : 4;
+        b->v = (uint32_t*)realloc(b->v, b->cap * sizeof(uint32_t));
+    }
+    memmove(b->v + ins + 1, b->v + ins, (size_t)(b->n - ins) * sizeof(uint32_t));
+    b->v[ins] = id;
+    ++b->n;
+    ++h->mem_count;
+}
+
+typedef struct { uint32_t g; uint32_t pos; uint64_t key; } idmer_t;
+
+/* MemHash::HashMatch MemHash.cpp:167-187 / MaskedMemHash::HashMatch          */
+/* MaskedMemHash.cpp:38-63, SetDirection MemHash.cpp:189-203.                 */
+static void hash_match(memhash_t* h, const oracle_params* prm, const idmer_t* lst, int cnt,
+                       int64_t* scratch) {
+    int G = h->x.G;
+    mhe_t m;
+    m.s = scratch;
+    memset(m.s, 0, (size_t)G * sizeof(int64_t));
+    m.len = h->x.L;
+    m.mersize = h->x.L;
+    int par[64] = {0};
+    for (int k = 0; k < cnt; ++k) { m.s[lst[k].g] = (int64_t)lst[k].pos + 1; par[lst[k].g] = (int)(lst[k].key & 1); }
+    int ref = first_start(&m, G);
+    int ref_forward = !par[ref];
+    for (int g = ref + 1; g < G; ++g)
+        if (m.s[g] != 0 && ref_forward == par[g]) m.s[g] = -m.s[g];
+    calc_offset(&m, G);
+    int mult = 0;
+    uint64_t match_number = 0;
+    for (int g = 0; g < G; ++g) {
+        match_number <<= 1;
+        if (m.s[g] != 0) { match_number |= 1; ++mult; }
+    }
+    if (prm->masked) {
+        if (prm->seq_mask == 0 || match_number == prm->seq_mask) add_hash_entry(h, &m);
+    } else if (mult >= 2) {
+        add_hash_entry(h, &m);
+    }
+}
+
+/* MatchFinder::EnumerateMatches (odometer): MatchFinder.cpp:342-393 */
+static void enumerate_odometer(memhash_t* h, const oracle_params* prm, idmer_t* lst, int cnt,
+                               int64_t* scratch) {
+    if (cnt == 2) { hash_match(h, prm, lst, cnt, scratch); return; }
+    /* stable sort by genome id (std::list::sort is stable) */
+    for (int a = 1; a < cnt; ++a) {
+        idmer_t t = lst[a]; int b = a - 1;
+        while (b >= 0 && lst[b].g > t.g) { lst[b + 1] = lst[b]; --b; }
+        lst[b + 1] = t;
+    }
+    int id_pos[64], id_end[65], nid = 0;
+    for (int a = 0; a < cnt; ++a) if (a == 0 || lst[a].g != lst[a - 1].g) id_pos[nid++] = a;
+    for (int k = 0; k < nid; ++k) id_end[k] = id_pos[k];
+    id_end[nid] = cnt;
+    idmer_t cm[64];
+    for (;;) {
+        for (int k = 0; k < nid; ++k) cm[k] = lst[id_pos[k]];
+        hash_match(h, prm, cm, nid, scratch);
+        int mm = nid - 1;
+        for (;;) {
+            ++id_pos[mm];
+            if (id_pos[mm] == id_end[mm + 1]) {
+                if (mm == 0) return;
+                id_pos[mm] = id_end[mm];
+                mm--;
+            } else break;
+        }
+    }
+}
+
+/* MemHash::EnumerateMatches: MemHash.cpp:139-162 */
+static void enumerate_matches(memhash_t* h, const oracle_params* prm, const idmer_t* grp, int cnt,
+                              idmer_t* hl, int64_t* scratch) {
+    uint32_t tally[64] = {0};
+    int nh = 0;
+    for (int k = 0; k < cnt; ++k) {
+        uint32_t g = grp[k].g;
+        if (tally[g] < prm->enum_tol) hl[nh++] = grp[k];
+        if (tally[g] > prm->repeat_tol) return;
+        ++tally[g];
+    }
+    if (nh > 1) {
+        if (prm->enum_tol == 1) hash_match(h, prm, hl, nh, scratch);
+        else enumerate_odometer(h, prm, hl, nh, scratch);
+    }
+}
+
+oracle_result* oracle_find_matches(int G, const char* const* seqs, const uint64_t* lens,
+                                   const oracle_params* prm) {
+    if (G < 1 || G > 64) return NULL;
+    oracle_result* res = (oracle_result*)calloc(1, sizeof(oracle_result));
+    res->G = G;
+    sml_ctx* ctx = (sml_ctx*)calloc((size_t)G, sizeof(sml_ctx));
+    uint32_t** words = (uint32_t**)calloc((size_t)G, sizeof(uint32_t*));
+    uint64_t** keys = (uint64_t**)calloc((size_t)G, sizeof(uint64_t*));
+    bmer_t** sml = (bmer_t**)calloc((size_t)G, sizeof(bmer_t*));
+    uint64_t* m = (uint64_t*)calloc((size_t)G, sizeof(uint64_t));
+    for (int g = 0; g < G; ++g) {
+        if (sml_init(&ctx[g], seqs[g], lens[g], prm->seed, &words[g])) { res->count = 0; goto done; }
+        m[g] = sml_length(lens[g], ctx[g].L);
+        keys[g] = (uint64_t*)malloc((m[g] ? m[g] : 1) * sizeof(uint64_t));
+        for (uint64_t p = 0; p < m[g]; ++p) keys[g][p] = get_dna_seed_mer(&ctx[g], p);
+        sml[g] = build_sml(&ctx[g], keys[g], m[g]);
+        res->seedmers += m[g];
+    }
+    {
+        memhash_t h;
+        memset(&h, 0, sizeof(h));
+        h.x.G = G;
+        h.x.L = ctx[0].L;
+        h.x.seed_mask = ctx[0].seed_mask;
+        h.x.keys = (const uint64_t**)keys;
+        h.x.n = lens;
+        h.x.gnseqi_end = prm->gnseqi_end_neg1 ? (int64_t)-1 : INT64_MAX;
+        h.table_size = prm->table_size ? prm->table_size : 40000;
+        h.buckets = (bucket_t*)calloc(h.table_size, sizeof(bucket_t));
+        int64_t* scratch = (int64_t*)malloc((size_t)G * sizeof(int64_t));
+
+        /* MatchFinder::SearchRange (MatchFinder.cpp:172-340): G-way merge of   */
+        /* the SMLs by masked key; a group = every occurrence of one masked key.*/
+        uint64_t* idx = (uint64_t*)calloc((size_t)G, sizeof(uint64_t));
+        uint64_t gcap = 1024;
+        idmer_t* grp = (idmer_t*)malloc(gcap * sizeof(idmer_t));
+        idmer_t* hl = (idmer_t*)malloc(gcap * sizeof(idmer_t));
+        const uint64_t mask = h.x.seed_mask;
+        for (;;) {
+            int have = 0; uint64_t mn = 0;
+            for (int g = 0; g < G; ++g) {
+                if (idx[g] < m[g]) {
+                    uint64_t k = sml[g][idx[g]].key & mask;
+                    if (!have || k < mn) { mn = k; have = 1; }
+                }
+            }
+            if (!have) break;
+            uint64_t cnt = 0;
+            for (int g = 0; g < G; ++g) {
+                while (idx[g] < m[g] && (sml[g][idx[g]].key & mask) == mn) {
+                    if (cnt == gcap) {
+                        gcap *= 2;
+                        grp = (idmer_t*)realloc(grp, gcap * sizeof(idmer_t));
+                        hl = (idmer_t*)realloc(hl, gcap * sizeof(idmer_t));
+                    }
+                    grp[cnt].g = (uint32_t)g;
+                    grp[cnt].pos = sml[g][idx[g]].pos;
+                    grp[cnt].key = sml[g][idx[g]].key;
+                    ++cnt; ++idx[g];
+                }
+            }
+            if (cnt > res->max_group) res->max_group = cnt;
+            if (cnt > 1) enumerate_matches(&h, prm, grp, (int)cnt, hl, scratch);
+        }
+        free(idx); free(grp); free(hl); free(scratch);
+
+        /* MemHash::GetMatchList: MemHash.h:182-203 (bucket-major) */
+        res->count = h.mem_count;
+        res->lengths = (uint64_t*)malloc((h.mem_count ? h.mem_count : 1) * sizeof(uint64_t));
+        res->starts = (int64_t*)malloc((h.mem_count ? h.mem_count : 1) * (size_t)G * sizeof(int64_t));
+        uint64_t o = 0;
+        for (uint32_t bi = 0; bi < h.table_size; ++bi) {
+            for (uint32_t k = 0; k < h.buckets[bi].n; ++k) {
+                const mhe_t* e = &h.pool[h.buckets[bi].v[k]];
+                res->lengths[o] = (uint64_t)e->len;
+                memcpy(res->starts + o * (uint64_t)G, e->s, (size_t)G * sizeof(int64_t));
+                ++o;
+            }
+            free(h.buckets[bi].v);
+        }
+        res->mem_count = h.mem_count;
+        res->collision_count = h.collisions;
+        res->probes = h.probes;
+        free(h.buckets); free(h.pool); free(h.spool);
+    }
+done:
+    for (int g = 0; g < G; ++g) { free(words[g]); free(keys[g]); free(sml[g]); }
+    free(ctx); free(words); free(keys); free(sml); free(m);
+    return res;
+}
+
+uint64_t oracle_result_count(const oracle_result* r) { return r ? r->count : 0; }
+int      oracle_result_seqcount(const oracle_result* r) { return r ? r->G : 0; }
+void     oracle_result_copy(const oracle_result* r, uint64_t* lengths, int64_t* starts) {
+    if (!r) return;
+    if (lengths) memcpy(lengths, r->lengths, r->count * sizeof(uint64_t));
+    if (starts) memcpy(starts, r->starts, r->count * (size_t)r->G * sizeof(int64_t));
+}
+uint64_t oracle_result_mem_count(const oracle_result* r) { return r ? r->mem_count : 0; }
+uint64_t oracle_result_collision_count(const oracle_result* r) { return r ? r->collision_count : 0; }
+uint64_t oracle_result_max_group(const oracle_result* r) { return r ? r->max_group : 0; }
+uint64_t oracle_result_probe_count(const oracle_result* r) { return r ? r->probes : 0; }
+uint64_t oracle_result_seedmers(const oracle_result* r) { return r ? r->seedmers : 0; }
+void     oracle_result_free(oracle_result* r) {
+    if (!r) return;
+    free(r->lengths); free(r->starts); free(r);
+}
+
+/* ------------------------------------------------------------------------- */
+/* Synthetic genomes: SURVEY.md Appendix C (std::mt19937_64 restated).        */
+/* ------------------------------------------------------------------------- */
+typedef struct { uint64_t mt[312]; int idx; } mt64_t;
+
+static void mt64_seed(mt64_t* r, uint64_t s) {
+    r->mt[0] = s;
+    for (int i = 1; i < 312; ++i)
+        r->mt[i] = 6364136223846793005ULL * (r->mt[i - 1] ^ (r->mt[i - 1] >> 62)) + (uint64_t)i;
+    r->idx = 312;
+}
+
+static uint64_t mt64_next(mt64_t* r) {
+    if (r->idx >= 312) {
+        for (int i = 0; i < 312; ++i) {
+            uint64_t x = (r->mt[i] & 0xFFFFFFFF80000000ULL) | (r->mt[(i + 1) % 312] & 0x7FFFFFFFULL);
+            uint64_t xa = x >> 1;
+            if (x & 1) xa ^= 0xB5026F5AA96619E9ULL;
+            r->mt[i] = r->mt[(i + 156) % 312] ^ xa;
+        }
+        r->idx = 0;
+    }
+    uint64_t y = r->mt[r->idx++];
+    y ^= (y >> 29) & 0x5555555555555555ULL;
+    y ^= (y << 17) & 0x71D67FFFEDA60000ULL;
+    y ^= (y << 37) & 0xFFF7EEE000000000ULL;
+    y ^= y >> 43;
+    return y;
+}
+
+void oracle_generate(int G, uint64_t n, double p, uint64_t rng_seed, char* out) {
+    static const char acgt[4] = {'A', 'C', 'G', 'T'};
+    mt64_t r;
+    mt64_seed(&r, rng_seed);
+    for (uint64_t i = 0; i < n; ++i) out[i] = acgt[mt64_next(&r) & 3];
+    const double thr = p * 1e6;
+    for (int g = 1; g < G; ++g) {
+        char* d = out + (uint64_t)g * n;
+        memcpy(d, out, n);
+        for (uint64_t i = 0; i < n; ++i)
+            if ((double)(mt64_next(&r) % 1000000) < thr) d[i] = acgt[mt64_next(&r) & 3];
+        if (g == 2) {
+            for (uint64_t a = 0, b = n ? n - 1 : 0; a < b; ++a, --b) { char t = d[a]; d[a] = d[b]; d[b] = t; }
+            for (uint64_t i = 0; i < n; ++i) {
+                char c = d[i];
+                d[i] = c == 'A' ? 'T' : c == 'C' ? 'G' : c == 'G' ? 'C' : 'A';
+            }
+        }
+    }
+}

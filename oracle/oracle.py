@@ -1,0 +1,139 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes wrapper of the C oracle (oracle/mums_oracle.c).
+
+The oracle is the CPU restatement of libMems' MemHash path used to check the
+HIP implementation.  Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg import this module; the product (libmems_amd) never does.
+Parity pinning: SURVEY.md Appendix C known-answer md5s (tests/test_oracle_pinning.py).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from typing import Sequence, Tuple
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "libmums_oracle.so")
+CLI = os.path.join(HERE, "build", "oracle_cli")
+
+_lib = None
+
+
+class _Params(ctypes.Structure):
+    _fields_ = [
+        ("seed", ctypes.c_uint64),
+        ("repeat_tol", ctypes.c_uint32),
+        ("enum_tol", ctypes.c_uint32),
+        ("table_size", ctypes.c_uint32),
+        ("masked", ctypes.c_int),
+        ("seq_mask", ctypes.c_uint64),
+        ("gnseqi_end_neg1", ctypes.c_int),
+    ]
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = ctypes.CDLL(LIB)
+        vp, u64 = ctypes.c_void_p, ctypes.c_uint64
+        L.oracle_get_seed.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.oracle_get_seed.restype = ctypes.c_int64
+        L.oracle_seed_length.argtypes = [ctypes.c_int64]
+        L.oracle_seed_weight.argtypes = [ctypes.c_int64]
+        L.oracle_default_seed_weight.argtypes = [u64]
+        L.oracle_default_seed_weight.restype = ctypes.c_uint
+        L.oracle_pack.argtypes = [ctypes.c_char_p, u64, vp]
+        L.oracle_pack.restype = ctypes.c_int64
+        L.oracle_seed_keys.argtypes = [ctypes.c_char_p, u64, u64, vp]
+        L.oracle_build_sml.argtypes = [ctypes.c_char_p, u64, u64, vp]
+        L.oracle_find_matches.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(u64),
+                                          ctypes.POINTER(_Params)]
+        L.oracle_find_matches.restype = vp
+        for f in ("count", "mem_count", "collision_count", "max_group", "probe_count", "seedmers"):
+            fn = getattr(L, f"oracle_result_{f}")
+            fn.argtypes = [vp]
+            fn.restype = u64
+        L.oracle_result_seqcount.argtypes = [vp]
+        L.oracle_result_copy.argtypes = [vp, vp, vp]
+        L.oracle_result_free.argtypes = [vp]
+        L.oracle_generate.argtypes = [ctypes.c_int, u64, ctypes.c_double, u64, ctypes.c_char_p]
+        _lib = L
+    return _lib
+
+
+def get_seed(weight: int, rank: int = 0) -> int:
+    return int(lib().oracle_get_seed(weight, rank)) & 0xFFFFFFFFFFFFFFFF
+
+
+def generate(G: int, n: int, p: float, seed: int = 12345) -> list:
+    """SURVEY.md Appendix C generator (std::mt19937_64)."""
+    buf = ctypes.create_string_buffer(G * n)
+    lib().oracle_generate(G, n, p, seed, buf)
+    raw = buf.raw
+    return [raw[g * n:(g + 1) * n] for g in range(G)]
+
+
+def pack(seq: bytes) -> np.ndarray:
+    nw = (2 * len(seq)) // 32 + (1 if (2 * len(seq)) % 32 else 0) + 2
+    out = np.zeros(nw, dtype=np.uint32)
+    rc = lib().oracle_pack(seq, len(seq), out.ctypes.data)
+    if rc < 0:
+        raise ValueError("gap in sequence")
+    return out
+
+
+def seed_keys(seq: bytes, seed: int) -> np.ndarray:
+    L = lib().oracle_seed_length(seed)
+    m = max(len(seq) - L + 1, 0)
+    out = np.zeros(max(m, 1), dtype=np.uint64)
+    lib().oracle_seed_keys(seq, len(seq), seed, out.ctypes.data)
+    return out[:m]
+
+
+def build_sml(seq: bytes, seed: int) -> np.ndarray:
+    L = lib().oracle_seed_length(seed)
+    m = max(len(seq) - L + 1, 0)
+    out = np.zeros(max(m, 1), dtype=np.uint32)
+    lib().oracle_build_sml(seq, len(seq), seed, out.ctypes.data)
+    return out[:m]
+
+
+def find_matches(seqs: Sequence[bytes], seed: int, repeat_tol: int = 0, enum_tol: int = 1,
+                 table_size: int = 40000, masked: bool = False, seq_mask: int = 0,
+                 gnseqi_end_neg1: bool = False) -> Tuple[np.ndarray, np.ndarray, dict]:
+    """MemHash::FindMatches restated; returns (lengths[M], starts[M,G], counters)."""
+    G = len(seqs)
+    arr = (ctypes.c_char_p * G)(*seqs)
+    lens = (ctypes.c_uint64 * G)(*[len(s) for s in seqs])
+    prm = _Params(seed, repeat_tol, enum_tol, table_size, int(masked), seq_mask, int(gnseqi_end_neg1))
+    L = lib()
+    r = L.oracle_find_matches(G, arr, lens, ctypes.byref(prm))
+    if not r:
+        raise ValueError("oracle rejected input")
+    try:
+        c = L.oracle_result_count(r)
+        lengths = np.zeros(c, dtype=np.uint64)
+        starts = np.zeros((c, G), dtype=np.int64)
+        if c:
+            L.oracle_result_copy(r, lengths.ctypes.data, starts.ctypes.data)
+        stats = dict(mem_count=L.oracle_result_mem_count(r), collision_count=L.oracle_result_collision_count(r),
+                     max_group=L.oracle_result_max_group(r), probes=L.oracle_result_probe_count(r),
+                     seedmers=L.oracle_result_seedmers(r))
+    finally:
+        L.oracle_result_free(r)
+    return lengths, starts, stats
+
+
+def match_text(lengths: np.ndarray, starts: np.ndarray) -> str:
+    if len(lengths) == 0:
+        return ""
+    arr = np.concatenate([lengths.astype(np.int64)[:, None], starts], axis=1)
+    return "".join("\t".join(map(str, row)) + "\n" for row in arr.tolist())
