@@ -90,6 +90,13 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         return _lib
     if not os.path.exists(path):
         raise ImportError(f"{path} not built: run `make -C {_HERE}` (hipcc --offload-arch=gfx950)")
+    # PyTorch-ROCm ships its own libamdhip64.so.7 (same soname as /opt/rocm's).  Load it
+    # first so this library binds to that one runtime instead of a second HIP/HSA runtime
+    # in the same process (two runtimes cannot share the device).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(path)
     vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
     lib.mums_abi_version.restype = i32

@@ -1,0 +1,208 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's known answers
+and against the pinned CPU oracle, bit for bit (integer/index work: exact)."""
+import hashlib
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+CASES = json.load(open(os.path.join(GOLDEN, "appendix_c.json")))["cases"]
+
+
+def gpu_find(lm, seqs, seed=0, masked=False, mask=0, repeat_tol=0, enum_tol=1, table_size=40000):
+    cls = lm.MaskedMemHash if masked else lm.MemHash
+    with cls(0) as mh:
+        mh.SetSeed(seed)
+        mh.SetTableSize(table_size)
+        mh.SetRepeatTolerance(repeat_tol)
+        mh.SetEnumerationTolerance(enum_tol)
+        if masked:
+            mh.SetMask(mask)
+        ml = mh.FindMatches(seqs)
+        return ml, mh.stats()
+
+
+def assert_same(ml, ref):
+    lengths, starts, _ = ref
+    assert len(ml) == len(lengths)
+    assert (ml.lengths == lengths).all()
+    assert (ml.starts == starts).all()
+
+
+# ---- reference known answers ---------------------------------
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"G{c['G']}_n{c['n']}_p{c['p']}_{c['mode']}")
+def test_reference_known_answers(gpu_lib, oracle_mod, case):
+    seqs = oracle_mod.generate(case["G"], case["n"], case["p"], 12345)
+    ml, st = gpu_find(gpu_lib, seqs, oracle_mod.get_seed(case["w"]), masked=case["mode"] == "MaskedMemHash",
+                      mask=case.get("mask", 0))
+    txt = ml.text()
+    assert len(ml) == case["matches"]
+    assert hashlib.md5(txt.encode()).hexdigest() == case["md5"]
+    if "collisions" in case:
+        assert st["collision_count"] == case["collisions"]
+    assert st["mem_count"] == case["matches"]
+    assert st["repeat_limit_groups"] == 0
+
+
+@pytest.mark.parametrize("name,cfg", [("c1_related.txt", (2, 1000000, 15, 0.01)), ("c1_iid.txt", (2, 1000000, 15, 1.0)),
+                                      ("g3_200k_p003.txt", (3, 200000, 15, 0.03))])
+def test_golden_text_fixtures(gpu_lib, oracle_mod, name, cfg):
+    G, n, w, p = cfg
+    ml, _ = gpu_find(gpu_lib, oracle_mod.generate(G, n, p, 12345), oracle_mod.get_seed(w))
+    assert ml.text() == open(os.path.join(GOLDEN, name)).read()
+
+
+# ---- oracle parity on varied shapes ----------------------------------------------
+SHAPES = [
+    # G, n, weight, rank, p, extra
+    (2, 50_000, 5, 0, 0.02, {}),
+    (2, 80_000, 7, 0, 0.02, {}),
+    (3, 60_000, 9, 1, 0.02, {}),
+    (3, 100_000, 11, 0, 0.02, {}),          # getSeed(11) is a weight-12 pattern
+    (3, 100_000, 13, 0, 0.03, {}),
+    (4, 150_000, 15, 1, 0.02, {}),           # non-default rank
+    (4, 150_000, 15, 2, 0.02, {}),
+    (5, 120_000, 17, 0, 0.01, {}),
+    (6, 120_000, 19, 0, 0.01, {}),
+    (3, 120_000, 19, 2, 0.01, {}),           # non-palindromic rank-2 pattern (weight 18)
+    (3, 150_000, 21, 1, 0.01, {}),           # non-palindromic rank-1 pattern
+    (3, 150_000, 25, 0, 0.005, {}),          # solid seed
+    (2, 150_000, 31, 0, 0.002, {}),          # solid, 63-bit keys
+    (9, 40_000, 15, 0, 0.02, {}),            # MG=16 kernels
+    (17, 20_000, 13, 0, 0.02, {}),           # MG=32 kernels
+    (4, 200_000, 15, 0, 0.03, {"table_size": 1}),
+    (4, 200_000, 15, 0, 0.03, {"table_size": 7}),
+    (3, 200_000, 15, 0, 0.03, {"table_size": 70001}),
+    (3, 200_000, 13, 0, 0.2, {"repeat_tol": 1}),
+    (3, 200_000, 11, 0, 0.5, {"repeat_tol": 2}),
+    (3, 100_000, 15, 0, 0.02, {"enum_tol": 0}),
+    (4, 200_000, 15, 0, 0.02, {"masked": True, "mask": 0}),
+    (4, 200_000, 15, 0, 0.02, {"masked": True, "mask": 0b1011}),
+    (4, 200_000, 15, 0, 1.0, {"masked": True, "mask": 0b0110}),
+]
+
+
+@pytest.mark.parametrize("G,n,w,rank,p,extra", SHAPES)
+def test_oracle_parity_shapes(gpu_lib, oracle_mod, G, n, w, rank, p, extra):
+    seqs = oracle_mod.generate(G, n, p, 1000 + G * 7 + w)
+    seed = oracle_mod.get_seed(w, rank)
+    masked = extra.get("masked", False)
+    kw = {k: v for k, v in extra.items() if k in ("repeat_tol", "enum_tol", "table_size")}
+    ref = oracle_mod.find_matches(seqs, seed, masked=masked, seq_mask=extra.get("mask", 0), **kw)
+    ml, st = gpu_find(gpu_lib, seqs, seed, masked=masked, mask=extra.get("mask", 0), **kw)
+    assert_same(ml, ref)
+    assert st["collision_count"] == ref[2]["collision_count"]
+    assert st["mem_count"] == ref[2]["mem_count"]
+
+
+def _mutate(rng, s: bytes, alphabet=b"ACGTNRYKMacgtn") -> bytes:
+    b = bytearray(s)
+    for _ in range(len(b) // 50):
+        b[rng.randrange(len(b))] = rng.choice(alphabet)
+    return bytes(b)
+
+
+def test_ragged_iupac_lowercase(gpu_lib, oracle_mod):
+    rng = random.Random(5)
+    base = oracle_mod.generate(1, 120_000, 1.0, 77)[0]
+    seqs = [base, _mutate(rng, base[:90_000]), _mutate(rng, base[20_000:]).lower(), base[:30] + b"N" * 500 + base[1000:5000]]
+    seed = oracle_mod.get_seed(15)
+    assert_same(gpu_find(gpu_lib, seqs, seed)[0], oracle_mod.find_matches(seqs, seed))
+
+
+def test_empty_short_and_single_genomes(gpu_lib, oracle_mod):
+    seed = oracle_mod.get_seed(15)
+    base = oracle_mod.generate(1, 10_000, 1.0, 3)[0]
+    for seqs in ([base, b""], [base, b"ACGT"], [base], [b"", b""], [base, base[:22], base[:23], base[:24]]):
+        assert_same(gpu_find(gpu_lib, seqs, seed)[0], oracle_mod.find_matches(seqs, seed))
+
+
+def test_gap_character_raises(gpu_lib, oracle_mod):
+    base = oracle_mod.generate(1, 5_000, 1.0, 3)[0]
+    with pytest.raises(gpu_lib.GapInSequence):
+        gpu_find(gpu_lib, [base, base[:100] + b"-" + base[101:]], oracle_mod.get_seed(15))
+
+
+def test_default_seed_from_lengths(gpu_lib, oracle_mod):
+    seqs = oracle_mod.generate(3, 300_000, 0.02, 11)
+    w = oracle_mod.lib().oracle_default_seed_weight(300_000)
+    ml, _ = gpu_find(gpu_lib, seqs, 0)
+    assert_same(ml, oracle_mod.find_matches(seqs, oracle_mod.get_seed(w)))
+
+
+def test_repeat_rich_input_counts_repeat_limit_groups(gpu_lib, oracle_mod):
+    """Long N runs collapse to one seed value: groups above MER_REPEAT_LIMIT are reported.
+    The reference re-scans there (MatchFinder.cpp:253-277); the count flags inputs where
+    its output could differ."""
+    base = oracle_mod.generate(1, 50_000, 1.0, 9)[0]
+    seqs = [base[:20000] + b"N" * 3000 + base[20000:], base]
+    ml, st = gpu_find(gpu_lib, seqs, oracle_mod.get_seed(15))
+    assert st["repeat_limit_groups"] >= 1
+
+
+# ---- rows A3-A5: keys and SortedMerList -------------------------------------------
+@pytest.mark.parametrize("w,rank", [(15, 0), (19, 0), (11, 0), (21, 1), (27, 0)])
+def test_seed_keys_and_sml(gpu_lib, oracle_mod, w, rank):
+    rng = random.Random(w)
+    seqs = [_mutate(rng, s) for s in oracle_mod.generate(2, 30_000, 0.05, 21)]
+    seed = oracle_mod.get_seed(w, rank)
+    with gpu_lib.MemHash(0) as mh:
+        mh.SetSeed(seed)
+        for s in seqs:
+            mh.AddSequence(s)
+        mh.FindStage(gpu_lib.STAGE_SEEDS)
+        for g, s in enumerate(seqs):
+            ref = oracle_mod.seed_keys(s, seed)
+            got = mh.SeedKeys(g, len(ref))
+            assert (got == ref).all()
+            assert (mh.SortedMerList(g, len(ref)) == oracle_mod.build_sml(s, seed)).all()
+
+
+def test_device_resident_input_and_repeatability(gpu_lib, oracle_mod):
+    import torch
+    seqs = oracle_mod.generate(3, 200_000, 0.03, 12345)
+    dev = [torch.frombuffer(bytearray(s), dtype=torch.uint8).cuda() for s in seqs]
+    seed = oracle_mod.get_seed(15)
+    with gpu_lib.MemHash(0) as mh:
+        mh.SetSeed(seed)
+        a = mh.FindMatches(dev)
+        mh.CreateMatches()
+        b = mh.GetMatchList()
+    assert a.text() == b.text() == open(os.path.join(GOLDEN, "g3_200k_p003.txt")).read()
+
+
+def test_c3_scale_seed_stage_properties(gpu_lib, oracle_mod):
+    """BASELINE config 3 shape (8 x 100 Mbp, w19) through the seed stage; size-independent
+    checks: every seed-mer is keyed exactly as the oracle keys sampled windows, the merged
+    SML stream covers each genome's positions exactly once."""
+    import torch
+    G, n = 8, 100_000_000
+    seqs = oracle_mod.generate(G, n, 0.01, 12345)
+    seed = oracle_mod.get_seed(19)
+    dev = [torch.frombuffer(bytearray(s), dtype=torch.uint8).cuda() for s in seqs]
+    with gpu_lib.MemHash(0) as mh:
+        mh.SetSeed(seed)
+        for d in dev:
+            mh.AddSequence(d)
+        mh.FindStage(gpu_lib.STAGE_SEEDS)
+        st = mh.stats()
+        m = n - 27 + 1
+        assert st["seedmers"] == G * m
+        rng = random.Random(1)
+        for g in (0, 2, 7):
+            keys = mh.SeedKeys(g, m)
+            for _ in range(3):
+                a = rng.randrange(0, m - 5000)
+                ref = oracle_mod.seed_keys(seqs[g][a:a + 5000 + 26], seed)
+                assert (keys[a:a + 5000] == ref).all()
+        sml = mh.SortedMerList(5, m)
+        assert np.bincount(sml, minlength=m).max() == 1
+        ks = mh.SeedKeys(5, m)[sml]
+        assert bool(np.all(ks[1:] >= ks[:-1]))
+        assert st["probes"] > 0.9 * m   # related genomes: almost every position is a shared seed
