@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""Benchmark: seed-mers/s sorted+matched on BASELINE config 3 (8 x 100 Mbp, w19) per MI355X.
+
+One step = one pass of the MemHash seed hot path over the whole input: canonical
+spaced-seed keys for every position of every genome, the radix sort that builds
+the G SortedMerLists merged into one key-ordered stream, the equal-key group scan
+with MemHash acceptance, probe construction (SetDirection, CalculateOffset) and the
+stable bucket partition of the probes (SURVEY.md 8(d) "sorted+matched").  Inputs
+(ASCII genomes) are resident in HBM before the timed region.  MUMs/s (full
+FindMatches incl. extension, bucket replay and MatchList output) is reported
+beside it on BASELINE config 2 (4 x 10 Mbp, w15).
+
+    python bench.py [--gpus N --steps K --warmup W]
+For N > 1 launch with torch.distributed.run (one rank per GPU).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402  (loaded before libmums_hip.so: one HIP runtime per process)
+import torch.distributed as dist  # noqa: E402
+
+import libmems_amd as lm  # noqa: E402
+
+METRIC = "seed-mers/sec sorted+matched (+ MUMs/sec) at 1/2/4/8 MI355X; HBM GB/s vs roofline"
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
+PROFILE_SUMMARY = os.path.join(ROOT, "profiles", "r01_dominant_kernel.json")
+
+
+def synth_genomes(G: int, n: int, p: float, seed: int, device: torch.device):
+    """Synthetic related genomes on the GPU: genome 0 iid ACGT; genome g>0 = genome 0 with
+    per-base substitution rate p; genome 2 reverse-complemented (SURVEY.md 8(d) shape)."""
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    lut = torch.tensor(list(b"ACGT"), dtype=torch.uint8, device=device)
+    comp = torch.zeros(256, dtype=torch.uint8, device=device)
+    for a, b in zip(b"ACGT", b"TGCA"):
+        comp[a] = b
+    base = lut[torch.randint(0, 4, (n,), generator=gen, device=device, dtype=torch.int64)]
+    out = [base]
+    for g in range(1, G):
+        mask = torch.rand(n, generator=gen, device=device) < p
+        sub = lut[torch.randint(0, 4, (n,), generator=gen, device=device, dtype=torch.int64)]
+        s = torch.where(mask, sub, base)
+        if g == 2:
+            s = comp[s.flip(0).long()]
+        out.append(s.contiguous())
+    torch.cuda.synchronize()
+    return out
+
+
+def cpu_baseline(seconds_hint: float = 20.0):
+    """Oracle (CPU restatement, 1 thread) on a bounded sample of the same workload shape."""
+    from oracle import oracle
+
+    G, n, p = 8, 4_000_000, 0.01
+    seqs = oracle.generate(G, n, p, 12345)
+    seed = lm.getSeed(19)
+    t0 = time.perf_counter()
+    _, _, st = oracle.find_matches(seqs, seed, seeds_only=True)
+    dt = time.perf_counter() - t0
+    return {
+        "value": st["seedmers"] / dt,
+        "unit": "seed-mers/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"oracle MemHash seed stage (keys+SML sort+merge+accept+probe/bucket), {G} x {n // 10**6} Mbp "
+                  f"related p={p}, w19 seed 0x7b974ef, {st['seedmers']} seed-mers in {dt:.1f} s, 1 thread",
+    }
+
+
+def run_mums(device: int, dev: torch.device):
+    """MUMs/s on BASELINE config 2 (4 x 10 Mbp related, w15): full FindMatches."""
+    seqs = synth_genomes(4, 10_000_000, 0.01, 777, dev)
+    with lm.MemHash(device) as mh:
+        mh.SetSeed(lm.getSeed(15))
+        for s in seqs:
+            mh.AddSequence(s)
+        mh.CreateMatches()  # warm
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        mh.CreateMatches()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        st = mh.stats()
+    return {"mums_per_s": st["mem_count"] / dt, "matches": st["mem_count"], "ms": dt * 1e3,
+            "workload": "4 x 10 Mbp related p=0.01, w15 (BASELINE config 2 shape), full FindMatches",
+            "phase_ms": {k: round(st[k], 3) for k in ("ms_keys", "ms_sort", "ms_groups", "ms_buckets", "ms_replay",
+                                                        "ms_output")}}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--genomes", type=int, default=8)
+    ap.add_argument("--length", type=int, default=100_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-mums", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")   # CPU barrier + max over ranks; the data path has no collective
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    G, n = args.genomes, args.length
+    genomes = synth_genomes(G, n, 0.01, 12345 + rank, dev)
+    mh = lm.MemHash(local)
+    seed = lm.getSeed(19)
+    mh.SetSeed(seed)
+    for s in genomes:
+        mh.AddSequence(s)
+    for _ in range(args.warmup):
+        mh.FindStage(lm.STAGE_SEEDS)
+    mh.SetProfiling(True)
+
+    ms_dom = 0.0
+    bytes_dom = 0
+    launches = 0
+    phase = {"ms_keys": 0.0, "ms_sort": 0.0, "ms_groups": 0.0, "ms_buckets": 0.0}
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        mh.FindStage(lm.STAGE_SEEDS)
+        st = mh.stats()
+        ms_dom += st["ms_dominant"]
+        bytes_dom += st["dominant_bytes"]
+        launches += st["dominant_launches"]
+        for k in phase:
+            phase[k] += st[k]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    tmax = torch.tensor([dt], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    dt = float(tmax.item())
+    seedmers = st["seedmers"]
+    key_bytes = st["key_bytes"]
+    probes = st["probes"]
+    mh.close()
+    del genomes
+
+    if rank == 0:
+        value = world * seedmers * args.steps / dt
+        achieved = bytes_dom / (ms_dom * 1e-3) / 1e9 if ms_dom > 0 else None
+        traffic = None
+        if os.path.exists(PROFILE_SUMMARY):
+            try:
+                traffic = json.load(open(PROFILE_SUMMARY)).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "seed-mers/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64" if key_bytes == 8 else "u32",
+            "data": "synthetic: 8 related genomes generated on the GPU (iid ACGT base, 1% substitutions, genome 2 "
+                    "reverse-complemented)",
+            "config": {"workload": f"BASELINE config 3: {G} x {n // 10**6} Mbp, seed weight 19 (0x7b974ef), "
+                                   f"MemHash seed stage (sorted+matched)",
+                       "genomes": G, "genome_length": n, "seedmers_per_gpu": seedmers, "probes_per_gpu": probes,
+                       "parallelism": f"replicas x{world}" if world > 1 else "1 GPU"},
+            "roofline": {
+                "bound": "hbm",
+                "kernel": f"rs_downsweep<uint{8 * key_bytes}> (seed-key radix sort, {launches // max(args.steps, 1)} "
+                          f"passes/step)",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                "traffic": traffic,
+                "bytes_per_launch": bytes_dom / max(launches, 1),
+                "avg_launch_ms": ms_dom / max(launches, 1),
+            },
+            "phase_ms_per_step": {k: round(v / args.steps, 3) for k, v in phase.items()},
+        }
+        if not args.no_mums:
+            try:
+                out["mums"] = run_mums(local, dev)
+            except Exception as e:  # report, never hide
+                out["mums"] = {"error": str(e)}
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -61,6 +61,14 @@ typedef struct mums_stats {
     double   ms_replay;
     double   ms_output;
     double   ms_total;
+    /* dominant-kernel instrumentation (mums_set_profiling(ctx, 1)): HIP events
+     * around every downsweep launch of the seed-key radix sort, on the
+     * context's stream; bytes = algorithmic HBM bytes of those launches. */
+    double   ms_dominant;
+    uint64_t dominant_launches;
+    uint64_t dominant_bytes;
+    uint64_t key_bytes;         /* 4 (2w+1 <= 32) or 8 */
+    uint64_t sort_passes;
 } mums_stats;
 
 /* MemHash::MemHash (MemHash.cpp:33-49); device = HIP ordinal. */
@@ -101,6 +109,8 @@ int  mums_result_copy(mums_ctx* ctx, uint64_t* lengths, int64_t* starts);
 
 /* MemCount / MemCollisionCount (MemHash.h:94-97) + per-phase device timings. */
 int  mums_get_stats(mums_ctx* ctx, mums_stats* out);
+/* Record HIP events around each dominant-kernel launch (adds a few us per run). */
+int  mums_set_profiling(mums_ctx* ctx, int enable);
 /* Message of the last failing call on this context ("" if none). */
 const char* mums_last_error(mums_ctx* ctx);
 

@@ -69,6 +69,11 @@ class _Stats(ctypes.Structure):
         ("ms_replay", ctypes.c_double),
         ("ms_output", ctypes.c_double),
         ("ms_total", ctypes.c_double),
+        ("ms_dominant", ctypes.c_double),
+        ("dominant_launches", ctypes.c_uint64),
+        ("dominant_bytes", ctypes.c_uint64),
+        ("key_bytes", ctypes.c_uint64),
+        ("sort_passes", ctypes.c_uint64),
     ]
 
 
@@ -77,7 +82,7 @@ EXPORTED_SYMBOLS = [
     "mums_set_params", "mums_set_mask", "mums_add_genome", "mums_add_genome_device", "mums_clear",
     "mums_find", "mums_find_stage", "mums_result_count", "mums_result_copy", "mums_get_stats",
     "mums_last_error", "mums_get_seed", "mums_default_seed_weight", "mums_copy_seed_keys",
-    "mums_build_sml",
+    "mums_build_sml", "mums_set_profiling",
 ]
 
 _lib: Optional[ctypes.CDLL] = None
@@ -122,6 +127,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mums_default_seed_weight.restype = u32
     lib.mums_copy_seed_keys.argtypes = [vp, u32, vp, u64]
     lib.mums_build_sml.argtypes = [vp, u32, vp, u64]
+    lib.mums_set_profiling.argtypes = [vp, i32]
     _lib = lib
     return lib
 
@@ -263,6 +269,9 @@ class MemHash:
         """MemHash::CreateMatches (MemHash.cpp:104-107)."""
         self._check(self._lib.mums_find(self._ctx))
         return True
+
+    def SetProfiling(self, enable: bool) -> None:
+        self._check(self._lib.mums_set_profiling(self._ctx, int(enable)))
 
     def FindStage(self, stage: int) -> None:
         self._check(self._lib.mums_find_stage(self._ctx, stage))

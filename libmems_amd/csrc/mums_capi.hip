@@ -69,6 +69,8 @@ struct mums_ctx {
     DevBuf ckey, kA, kB, vA, vB, tmp, partials, counters;
     DevBuf bstart, bend, tsize, obase, pool, tbl, out_len, out_s;
     hipEvent_t ev[EV_COUNT] = {};
+    bool profiling = false;
+    hipEvent_t ev_ds[16] = {};   // 2 per radix pass (<= 8 passes)
 
     // state of the last run
     int stage_done = 0;
@@ -194,8 +196,12 @@ int run_pipeline(mums_ctx* ctx, int stage) {
 
     // sort: the G SortedMerLists, merged
     int buf = 0;
+    const int passes = (2 * ctx->w + 1 + 7) / 8;
+    if (ctx->profiling && !ctx->ev_ds[0])
+        for (int i = 0; i < 16; ++i) HIPCHK(hipEventCreate(&ctx->ev_ds[i]));
     HIPCHK(radix_sort<K>(ctx->ckey.as<K>(), nullptr, N, 2 * ctx->w + 1, ctx->kA.as<K>(), ctx->vA.as<uint32_t>(),
-                         ctx->kB.as<K>(), ctx->vB.as<uint32_t>(), ctx->tmp.p, &buf, st));
+                         ctx->kB.as<K>(), ctx->vB.as<uint32_t>(), ctx->tmp.p, &buf, st,
+                         ctx->profiling ? ctx->ev_ds : nullptr));
     ctx->sorted_buf = buf;
     const K* skey = buf ? ctx->kB.as<K>() : ctx->kA.as<K>();
     const uint32_t* sidx = buf ? ctx->vB.as<uint32_t>() : ctx->vA.as<uint32_t>();
@@ -284,6 +290,18 @@ int run_pipeline(mums_ctx* ctx, int stage) {
     s.ms_keys = el(EV_START, EV_KEYS);
     s.ms_sort = el(EV_KEYS, EV_SORT);
     s.ms_groups = el(EV_SORT, EV_GROUPS);
+    s.key_bytes = sizeof(K);
+    s.sort_passes = (uint64_t)passes;
+    if (ctx->profiling && N > 0) {
+        // algorithmic bytes per downsweep launch: read K (+V after pass 0), write K+V
+        for (int p = 0; p < passes; ++p) {
+            float ms = 0.f;
+            (void)hipEventElapsedTime(&ms, ctx->ev_ds[2 * p], ctx->ev_ds[2 * p + 1]);
+            s.ms_dominant += ms;
+            s.dominant_bytes += N * (sizeof(K) + (p ? 4 : 0) + sizeof(K) + 4);
+        }
+        s.dominant_launches = (uint64_t)passes;
+    }
     s.ms_buckets = el(EV_GROUPS, EV_BUCKETS);
     if (ctx->stage_done >= MUMS_STAGE_ALL) {
         s.mem_count = ctx->hc.entries;
@@ -335,6 +353,8 @@ int mums_ctx_destroy(mums_ctx* ctx) {
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i < EV_COUNT; ++i)
         if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
+    for (int i = 0; i < 16; ++i)
+        if (ctx->ev_ds[i]) (void)hipEventDestroy(ctx->ev_ds[i]);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return MUMS_OK;
@@ -484,6 +504,12 @@ int mums_get_stats(mums_ctx* ctx, mums_stats* out) {
 }
 
 const char* mums_last_error(mums_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int mums_set_profiling(mums_ctx* ctx, int enable) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    ctx->profiling = enable != 0;
+    return MUMS_OK;
+}
 
 int mums_copy_seed_keys(mums_ctx* ctx, uint32_t genome, uint64_t* out, uint64_t cap) {
     if (check_ctx(ctx)) return MUMS_E_INVALID;

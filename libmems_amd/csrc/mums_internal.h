@@ -86,10 +86,11 @@ hipError_t exclusive_scan_u32(uint32_t* d_data, uint64_t n, void* d_tmp, uint32_
 // implicit indices 0..n-1 when vals_in == nullptr.  Returns which buffer holds
 // the result (0 = A, 1 = B).
 size_t radix_tmp_bytes(uint64_t n);
+// ev_ds (optional): 2 events per pass recorded around each downsweep launch.
 template <typename K>
 hipError_t radix_sort(const K* keys_in, const uint32_t* vals_in, uint64_t n, int bits,
                       K* kA, uint32_t* vA, K* kB, uint32_t* vB, void* d_tmp, int* out_buf,
-                      hipStream_t st);
+                      hipStream_t st, hipEvent_t* ev_ds = nullptr);
 
 // groups.hip
 uint64_t group_tiles(uint64_t N);

@@ -155,7 +155,7 @@ size_t radix_tmp_bytes(uint64_t n) {
 
 template <typename K>
 hipError_t radix_sort(const K* keys_in, const uint32_t* vals_in, uint64_t n, int bits, K* kA, uint32_t* vA,
-                      K* kB, uint32_t* vB, void* d_tmp, int* out_buf, hipStream_t st) {
+                      K* kB, uint32_t* vB, void* d_tmp, int* out_buf, hipStream_t st, hipEvent_t* ev_ds) {
     const int passes = (bits + 7) / 8;
     *out_buf = (passes - 1) % 2;
     if (n == 0 || passes == 0) return hipSuccess;
@@ -171,6 +171,7 @@ hipError_t radix_sort(const K* keys_in, const uint32_t* vals_in, uint64_t n, int
         hipLaunchKernelGGL(rs_upsweep<K>, dim3(nb), dim3(kBlock), 0, st, ksrc, n, shift, hist, nb);
         hipError_t e = exclusive_scan_u32(hist, (uint64_t)kDigits * nb, stmp, nullptr, st);
         if (e != hipSuccess) return e;
+        if (ev_ds) (void)hipEventRecord(ev_ds[2 * p], st);
         if (vsrc == nullptr)
             hipLaunchKernelGGL((rs_downsweep<K, true>), dim3(nb), dim3(kBlock), 0, st, ksrc, vsrc, n, shift, hist,
                                nb, kdst, vdst);
@@ -179,6 +180,7 @@ hipError_t radix_sort(const K* keys_in, const uint32_t* vals_in, uint64_t n, int
                                nb, kdst, vdst);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
+        if (ev_ds) (void)hipEventRecord(ev_ds[2 * p + 1], st);
         ksrc = kdst;
         vsrc = vdst;
     }
@@ -186,8 +188,8 @@ hipError_t radix_sort(const K* keys_in, const uint32_t* vals_in, uint64_t n, int
 }
 
 template hipError_t radix_sort<uint32_t>(const uint32_t*, const uint32_t*, uint64_t, int, uint32_t*, uint32_t*,
-                                         uint32_t*, uint32_t*, void*, int*, hipStream_t);
+                                         uint32_t*, uint32_t*, void*, int*, hipStream_t, hipEvent_t*);
 template hipError_t radix_sort<uint64_t>(const uint64_t*, const uint32_t*, uint64_t, int, uint64_t*, uint32_t*,
-                                         uint64_t*, uint32_t*, void*, int*, hipStream_t);
+                                         uint64_t*, uint32_t*, void*, int*, hipStream_t, hipEvent_t*);
 
 }  // namespace mums

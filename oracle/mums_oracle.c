@@ -408,6 +408,8 @@ struct oracle_result {
 
 typedef struct {
     ext_ctx x;
+    int seeds_only;
+    uint64_t bucket_sum;
     uint32_t table_size;
     bucket_t* buckets;
     mhe_t* pool; uint64_t pool_n, pool_cap;
@@ -455,6 +457,7 @@ static void add_hash_entry(memhash_t* h, mhe_t* p) {
     uint32_t bi = (uint32_t)(((p->offset % T) + T) % T);
     bucket_t* b = &h->buckets[bi];
     ++h->probes;
+    if (h->seeds_only) { h->bucket_sum += bi; return; }
     uint32_t it = lower_bound_mhe(h, b, p);
     if (it != b->n) {
         const mhe_t* e = &h->pool[b->v[it]];
@@ -580,6 +583,7 @@ oracle_result* oracle_find_matches(int G, const char* const* seqs, const uint64_
         h.x.n = lens;
         h.x.gnseqi_end = prm->gnseqi_end_neg1 ? (int64_t)-1 : INT64_MAX;
         h.table_size = prm->table_size ? prm->table_size : 40000;
+        h.seeds_only = prm->seeds_only;
         h.buckets = (bucket_t*)calloc(h.table_size, sizeof(bucket_t));
         int64_t* scratch = (int64_t*)malloc((size_t)G * sizeof(int64_t));
 

@@ -48,6 +48,9 @@ typedef struct oracle_params {
     uint64_t seq_mask;         /* MaskedMemHash::SetMask (0 = no filter)       */
     int      gnseqi_end_neg1;  /* 1: GNSEQI_END == UINT64_MAX (maxlen -1 in    *
                                 *    ExtendMatch); 0: INT64_MAX                 */
+    int      seeds_only;       /* 1: stop after probe construction (keys, SML  *
+                                *    sort, merge, accept, probe + bucket): the  *
+                                *    "sorted+matched" scope of the bench metric */
 } oracle_params;
 
 typedef struct oracle_result oracle_result;

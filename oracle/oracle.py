@@ -30,6 +30,7 @@ class _Params(ctypes.Structure):
         ("masked", ctypes.c_int),
         ("seq_mask", ctypes.c_uint64),
         ("gnseqi_end_neg1", ctypes.c_int),
+        ("seeds_only", ctypes.c_int),
     ]
 
 
@@ -108,12 +109,13 @@ def build_sml(seq: bytes, seed: int) -> np.ndarray:
 
 def find_matches(seqs: Sequence[bytes], seed: int, repeat_tol: int = 0, enum_tol: int = 1,
                  table_size: int = 40000, masked: bool = False, seq_mask: int = 0,
-                 gnseqi_end_neg1: bool = False) -> Tuple[np.ndarray, np.ndarray, dict]:
+                 gnseqi_end_neg1: bool = False, seeds_only: bool = False) -> Tuple[np.ndarray, np.ndarray, dict]:
     """MemHash::FindMatches restated; returns (lengths[M], starts[M,G], counters)."""
     G = len(seqs)
     arr = (ctypes.c_char_p * G)(*seqs)
     lens = (ctypes.c_uint64 * G)(*[len(s) for s in seqs])
-    prm = _Params(seed, repeat_tol, enum_tol, table_size, int(masked), seq_mask, int(gnseqi_end_neg1))
+    prm = _Params(seed, repeat_tol, enum_tol, table_size, int(masked), seq_mask, int(gnseqi_end_neg1),
+                  int(seeds_only))
     L = lib()
     r = L.oracle_find_matches(G, arr, lens, ctypes.byref(prm))
     if not r:
