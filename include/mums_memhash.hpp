@@ -1,0 +1,142 @@
+// mums_memhash.hpp -- header-only C++ mirror of libMems' MemHash / MaskedMemHash over the
+// C ABI in mums.h (libmums_hip.so).  Same member names, argument meaning and error
+// behaviour as the reference (libMems/MemHash.h:38-175, MaskedMemHash.h:25-40,
+// MatchFinder.h:46-118): failures throw (the reference throws gnException
+// InvalidData / "Gap in genome sequence"; here mums::InvalidData / mums::GapInSequence),
+// results come back as a MatchList in the reference's bucket-major order.
+//
+// This is what a C++ caller links against when it does not have libMems itself; the
+// adapter that plugs the same ABI into a real libMems build (HipMemHash : mems::MemHash)
+// is shown in INTEGRATION.md.
+#pragma once
+
+#include <cstdint>
+#include <ostream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "mums.h"
+
+namespace mums {
+
+struct InvalidData : std::runtime_error { using std::runtime_error::runtime_error; };
+struct GapInSequence : std::runtime_error { using std::runtime_error::runtime_error; };
+
+// UngappedLocalAlignment<HybridAbstractMatch<>> reduced to its values (Match.h:26):
+// one length and G signed 1-based starts (0 = NO_MATCH, AbstractMatch.h:27).
+struct Match {
+    uint64_t length = 0;
+    std::vector<int64_t> starts;
+    int64_t Start(uint32_t seqI) const { return starts[seqI]; }
+    uint64_t Length() const { return length; }
+    uint32_t SeqCount() const { return (uint32_t)starts.size(); }
+    uint32_t Multiplicity() const {
+        uint32_t m = 0;
+        for (int64_t s : starts) m += s != 0;
+        return m;
+    }
+};
+
+// operator<< of UngappedLocalAlignment (UngappedLocalAlignment.h:200-206)
+inline std::ostream& operator<<(std::ostream& os, const Match& m) {
+    os << m.length;
+    for (int64_t s : m.starts) os << '\t' << s;
+    return os;
+}
+
+struct MatchList : std::vector<Match> {
+    std::vector<std::string> seq_table;   // genomes in AddSequence order (MatchList.h:107)
+};
+
+class MemHash {
+public:
+    explicit MemHash(int device = 0) {
+        int rc = mums_ctx_create(device, &ctx_);
+        if (rc != MUMS_OK) throw InvalidData("mums_ctx_create failed (no HIP device?)");
+    }
+    virtual ~MemHash() { if (ctx_) mums_ctx_destroy(ctx_); }
+    MemHash(const MemHash&) = delete;
+    MemHash& operator=(const MemHash&) = delete;
+
+    // MemHash::Clear / ClearSequences (MemHash.cpp:80-93)
+    virtual void Clear() { check(mums_clear(ctx_)); }
+    virtual void ClearSequences() { Clear(); }
+    // MemHash::SetTableSize (MemHash.cpp:95-102), tolerances (MemHash.h:125-144)
+    void SetTableSize(uint32_t n) { table_size_ = n; push_params(); }
+    void SetRepeatTolerance(uint32_t t) { repeat_tol_ = t; push_params(); }
+    uint32_t GetRepeatTolerance() const { return repeat_tol_; }
+    void SetEnumerationTolerance(uint32_t t) { enum_tol_ = t; push_params(); }
+    uint32_t GetEnumerationTolerance() const { return enum_tol_; }
+    // seed pattern the SMLs are sorted on (SortedMerList::Create; 0 = default weight)
+    void SetSeed(uint64_t pattern) { check(mums_set_seed(ctx_, pattern)); }
+
+    // MatchFinder::AddSequence (MatchFinder.cpp:59-87): host ASCII, copied to HBM
+    virtual bool AddSequence(const std::string& seq) {
+        check(mums_add_genome(ctx_, seq.data(), seq.size()));
+        return true;
+    }
+    // device-resident ASCII (not copied)
+    bool AddSequenceDevice(const void* d_ascii, uint64_t n) {
+        check(mums_add_genome_device(ctx_, d_ascii, n));
+        return true;
+    }
+
+    // MemHash::FindMatches (MemHash.cpp:109-115): adds ml.seq_table, finds, fills ml
+    virtual void FindMatches(MatchList& ml) {
+        for (const auto& s : ml.seq_table) AddSequence(s);
+        check(mums_find(ctx_));
+        GetMatchList(ml);
+    }
+    // MemHash::CreateMatches (MemHash.cpp:104-107)
+    virtual bool CreateMatches() {
+        check(mums_find(ctx_));
+        return true;
+    }
+    // MemHash::GetMatchList (MemHash.h:182-203): clears the list first
+    void GetMatchList(MatchList& ml) const {
+        ml.clear();
+        uint64_t count = 0;
+        uint32_t G = 0;
+        check(mums_result_count(ctx_, &count, &G));
+        std::vector<uint64_t> len(count);
+        std::vector<int64_t> st(count * G);
+        if (count) check(mums_result_copy(ctx_, len.data(), st.data()));
+        ml.reserve(count);
+        for (uint64_t i = 0; i < count; ++i) {
+            Match m;
+            m.length = len[i];
+            m.starts.assign(st.begin() + i * G, st.begin() + (i + 1) * G);
+            ml.push_back(std::move(m));
+        }
+    }
+    // MemCount / MemCollisionCount (MemHash.h:94-97)
+    uint64_t MemCount() const { return stats().mem_count; }
+    uint64_t MemCollisionCount() const { return stats().collision_count; }
+    mums_stats stats() const {
+        mums_stats s{};
+        check(mums_get_stats(ctx_, &s));
+        return s;
+    }
+    mums_ctx* handle() const { return ctx_; }
+
+protected:
+    void check(int rc) const {
+        if (rc == MUMS_OK) return;
+        std::string msg = mums_last_error(ctx_);
+        if (rc == MUMS_E_GAP) throw GapInSequence(msg);
+        throw InvalidData(msg);
+    }
+    void push_params() { check(mums_set_params(ctx_, repeat_tol_, enum_tol_, table_size_)); }
+    mums_ctx* ctx_ = nullptr;
+    uint32_t repeat_tol_ = 0, enum_tol_ = 1, table_size_ = 40000;
+};
+
+// MaskedMemHash (MaskedMemHash.h:25-40)
+class MaskedMemHash : public MemHash {
+public:
+    explicit MaskedMemHash(int device = 0) : MemHash(device) { check(mums_set_mask(ctx_, 1, 0)); }
+    virtual void SetMask(uint64_t seq_mask) { check(mums_set_mask(ctx_, 1, seq_mask)); }
+};
+
+}  // namespace mums

@@ -1,0 +1,89 @@
+// mums_find.cpp -- C++ host driver over include/mums_memhash.hpp (the reference-language
+// host path).  Generates the SURVEY Appendix-C synthetic genomes (std::mt19937_64) or reads
+// one raw/FASTA sequence per file, runs mums::MemHash / MaskedMemHash on the GPU and prints
+// the MatchList text (UngappedLocalAlignment.h:200-206), one match per line.
+//   mums_find gen G n weight p [mask]        (mask > 0 selects MaskedMemHash)
+//   mums_find files weight f1 f2 ...
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <iostream>
+#include <random>
+#include <sstream>
+#include <string>
+
+#include "mums_memhash.hpp"
+
+static std::vector<std::string> generate(int G, uint64_t n, double p, uint64_t seed) {
+    std::mt19937_64 rng(seed);
+    const char* acgt = "ACGT";
+    std::vector<std::string> g(G);
+    g[0].resize(n);
+    for (uint64_t i = 0; i < n; ++i) g[0][i] = acgt[rng() & 3];
+    for (int k = 1; k < G; ++k) {
+        g[k] = g[0];
+        for (uint64_t i = 0; i < n; ++i)
+            if ((rng() % 1000000) < p * 1e6) g[k][i] = acgt[rng() & 3];
+        if (k == 2) {
+            std::string r(g[k].rbegin(), g[k].rend());
+            for (char& c : r) c = c == 'A' ? 'T' : c == 'C' ? 'G' : c == 'G' ? 'C' : 'A';
+            g[k] = r;
+        }
+    }
+    return g;
+}
+
+static std::string read_seq(const std::string& path) {
+    std::ifstream f(path);
+    std::string line, s;
+    while (std::getline(f, line)) {
+        if (!line.empty() && line[0] == '>') continue;
+        for (char c : line)
+            if (c != '\n' && c != '\r' && c != ' ') s.push_back(c);
+    }
+    return s;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 3) {
+        std::cerr << "usage: mums_find gen G n weight p [mask] | files weight f1 f2 ...\n";
+        return 2;
+    }
+    std::string mode = argv[1];
+    std::vector<std::string> seqs;
+    int weight = 0;
+    uint64_t mask = 0;
+    if (mode == "gen") {
+        int G = atoi(argv[2]);
+        uint64_t n = strtoull(argv[3], nullptr, 10);
+        weight = atoi(argv[4]);
+        double p = atof(argv[5]);
+        if (argc > 6) mask = strtoull(argv[6], nullptr, 0);
+        seqs = generate(G, n, p, 12345);
+    } else {
+        weight = atoi(argv[2]);
+        for (int i = 3; i < argc; ++i) seqs.push_back(read_seq(argv[i]));
+    }
+    try {
+        mums::MaskedMemHash mh(0);   // mask 0 behaves exactly like MemHash
+        if (mask) mh.SetMask(mask);
+        else mums_set_mask(mh.handle(), 0, 0);
+        mh.SetSeed(weight ? (uint64_t)mums_get_seed(weight, 0) : 0);
+        mums::MatchList ml;
+        ml.seq_table = seqs;
+        auto t0 = std::chrono::steady_clock::now();
+        mh.FindMatches(ml);
+        auto t1 = std::chrono::steady_clock::now();
+        std::ostringstream os;
+        for (const auto& m : ml) os << m << '\n';
+        std::cout << os.str();
+        auto st = mh.stats();
+        std::cerr << "matches " << ml.size() << " collisions " << st.collision_count << " ms "
+                  << std::chrono::duration<double, std::milli>(t1 - t0).count() << "\n";
+    } catch (const std::exception& e) {
+        std::cerr << "error: " << e.what() << "\n";
+        return 1;
+    }
+    return 0;
+}
