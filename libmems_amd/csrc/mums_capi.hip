@@ -67,7 +67,7 @@ struct mums_ctx {
     std::string err;
 
     DevBuf ckey, kA, kB, vA, vB, tmp, partials, counters;
-    DevBuf bstart, bend, tsize, obase, pool, tbl, out_len, out_s;
+    DevBuf bstart, bend, tsize, obase, pool, tbl, out_len, out_s, pbuf;
     hipEvent_t ev[EV_COUNT] = {};
     bool profiling = false;
     hipEvent_t ev_ds[16] = {};   // 2 per radix pass (<= 8 passes)
@@ -143,15 +143,16 @@ int seed_len(uint64_t s) {
 
 template <int MG, typename K>
 int run_groups(mums_ctx* ctx, const K* skey, const uint32_t* sidx, const MatchParams& mp, uint32_t* probe_head,
-               uint32_t* probe_bucket, hipStream_t st) {
+               uint32_t* probe_bucket, uint32_t* slot_head, uint32_t* slot_bucket, hipStream_t st) {
     const uint64_t nt = group_tiles(ctx->N);
-    uint32_t* partials = ctx->partials.as<uint32_t>();
+    uint32_t* counts = ctx->partials.as<uint32_t>();
+    uint32_t* offs = counts + nt + 32;
     DevCounters* dc = ctx->counters.as<DevCounters>();
-    HIPCHK((launch_probe_pass<MG, K>(skey, sidx, ctx->N, ctx->gt, mp, ctx->L, partials, probe_head, probe_bucket, dc,
-                                     false, st)));
-    HIPCHK(exclusive_scan_u32(partials, nt, ctx->tmp.p, &dc->nprobes, st));
-    HIPCHK((launch_probe_pass<MG, K>(skey, sidx, ctx->N, ctx->gt, mp, ctx->L, partials, probe_head, probe_bucket, dc,
-                                     true, st)));
+    HIPCHK((launch_probe_tiles<MG, K>(skey, sidx, ctx->N, ctx->gt, mp, ctx->L, counts, slot_head, slot_bucket, dc,
+                                      st)));
+    HIPCHK(hipMemcpyAsync(offs, counts, nt * 4, hipMemcpyDeviceToDevice, st));
+    HIPCHK(exclusive_scan_u32(offs, nt, ctx->tmp.p, &dc->nprobes, st));
+    HIPCHK(launch_probe_compact(ctx->N, counts, offs, slot_head, slot_bucket, probe_head, probe_bucket, st));
     return MUMS_OK;
 }
 
@@ -180,7 +181,10 @@ int run_pipeline(mums_ctx* ctx, int stage) {
     tmpb = std::max(tmpb, radix_tmp_bytes(N / 2 + 1));
     tmpb = std::max(tmpb, scan_tmp_bytes((uint64_t)ctx->table_size));
     HIPCHK(ctx->tmp.ensure(tmpb));
-    HIPCHK(ctx->partials.ensure((group_tiles(N) + 64) * 4));
+    HIPCHK(ctx->partials.ensure((2 * group_tiles(N) + 128) * 4));
+    const uint64_t pcap = N / 2 + 1;
+    const uint64_t nslots = group_slot_count(N);
+    HIPCHK(ctx->pbuf.ensure((4 * pcap + 2 * nslots + 64) * 4));
     HIPCHK(ctx->counters.ensure(sizeof(DevCounters)));
     DevCounters* dc = ctx->counters.as<DevCounters>();
 
@@ -205,21 +209,20 @@ int run_pipeline(mums_ctx* ctx, int stage) {
     ctx->sorted_buf = buf;
     const K* skey = buf ? ctx->kB.as<K>() : ctx->kA.as<K>();
     const uint32_t* sidx = buf ? ctx->vB.as<uint32_t>() : ctx->vA.as<uint32_t>();
-    char* fk = buf ? (char*)ctx->kA.p : (char*)ctx->kB.p;       // free pair for probes
-    char* fv = buf ? (char*)ctx->vA.p : (char*)ctx->vB.p;
     HIPCHK(hipEventRecord(ctx->ev[EV_SORT], st));
 
-    // groups -> probes (P <= N/2: both free buffers hold two P-long uint32 arrays)
-    const uint64_t pcap = N / 2 + 1;
-    uint32_t* bucketA = (uint32_t*)fk;
+    // groups -> probes (P <= N/2)
+    uint32_t* bucketA = ctx->pbuf.as<uint32_t>();
     uint32_t* bucketB = bucketA + pcap;
-    uint32_t* headA = (uint32_t*)fv;
+    uint32_t* headA = bucketB + pcap;
     uint32_t* headB = headA + pcap;
+    uint32_t* slot_head = headB + pcap;
+    uint32_t* slot_bucket = slot_head + nslots;
     int rc;
-    if (G <= 4) rc = run_groups<4, K>(ctx, skey, sidx, mp, headA, bucketA, st);
-    else if (G <= 8) rc = run_groups<8, K>(ctx, skey, sidx, mp, headA, bucketA, st);
-    else if (G <= 16) rc = run_groups<16, K>(ctx, skey, sidx, mp, headA, bucketA, st);
-    else rc = run_groups<32, K>(ctx, skey, sidx, mp, headA, bucketA, st);
+    if (G <= 4) rc = run_groups<4, K>(ctx, skey, sidx, mp, headA, bucketA, slot_head, slot_bucket, st);
+    else if (G <= 8) rc = run_groups<8, K>(ctx, skey, sidx, mp, headA, bucketA, slot_head, slot_bucket, st);
+    else if (G <= 16) rc = run_groups<16, K>(ctx, skey, sidx, mp, headA, bucketA, slot_head, slot_bucket, st);
+    else rc = run_groups<32, K>(ctx, skey, sidx, mp, headA, bucketA, slot_head, slot_bucket, st);
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -230,11 +233,11 @@ int run_pipeline(mums_ctx* ctx, int stage) {
     // probes grouped by hash bucket, key order kept (stable)
     int tbits = 1;
     while (tbits < 32 && ((uint64_t)1 << tbits) < (uint64_t)ctx->table_size) ++tbits;
-    int pbuf = 0;
-    HIPCHK(radix_sort<uint32_t>(bucketA, headA, ctx->P, tbits, bucketB, headB, bucketA, headA, ctx->tmp.p, &pbuf,
+    int pout = 0;
+    HIPCHK(radix_sort<uint32_t>(bucketA, headA, ctx->P, tbits, bucketB, headB, bucketA, headA, ctx->tmp.p, &pout,
                                 st));
-    ctx->sorted_buckets = pbuf ? bucketA : bucketB;
-    ctx->sorted_heads = pbuf ? headA : headB;
+    ctx->sorted_buckets = pout ? bucketA : bucketB;
+    ctx->sorted_heads = pout ? headA : headB;
     HIPCHK(hipEventRecord(ctx->ev[EV_BUCKETS], st));
     ctx->stage_done = MUMS_STAGE_SEEDS;
 
@@ -349,7 +352,7 @@ int mums_ctx_destroy(mums_ctx* ctx) {
     mums_clear(ctx);
     DevBuf* bufs[] = {&ctx->ckey, &ctx->kA, &ctx->kB, &ctx->vA, &ctx->vB, &ctx->tmp, &ctx->partials,
                       &ctx->counters, &ctx->bstart, &ctx->bend, &ctx->tsize, &ctx->obase, &ctx->pool,
-                      &ctx->tbl, &ctx->out_len, &ctx->out_s};
+                      &ctx->tbl, &ctx->out_len, &ctx->out_s, &ctx->pbuf};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i < EV_COUNT; ++i)
         if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
@@ -377,7 +380,8 @@ int mums_set_seed(mums_ctx* ctx, uint64_t pattern) {
 
 int mums_set_params(mums_ctx* ctx, uint32_t repeat_tol, uint32_t enum_tol, uint32_t table_size) {
     if (check_ctx(ctx)) return MUMS_E_INVALID;
-    if (table_size == 0) return fail(ctx, MUMS_E_INVALID, "table size must be > 0");
+    if (table_size == 0 || table_size > 0x7FFFFFFFu)
+        return fail(ctx, MUMS_E_INVALID, "table size must be in [1, 2^31)");
     ctx->repeat_tol = repeat_tol;
     ctx->enum_tol = enum_tol;
     ctx->table_size = table_size;

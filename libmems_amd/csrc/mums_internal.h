@@ -94,10 +94,14 @@ hipError_t radix_sort(const K* keys_in, const uint32_t* vals_in, uint64_t n, int
 
 // groups.hip
 uint64_t group_tiles(uint64_t N);
+uint64_t group_slot_count(uint64_t N);
 template <int MG, typename K>
-hipError_t launch_probe_pass(const K* skey, const uint32_t* sidx, uint64_t N, const GenomeTable& gt,
-                             const MatchParams& mp, int L, uint32_t* partials, uint32_t* probe_head,
-                             uint32_t* probe_bucket, void* counters, bool emit, hipStream_t st);
+hipError_t launch_probe_tiles(const K* skey, const uint32_t* sidx, uint64_t N, const GenomeTable& gt,
+                              const MatchParams& mp, int L, uint32_t* tile_count, uint32_t* slot_head,
+                              uint32_t* slot_bucket, void* counters, hipStream_t st);
+hipError_t launch_probe_compact(uint64_t N, const uint32_t* tile_count, const uint32_t* tile_off,
+                                const uint32_t* slot_head, const uint32_t* slot_bucket, uint32_t* probe_head,
+                                uint32_t* probe_bucket, hipStream_t st);
 
 // replay.hip
 hipError_t launch_bucket_ranges(const uint32_t* sb, uint64_t P, uint32_t* bstart, uint32_t* bend, hipStream_t st);
