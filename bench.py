@@ -185,7 +185,7 @@ def main():
                        "parallelism": f"replicas x{world}" if world > 1 else "1 GPU"},
             "roofline": {
                 "bound": "hbm",
-                "kernel": f"rs_downsweep<uint{8 * key_bytes}> (seed-key radix sort, {launches // max(args.steps, 1)} "
+                "kernel": f"seg_downsweep (packed-record seed-key radix sort, {launches // max(args.steps, 1)} "
                           f"passes/step)",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,

@@ -17,12 +17,13 @@
 // A second kernel concatenates the tiles' slots using the scanned tile counts, so
 // the probes end up in ascending key order = the reference's AddHashEntry order.
 #include "match_device.h"
+#include "seed_device.h"
 
 namespace mums {
 
 namespace {
 
-constexpr int kGTile = 4096;
+constexpr int kGTile = kSegTile;
 constexpr int kGRounds = kGTile / kBlock;
 constexpr int kSlots = kGTile / 2;
 
@@ -48,29 +49,36 @@ __device__ __forceinline__ uint32_t blk_excl_scan(uint32_t v, uint32_t* s_w, uin
     return pre + inc - v;
 }
 
-template <int MG, typename K>
-__global__ __launch_bounds__(kBlock) void probe_tile_kernel(const K* __restrict__ skey, const uint32_t* __restrict__ sidx,
-                                                            uint64_t N, GenomeTable gt, MatchParams mp, int L,
+template <int MG, typename View>
+__global__ __launch_bounds__(kBlock) void probe_tile_kernel(View v, const SegTile* __restrict__ tiles, uint64_t N,
+                                                            GenomeTable gt, MatchParams mp, int L,
                                                             uint32_t* __restrict__ tile_count,
-                                                            uint32_t* __restrict__ slot_head,
+                                                            uint64_t* __restrict__ slot_info,
                                                             uint32_t* __restrict__ slot_bucket,
                                                             DevCounters* __restrict__ ctr) {
     __shared__ uint16_t heads[kGTile];
     __shared__ uint32_t okb[kGTile];        // bucket | (ok << 31) per head (bucket < 2^31)
+    __shared__ uint16_t gsz16[kGTile];
     __shared__ uint32_t wcnt[kGRounds][kBlock / 64];
     __shared__ uint32_t s_w[kBlock / 64];
     __shared__ uint32_t s_red[2];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t tile0 = (uint64_t)blockIdx.x * kGTile;
+    const SegTile td = tiles[blockIdx.x];
+    if (td.count == 0) {
+        if (threadIdx.x == 0) tile_count[blockIdx.x] = 0;
+        return;
+    }
+    const uint64_t tile0 = td.start;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 
     // 1) heads in stream order
     uint32_t hmask = 0;
     #pragma unroll
     for (int r = 0; r < kGRounds; ++r) {
-        const uint64_t i = tile0 + (uint64_t)r * kBlock + threadIdx.x;
+        const uint32_t q = r * kBlock + threadIdx.x;
+        const uint64_t i = tile0 + q;
         bool head = false;
-        if (i < N) head = (i == 0) || ((skey[i] >> 1) != (skey[i - 1] >> 1));
+        if (q < td.count) head = (i == td.bstart) || (v.gkey(i) != v.gkey(i - 1));
         hmask |= (head ? 1u : 0u) << r;
         const uint64_t bal = __ballot(head);
         if (lane == 0) wcnt[r][wv] = (uint32_t)__popcll(bal);
@@ -97,9 +105,10 @@ __global__ __launch_bounds__(kBlock) void probe_tile_kernel(const K* __restrict_
     for (uint32_t j = threadIdx.x; j < H; j += kBlock) {
         Mhe<MG> P;
         uint32_t gsz = 0;
-        const bool ok = build_probe<MG, K>(skey, sidx, N, tile0 + heads[j], gt, mp, L, P, &gsz);
+        const bool ok = build_probe<MG, View>(v, tile0 + heads[j], td.bend, gt, mp, L, P, &gsz);
         nrep += gsz > (uint32_t)kRepeatLimit;
         okb[j] = ok ? (0x80000000u | bucket_of(P.offset, mp.table_size)) : 0u;
+        gsz16[j] = (uint16_t)(gsz > 65535u ? 65535u : gsz);
     }
     if (nrep) atomicAdd(&ctr->repeat_limit, (unsigned long long)nrep);
     __syncthreads();
@@ -109,13 +118,13 @@ __global__ __launch_bounds__(kBlock) void probe_tile_kernel(const K* __restrict_
     const uint64_t sb = (uint64_t)blockIdx.x * kSlots;
     for (uint32_t c = 0; c < H; c += kBlock) {
         const uint32_t j = c + threadIdx.x;
-        const uint32_t v = j < H ? okb[j] : 0u;
-        const uint32_t ok = v >> 31;
+        const uint32_t vv = j < H ? okb[j] : 0u;
+        const uint32_t ok = vv >> 31;
         uint32_t tot;
         const uint32_t o = blk_excl_scan(ok, s_w, &tot);
         if (ok) {
-            slot_head[sb + base + o] = (uint32_t)(tile0 + heads[j]);
-            slot_bucket[sb + base + o] = v & 0x7FFFFFFFu;
+            slot_info[sb + base + o] = (tile0 + heads[j]) | ((uint64_t)gsz16[j] << 32);
+            slot_bucket[sb + base + o] = vv & 0x7FFFFFFFu;
         }
         base += tot;
     }
@@ -127,56 +136,79 @@ __global__ __launch_bounds__(kBlock) void probe_tile_kernel(const K* __restrict_
 
 __global__ __launch_bounds__(kBlock) void probe_compact_kernel(const uint32_t* __restrict__ tile_count,
                                                                const uint32_t* __restrict__ tile_off,
-                                                               const uint32_t* __restrict__ slot_head,
+                                                               const uint64_t* __restrict__ slot_info,
                                                                const uint32_t* __restrict__ slot_bucket,
-                                                               uint32_t* __restrict__ probe_head,
+                                                               uint64_t* __restrict__ probe_info,
                                                                uint32_t* __restrict__ probe_bucket) {
     const uint32_t n = tile_count[blockIdx.x];
     const uint64_t o = tile_off[blockIdx.x];
     const uint64_t sb = (uint64_t)blockIdx.x * kSlots;
     for (uint32_t k = threadIdx.x; k < n; k += kBlock) {
-        probe_head[o + k] = slot_head[sb + k];
+        probe_info[o + k] = slot_info[sb + k];
         probe_bucket[o + k] = slot_bucket[sb + k];
     }
 }
 
+__global__ void flat_tiles_kernel(uint64_t N, uint64_t nt, SegTile* __restrict__ tiles) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nt) return;
+    SegTile d{};
+    d.start = t * kGTile;
+    d.bstart = 0;
+    d.bend = N;
+    const uint64_t rem = N - d.start;
+    d.count = (uint32_t)(rem < (uint64_t)kGTile ? rem : (uint64_t)kGTile);
+    d.hbase = 0;
+    d.ntb = (uint32_t)nt;
+    d.tb = (uint32_t)t;
+    tiles[t] = d;
+}
+
 }  // namespace
 
-uint64_t group_tiles(uint64_t N) { return (N + kGTile - 1) / kGTile; }
-uint64_t group_slot_count(uint64_t N) { return group_tiles(N) * kSlots; }
+uint64_t group_slot_count(uint64_t ntiles) { return ntiles * kSlots; }
 
-template <int MG, typename K>
-hipError_t launch_probe_tiles(const K* skey, const uint32_t* sidx, uint64_t N, const GenomeTable& gt,
-                              const MatchParams& mp, int L, uint32_t* tile_count, uint32_t* slot_head,
+hipError_t launch_flat_tiles(uint64_t N, SegTile* d_tiles, hipStream_t st) {
+    const uint64_t nt = (N + kGTile - 1) / kGTile;
+    if (nt == 0) return hipSuccess;
+    hipLaunchKernelGGL(flat_tiles_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, N, nt, d_tiles);
+    return hipGetLastError();
+}
+
+template <int MG, typename View>
+hipError_t launch_probe_tiles(View v, const SegTile* tiles, uint64_t ntiles, uint64_t N, const GenomeTable& gt,
+                              const MatchParams& mp, int L, uint32_t* tile_count, uint64_t* slot_info,
                               uint32_t* slot_bucket, void* counters, hipStream_t st) {
-    const unsigned nb = (unsigned)group_tiles(N);
-    if (nb == 0) return hipSuccess;
-    hipLaunchKernelGGL((probe_tile_kernel<MG, K>), dim3(nb), dim3(kBlock), 0, st, skey, sidx, N, gt, mp, L,
-                       tile_count, slot_head, slot_bucket, (DevCounters*)counters);
+    if (ntiles == 0) return hipSuccess;
+    hipLaunchKernelGGL((probe_tile_kernel<MG, View>), dim3((unsigned)ntiles), dim3(kBlock), 0, st, v, tiles, N, gt, mp,
+                       L, tile_count, slot_info, slot_bucket, (DevCounters*)counters);
     return hipGetLastError();
 }
 
-hipError_t launch_probe_compact(uint64_t N, const uint32_t* tile_count, const uint32_t* tile_off,
-                                const uint32_t* slot_head, const uint32_t* slot_bucket, uint32_t* probe_head,
+hipError_t launch_probe_compact(uint64_t ntiles, const uint32_t* tile_count, const uint32_t* tile_off,
+                                const uint64_t* slot_info, const uint32_t* slot_bucket, uint64_t* probe_info,
                                 uint32_t* probe_bucket, hipStream_t st) {
-    const unsigned nb = (unsigned)group_tiles(N);
-    if (nb == 0) return hipSuccess;
-    hipLaunchKernelGGL(probe_compact_kernel, dim3(nb), dim3(kBlock), 0, st, tile_count, tile_off, slot_head,
-                       slot_bucket, probe_head, probe_bucket);
+    if (ntiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(probe_compact_kernel, dim3((unsigned)ntiles), dim3(kBlock), 0, st, tile_count, tile_off,
+                       slot_info, slot_bucket, probe_info, probe_bucket);
     return hipGetLastError();
 }
 
-#define MUMS_INST_PROBE(MG, K)                                                                                    \
-    template hipError_t launch_probe_tiles<MG, K>(const K*, const uint32_t*, uint64_t, const GenomeTable&,       \
-                                                  const MatchParams&, int, uint32_t*, uint32_t*, uint32_t*, void*, \
+#define MUMS_INST_PROBE(MG, V)                                                                                     \
+    template hipError_t launch_probe_tiles<MG, V>(V, const SegTile*, uint64_t, uint64_t, const GenomeTable&,      \
+                                                  const MatchParams&, int, uint32_t*, uint64_t*, uint32_t*, void*, \
                                                   hipStream_t);
-MUMS_INST_PROBE(4, uint32_t)
-MUMS_INST_PROBE(8, uint32_t)
-MUMS_INST_PROBE(16, uint32_t)
-MUMS_INST_PROBE(32, uint32_t)
-MUMS_INST_PROBE(4, uint64_t)
-MUMS_INST_PROBE(8, uint64_t)
-MUMS_INST_PROBE(16, uint64_t)
-MUMS_INST_PROBE(32, uint64_t)
+MUMS_INST_PROBE(4, PairView<uint32_t>)
+MUMS_INST_PROBE(8, PairView<uint32_t>)
+MUMS_INST_PROBE(16, PairView<uint32_t>)
+MUMS_INST_PROBE(32, PairView<uint32_t>)
+MUMS_INST_PROBE(4, PairView<uint64_t>)
+MUMS_INST_PROBE(8, PairView<uint64_t>)
+MUMS_INST_PROBE(16, PairView<uint64_t>)
+MUMS_INST_PROBE(32, PairView<uint64_t>)
+MUMS_INST_PROBE(4, RecView)
+MUMS_INST_PROBE(8, RecView)
+MUMS_INST_PROBE(16, RecView)
+MUMS_INST_PROBE(32, RecView)
 
 }  // namespace mums

@@ -124,17 +124,17 @@ __device__ __forceinline__ uint32_t lower_bound_tbl(const uint32_t* tbl, uint32_
     return first;
 }
 
-// Build the seed probe of a masked-key group whose first sorted record is h.
-// MemHash::EnumerateMatches (MemHash.cpp:139-162) acceptance with enum_tol == 1,
+// Build the seed probe of a masked-key group whose first record in the sorted
+// stream is h (records of the group lie in [h, end)).
+// MemHash::EnumerateMatches (MemHash.cpp:139-162) acceptance with enum_tol <= 1,
 // HashMatch (:167-187) / MaskedMemHash::HashMatch (MaskedMemHash.cpp:38-63),
 // SetDirection (:189-203), CalculateOffset (MatchHashEntry.cpp:141-160).
 // Returns false when the group yields no AddHashEntry call.
 // *gsize receives the group size (counted up to kRepeatLimit + 1).
-template <int MG, typename K>
-__device__ __forceinline__ bool build_probe(const K* __restrict__ skey, const uint32_t* __restrict__ sidx, uint64_t N,
-                                            uint64_t h, const GenomeTable& gt, const MatchParams& mp, int L,
-                                            Mhe<MG>& P, uint32_t* gsize) {
-    const K v0 = skey[h] >> 1;
+template <int MG, typename View>
+__device__ __forceinline__ bool build_probe(const View& v, uint64_t h, uint64_t end, const GenomeTable& gt,
+                                            const MatchParams& mp, int L, Mhe<MG>& P, uint32_t* gsize) {
+    const uint64_t k0 = v.gkey(h);
     const uint32_t maxc = (uint32_t)gt.G * (mp.repeat_tol + 1u);
     uint32_t tally[MG];
     int64_t pos1[MG];
@@ -143,9 +143,8 @@ __device__ __forceinline__ bool build_probe(const K* __restrict__ skey, const ui
     for (int g = 0; g < MG; ++g) { tally[g] = 0; pos1[g] = 0; par[g] = 0; }
     uint32_t cnt = 0, nh = 0;
     bool reject = false;
-    for (uint64_t i = h; i < N; ++i) {
-        const K k = skey[i];
-        if ((k >> 1) != v0) break;
+    for (uint64_t i = h; i < end; ++i) {
+        if (v.gkey(i) != k0) break;
         ++cnt;
         if (cnt > maxc) {
             // some genome exceeds repeat_tol+1 occurrences: rejected.  Keep
@@ -155,13 +154,14 @@ __device__ __forceinline__ bool build_probe(const K* __restrict__ skey, const ui
             continue;
         }
         if (reject) continue;
-        const uint64_t gi = sidx[i];
+        const uint64_t gi = v.gidx(i);
         const int g = genome_of(gt, gi);
         const int64_t p = (int64_t)(gi - gt.base[g]);
+        const uint32_t pb = v.par(i);
         #pragma unroll
         for (int q = 0; q < MG; ++q) {
             if (q != g) continue;
-            if (tally[q] < mp.enum_tol) { pos1[q] = p + 1; par[q] = (uint32_t)(k & 1); ++nh; }
+            if (tally[q] < mp.enum_tol) { pos1[q] = p + 1; par[q] = pb; ++nh; }
             if (tally[q] > mp.repeat_tol) reject = true;
             ++tally[q];
         }

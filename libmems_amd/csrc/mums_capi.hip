@@ -20,6 +20,7 @@
 
 #include "../../include/mums.h"
 #include "mums_internal.h"
+#include "seed_device.h"
 
 using namespace mums;
 
@@ -66,8 +67,9 @@ struct mums_ctx {
     std::vector<GenomeIn> genomes;
     std::string err;
 
-    DevBuf ckey, kA, kB, vA, vB, tmp, partials, counters;
-    DevBuf bstart, bend, tsize, obase, pool, tbl, out_len, out_s, pbuf;
+    DevBuf packed, recA, recB, hist, tiles, ckey, kA, kB, vA, vB, tmp, partials, counters;
+    DevBuf bstart, bend, tsize, obase, pool, tbl, out_len, out_s, pbuf, keybuf, mstart;
+    bool use_onesweep = true;
     hipEvent_t ev[EV_COUNT] = {};
     bool profiling = false;
     hipEvent_t ev_ds[16] = {};   // 2 per radix pass (<= 8 passes)
@@ -75,14 +77,21 @@ struct mums_ctx {
     // state of the last run
     int stage_done = 0;
     bool key64 = false;
+    bool packed_path = false;
+    int msd_bits = 0;
     int L = 0, w = 0;
     uint64_t pattern = 0, N = 0, P = 0, M = 0;
     int sorted_buf = 0;
+    const uint64_t* sorted_rec = nullptr;   // packed path
+    const void* sorted_key = nullptr;       // pair path
+    const uint32_t* sorted_idx = nullptr;
     GenomeTable gt{};
+    SeedSpec ss{};
     DevCounters hc{};
     mums_stats st{};
-    const uint32_t* sorted_heads = nullptr;
+    const uint32_t* sorted_ids = nullptr;
     const uint32_t* sorted_buckets = nullptr;
+    const uint64_t* probe_info = nullptr;
 };
 
 namespace {
@@ -141,136 +150,231 @@ int seed_len(uint64_t s) {
     return hi - lo + 1;
 }
 
-template <int MG, typename K>
-int run_groups(mums_ctx* ctx, const K* skey, const uint32_t* sidx, const MatchParams& mp, uint32_t* probe_head,
-               uint32_t* probe_bucket, uint32_t* slot_head, uint32_t* slot_bucket, hipStream_t st) {
-    const uint64_t nt = group_tiles(ctx->N);
+// probes of the merged stream -> probe_info/probe_bucket (ascending key order)
+template <int MG, typename View>
+int run_groups(mums_ctx* ctx, View v, const SegTile* tiles, uint64_t ntiles, const MatchParams& mp,
+               uint64_t* probe_info, uint32_t* probe_bucket, uint64_t* slot_info, uint32_t* slot_bucket,
+               hipStream_t st) {
     uint32_t* counts = ctx->partials.as<uint32_t>();
-    uint32_t* offs = counts + nt + 32;
+    uint32_t* offs = counts + ntiles + 32;
     DevCounters* dc = ctx->counters.as<DevCounters>();
-    HIPCHK((launch_probe_tiles<MG, K>(skey, sidx, ctx->N, ctx->gt, mp, ctx->L, counts, slot_head, slot_bucket, dc,
-                                      st)));
-    HIPCHK(hipMemcpyAsync(offs, counts, nt * 4, hipMemcpyDeviceToDevice, st));
-    HIPCHK(exclusive_scan_u32(offs, nt, ctx->tmp.p, &dc->nprobes, st));
-    HIPCHK(launch_probe_compact(ctx->N, counts, offs, slot_head, slot_bucket, probe_head, probe_bucket, st));
+    HIPCHK((launch_probe_tiles<MG, View>(v, tiles, ntiles, ctx->N, ctx->gt, mp, ctx->L, counts, slot_info, slot_bucket,
+                                         dc, st)));
+    HIPCHK(hipMemcpyAsync(offs, counts, ntiles * 4, hipMemcpyDeviceToDevice, st));
+    HIPCHK(exclusive_scan_u32(offs, ntiles, ctx->tmp.p, &dc->nprobes, st));
+    HIPCHK(launch_probe_compact(ntiles, counts, offs, slot_info, slot_bucket, probe_info, probe_bucket, st));
     return MUMS_OK;
 }
 
-template <int MG, typename K>
-int run_replay(mums_ctx* ctx, const K* skey, const uint32_t* sidx, const MatchParams& mp, hipStream_t st) {
-    HIPCHK((launch_replay<MG, K>(skey, sidx, ctx->N, ctx->gt, mp, ctx->L, ctx->sorted_heads, ctx->bstart.as<uint32_t>(),
-                                 ctx->bend.as<uint32_t>(), ctx->tbl.as<uint32_t>(), ctx->pool.as<int64_t>(),
-                                 ctx->ckey.as<K>(), ctx->tsize.as<uint32_t>(), ctx->counters.p, st)));
+template <typename View>
+int groups_dispatch(mums_ctx* ctx, View v, const SegTile* tiles, uint64_t ntiles, const MatchParams& mp,
+                    uint64_t* pi, uint32_t* pb, uint64_t* si, uint32_t* sb, hipStream_t st) {
+    const int G = (int)ctx->genomes.size();
+    if (G <= 4) return run_groups<4, View>(ctx, v, tiles, ntiles, mp, pi, pb, si, sb, st);
+    if (G <= 8) return run_groups<8, View>(ctx, v, tiles, ntiles, mp, pi, pb, si, sb, st);
+    if (G <= 16) return run_groups<16, View>(ctx, v, tiles, ntiles, mp, pi, pb, si, sb, st);
+    return run_groups<32, View>(ctx, v, tiles, ntiles, mp, pi, pb, si, sb, st);
+}
+
+template <typename View>
+int replay_dispatch(mums_ctx* ctx, View v, const MatchParams& mp, hipStream_t st) {
+    const int G = (int)ctx->genomes.size();
+#define MUMS_REPLAY_CALL(MG)                                                                                        \
+    HIPCHK((launch_replay<MG, View>(v, ctx->N, ctx->gt, mp, ctx->ss, ctx->probe_info, ctx->sorted_ids,              \
+                                    ctx->bstart.as<uint32_t>(), ctx->bend.as<uint32_t>(), ctx->tbl.as<uint32_t>(),  \
+                                    ctx->pool.as<int64_t>(), ctx->packed.as<uint32_t>(), ctx->tsize.as<uint32_t>(), \
+                                    ctx->counters.p, st)))
+    if (G <= 4) MUMS_REPLAY_CALL(4);
+    else if (G <= 8) MUMS_REPLAY_CALL(8);
+    else if (G <= 16) MUMS_REPLAY_CALL(16);
+    else MUMS_REPLAY_CALL(32);
+#undef MUMS_REPLAY_CALL
     return MUMS_OK;
 }
 
-template <typename K>
+// keys -> sorted stream -> probes -> bucket-sorted probes [-> replay -> MatchList]
 int run_pipeline(mums_ctx* ctx, int stage) {
     hipStream_t st = ctx->stream;
     const int G = (int)ctx->genomes.size();
     const uint64_t N = ctx->N;
     MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, ctx->masked, ctx->seq_mask};
+    GenomeTable& gt = ctx->gt;
 
-    // workspace (grow-only; no allocation in steady state)
-    HIPCHK(ctx->ckey.ensure(N * sizeof(K) + 64));
-    HIPCHK(ctx->kA.ensure(N * sizeof(K) + 64));
-    HIPCHK(ctx->kB.ensure(N * sizeof(K) + 64));
-    HIPCHK(ctx->vA.ensure(N * 4 + 64));
-    HIPCHK(ctx->vB.ensure(N * 4 + 64));
-    size_t tmpb = std::max(radix_tmp_bytes(N), scan_tmp_bytes(N));
-    tmpb = std::max(tmpb, radix_tmp_bytes(N / 2 + 1));
-    tmpb = std::max(tmpb, scan_tmp_bytes((uint64_t)ctx->table_size));
-    HIPCHK(ctx->tmp.ensure(tmpb));
-    HIPCHK(ctx->partials.ensure((2 * group_tiles(N) + 128) * 4));
-    const uint64_t pcap = N / 2 + 1;
-    const uint64_t nslots = group_slot_count(N);
-    HIPCHK(ctx->pbuf.ensure((4 * pcap + 2 * nslots + 64) * 4));
+    // packed genomes + key-kernel tiles
+    uint64_t words = 0;
+    uint32_t T = 0;
+    for (int g = 0; g < G; ++g) {
+        gt.woff[g] = words;
+        words += (packed_words(gt.n[g]) + 3) & ~3ull;
+        gt.tfirst[g] = T;
+        T += (uint32_t)((gt.n[g] + kSeedTile - 1) / kSeedTile);
+    }
+    gt.woff[G] = words;
+    for (int g = G; g <= kMaxG; ++g) gt.tfirst[g] = T;
+    HIPCHK(ctx->packed.ensure(words * 4 + 64));
     HIPCHK(ctx->counters.ensure(sizeof(DevCounters)));
     DevCounters* dc = ctx->counters.as<DevCounters>();
+    std::vector<const char*> ptrs(G);
+    for (int g = 0; g < G; ++g) ptrs[g] = ctx->genomes[g].d_ptr;
+    const SeedSpec& ss = ctx->ss;
+
+    const int kbits = 2 * ctx->w + 1;
+    ctx->packed_path = kbits <= 32 + kMaxMsdBits;
+    ctx->msd_bits = ctx->packed_path ? std::max(0, kbits - 32) : 0;
+    const int B = ctx->msd_bits;
+    const int passes = ctx->packed_path ? (kbits - B + 7) / 8 : (kbits + 7) / 8;
+    const size_t kb = ctx->key64 ? 8 : 4;
+    const uint64_t ntiles_groups = ctx->packed_path ? seg_tiles_upper(N, B) : (N + kSegTile - 1) / kSegTile;
+    const uint64_t pcap = N / 2 + 1;
+    const uint64_t nslots = group_slot_count(ntiles_groups);
+
+    // workspace (grow-only; no allocation in steady state)
+    size_t tmpb = std::max(scan_tmp_bytes(N), radix_tmp_bytes(pcap));
+    tmpb = std::max(tmpb, scan_tmp_bytes((uint64_t)ctx->table_size));
+    if (ctx->packed_path) {
+        HIPCHK(ctx->recA.ensure(N * 8 + 64));
+        HIPCHK(ctx->recB.ensure(N * 8 + 64));
+        HIPCHK(ctx->tiles.ensure(ntiles_groups * sizeof(SegTile) + 64));
+        if (B > 0) HIPCHK(ctx->hist.ensure(((uint64_t)T << B) * 4 + 64));
+        tmpb = std::max(tmpb, seg_tmp_bytes(N, B));
+        tmpb = std::max(tmpb, onesweep_tmp_bytes(N, B, kbits - B));
+        HIPCHK(ctx->mstart.ensure(((1ull << B) + 64) * 4));
+        tmpb = std::max(tmpb, scan_tmp_bytes((uint64_t)T << B));
+    } else {
+        HIPCHK(ctx->ckey.ensure(N * kb + 64));
+        HIPCHK(ctx->kA.ensure(N * kb + 64));
+        HIPCHK(ctx->kB.ensure(N * kb + 64));
+        HIPCHK(ctx->vA.ensure(N * 4 + 64));
+        HIPCHK(ctx->vB.ensure(N * 4 + 64));
+        HIPCHK(ctx->tiles.ensure(ntiles_groups * sizeof(SegTile) + 64));
+        tmpb = std::max(tmpb, radix_tmp_bytes(N));
+    }
+    HIPCHK(ctx->tmp.ensure(tmpb));
+    HIPCHK(ctx->partials.ensure((2 * ntiles_groups + 128) * 4));
+    HIPCHK(ctx->pbuf.ensure(pcap * (8 + 4 * 4) + nslots * 12 + 256));
+    char* pb = (char*)ctx->pbuf.p;
+    uint64_t* probe_info = (uint64_t*)pb;
+    uint64_t* slot_info = probe_info + pcap;
+    uint32_t* probe_bucket = (uint32_t*)(slot_info + nslots);
+    uint32_t* bucketB = probe_bucket + pcap;
+    uint32_t* idsA = bucketB + pcap;
+    uint32_t* idsB = idsA + pcap;
+    uint32_t* slot_bucket = idsB + pcap;
 
     HIPCHK(hipEventRecord(ctx->ev[EV_START], st));
     HIPCHK(hipMemsetAsync(dc, 0, sizeof(DevCounters), st));
-
-    // keys
-    std::vector<const char*> ptrs(G);
-    for (int g = 0; g < G; ++g) ptrs[g] = ctx->genomes[g].d_ptr;
-    SeedSpec ss = make_seed_spec(ctx->pattern, ctx->L, ctx->w);
-    HIPCHK(launch_seed_keys(ss, ctx->gt, ptrs.data(), ctx->ckey.p, sizeof(K) == 8, &dc->err, st));
-    HIPCHK(hipEventRecord(ctx->ev[EV_KEYS], st));
-
-    // sort: the G SortedMerLists, merged
-    int buf = 0;
-    const int passes = (2 * ctx->w + 1 + 7) / 8;
-    if (ctx->profiling && !ctx->ev_ds[0])
+    const bool prof = ctx->profiling;
+    if (prof && !ctx->ev_ds[0])
         for (int i = 0; i < 16; ++i) HIPCHK(hipEventCreate(&ctx->ev_ds[i]));
-    HIPCHK(radix_sort<K>(ctx->ckey.as<K>(), nullptr, N, 2 * ctx->w + 1, ctx->kA.as<K>(), ctx->vA.as<uint32_t>(),
-                         ctx->kB.as<K>(), ctx->vB.as<uint32_t>(), ctx->tmp.p, &buf, st,
-                         ctx->profiling ? ctx->ev_ds : nullptr));
-    ctx->sorted_buf = buf;
-    const K* skey = buf ? ctx->kB.as<K>() : ctx->kA.as<K>();
-    const uint32_t* sidx = buf ? ctx->vB.as<uint32_t>() : ctx->vA.as<uint32_t>();
-    HIPCHK(hipEventRecord(ctx->ev[EV_SORT], st));
 
-    // groups -> probes (P <= N/2)
-    uint32_t* bucketA = ctx->pbuf.as<uint32_t>();
-    uint32_t* bucketB = bucketA + pcap;
-    uint32_t* headA = bucketB + pcap;
-    uint32_t* headB = headA + pcap;
-    uint32_t* slot_head = headB + pcap;
-    uint32_t* slot_bucket = slot_head + nslots;
-    int rc;
-    if (G <= 4) rc = run_groups<4, K>(ctx, skey, sidx, mp, headA, bucketA, slot_head, slot_bucket, st);
-    else if (G <= 8) rc = run_groups<8, K>(ctx, skey, sidx, mp, headA, bucketA, slot_head, slot_bucket, st);
-    else if (G <= 16) rc = run_groups<16, K>(ctx, skey, sidx, mp, headA, bucketA, slot_head, slot_bucket, st);
-    else rc = run_groups<32, K>(ctx, skey, sidx, mp, headA, bucketA, slot_head, slot_bucket, st);
+    int rc = MUMS_OK;
+    if (ctx->packed_path) {
+        SegTile* tiles = ctx->tiles.as<SegTile>();
+        uint32_t* hist = ctx->hist.as<uint32_t>();
+        HIPCHK(launch_seed_pack(ss, gt, ptrs.data(), ctx->packed.as<uint32_t>(), 1, true, nullptr, B, hist, T,
+                                &dc->err, st));
+        if (B > 0) HIPCHK(exclusive_scan_u32(hist, (uint64_t)T << B, ctx->tmp.p, nullptr, st));
+        HIPCHK(launch_seed_scatter(ss, gt, ctx->packed.as<uint32_t>(), B, hist, T, ctx->recA.as<uint64_t>(), st));
+        HIPCHK(hipEventRecord(ctx->ev[EV_KEYS], st));
+        HIPCHK(build_seg_tiles(B > 0 ? hist : nullptr, T, B, N, tiles, &dc->ntiles, ctx->mstart.as<uint32_t>(),
+                               ctx->tmp.p, st));
+        int buf = 0;
+        if (ctx->use_onesweep && N < (1ull << 30) && kbits - B <= 32)
+            HIPCHK(seg_onesweep_sort(ctx->recA.as<uint64_t>(), ctx->recB.as<uint64_t>(), N, kbits - B, B, tiles,
+                                     ntiles_groups, ctx->mstart.as<uint32_t>(), ctx->tmp.p, &dc->err, &buf, st,
+                                     prof ? ctx->ev_ds : nullptr));
+        else
+            HIPCHK(seg_radix_sort(ctx->recA.as<uint64_t>(), ctx->recB.as<uint64_t>(), N, kbits - B, tiles,
+                                  ntiles_groups, ctx->tmp.p, &buf, st, prof ? ctx->ev_ds : nullptr));
+        ctx->sorted_buf = buf;
+        ctx->sorted_rec = buf ? ctx->recB.as<uint64_t>() : ctx->recA.as<uint64_t>();
+        HIPCHK(hipEventRecord(ctx->ev[EV_SORT], st));
+        rc = groups_dispatch<RecView>(ctx, RecView{ctx->sorted_rec}, tiles, ntiles_groups, mp, probe_info,
+                                      probe_bucket, slot_info, slot_bucket, st);
+    } else {
+        HIPCHK(launch_seed_pack(ss, gt, ptrs.data(), ctx->packed.as<uint32_t>(), 0, ctx->key64, ctx->ckey.p, 0,
+                                nullptr, T, &dc->err, st));
+        HIPCHK(hipEventRecord(ctx->ev[EV_KEYS], st));
+        int buf = 0;
+        SegTile* tiles = ctx->tiles.as<SegTile>();
+        HIPCHK(launch_flat_tiles(N, tiles, st));
+        if (ctx->key64) {
+            HIPCHK(radix_sort<uint64_t>(ctx->ckey.as<uint64_t>(), nullptr, N, kbits, ctx->kA.as<uint64_t>(),
+                                        ctx->vA.as<uint32_t>(), ctx->kB.as<uint64_t>(), ctx->vB.as<uint32_t>(),
+                                        ctx->tmp.p, &buf, st, prof ? ctx->ev_ds : nullptr));
+        } else {
+            HIPCHK(radix_sort<uint32_t>(ctx->ckey.as<uint32_t>(), nullptr, N, kbits, ctx->kA.as<uint32_t>(),
+                                        ctx->vA.as<uint32_t>(), ctx->kB.as<uint32_t>(), ctx->vB.as<uint32_t>(),
+                                        ctx->tmp.p, &buf, st, prof ? ctx->ev_ds : nullptr));
+        }
+        ctx->sorted_buf = buf;
+        ctx->sorted_key = buf ? ctx->kB.p : ctx->kA.p;
+        ctx->sorted_idx = buf ? ctx->vB.as<uint32_t>() : ctx->vA.as<uint32_t>();
+        HIPCHK(hipEventRecord(ctx->ev[EV_SORT], st));
+        if (ctx->key64)
+            rc = groups_dispatch<PairView<uint64_t>>(ctx, PairView<uint64_t>{(const uint64_t*)ctx->sorted_key,
+                                                                             ctx->sorted_idx},
+                                                     tiles, ntiles_groups, mp, probe_info, probe_bucket, slot_info,
+                                                     slot_bucket, st);
+        else
+            rc = groups_dispatch<PairView<uint32_t>>(ctx, PairView<uint32_t>{(const uint32_t*)ctx->sorted_key,
+                                                                             ctx->sorted_idx},
+                                                     tiles, ntiles_groups, mp, probe_info, probe_bucket, slot_info,
+                                                     slot_bucket, st);
+    }
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     if (ctx->hc.err & 1u) return fail(ctx, MUMS_E_GAP, "Gap in genome sequence ('-' encountered)");
+    if (ctx->hc.err & 2u) return fail(ctx, MUMS_E_HIP, "sort look-back timed out (internal error)");
     ctx->P = ctx->hc.nprobes;
+    ctx->probe_info = probe_info;
     HIPCHK(hipEventRecord(ctx->ev[EV_GROUPS], st));
 
-    // probes grouped by hash bucket, key order kept (stable)
+    // probes grouped by hash bucket, key order kept (stable); values = probe ids
     int tbits = 1;
     while (tbits < 32 && ((uint64_t)1 << tbits) < (uint64_t)ctx->table_size) ++tbits;
     int pout = 0;
-    HIPCHK(radix_sort<uint32_t>(bucketA, headA, ctx->P, tbits, bucketB, headB, bucketA, headA, ctx->tmp.p, &pout,
-                                st));
-    ctx->sorted_buckets = pout ? bucketA : bucketB;
-    ctx->sorted_heads = pout ? headA : headB;
+    HIPCHK(radix_sort<uint32_t>(probe_bucket, nullptr, ctx->P, tbits, bucketB, idsA, probe_bucket, idsB, ctx->tmp.p,
+                                &pout, st));
+    ctx->sorted_buckets = pout ? probe_bucket : bucketB;
+    ctx->sorted_ids = pout ? idsB : idsA;
     HIPCHK(hipEventRecord(ctx->ev[EV_BUCKETS], st));
     ctx->stage_done = MUMS_STAGE_SEEDS;
 
     if (stage >= MUMS_STAGE_ALL) {
-        const uint32_t T = ctx->table_size;
-        HIPCHK(ctx->bstart.ensure((size_t)T * 4));
-        HIPCHK(ctx->bend.ensure((size_t)T * 4));
-        HIPCHK(ctx->tsize.ensure((size_t)T * 4));
-        HIPCHK(ctx->obase.ensure((size_t)T * 4 + 64));
+        const uint32_t Tb = ctx->table_size;
+        HIPCHK(ctx->bstart.ensure((size_t)Tb * 4));
+        HIPCHK(ctx->bend.ensure((size_t)Tb * 4));
+        HIPCHK(ctx->tsize.ensure((size_t)Tb * 4));
+        HIPCHK(ctx->obase.ensure((size_t)Tb * 4 + 64));
         HIPCHK(ctx->pool.ensure((ctx->P + 1) * (size_t)(G + 2) * 8));
         HIPCHK(ctx->tbl.ensure((ctx->P + 1) * 4));
-        HIPCHK(hipMemsetAsync(ctx->bstart.p, 0, (size_t)T * 4, st));
-        HIPCHK(hipMemsetAsync(ctx->bend.p, 0, (size_t)T * 4, st));
-        HIPCHK(hipMemsetAsync(ctx->tsize.p, 0, (size_t)T * 4, st));
+        HIPCHK(hipMemsetAsync(ctx->bstart.p, 0, (size_t)Tb * 4, st));
+        HIPCHK(hipMemsetAsync(ctx->bend.p, 0, (size_t)Tb * 4, st));
+        HIPCHK(hipMemsetAsync(ctx->tsize.p, 0, (size_t)Tb * 4, st));
         HIPCHK(launch_bucket_ranges(ctx->sorted_buckets, ctx->P, ctx->bstart.as<uint32_t>(), ctx->bend.as<uint32_t>(),
                                     st));
         if (ctx->P > 0) {
-            if (G <= 4) rc = run_replay<4, K>(ctx, skey, sidx, mp, st);
-            else if (G <= 8) rc = run_replay<8, K>(ctx, skey, sidx, mp, st);
-            else if (G <= 16) rc = run_replay<16, K>(ctx, skey, sidx, mp, st);
-            else rc = run_replay<32, K>(ctx, skey, sidx, mp, st);
+            if (ctx->packed_path) rc = replay_dispatch<RecView>(ctx, RecView{ctx->sorted_rec}, mp, st);
+            else if (ctx->key64)
+                rc = replay_dispatch<PairView<uint64_t>>(
+                    ctx, PairView<uint64_t>{(const uint64_t*)ctx->sorted_key, ctx->sorted_idx}, mp, st);
+            else
+                rc = replay_dispatch<PairView<uint32_t>>(
+                    ctx, PairView<uint32_t>{(const uint32_t*)ctx->sorted_key, ctx->sorted_idx}, mp, st);
             if (rc) return rc;
         }
         HIPCHK(hipEventRecord(ctx->ev[EV_REPLAY], st));
-        HIPCHK(hipMemcpyAsync(ctx->obase.p, ctx->tsize.p, (size_t)T * 4, hipMemcpyDeviceToDevice, st));
-        HIPCHK(exclusive_scan_u32(ctx->obase.as<uint32_t>(), T, ctx->tmp.p, &dc->nmatches, st));
+        HIPCHK(hipMemcpyAsync(ctx->obase.p, ctx->tsize.p, (size_t)Tb * 4, hipMemcpyDeviceToDevice, st));
+        HIPCHK(exclusive_scan_u32(ctx->obase.as<uint32_t>(), Tb, ctx->tmp.p, &dc->nmatches, st));
         HIPCHK(hipMemcpyAsync(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         ctx->M = ctx->hc.nmatches;
         HIPCHK(ctx->out_len.ensure((ctx->M + 1) * 8));
         HIPCHK(ctx->out_s.ensure((ctx->M + 1) * (size_t)G * 8));
         HIPCHK(launch_emit(ctx->tsize.as<uint32_t>(), ctx->obase.as<uint32_t>(), ctx->bstart.as<uint32_t>(),
-                           ctx->tbl.as<uint32_t>(), ctx->pool.as<int64_t>(), G, T, ctx->out_len.as<uint64_t>(),
+                           ctx->tbl.as<uint32_t>(), ctx->pool.as<int64_t>(), G, Tb, ctx->out_len.as<uint64_t>(),
                            ctx->out_s.as<int64_t>(), st));
         HIPCHK(hipEventRecord(ctx->ev[EV_OUTPUT], st));
         ctx->stage_done = MUMS_STAGE_ALL;
@@ -293,19 +397,20 @@ int run_pipeline(mums_ctx* ctx, int stage) {
     s.ms_keys = el(EV_START, EV_KEYS);
     s.ms_sort = el(EV_KEYS, EV_SORT);
     s.ms_groups = el(EV_SORT, EV_GROUPS);
-    s.key_bytes = sizeof(K);
+    s.ms_buckets = el(EV_GROUPS, EV_BUCKETS);
+    s.key_bytes = ctx->packed_path ? 8 : kb;
     s.sort_passes = (uint64_t)passes;
-    if (ctx->profiling && N > 0) {
-        // algorithmic bytes per downsweep launch: read K (+V after pass 0), write K+V
+    if (prof && N > 0) {
         for (int p = 0; p < passes; ++p) {
             float ms = 0.f;
             (void)hipEventElapsedTime(&ms, ctx->ev_ds[2 * p], ctx->ev_ds[2 * p + 1]);
             s.ms_dominant += ms;
-            s.dominant_bytes += N * (sizeof(K) + (p ? 4 : 0) + sizeof(K) + 4);
+            // algorithmic bytes of one downsweep launch: packed records read + written
+            // (8 + 8); pairs: read K (+4 after pass 0) and write K + 4
+            s.dominant_bytes += ctx->packed_path ? N * 16 : N * (kb + (p ? 4 : 0) + kb + 4);
         }
         s.dominant_launches = (uint64_t)passes;
     }
-    s.ms_buckets = el(EV_GROUPS, EV_BUCKETS);
     if (ctx->stage_done >= MUMS_STAGE_ALL) {
         s.mem_count = ctx->hc.entries;
         s.collision_count = ctx->hc.collisions;
@@ -350,9 +455,10 @@ int mums_ctx_destroy(mums_ctx* ctx) {
     if (!ctx) return MUMS_E_INVALID;
     (void)hipSetDevice(ctx->device);
     mums_clear(ctx);
-    DevBuf* bufs[] = {&ctx->ckey, &ctx->kA, &ctx->kB, &ctx->vA, &ctx->vB, &ctx->tmp, &ctx->partials,
-                      &ctx->counters, &ctx->bstart, &ctx->bend, &ctx->tsize, &ctx->obase, &ctx->pool,
-                      &ctx->tbl, &ctx->out_len, &ctx->out_s, &ctx->pbuf};
+    DevBuf* bufs[] = {&ctx->packed, &ctx->recA, &ctx->recB, &ctx->hist, &ctx->tiles, &ctx->ckey, &ctx->kA,
+                      &ctx->kB, &ctx->vA, &ctx->vB, &ctx->tmp, &ctx->partials, &ctx->counters, &ctx->bstart,
+                      &ctx->bend, &ctx->tsize, &ctx->obase, &ctx->pool, &ctx->tbl, &ctx->out_len, &ctx->out_s,
+                      &ctx->pbuf, &ctx->keybuf, &ctx->mstart};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i < EV_COUNT; ++i)
         if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
@@ -476,7 +582,8 @@ int mums_find_stage(mums_ctx* ctx, int stage) {
         ctx->st = mums_stats{};
         return MUMS_OK;
     }
-    int rc = ctx->key64 ? run_pipeline<uint64_t>(ctx, stage) : run_pipeline<uint32_t>(ctx, stage);
+    ctx->ss = make_seed_spec(pat, L, w);
+    int rc = run_pipeline(ctx, stage);
     return rc;
 }
 
@@ -521,17 +628,13 @@ int mums_copy_seed_keys(mums_ctx* ctx, uint32_t genome, uint64_t* out, uint64_t 
     if (genome >= ctx->genomes.size()) return fail(ctx, MUMS_E_INVALID, "genome index out of range");
     const uint64_t m = ctx->gt.m[genome];
     if (cap < m) return fail(ctx, MUMS_E_INVALID, "output buffer too small");
+    if (m == 0) return MUMS_OK;
     HIPCHK(hipSetDevice(ctx->device));
-    const int sh = 64 - 2 * ctx->w;
-    if (ctx->key64) {
-        std::vector<uint64_t> h(m);
-        if (m) HIPCHK(hipMemcpy(h.data(), ctx->ckey.as<uint64_t>() + ctx->gt.base[genome], m * 8, hipMemcpyDeviceToHost));
-        for (uint64_t p = 0; p < m; ++p) out[p] = ((h[p] >> 1) << sh) | (h[p] & 1);
-    } else {
-        std::vector<uint32_t> h(m);
-        if (m) HIPCHK(hipMemcpy(h.data(), ctx->ckey.as<uint32_t>() + ctx->gt.base[genome], m * 4, hipMemcpyDeviceToHost));
-        for (uint64_t p = 0; p < m; ++p) out[p] = (((uint64_t)h[p] >> 1) << sh) | (h[p] & 1);
-    }
+    HIPCHK(ctx->keybuf.ensure(m * 8));
+    HIPCHK(launch_keys_of_genome(ctx->ss, ctx->packed.as<uint32_t>() + ctx->gt.woff[genome], m,
+                                 ctx->keybuf.as<uint64_t>(), ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipMemcpy(out, ctx->keybuf.p, m * 8, hipMemcpyDeviceToHost));
     return MUMS_OK;
 }
 
@@ -543,12 +646,18 @@ int mums_build_sml(mums_ctx* ctx, uint32_t genome, uint32_t* positions, uint64_t
     if (cap < m) return fail(ctx, MUMS_E_INVALID, "output buffer too small");
     HIPCHK(hipSetDevice(ctx->device));
     // the merged sorted stream restricted to one genome is that genome's SML
-    std::vector<uint32_t> idx(ctx->N);
-    const uint32_t* sidx = ctx->sorted_buf ? ctx->vB.as<uint32_t>() : ctx->vA.as<uint32_t>();
-    if (ctx->N) HIPCHK(hipMemcpy(idx.data(), sidx, ctx->N * 4, hipMemcpyDeviceToHost));
+    const uint64_t N = ctx->N;
+    std::vector<uint32_t> idx(N);
+    if (ctx->packed_path) {
+        std::vector<uint64_t> rec(N);
+        if (N) HIPCHK(hipMemcpy(rec.data(), ctx->sorted_rec, N * 8, hipMemcpyDeviceToHost));
+        for (uint64_t i = 0; i < N; ++i) idx[i] = (uint32_t)rec[i];
+    } else if (N) {
+        HIPCHK(hipMemcpy(idx.data(), ctx->sorted_idx, N * 4, hipMemcpyDeviceToHost));
+    }
     const uint64_t lo = ctx->gt.base[genome], hi = ctx->gt.base[genome + 1];
     uint64_t o = 0;
-    for (uint64_t i = 0; i < ctx->N; ++i)
+    for (uint64_t i = 0; i < N; ++i)
         if (idx[i] >= lo && idx[i] < hi) positions[o++] = (uint32_t)(idx[i] - lo);
     return MUMS_OK;
 }

@@ -2,17 +2,18 @@
 //
 // Data layout in HBM (see DESIGN.md "Data layout"):
 //   * genome g's ASCII bytes (caller- or context-owned), n_g bytes
-//   * ckey[N]   : compact canonical spaced-seed key per seed-mer, indexed by the
-//                 global seed-mer index i = base_g + p (p = 0-based position in
-//                 genome g, 0 <= p < m_g = n_g - L + 1).  ckey = (v << 1) | parity,
-//                 v = the 2w-bit canonical seed value (top 2w bits of
-//                 GetDnaSeedMer, SortedMerList.cpp:764-769), parity = 1 iff the
-//                 reverse complement was chosen.  uint32 when 2w+1 <= 32, else uint64.
-//   * skey/sidx : (ckey, i) pairs radix-sorted by ckey (stable) = the G
-//                 SortedMerLists merged into one key-ordered stream
-//                 (MemorySML.cpp:45-60 + MatchFinder.cpp:172-340).
-//   * probes    : one per accepted masked-key group, as the sorted index of the
-//                 group head, bucket-sorted (stable) for the per-bucket replay.
+//   * packed[]  : 2-bit packed genomes, the reference SortedMerList::sequence layout
+//                 (translate32, SortedMerList.cpp:425-460), genome g at word woff[g]
+//   * the merged key-sorted stream of all seed-mers (the G SortedMerLists of
+//     MemorySML.cpp:45-60 merged as MatchFinder::SearchRange walks them,
+//     MatchFinder.cpp:172-340), in one of two forms:
+//       packed path (2w+1 <= 43): uint64 records (ckey_low << 32 | i), grouped by the
+//                 top B = 2w+1-32 ckey bits (MSD buckets; B = 0 for w <= 15)
+//       pair path  (larger w)   : (ckey, i) pairs, ckey uint32/uint64
+//     where ckey = (v << 1) | parity, v = canonical 2w-bit spaced seed, and
+//     i = base_g + position is the global seed-mer index (stable: ties by i).
+//   * probes    : one per accepted masked-key group in ascending key order,
+//                 (head index | group size << 32) + hash bucket, then bucket-sorted.
 //   * entries   : MatchHashEntry pool, int64 [len, offset, start_0..start_{G-1}].
 #pragma once
 
@@ -24,6 +25,9 @@ namespace mums {
 constexpr int kMaxG = 32;            // genomes per context (register arrays in the replay)
 constexpr int kRepeatLimit = 1000;   // MER_REPEAT_LIMIT, MatchFinder.cpp:166
 constexpr int kBlock = 256;          // threads per workgroup (4 waves of 64)
+constexpr int kSeedTile = 4096;      // positions per key-kernel workgroup
+constexpr int kSegTile = 4096;       // records per sort / group tile
+constexpr int kMaxMsdBits = 11;      // packed path: 2w+1 <= 32 + 11
 
 // Per-run constants shared by the kernels (passed by value).
 struct SeedSpec {
@@ -38,9 +42,11 @@ struct SeedSpec {
 
 struct GenomeTable {
     int G;
-    uint64_t n[kMaxG];      // sequence lengths
-    uint64_t m[kMaxG];      // SMLLength = n - L + 1 (0 if n < L)
-    uint64_t base[kMaxG + 1];  // global seed-mer index base; base[G] = N
+    uint64_t n[kMaxG];          // sequence lengths
+    uint64_t m[kMaxG];          // SMLLength = n - L + 1 (0 if n < L)
+    uint64_t base[kMaxG + 1];   // global seed-mer index base; base[G] = N
+    uint64_t woff[kMaxG + 1];   // word offset of genome g in the packed array
+    uint32_t tfirst[kMaxG + 1]; // first key-kernel tile of genome g (tiles cover n_g bytes)
 };
 
 struct MatchParams {
@@ -58,9 +64,23 @@ struct DevCounters {
     unsigned long long collisions;    // MemHash::m_collision_count
     unsigned long long entries;       // MemHash::m_mem_count (pool cursor)
     uint32_t err;                     // bit 0: '-' seen in a genome
-    uint32_t pad;
+    uint32_t ntiles;                  // segmented tiles in use
     uint32_t nprobes;                 // accepted probes (scan total)
     uint32_t nmatches;                // output matches (scan total)
+};
+
+// A tile of the segmented (per-MSD-bucket) sort/group passes.  Tiles never
+// straddle a bucket; hist index of (digit d) = hbase + d * ntb + tb.
+struct SegTile {
+    uint64_t start;     // first record
+    uint64_t bstart;    // bucket range [bstart, bend)
+    uint64_t bend;
+    uint32_t count;     // records in this tile (0 = unused)
+    uint32_t hbase;     // tfirst_b * 256
+    uint32_t ntb;       // tiles in this bucket
+    uint32_t tb;        // index of this tile within the bucket
+    uint32_t bucket;    // MSD bucket id
+    uint32_t pad;
 };
 
 // genome of a global seed-mer index (G <= 32: linear scan is cheapest)
@@ -71,45 +91,69 @@ __device__ __forceinline__ int genome_of(const GenomeTable& gt, uint64_t i) {
     return g;
 }
 
-// ---- host-side launchers (one per translation unit) -------------------------
-struct Workspace;
+__host__ __device__ inline uint64_t packed_words(uint64_t n) { return (2 * n) / 32 + (((2 * n) % 32) ? 1 : 0) + 2; }
 
-hipError_t launch_seed_keys(const SeedSpec& ss, const GenomeTable& gt, const char* const* d_ascii,
-                            void* d_ckey, bool key64, uint32_t* d_err, hipStream_t st);
+// ---- host-side launchers ------------------------------------------------------------
+// seeds.hip: pack + keys.  mode 0: write ckey[] (pair path, key64 selects width);
+// mode 1: MSD histogram hist[b * T + t] of the top msd_bits of ckey (packed path).
+hipError_t launch_seed_pack(const SeedSpec& ss, const GenomeTable& gt, const char* const* d_ascii,
+                            uint32_t* d_packed, int mode, bool key64, void* d_ckey, int msd_bits,
+                            uint32_t* d_hist, uint32_t ntiles, uint32_t* d_err, hipStream_t st);
+// packed path: scatter records into MSD buckets (offsets = scanned hist)
+hipError_t launch_seed_scatter(const SeedSpec& ss, const GenomeTable& gt, const uint32_t* d_packed, int msd_bits,
+                               const uint32_t* d_hist_scanned, uint32_t ntiles, uint64_t* d_rec, hipStream_t st);
+// ckey of every position of one genome (helper for mums_copy_seed_keys)
+hipError_t launch_keys_of_genome(const SeedSpec& ss, const uint32_t* d_words, uint64_t m, uint64_t* d_out,
+                                 hipStream_t st);
 
-// exclusive scan of n uint32 values in place; d_tmp needs scan_tmp_bytes(n)
+// scan.hip: exclusive scan of n uint32 values in place; d_tmp needs scan_tmp_bytes(n)
 size_t scan_tmp_bytes(uint64_t n);
-hipError_t exclusive_scan_u32(uint32_t* d_data, uint64_t n, void* d_tmp, uint32_t* d_total,
-                              hipStream_t st);
+hipError_t exclusive_scan_u32(uint32_t* d_data, uint64_t n, void* d_tmp, uint32_t* d_total, hipStream_t st);
 
-// stable LSD radix sort of keys over bit range [0, bits); values are the
-// implicit indices 0..n-1 when vals_in == nullptr.  Returns which buffer holds
-// the result (0 = A, 1 = B).
+// radix_sort.hip: stable LSD radix sort of keys over bit range [0, bits); values are
+// the implicit indices 0..n-1 when vals_in == nullptr.  ev_ds (optional): 2 events per
+// pass around each downsweep launch.
 size_t radix_tmp_bytes(uint64_t n);
-// ev_ds (optional): 2 events per pass recorded around each downsweep launch.
 template <typename K>
 hipError_t radix_sort(const K* keys_in, const uint32_t* vals_in, uint64_t n, int bits,
                       K* kA, uint32_t* vA, K* kB, uint32_t* vB, void* d_tmp, int* out_buf,
                       hipStream_t st, hipEvent_t* ev_ds = nullptr);
 
+// radix_seg.hip: segmented tiles + stable LSD sort of packed records on bits
+// [32, 32 + key_bits) inside each MSD bucket.
+uint64_t seg_tiles_upper(uint64_t n, int msd_bits);
+size_t seg_tmp_bytes(uint64_t n, int msd_bits);
+hipError_t build_seg_tiles(const uint32_t* d_hist_scanned, uint32_t T, int msd_bits, uint64_t n, SegTile* d_tiles,
+                           uint32_t* d_ntiles, uint32_t* d_bstart, void* d_tmp, hipStream_t st);
+hipError_t seg_radix_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key_bits, const SegTile* d_tiles,
+                          uint64_t ntiles_ub, void* d_tmp, int* out_buf, hipStream_t st,
+                          hipEvent_t* ev_ds = nullptr);
+// onesweep variant (n < 2^30): one histogram read for all passes, then one launch per
+// pass with decoupled look-back between consecutive tiles of a bucket.
+size_t onesweep_tmp_bytes(uint64_t n, int msd_bits, int key_bits);
+hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key_bits, int msd_bits,
+                             const SegTile* d_tiles, uint64_t ntiles_ub, const uint32_t* d_bstart, void* d_tmp,
+                             uint32_t* d_err, int* out_buf, hipStream_t st, hipEvent_t* ev_ds = nullptr);
+
 // groups.hip
-uint64_t group_tiles(uint64_t N);
-uint64_t group_slot_count(uint64_t N);
-template <int MG, typename K>
-hipError_t launch_probe_tiles(const K* skey, const uint32_t* sidx, uint64_t N, const GenomeTable& gt,
-                              const MatchParams& mp, int L, uint32_t* tile_count, uint32_t* slot_head,
+uint64_t group_slot_count(uint64_t ntiles);
+template <int MG, typename View>
+hipError_t launch_probe_tiles(View v, const SegTile* tiles, uint64_t ntiles, uint64_t N, const GenomeTable& gt,
+                              const MatchParams& mp, int L, uint32_t* tile_count, uint64_t* slot_info,
                               uint32_t* slot_bucket, void* counters, hipStream_t st);
-hipError_t launch_probe_compact(uint64_t N, const uint32_t* tile_count, const uint32_t* tile_off,
-                                const uint32_t* slot_head, const uint32_t* slot_bucket, uint32_t* probe_head,
+hipError_t launch_probe_compact(uint64_t ntiles, const uint32_t* tile_count, const uint32_t* tile_off,
+                                const uint64_t* slot_info, const uint32_t* slot_bucket, uint64_t* probe_info,
                                 uint32_t* probe_bucket, hipStream_t st);
+// flat tiles over [0, N) for the pair path (one bucket)
+hipError_t launch_flat_tiles(uint64_t N, SegTile* d_tiles, hipStream_t st);
 
 // replay.hip
 hipError_t launch_bucket_ranges(const uint32_t* sb, uint64_t P, uint32_t* bstart, uint32_t* bend, hipStream_t st);
-template <int MG, typename K>
-hipError_t launch_replay(const K* skey, const uint32_t* sidx, uint64_t N, const GenomeTable& gt,
-                         const MatchParams& mp, int L, const uint32_t* heads, const uint32_t* bstart,
-                         const uint32_t* bend, uint32_t* tbl, int64_t* pool, const K* ckey, uint32_t* tsize,
-                         void* ctr, hipStream_t st);
+template <int MG, typename View>
+hipError_t launch_replay(View v, uint64_t N, const GenomeTable& gt, const MatchParams& mp, const SeedSpec& ss,
+                         const uint64_t* probe_info, const uint32_t* sorted_ids, const uint32_t* bstart,
+                         const uint32_t* bend, uint32_t* tbl, int64_t* pool, const uint32_t* packed,
+                         uint32_t* tsize, void* ctr, hipStream_t st);
 hipError_t launch_emit(const uint32_t* tsize, const uint32_t* obase, const uint32_t* bstart, const uint32_t* tbl,
                        const int64_t* pool, int G, uint32_t table_size, uint64_t* out_len, int64_t* out_s,
                        hipStream_t st);

@@ -1,0 +1,483 @@
+// radix_seg.hip -- segmented stable LSD radix sort of packed 8-B seed records (row A5).
+//
+// Records are (ckey_low << 32 | global index) and already sit in their MSD bucket
+// (top B key bits, seeds.hip); each pass sorts one 8-bit digit of ckey_low inside
+// every bucket.  Replaces MemorySML::Create's std::sort of 16-B bmer records
+// (MemorySML.cpp:54, bmer_lessthan SortedMerList.h:311-314) and the G-way list merge
+// of MatchFinder::SearchRange (MatchFinder.cpp:236-333) in one stream.
+//
+// Tiles of 4096 records never straddle a bucket; the digit histogram of tile tb of
+// bucket b lives at hist[tfirst_b*256 + d*ntiles_b + tb], so ONE exclusive scan over
+// the whole histogram yields every (bucket, digit, tile) output offset.
+// Per pass: upsweep (tile digit histogram), scan, downsweep (wave64 ballot match-any
+// ranking, LDS reorder, digit-run-contiguous stores).
+// HBM bytes per record per pass: upsweep 8, downsweep 8 + 8.
+#include "mums_internal.h"
+
+namespace mums {
+
+namespace {
+
+constexpr int kTile = kSegTile;
+constexpr int kRounds = kTile / kBlock;  // 16
+constexpr int kWaves = kBlock / 64;
+constexpr int kDigits = 256;
+constexpr int kOnesweepIPT = 16;   // records per thread per onesweep tile (tile = kSegTile)
+inline uint64_t ub_status(uint64_t ub, int npass) { return ub * kDigits * (uint64_t)npass; }
+
+// bucket starts from the scanned MSD histogram: bstart[b] = scanned[b * T], bstart[nb] = n
+__global__ void bucket_starts_kernel(const uint32_t* __restrict__ scanned, uint32_t T, int nb, uint64_t n,
+                                     uint32_t* __restrict__ bstart, uint32_t* __restrict__ ntb) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b > nb) return;
+    const uint64_t s = (b == nb) ? n : (uint64_t)scanned[(uint64_t)b * T];
+    bstart[b] = (uint32_t)s;
+    if (b < nb) {
+        const uint64_t e = (b + 1 == nb) ? n : (uint64_t)scanned[(uint64_t)(b + 1) * T];
+        ntb[b] = (uint32_t)((e - s + kTile - 1) / kTile);
+    }
+}
+
+__global__ void single_bucket_kernel(uint64_t n, uint32_t* __restrict__ bstart, uint32_t* __restrict__ tfirst) {
+    if (threadIdx.x == 0) {
+        bstart[0] = 0;
+        bstart[1] = (uint32_t)n;
+        tfirst[0] = 0;
+        tfirst[1] = (uint32_t)((n + kTile - 1) / kTile);
+    }
+}
+
+__global__ void tiles_kernel(const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ tfirst, int nb,
+                             uint64_t ub, SegTile* __restrict__ tiles, uint32_t* __restrict__ ntiles_out) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ub) return;
+    const uint32_t total = tfirst[nb];
+    if (t == 0) *ntiles_out = total;
+    SegTile d{};
+    if (t < total) {
+        int lo = 0, hi = nb - 1;  // last bucket b with tfirst[b] <= t (buckets with 0 tiles skipped)
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (tfirst[mid] <= t) lo = mid;
+            else hi = mid - 1;
+        }
+        while (lo + 1 < nb && tfirst[lo + 1] <= t) ++lo;
+        const uint32_t tb = (uint32_t)(t - tfirst[lo]);
+        const uint32_t ntb = tfirst[lo + 1] - tfirst[lo];
+        d.bstart = bstart[lo];
+        d.bend = bstart[lo + 1];
+        d.start = d.bstart + (uint64_t)tb * kTile;
+        const uint64_t rem = d.bend - d.start;
+        d.count = (uint32_t)(rem < (uint64_t)kTile ? rem : (uint64_t)kTile);
+        d.hbase = tfirst[lo] * kDigits;
+        d.ntb = ntb;
+        d.tb = tb;
+        d.bucket = (uint32_t)lo;
+    } else {
+        d.count = 0;
+        d.hbase = (uint32_t)(t * kDigits);
+        d.ntb = 1;
+        d.tb = 0;
+    }
+    tiles[t] = d;
+}
+
+__global__ __launch_bounds__(kBlock) void seg_upsweep(const uint64_t* __restrict__ rec, const SegTile* __restrict__ tiles,
+                                                      int shift, uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[kWaves][kDigits];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const SegTile d = tiles[blockIdx.x];
+    for (int i = threadIdx.x; i < kWaves * kDigits; i += kBlock) (&h[0][0])[i] = 0;
+    __syncthreads();
+    const uint32_t b0 = wv * (kTile / kWaves);
+    #pragma unroll 4
+    for (int r = 0; r < kRounds; ++r) {
+        const uint32_t q = b0 + r * 64 + lane;
+        if (q < d.count) atomicAdd(&h[wv][(uint32_t)(rec[d.start + q] >> shift) & 0xFFu], 1u);
+    }
+    __syncthreads();
+    const int t = threadIdx.x;
+    uint32_t s = 0;
+    #pragma unroll
+    for (int w = 0; w < kWaves; ++w) s += h[w][t];
+    hist[(uint64_t)d.hbase + (uint64_t)t * d.ntb + d.tb] = s;
+}
+
+__global__ __launch_bounds__(kBlock) void seg_downsweep(const uint64_t* __restrict__ rin,
+                                                        const SegTile* __restrict__ tiles, int shift,
+                                                        const uint32_t* __restrict__ hist,
+                                                        uint64_t* __restrict__ rout) {
+    __shared__ uint64_t srec[kTile];
+    __shared__ uint32_t wcnt[kWaves][kDigits];
+    __shared__ uint32_t lstart[kDigits];
+    __shared__ uint32_t gofs[kDigits];
+    __shared__ uint32_t s_w[kWaves];
+    const SegTile d = tiles[blockIdx.x];
+    if (d.count == 0) return;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int i = threadIdx.x; i < kWaves * kDigits; i += kBlock) (&wcnt[0][0])[i] = 0;
+    __syncthreads();
+    const uint32_t q0 = wv * (kTile / kWaves);
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint64_t key[kRounds];
+    uint32_t rank[kRounds];
+    #pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+        const uint32_t q = q0 + r * 64 + lane;
+        key[r] = q < d.count ? rin[d.start + q] : 0ull;
+    }
+    #pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+        const uint32_t q = q0 + r * 64 + lane;
+        const bool valid = q < d.count;
+        const uint32_t dg = (uint32_t)(key[r] >> shift) & 0xFFu;
+        uint64_t peers = __ballot(valid);
+        #pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const bool bit = (dg >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            peers &= bit ? bb : ~bb;
+        }
+        const uint32_t rk = (uint32_t)__popcll(peers & lt);
+        uint32_t old = 0;
+        if (valid) old = wcnt[wv][dg];
+        if (valid && rk == 0) wcnt[wv][dg] = old + (uint32_t)__popcll(peers);
+        rank[r] = old + rk;
+    }
+    __syncthreads();
+    {
+        const int t = threadIdx.x;  // digit
+        uint32_t acc = 0;
+        #pragma unroll
+        for (int w = 0; w < kWaves; ++w) { const uint32_t c = wcnt[w][t]; wcnt[w][t] = acc; acc += c; }
+        uint32_t v = acc;
+        #pragma unroll
+        for (int dd = 1; dd < 64; dd <<= 1) {
+            const uint32_t x = __shfl_up(v, dd, 64);
+            if (lane >= dd) v += x;
+        }
+        if (lane == 63) s_w[wv] = v;
+        __syncthreads();
+        uint32_t wpre = 0;
+        #pragma unroll
+        for (int w = 0; w < kWaves; ++w) wpre += (w < wv) ? s_w[w] : 0u;
+        lstart[t] = wpre + v - acc;
+        gofs[t] = hist[(uint64_t)d.hbase + (uint64_t)t * d.ntb + d.tb];
+    }
+    __syncthreads();
+    #pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+        const uint32_t q = q0 + r * 64 + lane;
+        if (q < d.count) {
+            const uint32_t dg = (uint32_t)(key[r] >> shift) & 0xFFu;
+            srec[lstart[dg] + wcnt[wv][dg] + rank[r]] = key[r];
+        }
+    }
+    __syncthreads();
+    #pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+        const uint32_t s = threadIdx.x + r * kBlock;
+        if (s < d.count) {
+            const uint64_t k = srec[s];
+            const uint32_t dg = (uint32_t)(k >> shift) & 0xFFu;
+            rout[(uint64_t)gofs[dg] + (s - lstart[dg])] = k;
+        }
+    }
+}
+
+
+// ---------------------------------------------------------------------------------
+// Onesweep variant.  ghist[(b * npass + p) * 256 + d] = records of bucket b whose
+// pass-p digit is d (one read of the data for all passes); dbase = per-bucket
+// exclusive digit offsets + bucket start.  Each pass is then ONE launch: a tile
+// ranks its records, publishes its per-digit count, looks back over the preceding
+// tiles of its bucket for the exclusive prefix, and scatters.  Status words are one
+// 32-bit {flag:2, count:30} granule per (tile, digit), stored and polled with
+// agent-scope relaxed atomics (MI355X_MICROARCH.md "Valid forms": the data is the
+// flag).  Tile ids come from an atomic counter in launch order, so every tile a
+// block waits on is already resident: forward progress without a grid barrier.
+// Spins are bounded; a timeout sets err bit 1 instead of hanging the device.
+constexpr uint32_t kFlagAgg = 1u << 30;
+constexpr uint32_t kFlagInc = 2u << 30;
+constexpr uint32_t kValMask = (1u << 30) - 1;
+constexpr int kGhistTilesPerBlock = 16;
+
+__global__ __launch_bounds__(kBlock) void seg_ghist_kernel(const uint64_t* __restrict__ rec,
+                                                           const SegTile* __restrict__ tiles, uint64_t ntiles_ub,
+                                                           int npass, uint32_t* __restrict__ ghist) {
+    __shared__ uint32_t h[4][kDigits];
+    const int tid = threadIdx.x;
+    const uint64_t t0 = (uint64_t)blockIdx.x * kGhistTilesPerBlock;
+    uint32_t cur_b = 0xFFFFFFFFu;
+    for (int i = tid; i < 4 * kDigits; i += kBlock) (&h[0][0])[i] = 0;
+    __syncthreads();
+    for (int k = 0; k < kGhistTilesPerBlock; ++k) {
+        const uint64_t t = t0 + k;
+        if (t >= ntiles_ub) break;
+        const SegTile d = tiles[t];
+        if (d.count == 0) break;
+        if (d.bucket != cur_b) {
+            if (cur_b != 0xFFFFFFFFu) {
+                __syncthreads();
+                for (int p = 0; p < npass; ++p) {
+                    const uint32_t v = h[p][tid];
+                    if (v) atomicAdd(&ghist[((uint64_t)cur_b * npass + p) * kDigits + tid], v);
+                    h[p][tid] = 0;
+                }
+                __syncthreads();
+            }
+            cur_b = d.bucket;
+        }
+        for (uint32_t q = tid; q < d.count; q += kBlock) {
+            const uint64_t key = rec[d.start + q] >> 32;
+            for (int p = 0; p < npass; ++p) atomicAdd(&h[p][(uint32_t)(key >> (8 * p)) & 0xFFu], 1u);
+        }
+    }
+    __syncthreads();
+    if (cur_b != 0xFFFFFFFFu)
+        for (int p = 0; p < npass; ++p) {
+            const uint32_t v = h[p][tid];
+            if (v) atomicAdd(&ghist[((uint64_t)cur_b * npass + p) * kDigits + tid], v);
+        }
+}
+
+// one block per (bucket, pass): dbase = bstart[b] + exclusive scan over digits
+__global__ __launch_bounds__(kBlock) void seg_dbase_kernel(const uint32_t* __restrict__ ghist,
+                                                           const uint32_t* __restrict__ bstart, int npass,
+                                                           uint32_t* __restrict__ dbase) {
+    __shared__ uint32_t s_w[kWaves];
+    const uint64_t bp = blockIdx.x;
+    const uint32_t b = (uint32_t)(bp / npass);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t v = ghist[bp * kDigits + threadIdx.x];
+    uint32_t inc = v;
+    #pragma unroll
+    for (int dd = 1; dd < 64; dd <<= 1) {
+        const uint32_t x = __shfl_up(inc, dd, 64);
+        if (lane >= dd) inc += x;
+    }
+    if (lane == 63) s_w[wv] = inc;
+    __syncthreads();
+    uint32_t pre = 0;
+    #pragma unroll
+    for (int w = 0; w < kWaves; ++w) pre += (w < wv) ? s_w[w] : 0u;
+    dbase[bp * kDigits + threadIdx.x] = bstart[b] + pre + inc - v;
+}
+
+template <int kIPT>
+__global__ __launch_bounds__(kBlock) void seg_onesweep_kernel(const uint64_t* __restrict__ rin,
+                                                              uint64_t* __restrict__ rout,
+                                                              const SegTile* __restrict__ tiles, int shift, int pass,
+                                                              int npass, const uint32_t* __restrict__ dbase,
+                                                              uint32_t* status, uint32_t* tile_counter,
+                                                              uint32_t* err) {
+    constexpr int kT = kIPT * kBlock;
+    __shared__ uint64_t srec[kT];
+    __shared__ uint32_t wcnt[kWaves][kDigits];
+    __shared__ uint32_t lstart[kDigits];
+    __shared__ uint32_t gofs[kDigits];
+    __shared__ uint32_t s_w[kWaves];
+    __shared__ uint32_t s_tile;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (tid == 0) s_tile = atomicAdd(tile_counter, 1u);
+    for (int i = tid; i < kWaves * kDigits; i += kBlock) (&wcnt[0][0])[i] = 0;
+    __syncthreads();
+    const uint32_t t = s_tile;
+    const SegTile d = tiles[t];
+    if (d.count == 0) return;
+    const uint32_t q0 = wv * (kT / kWaves);
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint64_t key[kIPT];
+    uint32_t rank[kIPT];
+    #pragma unroll
+    for (int r = 0; r < kIPT; ++r) {
+        const uint32_t q = q0 + r * 64 + lane;
+        key[r] = q < d.count ? rin[d.start + q] : 0ull;
+    }
+    #pragma unroll
+    for (int r = 0; r < kIPT; ++r) {
+        const uint32_t q = q0 + r * 64 + lane;
+        const bool valid = q < d.count;
+        const uint32_t dg = (uint32_t)(key[r] >> shift) & 0xFFu;
+        uint64_t peers = __ballot(valid);
+        #pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const bool bit = (dg >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            peers &= bit ? bb : ~bb;
+        }
+        const uint32_t rk = (uint32_t)__popcll(peers & lt);
+        uint32_t old = 0;
+        if (valid) old = wcnt[wv][dg];
+        if (valid && rk == 0) wcnt[wv][dg] = old + (uint32_t)__popcll(peers);
+        rank[r] = old + rk;
+    }
+    __syncthreads();
+    {
+        const int dg = tid;  // digit
+        uint32_t acc = 0;
+        #pragma unroll
+        for (int w = 0; w < kWaves; ++w) { const uint32_t c = wcnt[w][dg]; wcnt[w][dg] = acc; acc += c; }
+        // publish, then look back over the bucket's preceding tiles
+        uint32_t* st = status + (uint64_t)t * kDigits + dg;
+        uint32_t prefix = 0;
+        if (d.tb == 0) {
+            __hip_atomic_store(st, kFlagInc | acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(st, kFlagAgg | acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            uint64_t j = (uint64_t)t - 1;
+            uint32_t spins = 0;
+            for (;;) {
+                const uint32_t s = __hip_atomic_load(status + j * kDigits + dg, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+                if ((s >> 30) == 0u) {
+                    if (++spins > (1u << 26)) { atomicOr(err, 2u); break; }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                prefix += s & kValMask;
+                if ((s & kFlagInc) != 0u) break;
+                --j;
+            }
+            __hip_atomic_store(st, kFlagInc | ((prefix + acc) & kValMask), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        gofs[dg] = dbase[((uint64_t)d.bucket * npass + pass) * kDigits + dg] + prefix;
+        // block-local digit starts
+        uint32_t v = acc;
+        #pragma unroll
+        for (int dd = 1; dd < 64; dd <<= 1) {
+            const uint32_t x = __shfl_up(v, dd, 64);
+            if (lane >= dd) v += x;
+        }
+        if (lane == 63) s_w[wv] = v;
+        __syncthreads();
+        uint32_t wpre = 0;
+        #pragma unroll
+        for (int w = 0; w < kWaves; ++w) wpre += (w < wv) ? s_w[w] : 0u;
+        lstart[dg] = wpre + v - acc;
+    }
+    __syncthreads();
+    #pragma unroll
+    for (int r = 0; r < kIPT; ++r) {
+        const uint32_t q = q0 + r * 64 + lane;
+        if (q < d.count) {
+            const uint32_t dg = (uint32_t)(key[r] >> shift) & 0xFFu;
+            srec[lstart[dg] + wcnt[wv][dg] + rank[r]] = key[r];
+        }
+    }
+    __syncthreads();
+    #pragma unroll
+    for (int r = 0; r < kIPT; ++r) {
+        const uint32_t s = tid + r * kBlock;
+        if (s < d.count) {
+            const uint64_t k = srec[s];
+            const uint32_t dg = (uint32_t)(k >> shift) & 0xFFu;
+            rout[(uint64_t)gofs[dg] + (s - lstart[dg])] = k;
+        }
+    }
+}
+
+}  // namespace
+
+uint64_t seg_tiles_upper(uint64_t n, int msd_bits) { return (n + kTile - 1) / kTile + (1ull << msd_bits) + 1; }
+
+size_t seg_tmp_bytes(uint64_t n, int msd_bits) {
+    const uint64_t ub = seg_tiles_upper(n, msd_bits);
+    const uint64_t nb = 1ull << msd_bits;
+    const uint64_t h = ub * kDigits;
+    return (h + 64) * 4 + (2 * nb + 130) * 4 + scan_tmp_bytes(h > nb ? h : nb) + 512;
+}
+
+// d_hist_scanned: the scanned MSD histogram [nb x T] (nullptr when msd_bits == 0).
+hipError_t build_seg_tiles(const uint32_t* d_hist_scanned, uint32_t T, int msd_bits, uint64_t n, SegTile* d_tiles,
+                           uint32_t* d_ntiles, uint32_t* bstart, void* d_tmp, hipStream_t st) {
+    const int nb = 1 << msd_bits;
+    const uint64_t ub = seg_tiles_upper(n, msd_bits);
+    uint32_t* tfirst = (uint32_t*)d_tmp;
+    void* stmp = (void*)(tfirst + nb + 64);
+    if (msd_bits == 0) {
+        hipLaunchKernelGGL(single_bucket_kernel, dim3(1), dim3(64), 0, st, n, bstart, tfirst);
+    } else {
+        hipLaunchKernelGGL(bucket_starts_kernel, dim3((nb + 256) / 256), dim3(256), 0, st, d_hist_scanned, T, nb, n,
+                           bstart, tfirst);
+        // tfirst[b] = exclusive scan of tiles per bucket; tfirst[nb] = total
+        hipError_t e = exclusive_scan_u32(tfirst, (uint64_t)nb + 1, stmp, nullptr, st);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(tiles_kernel, dim3((unsigned)((ub + 255) / 256)), dim3(256), 0, st, bstart, tfirst, nb, ub,
+                       d_tiles, d_ntiles);
+    return hipGetLastError();
+}
+
+size_t onesweep_tmp_bytes(uint64_t n, int msd_bits, int key_bits) {
+    const uint64_t ub = seg_tiles_upper(n, msd_bits);
+    const int npass = (key_bits + 7) / 8;
+    const uint64_t nb = 1ull << msd_bits;
+    return (ub * kDigits * (uint64_t)npass + 2 * nb * npass * kDigits + 64 + 64) * 4 + 4096;
+}
+
+hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key_bits, int msd_bits,
+                             const SegTile* d_tiles, uint64_t ntiles_ub, const uint32_t* d_bstart, void* d_tmp,
+                             uint32_t* d_err, int* out_buf, hipStream_t st, hipEvent_t* ev_ds) {
+    const int npass = (key_bits + 7) / 8;
+    *out_buf = npass % 2;
+    if (n == 0 || npass == 0) return hipSuccess;
+    if (npass > 4) return hipErrorInvalidValue;
+    const uint64_t nb = 1ull << msd_bits;
+    uint32_t* status = (uint32_t*)d_tmp;                       // [npass][ub][256]
+    uint32_t* ghist = status + ub_status(ntiles_ub, npass);    // [nb][npass][256]
+    uint32_t* dbase = ghist + nb * npass * kDigits;            // [nb][npass][256]
+    uint32_t* counters = dbase + nb * npass * kDigits;         // [npass]
+    const size_t zero_bytes = ((uint64_t)(counters - status) + 64) * 4;
+    hipError_t e = hipMemsetAsync(status, 0, zero_bytes, st);
+    if (e != hipSuccess) return e;
+    const unsigned gblocks = (unsigned)((ntiles_ub + kGhistTilesPerBlock - 1) / kGhistTilesPerBlock);
+    hipLaunchKernelGGL(seg_ghist_kernel, dim3(gblocks), dim3(kBlock), 0, st, recA, d_tiles, ntiles_ub, npass, ghist);
+    hipLaunchKernelGGL(seg_dbase_kernel, dim3((unsigned)(nb * npass)), dim3(kBlock), 0, st, ghist, d_bstart, npass,
+                       dbase);
+    uint64_t* src = recA;
+    uint64_t* dst = recB;
+    for (int p = 0; p < npass; ++p) {
+        if (ev_ds) (void)hipEventRecord(ev_ds[2 * p], st);
+        hipLaunchKernelGGL(seg_onesweep_kernel<kOnesweepIPT>, dim3((unsigned)ntiles_ub), dim3(kBlock), 0, st, src,
+                           dst, d_tiles, 32 + 8 * p, p, npass, dbase,
+                           status + (uint64_t)p * ntiles_ub * kDigits, counters + p, d_err);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        if (ev_ds) (void)hipEventRecord(ev_ds[2 * p + 1], st);
+        uint64_t* t = src;
+        src = dst;
+        dst = t;
+    }
+    return hipSuccess;
+}
+
+hipError_t seg_radix_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key_bits, const SegTile* d_tiles,
+                          uint64_t ntiles_ub, void* d_tmp, int* out_buf, hipStream_t st, hipEvent_t* ev_ds) {
+    const int passes = (key_bits + 7) / 8;
+    *out_buf = passes % 2;  // 0: result in recA, 1: in recB
+    if (n == 0 || passes == 0) return hipSuccess;
+    const uint64_t h = ntiles_ub * kDigits;
+    uint32_t* hist = (uint32_t*)d_tmp;
+    void* stmp = (void*)(hist + h + 64);
+    uint64_t* src = recA;
+    uint64_t* dst = recB;
+    for (int p = 0; p < passes; ++p) {
+        const int shift = 32 + 8 * p;
+        hipLaunchKernelGGL(seg_upsweep, dim3((unsigned)ntiles_ub), dim3(kBlock), 0, st, src, d_tiles, shift, hist);
+        hipError_t e = exclusive_scan_u32(hist, h, stmp, nullptr, st);
+        if (e != hipSuccess) return e;
+        if (ev_ds) (void)hipEventRecord(ev_ds[2 * p], st);
+        hipLaunchKernelGGL(seg_downsweep, dim3((unsigned)ntiles_ub), dim3(kBlock), 0, st, src, d_tiles, shift, hist,
+                           dst);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        if (ev_ds) (void)hipEventRecord(ev_ds[2 * p + 1], st);
+        uint64_t* t = src;
+        src = dst;
+        dst = t;
+    }
+    return hipSuccess;
+}
+
+}  // namespace mums

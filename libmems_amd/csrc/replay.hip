@@ -17,9 +17,10 @@
 // cooperatively and inserts it; everything before it is final.  Extension uses
 // the fixpoint of ExtendMatch's L-jump / single-step / restart loop: the
 // maximal chain of seed hits with gaps <= L through the probe,
-// found with 256 speculative L-jumps per round and an L-wide fine step, where a
-// hit is read from the resident per-position key array (no re-derivation).
+// found with 256 speculative L-jumps per round and an L-wide fine step; a hit
+// re-derives the components' seed keys from the resident 2-bit packed genomes.
 #include "match_device.h"
+#include "seed_device.h"
 
 namespace mums {
 
@@ -27,7 +28,7 @@ namespace {
 
 struct ExtComp {
     int64_t s;       // start (signed, 1-based)
-    uint64_t base;   // global seed-mer index base of the genome
+    uint64_t woff;   // word offset of the genome in the packed array
 };
 
 __device__ __forceinline__ int block_first_true(bool pred, int* red) {
@@ -56,41 +57,39 @@ __device__ __forceinline__ int block_last_true(bool pred, int* red) {
 
 // seed hit at alignment column c (MatchFinder.h:265-293): every component's
 // masked key and strand-relative parity agree, all windows inside the sequences.
-template <typename K>
 __device__ __forceinline__ bool hit_at(int64_t c, const ExtComp* comps, int nc, int64_t clo, int64_t chi,
-                                       const K* __restrict__ ckey) {
+                                       const uint32_t* __restrict__ packed, const SeedSpec& ss) {
     if (c < clo || c > chi) return false;
     uint64_t v0 = 0;
     uint32_t o0 = 0;
     bool ok = true;
-    for (int j = 0; j < nc; ++j) {
+    for (int j = 0; j < nc && ok; ++j) {
         const int64_t s = comps[j].s;
         const int64_t p = s > 0 ? s - 1 + c : -s - 1 - c;
-        const uint64_t k = (uint64_t)ckey[comps[j].base + (uint64_t)p];
+        const uint64_t k = ckey_at(packed + comps[j].woff, (uint64_t)p, ss);
         const uint64_t v = k >> 1;
         const uint32_t o = s > 0 ? (uint32_t)((k & 1) ^ 1) : (uint32_t)(k & 1);
         if (j == 0) { v0 = v; o0 = o; }
-        else ok = ok && (v == v0) && (o == o0);
+        else ok = (v == v0) && (o == o0);
     }
     return ok;
 }
 
 // rightmost (dir=+1) / leftmost (dir=-1) column of the hit chain through column 0
-template <typename K>
 __device__ int64_t chain_end(int dir, int L, const ExtComp* comps, int nc, int64_t clo, int64_t chi,
-                             const K* __restrict__ ckey, int* red) {
+                             const uint32_t* __restrict__ packed, const SeedSpec& ss, int* red) {
     const int tid = threadIdx.x;
     int64_t cur = 0;
     for (;;) {
         for (;;) {  // ExtendMatch directions 0/1: jumps of L while the seed at the new end matches
-            const bool h = hit_at<K>(cur + dir * (int64_t)(tid + 1) * L, comps, nc, clo, chi, ckey);
+            const bool h = hit_at(cur + dir * (int64_t)(tid + 1) * L, comps, nc, clo, chi, packed, ss);
             const int miss = block_first_true(!h, red);
             if (miss == kBlock) { cur += dir * (int64_t)kBlock * L; continue; }
             cur += dir * (int64_t)miss * L;
             break;
         }
         // directions 2/3: furthest hit within L single steps, then restart
-        const bool h2 = tid < L ? hit_at<K>(cur + dir * (int64_t)(tid + 1), comps, nc, clo, chi, ckey) : false;
+        const bool h2 = tid < L ? hit_at(cur + dir * (int64_t)(tid + 1), comps, nc, clo, chi, packed, ss) : false;
         const int far = block_last_true(h2, red);
         if (far < 0) break;
         cur += dir * (int64_t)(far + 1);
@@ -98,14 +97,15 @@ __device__ int64_t chain_end(int dir, int L, const ExtComp* comps, int nc, int64
     return cur;
 }
 
-template <int MG, typename K>
-__global__ __launch_bounds__(kBlock) void replay_kernel(const K* __restrict__ skey, const uint32_t* __restrict__ sidx,
-                                                        uint64_t N, GenomeTable gt, MatchParams mp, int L,
-                                                        const uint32_t* __restrict__ heads,
+template <int MG, typename View>
+__global__ __launch_bounds__(kBlock) void replay_kernel(View v, uint64_t N, GenomeTable gt, MatchParams mp, SeedSpec ss,
+                                                        const uint64_t* __restrict__ probe_info,
+                                                        const uint32_t* __restrict__ ids,
                                                         const uint32_t* __restrict__ bstart,
                                                         const uint32_t* __restrict__ bend, uint32_t* tbl,
-                                                        int64_t* pool, const K* __restrict__ ckey,
+                                                        int64_t* pool, const uint32_t* __restrict__ packed,
                                                         uint32_t* __restrict__ tsize, DevCounters* ctr) {
+    const int L = ss.L;
     __shared__ int red[kBlock / 64];
     __shared__ int64_t sP[MG + 2];
     __shared__ ExtComp comps[MG];
@@ -120,7 +120,7 @@ __global__ __launch_bounds__(kBlock) void replay_kernel(const K* __restrict__ sk
     if (K_b == 0) return;
     const int G = gt.G;
     uint32_t* tb = tbl + beg;
-    const uint32_t* hd = heads + beg;
+    const uint32_t* hd = ids + beg;
     uint32_t t = 0, i = 0;
     unsigned long long coll = 0;
 
@@ -130,7 +130,9 @@ __global__ __launch_bounds__(kBlock) void replay_kernel(const K* __restrict__ sk
         Mhe<MG> P;
         if ((uint32_t)tid < c) {
             uint32_t gs;
-            build_probe<MG, K>(skey, sidx, N, hd[i + tid], gt, mp, L, P, &gs);
+            const uint64_t info = probe_info[hd[i + tid]];
+            const uint64_t h = info & 0xFFFFFFFFull;
+            build_probe<MG, View>(v, h, h + ((info >> 32) & 0xFFFFull), gt, mp, L, P, &gs);
             const uint32_t lb = lower_bound_tbl<MG>(tb, t, pool, G, P);
             if (lb < t) {
                 Mhe<MG> E;
@@ -161,7 +163,7 @@ __global__ __launch_bounds__(kBlock) void replay_kernel(const K* __restrict__ sk
                 const int64_t s = sP[2 + g];
                 if (s == 0) continue;
                 comps[nc].s = s;
-                comps[nc].base = gt.base[g];
+                comps[nc].woff = gt.woff[g];
                 const int64_t m = (int64_t)gt.m[g];
                 const int64_t lo = s > 0 ? 1 - s : -s - m;
                 const int64_t hi = s > 0 ? m - s : -s - 1;
@@ -176,8 +178,8 @@ __global__ __launch_bounds__(kBlock) void replay_kernel(const K* __restrict__ sk
         __syncthreads();
         const int nc = s_nc;
         const int64_t clo = s_clo, chi = s_chi;
-        const int64_t cmax = chain_end<K>(+1, L, comps, nc, clo, chi, ckey, red);
-        const int64_t cmin = chain_end<K>(-1, L, comps, nc, clo, chi, ckey, red);
+        const int64_t cmax = chain_end(+1, L, comps, nc, clo, chi, packed, ss, red);
+        const int64_t cmin = chain_end(-1, L, comps, nc, clo, chi, packed, ss, red);
         if (tid == 0) {
             const uint32_t id = (uint32_t)atomicAdd(&ctr->entries, 1ull);
             Mhe<MG> E;
@@ -257,13 +259,13 @@ hipError_t launch_bucket_ranges(const uint32_t* sb, uint64_t P, uint32_t* bstart
     return hipGetLastError();
 }
 
-template <int MG, typename K>
-hipError_t launch_replay(const K* skey, const uint32_t* sidx, uint64_t N, const GenomeTable& gt,
-                         const MatchParams& mp, int L, const uint32_t* heads, const uint32_t* bstart,
-                         const uint32_t* bend, uint32_t* tbl, int64_t* pool, const K* ckey, uint32_t* tsize,
-                         void* ctr, hipStream_t st) {
-    hipLaunchKernelGGL((replay_kernel<MG, K>), dim3(mp.table_size), dim3(kBlock), 0, st, skey, sidx, N, gt, mp, L,
-                       heads, bstart, bend, tbl, pool, ckey, tsize, (DevCounters*)ctr);
+template <int MG, typename View>
+hipError_t launch_replay(View v, uint64_t N, const GenomeTable& gt, const MatchParams& mp, const SeedSpec& ss,
+                         const uint64_t* probe_info, const uint32_t* sorted_ids, const uint32_t* bstart,
+                         const uint32_t* bend, uint32_t* tbl, int64_t* pool, const uint32_t* packed,
+                         uint32_t* tsize, void* ctr, hipStream_t st) {
+    hipLaunchKernelGGL((replay_kernel<MG, View>), dim3(mp.table_size), dim3(kBlock), 0, st, v, N, gt, mp, ss,
+                       probe_info, sorted_ids, bstart, bend, tbl, pool, packed, tsize, (DevCounters*)ctr);
     return hipGetLastError();
 }
 
@@ -275,18 +277,21 @@ hipError_t launch_emit(const uint32_t* tsize, const uint32_t* obase, const uint3
     return hipGetLastError();
 }
 
-#define MUMS_INST_REPLAY(MG, K)                                                                                    \
-    template hipError_t launch_replay<MG, K>(const K*, const uint32_t*, uint64_t, const GenomeTable&,             \
-                                             const MatchParams&, int, const uint32_t*, const uint32_t*,            \
-                                             const uint32_t*, uint32_t*, int64_t*, const K*, uint32_t*, void*,     \
-                                             hipStream_t);
-MUMS_INST_REPLAY(4, uint32_t)
-MUMS_INST_REPLAY(8, uint32_t)
-MUMS_INST_REPLAY(16, uint32_t)
-MUMS_INST_REPLAY(32, uint32_t)
-MUMS_INST_REPLAY(4, uint64_t)
-MUMS_INST_REPLAY(8, uint64_t)
-MUMS_INST_REPLAY(16, uint64_t)
-MUMS_INST_REPLAY(32, uint64_t)
+#define MUMS_INST_REPLAY(MG, V)                                                                                   \
+    template hipError_t launch_replay<MG, V>(V, uint64_t, const GenomeTable&, const MatchParams&, const SeedSpec&, \
+                                             const uint64_t*, const uint32_t*, const uint32_t*, const uint32_t*,  \
+                                             uint32_t*, int64_t*, const uint32_t*, uint32_t*, void*, hipStream_t);
+MUMS_INST_REPLAY(4, PairView<uint32_t>)
+MUMS_INST_REPLAY(8, PairView<uint32_t>)
+MUMS_INST_REPLAY(16, PairView<uint32_t>)
+MUMS_INST_REPLAY(32, PairView<uint32_t>)
+MUMS_INST_REPLAY(4, PairView<uint64_t>)
+MUMS_INST_REPLAY(8, PairView<uint64_t>)
+MUMS_INST_REPLAY(16, PairView<uint64_t>)
+MUMS_INST_REPLAY(32, PairView<uint64_t>)
+MUMS_INST_REPLAY(4, RecView)
+MUMS_INST_REPLAY(8, RecView)
+MUMS_INST_REPLAY(16, RecView)
+MUMS_INST_REPLAY(32, RecView)
 
 }  // namespace mums

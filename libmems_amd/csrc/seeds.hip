@@ -1,4 +1,4 @@
-// seeds.hip -- ASCII -> canonical spaced-seed keys, one pass over HBM (rows A2-A4).
+// seeds.hip -- ASCII -> 2-bit packed genome + canonical spaced-seed keys (rows A2-A4).
 //
 // Reference: translate32 (SortedMerList.cpp:425-460) packs 2 bits/base with the
 // BasicDNATable (:29-47); GetSeedMer (:726-762) gathers the care bases of the
@@ -6,84 +6,97 @@
 // the forward and reverse-complement seeds (reverse gets bit 0 set);
 // FillDnaSeedSML (:771-783) does this for positions 0..n-L.
 //
-// MI355X mapping: one workgroup per 4096-position tile of one genome.  The tile's
-// ASCII (+L-1 halo) is read once with 16-B loads, 2-bit packed into LDS, and
-// each lane derives 16 keys from LDS windows; key stores are lane-contiguous.
-// HBM traffic per seed-mer: 1 B read + 4/8 B written.
-#include "mums_internal.h"
+// MI355X mapping: one workgroup per 4096-position tile of one genome.
+//   seed_pack_kernel   : the tile's ASCII (+L-1 halo) is read once with 16-B loads,
+//                        2-bit packed in LDS (written out: the packed genome is the only
+//                        copy of the sequence the later stages read), keys derived
+//                        from LDS windows; then either the per-position key array
+//                        (pair path) or a per-tile histogram of the top B key bits
+//                        (packed path, MSD split of the sort).
+//   seed_scatter_kernel: packed path, second pass: re-derives the keys from the packed
+//                        words (0.25 B/base), ranks them stably by MSD bucket with
+//                        wave64 ballot match-any, reorders through LDS and writes
+//                        (ckey_low << 32 | index) records into their buckets.
+// HBM bytes per seed-mer: pack 1 + 0.25 (packed path) ; scatter 0.25 + 8.
+#include "seed_device.h"
 
 namespace mums {
 
 namespace {
 
-constexpr int kTile = 4096;                 // positions per workgroup
+constexpr int kTile = kSeedTile;            // positions per workgroup
 constexpr int kPerThread = kTile / kBlock;  // 16
 constexpr int kHalo = 32;                   // >= L-1, rounded to 16
 constexpr int kTileBytes = kTile + kHalo;
 constexpr int kTileWords = kTileBytes / 16 + 3;
+constexpr int kWaves = kBlock / 64;
 
 struct AsciiPtrs { const char* p[kMaxG]; };
 
 // BasicDNATable (SortedMerList.cpp:29-47): c,b,y->1  g,s,k->2  t->3 (either case), else 0.
 __device__ __forceinline__ uint32_t dna2(uint32_t c) {
-    uint32_t lc = c | 0x20u;
-    uint32_t one = (lc == 'c') | (lc == 'b') | (lc == 'y');
-    uint32_t two = (lc == 'g') | (lc == 's') | (lc == 'k');
-    uint32_t three = (lc == 't');
+    const uint32_t lc = c | 0x20u;
+    const uint32_t one = (lc == 'c') | (lc == 'b') | (lc == 'y');
+    const uint32_t two = (lc == 'g') | (lc == 's') | (lc == 'k');
+    const uint32_t three = (lc == 't');
     return one | (two << 1) | (three * 3u);
 }
 
-// reverse complement of a 2w-bit value (RevCompMer restated on bottom-aligned bits)
-__device__ __forceinline__ uint64_t revcomp2w(uint64_t v, int w) {
-    uint64_t x = ~v;
-    x = __builtin_bitreverse64(x);
-    x = ((x >> 1) & 0x5555555555555555ull) | ((x & 0x5555555555555555ull) << 1);
-    return x >> (64 - 2 * w);
+__device__ __forceinline__ int tile_genome(const GenomeTable& gt, uint32_t t) {
+    int g = 0;
+    for (int k = 1; k < gt.G; ++k) g += (t >= gt.tfirst[k]) ? 1 : 0;
+    return g;
 }
 
-template <typename K>
-__global__ __launch_bounds__(kBlock) void seed_keys_kernel(SeedSpec ss, GenomeTable gt, AsciiPtrs ap,
-                                                           K* __restrict__ ckey, uint32_t* __restrict__ err) {
+template <int kMode, typename K>
+__global__ __launch_bounds__(kBlock) void seed_pack_kernel(SeedSpec ss, GenomeTable gt, AsciiPtrs ap,
+                                                           uint32_t* __restrict__ packed, K* __restrict__ ckey,
+                                                           int msd_bits, uint32_t* __restrict__ hist, uint32_t T,
+                                                           uint32_t* __restrict__ err) {
     __shared__ uint8_t bytes[kTileBytes + 16];
     __shared__ uint32_t words[kTileWords];
-    const int g = blockIdx.y;
+    __shared__ uint32_t bh[1 << kMaxMsdBits];
+    const uint32_t t = blockIdx.x;
+    const int g = tile_genome(gt, t);
+    const uint32_t x = t - gt.tfirst[g];
     const uint64_t n = gt.n[g];
     const uint64_t m = gt.m[g];
-    const uint64_t p0 = (uint64_t)blockIdx.x * kTile;
-    if (p0 >= n && !(p0 == 0 && n > 0)) return;
+    const uint64_t p0 = (uint64_t)x * kTile;
     const char* src = ap.p[g];
     const uint64_t avail = n - p0 < (uint64_t)kTileBytes ? n - p0 : (uint64_t)kTileBytes;
     const int tid = threadIdx.x;
+    const int nb = kMode == 1 ? (1 << msd_bits) : 0;
+    for (int i = tid; i < nb; i += kBlock) bh[i] = 0;
 
     // 1) stage the tile's ASCII in LDS (16-B loads when aligned)
-    uint32_t bad = 0;
     const bool aligned = (((uintptr_t)(src + p0)) & 15) == 0;
     if (aligned) {
         for (int c = tid; c * 16 < kTileBytes; c += kBlock) {
-            uint64_t off = (uint64_t)c * 16;
+            const uint64_t off = (uint64_t)c * 16;
             uint4 v = make_uint4(0, 0, 0, 0);
             if (off + 16 <= avail) {
                 v = *reinterpret_cast<const uint4*>(src + p0 + off);
             } else if (off < avail) {
-                uint8_t tmp[16] = {0};
-                for (uint64_t k = 0; k < avail - off; ++k) tmp[k] = (uint8_t)src[p0 + off + k];
-                v = *reinterpret_cast<uint4*>(tmp);
+                uint32_t wv[4] = {0, 0, 0, 0};
+                for (uint64_t k = 0; k < avail - off; ++k)
+                    wv[k >> 2] |= (uint32_t)(uint8_t)src[p0 + off + k] << (8 * (k & 3));
+                v = make_uint4(wv[0], wv[1], wv[2], wv[3]);
             }
             *reinterpret_cast<uint4*>(&bytes[off]) = v;
         }
     } else {
-        for (int c = tid; c < kTileBytes; c += kBlock)
-            bytes[c] = (uint64_t)c < avail ? (uint8_t)src[p0 + c] : 0;
+        for (int c = tid; c < kTileBytes; c += kBlock) bytes[c] = (uint64_t)c < avail ? (uint8_t)src[p0 + c] : 0;
     }
     __syncthreads();
 
     // 2) 2-bit pack 16 bases per word (MSB first, as translate32); detect '-'
+    uint32_t bad = 0;
     for (int wi = tid; wi < kTileWords; wi += kBlock) {
         uint32_t word = 0;
         #pragma unroll
         for (int k = 0; k < 16; ++k) {
-            int b = wi * 16 + k;
-            uint32_t c = b < kTileBytes ? bytes[b] : 0;
+            const int b = wi * 16 + k;
+            const uint32_t c = b < kTileBytes ? bytes[b] : 0;
             bad |= (c == '-') && ((uint64_t)b < avail);
             word |= dna2(c) << (30 - 2 * k);
         }
@@ -91,51 +104,235 @@ __global__ __launch_bounds__(kBlock) void seed_keys_kernel(SeedSpec ss, GenomeTa
     }
     if (bad) atomicOr(err, 1u);
     __syncthreads();
+    {   // this tile's packed words (the last tile also writes the two pad words)
+        const uint64_t pw = packed_words(n);
+        uint32_t* out = packed + gt.woff[g];
+        for (int k = tid; k < kTile / 16 + 2; k += kBlock) {
+            const uint64_t wi = (uint64_t)x * (kTile / 16) + k;
+            if ((k < kTile / 16 || p0 + kTile >= n) && wi < pw) out[wi] = words[k];
+        }
+    }
 
-    // 3) canonical key per position
+    // 3) keys
+    if (kMode == 1 && nb <= 1) return;   // no MSD split: the scatter pass derives the keys
     const uint64_t base = gt.base[g];
-    const uint64_t vmask = (ss.w >= 32) ? ~0ull : ((1ull << (2 * ss.w)) - 1);
+    const int klow = 2 * ss.w + 1 - msd_bits;
     #pragma unroll 4
     for (int j = 0; j < kPerThread; ++j) {
         const int q = tid + j * kBlock;
         const uint64_t p = p0 + (uint64_t)q;
         if (p >= m) break;
         const int wi = q >> 4, sh = 2 * (q & 15);
-        uint64_t hi = ((uint64_t)words[wi] << 32) | words[wi + 1];
-        uint64_t lo = words[wi + 2];
-        uint64_t mer = (hi << sh) | ((lo << sh) >> 32);
-        uint64_t v = 0;
-        for (int r = 0; r < ss.nruns; ++r) {
-            const int s = ss.run_start[r], l = ss.run_len[r];
-            uint64_t bits = (mer >> (64 - 2 * (s + l))) & ((1ull << (2 * l)) - 1);
-            v |= bits << ss.run_dst[r];
-        }
-        v &= vmask;
-        const uint64_t rc = revcomp2w(v, ss.w);
-        const uint64_t par = rc < v ? 1ull : 0ull;
-        const uint64_t kv = ((par ? rc : v) << 1) | par;
-        ckey[base + p] = (K)kv;
+        const uint64_t hi = ((uint64_t)words[wi] << 32) | words[wi + 1];
+        const uint64_t lo = words[wi + 2];
+        const uint64_t kv = ckey_from_mer((hi << sh) | ((lo << sh) >> 32), ss);
+        if (kMode == 0) ckey[base + p] = (K)kv;
+        else if (nb > 1) atomicAdd(&bh[(uint32_t)(kv >> klow)], 1u);
     }
+    if (kMode == 1 && nb > 1) {
+        __syncthreads();
+        for (int i = tid; i < nb; i += kBlock) hist[(uint64_t)i * T + t] = bh[i];
+    }
+}
+
+template <int kMaxDig>
+__global__ __launch_bounds__(kBlock) void seed_scatter_kernel(SeedSpec ss, GenomeTable gt,
+                                                              const uint32_t* __restrict__ packed, int msd_bits,
+                                                              const uint32_t* __restrict__ hist, uint32_t T,
+                                                              uint64_t* __restrict__ rec) {
+    __shared__ uint32_t words[kTileWords];
+    __shared__ uint64_t srec[kTile];
+    __shared__ uint16_t sdig[kTile];
+    __shared__ uint32_t wcnt[kWaves][kMaxDig];
+    __shared__ uint32_t lstart[kMaxDig];
+    __shared__ uint32_t gofs[kMaxDig];
+    __shared__ uint32_t s_w[kWaves];
+    const uint32_t t = blockIdx.x;
+    const int g = tile_genome(gt, t);
+    const uint32_t x = t - gt.tfirst[g];
+    const uint64_t m = gt.m[g];
+    const uint64_t p0 = (uint64_t)x * kTile;
+    if (p0 >= m) return;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int nd = 1 << msd_bits;
+    const int klow = 2 * ss.w + 1 - msd_bits;
+    const uint64_t lmask = (klow >= 64) ? ~0ull : ((1ull << klow) - 1);
+    const uint64_t pw = packed_words(gt.n[g]);
+    const uint32_t* W = packed + gt.woff[g];
+    for (int k = tid; k < kTileWords; k += kBlock) {
+        const uint64_t wi = (uint64_t)x * (kTile / 16) + k;
+        words[k] = wi < pw ? W[wi] : 0u;
+    }
+    for (int i = tid; i < kWaves * kMaxDig; i += kBlock) (&wcnt[0][0])[i] = 0;
+    __syncthreads();
+
+    const uint64_t base = gt.base[g];
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const int q0 = wv * (kTile / kWaves);
+    uint64_t r_rec[kPerThread];
+    uint32_t r_dig[kPerThread], r_rank[kPerThread];
+    #pragma unroll
+    for (int r = 0; r < kPerThread; ++r) {
+        const int q = q0 + r * 64 + lane;
+        const uint64_t p = p0 + (uint64_t)q;
+        const bool valid = p < m;
+        const int wi = q >> 4, sh = 2 * (q & 15);
+        const uint64_t hi = ((uint64_t)words[wi] << 32) | words[wi + 1];
+        const uint64_t lo = words[wi + 2];
+        const uint64_t kv = ckey_from_mer((hi << sh) | ((lo << sh) >> 32), ss);
+        const uint32_t d = valid ? (uint32_t)(kv >> klow) : 0u;
+        r_rec[r] = ((kv & lmask) << 32) | (base + p);
+        r_dig[r] = d;
+        uint64_t peers = __ballot(valid);
+        for (int b = 0; b < msd_bits; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            peers &= bit ? bb : ~bb;
+        }
+        const uint32_t rk = (uint32_t)__popcll(peers & lt);
+        uint32_t old = 0;
+        if (valid) old = wcnt[wv][d];
+        if (valid && rk == 0) wcnt[wv][d] = old + (uint32_t)__popcll(peers);
+        r_rank[r] = old + rk;
+    }
+    __syncthreads();
+    // per-digit wave offsets, block-local digit starts (each thread owns nd/256 digits)
+    {
+        const int per = (nd + kBlock - 1) / kBlock;
+        uint32_t tot_mine = 0;
+        for (int k = 0; k < per; ++k) {
+            const int d = tid * per + k;
+            if (d >= nd) break;
+            uint32_t acc = 0;
+            #pragma unroll
+            for (int w = 0; w < kWaves; ++w) { const uint32_t c = wcnt[w][d]; wcnt[w][d] = acc; acc += c; }
+            lstart[d] = acc;  // temporarily the digit total
+            tot_mine += acc;
+            gofs[d] = hist[(uint64_t)d * T + t];
+        }
+        uint32_t v = tot_mine;
+        #pragma unroll
+        for (int dd = 1; dd < 64; dd <<= 1) {
+            const uint32_t y = __shfl_up(v, dd, 64);
+            if (lane >= dd) v += y;
+        }
+        if (lane == 63) s_w[wv] = v;
+        __syncthreads();
+        uint32_t pre = v - tot_mine;
+        #pragma unroll
+        for (int w = 0; w < kWaves; ++w) pre += (w < wv) ? s_w[w] : 0u;
+        for (int k = 0; k < per; ++k) {
+            const int d = tid * per + k;
+            if (d >= nd) break;
+            const uint32_t c = lstart[d];
+            lstart[d] = pre;
+            pre += c;
+        }
+    }
+    __syncthreads();
+    #pragma unroll
+    for (int r = 0; r < kPerThread; ++r) {
+        const uint64_t p = p0 + (uint64_t)(q0 + r * 64 + lane);
+        if (p < m) {
+            const uint32_t d = r_dig[r];
+            const uint32_t lp = lstart[d] + wcnt[wv][d] + r_rank[r];
+            srec[lp] = r_rec[r];
+            sdig[lp] = (uint16_t)d;
+        }
+    }
+    __syncthreads();
+    const uint64_t cnt = (m - p0) < (uint64_t)kTile ? (m - p0) : (uint64_t)kTile;
+    #pragma unroll
+    for (int r = 0; r < kPerThread; ++r) {
+        const uint32_t s = tid + r * kBlock;
+        if (s < cnt) {
+            const uint32_t d = sdig[s];
+            rec[(uint64_t)gofs[d] + (s - lstart[d])] = srec[s];
+        }
+    }
+}
+
+// B == 0: one bucket, records land at their global index
+__global__ __launch_bounds__(kBlock) void seed_scatter_flat_kernel(SeedSpec ss, GenomeTable gt,
+                                                                   const uint32_t* __restrict__ packed,
+                                                                   uint64_t* __restrict__ rec) {
+    __shared__ uint32_t words[kTileWords];
+    const uint32_t t = blockIdx.x;
+    const int g = tile_genome(gt, t);
+    const uint32_t x = t - gt.tfirst[g];
+    const uint64_t m = gt.m[g];
+    const uint64_t p0 = (uint64_t)x * kTile;
+    if (p0 >= m) return;
+    const uint64_t pw = packed_words(gt.n[g]);
+    const uint32_t* W = packed + gt.woff[g];
+    for (int k = threadIdx.x; k < kTileWords; k += kBlock) {
+        const uint64_t wi = (uint64_t)x * (kTile / 16) + k;
+        words[k] = wi < pw ? W[wi] : 0u;
+    }
+    __syncthreads();
+    const uint64_t base = gt.base[g];
+    #pragma unroll 4
+    for (int j = 0; j < kPerThread; ++j) {
+        const int q = threadIdx.x + j * kBlock;
+        const uint64_t p = p0 + (uint64_t)q;
+        if (p >= m) break;
+        const int wi = q >> 4, sh = 2 * (q & 15);
+        const uint64_t hi = ((uint64_t)words[wi] << 32) | words[wi + 1];
+        const uint64_t lo = words[wi + 2];
+        const uint64_t kv = ckey_from_mer((hi << sh) | ((lo << sh) >> 32), ss);
+        rec[base + p] = (kv << 32) | (base + p);
+    }
+}
+
+__global__ void keys_of_genome_kernel(SeedSpec ss, const uint32_t* __restrict__ W, uint64_t m,
+                                      uint64_t* __restrict__ out) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= m) return;
+    const uint64_t k = ckey_at(W, p, ss);
+    out[p] = ((k >> 1) << (64 - 2 * ss.w)) | (k & 1);   // GetDnaSeedMer's left-aligned form
 }
 
 }  // namespace
 
-hipError_t launch_seed_keys(const SeedSpec& ss, const GenomeTable& gt, const char* const* d_ascii,
-                            void* d_ckey, bool key64, uint32_t* d_err, hipStream_t st) {
+hipError_t launch_seed_pack(const SeedSpec& ss, const GenomeTable& gt, const char* const* d_ascii,
+                            uint32_t* d_packed, int mode, bool key64, void* d_ckey, int msd_bits,
+                            uint32_t* d_hist, uint32_t ntiles, uint32_t* d_err, hipStream_t st) {
     AsciiPtrs ap{};
-    uint64_t maxn = 0;
-    for (int g = 0; g < gt.G; ++g) {
-        ap.p[g] = d_ascii[g];
-        if (gt.n[g] > maxn) maxn = gt.n[g];
+    for (int g = 0; g < gt.G; ++g) ap.p[g] = d_ascii[g];
+    if (ntiles == 0) return hipSuccess;
+    if (mode == 0) {
+        if (key64)
+            hipLaunchKernelGGL((seed_pack_kernel<0, uint64_t>), dim3(ntiles), dim3(kBlock), 0, st, ss, gt, ap,
+                               d_packed, (uint64_t*)d_ckey, 0, d_hist, ntiles, d_err);
+        else
+            hipLaunchKernelGGL((seed_pack_kernel<0, uint32_t>), dim3(ntiles), dim3(kBlock), 0, st, ss, gt, ap,
+                               d_packed, (uint32_t*)d_ckey, 0, d_hist, ntiles, d_err);
+    } else {
+        hipLaunchKernelGGL((seed_pack_kernel<1, uint64_t>), dim3(ntiles), dim3(kBlock), 0, st, ss, gt, ap, d_packed,
+                           (uint64_t*)nullptr, msd_bits, d_hist, ntiles, d_err);
     }
-    if (maxn == 0) return hipSuccess;
-    dim3 grid((unsigned)((maxn + kTile - 1) / kTile), (unsigned)gt.G);
-    if (key64)
-        hipLaunchKernelGGL(seed_keys_kernel<uint64_t>, grid, dim3(kBlock), 0, st, ss, gt, ap,
-                           (uint64_t*)d_ckey, d_err);
+    return hipGetLastError();
+}
+
+hipError_t launch_seed_scatter(const SeedSpec& ss, const GenomeTable& gt, const uint32_t* d_packed, int msd_bits,
+                               const uint32_t* d_hist_scanned, uint32_t ntiles, uint64_t* d_rec, hipStream_t st) {
+    if (ntiles == 0) return hipSuccess;
+    if (msd_bits == 0)
+        hipLaunchKernelGGL(seed_scatter_flat_kernel, dim3(ntiles), dim3(kBlock), 0, st, ss, gt, d_packed, d_rec);
+    else if (msd_bits <= 8)
+        hipLaunchKernelGGL(seed_scatter_kernel<256>, dim3(ntiles), dim3(kBlock), 0, st, ss, gt, d_packed, msd_bits,
+                           d_hist_scanned, ntiles, d_rec);
     else
-        hipLaunchKernelGGL(seed_keys_kernel<uint32_t>, grid, dim3(kBlock), 0, st, ss, gt, ap,
-                           (uint32_t*)d_ckey, d_err);
+        hipLaunchKernelGGL(seed_scatter_kernel<(1 << kMaxMsdBits)>, dim3(ntiles), dim3(kBlock), 0, st, ss, gt,
+                           d_packed, msd_bits, d_hist_scanned, ntiles, d_rec);
+    return hipGetLastError();
+}
+
+hipError_t launch_keys_of_genome(const SeedSpec& ss, const uint32_t* d_words, uint64_t m, uint64_t* d_out,
+                                 hipStream_t st) {
+    if (m == 0) return hipSuccess;
+    hipLaunchKernelGGL(keys_of_genome_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, ss, d_words, m,
+                       d_out);
     return hipGetLastError();
 }
 
