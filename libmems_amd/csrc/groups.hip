@@ -65,7 +65,10 @@ __global__ __launch_bounds__(kBlock) void probe_tile_kernel(View v, const SegTil
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const SegTile td = tiles[blockIdx.x];
     if (td.count == 0) {
-        if (threadIdx.x == 0) tile_count[blockIdx.x] = 0;
+        if (threadIdx.x == 0) {
+            tile_count[blockIdx.x] = 0;
+            tile_count[gridDim.x + 32 + blockIdx.x] = 0;
+        }
         return;
     }
     const uint64_t tile0 = td.start;
@@ -100,17 +103,25 @@ __global__ __launch_bounds__(kBlock) void probe_tile_kernel(View v, const SegTil
     __syncthreads();
     const uint32_t H = s_red[0];
 
-    // 2) one probe per lane
+    // 2) one probe per lane (offset only: the replay rebuilds the starts)
     uint32_t nrep = 0;
+    const bool fast = mp.repeat_tol == 0 && mp.enum_tol == 1;
     for (uint32_t j = threadIdx.x; j < H; j += kBlock) {
-        Mhe<MG> P;
         uint32_t gsz = 0;
-        const bool ok = build_probe<MG, View>(v, tile0 + heads[j], td.bend, gt, mp, L, P, &gsz);
+        int64_t off = 0;
+        bool ok;
+        if (fast) {
+            ok = probe_offset_fast<MG, View>(v, tile0 + heads[j], td.bend, gt, mp, L, &off, &gsz);
+        } else {
+            Mhe<MG> P;
+            ok = build_probe<MG, View>(v, tile0 + heads[j], td.bend, gt, mp, L, P, &gsz);
+            off = P.offset;
+        }
         nrep += gsz > (uint32_t)kRepeatLimit;
-        okb[j] = ok ? (0x80000000u | bucket_of(P.offset, mp.table_size)) : 0u;
+        okb[j] = ok ? (0x80000000u | bucket_of(off, mp.table_size)) : 0u;
         gsz16[j] = (uint16_t)(gsz > 65535u ? 65535u : gsz);
     }
-    if (nrep) atomicAdd(&ctr->repeat_limit, (unsigned long long)nrep);
+    if (nrep) atomicAdd(&ctr->repeat_limit, (unsigned long long)nrep);   // rare (repeat-rich input only)
     __syncthreads();
 
     // 3) compact accepted probes in head order into this tile's slots
@@ -130,7 +141,7 @@ __global__ __launch_bounds__(kBlock) void probe_tile_kernel(View v, const SegTil
     }
     if (threadIdx.x == 0) {
         tile_count[blockIdx.x] = base;
-        atomicAdd(&ctr->groups, (unsigned long long)H);
+        tile_count[gridDim.x + 32 + blockIdx.x] = H;   // per-tile group count (summed by the host side)
     }
 }
 

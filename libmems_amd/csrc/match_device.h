@@ -7,6 +7,7 @@
 #pragma once
 
 #include "mums_internal.h"
+#include "seed_device.h"
 
 namespace mums {
 
@@ -194,6 +195,83 @@ __device__ __forceinline__ bool build_probe(const View& v, uint64_t h, uint64_t 
     P.offset = off;
     if (mp.masked) return mp.seq_mask == 0 || match_number == mp.seq_mask;
     return mult >= 2;
+}
+
+// genome of a global seed-mer index, unrolled to MG so the bases stay in SGPRs
+template <int MG>
+__device__ __forceinline__ int genome_of_mg(const GenomeTable& gt, uint64_t i) {
+    int g = 0;
+    #pragma unroll
+    for (int k = 1; k < MG; ++k) g += (k < gt.G && i >= gt.base[k]) ? 1 : 0;
+    return g;
+}
+
+// Fast path of build_probe for the MemHash defaults repeat_tol = 0, enum_tol = 1
+// (MemHash.h:31-32): accept iff >= 2 records and no genome twice; the probe offset
+// (CalculateOffset, MatchHashEntry.cpp:141-160, after SetDirection) is summed
+// directly without materialising the starts.  An accepted group has <= G records,
+// so G+1 records are fetched as ONE batch of independent loads (no dependent load
+// chain); only groups larger than G fall back to a counting walk (for the
+// MER_REPEAT_LIMIT report).  Same results as build_probe.
+template <int MG, typename View>
+__device__ __forceinline__ bool probe_offset_fast(const View& v, uint64_t h, uint64_t end, const GenomeTable& gt,
+                                                  const MatchParams& mp, int L, int64_t* offset, uint32_t* gsize) {
+    const uint32_t G = (uint32_t)gt.G;
+    RecFields r[MG + 1];
+    #pragma unroll
+    for (int k = 0; k <= MG; ++k)
+        r[k] = ((uint32_t)k <= G && h + k < end) ? v.get(h + k) : RecFields{~0ull, 0u, 0u};
+    const uint64_t k0 = r[0].gk;
+    uint32_t cnt = 0;
+    bool run = true;
+    #pragma unroll
+    for (int k = 0; k <= MG; ++k) {
+        run = run && (r[k].gk == k0);
+        cnt += run ? 1u : 0u;
+    }
+    if (cnt > G) {   // pigeonhole: some genome twice -> rejected; count on for the report
+        uint64_t i = h + cnt;
+        while (i < end && cnt <= (uint32_t)kRepeatLimit && v.gkey(i) == k0) { ++cnt; ++i; }
+        *gsize = cnt;
+        return false;
+    }
+    *gsize = cnt;
+    if (cnt < 2) return false;
+    uint32_t mask = 0;
+    bool dup = false;
+    int gref = 64;
+    int64_t sref = 0;
+    uint32_t pref = 0;
+    int gk[MG + 1];
+    #pragma unroll
+    for (int k = 0; k <= MG; ++k) {
+        gk[k] = genome_of_mg<MG>(gt, r[k].idx);
+        if ((uint32_t)k < cnt) {
+            const int g = gk[k];
+            dup = dup || ((mask >> g) & 1u);
+            mask |= 1u << g;
+            if (g < gref) {
+                gref = g;
+                sref = (int64_t)(r[k].idx - gt.base[g]) + 1;
+                pref = r[k].par;
+            }
+        }
+    }
+    if (dup) return false;
+    int64_t off = 0;
+    #pragma unroll
+    for (int k = 0; k <= MG; ++k) {
+        if ((uint32_t)k < cnt && gk[k] != gref) {
+            const int64_t s = (int64_t)(r[k].idx - gt.base[gk[k]]) + 1;
+            off += (r[k].par != pref) ? (-s - sref - (int64_t)L) : (s - sref);
+        }
+    }
+    *offset = off;
+    if (mp.masked) {
+        const uint64_t match_number = (uint64_t)(__builtin_bitreverse32(mask) >> (32 - G));
+        return mp.seq_mask == 0 || match_number == mp.seq_mask;
+    }
+    return true;
 }
 
 __device__ __forceinline__ uint32_t bucket_of(int64_t offset, uint32_t table_size) {

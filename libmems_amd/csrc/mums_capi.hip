@@ -155,11 +155,13 @@ template <int MG, typename View>
 int run_groups(mums_ctx* ctx, View v, const SegTile* tiles, uint64_t ntiles, const MatchParams& mp,
                uint64_t* probe_info, uint32_t* probe_bucket, uint64_t* slot_info, uint32_t* slot_bucket,
                hipStream_t st) {
-    uint32_t* counts = ctx->partials.as<uint32_t>();
-    uint32_t* offs = counts + ntiles + 32;
+    uint32_t* counts = ctx->partials.as<uint32_t>();          // [ntiles] probes, then [ntiles] groups
+    uint32_t* gcounts = counts + ntiles + 32;
+    uint32_t* offs = gcounts + ntiles + 32;
     DevCounters* dc = ctx->counters.as<DevCounters>();
     HIPCHK((launch_probe_tiles<MG, View>(v, tiles, ntiles, ctx->N, ctx->gt, mp, ctx->L, counts, slot_info, slot_bucket,
                                          dc, st)));
+    HIPCHK(exclusive_scan_u32(gcounts, ntiles, ctx->tmp.p, &dc->ngroups, st));
     HIPCHK(hipMemcpyAsync(offs, counts, ntiles * 4, hipMemcpyDeviceToDevice, st));
     HIPCHK(exclusive_scan_u32(offs, ntiles, ctx->tmp.p, &dc->nprobes, st));
     HIPCHK(launch_probe_compact(ntiles, counts, offs, slot_info, slot_bucket, probe_info, probe_bucket, st));
@@ -250,7 +252,7 @@ int run_pipeline(mums_ctx* ctx, int stage) {
         tmpb = std::max(tmpb, radix_tmp_bytes(N));
     }
     HIPCHK(ctx->tmp.ensure(tmpb));
-    HIPCHK(ctx->partials.ensure((2 * ntiles_groups + 128) * 4));
+    HIPCHK(ctx->partials.ensure((3 * ntiles_groups + 128) * 4));
     HIPCHK(ctx->pbuf.ensure(pcap * (8 + 4 * 4) + nslots * 12 + 256));
     char* pb = (char*)ctx->pbuf.p;
     uint64_t* probe_info = (uint64_t*)pb;
@@ -386,7 +388,7 @@ int run_pipeline(mums_ctx* ctx, int stage) {
     mums_stats& s = ctx->st;
     s = mums_stats{};
     s.seedmers = N;
-    s.groups = ctx->hc.groups;
+    s.groups = ctx->hc.ngroups;
     s.probes = ctx->P;
     s.repeat_limit_groups = ctx->hc.repeat_limit;
     auto el = [&](int a, int b) {

@@ -67,6 +67,8 @@ struct DevCounters {
     uint32_t ntiles;                  // segmented tiles in use
     uint32_t nprobes;                 // accepted probes (scan total)
     uint32_t nmatches;                // output matches (scan total)
+    uint32_t ngroups;                 // distinct masked keys (scan total of per-tile counts)
+    uint32_t pad;
 };
 
 // A tile of the segmented (per-MSD-bucket) sort/group passes.  Tiles never

@@ -45,6 +45,12 @@ __device__ __forceinline__ uint64_t ckey_at(const uint32_t* __restrict__ W, uint
 }
 
 // ---- views of the merged, key-sorted stream ------------------------------------
+struct RecFields {
+    uint64_t gk;    // group key (masked ckey)
+    uint32_t par;   // strand parity
+    uint32_t idx;   // global seed-mer index
+};
+
 // PairView: (ckey, global index) pairs (generic path, any weight).
 template <typename K>
 struct PairView {
@@ -53,6 +59,10 @@ struct PairView {
     __device__ __forceinline__ uint64_t gkey(uint64_t i) const { return (uint64_t)key[i] >> 1; }
     __device__ __forceinline__ uint32_t par(uint64_t i) const { return (uint32_t)(key[i] & 1); }
     __device__ __forceinline__ uint32_t gidx(uint64_t i) const { return idx[i]; }
+    __device__ __forceinline__ RecFields get(uint64_t i) const {
+        const uint64_t k = (uint64_t)key[i];
+        return RecFields{k >> 1, (uint32_t)(k & 1), idx[i]};
+    }
 };
 
 // RecView: packed records (ckey_low << 32 | global index); the top ckey bits are the
@@ -62,6 +72,10 @@ struct RecView {
     __device__ __forceinline__ uint64_t gkey(uint64_t i) const { return rec[i] >> 33; }
     __device__ __forceinline__ uint32_t par(uint64_t i) const { return (uint32_t)(rec[i] >> 32) & 1u; }
     __device__ __forceinline__ uint32_t gidx(uint64_t i) const { return (uint32_t)rec[i]; }
+    __device__ __forceinline__ RecFields get(uint64_t i) const {
+        const uint64_t r = rec[i];
+        return RecFields{r >> 33, (uint32_t)(r >> 32) & 1u, (uint32_t)r};
+    }
 };
 
 }  // namespace mums
