@@ -26,7 +26,10 @@ constexpr int kMaxG = 32;            // genomes per context (register arrays in 
 constexpr int kRepeatLimit = 1000;   // MER_REPEAT_LIMIT, MatchFinder.cpp:166
 constexpr int kBlock = 256;          // threads per workgroup (4 waves of 64)
 constexpr int kSeedTile = 4096;      // positions per key-kernel workgroup
-constexpr int kSegTile = 4096;       // records per sort / group tile
+#ifndef MUMS_SEG_TILE
+#define MUMS_SEG_TILE 4096
+#endif
+constexpr int kSegTile = MUMS_SEG_TILE; // records per sort / group tile
 constexpr int kMaxMsdBits = 11;      // packed path: 2w+1 <= 32 + 11
 
 // Per-run constants shared by the kernels (passed by value).
@@ -82,7 +85,7 @@ struct SegTile {
     uint32_t ntb;       // tiles in this bucket
     uint32_t tb;        // index of this tile within the bucket
     uint32_t bucket;    // MSD bucket id
-    uint32_t pad;
+    uint32_t order;     // onesweep claim order: the c-th claimed block sorts tile tiles[c].order
 };
 
 // genome of a global seed-mer index (G <= 32: linear scan is cheapest)

@@ -22,7 +22,11 @@ constexpr int kTile = kSegTile;
 constexpr int kRounds = kTile / kBlock;  // 16
 constexpr int kWaves = kBlock / 64;
 constexpr int kDigits = 256;
-constexpr int kOnesweepIPT = 16;   // records per thread per onesweep tile (tile = kSegTile)
+constexpr int kOnesweepIPT = kTile / kBlock;   // records per thread per onesweep tile (tile = kSegTile)
+#ifndef MUMS_LOOKBACK
+#define MUMS_LOOKBACK 4
+#endif
+constexpr int kLookback = MUMS_LOOKBACK;       // predecessor statuses fetched per look-back step
 inline uint64_t ub_status(uint64_t ub, int npass) { return ub * kDigits * (uint64_t)npass; }
 
 // bucket starts from the scanned MSD histogram: bstart[b] = scanned[b * T], bstart[nb] = n
@@ -80,6 +84,33 @@ __global__ void tiles_kernel(const uint32_t* __restrict__ bstart, const uint32_t
         d.tb = 0;
     }
     tiles[t] = d;
+}
+
+// Claim order of the onesweep passes.  A tile waits only on the preceding tiles of
+// its own MSD bucket, so the buckets are independent look-back chains.  Claiming
+// tiles bucket-major would put every resident block on ONE chain (whose inclusive
+// prefix advances one look-back round trip at a time); claiming them in
+// (tile-in-bucket, bucket) order spreads the resident blocks over all chains.  A
+// tile's predecessor still precedes it in this order, so every tile a block waits
+// on was claimed earlier: forward progress is kept.
+// pos(k, b) = sum_b' min(ntb_b', k) + #{b' < b : ntb_b' > k}.
+__global__ __launch_bounds__(256) void claim_order_kernel(const uint32_t* __restrict__ tfirst, int nb, uint64_t ub,
+                                                          SegTile* __restrict__ tiles) {
+    __shared__ uint32_t s_n[1 << kMaxMsdBits];
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) s_n[b] = tfirst[b + 1] - tfirst[b];
+    __syncthreads();
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ub) return;
+    const uint32_t total = tfirst[nb];
+    if (t >= total) { tiles[t].order = (uint32_t)t; return; }
+    const SegTile d = tiles[t];
+    const uint32_t k = d.tb;
+    uint32_t pos = 0;
+    for (int b = 0; b < nb; ++b) {
+        const uint32_t n = s_n[b];
+        pos += (n < k ? n : k) + ((uint32_t)b < d.bucket && n > k ? 1u : 0u);
+    }
+    tiles[pos].order = (uint32_t)t;
 }
 
 __global__ __launch_bounds__(kBlock) void seg_upsweep(const uint64_t* __restrict__ rec, const SegTile* __restrict__ tiles,
@@ -265,12 +296,25 @@ __global__ __launch_bounds__(kBlock) void seg_dbase_kernel(const uint32_t* __res
 }
 
 template <int kIPT>
+__device__ __forceinline__ void onesweep_load(const uint64_t* __restrict__ rin, const SegTile& d, uint32_t q0, int lane,
+                                              uint64_t (&key)[kIPT]) {
+    #pragma unroll
+    for (int r = 0; r < kIPT; ++r) {
+        const uint32_t q = q0 + r * 64 + lane;
+        key[r] = q < d.count ? rin[d.start + q] : 0ull;
+    }
+}
+
+// One onesweep pass; each block claims one tile from an atomic counter (claim
+// order = tiles[c].order, see claim_order_kernel), so every tile it waits on was
+// claimed earlier by a resident block.
+template <int kIPT>
 __global__ __launch_bounds__(kBlock) void seg_onesweep_kernel(const uint64_t* __restrict__ rin,
                                                               uint64_t* __restrict__ rout,
-                                                              const SegTile* __restrict__ tiles, int shift, int pass,
-                                                              int npass, const uint32_t* __restrict__ dbase,
-                                                              uint32_t* status, uint32_t* tile_counter,
-                                                              uint32_t* err) {
+                                                              const SegTile* __restrict__ tiles, uint32_t nclaims,
+                                                              int shift, int pass, int npass,
+                                                              const uint32_t* __restrict__ dbase, uint32_t* status,
+                                                              uint32_t* tile_counter, uint32_t* err) {
     constexpr int kT = kIPT * kBlock;
     __shared__ uint64_t srec[kT];
     __shared__ uint32_t wcnt[kWaves][kDigits];
@@ -278,11 +322,15 @@ __global__ __launch_bounds__(kBlock) void seg_onesweep_kernel(const uint64_t* __
     __shared__ uint32_t gofs[kDigits];
     __shared__ uint32_t s_w[kWaves];
     __shared__ uint32_t s_tile;
+    __shared__ uint32_t hcnt[kDigits];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     if (tid == 0) s_tile = atomicAdd(tile_counter, 1u);
     for (int i = tid; i < kWaves * kDigits; i += kBlock) (&wcnt[0][0])[i] = 0;
+    hcnt[tid] = 0;
     __syncthreads();
-    const uint32_t t = s_tile;
+    const uint32_t c = __builtin_amdgcn_readfirstlane(s_tile);   // uniform: scalar descriptor loads
+    if (c >= nclaims) return;
+    const uint32_t t = __builtin_amdgcn_readfirstlane(tiles[c].order);
     const SegTile d = tiles[t];
     if (d.count == 0) return;
     const uint32_t q0 = wv * (kT / kWaves);
@@ -294,6 +342,17 @@ __global__ __launch_bounds__(kBlock) void seg_onesweep_kernel(const uint64_t* __
         const uint32_t q = q0 + r * 64 + lane;
         key[r] = q < d.count ? rin[d.start + q] : 0ull;
     }
+    // publish this tile's per-digit counts as soon as the keys are in: successors'
+    // look-backs then rarely find an unpublished predecessor.
+    #pragma unroll
+    for (int r = 0; r < kIPT; ++r) {
+        const uint32_t q = q0 + r * 64 + lane;
+        if (q < d.count) atomicAdd(&hcnt[(uint32_t)(key[r] >> shift) & 0xFFu], 1u);
+    }
+    __syncthreads();
+    if (d.tb != 0)
+        __hip_atomic_store(status + (uint64_t)t * kDigits + tid, kFlagAgg | hcnt[tid], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     #pragma unroll
     for (int r = 0; r < kIPT; ++r) {
         const uint32_t q = q0 + r * 64 + lane;
@@ -317,29 +376,47 @@ __global__ __launch_bounds__(kBlock) void seg_onesweep_kernel(const uint64_t* __
         const int dg = tid;  // digit
         uint32_t acc = 0;
         #pragma unroll
-        for (int w = 0; w < kWaves; ++w) { const uint32_t c = wcnt[w][dg]; wcnt[w][dg] = acc; acc += c; }
-        // publish, then look back over the bucket's preceding tiles
+        for (int w = 0; w < kWaves; ++w) { const uint32_t x = wcnt[w][dg]; wcnt[w][dg] = acc; acc += x; }
+        // look back over the bucket's preceding tiles, then publish the inclusive prefix
         uint32_t* st = status + (uint64_t)t * kDigits + dg;
         uint32_t prefix = 0;
         if (d.tb == 0) {
             __hip_atomic_store(st, kFlagInc | acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
-            __hip_atomic_store(st, kFlagAgg | acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            uint64_t j = (uint64_t)t - 1;
+            // windowed look-back: kLookback predecessor statuses per step as one batch of
+            // independent loads; tiles before the bucket's first tile are never read
+            // (the first tile always publishes an inclusive prefix).
+            const int64_t tfirst = (int64_t)t - (int64_t)d.tb;
+            int64_t j = (int64_t)t - 1;
             uint32_t spins = 0;
-            for (;;) {
-                const uint32_t s = __hip_atomic_load(status + j * kDigits + dg, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-                if ((s >> 30) == 0u) {
-                    if (++spins > (1u << 26)) { atomicOr(err, 2u); break; }
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
+            bool done = false;
+            while (!done) {
+                uint32_t sv[kLookback];
+                #pragma unroll
+                for (int k = 0; k < kLookback; ++k)
+                    sv[k] = (j - k >= tfirst) ? __hip_atomic_load(status + (uint64_t)(j - k) * kDigits + dg,
+                                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                              : kFlagInc;
+                int used = 0;
+                bool stall = false;
+                #pragma unroll
+                for (int k = 0; k < kLookback; ++k) {
+                    if (done || stall) continue;
+                    const uint32_t sx = sv[k];
+                    if ((sx >> 30) == 0u) { stall = true; continue; }
+                    prefix += sx & kValMask;
+                    ++used;
+                    if ((sx & kFlagInc) != 0u) done = true;
                 }
-                prefix += s & kValMask;
-                if ((s & kFlagInc) != 0u) break;
-                --j;
+                j -= used;
+                if (stall && !done) {
+                    if (++spins > (1u << 24)) { atomicOr(err, 2u); break; }
+                    if (spins < 8) __builtin_amdgcn_s_sleep(1);
+                    else __builtin_amdgcn_s_sleep(8);
+                }
             }
-            __hip_atomic_store(st, kFlagInc | ((prefix + acc) & kValMask), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(st, kFlagInc | ((prefix + acc) & kValMask), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         }
         gofs[dg] = dbase[((uint64_t)d.bucket * npass + pass) * kDigits + dg] + prefix;
         // block-local digit starts
@@ -368,11 +445,11 @@ __global__ __launch_bounds__(kBlock) void seg_onesweep_kernel(const uint64_t* __
     __syncthreads();
     #pragma unroll
     for (int r = 0; r < kIPT; ++r) {
-        const uint32_t s = tid + r * kBlock;
-        if (s < d.count) {
-            const uint64_t k = srec[s];
+        const uint32_t sidx = tid + r * kBlock;
+        if (sidx < d.count) {
+            const uint64_t k = srec[sidx];
             const uint32_t dg = (uint32_t)(k >> shift) & 0xFFu;
-            rout[(uint64_t)gofs[dg] + (s - lstart[dg])] = k;
+            rout[(uint64_t)gofs[dg] + (sidx - lstart[dg])] = k;
         }
     }
 }
@@ -406,6 +483,8 @@ hipError_t build_seg_tiles(const uint32_t* d_hist_scanned, uint32_t T, int msd_b
     }
     hipLaunchKernelGGL(tiles_kernel, dim3((unsigned)((ub + 255) / 256)), dim3(256), 0, st, bstart, tfirst, nb, ub,
                        d_tiles, d_ntiles);
+    hipLaunchKernelGGL(claim_order_kernel, dim3((unsigned)((ub + 255) / 256)), dim3(256), 0, st, tfirst, nb, ub,
+                       d_tiles);
     return hipGetLastError();
 }
 
@@ -439,8 +518,8 @@ hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key
     uint64_t* dst = recB;
     for (int p = 0; p < npass; ++p) {
         if (ev_ds) (void)hipEventRecord(ev_ds[2 * p], st);
-        hipLaunchKernelGGL(seg_onesweep_kernel<kOnesweepIPT>, dim3((unsigned)ntiles_ub), dim3(kBlock), 0, st, src,
-                           dst, d_tiles, 32 + 8 * p, p, npass, dbase,
+        hipLaunchKernelGGL(seg_onesweep_kernel<kOnesweepIPT>, dim3((unsigned)ntiles_ub), dim3(kBlock), 0, st, src, dst, d_tiles,
+                           (uint32_t)ntiles_ub, 32 + 8 * p, p, npass, dbase,
                            status + (uint64_t)p * ntiles_ub * kDigits, counters + p, d_err);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
