@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -223,6 +224,8 @@ int run_pipeline(mums_ctx* ctx, int stage) {
     const int kbits = 2 * ctx->w + 1;
     ctx->packed_path = kbits <= 32 + kMaxMsdBits;
     ctx->msd_bits = ctx->packed_path ? std::max(0, kbits - 32) : 0;
+    if (const char* e = getenv("MUMS_DEV_MSD_BITS"))   // development knob (sort layout experiments)
+        if (ctx->packed_path) ctx->msd_bits = std::min(kMaxMsdBits, std::max(ctx->msd_bits, atoi(e)));
     const int B = ctx->msd_bits;
     const int passes = ctx->packed_path ? (kbits - B + 7) / 8 : (kbits + 7) / 8;
     const size_t kb = ctx->key64 ? 8 : 4;

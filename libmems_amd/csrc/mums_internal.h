@@ -30,6 +30,7 @@ constexpr int kSeedTile = 4096;      // positions per key-kernel workgroup
 #define MUMS_SEG_TILE 4096
 #endif
 constexpr int kSegTile = MUMS_SEG_TILE; // records per sort / group tile
+constexpr int kLocalIPT = 16;        // records per lane of the LDS-resident local sort (local_sort.hip)
 constexpr int kMaxMsdBits = 11;      // packed path: 2w+1 <= 32 + 11
 
 // Per-run constants shared by the kernels (passed by value).
@@ -87,6 +88,26 @@ struct SegTile {
     uint32_t bucket;    // MSD bucket id
     uint32_t order;     // onesweep claim order: the c-th claimed block sorts tile tiles[c].order
 };
+
+// Stable wave64 "match any" on a kBits-bit digit: *peers_out = popcount of the lanes
+// (valid ones) holding the same digit, returned value = how many of them sit in lower
+// lanes.  Per digit bit: a 1-bit signed extract (0 / all ones), one ballot, and
+// peers &= ~(X ^ ext) on each 32-bit half (one v_bitop3 each); the rank is two mbcnt ops.
+template <int kBits>
+__device__ __forceinline__ uint32_t wave_match_rank(uint32_t dg, bool valid, uint32_t* peers_out) {
+    const uint64_t v = __ballot(valid);
+    uint32_t pl = (uint32_t)v, ph = (uint32_t)(v >> 32);
+    #pragma unroll
+    for (int b = 0; b < kBits; ++b) {
+        const uint32_t ms = (uint32_t)__builtin_amdgcn_sbfe((int32_t)dg, b, 1);   // all ones when set
+        const uint64_t x = __ballot(ms != 0u);
+        // p & ~(x ^ m): LUT index (p << 2 | x << 1 | m) -> bits 4 and 7
+        pl = __builtin_amdgcn_bitop3_b32(pl, (uint32_t)x, ms, 0x90);
+        ph = __builtin_amdgcn_bitop3_b32(ph, (uint32_t)(x >> 32), ms, 0x90);
+    }
+    *peers_out = (uint32_t)__builtin_popcount(pl) + (uint32_t)__builtin_popcount(ph);
+    return __builtin_amdgcn_mbcnt_hi(ph, __builtin_amdgcn_mbcnt_lo(pl, 0u));
+}
 
 // genome of a global seed-mer index (G <= 32: linear scan is cheapest)
 __device__ __forceinline__ int genome_of(const GenomeTable& gt, uint64_t i) {

@@ -149,7 +149,6 @@ __global__ __launch_bounds__(kBlock) void seg_downsweep(const uint64_t* __restri
     for (int i = threadIdx.x; i < kWaves * kDigits; i += kBlock) (&wcnt[0][0])[i] = 0;
     __syncthreads();
     const uint32_t q0 = wv * (kTile / kWaves);
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint64_t key[kRounds];
     uint32_t rank[kRounds];
     #pragma unroll
@@ -162,17 +161,11 @@ __global__ __launch_bounds__(kBlock) void seg_downsweep(const uint64_t* __restri
         const uint32_t q = q0 + r * 64 + lane;
         const bool valid = q < d.count;
         const uint32_t dg = (uint32_t)(key[r] >> shift) & 0xFFu;
-        uint64_t peers = __ballot(valid);
-        #pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            const bool bit = (dg >> b) & 1u;
-            const uint64_t bb = __ballot(bit);
-            peers &= bit ? bb : ~bb;
-        }
-        const uint32_t rk = (uint32_t)__popcll(peers & lt);
+        uint32_t tot;
+        const uint32_t rk = wave_match_rank<8>(dg, valid, &tot);
         uint32_t old = 0;
         if (valid) old = wcnt[wv][dg];
-        if (valid && rk == 0) wcnt[wv][dg] = old + (uint32_t)__popcll(peers);
+        if (valid && rk == 0) wcnt[wv][dg] = old + tot;
         rank[r] = old + rk;
     }
     __syncthreads();
@@ -334,7 +327,6 @@ __global__ __launch_bounds__(kBlock) void seg_onesweep_kernel(const uint64_t* __
     const SegTile d = tiles[t];
     if (d.count == 0) return;
     const uint32_t q0 = wv * (kT / kWaves);
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint64_t key[kIPT];
     uint32_t rank[kIPT];
     #pragma unroll
@@ -358,17 +350,11 @@ __global__ __launch_bounds__(kBlock) void seg_onesweep_kernel(const uint64_t* __
         const uint32_t q = q0 + r * 64 + lane;
         const bool valid = q < d.count;
         const uint32_t dg = (uint32_t)(key[r] >> shift) & 0xFFu;
-        uint64_t peers = __ballot(valid);
-        #pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            const bool bit = (dg >> b) & 1u;
-            const uint64_t bb = __ballot(bit);
-            peers &= bit ? bb : ~bb;
-        }
-        const uint32_t rk = (uint32_t)__popcll(peers & lt);
+        uint32_t tot;
+        const uint32_t rk = wave_match_rank<8>(dg, valid, &tot);
         uint32_t old = 0;
         if (valid) old = wcnt[wv][dg];
-        if (valid && rk == 0) wcnt[wv][dg] = old + (uint32_t)__popcll(peers);
+        if (valid && rk == 0) wcnt[wv][dg] = old + tot;
         rank[r] = old + rk;
     }
     __syncthreads();

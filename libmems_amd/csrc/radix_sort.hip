@@ -65,7 +65,6 @@ __global__ __launch_bounds__(kBlock) void rs_downsweep(const K* __restrict__ kin
 
     const uint64_t tile0 = (uint64_t)blockIdx.x * kRTile;
     const uint64_t b0 = tile0 + (uint64_t)wv * (kRTile / kWaves);
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     K key[kRounds];
     uint32_t val[kRounds];
     uint32_t rank[kRounds];
@@ -76,17 +75,11 @@ __global__ __launch_bounds__(kBlock) void rs_downsweep(const K* __restrict__ kin
         key[r] = valid ? kin[i] : (K)0;
         val[r] = kImplicitVals ? (uint32_t)i : (valid ? vin[i] : 0u);
         const uint32_t d = (uint32_t)(key[r] >> shift) & 0xFFu;
-        uint64_t peers = __ballot(valid);
-        #pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            const bool bit = (d >> b) & 1u;
-            const uint64_t bb = __ballot(bit);
-            peers &= bit ? bb : ~bb;
-        }
-        const uint32_t rk = (uint32_t)__popcll(peers & lt);
+        uint32_t tot;
+        const uint32_t rk = wave_match_rank<8>(d, valid, &tot);
         uint32_t old = 0;
         if (valid) old = wcnt[wv][d];
-        if (valid && rk == 0) wcnt[wv][d] = old + (uint32_t)__popcll(peers);
+        if (valid && rk == 0) wcnt[wv][d] = old + tot;
         rank[r] = old + rk;
     }
     __syncthreads();

@@ -167,7 +167,6 @@ __global__ __launch_bounds__(kBlock) void seed_scatter_kernel(SeedSpec ss, Genom
     __syncthreads();
 
     const uint64_t base = gt.base[g];
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const int q0 = wv * (kTile / kWaves);
     uint64_t r_rec[kPerThread];
     uint32_t r_dig[kPerThread], r_rank[kPerThread];
@@ -183,16 +182,12 @@ __global__ __launch_bounds__(kBlock) void seed_scatter_kernel(SeedSpec ss, Genom
         const uint32_t d = valid ? (uint32_t)(kv >> klow) : 0u;
         r_rec[r] = ((kv & lmask) << 32) | (base + p);
         r_dig[r] = d;
-        uint64_t peers = __ballot(valid);
-        for (int b = 0; b < msd_bits; ++b) {
-            const bool bit = (d >> b) & 1u;
-            const uint64_t bb = __ballot(bit);
-            peers &= bit ? bb : ~bb;
-        }
-        const uint32_t rk = (uint32_t)__popcll(peers & lt);
+        uint32_t tot;
+        // digits are < 2^msd_bits <= kMaxDig: the unused high bits rank as equal
+        const uint32_t rk = wave_match_rank<(kMaxDig > 256 ? kMaxMsdBits : 8)>(d, valid, &tot);
         uint32_t old = 0;
         if (valid) old = wcnt[wv][d];
-        if (valid && rk == 0) wcnt[wv][d] = old + (uint32_t)__popcll(peers);
+        if (valid && rk == 0) wcnt[wv][d] = old + tot;
         r_rank[r] = old + rk;
     }
     __syncthreads();
