@@ -11,7 +11,10 @@ FindMatches incl. extension, bucket replay and MatchList output) is reported
 beside it on BASELINE config 2 (4 x 10 Mbp, w15).
 
     python bench.py [--gpus N --steps K --warmup W]
-For N > 1 launch with torch.distributed.run (one rank per GPU).
+For N > 1 launch with torch.distributed.run (one rank per GPU): the same C3 input is
+split genome-block-per-rank and the seed stage runs sharded (libmems_amd/shard.py:
+keys per rank, RCCL all-to-all of key ranges, merge per key range), so the total
+work is fixed ("strong" scaling) and value = all seed-mers / max-over-ranks time.
 """
 from __future__ import annotations
 
@@ -28,6 +31,7 @@ import torch  # noqa: E402  (loaded before libmums_hip.so: one HIP runtime per p
 import torch.distributed as dist  # noqa: E402
 
 import libmems_amd as lm  # noqa: E402
+from libmems_amd.shard import HipShardEngine, ShardedSeedStage, genome_blocks  # noqa: E402
 
 METRIC = "seed-mers/sec sorted+matched (+ MUMs/sec) at 1/2/4/8 MI355X; HBM GB/s vs roofline"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
@@ -105,59 +109,88 @@ def main():
     ap.add_argument("--length", type=int, default=100_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-mums", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, default) or gloo (rehearsal)")
+    ap.add_argument("--device", type=int, default=None, help="force one HIP device for every rank (rehearsal)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("gloo")   # CPU barrier + max over ranks; the data path has no collective
+    local = int(os.environ.get("LOCAL_RANK", "0")) if args.device is None else args.device
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if world > 1:
+        # RCCL ("nccl" on ROCm) over xGMI: the key-range all-to-all of the sharded seed stage
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     G, n = args.genomes, args.length
-    genomes = synth_genomes(G, n, 0.01, 12345 + rank, dev)
-    mh = lm.MemHash(local)
     seed = lm.getSeed(19)
-    mh.SetSeed(seed)
-    for s in genomes:
-        mh.AddSequence(s)
-    for _ in range(args.warmup):
-        mh.FindStage(lm.STAGE_SEEDS)
-    mh.SetProfiling(True)
-
+    genomes = synth_genomes(G, n, 0.01, 12345, dev)
+    phase = {"ms_keys": 0.0, "ms_sort": 0.0, "ms_groups": 0.0, "ms_buckets": 0.0}
     ms_dom = 0.0
     bytes_dom = 0
     launches = 0
-    phase = {"ms_keys": 0.0, "ms_sort": 0.0, "ms_groups": 0.0, "ms_buckets": 0.0}
-    if world > 1:
-        dist.barrier()
+    exch_bytes = 0
+    if world == 1:
+        mh = lm.MemHash(local)
+        mh.SetSeed(seed)
+        for s in genomes:
+            mh.AddSequence(s)
+        run = lambda: mh.FindStage(lm.STAGE_SEEDS)  # noqa: E731
+        stats = mh.stats
+    else:
+        # genome block per rank; the whole C3 input is split, not replicated
+        first, count = genome_blocks(G, world)[rank]
+        mine = genomes[first:first + count]
+        del genomes
+        genomes = mine
+        eng = HipShardEngine(local, seed, [n] * G, first, genomes)
+        stage = ShardedSeedStage(eng)
+        mh = eng.mh
+        run = stage.run
+        stats = eng.stats
+    for _ in range(args.warmup):
+        run()
+    mh.SetProfiling(True)
+
+    def barrier():
+        if world > 1:
+            if args.dist_backend == "nccl":
+                dist.barrier(device_ids=[local])
+            else:
+                dist.barrier()
+
+    barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        mh.FindStage(lm.STAGE_SEEDS)
-        st = mh.stats()
+        run()
+        st = stats()
         ms_dom += st["ms_dominant"]
         bytes_dom += st["dominant_bytes"]
         launches += st["dominant_launches"]
         for k in phase:
             phase[k] += st[k]
+        if world > 1:
+            exch_bytes += stage.last_exchange_bytes
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    barrier()
     dt = time.perf_counter() - t0
-    tmax = torch.tensor([dt], dtype=torch.float64)
+    tmax = torch.tensor([dt], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     dt = float(tmax.item())
-    seedmers = st["seedmers"]
+    seedmers_total = sum(max(n - lm.getSeedLength(seed) + 1, 0) for _ in range(G))
+    seedmers_rank = st["seedmers"]
     key_bytes = st["key_bytes"]
     probes = st["probes"]
     mh.close()
     del genomes
 
     if rank == 0:
-        value = world * seedmers * args.steps / dt
+        value = seedmers_total * args.steps / dt
         achieved = bytes_dom / (ms_dom * 1e-3) / 1e9 if ms_dom > 0 else None
         traffic = None
         if os.path.exists(PROFILE_SUMMARY):
@@ -174,19 +207,22 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if world > 1 else "weak",
             "vs_baseline": None,
             "dtype": "u64" if key_bytes == 8 else "u32",
             "data": "synthetic: 8 related genomes generated on the GPU (iid ACGT base, 1% substitutions, genome 2 "
                     "reverse-complemented)",
             "config": {"workload": f"BASELINE config 3: {G} x {n // 10**6} Mbp, seed weight 19 (0x7b974ef), "
                                    f"MemHash seed stage (sorted+matched)",
-                       "genomes": G, "genome_length": n, "seedmers_per_gpu": seedmers, "probes_per_gpu": probes,
-                       "parallelism": f"replicas x{world}" if world > 1 else "1 GPU"},
+                       "genomes": G, "genome_length": n, "seedmers_total": seedmers_total,
+                       "seedmers_rank0": seedmers_rank, "probes_rank0": probes,
+                       "parallelism": (f"genome-sharded x{world}: genome block per rank, RCCL all-to-all of key "
+                                       f"ranges ({exch_bytes / max(args.steps, 1) / 1e9:.2f} GB/step sent by rank 0), "
+                                       f"merge per key range") if world > 1 else "1 GPU"},
             "roofline": {
                 "bound": "hbm",
-                "kernel": f"seg_downsweep (packed-record seed-key radix sort, {launches // max(args.steps, 1)} "
-                          f"passes/step)",
+                "kernel": f"seg_onesweep_kernel (segmented onesweep LSD pass over packed 8-B seed records, "
+                          f"{launches // max(args.steps, 1)} passes/step)",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -206,7 +242,7 @@ def main():
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out), flush=True)
     if world > 1:
-        dist.barrier()
+        barrier()
         dist.destroy_process_group()
 
 

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MUMS_ABI_VERSION 1
+#define MUMS_ABI_VERSION 2
 
 enum mums_status {
     MUMS_OK = 0,
@@ -125,6 +125,36 @@ int  mums_copy_seed_keys(mums_ctx* ctx, uint32_t genome, uint64_t* out, uint64_t
 /* MemorySML::Create (MemorySML.cpp:45-60): SML positions of genome g sorted by
  * full key, ties by ascending position. */
 int  mums_build_sml(mums_ctx* ctx, uint32_t genome, uint32_t* positions, uint64_t cap);
+
+/* ---- sharded seed stage across GPUs -----------------------
+ * Replaces the single-process G-way merge of MatchFinder::SearchRange
+ * (MatchFinder.cpp:172-340) over the G SortedMerLists (MemorySML::Create,
+ * MemorySML.cpp:45-60) when the genomes live on different GPUs; the result is
+ * the same key-ordered stream of accepted probes as mums_find_stage(SEEDS).
+ * One context per rank; the caller moves the records between ranks (RCCL
+ * all-to-all over xGMI, libmems_amd/shard.py).
+ *   1. mums_shard_layout: all G genome lengths; this context owns genomes
+ *      [first_genome, first_genome + #mums_add_genome calls).
+ *   2. mums_shard_keys: keys of the owned genomes as 8-B records
+ *      (ckey_low << 32 | global seed-mer index), stably bucketed by the top
+ *      msd_bits key bits into d_records; bucket_counts[2^msd_bits].
+ *   3. exchange: bucket range [first_bucket, first_bucket + nbuckets) of every
+ *      source rank goes to its owner rank, sources in rank order.
+ *   4. mums_shard_merge: the received records (source-major: each source's
+ *      buckets in order; counts[nsources][nbuckets]) -> sort -> groups ->
+ *      probes of this key range; stats via mums_get_stats. */
+int  mums_shard_layout(mums_ctx* ctx, uint32_t genomes_total, uint32_t first_genome, const uint64_t* lengths);
+/* msd_bits of the exchange and the number of records mums_shard_keys will write. */
+int  mums_shard_msd_bits(mums_ctx* ctx, uint32_t* msd_bits, uint64_t* local_records);
+int  mums_shard_keys(mums_ctx* ctx, uint64_t* d_records, uint64_t capacity, uint64_t* bucket_counts);
+int  mums_shard_merge(mums_ctx* ctx, const uint64_t* d_records, uint32_t nsources, uint32_t first_bucket,
+                      uint32_t nbuckets, const uint64_t* counts);
+/* Accepted probes of the last seed stage, in AddHashEntry call order
+ * (MemHash::EnumerateMatches -> AddHashEntry, MemHash.cpp:139-162, 209-251):
+ * hash bucket ((offset % T) + T) % T and the smallest global seed-mer index of
+ * the probe's key group (its identity; checking aid, host-side gather). */
+int  mums_probe_count(mums_ctx* ctx, uint64_t* count);
+int  mums_probe_copy(mums_ctx* ctx, uint32_t* buckets, uint64_t* ref_index, uint64_t capacity);
 
 int  mums_abi_version(void);
 

@@ -82,7 +82,8 @@ EXPORTED_SYMBOLS = [
     "mums_set_params", "mums_set_mask", "mums_add_genome", "mums_add_genome_device", "mums_clear",
     "mums_find", "mums_find_stage", "mums_result_count", "mums_result_copy", "mums_get_stats",
     "mums_last_error", "mums_get_seed", "mums_default_seed_weight", "mums_copy_seed_keys",
-    "mums_build_sml", "mums_set_profiling",
+    "mums_build_sml", "mums_set_profiling", "mums_shard_layout", "mums_shard_msd_bits", "mums_shard_keys",
+    "mums_shard_merge", "mums_probe_count", "mums_probe_copy",
 ]
 
 _lib: Optional[ctypes.CDLL] = None
@@ -128,6 +129,12 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mums_copy_seed_keys.argtypes = [vp, u32, vp, u64]
     lib.mums_build_sml.argtypes = [vp, u32, vp, u64]
     lib.mums_set_profiling.argtypes = [vp, i32]
+    lib.mums_shard_layout.argtypes = [vp, u32, u32, vp]
+    lib.mums_shard_msd_bits.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(u64)]
+    lib.mums_shard_keys.argtypes = [vp, vp, u64, vp]
+    lib.mums_shard_merge.argtypes = [vp, vp, u32, u32, u32, vp]
+    lib.mums_probe_count.argtypes = [vp, ctypes.POINTER(u64)]
+    lib.mums_probe_copy.argtypes = [vp, vp, vp, u64]
     _lib = lib
     return lib
 
@@ -297,6 +304,16 @@ class MemHash:
 
     def MemCollisionCount(self) -> int:
         return int(self.stats()["collision_count"])
+
+    def Probes(self):
+        """Accepted probes of the last seed stage in AddHashEntry order: (buckets u32[P],
+        ref_index u64[P]) -- hash bucket and smallest global seed-mer index of the group."""
+        cnt = ctypes.c_uint64()
+        self._check(self._lib.mums_probe_count(self._ctx, ctypes.byref(cnt)))
+        b = np.zeros(max(cnt.value, 1), dtype=np.uint32)
+        r = np.zeros(max(cnt.value, 1), dtype=np.uint64)
+        self._check(self._lib.mums_probe_copy(self._ctx, b.ctypes.data, r.ctypes.data, cnt.value))
+        return b[:cnt.value], r[:cnt.value]
 
     # ---- SortedMerList helpers (rows A3-A5) ------------------------------------------
     def SeedKeys(self, genome: int, m: int) -> np.ndarray:

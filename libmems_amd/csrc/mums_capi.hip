@@ -75,6 +75,14 @@ struct mums_ctx {
     bool profiling = false;
     hipEvent_t ev_ds[16] = {};   // 2 per radix pass (<= 8 passes)
 
+    // sharded seed stage: this context owns genomes [shard_first,
+    // shard_first + genomes.size()) of a problem whose genome lengths are shard_len
+    bool shard = false;
+    uint32_t shard_first = 0;
+    std::vector<uint64_t> shard_len;
+    GenomeTable lgt{};        // the owned genomes, global seed-mer bases
+    double shard_keys_ms = 0;
+
     // state of the last run
     int stage_done = 0;
     bool key64 = false;
@@ -83,6 +91,7 @@ struct mums_ctx {
     int L = 0, w = 0;
     uint64_t pattern = 0, N = 0, P = 0, M = 0;
     int sorted_buf = 0;
+    int sort_passes = 0;
     const uint64_t* sorted_rec = nullptr;   // packed path
     const void* sorted_key = nullptr;       // pair path
     const uint32_t* sorted_idx = nullptr;
@@ -172,7 +181,7 @@ int run_groups(mums_ctx* ctx, View v, const SegTile* tiles, uint64_t ntiles, con
 template <typename View>
 int groups_dispatch(mums_ctx* ctx, View v, const SegTile* tiles, uint64_t ntiles, const MatchParams& mp,
                     uint64_t* pi, uint32_t* pb, uint64_t* si, uint32_t* sb, hipStream_t st) {
-    const int G = (int)ctx->genomes.size();
+    const int G = ctx->gt.G;   // genomes of the whole problem (sharded contexts own a subset)
     if (G <= 4) return run_groups<4, View>(ctx, v, tiles, ntiles, mp, pi, pb, si, sb, st);
     if (G <= 8) return run_groups<8, View>(ctx, v, tiles, ntiles, mp, pi, pb, si, sb, st);
     if (G <= 16) return run_groups<16, View>(ctx, v, tiles, ntiles, mp, pi, pb, si, sb, st);
@@ -181,7 +190,7 @@ int groups_dispatch(mums_ctx* ctx, View v, const SegTile* tiles, uint64_t ntiles
 
 template <typename View>
 int replay_dispatch(mums_ctx* ctx, View v, const MatchParams& mp, hipStream_t st) {
-    const int G = (int)ctx->genomes.size();
+    const int G = ctx->gt.G;
 #define MUMS_REPLAY_CALL(MG)                                                                                        \
     HIPCHK((launch_replay<MG, View>(v, ctx->N, ctx->gt, mp, ctx->ss, ctx->probe_info, ctx->sorted_ids,              \
                                     ctx->bstart.as<uint32_t>(), ctx->bend.as<uint32_t>(), ctx->tbl.as<uint32_t>(),  \
@@ -195,6 +204,173 @@ int replay_dispatch(mums_ctx* ctx, View v, const MatchParams& mp, hipStream_t st
     return MUMS_OK;
 }
 
+// probe / slot arrays of the groups stage (one grow-only device buffer)
+struct ProbeSpace {
+    uint64_t* probe_info;
+    uint64_t* slot_info;
+    uint32_t* probe_bucket;
+    uint32_t* bucketB;
+    uint32_t* idsA;
+    uint32_t* idsB;
+    uint32_t* slot_bucket;
+};
+
+int ensure_probe_space(mums_ctx* ctx, uint64_t N, uint64_t ntiles_groups, ProbeSpace* ps) {
+    const uint64_t pcap = N / 2 + 1;
+    const uint64_t nslots = group_slot_count(ntiles_groups);
+    HIPCHK(ctx->partials.ensure((3 * ntiles_groups + 128) * 4));
+    HIPCHK(ctx->pbuf.ensure(pcap * (8 + 4 * 4) + nslots * 12 + 256));
+    char* pb = (char*)ctx->pbuf.p;
+    ps->probe_info = (uint64_t*)pb;
+    ps->slot_info = ps->probe_info + pcap;
+    ps->probe_bucket = (uint32_t*)(ps->slot_info + nslots);
+    ps->bucketB = ps->probe_bucket + pcap;
+    ps->idsA = ps->bucketB + pcap;
+    ps->idsB = ps->idsA + pcap;
+    ps->slot_bucket = ps->idsB + pcap;
+    return MUMS_OK;
+}
+
+// word offsets of the packed genomes and key-kernel tiles for the genomes of table t
+// (sets t.woff / t.tfirst); returns the tile count, *words = packed words
+uint32_t layout_packed(GenomeTable& t, uint64_t* words) {
+    uint64_t wsum = 0;
+    uint32_t T = 0;
+    for (int g = 0; g < t.G; ++g) {
+        t.woff[g] = wsum;
+        wsum += (packed_words(t.n[g]) + 3) & ~3ull;
+        t.tfirst[g] = T;
+        T += (uint32_t)((t.n[g] + kSeedTile - 1) / kSeedTile);
+    }
+    t.woff[t.G] = wsum;
+    for (int g = t.G; g <= kMaxG; ++g) t.tfirst[g] = T;
+    *words = wsum;
+    return T;
+}
+
+// Keys stage, packed path (rows A2-A4): pack the context's own genomes (table lgt, whose
+// bases are GLOBAL seed-mer indices), histogram the top B key bits per tile, then scatter
+// the (ckey_low << 32 | global index) records stably into their MSD buckets in out.
+// Bucket starts -> bstart[0 .. 2^B] (device).
+int keys_stage(mums_ctx* ctx, const GenomeTable& lgt, uint32_t T, int B, uint64_t n, uint64_t* out, uint32_t* bstart,
+               hipStream_t st) {
+    DevCounters* dc = ctx->counters.as<DevCounters>();
+    std::vector<const char*> ptrs(lgt.G);
+    for (int g = 0; g < lgt.G; ++g) ptrs[g] = ctx->genomes[g].d_ptr;
+    uint32_t* hist = ctx->hist.as<uint32_t>();
+    HIPCHK(launch_seed_pack(ctx->ss, lgt, ptrs.data(), ctx->packed.as<uint32_t>(), 1, true, nullptr, B, hist, T,
+                            &dc->err, st));
+    if (B > 0) HIPCHK(exclusive_scan_u32(hist, (uint64_t)T << B, ctx->tmp.p, nullptr, st));
+    HIPCHK(launch_seed_scatter(ctx->ss, lgt, ctx->packed.as<uint32_t>(), B, hist, T, out, st));
+    HIPCHK(seg_bucket_starts(B > 0 ? hist : nullptr, T, B, n, bstart, st));
+    return MUMS_OK;
+}
+
+// Workspace of the merge stage for n records in 2^mb buckets of key_bits key bits.
+int ensure_merge_space(mums_ctx* ctx, uint64_t n, int mb, int key_bits, ProbeSpace* ps) {
+    const uint64_t ub = seg_tiles_upper(n, mb);
+    HIPCHK(ctx->recA.ensure(n * 8 + 64));
+    HIPCHK(ctx->recB.ensure(n * 8 + 64));
+    HIPCHK(ctx->tiles.ensure(ub * sizeof(SegTile) + 64));
+    HIPCHK(ctx->mstart.ensure(((1ull << mb) + 64) * 4));
+    size_t tmpb = std::max(seg_tmp_bytes(n, mb), onesweep_tmp_bytes(n, mb, key_bits));
+    tmpb = std::max(tmpb, std::max(scan_tmp_bytes(n), radix_tmp_bytes(n / 2 + 1)));
+    tmpb = std::max(tmpb, scan_tmp_bytes((uint64_t)ctx->table_size));
+    HIPCHK(ctx->tmp.ensure(tmpb));
+    return ensure_probe_space(ctx, n, ub, ps);
+}
+
+// Merge stage (rows A5-A9): n records in recA, bucket-major over 2^mb buckets whose starts
+// are in ctx->mstart -> stable sort on record key bits [32, 32 + key_bits) inside every
+// bucket (the merged SortedMerList stream) -> equal-key groups -> accepted probes in key order.
+int merge_stage(mums_ctx* ctx, uint64_t n, int mb, int key_bits, const MatchParams& mp, const ProbeSpace& ps,
+                hipStream_t st) {
+    DevCounters* dc = ctx->counters.as<DevCounters>();
+    SegTile* tiles = ctx->tiles.as<SegTile>();
+    const uint32_t* bstart = ctx->mstart.as<uint32_t>();
+    const uint64_t ub = seg_tiles_upper(n, mb);
+    const bool prof = ctx->profiling;
+    HIPCHK(build_seg_tiles_from_starts(bstart, mb, n, tiles, &dc->ntiles, ctx->tmp.p, st));
+    int buf = 0;
+    if (ctx->use_onesweep && n < (1ull << 30) && key_bits <= 32)
+        HIPCHK(seg_onesweep_sort(ctx->recA.as<uint64_t>(), ctx->recB.as<uint64_t>(), n, key_bits, mb, tiles, ub, bstart,
+                                 ctx->tmp.p, &dc->err, &buf, st, prof ? ctx->ev_ds : nullptr));
+    else
+        HIPCHK(seg_radix_sort(ctx->recA.as<uint64_t>(), ctx->recB.as<uint64_t>(), n, key_bits, tiles, ub, ctx->tmp.p,
+                              &buf, st, prof ? ctx->ev_ds : nullptr));
+    ctx->sorted_buf = buf;
+    ctx->sorted_rec = buf ? ctx->recB.as<uint64_t>() : ctx->recA.as<uint64_t>();
+    ctx->sort_passes = (key_bits + 7) / 8;
+    HIPCHK(hipEventRecord(ctx->ev[EV_SORT], st));
+    return groups_dispatch<RecView>(ctx, RecView{ctx->sorted_rec}, tiles, ub, mp, ps.probe_info, ps.probe_bucket,
+                                    ps.slot_info, ps.slot_bucket, st);
+}
+
+// After the groups stage: counters to the host, error flags, then the probes grouped
+// by hash bucket (stable: key order kept inside a bucket; values = probe ids) (A10).
+int finish_seeds(mums_ctx* ctx, const ProbeSpace& ps, hipStream_t st) {
+    DevCounters* dc = ctx->counters.as<DevCounters>();
+    HIPCHK(hipMemcpyAsync(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (ctx->hc.err & 1u) return fail(ctx, MUMS_E_GAP, "Gap in genome sequence ('-' encountered)");
+    if (ctx->hc.err & 2u) return fail(ctx, MUMS_E_HIP, "sort look-back timed out (internal error)");
+    ctx->P = ctx->hc.nprobes;
+    ctx->probe_info = ps.probe_info;
+    HIPCHK(hipEventRecord(ctx->ev[EV_GROUPS], st));
+    int tbits = 1;
+    while (tbits < 32 && ((uint64_t)1 << tbits) < (uint64_t)ctx->table_size) ++tbits;
+    int pout = 0;
+    HIPCHK(radix_sort<uint32_t>(ps.probe_bucket, nullptr, ctx->P, tbits, ps.bucketB, ps.idsA, ps.probe_bucket,
+                                ps.idsB, ctx->tmp.p, &pout, st));
+    ctx->sorted_buckets = pout ? ps.probe_bucket : ps.bucketB;
+    ctx->sorted_ids = pout ? ps.idsB : ps.idsA;
+    HIPCHK(hipEventRecord(ctx->ev[EV_BUCKETS], st));
+    return MUMS_OK;
+}
+
+// per-run statistics (mums_stats) of the last seed stage [+ replay] over n records
+void fill_stats(mums_ctx* ctx, uint64_t n) {
+    mums_stats& s = ctx->st;
+    s = mums_stats{};
+    s.seedmers = n;
+    s.groups = ctx->hc.ngroups;
+    s.probes = ctx->P;
+    s.repeat_limit_groups = ctx->hc.repeat_limit;
+    auto el = [&](int a, int b) {
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, ctx->ev[a], ctx->ev[b]);
+        return (double)ms;
+    };
+    const size_t kb = ctx->key64 ? 8 : 4;
+    const int passes = ctx->sort_passes;
+    s.ms_keys = el(EV_START, EV_KEYS);
+    s.ms_sort = el(EV_KEYS, EV_SORT);
+    s.ms_groups = el(EV_SORT, EV_GROUPS);
+    s.ms_buckets = el(EV_GROUPS, EV_BUCKETS);
+    s.key_bytes = ctx->packed_path ? 8 : kb;
+    s.sort_passes = (uint64_t)passes;
+    if (ctx->profiling && n > 0) {
+        for (int p = 0; p < passes; ++p) {
+            float ms = 0.f;
+            (void)hipEventElapsedTime(&ms, ctx->ev_ds[2 * p], ctx->ev_ds[2 * p + 1]);
+            s.ms_dominant += ms;
+            // algorithmic bytes of one sort-pass launch: packed records read + written
+            // (8 + 8); pairs: read K (+4 after pass 0) and write K + 4
+            s.dominant_bytes += ctx->packed_path ? n * 16 : n * (kb + (p ? 4 : 0) + kb + 4);
+        }
+        s.dominant_launches = (uint64_t)passes;
+    }
+    if (ctx->stage_done >= MUMS_STAGE_ALL) {
+        s.mem_count = ctx->hc.entries;
+        s.collision_count = ctx->hc.collisions;
+        s.ms_replay = el(EV_BUCKETS, EV_REPLAY);
+        s.ms_output = el(EV_REPLAY, EV_OUTPUT);
+        s.ms_total = el(EV_START, EV_OUTPUT);
+    } else {
+        s.ms_total = el(EV_START, EV_BUCKETS);
+    }
+}
+
 // keys -> sorted stream -> probes -> bucket-sorted probes [-> replay -> MatchList]
 int run_pipeline(mums_ctx* ctx, int stage) {
     hipStream_t st = ctx->stream;
@@ -203,22 +379,11 @@ int run_pipeline(mums_ctx* ctx, int stage) {
     MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, ctx->masked, ctx->seq_mask};
     GenomeTable& gt = ctx->gt;
 
-    // packed genomes + key-kernel tiles
     uint64_t words = 0;
-    uint32_t T = 0;
-    for (int g = 0; g < G; ++g) {
-        gt.woff[g] = words;
-        words += (packed_words(gt.n[g]) + 3) & ~3ull;
-        gt.tfirst[g] = T;
-        T += (uint32_t)((gt.n[g] + kSeedTile - 1) / kSeedTile);
-    }
-    gt.woff[G] = words;
-    for (int g = G; g <= kMaxG; ++g) gt.tfirst[g] = T;
+    const uint32_t T = layout_packed(gt, &words);
     HIPCHK(ctx->packed.ensure(words * 4 + 64));
     HIPCHK(ctx->counters.ensure(sizeof(DevCounters)));
     DevCounters* dc = ctx->counters.as<DevCounters>();
-    std::vector<const char*> ptrs(G);
-    for (int g = 0; g < G; ++g) ptrs[g] = ctx->genomes[g].d_ptr;
     const SeedSpec& ss = ctx->ss;
 
     const int kbits = 2 * ctx->w + 1;
@@ -227,44 +392,28 @@ int run_pipeline(mums_ctx* ctx, int stage) {
     if (const char* e = getenv("MUMS_DEV_MSD_BITS"))   // development knob (sort layout experiments)
         if (ctx->packed_path) ctx->msd_bits = std::min(kMaxMsdBits, std::max(ctx->msd_bits, atoi(e)));
     const int B = ctx->msd_bits;
-    const int passes = ctx->packed_path ? (kbits - B + 7) / 8 : (kbits + 7) / 8;
     const size_t kb = ctx->key64 ? 8 : 4;
-    const uint64_t ntiles_groups = ctx->packed_path ? seg_tiles_upper(N, B) : (N + kSegTile - 1) / kSegTile;
-    const uint64_t pcap = N / 2 + 1;
-    const uint64_t nslots = group_slot_count(ntiles_groups);
-
-    // workspace (grow-only; no allocation in steady state)
-    size_t tmpb = std::max(scan_tmp_bytes(N), radix_tmp_bytes(pcap));
-    tmpb = std::max(tmpb, scan_tmp_bytes((uint64_t)ctx->table_size));
+    ProbeSpace ps{};
     if (ctx->packed_path) {
-        HIPCHK(ctx->recA.ensure(N * 8 + 64));
-        HIPCHK(ctx->recB.ensure(N * 8 + 64));
-        HIPCHK(ctx->tiles.ensure(ntiles_groups * sizeof(SegTile) + 64));
-        if (B > 0) HIPCHK(ctx->hist.ensure(((uint64_t)T << B) * 4 + 64));
-        tmpb = std::max(tmpb, seg_tmp_bytes(N, B));
-        tmpb = std::max(tmpb, onesweep_tmp_bytes(N, B, kbits - B));
-        HIPCHK(ctx->mstart.ensure(((1ull << B) + 64) * 4));
-        tmpb = std::max(tmpb, scan_tmp_bytes((uint64_t)T << B));
+        HIPCHK(ctx->hist.ensure(((uint64_t)T << B) * 4 + 64));
+        HIPCHK(ctx->tmp.ensure(scan_tmp_bytes((uint64_t)T << B)));
+        int rc0 = ensure_merge_space(ctx, N, B, kbits - B, &ps);
+        if (rc0) return rc0;
+        HIPCHK(ctx->tmp.ensure(std::max(scan_tmp_bytes((uint64_t)T << B), ctx->tmp.cap)));
     } else {
+        const uint64_t ntiles_groups = (N + kSegTile - 1) / kSegTile;
         HIPCHK(ctx->ckey.ensure(N * kb + 64));
         HIPCHK(ctx->kA.ensure(N * kb + 64));
         HIPCHK(ctx->kB.ensure(N * kb + 64));
         HIPCHK(ctx->vA.ensure(N * 4 + 64));
         HIPCHK(ctx->vB.ensure(N * 4 + 64));
         HIPCHK(ctx->tiles.ensure(ntiles_groups * sizeof(SegTile) + 64));
-        tmpb = std::max(tmpb, radix_tmp_bytes(N));
+        size_t tmpb = std::max(scan_tmp_bytes(N), radix_tmp_bytes(N));
+        tmpb = std::max(tmpb, scan_tmp_bytes((uint64_t)ctx->table_size));
+        HIPCHK(ctx->tmp.ensure(tmpb));
+        int rc0 = ensure_probe_space(ctx, N, ntiles_groups, &ps);
+        if (rc0) return rc0;
     }
-    HIPCHK(ctx->tmp.ensure(tmpb));
-    HIPCHK(ctx->partials.ensure((3 * ntiles_groups + 128) * 4));
-    HIPCHK(ctx->pbuf.ensure(pcap * (8 + 4 * 4) + nslots * 12 + 256));
-    char* pb = (char*)ctx->pbuf.p;
-    uint64_t* probe_info = (uint64_t*)pb;
-    uint64_t* slot_info = probe_info + pcap;
-    uint32_t* probe_bucket = (uint32_t*)(slot_info + nslots);
-    uint32_t* bucketB = probe_bucket + pcap;
-    uint32_t* idsA = bucketB + pcap;
-    uint32_t* idsB = idsA + pcap;
-    uint32_t* slot_bucket = idsB + pcap;
 
     HIPCHK(hipEventRecord(ctx->ev[EV_START], st));
     HIPCHK(hipMemsetAsync(dc, 0, sizeof(DevCounters), st));
@@ -274,34 +423,19 @@ int run_pipeline(mums_ctx* ctx, int stage) {
 
     int rc = MUMS_OK;
     if (ctx->packed_path) {
-        SegTile* tiles = ctx->tiles.as<SegTile>();
-        uint32_t* hist = ctx->hist.as<uint32_t>();
-        HIPCHK(launch_seed_pack(ss, gt, ptrs.data(), ctx->packed.as<uint32_t>(), 1, true, nullptr, B, hist, T,
-                                &dc->err, st));
-        if (B > 0) HIPCHK(exclusive_scan_u32(hist, (uint64_t)T << B, ctx->tmp.p, nullptr, st));
-        HIPCHK(launch_seed_scatter(ss, gt, ctx->packed.as<uint32_t>(), B, hist, T, ctx->recA.as<uint64_t>(), st));
+        rc = keys_stage(ctx, gt, T, B, N, ctx->recA.as<uint64_t>(), ctx->mstart.as<uint32_t>(), st);
+        if (rc) return rc;
         HIPCHK(hipEventRecord(ctx->ev[EV_KEYS], st));
-        HIPCHK(build_seg_tiles(B > 0 ? hist : nullptr, T, B, N, tiles, &dc->ntiles, ctx->mstart.as<uint32_t>(),
-                               ctx->tmp.p, st));
-        int buf = 0;
-        if (ctx->use_onesweep && N < (1ull << 30) && kbits - B <= 32)
-            HIPCHK(seg_onesweep_sort(ctx->recA.as<uint64_t>(), ctx->recB.as<uint64_t>(), N, kbits - B, B, tiles,
-                                     ntiles_groups, ctx->mstart.as<uint32_t>(), ctx->tmp.p, &dc->err, &buf, st,
-                                     prof ? ctx->ev_ds : nullptr));
-        else
-            HIPCHK(seg_radix_sort(ctx->recA.as<uint64_t>(), ctx->recB.as<uint64_t>(), N, kbits - B, tiles,
-                                  ntiles_groups, ctx->tmp.p, &buf, st, prof ? ctx->ev_ds : nullptr));
-        ctx->sorted_buf = buf;
-        ctx->sorted_rec = buf ? ctx->recB.as<uint64_t>() : ctx->recA.as<uint64_t>();
-        HIPCHK(hipEventRecord(ctx->ev[EV_SORT], st));
-        rc = groups_dispatch<RecView>(ctx, RecView{ctx->sorted_rec}, tiles, ntiles_groups, mp, probe_info,
-                                      probe_bucket, slot_info, slot_bucket, st);
+        rc = merge_stage(ctx, N, B, kbits - B, mp, ps, st);
     } else {
+        std::vector<const char*> ptrs(G);
+        for (int g = 0; g < G; ++g) ptrs[g] = ctx->genomes[g].d_ptr;
         HIPCHK(launch_seed_pack(ss, gt, ptrs.data(), ctx->packed.as<uint32_t>(), 0, ctx->key64, ctx->ckey.p, 0,
                                 nullptr, T, &dc->err, st));
         HIPCHK(hipEventRecord(ctx->ev[EV_KEYS], st));
         int buf = 0;
         SegTile* tiles = ctx->tiles.as<SegTile>();
+        const uint64_t ntiles_groups = (N + kSegTile - 1) / kSegTile;
         HIPCHK(launch_flat_tiles(N, tiles, st));
         if (ctx->key64) {
             HIPCHK(radix_sort<uint64_t>(ctx->ckey.as<uint64_t>(), nullptr, N, kbits, ctx->kA.as<uint64_t>(),
@@ -315,36 +449,22 @@ int run_pipeline(mums_ctx* ctx, int stage) {
         ctx->sorted_buf = buf;
         ctx->sorted_key = buf ? ctx->kB.p : ctx->kA.p;
         ctx->sorted_idx = buf ? ctx->vB.as<uint32_t>() : ctx->vA.as<uint32_t>();
+        ctx->sort_passes = (kbits + 7) / 8;
         HIPCHK(hipEventRecord(ctx->ev[EV_SORT], st));
         if (ctx->key64)
             rc = groups_dispatch<PairView<uint64_t>>(ctx, PairView<uint64_t>{(const uint64_t*)ctx->sorted_key,
                                                                              ctx->sorted_idx},
-                                                     tiles, ntiles_groups, mp, probe_info, probe_bucket, slot_info,
-                                                     slot_bucket, st);
+                                                     tiles, ntiles_groups, mp, ps.probe_info, ps.probe_bucket,
+                                                     ps.slot_info, ps.slot_bucket, st);
         else
             rc = groups_dispatch<PairView<uint32_t>>(ctx, PairView<uint32_t>{(const uint32_t*)ctx->sorted_key,
                                                                              ctx->sorted_idx},
-                                                     tiles, ntiles_groups, mp, probe_info, probe_bucket, slot_info,
-                                                     slot_bucket, st);
+                                                     tiles, ntiles_groups, mp, ps.probe_info, ps.probe_bucket,
+                                                     ps.slot_info, ps.slot_bucket, st);
     }
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    if (ctx->hc.err & 1u) return fail(ctx, MUMS_E_GAP, "Gap in genome sequence ('-' encountered)");
-    if (ctx->hc.err & 2u) return fail(ctx, MUMS_E_HIP, "sort look-back timed out (internal error)");
-    ctx->P = ctx->hc.nprobes;
-    ctx->probe_info = probe_info;
-    HIPCHK(hipEventRecord(ctx->ev[EV_GROUPS], st));
-
-    // probes grouped by hash bucket, key order kept (stable); values = probe ids
-    int tbits = 1;
-    while (tbits < 32 && ((uint64_t)1 << tbits) < (uint64_t)ctx->table_size) ++tbits;
-    int pout = 0;
-    HIPCHK(radix_sort<uint32_t>(probe_bucket, nullptr, ctx->P, tbits, bucketB, idsA, probe_bucket, idsB, ctx->tmp.p,
-                                &pout, st));
-    ctx->sorted_buckets = pout ? probe_bucket : bucketB;
-    ctx->sorted_ids = pout ? idsB : idsA;
-    HIPCHK(hipEventRecord(ctx->ev[EV_BUCKETS], st));
+    rc = finish_seeds(ctx, ps, st);
+    if (rc) return rc;
     ctx->stage_done = MUMS_STAGE_SEEDS;
 
     if (stage >= MUMS_STAGE_ALL) {
@@ -387,50 +507,95 @@ int run_pipeline(mums_ctx* ctx, int stage) {
     HIPCHK(hipStreamSynchronize(st));
     HIPCHK(hipMemcpy(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost));
 
-    // stats
-    mums_stats& s = ctx->st;
-    s = mums_stats{};
-    s.seedmers = N;
-    s.groups = ctx->hc.ngroups;
-    s.probes = ctx->P;
-    s.repeat_limit_groups = ctx->hc.repeat_limit;
-    auto el = [&](int a, int b) {
-        float ms = 0.f;
-        (void)hipEventElapsedTime(&ms, ctx->ev[a], ctx->ev[b]);
-        return (double)ms;
-    };
-    s.ms_keys = el(EV_START, EV_KEYS);
-    s.ms_sort = el(EV_KEYS, EV_SORT);
-    s.ms_groups = el(EV_SORT, EV_GROUPS);
-    s.ms_buckets = el(EV_GROUPS, EV_BUCKETS);
-    s.key_bytes = ctx->packed_path ? 8 : kb;
-    s.sort_passes = (uint64_t)passes;
-    if (prof && N > 0) {
-        for (int p = 0; p < passes; ++p) {
-            float ms = 0.f;
-            (void)hipEventElapsedTime(&ms, ctx->ev_ds[2 * p], ctx->ev_ds[2 * p + 1]);
-            s.ms_dominant += ms;
-            // algorithmic bytes of one downsweep launch: packed records read + written
-            // (8 + 8); pairs: read K (+4 after pass 0) and write K + 4
-            s.dominant_bytes += ctx->packed_path ? N * 16 : N * (kb + (p ? 4 : 0) + kb + 4);
-        }
-        s.dominant_launches = (uint64_t)passes;
+    fill_stats(ctx, N);
+    return MUMS_OK;
+}
+
+// Seed pattern (default from the mean genome length, MatchList.h:351-357; checks of
+// SortedMerList::Create :788-798) and the global genome table for genome lengths lens.
+int prepare_run(mums_ctx* ctx, const std::vector<uint64_t>& lens) {
+    ctx->stage_done = 0;
+    ctx->M = ctx->P = 0;
+    const int G = (int)lens.size();
+    if (ctx->enum_tol > 1)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "enumeration tolerance > 1 (MatchFinder::EnumerateMatches) not implemented");
+    uint64_t total = 0;
+    for (uint64_t n : lens) total += n;
+    uint64_t pat = ctx->seed;
+    if (pat == 0) {
+        uint32_t wdef = mums_default_seed_weight(G ? total / (uint64_t)G : 0);
+        pat = (uint64_t)mums_get_seed((int)wdef, 0);
     }
-    if (ctx->stage_done >= MUMS_STAGE_ALL) {
-        s.mem_count = ctx->hc.entries;
-        s.collision_count = ctx->hc.collisions;
-        s.ms_replay = el(EV_BUCKETS, EV_REPLAY);
-        s.ms_output = el(EV_REPLAY, EV_OUTPUT);
-        s.ms_total = el(EV_START, EV_OUTPUT);
-    } else {
-        s.ms_total = el(EV_START, EV_BUCKETS);
+    const int L = seed_len(pat), w = __builtin_popcountll(pat);
+    if (L == 0) return fail(ctx, MUMS_E_INVALID, "Can't have 0 seed length");
+    if (L > 32) return fail(ctx, MUMS_E_INVALID, "Mer size is too large");
+    if (w > 31) return fail(ctx, MUMS_E_UNSUPPORTED, "seed weight 32 not supported");
+    ctx->pattern = pat;
+    ctx->L = L;
+    ctx->w = w;
+    ctx->key64 = (2 * w + 1) > 32;
+    GenomeTable& gt = ctx->gt;
+    gt = GenomeTable{};
+    gt.G = G;
+    uint64_t N = 0;
+    for (int g = 0; g < G; ++g) {
+        gt.n[g] = lens[g];
+        gt.m[g] = gt.n[g] < (uint64_t)L ? 0 : gt.n[g] - L + 1;
+        gt.base[g] = N;
+        N += gt.m[g];
     }
+    gt.base[G] = N;
+    for (int g = G + 1; g <= kMaxG; ++g) gt.base[g] = N;
+    if (N >= 0xFFFFFFF0ull)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed-mers per context (chunked mode not implemented)");
+    ctx->N = N;
+    ctx->ss = make_seed_spec(pat, L, w);
     return MUMS_OK;
 }
 
 int check_ctx(mums_ctx* ctx) {
     if (!ctx) return MUMS_E_INVALID;
     ctx->err.clear();
+    return MUMS_OK;
+}
+
+// MSD bits of the sharded key exchange: at least the packed-record split (2w+1-32),
+// else 8 (256 key ranges to balance over the ranks), never the parity bit.
+int shard_msd_bits(int w) {
+    const int kbits = 2 * w + 1;
+    return std::min(kMaxMsdBits, std::max(kbits - 32, std::min(8, kbits - 1)));
+}
+
+int ceil_log2(uint64_t x) {
+    int b = 0;
+    while ((1ull << b) < x) ++b;
+    return b;
+}
+
+// sharded mode: global table from the layout, local table (owned genomes, global bases)
+int prepare_shard(mums_ctx* ctx) {
+    if (!ctx->shard) return fail(ctx, MUMS_E_INVALID, "no shard layout (mums_shard_layout)");
+    const uint32_t nl = (uint32_t)ctx->genomes.size();
+    if (ctx->shard_first + nl > ctx->shard_len.size())
+        return fail(ctx, MUMS_E_INVALID, "owned genomes exceed the shard layout");
+    for (uint32_t i = 0; i < nl; ++i)
+        if (ctx->genomes[i].n != ctx->shard_len[ctx->shard_first + i])
+            return fail(ctx, MUMS_E_INVALID, "owned genome length differs from the shard layout");
+    int rc = prepare_run(ctx, ctx->shard_len);
+    if (rc) return rc;
+    if (2 * ctx->w + 1 > 32 + kMaxMsdBits)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "sharded mode needs 2w+1 <= 43 (packed records)");
+    GenomeTable& l = ctx->lgt;
+    l = GenomeTable{};
+    l.G = (int)nl;
+    for (uint32_t i = 0; i < nl; ++i) {
+        l.n[i] = ctx->gt.n[ctx->shard_first + i];
+        l.m[i] = ctx->gt.m[ctx->shard_first + i];
+        l.base[i] = ctx->gt.base[ctx->shard_first + i];
+    }
+    for (int g = (int)nl; g <= kMaxG; ++g) l.base[g] = ctx->gt.base[ctx->shard_first + nl];
+    ctx->packed_path = true;
+    ctx->msd_bits = shard_msd_bits(ctx->w);
     return MUMS_OK;
 }
 
@@ -545,51 +710,18 @@ int mums_clear(mums_ctx* ctx) {
 int mums_find_stage(mums_ctx* ctx, int stage) {
     if (check_ctx(ctx)) return MUMS_E_INVALID;
     if (!have_device()) return fail(ctx, MUMS_E_NODEVICE, "no HIP device");
+    if (ctx->shard) return fail(ctx, MUMS_E_INVALID, "context is in sharded mode: use mums_shard_keys/merge");
     HIPCHK(hipSetDevice(ctx->device));
-    ctx->stage_done = 0;
-    ctx->M = ctx->P = 0;
-    const int G = (int)ctx->genomes.size();
-    if (ctx->enum_tol > 1)
-        return fail(ctx, MUMS_E_UNSUPPORTED, "enumeration tolerance > 1 (MatchFinder::EnumerateMatches) not implemented");
-    // seed (MatchList.h:351-357 default, SortedMerList::Create checks :788-798)
-    uint64_t total = 0;
-    for (auto& g : ctx->genomes) total += g.n;
-    uint64_t pat = ctx->seed;
-    if (pat == 0) {
-        uint32_t wdef = mums_default_seed_weight(G ? total / (uint64_t)G : 0);
-        pat = (uint64_t)mums_get_seed((int)wdef, 0);
-    }
-    const int L = seed_len(pat), w = __builtin_popcountll(pat);
-    if (L == 0) return fail(ctx, MUMS_E_INVALID, "Can't have 0 seed length");
-    if (L > 32) return fail(ctx, MUMS_E_INVALID, "Mer size is too large");
-    if (w > 31) return fail(ctx, MUMS_E_UNSUPPORTED, "seed weight 32 not supported");
-    ctx->pattern = pat;
-    ctx->L = L;
-    ctx->w = w;
-    ctx->key64 = (2 * w + 1) > 32;
-    GenomeTable& gt = ctx->gt;
-    gt = GenomeTable{};
-    gt.G = G;
-    uint64_t N = 0;
-    for (int g = 0; g < G; ++g) {
-        gt.n[g] = ctx->genomes[g].n;
-        gt.m[g] = gt.n[g] < (uint64_t)L ? 0 : gt.n[g] - L + 1;
-        gt.base[g] = N;
-        N += gt.m[g];
-    }
-    gt.base[G] = N;
-    for (int g = G + 1; g <= kMaxG; ++g) gt.base[g] = N;
-    if (N >= 0xFFFFFFF0ull)
-        return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed-mers per context (chunked mode not implemented)");
-    ctx->N = N;
-    if (G == 0) {
+    std::vector<uint64_t> lens;
+    for (auto& g : ctx->genomes) lens.push_back(g.n);
+    int rc = prepare_run(ctx, lens);
+    if (rc) return rc;
+    if (ctx->genomes.empty()) {
         ctx->stage_done = MUMS_STAGE_ALL;
         ctx->st = mums_stats{};
         return MUMS_OK;
     }
-    ctx->ss = make_seed_spec(pat, L, w);
-    int rc = run_pipeline(ctx, stage);
-    return rc;
+    return run_pipeline(ctx, stage);
 }
 
 int mums_find(mums_ctx* ctx) { return mums_find_stage(ctx, MUMS_STAGE_ALL); }
@@ -664,6 +796,182 @@ int mums_build_sml(mums_ctx* ctx, uint32_t genome, uint32_t* positions, uint64_t
     uint64_t o = 0;
     for (uint64_t i = 0; i < N; ++i)
         if (idx[i] >= lo && idx[i] < hi) positions[o++] = (uint32_t)(idx[i] - lo);
+    return MUMS_OK;
+}
+
+// ---- sharded seed stage -------------------------------------------
+
+int mums_shard_layout(mums_ctx* ctx, uint32_t genomes_total, uint32_t first_genome, const uint64_t* lengths) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (genomes_total > (uint32_t)kMaxG) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 32 genomes");
+    if (first_genome > genomes_total || (genomes_total && !lengths))
+        return fail(ctx, MUMS_E_INVALID, "bad shard layout");
+    ctx->shard = true;
+    ctx->shard_first = first_genome;
+    ctx->shard_len.assign(lengths, lengths + genomes_total);
+    ctx->stage_done = 0;
+    return MUMS_OK;
+}
+
+int mums_shard_msd_bits(mums_ctx* ctx, uint32_t* msd_bits, uint64_t* local_records) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    int rc = prepare_shard(ctx);
+    if (rc) return rc;
+    if (msd_bits) *msd_bits = (uint32_t)ctx->msd_bits;
+    if (local_records) {
+        uint64_t n = 0;
+        for (int g = 0; g < ctx->lgt.G; ++g) n += ctx->lgt.m[g];
+        *local_records = n;
+    }
+    return MUMS_OK;
+}
+
+int mums_shard_keys(mums_ctx* ctx, uint64_t* d_records, uint64_t capacity, uint64_t* bucket_counts) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (!have_device()) return fail(ctx, MUMS_E_NODEVICE, "no HIP device");
+    HIPCHK(hipSetDevice(ctx->device));
+    int rc = prepare_shard(ctx);
+    if (rc) return rc;
+    GenomeTable& l = ctx->lgt;
+    uint64_t n = 0;
+    for (int g = 0; g < l.G; ++g) n += l.m[g];
+    if (n > capacity || (n && !d_records)) return fail(ctx, MUMS_E_INVALID, "record buffer too small");
+    if (!bucket_counts) return fail(ctx, MUMS_E_INVALID, "null bucket_counts");
+    const int B = ctx->msd_bits;
+    const uint64_t nb = 1ull << B;
+    hipStream_t st = ctx->stream;
+    uint64_t words = 0;
+    const uint32_t T = layout_packed(l, &words);
+    HIPCHK(ctx->packed.ensure(words * 4 + 64));
+    HIPCHK(ctx->counters.ensure(sizeof(DevCounters)));
+    HIPCHK(ctx->hist.ensure(((uint64_t)T << B) * 4 + 64));
+    HIPCHK(ctx->tmp.ensure(scan_tmp_bytes(((uint64_t)T << B) + 1)));
+    HIPCHK(ctx->mstart.ensure((nb + 64) * 4));
+    DevCounters* dc = ctx->counters.as<DevCounters>();
+    HIPCHK(hipEventRecord(ctx->ev[EV_START], st));
+    HIPCHK(hipMemsetAsync(dc, 0, sizeof(DevCounters), st));
+    std::vector<uint32_t> hs(nb + 1, 0);
+    if (l.G > 0 && n > 0) {
+        rc = keys_stage(ctx, l, T, B, n, d_records, ctx->mstart.as<uint32_t>(), st);
+        if (rc) return rc;
+        HIPCHK(hipMemcpyAsync(hs.data(), ctx->mstart.p, (nb + 1) * 4, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(hipEventRecord(ctx->ev[EV_KEYS], st));
+    HIPCHK(hipMemcpyAsync(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (ctx->hc.err & 1u) return fail(ctx, MUMS_E_GAP, "Gap in genome sequence ('-' encountered)");
+    for (uint64_t b = 0; b < nb; ++b) bucket_counts[b] = (n > 0) ? (uint64_t)hs[b + 1] - hs[b] : 0;
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, ctx->ev[EV_START], ctx->ev[EV_KEYS]);
+    ctx->shard_keys_ms = ms;
+    return MUMS_OK;
+}
+
+int mums_shard_merge(mums_ctx* ctx, const uint64_t* d_records, uint32_t nsources, uint32_t first_bucket,
+                     uint32_t nbuckets, const uint64_t* counts) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (!have_device()) return fail(ctx, MUMS_E_NODEVICE, "no HIP device");
+    HIPCHK(hipSetDevice(ctx->device));
+    int rc = prepare_shard(ctx);
+    if (rc) return rc;
+    const int B = ctx->msd_bits;
+    if (nsources == 0 || (uint64_t)first_bucket + nbuckets > (1ull << B) || (nbuckets && !counts))
+        return fail(ctx, MUMS_E_INVALID, "bad shard merge arguments");
+    hipStream_t st = ctx->stream;
+    // chunk table: received source-major (each source's buckets in order) -> bucket-major
+    std::vector<uint64_t> tot(nbuckets, 0), chunks;
+    uint64_t n = 0;
+    for (uint32_t s = 0; s < nsources; ++s)
+        for (uint32_t b = 0; b < nbuckets; ++b) tot[b] += counts[(uint64_t)s * nbuckets + b];
+    for (uint32_t b = 0; b < nbuckets; ++b) n += tot[b];
+    if (n && !d_records) return fail(ctx, MUMS_E_INVALID, "null record buffer");
+    if (n >= 0xFFFFFFF0ull) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 records per shard");
+    const int mb = ceil_log2(nbuckets);
+    std::vector<uint32_t> bst((1ull << mb) + 1, (uint32_t)n);
+    {
+        std::vector<uint64_t> srcoff(nsources + 1, 0);
+        for (uint32_t s = 0; s < nsources; ++s) {
+            uint64_t c = 0;
+            for (uint32_t b = 0; b < nbuckets; ++b) c += counts[(uint64_t)s * nbuckets + b];
+            srcoff[s + 1] = srcoff[s] + c;
+        }
+        std::vector<uint64_t> inner(nsources, 0);   // running offset inside each source's block
+        uint64_t dst = 0;
+        for (uint32_t b = 0; b < nbuckets; ++b) {
+            bst[b] = (uint32_t)dst;
+            for (uint32_t s = 0; s < nsources; ++s) {
+                const uint64_t len = counts[(uint64_t)s * nbuckets + b];
+                if (len) {
+                    chunks.push_back(srcoff[s] + inner[s]);
+                    chunks.push_back(dst);
+                    chunks.push_back(len);
+                }
+                inner[s] += len;
+                dst += len;
+            }
+        }
+    }
+    ProbeSpace ps{};
+    rc = ensure_merge_space(ctx, n, mb, 2 * ctx->w + 1 - B, &ps);
+    if (rc) return rc;
+    HIPCHK(ctx->counters.ensure(sizeof(DevCounters)));
+    HIPCHK(ctx->keybuf.ensure(std::max<size_t>(chunks.size(), 1) * 8));
+    DevCounters* dc = ctx->counters.as<DevCounters>();
+    if (ctx->profiling && !ctx->ev_ds[0])
+        for (int i = 0; i < 16; ++i) HIPCHK(hipEventCreate(&ctx->ev_ds[i]));
+    HIPCHK(hipMemcpy(ctx->keybuf.p, chunks.data(), chunks.size() * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(ctx->mstart.p, bst.data(), bst.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipEventRecord(ctx->ev[EV_START], st));
+    HIPCHK(hipMemsetAsync(dc, 0, sizeof(DevCounters), st));
+    HIPCHK(launch_regroup(d_records, ctx->recA.as<uint64_t>(), ctx->keybuf.as<uint64_t>(),
+                          (uint32_t)(chunks.size() / 3), n, st));
+    HIPCHK(hipEventRecord(ctx->ev[EV_KEYS], st));
+    MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, ctx->masked, ctx->seq_mask};
+    ctx->N = n;
+    rc = merge_stage(ctx, n, mb, 2 * ctx->w + 1 - B, mp, ps, st);
+    if (rc) return rc;
+    rc = finish_seeds(ctx, ps, st);
+    if (rc) return rc;
+    ctx->stage_done = MUMS_STAGE_SEEDS;
+    HIPCHK(hipStreamSynchronize(st));
+    fill_stats(ctx, n);
+    float rg = 0.f;
+    (void)hipEventElapsedTime(&rg, ctx->ev[EV_START], ctx->ev[EV_KEYS]);
+    ctx->st.ms_sort += rg;                 // the regroup copy is part of the merge's sort
+    ctx->st.ms_keys = ctx->shard_keys_ms;  // keys stage of the owned genomes (mums_shard_keys)
+    return MUMS_OK;
+}
+
+int mums_probe_count(mums_ctx* ctx, uint64_t* count) {
+    if (check_ctx(ctx) || !count) return MUMS_E_INVALID;
+    if (ctx->stage_done < MUMS_STAGE_SEEDS) return fail(ctx, MUMS_E_INVALID, "no seed stage run");
+    *count = ctx->P;
+    return MUMS_OK;
+}
+
+int mums_probe_copy(mums_ctx* ctx, uint32_t* buckets, uint64_t* ref_index, uint64_t capacity) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (ctx->stage_done < MUMS_STAGE_SEEDS) return fail(ctx, MUMS_E_INVALID, "no seed stage run");
+    if (capacity < ctx->P) return fail(ctx, MUMS_E_INVALID, "output buffer too small");
+    if (!ctx->packed_path) return fail(ctx, MUMS_E_UNSUPPORTED, "probe export needs the packed-record path");
+    const uint64_t P = ctx->P, N = ctx->N;
+    if (P == 0) return MUMS_OK;
+    HIPCHK(hipSetDevice(ctx->device));
+    std::vector<uint64_t> info(P), rec(N);
+    std::vector<uint32_t> bkt(P), ids(P);
+    HIPCHK(hipMemcpy(info.data(), ctx->probe_info, P * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(rec.data(), ctx->sorted_rec, N * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(bkt.data(), ctx->sorted_buckets, P * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(ids.data(), ctx->sorted_ids, P * 4, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> bucket_of_probe(P);
+    for (uint64_t i = 0; i < P; ++i) bucket_of_probe[ids[i]] = bkt[i];
+    for (uint64_t k = 0; k < P; ++k) {
+        const uint64_t h = (uint32_t)info[k], gs = info[k] >> 32;
+        uint64_t mn = ~0ull;
+        for (uint64_t i = h; i < h + gs && i < N; ++i) mn = std::min<uint64_t>(mn, (uint32_t)rec[i]);
+        if (buckets) buckets[k] = bucket_of_probe[k];
+        if (ref_index) ref_index[k] = mn;
+    }
     return MUMS_OK;
 }
 

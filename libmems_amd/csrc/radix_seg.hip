@@ -36,18 +36,23 @@ __global__ void bucket_starts_kernel(const uint32_t* __restrict__ scanned, uint3
     if (b > nb) return;
     const uint64_t s = (b == nb) ? n : (uint64_t)scanned[(uint64_t)b * T];
     bstart[b] = (uint32_t)s;
-    if (b < nb) {
+    if (ntb && b < nb) {
         const uint64_t e = (b + 1 == nb) ? n : (uint64_t)scanned[(uint64_t)(b + 1) * T];
         ntb[b] = (uint32_t)((e - s + kTile - 1) / kTile);
     }
 }
 
-__global__ void single_bucket_kernel(uint64_t n, uint32_t* __restrict__ bstart, uint32_t* __restrict__ tfirst) {
+// tiles per bucket from bucket starts (tfirst[nb] = 0 so one scan gives the total)
+__global__ void ntb_from_starts_kernel(const uint32_t* __restrict__ bstart, int nb, uint32_t* __restrict__ ntb) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b > nb) return;
+    ntb[b] = (b == nb) ? 0u : (uint32_t)(((uint64_t)bstart[b + 1] - bstart[b] + kTile - 1) / kTile);
+}
+
+__global__ void single_bucket_kernel(uint64_t n, uint32_t* __restrict__ bstart) {
     if (threadIdx.x == 0) {
         bstart[0] = 0;
         bstart[1] = (uint32_t)n;
-        tfirst[0] = 0;
-        tfirst[1] = (uint32_t)((n + kTile - 1) / kTile);
     }
 }
 
@@ -451,27 +456,74 @@ size_t seg_tmp_bytes(uint64_t n, int msd_bits) {
     return (h + 64) * 4 + (2 * nb + 130) * 4 + scan_tmp_bytes(h > nb ? h : nb) + 512;
 }
 
-// d_hist_scanned: the scanned MSD histogram [nb x T] (nullptr when msd_bits == 0).
-hipError_t build_seg_tiles(const uint32_t* d_hist_scanned, uint32_t T, int msd_bits, uint64_t n, SegTile* d_tiles,
-                           uint32_t* d_ntiles, uint32_t* bstart, void* d_tmp, hipStream_t st) {
+// Regroup: dst[j] for j in [dst_off[c], dst_off[c] + len[c]) = src[src_off[c] + (j - dst_off[c])];
+// chunks sorted by dst_off and tiling [0, n).  One block per 4096 destination records:
+// the block's first chunk by binary search, then a short forward walk per element.
+__global__ __launch_bounds__(256) void regroup_kernel(const uint64_t* __restrict__ src, uint64_t* __restrict__ dst,
+                                                      const uint64_t* __restrict__ chunks, uint32_t nchunks,
+                                                      uint64_t n) {
+    __shared__ uint32_t s_c0;
+    const uint64_t j0 = (uint64_t)blockIdx.x * 4096;
+    if (threadIdx.x == 0) {
+        uint32_t lo = 0, hi = nchunks - 1;   // last chunk with dst_off <= j0
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (chunks[3 * mid + 1] <= j0) lo = mid;
+            else hi = mid - 1;
+        }
+        s_c0 = lo;
+    }
+    __syncthreads();
+    uint32_t c = s_c0;
+    for (uint64_t j = j0 + threadIdx.x; j < j0 + 4096 && j < n; j += 256) {
+        while (c + 1 < nchunks && chunks[3 * (c + 1) + 1] <= j) ++c;
+        dst[j] = src[chunks[3 * c] + (j - chunks[3 * c + 1])];
+    }
+}
+
+hipError_t launch_regroup(const uint64_t* src, uint64_t* dst, const uint64_t* d_chunks, uint32_t nchunks, uint64_t n,
+                          hipStream_t st) {
+    if (n == 0 || nchunks == 0) return hipSuccess;
+    hipLaunchKernelGGL(regroup_kernel, dim3((unsigned)((n + 4095) / 4096)), dim3(256), 0, st, src, dst, d_chunks,
+                       nchunks, n);
+    return hipGetLastError();
+}
+
+hipError_t seg_bucket_starts(const uint32_t* d_hist_scanned, uint32_t T, int msd_bits, uint64_t n, uint32_t* bstart,
+                             hipStream_t st) {
+    const int nb = 1 << msd_bits;
+    if (msd_bits == 0) {
+        hipLaunchKernelGGL(single_bucket_kernel, dim3(1), dim3(64), 0, st, n, bstart);
+    } else {
+        hipLaunchKernelGGL(bucket_starts_kernel, dim3((nb + 256) / 256), dim3(256), 0, st, d_hist_scanned, T, nb, n,
+                           bstart, (uint32_t*)nullptr);
+    }
+    return hipGetLastError();
+}
+
+hipError_t build_seg_tiles_from_starts(const uint32_t* bstart, int msd_bits, uint64_t n, SegTile* d_tiles,
+                                       uint32_t* d_ntiles, void* d_tmp, hipStream_t st) {
     const int nb = 1 << msd_bits;
     const uint64_t ub = seg_tiles_upper(n, msd_bits);
     uint32_t* tfirst = (uint32_t*)d_tmp;
     void* stmp = (void*)(tfirst + nb + 64);
-    if (msd_bits == 0) {
-        hipLaunchKernelGGL(single_bucket_kernel, dim3(1), dim3(64), 0, st, n, bstart, tfirst);
-    } else {
-        hipLaunchKernelGGL(bucket_starts_kernel, dim3((nb + 256) / 256), dim3(256), 0, st, d_hist_scanned, T, nb, n,
-                           bstart, tfirst);
-        // tfirst[b] = exclusive scan of tiles per bucket; tfirst[nb] = total
-        hipError_t e = exclusive_scan_u32(tfirst, (uint64_t)nb + 1, stmp, nullptr, st);
-        if (e != hipSuccess) return e;
-    }
+    hipLaunchKernelGGL(ntb_from_starts_kernel, dim3((nb + 256) / 256), dim3(256), 0, st, bstart, nb, tfirst);
+    // tfirst[b] = exclusive scan of tiles per bucket; tfirst[nb] = total
+    hipError_t e = exclusive_scan_u32(tfirst, (uint64_t)nb + 1, stmp, nullptr, st);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(tiles_kernel, dim3((unsigned)((ub + 255) / 256)), dim3(256), 0, st, bstart, tfirst, nb, ub,
                        d_tiles, d_ntiles);
     hipLaunchKernelGGL(claim_order_kernel, dim3((unsigned)((ub + 255) / 256)), dim3(256), 0, st, tfirst, nb, ub,
                        d_tiles);
     return hipGetLastError();
+}
+
+// d_hist_scanned: the scanned MSD histogram [nb x T] (nullptr when msd_bits == 0).
+hipError_t build_seg_tiles(const uint32_t* d_hist_scanned, uint32_t T, int msd_bits, uint64_t n, SegTile* d_tiles,
+                           uint32_t* d_ntiles, uint32_t* bstart, void* d_tmp, hipStream_t st) {
+    hipError_t e = seg_bucket_starts(d_hist_scanned, T, msd_bits, n, bstart, st);
+    if (e != hipSuccess) return e;
+    return build_seg_tiles_from_starts(bstart, msd_bits, n, d_tiles, d_ntiles, d_tmp, st);
 }
 
 size_t onesweep_tmp_bytes(uint64_t n, int msd_bits, int key_bits) {
@@ -504,8 +556,8 @@ hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key
     uint64_t* dst = recB;
     for (int p = 0; p < npass; ++p) {
         if (ev_ds) (void)hipEventRecord(ev_ds[2 * p], st);
-        hipLaunchKernelGGL(seg_onesweep_kernel<kOnesweepIPT>, dim3((unsigned)ntiles_ub), dim3(kBlock), 0, st, src, dst, d_tiles,
-                           (uint32_t)ntiles_ub, 32 + 8 * p, p, npass, dbase,
+        hipLaunchKernelGGL(seg_onesweep_kernel<kOnesweepIPT>, dim3((unsigned)ntiles_ub), dim3(kBlock), 0, st, src,
+                           dst, d_tiles, (uint32_t)ntiles_ub, 32 + 8 * p, p, npass, dbase,
                            status + (uint64_t)p * ntiles_ub * kDigits, counters + p, d_err);
         e = hipGetLastError();
         if (e != hipSuccess) return e;

@@ -1,0 +1,161 @@
+"""Sharded MemHash seed stage across GPUs: genome-per-rank keys,
+key-range exchange, per-rank merge of one key range.
+
+The reference builds one SortedMerList per genome (MemorySML::Create,
+MemorySML.cpp:45-60) and merges all G of them in masked-key order in one thread
+(MatchFinder::SearchRange, MatchFinder.cpp:172-340) before MemHash accepts each
+key group (MemHash::EnumerateMatches, MemHash.cpp:139-162).  Here every rank owns a
+contiguous block of genomes (one process per GPU):
+
+  1. keys    : the rank's genomes -> 8-B records (ckey_low << 32 | global index),
+               stably bucketed by the top B key bits (HIP, mums_shard_keys);
+  2. ranges  : per-bucket counts all-gathered; the 2^B buckets are cut into
+               world_size contiguous key ranges of balanced record counts;
+  3. exchange: one all-to-all (RCCL over xGMI on GPUs) sends every bucket range to
+               its owner; sources arrive in rank order = global index order;
+  4. merge   : each rank sorts / groups / accepts its key range (mums_shard_merge).
+
+Rank r's probes are the reference's AddHashEntry calls for the keys of range r, so
+concatenating the ranks' probe lists in rank order reproduces the single-process
+order exactly.  The engine is pluggable: HipShardEngine drives the C ABI; tests
+drive the same orchestration with a CPU engine over gloo.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import MemHash
+
+
+def key_ranges(bucket_totals: np.ndarray, world: int) -> List[Tuple[int, int]]:
+    """Cut buckets [0, nb) into `world` contiguous ranges (first, count) whose record
+    totals are as even as bucket granularity allows (boundary r at the first bucket whose
+    prefix sum reaches r/world of the total).  Deterministic from the totals alone, so
+    every rank computes the same cut."""
+    nb = int(bucket_totals.shape[0])
+    cum = np.concatenate([[0], np.cumsum(bucket_totals.astype(np.int64))])
+    total = int(cum[-1])
+    bounds = [0]
+    for r in range(1, world):
+        target = (total * r + world - 1) // world
+        b = int(np.searchsorted(cum, target, side="left"))
+        bounds.append(min(max(b, bounds[-1]), nb))
+    bounds.append(nb)
+    return [(bounds[r], bounds[r + 1] - bounds[r]) for r in range(world)]
+
+
+def genome_blocks(G: int, world: int) -> List[Tuple[int, int]]:
+    """Contiguous genome block (first, count) per rank; earlier ranks take the remainder."""
+    base, rem = divmod(G, world)
+    out, g = [], 0
+    for r in range(world):
+        c = base + (1 if r < rem else 0)
+        out.append((g, c))
+        g += c
+    return out
+
+
+class HipShardEngine:
+    """One rank's MemHash context in sharded mode (C ABI, HIP kernels on `device`)."""
+
+    def __init__(self, device: int, seed: int, lengths: Sequence[int], first: int, genomes: Sequence,
+                 profiling: bool = False):
+        self.mh = MemHash(device)
+        self.device = torch.device("cuda", device)
+        self.mh.SetSeed(seed)
+        for s in genomes:
+            self.mh.AddSequence(s)
+        lens = (ctypes.c_uint64 * len(lengths))(*[int(x) for x in lengths])
+        lib = self.mh._lib
+        self.mh._check(lib.mums_shard_layout(self.mh._ctx, len(lengths), first, lens))
+        if profiling:
+            self.mh.SetProfiling(True)
+
+    def msd_bits(self) -> Tuple[int, int]:
+        b, n = ctypes.c_uint32(), ctypes.c_uint64()
+        self.mh._check(self.mh._lib.mums_shard_msd_bits(self.mh._ctx, ctypes.byref(b), ctypes.byref(n)))
+        return int(b.value), int(n.value)
+
+    def alloc(self, n: int) -> torch.Tensor:
+        return torch.empty(max(n, 1), dtype=torch.int64, device=self.device)
+
+    def keys(self, rec: torch.Tensor, nb: int) -> np.ndarray:
+        counts = np.zeros(nb, dtype=np.uint64)
+        self.mh._check(self.mh._lib.mums_shard_keys(self.mh._ctx, ctypes.c_void_p(rec.data_ptr()), rec.numel(),
+                                                     counts.ctypes.data))
+        return counts
+
+    def merge(self, recv: torch.Tensor, nsrc: int, first: int, nbuckets: int, counts: np.ndarray) -> None:
+        c = np.ascontiguousarray(counts, dtype=np.uint64)
+        self.mh._check(self.mh._lib.mums_shard_merge(self.mh._ctx, ctypes.c_void_p(recv.data_ptr()), nsrc, first,
+                                                      nbuckets, c.ctypes.data))
+
+    def stats(self) -> dict:
+        return self.mh.stats()
+
+    def probes(self):
+        return self.mh.Probes()
+
+    def close(self) -> None:
+        self.mh.close()
+
+
+class ShardedSeedStage:
+    """Orchestrates steps 1-4 for one rank of the default process group (or `group`)."""
+
+    def __init__(self, engine, group: Optional[dist.ProcessGroup] = None):
+        self.engine = engine
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        backend = dist.get_backend(group) if dist.is_initialized() else "none"
+        # collectives run where the backend wants their tensors: RCCL on the GPU, gloo on the host
+        self.wire = "cuda" if backend == "nccl" else "cpu"
+        self.last_range: Tuple[int, int] = (0, 0)
+        self.last_exchange_bytes = 0
+
+    def _all_gather_counts(self, counts: np.ndarray) -> np.ndarray:
+        if self.world == 1:
+            return counts[None, :].astype(np.int64)
+        t = torch.from_numpy(counts.astype(np.int64)).to(self.wire)
+        parts = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(parts, t, group=self.group)
+        return torch.stack(parts).cpu().numpy()
+
+    def run(self) -> None:
+        eng = self.engine
+        B, n_local = eng.msd_bits()
+        nb = 1 << B
+        rec = eng.alloc(n_local)
+        counts = eng.keys(rec, nb)
+        C = self._all_gather_counts(counts)                 # [world, nb]
+        ranges = key_ranges(C.sum(axis=0), self.world)
+        first, cnt = ranges[self.rank]
+        self.last_range = (first, cnt)
+        sub = np.ascontiguousarray(C[:, first:first + cnt])
+        if self.world == 1:
+            eng.merge(rec, 1, first, cnt, sub)
+            return
+        send = [int(C[self.rank, f:f + c].sum()) for f, c in ranges]
+        recv = [int(C[s, first:first + cnt].sum()) for s in range(self.world)]
+        src = rec[:n_local] if n_local else rec[:0]
+        if self.wire == "cpu" and src.is_cuda:
+            src = src.cpu()
+        out = torch.empty(sum(recv), dtype=torch.int64, device=src.device)
+        dist.all_to_all_single(out, src.contiguous(), recv, send, group=self.group)
+        if self.wire == "cuda":
+            torch.cuda.current_stream().synchronize()     # the engine runs on its own stream
+        self.last_exchange_bytes = 8 * (sum(send) - send[self.rank])
+        if out.device != rec.device:
+            out = out.to(rec.device)
+            if out.is_cuda:
+                torch.cuda.current_stream().synchronize()
+        eng.merge(out, self.world, first, cnt, sub)
+
+
+__all__ = ["key_ranges", "genome_blocks", "HipShardEngine", "ShardedSeedStage"]

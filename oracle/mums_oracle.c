@@ -404,6 +404,8 @@ struct oracle_result {
     uint64_t* lengths;
     int64_t* starts;
     uint64_t mem_count, collision_count, max_group, probes, seedmers;
+    uint32_t* plog_bucket;    /* seeds_only: per AddHashEntry call, its bucket ... */
+    uint64_t* plog_ref;       /* ... and the global seed-mer index of the probe's first start */
 };
 
 typedef struct {
@@ -415,6 +417,8 @@ typedef struct {
     mhe_t* pool; uint64_t pool_n, pool_cap;
     int64_t* spool; uint64_t spool_n, spool_cap;
     uint64_t mem_count, collisions, probes;
+    const uint64_t* gbase;    /* global seed-mer index of each genome's position 0 */
+    uint32_t* plog_bucket; uint64_t* plog_ref; uint64_t plog_cap;
 } memhash_t;
 
 static uint32_t pool_add(memhash_t* h, const mhe_t* src) {
@@ -457,7 +461,20 @@ static void add_hash_entry(memhash_t* h, mhe_t* p) {
     uint32_t bi = (uint32_t)(((p->offset % T) + T) % T);
     bucket_t* b = &h->buckets[bi];
     ++h->probes;
-    if (h->seeds_only) { h->bucket_sum += bi; return; }
+    if (h->seeds_only) {
+        h->bucket_sum += bi;
+        /* probe log (checking aid): the probe's identity = global index of its first start */
+        if (h->probes > h->plog_cap) {
+            h->plog_cap = h->plog_cap ? 2 * h->plog_cap : 4096;
+            h->plog_bucket = (uint32_t*)realloc(h->plog_bucket, h->plog_cap * sizeof(uint32_t));
+            h->plog_ref = (uint64_t*)realloc(h->plog_ref, h->plog_cap * sizeof(uint64_t));
+        }
+        int f = first_start(p, h->x.G);
+        int64_t s0 = p->s[f] < 0 ? -p->s[f] : p->s[f];
+        h->plog_bucket[h->probes - 1] = bi;
+        h->plog_ref[h->probes - 1] = h->gbase[f] + (uint64_t)(s0 - 1);
+        return;
+    }
     uint32_t it = lower_bound_mhe(h, b, p);
     if (it != b->n) {
         const mhe_t* e = &h->pool[b->v[it]];
@@ -584,6 +601,9 @@ oracle_result* oracle_find_matches(int G, const char* const* seqs, const uint64_
         h.x.gnseqi_end = prm->gnseqi_end_neg1 ? (int64_t)-1 : INT64_MAX;
         h.table_size = prm->table_size ? prm->table_size : 40000;
         h.seeds_only = prm->seeds_only;
+        uint64_t* gbase = (uint64_t*)calloc((size_t)G + 1, sizeof(uint64_t));
+        for (int g = 0; g < G; ++g) gbase[g + 1] = gbase[g] + m[g];
+        h.gbase = gbase;
         h.buckets = (bucket_t*)calloc(h.table_size, sizeof(bucket_t));
         int64_t* scratch = (int64_t*)malloc((size_t)G * sizeof(int64_t));
 
@@ -639,7 +659,9 @@ oracle_result* oracle_find_matches(int G, const char* const* seqs, const uint64_
         res->mem_count = h.mem_count;
         res->collision_count = h.collisions;
         res->probes = h.probes;
-        free(h.buckets); free(h.pool); free(h.spool);
+        free(h.buckets); free(h.pool); free(h.spool); free(gbase);
+        res->plog_bucket = h.plog_bucket;
+        res->plog_ref = h.plog_ref;
     }
 done:
     for (int g = 0; g < G; ++g) { free(words[g]); free(keys[g]); free(sml[g]); }
@@ -658,10 +680,17 @@ uint64_t oracle_result_mem_count(const oracle_result* r) { return r ? r->mem_cou
 uint64_t oracle_result_collision_count(const oracle_result* r) { return r ? r->collision_count : 0; }
 uint64_t oracle_result_max_group(const oracle_result* r) { return r ? r->max_group : 0; }
 uint64_t oracle_result_probe_count(const oracle_result* r) { return r ? r->probes : 0; }
+/* seeds_only runs: the probe log (probe_count entries, AddHashEntry call order) */
+int oracle_result_probe_log(const oracle_result* r, uint32_t* buckets, uint64_t* ref) {
+    if (!r || !r->plog_bucket) return -1;
+    if (buckets) memcpy(buckets, r->plog_bucket, r->probes * sizeof(uint32_t));
+    if (ref) memcpy(ref, r->plog_ref, r->probes * sizeof(uint64_t));
+    return 0;
+}
 uint64_t oracle_result_seedmers(const oracle_result* r) { return r ? r->seedmers : 0; }
 void     oracle_result_free(oracle_result* r) {
     if (!r) return;
-    free(r->lengths); free(r->starts); free(r);
+    free(r->lengths); free(r->starts); free(r->plog_bucket); free(r->plog_ref); free(r);
 }
 
 /* ------------------------------------------------------------------------- */

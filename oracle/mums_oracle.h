@@ -65,6 +65,7 @@ uint64_t oracle_result_mem_count(const oracle_result* r);
 uint64_t oracle_result_collision_count(const oracle_result* r);
 uint64_t oracle_result_max_group(const oracle_result* r);
 uint64_t oracle_result_probe_count(const oracle_result* r);
+int      oracle_result_probe_log(const oracle_result* r, uint32_t* buckets, uint64_t* ref);
 uint64_t oracle_result_seedmers(const oracle_result* r);
 void     oracle_result_free(oracle_result* r);
 

@@ -63,6 +63,7 @@ def lib() -> ctypes.CDLL:
             fn.argtypes = [vp]
             fn.restype = u64
         L.oracle_result_seqcount.argtypes = [vp]
+        L.oracle_result_probe_log.argtypes = [vp, vp, vp]
         L.oracle_result_copy.argtypes = [vp, vp, vp]
         L.oracle_result_free.argtypes = [vp]
         L.oracle_generate.argtypes = [ctypes.c_int, u64, ctypes.c_double, u64, ctypes.c_char_p]
@@ -132,6 +133,30 @@ def find_matches(seqs: Sequence[bytes], seed: int, repeat_tol: int = 0, enum_tol
     finally:
         L.oracle_result_free(r)
     return lengths, starts, stats
+
+
+def seed_probes(seqs: Sequence[bytes], seed: int, table_size: int = 40000) -> Tuple[np.ndarray, np.ndarray, dict]:
+    """Seed stage only (keys, SMLs, G-way merge, acceptance, probes): the AddHashEntry calls
+    in order as (bucket[P], ref[P]) with ref = global seed-mer index of the probe's first
+    start (genome bases = cumulative SMLLength), plus the counters."""
+    G = len(seqs)
+    arr = (ctypes.c_char_p * G)(*seqs)
+    lens = (ctypes.c_uint64 * G)(*[len(s) for s in seqs])
+    prm = _Params(seed, 0, 1, table_size, 0, 0, 0, 1)
+    L = lib()
+    r = L.oracle_find_matches(G, arr, lens, ctypes.byref(prm))
+    if not r:
+        raise ValueError("oracle rejected input")
+    try:
+        P = L.oracle_result_probe_count(r)
+        b = np.zeros(max(P, 1), dtype=np.uint32)
+        ref = np.zeros(max(P, 1), dtype=np.uint64)
+        if P:
+            L.oracle_result_probe_log(r, b.ctypes.data, ref.ctypes.data)
+        stats = dict(probes=P, seedmers=L.oracle_result_seedmers(r), max_group=L.oracle_result_max_group(r))
+    finally:
+        L.oracle_result_free(r)
+    return b[:P], ref[:P], stats
 
 
 def match_text(lengths: np.ndarray, starts: np.ndarray) -> str:

@@ -1,0 +1,105 @@
+"""Sharded seed stage on CPU: gloo world_size 2 against the oracle.
+
+The rank orchestration of libmems_amd.shard (genome blocks, balanced key ranges,
+all-to-all splits, source order) runs over gloo with the CPU engine of
+tests/shard_engine_cpu.py; the concatenated per-rank probe lists must equal the
+oracle's AddHashEntry call sequence (bucket, first-start index) exactly.
+"""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from libmems_amd.shard import genome_blocks, key_ranges
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_key_ranges_balanced_and_contiguous():
+    rng = np.random.default_rng(1)
+    tot = rng.integers(0, 1000, size=256)
+    for world in (1, 2, 3, 4, 8):
+        r = key_ranges(tot, world)
+        assert len(r) == world
+        assert r[0][0] == 0 and sum(c for _, c in r) == 256
+        for (f0, c0), (f1, _) in zip(r, r[1:]):
+            assert f0 + c0 == f1
+        loads = [int(tot[f:f + c].sum()) for f, c in r]
+        assert max(loads) - min(loads) <= 2 * int(tot.max()) + 1
+
+
+def test_key_ranges_degenerate():
+    assert key_ranges(np.zeros(4, np.int64), 2) == [(0, 0), (0, 4)]
+    one = np.zeros(16, np.int64)
+    one[5] = 100                      # every record in one bucket: one rank gets it all
+    r = key_ranges(one, 4)
+    assert sum(c for _, c in r) == 16
+    assert sum(1 for f, c in r if one[f:f + c].sum() > 0) == 1
+
+
+def test_genome_blocks():
+    assert genome_blocks(8, 8) == [(g, 1) for g in range(8)]
+    assert genome_blocks(8, 3) == [(0, 3), (3, 3), (6, 2)]
+    assert genome_blocks(2, 4) == [(0, 1), (1, 1), (2, 0), (2, 0)]
+
+
+def _worker(rank, world, port, seqs, seed, outdir):
+    import torch.distributed as dist
+    from libmems_amd.shard import ShardedSeedStage, genome_blocks
+    from tests.shard_engine_cpu import CpuShardEngine
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        first, count = genome_blocks(len(seqs), world)[rank]
+        eng = CpuShardEngine(seqs, first, count, seed)
+        stage = ShardedSeedStage(eng)
+        stage.run()
+        b, r = eng.probes()
+        np.save(os.path.join(outdir, f"b{rank}.npy"), b)
+        np.save(os.path.join(outdir, f"r{rank}.npy"), r)
+    finally:
+        dist.destroy_process_group()
+
+
+def _sharded_probes(seqs, seed, world):
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(world, _free_port(), seqs, seed, d), nprocs=world, join=True)
+        b = np.concatenate([np.load(os.path.join(d, f"b{r}.npy")) for r in range(world)])
+        r = np.concatenate([np.load(os.path.join(d, f"r{r}.npy")) for r in range(world)])
+    return b, r
+
+
+@pytest.mark.parametrize("G,n,p,w,world", [(4, 60_000, 0.03, 15, 2), (3, 40_000, 0.05, 19, 2),
+                                             (6, 20_000, 0.03, 19, 2)])
+def test_sharded_seed_stage_matches_oracle(oracle_mod, G, n, p, w, world):
+    seqs = oracle_mod.generate(G, n, p, 4242 + G)
+    seed = oracle_mod.get_seed(w)
+    ob, orf, st = oracle_mod.seed_probes(seqs, seed)
+    assert st["probes"] > 1000
+    b, r = _sharded_probes(seqs, seed, world)
+    assert len(b) == len(ob)
+    assert np.array_equal(b, ob)
+    assert np.array_equal(r, orf)
+
+
+def test_single_rank_engine_matches_oracle(oracle_mod):
+    """The CPU engine alone (world 1, no process group) reproduces the oracle."""
+    from libmems_amd.shard import ShardedSeedStage
+    from tests.shard_engine_cpu import CpuShardEngine
+
+    seqs = oracle_mod.generate(3, 30_000, 0.02, 99)
+    seed = oracle_mod.get_seed(15)
+    eng = CpuShardEngine(seqs, 0, 3, seed)
+    ShardedSeedStage(eng).run()
+    b, r = eng.probes()
+    ob, orf, _ = oracle_mod.seed_probes(seqs, seed)
+    assert np.array_equal(b, ob) and np.array_equal(r, orf)
