@@ -16,6 +16,9 @@
 //      (a group needs >= 2 records, so <= 2048 probes per tile).
 // A second kernel concatenates the tiles' slots using the scanned tile counts, so
 // the probes end up in ascending key order = the reference's AddHashEntry order.
+#include <cstdlib>
+#include <type_traits>
+
 #include "match_device.h"
 #include "seed_device.h"
 
@@ -145,6 +148,169 @@ __global__ __launch_bounds__(kBlock) void probe_tile_kernel(View v, const SegTil
     }
 }
 
+// Packed-record path: the tile's records are staged in LDS once; head detection and
+// the probes read them there (a group that runs past the tile end falls back to the
+// global stream), and the compaction is fused into the probe loop, so a block makes one
+// global load round and one store round.
+typedef __attribute__((address_space(3))) const uint64_t lds_u64;
+
+struct TileRecView {
+    lds_u64* lds;           // records [t0, t0 + count) of the sorted stream (LDS)
+    const uint64_t* glob;   // the whole sorted stream
+    uint64_t t0;
+    uint32_t count;
+    __device__ __forceinline__ uint64_t raw(uint64_t i) const {
+        const uint64_t k = i - t0;
+        return k < count ? lds[k] : glob[i];
+    }
+    __device__ __forceinline__ uint64_t gkey(uint64_t i) const { return raw(i) >> 33; }
+    __device__ __forceinline__ uint32_t par(uint64_t i) const { return (uint32_t)(raw(i) >> 32) & 1u; }
+    __device__ __forceinline__ uint32_t gidx(uint64_t i) const { return (uint32_t)raw(i); }
+    __device__ __forceinline__ RecFields get(uint64_t i) const {
+        const uint64_t r = raw(i);
+        return RecFields{r >> 33, (uint32_t)(r >> 32) & 1u, (uint32_t)r};
+    }
+};
+
+template <int MG>
+__global__ __launch_bounds__(kBlock) void probe_tile_rec_kernel(const uint64_t* __restrict__ rec,
+                                                                const SegTile* __restrict__ tiles, GenomeTable gt,
+                                                                MatchParams mp, int L,
+                                                                uint32_t* __restrict__ tile_count,
+                                                                uint64_t* __restrict__ slot_info,
+                                                                uint32_t* __restrict__ slot_bucket,
+                                                                DevCounters* __restrict__ ctr, int abl) {
+    __shared__ uint64_t srec[kGTile];
+    __shared__ uint16_t heads[kGTile];
+    __shared__ uint32_t wcnt[kGRounds][kBlock / 64];
+    __shared__ uint32_t s_w[kBlock / 64];
+    __shared__ uint32_t s_red[2];
+    __shared__ uint64_t s_prev;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const SegTile td = tiles[blockIdx.x];
+    if (td.count == 0) {
+        if (threadIdx.x == 0) {
+            tile_count[blockIdx.x] = 0;
+            tile_count[gridDim.x + 32 + blockIdx.x] = 0;
+        }
+        return;
+    }
+    const uint64_t tile0 = td.start;
+    const uint32_t cnt = td.count;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+
+    // 1) stage the tile (lane-contiguous, coalesced) + the record before it.  The loads
+    //    use clamped indices so all kGRounds are in flight before the first LDS store.
+    {
+        uint64_t x[kGRounds];
+        #pragma unroll
+        for (int r = 0; r < kGRounds; ++r) {
+            const uint32_t q = r * kBlock + threadIdx.x;
+            x[r] = rec[tile0 + (q < cnt ? q : cnt - 1)];
+        }
+        #pragma unroll
+        for (int r = 0; r < kGRounds; ++r) {
+            const uint32_t q = r * kBlock + threadIdx.x;
+            if (q < cnt) srec[q] = x[r];
+        }
+    }
+    if (threadIdx.x == 0) s_prev = (tile0 > td.bstart) ? rec[tile0 - 1] : ~0ull;
+    __syncthreads();
+
+    // 2) heads in stream order
+    uint32_t hmask = 0;
+    #pragma unroll
+    for (int r = 0; r < kGRounds; ++r) {
+        const uint32_t q = r * kBlock + threadIdx.x;
+        bool head = false;
+        if (q < cnt) {
+            const uint64_t here = srec[q] >> 33;
+            if (q == 0) head = (tile0 == td.bstart) || (here != (s_prev >> 33));
+            else head = here != (srec[q - 1] >> 33);
+        }
+        hmask |= (head ? 1u : 0u) << r;
+        const uint64_t bal = __ballot(head);
+        if (lane == 0) wcnt[r][wv] = (uint32_t)__popcll(bal);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int r = 0; r < kGRounds; ++r)
+            for (int w = 0; w < kBlock / 64; ++w) { const uint32_t c = wcnt[r][w]; wcnt[r][w] = acc; acc += c; }
+        s_red[0] = acc;
+    }
+    __syncthreads();
+    #pragma unroll
+    for (int r = 0; r < kGRounds; ++r) {
+        const bool head = (hmask >> r) & 1u;
+        const uint64_t bal = __ballot(head);
+        if (head) heads[wcnt[r][wv] + (uint32_t)__popcll(bal & lt)] = (uint16_t)(r * kBlock + threadIdx.x);
+    }
+    __syncthreads();
+    const uint32_t H = s_red[0];
+
+    // 3) one probe per lane, compacted in head order into this tile's slots
+    const TileRecView v{(lds_u64*)srec, rec, tile0, cnt};
+    const bool fast = mp.repeat_tol == 0 && mp.enum_tol == 1;
+    const double inv_t = 1.0 / (double)mp.table_size;
+    const uint64_t sb = (uint64_t)blockIdx.x * kSlots;
+    uint32_t nrep = 0, base = 0;
+    for (uint32_t c = 0; c < H; c += kBlock) {
+        const uint32_t j = c + threadIdx.x;
+        bool ok = false;
+        uint32_t gsz = 0, bkt = 0;
+        uint64_t h = 0;
+        if (j < H) {
+            h = tile0 + heads[j];
+            int64_t off = 0;
+            if (abl == 1) {
+                ok = (heads[j] & 7u) == 0u;
+                off = heads[j];
+            } else if (fast) {
+                // the batch (records h .. h + G) from LDS when it lies in the tile, without
+                // branches; a group crossing the tile end reads the global stream
+                const uint32_t q = heads[j];
+                uint64_t xb[MG + 1];
+                if (q + (uint32_t)gt.G < cnt) {
+                    #pragma unroll
+                    for (int k = 0; k <= MG; ++k) {
+                        const uint32_t qk = q + ((uint32_t)k <= (uint32_t)gt.G ? (uint32_t)k : 0u);
+                        xb[k] = ((uint32_t)k <= (uint32_t)gt.G) ? v.lds[qk] : ~0ull;
+                    }
+                } else {
+                    #pragma unroll
+                    for (int k = 0; k <= MG; ++k)
+                        xb[k] = ((uint32_t)k <= (uint32_t)gt.G && h + k < td.bend) ? rec[h + k] : ~0ull;
+                }
+                ok = probe_fast_raw<MG>(xb, gt, mp, L, &off, &gsz);
+                if (gsz > (uint32_t)gt.G) {   // oversize group: rejected; count on for the report
+                    uint64_t i = h + gsz;
+                    const uint32_t k0 = (uint32_t)(xb[0] >> 33);
+                    while (i < td.bend && gsz <= (uint32_t)kRepeatLimit && (uint32_t)v.gkey(i) == k0) { ++gsz; ++i; }
+                }
+            } else {
+                Mhe<MG> P;
+                ok = build_probe<MG, TileRecView>(v, h, td.bend, gt, mp, L, P, &gsz);
+                off = P.offset;
+            }
+            nrep += gsz > (uint32_t)kRepeatLimit;
+            if (ok) bkt = (abl == 2) ? (uint32_t)(off & 0x7FFF) : bucket_of_fast(off, mp.table_size, inv_t);
+        }
+        uint32_t tot;
+        const uint32_t o = blk_excl_scan(ok ? 1u : 0u, s_w, &tot);
+        if (ok) {
+            slot_info[sb + base + o] = h | ((uint64_t)(gsz > 65535u ? 65535u : gsz) << 32);
+            slot_bucket[sb + base + o] = bkt;
+        }
+        base += tot;
+    }
+    if (nrep) atomicAdd(&ctr->repeat_limit, (unsigned long long)nrep);   // rare (repeat-rich input only)
+    if (threadIdx.x == 0) {
+        tile_count[blockIdx.x] = base;
+        tile_count[gridDim.x + 32 + blockIdx.x] = H;   // per-tile group count (summed by the host side)
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void probe_compact_kernel(const uint32_t* __restrict__ tile_count,
                                                                const uint32_t* __restrict__ tile_off,
                                                                const uint64_t* __restrict__ slot_info,
@@ -191,8 +357,19 @@ hipError_t launch_probe_tiles(View v, const SegTile* tiles, uint64_t ntiles, uin
                               const MatchParams& mp, int L, uint32_t* tile_count, uint64_t* slot_info,
                               uint32_t* slot_bucket, void* counters, hipStream_t st) {
     if (ntiles == 0) return hipSuccess;
-    hipLaunchKernelGGL((probe_tile_kernel<MG, View>), dim3((unsigned)ntiles), dim3(kBlock), 0, st, v, tiles, N, gt, mp,
-                       L, tile_count, slot_info, slot_bucket, (DevCounters*)counters);
+    static const int abl = getenv("MUMS_DEV_PROBE_ABL") ? atoi(getenv("MUMS_DEV_PROBE_ABL")) : 0;   // dev knob
+    if constexpr (std::is_same<View, RecView>::value) {
+        if (abl != 3) {
+            hipLaunchKernelGGL((probe_tile_rec_kernel<MG>), dim3((unsigned)ntiles), dim3(kBlock), 0, st, v.rec, tiles,
+                               gt, mp, L, tile_count, slot_info, slot_bucket, (DevCounters*)counters, abl);
+            return hipGetLastError();
+        }
+    }
+    if (false)
+        ;
+    else
+        hipLaunchKernelGGL((probe_tile_kernel<MG, View>), dim3((unsigned)ntiles), dim3(kBlock), 0, st, v, tiles, N, gt,
+                           mp, L, tile_count, slot_info, slot_bucket, (DevCounters*)counters);
     return hipGetLastError();
 }
 

@@ -213,14 +213,13 @@ __device__ __forceinline__ int genome_of_mg(const GenomeTable& gt, uint64_t i) {
 // so G+1 records are fetched as ONE batch of independent loads (no dependent load
 // chain); only groups larger than G fall back to a counting walk (for the
 // MER_REPEAT_LIMIT report).  Same results as build_probe.
+// r[k] = record h + k for k <= G and h + k < end, else {~0, 0, 0} (the batch); v is only
+// read past the batch, by the counting walk of an oversize group.
 template <int MG, typename View>
-__device__ __forceinline__ bool probe_offset_fast(const View& v, uint64_t h, uint64_t end, const GenomeTable& gt,
-                                                  const MatchParams& mp, int L, int64_t* offset, uint32_t* gsize) {
+__device__ __forceinline__ bool probe_offset_batch(const RecFields (&r)[MG + 1], const View& v, uint64_t h,
+                                                   uint64_t end, const GenomeTable& gt, const MatchParams& mp, int L,
+                                                   int64_t* offset, uint32_t* gsize) {
     const uint32_t G = (uint32_t)gt.G;
-    RecFields r[MG + 1];
-    #pragma unroll
-    for (int k = 0; k <= MG; ++k)
-        r[k] = ((uint32_t)k <= G && h + k < end) ? v.get(h + k) : RecFields{~0ull, 0u, 0u};
     const uint64_t k0 = r[0].gk;
     uint32_t cnt = 0;
     bool run = true;
@@ -272,6 +271,86 @@ __device__ __forceinline__ bool probe_offset_fast(const View& v, uint64_t h, uin
         return mp.seq_mask == 0 || match_number == mp.seq_mask;
     }
     return true;
+}
+
+template <int MG, typename View>
+__device__ __forceinline__ bool probe_offset_fast(const View& v, uint64_t h, uint64_t end, const GenomeTable& gt,
+                                                  const MatchParams& mp, int L, int64_t* offset, uint32_t* gsize) {
+    RecFields r[MG + 1];
+    #pragma unroll
+    for (int k = 0; k <= MG; ++k)
+        r[k] = ((uint32_t)k <= (uint32_t)gt.G && h + k < end) ? v.get(h + k) : RecFields{~0ull, 0u, 0u};
+    return probe_offset_batch<MG, View>(r, v, h, end, gt, mp, L, offset, gsize);
+}
+
+// ((offset % T) + T) % T without a 64-bit division: quotient from a double reciprocal
+// (exact to within one for |offset| < 2^52), then one correction step.
+__device__ __forceinline__ uint32_t bucket_of_fast(int64_t offset, uint32_t table_size, double inv_t) {
+    const int64_t T = (int64_t)table_size;
+    const int64_t q = (int64_t)floor((double)offset * inv_t);
+    int64_t r = offset - q * T;
+    r = r < 0 ? r + T : r;
+    r = r >= T ? r - T : r;
+    return (uint32_t)r;
+}
+
+// Default-tolerance probe (repeat_tol 0, enum_tol 1) from the raw packed records
+// x[k] = record h + k (k <= G, inside the bucket; others = ~0), branch-free: the same
+// results as probe_offset_fast.  gsize_batch = equal-key run length inside the batch
+// (the caller walks on when it exceeds G).  Genome and base of each record come from
+// one unrolled compare/select pass over the (32-bit) genome bases.
+template <int MG>
+__device__ __forceinline__ bool probe_fast_raw(const uint64_t (&x)[MG + 1], const GenomeTable& gt,
+                                               const MatchParams& mp, int L, int64_t* offset, uint32_t* gsize) {
+    const uint32_t G = (uint32_t)gt.G;
+    const uint32_t k0 = (uint32_t)(x[0] >> 33);
+    uint32_t cnt = 0;
+    bool run = true;
+    #pragma unroll
+    for (int k = 0; k <= MG; ++k) {
+        run = run && ((uint32_t)(x[k] >> 33) == k0) && (x[k] != ~0ull);
+        cnt += run ? 1u : 0u;
+    }
+    *gsize = cnt;
+    uint32_t mask = 0, gref = 64, sref = 0, pref = 0;
+    bool dup = false;
+    uint32_t gk[MG + 1], sk[MG + 1];
+    #pragma unroll
+    for (int k = 0; k <= MG; ++k) {
+        const uint32_t idx = (uint32_t)x[k];
+        uint32_t g = 0, b = 0;
+        #pragma unroll
+        for (int j = 1; j < MG; ++j) {
+            const uint32_t bj = (uint32_t)gt.base[j];
+            const bool ge = (uint32_t)j < G && idx >= bj;
+            g = ge ? (uint32_t)j : g;
+            b = ge ? bj : b;
+        }
+        gk[k] = g;
+        sk[k] = idx - b + 1u;   // 1-based start in genome g
+        const bool in = (uint32_t)k < cnt;
+        dup = dup || (in && ((mask >> g) & 1u));
+        mask |= in ? (1u << g) : 0u;
+        const bool better = in && g < gref;
+        gref = better ? g : gref;
+        sref = better ? sk[k] : sref;
+        pref = better ? (uint32_t)(x[k] >> 32) & 1u : pref;
+    }
+    int64_t off = 0;
+    #pragma unroll
+    for (int k = 0; k <= MG; ++k) {
+        const bool use = (uint32_t)k < cnt && gk[k] != gref;
+        const int64_t sv = (int64_t)sk[k], sr = (int64_t)sref;
+        const int64_t term = (((uint32_t)(x[k] >> 32) & 1u) != pref) ? (-sv - sr - (int64_t)L) : (sv - sr);
+        off += use ? term : 0;
+    }
+    *offset = off;
+    const bool accept = cnt >= 2 && cnt <= G && !dup;
+    if (mp.masked) {
+        const uint64_t match_number = (uint64_t)(__builtin_bitreverse32(mask) >> (32 - G));
+        return accept && (mp.seq_mask == 0 || match_number == mp.seq_mask);
+    }
+    return accept;
 }
 
 __device__ __forceinline__ uint32_t bucket_of(int64_t offset, uint32_t table_size) {

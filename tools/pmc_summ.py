@@ -5,7 +5,8 @@ for d in sys.argv[1:]:
         agg = collections.defaultdict(float)
         disp = collections.defaultdict(set)
         for r in csv.DictReader(open(f)):
-            k = re.sub(r"\(.*", "", r["Kernel_Name"])[-60:]
+            m = re.findall(r"(\w+)(<[^()]*>)?\(", r["Kernel_Name"].replace("(anonymous namespace)", "anon"))
+            k = (m[0][0] + m[0][1])[:60] if m else r["Kernel_Name"][:60]
             agg[(k, r["Counter_Name"])] += float(r["Counter_Value"])
             disp[k].add(r["Dispatch_Id"])
         for (k, c), v in sorted(agg.items()):
