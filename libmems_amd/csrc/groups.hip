@@ -7,8 +7,10 @@
 // CalculateOffset MatchHashEntry.cpp:141-160) whose hash bucket is
 // ((offset % T) + T) % T (MemHash.cpp:213).
 //
-// Here the merged stream is the radix-sorted (ckey, index) array; a group is a
-// run of equal ckey>>1.  One workgroup per 4096-record tile:
+// Here the merged stream is the radix-sorted record array; a group is a run of
+// equal ckey>>1.  One workgroup per 4096-record tile (probe_tile_rec_kernel for
+// the packed records: the tile is staged in LDS and the default-tolerance probe is
+// branch-free; probe_tile_kernel for the (key, index) pair path):
 //   1. lane-contiguous head detection (16 rounds), heads compacted into an LDS
 //      list in stream order (ballot + per-(round, wave) counts);
 //   2. every lane builds the probe of one head (no lane idles on non-heads);
@@ -16,7 +18,6 @@
 //      (a group needs >= 2 records, so <= 2048 probes per tile).
 // A second kernel concatenates the tiles' slots using the scanned tile counts, so
 // the probes end up in ascending key order = the reference's AddHashEntry order.
-#include <cstdlib>
 #include <type_traits>
 
 #include "match_device.h"
@@ -179,7 +180,7 @@ __global__ __launch_bounds__(kBlock) void probe_tile_rec_kernel(const uint64_t* 
                                                                 uint32_t* __restrict__ tile_count,
                                                                 uint64_t* __restrict__ slot_info,
                                                                 uint32_t* __restrict__ slot_bucket,
-                                                                DevCounters* __restrict__ ctr, int abl) {
+                                                                DevCounters* __restrict__ ctr) {
     __shared__ uint64_t srec[kGTile];
     __shared__ uint16_t heads[kGTile];
     __shared__ uint32_t wcnt[kGRounds][kBlock / 64];
@@ -263,10 +264,7 @@ __global__ __launch_bounds__(kBlock) void probe_tile_rec_kernel(const uint64_t* 
         if (j < H) {
             h = tile0 + heads[j];
             int64_t off = 0;
-            if (abl == 1) {
-                ok = (heads[j] & 7u) == 0u;
-                off = heads[j];
-            } else if (fast) {
+            if (fast) {
                 // the batch (records h .. h + G) from LDS when it lies in the tile, without
                 // branches; a group crossing the tile end reads the global stream
                 const uint32_t q = heads[j];
@@ -294,7 +292,7 @@ __global__ __launch_bounds__(kBlock) void probe_tile_rec_kernel(const uint64_t* 
                 off = P.offset;
             }
             nrep += gsz > (uint32_t)kRepeatLimit;
-            if (ok) bkt = (abl == 2) ? (uint32_t)(off & 0x7FFF) : bucket_of_fast(off, mp.table_size, inv_t);
+            if (ok) bkt = bucket_of_fast(off, mp.table_size, inv_t);
         }
         uint32_t tot;
         const uint32_t o = blk_excl_scan(ok ? 1u : 0u, s_w, &tot);
@@ -357,16 +355,9 @@ hipError_t launch_probe_tiles(View v, const SegTile* tiles, uint64_t ntiles, uin
                               const MatchParams& mp, int L, uint32_t* tile_count, uint64_t* slot_info,
                               uint32_t* slot_bucket, void* counters, hipStream_t st) {
     if (ntiles == 0) return hipSuccess;
-    static const int abl = getenv("MUMS_DEV_PROBE_ABL") ? atoi(getenv("MUMS_DEV_PROBE_ABL")) : 0;   // dev knob
-    if constexpr (std::is_same<View, RecView>::value) {
-        if (abl != 3) {
-            hipLaunchKernelGGL((probe_tile_rec_kernel<MG>), dim3((unsigned)ntiles), dim3(kBlock), 0, st, v.rec, tiles,
-                               gt, mp, L, tile_count, slot_info, slot_bucket, (DevCounters*)counters, abl);
-            return hipGetLastError();
-        }
-    }
-    if (false)
-        ;
+    if constexpr (std::is_same<View, RecView>::value)
+        hipLaunchKernelGGL((probe_tile_rec_kernel<MG>), dim3((unsigned)ntiles), dim3(kBlock), 0, st, v.rec, tiles, gt,
+                           mp, L, tile_count, slot_info, slot_bucket, (DevCounters*)counters);
     else
         hipLaunchKernelGGL((probe_tile_kernel<MG, View>), dim3((unsigned)ntiles), dim3(kBlock), 0, st, v, tiles, N, gt,
                            mp, L, tile_count, slot_info, slot_bucket, (DevCounters*)counters);

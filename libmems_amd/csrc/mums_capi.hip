@@ -150,6 +150,8 @@ SeedSpec make_seed_spec(uint64_t pattern, int L, int w) {
     for (int i = 0; i < ss.nruns; ++i) {
         cum += ss.run_len[i];
         ss.run_dst[i] = 2 * (w - cum);
+        ss.run_sh[i] = 64 - 2 * (ss.run_start[i] + ss.run_len[i]) - ss.run_dst[i];
+        ss.run_mask[i] = ((ss.run_len[i] >= 32) ? ~0ull : ((1ull << (2 * ss.run_len[i])) - 1)) << ss.run_dst[i];
     }
     return ss;
 }

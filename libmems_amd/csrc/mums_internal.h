@@ -34,6 +34,8 @@ constexpr int kLocalIPT = 16;        // records per lane of the LDS-resident loc
 constexpr int kMaxMsdBits = 11;      // packed path: 2w+1 <= 32 + 11
 
 // Per-run constants shared by the kernels (passed by value).
+constexpr int kMaxSeedRuns = 16;     // runs of care positions in a seed of length <= 32
+
 struct SeedSpec {
     uint64_t pattern;
     int L;                  // seed length   (getSeedLength, SeedMasks.h:335)
@@ -42,6 +44,10 @@ struct SeedSpec {
     int run_start[32];      // first base offset of each run (0 = first base)
     int run_len[32];        // bases in the run
     int run_dst[32];        // bit shift of the run inside the 2w-bit seed value
+    // device form: run r of the 64-bit window lands at its seed bits as
+    // ((sh >= 0 ? mer >> sh : mer << -sh) & mask); sh = 64 - 2(start + len) - dst
+    int run_sh[kMaxSeedRuns];
+    uint64_t run_mask[kMaxSeedRuns];
 };
 
 struct GenomeTable {

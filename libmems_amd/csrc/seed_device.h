@@ -21,16 +21,79 @@ __device__ __forceinline__ uint64_t revcomp2w(uint64_t v, int w) {
 // compact canonical key (v << 1) | parity from a 64-bit window whose first base sits in
 // bits 63-62 (GetMer, :321-342): v = min(forward seed, reverse-complement seed)
 // (GetSeedMer :726-762 + GetDnaSeedMer :764-769); parity = 1 iff the RC was chosen.
-__device__ __forceinline__ uint64_t ckey_from_mer(uint64_t mer, const SeedSpec& ss) {
-    uint64_t v = 0;
-    for (int r = 0; r < ss.nruns; ++r) {
-        const int s = ss.run_start[r], l = ss.run_len[r];
-        v |= ((mer >> (64 - 2 * (s + l))) & ((1ull << (2 * l)) - 1)) << ss.run_dst[r];
-    }
-    const uint64_t rc = revcomp2w(v, ss.w);
+__device__ __forceinline__ uint64_t ckey_finish(uint64_t v, int w) {
+    const uint64_t rc = revcomp2w(v, w);
     const uint64_t par = rc < v ? 1ull : 0ull;
     return ((par ? rc : v) << 1) | par;
 }
+
+__device__ __forceinline__ uint64_t ckey_from_mer(uint64_t mer, const SeedSpec& ss) {
+    uint64_t v = 0;
+    for (int r = 0; r < ss.nruns; ++r) {
+        const int sh = ss.run_sh[r];
+        v |= (sh >= 0 ? (mer >> sh) : (mer << -sh)) & ss.run_mask[r];
+    }
+    return ckey_finish(v, ss.w);
+}
+
+// Compile-time seed patterns (the BASELINE seeds): the run table is a constant, so the
+// extraction unrolls to one shift + mask + or per run with immediate operands.
+struct SeedRuns {
+    int n = 0, L = 0, w = 0;
+    int sh[kMaxSeedRuns] = {};
+    uint64_t mask[kMaxSeedRuns] = {};
+};
+
+// same derivation as the host's make_seed_spec (mums_capi.hip)
+constexpr SeedRuns seed_runs(uint64_t pat) {
+    SeedRuns R{};
+    int lo = 0, hi = 63;
+    while (lo < 64 && !((pat >> lo) & 1)) ++lo;
+    while (hi >= 0 && !((pat >> hi) & 1)) --hi;
+    R.L = hi - lo + 1;
+    int start[kMaxSeedRuns] = {}, len[kMaxSeedRuns] = {};
+    int r = -1;
+    bool prev = false;
+    for (int k = 0; k < R.L; ++k) {
+        const bool care = (pat >> (R.L - 1 - k)) & 1;
+        if (care) {
+            if (!prev) { ++r; start[r] = k; len[r] = 0; }
+            ++len[r];
+            ++R.w;
+        }
+        prev = care;
+    }
+    R.n = r + 1;
+    int cum = 0;
+    for (int i = 0; i < R.n; ++i) {
+        cum += len[i];
+        const int dst = 2 * (R.w - cum);
+        R.sh[i] = 64 - 2 * (start[i] + len[i]) - dst;
+        R.mask[i] = ((len[i] >= 32) ? ~0ull : ((1ull << (2 * len[i])) - 1)) << dst;
+    }
+    return R;
+}
+
+template <uint64_t PAT>
+__device__ __forceinline__ uint64_t ckey_static(uint64_t mer) {
+    constexpr SeedRuns R = seed_runs(PAT);
+    static_assert(R.n > 0 && R.n <= kMaxSeedRuns, "bad static seed");
+    uint64_t v = 0;
+    #pragma unroll
+    for (int r = 0; r < R.n; ++r) v |= (R.sh[r] >= 0 ? (mer >> R.sh[r]) : (mer << -R.sh[r])) & R.mask[r];
+    return ckey_finish(v, R.w);
+}
+
+// key of a 64-bit window: static pattern PAT when non-zero, else the run table of ss
+template <uint64_t PAT>
+__device__ __forceinline__ uint64_t ckey_of(uint64_t mer, const SeedSpec& ss) {
+    if constexpr (PAT != 0) return ckey_static<PAT>(mer);
+    else return ckey_from_mer(mer, ss);
+}
+
+// the patterns with compiled-in run tables (getSeed(15), getSeed(19): SeedMasks.h)
+constexpr uint64_t kSeedW15 = 0x7ac9afull;
+constexpr uint64_t kSeedW19 = 0x7b974efull;
 
 __device__ __forceinline__ uint64_t window_at(const uint32_t* __restrict__ W, uint64_t p) {
     const uint64_t wi = p >> 4;

@@ -48,7 +48,7 @@ __device__ __forceinline__ int tile_genome(const GenomeTable& gt, uint32_t t) {
     return g;
 }
 
-template <int kMode, typename K>
+template <int kMode, typename K, uint64_t PAT = 0>
 __global__ __launch_bounds__(kBlock) void seed_pack_kernel(SeedSpec ss, GenomeTable gt, AsciiPtrs ap,
                                                            uint32_t* __restrict__ packed, K* __restrict__ ckey,
                                                            int msd_bits, uint32_t* __restrict__ hist, uint32_t T,
@@ -125,7 +125,7 @@ __global__ __launch_bounds__(kBlock) void seed_pack_kernel(SeedSpec ss, GenomeTa
         const int wi = q >> 4, sh = 2 * (q & 15);
         const uint64_t hi = ((uint64_t)words[wi] << 32) | words[wi + 1];
         const uint64_t lo = words[wi + 2];
-        const uint64_t kv = ckey_from_mer((hi << sh) | ((lo << sh) >> 32), ss);
+        const uint64_t kv = ckey_of<PAT>((hi << sh) | ((lo << sh) >> 32), ss);
         if (kMode == 0) ckey[base + p] = (K)kv;
         else if (nb > 1) atomicAdd(&bh[(uint32_t)(kv >> klow)], 1u);
     }
@@ -135,7 +135,7 @@ __global__ __launch_bounds__(kBlock) void seed_pack_kernel(SeedSpec ss, GenomeTa
     }
 }
 
-template <int kMaxDig>
+template <int kMaxDig, uint64_t PAT = 0>
 __global__ __launch_bounds__(kBlock) void seed_scatter_kernel(SeedSpec ss, GenomeTable gt,
                                                               const uint32_t* __restrict__ packed, int msd_bits,
                                                               const uint32_t* __restrict__ hist, uint32_t T,
@@ -178,7 +178,7 @@ __global__ __launch_bounds__(kBlock) void seed_scatter_kernel(SeedSpec ss, Genom
         const int wi = q >> 4, sh = 2 * (q & 15);
         const uint64_t hi = ((uint64_t)words[wi] << 32) | words[wi + 1];
         const uint64_t lo = words[wi + 2];
-        const uint64_t kv = ckey_from_mer((hi << sh) | ((lo << sh) >> 32), ss);
+        const uint64_t kv = ckey_of<PAT>((hi << sh) | ((lo << sh) >> 32), ss);
         const uint32_t d = valid ? (uint32_t)(kv >> klow) : 0u;
         r_rec[r] = ((kv & lmask) << 32) | (base + p);
         r_dig[r] = d;
@@ -248,6 +248,7 @@ __global__ __launch_bounds__(kBlock) void seed_scatter_kernel(SeedSpec ss, Genom
 }
 
 // B == 0: one bucket, records land at their global index
+template <uint64_t PAT = 0>
 __global__ __launch_bounds__(kBlock) void seed_scatter_flat_kernel(SeedSpec ss, GenomeTable gt,
                                                                    const uint32_t* __restrict__ packed,
                                                                    uint64_t* __restrict__ rec) {
@@ -274,7 +275,7 @@ __global__ __launch_bounds__(kBlock) void seed_scatter_flat_kernel(SeedSpec ss, 
         const int wi = q >> 4, sh = 2 * (q & 15);
         const uint64_t hi = ((uint64_t)words[wi] << 32) | words[wi + 1];
         const uint64_t lo = words[wi + 2];
-        const uint64_t kv = ckey_from_mer((hi << sh) | ((lo << sh) >> 32), ss);
+        const uint64_t kv = ckey_of<PAT>((hi << sh) | ((lo << sh) >> 32), ss);
         rec[base + p] = (kv << 32) | (base + p);
     }
 }
@@ -303,8 +304,13 @@ hipError_t launch_seed_pack(const SeedSpec& ss, const GenomeTable& gt, const cha
             hipLaunchKernelGGL((seed_pack_kernel<0, uint32_t>), dim3(ntiles), dim3(kBlock), 0, st, ss, gt, ap,
                                d_packed, (uint32_t*)d_ckey, 0, d_hist, ntiles, d_err);
     } else {
-        hipLaunchKernelGGL((seed_pack_kernel<1, uint64_t>), dim3(ntiles), dim3(kBlock), 0, st, ss, gt, ap, d_packed,
-                           (uint64_t*)nullptr, msd_bits, d_hist, ntiles, d_err);
+#define MUMS_PACK1(PAT)                                                                                  \
+    hipLaunchKernelGGL((seed_pack_kernel<1, uint64_t, PAT>), dim3(ntiles), dim3(kBlock), 0, st, ss, gt, ap, d_packed, \
+                       (uint64_t*)nullptr, msd_bits, d_hist, ntiles, d_err)
+        if (ss.pattern == kSeedW19) MUMS_PACK1(kSeedW19);
+        else if (ss.pattern == kSeedW15) MUMS_PACK1(kSeedW15);
+        else MUMS_PACK1(0);
+#undef MUMS_PACK1
     }
     return hipGetLastError();
 }
@@ -312,14 +318,27 @@ hipError_t launch_seed_pack(const SeedSpec& ss, const GenomeTable& gt, const cha
 hipError_t launch_seed_scatter(const SeedSpec& ss, const GenomeTable& gt, const uint32_t* d_packed, int msd_bits,
                                const uint32_t* d_hist_scanned, uint32_t ntiles, uint64_t* d_rec, hipStream_t st) {
     if (ntiles == 0) return hipSuccess;
-    if (msd_bits == 0)
-        hipLaunchKernelGGL(seed_scatter_flat_kernel, dim3(ntiles), dim3(kBlock), 0, st, ss, gt, d_packed, d_rec);
-    else if (msd_bits <= 8)
-        hipLaunchKernelGGL(seed_scatter_kernel<256>, dim3(ntiles), dim3(kBlock), 0, st, ss, gt, d_packed, msd_bits,
-                           d_hist_scanned, ntiles, d_rec);
-    else
-        hipLaunchKernelGGL(seed_scatter_kernel<(1 << kMaxMsdBits)>, dim3(ntiles), dim3(kBlock), 0, st, ss, gt,
+    const uint64_t pat = (ss.pattern == kSeedW19 || ss.pattern == kSeedW15) ? ss.pattern : 0;
+#define MUMS_SCATTER(PAT)                                                                                         \
+    do {                                                                                                          \
+        if (msd_bits == 0)                                                                                        \
+            hipLaunchKernelGGL(seed_scatter_flat_kernel<PAT>, dim3(ntiles), dim3(kBlock), 0, st, ss, gt, d_packed, \
+                               d_rec);                                                                            \
+        else                                                                                                      \
+            hipLaunchKernelGGL((seed_scatter_kernel<256, PAT>), dim3(ntiles), dim3(kBlock), 0, st, ss, gt,         \
+                               d_packed, msd_bits, d_hist_scanned, ntiles, d_rec);                                \
+    } while (0)
+    if (msd_bits > 8) {
+        hipLaunchKernelGGL((seed_scatter_kernel<(1 << kMaxMsdBits), 0>), dim3(ntiles), dim3(kBlock), 0, st, ss, gt,
                            d_packed, msd_bits, d_hist_scanned, ntiles, d_rec);
+    } else if (pat == kSeedW19) {
+        MUMS_SCATTER(kSeedW19);
+    } else if (pat == kSeedW15) {
+        MUMS_SCATTER(kSeedW15);
+    } else {
+        MUMS_SCATTER(0);
+    }
+#undef MUMS_SCATTER
     return hipGetLastError();
 }
 
