@@ -96,7 +96,7 @@ def run_mums(device: int, dev: torch.device):
         st = mh.stats()
     return {"mums_per_s": st["mem_count"] / dt, "matches": st["mem_count"], "ms": dt * 1e3,
             "workload": "4 x 10 Mbp related p=0.01, w15 (BASELINE config 2 shape), full FindMatches",
-            "phase_ms": {k: round(st[k], 3) for k in ("ms_keys", "ms_sort", "ms_groups", "ms_buckets", "ms_replay",
+            "phase_ms": {k: round(st[k], 3) for k in ("ms_keys", "ms_sort", "ms_groups", "ms_buckets", "ms_chains", "ms_replay",
                                                         "ms_output")}}
 
 

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MUMS_ABI_VERSION 2
+#define MUMS_ABI_VERSION 3
 
 enum mums_status {
     MUMS_OK = 0,
@@ -69,6 +69,8 @@ typedef struct mums_stats {
     uint64_t dominant_bytes;
     uint64_t key_bytes;         /* 4 (2w+1 <= 32) or 8 */
     uint64_t sort_passes;
+    double   ms_chains;         /* seed-chain labelling before the replay (ExtendMatch results)        */
+    uint64_t chains;            /* seed chains among the probes                                        */
 } mums_stats;
 
 /* MemHash::MemHash (MemHash.cpp:33-49); device = HIP ordinal. */

@@ -74,6 +74,8 @@ class _Stats(ctypes.Structure):
         ("dominant_bytes", ctypes.c_uint64),
         ("key_bytes", ctypes.c_uint64),
         ("sort_passes", ctypes.c_uint64),
+        ("ms_chains", ctypes.c_double),
+        ("chains", ctypes.c_uint64),
     ]
 
 

@@ -53,7 +53,9 @@ struct GenomeIn {
     bool owned;
 };
 
-enum { EV_START, EV_KEYS, EV_SORT, EV_GROUPS, EV_BUCKETS, EV_REPLAY, EV_OUTPUT, EV_COUNT };
+enum { EV_START, EV_KEYS, EV_SORT, EV_GROUPS, EV_BUCKETS, EV_CHAINS, EV_REPLAY, EV_OUTPUT, EV_COUNT };
+
+constexpr uint32_t kReplayLdsIds = 8192;    // 16-B slots: 128 KiB of LDS per replay workgroup
 
 }  // namespace
 
@@ -70,6 +72,7 @@ struct mums_ctx {
 
     DevBuf packed, recA, recB, hist, tiles, ckey, kA, kB, vA, vB, tmp, partials, counters;
     DevBuf bstart, bend, tsize, obase, pool, tbl, out_len, out_s, pbuf, keybuf, mstart;
+    DevBuf chain_tmp, chain_of, radix_tmp, spill, summ, dbgbuf;
     bool use_onesweep = true;
     hipEvent_t ev[EV_COUNT] = {};
     bool profiling = false;
@@ -190,20 +193,54 @@ int groups_dispatch(mums_ctx* ctx, View v, const SegTile* tiles, uint64_t ntiles
     return run_groups<32, View>(ctx, v, tiles, ntiles, mp, pi, pb, si, sb, st);
 }
 
+// chain labelling (chains.hip) then the per-bucket replay (replay.hip)
+template <int MG, typename View>
+int replay_run(mums_ctx* ctx, View v, const MatchParams& mp, hipStream_t st) {
+    DevCounters* dc = ctx->counters.as<DevCounters>();
+    const uint64_t P = ctx->P;
+    HIPCHK((launch_chains<MG, View>(v, ctx->probe_info, P, ctx->gt, mp, ctx->ss, ctx->packed.as<uint32_t>(),
+                                    ctx->chain_tmp.p, ctx->tmp.p, ctx->radix_tmp.p, ctx->chain_of.as<uint32_t>(),
+                                    ctx->pool.as<int64_t>(), &dc->nchains, st)));
+    HIPCHK(hipEventRecord(ctx->ev[EV_CHAINS], st));
+    HIPCHK(hipMemcpyAsync(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    uint64_t* dbg = nullptr;
+    if (getenv("MUMS_DEV_REPLAY_DEBUG")) {
+        HIPCHK(ctx->dbgbuf.ensure((size_t)ctx->table_size * 64));
+        HIPCHK(hipMemsetAsync(ctx->dbgbuf.p, 0, (size_t)ctx->table_size * 64, st));
+        dbg = ctx->dbgbuf.as<uint64_t>();
+    }
+    // the fullest bucket's vector in LDS when it fits (it holds <= its probes)
+    const uint32_t lds_cap = std::max<uint32_t>(64, std::min<uint32_t>(ctx->hc.max_bucket, kReplayLdsIds));
+    HIPCHK((launch_replay<MG, View>(v, ctx->gt, mp, ctx->L, ctx->probe_info, ctx->sorted_ids, P,
+                                    ctx->bstart.as<uint32_t>(), ctx->bend.as<uint32_t>(), ctx->tbl.as<uint32_t>(),
+                                    ctx->spill.p, ctx->summ.p, ctx->pool.as<int64_t>(), ctx->chain_of.as<uint32_t>(),
+                                    lds_cap,
+                                    ctx->tsize.as<uint32_t>(), ctx->counters.p, dbg, st)));
+    if (dbg) {   // development instrumentation: the slowest buckets of the replay
+        std::vector<uint64_t> h((size_t)ctx->table_size * 8);
+        HIPCHK(hipMemcpyAsync(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        std::vector<uint32_t> idx(ctx->table_size);
+        for (uint32_t i = 0; i < ctx->table_size; ++i) idx[i] = i;
+        std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return h[a * 8 + 7] > h[b * 8 + 7]; });
+        for (int k = 0; k < 5; ++k) {
+            const uint64_t* d = &h[(size_t)idx[k] * 8];
+            fprintf(stderr, "replay bucket %u: probes %lu entries %lu windows %lu rounds %lu | us win %.1f round %.1f "
+                    "ins %.1f total %.1f\n", idx[k], (unsigned long)d[0], (unsigned long)d[1], (unsigned long)d[2],
+                    (unsigned long)d[3], d[4] / 100.0, d[5] / 100.0, d[6] / 100.0, d[7] / 100.0);
+        }
+    }
+    return MUMS_OK;
+}
+
 template <typename View>
 int replay_dispatch(mums_ctx* ctx, View v, const MatchParams& mp, hipStream_t st) {
     const int G = ctx->gt.G;
-#define MUMS_REPLAY_CALL(MG)                                                                                        \
-    HIPCHK((launch_replay<MG, View>(v, ctx->N, ctx->gt, mp, ctx->ss, ctx->probe_info, ctx->sorted_ids,              \
-                                    ctx->bstart.as<uint32_t>(), ctx->bend.as<uint32_t>(), ctx->tbl.as<uint32_t>(),  \
-                                    ctx->pool.as<int64_t>(), ctx->packed.as<uint32_t>(), ctx->tsize.as<uint32_t>(), \
-                                    ctx->counters.p, st)))
-    if (G <= 4) MUMS_REPLAY_CALL(4);
-    else if (G <= 8) MUMS_REPLAY_CALL(8);
-    else if (G <= 16) MUMS_REPLAY_CALL(16);
-    else MUMS_REPLAY_CALL(32);
-#undef MUMS_REPLAY_CALL
-    return MUMS_OK;
+    if (G <= 4) return replay_run<4, View>(ctx, v, mp, st);
+    if (G <= 8) return replay_run<8, View>(ctx, v, mp, st);
+    if (G <= 16) return replay_run<16, View>(ctx, v, mp, st);
+    return replay_run<32, View>(ctx, v, mp, st);
 }
 
 // probe / slot arrays of the groups stage (one grow-only device buffer)
@@ -365,7 +402,9 @@ void fill_stats(mums_ctx* ctx, uint64_t n) {
     if (ctx->stage_done >= MUMS_STAGE_ALL) {
         s.mem_count = ctx->hc.entries;
         s.collision_count = ctx->hc.collisions;
-        s.ms_replay = el(EV_BUCKETS, EV_REPLAY);
+        s.ms_chains = el(EV_BUCKETS, EV_CHAINS);
+        s.ms_replay = el(EV_CHAINS, EV_REPLAY);
+        s.chains = ctx->hc.nchains;
         s.ms_output = el(EV_REPLAY, EV_OUTPUT);
         s.ms_total = el(EV_START, EV_OUTPUT);
     } else {
@@ -477,11 +516,19 @@ int run_pipeline(mums_ctx* ctx, int stage) {
         HIPCHK(ctx->obase.ensure((size_t)Tb * 4 + 64));
         HIPCHK(ctx->pool.ensure((ctx->P + 1) * (size_t)(G + 2) * 8));
         HIPCHK(ctx->tbl.ensure((ctx->P + 1) * 4));
+        HIPCHK(ctx->chain_of.ensure((ctx->P + 1) * 4));
+        HIPCHK(ctx->spill.ensure((ctx->P + 1) * 16));
+        HIPCHK(ctx->summ.ensure((ctx->P + 1) * 16));
+        HIPCHK(ctx->chain_tmp.ensure(chain_tmp_bytes(ctx->P + 1)));
+        HIPCHK(ctx->radix_tmp.ensure(radix_tmp_bytes(ctx->P + 1)));
+        HIPCHK(ctx->tmp.ensure(std::max(scan_tmp_bytes(ctx->P + 1), scan_tmp_bytes(Tb))));
+        HIPCHK(hipMemsetAsync(&dc->max_bucket, 0, 4, st));
         HIPCHK(hipMemsetAsync(ctx->bstart.p, 0, (size_t)Tb * 4, st));
         HIPCHK(hipMemsetAsync(ctx->bend.p, 0, (size_t)Tb * 4, st));
         HIPCHK(hipMemsetAsync(ctx->tsize.p, 0, (size_t)Tb * 4, st));
         HIPCHK(launch_bucket_ranges(ctx->sorted_buckets, ctx->P, ctx->bstart.as<uint32_t>(), ctx->bend.as<uint32_t>(),
-                                    st));
+                                    &dc->max_bucket, st));
+        if (ctx->P == 0) HIPCHK(hipEventRecord(ctx->ev[EV_CHAINS], st));
         if (ctx->P > 0) {
             if (ctx->packed_path) rc = replay_dispatch<RecView>(ctx, RecView{ctx->sorted_rec}, mp, st);
             else if (ctx->key64)

@@ -78,6 +78,8 @@ struct DevCounters {
     uint32_t nprobes;                 // accepted probes (scan total)
     uint32_t nmatches;                // output matches (scan total)
     uint32_t ngroups;                 // distinct masked keys (scan total of per-tile counts)
+    uint32_t nchains;                 // seed chains among the probes (chains.hip)
+    uint32_t max_bucket;              // probes in the fullest hash bucket
     uint32_t pad;
 };
 
@@ -187,12 +189,19 @@ hipError_t launch_probe_compact(uint64_t ntiles, const uint32_t* tile_count, con
 hipError_t launch_flat_tiles(uint64_t N, SegTile* d_tiles, hipStream_t st);
 
 // replay.hip
-hipError_t launch_bucket_ranges(const uint32_t* sb, uint64_t P, uint32_t* bstart, uint32_t* bend, hipStream_t st);
+hipError_t launch_bucket_ranges(const uint32_t* sb, uint64_t P, uint32_t* bstart, uint32_t* bend, uint32_t* d_max,
+                                hipStream_t st);
 template <int MG, typename View>
-hipError_t launch_replay(View v, uint64_t N, const GenomeTable& gt, const MatchParams& mp, const SeedSpec& ss,
-                         const uint64_t* probe_info, const uint32_t* sorted_ids, const uint32_t* bstart,
-                         const uint32_t* bend, uint32_t* tbl, int64_t* pool, const uint32_t* packed,
-                         uint32_t* tsize, void* ctr, hipStream_t st);
+hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, int L, const uint64_t* probe_info,
+                         const uint32_t* sorted_ids, uint64_t P, const uint32_t* bstart, const uint32_t* bend,
+                         uint32_t* tbl, void* spill, void* summ, const int64_t* pool, const uint32_t* chain_of,
+                         uint32_t lds_cap, uint32_t* tsize, void* ctr, uint64_t* dbg, hipStream_t st);
+// chains.hip: chain labelling of the probes (key order) before the replay
+size_t chain_tmp_bytes(uint64_t P);
+template <int MG, typename View>
+hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const GenomeTable& gt, const MatchParams& mp,
+                         const SeedSpec& ss, const uint32_t* packed, void* d_chain_tmp, void* d_scan_tmp,
+                         void* d_radix_tmp, uint32_t* chain_of, int64_t* pool, uint32_t* d_nchains, hipStream_t st);
 hipError_t launch_emit(const uint32_t* tsize, const uint32_t* obase, const uint32_t* bstart, const uint32_t* tbl,
                        const int64_t* pool, int G, uint32_t table_size, uint64_t* out_len, int64_t* out_s,
                        hipStream_t st);

@@ -1,4 +1,4 @@
-// replay.hip -- per-bucket AddHashEntry replay + seed-chain extension (rows A10-A12).
+// replay.hip -- per-bucket AddHashEntry replay (rows A10-A12).
 //
 // Reference: MemHash::AddHashEntry (MemHash.cpp:209-251) keeps every hash
 // bucket as a vector sorted by MheCompare (MatchHashEntry.h:121-143); each probe
@@ -10,15 +10,16 @@
 // binary-search probe sequence matters; it is replayed here
 // with the libstdc++ __lower_bound recurrence.
 //
-// MI355X mapping: one 256-lane workgroup per hash bucket.  Buckets are
-// independent; inside a bucket the workgroup evaluates up to 256 consecutive
-// probes against the current table in parallel (one lower_bound per lane),
-// takes the first non-colliding one (a workgroup ballot), extends it
-// cooperatively and inserts it; everything before it is final.  Extension uses
-// the fixpoint of ExtendMatch's L-jump / single-step / restart loop: the
-// maximal chain of seed hits with gaps <= L through the probe,
-// found with 256 speculative L-jumps per round and an L-wide fine step; a hit
-// re-derives the components' seed keys from the resident 2-bit packed genomes.
+// MI355X mapping: one workgroup (1024 / 512 / 256 lanes for G <= 4 / 8 / more) per hash bucket.
+// Extensions are not computed here: chains.hip has labelled every probe with its
+// chain, whose extended entry sits in the chain pool, so an insert is a pool id.
+// The bucket's vector lives in LDS as 16-B slots {id, presence mask, first-genome
+// start, length} (spilling to a global slice when it outgrows the LDS capacity), so
+// the binary search reads LDS and touches an entry in HBM only where a span could
+// contain the probe.  A window of up to RB consecutive probes stays in the lanes'
+// registers; per round every unconsumed lane runs its lower_bound against the
+// current vector, the workgroup takes the first non-colliding probe (ballot),
+// inserts its chain entry with a one-barrier LDS shift and goes on after it.
 #include "match_device.h"
 #include "seed_device.h"
 
@@ -26,92 +27,195 @@ namespace mums {
 
 namespace {
 
-struct ExtComp {
-    int64_t s;       // start (signed, 1-based)
-    uint64_t woff;   // word offset of the genome in the packed array
-};
-
+template <int RB>
 __device__ __forceinline__ int block_first_true(bool pred, int* red) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint64_t b = __ballot(pred);
-    if (lane == 0) red[wv] = b ? wv * 64 + (__ffsll((long long)b) - 1) : kBlock;
+    if (lane == 0) red[wv] = b ? wv * 64 + (__ffsll((long long)b) - 1) : RB;
     __syncthreads();
     int r = red[0];
     #pragma unroll
-    for (int w = 1; w < kBlock / 64; ++w) r = min(r, red[w]);
+    for (int w = 1; w < RB / 64; ++w) r = min(r, red[w]);
     __syncthreads();
     return r;
 }
 
-__device__ __forceinline__ int block_last_true(bool pred, int* red) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t b = __ballot(pred);
-    if (lane == 0) red[wv] = b ? wv * 64 + 63 - __clzll((long long)b) : -1;
-    __syncthreads();
-    int r = red[0];
-    #pragma unroll
-    for (int w = 1; w < kBlock / 64; ++w) r = max(r, red[w]);
-    __syncthreads();
-    return r;
-}
-
-// seed hit at alignment column c (MatchFinder.h:265-293): every component's
-// masked key and strand-relative parity agree, all windows inside the sequences.
-__device__ __forceinline__ bool hit_at(int64_t c, const ExtComp* comps, int nc, int64_t clo, int64_t chi,
-                                       const uint32_t* __restrict__ packed, const SeedSpec& ss) {
-    if (c < clo || c > chi) return false;
-    uint64_t v0 = 0;
-    uint32_t o0 = 0;
-    bool ok = true;
-    for (int j = 0; j < nc && ok; ++j) {
-        const int64_t s = comps[j].s;
-        const int64_t p = s > 0 ? s - 1 + c : -s - 1 - c;
-        const uint64_t k = ckey_at(packed + comps[j].woff, (uint64_t)p, ss);
-        const uint64_t v = k >> 1;
-        const uint32_t o = s > 0 ? (uint32_t)((k & 1) ^ 1) : (uint32_t)(k & 1);
-        if (j == 0) { v0 = v; o0 = o; }
-        else ok = (v == v0) && (o == o0);
+// A vector slot: {pool id, presence mask (bit g = genome g), first-genome start, length}.
+// The slot decides MheCompare (MatchHashEntry.h:121-143) without the entry unless one
+// first-genome span can contain the other:
+//   * X is V's own chain entry (same pool id): X contains V -> equivalent
+//   * masks differ: FirstStart index, then the first genome present in only one
+//   * same mask, V starts before X: only V can contain X (needs X's span inside V's)
+//   * same mask, V starts after X : only X can contain V (needs V's span inside X's)
+// with no containment possible, strict_start_lessthan_ptr is decided by the first
+// genome's (positive) start.  Returns 0 / 1 (X < V false / true), 2 = needs the entries.
+__device__ __forceinline__ int slot_cmp(const uint4 X, uint32_t vmask, int64_t vs, int64_t vl, uint32_t vcid) {
+    if (X.x == vcid) return 0;
+    if (X.y != vmask) {
+        const int fa = __builtin_ctz(X.y), fb = __builtin_ctz(vmask);
+        if (fa != fb) return fa > fb ? 1 : 0;
+        return ((X.y >> __builtin_ctz(X.y ^ vmask)) & 1u) == 0u ? 1 : 0;
     }
-    return ok;
+    const int64_t xs = (int64_t)X.z, xl = (int64_t)X.w;
+    if (vs < xs) return (xs + xl > vs + vl) ? 0 : 2;
+    if (vs > xs) return (vs + vl > xs + xl) ? 1 : 2;
+    return 2;
 }
 
-// rightmost (dir=+1) / leftmost (dir=-1) column of the hit chain through column 0
-__device__ int64_t chain_end(int dir, int L, const ExtComp* comps, int nc, int64_t clo, int64_t chi,
-                             const uint32_t* __restrict__ packed, const SeedSpec& ss, int* red) {
-    const int tid = threadIdx.x;
-    int64_t cur = 0;
-    for (;;) {
-        for (;;) {  // ExtendMatch directions 0/1: jumps of L while the seed at the new end matches
-            const bool h = hit_at(cur + dir * (int64_t)(tid + 1) * L, comps, nc, clo, chi, packed, ss);
-            const int miss = block_first_true(!h, red);
-            if (miss == kBlock) { cur += dir * (int64_t)kBlock * L; continue; }
-            cur += dir * (int64_t)miss * L;
-            break;
+// can X and V be equivalent (one contains the other)?  0 no, 1 yes, 2 needs the entries
+__device__ __forceinline__ int slot_equiv(const uint4 X, uint32_t vmask, int64_t vs, int64_t vl, uint32_t vcid) {
+    if (X.x == vcid) return 1;
+    if (X.y != vmask) return 0;
+    const int64_t xs = (int64_t)X.z, xl = (int64_t)X.w;
+    if (vs < xs) return (xs + xl > vs + vl) ? 0 : 2;
+    if (vs > xs) return (vs + vl > xs + xl) ? 0 : 2;
+    return 2;
+}
+
+// std::lower_bound (libstdc++: half = len >> 1, middle = first + half) over slots
+// tb[0..t); full(id) = MheCompare(entry id, V) for the rare undecided slots
+template <typename Full>
+__device__ __forceinline__ uint32_t lower_bound_slots(const uint4* tb, uint32_t t, uint32_t vmask, int64_t vs,
+                                                     int64_t vl, uint32_t vcid, Full&& full) {
+    uint32_t first = 0, len = t;
+    while (len > 0) {
+        const uint32_t half = len >> 1, mid = first + half;
+        const uint4 X = tb[mid];
+        int r = slot_cmp(X, vmask, vs, vl, vcid);
+        if (r == 2) r = full(X.x) ? 1 : 0;
+        if (r) {
+            first = mid + 1;
+            len = len - half - 1;
+        } else {
+            len = half;
         }
-        // directions 2/3: furthest hit within L single steps, then restart
-        const bool h2 = tid < L ? hit_at(cur + dir * (int64_t)(tid + 1), comps, nc, clo, chi, packed, ss) : false;
-        const int far = block_last_true(h2, red);
-        if (far < 0) break;
-        cur += dir * (int64_t)(far + 1);
     }
-    return cur;
+    return first;
 }
+
+template <int MG>
+__device__ __forceinline__ uint32_t mask_of(const Mhe<MG>& m, int G) {
+    uint32_t k = 0;
+    #pragma unroll
+    for (int g = 0; g < MG; ++g) k |= (g < G && m.s[g] != 0) ? (1u << g) : 0u;
+    return k;
+}
+
+// per probe in bucket order: {presence mask, first-genome start, chain id, probe id}
+template <int MG, typename View>
+__global__ __launch_bounds__(kBlock) void probe_summary_kernel(View v, GenomeTable gt, MatchParams mp, int L,
+                                                               const uint64_t* __restrict__ probe_info,
+                                                               const uint32_t* __restrict__ ids, uint64_t P,
+                                                               const uint32_t* __restrict__ chain_of,
+                                                               uint4* __restrict__ summ) {
+    const uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (q >= P) return;
+    const uint32_t k = ids[q];
+    Mhe<MG> Q;
+    uint32_t gs;
+    const uint64_t info = probe_info[k];
+    const uint64_t h = info & 0xFFFFFFFFull;
+    build_probe<MG, View>(v, h, h + ((info >> 32) & 0xFFFFull), gt, mp, L, Q, &gs);
+    summ[q] = make_uint4(mask_of<MG>(Q, gt.G), (uint32_t)start_at(Q, first_start(Q)), chain_of[k], k);
+}
+
+// the probe of stream group k (AddHashEntry's argument), built on the rare slow path
+template <int MG, typename View>
+__device__ __noinline__ void probe_full(const View& v, const GenomeTable& gt, const MatchParams& mp, int L,
+                                        const uint64_t* __restrict__ probe_info, uint32_t k, Mhe<MG>& P) {
+    uint32_t gs;
+    const uint64_t info = probe_info[k];
+    const uint64_t h = info & 0xFFFFFFFFull;
+    build_probe<MG, View>(v, h, h + ((info >> 32) & 0xFFFFull), gt, mp, L, P, &gs);
+}
+
+// one round: every unconsumed lane of the window runs its lower_bound against the
+// current vector (AddHashEntry's lookup, MemHash.cpp:215-218); returns the first lane
+// whose probe is not a collision (RB if none).  tb is an LDS or a global slot array.
+template <int MG, int RB, typename View>
+__device__ __forceinline__ int round_first(const uint4* tb, uint32_t t, uint32_t done, uint32_t c, uint4 me,
+                                           const View& v, const GenomeTable& gt, const MatchParams& mp, int L,
+                                           const uint64_t* __restrict__ probe_info,
+                                           const int64_t* __restrict__ pool, int* red) {
+    const uint32_t tid = threadIdx.x;
+    bool isnew = false;
+    if (tid >= done && tid < c) {
+        const int G = gt.G;
+        const uint32_t pmask = me.x, pcid = me.z;
+        const int64_t ps = (int64_t)me.y, pl = L;
+        Mhe<MG> P;
+        bool have = false;
+        auto full = [&](uint32_t xid) -> bool {
+            if (!have) { probe_full<MG, View>(v, gt, mp, L, probe_info, me.w, P); have = true; }
+            Mhe<MG> E;
+            load_entry<MG>(pool, xid, G, E);
+            return mhe_less(E, P);
+        };
+        const uint32_t lb = lower_bound_slots(tb, t, pmask, ps, pl, pcid, full);
+        if (lb < t) {
+            const uint4 X = tb[lb];
+            int q = slot_equiv(X, pmask, ps, pl, pcid);
+            if (q == 2) {
+                if (!have) { probe_full<MG, View>(v, gt, mp, L, probe_info, me.w, P); have = true; }
+                Mhe<MG> E;
+                load_entry<MG>(pool, X.x, G, E);
+                q = (mhe_less(E, P) || mhe_less(P, E)) ? 0 : 1;
+            }
+            isnew = q == 0;
+        } else {
+            isnew = true;
+        }
+    }
+    return block_first_true<RB>(isnew, red);
+}
+
+// insert position of chain entry E (lower_bound of the extended copy, MemHash.cpp:247)
+template <int MG>
+__device__ __forceinline__ uint32_t insert_pos(const uint4* tb, uint32_t t, const Mhe<MG>& E, uint32_t em, int64_t es,
+                                              uint32_t cid, const int64_t* __restrict__ pool, int G) {
+    auto full = [&](uint32_t xid) -> bool {
+        Mhe<MG> X;
+        load_entry<MG>(pool, xid, G, X);
+        return mhe_less(X, E);
+    };
+    return lower_bound_slots(tb, t, em, es, E.len, cid, full);
+}
+
+// vector insert at ins (MemHash.cpp:247): shift tb[ins, t) up by one.  Each lane owns
+// a contiguous run [ra, re); it reads the run's first slot before the barrier and
+// moves the run top-down after it (the slot it overwrites was read by its owner).
+template <int RB>
+__device__ __forceinline__ void shift_insert(uint4* tb, uint32_t t, uint32_t ins, uint4 nv) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t n = t - ins;
+    const uint32_t per = (n + RB - 1) / RB;
+    const uint32_t ra = ins + min(n, tid * per), re = ins + min(n, (tid + 1) * per);
+    const uint4 head = ra < re ? tb[ra] : make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    if (ra < re) {
+        for (uint32_t k = re - 1; k > ra; --k) tb[k + 1] = tb[k];
+        tb[ra + 1] = head;
+    }
+    if (tid == 0) tb[ins] = nv;
+    __syncthreads();
+}
+
+template <int MG>
+constexpr int replay_block() { return MG <= 4 ? 1024 : (MG <= 8 ? 512 : 256); }
 
 template <int MG, typename View>
-__global__ __launch_bounds__(kBlock) void replay_kernel(View v, uint64_t N, GenomeTable gt, MatchParams mp, SeedSpec ss,
-                                                        const uint64_t* __restrict__ probe_info,
-                                                        const uint32_t* __restrict__ ids,
-                                                        const uint32_t* __restrict__ bstart,
-                                                        const uint32_t* __restrict__ bend, uint32_t* tbl,
-                                                        int64_t* pool, const uint32_t* __restrict__ packed,
-                                                        uint32_t* __restrict__ tsize, DevCounters* ctr) {
-    const int L = ss.L;
-    __shared__ int red[kBlock / 64];
-    __shared__ int64_t sP[MG + 2];
-    __shared__ ExtComp comps[MG];
-    __shared__ int s_nc;
-    __shared__ int64_t s_clo, s_chi;
-    __shared__ uint32_t s_ins, s_id;
+__global__ __launch_bounds__(replay_block<MG>()) void replay_kernel(
+    View v, GenomeTable gt, MatchParams mp, int L, const uint64_t* __restrict__ probe_info,
+    const uint4* __restrict__ summ, const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend,
+    uint32_t* __restrict__ tbl, uint4* __restrict__ spill, const int64_t* __restrict__ pool, uint32_t lds_cap,
+    uint32_t* __restrict__ tsize, DevCounters* ctr, uint64_t* __restrict__ dbg) {
+    constexpr int RB = replay_block<MG>();
+    extern __shared__ uint4 s_tab[];
+    __shared__ int red[RB / 64];
+    __shared__ uint32_t s_ins;
+    __shared__ uint4 s_new;
+    uint64_t c_win = 0, c_round = 0, c_ins = 0, n_win = 0, n_round = 0, t0 = 0;
+    const uint64_t t_all = dbg ? wall_clock64() : 0;
 
     const int tid = threadIdx.x;
     const uint32_t b = blockIdx.x;
@@ -119,116 +223,84 @@ __global__ __launch_bounds__(kBlock) void replay_kernel(View v, uint64_t N, Geno
     const uint32_t K_b = bend[b] - beg;
     if (K_b == 0) return;
     const int G = gt.G;
-    uint32_t* tb = tbl + beg;
-    const uint32_t* hd = ids + beg;
-    uint32_t t = 0, i = 0;
+    bool in_lds = true;
+    uint32_t t = 0;
     unsigned long long coll = 0;
 
-    while (i < K_b) {
-        const uint32_t c = min((uint32_t)kBlock, K_b - i);
-        bool isnew = false;
-        Mhe<MG> P;
-        if ((uint32_t)tid < c) {
-            uint32_t gs;
-            const uint64_t info = probe_info[hd[i + tid]];
-            const uint64_t h = info & 0xFFFFFFFFull;
-            build_probe<MG, View>(v, h, h + ((info >> 32) & 0xFFFFull), gt, mp, L, P, &gs);
-            const uint32_t lb = lower_bound_tbl<MG>(tb, t, pool, G, P);
-            if (lb < t) {
+    // the window of probes [w0, w0 + c) stays in the lanes' registers until every
+    // one of them is consumed (collided or inserted); `done` = consumed prefix
+    uint4 nxt = (uint32_t)tid < K_b ? summ[beg + tid] : make_uint4(0, 0, 0, 0);
+    for (uint32_t w0 = 0; w0 < K_b; w0 += RB) {
+        const uint32_t c = min((uint32_t)RB, K_b - w0);
+        if (dbg) { t0 = wall_clock64(); ++n_win; }
+        const uint4 me = nxt;
+        if (w0 + RB + tid < K_b) nxt = summ[beg + w0 + RB + tid];   // prefetch the next window
+        if (dbg) { __syncthreads(); c_win += wall_clock64() - t0; }
+        uint32_t done = 0;
+        while (done < c) {
+            if (dbg) { t0 = wall_clock64(); ++n_round; }
+            const int first = in_lds
+                ? round_first<MG, RB, View>(s_tab, t, done, c, me, v, gt, mp, L, probe_info, pool, red)
+                : round_first<MG, RB, View>(spill + beg, t, done, c, me, v, gt, mp, L, probe_info, pool, red);
+            if (dbg) { const uint64_t t1 = wall_clock64(); c_round += t1 - t0; t0 = t1; }
+            if (first == RB) {
+                coll += c - done;
+                break;
+            }
+            coll += (unsigned long long)(first - (int)done);
+            if (tid == first) {
                 Mhe<MG> E;
-                load_entry<MG>(pool, tb[lb], G, E);
-                isnew = mhe_less(E, P) || mhe_less(P, E);
-            } else {
-                isnew = true;
+                load_entry<MG>(pool, me.z, G, E);
+                const uint32_t em = mask_of<MG>(E, G);
+                const int64_t es = start_at(E, first_start(E));
+                s_ins = in_lds ? insert_pos<MG>(s_tab, t, E, em, es, me.z, pool, G)
+                               : insert_pos<MG>(spill + beg, t, E, em, es, me.z, pool, G);
+                s_new = make_uint4(me.z, em, (uint32_t)es, (uint32_t)E.len);
             }
-        }
-        const int first = block_first_true(isnew, red);
-        if (first == kBlock) {
-            coll += c;
-            i += c;
-            continue;
-        }
-        coll += (unsigned long long)first;
-        if (tid == first) {
-            sP[0] = P.len;
-            sP[1] = P.offset;
-            #pragma unroll
-            for (int g = 0; g < MG; ++g) sP[2 + g] = P.s[g];
-        }
-        __syncthreads();
-        if (tid == 0) {
-            int nc = 0;
-            int64_t clo = INT64_MIN, chi = INT64_MAX;
-            for (int g = 0; g < G; ++g) {
-                const int64_t s = sP[2 + g];
-                if (s == 0) continue;
-                comps[nc].s = s;
-                comps[nc].woff = gt.woff[g];
-                const int64_t m = (int64_t)gt.m[g];
-                const int64_t lo = s > 0 ? 1 - s : -s - m;
-                const int64_t hi = s > 0 ? m - s : -s - 1;
-                clo = lo > clo ? lo : clo;
-                chi = hi < chi ? hi : chi;
-                ++nc;
+            if (in_lds && t + 1 > lds_cap) {   // spill the vector to the bucket's global slice
+                for (uint32_t k = tid; k < t; k += RB) spill[beg + k] = s_tab[k];
+                in_lds = false;
             }
-            s_nc = nc;
-            s_clo = clo;
-            s_chi = chi;
-        }
-        __syncthreads();
-        const int nc = s_nc;
-        const int64_t clo = s_clo, chi = s_chi;
-        const int64_t cmax = chain_end(+1, L, comps, nc, clo, chi, packed, ss, red);
-        const int64_t cmin = chain_end(-1, L, comps, nc, clo, chi, packed, ss, red);
-        if (tid == 0) {
-            const uint32_t id = (uint32_t)atomicAdd(&ctr->entries, 1ull);
-            Mhe<MG> E;
-            E.len = cmax - cmin + L;
-            E.offset = sP[1];
-            E.mersize = 0;
-            #pragma unroll
-            for (int g = 0; g < MG; ++g) {
-                const int64_t s = sP[2 + g];
-                E.s[g] = s > 0 ? s + cmin : (s < 0 ? -((-s) - cmax) : 0);
-            }
-            int64_t* e = pool + (uint64_t)id * (uint64_t)(G + 2);
-            e[0] = E.len;
-            e[1] = E.offset;
-            #pragma unroll
-            for (int g = 0; g < MG; ++g)
-                if (g < G) e[2 + g] = E.s[g];
-            s_ins = lower_bound_tbl<MG>(tb, t, pool, G, E);
-            s_id = id;
-        }
-        __syncthreads();
-        const uint32_t ins = s_ins;
-        for (int64_t top = t; top > (int64_t)ins; top -= kBlock) {
-            const int64_t lo = top - kBlock > (int64_t)ins ? top - kBlock : (int64_t)ins;
-            const int64_t j = lo + tid;
-            uint32_t v = 0;
-            if (j < top) v = tb[j];
             __syncthreads();
-            if (j < top) tb[j + 1] = v;
-            __syncthreads();
+            if (in_lds) shift_insert<RB>(s_tab, t, s_ins, s_new);
+            else shift_insert<RB>(spill + beg, t, s_ins, s_new);
+            if (dbg) c_ins += wall_clock64() - t0;
+            t += 1;
+            done = (uint32_t)first + 1;
         }
-        if (tid == 0) tb[ins] = s_id;
-        __syncthreads();
-        t += 1;
-        i += (uint32_t)first + 1;
     }
+    if (in_lds)
+        for (uint32_t k = tid; k < t; k += RB) tbl[beg + k] = s_tab[k].x;
+    else
+        for (uint32_t k = tid; k < t; k += RB) tbl[beg + k] = spill[beg + k].x;
     if (tid == 0) {
         tsize[b] = t;
         atomicAdd(&ctr->collisions, coll);
+        atomicAdd(&ctr->entries, (unsigned long long)t);
+        if (dbg) {
+            uint64_t* d = dbg + (uint64_t)b * 8;
+            d[0] = K_b; d[1] = t; d[2] = n_win; d[3] = n_round;
+            d[4] = c_win; d[5] = c_round; d[6] = c_ins; d[7] = wall_clock64() - t_all;
+        }
     }
 }
 
 __global__ void bucket_ranges_kernel(const uint32_t* __restrict__ sb, uint64_t P, uint32_t* __restrict__ bstart,
-                                     uint32_t* __restrict__ bend) {
+                                     uint32_t* __restrict__ bend, uint32_t* __restrict__ d_max) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= P) return;
     const uint32_t b = sb[k];
     if (k == 0 || sb[k - 1] != b) bstart[b] = (uint32_t)k;
-    if (k == P - 1 || sb[k + 1] != b) bend[b] = (uint32_t)(k + 1);
+    if (k == P - 1 || sb[k + 1] != b) {
+        bend[b] = (uint32_t)(k + 1);
+        uint64_t lo = k;   // first probe of this bucket: binary search back over sb
+        uint64_t a = 0;
+        while (a < lo) {
+            const uint64_t m = (a + lo) >> 1;
+            if (sb[m] < b) a = m + 1; else lo = m;
+        }
+        atomicMax(d_max, (uint32_t)(k + 1 - a));
+    }
 }
 
 // MemHash::GetMatchList (MemHash.h:182-203): bucket-major, vector order
@@ -253,19 +325,30 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(const uint32_t* __restrict
 
 }  // namespace
 
-hipError_t launch_bucket_ranges(const uint32_t* sb, uint64_t P, uint32_t* bstart, uint32_t* bend, hipStream_t st) {
+hipError_t launch_bucket_ranges(const uint32_t* sb, uint64_t P, uint32_t* bstart, uint32_t* bend, uint32_t* d_max,
+                                hipStream_t st) {
     if (P == 0) return hipSuccess;
-    hipLaunchKernelGGL(bucket_ranges_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st, sb, P, bstart, bend);
+    hipLaunchKernelGGL(bucket_ranges_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st, sb, P, bstart, bend,
+                       d_max);
     return hipGetLastError();
 }
 
 template <int MG, typename View>
-hipError_t launch_replay(View v, uint64_t N, const GenomeTable& gt, const MatchParams& mp, const SeedSpec& ss,
-                         const uint64_t* probe_info, const uint32_t* sorted_ids, const uint32_t* bstart,
-                         const uint32_t* bend, uint32_t* tbl, int64_t* pool, const uint32_t* packed,
-                         uint32_t* tsize, void* ctr, hipStream_t st) {
-    hipLaunchKernelGGL((replay_kernel<MG, View>), dim3(mp.table_size), dim3(kBlock), 0, st, v, N, gt, mp, ss,
-                       probe_info, sorted_ids, bstart, bend, tbl, pool, packed, tsize, (DevCounters*)ctr);
+hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, int L, const uint64_t* probe_info,
+                         const uint32_t* sorted_ids, uint64_t P, const uint32_t* bstart, const uint32_t* bend,
+                         uint32_t* tbl, void* spill, void* summ, const int64_t* pool, const uint32_t* chain_of,
+                         uint32_t lds_cap, uint32_t* tsize, void* ctr, uint64_t* dbg, hipStream_t st) {
+    hipLaunchKernelGGL((probe_summary_kernel<MG, View>), dim3((unsigned)((P + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       st, v, gt, mp, L, probe_info, sorted_ids, P, chain_of, (uint4*)summ);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const size_t lds = (size_t)lds_cap * sizeof(uint4);
+    e = hipFuncSetAttribute((const void*)replay_kernel<MG, View>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((replay_kernel<MG, View>), dim3(mp.table_size), dim3(replay_block<MG>()), lds, st, v, gt, mp, L,
+                       probe_info, (const uint4*)summ, bstart, bend, tbl, (uint4*)spill, pool, lds_cap, tsize,
+                       (DevCounters*)ctr, dbg);
     return hipGetLastError();
 }
 
@@ -278,9 +361,10 @@ hipError_t launch_emit(const uint32_t* tsize, const uint32_t* obase, const uint3
 }
 
 #define MUMS_INST_REPLAY(MG, V)                                                                                   \
-    template hipError_t launch_replay<MG, V>(V, uint64_t, const GenomeTable&, const MatchParams&, const SeedSpec&, \
-                                             const uint64_t*, const uint32_t*, const uint32_t*, const uint32_t*,  \
-                                             uint32_t*, int64_t*, const uint32_t*, uint32_t*, void*, hipStream_t);
+    template hipError_t launch_replay<MG, V>(V, const GenomeTable&, const MatchParams&, int, const uint64_t*,      \
+                                             const uint32_t*, uint64_t, const uint32_t*, const uint32_t*,          \
+                                             uint32_t*, void*, void*, const int64_t*, const uint32_t*, uint32_t,   \
+                                             uint32_t*, void*, uint64_t*, hipStream_t);
 MUMS_INST_REPLAY(4, PairView<uint32_t>)
 MUMS_INST_REPLAY(8, PairView<uint32_t>)
 MUMS_INST_REPLAY(16, PairView<uint32_t>)
