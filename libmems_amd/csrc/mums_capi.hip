@@ -198,6 +198,8 @@ template <int MG, typename View>
 int replay_run(mums_ctx* ctx, View v, const MatchParams& mp, hipStream_t st) {
     DevCounters* dc = ctx->counters.as<DevCounters>();
     const uint64_t P = ctx->P;
+    if (P >= (1ull << 30))   // probe ids share a word with two replay flags (replay.hip)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^30 seed probes in one FindMatches");
     HIPCHK((launch_chains<MG, View>(v, ctx->probe_info, P, ctx->gt, mp, ctx->ss, ctx->packed.as<uint32_t>(),
                                     ctx->chain_tmp.p, ctx->tmp.p, ctx->radix_tmp.p, ctx->chain_of.as<uint32_t>(),
                                     ctx->pool.as<int64_t>(), &dc->nchains, st)));
@@ -215,7 +217,7 @@ int replay_run(mums_ctx* ctx, View v, const MatchParams& mp, hipStream_t st) {
     HIPCHK((launch_replay<MG, View>(v, ctx->gt, mp, ctx->L, ctx->probe_info, ctx->sorted_ids, P,
                                     ctx->bstart.as<uint32_t>(), ctx->bend.as<uint32_t>(), ctx->tbl.as<uint32_t>(),
                                     ctx->spill.p, ctx->summ.p, ctx->pool.as<int64_t>(), ctx->chain_of.as<uint32_t>(),
-                                    lds_cap,
+                                    ctx->hc.nchains, ctx->chain_tmp.p, ctx->radix_tmp.p, lds_cap,
                                     ctx->tsize.as<uint32_t>(), ctx->counters.p, dbg, st)));
     if (dbg) {   // development instrumentation: the slowest buckets of the replay
         std::vector<uint64_t> h((size_t)ctx->table_size * 8);

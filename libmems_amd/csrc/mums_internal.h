@@ -195,7 +195,8 @@ template <int MG, typename View>
 hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, int L, const uint64_t* probe_info,
                          const uint32_t* sorted_ids, uint64_t P, const uint32_t* bstart, const uint32_t* bend,
                          uint32_t* tbl, void* spill, void* summ, const int64_t* pool, const uint32_t* chain_of,
-                         uint32_t lds_cap, uint32_t* tsize, void* ctr, uint64_t* dbg, hipStream_t st);
+                         uint32_t nch, void* d_tmp, void* d_radix_tmp, uint32_t lds_cap, uint32_t* tsize, void* ctr,
+                         uint64_t* dbg, hipStream_t st);
 // chains.hip: chain labelling of the probes (key order) before the replay
 size_t chain_tmp_bytes(uint64_t P);
 template <int MG, typename View>

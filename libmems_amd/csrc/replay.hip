@@ -101,13 +101,14 @@ __device__ __forceinline__ uint32_t mask_of(const Mhe<MG>& m, int G) {
     return k;
 }
 
-// per probe in bucket order: {presence mask, first-genome start, chain id, probe id}
+// per probe in bucket order: {presence mask, first-genome start, chain id, probe id | flags}
 template <int MG, typename View>
 __global__ __launch_bounds__(kBlock) void probe_summary_kernel(View v, GenomeTable gt, MatchParams mp, int L,
                                                                const uint64_t* __restrict__ probe_info,
                                                                const uint32_t* __restrict__ ids, uint64_t P,
                                                                const uint32_t* __restrict__ chain_of,
-                                                               uint4* __restrict__ summ) {
+                                                               uint4* __restrict__ summ,
+                                                               uint32_t* __restrict__ first_pos) {
     const uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (q >= P) return;
     const uint32_t k = ids[q];
@@ -116,7 +117,76 @@ __global__ __launch_bounds__(kBlock) void probe_summary_kernel(View v, GenomeTab
     const uint64_t info = probe_info[k];
     const uint64_t h = info & 0xFFFFFFFFull;
     build_probe<MG, View>(v, h, h + ((info >> 32) & 0xFFFFull), gt, mp, L, Q, &gs);
-    summ[q] = make_uint4(mask_of<MG>(Q, gt.G), (uint32_t)start_at(Q, first_start(Q)), chain_of[k], k);
+    const uint32_t cid = chain_of[k];
+    summ[q] = make_uint4(mask_of<MG>(Q, gt.G), (uint32_t)start_at(Q, first_start(Q)), cid, k);
+    atomicMin(&first_pos[cid], (uint32_t)q);
+}
+
+// Sort keys of the chain entries: (hash bucket, presence mask) and first-genome start.
+__global__ __launch_bounds__(kBlock) void chain_keys_kernel(const int64_t* __restrict__ pool, uint32_t nch, int G,
+                                                            uint32_t table_size, double inv_t,
+                                                            uint64_t* __restrict__ key_s, uint64_t* __restrict__ key_b) {
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    if (c >= nch) return;
+    const int64_t* e = pool + (uint64_t)c * (uint64_t)(G + 2);
+    uint32_t m = 0;
+    int64_t s0 = 0;
+    for (int g = G - 1; g >= 0; --g) {
+        const int64_t sg = e[2 + g];
+        if (sg != 0) { m |= 1u << g; s0 = sg; }
+    }
+    key_s[c] = (uint64_t)s0;
+    key_b[c] = ((uint64_t)bucket_of_fast(e[1], table_size, inv_t) << 32) | m;
+}
+
+__global__ __launch_bounds__(kBlock) void gather_u64_kernel(const uint64_t* __restrict__ src,
+                                                            const uint32_t* __restrict__ idx, uint32_t n,
+                                                            uint64_t* __restrict__ dst) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) dst[i] = src[idx[i]];
+}
+
+// next_s[c] = smallest first-genome start >= c's among the OTHER chains of c's bucket
+// and presence mask (c's own start on a tie), ~0 if none.  Chains are in (bucket, mask,
+// start) order.
+__global__ __launch_bounds__(kBlock) void chain_next_kernel(const uint32_t* __restrict__ ord,
+                                                            const uint64_t* __restrict__ key_s,
+                                                            const uint64_t* __restrict__ key_b, uint32_t nch,
+                                                            uint32_t* __restrict__ next_s) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= nch) return;
+    const uint32_t c = ord[i];
+    const uint64_t g = key_b[c], sc = key_s[c];
+    uint64_t nx = ~0ull;
+    if (i + 1 < nch) {
+        const uint32_t d = ord[i + 1];
+        if (key_b[d] == g) nx = key_s[d];
+    }
+    if (i > 0) {
+        const uint32_t d = ord[i - 1];
+        if (key_b[d] == g && key_s[d] == sc) nx = sc;
+    }
+    next_s[c] = nx > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)nx;
+}
+
+// Per-probe decision flags (bits 31 / 30 of summ.w):
+//   first: the earliest probe of its chain in the bucket -> AddHashEntry inserts it (no
+//          entry can contain it: only its own chain's entries do)
+//   susp : another chain of the bucket and mask starts inside [chain start, probe start];
+//          only then can lower_bound miss the probe's chain entry (the non-transitive
+//          MheCompare case), so only these probes run the exact search.
+// Every other probe collides with its chain entry: the vector stays sorted by (block,
+// first-genome start) and is partitioned with respect to such a probe.
+__global__ __launch_bounds__(kBlock) void probe_flags_kernel(uint4* __restrict__ summ, uint64_t P,
+                                                             const uint32_t* __restrict__ first_pos,
+                                                             const uint32_t* __restrict__ next_s) {
+    const uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (q >= P) return;
+    uint4 r = summ[q];
+    const bool first = first_pos[r.z] == (uint32_t)q;
+    const bool susp = !first && r.y >= next_s[r.z];
+    r.w |= (first ? 0x80000000u : 0u) | (susp ? 0x40000000u : 0u);
+    summ[q] = r;
 }
 
 // the probe of stream group k (AddHashEntry's argument), built on the rare slow path
@@ -139,14 +209,16 @@ __device__ __forceinline__ int round_first(const uint4* tb, uint32_t t, uint32_t
                                            const int64_t* __restrict__ pool, int* red) {
     const uint32_t tid = threadIdx.x;
     bool isnew = false;
-    if (tid >= done && tid < c) {
+    if (tid >= done && tid < c && (me.w & 0x80000000u)) {
+        isnew = true;
+    } else if (tid >= done && tid < c && (me.w & 0x40000000u)) {
         const int G = gt.G;
         const uint32_t pmask = me.x, pcid = me.z;
         const int64_t ps = (int64_t)me.y, pl = L;
         Mhe<MG> P;
         bool have = false;
         auto full = [&](uint32_t xid) -> bool {
-            if (!have) { probe_full<MG, View>(v, gt, mp, L, probe_info, me.w, P); have = true; }
+            if (!have) { probe_full<MG, View>(v, gt, mp, L, probe_info, me.w & 0x3FFFFFFFu, P); have = true; }
             Mhe<MG> E;
             load_entry<MG>(pool, xid, G, E);
             return mhe_less(E, P);
@@ -156,7 +228,7 @@ __device__ __forceinline__ int round_first(const uint4* tb, uint32_t t, uint32_t
             const uint4 X = tb[lb];
             int q = slot_equiv(X, pmask, ps, pl, pcid);
             if (q == 2) {
-                if (!have) { probe_full<MG, View>(v, gt, mp, L, probe_info, me.w, P); have = true; }
+                if (!have) { probe_full<MG, View>(v, gt, mp, L, probe_info, me.w & 0x3FFFFFFFu, P); have = true; }
                 Mhe<MG> E;
                 load_entry<MG>(pool, X.x, G, E);
                 q = (mhe_less(E, P) || mhe_less(P, E)) ? 0 : 1;
@@ -337,11 +409,50 @@ template <int MG, typename View>
 hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, int L, const uint64_t* probe_info,
                          const uint32_t* sorted_ids, uint64_t P, const uint32_t* bstart, const uint32_t* bend,
                          uint32_t* tbl, void* spill, void* summ, const int64_t* pool, const uint32_t* chain_of,
-                         uint32_t lds_cap, uint32_t* tsize, void* ctr, uint64_t* dbg, hipStream_t st) {
-    hipLaunchKernelGGL((probe_summary_kernel<MG, View>), dim3((unsigned)((P + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                       st, v, gt, mp, L, probe_info, sorted_ids, P, chain_of, (uint4*)summ);
-    hipError_t e = hipGetLastError();
+                         uint32_t nch, void* d_tmp, void* d_radix_tmp, uint32_t lds_cap, uint32_t* tsize, void* ctr,
+                         uint64_t* dbg, hipStream_t st) {
+    char* p = (char*)d_tmp;
+    auto carve = [&](size_t bytes) {
+        char* r = p;
+        p += (bytes + 255) & ~(size_t)255;
+        return (void*)r;
+    };
+    uint64_t* key_s = (uint64_t*)carve((size_t)nch * 8);
+    uint64_t* key_b = (uint64_t*)carve((size_t)nch * 8);
+    uint64_t* key_g = (uint64_t*)carve((size_t)nch * 8);
+    uint64_t* kA = (uint64_t*)carve((size_t)nch * 8);
+    uint64_t* kB = (uint64_t*)carve((size_t)nch * 8);
+    uint32_t* vA = (uint32_t*)carve((size_t)nch * 4);
+    uint32_t* vB = (uint32_t*)carve((size_t)nch * 4);
+    uint32_t* first_pos = (uint32_t*)carve((size_t)nch * 4);
+    uint32_t* next_s = (uint32_t*)carve((size_t)nch * 4);
+    const unsigned pgrid = (unsigned)((P + kBlock - 1) / kBlock), cgrid = (nch + kBlock - 1) / kBlock;
+    hipError_t e = hipMemsetAsync(first_pos, 0xFF, (size_t)nch * 4, st);
     if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((probe_summary_kernel<MG, View>), dim3(pgrid), dim3(kBlock), 0, st, v, gt, mp, L, probe_info,
+                       sorted_ids, P, chain_of, (uint4*)summ, first_pos);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // chains in (bucket, mask, first start) order -> next_s per chain
+    hipLaunchKernelGGL(chain_keys_kernel, dim3(cgrid), dim3(kBlock), 0, st, pool, nch, gt.G, mp.table_size,
+                       1.0 / (double)mp.table_size, key_s, key_b);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    int buf = 0;
+    if ((e = radix_sort<uint64_t>(key_s, nullptr, nch, 32, kA, vA, kB, vB, d_radix_tmp, &buf, st)) != hipSuccess)
+        return e;
+    const uint32_t* ord1 = buf ? vB : vA;
+    hipLaunchKernelGGL(gather_u64_kernel, dim3(cgrid), dim3(kBlock), 0, st, key_b, ord1, nch, key_g);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    uint32_t* vin = buf ? vB : vA;
+    uint32_t* vout = buf ? vA : vB;
+    int buf2 = 0;
+    // pass 0 reads vin and writes vout; later passes ping-pong between vout and vin
+    if ((e = radix_sort<uint64_t>(key_g, vin, nch, 64, kA, vout, kB, vin, d_radix_tmp, &buf2, st)) != hipSuccess)
+        return e;
+    const uint32_t* ord = buf2 ? vin : vout;
+    hipLaunchKernelGGL(chain_next_kernel, dim3(cgrid), dim3(kBlock), 0, st, ord, key_s, key_b, nch, next_s);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(probe_flags_kernel, dim3(pgrid), dim3(kBlock), 0, st, (uint4*)summ, P, first_pos, next_s);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     const size_t lds = (size_t)lds_cap * sizeof(uint4);
     e = hipFuncSetAttribute((const void*)replay_kernel<MG, View>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
@@ -364,7 +475,7 @@ hipError_t launch_emit(const uint32_t* tsize, const uint32_t* obase, const uint3
     template hipError_t launch_replay<MG, V>(V, const GenomeTable&, const MatchParams&, int, const uint64_t*,      \
                                              const uint32_t*, uint64_t, const uint32_t*, const uint32_t*,          \
                                              uint32_t*, void*, void*, const int64_t*, const uint32_t*, uint32_t,   \
-                                             uint32_t*, void*, uint64_t*, hipStream_t);
+                                             void*, void*, uint32_t, uint32_t*, void*, uint64_t*, hipStream_t);
 MUMS_INST_REPLAY(4, PairView<uint32_t>)
 MUMS_INST_REPLAY(8, PairView<uint32_t>)
 MUMS_INST_REPLAY(16, PairView<uint32_t>)
