@@ -22,6 +22,9 @@
 // The replay (replay.hip) then inserts chain entries without extending anything.
 // A 32-bit line-hash collision only splits runs of a line: every probe still gets
 // its true chain ends (a segment end always walks to the real end of its chain).
+#include <cstdio>
+#include <cstdlib>
+
 #include "match_device.h"
 #include "seed_device.h"
 
@@ -273,7 +276,14 @@ __global__ __launch_bounds__(kBlock) void chain_left_kernel(View v, const uint64
     }
 }
 
-// Long walks, one workgroup per item (grid-stride over the queue).
+// Long walks, one workgroup per item (grid-stride over the queue).  Each iteration
+// evaluates the 1024 columns after the current chain end (4 per lane, one 64-column
+// ballot word per wave and sub-step) and one lane scans the 16 words for the first
+// run of >= L columns without a hit: the chain ends at the last hit before it (the
+// maximal chain of hits with gaps <= L); without such a run the walk
+// continues from the last hit of the window.
+constexpr int kWalkCols = 4 * kBlock;
+
 template <int MG, typename View>
 __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64_t* __restrict__ probe_info,
                                                             GenomeTable gt, MatchParams mp, SeedSpec ss,
@@ -283,8 +293,10 @@ __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64
                                                             const unsigned int* __restrict__ qcount,
                                                             uint8_t* __restrict__ link, int64_t* __restrict__ rcol,
                                                             int64_t* __restrict__ lcol) {
-    __shared__ int red[kBlock / 64];
-    const int tid = threadIdx.x;
+    __shared__ uint64_t words[kWalkCols / 64];
+    __shared__ int64_t s_adv;
+    __shared__ int s_broke;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int L = ss.L;
     const unsigned nq = *qcount;
     for (unsigned qi = blockIdx.x; qi < nq; qi += gridDim.x) {
@@ -299,24 +311,53 @@ __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64
         bool reached = false;
         for (;;) {
             if (dir > 0 ? cur >= it.stop : cur <= it.stop) { reached = true; break; }
-            // ExtendMatch directions 0/1: jumps of L while the seed at the new end hits
-            for (;;) {
-                const bool h = hit_lane<MG>(cur + dir * (int64_t)(tid + 1) * L, A, gt, clo, chi, packed, ss);
-                const int miss = wg_first_true(!h, red);
-                if (miss == kBlock) {
-                    cur += dir * (int64_t)kBlock * L;
-                    if (dir > 0 ? cur >= it.stop : cur <= it.stop) break;
-                    continue;
+            #pragma unroll
+            for (int r = 0; r < kWalkCols / kBlock; ++r) {   // column offsets 1 + 256 r + tid
+                const int64_t k = 1 + (int64_t)r * kBlock + tid;
+                const uint64_t m = __ballot(hit_lane<MG>(cur + dir * k, A, gt, clo, chi, packed, ss));
+                if (lane == 0) words[r * (kBlock / 64) + wv] = m;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                int64_t last = 0;   // offset of the last reachable hit (0 = cur)
+                int carry = 0;      // columns without a hit since it
+                int broke = 0;
+                for (int wi = 0; wi < kWalkCols / 64 && !broke; ++wi) {
+                    const uint64_t x = words[wi];
+                    if (x == 0) {
+                        carry += 64;
+                        broke = carry >= L;
+                        continue;
+                    }
+                    const int f = __builtin_ctzll(x);
+                    if (carry + f >= L) { broke = 1; break; }
+                    // bit i of a: columns i .. i+L-1 of this word all miss
+                    uint64_t a = ~x;
+                    int len = 1;
+                    while (2 * len <= L) { a &= a >> len; len *= 2; }
+                    if (len < L) a &= a >> (L - len);
+                    if (a) {
+                        const int r0 = __builtin_ctzll(a);
+                        const uint64_t below = x & ((1ull << r0) - 1);
+                        last = (int64_t)wi * 64 + (63 - __builtin_clzll(below)) + 1;
+                        broke = 1;
+                        break;
+                    }
+                    const int hb = 63 - __builtin_clzll(x);
+                    last = (int64_t)wi * 64 + hb + 1;
+                    carry = 63 - hb;
                 }
-                cur += dir * (int64_t)miss * L;
+                s_adv = last;
+                s_broke = broke;
+            }
+            __syncthreads();
+            cur += dir * s_adv;
+            const int broke = s_broke;
+            __syncthreads();
+            if (broke) {
+                reached = dir > 0 ? cur >= it.stop : cur <= it.stop;
                 break;
             }
-            if (dir > 0 ? cur >= it.stop : cur <= it.stop) { reached = true; break; }
-            // directions 2/3: the furthest hit within L single steps
-            const bool h2 = tid < L ? hit_lane<MG>(cur + dir * (int64_t)(tid + 1), A, gt, clo, chi, packed, ss) : false;
-            const int far = wg_last_true(h2, red);
-            if (far < 0) break;
-            cur += dir * (int64_t)(far + 1);
         }
         if (tid == 0) {
             if (it.kind == 0) {
@@ -441,6 +482,12 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
         hipLaunchKernelGGL((chain_walk_kernel<MG, View>), dim3(walk_grid), dim3(kBlock), 0, st, v, probe_info, gt, mp,
                            ss, ord, packed, queue, qcount, link, rcol, lcol);
         if ((e = hipGetLastError()) != hipSuccess) return e;
+        if (getenv("MUMS_DEV_CHAIN_DEBUG")) {   // development: long-walk queue sizes
+            unsigned hq = 0;
+            (void)hipMemcpyAsync(&hq, qcount, 4, hipMemcpyDeviceToHost, st);
+            (void)hipStreamSynchronize(st);
+            fprintf(stderr, "chains: pass %d long walks %u of %lu probes\n", pass, hq, (unsigned long)P);
+        }
     }
     hipLaunchKernelGGL(chain_flag_kernel, dim3(grid), dim3(kBlock), 0, st, link, P, seg);
     if ((e = hipGetLastError()) != hipSuccess) return e;

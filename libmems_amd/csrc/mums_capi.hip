@@ -520,7 +520,7 @@ int run_pipeline(mums_ctx* ctx, int stage) {
         HIPCHK(ctx->tbl.ensure((ctx->P + 1) * 4));
         HIPCHK(ctx->chain_of.ensure((ctx->P + 1) * 4));
         HIPCHK(ctx->spill.ensure((ctx->P + 1) * 16));
-        HIPCHK(ctx->summ.ensure((ctx->P + 1) * 16));
+        HIPCHK(ctx->summ.ensure((ctx->P + 1) * 32));
         HIPCHK(ctx->chain_tmp.ensure(chain_tmp_bytes(ctx->P + 1)));
         HIPCHK(ctx->radix_tmp.ensure(radix_tmp_bytes(ctx->P + 1)));
         HIPCHK(ctx->tmp.ensure(std::max(scan_tmp_bytes(ctx->P + 1), scan_tmp_bytes(Tb))));

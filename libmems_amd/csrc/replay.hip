@@ -119,10 +119,14 @@ __global__ __launch_bounds__(kBlock) void probe_summary_kernel(View v, GenomeTab
     build_probe<MG, View>(v, h, h + ((info >> 32) & 0xFFFFull), gt, mp, L, Q, &gs);
     const uint32_t cid = chain_of[k];
     summ[q] = make_uint4(mask_of<MG>(Q, gt.G), (uint32_t)start_at(Q, first_start(Q)), cid, k);
-    atomicMin(&first_pos[cid], (uint32_t)q);
+    // probes run in ascending q, so the plain read filters nearly every later atomic
+    if ((uint32_t)q < __hip_atomic_load(&first_pos[cid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMin(&first_pos[cid], (uint32_t)q);
 }
 
-// Sort keys of the chain entries: (hash bucket, presence mask) and first-genome start.
+// Sort keys of the chain entries: (hash bucket, block) and first-genome start, where the
+// block key bitreverse(presence mask) orders blocks as MheCompare does (FirstStart
+// index descending, then the first genome present in only one: absent first).
 __global__ __launch_bounds__(kBlock) void chain_keys_kernel(const int64_t* __restrict__ pool, uint32_t nch, int G,
                                                             uint32_t table_size, double inv_t,
                                                             uint64_t* __restrict__ key_s, uint64_t* __restrict__ key_b) {
@@ -136,7 +140,7 @@ __global__ __launch_bounds__(kBlock) void chain_keys_kernel(const int64_t* __res
         if (sg != 0) { m |= 1u << g; s0 = sg; }
     }
     key_s[c] = (uint64_t)s0;
-    key_b[c] = ((uint64_t)bucket_of_fast(e[1], table_size, inv_t) << 32) | m;
+    key_b[c] = ((uint64_t)bucket_of_fast(e[1], table_size, inv_t) << 32) | __builtin_bitreverse32(m);
 }
 
 __global__ __launch_bounds__(kBlock) void gather_u64_kernel(const uint64_t* __restrict__ src,
@@ -147,26 +151,31 @@ __global__ __launch_bounds__(kBlock) void gather_u64_kernel(const uint64_t* __re
 }
 
 // next_s[c] = smallest first-genome start >= c's among the OTHER chains of c's bucket
-// and presence mask (c's own start on a tie), ~0 if none.  Chains are in (bucket, mask,
-// start) order.
+// and presence mask (c's own start on a tie), ~0 if none.  rank[c] = c's index in
+// (bucket, block, start) order = MheCompare order inside a bucket, bit 31 set when
+// another chain of the block has the same start (order then decided by later genomes).
 __global__ __launch_bounds__(kBlock) void chain_next_kernel(const uint32_t* __restrict__ ord,
                                                             const uint64_t* __restrict__ key_s,
                                                             const uint64_t* __restrict__ key_b, uint32_t nch,
-                                                            uint32_t* __restrict__ next_s) {
+                                                            uint32_t* __restrict__ next_s,
+                                                            uint32_t* __restrict__ rank) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= nch) return;
     const uint32_t c = ord[i];
     const uint64_t g = key_b[c], sc = key_s[c];
     uint64_t nx = ~0ull;
+    bool tie = false;
     if (i + 1 < nch) {
         const uint32_t d = ord[i + 1];
         if (key_b[d] == g) nx = key_s[d];
+        tie = nx == sc;
     }
     if (i > 0) {
         const uint32_t d = ord[i - 1];
-        if (key_b[d] == g && key_s[d] == sc) nx = sc;
+        if (key_b[d] == g && key_s[d] == sc) { nx = sc; tie = true; }
     }
     next_s[c] = nx > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)nx;
+    rank[c] = i | (tie ? 0x80000000u : 0u);
 }
 
 // Per-probe decision flags (bits 31 / 30 of summ.w):
@@ -177,9 +186,13 @@ __global__ __launch_bounds__(kBlock) void chain_next_kernel(const uint32_t* __re
 //          MheCompare case), so only these probes run the exact search.
 // Every other probe collides with its chain entry: the vector stays sorted by (block,
 // first-genome start) and is partitioned with respect to such a probe.
-__global__ __launch_bounds__(kBlock) void probe_flags_kernel(uint4* __restrict__ summ, uint64_t P,
-                                                             const uint32_t* __restrict__ first_pos,
-                                                             const uint32_t* __restrict__ next_s) {
+// summ_b[q] = {chain entry's first-genome start, its length, its rank | tie}: the slot
+// an insert of this probe's chain writes, and its order among the bucket's chains.
+__global__ __launch_bounds__(kBlock) void probe_flags_kernel(uint4* __restrict__ summ, uint4* __restrict__ summ_b,
+                                                             uint64_t P, const uint32_t* __restrict__ first_pos,
+                                                             const uint32_t* __restrict__ next_s,
+                                                             const uint32_t* __restrict__ rank,
+                                                             const int64_t* __restrict__ pool, int G) {
     const uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (q >= P) return;
     uint4 r = summ[q];
@@ -187,6 +200,10 @@ __global__ __launch_bounds__(kBlock) void probe_flags_kernel(uint4* __restrict__
     const bool susp = !first && r.y >= next_s[r.z];
     r.w |= (first ? 0x80000000u : 0u) | (susp ? 0x40000000u : 0u);
     summ[q] = r;
+    const int64_t* e = pool + (uint64_t)r.z * (uint64_t)(G + 2);
+    int64_t es = 0;
+    for (int g = G - 1; g >= 0; --g) es = e[2 + g] != 0 ? e[2 + g] : es;
+    summ_b[q] = make_uint4((uint32_t)es, (uint32_t)e[0], rank[r.z], 0u);
 }
 
 // the probe of stream group k (AddHashEntry's argument), built on the rare slow path
@@ -241,16 +258,20 @@ __device__ __forceinline__ int round_first(const uint4* tb, uint32_t t, uint32_t
     return block_first_true<RB>(isnew, red);
 }
 
-// insert position of chain entry E (lower_bound of the extended copy, MemHash.cpp:247)
+// insert position of chain entry cid (lower_bound of the extended copy, MemHash.cpp:247);
+// the entries are read only for the rare undecided slots
 template <int MG>
-__device__ __forceinline__ uint32_t insert_pos(const uint4* tb, uint32_t t, const Mhe<MG>& E, uint32_t em, int64_t es,
-                                              uint32_t cid, const int64_t* __restrict__ pool, int G) {
+__device__ __forceinline__ uint32_t insert_pos(const uint4* tb, uint32_t t, uint32_t cid, uint32_t em, int64_t es,
+                                              int64_t el, const int64_t* __restrict__ pool, int G) {
+    Mhe<MG> E;
+    bool have = false;
     auto full = [&](uint32_t xid) -> bool {
+        if (!have) { load_entry<MG>(pool, cid, G, E); have = true; }
         Mhe<MG> X;
         load_entry<MG>(pool, xid, G, X);
         return mhe_less(X, E);
     };
-    return lower_bound_slots(tb, t, em, es, E.len, cid, full);
+    return lower_bound_slots(tb, t, em, es, el, cid, full);
 }
 
 // vector insert at ins (MemHash.cpp:247): shift tb[ins, t) up by one.  Each lane owns
@@ -278,13 +299,14 @@ constexpr int replay_block() { return MG <= 4 ? 1024 : (MG <= 8 ? 512 : 256); }
 template <int MG, typename View>
 __global__ __launch_bounds__(replay_block<MG>()) void replay_kernel(
     View v, GenomeTable gt, MatchParams mp, int L, const uint64_t* __restrict__ probe_info,
-    const uint4* __restrict__ summ, const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ bend,
+    const uint4* __restrict__ summ, const uint4* __restrict__ summ_b, const uint32_t* __restrict__ bstart,
+    const uint32_t* __restrict__ bend,
     uint32_t* __restrict__ tbl, uint4* __restrict__ spill, const int64_t* __restrict__ pool, uint32_t lds_cap,
     uint32_t* __restrict__ tsize, DevCounters* ctr, uint64_t* __restrict__ dbg) {
     constexpr int RB = replay_block<MG>();
     extern __shared__ uint4 s_tab[];
     __shared__ int red[RB / 64];
-    __shared__ uint32_t s_ins;
+    __shared__ uint32_t s_ins, s_rank;
     __shared__ uint4 s_new;
     uint64_t c_win = 0, c_round = 0, c_ins = 0, n_win = 0, n_round = 0, t0 = 0;
     const uint64_t t_all = dbg ? wall_clock64() : 0;
@@ -301,12 +323,24 @@ __global__ __launch_bounds__(replay_block<MG>()) void replay_kernel(
 
     // the window of probes [w0, w0 + c) stays in the lanes' registers until every
     // one of them is consumed (collided or inserted); `done` = consumed prefix
+    // A chain-first lane keeps the insert position of its chain entry up to date: an
+    // insert at ins moves it up iff ins < pos, or ins == pos and the inserted chain
+    // precedes it (rank); chains tied on their first-genome start re-search instead.
     uint4 nxt = (uint32_t)tid < K_b ? summ[beg + tid] : make_uint4(0, 0, 0, 0);
+    uint4 nxt_b = (uint32_t)tid < K_b ? summ_b[beg + tid] : make_uint4(0, 0, 0, 0);
     for (uint32_t w0 = 0; w0 < K_b; w0 += RB) {
         const uint32_t c = min((uint32_t)RB, K_b - w0);
         if (dbg) { t0 = wall_clock64(); ++n_win; }
-        const uint4 me = nxt;
-        if (w0 + RB + tid < K_b) nxt = summ[beg + w0 + RB + tid];   // prefetch the next window
+        const uint4 me = nxt, mb = nxt_b;
+        if (w0 + RB + tid < K_b) {   // prefetch the next window
+            nxt = summ[beg + w0 + RB + tid];
+            nxt_b = summ_b[beg + w0 + RB + tid];
+        }
+        const bool is_first = (uint32_t)tid < c && (me.w & 0x80000000u) && !(mb.z & 0x80000000u);
+        uint32_t mypos = 0;
+        if (is_first)
+            mypos = in_lds ? insert_pos<MG>(s_tab, t, me.z, me.x, (int64_t)mb.x, (int64_t)mb.y, pool, G)
+                           : insert_pos<MG>(spill + beg, t, me.z, me.x, (int64_t)mb.x, (int64_t)mb.y, pool, G);
         if (dbg) { __syncthreads(); c_win += wall_clock64() - t0; }
         uint32_t done = 0;
         while (done < c) {
@@ -321,13 +355,13 @@ __global__ __launch_bounds__(replay_block<MG>()) void replay_kernel(
             }
             coll += (unsigned long long)(first - (int)done);
             if (tid == first) {
-                Mhe<MG> E;
-                load_entry<MG>(pool, me.z, G, E);
-                const uint32_t em = mask_of<MG>(E, G);
-                const int64_t es = start_at(E, first_start(E));
-                s_ins = in_lds ? insert_pos<MG>(s_tab, t, E, em, es, me.z, pool, G)
-                               : insert_pos<MG>(spill + beg, t, E, em, es, me.z, pool, G);
-                s_new = make_uint4(me.z, em, (uint32_t)es, (uint32_t)E.len);
+                if (is_first)
+                    s_ins = mypos;
+                else
+                    s_ins = in_lds ? insert_pos<MG>(s_tab, t, me.z, me.x, (int64_t)mb.x, (int64_t)mb.y, pool, G)
+                                   : insert_pos<MG>(spill + beg, t, me.z, me.x, (int64_t)mb.x, (int64_t)mb.y, pool, G);
+                s_rank = mb.z & 0x7FFFFFFFu;
+                s_new = make_uint4(me.z, me.x, mb.x, mb.y);
             }
             if (in_lds && t + 1 > lds_cap) {   // spill the vector to the bucket's global slice
                 for (uint32_t k = tid; k < t; k += RB) spill[beg + k] = s_tab[k];
@@ -336,6 +370,8 @@ __global__ __launch_bounds__(replay_block<MG>()) void replay_kernel(
             __syncthreads();
             if (in_lds) shift_insert<RB>(s_tab, t, s_ins, s_new);
             else shift_insert<RB>(spill + beg, t, s_ins, s_new);
+            if (is_first && tid > first)
+                mypos += (s_ins < mypos || (s_ins == mypos && s_rank < (mb.z & 0x7FFFFFFFu))) ? 1u : 0u;
             if (dbg) c_ins += wall_clock64() - t0;
             t += 1;
             done = (uint32_t)first + 1;
@@ -426,6 +462,8 @@ hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, i
     uint32_t* vB = (uint32_t*)carve((size_t)nch * 4);
     uint32_t* first_pos = (uint32_t*)carve((size_t)nch * 4);
     uint32_t* next_s = (uint32_t*)carve((size_t)nch * 4);
+    uint32_t* rank = (uint32_t*)carve((size_t)nch * 4);
+    uint4* summ_b = (uint4*)summ + (P + 1);
     const unsigned pgrid = (unsigned)((P + kBlock - 1) / kBlock), cgrid = (nch + kBlock - 1) / kBlock;
     hipError_t e = hipMemsetAsync(first_pos, 0xFF, (size_t)nch * 4, st);
     if (e != hipSuccess) return e;
@@ -449,16 +487,18 @@ hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, i
     if ((e = radix_sort<uint64_t>(key_g, vin, nch, 64, kA, vout, kB, vin, d_radix_tmp, &buf2, st)) != hipSuccess)
         return e;
     const uint32_t* ord = buf2 ? vin : vout;
-    hipLaunchKernelGGL(chain_next_kernel, dim3(cgrid), dim3(kBlock), 0, st, ord, key_s, key_b, nch, next_s);
+    hipLaunchKernelGGL(chain_next_kernel, dim3(cgrid), dim3(kBlock), 0, st, ord, key_s, key_b, nch, next_s, rank);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(probe_flags_kernel, dim3(pgrid), dim3(kBlock), 0, st, (uint4*)summ, P, first_pos, next_s);
+    hipLaunchKernelGGL(probe_flags_kernel, dim3(pgrid), dim3(kBlock), 0, st, (uint4*)summ, summ_b, P, first_pos,
+                       next_s, rank, pool, gt.G);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const size_t lds = (size_t)lds_cap * sizeof(uint4);
     e = hipFuncSetAttribute((const void*)replay_kernel<MG, View>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((replay_kernel<MG, View>), dim3(mp.table_size), dim3(replay_block<MG>()), lds, st, v, gt, mp, L,
-                       probe_info, (const uint4*)summ, bstart, bend, tbl, (uint4*)spill, pool, lds_cap, tsize,
+                       probe_info, (const uint4*)summ, (const uint4*)summ_b, bstart, bend, tbl, (uint4*)spill,
+                       pool, lds_cap, tsize,
                        (DevCounters*)ctr, dbg);
     return hipGetLastError();
 }
