@@ -296,14 +296,15 @@ __device__ __forceinline__ void shift_insert(uint4* tb, uint32_t t, uint32_t ins
 template <int MG>
 constexpr int replay_block() { return MG <= 4 ? 1024 : (MG <= 8 ? 512 : 256); }
 
-template <int MG, typename View>
-__global__ __launch_bounds__(replay_block<MG>()) void replay_kernel(
+// RB lanes per bucket; the kernel takes the buckets with kmin < probes <= kmax (small
+// buckets run as single waves: their rounds cost no workgroup barriers).
+template <int MG, int RB, typename View>
+__global__ __launch_bounds__(RB) void replay_kernel(
     View v, GenomeTable gt, MatchParams mp, int L, const uint64_t* __restrict__ probe_info,
     const uint4* __restrict__ summ, const uint4* __restrict__ summ_b, const uint32_t* __restrict__ bstart,
     const uint32_t* __restrict__ bend,
     uint32_t* __restrict__ tbl, uint4* __restrict__ spill, const int64_t* __restrict__ pool, uint32_t lds_cap,
-    uint32_t* __restrict__ tsize, DevCounters* ctr, uint64_t* __restrict__ dbg) {
-    constexpr int RB = replay_block<MG>();
+    uint32_t* __restrict__ tsize, DevCounters* ctr, uint64_t* __restrict__ dbg, uint32_t kmin, uint32_t kmax) {
     extern __shared__ uint4 s_tab[];
     __shared__ int red[RB / 64];
     __shared__ uint32_t s_ins, s_rank;
@@ -315,7 +316,7 @@ __global__ __launch_bounds__(replay_block<MG>()) void replay_kernel(
     const uint32_t b = blockIdx.x;
     const uint32_t beg = bstart[b];
     const uint32_t K_b = bend[b] - beg;
-    if (K_b == 0) return;
+    if (K_b <= kmin || K_b > kmax) return;
     const int G = gt.G;
     bool in_lds = true;
     uint32_t t = 0;
@@ -492,14 +493,21 @@ hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, i
     hipLaunchKernelGGL(probe_flags_kernel, dim3(pgrid), dim3(kBlock), 0, st, (uint4*)summ, summ_b, P, first_pos,
                        next_s, rank, pool, gt.G);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    // buckets of <= 64 probes: one wave each; the rest: one big workgroup each
+    constexpr uint32_t kSmall = 64;
+    hipLaunchKernelGGL((replay_kernel<MG, 64, View>), dim3(mp.table_size), dim3(64), kSmall * sizeof(uint4), st, v, gt,
+                       mp, L, probe_info, (const uint4*)summ, (const uint4*)summ_b, bstart, bend, tbl, (uint4*)spill,
+                       pool, kSmall, tsize, (DevCounters*)ctr, dbg, 0u, kSmall);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (lds_cap <= kSmall) return hipSuccess;   // lds_cap = min(fullest bucket, LDS slots)
+    constexpr int RB = replay_block<MG>();
     const size_t lds = (size_t)lds_cap * sizeof(uint4);
-    e = hipFuncSetAttribute((const void*)replay_kernel<MG, View>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    e = hipFuncSetAttribute((const void*)replay_kernel<MG, RB, View>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((replay_kernel<MG, View>), dim3(mp.table_size), dim3(replay_block<MG>()), lds, st, v, gt, mp, L,
-                       probe_info, (const uint4*)summ, (const uint4*)summ_b, bstart, bend, tbl, (uint4*)spill,
-                       pool, lds_cap, tsize,
-                       (DevCounters*)ctr, dbg);
+    hipLaunchKernelGGL((replay_kernel<MG, RB, View>), dim3(mp.table_size), dim3(RB), lds, st, v, gt, mp, L, probe_info,
+                       (const uint4*)summ, (const uint4*)summ_b, bstart, bend, tbl, (uint4*)spill, pool, lds_cap,
+                       tsize, (DevCounters*)ctr, dbg, kSmall, 0xFFFFFFFFu);
     return hipGetLastError();
 }
 
