@@ -22,7 +22,8 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmums_hip.so")
+# MUMS_DEV_LIB: development builds of the same sources (libmems_amd/Makefile EXTRA=...)
+LIB_PATH = os.environ.get("MUMS_DEV_LIB") or os.path.join(_HERE, "libmums_hip.so")
 
 MUMS_OK = 0
 MUMS_E_INVALID = -1

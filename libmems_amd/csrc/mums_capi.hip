@@ -334,7 +334,7 @@ int merge_stage(mums_ctx* ctx, uint64_t n, int mb, int key_bits, const MatchPara
     HIPCHK(build_seg_tiles_from_starts(bstart, mb, n, tiles, &dc->ntiles, ctx->tmp.p, st));
     int buf = 0;
     if (ctx->use_onesweep && n < (1ull << 30) && key_bits <= 32)
-        HIPCHK(seg_onesweep_sort(ctx->recA.as<uint64_t>(), ctx->recB.as<uint64_t>(), n, key_bits, mb, tiles, ub, bstart,
+        HIPCHK(seg_onesweep_sort(ctx->recA.as<uint64_t>(), ctx->recB.as<uint64_t>(), n, key_bits, mb, bstart,
                                  ctx->tmp.p, &dc->err, &buf, st, prof ? ctx->ev_ds : nullptr));
     else
         HIPCHK(seg_radix_sort(ctx->recA.as<uint64_t>(), ctx->recB.as<uint64_t>(), n, key_bits, tiles, ub, ctx->tmp.p,

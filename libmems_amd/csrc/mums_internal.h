@@ -155,7 +155,7 @@ hipError_t radix_sort(const K* keys_in, const uint32_t* vals_in, uint64_t n, int
 
 // radix_seg.hip: segmented tiles + stable LSD sort of packed records on bits
 // [32, 32 + key_bits) inside each MSD bucket.
-uint64_t seg_tiles_upper(uint64_t n, int msd_bits);
+uint64_t seg_tiles_upper(uint64_t n, int msd_bits, uint32_t tile = kSegTile);
 size_t seg_tmp_bytes(uint64_t n, int msd_bits);
 // chunks[3c .. 3c+2] = {src_off, dst_off, len}, sorted by dst_off, tiling [0, n)
 hipError_t launch_regroup(const uint64_t* src, uint64_t* dst, const uint64_t* d_chunks, uint32_t nchunks, uint64_t n,
@@ -163,7 +163,7 @@ hipError_t launch_regroup(const uint64_t* src, uint64_t* dst, const uint64_t* d_
 hipError_t seg_bucket_starts(const uint32_t* d_hist_scanned, uint32_t T, int msd_bits, uint64_t n, uint32_t* bstart,
                              hipStream_t st);
 hipError_t build_seg_tiles_from_starts(const uint32_t* bstart, int msd_bits, uint64_t n, SegTile* d_tiles,
-                                       uint32_t* d_ntiles, void* d_tmp, hipStream_t st);
+                                       uint32_t* d_ntiles, void* d_tmp, hipStream_t st, uint32_t tile = kSegTile);
 hipError_t build_seg_tiles(const uint32_t* d_hist_scanned, uint32_t T, int msd_bits, uint64_t n, SegTile* d_tiles,
                            uint32_t* d_ntiles, uint32_t* d_bstart, void* d_tmp, hipStream_t st);
 hipError_t seg_radix_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key_bits, const SegTile* d_tiles,
@@ -173,8 +173,8 @@ hipError_t seg_radix_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key_bi
 // pass with decoupled look-back between consecutive tiles of a bucket.
 size_t onesweep_tmp_bytes(uint64_t n, int msd_bits, int key_bits);
 hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key_bits, int msd_bits,
-                             const SegTile* d_tiles, uint64_t ntiles_ub, const uint32_t* d_bstart, void* d_tmp,
-                             uint32_t* d_err, int* out_buf, hipStream_t st, hipEvent_t* ev_ds = nullptr);
+                             const uint32_t* d_bstart, void* d_tmp, uint32_t* d_err, int* out_buf, hipStream_t st,
+                             hipEvent_t* ev_ds = nullptr);
 
 // groups.hip
 uint64_t group_slot_count(uint64_t ntiles);

@@ -12,6 +12,8 @@
 // Per pass: upsweep (tile digit histogram), scan, downsweep (wave64 ballot match-any
 // ranking, LDS reorder, digit-run-contiguous stores).
 // HBM bytes per record per pass: upsweep 8, downsweep 8 + 8.
+#include <algorithm>
+
 #include "mums_internal.h"
 
 namespace mums {
@@ -22,7 +24,17 @@ constexpr int kTile = kSegTile;
 constexpr int kRounds = kTile / kBlock;  // 16
 constexpr int kWaves = kBlock / 64;
 constexpr int kDigits = 256;
-constexpr int kOnesweepIPT = kTile / kBlock;   // records per thread per onesweep tile (tile = kSegTile)
+#ifndef MUMS_SORT_BLOCK
+#define MUMS_SORT_BLOCK 512
+#endif
+#ifndef MUMS_SORT_TILE
+#define MUMS_SORT_TILE 8192
+#endif
+#ifndef MUMS_SORT_PERSIST
+#define MUMS_SORT_PERSIST 0
+#endif
+constexpr int kSortBlock = MUMS_SORT_BLOCK;    // threads per onesweep block
+constexpr int kSortTile = MUMS_SORT_TILE;      // records per onesweep tile (longer digit runs per store)
 #ifndef MUMS_LOOKBACK
 #define MUMS_LOOKBACK 4
 #endif
@@ -43,10 +55,11 @@ __global__ void bucket_starts_kernel(const uint32_t* __restrict__ scanned, uint3
 }
 
 // tiles per bucket from bucket starts (tfirst[nb] = 0 so one scan gives the total)
-__global__ void ntb_from_starts_kernel(const uint32_t* __restrict__ bstart, int nb, uint32_t* __restrict__ ntb) {
+__global__ void ntb_from_starts_kernel(const uint32_t* __restrict__ bstart, int nb, uint32_t tile,
+                                       uint32_t* __restrict__ ntb) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b > nb) return;
-    ntb[b] = (b == nb) ? 0u : (uint32_t)(((uint64_t)bstart[b + 1] - bstart[b] + kTile - 1) / kTile);
+    ntb[b] = (b == nb) ? 0u : (uint32_t)(((uint64_t)bstart[b + 1] - bstart[b] + tile - 1) / tile);
 }
 
 __global__ void single_bucket_kernel(uint64_t n, uint32_t* __restrict__ bstart) {
@@ -57,7 +70,8 @@ __global__ void single_bucket_kernel(uint64_t n, uint32_t* __restrict__ bstart) 
 }
 
 __global__ void tiles_kernel(const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ tfirst, int nb,
-                             uint64_t ub, SegTile* __restrict__ tiles, uint32_t* __restrict__ ntiles_out) {
+                             uint64_t ub, uint32_t tile, SegTile* __restrict__ tiles,
+                             uint32_t* __restrict__ ntiles_out) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ub) return;
     const uint32_t total = tfirst[nb];
@@ -75,9 +89,9 @@ __global__ void tiles_kernel(const uint32_t* __restrict__ bstart, const uint32_t
         const uint32_t ntb = tfirst[lo + 1] - tfirst[lo];
         d.bstart = bstart[lo];
         d.bend = bstart[lo + 1];
-        d.start = d.bstart + (uint64_t)tb * kTile;
+        d.start = d.bstart + (uint64_t)tb * tile;
         const uint64_t rem = d.bend - d.start;
-        d.count = (uint32_t)(rem < (uint64_t)kTile ? rem : (uint64_t)kTile);
+        d.count = (uint32_t)(rem < (uint64_t)tile ? rem : (uint64_t)tile);
         d.hbase = tfirst[lo] * kDigits;
         d.ntb = ntb;
         d.tb = tb;
@@ -305,33 +319,36 @@ __device__ __forceinline__ void onesweep_load(const uint64_t* __restrict__ rin, 
 
 // One onesweep pass; each block claims one tile from an atomic counter (claim
 // order = tiles[c].order, see claim_order_kernel), so every tile it waits on was
-// claimed earlier by a resident block.
-template <int kIPT>
-__global__ __launch_bounds__(kBlock) void seg_onesweep_kernel(const uint64_t* __restrict__ rin,
-                                                              uint64_t* __restrict__ rout,
-                                                              const SegTile* __restrict__ tiles, uint32_t nclaims,
-                                                              int shift, int pass, int npass,
-                                                              const uint32_t* __restrict__ dbase, uint32_t* status,
-                                                              uint32_t* tile_counter, uint32_t* err) {
-    constexpr int kT = kIPT * kBlock;
+// claimed earlier by a resident block.  OB threads x kIPT records per tile; the first
+// 256 threads also own one digit each for the look-back and the digit starts.
+template <int OB, int kIPT>
+__global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __restrict__ rin,
+                                                          uint64_t* __restrict__ rout,
+                                                          const SegTile* __restrict__ tiles, uint32_t nclaims,
+                                                          int shift, int pass, int npass,
+                                                          const uint32_t* __restrict__ dbase, uint32_t* status,
+                                                          uint32_t* tile_counter, uint32_t* err) {
+    constexpr int kT = kIPT * OB;
+    constexpr int kW = OB / 64;
+    static_assert(OB >= kDigits, "one thread per digit");
     __shared__ uint64_t srec[kT];
-    __shared__ uint32_t wcnt[kWaves][kDigits];
+    __shared__ uint32_t wcnt[kW][kDigits];
     __shared__ uint32_t lstart[kDigits];
     __shared__ uint32_t gofs[kDigits];
-    __shared__ uint32_t s_w[kWaves];
+    __shared__ uint32_t s_w[kDigits / 64];
     __shared__ uint32_t s_tile;
     __shared__ uint32_t hcnt[kDigits];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     if (tid == 0) s_tile = atomicAdd(tile_counter, 1u);
-    for (int i = tid; i < kWaves * kDigits; i += kBlock) (&wcnt[0][0])[i] = 0;
-    hcnt[tid] = 0;
+    for (int i = tid; i < kW * kDigits; i += OB) (&wcnt[0][0])[i] = 0;
+    if (tid < kDigits) hcnt[tid] = 0;
     __syncthreads();
     const uint32_t c = __builtin_amdgcn_readfirstlane(s_tile);   // uniform: scalar descriptor loads
     if (c >= nclaims) return;
     const uint32_t t = __builtin_amdgcn_readfirstlane(tiles[c].order);
     const SegTile d = tiles[t];
     if (d.count == 0) return;
-    const uint32_t q0 = wv * (kT / kWaves);
+    const uint32_t q0 = wv * (kT / kW);
     uint64_t key[kIPT];
     uint32_t rank[kIPT];
     #pragma unroll
@@ -347,7 +364,7 @@ __global__ __launch_bounds__(kBlock) void seg_onesweep_kernel(const uint64_t* __
         if (q < d.count) atomicAdd(&hcnt[(uint32_t)(key[r] >> shift) & 0xFFu], 1u);
     }
     __syncthreads();
-    if (d.tb != 0)
+    if (d.tb != 0 && tid < kDigits)
         __hip_atomic_store(status + (uint64_t)t * kDigits + tid, kFlagAgg | hcnt[tid], __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     #pragma unroll
@@ -363,11 +380,11 @@ __global__ __launch_bounds__(kBlock) void seg_onesweep_kernel(const uint64_t* __
         rank[r] = old + rk;
     }
     __syncthreads();
-    {
+    uint32_t v = 0, acc = 0;
+    if (tid < kDigits) {
         const int dg = tid;  // digit
-        uint32_t acc = 0;
         #pragma unroll
-        for (int w = 0; w < kWaves; ++w) { const uint32_t x = wcnt[w][dg]; wcnt[w][dg] = acc; acc += x; }
+        for (int w = 0; w < kW; ++w) { const uint32_t x = wcnt[w][dg]; wcnt[w][dg] = acc; acc += x; }
         // look back over the bucket's preceding tiles, then publish the inclusive prefix
         uint32_t* st = status + (uint64_t)t * kDigits + dg;
         uint32_t prefix = 0;
@@ -411,18 +428,20 @@ __global__ __launch_bounds__(kBlock) void seg_onesweep_kernel(const uint64_t* __
         }
         gofs[dg] = dbase[((uint64_t)d.bucket * npass + pass) * kDigits + dg] + prefix;
         // block-local digit starts
-        uint32_t v = acc;
+        v = acc;
         #pragma unroll
         for (int dd = 1; dd < 64; dd <<= 1) {
             const uint32_t x = __shfl_up(v, dd, 64);
             if (lane >= dd) v += x;
         }
         if (lane == 63) s_w[wv] = v;
-        __syncthreads();
+    }
+    __syncthreads();
+    if (tid < kDigits) {
         uint32_t wpre = 0;
         #pragma unroll
-        for (int w = 0; w < kWaves; ++w) wpre += (w < wv) ? s_w[w] : 0u;
-        lstart[dg] = wpre + v - acc;
+        for (int w = 0; w < kDigits / 64; ++w) wpre += (w < wv) ? s_w[w] : 0u;
+        lstart[tid] = wpre + v - acc;
     }
     __syncthreads();
     #pragma unroll
@@ -436,7 +455,7 @@ __global__ __launch_bounds__(kBlock) void seg_onesweep_kernel(const uint64_t* __
     __syncthreads();
     #pragma unroll
     for (int r = 0; r < kIPT; ++r) {
-        const uint32_t sidx = tid + r * kBlock;
+        const uint32_t sidx = tid + r * OB;
         if (sidx < d.count) {
             const uint64_t k = srec[sidx];
             const uint32_t dg = (uint32_t)(k >> shift) & 0xFFu;
@@ -445,9 +464,179 @@ __global__ __launch_bounds__(kBlock) void seg_onesweep_kernel(const uint64_t* __
     }
 }
 
+
+// Persistent onesweep pass: a resident grid of blocks, each claiming tiles in claim
+// order from the counter until none is left.  The next tile's records are loaded
+// right after the current tile's look-back, so their HBM latency overlaps the current
+// tile's LDS reorder and stores.  A block holds at most its current tile and the one
+// after it; the earliest unfinished claim is always a current tile whose predecessors
+// are all finished, so the look-back chain always progresses.
+template <int OB, int kIPT>
+__global__ __launch_bounds__(OB) __attribute__((amdgpu_waves_per_eu(4))) void seg_onesweep_persist_kernel(const uint64_t* __restrict__ rin,
+                                                                  uint64_t* __restrict__ rout,
+                                                                  const SegTile* __restrict__ tiles,
+                                                                  uint32_t nclaims, int shift, int pass, int npass,
+                                                                  const uint32_t* __restrict__ dbase,
+                                                                  uint32_t* status, uint32_t* tile_counter,
+                                                                  uint32_t* err) {
+    constexpr int kT = kIPT * OB;
+    constexpr int kW = OB / 64;
+    static_assert(OB >= kDigits, "one thread per digit");
+    __shared__ uint64_t srec[kT];
+    __shared__ uint32_t wcnt[kW][kDigits];
+    __shared__ uint32_t lstart[kDigits];
+    __shared__ uint32_t gofs[kDigits];
+    __shared__ uint32_t s_w[kDigits / 64];
+    __shared__ uint32_t s_tile[2];
+    __shared__ uint32_t hcnt[kDigits];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t q0 = wv * (kT / kW);
+    if (tid == 0) s_tile[0] = atomicAdd(tile_counter, 1u);
+    __syncthreads();
+    uint32_t c = __builtin_amdgcn_readfirstlane(s_tile[0]);
+    uint64_t key[kIPT];
+    uint32_t rank[kIPT];
+    SegTile d{};
+    uint32_t t = 0;
+    if (c < nclaims) {
+        t = __builtin_amdgcn_readfirstlane(tiles[c].order);
+        d = tiles[t];
+        #pragma unroll
+        for (int r = 0; r < kIPT; ++r) {
+            const uint32_t q = q0 + r * 64 + lane;
+            key[r] = q < d.count ? rin[d.start + q] : 0ull;
+        }
+    }
+    int par = 0;
+    while (c < nclaims) {
+        // claim the next tile now (its id is needed before the prefetch below)
+        if (tid == 0) s_tile[par ^ 1] = atomicAdd(tile_counter, 1u);
+        for (int i = tid; i < kW * kDigits; i += OB) (&wcnt[0][0])[i] = 0;
+        if (tid < kDigits) hcnt[tid] = 0;
+        __syncthreads();
+        const uint32_t cn = __builtin_amdgcn_readfirstlane(s_tile[par ^ 1]);
+        #pragma unroll
+        for (int r = 0; r < kIPT; ++r) {
+            const uint32_t q = q0 + r * 64 + lane;
+            if (q < d.count) atomicAdd(&hcnt[(uint32_t)(key[r] >> shift) & 0xFFu], 1u);
+        }
+        __syncthreads();
+        if (d.tb != 0 && tid < kDigits)
+            __hip_atomic_store(status + (uint64_t)t * kDigits + tid, kFlagAgg | hcnt[tid], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        #pragma unroll
+        for (int r = 0; r < kIPT; ++r) {
+            const uint32_t q = q0 + r * 64 + lane;
+            const bool valid = q < d.count;
+            const uint32_t dg = (uint32_t)(key[r] >> shift) & 0xFFu;
+            uint32_t tot;
+            const uint32_t rk = wave_match_rank<8>(dg, valid, &tot);
+            uint32_t old = 0;
+            if (valid) old = wcnt[wv][dg];
+            if (valid && rk == 0) wcnt[wv][dg] = old + tot;
+            rank[r] = old + rk;
+        }
+        __syncthreads();
+        uint32_t v = 0, acc = 0;
+        if (tid < kDigits) {
+            const int dg = tid;
+            #pragma unroll
+            for (int w = 0; w < kW; ++w) { const uint32_t x = wcnt[w][dg]; wcnt[w][dg] = acc; acc += x; }
+            uint32_t* st = status + (uint64_t)t * kDigits + dg;
+            uint32_t prefix = 0;
+            if (d.tb == 0) {
+                __hip_atomic_store(st, kFlagInc | acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                const int64_t tfirst = (int64_t)t - (int64_t)d.tb;
+                int64_t j = (int64_t)t - 1;
+                uint32_t spins = 0;
+                bool done = false;
+                while (!done) {
+                    uint32_t sv[kLookback];
+                    #pragma unroll
+                    for (int k = 0; k < kLookback; ++k)
+                        sv[k] = (j - k >= tfirst) ? __hip_atomic_load(status + (uint64_t)(j - k) * kDigits + dg,
+                                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                                  : kFlagInc;
+                    int used = 0;
+                    bool stall = false;
+                    #pragma unroll
+                    for (int k = 0; k < kLookback; ++k) {
+                        if (done || stall) continue;
+                        const uint32_t sx = sv[k];
+                        if ((sx >> 30) == 0u) { stall = true; continue; }
+                        prefix += sx & kValMask;
+                        ++used;
+                        if ((sx & kFlagInc) != 0u) done = true;
+                    }
+                    j -= used;
+                    if (stall && !done) {
+                        if (++spins > (1u << 24)) { atomicOr(err, 2u); break; }
+                        if (spins < 8) __builtin_amdgcn_s_sleep(1);
+                        else __builtin_amdgcn_s_sleep(8);
+                    }
+                }
+                __hip_atomic_store(st, kFlagInc | ((prefix + acc) & kValMask), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+            gofs[dg] = dbase[((uint64_t)d.bucket * npass + pass) * kDigits + dg] + prefix;
+            v = acc;
+            #pragma unroll
+            for (int dd = 1; dd < 64; dd <<= 1) {
+                const uint32_t x = __shfl_up(v, dd, 64);
+                if (lane >= dd) v += x;
+            }
+            if (lane == 63) s_w[wv] = v;
+        }
+        __syncthreads();
+        if (tid < kDigits) {
+            uint32_t wpre = 0;
+            #pragma unroll
+            for (int w = 0; w < kDigits / 64; ++w) wpre += (w < wv) ? s_w[w] : 0u;
+            lstart[tid] = wpre + v - acc;
+        }
+        __syncthreads();
+        #pragma unroll
+        for (int r = 0; r < kIPT; ++r) {
+            const uint32_t q = q0 + r * 64 + lane;
+            if (q < d.count) {
+                const uint32_t dg = (uint32_t)(key[r] >> shift) & 0xFFu;
+                srec[lstart[dg] + wcnt[wv][dg] + rank[r]] = key[r];
+            }
+        }
+        // prefetch the next tile's records into the key registers (now free)
+        SegTile dn{};
+        uint32_t tn = 0;
+        if (cn < nclaims) {
+            tn = __builtin_amdgcn_readfirstlane(tiles[cn].order);
+            dn = tiles[tn];
+            #pragma unroll
+            for (int r = 0; r < kIPT; ++r) {
+                const uint32_t q = q0 + r * 64 + lane;
+                key[r] = q < dn.count ? rin[dn.start + q] : 0ull;
+            }
+        }
+        __syncthreads();
+        #pragma unroll
+        for (int r = 0; r < kIPT; ++r) {
+            const uint32_t sidx = tid + r * OB;
+            if (sidx < d.count) {
+                const uint64_t k = srec[sidx];
+                const uint32_t dg = (uint32_t)(k >> shift) & 0xFFu;
+                rout[(uint64_t)gofs[dg] + (sidx - lstart[dg])] = k;
+            }
+        }
+        __syncthreads();   // srec / gofs / lstart are rewritten by the next tile
+        c = cn;
+        d = dn;
+        t = tn;
+        par ^= 1;
+    }
+}
+
 }  // namespace
 
-uint64_t seg_tiles_upper(uint64_t n, int msd_bits) { return (n + kTile - 1) / kTile + (1ull << msd_bits) + 1; }
+uint64_t seg_tiles_upper(uint64_t n, int msd_bits, uint32_t tile) { return (n + tile - 1) / tile + (1ull << msd_bits) + 1; }
 
 size_t seg_tmp_bytes(uint64_t n, int msd_bits) {
     const uint64_t ub = seg_tiles_upper(n, msd_bits);
@@ -502,17 +691,17 @@ hipError_t seg_bucket_starts(const uint32_t* d_hist_scanned, uint32_t T, int msd
 }
 
 hipError_t build_seg_tiles_from_starts(const uint32_t* bstart, int msd_bits, uint64_t n, SegTile* d_tiles,
-                                       uint32_t* d_ntiles, void* d_tmp, hipStream_t st) {
+                                       uint32_t* d_ntiles, void* d_tmp, hipStream_t st, uint32_t tile) {
     const int nb = 1 << msd_bits;
-    const uint64_t ub = seg_tiles_upper(n, msd_bits);
+    const uint64_t ub = seg_tiles_upper(n, msd_bits, tile);
     uint32_t* tfirst = (uint32_t*)d_tmp;
     void* stmp = (void*)(tfirst + nb + 64);
-    hipLaunchKernelGGL(ntb_from_starts_kernel, dim3((nb + 256) / 256), dim3(256), 0, st, bstart, nb, tfirst);
+    hipLaunchKernelGGL(ntb_from_starts_kernel, dim3((nb + 256) / 256), dim3(256), 0, st, bstart, nb, tile, tfirst);
     // tfirst[b] = exclusive scan of tiles per bucket; tfirst[nb] = total
     hipError_t e = exclusive_scan_u32(tfirst, (uint64_t)nb + 1, stmp, nullptr, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(tiles_kernel, dim3((unsigned)((ub + 255) / 256)), dim3(256), 0, st, bstart, tfirst, nb, ub,
-                       d_tiles, d_ntiles);
+                       tile, d_tiles, d_ntiles);
     hipLaunchKernelGGL(claim_order_kernel, dim3((unsigned)((ub + 255) / 256)), dim3(256), 0, st, tfirst, nb, ub,
                        d_tiles);
     return hipGetLastError();
@@ -526,39 +715,66 @@ hipError_t build_seg_tiles(const uint32_t* d_hist_scanned, uint32_t T, int msd_b
     return build_seg_tiles_from_starts(bstart, msd_bits, n, d_tiles, d_ntiles, d_tmp, st);
 }
 
+// d_tmp layout: status [npass][ub][256] | ghist [nb][npass][256] | dbase [nb][npass][256]
+// | counters [npass] (all zeroed per sort) | sort tiles [ub] | tile-build scratch
 size_t onesweep_tmp_bytes(uint64_t n, int msd_bits, int key_bits) {
-    const uint64_t ub = seg_tiles_upper(n, msd_bits);
+    const uint64_t ub = seg_tiles_upper(n, msd_bits, kSortTile);
     const int npass = (key_bits + 7) / 8;
     const uint64_t nb = 1ull << msd_bits;
-    return (ub * kDigits * (uint64_t)npass + 2 * nb * npass * kDigits + 64 + 64) * 4 + 4096;
+    return (ub * kDigits * (uint64_t)npass + 2 * nb * npass * kDigits + 64 + 64) * 4 + ub * sizeof(SegTile) + 256 +
+           (nb + 128) * 4 + scan_tmp_bytes(nb + 1) + 4096;
 }
 
 hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key_bits, int msd_bits,
-                             const SegTile* d_tiles, uint64_t ntiles_ub, const uint32_t* d_bstart, void* d_tmp,
-                             uint32_t* d_err, int* out_buf, hipStream_t st, hipEvent_t* ev_ds) {
+                             const uint32_t* d_bstart, void* d_tmp, uint32_t* d_err, int* out_buf, hipStream_t st,
+                             hipEvent_t* ev_ds) {
     const int npass = (key_bits + 7) / 8;
     *out_buf = npass % 2;
     if (n == 0 || npass == 0) return hipSuccess;
     if (npass > 4) return hipErrorInvalidValue;
     const uint64_t nb = 1ull << msd_bits;
+    const uint64_t ub = seg_tiles_upper(n, msd_bits, kSortTile);
     uint32_t* status = (uint32_t*)d_tmp;                       // [npass][ub][256]
-    uint32_t* ghist = status + ub_status(ntiles_ub, npass);    // [nb][npass][256]
+    uint32_t* ghist = status + ub_status(ub, npass);           // [nb][npass][256]
     uint32_t* dbase = ghist + nb * npass * kDigits;            // [nb][npass][256]
-    uint32_t* counters = dbase + nb * npass * kDigits;         // [npass]
+    uint32_t* counters = dbase + nb * npass * kDigits;         // [npass] + ntiles
     const size_t zero_bytes = ((uint64_t)(counters - status) + 64) * 4;
+    SegTile* stiles = (SegTile*)((char*)d_tmp + ((zero_bytes + 255) & ~(size_t)255));
+    void* btmp = (void*)((char*)stiles + ((ub * sizeof(SegTile) + 255) & ~(size_t)255));
     hipError_t e = hipMemsetAsync(status, 0, zero_bytes, st);
     if (e != hipSuccess) return e;
-    const unsigned gblocks = (unsigned)((ntiles_ub + kGhistTilesPerBlock - 1) / kGhistTilesPerBlock);
-    hipLaunchKernelGGL(seg_ghist_kernel, dim3(gblocks), dim3(kBlock), 0, st, recA, d_tiles, ntiles_ub, npass, ghist);
+    e = build_seg_tiles_from_starts(d_bstart, msd_bits, n, stiles, counters + 32, btmp, st, kSortTile);
+    if (e != hipSuccess) return e;
+    const unsigned gblocks = (unsigned)((ub + kGhistTilesPerBlock - 1) / kGhistTilesPerBlock);
+    hipLaunchKernelGGL(seg_ghist_kernel, dim3(gblocks), dim3(kBlock), 0, st, recA, stiles, ub, npass, ghist);
     hipLaunchKernelGGL(seg_dbase_kernel, dim3((unsigned)(nb * npass)), dim3(kBlock), 0, st, ghist, d_bstart, npass,
                        dbase);
+#if MUMS_SORT_PERSIST
+    // resident blocks of the persistent pass: occupancy x CUs
+    static uint64_t persist_grid = 0;
+    if (persist_grid == 0) {
+        int dev = 0, cus = 0, per = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per, (const void*)seg_onesweep_persist_kernel<kSortBlock, kSortTile / kSortBlock>, kSortBlock, 0);
+        persist_grid = (uint64_t)std::max(cus, 1) * (uint64_t)std::max(per, 1);
+    }
+#endif
     uint64_t* src = recA;
     uint64_t* dst = recB;
     for (int p = 0; p < npass; ++p) {
         if (ev_ds) (void)hipEventRecord(ev_ds[2 * p], st);
-        hipLaunchKernelGGL(seg_onesweep_kernel<kOnesweepIPT>, dim3((unsigned)ntiles_ub), dim3(kBlock), 0, st, src,
-                           dst, d_tiles, (uint32_t)ntiles_ub, 32 + 8 * p, p, npass, dbase,
-                           status + (uint64_t)p * ntiles_ub * kDigits, counters + p, d_err);
+#if MUMS_SORT_PERSIST
+        hipLaunchKernelGGL((seg_onesweep_persist_kernel<kSortBlock, kSortTile / kSortBlock>),
+                           dim3((unsigned)std::min<uint64_t>(ub, persist_grid)), dim3(kSortBlock), 0, st, src, dst,
+                           stiles, (uint32_t)ub, 32 + 8 * p, p, npass, dbase, status + (uint64_t)p * ub * kDigits,
+                           counters + p, d_err);
+#else
+        hipLaunchKernelGGL((seg_onesweep_kernel<kSortBlock, kSortTile / kSortBlock>), dim3((unsigned)ub),
+                           dim3(kSortBlock), 0, st, src, dst, stiles, (uint32_t)ub, 32 + 8 * p, p, npass, dbase,
+                           status + (uint64_t)p * ub * kDigits, counters + p, d_err);
+#endif
         e = hipGetLastError();
         if (e != hipSuccess) return e;
         if (ev_ds) (void)hipEventRecord(ev_ds[2 * p + 1], st);
