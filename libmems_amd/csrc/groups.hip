@@ -182,11 +182,11 @@ __global__ __launch_bounds__(kBlock) void probe_tile_rec_kernel(const uint64_t* 
                                                                 uint32_t* __restrict__ slot_bucket,
                                                                 DevCounters* __restrict__ ctr) {
     __shared__ uint64_t srec[kGTile];
-    __shared__ uint16_t heads[kGTile];
-    __shared__ uint32_t wcnt[kGRounds][kBlock / 64];
+    __shared__ uint16_t heads[kSlots];     // heads of groups of >= 2 records (<= kGTile / 2)
+    __shared__ uint32_t wcnt[kGRounds * (kBlock / 64)];
     __shared__ uint32_t s_w[kBlock / 64];
     __shared__ uint32_t s_red[2];
-    __shared__ uint64_t s_prev;
+    __shared__ uint64_t s_prev, s_next;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const SegTile td = tiles[blockIdx.x];
     if (td.count == 0) {
@@ -200,8 +200,9 @@ __global__ __launch_bounds__(kBlock) void probe_tile_rec_kernel(const uint64_t* 
     const uint32_t cnt = td.count;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 
-    // 1) stage the tile (lane-contiguous, coalesced) + the record before it.  The loads
-    //    use clamped indices so all kGRounds are in flight before the first LDS store.
+    // 1) stage the tile (lane-contiguous, coalesced) + the records just before and after
+    //    it.  The loads use clamped indices so all kGRounds are in flight before the
+    //    first LDS store.
     {
         uint64_t x[kGRounds];
         #pragma unroll
@@ -216,36 +217,47 @@ __global__ __launch_bounds__(kBlock) void probe_tile_rec_kernel(const uint64_t* 
         }
     }
     if (threadIdx.x == 0) s_prev = (tile0 > td.bstart) ? rec[tile0 - 1] : ~0ull;
+    if (threadIdx.x == 64) s_next = (tile0 + cnt < td.bend) ? rec[tile0 + cnt] : ~0ull;
     __syncthreads();
 
-    // 2) heads in stream order
-    uint32_t hmask = 0;
+    // 2) group heads in stream order; a head is kept only when its group has >= 2
+    //    records (a single record is never an AddHashEntry call)
+    uint32_t hmask = 0, ngrp = 0;
     #pragma unroll
     for (int r = 0; r < kGRounds; ++r) {
         const uint32_t q = r * kBlock + threadIdx.x;
-        bool head = false;
+        bool keep = false;
         if (q < cnt) {
             const uint64_t here = srec[q] >> 33;
-            if (q == 0) head = (tile0 == td.bstart) || (here != (s_prev >> 33));
-            else head = here != (srec[q - 1] >> 33);
+            const uint64_t prev = (q == 0) ? ((tile0 == td.bstart) ? ~0ull : (s_prev >> 33)) : (srec[q - 1] >> 33);
+            const uint64_t next = (q + 1 < cnt) ? (srec[q + 1] >> 33) : (s_next >> 33);
+            const bool head = (q == 0 && tile0 == td.bstart) || here != prev;
+            ngrp += head ? 1u : 0u;
+            keep = head && next == here;
         }
-        hmask |= (head ? 1u : 0u) << r;
-        const uint64_t bal = __ballot(head);
-        if (lane == 0) wcnt[r][wv] = (uint32_t)__popcll(bal);
+        hmask |= (keep ? 1u : 0u) << r;
+        const uint64_t bal = __ballot(keep);
+        if (lane == 0) wcnt[r * (kBlock / 64) + wv] = (uint32_t)__popcll(bal);
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t acc = 0;
-        for (int r = 0; r < kGRounds; ++r)
-            for (int w = 0; w < kBlock / 64; ++w) { const uint32_t c = wcnt[r][w]; wcnt[r][w] = acc; acc += c; }
-        s_red[0] = acc;
+    if (wv == 0) {   // exclusive scan of the kGRounds x waves counts (one wave, 64 entries)
+        static_assert(kGRounds * (kBlock / 64) == 64, "one entry per lane");
+        const uint32_t c0 = wcnt[lane];
+        uint32_t inc = c0;
+        #pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t t = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += t;
+        }
+        wcnt[lane] = inc - c0;
+        if (lane == 63) s_red[0] = inc;
     }
     __syncthreads();
     #pragma unroll
     for (int r = 0; r < kGRounds; ++r) {
-        const bool head = (hmask >> r) & 1u;
-        const uint64_t bal = __ballot(head);
-        if (head) heads[wcnt[r][wv] + (uint32_t)__popcll(bal & lt)] = (uint16_t)(r * kBlock + threadIdx.x);
+        const bool keep = (hmask >> r) & 1u;
+        const uint64_t bal = __ballot(keep);
+        if (keep) heads[wcnt[r * (kBlock / 64) + wv] + (uint32_t)__popcll(bal & lt)] = (uint16_t)(r * kBlock + threadIdx.x);
     }
     __syncthreads();
     const uint32_t H = s_red[0];
@@ -303,9 +315,11 @@ __global__ __launch_bounds__(kBlock) void probe_tile_rec_kernel(const uint64_t* 
         base += tot;
     }
     if (nrep) atomicAdd(&ctr->repeat_limit, (unsigned long long)nrep);   // rare (repeat-rich input only)
+    uint32_t gtot;
+    (void)blk_excl_scan(ngrp, s_w, &gtot);
     if (threadIdx.x == 0) {
         tile_count[blockIdx.x] = base;
-        tile_count[gridDim.x + 32 + blockIdx.x] = H;   // per-tile group count (summed by the host side)
+        tile_count[gridDim.x + 32 + blockIdx.x] = gtot;   // per-tile group count (summed by the host side)
     }
 }
 
