@@ -52,12 +52,9 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
 
 // probe of sorted-stream group k (the AddHashEntry argument), see build_probe
 template <int MG, typename View>
-__device__ __forceinline__ bool probe_of(const View& v, const uint64_t* __restrict__ probe_info, uint32_t k,
-                                         const GenomeTable& gt, const MatchParams& mp, int L, Mhe<MG>& P) {
-    const uint64_t info = probe_info[k];
-    const uint64_t h = info & 0xFFFFFFFFull;
-    uint32_t gs;
-    return build_probe<MG, View>(v, h, h + ((info >> 32) & 0xFFFFull), gt, mp, L, P, &gs);
+__device__ __forceinline__ void probe_of(const View& v, const uint64_t* __restrict__ /*probe_info*/, uint32_t k,
+                                         const GenomeTable& gt, const MatchParams& /*mp*/, int L, Mhe<MG>& P) {
+    load_probe<MG>(v, k, gt.G, L, P);
 }
 
 // line invariants: reference start x = s_ref (> 0); per other component the
@@ -503,17 +500,9 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
     template hipError_t launch_chains<MG, V>(V, const uint64_t*, uint64_t, const GenomeTable&, const MatchParams&, \
                                              const SeedSpec&, const uint32_t*, void*, void*, void*, uint32_t*,     \
                                              int64_t*, uint32_t*, hipStream_t);
-MUMS_INST_CHAINS(4, PairView<uint32_t>)
-MUMS_INST_CHAINS(8, PairView<uint32_t>)
-MUMS_INST_CHAINS(16, PairView<uint32_t>)
-MUMS_INST_CHAINS(32, PairView<uint32_t>)
-MUMS_INST_CHAINS(4, PairView<uint64_t>)
-MUMS_INST_CHAINS(8, PairView<uint64_t>)
-MUMS_INST_CHAINS(16, PairView<uint64_t>)
-MUMS_INST_CHAINS(32, PairView<uint64_t>)
-MUMS_INST_CHAINS(4, RecView)
-MUMS_INST_CHAINS(8, RecView)
-MUMS_INST_CHAINS(16, RecView)
-MUMS_INST_CHAINS(32, RecView)
+MUMS_INST_CHAINS(4, MatProbes)
+MUMS_INST_CHAINS(8, MatProbes)
+MUMS_INST_CHAINS(16, MatProbes)
+MUMS_INST_CHAINS(32, MatProbes)
 
 }  // namespace mums

@@ -353,9 +353,38 @@ __global__ void flat_tiles_kernel(uint64_t N, uint64_t nt, SegTile* __restrict__
     tiles[t] = d;
 }
 
+// probe k (key order) -> MatProbes row k: build_probe once per probe for the replay
+template <int MG, typename View>
+__global__ __launch_bounds__(kBlock) void probe_materialize_kernel(View v, const uint64_t* __restrict__ probe_info,
+                                                                   uint64_t P, GenomeTable gt, MatchParams mp, int L,
+                                                                   int64_t* __restrict__ s_out,
+                                                                   int64_t* __restrict__ off_out) {
+    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= P) return;
+    const uint64_t info = probe_info[k];
+    const uint64_t h = info & 0xFFFFFFFFull;
+    Mhe<MG> Q;
+    uint32_t gs;
+    build_probe<MG, View>(v, h, h + ((info >> 32) & 0xFFFFull), gt, mp, L, Q, &gs);
+    int64_t* row = s_out + k * (uint64_t)gt.G;
+    #pragma unroll
+    for (int g = 0; g < MG; ++g)
+        if (g < gt.G) row[g] = Q.s[g];
+    off_out[k] = Q.offset;
+}
+
 }  // namespace
 
 uint64_t group_slot_count(uint64_t ntiles) { return ntiles * kSlots; }
+
+template <int MG, typename View>
+hipError_t launch_materialize(View v, const uint64_t* probe_info, uint64_t P, const GenomeTable& gt,
+                              const MatchParams& mp, int L, int64_t* s_out, int64_t* off_out, hipStream_t st) {
+    if (P == 0) return hipSuccess;
+    hipLaunchKernelGGL((probe_materialize_kernel<MG, View>), dim3((unsigned)((P + kBlock - 1) / kBlock)), dim3(kBlock),
+                       0, st, v, probe_info, P, gt, mp, L, s_out, off_out);
+    return hipGetLastError();
+}
 
 hipError_t launch_flat_tiles(uint64_t N, SegTile* d_tiles, hipStream_t st) {
     const uint64_t nt = (N + kGTile - 1) / kGTile;
@@ -399,6 +428,21 @@ MUMS_INST_PROBE(4, PairView<uint64_t>)
 MUMS_INST_PROBE(8, PairView<uint64_t>)
 MUMS_INST_PROBE(16, PairView<uint64_t>)
 MUMS_INST_PROBE(32, PairView<uint64_t>)
+#define MUMS_INST_MAT(MG, V)                                                                                      \
+    template hipError_t launch_materialize<MG, V>(V, const uint64_t*, uint64_t, const GenomeTable&,                \
+                                                  const MatchParams&, int, int64_t*, int64_t*, hipStream_t);
+MUMS_INST_MAT(4, PairView<uint32_t>)
+MUMS_INST_MAT(8, PairView<uint32_t>)
+MUMS_INST_MAT(16, PairView<uint32_t>)
+MUMS_INST_MAT(32, PairView<uint32_t>)
+MUMS_INST_MAT(4, PairView<uint64_t>)
+MUMS_INST_MAT(8, PairView<uint64_t>)
+MUMS_INST_MAT(16, PairView<uint64_t>)
+MUMS_INST_MAT(32, PairView<uint64_t>)
+MUMS_INST_MAT(4, RecView)
+MUMS_INST_MAT(8, RecView)
+MUMS_INST_MAT(16, RecView)
+MUMS_INST_MAT(32, RecView)
 MUMS_INST_PROBE(4, RecView)
 MUMS_INST_PROBE(8, RecView)
 MUMS_INST_PROBE(16, RecView)

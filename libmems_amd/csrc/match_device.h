@@ -353,6 +353,26 @@ __device__ __forceinline__ bool probe_fast_raw(const uint64_t (&x)[MG + 1], cons
     return accept;
 }
 
+// Materialized probes: the AddHashEntry arguments of the seed stage in key order, as
+// P x G signed 1-based starts (after SetDirection) + their CalculateOffset values.  The
+// chain labelling and the replay read probes only through this (one coalesced row per
+// probe instead of G+1 gathers from the record stream); the sharded FindMatches ships
+// the same rows between ranks.
+struct MatProbes {
+    const int64_t* s;     // [P][G]
+    const int64_t* off;   // [P]
+};
+
+template <int MG>
+__device__ __forceinline__ void load_probe(const MatProbes& m, uint64_t k, int G, int L, Mhe<MG>& P) {
+    P.len = L;
+    P.mersize = L;
+    P.offset = m.off[k];
+    const int64_t* row = m.s + k * (uint64_t)G;
+    #pragma unroll
+    for (int g = 0; g < MG; ++g) P.s[g] = (g < G) ? row[g] : 0;
+}
+
 __device__ __forceinline__ uint32_t bucket_of(int64_t offset, uint32_t table_size) {
     const int64_t T = (int64_t)table_size;
     return (uint32_t)(((offset % T) + T) % T);  // MemHash.cpp:213

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../../include/mums.h"
+#include "match_device.h"
 #include "mums_internal.h"
 #include "seed_device.h"
 
@@ -72,7 +73,7 @@ struct mums_ctx {
 
     DevBuf packed, recA, recB, hist, tiles, ckey, kA, kB, vA, vB, tmp, partials, counters;
     DevBuf bstart, bend, tsize, obase, pool, tbl, out_len, out_s, pbuf, keybuf, mstart;
-    DevBuf chain_tmp, chain_of, radix_tmp, spill, summ, dbgbuf;
+    DevBuf chain_tmp, chain_of, radix_tmp, spill, summ, dbgbuf, mprobe;
     bool use_onesweep = true;
     hipEvent_t ev[EV_COUNT] = {};
     bool profiling = false;
@@ -195,12 +196,18 @@ int groups_dispatch(mums_ctx* ctx, View v, const SegTile* tiles, uint64_t ntiles
 
 // chain labelling (chains.hip) then the per-bucket replay (replay.hip)
 template <int MG, typename View>
-int replay_run(mums_ctx* ctx, View v, const MatchParams& mp, hipStream_t st) {
+int replay_run(mums_ctx* ctx, View sv, const MatchParams& mp, hipStream_t st) {
     DevCounters* dc = ctx->counters.as<DevCounters>();
     const uint64_t P = ctx->P;
     if (P >= (1ull << 30))   // probe ids share a word with two replay flags (replay.hip)
         return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^30 seed probes in one FindMatches");
-    HIPCHK((launch_chains<MG, View>(v, ctx->probe_info, P, ctx->gt, mp, ctx->ss, ctx->packed.as<uint32_t>(),
+    // the probes as rows (one build_probe each), then everything reads the rows
+    const int G = ctx->gt.G;
+    HIPCHK(ctx->mprobe.ensure((P + 1) * (size_t)(G + 1) * 8));
+    const MatProbes v{ctx->mprobe.as<int64_t>(), ctx->mprobe.as<int64_t>() + (P + 1) * (uint64_t)G};
+    HIPCHK((launch_materialize<MG, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, (int64_t*)v.s, (int64_t*)v.off,
+                                         st)));
+    HIPCHK((launch_chains<MG, MatProbes>(v, nullptr, P, ctx->gt, mp, ctx->ss, ctx->packed.as<uint32_t>(),
                                     ctx->chain_tmp.p, ctx->tmp.p, ctx->radix_tmp.p, ctx->chain_of.as<uint32_t>(),
                                     ctx->pool.as<int64_t>(), &dc->nchains, st)));
     HIPCHK(hipEventRecord(ctx->ev[EV_CHAINS], st));
@@ -214,7 +221,7 @@ int replay_run(mums_ctx* ctx, View v, const MatchParams& mp, hipStream_t st) {
     }
     // the fullest bucket's vector in LDS when it fits (it holds <= its probes)
     const uint32_t lds_cap = std::max<uint32_t>(64, std::min<uint32_t>(ctx->hc.max_bucket, kReplayLdsIds));
-    HIPCHK((launch_replay<MG, View>(v, ctx->gt, mp, ctx->L, ctx->probe_info, ctx->sorted_ids, P,
+    HIPCHK((launch_replay<MG, MatProbes>(v, ctx->gt, mp, ctx->L, nullptr, ctx->sorted_ids, P,
                                     ctx->bstart.as<uint32_t>(), ctx->bend.as<uint32_t>(), ctx->tbl.as<uint32_t>(),
                                     ctx->spill.p, ctx->summ.p, ctx->pool.as<int64_t>(), ctx->chain_of.as<uint32_t>(),
                                     ctx->hc.nchains, ctx->chain_tmp.p, ctx->radix_tmp.p, lds_cap,

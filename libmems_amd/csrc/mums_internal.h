@@ -185,6 +185,10 @@ hipError_t launch_probe_tiles(View v, const SegTile* tiles, uint64_t ntiles, uin
 hipError_t launch_probe_compact(uint64_t ntiles, const uint32_t* tile_count, const uint32_t* tile_off,
                                 const uint64_t* slot_info, const uint32_t* slot_bucket, uint64_t* probe_info,
                                 uint32_t* probe_bucket, hipStream_t st);
+// probes (key order) -> materialized rows (MatProbes, match_device.h)
+template <int MG, typename View>
+hipError_t launch_materialize(View v, const uint64_t* probe_info, uint64_t P, const GenomeTable& gt,
+                              const MatchParams& mp, int L, int64_t* s_out, int64_t* off_out, hipStream_t st);
 // flat tiles over [0, N) for the pair path (one bucket)
 hipError_t launch_flat_tiles(uint64_t N, SegTile* d_tiles, hipStream_t st);
 

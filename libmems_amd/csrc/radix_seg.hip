@@ -30,6 +30,9 @@ constexpr int kDigits = 256;
 #ifndef MUMS_SORT_TILE
 #define MUMS_SORT_TILE 8192
 #endif
+#ifndef MUMS_SORT_NT
+#define MUMS_SORT_NT 0      // bit 0: non-temporal record loads, bit 1: non-temporal stores
+#endif
 #ifndef MUMS_SORT_PERSIST
 #define MUMS_SORT_PERSIST 0
 #endif
@@ -354,7 +357,11 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
     #pragma unroll
     for (int r = 0; r < kIPT; ++r) {
         const uint32_t q = q0 + r * 64 + lane;
+#if MUMS_SORT_NT & 1
+        key[r] = q < d.count ? __builtin_nontemporal_load(rin + d.start + q) : 0ull;   // read once per pass
+#else
         key[r] = q < d.count ? rin[d.start + q] : 0ull;
+#endif
     }
     // publish this tile's per-digit counts as soon as the keys are in: successors'
     // look-backs then rarely find an unpublished predecessor.
@@ -459,7 +466,11 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
         if (sidx < d.count) {
             const uint64_t k = srec[sidx];
             const uint32_t dg = (uint32_t)(k >> shift) & 0xFFu;
+#if MUMS_SORT_NT & 2
+            __builtin_nontemporal_store(k, rout + (uint64_t)gofs[dg] + (sidx - lstart[dg]));
+#else
             rout[(uint64_t)gofs[dg] + (sidx - lstart[dg])] = k;
+#endif
         }
     }
 }

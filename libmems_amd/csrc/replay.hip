@@ -113,10 +113,7 @@ __global__ __launch_bounds__(kBlock) void probe_summary_kernel(View v, GenomeTab
     if (q >= P) return;
     const uint32_t k = ids[q];
     Mhe<MG> Q;
-    uint32_t gs;
-    const uint64_t info = probe_info[k];
-    const uint64_t h = info & 0xFFFFFFFFull;
-    build_probe<MG, View>(v, h, h + ((info >> 32) & 0xFFFFull), gt, mp, L, Q, &gs);
+    load_probe<MG>(v, k, gt.G, L, Q);
     const uint32_t cid = chain_of[k];
     summ[q] = make_uint4(mask_of<MG>(Q, gt.G), (uint32_t)start_at(Q, first_start(Q)), cid, k);
     // probes run in ascending q, so the plain read filters nearly every later atomic
@@ -208,12 +205,9 @@ __global__ __launch_bounds__(kBlock) void probe_flags_kernel(uint4* __restrict__
 
 // the probe of stream group k (AddHashEntry's argument), built on the rare slow path
 template <int MG, typename View>
-__device__ __noinline__ void probe_full(const View& v, const GenomeTable& gt, const MatchParams& mp, int L,
-                                        const uint64_t* __restrict__ probe_info, uint32_t k, Mhe<MG>& P) {
-    uint32_t gs;
-    const uint64_t info = probe_info[k];
-    const uint64_t h = info & 0xFFFFFFFFull;
-    build_probe<MG, View>(v, h, h + ((info >> 32) & 0xFFFFull), gt, mp, L, P, &gs);
+__device__ __noinline__ void probe_full(const View& v, const GenomeTable& gt, const MatchParams& /*mp*/, int L,
+                                        const uint64_t* __restrict__ /*probe_info*/, uint32_t k, Mhe<MG>& P) {
+    load_probe<MG>(v, k, gt.G, L, P);
 }
 
 // one round: every unconsumed lane of the window runs its lower_bound against the
@@ -524,17 +518,9 @@ hipError_t launch_emit(const uint32_t* tsize, const uint32_t* obase, const uint3
                                              const uint32_t*, uint64_t, const uint32_t*, const uint32_t*,          \
                                              uint32_t*, void*, void*, const int64_t*, const uint32_t*, uint32_t,   \
                                              void*, void*, uint32_t, uint32_t*, void*, uint64_t*, hipStream_t);
-MUMS_INST_REPLAY(4, PairView<uint32_t>)
-MUMS_INST_REPLAY(8, PairView<uint32_t>)
-MUMS_INST_REPLAY(16, PairView<uint32_t>)
-MUMS_INST_REPLAY(32, PairView<uint32_t>)
-MUMS_INST_REPLAY(4, PairView<uint64_t>)
-MUMS_INST_REPLAY(8, PairView<uint64_t>)
-MUMS_INST_REPLAY(16, PairView<uint64_t>)
-MUMS_INST_REPLAY(32, PairView<uint64_t>)
-MUMS_INST_REPLAY(4, RecView)
-MUMS_INST_REPLAY(8, RecView)
-MUMS_INST_REPLAY(16, RecView)
-MUMS_INST_REPLAY(32, RecView)
+MUMS_INST_REPLAY(4, MatProbes)
+MUMS_INST_REPLAY(8, MatProbes)
+MUMS_INST_REPLAY(16, MatProbes)
+MUMS_INST_REPLAY(32, MatProbes)
 
 }  // namespace mums
