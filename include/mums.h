@@ -156,6 +156,28 @@ int  mums_shard_merge(mums_ctx* ctx, const uint64_t* d_records, uint32_t nsource
  * hash bucket ((offset % T) + T) % T and the smallest global seed-mer index of
  * the probe's key group (its identity; checking aid, host-side gather). */
 int  mums_probe_count(mums_ctx* ctx, uint64_t* count);
+/* ---- sharded FindMatches, after mums_shard_merge on every rank ---
+ * Replaces the single-process AddHashEntry replay (MemHash::AddHashEntry,
+ * MemHash.cpp:209-251; ExtendMatch, MatchFinder.h:218-374; GetMatchList,
+ * MemHash.h:182-203) when the probes of one MemHash live on several GPUs.  Rank r owns
+ * the hash buckets [bounds[r], bounds[r+1]); the ranks' key ranges are in rank order,
+ * so every bucket's probes arrive in the reference's AddHashEntry order and the
+ * ranks' outputs concatenated in rank order are the bucket-major MatchList.
+ *   1. mums_shard_bucket_counts: probes of this rank per hash bucket (host, table_size);
+ *   2. mums_shard_probe_rows: this rank's probes (key order) as rows of G+1 int64
+ *      {signed starts (SetDirection), CalculateOffset} into d_rows, stably grouped by
+ *      destination rank; counts[r] rows go to rank r;
+ *   3. the caller exchanges the rows (all-to-all, sources in rank order) and assembles
+ *      all genomes' 2-bit packed words (mums_shard_packed_info / _copy: this rank's
+ *      slice [word_offset, word_offset + nwords) of the total_words array);
+ *   4. mums_shard_find: chain labelling + replay of the received rows; results via
+ *      mums_result_count / mums_result_copy (this rank's buckets, bucket-major). */
+int  mums_shard_bucket_counts(mums_ctx* ctx, uint64_t* counts);
+int  mums_shard_probe_rows(mums_ctx* ctx, uint32_t nranks, const uint32_t* bounds, int64_t* d_rows,
+                           uint64_t capacity_rows, uint64_t* counts);
+int  mums_shard_packed_info(mums_ctx* ctx, uint64_t* word_offset, uint64_t* nwords, uint64_t* total_words);
+int  mums_shard_packed_copy(mums_ctx* ctx, uint32_t* d_dst);
+int  mums_shard_find(mums_ctx* ctx, const int64_t* d_rows, uint64_t nrows, const uint32_t* d_packed_all);
 int  mums_probe_copy(mums_ctx* ctx, uint32_t* buckets, uint64_t* ref_index, uint64_t capacity);
 
 int  mums_abi_version(void);

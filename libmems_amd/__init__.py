@@ -86,7 +86,8 @@ EXPORTED_SYMBOLS = [
     "mums_find", "mums_find_stage", "mums_result_count", "mums_result_copy", "mums_get_stats",
     "mums_last_error", "mums_get_seed", "mums_default_seed_weight", "mums_copy_seed_keys",
     "mums_build_sml", "mums_set_profiling", "mums_shard_layout", "mums_shard_msd_bits", "mums_shard_keys",
-    "mums_shard_merge", "mums_probe_count", "mums_probe_copy",
+    "mums_shard_merge", "mums_probe_count", "mums_probe_copy", "mums_shard_bucket_counts", "mums_shard_probe_rows",
+    "mums_shard_packed_info", "mums_shard_packed_copy", "mums_shard_find",
 ]
 
 _lib: Optional[ctypes.CDLL] = None
@@ -138,6 +139,11 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mums_shard_merge.argtypes = [vp, vp, u32, u32, u32, vp]
     lib.mums_probe_count.argtypes = [vp, ctypes.POINTER(u64)]
     lib.mums_probe_copy.argtypes = [vp, vp, vp, u64]
+    lib.mums_shard_bucket_counts.argtypes = [vp, vp]
+    lib.mums_shard_probe_rows.argtypes = [vp, u32, vp, vp, u64, vp]
+    lib.mums_shard_packed_info.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]
+    lib.mums_shard_packed_copy.argtypes = [vp, vp]
+    lib.mums_shard_find.argtypes = [vp, vp, u64, vp]
     _lib = lib
     return lib
 

@@ -357,8 +357,7 @@ __global__ void flat_tiles_kernel(uint64_t N, uint64_t nt, SegTile* __restrict__
 template <int MG, typename View>
 __global__ __launch_bounds__(kBlock) void probe_materialize_kernel(View v, const uint64_t* __restrict__ probe_info,
                                                                    uint64_t P, GenomeTable gt, MatchParams mp, int L,
-                                                                   int64_t* __restrict__ s_out,
-                                                                   int64_t* __restrict__ off_out) {
+                                                                   int64_t* __restrict__ rows) {
     const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (k >= P) return;
     const uint64_t info = probe_info[k];
@@ -366,11 +365,35 @@ __global__ __launch_bounds__(kBlock) void probe_materialize_kernel(View v, const
     Mhe<MG> Q;
     uint32_t gs;
     build_probe<MG, View>(v, h, h + ((info >> 32) & 0xFFFFull), gt, mp, L, Q, &gs);
-    int64_t* row = s_out + k * (uint64_t)gt.G;
+    int64_t* row = rows + k * (uint64_t)(gt.G + 1);
     #pragma unroll
     for (int g = 0; g < MG; ++g)
         if (g < gt.G) row[g] = Q.s[g];
-    off_out[k] = Q.offset;
+    row[gt.G] = Q.offset;
+}
+
+// bucket (MemHash.cpp:213) of every row; dest = owning rank of that bucket when bounds
+// (nranks + 1 bucket boundaries) are given
+__global__ __launch_bounds__(kBlock) void row_bucket_kernel(const int64_t* __restrict__ rows, uint64_t P, int G,
+                                                            uint32_t table_size, double inv_t,
+                                                            const uint32_t* __restrict__ bounds, uint32_t nranks,
+                                                            uint32_t* __restrict__ out) {
+    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= P) return;
+    const uint32_t b = bucket_of_fast(rows[k * (uint64_t)(G + 1) + G], table_size, inv_t);
+    if (!bounds) { out[k] = b; return; }
+    uint32_t r = 0;
+    while (r + 1 < nranks && bounds[r + 1] <= b) ++r;
+    out[k] = r;
+}
+
+__global__ __launch_bounds__(kBlock) void gather_rows_kernel(const int64_t* __restrict__ src,
+                                                             const uint32_t* __restrict__ perm, uint64_t P, int W,
+                                                             int64_t* __restrict__ dst) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= P * (uint64_t)W) return;
+    const uint64_t k = i / (uint64_t)W, c = i - k * (uint64_t)W;
+    dst[i] = src[(uint64_t)perm[k] * W + c];
 }
 
 }  // namespace
@@ -379,10 +402,27 @@ uint64_t group_slot_count(uint64_t ntiles) { return ntiles * kSlots; }
 
 template <int MG, typename View>
 hipError_t launch_materialize(View v, const uint64_t* probe_info, uint64_t P, const GenomeTable& gt,
-                              const MatchParams& mp, int L, int64_t* s_out, int64_t* off_out, hipStream_t st) {
+                              const MatchParams& mp, int L, int64_t* rows, hipStream_t st) {
     if (P == 0) return hipSuccess;
     hipLaunchKernelGGL((probe_materialize_kernel<MG, View>), dim3((unsigned)((P + kBlock - 1) / kBlock)), dim3(kBlock),
-                       0, st, v, probe_info, P, gt, mp, L, s_out, off_out);
+                       0, st, v, probe_info, P, gt, mp, L, rows);
+    return hipGetLastError();
+}
+
+hipError_t launch_row_buckets(const int64_t* rows, uint64_t P, int G, uint32_t table_size, const uint32_t* d_bounds,
+                              uint32_t nranks, uint32_t* out, hipStream_t st) {
+    if (P == 0) return hipSuccess;
+    hipLaunchKernelGGL(row_bucket_kernel, dim3((unsigned)((P + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, rows, P, G,
+                       table_size, 1.0 / (double)table_size, d_bounds, nranks, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_rows(const int64_t* src, const uint32_t* perm, uint64_t P, int G, int64_t* dst,
+                              hipStream_t st) {
+    if (P == 0) return hipSuccess;
+    const uint64_t n = P * (uint64_t)(G + 1);
+    hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, src, perm,
+                       P, G + 1, dst);
     return hipGetLastError();
 }
 
@@ -430,7 +470,7 @@ MUMS_INST_PROBE(16, PairView<uint64_t>)
 MUMS_INST_PROBE(32, PairView<uint64_t>)
 #define MUMS_INST_MAT(MG, V)                                                                                      \
     template hipError_t launch_materialize<MG, V>(V, const uint64_t*, uint64_t, const GenomeTable&,                \
-                                                  const MatchParams&, int, int64_t*, int64_t*, hipStream_t);
+                                                  const MatchParams&, int, int64_t*, hipStream_t);
 MUMS_INST_MAT(4, PairView<uint32_t>)
 MUMS_INST_MAT(8, PairView<uint32_t>)
 MUMS_INST_MAT(16, PairView<uint32_t>)

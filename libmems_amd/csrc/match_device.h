@@ -353,22 +353,21 @@ __device__ __forceinline__ bool probe_fast_raw(const uint64_t (&x)[MG + 1], cons
     return accept;
 }
 
-// Materialized probes: the AddHashEntry arguments of the seed stage in key order, as
-// P x G signed 1-based starts (after SetDirection) + their CalculateOffset values.  The
-// chain labelling and the replay read probes only through this (one coalesced row per
-// probe instead of G+1 gathers from the record stream); the sharded FindMatches ships
-// the same rows between ranks.
+// Materialized probes: the AddHashEntry arguments of the seed stage in key order, one
+// row of G+1 int64 per probe: the signed 1-based starts (after SetDirection) and the
+// CalculateOffset value.  The chain labelling and the replay read probes only through
+// this (one contiguous row per probe instead of G+1 gathers from the record stream);
+// the sharded FindMatches ships the same rows between ranks.
 struct MatProbes {
-    const int64_t* s;     // [P][G]
-    const int64_t* off;   // [P]
+    const int64_t* rows;   // [P][G + 1]
 };
 
 template <int MG>
 __device__ __forceinline__ void load_probe(const MatProbes& m, uint64_t k, int G, int L, Mhe<MG>& P) {
+    const int64_t* row = m.rows + k * (uint64_t)(G + 1);
     P.len = L;
     P.mersize = L;
-    P.offset = m.off[k];
-    const int64_t* row = m.s + k * (uint64_t)G;
+    P.offset = row[G];
     #pragma unroll
     for (int g = 0; g < MG; ++g) P.s[g] = (g < G) ? row[g] : 0;
 }

@@ -73,7 +73,7 @@ struct mums_ctx {
 
     DevBuf packed, recA, recB, hist, tiles, ckey, kA, kB, vA, vB, tmp, partials, counters;
     DevBuf bstart, bend, tsize, obase, pool, tbl, out_len, out_s, pbuf, keybuf, mstart;
-    DevBuf chain_tmp, chain_of, radix_tmp, spill, summ, dbgbuf, mprobe;
+    DevBuf chain_tmp, chain_of, radix_tmp, spill, summ, dbgbuf, mprobe, rowtmp;
     bool use_onesweep = true;
     hipEvent_t ev[EV_COUNT] = {};
     bool profiling = false;
@@ -194,20 +194,15 @@ int groups_dispatch(mums_ctx* ctx, View v, const SegTile* tiles, uint64_t ntiles
     return run_groups<32, View>(ctx, v, tiles, ntiles, mp, pi, pb, si, sb, st);
 }
 
-// chain labelling (chains.hip) then the per-bucket replay (replay.hip)
-template <int MG, typename View>
-int replay_run(mums_ctx* ctx, View sv, const MatchParams& mp, hipStream_t st) {
+// chain labelling (chains.hip) then the per-bucket replay (replay.hip) of the P probe
+// rows v (key order), bucket-sorted as ctx->sorted_ids; packed = all genomes (gt layout)
+template <int MG>
+int find_rows(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const MatchParams& mp, hipStream_t st) {
     DevCounters* dc = ctx->counters.as<DevCounters>();
     const uint64_t P = ctx->P;
     if (P >= (1ull << 30))   // probe ids share a word with two replay flags (replay.hip)
         return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^30 seed probes in one FindMatches");
-    // the probes as rows (one build_probe each), then everything reads the rows
-    const int G = ctx->gt.G;
-    HIPCHK(ctx->mprobe.ensure((P + 1) * (size_t)(G + 1) * 8));
-    const MatProbes v{ctx->mprobe.as<int64_t>(), ctx->mprobe.as<int64_t>() + (P + 1) * (uint64_t)G};
-    HIPCHK((launch_materialize<MG, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, (int64_t*)v.s, (int64_t*)v.off,
-                                         st)));
-    HIPCHK((launch_chains<MG, MatProbes>(v, nullptr, P, ctx->gt, mp, ctx->ss, ctx->packed.as<uint32_t>(),
+    HIPCHK((launch_chains<MG, MatProbes>(v, nullptr, P, ctx->gt, mp, ctx->ss, packed,
                                     ctx->chain_tmp.p, ctx->tmp.p, ctx->radix_tmp.p, ctx->chain_of.as<uint32_t>(),
                                     ctx->pool.as<int64_t>(), &dc->nchains, st)));
     HIPCHK(hipEventRecord(ctx->ev[EV_CHAINS], st));
@@ -243,13 +238,84 @@ int replay_run(mums_ctx* ctx, View sv, const MatchParams& mp, hipStream_t st) {
     return MUMS_OK;
 }
 
-template <typename View>
-int replay_dispatch(mums_ctx* ctx, View v, const MatchParams& mp, hipStream_t st) {
+int find_rows_dispatch(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const MatchParams& mp, hipStream_t st) {
     const int G = ctx->gt.G;
-    if (G <= 4) return replay_run<4, View>(ctx, v, mp, st);
-    if (G <= 8) return replay_run<8, View>(ctx, v, mp, st);
-    if (G <= 16) return replay_run<16, View>(ctx, v, mp, st);
-    return replay_run<32, View>(ctx, v, mp, st);
+    if (G <= 4) return find_rows<4>(ctx, v, packed, mp, st);
+    if (G <= 8) return find_rows<8>(ctx, v, packed, mp, st);
+    if (G <= 16) return find_rows<16>(ctx, v, packed, mp, st);
+    return find_rows<32>(ctx, v, packed, mp, st);
+}
+
+// the probes of the seed stage as rows (one build_probe each) in ctx->mprobe
+template <typename View>
+int materialize_dispatch(mums_ctx* ctx, View sv, const MatchParams& mp, hipStream_t st) {
+    const int G = ctx->gt.G;
+    const uint64_t P = ctx->P;
+    HIPCHK(ctx->mprobe.ensure((P + 1) * (size_t)(G + 1) * 8));
+    int64_t* rows = ctx->mprobe.as<int64_t>();
+    if (G <= 4) HIPCHK((launch_materialize<4, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st)));
+    else if (G <= 8) HIPCHK((launch_materialize<8, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st)));
+    else if (G <= 16) HIPCHK((launch_materialize<16, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st)));
+    else HIPCHK((launch_materialize<32, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st)));
+    return MUMS_OK;
+}
+
+int materialize_seeds(mums_ctx* ctx, const MatchParams& mp, hipStream_t st) {
+    if (ctx->packed_path) return materialize_dispatch<RecView>(ctx, RecView{ctx->sorted_rec}, mp, st);
+    if (ctx->key64)
+        return materialize_dispatch<PairView<uint64_t>>(
+            ctx, PairView<uint64_t>{(const uint64_t*)ctx->sorted_key, ctx->sorted_idx}, mp, st);
+    return materialize_dispatch<PairView<uint32_t>>(
+        ctx, PairView<uint32_t>{(const uint32_t*)ctx->sorted_key, ctx->sorted_idx}, mp, st);
+}
+
+// FindMatches after the bucket sort (ctx->P probes, ctx->sorted_ids / sorted_buckets):
+// workspace, bucket ranges, [rows()] materialize, chains + replay, MatchList (A10-A12)
+template <typename Rows>
+int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows&& rows, hipStream_t st) {
+    DevCounters* dc = ctx->counters.as<DevCounters>();
+    const int G = ctx->gt.G;
+    const uint32_t Tb = ctx->table_size;
+    HIPCHK(ctx->bstart.ensure((size_t)Tb * 4));
+    HIPCHK(ctx->bend.ensure((size_t)Tb * 4));
+    HIPCHK(ctx->tsize.ensure((size_t)Tb * 4));
+    HIPCHK(ctx->obase.ensure((size_t)Tb * 4 + 64));
+    HIPCHK(ctx->pool.ensure((ctx->P + 1) * (size_t)(G + 2) * 8));
+    HIPCHK(ctx->tbl.ensure((ctx->P + 1) * 4));
+    HIPCHK(ctx->chain_of.ensure((ctx->P + 1) * 4));
+    HIPCHK(ctx->spill.ensure((ctx->P + 1) * 16));
+    HIPCHK(ctx->summ.ensure((ctx->P + 1) * 32));
+    HIPCHK(ctx->chain_tmp.ensure(chain_tmp_bytes(ctx->P + 1)));
+    HIPCHK(ctx->radix_tmp.ensure(radix_tmp_bytes(ctx->P + 1)));
+    HIPCHK(ctx->tmp.ensure(std::max(scan_tmp_bytes(ctx->P + 1), scan_tmp_bytes(Tb))));
+    HIPCHK(hipMemsetAsync(&dc->max_bucket, 0, 4, st));
+    HIPCHK(hipMemsetAsync(ctx->bstart.p, 0, (size_t)Tb * 4, st));
+    HIPCHK(hipMemsetAsync(ctx->bend.p, 0, (size_t)Tb * 4, st));
+    HIPCHK(hipMemsetAsync(ctx->tsize.p, 0, (size_t)Tb * 4, st));
+    HIPCHK(launch_bucket_ranges(ctx->sorted_buckets, ctx->P, ctx->bstart.as<uint32_t>(), ctx->bend.as<uint32_t>(),
+                                &dc->max_bucket, st));
+    if (ctx->P == 0) HIPCHK(hipEventRecord(ctx->ev[EV_CHAINS], st));
+    if (ctx->P > 0) {
+        MatProbes v{};
+        int rc = rows(&v);
+        if (rc) return rc;
+        rc = find_rows_dispatch(ctx, v, packed, mp, st);
+        if (rc) return rc;
+    }
+    HIPCHK(hipEventRecord(ctx->ev[EV_REPLAY], st));
+    HIPCHK(hipMemcpyAsync(ctx->obase.p, ctx->tsize.p, (size_t)Tb * 4, hipMemcpyDeviceToDevice, st));
+    HIPCHK(exclusive_scan_u32(ctx->obase.as<uint32_t>(), Tb, ctx->tmp.p, &dc->nmatches, st));
+    HIPCHK(hipMemcpyAsync(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    ctx->M = ctx->hc.nmatches;
+    HIPCHK(ctx->out_len.ensure((ctx->M + 1) * 8));
+    HIPCHK(ctx->out_s.ensure((ctx->M + 1) * (size_t)G * 8));
+    HIPCHK(launch_emit(ctx->tsize.as<uint32_t>(), ctx->obase.as<uint32_t>(), ctx->bstart.as<uint32_t>(),
+                       ctx->tbl.as<uint32_t>(), ctx->pool.as<int64_t>(), G, Tb, ctx->out_len.as<uint64_t>(),
+                       ctx->out_s.as<int64_t>(), st));
+    HIPCHK(hipEventRecord(ctx->ev[EV_OUTPUT], st));
+    ctx->stage_done = MUMS_STAGE_ALL;
+    return MUMS_OK;
 }
 
 // probe / slot arrays of the groups stage (one grow-only device buffer)
@@ -518,49 +584,12 @@ int run_pipeline(mums_ctx* ctx, int stage) {
     ctx->stage_done = MUMS_STAGE_SEEDS;
 
     if (stage >= MUMS_STAGE_ALL) {
-        const uint32_t Tb = ctx->table_size;
-        HIPCHK(ctx->bstart.ensure((size_t)Tb * 4));
-        HIPCHK(ctx->bend.ensure((size_t)Tb * 4));
-        HIPCHK(ctx->tsize.ensure((size_t)Tb * 4));
-        HIPCHK(ctx->obase.ensure((size_t)Tb * 4 + 64));
-        HIPCHK(ctx->pool.ensure((ctx->P + 1) * (size_t)(G + 2) * 8));
-        HIPCHK(ctx->tbl.ensure((ctx->P + 1) * 4));
-        HIPCHK(ctx->chain_of.ensure((ctx->P + 1) * 4));
-        HIPCHK(ctx->spill.ensure((ctx->P + 1) * 16));
-        HIPCHK(ctx->summ.ensure((ctx->P + 1) * 32));
-        HIPCHK(ctx->chain_tmp.ensure(chain_tmp_bytes(ctx->P + 1)));
-        HIPCHK(ctx->radix_tmp.ensure(radix_tmp_bytes(ctx->P + 1)));
-        HIPCHK(ctx->tmp.ensure(std::max(scan_tmp_bytes(ctx->P + 1), scan_tmp_bytes(Tb))));
-        HIPCHK(hipMemsetAsync(&dc->max_bucket, 0, 4, st));
-        HIPCHK(hipMemsetAsync(ctx->bstart.p, 0, (size_t)Tb * 4, st));
-        HIPCHK(hipMemsetAsync(ctx->bend.p, 0, (size_t)Tb * 4, st));
-        HIPCHK(hipMemsetAsync(ctx->tsize.p, 0, (size_t)Tb * 4, st));
-        HIPCHK(launch_bucket_ranges(ctx->sorted_buckets, ctx->P, ctx->bstart.as<uint32_t>(), ctx->bend.as<uint32_t>(),
-                                    &dc->max_bucket, st));
-        if (ctx->P == 0) HIPCHK(hipEventRecord(ctx->ev[EV_CHAINS], st));
-        if (ctx->P > 0) {
-            if (ctx->packed_path) rc = replay_dispatch<RecView>(ctx, RecView{ctx->sorted_rec}, mp, st);
-            else if (ctx->key64)
-                rc = replay_dispatch<PairView<uint64_t>>(
-                    ctx, PairView<uint64_t>{(const uint64_t*)ctx->sorted_key, ctx->sorted_idx}, mp, st);
-            else
-                rc = replay_dispatch<PairView<uint32_t>>(
-                    ctx, PairView<uint32_t>{(const uint32_t*)ctx->sorted_key, ctx->sorted_idx}, mp, st);
-            if (rc) return rc;
-        }
-        HIPCHK(hipEventRecord(ctx->ev[EV_REPLAY], st));
-        HIPCHK(hipMemcpyAsync(ctx->obase.p, ctx->tsize.p, (size_t)Tb * 4, hipMemcpyDeviceToDevice, st));
-        HIPCHK(exclusive_scan_u32(ctx->obase.as<uint32_t>(), Tb, ctx->tmp.p, &dc->nmatches, st));
-        HIPCHK(hipMemcpyAsync(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        ctx->M = ctx->hc.nmatches;
-        HIPCHK(ctx->out_len.ensure((ctx->M + 1) * 8));
-        HIPCHK(ctx->out_s.ensure((ctx->M + 1) * (size_t)G * 8));
-        HIPCHK(launch_emit(ctx->tsize.as<uint32_t>(), ctx->obase.as<uint32_t>(), ctx->bstart.as<uint32_t>(),
-                           ctx->tbl.as<uint32_t>(), ctx->pool.as<int64_t>(), G, Tb, ctx->out_len.as<uint64_t>(),
-                           ctx->out_s.as<int64_t>(), st));
-        HIPCHK(hipEventRecord(ctx->ev[EV_OUTPUT], st));
-        ctx->stage_done = MUMS_STAGE_ALL;
+        rc = find_tail(ctx, mp, ctx->packed.as<uint32_t>(), [&](MatProbes* v) {
+            const int r = materialize_seeds(ctx, mp, st);
+            v->rows = ctx->mprobe.as<int64_t>();
+            return r;
+        }, st);
+        if (rc) return rc;
     }
     HIPCHK(hipStreamSynchronize(st));
     HIPCHK(hipMemcpy(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost));
@@ -788,7 +817,7 @@ int mums_result_count(mums_ctx* ctx, uint64_t* count, uint32_t* seq_count) {
     if (check_ctx(ctx)) return MUMS_E_INVALID;
     if (ctx->stage_done < MUMS_STAGE_ALL) return fail(ctx, MUMS_E_INVALID, "no completed FindMatches on this context");
     if (count) *count = ctx->M;
-    if (seq_count) *seq_count = (uint32_t)ctx->genomes.size();
+    if (seq_count) *seq_count = (uint32_t)ctx->gt.G;   // all genomes of the problem (sharded: not only the owned)
     return MUMS_OK;
 }
 
@@ -797,7 +826,7 @@ int mums_result_copy(mums_ctx* ctx, uint64_t* lengths, int64_t* starts) {
     if (ctx->stage_done < MUMS_STAGE_ALL) return fail(ctx, MUMS_E_INVALID, "no completed FindMatches on this context");
     if (ctx->M == 0) return MUMS_OK;
     HIPCHK(hipSetDevice(ctx->device));
-    const size_t G = ctx->genomes.size();
+    const size_t G = (size_t)ctx->gt.G;
     if (lengths) HIPCHK(hipMemcpy(lengths, ctx->out_len.p, ctx->M * 8, hipMemcpyDeviceToHost));
     if (starts) HIPCHK(hipMemcpy(starts, ctx->out_s.p, ctx->M * G * 8, hipMemcpyDeviceToHost));
     return MUMS_OK;
@@ -1030,6 +1059,159 @@ int mums_probe_copy(mums_ctx* ctx, uint32_t* buckets, uint64_t* ref_index, uint6
         if (buckets) buckets[k] = bucket_of_probe[k];
         if (ref_index) ref_index[k] = mn;
     }
+    return MUMS_OK;
+}
+
+
+// ---- sharded FindMatches -------------------------------------------
+
+namespace {
+
+int shard_seeds_done(mums_ctx* ctx) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (!ctx->shard) return fail(ctx, MUMS_E_INVALID, "not a sharded context (mums_shard_layout)");
+    if (ctx->stage_done < MUMS_STAGE_SEEDS) return fail(ctx, MUMS_E_INVALID, "no sharded seed stage run");
+    return MUMS_OK;
+}
+
+// stable sort of P u32 keys (< 2^bits) -> ctx->sorted_ids / sorted_buckets (rowtmp)
+int sort_row_keys(mums_ctx* ctx, uint32_t* keys, uint64_t P, int bits, hipStream_t st) {
+    uint32_t* kB = (uint32_t*)ctx->rowtmp.p + (P + 64);
+    uint32_t* iA = kB + (P + 64);
+    uint32_t* iB = iA + (P + 64);
+    HIPCHK(ctx->radix_tmp.ensure(radix_tmp_bytes(P + 1)));
+    int out = 0;
+    HIPCHK(radix_sort<uint32_t>(keys, nullptr, P, bits, kB, iA, keys, iB, ctx->radix_tmp.p, &out, st));
+    ctx->sorted_buckets = out ? keys : kB;
+    ctx->sorted_ids = out ? iB : iA;
+    return MUMS_OK;
+}
+
+}  // namespace
+
+int mums_shard_bucket_counts(mums_ctx* ctx, uint64_t* counts) {
+    int rc = shard_seeds_done(ctx);
+    if (rc) return rc;
+    if (!counts) return fail(ctx, MUMS_E_INVALID, "null counts");
+    HIPCHK(hipSetDevice(ctx->device));
+    const uint32_t Tb = ctx->table_size;
+    std::fill(counts, counts + Tb, 0ull);
+    if (ctx->P == 0) return MUMS_OK;
+    hipStream_t st = ctx->stream;
+    DevCounters* dc = ctx->counters.as<DevCounters>();
+    HIPCHK(ctx->bstart.ensure((size_t)Tb * 4));
+    HIPCHK(ctx->bend.ensure((size_t)Tb * 4));
+    HIPCHK(hipMemsetAsync(ctx->bstart.p, 0, (size_t)Tb * 4, st));
+    HIPCHK(hipMemsetAsync(ctx->bend.p, 0, (size_t)Tb * 4, st));
+    HIPCHK(launch_bucket_ranges(ctx->sorted_buckets, ctx->P, ctx->bstart.as<uint32_t>(), ctx->bend.as<uint32_t>(),
+                                &dc->max_bucket, st));
+    std::vector<uint32_t> b0(Tb), b1(Tb);
+    HIPCHK(hipMemcpyAsync(b0.data(), ctx->bstart.p, (size_t)Tb * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(b1.data(), ctx->bend.p, (size_t)Tb * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    for (uint32_t b = 0; b < Tb; ++b) counts[b] = b1[b] - b0[b];
+    return MUMS_OK;
+}
+
+int mums_shard_probe_rows(mums_ctx* ctx, uint32_t nranks, const uint32_t* bounds, int64_t* d_rows,
+                          uint64_t capacity_rows, uint64_t* counts) {
+    int rc = shard_seeds_done(ctx);
+    if (rc) return rc;
+    if (nranks == 0 || nranks > 1024 || !bounds || !counts) return fail(ctx, MUMS_E_INVALID, "bad rank bounds");
+    if (bounds[0] != 0 || bounds[nranks] != ctx->table_size)
+        return fail(ctx, MUMS_E_INVALID, "bucket bounds must cover [0, table_size)");
+    for (uint32_t r = 0; r < nranks; ++r)
+        if (bounds[r] > bounds[r + 1]) return fail(ctx, MUMS_E_INVALID, "bucket bounds must not decrease");
+    const uint64_t P = ctx->P;
+    if (capacity_rows < P) return fail(ctx, MUMS_E_INVALID, "row buffer too small");
+    std::fill(counts, counts + nranks, 0ull);
+    if (P == 0) return MUMS_OK;
+    if (!d_rows) return fail(ctx, MUMS_E_INVALID, "null row buffer");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, ctx->masked, ctx->seq_mask};
+    rc = materialize_seeds(ctx, mp, st);
+    if (rc) return rc;
+    const int G = ctx->gt.G;
+    HIPCHK(ctx->rowtmp.ensure((P + 64) * 16 + 8192));
+    HIPCHK(ctx->keybuf.ensure((size_t)(nranks + 1) * 8 + 64));
+    HIPCHK(hipMemcpyAsync(ctx->keybuf.p, bounds, (size_t)(nranks + 1) * 4, hipMemcpyHostToDevice, st));
+    uint32_t* dest = (uint32_t*)ctx->rowtmp.p;
+    HIPCHK(launch_row_buckets(ctx->mprobe.as<int64_t>(), P, G, ctx->table_size, ctx->keybuf.as<uint32_t>(), nranks,
+                              dest, st));
+    rc = sort_row_keys(ctx, dest, P, std::max(1, ceil_log2(nranks)), st);   // stable: key order per rank
+    if (rc) return rc;
+    const uint32_t* perm = ctx->sorted_ids;
+    HIPCHK(launch_gather_rows(ctx->mprobe.as<int64_t>(), perm, P, G, d_rows, st));
+    // rows per destination rank = run lengths of the sorted destinations
+    std::vector<uint32_t> sd(P);
+    HIPCHK(hipMemcpyAsync(sd.data(), ctx->sorted_buckets, P * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    for (uint64_t i = 0; i < P; ++i) ++counts[sd[i]];
+    return MUMS_OK;
+}
+
+int mums_shard_packed_info(mums_ctx* ctx, uint64_t* word_offset, uint64_t* nwords, uint64_t* total_words) {
+    int rc = shard_seeds_done(ctx);
+    if (rc) return rc;
+    GenomeTable g = ctx->gt;
+    uint64_t total = 0;
+    (void)layout_packed(g, &total);
+    const uint32_t nl = (uint32_t)ctx->genomes.size();
+    if (word_offset) *word_offset = g.woff[ctx->shard_first];
+    if (nwords) *nwords = g.woff[ctx->shard_first + nl] - g.woff[ctx->shard_first];
+    if (total_words) *total_words = total;
+    return MUMS_OK;
+}
+
+int mums_shard_packed_copy(mums_ctx* ctx, uint32_t* d_dst) {
+    uint64_t off = 0, n = 0, tot = 0;
+    int rc = mums_shard_packed_info(ctx, &off, &n, &tot);
+    if (rc) return rc;
+    if (n == 0) return MUMS_OK;
+    if (!d_dst) return fail(ctx, MUMS_E_INVALID, "null destination");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipMemcpyAsync(d_dst, ctx->packed.p, n * 4, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return MUMS_OK;
+}
+
+int mums_shard_find(mums_ctx* ctx, const int64_t* d_rows, uint64_t nrows, const uint32_t* d_packed_all) {
+    int rc = shard_seeds_done(ctx);
+    if (rc) return rc;
+    if (nrows && (!d_rows || !d_packed_all)) return fail(ctx, MUMS_E_INVALID, "null rows / packed genomes");
+    if (nrows >= (1ull << 30)) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^30 seed probes on one rank");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    uint64_t words = 0;
+    (void)layout_packed(ctx->gt, &words);        // chain walks read every genome at its global offset
+    HIPCHK(ctx->counters.ensure(sizeof(DevCounters)));
+    DevCounters* dc = ctx->counters.as<DevCounters>();
+    HIPCHK(hipEventRecord(ctx->ev[EV_START], st));
+    HIPCHK(hipMemsetAsync(dc, 0, sizeof(DevCounters), st));
+    for (int e = EV_KEYS; e <= EV_GROUPS; ++e) HIPCHK(hipEventRecord(ctx->ev[e], st));
+    ctx->P = nrows;
+    ctx->probe_info = nullptr;
+    MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, ctx->masked, ctx->seq_mask};
+    int tbits = 1;
+    while (tbits < 32 && ((uint64_t)1 << tbits) < (uint64_t)ctx->table_size) ++tbits;
+    if (nrows) {
+        HIPCHK(ctx->rowtmp.ensure((nrows + 64) * 16 + 8192));
+        uint32_t* bkt = (uint32_t*)ctx->rowtmp.p;
+        HIPCHK(launch_row_buckets(d_rows, nrows, ctx->gt.G, ctx->table_size, nullptr, 0, bkt, st));
+        rc = sort_row_keys(ctx, bkt, nrows, tbits, st);   // stable: key order inside every bucket
+        if (rc) return rc;
+    }
+    HIPCHK(hipEventRecord(ctx->ev[EV_BUCKETS], st));
+    rc = find_tail(ctx, mp, d_packed_all, [&](MatProbes* v) {
+        v->rows = d_rows;
+        return MUMS_OK;
+    }, st);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipMemcpy(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost));
+    fill_stats(ctx, 0);
+    ctx->st.probes = nrows;
     return MUMS_OK;
 }
 

@@ -188,7 +188,12 @@ hipError_t launch_probe_compact(uint64_t ntiles, const uint32_t* tile_count, con
 // probes (key order) -> materialized rows (MatProbes, match_device.h)
 template <int MG, typename View>
 hipError_t launch_materialize(View v, const uint64_t* probe_info, uint64_t P, const GenomeTable& gt,
-                              const MatchParams& mp, int L, int64_t* s_out, int64_t* off_out, hipStream_t st);
+                              const MatchParams& mp, int L, int64_t* rows, hipStream_t st);
+// hash bucket of every row (d_bounds == nullptr) or its owning rank (bucket ranges)
+hipError_t launch_row_buckets(const int64_t* rows, uint64_t P, int G, uint32_t table_size, const uint32_t* d_bounds,
+                              uint32_t nranks, uint32_t* out, hipStream_t st);
+hipError_t launch_gather_rows(const int64_t* src, const uint32_t* perm, uint64_t P, int G, int64_t* dst,
+                              hipStream_t st);
 // flat tiles over [0, N) for the pair path (one bucket)
 hipError_t launch_flat_tiles(uint64_t N, SegTile* d_tiles, hipStream_t st);
 

@@ -64,9 +64,12 @@ class HipShardEngine:
     """One rank's MemHash context in sharded mode (C ABI, HIP kernels on `device`)."""
 
     def __init__(self, device: int, seed: int, lengths: Sequence[int], first: int, genomes: Sequence,
-                 profiling: bool = False):
+                 profiling: bool = False, table_size: int = 40000):
         self.mh = MemHash(device)
         self.device = torch.device("cuda", device)
+        self.G = len(lengths)
+        self.table_size = int(table_size)
+        self.mh.SetTableSize(self.table_size)
         self.mh.SetSeed(seed)
         for s in genomes:
             self.mh.AddSequence(s)
@@ -100,6 +103,41 @@ class HipShardEngine:
 
     def probes(self):
         return self.mh.Probes()
+
+    # ---- sharded FindMatches (mums_shard_bucket_counts / probe_rows / packed / find)
+    def bucket_counts(self) -> np.ndarray:
+        c = np.zeros(self.table_size, dtype=np.uint64)
+        self.mh._check(self.mh._lib.mums_shard_bucket_counts(self.mh._ctx, c.ctypes.data))
+        return c
+
+    def probe_rows(self, bounds: Sequence[int]) -> Tuple[torch.Tensor, np.ndarray]:
+        n = ctypes.c_uint64()
+        self.mh._check(self.mh._lib.mums_probe_count(self.mh._ctx, ctypes.byref(n)))
+        rows = torch.empty((max(n.value, 1), self.G + 1), dtype=torch.int64, device=self.device)
+        b = np.ascontiguousarray(bounds, dtype=np.uint32)
+        counts = np.zeros(len(bounds) - 1, dtype=np.uint64)
+        self.mh._check(self.mh._lib.mums_shard_probe_rows(self.mh._ctx, len(bounds) - 1, b.ctypes.data,
+                                                           ctypes.c_void_p(rows.data_ptr()), rows.shape[0],
+                                                           counts.ctypes.data))
+        return rows[:n.value], counts
+
+    def packed(self) -> Tuple[int, torch.Tensor, int]:
+        off, n, tot = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        self.mh._check(self.mh._lib.mums_shard_packed_info(self.mh._ctx, ctypes.byref(off), ctypes.byref(n),
+                                                            ctypes.byref(tot)))
+        words = torch.empty(max(n.value, 1), dtype=torch.int32, device=self.device)
+        self.mh._check(self.mh._lib.mums_shard_packed_copy(self.mh._ctx, ctypes.c_void_p(words.data_ptr())))
+        return int(off.value), words[:n.value], int(tot.value)
+
+    def find(self, rows: torch.Tensor, packed_all: torch.Tensor) -> None:
+        rows = rows.to(self.device).contiguous()
+        packed_all = packed_all.to(self.device).contiguous()
+        torch.cuda.synchronize(self.device)
+        self.mh._check(self.mh._lib.mums_shard_find(self.mh._ctx, ctypes.c_void_p(rows.data_ptr()), rows.shape[0],
+                                                     ctypes.c_void_p(packed_all.data_ptr())))
+
+    def matches(self):
+        return self.mh.GetMatchList()
 
     def close(self) -> None:
         self.mh.close()
@@ -158,4 +196,78 @@ class ShardedSeedStage:
         eng.merge(out, self.world, first, cnt, sub)
 
 
-__all__ = ["key_ranges", "genome_blocks", "HipShardEngine", "ShardedSeedStage"]
+class ShardedFindMatches:
+    """Sharded MemHash::FindMatches (SURVEY.md 8(e)) for one rank: the sharded seed
+    stage, then the probes move to the rank owning their hash bucket and every rank
+    replays its bucket range (chain labelling + AddHashEntry, MemHash.cpp:209-251):
+
+      5. buckets : per-bucket probe counts all-gathered; the hash buckets are cut into
+                   world_size contiguous ranges of balanced probe counts;
+      6. rows    : every probe as G+1 int64 {starts, offset}, grouped by owner rank in
+                   key order; one all-to-all (sources in rank order = key order);
+      7. genomes : every rank's 2-bit packed genomes all-gathered (chain walks read any
+                   genome);
+      8. find    : chain labelling + replay of the rank's buckets (mums_shard_find).
+
+    The ranks' MatchLists concatenated in rank order are the reference's bucket-major
+    MatchList (MemHash.h:182-203)."""
+
+    def __init__(self, engine, group: Optional[dist.ProcessGroup] = None):
+        self.engine = engine
+        self.group = group
+        self.seeds = ShardedSeedStage(engine, group)
+        self.world, self.rank, self.wire = self.seeds.world, self.seeds.rank, self.seeds.wire
+        self.bucket_range: Tuple[int, int] = (0, 0)
+        self.last_exchange_bytes = 0
+
+    def _gather_np(self, a: np.ndarray) -> np.ndarray:
+        return self.seeds._all_gather_counts(a)
+
+    def run(self):
+        eng = self.engine
+        self.seeds.run()
+        T = eng.table_size
+        C = self._gather_np(eng.bucket_counts())                     # [world, T]
+        ranges = key_ranges(C.sum(axis=0), self.world)
+        bounds = [f for f, _ in ranges] + [T]
+        self.bucket_range = ranges[self.rank]
+        rows, send = eng.probe_rows(bounds)                           # [P, G+1], per-destination counts
+        W = rows.shape[1]
+        S = self._gather_np(send.astype(np.int64))                    # [src, dst]
+        recv = [int(S[s, self.rank]) for s in range(self.world)]
+        if self.world == 1:
+            recv_rows = rows
+        else:
+            src = rows if self.wire == "cuda" else rows.cpu()
+            out = torch.empty((sum(recv), W), dtype=torch.int64, device=src.device)
+            dist.all_to_all_single(out.view(-1), src.contiguous().view(-1), [r * W for r in recv],
+                                   [int(c) * W for c in send], group=self.group)
+            if self.wire == "cuda":
+                torch.cuda.current_stream().synchronize()
+            self.last_exchange_bytes = 8 * W * (int(send.sum()) - int(send[self.rank]))
+            recv_rows = out
+        off, words, total = eng.packed()
+        full = self._all_gather_packed(off, words, total)
+        eng.find(recv_rows, full)
+        return eng.matches()
+
+    def _all_gather_packed(self, off: int, words: torch.Tensor, total: int) -> torch.Tensor:
+        if self.world == 1:
+            full = torch.zeros(total, dtype=torch.int32, device=words.device)
+            full[off:off + words.numel()] = words
+            return full
+        meta = self._gather_np(np.array([off, words.numel()], dtype=np.int64))
+        mx = int(meta[:, 1].max())
+        dev = words.device if self.wire == "cuda" else torch.device("cpu")
+        pad = torch.zeros(max(mx, 1), dtype=torch.int32, device=dev)
+        pad[:words.numel()] = words.to(dev)
+        parts = [torch.empty_like(pad) for _ in range(self.world)]
+        dist.all_gather(parts, pad, group=self.group)
+        full = torch.zeros(total, dtype=torch.int32, device=dev)
+        for r in range(self.world):
+            o, n = int(meta[r, 0]), int(meta[r, 1])
+            full[o:o + n] = parts[r][:n]
+        return full
+
+
+__all__ = ["key_ranges", "genome_blocks", "HipShardEngine", "ShardedSeedStage", "ShardedFindMatches"]

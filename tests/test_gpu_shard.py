@@ -55,3 +55,25 @@ def test_sharded_seed_stage_gpu(oracle_mod, G, n, p, w, world):
     assert sum(int(x[0]) for x in s) == st["seedmers"]
     assert np.array_equal(b, ob)
     assert np.array_equal(r, orf)
+
+
+@pytest.mark.parametrize("G,n,p,w,world,T", [(4, 300_000, 0.02, 15, 2, 40000), (3, 200_000, 0.05, 19, 3, 40000),
+                                               (5, 100_000, 1.0, 15, 2, 40000), (4, 200_000, 0.01, 15, 3, 7)])
+def test_sharded_find_matches_gpu(oracle_mod, G, n, p, w, world, T):
+    """Sharded FindMatches (probe rows to bucket owners, packed-genome allgather, per-rank
+    replay): the ranks' MatchLists in rank order = the oracle's MatchList, bit for bit."""
+    seqs = oracle_mod.generate(G, n, p, 4242 + G)
+    ref_len, ref_st, ref_stats = oracle_mod.find_matches(seqs, oracle_mod.get_seed(w), table_size=T)
+    with tempfile.TemporaryDirectory() as d:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+               "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+               os.path.join(ROOT, "tests", "gpu_shard_find_worker.py"), d, str(G), str(n), str(p), str(w), str(T)]
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        res = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+        assert res.returncode == 0, res.stderr[-3000:]
+        lens = np.concatenate([np.load(os.path.join(d, f"len{r}.npy")) for r in range(world)])
+        sts = np.concatenate([np.load(os.path.join(d, f"st{r}.npy")).reshape(-1, G) for r in range(world)])
+        stats = sum(np.load(os.path.join(d, f"stats{r}.npy")) for r in range(world))
+    assert len(lens) == len(ref_len)
+    assert (lens == ref_len).all() and (sts == ref_st).all()
+    assert int(stats[0]) == ref_stats["mem_count"] and int(stats[1]) == ref_stats["collision_count"]
