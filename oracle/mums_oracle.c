@@ -669,6 +669,70 @@ done:
     return res;
 }
 
+/* AddHashEntry replay of given probes (test aid for the sharded FindMatches): rows of
+ * G+1 int64 {signed starts after SetDirection, offset} in AddHashEntry order; each is
+ * looked up, extended and inserted exactly as in oracle_find_matches. */
+oracle_result* oracle_replay_rows(int G, const char* const* seqs, const uint64_t* lens, const oracle_params* prm,
+                                  const int64_t* rows, uint64_t nrows) {
+    if (G < 1 || G > 64) return NULL;
+    oracle_result* res = (oracle_result*)calloc(1, sizeof(oracle_result));
+    res->G = G;
+    sml_ctx* ctx = (sml_ctx*)calloc((size_t)G, sizeof(sml_ctx));
+    uint32_t** words = (uint32_t**)calloc((size_t)G, sizeof(uint32_t*));
+    uint64_t** keys = (uint64_t**)calloc((size_t)G, sizeof(uint64_t*));
+    for (int g = 0; g < G; ++g) {
+        if (sml_init(&ctx[g], seqs[g], lens[g], prm->seed, &words[g])) goto done;
+        uint64_t m = sml_length(lens[g], ctx[g].L);
+        keys[g] = (uint64_t*)malloc((m ? m : 1) * sizeof(uint64_t));
+        for (uint64_t q = 0; q < m; ++q) keys[g][q] = get_dna_seed_mer(&ctx[g], q);
+    }
+    {
+        memhash_t h;
+        memset(&h, 0, sizeof(h));
+        h.x.G = G;
+        h.x.L = ctx[0].L;
+        h.x.seed_mask = ctx[0].seed_mask;
+        h.x.keys = (const uint64_t**)keys;
+        h.x.n = lens;
+        h.x.gnseqi_end = prm->gnseqi_end_neg1 ? (int64_t)-1 : INT64_MAX;
+        h.table_size = prm->table_size ? prm->table_size : 40000;
+        h.buckets = (bucket_t*)calloc(h.table_size, sizeof(bucket_t));
+        int64_t* sv = (int64_t*)malloc((size_t)G * sizeof(int64_t));
+        for (uint64_t r = 0; r < nrows; ++r) {
+            const int64_t* row = rows + r * (uint64_t)(G + 1);
+            mhe_t p;
+            memcpy(sv, row, (size_t)G * sizeof(int64_t));
+            p.s = sv;
+            p.len = h.x.L;
+            p.mersize = h.x.L;
+            calc_offset(&p, G);
+            add_hash_entry(&h, &p);
+        }
+        free(sv);
+        res->count = h.mem_count;
+        res->lengths = (uint64_t*)malloc((h.mem_count ? h.mem_count : 1) * sizeof(uint64_t));
+        res->starts = (int64_t*)malloc((h.mem_count ? h.mem_count : 1) * (size_t)G * sizeof(int64_t));
+        uint64_t o = 0;
+        for (uint32_t bi = 0; bi < h.table_size; ++bi) {
+            for (uint32_t k = 0; k < h.buckets[bi].n; ++k) {
+                const mhe_t* e = &h.pool[h.buckets[bi].v[k]];
+                res->lengths[o] = (uint64_t)e->len;
+                memcpy(res->starts + o * (uint64_t)G, e->s, (size_t)G * sizeof(int64_t));
+                ++o;
+            }
+            free(h.buckets[bi].v);
+        }
+        res->mem_count = h.mem_count;
+        res->collision_count = h.collisions;
+        res->probes = h.probes;
+        free(h.buckets); free(h.pool); free(h.spool);
+    }
+done:
+    for (int g = 0; g < G; ++g) { free(words[g]); free(keys[g]); }
+    free(ctx); free(words); free(keys);
+    return res;
+}
+
 uint64_t oracle_result_count(const oracle_result* r) { return r ? r->count : 0; }
 int      oracle_result_seqcount(const oracle_result* r) { return r ? r->G : 0; }
 void     oracle_result_copy(const oracle_result* r, uint64_t* lengths, int64_t* starts) {

@@ -68,6 +68,9 @@ uint64_t oracle_result_probe_count(const oracle_result* r);
 int      oracle_result_probe_log(const oracle_result* r, uint32_t* buckets, uint64_t* ref);
 uint64_t oracle_result_seedmers(const oracle_result* r);
 void     oracle_result_free(oracle_result* r);
+/* AddHashEntry replay of probe rows {starts[G], offset} (sharded FindMatches checks). */
+oracle_result* oracle_replay_rows(int G, const char* const* seqs, const uint64_t* lens, const oracle_params* prm,
+                                  const int64_t* rows, uint64_t nrows);
 
 /* ---- synthetic genomes (SURVEY.md Appendix C generator) ---- */
 /* fills G buffers of n bytes each (caller allocates G*n bytes, genome-major) */

@@ -135,6 +135,33 @@ def find_matches(seqs: Sequence[bytes], seed: int, repeat_tol: int = 0, enum_tol
     return lengths, starts, stats
 
 
+def replay_rows(seqs: Sequence[bytes], seed: int, rows: np.ndarray, table_size: int = 40000):
+    """AddHashEntry replay (extension + bucket insertion) of given probe rows
+    {starts[G], offset} in order; returns (lengths, starts, counters) like find_matches."""
+    G = len(seqs)
+    arr = (ctypes.c_char_p * G)(*seqs)
+    lens = (ctypes.c_uint64 * G)(*[len(s) for s in seqs])
+    prm = _Params(seed, 0, 1, table_size, 0, 0, 0, 0)
+    rows = np.ascontiguousarray(rows, dtype=np.int64).reshape(-1, G + 1)
+    L = lib()
+    L.oracle_replay_rows.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_uint64),
+                                     ctypes.POINTER(_Params), ctypes.c_void_p, ctypes.c_uint64]
+    L.oracle_replay_rows.restype = ctypes.c_void_p
+    r = L.oracle_replay_rows(G, arr, lens, ctypes.byref(prm), rows.ctypes.data, rows.shape[0])
+    if not r:
+        raise ValueError("oracle rejected input")
+    try:
+        c = L.oracle_result_count(r)
+        lengths = np.zeros(c, dtype=np.uint64)
+        starts = np.zeros((c, G), dtype=np.int64)
+        if c:
+            L.oracle_result_copy(r, lengths.ctypes.data, starts.ctypes.data)
+        stats = dict(mem_count=L.oracle_result_mem_count(r), collision_count=L.oracle_result_collision_count(r))
+    finally:
+        L.oracle_result_free(r)
+    return lengths, starts, stats
+
+
 def seed_probes(seqs: Sequence[bytes], seed: int, table_size: int = 40000) -> Tuple[np.ndarray, np.ndarray, dict]:
     """Seed stage only (keys, SMLs, G-way merge, acceptance, probes): the AddHashEntry calls
     in order as (bucket[P], ref[P]) with ref = global seed-mer index of the probe's first

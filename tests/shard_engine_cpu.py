@@ -31,8 +31,11 @@ class CpuShardEngine:
         self.m = [max(len(s) - self.L + 1, 0) for s in seqs]
         self.base = np.concatenate([[0], np.cumsum(self.m)]).astype(np.int64)
         self.klow = self.kbits - self.B
+        self.table_size = table_size
         self.probe_buckets = np.zeros(0, np.uint32)
         self.probe_refs = np.zeros(0, np.uint64)
+        self.probe_rows_ = np.zeros((0, len(seqs) + 1), np.int64)
+        self.result = None
 
     def msd_bits(self):
         return self.B, int(sum(self.m[self.first:self.first + self.count]))
@@ -77,7 +80,7 @@ class CpuShardEngine:
         G = len(self.seqs)
         heads = np.flatnonzero(np.concatenate([[True], gk[1:] != gk[:-1]])) if ck.size else np.zeros(0, int)
         ends = np.concatenate([heads[1:], [ck.size]]).astype(int)
-        pb, pr = [], []
+        pb, pr, rows = [], [], []
         T = self.T
         for h, e in zip(heads, ends):
             if e - h < 2 or e - h > G:
@@ -97,8 +100,41 @@ class CpuShardEngine:
                 off += (-s - sref - self.L) if int(par[h + j]) != pref else (s - sref)
             pb.append(((off % T) + T) % T)
             pr.append(int(idx.min()))
+            row = np.zeros(G + 1, np.int64)   # SetDirection (MemHash.cpp:189-203) + CalculateOffset
+            for j in range(e - h):
+                s = int(idx[j] - self.base[gen[j]]) + 1
+                row[gen[j]] = -s if (j != k and int(par[h + j]) != pref) else s
+            row[G] = off
+            rows.append(row)
         self.probe_buckets = np.array(pb, dtype=np.uint32)
         self.probe_refs = np.array(pr, dtype=np.uint64)
+        self.probe_rows_ = np.array(rows, dtype=np.int64).reshape(-1, G + 1)
 
     def probes(self):
         return self.probe_buckets, self.probe_refs
+
+    # ---- sharded FindMatches contract (mums_shard_bucket_counts / probe_rows / packed / find)
+    def bucket_counts(self) -> np.ndarray:
+        return np.bincount(self.probe_buckets, minlength=self.T).astype(np.uint64)
+
+    def probe_rows(self, bounds):
+        dest = np.searchsorted(np.asarray(bounds), self.probe_buckets, side="right") - 1
+        order = np.argsort(dest, kind="stable")
+        counts = np.bincount(dest, minlength=len(bounds) - 1).astype(np.uint64)
+        return torch.from_numpy(np.ascontiguousarray(self.probe_rows_[order])), counts
+
+    def packed(self):
+        return 0, torch.zeros(0, dtype=torch.int32), 0   # the oracle replay reads the sequences
+
+    def find(self, rows: torch.Tensor, packed_all: torch.Tensor) -> None:
+        self.result = oracle.replay_rows(self.seqs, self.seed, rows.numpy(), self.T)
+
+    def matches(self):
+        class _ML:
+            pass
+        ml = _ML()
+        ml.lengths, ml.starts = self.result[0], self.result[1]
+        return ml
+
+    def stats(self) -> dict:
+        return dict(self.result[2]) if self.result else {}

@@ -103,3 +103,42 @@ def test_single_rank_engine_matches_oracle(oracle_mod):
     b, r = eng.probes()
     ob, orf, _ = oracle_mod.seed_probes(seqs, seed)
     assert np.array_equal(b, ob) and np.array_equal(r, orf)
+
+
+def _find_worker(rank, world, port, seqs, seed, T, outdir):
+    import torch.distributed as dist
+    from libmems_amd.shard import ShardedFindMatches, genome_blocks
+    from tests.shard_engine_cpu import CpuShardEngine
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        first, count = genome_blocks(len(seqs), world)[rank]
+        eng = CpuShardEngine(seqs, first, count, seed, table_size=T)
+        ml = ShardedFindMatches(eng).run()
+        st = eng.stats()
+        np.save(os.path.join(outdir, f"l{rank}.npy"), ml.lengths)
+        np.save(os.path.join(outdir, f"s{rank}.npy"), ml.starts)
+        np.save(os.path.join(outdir, f"c{rank}.npy"), np.array([st["mem_count"], st["collision_count"]]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("G,n,p,w,T", [(4, 60_000, 0.02, 15, 40000), (3, 50_000, 0.05, 15, 13)])
+def test_sharded_find_matches_gloo_world2(oracle_mod, G, n, p, w, T):
+    """Sharded FindMatches orchestration (bucket ranges, row all-to-all, packed allgather)
+    under gloo world_size 2 with the CPU engine: ranks' MatchLists in rank order = the
+    oracle's serial MemHash MatchList."""
+    seqs = oracle_mod.generate(G, n, p, 99 + G)
+    seed = oracle_mod.get_seed(w)
+    ref_l, ref_s, ref_st = oracle_mod.find_matches(seqs, seed, table_size=T)
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_find_worker, args=(world, _free_port(), seqs, seed, T, d), nprocs=world, join=True)
+        lens = np.concatenate([np.load(os.path.join(d, f"l{r}.npy")) for r in range(world)])
+        sts = np.concatenate([np.load(os.path.join(d, f"s{r}.npy")).reshape(-1, G) for r in range(world)])
+        cnt = sum(np.load(os.path.join(d, f"c{r}.npy")) for r in range(world))
+    assert len(lens) == len(ref_l) > 0
+    assert (lens == ref_l).all() and (sts == ref_s).all()
+    assert int(cnt[0]) == ref_st["mem_count"] and int(cnt[1]) == ref_st["collision_count"]
