@@ -71,6 +71,7 @@ typedef struct mums_stats {
     uint64_t sort_passes;
     double   ms_chains;         /* seed-chain labelling before the replay (ExtendMatch results)        */
     uint64_t chains;            /* seed chains among the probes                                        */
+    uint64_t chunks;            /* ParallelMemHash compat: SML chunks searched (ParallelMemHash.cpp:75-83) */
 } mums_stats;
 
 /* MemHash::MemHash (MemHash.cpp:33-49); device = HIP ordinal. */
@@ -90,6 +91,13 @@ int  mums_set_params(mums_ctx* ctx, uint32_t repeat_tol, uint32_t enum_tol, uint
 /* MaskedMemHash (MaskedMemHash.h:25-40): masked=1 selects MaskedMemHash::HashMatch
  * semantics; seq_mask = MaskedMemHash::SetMask (genome 0 = most significant bit). */
 int  mums_set_mask(mums_ctx* ctx, int masked, uint64_t seq_mask);
+/* ParallelMemHash (ParallelMemHash.h:29-48, FindMatches ParallelMemHash.cpp:42-103):
+ * enable=1 reproduces its chunked search -- SML chunks of chunk_size mers of the
+ * longest SML cut by MatchFinder::GetBreakpoint (MatchFinder.cpp:89-126), searched
+ * one by one, thread tables merged by MergeTable (:105-121) -- so the MatchList is
+ * the (patched) OpenMP reference's.  chunk_size 0 = the
+ * reference's CHUNK_SIZE 200000 (:51).  enable=0 = serial MemHash (default). */
+int  mums_set_parallel_compat(mums_ctx* ctx, int enable, uint64_t chunk_size);
 
 /* MatchFinder::AddSequence (MatchFinder.cpp:59-87) for a host ASCII genome
  * (copied to HBM).  Genome ids are assigned in call order. */

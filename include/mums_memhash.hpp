@@ -139,4 +139,14 @@ public:
     virtual void SetMask(uint64_t seq_mask) { check(mums_set_mask(ctx_, 1, seq_mask)); }
 };
 
+// ParallelMemHash (ParallelMemHash.h:29-48): same API, the chunked search of
+// ParallelMemHash::FindMatches (ParallelMemHash.cpp:42-121) -- its MatchList, not
+// MemHash's, at chunk boundaries.  chunk_size = CHUNK_SIZE (ParallelMemHash.cpp:51).
+class ParallelMemHash : public MemHash {
+public:
+    explicit ParallelMemHash(int device = 0, uint64_t chunk_size = 200000) : MemHash(device) {
+        check(mums_set_parallel_compat(ctx_, 1, chunk_size));
+    }
+};
+
 }  // namespace mums

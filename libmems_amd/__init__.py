@@ -77,6 +77,7 @@ class _Stats(ctypes.Structure):
         ("sort_passes", ctypes.c_uint64),
         ("ms_chains", ctypes.c_double),
         ("chains", ctypes.c_uint64),
+        ("chunks", ctypes.c_uint64),
     ]
 
 
@@ -87,7 +88,7 @@ EXPORTED_SYMBOLS = [
     "mums_last_error", "mums_get_seed", "mums_default_seed_weight", "mums_copy_seed_keys",
     "mums_build_sml", "mums_set_profiling", "mums_shard_layout", "mums_shard_msd_bits", "mums_shard_keys",
     "mums_shard_merge", "mums_probe_count", "mums_probe_copy", "mums_shard_bucket_counts", "mums_shard_probe_rows",
-    "mums_shard_packed_info", "mums_shard_packed_copy", "mums_shard_find",
+    "mums_shard_packed_info", "mums_shard_packed_copy", "mums_shard_find", "mums_set_parallel_compat",
 ]
 
 _lib: Optional[ctypes.CDLL] = None
@@ -144,6 +145,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mums_shard_packed_info.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]
     lib.mums_shard_packed_copy.argtypes = [vp, vp]
     lib.mums_shard_find.argtypes = [vp, vp, u64, vp]
+    lib.mums_set_parallel_compat.argtypes = [vp, i32, u64]
     _lib = lib
     return lib
 
@@ -346,7 +348,20 @@ class MaskedMemHash(MemHash):
         self._check(self._lib.mums_set_mask(self._ctx, 1, seq_mask))
 
 
+class ParallelMemHash(MemHash):
+    """ParallelMemHash (ParallelMemHash.h:29-48): the chunked OpenMP MemHash whose MatchList
+    differs from MemHash's at chunk boundaries (ParallelMemHash.cpp:42-121).  The GPU
+    reproduces its output (chunks cut by GetBreakpoint, searched in order, thread tables
+    merged by MergeTable); chunk_size is its CHUNK_SIZE (200000, :51)."""
+
+    CHUNK_SIZE = 200000
+
+    def __init__(self, device: int = 0, chunk_size: int = CHUNK_SIZE):
+        super().__init__(device)
+        self._check(self._lib.mums_set_parallel_compat(self._ctx, 1, chunk_size))
+
+
 __all__ = [
-    "MemHash", "MaskedMemHash", "MatchList", "MumsError", "GapInSequence", "getSeed", "getSeedLength",
+    "MemHash", "MaskedMemHash", "ParallelMemHash", "MatchList", "MumsError", "GapInSequence", "getSeed", "getSeedLength",
     "getSeedWeight", "getDefaultSeedWeight", "load_library", "EXPORTED_SYMBOLS", "STAGE_SEEDS", "STAGE_ALL",
 ]

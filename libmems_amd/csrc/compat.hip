@@ -1,0 +1,204 @@
+// compat.hip -- ParallelMemHash chunk-compat mode.
+//
+// ParallelMemHash::FindMatches (ParallelMemHash.cpp:42-103) cuts the SMLs into chunks:
+// chunk starts come from MatchFinder::GetBreakpoint (MatchFinder.cpp:89-126) every
+// CHUNK_SIZE (200000) mers of the longest SML, each chunk is searched on its own
+// (SearchRange, MatchFinder.cpp:172-340) and the thread tables are re-added into one
+// table (MergeTable, :105-121).  A masked-key group whose records straddle a chunk
+// boundary in some genome is therefore searched as several smaller groups.
+//
+// On the GPU the chunk becomes part of the sort key: every record gets
+// key2 = (chunk << (2w+1)) | ckey, so one stable sort of (key2, index) yields the
+// chunk-major probe order the reference's AddHashEntry calls follow, and the unchanged
+// group / probe / chain / replay kernels run on it.  The MergeTable re-insertion is
+// replayed per bucket at the end (compat_merge_kernel).
+//
+//   1. genome_keys_kernel     key' = genome << kbits | ckey; one stable sort of key'
+//                             gives every genome's SortedMerList as a segment
+//   2. compat_breaks_kernel   chunk starts on the longest SML (sequential walk)
+//   3. compat_find_kernel     FindMer (bsearch) of each break mer in the other SMLs
+//   4. compat_chunk_keys      chunk of every record -> key2
+//   5. compat_merge_kernel    MergeTable: re-add each bucket's entries in vector order
+#include <hip/hip_runtime.h>
+
+#include "match_device.h"
+#include "mums_internal.h"
+
+namespace mums {
+namespace {
+
+// key' = genome << kbits | ckey (the genome's SML becomes a contiguous segment of the
+// sorted key' order: positions ascending within equal ckey, MemorySML.cpp:45-60)
+__global__ void genome_keys_kernel(uint64_t* __restrict__ ckey, uint64_t N, GenomeTable gt, int kbits) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    ckey[i] |= (uint64_t)genome_of(gt, i) << kbits;
+}
+
+// MatchFinder::GetBreakpoint on the longest SML mx, repeated as ParallelMemHash.cpp:75-83
+// does: start = previous + chunk; walk back to the first index of the start's masked key.
+// cs[k * G + g] = start of chunk k in SML g (row 0 pre-zeroed); bm[k] = break mer.
+// Error bits: 4 = chunk cap exceeded (a masked-key group >= chunk: the reference loops
+// forever), 8 = start past the SML end (operator[] out of range in the reference).
+__global__ void compat_breaks_kernel(const uint64_t* __restrict__ sk, GenomeTable gt, uint64_t kmask, int mx,
+                                     uint64_t chunk, uint64_t* __restrict__ cs, uint64_t* __restrict__ bm,
+                                     uint32_t cap, uint32_t* __restrict__ d_nch, uint32_t* __restrict__ err) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    const uint64_t* seg = sk + gt.base[mx];
+    const uint64_t m = gt.m[mx], n = gt.n[mx];
+    const int G = gt.G;
+    uint32_t k = 1;
+    uint64_t s = 0;
+    while (s + chunk < n) {   // Length() = sequence length (SortedMerList.cpp:284-286)
+        if (k >= cap) { atomicOr(err, 4u); break; }
+        uint64_t i = s + chunk;
+        if (i >= m) { atomicOr(err, 8u); break; }
+        const uint64_t b = seg[i] & kmask;
+        uint64_t prev = b;
+        while ((prev >> 1) == (b >> 1)) {   // masked key = ckey without the parity bit
+            if (i == 0) { i = ~0ull; break; }
+            --i;
+            prev = seg[i] & kmask;
+        }
+        ++i;
+        cs[(uint64_t)k * G + mx] = i;
+        bm[k] = b;
+        s = i;
+        ++k;
+    }
+    *d_nch = k;
+}
+
+// The other SMLs' chunk starts: SortedMerList::FindMer (SortedMerList.cpp:170-179) with
+// the full break mer; bsearch (:380-394) returns the probed middle when absent.  The
+// backward loop of GetBreakpoint (MatchFinder.cpp:114-121) compares with
+// (break_mer.mer && mer_mask), a bool: it never runs unless the break mer is 0, where it
+// runs down to -1.  So a found mer starts the chunk one past it (or at 0 for mer 0).
+__global__ void compat_find_kernel(const uint64_t* __restrict__ sk, GenomeTable gt, uint64_t kmask, int mx, int L,
+                                   uint64_t* __restrict__ cs, const uint64_t* __restrict__ bm, uint32_t nch) {
+    const int G = gt.G;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (uint64_t)(nch - 1) * G) return;
+    const uint32_t k = 1 + (uint32_t)(t / G);
+    const int g = (int)(t % G);
+    if (g == mx) return;
+    const uint64_t q = bm[k];
+    const uint64_t n = gt.n[g];
+    uint64_t cur = 0;   // FindMer's early return leaves the caller's value (0 here)
+    if (n != 0 && n >= (uint64_t)L) {
+        const uint64_t* seg = sk + gt.base[g];
+        uint64_t start = 0, end = n - (uint64_t)L;
+        for (;;) {
+            const uint64_t mid = (start + end) / 2;
+            const uint64_t v = seg[mid] & kmask;
+            cur = mid;
+            if (v == q) break;
+            if (v < q && mid < end) start = mid + 1;
+            else if (v > q && start < mid) end = mid - 1;
+            else break;
+        }
+        if ((seg[cur] & kmask) == q) cur = (q == 0) ? 0 : cur + 1;
+    }
+    cs[(uint64_t)k * G + g] = cur;
+}
+
+// chunk of SML index r of genome g = last k with cs[k][g] <= r (cs[0][g] = 0)
+__global__ void compat_chunk_keys_kernel(const uint64_t* __restrict__ sk, const uint32_t* __restrict__ sv, uint64_t N,
+                                         GenomeTable gt, int kbits, const uint64_t* __restrict__ cs, uint32_t nch,
+                                         uint64_t* __restrict__ key2, uint32_t* __restrict__ val2) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= N) return;
+    const uint64_t kmask = (kbits >= 64) ? ~0ull : ((1ull << kbits) - 1);
+    const uint64_t x = sk[j];
+    const int g = (int)(x >> kbits);
+    const uint64_t r = j - gt.base[g];
+    const int G = gt.G;
+    uint32_t lo = 0, hi = nch - 1;   // invariant: cs[lo][g] <= r
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (cs[(uint64_t)mid * G + g] <= r) lo = mid;
+        else hi = mid - 1;
+    }
+    key2[j] = ((uint64_t)lo << kbits) | (x & kmask);
+    val2[j] = sv[j];
+}
+
+// MergeTable (ParallelMemHash.cpp:105-121): every entry of the thread table is re-added
+// with AddHashEntry (MemHash.cpp:209-251) into the global table: lower_bound, a
+// collision when equivalent (MheCompare both ways false), else inserted at the
+// lower_bound; entries are already Extended() (:223), so nothing is re-extended.  One
+// thread per bucket, in place: the merged prefix never overtakes the entry being read.
+template <int MG>
+__global__ __launch_bounds__(256) void compat_merge_kernel(uint32_t* __restrict__ tsize,
+                                                           const uint32_t* __restrict__ bstart,
+                                                           uint32_t* __restrict__ tbl,
+                                                           const int64_t* __restrict__ pool, int G, uint32_t Tb,
+                                                           unsigned long long* __restrict__ collisions) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= Tb) return;
+    const uint32_t n = tsize[b];
+    if (n < 2) return;
+    uint32_t* v = tbl + bstart[b];
+    uint32_t out = 0, dropped = 0;
+    Mhe<MG> e, x;
+    for (uint32_t j = 0; j < n; ++j) {
+        const uint32_t id = v[j];
+        load_entry(pool, id, G, e);
+        const uint32_t it = lower_bound_tbl<MG>(v, out, pool, G, e);
+        if (it != out) {
+            load_entry(pool, v[it], G, x);
+            if (!mhe_less(x, e) && !mhe_less(e, x)) { ++dropped; continue; }
+        }
+        for (uint32_t q = out; q > it; --q) v[q] = v[q - 1];
+        v[it] = id;
+        ++out;
+    }
+    tsize[b] = out;
+    if (dropped) atomicAdd(collisions, (unsigned long long)dropped);
+}
+
+}  // namespace
+
+hipError_t launch_genome_keys(uint64_t* ckey, uint64_t N, const GenomeTable& gt, int kbits, hipStream_t st) {
+    if (N == 0) return hipSuccess;
+    hipLaunchKernelGGL(genome_keys_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, ckey, N, gt, kbits);
+    return hipGetLastError();
+}
+
+hipError_t launch_compat_breaks(const uint64_t* sk, const GenomeTable& gt, uint64_t kmask, int mx, uint64_t chunk,
+                                uint64_t* cs, uint64_t* bm, uint32_t cap, uint32_t* d_nch, uint32_t* err,
+                                hipStream_t st) {
+    hipLaunchKernelGGL(compat_breaks_kernel, dim3(1), dim3(64), 0, st, sk, gt, kmask, mx, chunk, cs, bm, cap, d_nch,
+                       err);
+    return hipGetLastError();
+}
+
+hipError_t launch_compat_find(const uint64_t* sk, const GenomeTable& gt, uint64_t kmask, int mx, int L, uint64_t* cs,
+                              const uint64_t* bm, uint32_t nch, hipStream_t st) {
+    if (nch < 2) return hipSuccess;
+    const uint64_t t = (uint64_t)(nch - 1) * gt.G;
+    hipLaunchKernelGGL(compat_find_kernel, dim3((unsigned)((t + 255) / 256)), dim3(256), 0, st, sk, gt, kmask, mx, L,
+                       cs, bm, nch);
+    return hipGetLastError();
+}
+
+hipError_t launch_compat_chunk_keys(const uint64_t* sk, const uint32_t* sv, uint64_t N, const GenomeTable& gt,
+                                    int kbits, const uint64_t* cs, uint32_t nch, uint64_t* key2, uint32_t* val2,
+                                    hipStream_t st) {
+    if (N == 0) return hipSuccess;
+    hipLaunchKernelGGL(compat_chunk_keys_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, sk, sv, N, gt,
+                       kbits, cs, nch, key2, val2);
+    return hipGetLastError();
+}
+
+hipError_t launch_compat_merge(uint32_t* tsize, const uint32_t* bstart, uint32_t* tbl, const int64_t* pool, int G,
+                               uint32_t Tb, unsigned long long* collisions, hipStream_t st) {
+    const dim3 grid((Tb + 255) / 256), blk(256);
+    if (G <= 4) hipLaunchKernelGGL(compat_merge_kernel<4>, grid, blk, 0, st, tsize, bstart, tbl, pool, G, Tb, collisions);
+    else if (G <= 8) hipLaunchKernelGGL(compat_merge_kernel<8>, grid, blk, 0, st, tsize, bstart, tbl, pool, G, Tb, collisions);
+    else if (G <= 16) hipLaunchKernelGGL(compat_merge_kernel<16>, grid, blk, 0, st, tsize, bstart, tbl, pool, G, Tb, collisions);
+    else hipLaunchKernelGGL(compat_merge_kernel<32>, grid, blk, 0, st, tsize, bstart, tbl, pool, G, Tb, collisions);
+    return hipGetLastError();
+}
+
+}  // namespace mums

@@ -75,6 +75,11 @@ struct mums_ctx {
     DevBuf bstart, bend, tsize, obase, pool, tbl, out_len, out_s, pbuf, keybuf, mstart;
     DevBuf chain_tmp, chain_of, radix_tmp, spill, summ, dbgbuf, mprobe, rowtmp;
     bool use_onesweep = true;
+    // ParallelMemHash chunk-compat mode (compat.hip): chunk = CHUNK_SIZE, ParallelMemHash.cpp:51
+    bool pcompat = false;
+    uint64_t chunk_size = 200000;
+    uint32_t nchunks = 0;
+    DevBuf cval, ctab;
     hipEvent_t ev[EV_COUNT] = {};
     bool profiling = false;
     hipEvent_t ev_ds[16] = {};   // 2 per radix pass (<= 8 passes)
@@ -301,6 +306,9 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
         if (rc) return rc;
         rc = find_rows_dispatch(ctx, v, packed, mp, st);
         if (rc) return rc;
+        if (ctx->pcompat)   // ParallelMemHash::MergeTable (ParallelMemHash.cpp:105-121)
+            HIPCHK(launch_compat_merge(ctx->tsize.as<uint32_t>(), ctx->bstart.as<uint32_t>(), ctx->tbl.as<uint32_t>(),
+                                       ctx->pool.as<int64_t>(), G, Tb, &dc->collisions, st));
     }
     HIPCHK(hipEventRecord(ctx->ev[EV_REPLAY], st));
     HIPCHK(hipMemcpyAsync(ctx->obase.p, ctx->tsize.p, (size_t)Tb * 4, hipMemcpyDeviceToDevice, st));
@@ -474,8 +482,9 @@ void fill_stats(mums_ctx* ctx, uint64_t n) {
         }
         s.dominant_launches = (uint64_t)passes;
     }
+    s.chunks = ctx->nchunks;
     if (ctx->stage_done >= MUMS_STAGE_ALL) {
-        s.mem_count = ctx->hc.entries;
+        s.mem_count = ctx->pcompat ? ctx->M : ctx->hc.entries;   // compat: entries of the merged table
         s.collision_count = ctx->hc.collisions;
         s.ms_chains = el(EV_BUCKETS, EV_CHAINS);
         s.ms_replay = el(EV_CHAINS, EV_REPLAY);
@@ -640,6 +649,136 @@ int prepare_run(mums_ctx* ctx, const std::vector<uint64_t>& lens) {
     return MUMS_OK;
 }
 
+// ParallelMemHash::FindMatches (ParallelMemHash.cpp:42-103) compat pipeline (compat.hip):
+// pair path; one sort of (genome, ckey) gives the G SortedMerLists, the chunk starts
+// follow GetBreakpoint, and a second sort of (chunk, ckey) yields the chunk-major probe
+// order; groups / probes / chains / replay are the serial kernels, then MergeTable.
+int run_pipeline_compat(mums_ctx* ctx, int stage) {
+    hipStream_t st = ctx->stream;
+    const int G = (int)ctx->genomes.size();
+    const uint64_t N = ctx->N;
+    MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, ctx->masked, ctx->seq_mask};
+    GenomeTable& gt = ctx->gt;
+    const int kbits = 2 * ctx->w + 1;
+    int gbits = 0;
+    while ((1 << gbits) < G) ++gbits;
+    if (kbits + gbits > 63) return fail(ctx, MUMS_E_UNSUPPORTED, "ParallelMemHash compat: seed weight too large");
+    ctx->packed_path = false;
+    ctx->key64 = true;
+    ctx->msd_bits = 0;
+    const uint64_t kmask = (1ull << kbits) - 1;
+
+    uint64_t words = 0;
+    const uint32_t T = layout_packed(gt, &words);
+    HIPCHK(ctx->packed.ensure(words * 4 + 64));
+    HIPCHK(ctx->counters.ensure(sizeof(DevCounters)));
+    DevCounters* dc = ctx->counters.as<DevCounters>();
+    const uint64_t ntiles_groups = (N + kSegTile - 1) / kSegTile;
+    HIPCHK(ctx->ckey.ensure(N * 8 + 64));
+    HIPCHK(ctx->kA.ensure(N * 8 + 64));
+    HIPCHK(ctx->kB.ensure(N * 8 + 64));
+    HIPCHK(ctx->vA.ensure(N * 4 + 64));
+    HIPCHK(ctx->vB.ensure(N * 4 + 64));
+    HIPCHK(ctx->cval.ensure(N * 4 + 64));
+    HIPCHK(ctx->tiles.ensure(ntiles_groups * sizeof(SegTile) + 64));
+    size_t tmpb = std::max(scan_tmp_bytes(N), radix_tmp_bytes(N));
+    tmpb = std::max(tmpb, scan_tmp_bytes((uint64_t)ctx->table_size));
+    HIPCHK(ctx->tmp.ensure(tmpb));
+    ProbeSpace ps{};
+    int rc = ensure_probe_space(ctx, N, ntiles_groups, &ps);
+    if (rc) return rc;
+
+    int mx = -1;   // the longest SML by Length() = sequence length (ParallelMemHash.cpp:64-73)
+    uint64_t maxlen = 0;
+    for (int g = 0; g < G; ++g)
+        if (gt.n[g] > maxlen) { maxlen = gt.n[g]; mx = g; }
+    const uint64_t chunk = ctx->chunk_size;
+    const uint32_t cap = (uint32_t)std::min<uint64_t>(2 * (maxlen / chunk) + 4, 1u << 24);
+    HIPCHK(ctx->ctab.ensure((size_t)cap * (G + 1) * 8 + 64));
+    uint64_t* cs = ctx->ctab.as<uint64_t>();
+    uint64_t* bm = cs + (size_t)cap * G;
+    uint32_t* d_nch = (uint32_t*)(bm + cap);
+
+    HIPCHK(hipEventRecord(ctx->ev[EV_START], st));
+    HIPCHK(hipMemsetAsync(dc, 0, sizeof(DevCounters), st));
+    HIPCHK(hipMemsetAsync(cs, 0, (size_t)cap * G * 8, st));
+    std::vector<const char*> ptrs(G);
+    for (int g = 0; g < G; ++g) ptrs[g] = ctx->genomes[g].d_ptr;
+    HIPCHK(launch_seed_pack(ctx->ss, gt, ptrs.data(), ctx->packed.as<uint32_t>(), 0, true, ctx->ckey.p, 0, nullptr, T,
+                            &dc->err, st));
+    HIPCHK(launch_genome_keys(ctx->ckey.as<uint64_t>(), N, gt, kbits, st));
+    HIPCHK(hipEventRecord(ctx->ev[EV_KEYS], st));
+    int buf = 0;
+    HIPCHK(radix_sort<uint64_t>(ctx->ckey.as<uint64_t>(), nullptr, N, kbits + gbits, ctx->kA.as<uint64_t>(),
+                                ctx->vA.as<uint32_t>(), ctx->kB.as<uint64_t>(), ctx->vB.as<uint32_t>(), ctx->tmp.p,
+                                &buf, st));
+    const uint64_t* sk = buf ? ctx->kB.as<uint64_t>() : ctx->kA.as<uint64_t>();
+    const uint32_t* sv = buf ? ctx->vB.as<uint32_t>() : ctx->vA.as<uint32_t>();
+    uint32_t nch = 1;
+    if (mx >= 0) {
+        HIPCHK(launch_compat_breaks(sk, gt, kmask, mx, chunk, cs, bm, cap, d_nch, &dc->err, st));
+        uint32_t h[2] = {0, 0};
+        HIPCHK(hipMemcpyAsync(&h[0], d_nch, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(&h[1], &dc->err, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        if (h[1] & 1u) return fail(ctx, MUMS_E_GAP, "Gap in genome sequence ('-' encountered)");
+        if (h[1] & 4u)
+            return fail(ctx, MUMS_E_UNSUPPORTED, "ParallelMemHash compat: a masked-key group spans a whole chunk "
+                                                 "(the reference's chunking loop does not terminate)");
+        if (h[1] & 8u)
+            return fail(ctx, MUMS_E_UNSUPPORTED, "ParallelMemHash compat: chunk breakpoint past the SML end "
+                                                 "(out-of-range SortedMerList::operator[] in the reference)");
+        nch = h[0];
+        HIPCHK(launch_compat_find(sk, gt, kmask, mx, ctx->L, cs, bm, nch, st));
+        std::vector<uint64_t> hcs((size_t)nch * G);
+        HIPCHK(hipMemcpyAsync(hcs.data(), cs, hcs.size() * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        for (uint32_t k = 1; k < nch; ++k)
+            for (int g = 0; g < G; ++g)
+                if (hcs[(size_t)k * G + g] < hcs[(size_t)(k - 1) * G + g])
+                    return fail(ctx, MUMS_E_UNSUPPORTED, "ParallelMemHash compat: decreasing chunk starts "
+                                                         "(overlapping chunk ranges) not reproduced");
+    }
+    ctx->nchunks = nch;
+    int cbits = 0;
+    while (((uint64_t)1 << cbits) < (uint64_t)nch) ++cbits;
+    if (kbits + cbits > 64) return fail(ctx, MUMS_E_UNSUPPORTED, "ParallelMemHash compat: too many chunks");
+    HIPCHK(launch_compat_chunk_keys(sk, sv, N, gt, kbits, cs, nch, ctx->ckey.as<uint64_t>(), ctx->cval.as<uint32_t>(),
+                                    st));
+    HIPCHK(radix_sort<uint64_t>(ctx->ckey.as<uint64_t>(), ctx->cval.as<uint32_t>(), N, kbits + cbits,
+                                ctx->kA.as<uint64_t>(), ctx->vA.as<uint32_t>(), ctx->kB.as<uint64_t>(),
+                                ctx->vB.as<uint32_t>(), ctx->tmp.p, &buf, st));
+    ctx->sorted_buf = buf;
+    ctx->sorted_key = buf ? ctx->kB.p : ctx->kA.p;
+    ctx->sorted_idx = buf ? ctx->vB.as<uint32_t>() : ctx->vA.as<uint32_t>();
+    ctx->sort_passes = (kbits + cbits + 7) / 8;
+    HIPCHK(hipEventRecord(ctx->ev[EV_SORT], st));
+    SegTile* tiles = ctx->tiles.as<SegTile>();
+    HIPCHK(launch_flat_tiles(N, tiles, st));
+    rc = groups_dispatch<PairView<uint64_t>>(
+        ctx, PairView<uint64_t>{(const uint64_t*)ctx->sorted_key, ctx->sorted_idx}, tiles, ntiles_groups, mp,
+        ps.probe_info, ps.probe_bucket, ps.slot_info, ps.slot_bucket, st);
+    if (rc) return rc;
+    rc = finish_seeds(ctx, ps, st);
+    if (rc) return rc;
+    if (ctx->hc.repeat_limit)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "ParallelMemHash compat: a seed group above MER_REPEAT_LIMIT ends its "
+                                             "chunk in the reference (SearchRange's ignored return) - not reproduced");
+    ctx->stage_done = MUMS_STAGE_SEEDS;
+    if (stage >= MUMS_STAGE_ALL) {
+        rc = find_tail(ctx, mp, ctx->packed.as<uint32_t>(), [&](MatProbes* v) {
+            const int r = materialize_seeds(ctx, mp, st);
+            v->rows = ctx->mprobe.as<int64_t>();
+            return r;
+        }, st);
+        if (rc) return rc;
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipMemcpy(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost));
+    fill_stats(ctx, N);
+    return MUMS_OK;
+}
+
 int check_ctx(mums_ctx* ctx) {
     if (!ctx) return MUMS_E_INVALID;
     ctx->err.clear();
@@ -715,7 +854,9 @@ int mums_ctx_destroy(mums_ctx* ctx) {
     DevBuf* bufs[] = {&ctx->packed, &ctx->recA, &ctx->recB, &ctx->hist, &ctx->tiles, &ctx->ckey, &ctx->kA,
                       &ctx->kB, &ctx->vA, &ctx->vB, &ctx->tmp, &ctx->partials, &ctx->counters, &ctx->bstart,
                       &ctx->bend, &ctx->tsize, &ctx->obase, &ctx->pool, &ctx->tbl, &ctx->out_len, &ctx->out_s,
-                      &ctx->pbuf, &ctx->keybuf, &ctx->mstart};
+                      &ctx->pbuf, &ctx->keybuf, &ctx->mstart, &ctx->chain_tmp, &ctx->chain_of,
+                      &ctx->radix_tmp, &ctx->spill, &ctx->summ, &ctx->dbgbuf, &ctx->mprobe, &ctx->rowtmp,
+                      &ctx->cval, &ctx->ctab};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i < EV_COUNT; ++i)
         if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
@@ -808,7 +949,15 @@ int mums_find_stage(mums_ctx* ctx, int stage) {
         ctx->st = mums_stats{};
         return MUMS_OK;
     }
-    return run_pipeline(ctx, stage);
+    return ctx->pcompat ? run_pipeline_compat(ctx, stage) : run_pipeline(ctx, stage);
+}
+
+int mums_set_parallel_compat(mums_ctx* ctx, int enable, uint64_t chunk_size) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (enable && chunk_size == 0) chunk_size = 200000;   // CHUNK_SIZE, ParallelMemHash.cpp:51
+    ctx->pcompat = enable != 0;
+    ctx->chunk_size = chunk_size ? chunk_size : 200000;
+    return MUMS_OK;
 }
 
 int mums_find(mums_ctx* ctx) { return mums_find_stage(ctx, MUMS_STAGE_ALL); }

@@ -216,4 +216,17 @@ hipError_t launch_emit(const uint32_t* tsize, const uint32_t* obase, const uint3
                        const int64_t* pool, int G, uint32_t table_size, uint64_t* out_len, int64_t* out_s,
                        hipStream_t st);
 
+// compat.hip: ParallelMemHash chunk-compat mode (ParallelMemHash.cpp:42-121)
+hipError_t launch_genome_keys(uint64_t* ckey, uint64_t N, const GenomeTable& gt, int kbits, hipStream_t st);
+hipError_t launch_compat_breaks(const uint64_t* sk, const GenomeTable& gt, uint64_t kmask, int mx, uint64_t chunk,
+                                uint64_t* cs, uint64_t* bm, uint32_t cap, uint32_t* d_nch, uint32_t* err,
+                                hipStream_t st);
+hipError_t launch_compat_find(const uint64_t* sk, const GenomeTable& gt, uint64_t kmask, int mx, int L, uint64_t* cs,
+                              const uint64_t* bm, uint32_t nch, hipStream_t st);
+hipError_t launch_compat_chunk_keys(const uint64_t* sk, const uint32_t* sv, uint64_t N, const GenomeTable& gt,
+                                    int kbits, const uint64_t* cs, uint32_t nch, uint64_t* key2, uint32_t* val2,
+                                    hipStream_t st);
+hipError_t launch_compat_merge(uint32_t* tsize, const uint32_t* bstart, uint32_t* tbl, const int64_t* pool, int G,
+                               uint32_t Tb, unsigned long long* collisions, hipStream_t st);
+
 }  // namespace mums

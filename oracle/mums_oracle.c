@@ -398,12 +398,14 @@ static void extend_match(const ext_ctx* x, mhe_t* m) {
 /* ------------------------------------------------------------------------- */
 typedef struct { uint32_t* v; uint32_t n, cap; } bucket_t;
 
+#define MER_REPEAT_LIMIT 1000   /* MatchFinder.cpp:166 */
+
 struct oracle_result {
     int G;
     uint64_t count;
     uint64_t* lengths;
     int64_t* starts;
-    uint64_t mem_count, collision_count, max_group, probes, seedmers;
+    uint64_t mem_count, collision_count, max_group, probes, seedmers, chunks;
     uint32_t* plog_bucket;    /* seeds_only: per AddHashEntry call, its bucket ... */
     uint64_t* plog_ref;       /* ... and the global seed-mer index of the probe's first start */
 };
@@ -419,6 +421,7 @@ typedef struct {
     uint64_t mem_count, collisions, probes;
     const uint64_t* gbase;    /* global seed-mer index of each genome's position 0 */
     uint32_t* plog_bucket; uint64_t* plog_ref; uint64_t plog_cap;
+    int64_t* scratch;         /* G starts of the probe under construction */
 } memhash_t;
 
 static uint32_t pool_add(memhash_t* h, const mhe_t* src) {
@@ -572,11 +575,191 @@ static void enumerate_matches(memhash_t* h, const oracle_params* prm, const idme
     }
 }
 
+/* MatchFinder::SearchRange (MatchFinder.cpp:172-340): G-way merge of the SMLs  */
+/* restricted to index ranges [lo[g], hi[g]) by masked key; a group = every      */
+/* occurrence of one masked key inside the ranges.  compat != 0 adds the         */
+/* MER_REPEAT_LIMIT early return (:215-239) as ParallelMemHash sees it: the      */
+/* return value is ignored (ParallelMemHash.cpp:99), so a group above 1000        */
+/* records ends the chunk unless nothing follows it (the check runs at the top   */
+/* of the next merge iteration, the final group is hashed at :335-336).          */
+static void search_range(memhash_t* h, const oracle_params* prm, int G, bmer_t* const* sml, const uint64_t* lo,
+                         const uint64_t* hi, int compat, oracle_result* res) {
+    uint64_t* idx = (uint64_t*)calloc((size_t)G, sizeof(uint64_t));
+    for (int g = 0; g < G; ++g) idx[g] = lo[g] < hi[g] ? lo[g] : hi[g];
+    uint64_t gcap = 1024;
+    idmer_t* grp = (idmer_t*)malloc(gcap * sizeof(idmer_t));
+    idmer_t* hl = (idmer_t*)malloc(gcap * sizeof(idmer_t));
+    const uint64_t mask = h->x.seed_mask;
+    for (;;) {
+        int have = 0; uint64_t mn = 0;
+        for (int g = 0; g < G; ++g) {
+            if (idx[g] < hi[g]) {
+                uint64_t k = sml[g][idx[g]].key & mask;
+                if (!have || k < mn) { mn = k; have = 1; }
+            }
+        }
+        if (!have) break;
+        uint64_t cnt = 0;
+        for (int g = 0; g < G; ++g) {
+            while (idx[g] < hi[g] && (sml[g][idx[g]].key & mask) == mn) {
+                if (cnt == gcap) {
+                    gcap *= 2;
+                    grp = (idmer_t*)realloc(grp, gcap * sizeof(idmer_t));
+                    hl = (idmer_t*)realloc(hl, gcap * sizeof(idmer_t));
+                }
+                grp[cnt].g = (uint32_t)g;
+                grp[cnt].pos = sml[g][idx[g]].pos;
+                grp[cnt].key = sml[g][idx[g]].key;
+                ++cnt; ++idx[g];
+            }
+        }
+        if (cnt > res->max_group) res->max_group = cnt;
+        if (compat && cnt > MER_REPEAT_LIMIT) {
+            int more = 0;
+            for (int g = 0; g < G; ++g) more |= idx[g] < hi[g];
+            if (more) break;
+        }
+        if (cnt > 1) enumerate_matches(h, prm, grp, (int)cnt, hl, h->scratch);
+    }
+    free(idx); free(grp); free(hl);
+}
+
+/* SortedMerList::bsearch (SortedMerList.cpp:380-394), recursion unrolled; unsigned */
+static uint64_t sml_bsearch(const bmer_t* v, uint64_t q, uint64_t start, uint64_t end) {
+    for (;;) {
+        uint64_t middle = (start + end) / 2;
+        uint64_t k = v[middle].key;
+        if (k == q) return middle;
+        if (k < q && middle < end) start = middle + 1;
+        else if (k > q && start < middle) end = middle - 1;
+        else return middle;
+    }
+}
+
+/* SortedMerList::FindMer (SortedMerList.cpp:170-179); Length() = sequence length. */
+/* On the early-return path the reference leaves `result` untouched (the caller's */
+/* uninitialised cur_start); here it is 0.                                          */
+static int sml_find_mer(const bmer_t* v, uint64_t n, int L, uint64_t q, uint64_t* result) {
+    if (n == 0 || n < (uint64_t)L) { *result = 0; return 0; }
+    uint64_t last_pos = n - (uint64_t)L;
+    *result = sml_bsearch(v, q, 0, last_pos);
+    return v[*result].key == q;
+}
+
+/* MatchFinder::GetBreakpoint (MatchFinder.cpp:89-126).  The backward loop for the */
+/* other SMLs compares against (break_mer.mer && mer_mask) (a bool) and re-reads   */
+/* cur_start: it never runs unless break_mer.mer == 0, where it runs down to -1.   */
+/* Returns -1 when startI is past the SML (operator[] out of range in the ref).    */
+static int get_breakpoint(int sarI, uint64_t startI, int G, bmer_t* const* sml, const uint64_t* m,
+                          const uint64_t* lens, int L, uint64_t mask, uint64_t* bp) {
+    if (startI >= m[sarI]) return -1;
+    const uint64_t bm = sml[sarI][startI].key;
+    uint64_t prev = bm;
+    while ((prev & mask) == (bm & mask)) {
+        if (startI == 0) { startI--; break; }
+        startI--;
+        prev = sml[sarI][startI].key;
+    }
+    ++startI;
+    for (int i = 0; i < G; ++i) {
+        if (i == sarI) { bp[i] = startI; continue; }
+        uint64_t cur = 0;
+        if (sml_find_mer(sml[i], lens[i], L, bm, &cur)) {
+            int64_t cur_matchI = (int64_t)cur;
+            const uint64_t lhs = sml[i][cur].key & mask, rhs = (bm && mask) ? 1u : 0u;
+            while (cur_matchI >= 0 && lhs == rhs) cur_matchI--;
+            cur = (uint64_t)(cur_matchI + 1);
+        }
+        bp[i] = cur;
+    }
+    return 0;
+}
+
+/* Re-add of an already extended entry into another table (the patched 2-argument */
+/* AddHashEntry of SURVEY.md Appendix B.3 as MergeTable calls it,                  */
+/* ParallelMemHash.cpp:105-121): lower_bound, collision if equivalent, else insert;*/
+/* Extended() is set, so no extension (MemHash.cpp:223-224).                        */
+static void merge_entry(memhash_t* h, bucket_t* b, uint32_t id) {
+    const mhe_t* e = &h->pool[id];
+    uint32_t it = lower_bound_mhe(h, b, e);
+    if (it != b->n) {
+        const mhe_t* x = &h->pool[b->v[it]];
+        if (!mhe_less(x, e, h->x.G) && !mhe_less(e, x, h->x.G)) { ++h->collisions; return; }
+    }
+    if (b->n == b->cap) {
+        b->cap = b->cap ? b->cap * 2 : 4;
+        b->v = (uint32_t*)realloc(b->v, b->cap * sizeof(uint32_t));
+    }
+    memmove(b->v + it + 1, b->v + it, (size_t)(b->n - it) * sizeof(uint32_t));
+    b->v[it] = id;
+    ++b->n;
+}
+
+/* ParallelMemHash::FindMatches (ParallelMemHash.cpp:42-103) with the thread     */
+/* schedule of one OpenMP thread (the reference's output is the same for 1/4/8   */
+/* threads): chunk starts from GetBreakpoint on the longest */
+/* SML every chunk_size (200000, :51) mers; per chunk, SearchRange into the      */
+/* thread table T (= the global table G after the previous merge) and MergeTable */
+/* (:105-121): every entry of T re-added into G in bucket/vector order, then     */
+/* T = G.  On return h->buckets holds G.  Returns -1 for inputs the reference    */
+/* handles through undefined behaviour (a breakpoint past the SML end).          */
+static int parallel_compat_search(memhash_t* h, const oracle_params* prm, int G, const uint64_t* lens,
+                                  bmer_t* const* sml, const uint64_t* m, oracle_result* res) {
+    const uint64_t chunk = prm->chunk_size ? prm->chunk_size : 200000;
+    int mx = -1;
+    uint64_t maxlen = 0;
+    for (int g = 0; g < G; ++g) if (lens[g] > maxlen) { maxlen = lens[g]; mx = g; }
+    if (mx < 0) return 0;
+    uint64_t ncap = 16, nch = 1;
+    uint64_t* cs = (uint64_t*)calloc(ncap * (size_t)G, sizeof(uint64_t));
+    while (cs[(nch - 1) * G + mx] + chunk < lens[mx]) {
+        if (nch == ncap) {
+            ncap *= 2;
+            cs = (uint64_t*)realloc(cs, ncap * (size_t)G * sizeof(uint64_t));
+        }
+        if (get_breakpoint(mx, cs[(nch - 1) * G + mx] + chunk, G, sml, m, lens, h->x.L, h->x.seed_mask,
+                           cs + nch * G)) { free(cs); return -1; }
+        ++nch;
+    }
+    const uint32_t T = h->table_size;
+    bucket_t* gb = (bucket_t*)calloc(T, sizeof(bucket_t));   /* global table G */
+    uint64_t* lo = (uint64_t*)malloc((size_t)G * sizeof(uint64_t));
+    uint64_t* hi = (uint64_t*)malloc((size_t)G * sizeof(uint64_t));
+    for (uint64_t i = 0; i < nch; ++i) {
+        for (int g = 0; g < G; ++g) {
+            lo[g] = cs[i * G + g];
+            /* chunk_lens = next start - start (gnSeqI, wraps) or GNSEQI_END */
+            uint64_t len = (i + 1 < nch) ? cs[(i + 1) * G + g] - cs[i * G + g] : UINT64_MAX;
+            hi[g] = (lo[g] >= m[g] || len > m[g] - lo[g]) ? m[g] : lo[g] + len;
+        }
+        search_range(h, prm, G, sml, lo, hi, 1, res);
+        if (prm->parallel_compat == 2 && i + 1 < nch) continue;   /* checking aid: one deferred merge */
+        for (uint32_t bI = 0; bI < T; ++bI)
+            for (uint32_t k = 0; k < h->buckets[bI].n; ++k) merge_entry(h, &gb[bI], h->buckets[bI].v[k]);
+        for (uint32_t bI = 0; bI < T; ++bI) {   /* thread table = global table */
+            bucket_t* tb = &h->buckets[bI];
+            if (tb->cap < gb[bI].n) {
+                tb->cap = gb[bI].n;
+                tb->v = (uint32_t*)realloc(tb->v, tb->cap * sizeof(uint32_t));
+            }
+            if (gb[bI].n) memcpy(tb->v, gb[bI].v, gb[bI].n * sizeof(uint32_t));
+            tb->n = gb[bI].n;
+        }
+    }
+    uint64_t entries = 0;
+    for (uint32_t bI = 0; bI < T; ++bI) { entries += gb[bI].n; free(gb[bI].v); }
+    h->mem_count = entries;   /* MemCount of the merged table */
+    free(gb); free(lo); free(hi); free(cs);
+    res->chunks = nch;
+    return 0;
+}
+
 oracle_result* oracle_find_matches(int G, const char* const* seqs, const uint64_t* lens,
                                    const oracle_params* prm) {
     if (G < 1 || G > 64) return NULL;
     oracle_result* res = (oracle_result*)calloc(1, sizeof(oracle_result));
     res->G = G;
+    int bad = 0;
     sml_ctx* ctx = (sml_ctx*)calloc((size_t)G, sizeof(sml_ctx));
     uint32_t** words = (uint32_t**)calloc((size_t)G, sizeof(uint32_t*));
     uint64_t** keys = (uint64_t**)calloc((size_t)G, sizeof(uint64_t*));
@@ -606,41 +789,16 @@ oracle_result* oracle_find_matches(int G, const char* const* seqs, const uint64_
         h.gbase = gbase;
         h.buckets = (bucket_t*)calloc(h.table_size, sizeof(bucket_t));
         int64_t* scratch = (int64_t*)malloc((size_t)G * sizeof(int64_t));
+        h.scratch = scratch;
 
-        /* MatchFinder::SearchRange (MatchFinder.cpp:172-340): G-way merge of   */
-        /* the SMLs by masked key; a group = every occurrence of one masked key.*/
-        uint64_t* idx = (uint64_t*)calloc((size_t)G, sizeof(uint64_t));
-        uint64_t gcap = 1024;
-        idmer_t* grp = (idmer_t*)malloc(gcap * sizeof(idmer_t));
-        idmer_t* hl = (idmer_t*)malloc(gcap * sizeof(idmer_t));
-        const uint64_t mask = h.x.seed_mask;
-        for (;;) {
-            int have = 0; uint64_t mn = 0;
-            for (int g = 0; g < G; ++g) {
-                if (idx[g] < m[g]) {
-                    uint64_t k = sml[g][idx[g]].key & mask;
-                    if (!have || k < mn) { mn = k; have = 1; }
-                }
-            }
-            if (!have) break;
-            uint64_t cnt = 0;
-            for (int g = 0; g < G; ++g) {
-                while (idx[g] < m[g] && (sml[g][idx[g]].key & mask) == mn) {
-                    if (cnt == gcap) {
-                        gcap *= 2;
-                        grp = (idmer_t*)realloc(grp, gcap * sizeof(idmer_t));
-                        hl = (idmer_t*)realloc(hl, gcap * sizeof(idmer_t));
-                    }
-                    grp[cnt].g = (uint32_t)g;
-                    grp[cnt].pos = sml[g][idx[g]].pos;
-                    grp[cnt].key = sml[g][idx[g]].key;
-                    ++cnt; ++idx[g];
-                }
-            }
-            if (cnt > res->max_group) res->max_group = cnt;
-            if (cnt > 1) enumerate_matches(&h, prm, grp, (int)cnt, hl, scratch);
+        if (prm->parallel_compat) {
+            bad = parallel_compat_search(&h, prm, G, lens, sml, m, res);
+        } else {
+            uint64_t* lo = (uint64_t*)calloc((size_t)G, sizeof(uint64_t));
+            search_range(&h, prm, G, sml, lo, m, 0, res);
+            free(lo);
         }
-        free(idx); free(grp); free(hl); free(scratch);
+        free(scratch);
 
         /* MemHash::GetMatchList: MemHash.h:182-203 (bucket-major) */
         res->count = h.mem_count;
@@ -666,6 +824,7 @@ oracle_result* oracle_find_matches(int G, const char* const* seqs, const uint64_
 done:
     for (int g = 0; g < G; ++g) { free(words[g]); free(keys[g]); free(sml[g]); }
     free(ctx); free(words); free(keys); free(sml); free(m);
+    if (bad) { oracle_result_free(res); return NULL; }
     return res;
 }
 
@@ -752,6 +911,7 @@ int oracle_result_probe_log(const oracle_result* r, uint32_t* buckets, uint64_t*
     return 0;
 }
 uint64_t oracle_result_seedmers(const oracle_result* r) { return r ? r->seedmers : 0; }
+uint64_t oracle_result_chunks(const oracle_result* r) { return r ? r->chunks : 0; }
 void     oracle_result_free(oracle_result* r) {
     if (!r) return;
     free(r->lengths); free(r->starts); free(r->plog_bucket); free(r->plog_ref); free(r);

@@ -51,6 +51,11 @@ typedef struct oracle_params {
     int      seeds_only;       /* 1: stop after probe construction (keys, SML  *
                                 *    sort, merge, accept, probe + bucket): the  *
                                 *    "sorted+matched" scope of the bench metric */
+    int      parallel_compat;  /* 1: ParallelMemHash::FindMatches chunking +    *
+                                *    MergeTable (ParallelMemHash.cpp:42-121);    *
+                                *    2: same chunks, one MergeTable at the end   *
+                                *    (checking aid for the GPU's model)          */
+    uint64_t chunk_size;       /* its CHUNK_SIZE (0 = 200000, :51)              */
 } oracle_params;
 
 typedef struct oracle_result oracle_result;
@@ -67,6 +72,7 @@ uint64_t oracle_result_max_group(const oracle_result* r);
 uint64_t oracle_result_probe_count(const oracle_result* r);
 int      oracle_result_probe_log(const oracle_result* r, uint32_t* buckets, uint64_t* ref);
 uint64_t oracle_result_seedmers(const oracle_result* r);
+uint64_t oracle_result_chunks(const oracle_result* r);     /* compat: chunks searched */
 void     oracle_result_free(oracle_result* r);
 /* AddHashEntry replay of probe rows {starts[G], offset} (sharded FindMatches checks). */
 oracle_result* oracle_replay_rows(int G, const char* const* seqs, const uint64_t* lens, const oracle_params* prm,

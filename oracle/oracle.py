@@ -31,6 +31,8 @@ class _Params(ctypes.Structure):
         ("seq_mask", ctypes.c_uint64),
         ("gnseqi_end_neg1", ctypes.c_int),
         ("seeds_only", ctypes.c_int),
+        ("parallel_compat", ctypes.c_int),
+        ("chunk_size", ctypes.c_uint64),
     ]
 
 
@@ -58,7 +60,7 @@ def lib() -> ctypes.CDLL:
         L.oracle_find_matches.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(u64),
                                           ctypes.POINTER(_Params)]
         L.oracle_find_matches.restype = vp
-        for f in ("count", "mem_count", "collision_count", "max_group", "probe_count", "seedmers"):
+        for f in ("count", "mem_count", "collision_count", "max_group", "probe_count", "seedmers", "chunks"):
             fn = getattr(L, f"oracle_result_{f}")
             fn.argtypes = [vp]
             fn.restype = u64
@@ -110,13 +112,16 @@ def build_sml(seq: bytes, seed: int) -> np.ndarray:
 
 def find_matches(seqs: Sequence[bytes], seed: int, repeat_tol: int = 0, enum_tol: int = 1,
                  table_size: int = 40000, masked: bool = False, seq_mask: int = 0,
-                 gnseqi_end_neg1: bool = False, seeds_only: bool = False) -> Tuple[np.ndarray, np.ndarray, dict]:
-    """MemHash::FindMatches restated; returns (lengths[M], starts[M,G], counters)."""
+                 gnseqi_end_neg1: bool = False, seeds_only: bool = False, parallel_compat: bool = False,
+                 chunk_size: int = 0) -> Tuple[np.ndarray, np.ndarray, dict]:
+    """MemHash::FindMatches restated; returns (lengths[M], starts[M,G], counters).
+    parallel_compat: ParallelMemHash::FindMatches instead (ParallelMemHash.cpp:42-121),
+    chunk_size = its CHUNK_SIZE (0 = 200000)."""
     G = len(seqs)
     arr = (ctypes.c_char_p * G)(*seqs)
     lens = (ctypes.c_uint64 * G)(*[len(s) for s in seqs])
     prm = _Params(seed, repeat_tol, enum_tol, table_size, int(masked), seq_mask, int(gnseqi_end_neg1),
-                  int(seeds_only))
+                  int(seeds_only), int(parallel_compat), chunk_size)
     L = lib()
     r = L.oracle_find_matches(G, arr, lens, ctypes.byref(prm))
     if not r:
@@ -129,7 +134,7 @@ def find_matches(seqs: Sequence[bytes], seed: int, repeat_tol: int = 0, enum_tol
             L.oracle_result_copy(r, lengths.ctypes.data, starts.ctypes.data)
         stats = dict(mem_count=L.oracle_result_mem_count(r), collision_count=L.oracle_result_collision_count(r),
                      max_group=L.oracle_result_max_group(r), probes=L.oracle_result_probe_count(r),
-                     seedmers=L.oracle_result_seedmers(r))
+                     seedmers=L.oracle_result_seedmers(r), chunks=L.oracle_result_chunks(r))
     finally:
         L.oracle_result_free(r)
     return lengths, starts, stats
@@ -162,14 +167,15 @@ def replay_rows(seqs: Sequence[bytes], seed: int, rows: np.ndarray, table_size: 
     return lengths, starts, stats
 
 
-def seed_probes(seqs: Sequence[bytes], seed: int, table_size: int = 40000) -> Tuple[np.ndarray, np.ndarray, dict]:
+def seed_probes(seqs: Sequence[bytes], seed: int, table_size: int = 40000, parallel_compat: bool = False,
+                chunk_size: int = 0) -> Tuple[np.ndarray, np.ndarray, dict]:
     """Seed stage only (keys, SMLs, G-way merge, acceptance, probes): the AddHashEntry calls
     in order as (bucket[P], ref[P]) with ref = global seed-mer index of the probe's first
     start (genome bases = cumulative SMLLength), plus the counters."""
     G = len(seqs)
     arr = (ctypes.c_char_p * G)(*seqs)
     lens = (ctypes.c_uint64 * G)(*[len(s) for s in seqs])
-    prm = _Params(seed, 0, 1, table_size, 0, 0, 0, 1)
+    prm = _Params(seed, 0, 1, table_size, 0, 0, 0, 1, int(parallel_compat), chunk_size)
     L = lib()
     r = L.oracle_find_matches(G, arr, lens, ctypes.byref(prm))
     if not r:

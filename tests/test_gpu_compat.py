@@ -1,0 +1,76 @@
+"""GPU ParallelMemHash chunk-compat mode (compat.hip)
+against the reference's known answer and the pinned oracle restatement, bit for bit."""
+import hashlib
+import json
+import os
+
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+PCOMPAT = json.load(open(os.path.join(GOLDEN, "appendix_c.json")))["parallel_compat"]
+
+
+def gpu_parallel(lm, seqs, seed, chunk, masked=False, mask=0):
+    with lm.ParallelMemHash(0, chunk) as mh:
+        mh.SetSeed(seed)
+        if masked:
+            mh._check(mh._lib.mums_set_mask(mh._ctx, 1, mask))
+        ml = mh.FindMatches(seqs)
+        return ml, mh.stats()
+
+
+@pytest.mark.parametrize("case", PCOMPAT, ids=lambda c: f"G{c['G']}_n{c['n']}_p{c['p']}")
+def test_parallel_known_answer(gpu_lib, oracle_mod, case):
+    """4 x 10 Mbp related: the patched OpenMP reference's 15 893 matches, md5 of the text."""
+    seqs = oracle_mod.generate(case["G"], case["n"], case["p"], 12345)
+    ml, st = gpu_parallel(gpu_lib, seqs, oracle_mod.get_seed(case["w"]), case["chunk_size"])
+    txt = ml.text()
+    assert st["chunks"] == case["chunks"]
+    assert len(ml) == case["matches"]
+    assert hashlib.md5(txt.encode()).hexdigest() == case["md5"]
+    assert st["mem_count"] == case["matches"]
+
+
+COMPAT_SMALL = [(2, 200000, 0.01, 15, 5000, 1), (3, 300000, 0.03, 15, 3000, 2), (4, 200000, 0.01, 15, 2000, 3),
+                (3, 500000, 0.05, 15, 7000, 4), (3, 200000, 1.0, 11, 1003, 6), (3, 200000, 0.01, 12, 999, 8),
+                (2, 1000000, 0.01, 15, 200000, 12345), (5, 300000, 0.02, 17, 4000, 9)]
+
+
+@pytest.mark.parametrize("G,n,p,w,chunk,gseed", COMPAT_SMALL)
+def test_parallel_vs_oracle(gpu_lib, oracle_mod, G, n, p, w, chunk, gseed):
+    seqs = oracle_mod.generate(G, n, p, gseed)
+    seed = oracle_mod.get_seed(w)
+    lengths, starts, ost = oracle_mod.find_matches(seqs, seed, parallel_compat=True, chunk_size=chunk)
+    ml, st = gpu_parallel(gpu_lib, seqs, seed, chunk)
+    assert st["chunks"] == ost["chunks"]
+    assert len(ml) == len(lengths)
+    assert (ml.lengths == lengths).all() and (ml.starts == starts).all()
+
+
+def test_parallel_masked_and_ragged(gpu_lib, oracle_mod):
+    """MaskedMemHash semantics inside the chunked search, genomes of different lengths
+    (the longest SML defines the chunks, ParallelMemHash.cpp:64-73)."""
+    seqs = oracle_mod.generate(3, 400000, 0.02, 77)
+    seqs = [seqs[0], seqs[1][:250000], seqs[2][50000:]]
+    seed = oracle_mod.get_seed(15)
+    for masked, mask in ((False, 0), (True, 7), (True, 6)):
+        lengths, starts, _ = oracle_mod.find_matches(seqs, seed, masked=masked, seq_mask=mask, parallel_compat=True,
+                                                     chunk_size=3000)
+        ml, _ = gpu_parallel(gpu_lib, seqs, seed, 3000, masked=masked, mask=mask)
+        assert (ml.lengths == lengths).all() and (ml.starts == starts).all()
+
+
+def test_parallel_single_chunk_equals_serial(gpu_lib, oracle_mod):
+    """One chunk (every SML shorter than CHUNK_SIZE): ParallelMemHash = MemHash minus the
+    duplicates MergeTable collapses."""
+    seqs = oracle_mod.generate(3, 150000, 0.03, 5)
+    seed = oracle_mod.get_seed(15)
+    ml, st = gpu_parallel(gpu_lib, seqs, seed, 200000)
+    lengths, starts, _ = oracle_mod.find_matches(seqs, seed)
+    assert st["chunks"] == 1
+    serial = oracle_mod.match_text(lengths, starts).splitlines()
+    dedup = [l for i, l in enumerate(serial) if i == 0 or serial[i - 1] != l]
+    assert ml.text().splitlines() == dedup

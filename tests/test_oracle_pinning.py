@@ -54,3 +54,40 @@ def test_extension_insensitive_to_gnseqi_end(oracle_mod, G, n, p):
     a = oracle_mod.find_matches(seqs, oracle_mod.get_seed(15), gnseqi_end_neg1=False)
     b = oracle_mod.find_matches(seqs, oracle_mod.get_seed(15), gnseqi_end_neg1=True)
     assert (a[0] == b[0]).all() and (a[1] == b[1]).all()
+
+
+PCOMPAT = json.load(open(os.path.join(GOLDEN, "appendix_c.json")))["parallel_compat"]
+
+
+@pytest.mark.parametrize("case", PCOMPAT, ids=lambda c: f"G{c['G']}_n{c['n']}_p{c['p']}_ParallelMemHash")
+def test_oracle_parallel_compat_matches_reference_md5(oracle_mod, case):
+    """ParallelMemHash (patched) known answer: the oracle's restatement of
+    ParallelMemHash::FindMatches (chunking by GetBreakpoint, per-chunk SearchRange, MergeTable)
+    reproduces the reference's 15 893-match MatchList byte for byte."""
+    seqs = oracle_mod.generate(case["G"], case["n"], case["p"], 12345)
+    lengths, starts, st = oracle_mod.find_matches(seqs, oracle_mod.get_seed(case["w"]), parallel_compat=True,
+                                                  chunk_size=case["chunk_size"])
+    txt = oracle_mod.match_text(lengths, starts)
+    assert st["chunks"] == case["chunks"]
+    assert len(lengths) == case["matches"]
+    assert hashlib.md5(txt.encode()).hexdigest() == case["md5"]
+    assert txt.count("\n") == len(set(txt.splitlines()))   # MergeTable collapsed the serial duplicate
+
+
+# (G, n, p, w, chunk_size, generator seed): many chunks on small inputs
+COMPAT_SMALL = [(2, 200000, 0.01, 15, 5000, 1), (3, 300000, 0.03, 15, 3000, 2), (4, 200000, 0.01, 15, 2000, 3),
+                (3, 500000, 0.05, 15, 7000, 4), (3, 200000, 1.0, 11, 1003, 6), (3, 200000, 0.01, 12, 999, 8)]
+
+
+@pytest.mark.parametrize("G,n,p,w,chunk,gseed", COMPAT_SMALL)
+def test_parallel_compat_deferred_merge_equivalent(oracle_mod, G, n, p, w, chunk, gseed):
+    """The GPU reproduces MergeTable once, after all chunks (compat.hip); the literal
+    restatement merges after every chunk.  Both give the same MatchList (which differs from
+    serial MemHash's at the chunk boundaries)."""
+    seqs = oracle_mod.generate(G, n, p, gseed)
+    seed = oracle_mod.get_seed(w)
+    a = oracle_mod.find_matches(seqs, seed, parallel_compat=1, chunk_size=chunk)
+    b = oracle_mod.find_matches(seqs, seed, parallel_compat=2, chunk_size=chunk)
+    ta, tb = (oracle_mod.match_text(x[0], x[1]) for x in (a, b))
+    assert ta == tb
+    assert a[2]["chunks"] > 10
