@@ -64,7 +64,7 @@ def cpu_baseline(seconds_hint: float = 20.0):
     """Oracle (CPU restatement, 1 thread) on a bounded sample of the same workload shape."""
     from oracle import oracle
 
-    G, n, p = 8, 4_000_000, 0.01
+    G, n, p = 8, 16_000_000, 0.01   # about 20 s of one core
     seqs = oracle.generate(G, n, p, 12345)
     seed = lm.getSeed(19)
     t0 = time.perf_counter()
@@ -81,10 +81,11 @@ def cpu_baseline(seconds_hint: float = 20.0):
 
 
 def cpu_baseline_mums():
-    """Oracle full FindMatches (1 thread) on a bounded sample of the config-2 shape."""
+    """Oracle full FindMatches (1 thread) on the config-2 shape itself (4 x 10 Mbp related,
+    w15; about 15-20 s of one core)."""
     from oracle import oracle
 
-    G, n, p = 4, 2_000_000, 0.01
+    G, n, p = 4, 10_000_000, 0.01
     seqs = oracle.generate(G, n, p, 12345)
     t0 = time.perf_counter()
     lengths, _, _ = oracle.find_matches(seqs, lm.getSeed(15))

@@ -135,6 +135,14 @@ int  mums_copy_seed_keys(mums_ctx* ctx, uint32_t genome, uint64_t* out, uint64_t
 /* MemorySML::Create (MemorySML.cpp:45-60): SML positions of genome g sorted by
  * full key, ties by ascending position. */
 int  mums_build_sml(mums_ctx* ctx, uint32_t genome, uint32_t* positions, uint64_t cap);
+/* SeedOccurrenceList::construct (SeedOccurrenceList.h:22-61) + smoothFrequencies
+ * (:71-87) over genome's SortedMerList: freq[p] (float32, n entries) = mean masked-key
+ * frequency of the seeds covering position p (getFrequency, :64-67). */
+int  mums_seed_occurrence(mums_ctx* ctx, uint32_t genome, float* freq, uint64_t cap);
+/* GenericMatchList::MultiplicityFilter / LengthFilter (MatchList.h:636-664) applied to
+ * the context's last MatchList in place (order kept). */
+int  mums_multiplicity_filter(mums_ctx* ctx, uint32_t multiplicity);
+int  mums_length_filter(mums_ctx* ctx, uint64_t min_length);
 
 /* ---- sharded seed stage across GPUs -----------------------
  * Replaces the single-process G-way merge of MatchFinder::SearchRange

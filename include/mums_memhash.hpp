@@ -120,6 +120,17 @@ public:
     }
     mums_ctx* handle() const { return ctx_; }
 
+    // GenericMatchList::MultiplicityFilter / LengthFilter (MatchList.h:636-664), applied on
+    // the device copy of the last MatchList before GetMatchList
+    void MultiplicityFilter(unsigned mult) { check(mums_multiplicity_filter(ctx_, mult)); }
+    void LengthFilter(uint64_t length) { check(mums_length_filter(ctx_, length)); }
+    // SeedOccurrenceList::construct + getFrequency (SeedOccurrenceList.h:22-67) for genome g
+    std::vector<float> SeedOccurrence(uint32_t genome, uint64_t length) const {
+        std::vector<float> f(length);
+        check(mums_seed_occurrence(ctx_, genome, f.data(), length));
+        return f;
+    }
+
 protected:
     void check(int rc) const {
         if (rc == MUMS_OK) return;

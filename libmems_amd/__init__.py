@@ -89,6 +89,7 @@ EXPORTED_SYMBOLS = [
     "mums_build_sml", "mums_set_profiling", "mums_shard_layout", "mums_shard_msd_bits", "mums_shard_keys",
     "mums_shard_merge", "mums_probe_count", "mums_probe_copy", "mums_shard_bucket_counts", "mums_shard_probe_rows",
     "mums_shard_packed_info", "mums_shard_packed_copy", "mums_shard_find", "mums_set_parallel_compat",
+    "mums_seed_occurrence", "mums_multiplicity_filter", "mums_length_filter",
 ]
 
 _lib: Optional[ctypes.CDLL] = None
@@ -146,6 +147,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mums_shard_packed_copy.argtypes = [vp, vp]
     lib.mums_shard_find.argtypes = [vp, vp, u64, vp]
     lib.mums_set_parallel_compat.argtypes = [vp, i32, u64]
+    lib.mums_seed_occurrence.argtypes = [vp, u32, vp, u64]
+    lib.mums_multiplicity_filter.argtypes = [vp, u32]
+    lib.mums_length_filter.argtypes = [vp, u64]
     _lib = lib
     return lib
 
@@ -336,6 +340,20 @@ class MemHash:
         out = np.zeros(max(m, 1), dtype=np.uint32)
         self._check(self._lib.mums_build_sml(self._ctx, genome, out.ctypes.data, m))
         return out[:m]
+
+    def SeedOccurrence(self, genome: int, n: int) -> np.ndarray:
+        """SeedOccurrenceList::construct over genome's SML (SeedOccurrenceList.h:22-87):
+        float32 getFrequency() of every position 0..n-1 (n = genome length)."""
+        out = np.zeros(max(n, 1), dtype=np.float32)
+        self._check(self._lib.mums_seed_occurrence(self._ctx, genome, out.ctypes.data, n))
+        return out[:n]
+
+    # ---- MatchList filters (MatchList.h:636-664), on the device copy of the result ----
+    def MultiplicityFilter(self, mult: int) -> None:
+        self._check(self._lib.mums_multiplicity_filter(self._ctx, mult))
+
+    def LengthFilter(self, length: int) -> None:
+        self._check(self._lib.mums_length_filter(self._ctx, length))
 
 
 class MaskedMemHash(MemHash):

@@ -80,6 +80,8 @@ struct mums_ctx {
     uint64_t chunk_size = 200000;
     uint32_t nchunks = 0;
     DevBuf cval, ctab;
+    // one genome's SML / seed frequencies (sml_tools.hip) and filtered MatchLists
+    DevBuf smlk0, smlkA, smlkB, smlvA, smlvB, smltmp, flen, fs;
     hipEvent_t ev[EV_COUNT] = {};
     bool profiling = false;
     hipEvent_t ev_ds[16] = {};   // 2 per radix pass (<= 8 passes)
@@ -856,7 +858,8 @@ int mums_ctx_destroy(mums_ctx* ctx) {
                       &ctx->bend, &ctx->tsize, &ctx->obase, &ctx->pool, &ctx->tbl, &ctx->out_len, &ctx->out_s,
                       &ctx->pbuf, &ctx->keybuf, &ctx->mstart, &ctx->chain_tmp, &ctx->chain_of,
                       &ctx->radix_tmp, &ctx->spill, &ctx->summ, &ctx->dbgbuf, &ctx->mprobe, &ctx->rowtmp,
-                      &ctx->cval, &ctx->ctab};
+                      &ctx->cval, &ctx->ctab, &ctx->smlk0, &ctx->smlkA, &ctx->smlkB, &ctx->smlvA,
+                      &ctx->smlvB, &ctx->smltmp, &ctx->flen, &ctx->fs};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i < EV_COUNT; ++i)
         if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
@@ -1011,6 +1014,30 @@ int mums_copy_seed_keys(mums_ctx* ctx, uint32_t genome, uint64_t* out, uint64_t 
     return MUMS_OK;
 }
 
+// One genome's SortedMerList on the device (MemorySML::Create, MemorySML.cpp:45-60):
+// its ckeys from the packed genome, stably sorted (ties by position) -> *sk, *sv.
+int genome_sml(mums_ctx* ctx, uint32_t genome, const uint64_t** sk, const uint32_t** sv) {
+    const uint64_t m = ctx->gt.m[genome];
+    hipStream_t st = ctx->stream;
+    HIPCHK(ctx->smlk0.ensure(m * 8 + 64));
+    HIPCHK(ctx->smlkA.ensure(m * 8 + 64));
+    HIPCHK(ctx->smlkB.ensure(m * 8 + 64));
+    HIPCHK(ctx->smlvA.ensure(m * 4 + 64));
+    HIPCHK(ctx->smlvB.ensure(m * 4 + 64));
+    HIPCHK(ctx->smltmp.ensure(std::max(radix_tmp_bytes(m + 1), occ_tmp_bytes(m + 1))));
+    int buf = 0;
+    if (m) {
+        HIPCHK(launch_keys_of_genome(ctx->ss, ctx->packed.as<uint32_t>() + ctx->gt.woff[genome], m,
+                                     ctx->smlk0.as<uint64_t>(), st, false));
+        HIPCHK(radix_sort<uint64_t>(ctx->smlk0.as<uint64_t>(), nullptr, m, 2 * ctx->w + 1, ctx->smlkA.as<uint64_t>(),
+                                    ctx->smlvA.as<uint32_t>(), ctx->smlkB.as<uint64_t>(), ctx->smlvB.as<uint32_t>(),
+                                    ctx->smltmp.p, &buf, st));
+    }
+    *sk = buf ? ctx->smlkB.as<uint64_t>() : ctx->smlkA.as<uint64_t>();
+    *sv = buf ? ctx->smlvB.as<uint32_t>() : ctx->smlvA.as<uint32_t>();
+    return MUMS_OK;
+}
+
 int mums_build_sml(mums_ctx* ctx, uint32_t genome, uint32_t* positions, uint64_t cap) {
     if (check_ctx(ctx)) return MUMS_E_INVALID;
     if (ctx->stage_done < MUMS_STAGE_SEEDS) return fail(ctx, MUMS_E_INVALID, "keys not sorted yet");
@@ -1018,22 +1045,64 @@ int mums_build_sml(mums_ctx* ctx, uint32_t genome, uint32_t* positions, uint64_t
     const uint64_t m = ctx->gt.m[genome];
     if (cap < m) return fail(ctx, MUMS_E_INVALID, "output buffer too small");
     HIPCHK(hipSetDevice(ctx->device));
-    // the merged sorted stream restricted to one genome is that genome's SML
-    const uint64_t N = ctx->N;
-    std::vector<uint32_t> idx(N);
-    if (ctx->packed_path) {
-        std::vector<uint64_t> rec(N);
-        if (N) HIPCHK(hipMemcpy(rec.data(), ctx->sorted_rec, N * 8, hipMemcpyDeviceToHost));
-        for (uint64_t i = 0; i < N; ++i) idx[i] = (uint32_t)rec[i];
-    } else if (N) {
-        HIPCHK(hipMemcpy(idx.data(), ctx->sorted_idx, N * 4, hipMemcpyDeviceToHost));
-    }
-    const uint64_t lo = ctx->gt.base[genome], hi = ctx->gt.base[genome + 1];
-    uint64_t o = 0;
-    for (uint64_t i = 0; i < N; ++i)
-        if (idx[i] >= lo && idx[i] < hi) positions[o++] = (uint32_t)(idx[i] - lo);
+    const uint64_t* sk = nullptr;
+    const uint32_t* sv = nullptr;
+    int rc = genome_sml(ctx, genome, &sk, &sv);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (m) HIPCHK(hipMemcpy(positions, sv, m * 4, hipMemcpyDeviceToHost));
     return MUMS_OK;
 }
+
+int mums_seed_occurrence(mums_ctx* ctx, uint32_t genome, float* freq, uint64_t cap) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (ctx->stage_done < MUMS_STAGE_SEEDS) return fail(ctx, MUMS_E_INVALID, "keys not computed yet");
+    if (genome >= ctx->genomes.size()) return fail(ctx, MUMS_E_INVALID, "genome index out of range");
+    const uint64_t m = ctx->gt.m[genome], n = ctx->gt.n[genome];
+    if (cap < n) return fail(ctx, MUMS_E_INVALID, "output buffer too small");
+    if (n >= 0xFFFFFFF0ull) return fail(ctx, MUMS_E_UNSUPPORTED, "genome longer than 2^32");
+    HIPCHK(hipSetDevice(ctx->device));
+    const uint64_t* sk = nullptr;
+    const uint32_t* sv = nullptr;
+    int rc = genome_sml(ctx, genome, &sk, &sv);
+    if (rc) return rc;
+    HIPCHK(ctx->keybuf.ensure(n * 4 + 64));
+    HIPCHK(launch_seed_occurrence(sk, sv, m, n, ctx->L, ctx->smltmp.p, ctx->keybuf.as<float>(), ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (n) HIPCHK(hipMemcpy(freq, ctx->keybuf.p, n * 4, hipMemcpyDeviceToHost));
+    return MUMS_OK;
+}
+
+// MultiplicityFilter / LengthFilter (MatchList.h:636-664) on the context's MatchList
+int match_filter(mums_ctx* ctx, uint32_t mult, uint64_t min_len) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (ctx->stage_done < MUMS_STAGE_ALL) return fail(ctx, MUMS_E_INVALID, "no completed FindMatches on this context");
+    HIPCHK(hipSetDevice(ctx->device));
+    const int G = ctx->gt.G;
+    const uint64_t M = ctx->M;
+    hipStream_t st = ctx->stream;
+    HIPCHK(ctx->flen.ensure((M + 1) * 8));
+    HIPCHK(ctx->fs.ensure((M + 1) * (size_t)G * 8 + 8));
+    HIPCHK(ctx->smltmp.ensure(filter_tmp_bytes(M + 1) + 64));
+    uint32_t* d_kept = (uint32_t*)ctx->smltmp.p;
+    HIPCHK(launch_match_filter(ctx->out_len.as<uint64_t>(), ctx->out_s.as<int64_t>(), M, G, mult, min_len,
+                               (char*)ctx->smltmp.p + 256, d_kept, ctx->flen.as<uint64_t>(), ctx->fs.as<int64_t>(),
+                               st));
+    uint32_t kept = 0;
+    HIPCHK(hipMemcpyAsync(&kept, d_kept, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    std::swap(ctx->out_len, ctx->flen);
+    std::swap(ctx->out_s, ctx->fs);
+    ctx->M = kept;
+    return MUMS_OK;
+}
+
+int mums_multiplicity_filter(mums_ctx* ctx, uint32_t mult) {
+    if (mult == 0) return check_ctx(ctx) ? MUMS_E_INVALID : fail(ctx, MUMS_E_INVALID, "multiplicity 0");
+    return match_filter(ctx, mult, 0);
+}
+
+int mums_length_filter(mums_ctx* ctx, uint64_t min_len) { return match_filter(ctx, 0, min_len); }
 
 // ---- sharded seed stage -------------------------------------------
 

@@ -136,9 +136,10 @@ hipError_t launch_seed_pack(const SeedSpec& ss, const GenomeTable& gt, const cha
 // packed path: scatter records into MSD buckets (offsets = scanned hist)
 hipError_t launch_seed_scatter(const SeedSpec& ss, const GenomeTable& gt, const uint32_t* d_packed, int msd_bits,
                                const uint32_t* d_hist_scanned, uint32_t ntiles, uint64_t* d_rec, hipStream_t st);
-// ckey of every position of one genome (helper for mums_copy_seed_keys)
+// key of every position of one genome: ref_form = GetDnaSeedMer's left-aligned 64-bit mer
+// (mums_copy_seed_keys), else the 2w+1-bit ckey (same order; one genome's SML sort)
 hipError_t launch_keys_of_genome(const SeedSpec& ss, const uint32_t* d_words, uint64_t m, uint64_t* d_out,
-                                 hipStream_t st);
+                                 hipStream_t st, bool ref_form = true);
 
 // scan.hip: exclusive scan of n uint32 values in place; d_tmp needs scan_tmp_bytes(n)
 size_t scan_tmp_bytes(uint64_t n);
@@ -215,6 +216,15 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
 hipError_t launch_emit(const uint32_t* tsize, const uint32_t* obase, const uint32_t* bstart, const uint32_t* tbl,
                        const int64_t* pool, int G, uint32_t table_size, uint64_t* out_len, int64_t* out_s,
                        hipStream_t st);
+
+// sml_tools.hip: SeedOccurrenceList and MatchList filters
+size_t occ_tmp_bytes(uint64_t m);
+hipError_t launch_seed_occurrence(const uint64_t* sk, const uint32_t* sv, uint64_t m, uint64_t n, int L, void* d_tmp,
+                                  float* out, hipStream_t st);
+size_t filter_tmp_bytes(uint64_t M);
+hipError_t launch_match_filter(const uint64_t* len, const int64_t* s, uint64_t M, int G, uint32_t mult,
+                               uint64_t min_len, void* d_tmp, uint32_t* d_kept, uint64_t* len2, int64_t* s2,
+                               hipStream_t st);
 
 // compat.hip: ParallelMemHash chunk-compat mode (ParallelMemHash.cpp:42-121)
 hipError_t launch_genome_keys(uint64_t* ckey, uint64_t N, const GenomeTable& gt, int kbits, hipStream_t st);

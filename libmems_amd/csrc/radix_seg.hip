@@ -38,6 +38,12 @@ constexpr int kDigits = 256;
 #endif
 constexpr int kSortBlock = MUMS_SORT_BLOCK;    // threads per onesweep block
 constexpr int kSortTile = MUMS_SORT_TILE;      // records per onesweep tile (longer digit runs per store)
+#ifndef MUMS_OS_LATEPUB
+#define MUMS_OS_LATEPUB 0   // 1: publish the tile aggregate after ranking (no early per-digit atomics)
+#endif
+#ifndef MUMS_OS_FUSED
+#define MUMS_OS_FUSED 0     // 1: fold lstart into the per-wave bases and the output offsets
+#endif
 #ifndef MUMS_LOOKBACK
 #define MUMS_LOOKBACK 4
 #endif
@@ -363,6 +369,7 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
         key[r] = q < d.count ? rin[d.start + q] : 0ull;
 #endif
     }
+#if !MUMS_OS_LATEPUB
     // publish this tile's per-digit counts as soon as the keys are in: successors'
     // look-backs then rarely find an unpublished predecessor.
     #pragma unroll
@@ -374,6 +381,7 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
     if (d.tb != 0 && tid < kDigits)
         __hip_atomic_store(status + (uint64_t)t * kDigits + tid, kFlagAgg | hcnt[tid], __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
+#endif
     #pragma unroll
     for (int r = 0; r < kIPT; ++r) {
         const uint32_t q = q0 + r * 64 + lane;
@@ -394,6 +402,9 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
         for (int w = 0; w < kW; ++w) { const uint32_t x = wcnt[w][dg]; wcnt[w][dg] = acc; acc += x; }
         // look back over the bucket's preceding tiles, then publish the inclusive prefix
         uint32_t* st = status + (uint64_t)t * kDigits + dg;
+#if MUMS_OS_LATEPUB
+        if (d.tb != 0) __hip_atomic_store(st, kFlagAgg | acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
         uint32_t prefix = 0;
         if (d.tb == 0) {
             __hip_atomic_store(st, kFlagInc | acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -449,6 +460,14 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
         #pragma unroll
         for (int w = 0; w < kDigits / 64; ++w) wpre += (w < wv) ? s_w[w] : 0u;
         lstart[tid] = wpre + v - acc;
+#if MUMS_OS_FUSED
+        // one LDS read per record in each scatter: per-wave LDS slot base and the
+        // tile-slot -> output offset of every digit
+        const uint32_t ls = wpre + v - acc;
+        #pragma unroll
+        for (int w = 0; w < kW; ++w) wcnt[w][tid] += ls;
+        gofs[tid] -= ls;
+#endif
     }
     __syncthreads();
     #pragma unroll
@@ -456,7 +475,11 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
         const uint32_t q = q0 + r * 64 + lane;
         if (q < d.count) {
             const uint32_t dg = (uint32_t)(key[r] >> shift) & 0xFFu;
+#if MUMS_OS_FUSED
+            srec[wcnt[wv][dg] + rank[r]] = key[r];
+#else
             srec[lstart[dg] + wcnt[wv][dg] + rank[r]] = key[r];
+#endif
         }
     }
     __syncthreads();
@@ -466,10 +489,15 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
         if (sidx < d.count) {
             const uint64_t k = srec[sidx];
             const uint32_t dg = (uint32_t)(k >> shift) & 0xFFu;
-#if MUMS_SORT_NT & 2
-            __builtin_nontemporal_store(k, rout + (uint64_t)gofs[dg] + (sidx - lstart[dg]));
+#if MUMS_OS_FUSED
+            const uint64_t o = (uint64_t)(uint32_t)(gofs[dg] + sidx);   // gofs holds out offset - lstart (mod 2^32)
 #else
-            rout[(uint64_t)gofs[dg] + (sidx - lstart[dg])] = k;
+            const uint64_t o = (uint64_t)gofs[dg] + (sidx - lstart[dg]);
+#endif
+#if MUMS_SORT_NT & 2
+            __builtin_nontemporal_store(k, rout + o);
+#else
+            rout[o] = k;
 #endif
         }
     }

@@ -281,11 +281,12 @@ __global__ __launch_bounds__(kBlock) void seed_scatter_flat_kernel(SeedSpec ss, 
 }
 
 __global__ void keys_of_genome_kernel(SeedSpec ss, const uint32_t* __restrict__ W, uint64_t m,
-                                      uint64_t* __restrict__ out) {
+                                      uint64_t* __restrict__ out, int ref_form) {
     const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= m) return;
     const uint64_t k = ckey_at(W, p, ss);
-    out[p] = ((k >> 1) << (64 - 2 * ss.w)) | (k & 1);   // GetDnaSeedMer's left-aligned form
+    out[p] = ref_form ? (((k >> 1) << (64 - 2 * ss.w)) | (k & 1))   // GetDnaSeedMer's left-aligned form
+                      : k;                                          // ckey = v << 1 | parity (same order)
 }
 
 }  // namespace
@@ -343,10 +344,10 @@ hipError_t launch_seed_scatter(const SeedSpec& ss, const GenomeTable& gt, const 
 }
 
 hipError_t launch_keys_of_genome(const SeedSpec& ss, const uint32_t* d_words, uint64_t m, uint64_t* d_out,
-                                 hipStream_t st) {
+                                 hipStream_t st, bool ref_form) {
     if (m == 0) return hipSuccess;
     hipLaunchKernelGGL(keys_of_genome_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, ss, d_words, m,
-                       d_out);
+                       d_out, ref_form ? 1 : 0);
     return hipGetLastError();
 }
 

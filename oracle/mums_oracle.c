@@ -224,6 +224,50 @@ int oracle_build_sml(const char* seq, uint64_t n, uint64_t seed, uint32_t* out_p
     return 0;
 }
 
+/* SeedOccurrenceList::construct (SeedOccurrenceList.h:22-61) and          */
+/* smoothFrequencies (:71-87), literally: float32 counts, double running sum. */
+int oracle_seed_occurrence(const char* seq, uint64_t n, uint64_t seed, float* count) {
+    sml_ctx c; uint32_t* w;
+    int rc = sml_init(&c, seq, n, seed, &w);
+    if (rc) return rc;
+    uint64_t m = sml_length(n, c.L);
+    uint64_t* keys = (uint64_t*)malloc((m ? m : 1) * sizeof(uint64_t));
+    for (uint64_t p = 0; p < m; ++p) keys[p] = get_dna_seed_mer(&c, p);
+    bmer_t* sml = build_sml(&c, keys, m);
+    const uint64_t total_len = n, mask = c.seed_mask;
+    for (uint64_t i = 0; i < total_len; ++i) count[i] = 0.0f;
+    uint64_t seed_start = 0, cur_seed_count = 1, seedI = 1;
+    for (seedI = 1; seedI < m; seedI++) {
+        if ((sml[seedI].key & mask) == (sml[seedI - 1].key & mask)) { ++cur_seed_count; continue; }
+        for (uint64_t i = seed_start; i < seedI; ++i) count[sml[i].pos] = (float)cur_seed_count;
+        seed_start = seedI;
+        cur_seed_count = 1;
+    }
+    for (uint64_t i = seed_start; i < seedI && i < m; ++i) count[sml[i].pos] = (float)cur_seed_count;
+    for (; seedI < total_len; ++seedI) count[seedI] = 1;
+    /* smoothFrequencies */
+    {
+        const uint64_t L = (uint64_t)c.L;
+        float* buf = (float*)malloc(L * sizeof(float));
+        for (uint64_t k = 0; k < L; ++k) buf[k] = 1.0f;
+        if (total_len > 0) {
+            double sum = (double)(L - 1) + count[0];
+            buf[0] = count[0];
+            for (uint64_t i = 1; i < total_len; i++) {
+                count[i - 1] = (float)(sum / (double)L);
+                sum += count[i];
+                uint64_t bufI = i % L;
+                sum -= buf[bufI];
+                buf[bufI] = count[i];
+            }
+        }
+        free(buf);
+    }
+    for (uint64_t i = 0; i < total_len; ++i) if (count[i] == 0) count[i] = 1;
+    free(sml); free(keys); free(w);
+    return 0;
+}
+
 /* ------------------------------------------------------------------------- */
 /* MatchHashEntry (MatchHashEntry.h:30-103, MatchHashEntry.cpp).              */
 /* A match = one length + G signed 1-based starts (0 = NO_MATCH,             */

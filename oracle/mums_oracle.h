@@ -37,6 +37,8 @@ int64_t  oracle_pack(const char* seq, uint64_t n, uint32_t* out_words);
 int      oracle_seed_keys(const char* seq, uint64_t n, uint64_t seed, uint64_t* out_keys);
 /* MemorySML::Create: positions sorted by full 64-bit key (ties: position asc) */
 int      oracle_build_sml(const char* seq, uint64_t n, uint64_t seed, uint32_t* out_pos);
+/* SeedOccurrenceList::construct + smoothFrequencies: n float32 frequencies */
+int      oracle_seed_occurrence(const char* seq, uint64_t n, uint64_t seed, float* out);
 
 /* ---- MemHash::FindMatches ---- */
 typedef struct oracle_params {

@@ -110,6 +110,16 @@ def build_sml(seq: bytes, seed: int) -> np.ndarray:
     return out[:m]
 
 
+def seed_occurrence(seq: bytes, seed: int) -> np.ndarray:
+    """SeedOccurrenceList::construct (SeedOccurrenceList.h:22-87): float32 per position."""
+    out = np.zeros(max(len(seq), 1), dtype=np.float32)
+    lib().oracle_seed_occurrence.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]
+    rc = lib().oracle_seed_occurrence(seq, len(seq), seed, out.ctypes.data)
+    if rc:
+        raise ValueError("oracle rejected input")
+    return out[:len(seq)]
+
+
 def find_matches(seqs: Sequence[bytes], seed: int, repeat_tol: int = 0, enum_tol: int = 1,
                  table_size: int = 40000, masked: bool = False, seq_mask: int = 0,
                  gnseqi_end_neg1: bool = False, seeds_only: bool = False, parallel_compat: bool = False,
