@@ -142,6 +142,14 @@ int  mums_seed_occurrence(mums_ctx* ctx, uint32_t genome, float* freq, uint64_t 
 /* GenericMatchList::MultiplicityFilter / LengthFilter (MatchList.h:636-664) applied to
  * the context's last MatchList in place (order kept). */
 int  mums_multiplicity_filter(mums_ctx* ctx, uint32_t multiplicity);
+/* DNAFileSML (format version 5, DNAFileSML.h:58-62) writer, FileSML::Create's file
+ * (FileSML.cpp:316-374): SMLHeader + 2-bit sequence words + SML positions, for genome g
+ * of a context whose seed stage ran.  Readable by FileSML::LoadFile (FileSML.cpp:46-110)
+ * so LoadSMLs callers (MatchList.h:261-349) reuse GPU-built SMLs. */
+int  mums_write_sml(mums_ctx* ctx, uint32_t genome, const char* path, const char* description);
+/* FileSML::LoadFile (FileSML.cpp:46-110) of such a file: its sequence becomes the next
+ * genome of the context; *seed_out = the file's seed pattern (may be NULL). */
+int  mums_add_genome_sml(mums_ctx* ctx, const char* path, uint64_t* seed_out);
 int  mums_length_filter(mums_ctx* ctx, uint64_t min_length);
 
 /* ---- sharded seed stage across GPUs -----------------------

@@ -89,7 +89,8 @@ EXPORTED_SYMBOLS = [
     "mums_build_sml", "mums_set_profiling", "mums_shard_layout", "mums_shard_msd_bits", "mums_shard_keys",
     "mums_shard_merge", "mums_probe_count", "mums_probe_copy", "mums_shard_bucket_counts", "mums_shard_probe_rows",
     "mums_shard_packed_info", "mums_shard_packed_copy", "mums_shard_find", "mums_set_parallel_compat",
-    "mums_seed_occurrence", "mums_multiplicity_filter", "mums_length_filter",
+    "mums_seed_occurrence", "mums_multiplicity_filter", "mums_length_filter", "mums_write_sml",
+    "mums_add_genome_sml",
 ]
 
 _lib: Optional[ctypes.CDLL] = None
@@ -150,6 +151,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mums_seed_occurrence.argtypes = [vp, u32, vp, u64]
     lib.mums_multiplicity_filter.argtypes = [vp, u32]
     lib.mums_length_filter.argtypes = [vp, u64]
+    lib.mums_write_sml.argtypes = [vp, u32, ctypes.c_char_p, ctypes.c_char_p]
+    lib.mums_add_genome_sml.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(u64)]
     _lib = lib
     return lib
 
@@ -347,6 +350,16 @@ class MemHash:
         out = np.zeros(max(n, 1), dtype=np.float32)
         self._check(self._lib.mums_seed_occurrence(self._ctx, genome, out.ctypes.data, n))
         return out[:n]
+
+    # ---- on-disk SortedMerList (DNAFileSML v5: FileSML.cpp:46-110, 316-374) --------------
+    def WriteSML(self, genome: int, path: str, description: str = "") -> None:
+        self._check(self._lib.mums_write_sml(self._ctx, genome, path.encode(), description.encode()))
+
+    def AddSequenceFromSML(self, path: str) -> int:
+        """FileSML::LoadFile: the file's sequence becomes the next genome; returns its seed."""
+        seed = ctypes.c_uint64()
+        self._check(self._lib.mums_add_genome_sml(self._ctx, path.encode(), ctypes.byref(seed)))
+        return seed.value
 
     # ---- MatchList filters (MatchList.h:636-664), on the device copy of the result ----
     def MultiplicityFilter(self, mult: int) -> None:

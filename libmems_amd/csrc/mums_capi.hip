@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1070,6 +1071,118 @@ int mums_seed_occurrence(mums_ctx* ctx, uint32_t genome, float* freq, uint64_t c
     HIPCHK(launch_seed_occurrence(sk, sv, m, n, ctx->L, ctx->smltmp.p, ctx->keybuf.as<float>(), ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     if (n) HIPCHK(hipMemcpy(freq, ctx->keybuf.p, n * 4, hipMemcpyDeviceToHost));
+    return MUMS_OK;
+}
+
+// ---- on-disk SortedMerList, DNAFileSML format version 5 ------------
+// File = SMLHeader (SortedMerList.h:48-63, written raw: FileSML.cpp:336) + the 2-bit
+// sequence words (binary_seq_len = ceil(2n/32) + 2, :340) + SMLLength() uint32 positions in
+// SML order (:344-345).  Header values as dmSML's InitSML writes them (dmSML/sml.c:9-24).
+// Layout on x86-64 with libGenome's one-byte boolean: 2352 bytes.
+struct SmlHeaderV5 {
+    uint32_t version;
+    uint32_t alphabet_bits;
+    uint64_t seed;
+    uint32_t seed_length;
+    uint32_t seed_weight;
+    uint64_t length;
+    uint32_t unique_mers;
+    uint32_t word_size;
+    uint8_t little_endian;
+    int16_t id;
+    uint8_t circular;
+    uint8_t translation_table[255];   // UINT8_MAX entries
+    char description[2048];           // DESCRIPTION_SIZE
+};
+static_assert(sizeof(SmlHeaderV5) == 2352, "SMLHeader layout");
+static_assert(offsetof(SmlHeaderV5, id) == 42 && offsetof(SmlHeaderV5, circular) == 44 &&
+              offsetof(SmlHeaderV5, translation_table) == 45 && offsetof(SmlHeaderV5, description) == 300,
+              "SMLHeader field offsets");
+constexpr uint32_t kDnaFileSmlVersion = 5;   // DNAFileSML::FormatVersion (DNAFileSML.h:58-62)
+
+void basic_dna_table(uint8_t* t) {   // SortedMerList::CreateBasicDNATable (SortedMerList.cpp:29-47)
+    memset(t, 0, 255);
+    const char* c1 = "cCbByY";
+    const char* c2 = "gGsSkK";
+    for (const char* p = c1; *p; ++p) t[(uint8_t)*p] = 1;
+    for (const char* p = c2; *p; ++p) t[(uint8_t)*p] = 2;
+    t['t'] = 3;
+    t['T'] = 3;
+}
+
+int mums_write_sml(mums_ctx* ctx, uint32_t genome, const char* path, const char* description) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (ctx->stage_done < MUMS_STAGE_SEEDS) return fail(ctx, MUMS_E_INVALID, "keys not computed yet");
+    if (genome >= ctx->genomes.size()) return fail(ctx, MUMS_E_INVALID, "genome index out of range");
+    if (!path) return fail(ctx, MUMS_E_INVALID, "null path");
+    HIPCHK(hipSetDevice(ctx->device));
+    const uint64_t n = ctx->gt.n[genome], m = ctx->gt.m[genome];
+    const uint64_t words = packed_words(n);
+    const uint64_t* sk = nullptr;
+    const uint32_t* sv = nullptr;
+    int rc = genome_sml(ctx, genome, &sk, &sv);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    std::vector<uint32_t> w(words), pos(m);
+    HIPCHK(hipMemcpy(w.data(), ctx->packed.as<uint32_t>() + ctx->gt.woff[genome], words * 4, hipMemcpyDeviceToHost));
+    if (m) HIPCHK(hipMemcpy(pos.data(), sv, m * 4, hipMemcpyDeviceToHost));
+    SmlHeaderV5 h;
+    memset(&h, 0, sizeof(h));
+    h.version = kDnaFileSmlVersion;
+    h.alphabet_bits = 2;
+    h.seed = ctx->pattern;
+    h.seed_length = (uint32_t)ctx->L;
+    h.seed_weight = (uint32_t)ctx->w;
+    h.length = n;
+    h.unique_mers = 0xFFFFFFFFu;   // NO_UNIQUE_COUNT (SortedMerList.h:36)
+    h.word_size = 32;
+    h.little_endian = 1;
+    basic_dna_table(h.translation_table);
+    if (description) strncpy(h.description, description, sizeof(h.description) - 1);
+    FILE* f = fopen(path, "wb");
+    if (!f) return fail(ctx, MUMS_E_INVALID, "Unable to open file for writing.");   // FileSML.cpp:125
+    bool ok = fwrite(&h, sizeof(h), 1, f) == 1;
+    ok = ok && fwrite(w.data(), 4, words, f) == words;
+    ok = ok && (m == 0 || fwrite(pos.data(), 4, m, f) == m);
+    ok = (fclose(f) == 0) && ok;
+    if (!ok) return fail(ctx, MUMS_E_INVALID, "Error writing sorted mer list to disk.");   // FileSML.cpp:349
+    return MUMS_OK;
+}
+
+// FileSML::LoadFile (FileSML.cpp:46-110): header check, then the 2-bit sequence becomes a
+// context-owned genome (unpacked on the device; ExtendMatch and the keys only ever see
+// the 2-bit codes, so A/C/G/T re-pack to the same words).  *seed_out = header.seed.
+int mums_add_genome_sml(mums_ctx* ctx, const char* path, uint64_t* seed_out) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (!path) return fail(ctx, MUMS_E_INVALID, "null path");
+    if (ctx->genomes.size() >= (size_t)kMaxG)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "more than 32 genomes per context");
+    FILE* f = fopen(path, "rb");
+    if (!f) return fail(ctx, MUMS_E_INVALID, "Unable to open file.");   // FileSML.cpp:51
+    SmlHeaderV5 h;
+    if (fread(&h, sizeof(h), 1, f) != 1) { fclose(f); return fail(ctx, MUMS_E_INVALID, "Unable to read file."); }
+    if (h.version != kDnaFileSmlVersion) { fclose(f); return fail(ctx, MUMS_E_INVALID, "Unsupported file format."); }
+    if (h.alphabet_bits != 2 || h.circular) {
+        fclose(f);
+        return fail(ctx, MUMS_E_UNSUPPORTED, "only linear DNA sorted mer lists are supported");
+    }
+    const uint64_t n = h.length, words = packed_words(n);
+    std::vector<uint32_t> w(words);
+    const bool ok = fread(w.data(), 4, words, f) == words;
+    fclose(f);
+    if (!ok) return fail(ctx, MUMS_E_INVALID, "Error reading sequence data.");   // FileSML.cpp:86
+    HIPCHK(hipSetDevice(ctx->device));
+    char* d = nullptr;
+    uint32_t* dw = nullptr;
+    HIPCHK(hipMalloc(&d, n + 16));
+    HIPCHK(hipMalloc(&dw, words * 4 + 16));
+    HIPCHK(hipMemcpy(dw, w.data(), words * 4, hipMemcpyHostToDevice));
+    HIPCHK(launch_unpack(dw, n, d, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipFree(dw));
+    ctx->genomes.push_back({d, n, true});
+    ctx->stage_done = 0;
+    if (seed_out) *seed_out = h.seed;
     return MUMS_OK;
 }
 

@@ -221,6 +221,7 @@ hipError_t launch_emit(const uint32_t* tsize, const uint32_t* obase, const uint3
 size_t occ_tmp_bytes(uint64_t m);
 hipError_t launch_seed_occurrence(const uint64_t* sk, const uint32_t* sv, uint64_t m, uint64_t n, int L, void* d_tmp,
                                   float* out, hipStream_t st);
+hipError_t launch_unpack(const uint32_t* words, uint64_t n, char* out, hipStream_t st);
 size_t filter_tmp_bytes(uint64_t M);
 hipError_t launch_match_filter(const uint64_t* len, const int64_t* s, uint64_t M, int G, uint32_t mult,
                                uint64_t min_len, void* d_tmp, uint32_t* d_kept, uint64_t* len2, int64_t* s2,

@@ -2,7 +2,8 @@
 //   * one genome's SortedMerList (MemorySML::Create, MemorySML.cpp:45-60) on its own;
 //   * SeedOccurrenceList::construct (SeedOccurrenceList.h:22-61) + smoothFrequencies
 //     (:71-87): per-position seed frequency from the masked-key runs of that SML;
-//   * MatchList::MultiplicityFilter / LengthFilter (MatchList.h:636-664) on the result.
+//   * MatchList::MultiplicityFilter / LengthFilter (MatchList.h:636-664) on the result;
+//   * 2-bit words -> ASCII for sequences read from DNAFileSML files (FileSML::LoadFile).
 #include <hip/hip_runtime.h>
 
 #include "mums_internal.h"
@@ -93,6 +94,14 @@ __global__ void match_compact_kernel(const uint64_t* __restrict__ len, const int
     for (int g = 0; g < G; ++g) s2[(uint64_t)o * G + g] = s[k * (uint64_t)G + g];
 }
 
+// 2-bit words (translate32 layout, MSB-first) -> ASCII A/C/G/T
+__global__ void unpack_kernel(const uint32_t* __restrict__ W, uint64_t n, char* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t c = (W[i >> 4] >> (30 - 2 * (uint32_t)(i & 15))) & 3u;
+    out[i] = "ACGT"[c];
+}
+
 inline dim3 grid_of(uint64_t n) { return dim3((unsigned)((n + 255) / 256)); }
 
 }  // namespace
@@ -114,6 +123,12 @@ hipError_t launch_seed_occurrence(const uint64_t* sk, const uint32_t* sv, uint64
         hipLaunchKernelGGL(occ_count_kernel, grid_of(m), dim3(256), 0, st, sk, sv, m, a, rstart, nruns, cnt);
     }
     if (n) hipLaunchKernelGGL(occ_smooth_kernel, grid_of(n), dim3(256), 0, st, cnt, m, n, L, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_unpack(const uint32_t* words, uint64_t n, char* out, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(unpack_kernel, grid_of(n), dim3(256), 0, st, words, n, out);
     return hipGetLastError();
 }
 
