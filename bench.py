@@ -212,7 +212,8 @@ def main():
         value = seedmers_total * args.steps / dt
         achieved = bytes_dom / (ms_dom * 1e-3) / 1e9 if ms_dom > 0 else None
         traffic = None
-        if os.path.exists(PROFILE_SUMMARY):
+        # the committed PMC summary was measured on the default N=1 workload only
+        if world == 1 and (G, n) == (8, 100_000_000) and os.path.exists(PROFILE_SUMMARY):
             try:
                 traffic = json.load(open(PROFILE_SUMMARY)).get("hbm_bytes_per_launch")
             except Exception:
@@ -235,7 +236,8 @@ def main():
                                    f"MemHash seed stage (sorted+matched)",
                        "genomes": G, "genome_length": n, "seedmers_total": seedmers_total,
                        "seedmers_rank0": seedmers_rank, "probes_rank0": probes,
-                       "parallelism": (f"genome-sharded x{world}: genome block per rank, RCCL all-to-all of key "
+                       "parallelism": (f"genome-sharded x{world}: genome block per rank, "
+                                       f"{'RCCL' if args.dist_backend == 'nccl' else args.dist_backend} all-to-all of key "
                                        f"ranges ({exch_bytes / max(args.steps, 1) / 1e9:.2f} GB/step sent by rank 0), "
                                        f"merge per key range") if world > 1 else "1 GPU"},
             "roofline": {
