@@ -98,6 +98,10 @@ int  mums_set_mask(mums_ctx* ctx, int masked, uint64_t seq_mask);
  * the (patched) OpenMP reference's.  chunk_size 0 = the
  * reference's CHUNK_SIZE 200000 (:51).  enable=0 = serial MemHash (default). */
 int  mums_set_parallel_compat(mums_ctx* ctx, int enable, uint64_t chunk_size);
+/* PairwiseMatchFinder (PairwiseMatchFinder.h:23-33): a MemHash whose EnumerateMatches
+ * (PairwiseMatchFinder.cpp:37-73) hashes every pair of genomes occurring once in a seed
+ * group instead of one multi-genome seed.  enable=0 = MemHash. */
+int  mums_set_pairwise(mums_ctx* ctx, int enable);
 
 /* MatchFinder::AddSequence (MatchFinder.cpp:59-87) for a host ASCII genome
  * (copied to HBM).  Genome ids are assigned in call order. */

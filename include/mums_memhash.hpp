@@ -160,4 +160,11 @@ public:
     }
 };
 
+// PairwiseMatchFinder (PairwiseMatchFinder.h:23-33): MemHash hashing every pair of
+// single-copy genomes of a seed group (PairwiseMatchFinder.cpp:37-73).
+class PairwiseMatchFinder : public MemHash {
+public:
+    explicit PairwiseMatchFinder(int device = 0) : MemHash(device) { check(mums_set_pairwise(ctx_, 1)); }
+};
+
 }  // namespace mums

@@ -90,7 +90,7 @@ EXPORTED_SYMBOLS = [
     "mums_shard_merge", "mums_probe_count", "mums_probe_copy", "mums_shard_bucket_counts", "mums_shard_probe_rows",
     "mums_shard_packed_info", "mums_shard_packed_copy", "mums_shard_find", "mums_set_parallel_compat",
     "mums_seed_occurrence", "mums_multiplicity_filter", "mums_length_filter", "mums_write_sml",
-    "mums_add_genome_sml",
+    "mums_add_genome_sml", "mums_set_pairwise",
 ]
 
 _lib: Optional[ctypes.CDLL] = None
@@ -153,6 +153,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mums_length_filter.argtypes = [vp, u64]
     lib.mums_write_sml.argtypes = [vp, u32, ctypes.c_char_p, ctypes.c_char_p]
     lib.mums_add_genome_sml.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(u64)]
+    lib.mums_set_pairwise.argtypes = [vp, i32]
     _lib = lib
     return lib
 
@@ -392,7 +393,16 @@ class ParallelMemHash(MemHash):
         self._check(self._lib.mums_set_parallel_compat(self._ctx, 1, chunk_size))
 
 
+class PairwiseMatchFinder(MemHash):
+    """PairwiseMatchFinder (PairwiseMatchFinder.h:23-33): every pair of genomes that occur
+    once in a seed group is hashed as a two-genome seed (PairwiseMatchFinder.cpp:37-73)."""
+
+    def __init__(self, device: int = 0):
+        super().__init__(device)
+        self._check(self._lib.mums_set_pairwise(self._ctx, 1))
+
+
 __all__ = [
-    "MemHash", "MaskedMemHash", "ParallelMemHash", "MatchList", "MumsError", "GapInSequence", "getSeed", "getSeedLength",
+    "MemHash", "MaskedMemHash", "ParallelMemHash", "PairwiseMatchFinder", "MatchList", "MumsError", "GapInSequence", "getSeed", "getSeedLength",
     "getSeedWeight", "getDefaultSeedWeight", "load_library", "EXPORTED_SYMBOLS", "STAGE_SEEDS", "STAGE_ALL",
 ]

@@ -78,6 +78,7 @@ struct mums_ctx {
     bool use_onesweep = true;
     // ParallelMemHash chunk-compat mode (compat.hip): chunk = CHUNK_SIZE, ParallelMemHash.cpp:51
     bool pcompat = false;
+    bool pairwise = false;   // PairwiseMatchFinder (pairwise.hip)
     uint64_t chunk_size = 200000;
     uint32_t nchunks = 0;
     DevBuf cval, ctab;
@@ -782,6 +783,8 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
     return MUMS_OK;
 }
 
+int run_pipeline_pairwise(mums_ctx* ctx, int stage);   // after sort_row_keys below
+
 int check_ctx(mums_ctx* ctx) {
     if (!ctx) return MUMS_E_INVALID;
     ctx->err.clear();
@@ -953,7 +956,14 @@ int mums_find_stage(mums_ctx* ctx, int stage) {
         ctx->st = mums_stats{};
         return MUMS_OK;
     }
+    if (ctx->pairwise) return run_pipeline_pairwise(ctx, stage);
     return ctx->pcompat ? run_pipeline_compat(ctx, stage) : run_pipeline(ctx, stage);
+}
+
+int mums_set_pairwise(mums_ctx* ctx, int enable) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    ctx->pairwise = enable != 0;
+    return MUMS_OK;
 }
 
 int mums_set_parallel_compat(mums_ctx* ctx, int enable, uint64_t chunk_size) {
@@ -1415,6 +1425,106 @@ int sort_row_keys(mums_ctx* ctx, uint32_t* keys, uint64_t P, int bits, hipStream
     HIPCHK(radix_sort<uint32_t>(keys, nullptr, P, bits, kB, iA, keys, iB, ctx->radix_tmp.p, &out, st));
     ctx->sorted_buckets = out ? keys : kB;
     ctx->sorted_ids = out ? iB : iA;
+    return MUMS_OK;
+}
+
+// PairwiseMatchFinder::FindMatches (PairwiseMatchFinder.cpp:37-73 over MemHash): pair
+// path keys + sort, one probe row per single-copy genome pair of every group
+// (pairwise.hip), then the rows' buckets and the FindMatches tail.
+extern "C++" {
+template <typename K>
+int pairwise_rows(mums_ctx* ctx, uint64_t N, hipStream_t st) {
+    DevCounters* dc = ctx->counters.as<DevCounters>();
+    const PairView<K> v{(const K*)ctx->sorted_key, ctx->sorted_idx};
+    uint32_t* npairs = ctx->cval.as<uint32_t>();
+    uint32_t* off = npairs + N + 64;
+    HIPCHK(launch_pairwise_count<PairView<K>>(v, N, ctx->gt, npairs, dc, st));
+    HIPCHK(hipMemcpyAsync(off, npairs, N * 4, hipMemcpyDeviceToDevice, st));
+    HIPCHK(exclusive_scan_u32(off, N, ctx->tmp.p, &dc->nprobes, st));
+    uint32_t P = 0;
+    HIPCHK(hipMemcpyAsync(&P, &dc->nprobes, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    ctx->P = P;
+    HIPCHK(ctx->mprobe.ensure(((uint64_t)P + 1) * (size_t)(ctx->gt.G + 1) * 8));
+    HIPCHK(launch_pairwise_emit<PairView<K>>(v, N, ctx->gt, ctx->L, npairs, off, ctx->mprobe.as<int64_t>(), st));
+    return MUMS_OK;
+}
+}  // extern "C++"
+
+int run_pipeline_pairwise(mums_ctx* ctx, int stage) {
+    hipStream_t st = ctx->stream;
+    const int G = (int)ctx->genomes.size();
+    const uint64_t N = ctx->N;
+    MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, 0, 0};
+    GenomeTable& gt = ctx->gt;
+    const int kbits = 2 * ctx->w + 1;
+    ctx->packed_path = false;
+    ctx->msd_bits = 0;
+    const size_t kb = ctx->key64 ? 8 : 4;
+    uint64_t words = 0;
+    const uint32_t T = layout_packed(gt, &words);
+    HIPCHK(ctx->packed.ensure(words * 4 + 64));
+    HIPCHK(ctx->counters.ensure(sizeof(DevCounters)));
+    DevCounters* dc = ctx->counters.as<DevCounters>();
+    HIPCHK(ctx->ckey.ensure(N * kb + 64));
+    HIPCHK(ctx->kA.ensure(N * kb + 64));
+    HIPCHK(ctx->kB.ensure(N * kb + 64));
+    HIPCHK(ctx->vA.ensure(N * 4 + 64));
+    HIPCHK(ctx->vB.ensure(N * 4 + 64));
+    HIPCHK(ctx->cval.ensure(2 * (N + 64) * 4));
+    HIPCHK(ctx->tmp.ensure(std::max(std::max(scan_tmp_bytes(N + 1), radix_tmp_bytes(N + 1)),
+                                    scan_tmp_bytes((uint64_t)ctx->table_size))));
+    HIPCHK(hipEventRecord(ctx->ev[EV_START], st));
+    HIPCHK(hipMemsetAsync(dc, 0, sizeof(DevCounters), st));
+    std::vector<const char*> ptrs(G);
+    for (int g = 0; g < G; ++g) ptrs[g] = ctx->genomes[g].d_ptr;
+    HIPCHK(launch_seed_pack(ctx->ss, gt, ptrs.data(), ctx->packed.as<uint32_t>(), 0, ctx->key64, ctx->ckey.p, 0,
+                            nullptr, T, &dc->err, st));
+    HIPCHK(hipEventRecord(ctx->ev[EV_KEYS], st));
+    int buf = 0;
+    if (ctx->key64)
+        HIPCHK(radix_sort<uint64_t>(ctx->ckey.as<uint64_t>(), nullptr, N, kbits, ctx->kA.as<uint64_t>(),
+                                    ctx->vA.as<uint32_t>(), ctx->kB.as<uint64_t>(), ctx->vB.as<uint32_t>(),
+                                    ctx->tmp.p, &buf, st));
+    else
+        HIPCHK(radix_sort<uint32_t>(ctx->ckey.as<uint32_t>(), nullptr, N, kbits, ctx->kA.as<uint32_t>(),
+                                    ctx->vA.as<uint32_t>(), ctx->kB.as<uint32_t>(), ctx->vB.as<uint32_t>(),
+                                    ctx->tmp.p, &buf, st));
+    ctx->sorted_buf = buf;
+    ctx->sorted_key = buf ? ctx->kB.p : ctx->kA.p;
+    ctx->sorted_idx = buf ? ctx->vB.as<uint32_t>() : ctx->vA.as<uint32_t>();
+    ctx->sort_passes = (kbits + 7) / 8;
+    HIPCHK(hipEventRecord(ctx->ev[EV_SORT], st));
+    int rc = ctx->key64 ? pairwise_rows<uint64_t>(ctx, N, st) : pairwise_rows<uint32_t>(ctx, N, st);
+    if (rc) return rc;
+    HIPCHK(hipMemcpy(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost));
+    if (ctx->hc.err & 1u) return fail(ctx, MUMS_E_GAP, "Gap in genome sequence ('-' encountered)");
+    HIPCHK(hipEventRecord(ctx->ev[EV_GROUPS], st));
+    const uint64_t P = ctx->P;
+    if (P >= (1ull << 30)) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^30 seed probes in one FindMatches");
+    ctx->probe_info = nullptr;
+    int tbits = 1;
+    while (tbits < 32 && ((uint64_t)1 << tbits) < (uint64_t)ctx->table_size) ++tbits;
+    if (P) {
+        HIPCHK(ctx->rowtmp.ensure((P + 64) * 16 + 8192));
+        uint32_t* bkt = (uint32_t*)ctx->rowtmp.p;
+        HIPCHK(launch_row_buckets(ctx->mprobe.as<int64_t>(), P, G, ctx->table_size, nullptr, 0, bkt, st));
+        rc = sort_row_keys(ctx, bkt, P, tbits, st);
+        if (rc) return rc;
+    }
+    HIPCHK(hipEventRecord(ctx->ev[EV_BUCKETS], st));
+    ctx->stage_done = MUMS_STAGE_SEEDS;
+    if (stage >= MUMS_STAGE_ALL) {
+        rc = find_tail(ctx, mp, ctx->packed.as<uint32_t>(), [&](MatProbes* v) {
+            v->rows = ctx->mprobe.as<int64_t>();
+            return MUMS_OK;
+        }, st);
+        if (rc) return rc;
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipMemcpy(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost));
+    fill_stats(ctx, N);
+    ctx->st.probes = P;
     return MUMS_OK;
 }
 

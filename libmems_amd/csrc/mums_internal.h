@@ -227,6 +227,14 @@ hipError_t launch_match_filter(const uint64_t* len, const int64_t* s, uint64_t M
                                uint64_t min_len, void* d_tmp, uint32_t* d_kept, uint64_t* len2, int64_t* s2,
                                hipStream_t st);
 
+// pairwise.hip: PairwiseMatchFinder probe rows (PairwiseMatchFinder.cpp:37-73)
+template <typename View>
+hipError_t launch_pairwise_count(View v, uint64_t N, const GenomeTable& gt, uint32_t* npairs, void* ctr,
+                                 hipStream_t st);
+template <typename View>
+hipError_t launch_pairwise_emit(View v, uint64_t N, const GenomeTable& gt, int L, const uint32_t* npairs,
+                                const uint32_t* off, int64_t* rows, hipStream_t st);
+
 // compat.hip: ParallelMemHash chunk-compat mode (ParallelMemHash.cpp:42-121)
 hipError_t launch_genome_keys(uint64_t* ckey, uint64_t N, const GenomeTable& gt, int kbits, hipStream_t st);
 hipError_t launch_compat_breaks(const uint64_t* sk, const GenomeTable& gt, uint64_t kmask, int mx, uint64_t chunk,

@@ -619,6 +619,26 @@ static void enumerate_matches(memhash_t* h, const oracle_params* prm, const idme
     }
 }
 
+/* PairwiseMatchFinder::EnumerateMatches (PairwiseMatchFinder.cpp:37-73): the group   */
+/* sorted by genome id (std::list::sort, stable; grp is genome-major already), the     */
+/* genomes occurring exactly once kept in order, then MemHash::HashMatch of every pair  */
+/* (a before b).  HashMatch always returns true, so the && chain never short-circuits.  */
+static void enumerate_pairwise(memhash_t* h, const oracle_params* prm, const idmer_t* grp, int cnt, idmer_t* uniq,
+                               int64_t* scratch) {
+    int nu = 0;
+    for (int a = 0; a < cnt;) {
+        int b = a + 1;
+        while (b < cnt && grp[b].g == grp[a].g) ++b;
+        if (b - a == 1) uniq[nu++] = grp[a];
+        a = b;
+    }
+    for (int a = 0; a < nu; ++a)
+        for (int b = a + 1; b < nu; ++b) {
+            idmer_t pr[2] = {uniq[a], uniq[b]};
+            hash_match(h, prm, pr, 2, scratch);
+        }
+}
+
 /* MatchFinder::SearchRange (MatchFinder.cpp:172-340): G-way merge of the SMLs  */
 /* restricted to index ranges [lo[g], hi[g]) by masked key; a group = every      */
 /* occurrence of one masked key inside the ranges.  compat != 0 adds the         */
@@ -663,7 +683,12 @@ static void search_range(memhash_t* h, const oracle_params* prm, int G, bmer_t* 
             for (int g = 0; g < G; ++g) more |= idx[g] < hi[g];
             if (more) break;
         }
-        if (cnt > 1) enumerate_matches(h, prm, grp, (int)cnt, hl, h->scratch);
+        if (prm->pairwise) {
+            /* SearchRange skips a group above MER_REPEAT_LIMIT (MatchFinder.cpp:215-239) */
+            if (cnt > 1 && cnt <= MER_REPEAT_LIMIT) enumerate_pairwise(h, prm, grp, (int)cnt, hl, h->scratch);
+        } else if (cnt > 1) {
+            enumerate_matches(h, prm, grp, (int)cnt, hl, h->scratch);
+        }
     }
     free(idx); free(grp); free(hl);
 }

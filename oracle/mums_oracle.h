@@ -58,6 +58,8 @@ typedef struct oracle_params {
                                 *    2: same chunks, one MergeTable at the end   *
                                 *    (checking aid for the GPU's model)          */
     uint64_t chunk_size;       /* its CHUNK_SIZE (0 = 200000, :51)              */
+    int      pairwise;         /* 1: PairwiseMatchFinder::EnumerateMatches      *
+                                *    (PairwiseMatchFinder.cpp:37-73)             */
 } oracle_params;
 
 typedef struct oracle_result oracle_result;

@@ -33,6 +33,7 @@ class _Params(ctypes.Structure):
         ("seeds_only", ctypes.c_int),
         ("parallel_compat", ctypes.c_int),
         ("chunk_size", ctypes.c_uint64),
+        ("pairwise", ctypes.c_int),
     ]
 
 
@@ -123,7 +124,7 @@ def seed_occurrence(seq: bytes, seed: int) -> np.ndarray:
 def find_matches(seqs: Sequence[bytes], seed: int, repeat_tol: int = 0, enum_tol: int = 1,
                  table_size: int = 40000, masked: bool = False, seq_mask: int = 0,
                  gnseqi_end_neg1: bool = False, seeds_only: bool = False, parallel_compat: bool = False,
-                 chunk_size: int = 0) -> Tuple[np.ndarray, np.ndarray, dict]:
+                 chunk_size: int = 0, pairwise: bool = False) -> Tuple[np.ndarray, np.ndarray, dict]:
     """MemHash::FindMatches restated; returns (lengths[M], starts[M,G], counters).
     parallel_compat: ParallelMemHash::FindMatches instead (ParallelMemHash.cpp:42-121),
     chunk_size = its CHUNK_SIZE (0 = 200000)."""
@@ -131,7 +132,7 @@ def find_matches(seqs: Sequence[bytes], seed: int, repeat_tol: int = 0, enum_tol
     arr = (ctypes.c_char_p * G)(*seqs)
     lens = (ctypes.c_uint64 * G)(*[len(s) for s in seqs])
     prm = _Params(seed, repeat_tol, enum_tol, table_size, int(masked), seq_mask, int(gnseqi_end_neg1),
-                  int(seeds_only), int(parallel_compat), chunk_size)
+                  int(seeds_only), int(parallel_compat), chunk_size, int(pairwise))
     L = lib()
     r = L.oracle_find_matches(G, arr, lens, ctypes.byref(prm))
     if not r:

@@ -91,3 +91,15 @@ def test_parallel_compat_deferred_merge_equivalent(oracle_mod, G, n, p, w, chunk
     ta, tb = (oracle_mod.match_text(x[0], x[1]) for x in (a, b))
     assert ta == tb
     assert a[2]["chunks"] > 10
+
+
+@pytest.mark.parametrize("n,p,gseed", [(1000000, 0.01, 12345), (1000000, 1.0, 12345), (300000, 0.05, 3)])
+def test_pairwise_equals_memhash_for_two_genomes(oracle_mod, n, p, gseed):
+    """PairwiseMatchFinder (PairwiseMatchFinder.cpp:37-73) with two genomes hashes exactly the
+    probes MemHash does (both single-copy <=> MemHash's repeat_tol 0 acceptance), so its
+    MatchList equals MemHash's, which is pinned to the reference for the first two cases."""
+    seqs = oracle_mod.generate(2, n, p, gseed)
+    seed = oracle_mod.get_seed(15)
+    a = oracle_mod.find_matches(seqs, seed, pairwise=True)
+    b = oracle_mod.find_matches(seqs, seed)
+    assert (a[0] == b[0]).all() and (a[1] == b[1]).all() and a[2]["probes"] == b[2]["probes"]
