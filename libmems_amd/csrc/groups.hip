@@ -155,7 +155,8 @@ __global__ __launch_bounds__(kBlock) void probe_tile_kernel(View v, const SegTil
 // global load round and one store round.
 typedef __attribute__((address_space(3))) const uint64_t lds_u64;
 
-struct TileRecView {
+template <int IB>
+struct TileRecViewT {
     lds_u64* lds;           // records [t0, t0 + count) of the sorted stream (LDS)
     const uint64_t* glob;   // the whole sorted stream
     uint64_t t0;
@@ -164,16 +165,16 @@ struct TileRecView {
         const uint64_t k = i - t0;
         return k < count ? lds[k] : glob[i];
     }
-    __device__ __forceinline__ uint64_t gkey(uint64_t i) const { return raw(i) >> 33; }
-    __device__ __forceinline__ uint32_t par(uint64_t i) const { return (uint32_t)(raw(i) >> 32) & 1u; }
-    __device__ __forceinline__ uint32_t gidx(uint64_t i) const { return (uint32_t)raw(i); }
+    __device__ __forceinline__ uint64_t gkey(uint64_t i) const { return raw(i) >> (IB + 1); }
+    __device__ __forceinline__ uint32_t par(uint64_t i) const { return (uint32_t)(raw(i) >> IB) & 1u; }
+    __device__ __forceinline__ uint64_t gidx(uint64_t i) const { return raw(i) & ((1ull << IB) - 1); }
     __device__ __forceinline__ RecFields get(uint64_t i) const {
         const uint64_t r = raw(i);
-        return RecFields{r >> 33, (uint32_t)(r >> 32) & 1u, (uint32_t)r};
+        return RecFields{r >> (IB + 1), (uint32_t)(r >> IB) & 1u, r & ((1ull << IB) - 1)};
     }
 };
 
-template <int MG>
+template <int MG, int IB>
 __global__ __launch_bounds__(kBlock) void probe_tile_rec_kernel(const uint64_t* __restrict__ rec,
                                                                 const SegTile* __restrict__ tiles, GenomeTable gt,
                                                                 MatchParams mp, int L,
@@ -228,9 +229,10 @@ __global__ __launch_bounds__(kBlock) void probe_tile_rec_kernel(const uint64_t* 
         const uint32_t q = r * kBlock + threadIdx.x;
         bool keep = false;
         if (q < cnt) {
-            const uint64_t here = srec[q] >> 33;
-            const uint64_t prev = (q == 0) ? ((tile0 == td.bstart) ? ~0ull : (s_prev >> 33)) : (srec[q - 1] >> 33);
-            const uint64_t next = (q + 1 < cnt) ? (srec[q + 1] >> 33) : (s_next >> 33);
+            const uint64_t here = srec[q] >> (IB + 1);
+            const uint64_t prev = (q == 0) ? ((tile0 == td.bstart) ? ~0ull : (s_prev >> (IB + 1)))
+                                           : (srec[q - 1] >> (IB + 1));
+            const uint64_t next = (q + 1 < cnt) ? (srec[q + 1] >> (IB + 1)) : (s_next >> (IB + 1));
             const bool head = (q == 0 && tile0 == td.bstart) || here != prev;
             ngrp += head ? 1u : 0u;
             keep = head && next == here;
@@ -263,7 +265,7 @@ __global__ __launch_bounds__(kBlock) void probe_tile_rec_kernel(const uint64_t* 
     const uint32_t H = s_red[0];
 
     // 3) one probe per lane, compacted in head order into this tile's slots
-    const TileRecView v{(lds_u64*)srec, rec, tile0, cnt};
+    const TileRecViewT<IB> v{(lds_u64*)srec, rec, tile0, cnt};
     const bool fast = mp.repeat_tol == 0 && mp.enum_tol == 1;
     const double inv_t = 1.0 / (double)mp.table_size;
     const uint64_t sb = (uint64_t)blockIdx.x * kSlots;
@@ -292,15 +294,15 @@ __global__ __launch_bounds__(kBlock) void probe_tile_rec_kernel(const uint64_t* 
                     for (int k = 0; k <= MG; ++k)
                         xb[k] = ((uint32_t)k <= (uint32_t)gt.G && h + k < td.bend) ? rec[h + k] : ~0ull;
                 }
-                ok = probe_fast_raw<MG>(xb, gt, mp, L, &off, &gsz);
+                ok = probe_fast_raw<MG, IB>(xb, gt, mp, L, &off, &gsz);
                 if (gsz > (uint32_t)gt.G) {   // oversize group: rejected; count on for the report
                     uint64_t i = h + gsz;
-                    const uint32_t k0 = (uint32_t)(xb[0] >> 33);
+                    const uint32_t k0 = (uint32_t)(xb[0] >> (IB + 1));
                     while (i < td.bend && gsz <= (uint32_t)kRepeatLimit && (uint32_t)v.gkey(i) == k0) { ++gsz; ++i; }
                 }
             } else {
                 Mhe<MG> P;
-                ok = build_probe<MG, TileRecView>(v, h, td.bend, gt, mp, L, P, &gsz);
+                ok = build_probe<MG, TileRecViewT<IB>>(v, h, td.bend, gt, mp, L, P, &gsz);
                 off = P.offset;
             }
             nrep += gsz > (uint32_t)kRepeatLimit;
@@ -438,9 +440,9 @@ hipError_t launch_probe_tiles(View v, const SegTile* tiles, uint64_t ntiles, uin
                               const MatchParams& mp, int L, uint32_t* tile_count, uint64_t* slot_info,
                               uint32_t* slot_bucket, void* counters, hipStream_t st) {
     if (ntiles == 0) return hipSuccess;
-    if constexpr (std::is_same<View, RecView>::value)
-        hipLaunchKernelGGL((probe_tile_rec_kernel<MG>), dim3((unsigned)ntiles), dim3(kBlock), 0, st, v.rec, tiles, gt,
-                           mp, L, tile_count, slot_info, slot_bucket, (DevCounters*)counters);
+    if constexpr (RecIB<View>::value > 0)
+        hipLaunchKernelGGL((probe_tile_rec_kernel<MG, RecIB<View>::value>), dim3((unsigned)ntiles), dim3(kBlock), 0, st, v.rec,
+                           tiles, gt, mp, L, tile_count, slot_info, slot_bucket, (DevCounters*)counters);
     else
         hipLaunchKernelGGL((probe_tile_kernel<MG, View>), dim3((unsigned)ntiles), dim3(kBlock), 0, st, v, tiles, N, gt,
                            mp, L, tile_count, slot_info, slot_bucket, (DevCounters*)counters);
@@ -487,5 +489,14 @@ MUMS_INST_PROBE(4, RecView)
 MUMS_INST_PROBE(8, RecView)
 MUMS_INST_PROBE(16, RecView)
 MUMS_INST_PROBE(32, RecView)
+// chunked mode (> 2^32 seed-mers): 33-bit record indices
+MUMS_INST_MAT(4, RecViewT<33>)
+MUMS_INST_MAT(8, RecViewT<33>)
+MUMS_INST_MAT(16, RecViewT<33>)
+MUMS_INST_MAT(32, RecViewT<33>)
+MUMS_INST_PROBE(4, RecViewT<33>)
+MUMS_INST_PROBE(8, RecViewT<33>)
+MUMS_INST_PROBE(16, RecViewT<33>)
+MUMS_INST_PROBE(32, RecViewT<33>)
 
 }  // namespace mums

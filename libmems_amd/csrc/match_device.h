@@ -6,6 +6,8 @@
 // which is neutral for every function below.
 #pragma once
 
+#include <type_traits>
+
 #include "mums_internal.h"
 #include "seed_device.h"
 
@@ -299,29 +301,34 @@ __device__ __forceinline__ uint32_t bucket_of_fast(int64_t offset, uint32_t tabl
 // results as probe_offset_fast.  gsize_batch = equal-key run length inside the batch
 // (the caller walks on when it exceeds G).  Genome and base of each record come from
 // one unrolled compare/select pass over the (32-bit) genome bases.
-template <int MG>
+template <int MG, int IB = 32>
 __device__ __forceinline__ bool probe_fast_raw(const uint64_t (&x)[MG + 1], const GenomeTable& gt,
                                                const MatchParams& mp, int L, int64_t* offset, uint32_t* gsize) {
     const uint32_t G = (uint32_t)gt.G;
-    const uint32_t k0 = (uint32_t)(x[0] >> 33);
+    const uint32_t k0 = (uint32_t)(x[0] >> (IB + 1));
     uint32_t cnt = 0;
     bool run = true;
     #pragma unroll
     for (int k = 0; k <= MG; ++k) {
-        run = run && ((uint32_t)(x[k] >> 33) == k0) && (x[k] != ~0ull);
+        run = run && ((uint32_t)(x[k] >> (IB + 1)) == k0) && (x[k] != ~0ull);
         cnt += run ? 1u : 0u;
     }
     *gsize = cnt;
-    uint32_t mask = 0, gref = 64, sref = 0, pref = 0;
+    uint32_t mask = 0, gref = 64, pref = 0;
+    // 32-bit starts and bases for 32-bit record indices; 64-bit in the chunked mode
+    using IdxT = typename std::conditional<(IB > 32), uint64_t, uint32_t>::type;
+    IdxT sref = 0;
     bool dup = false;
-    uint32_t gk[MG + 1], sk[MG + 1];
+    uint32_t gk[MG + 1];
+    IdxT sk[MG + 1];
     #pragma unroll
     for (int k = 0; k <= MG; ++k) {
-        const uint32_t idx = (uint32_t)x[k];
-        uint32_t g = 0, b = 0;
+        const IdxT idx = (IdxT)(x[k] & ((1ull << IB) - 1));
+        uint32_t g = 0;
+        IdxT b = 0;
         #pragma unroll
         for (int j = 1; j < MG; ++j) {
-            const uint32_t bj = (uint32_t)gt.base[j];
+            const IdxT bj = (IdxT)gt.base[j];
             const bool ge = (uint32_t)j < G && idx >= bj;
             g = ge ? (uint32_t)j : g;
             b = ge ? bj : b;
@@ -334,14 +341,14 @@ __device__ __forceinline__ bool probe_fast_raw(const uint64_t (&x)[MG + 1], cons
         const bool better = in && g < gref;
         gref = better ? g : gref;
         sref = better ? sk[k] : sref;
-        pref = better ? (uint32_t)(x[k] >> 32) & 1u : pref;
+        pref = better ? (uint32_t)(x[k] >> IB) & 1u : pref;
     }
     int64_t off = 0;
     #pragma unroll
     for (int k = 0; k <= MG; ++k) {
         const bool use = (uint32_t)k < cnt && gk[k] != gref;
         const int64_t sv = (int64_t)sk[k], sr = (int64_t)sref;
-        const int64_t term = (((uint32_t)(x[k] >> 32) & 1u) != pref) ? (-sv - sr - (int64_t)L) : (sv - sr);
+        const int64_t term = (((uint32_t)(x[k] >> IB) & 1u) != pref) ? (-sv - sr - (int64_t)L) : (sv - sr);
         off += use ? term : 0;
     }
     *offset = off;

@@ -84,6 +84,7 @@ struct mums_ctx {
     DevBuf cval, ctab;
     // one genome's SML / seed frequencies (sml_tools.hip) and filtered MatchLists
     DevBuf smlk0, smlkA, smlkB, smlvA, smlvB, smltmp, flen, fs;
+    DevBuf rowsall;          // chunked mode: probe rows of all chunks
     hipEvent_t ev[EV_COUNT] = {};
     bool profiling = false;
     hipEvent_t ev_ds[16] = {};   // 2 per radix pass (<= 8 passes)
@@ -646,8 +647,8 @@ int prepare_run(mums_ctx* ctx, const std::vector<uint64_t>& lens) {
     }
     gt.base[G] = N;
     for (int g = G + 1; g <= kMaxG; ++g) gt.base[g] = N;
-    if (N >= 0xFFFFFFF0ull)
-        return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed-mers per context (chunked mode not implemented)");
+    if (N >= (1ull << 33))
+        return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^33 seed-mers per context");
     ctx->N = N;
     ctx->ss = make_seed_spec(pat, L, w);
     return MUMS_OK;
@@ -784,6 +785,7 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
 }
 
 int run_pipeline_pairwise(mums_ctx* ctx, int stage);   // after sort_row_keys below
+int run_pipeline_chunked(mums_ctx* ctx, int stage);
 
 int check_ctx(mums_ctx* ctx) {
     if (!ctx) return MUMS_E_INVALID;
@@ -863,7 +865,7 @@ int mums_ctx_destroy(mums_ctx* ctx) {
                       &ctx->pbuf, &ctx->keybuf, &ctx->mstart, &ctx->chain_tmp, &ctx->chain_of,
                       &ctx->radix_tmp, &ctx->spill, &ctx->summ, &ctx->dbgbuf, &ctx->mprobe, &ctx->rowtmp,
                       &ctx->cval, &ctx->ctab, &ctx->smlk0, &ctx->smlkA, &ctx->smlkB, &ctx->smlvA,
-                      &ctx->smlvB, &ctx->smltmp, &ctx->flen, &ctx->fs};
+                      &ctx->smlvB, &ctx->smltmp, &ctx->flen, &ctx->fs, &ctx->rowsall};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i < EV_COUNT; ++i)
         if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
@@ -956,8 +958,12 @@ int mums_find_stage(mums_ctx* ctx, int stage) {
         ctx->st = mums_stats{};
         return MUMS_OK;
     }
+    const bool big = ctx->N >= 0xFFFFFFF0ull || getenv("MUMS_DEV_CHUNK_RECORDS") != nullptr;
+    if (big && (ctx->pairwise || ctx->pcompat))
+        return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed-mers: only MemHash / MaskedMemHash");
     if (ctx->pairwise) return run_pipeline_pairwise(ctx, stage);
-    return ctx->pcompat ? run_pipeline_compat(ctx, stage) : run_pipeline(ctx, stage);
+    if (ctx->pcompat) return run_pipeline_compat(ctx, stage);
+    return big ? run_pipeline_chunked(ctx, stage) : run_pipeline(ctx, stage);
 }
 
 int mums_set_pairwise(mums_ctx* ctx, int enable) {
@@ -1525,6 +1531,215 @@ int run_pipeline_pairwise(mums_ctx* ctx, int stage) {
     HIPCHK(hipMemcpy(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost));
     fill_stats(ctx, N);
     ctx->st.probes = P;
+    return MUMS_OK;
+}
+
+// > 2^32 seed-mers per context (BASELINE config 5, chunked.hip): records with 33-bit
+// global indices; the 2w+1-31 MSD digits are cut into power-of-two chunks of < 2^30
+// records and every chunk runs scatter -> onesweep -> groups -> probe buckets [-> rows]
+// on its own, in key order; the FindMatches tail then replays all chunks' rows.
+int run_pipeline_chunked(mums_ctx* ctx, int stage) {
+    hipStream_t st = ctx->stream;
+    const int G = (int)ctx->genomes.size();
+    const uint64_t N = ctx->N;
+    MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, ctx->masked, ctx->seq_mask};
+    GenomeTable& gt = ctx->gt;
+    const int kbits = 2 * ctx->w + 1;
+    const int B = kbits - 31;   // MSD digit bits: the record keeps 31 key bits + 33 index bits
+    if (B < 1 || B > 8)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed-mers (chunked mode) needs seed weight 16-19");
+    if (N >= (1ull << 33)) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^33 seed-mers per context");
+    ctx->packed_path = true;
+    ctx->key64 = true;
+    ctx->msd_bits = B;
+    uint64_t words = 0;
+    const uint32_t T = layout_packed(gt, &words);
+    HIPCHK(ctx->packed.ensure(words * 4 + 64));
+    HIPCHK(ctx->counters.ensure(sizeof(DevCounters)));
+    HIPCHK(ctx->hist.ensure(((uint64_t)T << B) * 4 + 64));
+    HIPCHK(ctx->ctab.ensure((1u << B) * 8 + 64));
+    DevCounters* dc = ctx->counters.as<DevCounters>();
+    const bool prof = ctx->profiling;
+    if (prof && !ctx->ev_ds[0])
+        for (int i = 0; i < 16; ++i) HIPCHK(hipEventCreate(&ctx->ev_ds[i]));
+    HIPCHK(hipEventRecord(ctx->ev[EV_START], st));
+    HIPCHK(hipMemsetAsync(dc, 0, sizeof(DevCounters), st));
+    std::vector<const char*> ptrs(G);
+    for (int g = 0; g < G; ++g) ptrs[g] = ctx->genomes[g].d_ptr;
+    uint32_t* hist = ctx->hist.as<uint32_t>();
+    HIPCHK(launch_seed_pack(ctx->ss, gt, ptrs.data(), ctx->packed.as<uint32_t>(), 1, true, nullptr, B, hist, T,
+                            &dc->err, st));
+    HIPCHK(hipEventRecord(ctx->ev[EV_KEYS], st));
+    const uint32_t nd = 1u << B;
+    HIPCHK(launch_digit_totals(hist, nd, T, ctx->ctab.as<unsigned long long>(), st));
+    std::vector<unsigned long long> tot(nd);
+    HIPCHK(hipMemcpyAsync(tot.data(), ctx->ctab.p, nd * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (ctx->hc.err & 1u) return fail(ctx, MUMS_E_GAP, "Gap in genome sequence ('-' encountered)");
+    // chunk bits: the fewest power-of-two digit groups each holding < cap records
+    uint64_t cap = (1ull << 30) - 4096;
+    if (const char* e = getenv("MUMS_DEV_CHUNK_RECORDS")) cap = std::min<uint64_t>(cap, strtoull(e, nullptr, 10));
+    int cb = 0;
+    for (; cb <= B; ++cb) {
+        const uint32_t per = 1u << (B - cb);
+        bool ok = true;
+        for (uint32_t d0 = 0; d0 < nd && ok; d0 += per) {
+            uint64_t sum = 0;
+            for (uint32_t d = d0; d < d0 + per; ++d) sum += tot[d];
+            ok = sum < cap;
+        }
+        if (ok) break;
+    }
+    if (cb > B) return fail(ctx, MUMS_E_UNSUPPORTED, "chunked mode: one MSD digit holds more seed-mers than a chunk (2^30)");
+    const int mb = B - cb;
+    const uint32_t nbc = 1u << mb, nch = 1u << cb;
+    uint64_t nmax = 0;
+    for (uint32_t c = 0; c < nch; ++c) {
+        uint64_t sum = 0;
+        for (uint32_t d = c * nbc; d < (c + 1) * nbc; ++d) sum += tot[d];
+        nmax = std::max(nmax, sum);
+    }
+    ProbeSpace ps{};
+    int rc = ensure_merge_space(ctx, nmax + 1, mb, 31, &ps);
+    if (rc) return rc;
+    HIPCHK(ctx->tmp.ensure(std::max(ctx->tmp.cap, scan_tmp_bytes((uint64_t)nbc * T + 1))));
+    // resident layout (the 288 GB of HBM hold all 2 x N records): every chunk's slice of
+    // the MSD histogram scanned on its own, ONE scatter of all records to their chunk
+    // (64-bit chunk bases), then each chunk sorted / grouped in place.  Otherwise (or
+    // with MUMS_DEV_CHUNK_STREAM set) the scatter runs once per chunk into a chunk-sized
+    // buffer, recomputing the keys every time.
+    std::vector<uint64_t> cbase(nch + 1, 0);
+    for (uint32_t c = 0; c < nch; ++c) {
+        uint64_t sum = 0;
+        for (uint32_t d = c * nbc; d < (c + 1) * nbc; ++d) sum += tot[d];
+        cbase[c + 1] = cbase[c] + sum;
+    }
+    bool resident = getenv("MUMS_DEV_CHUNK_STREAM") == nullptr;
+    if (resident) {
+        size_t fr = 0, total_mem = 0;
+        HIPCHK(hipMemGetInfo(&fr, &total_mem));
+        const uint64_t need = 2 * (N + 64) * 8;
+        resident = need + (uint64_t)(1ull << 30) < (uint64_t)fr + ctx->recA.cap + ctx->recB.cap;
+    }
+    if (resident) {
+        HIPCHK(ctx->recA.ensure((N + 64) * 8));
+        HIPCHK(ctx->recB.ensure((N + 64) * 8));
+        HIPCHK(ctx->ctab.ensure((nd + nch + 8) * 8 + 64));
+        uint64_t* d_cbase = ctx->ctab.as<uint64_t>() + nd;
+        HIPCHK(hipMemcpyAsync(d_cbase, cbase.data(), nch * 8, hipMemcpyHostToDevice, st));
+        for (uint32_t c = 0; c < nch; ++c)
+            HIPCHK(exclusive_scan_u32(hist + (uint64_t)c * nbc * T, (uint64_t)nbc * T, ctx->tmp.p, nullptr, st));
+        HIPCHK(launch_seed_scatter_chunk(ctx->ss, gt, ctx->packed.as<uint32_t>(), B, hist, T, 0, 0,
+                                         ctx->recA.as<uint64_t>(), st, d_cbase, mb));
+    }
+    uint64_t P_total = 0, groups = 0;
+    double ms_sort = 0, ms_groups = 0, ms_buckets = 0, ms_dom = 0;
+    uint64_t dom_bytes = 0, dom_launches = 0;
+    auto el = [&](int a, int b) {
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, ctx->ev[a], ctx->ev[b]);
+        return (double)ms;
+    };
+    const int npass = (31 + 7) / 8;
+    for (uint32_t c = 0; c < nch; ++c) {
+        const uint32_t dlo = c * nbc;
+        uint64_t n_c = 0;
+        for (uint32_t d = dlo; d < dlo + nbc; ++d) n_c += tot[d];
+        if (n_c == 0) continue;
+        uint32_t* slice = hist + (uint64_t)dlo * T;
+        const uint64_t o = resident ? cbase[c] : 0;
+        uint64_t* rA = ctx->recA.as<uint64_t>() + o;
+        uint64_t* rB = ctx->recB.as<uint64_t>() + o;
+        HIPCHK(hipEventRecord(ctx->ev[EV_CHAINS], st));   // chunk start (scatter counts as sort)
+        if (!resident) {
+            HIPCHK(exclusive_scan_u32(slice, (uint64_t)nbc * T, ctx->tmp.p, nullptr, st));
+            HIPCHK(launch_seed_scatter_chunk(ctx->ss, gt, ctx->packed.as<uint32_t>(), B, slice, T, dlo, nbc, rA, st));
+        }
+        uint32_t* bstart = ctx->mstart.as<uint32_t>();
+        HIPCHK(seg_bucket_starts(mb > 0 ? slice : nullptr, T, mb, n_c, bstart, st));
+        SegTile* tiles = ctx->tiles.as<SegTile>();
+        const uint64_t ub = seg_tiles_upper(n_c, mb);
+        HIPCHK(build_seg_tiles_from_starts(bstart, mb, n_c, tiles, &dc->ntiles, ctx->tmp.p, st));
+        int buf = 0;
+        HIPCHK(seg_onesweep_sort(rA, rB, n_c, 31, mb, bstart, ctx->tmp.p, &dc->err, &buf, st,
+                                 prof ? ctx->ev_ds : nullptr, 33));
+        ctx->sorted_buf = buf;
+        ctx->sorted_rec = buf ? rB : rA;
+        HIPCHK(hipEventRecord(ctx->ev[EV_SORT], st));
+        rc = groups_dispatch<RecViewT<33>>(ctx, RecViewT<33>{ctx->sorted_rec}, tiles, ub, mp, ps.probe_info,
+                                           ps.probe_bucket, ps.slot_info, ps.slot_bucket, st);
+        if (rc) return rc;
+        rc = finish_seeds(ctx, ps, st);
+        if (rc) return rc;
+        HIPCHK(hipEventSynchronize(ctx->ev[EV_BUCKETS]));
+        ms_sort += el(EV_CHAINS, EV_SORT);
+        ms_groups += el(EV_SORT, EV_GROUPS);
+        ms_buckets += el(EV_GROUPS, EV_BUCKETS);
+        if (prof)
+            for (int p = 0; p < npass; ++p) {
+                float ms = 0.f;
+                (void)hipEventElapsedTime(&ms, ctx->ev_ds[2 * p], ctx->ev_ds[2 * p + 1]);
+                ms_dom += ms;
+            }
+        dom_bytes += n_c * 16 * (uint64_t)npass;
+        dom_launches += (uint64_t)npass;
+        groups += ctx->hc.ngroups;
+        const uint64_t Pc = ctx->P;
+        if (stage >= MUMS_STAGE_ALL && Pc) {
+            if (P_total + Pc >= (1ull << 30))
+                return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^30 seed probes in one FindMatches");
+            rc = materialize_dispatch<RecViewT<33>>(ctx, RecViewT<33>{ctx->sorted_rec}, mp, st);
+            if (rc) return rc;
+            const size_t W = (size_t)(G + 1) * 8;
+            if (ctx->rowsall.cap < (P_total + Pc + 1) * W) {   // grow, keeping the rows so far
+                DevBuf nb;
+                HIPCHK(nb.ensure((P_total + Pc + 1) * W * 2));
+                if (P_total) HIPCHK(hipMemcpyAsync(nb.p, ctx->rowsall.p, P_total * W, hipMemcpyDeviceToDevice, st));
+                HIPCHK(hipStreamSynchronize(st));
+                ctx->rowsall.release();
+                ctx->rowsall = nb;
+            }
+            HIPCHK(hipMemcpyAsync((char*)ctx->rowsall.p + P_total * W, ctx->mprobe.p, Pc * W,
+                                  hipMemcpyDeviceToDevice, st));
+        }
+        P_total += Pc;
+    }
+    ctx->P = P_total;
+    ctx->stage_done = MUMS_STAGE_SEEDS;
+    if (stage >= MUMS_STAGE_ALL) {
+        int tbits = 1;
+        while (tbits < 32 && ((uint64_t)1 << tbits) < (uint64_t)ctx->table_size) ++tbits;
+        ctx->probe_info = nullptr;
+        if (P_total) {
+            HIPCHK(ctx->rowtmp.ensure((P_total + 64) * 16 + 8192));
+            uint32_t* bkt = (uint32_t*)ctx->rowtmp.p;
+            HIPCHK(launch_row_buckets(ctx->rowsall.as<int64_t>(), P_total, G, ctx->table_size, nullptr, 0, bkt, st));
+            rc = sort_row_keys(ctx, bkt, P_total, tbits, st);
+            if (rc) return rc;
+        }
+        HIPCHK(hipEventRecord(ctx->ev[EV_BUCKETS], st));
+        rc = find_tail(ctx, mp, ctx->packed.as<uint32_t>(), [&](MatProbes* v) {
+            v->rows = ctx->rowsall.as<int64_t>();
+            return MUMS_OK;
+        }, st);
+        if (rc) return rc;
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipMemcpy(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost));
+    fill_stats(ctx, N);
+    mums_stats& s = ctx->st;
+    s.probes = P_total;
+    s.groups = groups;
+    s.ms_sort = ms_sort;
+    s.ms_groups = ms_groups;
+    s.ms_buckets = ms_buckets;
+    s.chunks = nch;
+    s.sort_passes = (uint64_t)npass;
+    s.key_bytes = 8;
+    s.ms_dominant = prof ? ms_dom : 0.0;
+    s.dominant_bytes = prof ? dom_bytes : 0;
+    s.dominant_launches = prof ? dom_launches : 0;
     return MUMS_OK;
 }
 

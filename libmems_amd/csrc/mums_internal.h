@@ -136,6 +136,11 @@ hipError_t launch_seed_pack(const SeedSpec& ss, const GenomeTable& gt, const cha
 // packed path: scatter records into MSD buckets (offsets = scanned hist)
 hipError_t launch_seed_scatter(const SeedSpec& ss, const GenomeTable& gt, const uint32_t* d_packed, int msd_bits,
                                const uint32_t* d_hist_scanned, uint32_t ntiles, uint64_t* d_rec, hipStream_t st);
+// chunked mode (> 2^32 seed-mers), 33-bit record indices: only MSD digits [dlo, dlo + nbc)
+// (d_cbase null), or every digit d at d_cbase[d >> mb] + its offset inside its chunk
+hipError_t launch_seed_scatter_chunk(const SeedSpec& ss, const GenomeTable& gt, const uint32_t* d_packed, int msd_bits,
+                                     const uint32_t* d_hist_slice, uint32_t ntiles, uint32_t dlo, uint32_t nbc,
+                                     uint64_t* d_rec, hipStream_t st, const uint64_t* d_cbase = nullptr, int mb = 0);
 // key of every position of one genome: ref_form = GetDnaSeedMer's left-aligned 64-bit mer
 // (mums_copy_seed_keys), else the 2w+1-bit ckey (same order; one genome's SML sort)
 hipError_t launch_keys_of_genome(const SeedSpec& ss, const uint32_t* d_words, uint64_t m, uint64_t* d_out,
@@ -173,9 +178,10 @@ hipError_t seg_radix_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key_bi
 // onesweep variant (n < 2^30): one histogram read for all passes, then one launch per
 // pass with decoupled look-back between consecutive tiles of a bucket.
 size_t onesweep_tmp_bytes(uint64_t n, int msd_bits, int key_bits);
+// key_shift: first key bit of the records (32; 33 in the chunked mode)
 hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key_bits, int msd_bits,
                              const uint32_t* d_bstart, void* d_tmp, uint32_t* d_err, int* out_buf, hipStream_t st,
-                             hipEvent_t* ev_ds = nullptr);
+                             hipEvent_t* ev_ds = nullptr, int key_shift = 32);
 
 // groups.hip
 uint64_t group_slot_count(uint64_t ntiles);
@@ -234,6 +240,10 @@ hipError_t launch_pairwise_count(View v, uint64_t N, const GenomeTable& gt, uint
 template <typename View>
 hipError_t launch_pairwise_emit(View v, uint64_t N, const GenomeTable& gt, int L, const uint32_t* npairs,
                                 const uint32_t* off, int64_t* rows, hipStream_t st);
+
+// chunked.hip: records per MSD digit (chunked mode, > 2^32 seed-mers)
+hipError_t launch_digit_totals(const uint32_t* hist, uint32_t ndigits, uint32_t T, unsigned long long* out,
+                               hipStream_t st);
 
 // compat.hip: ParallelMemHash chunk-compat mode (ParallelMemHash.cpp:42-121)
 hipError_t launch_genome_keys(uint64_t* ckey, uint64_t N, const GenomeTable& gt, int kbits, hipStream_t st);

@@ -256,7 +256,7 @@ constexpr int kGhistTilesPerBlock = 16;
 
 __global__ __launch_bounds__(kBlock) void seg_ghist_kernel(const uint64_t* __restrict__ rec,
                                                            const SegTile* __restrict__ tiles, uint64_t ntiles_ub,
-                                                           int npass, uint32_t* __restrict__ ghist) {
+                                                           int npass, uint32_t* __restrict__ ghist, int key_shift) {
     __shared__ uint32_t h[4][kDigits];
     const int tid = threadIdx.x;
     const uint64_t t0 = (uint64_t)blockIdx.x * kGhistTilesPerBlock;
@@ -281,7 +281,7 @@ __global__ __launch_bounds__(kBlock) void seg_ghist_kernel(const uint64_t* __res
             cur_b = d.bucket;
         }
         for (uint32_t q = tid; q < d.count; q += kBlock) {
-            const uint64_t key = rec[d.start + q] >> 32;
+            const uint64_t key = rec[d.start + q] >> key_shift;
             for (int p = 0; p < npass; ++p) atomicAdd(&h[p][(uint32_t)(key >> (8 * p)) & 0xFFu], 1u);
         }
     }
@@ -766,7 +766,7 @@ size_t onesweep_tmp_bytes(uint64_t n, int msd_bits, int key_bits) {
 
 hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key_bits, int msd_bits,
                              const uint32_t* d_bstart, void* d_tmp, uint32_t* d_err, int* out_buf, hipStream_t st,
-                             hipEvent_t* ev_ds) {
+                             hipEvent_t* ev_ds, int key_shift) {
     const int npass = (key_bits + 7) / 8;
     *out_buf = npass % 2;
     if (n == 0 || npass == 0) return hipSuccess;
@@ -785,7 +785,8 @@ hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key
     e = build_seg_tiles_from_starts(d_bstart, msd_bits, n, stiles, counters + 32, btmp, st, kSortTile);
     if (e != hipSuccess) return e;
     const unsigned gblocks = (unsigned)((ub + kGhistTilesPerBlock - 1) / kGhistTilesPerBlock);
-    hipLaunchKernelGGL(seg_ghist_kernel, dim3(gblocks), dim3(kBlock), 0, st, recA, stiles, ub, npass, ghist);
+    hipLaunchKernelGGL(seg_ghist_kernel, dim3(gblocks), dim3(kBlock), 0, st, recA, stiles, ub, npass, ghist,
+                       key_shift);
     hipLaunchKernelGGL(seg_dbase_kernel, dim3((unsigned)(nb * npass)), dim3(kBlock), 0, st, ghist, d_bstart, npass,
                        dbase);
 #if MUMS_SORT_PERSIST
@@ -807,12 +808,12 @@ hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key
 #if MUMS_SORT_PERSIST
         hipLaunchKernelGGL((seg_onesweep_persist_kernel<kSortBlock, kSortTile / kSortBlock>),
                            dim3((unsigned)std::min<uint64_t>(ub, persist_grid)), dim3(kSortBlock), 0, st, src, dst,
-                           stiles, (uint32_t)ub, 32 + 8 * p, p, npass, dbase, status + (uint64_t)p * ub * kDigits,
-                           counters + p, d_err);
+                           stiles, (uint32_t)ub, key_shift + 8 * p, p, npass, dbase,
+                           status + (uint64_t)p * ub * kDigits, counters + p, d_err);
 #else
         hipLaunchKernelGGL((seg_onesweep_kernel<kSortBlock, kSortTile / kSortBlock>), dim3((unsigned)ub),
-                           dim3(kSortBlock), 0, st, src, dst, stiles, (uint32_t)ub, 32 + 8 * p, p, npass, dbase,
-                           status + (uint64_t)p * ub * kDigits, counters + p, d_err);
+                           dim3(kSortBlock), 0, st, src, dst, stiles, (uint32_t)ub, key_shift + 8 * p, p, npass,
+                           dbase, status + (uint64_t)p * ub * kDigits, counters + p, d_err);
 #endif
         e = hipGetLastError();
         if (e != hipSuccess) return e;

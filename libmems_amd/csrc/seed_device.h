@@ -111,7 +111,7 @@ __device__ __forceinline__ uint64_t ckey_at(const uint32_t* __restrict__ W, uint
 struct RecFields {
     uint64_t gk;    // group key (masked ckey)
     uint32_t par;   // strand parity
-    uint32_t idx;   // global seed-mer index
+    uint64_t idx;   // global seed-mer index
 };
 
 // PairView: (ckey, global index) pairs (generic path, any weight).
@@ -121,24 +121,34 @@ struct PairView {
     const uint32_t* idx;
     __device__ __forceinline__ uint64_t gkey(uint64_t i) const { return (uint64_t)key[i] >> 1; }
     __device__ __forceinline__ uint32_t par(uint64_t i) const { return (uint32_t)(key[i] & 1); }
-    __device__ __forceinline__ uint32_t gidx(uint64_t i) const { return idx[i]; }
+    __device__ __forceinline__ uint64_t gidx(uint64_t i) const { return idx[i]; }
     __device__ __forceinline__ RecFields get(uint64_t i) const {
         const uint64_t k = (uint64_t)key[i];
         return RecFields{k >> 1, (uint32_t)(k & 1), idx[i]};
     }
 };
 
-// RecView: packed records (ckey_low << 32 | global index); the top ckey bits are the
-// MSD bucket the record sits in, so groups never cross a bucket boundary.
-struct RecView {
+// RecView: packed records (ckey_low << IB | global index), IB index bits (32; 33 in the
+// chunked mode for > 2^32 seed-mers); the top ckey bits are the MSD bucket the record
+// sits in, so groups never cross a bucket boundary.
+template <int IB = 32>
+struct RecViewT {
+    static constexpr int kIB = IB;
     const uint64_t* rec;
-    __device__ __forceinline__ uint64_t gkey(uint64_t i) const { return rec[i] >> 33; }
-    __device__ __forceinline__ uint32_t par(uint64_t i) const { return (uint32_t)(rec[i] >> 32) & 1u; }
-    __device__ __forceinline__ uint32_t gidx(uint64_t i) const { return (uint32_t)rec[i]; }
+    __device__ __forceinline__ uint64_t gkey(uint64_t i) const { return rec[i] >> (IB + 1); }
+    __device__ __forceinline__ uint32_t par(uint64_t i) const { return (uint32_t)(rec[i] >> IB) & 1u; }
+    __device__ __forceinline__ uint64_t gidx(uint64_t i) const { return rec[i] & ((1ull << IB) - 1); }
     __device__ __forceinline__ RecFields get(uint64_t i) const {
         const uint64_t r = rec[i];
-        return RecFields{r >> 33, (uint32_t)(r >> 32) & 1u, (uint32_t)r};
+        return RecFields{r >> (IB + 1), (uint32_t)(r >> IB) & 1u, r & ((1ull << IB) - 1)};
     }
 };
+using RecView = RecViewT<32>;
+
+// index bits of a packed-record view (0 for the pair views)
+template <class V>
+struct RecIB { static constexpr int value = 0; };
+template <int IB>
+struct RecIB<RecViewT<IB>> { static constexpr int value = IB; };
 
 }  // namespace mums

@@ -135,11 +135,18 @@ __global__ __launch_bounds__(kBlock) void seed_pack_kernel(SeedSpec ss, GenomeTa
     }
 }
 
-template <int kMaxDig, uint64_t PAT = 0>
+// Chunked mode (IB-bit record indices): kChunk keeps only the records whose MSD digit
+// lies in [dlo, dlo + nbc) (hist = that digit range's scanned slice); with cbase != null
+// every record is kept and lands at cbase[digit >> cbits_low] + its offset inside its
+// chunk (hist = all slices, each scanned on its own: 32-bit offsets inside a chunk).
+template <int kMaxDig, uint64_t PAT = 0, int IB = 32, bool kChunk = false>
 __global__ __launch_bounds__(kBlock) void seed_scatter_kernel(SeedSpec ss, GenomeTable gt,
                                                               const uint32_t* __restrict__ packed, int msd_bits,
                                                               const uint32_t* __restrict__ hist, uint32_t T,
-                                                              uint64_t* __restrict__ rec) {
+                                                              uint64_t* __restrict__ rec, uint32_t dlo = 0,
+                                                              uint32_t nbc = 0,
+                                                              const uint64_t* __restrict__ cbase = nullptr,
+                                                              int mb = 0) {
     __shared__ uint32_t words[kTileWords];
     __shared__ uint64_t srec[kTile];
     __shared__ uint16_t sdig[kTile];
@@ -147,6 +154,7 @@ __global__ __launch_bounds__(kBlock) void seed_scatter_kernel(SeedSpec ss, Genom
     __shared__ uint32_t lstart[kMaxDig];
     __shared__ uint32_t gofs[kMaxDig];
     __shared__ uint32_t s_w[kWaves];
+    __shared__ uint32_t s_kept;
     const uint32_t t = blockIdx.x;
     const int g = tile_genome(gt, t);
     const uint32_t x = t - gt.tfirst[g];
@@ -154,7 +162,9 @@ __global__ __launch_bounds__(kBlock) void seed_scatter_kernel(SeedSpec ss, Genom
     const uint64_t p0 = (uint64_t)x * kTile;
     if (p0 >= m) return;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int nd = 1 << msd_bits;
+    const bool all_chunks = kChunk && cbase != nullptr;
+    const int nd = (kChunk && !all_chunks) ? (int)nbc : (1 << msd_bits);
+    if (kChunk && tid == 0) s_kept = 0;
     const int klow = 2 * ss.w + 1 - msd_bits;
     const uint64_t lmask = (klow >= 64) ? ~0ull : ((1ull << klow) - 1);
     const uint64_t pw = packed_words(gt.n[g]);
@@ -174,13 +184,18 @@ __global__ __launch_bounds__(kBlock) void seed_scatter_kernel(SeedSpec ss, Genom
     for (int r = 0; r < kPerThread; ++r) {
         const int q = q0 + r * 64 + lane;
         const uint64_t p = p0 + (uint64_t)q;
-        const bool valid = p < m;
+        bool valid = p < m;
         const int wi = q >> 4, sh = 2 * (q & 15);
         const uint64_t hi = ((uint64_t)words[wi] << 32) | words[wi + 1];
         const uint64_t lo = words[wi + 2];
         const uint64_t kv = ckey_of<PAT>((hi << sh) | ((lo << sh) >> 32), ss);
-        const uint32_t d = valid ? (uint32_t)(kv >> klow) : 0u;
-        r_rec[r] = ((kv & lmask) << 32) | (base + p);
+        uint32_t d = valid ? (uint32_t)(kv >> klow) : 0u;
+        if (kChunk && !all_chunks) {
+            d -= dlo;
+            valid = valid && d < nbc;
+            d = valid ? d : 0u;
+        }
+        r_rec[r] = ((kv & lmask) << IB) | (base + p);
         r_dig[r] = d;
         uint32_t tot;
         // digits are < 2^msd_bits <= kMaxDig: the unused high bits rank as equal
@@ -188,7 +203,7 @@ __global__ __launch_bounds__(kBlock) void seed_scatter_kernel(SeedSpec ss, Genom
         uint32_t old = 0;
         if (valid) old = wcnt[wv][d];
         if (valid && rk == 0) wcnt[wv][d] = old + tot;
-        r_rank[r] = old + rk;
+        r_rank[r] = valid ? old + rk : 0xFFFFFFFFu;   // invalid: not stored
     }
     __syncthreads();
     // per-digit wave offsets, block-local digit starts (each thread owns nd/256 digits)
@@ -205,6 +220,7 @@ __global__ __launch_bounds__(kBlock) void seed_scatter_kernel(SeedSpec ss, Genom
             tot_mine += acc;
             gofs[d] = hist[(uint64_t)d * T + t];
         }
+        if (kChunk && tot_mine) atomicAdd(&s_kept, tot_mine);
         uint32_t v = tot_mine;
         #pragma unroll
         for (int dd = 1; dd < 64; dd <<= 1) {
@@ -228,7 +244,7 @@ __global__ __launch_bounds__(kBlock) void seed_scatter_kernel(SeedSpec ss, Genom
     #pragma unroll
     for (int r = 0; r < kPerThread; ++r) {
         const uint64_t p = p0 + (uint64_t)(q0 + r * 64 + lane);
-        if (p < m) {
+        if (p < m && (!kChunk || r_rank[r] != 0xFFFFFFFFu)) {
             const uint32_t d = r_dig[r];
             const uint32_t lp = lstart[d] + wcnt[wv][d] + r_rank[r];
             srec[lp] = r_rec[r];
@@ -236,13 +252,14 @@ __global__ __launch_bounds__(kBlock) void seed_scatter_kernel(SeedSpec ss, Genom
         }
     }
     __syncthreads();
-    const uint64_t cnt = (m - p0) < (uint64_t)kTile ? (m - p0) : (uint64_t)kTile;
+    const uint64_t cnt = kChunk ? (uint64_t)s_kept : ((m - p0) < (uint64_t)kTile ? (m - p0) : (uint64_t)kTile);
     #pragma unroll
     for (int r = 0; r < kPerThread; ++r) {
         const uint32_t s = tid + r * kBlock;
         if (s < cnt) {
             const uint32_t d = sdig[s];
-            rec[(uint64_t)gofs[d] + (s - lstart[d])] = srec[s];
+            const uint64_t b = (kChunk && all_chunks) ? cbase[d >> mb] : 0ull;
+            rec[b + (uint64_t)gofs[d] + (s - lstart[d])] = srec[s];
         }
     }
 }
@@ -340,6 +357,22 @@ hipError_t launch_seed_scatter(const SeedSpec& ss, const GenomeTable& gt, const 
         MUMS_SCATTER(0);
     }
 #undef MUMS_SCATTER
+    return hipGetLastError();
+}
+
+// chunked mode: records of MSD digits [dlo, dlo + nbc) only, 33-bit indices
+// (requires 2w+1 - msd_bits == 31); hist_slice = the scanned histogram rows of those digits
+hipError_t launch_seed_scatter_chunk(const SeedSpec& ss, const GenomeTable& gt, const uint32_t* d_packed, int msd_bits,
+                                     const uint32_t* d_hist_slice, uint32_t ntiles, uint32_t dlo, uint32_t nbc,
+                                     uint64_t* d_rec, hipStream_t st, const uint64_t* d_cbase, int mb) {
+    if (ntiles == 0) return hipSuccess;
+    if (2 * ss.w + 1 - msd_bits != 64 - 33 || msd_bits > 8 || (nbc == 0 && !d_cbase)) return hipErrorInvalidValue;
+#define MUMS_SCATTER_C(PAT)                                                                                      \
+    hipLaunchKernelGGL((seed_scatter_kernel<256, PAT, 33, true>), dim3(ntiles), dim3(kBlock), 0, st, ss, gt,     \
+                       d_packed, msd_bits, d_hist_slice, ntiles, d_rec, dlo, nbc, d_cbase, mb)
+    if (ss.pattern == kSeedW19) MUMS_SCATTER_C(kSeedW19);
+    else MUMS_SCATTER_C(0);
+#undef MUMS_SCATTER_C
     return hipGetLastError();
 }
 

@@ -1,0 +1,88 @@
+#!/usr/bin/env python3
+"""BASELINE config 5 on one MI355X: 2 x 3 Gbp related synthetic genomes, seed weight 19,
+MemHash seed stage ("sorted+matched") in the chunked mode (> 2^32 seed-mers per context,
+libmems_amd/csrc/chunked.hip).  Reports seed-mers/s and, as size-independent parity
+checks, that a finer chunking (MUMS_DEV_CHUNK_RECORDS) gives the same probe and group
+counts, and that the run is repeatable.
+
+    python tools/bench_c5.py [--length 3000000000] [--steps 2]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+import libmems_amd as lm  # noqa: E402
+
+
+def synth_pair(n: int, p: float, seed: int, dev):
+    """genome 0 iid ACGT; genome 1 = genome 0 with substitution rate p (chunked generation)."""
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(seed)
+    lut = torch.tensor(list(b"ACGT"), dtype=torch.uint8, device=dev)
+    a = torch.empty(n, dtype=torch.uint8, device=dev)
+    b = torch.empty(n, dtype=torch.uint8, device=dev)
+    step = 1 << 28
+    for o in range(0, n, step):
+        k = min(step, n - o)
+        x = lut[torch.randint(0, 4, (k,), generator=gen, device=dev, dtype=torch.uint8).long()]
+        a[o:o + k] = x
+        mut = torch.rand(k, generator=gen, device=dev) < p
+        sub = lut[torch.randint(0, 4, (k,), generator=gen, device=dev, dtype=torch.uint8).long()]
+        b[o:o + k] = torch.where(mut, sub, x)
+    torch.cuda.synchronize()
+    return a, b
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--length", type=int, default=3_000_000_000)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--fine-cap", type=int, default=400_000_000)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    t0 = time.perf_counter()
+    a, b = synth_pair(args.length, 0.01, 2024, dev)
+    gen_s = time.perf_counter() - t0
+    print(f"generated 2 x {args.length} bp in {gen_s:.1f} s", flush=True)
+    out = {"config": "BASELINE config 5 shape on 1 GPU: 2 x %d bp related p=0.01, w19 (0x7b974ef), MemHash seed stage"
+                     % args.length}
+    with lm.MemHash(0) as mh:
+        mh.SetSeed(lm.getSeed(19))
+        mh.AddSequence(a)
+        mh.AddSequence(b)
+        mh.FindStage(lm.STAGE_SEEDS)   # warm
+        print("warm run done", flush=True)
+        ts = []
+        for _ in range(args.steps):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            mh.FindStage(lm.STAGE_SEEDS)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t1)
+            print(f"step {ts[-1] * 1e3:.1f} ms", flush=True)
+        st = mh.stats()
+        os.environ["MUMS_DEV_CHUNK_RECORDS"] = str(args.fine_cap)
+        mh.FindStage(lm.STAGE_SEEDS)
+        fine = mh.stats()
+        os.environ.pop("MUMS_DEV_CHUNK_RECORDS")
+    dt = min(ts)
+    out.update({
+        "seedmers": st["seedmers"], "seedmers_per_s": st["seedmers"] / dt, "ms_per_step": dt * 1e3,
+        "chunks": st["chunks"], "probes": st["probes"], "groups": st["groups"],
+        "phase_ms": {k: round(st[k], 2) for k in ("ms_keys", "ms_sort", "ms_groups", "ms_buckets", "ms_total")},
+        "finer_chunking": {"chunks": fine["chunks"], "probes": fine["probes"], "groups": fine["groups"],
+                           "same_counts": (fine["probes"], fine["groups"]) == (st["probes"], st["groups"])},
+    })
+    print(json.dumps(out), flush=True)
+    if not out["finer_chunking"]["same_counts"]:
+        sys.exit(3)
+
+
+if __name__ == "__main__":
+    main()
