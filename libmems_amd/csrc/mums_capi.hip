@@ -294,7 +294,9 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
     HIPCHK(ctx->tbl.ensure((ctx->P + 1) * 4));
     HIPCHK(ctx->chain_of.ensure((ctx->P + 1) * 4));
     HIPCHK(ctx->spill.ensure((ctx->P + 1) * 16));
-    HIPCHK(ctx->summ.ensure((ctx->P + 1) * 32));
+    // summaries, their compacted copies, keep-flag scan, compacted bucket ranges (replay.hip)
+    HIPCHK(ctx->summ.ensure((ctx->P + 1) * 64 + (ctx->P + 64) * 4 + ((size_t)Tb + 64) * 8 +
+                            scan_tmp_bytes(ctx->P + 2) + 4096));
     HIPCHK(ctx->chain_tmp.ensure(chain_tmp_bytes(ctx->P + 1)));
     HIPCHK(ctx->radix_tmp.ensure(radix_tmp_bytes(ctx->P + 1)));
     HIPCHK(ctx->tmp.ensure(std::max(scan_tmp_bytes(ctx->P + 1), scan_tmp_bytes(Tb))));

@@ -296,7 +296,7 @@ template <int MG, int RB, typename View>
 __global__ __launch_bounds__(RB) void replay_kernel(
     View v, GenomeTable gt, MatchParams mp, int L, const uint64_t* __restrict__ probe_info,
     const uint4* __restrict__ summ, const uint4* __restrict__ summ_b, const uint32_t* __restrict__ bstart,
-    const uint32_t* __restrict__ bend,
+    const uint32_t* __restrict__ bend, const uint32_t* __restrict__ obase,
     uint32_t* __restrict__ tbl, uint4* __restrict__ spill, const int64_t* __restrict__ pool, uint32_t lds_cap,
     uint32_t* __restrict__ tsize, DevCounters* ctr, uint64_t* __restrict__ dbg, uint32_t kmin, uint32_t kmax) {
     extern __shared__ uint4 s_tab[];
@@ -308,9 +308,10 @@ __global__ __launch_bounds__(RB) void replay_kernel(
 
     const int tid = threadIdx.x;
     const uint32_t b = blockIdx.x;
-    const uint32_t beg = bstart[b];
+    const uint32_t beg = bstart[b];       // this bucket's probes in the (compacted) summaries
     const uint32_t K_b = bend[b] - beg;
     if (K_b <= kmin || K_b > kmax) return;
+    const uint32_t ob = obase[b];         // its slice of tbl / spill (>= the entries it ends with)
     const int G = gt.G;
     bool in_lds = true;
     uint32_t t = 0;
@@ -335,14 +336,14 @@ __global__ __launch_bounds__(RB) void replay_kernel(
         uint32_t mypos = 0;
         if (is_first)
             mypos = in_lds ? insert_pos<MG>(s_tab, t, me.z, me.x, (int64_t)mb.x, (int64_t)mb.y, pool, G)
-                           : insert_pos<MG>(spill + beg, t, me.z, me.x, (int64_t)mb.x, (int64_t)mb.y, pool, G);
+                           : insert_pos<MG>(spill + ob, t, me.z, me.x, (int64_t)mb.x, (int64_t)mb.y, pool, G);
         if (dbg) { __syncthreads(); c_win += wall_clock64() - t0; }
         uint32_t done = 0;
         while (done < c) {
             if (dbg) { t0 = wall_clock64(); ++n_round; }
             const int first = in_lds
                 ? round_first<MG, RB, View>(s_tab, t, done, c, me, v, gt, mp, L, probe_info, pool, red)
-                : round_first<MG, RB, View>(spill + beg, t, done, c, me, v, gt, mp, L, probe_info, pool, red);
+                : round_first<MG, RB, View>(spill + ob, t, done, c, me, v, gt, mp, L, probe_info, pool, red);
             if (dbg) { const uint64_t t1 = wall_clock64(); c_round += t1 - t0; t0 = t1; }
             if (first == RB) {
                 coll += c - done;
@@ -354,17 +355,17 @@ __global__ __launch_bounds__(RB) void replay_kernel(
                     s_ins = mypos;
                 else
                     s_ins = in_lds ? insert_pos<MG>(s_tab, t, me.z, me.x, (int64_t)mb.x, (int64_t)mb.y, pool, G)
-                                   : insert_pos<MG>(spill + beg, t, me.z, me.x, (int64_t)mb.x, (int64_t)mb.y, pool, G);
+                                   : insert_pos<MG>(spill + ob, t, me.z, me.x, (int64_t)mb.x, (int64_t)mb.y, pool, G);
                 s_rank = mb.z & 0x7FFFFFFFu;
                 s_new = make_uint4(me.z, me.x, mb.x, mb.y);
             }
             if (in_lds && t + 1 > lds_cap) {   // spill the vector to the bucket's global slice
-                for (uint32_t k = tid; k < t; k += RB) spill[beg + k] = s_tab[k];
+                for (uint32_t k = tid; k < t; k += RB) spill[ob + k] = s_tab[k];
                 in_lds = false;
             }
             __syncthreads();
             if (in_lds) shift_insert<RB>(s_tab, t, s_ins, s_new);
-            else shift_insert<RB>(spill + beg, t, s_ins, s_new);
+            else shift_insert<RB>(spill + ob, t, s_ins, s_new);
             if (is_first && tid > first)
                 mypos += (s_ins < mypos || (s_ins == mypos && s_rank < (mb.z & 0x7FFFFFFFu))) ? 1u : 0u;
             if (dbg) c_ins += wall_clock64() - t0;
@@ -373,9 +374,9 @@ __global__ __launch_bounds__(RB) void replay_kernel(
         }
     }
     if (in_lds)
-        for (uint32_t k = tid; k < t; k += RB) tbl[beg + k] = s_tab[k].x;
+        for (uint32_t k = tid; k < t; k += RB) tbl[ob + k] = s_tab[k].x;
     else
-        for (uint32_t k = tid; k < t; k += RB) tbl[beg + k] = spill[beg + k].x;
+        for (uint32_t k = tid; k < t; k += RB) tbl[ob + k] = spill[ob + k].x;
     if (tid == 0) {
         tsize[b] = t;
         atomicAdd(&ctr->collisions, coll);
@@ -386,6 +387,42 @@ __global__ __launch_bounds__(RB) void replay_kernel(
             d[4] = c_win; d[5] = c_round; d[6] = c_ins; d[7] = wall_clock64() - t_all;
         }
     }
+}
+
+// Probes that are neither chain-first nor suspicious (flag bits 31 / 30 clear) collide
+// with their chain entry without touching the vector, so the replay only needs the
+// others: keep flags -> exclusive scan -> compacted summaries and bucket ranges; the
+// dropped probes are counted as collisions (MemHash::m_collision_count) up front.
+__global__ __launch_bounds__(kBlock) void keep_flags_kernel(const uint4* __restrict__ summ, uint64_t P,
+                                                            uint32_t* __restrict__ keep) {
+    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k <= P) keep[k] = (k < P && (summ[k].w & 0xC0000000u)) ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(kBlock) void compact_summ_kernel(const uint4* __restrict__ summ,
+                                                              const uint4* __restrict__ summ_b,
+                                                              const uint32_t* __restrict__ pos, uint64_t P,
+                                                              uint4* __restrict__ sc, uint4* __restrict__ sbc) {
+    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= P) return;
+    const uint4 x = summ[k];
+    if (x.w & 0xC0000000u) {
+        sc[pos[k]] = x;
+        sbc[pos[k]] = summ_b[k];
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void compact_ranges_kernel(const uint32_t* __restrict__ bstart,
+                                                                const uint32_t* __restrict__ bend,
+                                                                const uint32_t* __restrict__ pos, uint32_t Tb,
+                                                                uint64_t P, uint32_t* __restrict__ cbeg,
+                                                                uint32_t* __restrict__ cend,
+                                                                DevCounters* __restrict__ ctr) {
+    const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
+    if (b == 0) atomicAdd(&ctr->collisions, (unsigned long long)(P - pos[P]));
+    if (b >= Tb) return;
+    cbeg[b] = pos[bstart[b]];
+    cend[b] = pos[bend[b]];
 }
 
 __global__ void bucket_ranges_kernel(const uint32_t* __restrict__ sb, uint64_t P, uint32_t* __restrict__ bstart,
@@ -487,11 +524,27 @@ hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, i
     hipLaunchKernelGGL(probe_flags_kernel, dim3(pgrid), dim3(kBlock), 0, st, (uint4*)summ, summ_b, P, first_pos,
                        next_s, rank, pool, gt.G);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    // the replay reads only chain-first / suspicious probes (summ buffer: 2 more uint4
+    // arrays, the scanned keep flags and the compacted bucket ranges after the originals)
+    uint4* summ_c = summ_b + (P + 1);
+    uint4* summ_bc = summ_c + (P + 1);
+    uint32_t* pos = (uint32_t*)(summ_bc + (P + 1));
+    uint32_t* cbeg = pos + (P + 64);
+    uint32_t* cend = cbeg + mp.table_size + 64;
+    void* stmp = (void*)(((uintptr_t)(cend + mp.table_size + 64) + 255) & ~(uintptr_t)255);
+    hipLaunchKernelGGL(keep_flags_kernel, dim3((unsigned)((P + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+                       (const uint4*)summ, P, pos);
+    if ((e = exclusive_scan_u32(pos, P + 1, stmp, nullptr, st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(compact_summ_kernel, dim3(pgrid), dim3(kBlock), 0, st, (const uint4*)summ,
+                       (const uint4*)summ_b, pos, P, summ_c, summ_bc);
+    hipLaunchKernelGGL(compact_ranges_kernel, dim3((mp.table_size + kBlock - 1) / kBlock), dim3(kBlock), 0, st,
+                       bstart, bend, pos, mp.table_size, P, cbeg, cend, (DevCounters*)ctr);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     // buckets of <= 64 probes: one wave each; the rest: one big workgroup each
     constexpr uint32_t kSmall = 64;
     hipLaunchKernelGGL((replay_kernel<MG, 64, View>), dim3(mp.table_size), dim3(64), kSmall * sizeof(uint4), st, v, gt,
-                       mp, L, probe_info, (const uint4*)summ, (const uint4*)summ_b, bstart, bend, tbl, (uint4*)spill,
-                       pool, kSmall, tsize, (DevCounters*)ctr, dbg, 0u, kSmall);
+                       mp, L, probe_info, (const uint4*)summ_c, (const uint4*)summ_bc, cbeg, cend, bstart, tbl,
+                       (uint4*)spill, pool, kSmall, tsize, (DevCounters*)ctr, dbg, 0u, kSmall);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (lds_cap <= kSmall) return hipSuccess;   // lds_cap = min(fullest bucket, LDS slots)
     constexpr int RB = replay_block<MG>();
@@ -500,8 +553,8 @@ hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, i
                             (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((replay_kernel<MG, RB, View>), dim3(mp.table_size), dim3(RB), lds, st, v, gt, mp, L, probe_info,
-                       (const uint4*)summ, (const uint4*)summ_b, bstart, bend, tbl, (uint4*)spill, pool, lds_cap,
-                       tsize, (DevCounters*)ctr, dbg, kSmall, 0xFFFFFFFFu);
+                       (const uint4*)summ_c, (const uint4*)summ_bc, cbeg, cend, bstart, tbl, (uint4*)spill, pool,
+                       lds_cap, tsize, (DevCounters*)ctr, dbg, kSmall, 0xFFFFFFFFu);
     return hipGetLastError();
 }
 
