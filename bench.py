@@ -31,7 +31,7 @@ import torch  # noqa: E402  (loaded before libmums_hip.so: one HIP runtime per p
 import torch.distributed as dist  # noqa: E402
 
 import libmems_amd as lm  # noqa: E402
-from libmems_amd.shard import HipShardEngine, ShardedSeedStage, genome_blocks  # noqa: E402
+from libmems_amd.shard import HipShardEngine, ShardedSeedStage, genome_blocks, genome_slices  # noqa: E402
 
 METRIC = "seed-mers/sec sorted+matched (+ MUMs/sec) at 1/2/4/8 MI355X; HBM GB/s vs roofline"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
@@ -41,6 +41,8 @@ PROFILE_SUMMARY = os.path.join(ROOT, "profiles", "r01_dominant_kernel.json")
 def synth_genomes(G: int, n: int, p: float, seed: int, device: torch.device):
     """Synthetic related genomes on the GPU: genome 0 iid ACGT; genome g>0 = genome 0 with
     per-base substitution rate p; genome 2 reverse-complemented (SURVEY.md 8(d) shape)."""
+    if n > (1 << 28):
+        return synth_genomes_large(G, n, p, seed, device)
     gen = torch.Generator(device=device)
     gen.manual_seed(seed)
     lut = torch.tensor(list(b"ACGT"), dtype=torch.uint8, device=device)
@@ -56,6 +58,26 @@ def synth_genomes(G: int, n: int, p: float, seed: int, device: torch.device):
         if g == 2:
             s = comp[s.flip(0).long()]
         out.append(s.contiguous())
+    torch.cuda.synchronize()
+    return out
+
+
+def synth_genomes_large(G: int, n: int, p: float, seed: int, device: torch.device):
+    """synth_genomes for mammalian-scale n (BASELINE config 5), generated 2^28 bases at a
+    time; no reverse complement (config 5 has two genomes)."""
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    lut = torch.tensor(list(b"ACGT"), dtype=torch.uint8, device=device)
+    out = [torch.empty(n, dtype=torch.uint8, device=device) for _ in range(G)]
+    step = 1 << 28
+    for o in range(0, n, step):
+        k = min(step, n - o)
+        x = lut[torch.randint(0, 4, (k,), generator=gen, device=device, dtype=torch.uint8).long()]
+        out[0][o:o + k] = x
+        for g in range(1, G):
+            mut = torch.rand(k, generator=gen, device=device) < p
+            sub = lut[torch.randint(0, 4, (k,), generator=gen, device=device, dtype=torch.uint8).long()]
+            out[g][o:o + k] = torch.where(mut, sub, x)
     torch.cuda.synchronize()
     return out
 
@@ -130,7 +152,16 @@ def main():
     ap.add_argument("--no-mums", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, default) or gloo (rehearsal)")
     ap.add_argument("--device", type=int, default=None, help="force one HIP device for every rank (rehearsal)")
+    ap.add_argument("--workload", choices=("c3", "c5"), default="c3",
+                    help="c3 (default, the metric's config): 8 x 100 Mbp; c5: 2 x 3 Gbp (chunked mode on 1 GPU, "
+                         "position-sharded genomes on N GPUs, N a multiple of 8)")
     args = ap.parse_args()
+    if args.workload == "c5":
+        args.genomes = 2
+        if args.length == 100_000_000:   # not overridden: the config's 3 Gbp
+            args.length = 3_000_000_000
+        args.no_mums = True
+        args.no_cpu_baseline = True
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -159,6 +190,17 @@ def main():
             mh.AddSequence(s)
         run = lambda: mh.FindStage(lm.STAGE_SEEDS)  # noqa: E731
         stats = mh.stats
+    elif args.workload == "c5":
+        # genome position slices (each 3 Gbp genome over world/G ranks)
+        L = lm.getSeedLength(seed)
+        g, b0, b1 = genome_slices([n] * G, L, world)[rank]
+        mine = [genomes[g][b0:min(n, b1 + L - 1)]]
+        eng = HipShardEngine(local, seed, [n] * G, g, mine, slice_of=(g, b0, b1))
+        genomes = mine   # views into genome g keep its storage alive
+        stage = ShardedSeedStage(eng)
+        mh = eng.mh
+        run = stage.run
+        stats = eng.stats
     else:
         # genome block per rank; the whole C3 input is split, not replicated
         first, count = genome_blocks(G, world)[rank]
@@ -230,13 +272,16 @@ def main():
             "scaling": "strong",   # the C3 input is fixed and split over the ranks
             "vs_baseline": None,
             "dtype": "u64" if key_bytes == 8 else "u32",
-            "data": "synthetic: 8 related genomes generated on the GPU (iid ACGT base, 1% substitutions, genome 2 "
-                    "reverse-complemented)",
-            "config": {"workload": f"BASELINE config 3: {G} x {n // 10**6} Mbp, seed weight 19 (0x7b974ef), "
-                                   f"MemHash seed stage (sorted+matched)",
+            "data": (f"synthetic: {G} related genomes generated on the GPU (iid ACGT base, 1% substitutions"
+                     + (", genome 2 reverse-complemented)" if G >= 3 else ")")),
+            "config": {"workload": f"BASELINE config {5 if args.workload == 'c5' else 3}: {G} x {n // 10**6} Mbp, "
+                                   f"seed weight 19 (0x7b974ef), MemHash seed stage (sorted+matched)"
+                                   + (f", {st.get('chunks', 0)} key chunks" if world == 1 and args.workload == 'c5'
+                                      else ""),
                        "genomes": G, "genome_length": n, "seedmers_total": seedmers_total,
                        "seedmers_rank0": seedmers_rank, "probes_rank0": probes,
-                       "parallelism": (f"genome-sharded x{world}: genome block per rank, "
+                       "parallelism": (f"genome-sharded x{world}: "
+                                       f"{'position slice' if args.workload == 'c5' else 'genome block'} per rank, "
                                        f"{'RCCL' if args.dist_backend == 'nccl' else args.dist_backend} all-to-all of key "
                                        f"ranges ({exch_bytes / max(args.steps, 1) / 1e9:.2f} GB/step sent by rank 0), "
                                        f"merge per key range") if world > 1 else "1 GPU"},

@@ -175,6 +175,13 @@ int  mums_length_filter(mums_ctx* ctx, uint64_t min_length);
  *      probes of this key range; stats via mums_get_stats. */
 int  mums_shard_layout(mums_ctx* ctx, uint32_t genomes_total, uint32_t first_genome, const uint64_t* lengths);
 /* msd_bits of the exchange and the number of records mums_shard_keys will write. */
+/* Position-sharded layout (BASELINE config 5 on 8 GPUs): the context's
+ * one genome is the ASCII of genome `genome`'s bases [pos_begin, pos_end + L - 1) (L = seed
+ * length, clipped at the genome end) and this rank owns its SML positions [pos_begin,
+ * pos_end); records carry global seed-mer indices (33-bit above 2^32 seed-mers).  Seed
+ * stage only (mums_shard_keys / mums_shard_merge). */
+int  mums_shard_slice(mums_ctx* ctx, uint32_t genomes_total, const uint64_t* lengths, uint32_t genome,
+                      uint64_t pos_begin, uint64_t pos_end);
 int  mums_shard_msd_bits(mums_ctx* ctx, uint32_t* msd_bits, uint64_t* local_records);
 int  mums_shard_keys(mums_ctx* ctx, uint64_t* d_records, uint64_t capacity, uint64_t* bucket_counts);
 int  mums_shard_merge(mums_ctx* ctx, const uint64_t* d_records, uint32_t nsources, uint32_t first_bucket,

@@ -90,7 +90,7 @@ EXPORTED_SYMBOLS = [
     "mums_shard_merge", "mums_probe_count", "mums_probe_copy", "mums_shard_bucket_counts", "mums_shard_probe_rows",
     "mums_shard_packed_info", "mums_shard_packed_copy", "mums_shard_find", "mums_set_parallel_compat",
     "mums_seed_occurrence", "mums_multiplicity_filter", "mums_length_filter", "mums_write_sml",
-    "mums_add_genome_sml", "mums_set_pairwise",
+    "mums_add_genome_sml", "mums_set_pairwise", "mums_shard_slice",
 ]
 
 _lib: Optional[ctypes.CDLL] = None
@@ -154,6 +154,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mums_write_sml.argtypes = [vp, u32, ctypes.c_char_p, ctypes.c_char_p]
     lib.mums_add_genome_sml.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(u64)]
     lib.mums_set_pairwise.argtypes = [vp, i32]
+    lib.mums_shard_slice.argtypes = [vp, u32, vp, u32, u64, u64]
     _lib = lib
     return lib
 

@@ -96,6 +96,13 @@ struct mums_ctx {
     std::vector<uint64_t> shard_len;
     GenomeTable lgt{};        // the owned genomes, global seed-mer bases
     double shard_keys_ms = 0;
+    // position-sharded layout (BASELINE config 5 on 8 GPUs): this context's one genome is
+    // the ASCII of genome slice_genome's bases [slice_begin, slice_end + L - 1), it owns
+    // the SML positions [slice_begin, slice_end)
+    bool slice = false;
+    uint32_t slice_genome = 0;
+    uint64_t slice_begin = 0, slice_end = 0;
+    int rec_ib = 32;          // index bits of the packed records (33: > 2^32 seed-mers)
 
     // state of the last run
     int stage_done = 0;
@@ -271,6 +278,8 @@ int materialize_dispatch(mums_ctx* ctx, View sv, const MatchParams& mp, hipStrea
 }
 
 int materialize_seeds(mums_ctx* ctx, const MatchParams& mp, hipStream_t st) {
+    if (ctx->packed_path && ctx->rec_ib == 33)
+        return materialize_dispatch<RecViewT<33>>(ctx, RecViewT<33>{ctx->sorted_rec}, mp, st);
     if (ctx->packed_path) return materialize_dispatch<RecView>(ctx, RecView{ctx->sorted_rec}, mp, st);
     if (ctx->key64)
         return materialize_dispatch<PairView<uint64_t>>(
@@ -382,7 +391,7 @@ uint32_t layout_packed(GenomeTable& t, uint64_t* words) {
 // the (ckey_low << 32 | global index) records stably into their MSD buckets in out.
 // Bucket starts -> bstart[0 .. 2^B] (device).
 int keys_stage(mums_ctx* ctx, const GenomeTable& lgt, uint32_t T, int B, uint64_t n, uint64_t* out, uint32_t* bstart,
-               hipStream_t st) {
+               hipStream_t st, int ib = 32) {
     DevCounters* dc = ctx->counters.as<DevCounters>();
     std::vector<const char*> ptrs(lgt.G);
     for (int g = 0; g < lgt.G; ++g) ptrs[g] = ctx->genomes[g].d_ptr;
@@ -390,7 +399,14 @@ int keys_stage(mums_ctx* ctx, const GenomeTable& lgt, uint32_t T, int B, uint64_
     HIPCHK(launch_seed_pack(ctx->ss, lgt, ptrs.data(), ctx->packed.as<uint32_t>(), 1, true, nullptr, B, hist, T,
                             &dc->err, st));
     if (B > 0) HIPCHK(exclusive_scan_u32(hist, (uint64_t)T << B, ctx->tmp.p, nullptr, st));
-    HIPCHK(launch_seed_scatter(ctx->ss, lgt, ctx->packed.as<uint32_t>(), B, hist, T, out, st));
+    if (ib == 32) {
+        HIPCHK(launch_seed_scatter(ctx->ss, lgt, ctx->packed.as<uint32_t>(), B, hist, T, out, st));
+    } else {   // 33-bit indices: every digit kept, one chunk at base 0 (chunked.hip's scatter)
+        HIPCHK(ctx->ctab.ensure(64));
+        HIPCHK(hipMemsetAsync(ctx->ctab.p, 0, 64, st));
+        HIPCHK(launch_seed_scatter_chunk(ctx->ss, lgt, ctx->packed.as<uint32_t>(), B, hist, T, 0, 0, out, st,
+                                         ctx->ctab.as<uint64_t>(), B));
+    }
     HIPCHK(seg_bucket_starts(B > 0 ? hist : nullptr, T, B, n, bstart, st));
     return MUMS_OK;
 }
@@ -413,7 +429,7 @@ int ensure_merge_space(mums_ctx* ctx, uint64_t n, int mb, int key_bits, ProbeSpa
 // are in ctx->mstart -> stable sort on record key bits [32, 32 + key_bits) inside every
 // bucket (the merged SortedMerList stream) -> equal-key groups -> accepted probes in key order.
 int merge_stage(mums_ctx* ctx, uint64_t n, int mb, int key_bits, const MatchParams& mp, const ProbeSpace& ps,
-                hipStream_t st) {
+                hipStream_t st, int ib = 32) {
     DevCounters* dc = ctx->counters.as<DevCounters>();
     SegTile* tiles = ctx->tiles.as<SegTile>();
     const uint32_t* bstart = ctx->mstart.as<uint32_t>();
@@ -421,9 +437,11 @@ int merge_stage(mums_ctx* ctx, uint64_t n, int mb, int key_bits, const MatchPara
     const bool prof = ctx->profiling;
     HIPCHK(build_seg_tiles_from_starts(bstart, mb, n, tiles, &dc->ntiles, ctx->tmp.p, st));
     int buf = 0;
+    if (ib != 32 && !(n < (1ull << 30) && key_bits <= 32))
+        return fail(ctx, MUMS_E_UNSUPPORTED, "33-bit records need < 2^30 records per merge");
     if (ctx->use_onesweep && n < (1ull << 30) && key_bits <= 32)
         HIPCHK(seg_onesweep_sort(ctx->recA.as<uint64_t>(), ctx->recB.as<uint64_t>(), n, key_bits, mb, bstart,
-                                 ctx->tmp.p, &dc->err, &buf, st, prof ? ctx->ev_ds : nullptr));
+                                 ctx->tmp.p, &dc->err, &buf, st, prof ? ctx->ev_ds : nullptr, ib));
     else
         HIPCHK(seg_radix_sort(ctx->recA.as<uint64_t>(), ctx->recB.as<uint64_t>(), n, key_bits, tiles, ub, ctx->tmp.p,
                               &buf, st, prof ? ctx->ev_ds : nullptr));
@@ -431,6 +449,9 @@ int merge_stage(mums_ctx* ctx, uint64_t n, int mb, int key_bits, const MatchPara
     ctx->sorted_rec = buf ? ctx->recB.as<uint64_t>() : ctx->recA.as<uint64_t>();
     ctx->sort_passes = (key_bits + 7) / 8;
     HIPCHK(hipEventRecord(ctx->ev[EV_SORT], st));
+    if (ib == 33)
+        return groups_dispatch<RecViewT<33>>(ctx, RecViewT<33>{ctx->sorted_rec}, tiles, ub, mp, ps.probe_info,
+                                             ps.probe_bucket, ps.slot_info, ps.slot_bucket, st);
     return groups_dispatch<RecView>(ctx, RecView{ctx->sorted_rec}, tiles, ub, mp, ps.probe_info, ps.probe_bucket,
                                     ps.slot_info, ps.slot_bucket, st);
 }
@@ -812,26 +833,49 @@ int ceil_log2(uint64_t x) {
 int prepare_shard(mums_ctx* ctx) {
     if (!ctx->shard) return fail(ctx, MUMS_E_INVALID, "no shard layout (mums_shard_layout)");
     const uint32_t nl = (uint32_t)ctx->genomes.size();
-    if (ctx->shard_first + nl > ctx->shard_len.size())
-        return fail(ctx, MUMS_E_INVALID, "owned genomes exceed the shard layout");
-    for (uint32_t i = 0; i < nl; ++i)
-        if (ctx->genomes[i].n != ctx->shard_len[ctx->shard_first + i])
-            return fail(ctx, MUMS_E_INVALID, "owned genome length differs from the shard layout");
+    if (!ctx->slice) {
+        if (ctx->shard_first + nl > ctx->shard_len.size())
+            return fail(ctx, MUMS_E_INVALID, "owned genomes exceed the shard layout");
+        for (uint32_t i = 0; i < nl; ++i)
+            if (ctx->genomes[i].n != ctx->shard_len[ctx->shard_first + i])
+                return fail(ctx, MUMS_E_INVALID, "owned genome length differs from the shard layout");
+    }
     int rc = prepare_run(ctx, ctx->shard_len);
     if (rc) return rc;
     if (2 * ctx->w + 1 > 32 + kMaxMsdBits)
         return fail(ctx, MUMS_E_UNSUPPORTED, "sharded mode needs 2w+1 <= 43 (packed records)");
     GenomeTable& l = ctx->lgt;
     l = GenomeTable{};
-    l.G = (int)nl;
-    for (uint32_t i = 0; i < nl; ++i) {
-        l.n[i] = ctx->gt.n[ctx->shard_first + i];
-        l.m[i] = ctx->gt.m[ctx->shard_first + i];
-        l.base[i] = ctx->gt.base[ctx->shard_first + i];
+    if (ctx->slice) {   // one genome slice: its SML positions [slice_begin, slice_end)
+        const uint32_t g = ctx->slice_genome;
+        const uint64_t mg = ctx->gt.m[g], b0 = ctx->slice_begin, b1 = ctx->slice_end;
+        if (g >= (uint32_t)ctx->gt.G || b0 > b1 || b1 > mg || nl != 1)
+            return fail(ctx, MUMS_E_INVALID, "bad genome slice");
+        const uint64_t want = (b1 > b0) ? std::min<uint64_t>(ctx->gt.n[g], b1 + ctx->L - 1) - b0 : 0;
+        if (ctx->genomes[0].n != want)
+            return fail(ctx, MUMS_E_INVALID, "slice ASCII must hold bases [begin, end + L - 1) of its genome");
+        l.G = 1;
+        l.n[0] = want;
+        l.m[0] = b1 - b0;
+        l.base[0] = ctx->gt.base[g] + b0;
+        for (int k = 1; k <= kMaxG; ++k) l.base[k] = l.base[0] + l.m[0];
+    } else {
+        l.G = (int)nl;
+        for (uint32_t i = 0; i < nl; ++i) {
+            l.n[i] = ctx->gt.n[ctx->shard_first + i];
+            l.m[i] = ctx->gt.m[ctx->shard_first + i];
+            l.base[i] = ctx->gt.base[ctx->shard_first + i];
+        }
+        for (int g = (int)nl; g <= kMaxG; ++g) l.base[g] = ctx->gt.base[ctx->shard_first + nl];
     }
-    for (int g = (int)nl; g <= kMaxG; ++g) l.base[g] = ctx->gt.base[ctx->shard_first + nl];
     ctx->packed_path = true;
     ctx->msd_bits = shard_msd_bits(ctx->w);
+    // records: 32-bit global indices up to 2^32 seed-mers, 33-bit beyond (the key part
+    // then holds 2w+1-B = 31 bits: w19 with B = 8)
+    const bool big = ctx->gt.base[ctx->gt.G] >= 0xFFFFFFF0ull || getenv("MUMS_DEV_SHARD_IB33") != nullptr;
+    ctx->rec_ib = big ? 33 : 32;
+    if (big && (2 * ctx->w + 1 - ctx->msd_bits != 31 || ctx->msd_bits > 8))
+        return fail(ctx, MUMS_E_UNSUPPORTED, "sharded mode above 2^32 seed-mers needs seed weight 19");
     return MUMS_OK;
 }
 
@@ -1243,7 +1287,24 @@ int mums_shard_layout(mums_ctx* ctx, uint32_t genomes_total, uint32_t first_geno
     if (first_genome > genomes_total || (genomes_total && !lengths))
         return fail(ctx, MUMS_E_INVALID, "bad shard layout");
     ctx->shard = true;
+    ctx->slice = false;
     ctx->shard_first = first_genome;
+    ctx->shard_len.assign(lengths, lengths + genomes_total);
+    ctx->stage_done = 0;
+    return MUMS_OK;
+}
+
+int mums_shard_slice(mums_ctx* ctx, uint32_t genomes_total, const uint64_t* lengths, uint32_t genome,
+                     uint64_t pos_begin, uint64_t pos_end) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (genomes_total > (uint32_t)kMaxG) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 32 genomes");
+    if (genome >= genomes_total || !lengths || pos_begin > pos_end) return fail(ctx, MUMS_E_INVALID, "bad slice");
+    ctx->shard = true;
+    ctx->slice = true;
+    ctx->shard_first = genome;
+    ctx->slice_genome = genome;
+    ctx->slice_begin = pos_begin;
+    ctx->slice_end = pos_end;
     ctx->shard_len.assign(lengths, lengths + genomes_total);
     ctx->stage_done = 0;
     return MUMS_OK;
@@ -1288,7 +1349,7 @@ int mums_shard_keys(mums_ctx* ctx, uint64_t* d_records, uint64_t capacity, uint6
     HIPCHK(hipMemsetAsync(dc, 0, sizeof(DevCounters), st));
     std::vector<uint32_t> hs(nb + 1, 0);
     if (l.G > 0 && n > 0) {
-        rc = keys_stage(ctx, l, T, B, n, d_records, ctx->mstart.as<uint32_t>(), st);
+        rc = keys_stage(ctx, l, T, B, n, d_records, ctx->mstart.as<uint32_t>(), st, ctx->rec_ib);
         if (rc) return rc;
         HIPCHK(hipMemcpyAsync(hs.data(), ctx->mstart.p, (nb + 1) * 4, hipMemcpyDeviceToHost, st));
     }
@@ -1364,7 +1425,7 @@ int mums_shard_merge(mums_ctx* ctx, const uint64_t* d_records, uint32_t nsources
     HIPCHK(hipEventRecord(ctx->ev[EV_KEYS], st));
     MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, ctx->masked, ctx->seq_mask};
     ctx->N = n;
-    rc = merge_stage(ctx, n, mb, 2 * ctx->w + 1 - B, mp, ps, st);
+    rc = merge_stage(ctx, n, mb, 2 * ctx->w + 1 - B, mp, ps, st, ctx->rec_ib);
     if (rc) return rc;
     rc = finish_seeds(ctx, ps, st);
     if (rc) return rc;
@@ -1404,7 +1465,8 @@ int mums_probe_copy(mums_ctx* ctx, uint32_t* buckets, uint64_t* ref_index, uint6
     for (uint64_t k = 0; k < P; ++k) {
         const uint64_t h = (uint32_t)info[k], gs = info[k] >> 32;
         uint64_t mn = ~0ull;
-        for (uint64_t i = h; i < h + gs && i < N; ++i) mn = std::min<uint64_t>(mn, (uint32_t)rec[i]);
+        const uint64_t imask = (1ull << ctx->rec_ib) - 1;
+        for (uint64_t i = h; i < h + gs && i < N; ++i) mn = std::min<uint64_t>(mn, rec[i] & imask);
         if (buckets) buckets[k] = bucket_of_probe[k];
         if (ref_index) ref_index[k] = mn;
     }
@@ -1812,6 +1874,8 @@ int mums_shard_probe_rows(mums_ctx* ctx, uint32_t nranks, const uint32_t* bounds
 int mums_shard_packed_info(mums_ctx* ctx, uint64_t* word_offset, uint64_t* nwords, uint64_t* total_words) {
     int rc = shard_seeds_done(ctx);
     if (rc) return rc;
+    if (ctx->slice)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "sharded FindMatches needs whole genomes per rank (slices: seed stage)");
     GenomeTable g = ctx->gt;
     uint64_t total = 0;
     (void)layout_packed(g, &total);

@@ -60,11 +60,31 @@ def genome_blocks(G: int, world: int) -> List[Tuple[int, int]]:
     return out
 
 
+def genome_slices(lengths: Sequence[int], L: int, world: int) -> List[Tuple[int, int, int]]:
+    """Position-sharded layout (BASELINE config 5: each 3 Gbp genome over world/G ranks):
+    rank r owns SML positions [begin, end) of genome g = r // (world / G), the genome's
+    SMLLength cut into world / G equal ranges.  Rank order = genome-major, position order =
+    global seed-mer index order, as the exchange requires."""
+    G = len(lengths)
+    if G == 0 or world % G:
+        raise ValueError("position sharding needs world_size to be a multiple of the genome count")
+    k = world // G
+    out = []
+    for g, n in enumerate(lengths):
+        m = max(int(n) - L + 1, 0)
+        for j in range(k):
+            out.append((g, m * j // k, m * (j + 1) // k))
+    return out
+
+
 class HipShardEngine:
-    """One rank's MemHash context in sharded mode (C ABI, HIP kernels on `device`)."""
+    """One rank's MemHash context in sharded mode (C ABI, HIP kernels on `device`).
+    slice_of = (genome, begin, end): position-sharded layout (genome_slices); `genomes`
+    is then the one ASCII slice holding bases [begin, end + L - 1) of that genome."""
 
     def __init__(self, device: int, seed: int, lengths: Sequence[int], first: int, genomes: Sequence,
-                 profiling: bool = False, table_size: int = 40000):
+                 profiling: bool = False, table_size: int = 40000,
+                 slice_of: Optional[Tuple[int, int, int]] = None):
         self.mh = MemHash(device)
         self.device = torch.device("cuda", device)
         self.G = len(lengths)
@@ -75,7 +95,11 @@ class HipShardEngine:
             self.mh.AddSequence(s)
         lens = (ctypes.c_uint64 * len(lengths))(*[int(x) for x in lengths])
         lib = self.mh._lib
-        self.mh._check(lib.mums_shard_layout(self.mh._ctx, len(lengths), first, lens))
+        if slice_of is None:
+            self.mh._check(lib.mums_shard_layout(self.mh._ctx, len(lengths), first, lens))
+        else:
+            g, b0, b1 = slice_of
+            self.mh._check(lib.mums_shard_slice(self.mh._ctx, len(lengths), lens, g, b0, b1))
         if profiling:
             self.mh.SetProfiling(True)
 

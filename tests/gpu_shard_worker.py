@@ -1,9 +1,9 @@
 """TEST INFRASTRUCTURE: one rank of the sharded seed stage on the HIP engine.
 
 Launched by tests/test_gpu_shard.py as
-    python -m torch.distributed.run --nproc-per-node R ... tests/gpu_shard_worker.py OUTDIR G n p w
-Every rank runs its genome block on cuda:0 (the test box has one GPU; the exchange
-goes over gloo on the host) and saves its probe list.
+    python -m torch.distributed.run --nproc-per-node R ... tests/gpu_shard_worker.py OUTDIR G n p w [slices]
+Every rank runs its genome block (or, with "slices", its genome position slice) on cuda:0
+(the test box has one GPU; the exchange goes over gloo on the host) and saves its probe list.
 """
 import os
 import sys
@@ -15,7 +15,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from libmems_amd.shard import HipShardEngine, ShardedSeedStage, genome_blocks  # noqa: E402
+from libmems_amd.shard import HipShardEngine, ShardedSeedStage, genome_blocks, genome_slices  # noqa: E402
 from oracle import oracle  # noqa: E402
 
 
@@ -25,10 +25,19 @@ def main():
     rank, world = dist.get_rank(), dist.get_world_size()
     seqs = oracle.generate(G, n, p, 4242 + G)
     seed = oracle.get_seed(w)
-    first, count = genome_blocks(G, world)[rank]
     dev = torch.device("cuda", 0)
-    local = [torch.frombuffer(bytearray(s), dtype=torch.uint8).to(dev) for s in seqs[first:first + count]]
-    eng = HipShardEngine(0, seed, [len(s) for s in seqs], first, local)
+    lens = [len(s) for s in seqs]
+    if len(sys.argv) > 6 and sys.argv[6] == "slices":
+        L = oracle.lib().oracle_seed_length(seed)
+        g, b0, b1 = genome_slices(lens, L, world)[rank]
+        part = seqs[g][b0:min(lens[g], b1 + L - 1)] if b1 > b0 else b""
+        local = [torch.frombuffer(bytearray(part), dtype=torch.uint8).to(dev)] if part else \
+            [torch.zeros(0, dtype=torch.uint8, device=dev)]
+        eng = HipShardEngine(0, seed, lens, g, local, slice_of=(g, b0, b1))
+    else:
+        first, count = genome_blocks(G, world)[rank]
+        local = [torch.frombuffer(bytearray(s), dtype=torch.uint8).to(dev) for s in seqs[first:first + count]]
+        eng = HipShardEngine(0, seed, lens, first, local)
     ShardedSeedStage(eng).run()
     b, r = eng.probes()
     st = eng.stats()

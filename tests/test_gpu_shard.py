@@ -57,6 +57,32 @@ def test_sharded_seed_stage_gpu(oracle_mod, G, n, p, w, world):
     assert np.array_equal(r, orf)
 
 
+@pytest.mark.parametrize("G,n,p,w,world,ib33", [(2, 300_000, 0.02, 19, 4, False), (2, 300_000, 0.02, 19, 4, True),
+                                                  (3, 200_000, 0.03, 19, 6, True), (2, 400_000, 0.01, 15, 2, False),
+                                                  (2, 250_000, 0.05, 17, 8, False)])
+def test_sharded_slices_gpu(oracle_mod, G, n, p, w, world, ib33):
+    """Position-sharded seed stage (BASELINE config 5 layout: every genome cut into
+    world/G position slices), optionally with the 33-bit records of the > 2^32 seed-mer
+    case forced: the ranks' probe lists concatenated = the oracle's AddHashEntry sequence."""
+    seqs = oracle_mod.generate(G, n, p, 4242 + G)
+    ob, orf, st = oracle_mod.seed_probes(seqs, oracle_mod.get_seed(w))
+    with tempfile.TemporaryDirectory() as d:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+               "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+               os.path.join(ROOT, "tests", "gpu_shard_worker.py"), d, str(G), str(n), str(p), str(w), "slices"]
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        if ib33:
+            env["MUMS_DEV_SHARD_IB33"] = "1"
+        res = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+        assert res.returncode == 0, res.stderr[-3000:]
+        b = np.concatenate([np.load(os.path.join(d, f"b{r}.npy")) for r in range(world)])
+        r = np.concatenate([np.load(os.path.join(d, f"r{r}.npy")) for r in range(world)])
+        s = [np.load(os.path.join(d, f"s{r}.npy")) for r in range(world)]
+    assert sum(int(x[0]) for x in s) == st["seedmers"]
+    assert np.array_equal(b, ob)
+    assert np.array_equal(r, orf)
+
+
 @pytest.mark.parametrize("G,n,p,w,world,T", [(4, 300_000, 0.02, 15, 2, 40000), (3, 200_000, 0.05, 19, 3, 40000),
                                                (5, 100_000, 1.0, 15, 2, 40000), (4, 200_000, 0.01, 15, 3, 7)])
 def test_sharded_find_matches_gpu(oracle_mod, G, n, p, w, world, T):

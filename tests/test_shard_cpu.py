@@ -142,3 +142,19 @@ def test_sharded_find_matches_gloo_world2(oracle_mod, G, n, p, w, T):
     assert len(lens) == len(ref_l) > 0
     assert (lens == ref_l).all() and (sts == ref_s).all()
     assert int(cnt[0]) == ref_st["mem_count"] and int(cnt[1]) == ref_st["collision_count"]
+
+
+def test_genome_slices_cover_every_position_in_order():
+    """Position-sharded layout (BASELINE config 5): genome-major, position-ordered slices that
+    tile every genome's SML positions exactly once (the exchange relies on rank order =
+    global seed-mer index order)."""
+    from libmems_amd.shard import genome_slices
+    lens, L = [3_000_003, 2_000_000], 27
+    sl = genome_slices(lens, L, 8)
+    assert [g for g, _, _ in sl] == [0, 0, 0, 0, 1, 1, 1, 1]
+    for g, n in enumerate(lens):
+        parts = [(b0, b1) for gg, b0, b1 in sl if gg == g]
+        assert parts[0][0] == 0 and parts[-1][1] == n - L + 1
+        assert all(parts[i][1] == parts[i + 1][0] for i in range(len(parts) - 1))
+    with pytest.raises(ValueError):
+        genome_slices(lens, L, 3)
