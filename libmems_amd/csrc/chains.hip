@@ -32,7 +32,10 @@ namespace mums {
 
 namespace {
 
-constexpr int kWalkBudget = 384;   // hit evaluations per lane before a walk is handed to a workgroup
+#ifndef MUMS_WALK_BUDGET
+#define MUMS_WALK_BUDGET 48   // measured: 24 / 48 / 96 / 384 -> chains 6.0 / 5.6 / 6.1 / 8.5 ms (related 4 x 10 Mbp)
+#endif
+constexpr int kWalkBudget = MUMS_WALK_BUDGET;   // hit evaluations per lane before a walk goes to a workgroup
 
 struct WalkItem {
     uint32_t j;      // position in line order
