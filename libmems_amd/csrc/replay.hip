@@ -317,6 +317,37 @@ __global__ __launch_bounds__(RB) void replay_kernel(
     uint32_t t = 0;
     unsigned long long coll = 0;
 
+    // Fast path: every (compacted) probe is its chain's first, none is suspicious and no
+    // two chains tie on their first-genome start.  Then every probe inserts, every
+    // lower_bound lands on the sorted position, and the vector ends as the bucket's chains
+    // in (block, first-genome start) order = their rank order (chain_next_kernel).
+    {
+        __shared__ uint32_t s_ok, s_rmin, s_rmax;
+        if (tid == 0) { s_ok = 1u; s_rmin = 0xFFFFFFFFu; s_rmax = 0u; }
+        __syncthreads();
+        uint32_t ok = 1u, rmin = 0xFFFFFFFFu, rmax = 0u;
+        for (uint32_t k = tid; k < K_b; k += RB) {
+            const uint4 a = summ[beg + k], c = summ_b[beg + k];
+            ok &= ((a.w & 0xC0000000u) == 0x80000000u && !(c.z & 0x80000000u)) ? 1u : 0u;
+            rmin = min(rmin, c.z & 0x7FFFFFFFu);
+            rmax = max(rmax, c.z & 0x7FFFFFFFu);
+        }
+        if (!ok) atomicAnd(&s_ok, 0u);
+        atomicMin(&s_rmin, rmin);
+        atomicMax(&s_rmax, rmax);
+        __syncthreads();
+        if (s_ok && s_rmax - s_rmin + 1u == K_b) {
+            const uint32_t r0 = s_rmin;
+            for (uint32_t k = tid; k < K_b; k += RB)
+                tbl[ob + ((summ_b[beg + k].z & 0x7FFFFFFFu) - r0)] = summ[beg + k].z;
+            if (tid == 0) {
+                tsize[b] = K_b;
+                atomicAdd(&ctr->entries, (unsigned long long)K_b);
+            }
+            return;
+        }
+    }
+
     // the window of probes [w0, w0 + c) stays in the lanes' registers until every
     // one of them is consumed (collided or inserted); `done` = consumed prefix
     // A chain-first lane keeps the insert position of its chain entry up to date: an
