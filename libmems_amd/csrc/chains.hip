@@ -282,7 +282,10 @@ __global__ __launch_bounds__(kBlock) void chain_left_kernel(View v, const uint64
 // run of >= L columns without a hit: the chain ends at the last hit before it (the
 // maximal chain of hits with gaps <= L); without such a run the walk
 // continues from the last hit of the window.
-constexpr int kWalkCols = 4 * kBlock;
+#ifndef MUMS_WALK_CPL
+#define MUMS_WALK_CPL 4
+#endif
+constexpr int kWalkCols = MUMS_WALK_CPL * kBlock;   // columns per workgroup step (per lane: MUMS_WALK_CPL)
 
 template <int MG, typename View>
 __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64_t* __restrict__ probe_info,

@@ -641,8 +641,8 @@ int prepare_run(mums_ctx* ctx, const std::vector<uint64_t>& lens) {
     ctx->stage_done = 0;
     ctx->M = ctx->P = 0;
     const int G = (int)lens.size();
-    if (ctx->enum_tol > 1)
-        return fail(ctx, MUMS_E_UNSUPPORTED, "enumeration tolerance > 1 (MatchFinder::EnumerateMatches) not implemented");
+    if (ctx->enum_tol > 8)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "enumeration tolerance above 8 (odometer slots of the GPU path)");
     uint64_t total = 0;
     for (uint64_t n : lens) total += n;
     uint64_t pat = ctx->seed;
@@ -842,6 +842,8 @@ int prepare_shard(mums_ctx* ctx) {
     }
     int rc = prepare_run(ctx, ctx->shard_len);
     if (rc) return rc;
+    if (ctx->enum_tol > 1)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "sharded mode: enumeration tolerance > 1 runs single-GPU only");
     if (2 * ctx->w + 1 > 32 + kMaxMsdBits)
         return fail(ctx, MUMS_E_UNSUPPORTED, "sharded mode needs 2w+1 <= 43 (packed records)");
     GenomeTable& l = ctx->lgt;
@@ -1005,9 +1007,11 @@ int mums_find_stage(mums_ctx* ctx, int stage) {
         return MUMS_OK;
     }
     const bool big = ctx->N >= 0xFFFFFFF0ull || getenv("MUMS_DEV_CHUNK_RECORDS") != nullptr;
-    if (big && (ctx->pairwise || ctx->pcompat))
-        return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed-mers: only MemHash / MaskedMemHash");
-    if (ctx->pairwise) return run_pipeline_pairwise(ctx, stage);
+    if (big && (ctx->pairwise || ctx->pcompat || ctx->enum_tol > 1))
+        return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed-mers: only MemHash / MaskedMemHash, enum_tol <= 1");
+    if (ctx->pcompat && ctx->enum_tol > 1)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "ParallelMemHash compat with enumeration tolerance > 1");
+    if (ctx->pairwise || ctx->enum_tol > 1) return run_pipeline_pairwise(ctx, stage);
     if (ctx->pcompat) return run_pipeline_compat(ctx, stage);
     return big ? run_pipeline_chunked(ctx, stage) : run_pipeline(ctx, stage);
 }
@@ -1508,7 +1512,9 @@ int pairwise_rows(mums_ctx* ctx, uint64_t N, hipStream_t st) {
     const PairView<K> v{(const K*)ctx->sorted_key, ctx->sorted_idx};
     uint32_t* npairs = ctx->cval.as<uint32_t>();
     uint32_t* off = npairs + N + 64;
-    HIPCHK(launch_pairwise_count<PairView<K>>(v, N, ctx->gt, npairs, dc, st));
+    const MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, ctx->masked, ctx->seq_mask};
+    if (ctx->pairwise) HIPCHK(launch_pairwise_count<PairView<K>>(v, N, ctx->gt, npairs, dc, st));
+    else HIPCHK(launch_enum_count<PairView<K>>(v, N, ctx->gt, mp, npairs, dc, st));
     HIPCHK(hipMemcpyAsync(off, npairs, N * 4, hipMemcpyDeviceToDevice, st));
     HIPCHK(exclusive_scan_u32(off, N, ctx->tmp.p, &dc->nprobes, st));
     uint32_t P = 0;
@@ -1516,16 +1522,22 @@ int pairwise_rows(mums_ctx* ctx, uint64_t N, hipStream_t st) {
     HIPCHK(hipStreamSynchronize(st));
     ctx->P = P;
     HIPCHK(ctx->mprobe.ensure(((uint64_t)P + 1) * (size_t)(ctx->gt.G + 1) * 8));
-    HIPCHK(launch_pairwise_emit<PairView<K>>(v, N, ctx->gt, ctx->L, npairs, off, ctx->mprobe.as<int64_t>(), st));
+    if (ctx->pairwise)
+        HIPCHK(launch_pairwise_emit<PairView<K>>(v, N, ctx->gt, ctx->L, npairs, off, ctx->mprobe.as<int64_t>(), st));
+    else
+        HIPCHK(launch_enum_emit<PairView<K>>(v, N, ctx->gt, mp, ctx->L, npairs, off, ctx->mprobe.as<int64_t>(), st));
     return MUMS_OK;
 }
 }  // extern "C++"
 
+// Also MemHash with enumeration tolerance > 1 (MemHash.cpp:139-162 -> the odometer of
+// MatchFinder::EnumerateMatches, MatchFinder.cpp:342-393): one row per AddHashEntry call.
 int run_pipeline_pairwise(mums_ctx* ctx, int stage) {
     hipStream_t st = ctx->stream;
     const int G = (int)ctx->genomes.size();
     const uint64_t N = ctx->N;
-    MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, 0, 0};
+    MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, ctx->pairwise ? 0 : ctx->masked,
+                   ctx->pairwise ? 0 : ctx->seq_mask};
     GenomeTable& gt = ctx->gt;
     const int kbits = 2 * ctx->w + 1;
     ctx->packed_path = false;

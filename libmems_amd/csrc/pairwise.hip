@@ -1,4 +1,8 @@
-// pairwise.hip -- PairwiseMatchFinder (PairwiseMatchFinder.h:23-33).
+// pairwise.hip -- group enumerations that issue several AddHashEntry calls per seed group,
+// written as probe rows for the FindMatches tail:
+//   * PairwiseMatchFinder (PairwiseMatchFinder.h:23-33);
+//   * MemHash with enumeration tolerance > 1 (MemHash::EnumerateMatches, MemHash.cpp:139-162,
+//     -> MatchFinder::EnumerateMatches' odometer, MatchFinder.cpp:342-393).
 //
 // PairwiseMatchFinder is a MemHash whose EnumerateMatches (PairwiseMatchFinder.cpp:37-73)
 // hashes, for every masked-key group, each PAIR of genomes that occur exactly once in
@@ -93,6 +97,122 @@ __global__ void pw_emit_kernel(View v, uint64_t N, GenomeTable gt, int L, const 
     }
 }
 
+// ---- enumeration tolerance > 1 -------------------------------------------------------
+constexpr int kEnumMax = 8;   // enum_tol bound of the GPU path (per-genome record slots)
+
+// MemHash::EnumerateMatches over the group at head h (per genome in SML order): per genome the
+// first min(count, enum_tol) records; rejected (false) when a genome has more than
+// repeat_tol + 1 records or the group exceeds MER_REPEAT_LIMIT.  c[g] = kept records of g,
+// pos[g][i] / par[g][i] their positions and strand parities.
+template <typename View>
+__device__ bool en_collect(const View& v, uint64_t h, uint64_t N, const GenomeTable& gt, const MatchParams& mp,
+                           uint32_t (&c)[kMaxG], uint32_t (&pos)[kMaxG][kEnumMax], uint8_t (&par)[kMaxG][kEnumMax],
+                           uint32_t* size) {
+    const uint64_t k0 = v.gkey(h);
+    uint32_t tally[kMaxG];
+    for (int g = 0; g < kMaxG; ++g) { tally[g] = 0; c[g] = 0; }
+    uint32_t n = 0;
+    bool ok = true;
+    // stream order inside a group = (parity, genome, position): restricted to one genome
+    // that is its SortedMerList order (full key, then position)
+    for (uint64_t j = h; j < N && v.gkey(j) == k0; ++j) {
+        if (++n > (uint32_t)kRepeatLimit) break;
+        const RecFields r = v.get(j);
+        const int g = genome_of(gt, r.idx);
+        if (tally[g] < mp.enum_tol) {
+            pos[g][c[g]] = (uint32_t)(r.idx - gt.base[g]);
+            par[g][c[g]] = (uint8_t)r.par;
+            ++c[g];
+        }
+        if (tally[g] > mp.repeat_tol) ok = false;
+        ++tally[g];
+    }
+    *size = n;
+    return ok && n <= (uint32_t)kRepeatLimit;
+}
+
+// AddHashEntry calls of a group: the odometer's combinations (one record per present
+// genome), or the single HashMatch of a two-record list; HashMatch / MaskedMemHash::
+// HashMatch decide whether each combination is added (same genome set for all of them).
+__device__ __forceinline__ uint32_t en_calls(const uint32_t (&c)[kMaxG], int G, const MatchParams& mp, bool* two) {
+    uint32_t total = 0, nid = 0, combos = 1;
+    uint64_t mn = 0;
+    for (int g = 0; g < G; ++g) {
+        total += c[g];
+        mn <<= 1;
+        if (c[g]) { ++nid; combos *= c[g]; mn |= 1; }
+    }
+    *two = total == 2;
+    if (total < 2) return 0;
+    // Multiplicity = genomes present (a two-record list of one genome has 1: no AddHashEntry)
+    const bool add = mp.masked ? (mp.seq_mask == 0 || mn == mp.seq_mask) : nid >= 2;
+    if (!add) return 0;
+    return (total == 2) ? 1u : combos;
+}
+
+template <typename View>
+__global__ void en_count_kernel(View v, uint64_t N, GenomeTable gt, MatchParams mp, uint32_t* __restrict__ ncalls,
+                                DevCounters* __restrict__ ctr) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    uint32_t k = 0;
+    if (pw_head(v, i)) {
+        uint32_t c[kMaxG], pos[kMaxG][kEnumMax], size = 0;
+        uint8_t par[kMaxG][kEnumMax];
+        const bool ok = en_collect(v, i, N, gt, mp, c, pos, par, &size);
+        if (size > (uint32_t)kRepeatLimit) atomicAdd(&ctr->repeat_limit, 1ull);
+        bool two;
+        if (ok && size >= 2) k = en_calls(c, gt.G, mp, &two);
+    }
+    ncalls[i] = k;
+}
+
+template <typename View>
+__global__ void en_emit_kernel(View v, uint64_t N, GenomeTable gt, MatchParams mp, int L,
+                               const uint32_t* __restrict__ ncalls, const uint32_t* __restrict__ off,
+                               int64_t* __restrict__ rows) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N || ncalls[i] == 0) return;
+    const int G = gt.G;
+    uint32_t c[kMaxG], pos[kMaxG][kEnumMax], size = 0;
+    uint8_t par[kMaxG][kEnumMax];
+    (void)en_collect(v, i, N, gt, mp, c, pos, par, &size);
+    bool two;
+    const uint32_t K = en_calls(c, G, mp, &two);
+    uint64_t o = off[i];
+    for (uint32_t t = 0; t < K; ++t) {
+        int64_t sv[kMaxG];
+        uint32_t pv[kMaxG];
+        for (int g = 0; g < G; ++g) { sv[g] = 0; pv[g] = 0; }
+        if (two) {   // HashMatch of the two listed records (MatchFinder.cpp:344-347)
+            for (int g = 0; g < G; ++g)
+                for (uint32_t q = 0; q < c[g]; ++q) { sv[g] = (int64_t)pos[g][q] + 1; pv[g] = par[g][q]; }
+        } else {     // odometer: the last genome varies fastest (MatchFinder.cpp:371-390)
+            uint32_t rem = t;
+            for (int g = G - 1; g >= 0; --g) {
+                if (!c[g]) continue;
+                const uint32_t q = rem % c[g];
+                rem /= c[g];
+                sv[g] = (int64_t)pos[g][q] + 1;
+                pv[g] = par[g][q];
+            }
+        }
+        // SetDirection (MemHash.cpp:189-203) + CalculateOffset (MatchHashEntry.cpp:141-160)
+        int ref = -1;
+        for (int g = 0; g < G && ref < 0; ++g)
+            if (sv[g] != 0) ref = g;
+        int64_t offset = 0;
+        for (int g = ref + 1; g < G; ++g) {
+            if (sv[g] == 0) continue;
+            if (pv[g] != pv[ref]) sv[g] = -sv[g];
+            offset += sv[g] - sv[ref] - (sv[g] < 0 ? (int64_t)L : 0);
+        }
+        int64_t* row = rows + (o + t) * (uint64_t)(G + 1);
+        for (int g = 0; g < G; ++g) row[g] = sv[g];
+        row[G] = offset;
+    }
+}
+
 inline dim3 grid_of(uint64_t n) { return dim3((unsigned)((n + 255) / 256)); }
 
 }  // namespace
@@ -113,10 +233,30 @@ hipError_t launch_pairwise_emit(View v, uint64_t N, const GenomeTable& gt, int L
     return hipGetLastError();
 }
 
+template <typename View>
+hipError_t launch_enum_count(View v, uint64_t N, const GenomeTable& gt, const MatchParams& mp, uint32_t* ncalls,
+                             void* ctr, hipStream_t st) {
+    if (N == 0) return hipSuccess;
+    hipLaunchKernelGGL(en_count_kernel<View>, grid_of(N), dim3(256), 0, st, v, N, gt, mp, ncalls, (DevCounters*)ctr);
+    return hipGetLastError();
+}
+
+template <typename View>
+hipError_t launch_enum_emit(View v, uint64_t N, const GenomeTable& gt, const MatchParams& mp, int L,
+                            const uint32_t* ncalls, const uint32_t* off, int64_t* rows, hipStream_t st) {
+    if (N == 0) return hipSuccess;
+    hipLaunchKernelGGL(en_emit_kernel<View>, grid_of(N), dim3(256), 0, st, v, N, gt, mp, L, ncalls, off, rows);
+    return hipGetLastError();
+}
+
 #define MUMS_INST_PW(V)                                                                                             \
     template hipError_t launch_pairwise_count<V>(V, uint64_t, const GenomeTable&, uint32_t*, void*, hipStream_t);   \
     template hipError_t launch_pairwise_emit<V>(V, uint64_t, const GenomeTable&, int, const uint32_t*,              \
-                                                const uint32_t*, int64_t*, hipStream_t);
+                                                const uint32_t*, int64_t*, hipStream_t);                            \
+    template hipError_t launch_enum_count<V>(V, uint64_t, const GenomeTable&, const MatchParams&, uint32_t*, void*, \
+                                             hipStream_t);                                                          \
+    template hipError_t launch_enum_emit<V>(V, uint64_t, const GenomeTable&, const MatchParams&, int,               \
+                                            const uint32_t*, const uint32_t*, int64_t*, hipStream_t);
 MUMS_INST_PW(PairView<uint32_t>)
 MUMS_INST_PW(PairView<uint64_t>)
 
