@@ -103,6 +103,7 @@ struct mums_ctx {
     uint32_t slice_genome = 0;
     uint64_t slice_begin = 0, slice_end = 0;
     int rec_ib = 32;          // index bits of the packed records (33: > 2^32 seed-mers)
+    bool merge_chunked = false;   // the last shard merge ran in key chunks (probe exports: last chunk only)
 
     // state of the last run
     int stage_done = 0;
@@ -429,8 +430,10 @@ int ensure_merge_space(mums_ctx* ctx, uint64_t n, int mb, int key_bits, ProbeSpa
 // are in ctx->mstart -> stable sort on record key bits [32, 32 + key_bits) inside every
 // bucket (the merged SortedMerList stream) -> equal-key groups -> accepted probes in key order.
 int merge_stage(mums_ctx* ctx, uint64_t n, int mb, int key_bits, const MatchParams& mp, const ProbeSpace& ps,
-                hipStream_t st, int ib = 32) {
+                hipStream_t st, int ib = 32, uint64_t* rA = nullptr, uint64_t* rB = nullptr) {
     DevCounters* dc = ctx->counters.as<DevCounters>();
+    if (!rA) rA = ctx->recA.as<uint64_t>();
+    if (!rB) rB = ctx->recB.as<uint64_t>();
     SegTile* tiles = ctx->tiles.as<SegTile>();
     const uint32_t* bstart = ctx->mstart.as<uint32_t>();
     const uint64_t ub = seg_tiles_upper(n, mb);
@@ -440,13 +443,12 @@ int merge_stage(mums_ctx* ctx, uint64_t n, int mb, int key_bits, const MatchPara
     if (ib != 32 && !(n < (1ull << 30) && key_bits <= 32))
         return fail(ctx, MUMS_E_UNSUPPORTED, "33-bit records need < 2^30 records per merge");
     if (ctx->use_onesweep && n < (1ull << 30) && key_bits <= 32)
-        HIPCHK(seg_onesweep_sort(ctx->recA.as<uint64_t>(), ctx->recB.as<uint64_t>(), n, key_bits, mb, bstart,
-                                 ctx->tmp.p, &dc->err, &buf, st, prof ? ctx->ev_ds : nullptr, ib));
+        HIPCHK(seg_onesweep_sort(rA, rB, n, key_bits, mb, bstart, ctx->tmp.p, &dc->err, &buf, st,
+                                 prof ? ctx->ev_ds : nullptr, ib));
     else
-        HIPCHK(seg_radix_sort(ctx->recA.as<uint64_t>(), ctx->recB.as<uint64_t>(), n, key_bits, tiles, ub, ctx->tmp.p,
-                              &buf, st, prof ? ctx->ev_ds : nullptr));
+        HIPCHK(seg_radix_sort(rA, rB, n, key_bits, tiles, ub, ctx->tmp.p, &buf, st, prof ? ctx->ev_ds : nullptr));
     ctx->sorted_buf = buf;
-    ctx->sorted_rec = buf ? ctx->recB.as<uint64_t>() : ctx->recA.as<uint64_t>();
+    ctx->sorted_rec = buf ? rB : rA;
     ctx->sort_passes = (key_bits + 7) / 8;
     HIPCHK(hipEventRecord(ctx->ev[EV_SORT], st));
     if (ib == 33)
@@ -1429,13 +1431,47 @@ int mums_shard_merge(mums_ctx* ctx, const uint64_t* d_records, uint32_t nsources
     HIPCHK(hipEventRecord(ctx->ev[EV_KEYS], st));
     MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, ctx->masked, ctx->seq_mask};
     ctx->N = n;
-    rc = merge_stage(ctx, n, mb, 2 * ctx->w + 1 - B, mp, ps, st, ctx->rec_ib);
-    if (rc) return rc;
-    rc = finish_seeds(ctx, ps, st);
-    if (rc) return rc;
+    // a key range above one onesweep merge (2^30 records: BASELINE config 5 on 2 or 4 GPUs)
+    // is merged in chunks of consecutive buckets, in key order (seed-stage counts only)
+    uint64_t cap = (1ull << 30) - 4096;
+    if (const char* e = getenv("MUMS_DEV_CHUNK_RECORDS")) cap = std::min<uint64_t>(cap, strtoull(e, nullptr, 10));
+    ctx->merge_chunked = n >= cap;
+    uint64_t P_total = 0, groups = 0;
+    if (!ctx->merge_chunked) {
+        rc = merge_stage(ctx, n, mb, 2 * ctx->w + 1 - B, mp, ps, st, ctx->rec_ib);
+        if (rc) return rc;
+        rc = finish_seeds(ctx, ps, st);
+        if (rc) return rc;
+    } else {
+        const uint32_t nbk = 1u << mb;
+        uint32_t b0 = 0;
+        while (b0 < nbuckets) {
+            uint32_t b1 = b0;
+            while (b1 < nbuckets && (uint64_t)bst[b1 + 1] - bst[b0] < cap) ++b1;
+            if (b1 == b0) return fail(ctx, MUMS_E_UNSUPPORTED, "one MSD bucket holds more than 2^30 records");
+            const uint64_t o = bst[b0], nc = (uint64_t)bst[b1] - o;
+            std::vector<uint32_t> sub(nbk + 1);
+            for (uint32_t b = 0; b <= nbk; ++b)
+                sub[b] = b < b0 ? 0u : (b < b1 ? (uint32_t)(bst[b] - o) : (uint32_t)nc);
+            HIPCHK(hipMemcpy(ctx->mstart.p, sub.data(), sub.size() * 4, hipMemcpyHostToDevice));
+            rc = merge_stage(ctx, nc, mb, 2 * ctx->w + 1 - B, mp, ps, st, ctx->rec_ib, ctx->recA.as<uint64_t>() + o,
+                             ctx->recB.as<uint64_t>() + o);
+            if (rc) return rc;
+            rc = finish_seeds(ctx, ps, st);
+            if (rc) return rc;
+            P_total += ctx->P;
+            groups += ctx->hc.ngroups;
+            b0 = b1;
+        }
+    }
     ctx->stage_done = MUMS_STAGE_SEEDS;
     HIPCHK(hipStreamSynchronize(st));
     fill_stats(ctx, n);
+    if (ctx->merge_chunked) {
+        ctx->P = P_total;
+        ctx->st.probes = P_total;
+        ctx->st.groups = groups;
+    }
     float rg = 0.f;
     (void)hipEventElapsedTime(&rg, ctx->ev[EV_START], ctx->ev[EV_KEYS]);
     ctx->st.ms_sort += rg;                 // the regroup copy is part of the merge's sort
@@ -1453,6 +1489,8 @@ int mums_probe_count(mums_ctx* ctx, uint64_t* count) {
 int mums_probe_copy(mums_ctx* ctx, uint32_t* buckets, uint64_t* ref_index, uint64_t capacity) {
     if (check_ctx(ctx)) return MUMS_E_INVALID;
     if (ctx->stage_done < MUMS_STAGE_SEEDS) return fail(ctx, MUMS_E_INVALID, "no seed stage run");
+    if (ctx->shard && ctx->merge_chunked)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "probe export after a chunked shard merge");
     if (capacity < ctx->P) return fail(ctx, MUMS_E_INVALID, "output buffer too small");
     if (!ctx->packed_path) return fail(ctx, MUMS_E_UNSUPPORTED, "probe export needs the packed-record path");
     const uint64_t P = ctx->P, N = ctx->N;
@@ -1486,6 +1524,8 @@ int shard_seeds_done(mums_ctx* ctx) {
     if (check_ctx(ctx)) return MUMS_E_INVALID;
     if (!ctx->shard) return fail(ctx, MUMS_E_INVALID, "not a sharded context (mums_shard_layout)");
     if (ctx->stage_done < MUMS_STAGE_SEEDS) return fail(ctx, MUMS_E_INVALID, "no sharded seed stage run");
+    if (ctx->merge_chunked)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "sharded FindMatches after a chunked merge (> 2^30 records per rank)");
     return MUMS_OK;
 }
 

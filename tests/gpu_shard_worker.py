@@ -39,8 +39,11 @@ def main():
         local = [torch.frombuffer(bytearray(s), dtype=torch.uint8).to(dev) for s in seqs[first:first + count]]
         eng = HipShardEngine(0, seed, lens, first, local)
     ShardedSeedStage(eng).run()
-    b, r = eng.probes()
     st = eng.stats()
+    if os.environ.get("MUMS_DEV_CHUNK_RECORDS"):   # chunked merge: counts only (no probe export)
+        b, r = np.zeros(0, dtype=np.uint32), np.zeros(0, dtype=np.uint64)
+    else:
+        b, r = eng.probes()
     np.save(os.path.join(outdir, f"b{rank}.npy"), b)
     np.save(os.path.join(outdir, f"r{rank}.npy"), r)
     np.save(os.path.join(outdir, f"s{rank}.npy"), np.array([st["seedmers"], st["probes"], st["groups"]]))

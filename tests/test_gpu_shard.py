@@ -83,6 +83,26 @@ def test_sharded_slices_gpu(oracle_mod, G, n, p, w, world, ib33):
     assert np.array_equal(r, orf)
 
 
+@pytest.mark.parametrize("G,n,p,w,world", [(2, 400_000, 0.02, 19, 2), (2, 300_000, 0.03, 19, 4)])
+def test_sharded_slices_chunked_merge_gpu(oracle_mod, G, n, p, w, world):
+    """A rank's key range above one onesweep merge (BASELINE config 5 on 2 or 4 GPUs: > 2^30
+    records per rank) is merged in bucket chunks; forced small here (MUMS_DEV_CHUNK_RECORDS),
+    with 33-bit records: the ranks' probe counts add up to the oracle's."""
+    seqs = oracle_mod.generate(G, n, p, 4242 + G)
+    _, _, st = oracle_mod.seed_probes(seqs, oracle_mod.get_seed(w))
+    with tempfile.TemporaryDirectory() as d:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+               "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+               os.path.join(ROOT, "tests", "gpu_shard_worker.py"), d, str(G), str(n), str(p), str(w), "slices"]
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MUMS_DEV_SHARD_IB33="1",
+                   MUMS_DEV_CHUNK_RECORDS=str(n // 3))
+        res = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+        assert res.returncode == 0, res.stderr[-3000:]
+        s = [np.load(os.path.join(d, f"s{r}.npy")) for r in range(world)]
+    assert sum(int(x[0]) for x in s) == st["seedmers"]
+    assert sum(int(x[1]) for x in s) == st["probes"]
+
+
 @pytest.mark.parametrize("G,n,p,w,world,T", [(4, 300_000, 0.02, 15, 2, 40000), (3, 200_000, 0.05, 19, 3, 40000),
                                                (5, 100_000, 1.0, 15, 2, 40000), (4, 200_000, 0.01, 15, 3, 7)])
 def test_sharded_find_matches_gpu(oracle_mod, G, n, p, w, world, T):
