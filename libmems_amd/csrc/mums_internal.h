@@ -25,7 +25,10 @@ namespace mums {
 constexpr int kMaxG = 32;            // genomes per context (register arrays in the replay)
 constexpr int kRepeatLimit = 1000;   // MER_REPEAT_LIMIT, MatchFinder.cpp:166
 constexpr int kBlock = 256;          // threads per workgroup (4 waves of 64)
-constexpr int kSeedTile = 4096;      // positions per key-kernel workgroup
+#ifndef MUMS_SEED_TILE
+#define MUMS_SEED_TILE 4096
+#endif
+constexpr int kSeedTile = MUMS_SEED_TILE;  // positions per key-kernel workgroup
 #ifndef MUMS_SEG_TILE
 #define MUMS_SEG_TILE 4096
 #endif

@@ -18,6 +18,8 @@
 //                        wave64 ballot match-any, reorders through LDS and writes
 //                        (ckey_low << 32 | index) records into their buckets.
 // HBM bytes per seed-mer: pack 1 + 0.25 (packed path) ; scatter 0.25 + 8.
+#include <type_traits>
+
 #include "seed_device.h"
 
 namespace mums {
@@ -140,21 +142,27 @@ __global__ __launch_bounds__(kBlock) void seed_pack_kernel(SeedSpec ss, GenomeTa
 // every record is kept and lands at cbase[digit >> cbits_low] + its offset inside its
 // chunk (hist = all slices, each scanned on its own: 32-bit offsets inside a chunk).
 template <int kMaxDig, uint64_t PAT = 0, int IB = 32, bool kChunk = false>
-__global__ __launch_bounds__(kBlock) void seed_scatter_kernel(SeedSpec ss, GenomeTable gt,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void seed_scatter_kernel(SeedSpec ss, GenomeTable gt,
                                                               const uint32_t* __restrict__ packed, int msd_bits,
                                                               const uint32_t* __restrict__ hist, uint32_t T,
                                                               uint64_t* __restrict__ rec, uint32_t dlo = 0,
                                                               uint32_t nbc = 0,
                                                               const uint64_t* __restrict__ cbase = nullptr,
                                                               int mb = 0) {
-    __shared__ uint32_t words[kTileWords];
+    // LDS (<= 40 KB at kMaxDig 256, four blocks per CU): the packed words alias the
+    // record staging area (read only before the records are placed), wave digit
+    // offsets are 16-bit (<= kTile) and fold in the block-local digit starts, and gofs
+    // folds in minus those starts (u32 arithmetic: the sum is < 2^32).
+    using DigT = typename std::conditional<(kMaxDig <= 256), uint8_t, uint16_t>::type;
     __shared__ uint64_t srec[kTile];
-    __shared__ uint16_t sdig[kTile];
-    __shared__ uint32_t wcnt[kWaves][kMaxDig];
-    __shared__ uint32_t lstart[kMaxDig];
+    __shared__ DigT sdig[kTile];
+    __shared__ uint16_t wcnt[kWaves][kMaxDig];
     __shared__ uint32_t gofs[kMaxDig];
     __shared__ uint32_t s_w[kWaves];
     __shared__ uint32_t s_kept;
+    static_assert(kTileWords * 4 <= kTile * 8, "words alias srec");
+    static_assert(kTile <= 65535, "16-bit wave digit offsets");
+    uint32_t* words = reinterpret_cast<uint32_t*>(srec);
     const uint32_t t = blockIdx.x;
     const int g = tile_genome(gt, t);
     const uint32_t x = t - gt.tfirst[g];
@@ -166,7 +174,7 @@ __global__ __launch_bounds__(kBlock) void seed_scatter_kernel(SeedSpec ss, Genom
     const int nd = (kChunk && !all_chunks) ? (int)nbc : (1 << msd_bits);
     if (kChunk && tid == 0) s_kept = 0;
     const int klow = 2 * ss.w + 1 - msd_bits;
-    const uint64_t lmask = (klow >= 64) ? ~0ull : ((1ull << klow) - 1);
+    const uint64_t lmask = (klow >= 64) ? ~0ull : ((1ull << klow) - 1);   // klow <= 64 - IB
     const uint64_t pw = packed_words(gt.n[g]);
     const uint32_t* W = packed + gt.woff[g];
     for (int k = tid; k < kTileWords; k += kBlock) {
@@ -178,8 +186,9 @@ __global__ __launch_bounds__(kBlock) void seed_scatter_kernel(SeedSpec ss, Genom
 
     const uint64_t base = gt.base[g];
     const int q0 = wv * (kTile / kWaves);
-    uint64_t r_rec[kPerThread];
-    uint32_t r_dig[kPerThread], r_rank[kPerThread];
+    // the record's key part (<= 64 - IB <= 32 bits); its index part is base + p0 + q
+    uint32_t r_key[kPerThread];
+    uint32_t r_pk[kPerThread];   // wave rank << 16 | digit; ~0 = not stored
     #pragma unroll
     for (int r = 0; r < kPerThread; ++r) {
         const int q = q0 + r * 64 + lane;
@@ -195,30 +204,32 @@ __global__ __launch_bounds__(kBlock) void seed_scatter_kernel(SeedSpec ss, Genom
             valid = valid && d < nbc;
             d = valid ? d : 0u;
         }
-        r_rec[r] = ((kv & lmask) << IB) | (base + p);
-        r_dig[r] = d;
+        r_key[r] = (uint32_t)(kv & lmask);
         uint32_t tot;
         // digits are < 2^msd_bits <= kMaxDig: the unused high bits rank as equal
         const uint32_t rk = wave_match_rank<(kMaxDig > 256 ? kMaxMsdBits : 8)>(d, valid, &tot);
         uint32_t old = 0;
         if (valid) old = wcnt[wv][d];
-        if (valid && rk == 0) wcnt[wv][d] = old + tot;
-        r_rank[r] = valid ? old + rk : 0xFFFFFFFFu;   // invalid: not stored
+        if (valid && rk == 0) wcnt[wv][d] = (uint16_t)(old + tot);
+        r_pk[r] = valid ? (((old + rk) << 16) | d) : 0xFFFFFFFFu;
     }
     __syncthreads();
-    // per-digit wave offsets, block-local digit starts (each thread owns nd/256 digits)
+    // per-digit wave offsets + block-local digit starts (each thread owns nd/256 digits)
     {
+        constexpr int kPer = (kMaxDig + kBlock - 1) / kBlock;
         const int per = (nd + kBlock - 1) / kBlock;
+        uint32_t dt[kPer];
         uint32_t tot_mine = 0;
-        for (int k = 0; k < per; ++k) {
+        #pragma unroll
+        for (int k = 0; k < kPer; ++k) {
             const int d = tid * per + k;
-            if (d >= nd) break;
+            dt[k] = 0;
+            if (k >= per || d >= nd) continue;
             uint32_t acc = 0;
             #pragma unroll
-            for (int w = 0; w < kWaves; ++w) { const uint32_t c = wcnt[w][d]; wcnt[w][d] = acc; acc += c; }
-            lstart[d] = acc;  // temporarily the digit total
+            for (int w = 0; w < kWaves; ++w) { const uint32_t c = wcnt[w][d]; wcnt[w][d] = (uint16_t)acc; acc += c; }
+            dt[k] = acc;
             tot_mine += acc;
-            gofs[d] = hist[(uint64_t)d * T + t];
         }
         if (kChunk && tot_mine) atomicAdd(&s_kept, tot_mine);
         uint32_t v = tot_mine;
@@ -232,23 +243,25 @@ __global__ __launch_bounds__(kBlock) void seed_scatter_kernel(SeedSpec ss, Genom
         uint32_t pre = v - tot_mine;
         #pragma unroll
         for (int w = 0; w < kWaves; ++w) pre += (w < wv) ? s_w[w] : 0u;
-        for (int k = 0; k < per; ++k) {
+        #pragma unroll
+        for (int k = 0; k < kPer; ++k) {
             const int d = tid * per + k;
-            if (d >= nd) break;
-            const uint32_t c = lstart[d];
-            lstart[d] = pre;
-            pre += c;
+            if (k >= per || d >= nd) continue;
+            #pragma unroll
+            for (int w = 0; w < kWaves; ++w) wcnt[w][d] = (uint16_t)(wcnt[w][d] + pre);
+            gofs[d] = hist[(uint64_t)d * T + t] - pre;
+            pre += dt[k];
         }
     }
     __syncthreads();
     #pragma unroll
     for (int r = 0; r < kPerThread; ++r) {
-        const uint64_t p = p0 + (uint64_t)(q0 + r * 64 + lane);
-        if (p < m && (!kChunk || r_rank[r] != 0xFFFFFFFFu)) {
-            const uint32_t d = r_dig[r];
-            const uint32_t lp = lstart[d] + wcnt[wv][d] + r_rank[r];
-            srec[lp] = r_rec[r];
-            sdig[lp] = (uint16_t)d;
+        const uint32_t pk = r_pk[r];
+        if (pk != 0xFFFFFFFFu) {
+            const uint32_t d = pk & 0xFFFFu;
+            const uint32_t lp = (uint32_t)wcnt[wv][d] + (pk >> 16);
+            srec[lp] = ((uint64_t)r_key[r] << IB) | (base + p0 + (uint64_t)(q0 + r * 64 + lane));
+            sdig[lp] = (DigT)d;
         }
     }
     __syncthreads();
@@ -259,7 +272,7 @@ __global__ __launch_bounds__(kBlock) void seed_scatter_kernel(SeedSpec ss, Genom
         if (s < cnt) {
             const uint32_t d = sdig[s];
             const uint64_t b = (kChunk && all_chunks) ? cbase[d >> mb] : 0ull;
-            rec[b + (uint64_t)gofs[d] + (s - lstart[d])] = srec[s];
+            rec[b + (uint64_t)(uint32_t)(gofs[d] + s)] = srec[s];
         }
     }
 }
