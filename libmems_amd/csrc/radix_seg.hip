@@ -253,6 +253,10 @@ constexpr uint32_t kFlagAgg = 1u << 30;
 constexpr uint32_t kFlagInc = 2u << 30;
 constexpr uint32_t kValMask = (1u << 30) - 1;
 constexpr int kGhistTilesPerBlock = 16;
+#ifndef MUMS_GHIST_BATCH
+#define MUMS_GHIST_BATCH 8
+#endif
+constexpr int kGhistBatch = MUMS_GHIST_BATCH;   // records per lane loaded as one batch
 
 __global__ __launch_bounds__(kBlock) void seg_ghist_kernel(const uint64_t* __restrict__ rec,
                                                            const SegTile* __restrict__ tiles, uint64_t ntiles_ub,
@@ -280,9 +284,20 @@ __global__ __launch_bounds__(kBlock) void seg_ghist_kernel(const uint64_t* __res
             }
             cur_b = d.bucket;
         }
-        for (uint32_t q = tid; q < d.count; q += kBlock) {
-            const uint64_t key = rec[d.start + q] >> key_shift;
-            for (int p = 0; p < npass; ++p) atomicAdd(&h[p][(uint32_t)(key >> (8 * p)) & 0xFFu], 1u);
+        // kGhistBatch loads in flight per lane before the LDS counting
+        for (uint32_t q0 = 0; q0 < d.count; q0 += kBlock * kGhistBatch) {
+            uint64_t kk[kGhistBatch];
+            #pragma unroll
+            for (int u = 0; u < kGhistBatch; ++u) {
+                const uint32_t q = q0 + u * kBlock + tid;
+                kk[u] = q < d.count ? rec[d.start + q] : 0ull;
+            }
+            #pragma unroll
+            for (int u = 0; u < kGhistBatch; ++u) {
+                if (q0 + u * kBlock + tid >= d.count) break;
+                const uint64_t key = kk[u] >> key_shift;
+                for (int p = 0; p < npass; ++p) atomicAdd(&h[p][(uint32_t)(key >> (8 * p)) & 0xFFu], 1u);
+            }
         }
     }
     __syncthreads();
