@@ -91,6 +91,28 @@ __device__ __forceinline__ uint64_t ckey_of(uint64_t mer, const SeedSpec& ss) {
     else return ckey_from_mer(mer, ss);
 }
 
+// Top K bits of the (2w+1)-bit canonical key of a static pattern, without building the
+// key: ckey = min(v, rc) << 1 | parity, so its top K bits are the top K bits of
+// min(v, rc) = min(top_K(v), top_K(rc)) (the minimum of two equal-width integers has the
+// smaller prefix).  top_K(v) needs only the runs under v's top K bits, top_K(rc) only
+// v's low ceil(K/2) bases (complemented, base order reversed); the constant run masks
+// let the compiler drop every other run.  Used for the MSD histogram of the keys pass.
+template <uint64_t PAT, int K>
+__device__ __forceinline__ uint32_t ckey_top_static(uint64_t mer) {
+    constexpr SeedRuns R = seed_runs(PAT);
+    constexpr int B = (K + 1) / 2;
+    static_assert(K >= 1 && 2 * B <= 2 * R.w && 2 * B <= 32, "top digit wider than the seed");
+    uint64_t v = 0;
+    #pragma unroll
+    for (int r = 0; r < R.n; ++r) v |= (R.sh[r] >= 0 ? (mer >> R.sh[r]) : (mer << -R.sh[r])) & R.mask[r];
+    const uint32_t ft = (uint32_t)(v >> (2 * R.w - K));
+    const uint32_t lowc = ~(uint32_t)v & (uint32_t)((1ull << (2 * B)) - 1);
+    uint32_t rr = __builtin_bitreverse32(lowc) >> (32 - 2 * B);
+    rr = ((rr >> 1) & 0x55555555u) | ((rr & 0x55555555u) << 1);
+    const uint32_t rt = rr >> (2 * B - K);
+    return ft < rt ? ft : rt;
+}
+
 // the patterns with compiled-in run tables (getSeed(15), getSeed(19): SeedMasks.h)
 constexpr uint64_t kSeedW15 = 0x7ac9afull;
 constexpr uint64_t kSeedW19 = 0x7b974efull;

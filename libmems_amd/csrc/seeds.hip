@@ -35,6 +35,11 @@ constexpr int kWaves = kBlock / 64;
 
 struct AsciiPtrs { const char* p[kMaxG]; };
 
+// MSD bits of the default split for a static pattern: 2w + 1 - 32 (0 when the key fits
+// the record); the keys pass builds only this top digit
+template <uint64_t PAT>
+constexpr int kStaticMsd = PAT == 0 ? 0 : (2 * seed_runs(PAT).w + 1 > 32 ? 2 * seed_runs(PAT).w + 1 - 32 : 0);
+
 // BasicDNATable (SortedMerList.cpp:29-47): c,b,y->1  g,s,k->2  t->3 (either case), else 0.
 __device__ __forceinline__ uint32_t dna2(uint32_t c) {
     const uint32_t lc = c | 0x20u;
@@ -119,6 +124,23 @@ __global__ __launch_bounds__(kBlock) void seed_pack_kernel(SeedSpec ss, GenomeTa
     if (kMode == 1 && nb <= 1) return;   // no MSD split: the scatter pass derives the keys
     const uint64_t base = gt.base[g];
     const int klow = 2 * ss.w + 1 - msd_bits;
+    if constexpr (kMode == 1 && PAT != 0 && kStaticMsd<PAT> >= 1 && kStaticMsd<PAT> <= kMaxMsdBits) {
+        if (msd_bits == kStaticMsd<PAT>) {   // the default split: top digit only
+            #pragma unroll 4
+            for (int j = 0; j < kPerThread; ++j) {
+                const int q = tid + j * kBlock;
+                const uint64_t p = p0 + (uint64_t)q;
+                if (p >= m) break;
+                const int wi = q >> 4, sh = 2 * (q & 15);
+                const uint64_t hi = ((uint64_t)words[wi] << 32) | words[wi + 1];
+                const uint64_t lo = words[wi + 2];
+                atomicAdd(&bh[ckey_top_static<PAT, kStaticMsd<PAT>>((hi << sh) | ((lo << sh) >> 32))], 1u);
+            }
+            __syncthreads();
+            for (int i = tid; i < nb; i += kBlock) hist[(uint64_t)i * T + t] = bh[i];
+            return;
+        }
+    }
     #pragma unroll 4
     for (int j = 0; j < kPerThread; ++j) {
         const int q = tid + j * kBlock;
@@ -141,6 +163,10 @@ __global__ __launch_bounds__(kBlock) void seed_pack_kernel(SeedSpec ss, GenomeTa
 // lies in [dlo, dlo + nbc) (hist = that digit range's scanned slice); with cbase != null
 // every record is kept and lands at cbase[digit >> cbits_low] + its offset inside its
 // chunk (hist = all slices, each scanned on its own: 32-bit offsets inside a chunk).
+// four waves per SIMD for the <= 256-digit forms (the 2^11-digit development form
+// cannot reach it: its LDS alone allows two blocks per CU)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wpass-failed"
 template <int kMaxDig, uint64_t PAT = 0, int IB = 32, bool kChunk = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void seed_scatter_kernel(SeedSpec ss, GenomeTable gt,
                                                               const uint32_t* __restrict__ packed, int msd_bits,
@@ -276,6 +302,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         }
     }
 }
+
+#pragma clang diagnostic pop
 
 // B == 0: one bucket, records land at their global index
 template <uint64_t PAT = 0>
