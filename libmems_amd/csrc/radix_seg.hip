@@ -41,6 +41,9 @@ constexpr int kSortTile = MUMS_SORT_TILE;      // records per onesweep tile (lon
 #ifndef MUMS_OS_LATEPUB
 #define MUMS_OS_LATEPUB 0   // 1: publish the tile aggregate after ranking (no early per-digit atomics)
 #endif
+#ifndef MUMS_OS_NEXTHIST
+#define MUMS_OS_NEXTHIST 0  // 1: pass p counts the pass-(p+1) digits (the histogram read covers digit 0 only)
+#endif
 #ifndef MUMS_OS_FUSED
 #define MUMS_OS_FUSED 0     // 1: fold lstart into the per-wave bases and the output offsets
 #endif
@@ -260,7 +263,8 @@ constexpr int kGhistBatch = MUMS_GHIST_BATCH;   // records per lane loaded as on
 
 __global__ __launch_bounds__(kBlock) void seg_ghist_kernel(const uint64_t* __restrict__ rec,
                                                            const SegTile* __restrict__ tiles, uint64_t ntiles_ub,
-                                                           int npass, uint32_t* __restrict__ ghist, int key_shift) {
+                                                           int npass, uint32_t* __restrict__ ghist, int key_shift,
+                                                           int nh) {
     __shared__ uint32_t h[4][kDigits];
     const int tid = threadIdx.x;
     const uint64_t t0 = (uint64_t)blockIdx.x * kGhistTilesPerBlock;
@@ -275,7 +279,7 @@ __global__ __launch_bounds__(kBlock) void seg_ghist_kernel(const uint64_t* __res
         if (d.bucket != cur_b) {
             if (cur_b != 0xFFFFFFFFu) {
                 __syncthreads();
-                for (int p = 0; p < npass; ++p) {
+                for (int p = 0; p < nh; ++p) {
                     const uint32_t v = h[p][tid];
                     if (v) atomicAdd(&ghist[((uint64_t)cur_b * npass + p) * kDigits + tid], v);
                     h[p][tid] = 0;
@@ -296,13 +300,13 @@ __global__ __launch_bounds__(kBlock) void seg_ghist_kernel(const uint64_t* __res
             for (int u = 0; u < kGhistBatch; ++u) {
                 if (q0 + u * kBlock + tid >= d.count) break;
                 const uint64_t key = kk[u] >> key_shift;
-                for (int p = 0; p < npass; ++p) atomicAdd(&h[p][(uint32_t)(key >> (8 * p)) & 0xFFu], 1u);
+                for (int p = 0; p < nh; ++p) atomicAdd(&h[p][(uint32_t)(key >> (8 * p)) & 0xFFu], 1u);
             }
         }
     }
     __syncthreads();
     if (cur_b != 0xFFFFFFFFu)
-        for (int p = 0; p < npass; ++p) {
+        for (int p = 0; p < nh; ++p) {
             const uint32_t v = h[p][tid];
             if (v) atomicAdd(&ghist[((uint64_t)cur_b * npass + p) * kDigits + tid], v);
         }
@@ -311,9 +315,10 @@ __global__ __launch_bounds__(kBlock) void seg_ghist_kernel(const uint64_t* __res
 // one block per (bucket, pass): dbase = bstart[b] + exclusive scan over digits
 __global__ __launch_bounds__(kBlock) void seg_dbase_kernel(const uint32_t* __restrict__ ghist,
                                                            const uint32_t* __restrict__ bstart, int npass,
-                                                           uint32_t* __restrict__ dbase) {
+                                                           uint32_t* __restrict__ dbase, int pass) {
     __shared__ uint32_t s_w[kWaves];
-    const uint64_t bp = blockIdx.x;
+    // pass < 0: one block per (bucket, pass); else one block per bucket for that pass
+    const uint64_t bp = pass < 0 ? (uint64_t)blockIdx.x : (uint64_t)blockIdx.x * npass + pass;
     const uint32_t b = (uint32_t)(bp / npass);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t v = ghist[bp * kDigits + threadIdx.x];
@@ -351,7 +356,8 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
                                                           const SegTile* __restrict__ tiles, uint32_t nclaims,
                                                           int shift, int pass, int npass,
                                                           const uint32_t* __restrict__ dbase, uint32_t* status,
-                                                          uint32_t* tile_counter, uint32_t* err) {
+                                                          uint32_t* tile_counter, uint32_t* err,
+                                                          uint32_t* __restrict__ ghist_next) {
     constexpr int kT = kIPT * OB;
     constexpr int kW = OB / 64;
     static_assert(OB >= kDigits, "one thread per digit");
@@ -362,10 +368,11 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
     __shared__ uint32_t s_w[kDigits / 64];
     __shared__ uint32_t s_tile;
     __shared__ uint32_t hcnt[kDigits];
+    __shared__ uint32_t hnext[kDigits];   // next pass's digit counts (ghist_next != null)
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     if (tid == 0) s_tile = atomicAdd(tile_counter, 1u);
     for (int i = tid; i < kW * kDigits; i += OB) (&wcnt[0][0])[i] = 0;
-    if (tid < kDigits) hcnt[tid] = 0;
+    if (tid < kDigits) { hcnt[tid] = 0; hnext[tid] = 0; }
     __syncthreads();
     const uint32_t c = __builtin_amdgcn_readfirstlane(s_tile);   // uniform: scalar descriptor loads
     if (c >= nclaims) return;
@@ -397,6 +404,13 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
         __hip_atomic_store(status + (uint64_t)t * kDigits + tid, kFlagAgg | hcnt[tid], __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
 #endif
+    if (ghist_next) {   // uniform: the next pass's histogram rides on this pass's read
+        #pragma unroll
+        for (int r = 0; r < kIPT; ++r) {
+            const uint32_t q = q0 + r * 64 + lane;
+            if (q < d.count) atomicAdd(&hnext[(uint32_t)(key[r] >> (shift + 8)) & 0xFFu], 1u);
+        }
+    }
     #pragma unroll
     for (int r = 0; r < kIPT; ++r) {
         const uint32_t q = q0 + r * 64 + lane;
@@ -515,6 +529,10 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
             rout[o] = k;
 #endif
         }
+    }
+    if (ghist_next && tid < kDigits) {   // hnext complete: barriers since its atomics
+        const uint32_t c = hnext[tid];
+        if (c) atomicAdd(&ghist_next[((uint64_t)d.bucket * npass + pass + 1) * kDigits + tid], c);
     }
 }
 
@@ -800,10 +818,17 @@ hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key
     e = build_seg_tiles_from_starts(d_bstart, msd_bits, n, stiles, counters + 32, btmp, st, kSortTile);
     if (e != hipSuccess) return e;
     const unsigned gblocks = (unsigned)((ub + kGhistTilesPerBlock - 1) / kGhistTilesPerBlock);
+    // the histogram read counts digit 0 only when every later pass's digits are
+    // counted by the pass before it (MUMS_OS_NEXTHIST, plain onesweep kernel)
+    const bool nexthist = MUMS_OS_NEXTHIST && !MUMS_SORT_PERSIST;
     hipLaunchKernelGGL(seg_ghist_kernel, dim3(gblocks), dim3(kBlock), 0, st, recA, stiles, ub, npass, ghist,
-                       key_shift);
-    hipLaunchKernelGGL(seg_dbase_kernel, dim3((unsigned)(nb * npass)), dim3(kBlock), 0, st, ghist, d_bstart, npass,
-                       dbase);
+                       key_shift, nexthist ? 1 : npass);
+    if (nexthist)
+        hipLaunchKernelGGL(seg_dbase_kernel, dim3((unsigned)nb), dim3(kBlock), 0, st, ghist, d_bstart, npass, dbase,
+                           0);
+    else
+        hipLaunchKernelGGL(seg_dbase_kernel, dim3((unsigned)(nb * npass)), dim3(kBlock), 0, st, ghist, d_bstart,
+                           npass, dbase, -1);
 #if MUMS_SORT_PERSIST
     // resident blocks of the persistent pass: occupancy x CUs
     static uint64_t persist_grid = 0;
@@ -828,10 +853,14 @@ hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key
 #else
         hipLaunchKernelGGL((seg_onesweep_kernel<kSortBlock, kSortTile / kSortBlock>), dim3((unsigned)ub),
                            dim3(kSortBlock), 0, st, src, dst, stiles, (uint32_t)ub, key_shift + 8 * p, p, npass,
-                           dbase, status + (uint64_t)p * ub * kDigits, counters + p, d_err);
+                           dbase, status + (uint64_t)p * ub * kDigits, counters + p, d_err,
+                           (nexthist && p + 1 < npass) ? ghist : (uint32_t*)nullptr);
 #endif
         e = hipGetLastError();
         if (e != hipSuccess) return e;
+        if (nexthist && p + 1 < npass)
+            hipLaunchKernelGGL(seg_dbase_kernel, dim3((unsigned)nb), dim3(kBlock), 0, st, ghist, d_bstart, npass,
+                               dbase, p + 1);
         if (ev_ds) (void)hipEventRecord(ev_ds[2 * p + 1], st);
         uint64_t* t = src;
         src = dst;
