@@ -99,3 +99,31 @@ def test_short_and_empty_sequences(oracle_mod):
     assert len(oracle_mod.seed_keys(b"ACGT", seed)) == 0          # SMLLength 0 when n < L
     l, s, st = oracle_mod.find_matches([b"ACGT" * 3, b""], seed)
     assert len(l) == 0 and st["seedmers"] == 0
+
+
+@pytest.mark.parametrize("w", [16, 17, 19, 21, 24])
+def test_top_digit_identity(w):
+    """seeds.hip builds the keys pass's MSD histogram with ckey_top_static (seed_device.h):
+    the top K = 2w+1-32 bits of the canonical key (min(v, rc) << 1 | parity) equal
+    min(top_K(v), top_K(rc)), and top_K(rc) needs only v's low ceil(K/2) bases
+    (complemented, base order reversed).  Checked on random and low-entropy seed values."""
+    K = 2 * w + 1 - 32
+    B = (K + 1) // 2
+    rnd = random.Random(w)
+    for i in range(20000):
+        v = rnd.getrandbits(2 * w)
+        if i % 5 == 0:   # long runs of one base / near-palindromes
+            v = rnd.choice([0, (1 << 2 * w) - 1, int("01" * w, 2), int("10" * w, 2)]) ^ (rnd.getrandbits(4) << rnd.randrange(2 * w - 4))
+        rc = 0
+        for k in range(w):
+            rc = (rc << 2) | (3 - ((v >> (2 * k)) & 3))
+        par = 1 if rc < v else 0
+        ckey = ((rc if par else v) << 1) | par
+        want = ckey >> (2 * w + 1 - K)
+        ft = v >> (2 * w - K)
+        lowc = ~v & ((1 << 2 * B) - 1)
+        rr = 0
+        for k in range(B):   # base k of the low bases lands at base position k from the top
+            rr = (rr << 2) | ((lowc >> (2 * k)) & 3)
+        rt = rr >> (2 * B - K)
+        assert want == min(ft, rt), (w, hex(v))
