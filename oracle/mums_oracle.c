@@ -441,6 +441,7 @@ static void extend_match(const ext_ctx* x, mhe_t* m) {
 /* MemHash table (MemHash.cpp:209-251) and driver                             */
 /* ------------------------------------------------------------------------- */
 typedef struct { uint32_t* v; uint32_t n, cap; } bucket_t;
+typedef struct { uint32_t g; uint32_t pos; uint64_t key; } idmer_t;
 
 #define MER_REPEAT_LIMIT 1000   /* MatchFinder.cpp:166 */
 
@@ -449,7 +450,7 @@ struct oracle_result {
     uint64_t count;
     uint64_t* lengths;
     int64_t* starts;
-    uint64_t mem_count, collision_count, max_group, probes, seedmers, chunks;
+    uint64_t mem_count, collision_count, max_group, probes, seedmers, chunks, restarts;
     uint32_t* plog_bucket;    /* seeds_only: per AddHashEntry call, its bucket ... */
     uint64_t* plog_ref;       /* ... and the global seed-mer index of the probe's first start */
 };
@@ -466,6 +467,7 @@ typedef struct {
     const uint64_t* gbase;    /* global seed-mer index of each genome's position 0 */
     uint32_t* plog_bucket; uint64_t* plog_ref; uint64_t plog_cap;
     int64_t* scratch;         /* G starts of the probe under construction */
+    idmer_t* cm; idmer_t* hl; uint64_t cm_cap;   /* SearchRange's cur_match + hash list */
 } memhash_t;
 
 static uint32_t pool_add(memhash_t* h, const mhe_t* src) {
@@ -540,7 +542,6 @@ static void add_hash_entry(memhash_t* h, mhe_t* p) {
     ++h->mem_count;
 }
 
-typedef struct { uint32_t g; uint32_t pos; uint64_t key; } idmer_t;
 
 /* MemHash::HashMatch MemHash.cpp:167-187 / MaskedMemHash::HashMatch          */
 /* MaskedMemHash.cpp:38-63, SetDirection MemHash.cpp:189-203.                 */
@@ -639,58 +640,147 @@ static void enumerate_pairwise(memhash_t* h, const oracle_params* prm, const idm
         }
 }
 
-/* MatchFinder::SearchRange (MatchFinder.cpp:172-340): G-way merge of the SMLs  */
-/* restricted to index ranges [lo[g], hi[g]) by masked key; a group = every      */
-/* occurrence of one masked key inside the ranges.  compat != 0 adds the         */
-/* MER_REPEAT_LIMIT early return (:215-239) as ParallelMemHash sees it: the      */
-/* return value is ignored (ParallelMemHash.cpp:99), so a group above 1000        */
-/* records ends the chunk unless nothing follows it (the check runs at the top   */
-/* of the next merge iteration, the final group is hashed at :335-336).          */
-static void search_range(memhash_t* h, const oracle_params* prm, int G, bmer_t* const* sml, const uint64_t* lo,
-                         const uint64_t* hi, int compat, oracle_result* res) {
-    uint64_t* idx = (uint64_t*)calloc((size_t)G, sizeof(uint64_t));
-    for (int g = 0; g < G; ++g) idx[g] = lo[g] < hi[g] ? lo[g] : hi[g];
-    uint64_t gcap = 1024;
-    idmer_t* grp = (idmer_t*)malloc(gcap * sizeof(idmer_t));
-    idmer_t* hl = (idmer_t*)malloc(gcap * sizeof(idmer_t));
+/* One group handed to EnumerateMatches (MatchFinder.cpp:242-246, :335-336). */
+static void enumerate_group(memhash_t* h, const oracle_params* prm, idmer_t* grp, uint64_t cnt, idmer_t* hl,
+                            oracle_result* res) {
+    if (cnt > res->max_group) res->max_group = cnt;
+    if (cnt < 2) return;
+    if (prm->pairwise) enumerate_pairwise(h, prm, grp, (int)cnt, hl, h->scratch);
+    else enumerate_matches(h, prm, grp, (int)cnt, hl, h->scratch);
+}
+
+static int sml_find_mer_lit(const bmer_t* v, uint64_t n, int L, uint64_t q, uint64_t* result);
+static int get_breakpoint(int sarI, uint64_t startI, int G, bmer_t* const* sml, const uint64_t* m,
+                          const uint64_t* lens, int L, uint64_t mask, uint64_t* bp);
+
+#define MER_BUFFER_SIZE 10000u   /* MatchFinder.cpp:175 */
+
+/* MatchFinder::SearchRange (MatchFinder.cpp:172-340), literally: per SML a buffer   */
+/* of MER_BUFFER_SIZE entries read from start_points + mer_baseindex                 */
+/* (MemorySML::Read, MemorySML.cpp:62-82); cur_mers = the list of buffer heads by    */
+/* masked key (initial std::list::sort is stable; a new head goes before the first   */
+/* head whose key is >= its own, :320-332); cur_match = the records of the current   */
+/* key collected head by head (:281-291).  The MER_REPEAT_LIMIT check runs at the    */
+/* top of every iteration (:253-277): with more than 1000 records collected for the  */
+/* current key the group is dropped, start_points are moved to the GetBreakpoint     */
+/* positions of the next key (never backwards, genomes before seqI exhausted) and 0  */
+/* is returned (FindMatchSeeds calls again).  Returns 1 when the merge completes.    */
+static int search_range_lit(memhash_t* h, const oracle_params* prm, int G, bmer_t* const* sml, const uint64_t* m,
+                            const uint64_t* lens, uint64_t* start_points, const uint64_t* search_len,
+                            oracle_result* res) {
+    if (G < 1) return 1;
     const uint64_t mask = h->x.seed_mask;
-    for (;;) {
-        int have = 0; uint64_t mn = 0;
-        for (int g = 0; g < G; ++g) {
-            if (idx[g] < hi[g]) {
-                uint64_t k = sml[g][idx[g]].key & mask;
-                if (!have || k < mn) { mn = k; have = 1; }
-            }
-        }
-        if (!have) break;
-        uint64_t cnt = 0;
-        for (int g = 0; g < G; ++g) {
-            while (idx[g] < hi[g] && (sml[g][idx[g]].key & mask) == mn) {
-                if (cnt == gcap) {
-                    gcap *= 2;
-                    grp = (idmer_t*)realloc(grp, gcap * sizeof(idmer_t));
-                    hl = (idmer_t*)realloc(hl, gcap * sizeof(idmer_t));
-                }
-                grp[cnt].g = (uint32_t)g;
-                grp[cnt].pos = sml[g][idx[g]].pos;
-                grp[cnt].key = sml[g][idx[g]].key;
-                ++cnt; ++idx[g];
-            }
-        }
-        if (cnt > res->max_group) res->max_group = cnt;
-        if (compat && cnt > MER_REPEAT_LIMIT) {
-            int more = 0;
-            for (int g = 0; g < G; ++g) more |= idx[g] < hi[g];
-            if (more) break;
-        }
-        if (prm->pairwise) {
-            /* SearchRange skips a group above MER_REPEAT_LIMIT (MatchFinder.cpp:215-239) */
-            if (cnt > 1 && cnt <= MER_REPEAT_LIMIT) enumerate_pairwise(h, prm, grp, (int)cnt, hl, h->scratch);
-        } else if (cnt > 1) {
-            enumerate_matches(h, prm, grp, (int)cnt, hl, h->scratch);
+    uint64_t vlo[64], vn[64];              /* buffer = sml[g][vlo .. vlo + vn) */
+    uint32_t mer_index[64], mer_baseindex[64];
+    idmer_t lst[64];                       /* cur_mers (key field = masked key) */
+    int nl = 0;
+    #define BUF_READ(g, size, off)                                                    \
+        do {                                                                          \
+            uint64_t o_ = (off), e_ = o_ + (uint64_t)(size);                          \
+            if (o_ > m[g]) { vlo[g] = 0; vn[g] = 0; }                                 \
+            else { if (e_ > m[g]) e_ = m[g]; vlo[g] = o_; vn[g] = e_ - o_; }          \
+        } while (0)
+    for (int g = 0; g < G; ++g) {
+        uint64_t rs = MER_BUFFER_SIZE < search_len[g] ? MER_BUFFER_SIZE : search_len[g];
+        BUF_READ(g, (uint32_t)rs, start_points[g]);
+        mer_index[g] = 0;
+        mer_baseindex[g] = 0;
+        if (vn[g] > 0) {
+            const bmer_t* b = &sml[g][vlo[g]];
+            lst[nl].g = (uint32_t)g; lst[nl].pos = b->pos; lst[nl].key = b->key & mask;
+            ++nl;
         }
     }
-    free(idx); free(grp); free(hl);
+    for (int a = 1; a < nl; ++a) {   /* stable sort of the initial heads by masked key */
+        idmer_t t = lst[a]; int b = a - 1;
+        while (b >= 0 && lst[b].key > t.key) { lst[b + 1] = lst[b]; --b; }
+        lst[b + 1] = t;
+    }
+    uint64_t cap = h->cm_cap, cn = 0;
+    idmer_t* cm = h->cm;
+    while (nl > 0) {
+        const uint32_t cur = lst[0].g;
+        const uint64_t hk = lst[0].key;
+        if (cn > 0) {
+            if (hk > (cm[0].key & mask)) {
+                enumerate_group(h, prm, cm, cn, h->hl, res);
+                cn = 0;
+            }
+        }
+        if (cn > MER_REPEAT_LIMIT) {
+            /* scan past the repetitive mers: the lexicographically next masked key */
+            const uint64_t next_mer = (cm[0].key & mask) + (~mask + 1);
+            if (cn > res->max_group) res->max_group = cn;
+            uint64_t next_pos = 0;
+            int seqI = 0;
+            for (; seqI < G; ++seqI) {
+                if (!sml_find_mer_lit(sml[seqI], lens[seqI], h->x.L, next_mer, &next_pos)) ++next_pos;
+                if (next_pos < m[seqI]) break;
+            }
+            uint64_t old[64];
+            for (int g = 0; g < G; ++g) old[g] = start_points[g];
+            if (seqI < G) get_breakpoint(seqI, next_pos, G, sml, m, lens, h->x.L, mask, start_points);
+            for (int g = 0; g < G; ++g) {
+                const uint64_t done = old[g] + (uint64_t)(uint32_t)(mer_index[g] + mer_baseindex[g]);
+                if (start_points[g] < done) start_points[g] = done;   /* don't move backwards */
+                if (g < seqI) start_points[g] = m[g];
+            }
+            ++res->restarts;
+            return 0;
+        }
+        uint64_t merI = mer_index[cur];
+        int exhausted = merI < vn[cur] ? 0 : 1;
+        while (!exhausted && hk == (sml[cur][vlo[cur] + merI].key & mask)) {
+            if (cn == cap) {
+                cap = cap ? 2 * cap : 4096;
+                cm = (idmer_t*)realloc(cm, cap * sizeof(idmer_t));
+                h->hl = (idmer_t*)realloc(h->hl, cap * sizeof(idmer_t));
+            }
+            const bmer_t* b = &sml[cur][vlo[cur] + merI];
+            cm[cn].g = cur; cm[cn].pos = b->pos; cm[cn].key = b->key;
+            ++cn;
+            ++merI;
+            ++mer_index[cur];
+            if (merI == vn[cur]) exhausted = 1;
+        }
+        if (exhausted) {
+            mer_baseindex[cur] += (uint32_t)vn[cur];
+            uint32_t rs = MER_BUFFER_SIZE;
+            if ((uint64_t)MER_BUFFER_SIZE + mer_baseindex[cur] > search_len[cur])
+                rs = (uint32_t)(search_len[cur] - mer_baseindex[cur]);
+            BUF_READ(cur, rs, start_points[cur] + mer_baseindex[cur]);
+            mer_index[cur] = 0;
+            if (vn[cur] == 0) {   /* this SML is finished: forget its head */
+                memmove(lst, lst + 1, (size_t)(nl - 1) * sizeof(idmer_t));
+                --nl;
+            }
+        } else {
+            memmove(lst, lst + 1, (size_t)(nl - 1) * sizeof(idmer_t));
+            --nl;
+            const bmer_t* b = &sml[cur][vlo[cur] + merI];
+            idmer_t nm;
+            nm.g = cur; nm.pos = b->pos; nm.key = b->key & mask;
+            int at = 0;
+            while (at < nl && lst[at].key < nm.key) ++at;
+            memmove(lst + at + 1, lst + at, (size_t)(nl - at) * sizeof(idmer_t));
+            lst[at] = nm;
+            ++nl;
+        }
+    }
+    #undef BUF_READ
+    if (cn > 1) enumerate_group(h, prm, cm, cn, h->hl, res);   /* :335-336 */
+    else if (cn > res->max_group) res->max_group = cn;
+    h->cm = cm; h->cm_cap = cap;
+    return 1;
+}
+
+/* MatchFinder::FindMatchSeeds(start_offsets) (MatchFinder.cpp:137-164): SearchRange    */
+/* over the whole SMLs (search_len = GNSEQI_END) until it completes.                     */
+static void find_match_seeds(memhash_t* h, const oracle_params* prm, int G, bmer_t* const* sml, const uint64_t* m,
+                             const uint64_t* lens, const uint64_t* start_offsets, oracle_result* res) {
+    uint64_t sp[64], sl[64];
+    for (int g = 0; g < G; ++g) { sp[g] = start_offsets ? start_offsets[g] : 0; sl[g] = UINT64_MAX; }
+    while (!search_range_lit(h, prm, G, sml, m, lens, sp, sl, res)) {}
 }
 
 /* SortedMerList::bsearch (SortedMerList.cpp:380-394), recursion unrolled; unsigned */
@@ -712,6 +802,14 @@ static int sml_find_mer(const bmer_t* v, uint64_t n, int L, uint64_t q, uint64_t
     if (n == 0 || n < (uint64_t)L) { *result = 0; return 0; }
     uint64_t last_pos = n - (uint64_t)L;
     *result = sml_bsearch(v, q, 0, last_pos);
+    return v[*result].key == q;
+}
+
+/* FindMer exactly as SortedMerList.cpp:170-179: on the early return (empty SML) the */
+/* caller's result is left untouched (SearchRange's next_pos then counts on, :260). */
+static int sml_find_mer_lit(const bmer_t* v, uint64_t n, int L, uint64_t q, uint64_t* result) {
+    if (n == 0 || n < (uint64_t)L) return 0;
+    *result = sml_bsearch(v, q, 0, n - (uint64_t)L);
     return v[*result].key == q;
 }
 
@@ -797,11 +895,10 @@ static int parallel_compat_search(memhash_t* h, const oracle_params* prm, int G,
     for (uint64_t i = 0; i < nch; ++i) {
         for (int g = 0; g < G; ++g) {
             lo[g] = cs[i * G + g];
-            /* chunk_lens = next start - start (gnSeqI, wraps) or GNSEQI_END */
-            uint64_t len = (i + 1 < nch) ? cs[(i + 1) * G + g] - cs[i * G + g] : UINT64_MAX;
-            hi[g] = (lo[g] >= m[g] || len > m[g] - lo[g]) ? m[g] : lo[g] + len;
+            /* chunk_lens = next start - start (gnSeqI, wraps) or GNSEQI_END (:91-96) */
+            hi[g] = (i + 1 < nch) ? cs[(i + 1) * G + g] - cs[i * G + g] : UINT64_MAX;
         }
-        search_range(h, prm, G, sml, lo, hi, 1, res);
+        (void)search_range_lit(h, prm, G, sml, m, lens, lo, hi, res);   /* return value ignored (:97) */
         if (prm->parallel_compat == 2 && i + 1 < nch) continue;   /* checking aid: one deferred merge */
         for (uint32_t bI = 0; bI < T; ++bI)
             for (uint32_t k = 0; k < h->buckets[bI].n; ++k) merge_entry(h, &gb[bI], h->buckets[bI].v[k]);
@@ -863,9 +960,7 @@ oracle_result* oracle_find_matches(int G, const char* const* seqs, const uint64_
         if (prm->parallel_compat) {
             bad = parallel_compat_search(&h, prm, G, lens, sml, m, res);
         } else {
-            uint64_t* lo = (uint64_t*)calloc((size_t)G, sizeof(uint64_t));
-            search_range(&h, prm, G, sml, lo, m, 0, res);
-            free(lo);
+            find_match_seeds(&h, prm, G, sml, m, lens, prm->start_points, res);
         }
         free(scratch);
 
@@ -886,7 +981,7 @@ oracle_result* oracle_find_matches(int G, const char* const* seqs, const uint64_
         res->mem_count = h.mem_count;
         res->collision_count = h.collisions;
         res->probes = h.probes;
-        free(h.buckets); free(h.pool); free(h.spool); free(gbase);
+        free(h.buckets); free(h.pool); free(h.spool); free(gbase); free(h.cm); free(h.hl);
         res->plog_bucket = h.plog_bucket;
         res->plog_ref = h.plog_ref;
     }
@@ -981,6 +1076,7 @@ int oracle_result_probe_log(const oracle_result* r, uint32_t* buckets, uint64_t*
 }
 uint64_t oracle_result_seedmers(const oracle_result* r) { return r ? r->seedmers : 0; }
 uint64_t oracle_result_chunks(const oracle_result* r) { return r ? r->chunks : 0; }
+uint64_t oracle_result_restarts(const oracle_result* r) { return r ? r->restarts : 0; }
 void     oracle_result_free(oracle_result* r) {
     if (!r) return;
     free(r->lengths); free(r->starts); free(r->plog_bucket); free(r->plog_ref); free(r);

@@ -60,6 +60,8 @@ typedef struct oracle_params {
     uint64_t chunk_size;       /* its CHUNK_SIZE (0 = 200000, :51)              */
     int      pairwise;         /* 1: PairwiseMatchFinder::EnumerateMatches      *
                                 *    (PairwiseMatchFinder.cpp:37-73)             */
+    const uint64_t* start_points; /* MemHash::FindMatchesFromPosition start SML  *
+                                *    indices (MemHash.cpp:117-127); NULL = 0     */
 } oracle_params;
 
 typedef struct oracle_result oracle_result;
@@ -77,6 +79,7 @@ uint64_t oracle_result_probe_count(const oracle_result* r);
 int      oracle_result_probe_log(const oracle_result* r, uint32_t* buckets, uint64_t* ref);
 uint64_t oracle_result_seedmers(const oracle_result* r);
 uint64_t oracle_result_chunks(const oracle_result* r);     /* compat: chunks searched */
+uint64_t oracle_result_restarts(const oracle_result* r);   /* MER_REPEAT_LIMIT restarts */
 void     oracle_result_free(oracle_result* r);
 /* AddHashEntry replay of probe rows {starts[G], offset} (sharded FindMatches checks). */
 oracle_result* oracle_replay_rows(int G, const char* const* seqs, const uint64_t* lens, const oracle_params* prm,

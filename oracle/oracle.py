@@ -34,6 +34,7 @@ class _Params(ctypes.Structure):
         ("parallel_compat", ctypes.c_int),
         ("chunk_size", ctypes.c_uint64),
         ("pairwise", ctypes.c_int),
+        ("start_points", ctypes.c_void_p),
     ]
 
 
@@ -61,7 +62,7 @@ def lib() -> ctypes.CDLL:
         L.oracle_find_matches.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(u64),
                                           ctypes.POINTER(_Params)]
         L.oracle_find_matches.restype = vp
-        for f in ("count", "mem_count", "collision_count", "max_group", "probe_count", "seedmers", "chunks"):
+        for f in ("count", "mem_count", "collision_count", "max_group", "probe_count", "seedmers", "chunks", "restarts"):
             fn = getattr(L, f"oracle_result_{f}")
             fn.argtypes = [vp]
             fn.restype = u64
@@ -124,15 +125,21 @@ def seed_occurrence(seq: bytes, seed: int) -> np.ndarray:
 def find_matches(seqs: Sequence[bytes], seed: int, repeat_tol: int = 0, enum_tol: int = 1,
                  table_size: int = 40000, masked: bool = False, seq_mask: int = 0,
                  gnseqi_end_neg1: bool = False, seeds_only: bool = False, parallel_compat: bool = False,
-                 chunk_size: int = 0, pairwise: bool = False) -> Tuple[np.ndarray, np.ndarray, dict]:
+                 chunk_size: int = 0, pairwise: bool = False,
+                 start_points: Sequence[int] | None = None) -> Tuple[np.ndarray, np.ndarray, dict]:
     """MemHash::FindMatches restated; returns (lengths[M], starts[M,G], counters).
     parallel_compat: ParallelMemHash::FindMatches instead (ParallelMemHash.cpp:42-121),
-    chunk_size = its CHUNK_SIZE (0 = 200000)."""
+    chunk_size = its CHUNK_SIZE (0 = 200000).  start_points: FindMatchesFromPosition
+    (MemHash.cpp:117-127) start SML index per genome."""
     G = len(seqs)
     arr = (ctypes.c_char_p * G)(*seqs)
     lens = (ctypes.c_uint64 * G)(*[len(s) for s in seqs])
+    sp = None
+    if start_points is not None:
+        sp = (ctypes.c_uint64 * G)(*[int(x) for x in start_points])
     prm = _Params(seed, repeat_tol, enum_tol, table_size, int(masked), seq_mask, int(gnseqi_end_neg1),
-                  int(seeds_only), int(parallel_compat), chunk_size, int(pairwise))
+                  int(seeds_only), int(parallel_compat), chunk_size, int(pairwise),
+                  ctypes.cast(sp, ctypes.c_void_p) if sp is not None else None)
     L = lib()
     r = L.oracle_find_matches(G, arr, lens, ctypes.byref(prm))
     if not r:
@@ -145,7 +152,8 @@ def find_matches(seqs: Sequence[bytes], seed: int, repeat_tol: int = 0, enum_tol
             L.oracle_result_copy(r, lengths.ctypes.data, starts.ctypes.data)
         stats = dict(mem_count=L.oracle_result_mem_count(r), collision_count=L.oracle_result_collision_count(r),
                      max_group=L.oracle_result_max_group(r), probes=L.oracle_result_probe_count(r),
-                     seedmers=L.oracle_result_seedmers(r), chunks=L.oracle_result_chunks(r))
+                     seedmers=L.oracle_result_seedmers(r), chunks=L.oracle_result_chunks(r),
+                     restarts=L.oracle_result_restarts(r))
     finally:
         L.oracle_result_free(r)
     return lengths, starts, stats
