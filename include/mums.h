@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MUMS_ABI_VERSION 3
+#define MUMS_ABI_VERSION 4
 
 enum mums_status {
     MUMS_OK = 0,
@@ -72,6 +72,7 @@ typedef struct mums_stats {
     double   ms_chains;         /* seed-chain labelling before the replay (ExtendMatch results)        */
     uint64_t chains;            /* seed chains among the probes                                        */
     uint64_t chunks;            /* ParallelMemHash compat: SML chunks searched (ParallelMemHash.cpp:75-83) */
+    uint64_t restarts;          /* MER_REPEAT_LIMIT restarts of the merge (MatchFinder.cpp:253-277)      */
 } mums_stats;
 
 /* MemHash::MemHash (MemHash.cpp:33-49); device = HIP ordinal. */
@@ -111,7 +112,20 @@ int  mums_add_genome_device(mums_ctx* ctx, const void* d_ascii, uint64_t n);
 /* MemHash::Clear / ClearSequences (MemHash.cpp:80-93): drops genomes and results. */
 int  mums_clear(mums_ctx* ctx);
 
-/* MemHash::FindMatches(MatchList&) (MemHash.cpp:109-115) / CreateMatches (:104-107). */
+/* MemHash::FindMatchesFromPosition (MemHash.cpp:117-127) -> FindMatchSeeds(start_points)
+ * (MatchFinder.cpp:137-164): the merge of the next finds starts at SML index
+ * start_points[g] of genome g (count = genome count; count 0 = from 0, FindMatches).
+ * Single-context MemHash / MaskedMemHash / PairwiseMatchFinder only. */
+int  mums_set_start_points(mums_ctx* ctx, const uint64_t* start_points, uint32_t count);
+/* MatchFinder::SetOffsetLog (MatchFinder.h:81; written MatchFinder.cpp:152-162): the start
+ * points after every MER_REPEAT_LIMIT restart of the last find, one row of genome-count
+ * entries per restart.  *rows = row count, *seq_count = entries per row (may be NULL);
+ * out (cap_rows rows) may be NULL to query. */
+int  mums_get_offset_log(mums_ctx* ctx, uint64_t* out, uint64_t cap_rows, uint64_t* rows, uint32_t* seq_count);
+/* MemHash::FindMatches(MatchList&) (MemHash.cpp:109-115) / CreateMatches (:104-107).
+ * SearchRange's MER_REPEAT_LIMIT restart (MatchFinder.cpp:253-277) is reproduced
+ * (mums_stats.restarts); the chunked (> 2^32 seed-mers) and sharded modes refuse an
+ * input that has a seed group above MER_REPEAT_LIMIT (MUMS_E_UNSUPPORTED). */
 int  mums_find(mums_ctx* ctx);
 /* Run only up to a stage (benchmarks); MUMS_STAGE_ALL == mums_find. */
 int  mums_find_stage(mums_ctx* ctx, int stage);

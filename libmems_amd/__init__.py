@@ -78,6 +78,7 @@ class _Stats(ctypes.Structure):
         ("ms_chains", ctypes.c_double),
         ("chains", ctypes.c_uint64),
         ("chunks", ctypes.c_uint64),
+        ("restarts", ctypes.c_uint64),
     ]
 
 
@@ -90,7 +91,8 @@ EXPORTED_SYMBOLS = [
     "mums_shard_merge", "mums_probe_count", "mums_probe_copy", "mums_shard_bucket_counts", "mums_shard_probe_rows",
     "mums_shard_packed_info", "mums_shard_packed_copy", "mums_shard_find", "mums_set_parallel_compat",
     "mums_seed_occurrence", "mums_multiplicity_filter", "mums_length_filter", "mums_write_sml",
-    "mums_add_genome_sml", "mums_set_pairwise", "mums_shard_slice",
+    "mums_add_genome_sml", "mums_set_pairwise", "mums_shard_slice", "mums_set_start_points",
+    "mums_get_offset_log",
 ]
 
 _lib: Optional[ctypes.CDLL] = None
@@ -155,6 +157,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mums_add_genome_sml.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(u64)]
     lib.mums_set_pairwise.argtypes = [vp, i32]
     lib.mums_shard_slice.argtypes = [vp, u32, vp, u32, u64, u64]
+    lib.mums_set_start_points.argtypes = [vp, vp, u32]
+    lib.mums_get_offset_log.argtypes = [vp, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(u32)]
     _lib = lib
     return lib
 
@@ -291,6 +295,31 @@ class MemHash:
                 self.AddSequence(s)
         self._check(self._lib.mums_find(self._ctx))
         return self.GetMatchList()
+
+    def FindMatchesFromPosition(self, sequences: Optional[Sequence], start_points: Sequence[int]) -> MatchList:
+        """MemHash::FindMatchesFromPosition (MemHash.cpp:117-127): the merge starts at SML
+        index start_points[g] of every genome (FindMatchSeeds, MatchFinder.cpp:137-164)."""
+        if sequences is not None:
+            for s in sequences:
+                self.AddSequence(s)
+        sp = np.ascontiguousarray(np.asarray(start_points, dtype=np.uint64))
+        self._check(self._lib.mums_set_start_points(self._ctx, sp.ctypes.data, len(sp)))
+        try:
+            self._check(self._lib.mums_find(self._ctx))
+        finally:
+            self._check(self._lib.mums_set_start_points(self._ctx, None, 0))
+        return self.GetMatchList()
+
+    def OffsetLog(self) -> np.ndarray:
+        """Start points after every MER_REPEAT_LIMIT restart of the last find, one row per
+        restart -- the lines MatchFinder::SetOffsetLog's stream receives (MatchFinder.cpp:152-162)."""
+        rows, g = ctypes.c_uint64(), ctypes.c_uint32()
+        self._check(self._lib.mums_get_offset_log(self._ctx, None, 0, ctypes.byref(rows), ctypes.byref(g)))
+        out = np.zeros((int(rows.value), int(g.value)), dtype=np.uint64)
+        if rows.value:
+            self._check(self._lib.mums_get_offset_log(self._ctx, out.ctypes.data, rows.value, ctypes.byref(rows),
+                                                      ctypes.byref(g)))
+        return out
 
     def CreateMatches(self) -> bool:
         """MemHash::CreateMatches (MemHash.cpp:104-107)."""

@@ -85,6 +85,11 @@ struct mums_ctx {
     // one genome's SML / seed frequencies (sml_tools.hip) and filtered MatchLists
     DevBuf smlk0, smlkA, smlkB, smlvA, smlvB, smltmp, flen, fs;
     DevBuf rowsall;          // chunked mode: probe rows of all chunks
+    // MER_REPEAT_LIMIT restart / FindMatchesFromPosition (restart.hip)
+    std::vector<uint64_t> start_points;   // per genome SML start index (empty = all 0)
+    DevBuf rsbuf, rsplan, rsbst;
+    uint64_t restarts = 0;
+    std::vector<uint64_t> offset_log;     // start points after every restart (R x G)
     hipEvent_t ev[EV_COUNT] = {};
     bool profiling = false;
     hipEvent_t ev_ds[16] = {};   // 2 per radix pass (<= 8 passes)
@@ -488,6 +493,7 @@ void fill_stats(mums_ctx* ctx, uint64_t n) {
     s.groups = ctx->hc.ngroups;
     s.probes = ctx->P;
     s.repeat_limit_groups = ctx->hc.repeat_limit;
+    s.restarts = ctx->restarts;
     auto el = [&](int a, int b) {
         float ms = 0.f;
         (void)hipEventElapsedTime(&ms, ctx->ev[a], ctx->ev[b]);
@@ -524,6 +530,145 @@ void fill_stats(mums_ctx* ctx, uint64_t n) {
     } else {
         s.ms_total = el(EV_START, EV_BUCKETS);
     }
+}
+
+bool have_start_points(const mums_ctx* ctx) {
+    for (uint64_t x : ctx->start_points)
+        if (x) return true;
+    return false;
+}
+
+// MER_REPEAT_LIMIT restart (MatchFinder.cpp:253-277) and FindMatchSeeds start points
+// (MemHash.cpp:117-127) on the merged stream s of n records (restart.hip): plan the
+// restarts, then compact the live records in order into dst (records / keys + dst_idx;
+// packed records also get their new bucket starts in dst_bstart).  *n_live = kept
+// records; *changed = false when every record lives (the groups already stand).
+int restart_fixup(mums_ctx* ctx, const RsStream& s, uint64_t n, void* dst_a, uint32_t* dst_idx, uint32_t* dst_bstart,
+                  uint64_t* n_live, bool* changed, hipStream_t st) {
+    const GenomeTable& gt = ctx->gt;
+    const int G = gt.G;
+    *changed = false;
+    *n_live = n;
+    ctx->restarts = 0;
+    ctx->offset_log.clear();
+    if (n >= 0xFFFFFFF0ull) return fail(ctx, MUMS_E_UNSUPPORTED, "MER_REPEAT_LIMIT restart above 2^32 records");
+    std::vector<uint64_t> S0(G, 0);
+    for (int g = 0; g < G && g < (int)ctx->start_points.size(); ++g) S0[g] = ctx->start_points[g];
+    HIPCHK(ctx->rsbuf.ensure(restart_ws_bytes(n, G)));
+    const RestartWs w = restart_ws_layout(ctx->rsbuf.p, n, G);
+    HIPCHK(launch_restart_smls(s, n, gt, w, st));
+    // candidates: one per group above MER_REPEAT_LIMIT (counted by the groups stage)
+    const uint64_t cap = ctx->hc.repeat_limit + 16;
+    const uint64_t Gu = (uint64_t)G;
+    const size_t plan_words = cap + 1 + 3 * cap * Gu + (cap + 1) / 2 + 2 * Gu + 16 + cap + cap * Gu;
+    HIPCHK(ctx->rsplan.ensure(plan_words * 8 + sizeof(restart::PlanOut) + 256));
+    uint64_t* d_list = ctx->rsplan.as<uint64_t>();
+    unsigned long long* d_cnt = (unsigned long long*)(d_list + cap);
+    uint64_t* d_pre = d_list + cap + 1;
+    uint64_t* d_S = d_pre + 3 * cap * Gu + (cap + 1) / 2;
+    uint64_t* d_S0 = d_S + Gu;
+    restart::PlanOut* d_out = (restart::PlanOut*)(d_S0 + Gu);
+    uint64_t* d_rkey = d_S0 + Gu + 16;
+    uint64_t* d_rS = d_rkey + cap;
+    HIPCHK(launch_restart_cands(w, n, d_list, d_cnt, cap, st));
+    unsigned long long C = 0;
+    HIPCHK(hipMemcpyAsync(&C, d_cnt, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (C > cap) return fail(ctx, MUMS_E_HIP, "restart candidates exceed the groups stage's count (internal error)");
+    std::vector<uint64_t> cand(C);
+    if (C) {
+        HIPCHK(hipMemcpy(cand.data(), d_list, C * 8, hipMemcpyDeviceToHost));
+        std::sort(cand.begin(), cand.end());
+        HIPCHK(hipMemcpyAsync(d_list, cand.data(), C * 8, hipMemcpyHostToDevice, st));
+    }
+    HIPCHK(hipMemcpyAsync(d_S, S0.data(), Gu * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_S0, S0.data(), Gu * 8, hipMemcpyHostToDevice, st));
+    restart::PlanOut po{};
+    po.cap = C;
+    po.rkey = d_rkey;
+    po.rS = d_rS;
+    po.status = restart::kPlanOk;
+    HIPCHK(hipMemcpyAsync(d_out, &po, sizeof(po), hipMemcpyHostToDevice, st));
+    HIPCHK(launch_restart_plan(w, G, d_list, C, d_pre, d_S, d_out, st));
+    HIPCHK(hipMemcpyAsync(&po, d_out, sizeof(po), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (po.status != restart::kPlanOk) return fail(ctx, MUMS_E_HIP, "restart plan table full (internal error)");
+    ctx->restarts = po.nrestarts;
+    ctx->offset_log.assign(po.nrestarts * Gu, 0);
+    if (po.nrestarts) HIPCHK(hipMemcpy(ctx->offset_log.data(), d_rS, po.nrestarts * Gu * 8, hipMemcpyDeviceToHost));
+    if (po.nrestarts == 0 && !have_start_points(ctx)) return MUMS_OK;
+    uint32_t* d_total = (uint32_t*)d_cnt;
+    HIPCHK(launch_restart_compact(s, n, G, w, d_rkey, po.nrestarts, d_rS, d_S0, dst_a, dst_idx, dst_bstart, d_total,
+                                  st));
+    uint32_t tot = 0;
+    HIPCHK(hipMemcpyAsync(&tot, d_total, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    *n_live = tot;
+    *changed = true;
+    return MUMS_OK;
+}
+
+// run_pipeline's restart stage: after the groups stage saw a group above MER_REPEAT_LIMIT
+// (or with start points), fix the stream up and run the groups stage again on it.
+int restart_stage(mums_ctx* ctx, const MatchParams& mp, const ProbeSpace& ps, hipStream_t st) {
+    if (!ctx->hc.repeat_limit && !have_start_points(ctx)) return MUMS_OK;
+    DevCounters* dc = ctx->counters.as<DevCounters>();
+    const uint64_t rep = ctx->hc.repeat_limit;
+    const uint64_t N = ctx->N;
+    RsStream s{};
+    uint64_t nl = N;
+    bool changed = false;
+    int rc;
+    if (ctx->packed_path) {
+        const int B = ctx->msd_bits;
+        s.kind = 0;
+        s.rec = ctx->sorted_rec;
+        s.bstart = ctx->mstart.as<uint32_t>();
+        s.B = B;
+        s.kbits = 2 * ctx->w + 1;
+        uint64_t* dst = ctx->sorted_buf ? ctx->recA.as<uint64_t>() : ctx->recB.as<uint64_t>();
+        HIPCHK(ctx->rsbst.ensure(((1ull << B) + 64) * 4));
+        rc = restart_fixup(ctx, s, N, dst, nullptr, ctx->rsbst.as<uint32_t>(), &nl, &changed, st);
+        if (rc || !changed) return rc;
+        HIPCHK(hipMemcpyAsync(ctx->mstart.p, ctx->rsbst.p, ((1ull << B) + 1) * 4, hipMemcpyDeviceToDevice, st));
+        ctx->sorted_buf ^= 1;
+        ctx->sorted_rec = dst;
+        SegTile* tiles = ctx->tiles.as<SegTile>();
+        HIPCHK(build_seg_tiles_from_starts(ctx->mstart.as<uint32_t>(), B, nl, tiles, &dc->ntiles, ctx->tmp.p, st));
+        HIPCHK(hipMemsetAsync(&dc->repeat_limit, 0, 8, st));
+        rc = groups_dispatch<RecView>(ctx, RecView{dst}, tiles, seg_tiles_upper(nl, B), mp, ps.probe_info,
+                                      ps.probe_bucket, ps.slot_info, ps.slot_bucket, st);
+    } else {
+        const size_t kb = ctx->key64 ? 8 : 4;
+        (void)kb;
+        s.kind = ctx->key64 ? 2 : 1;
+        s.key = ctx->sorted_key;
+        s.idx = ctx->sorted_idx;
+        void* dk = ctx->sorted_buf ? ctx->kA.p : ctx->kB.p;
+        uint32_t* dv = ctx->sorted_buf ? ctx->vA.as<uint32_t>() : ctx->vB.as<uint32_t>();
+        rc = restart_fixup(ctx, s, N, dk, dv, nullptr, &nl, &changed, st);
+        if (rc || !changed) return rc;
+        ctx->sorted_buf ^= 1;
+        ctx->sorted_key = dk;
+        ctx->sorted_idx = dv;
+        SegTile* tiles = ctx->tiles.as<SegTile>();
+        const uint64_t nt = (nl + kSegTile - 1) / kSegTile;
+        HIPCHK(launch_flat_tiles(nl, tiles, st));
+        HIPCHK(hipMemsetAsync(&dc->repeat_limit, 0, 8, st));
+        if (ctx->key64)
+            rc = groups_dispatch<PairView<uint64_t>>(ctx, PairView<uint64_t>{(const uint64_t*)dk, dv}, tiles, nt, mp,
+                                                     ps.probe_info, ps.probe_bucket, ps.slot_info, ps.slot_bucket, st);
+        else
+            rc = groups_dispatch<PairView<uint32_t>>(ctx, PairView<uint32_t>{(const uint32_t*)dk, dv}, tiles, nt, mp,
+                                                     ps.probe_info, ps.probe_bucket, ps.slot_info, ps.slot_bucket, st);
+    }
+    if (rc) return rc;
+    rc = finish_seeds(ctx, ps, st);
+    if (rc) return rc;
+    // the report counts the groups above MER_REPEAT_LIMIT of the whole stream
+    HIPCHK(hipMemcpy(&dc->repeat_limit, &rep, 8, hipMemcpyHostToDevice));
+    ctx->hc.repeat_limit = rep;
+    return MUMS_OK;
 }
 
 // keys -> sorted stream -> probes -> bucket-sorted probes [-> replay -> MatchList]
@@ -620,6 +765,8 @@ int run_pipeline(mums_ctx* ctx, int stage) {
     if (rc) return rc;
     rc = finish_seeds(ctx, ps, st);
     if (rc) return rc;
+    rc = restart_stage(ctx, mp, ps, st);
+    if (rc) return rc;
     ctx->stage_done = MUMS_STAGE_SEEDS;
 
     if (stage >= MUMS_STAGE_ALL) {
@@ -641,6 +788,8 @@ int run_pipeline(mums_ctx* ctx, int stage) {
 // SortedMerList::Create :788-798) and the global genome table for genome lengths lens.
 int prepare_run(mums_ctx* ctx, const std::vector<uint64_t>& lens) {
     ctx->stage_done = 0;
+    ctx->restarts = 0;
+    ctx->offset_log.clear();
     ctx->M = ctx->P = 0;
     const int G = (int)lens.size();
     if (ctx->enum_tol > 8)
@@ -1013,9 +1162,29 @@ int mums_find_stage(mums_ctx* ctx, int stage) {
         return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed-mers: only MemHash / MaskedMemHash, enum_tol <= 1");
     if (ctx->pcompat && ctx->enum_tol > 1)
         return fail(ctx, MUMS_E_UNSUPPORTED, "ParallelMemHash compat with enumeration tolerance > 1");
+    if (have_start_points(ctx) && (big || ctx->pcompat))
+        return fail(ctx, MUMS_E_UNSUPPORTED, "start points (FindMatchesFromPosition) in the chunked / compat modes");
     if (ctx->pairwise || ctx->enum_tol > 1) return run_pipeline_pairwise(ctx, stage);
     if (ctx->pcompat) return run_pipeline_compat(ctx, stage);
     return big ? run_pipeline_chunked(ctx, stage) : run_pipeline(ctx, stage);
+}
+
+int mums_set_start_points(mums_ctx* ctx, const uint64_t* start_points, uint32_t count) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (count && !start_points) return fail(ctx, MUMS_E_INVALID, "null start points");
+    ctx->start_points.assign(start_points, start_points + count);
+    return MUMS_OK;
+}
+
+int mums_get_offset_log(mums_ctx* ctx, uint64_t* out, uint64_t cap_rows, uint64_t* rows, uint32_t* seq_count) {
+    if (check_ctx(ctx) || !rows) return MUMS_E_INVALID;
+    const uint64_t G = (uint64_t)ctx->gt.G, R = G ? ctx->offset_log.size() / G : 0;
+    *rows = R;
+    if (seq_count) *seq_count = (uint32_t)G;
+    if (!out || cap_rows == 0) return MUMS_OK;
+    if (cap_rows < R) return fail(ctx, MUMS_E_INVALID, "output buffer too small");
+    std::copy(ctx->offset_log.begin(), ctx->offset_log.end(), out);
+    return MUMS_OK;
 }
 
 int mums_set_pairwise(mums_ctx* ctx, int enable) {
@@ -1464,6 +1633,9 @@ int mums_shard_merge(mums_ctx* ctx, const uint64_t* d_records, uint32_t nsources
             b0 = b1;
         }
     }
+    if (ctx->hc.repeat_limit)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "sharded mode: a seed group above MER_REPEAT_LIMIT (the reference's "
+                                             "SearchRange restart is reproduced on one context only)");
     ctx->stage_done = MUMS_STAGE_SEEDS;
     HIPCHK(hipStreamSynchronize(st));
     fill_stats(ctx, n);
@@ -1621,6 +1793,28 @@ int run_pipeline_pairwise(mums_ctx* ctx, int stage) {
     if (rc) return rc;
     HIPCHK(hipMemcpy(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost));
     if (ctx->hc.err & 1u) return fail(ctx, MUMS_E_GAP, "Gap in genome sequence ('-' encountered)");
+    if (ctx->hc.repeat_limit || have_start_points(ctx)) {   // MER_REPEAT_LIMIT restart (restart.hip)
+        const uint64_t rep = ctx->hc.repeat_limit;
+        RsStream s{};
+        s.kind = ctx->key64 ? 2 : 1;
+        s.key = ctx->sorted_key;
+        s.idx = ctx->sorted_idx;
+        void* dk = ctx->sorted_buf ? ctx->kA.p : ctx->kB.p;
+        uint32_t* dv = ctx->sorted_buf ? ctx->vA.as<uint32_t>() : ctx->vB.as<uint32_t>();
+        uint64_t nl = N;
+        bool changed = false;
+        rc = restart_fixup(ctx, s, N, dk, dv, nullptr, &nl, &changed, st);
+        if (rc) return rc;
+        if (changed) {
+            ctx->sorted_buf ^= 1;
+            ctx->sorted_key = dk;
+            ctx->sorted_idx = dv;
+            rc = ctx->key64 ? pairwise_rows<uint64_t>(ctx, nl, st) : pairwise_rows<uint32_t>(ctx, nl, st);
+            if (rc) return rc;
+            HIPCHK(hipMemcpy(&dc->repeat_limit, &rep, 8, hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost));
+        }
+    }
     HIPCHK(hipEventRecord(ctx->ev[EV_GROUPS], st));
     const uint64_t P = ctx->P;
     if (P >= (1ull << 30)) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^30 seed probes in one FindMatches");
@@ -1788,6 +1982,9 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
         if (rc) return rc;
         rc = finish_seeds(ctx, ps, st);
         if (rc) return rc;
+        if (ctx->hc.repeat_limit)
+            return fail(ctx, MUMS_E_UNSUPPORTED, "chunked mode: a seed group above MER_REPEAT_LIMIT (the reference's "
+                                                 "SearchRange restart is reproduced below 2^32 seed-mers only)");
         HIPCHK(hipEventSynchronize(ctx->ev[EV_BUCKETS]));
         ms_sort += el(EV_CHAINS, EV_SORT);
         ms_groups += el(EV_SORT, EV_GROUPS);

@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "restart_plan.h"
+
 namespace mums {
 
 constexpr int kMaxG = 32;            // genomes per context (register arrays in the replay)
@@ -268,5 +270,41 @@ hipError_t launch_compat_chunk_keys(const uint64_t* sk, const uint32_t* sv, uint
                                     hipStream_t st);
 hipError_t launch_compat_merge(uint32_t* tsize, const uint32_t* bstart, uint32_t* tbl, const int64_t* pool, int G,
                                uint32_t Tb, unsigned long long* collisions, hipStream_t st);
+
+// restart.hip: MER_REPEAT_LIMIT restart (MatchFinder.cpp:253-277) / start points
+// (MemHash.cpp:117-127) as a fix-up of the merged stream
+struct RsStream {
+    int kind;                  // 0: packed records, 1: (u32 ckey, idx) pairs, 2: (u64 ckey, idx) pairs
+    const uint64_t* rec;       // kind 0
+    const uint32_t* bstart;    // kind 0: 2^B + 1 MSD bucket starts
+    int B, kbits;              // kind 0: MSD bits, 2w+1
+    const void* key;           // kind 1/2
+    const uint32_t* idx;
+};
+struct RestartWs {             // workspace carved from one device buffer
+    uint64_t* ckf;             // full ckey per stream record
+    uint64_t* ck;              // ckeys genome-major (the G SortedMerLists)
+    uint32_t* gen;             // genome per stream record
+    uint32_t* inv;             // genome-major slot per stream record
+    uint32_t *kA, *kB, *vA, *vB;
+    uint64_t* dm;              // SMLLength per genome
+    uint64_t* dbase;           // first genome-major slot per genome
+    void* tmp;
+    size_t bytes;
+};
+RestartWs restart_ws_layout(void* base, uint64_t n, int G);
+size_t restart_ws_bytes(uint64_t n, int G);
+hipError_t launch_restart_smls(const RsStream& s, uint64_t n, const GenomeTable& gt, const RestartWs& w,
+                               hipStream_t st);
+hipError_t launch_restart_cands(const RestartWs& w, uint64_t n, uint64_t* d_list, unsigned long long* d_cnt,
+                                uint64_t cap, hipStream_t st);
+// d_pre: 3 * C * G uint64 + C int; d_S: G start points in / last phase's out
+hipError_t launch_restart_plan(const RestartWs& w, int G, const uint64_t* d_cand, uint64_t C, uint64_t* d_pre,
+                               uint64_t* d_S, restart::PlanOut* d_out, hipStream_t st);
+// live records (SML index >= start point of their key's phase) compacted in order into
+// dst (records, or keys + dst_idx); kind 0 also writes the new bucket starts
+hipError_t launch_restart_compact(const RsStream& s, uint64_t n, int G, const RestartWs& w, const uint64_t* d_rkey,
+                                  uint64_t R, const uint64_t* d_rS, const uint64_t* d_S0, void* dst_a, uint32_t* dst_idx,
+                                  uint32_t* dst_bstart, uint32_t* d_total, hipStream_t st);
 
 }  // namespace mums

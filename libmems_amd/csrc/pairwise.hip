@@ -33,7 +33,7 @@ __device__ __forceinline__ uint32_t pw_unique(const View& v, uint64_t h, uint64_
     const uint64_t k0 = v.gkey(h);
     uint32_t seen = 0, dup = 0, n = 0;
     for (uint64_t j = h; j < N && v.gkey(j) == k0; ++j) {
-        if (++n > (uint32_t)kRepeatLimit) break;
+        ++n;
         const uint32_t b = 1u << genome_of(gt, v.gidx(j));
         dup |= seen & b;
         seen |= b;
@@ -52,8 +52,10 @@ __global__ void pw_count_kernel(View v, uint64_t N, GenomeTable gt, uint32_t* __
         uint32_t size = 0;
         const uint32_t u = pw_unique(v, i, N, gt, &size);
         const uint32_t k = (uint32_t)__builtin_popcount(u);
+        // a group above MER_REPEAT_LIMIT that survived the restart fix-up (restart.hip) is
+        // enumerated like any other (SearchRange hands it to EnumerateMatches, :242-246)
         if (size > (uint32_t)kRepeatLimit) atomicAdd(&ctr->repeat_limit, 1ull);
-        else if (size >= 2) c = k * (k - 1) / 2;
+        if (size >= 2) c = k * (k - 1) / 2;
     }
     npairs[i] = c;
 }
@@ -102,7 +104,8 @@ constexpr int kEnumMax = 8;   // enum_tol bound of the GPU path (per-genome reco
 
 // MemHash::EnumerateMatches over the group at head h (per genome in SML order): per genome the
 // first min(count, enum_tol) records; rejected (false) when a genome has more than
-// repeat_tol + 1 records or the group exceeds MER_REPEAT_LIMIT.  c[g] = kept records of g,
+// repeat_tol + 1 records (groups above MER_REPEAT_LIMIT reach here only when the
+// reference's merge hands them over whole: restart.hip).  c[g] = kept records of g,
 // pos[g][i] / par[g][i] their positions and strand parities.
 template <typename View>
 __device__ bool en_collect(const View& v, uint64_t h, uint64_t N, const GenomeTable& gt, const MatchParams& mp,
@@ -116,7 +119,7 @@ __device__ bool en_collect(const View& v, uint64_t h, uint64_t N, const GenomeTa
     // stream order inside a group = (parity, genome, position): restricted to one genome
     // that is its SortedMerList order (full key, then position)
     for (uint64_t j = h; j < N && v.gkey(j) == k0; ++j) {
-        if (++n > (uint32_t)kRepeatLimit) break;
+        ++n;
         const RecFields r = v.get(j);
         const int g = genome_of(gt, r.idx);
         if (tally[g] < mp.enum_tol) {
@@ -128,7 +131,7 @@ __device__ bool en_collect(const View& v, uint64_t h, uint64_t N, const GenomeTa
         ++tally[g];
     }
     *size = n;
-    return ok && n <= (uint32_t)kRepeatLimit;
+    return ok;
 }
 
 // AddHashEntry calls of a group: the odometer's combinations (one record per present

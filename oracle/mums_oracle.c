@@ -451,6 +451,8 @@ struct oracle_result {
     uint64_t* lengths;
     int64_t* starts;
     uint64_t mem_count, collision_count, max_group, probes, seedmers, chunks, restarts;
+    uint64_t* offlog;         /* start points after every restart (SetOffsetLog, MatchFinder.cpp:152-162) */
+    int offlog_g;
     uint32_t* plog_bucket;    /* seeds_only: per AddHashEntry call, its bucket ... */
     uint64_t* plog_ref;       /* ... and the global seed-mer index of the probe's first start */
 };
@@ -780,7 +782,12 @@ static void find_match_seeds(memhash_t* h, const oracle_params* prm, int G, bmer
                              const uint64_t* lens, const uint64_t* start_offsets, oracle_result* res) {
     uint64_t sp[64], sl[64];
     for (int g = 0; g < G; ++g) { sp[g] = start_offsets ? start_offsets[g] : 0; sl[g] = UINT64_MAX; }
-    while (!search_range_lit(h, prm, G, sml, m, lens, sp, sl, res)) {}
+    while (!search_range_lit(h, prm, G, sml, m, lens, sp, sl, res)) {
+        /* the offset stream line of this restart (MatchFinder.cpp:152-162) */
+        res->offlog = (uint64_t*)realloc(res->offlog, (size_t)res->restarts * (size_t)G * sizeof(uint64_t));
+        memcpy(res->offlog + (res->restarts - 1) * (uint64_t)G, sp, (size_t)G * sizeof(uint64_t));
+        res->offlog_g = G;
+    }
 }
 
 /* SortedMerList::bsearch (SortedMerList.cpp:380-394), recursion unrolled; unsigned */
@@ -1077,9 +1084,15 @@ int oracle_result_probe_log(const oracle_result* r, uint32_t* buckets, uint64_t*
 uint64_t oracle_result_seedmers(const oracle_result* r) { return r ? r->seedmers : 0; }
 uint64_t oracle_result_chunks(const oracle_result* r) { return r ? r->chunks : 0; }
 uint64_t oracle_result_restarts(const oracle_result* r) { return r ? r->restarts : 0; }
+/* rows = restarts, G entries each; returns 0 */
+int oracle_result_offset_log(const oracle_result* r, uint64_t* out) {
+    if (!r) return -1;
+    if (r->offlog && r->restarts) memcpy(out, r->offlog, (size_t)r->restarts * (size_t)r->offlog_g * sizeof(uint64_t));
+    return 0;
+}
 void     oracle_result_free(oracle_result* r) {
     if (!r) return;
-    free(r->lengths); free(r->starts); free(r->plog_bucket); free(r->plog_ref); free(r);
+    free(r->lengths); free(r->starts); free(r->plog_bucket); free(r->plog_ref); free(r->offlog); free(r);
 }
 
 /* ------------------------------------------------------------------------- */

@@ -69,6 +69,7 @@ def lib() -> ctypes.CDLL:
         L.oracle_result_seqcount.argtypes = [vp]
         L.oracle_result_probe_log.argtypes = [vp, vp, vp]
         L.oracle_result_copy.argtypes = [vp, vp, vp]
+        L.oracle_result_offset_log.argtypes = [vp, vp]
         L.oracle_result_free.argtypes = [vp]
         L.oracle_generate.argtypes = [ctypes.c_int, u64, ctypes.c_double, u64, ctypes.c_char_p]
         _lib = L
@@ -154,6 +155,10 @@ def find_matches(seqs: Sequence[bytes], seed: int, repeat_tol: int = 0, enum_tol
                      max_group=L.oracle_result_max_group(r), probes=L.oracle_result_probe_count(r),
                      seedmers=L.oracle_result_seedmers(r), chunks=L.oracle_result_chunks(r),
                      restarts=L.oracle_result_restarts(r))
+        offlog = np.zeros((int(stats["restarts"]), G), dtype=np.uint64)
+        if stats["restarts"] and not parallel_compat:
+            L.oracle_result_offset_log(r, offlog.ctypes.data)
+        stats["offset_log"] = offlog
     finally:
         L.oracle_result_free(r)
     return lengths, starts, stats
