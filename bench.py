@@ -82,39 +82,66 @@ def synth_genomes_large(G: int, n: int, p: float, seed: int, device: torch.devic
     return out
 
 
-def cpu_baseline(seconds_hint: float = 20.0):
-    """Oracle (CPU restatement, 1 thread) on a bounded sample of the same workload shape."""
+def cpu_threads() -> int:
+    """Host threads of the CPU baseline: the GPU box's CPU share (16 per GPU), capped by
+    the CPUs this process may run on."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline():
+    """OpenMP CPU path (oracle_find_matches_omp: per-genome SMLs in parallel, merge split by
+    key range; bit-identical to the serial restatement) on the host cores, seed stage of
+    BASELINE config 3 itself (8 x 100 Mbp related, w19)."""
     from oracle import oracle
 
-    G, n, p = 8, 16_000_000, 0.01   # about 20 s of one core
+    G, n, p = 8, 100_000_000, 0.01
+    th = cpu_threads()
     seqs = oracle.generate(G, n, p, 12345)
     seed = lm.getSeed(19)
     t0 = time.perf_counter()
-    _, _, st = oracle.find_matches(seqs, seed, seeds_only=True)
+    _, _, st = oracle.seed_probes(seqs, seed, omp_threads=th)
     dt = time.perf_counter() - t0
     return {
         "value": st["seedmers"] / dt,
         "unit": "seed-mers/s",
-        "cores": 1,
+        "cores": th,
         "kind": "port",
-        "sample": f"oracle MemHash seed stage (keys+SML sort+merge+accept+probe/bucket), {G} x {n // 10**6} Mbp "
-                  f"related p={p}, w19 seed 0x7b974ef, {st['seedmers']} seed-mers in {dt:.1f} s, 1 thread",
+        "cpu": cpu_model(),
+        "sample": f"OpenMP oracle MemHash seed stage (keys + per-genome SML sort in parallel, G-way merge split "
+                  f"by key range, acceptance, probes + buckets), BASELINE config 3 itself: {G} x {n // 10**6} Mbp "
+                  f"related p={p}, w19 seed 0x7b974ef, {st['seedmers']} seed-mers in {dt:.1f} s, {th} threads",
     }
 
 
 def cpu_baseline_mums():
-    """Oracle full FindMatches (1 thread) on the config-2 shape itself (4 x 10 Mbp related,
-    w15; about 15-20 s of one core)."""
+    """OpenMP oracle FindMatches (bucket replay in parallel, same MatchList as serial) on
+    the config-2 shape itself (4 x 10 Mbp related, w15)."""
     from oracle import oracle
 
     G, n, p = 4, 10_000_000, 0.01
+    th = cpu_threads()
     seqs = oracle.generate(G, n, p, 12345)
     t0 = time.perf_counter()
-    lengths, _, _ = oracle.find_matches(seqs, lm.getSeed(15))
+    lengths, _, _ = oracle.find_matches(seqs, lm.getSeed(15), omp_threads=th)
     dt = time.perf_counter() - t0
-    return {"value": len(lengths) / dt, "unit": "MUMs/s", "cores": 1, "kind": "port",
-            "sample": f"oracle MemHash::FindMatches (keys, SML sort, merge, ExtendMatch, AddHashEntry), {G} x "
-                      f"{n // 10**6} Mbp related p={p}, w15, {len(lengths)} matches in {dt:.1f} s, 1 thread"}
+    return {"value": len(lengths) / dt, "unit": "MUMs/s", "cores": th, "kind": "port", "cpu": cpu_model(),
+            "sample": f"OpenMP oracle MemHash::FindMatches (SMLs, merge by key range, ExtendMatch + AddHashEntry "
+                      f"per hash bucket in parallel), {G} x {n // 10**6} Mbp related p={p}, w15, {len(lengths)} "
+                      f"matches in {dt:.1f} s, {th} threads"}
 
 
 def run_mums(device: int, dev: torch.device, p: float = 0.01, reps: int = 3):
@@ -214,7 +241,6 @@ def main():
         stats = eng.stats
     for _ in range(args.warmup):
         run()
-    mh.SetProfiling(True)
 
     def barrier():
         if world > 1:
@@ -223,17 +249,12 @@ def main():
             else:
                 dist.barrier()
 
+    # timed region: K steps, no per-pass instrumentation events
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         run()
-        st = stats()
-        ms_dom += st["ms_dominant"]
-        bytes_dom += st["dominant_bytes"]
-        launches += st["dominant_launches"]
-        for k in phase:
-            phase[k] += st[k]
         if world > 1:
             exch_bytes += stage.last_exchange_bytes
     torch.cuda.synchronize()
@@ -243,6 +264,38 @@ def main():
     if world > 1:
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     dt = float(tmax.item())
+    # after it, the same K steps with HIP events around every sort-pass launch (on the
+    # context's stream) for the dominant kernel's live duration and the phase split
+    mh.SetProfiling(True)
+    for _ in range(args.steps):
+        run()
+        st = stats()
+        ms_dom += st["ms_dominant"]
+        bytes_dom += st["dominant_bytes"]
+        launches += st["dominant_launches"]
+        for k in phase:
+            phase[k] += st[k]
+    mh.SetProfiling(False)
+    mums_c3 = None
+    if world == 1 and args.workload == "c3" and not args.no_mums:
+        # MUMs/s on the metric's own config: full FindMatches of the resident C3 genomes
+        try:
+            mh.CreateMatches()   # warm
+            best = float("inf")
+            for _ in range(2):
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                mh.CreateMatches()
+                torch.cuda.synchronize()
+                best = min(best, time.perf_counter() - t1)
+            sm = mh.stats()
+            mums_c3 = {"mums_per_s": sm["mem_count"] / best, "matches": sm["mem_count"], "ms": best * 1e3,
+                       "probes": sm["probes"], "chains": sm["chains"], "collisions": sm["collision_count"],
+                       "workload": f"BASELINE config 3: {G} x {n // 10**6} Mbp related p=0.01, w19, full FindMatches",
+                       "phase_ms": {k: round(sm[k], 3) for k in ("ms_keys", "ms_sort", "ms_groups", "ms_buckets",
+                                                                  "ms_chains", "ms_replay", "ms_output")}}
+        except Exception as e:  # report, never hide
+            mums_c3 = {"error": str(e)}
     seedmers_total = sum(max(n - lm.getSeedLength(seed) + 1, 0) for _ in range(G))
     seedmers_rank = st["seedmers"]
     key_bytes = st["key_bytes"]
@@ -254,10 +307,13 @@ def main():
         value = seedmers_total * args.steps / dt
         achieved = bytes_dom / (ms_dom * 1e-3) / 1e9 if ms_dom > 0 else None
         traffic = None
-        # the committed PMC summary was measured on the default N=1 workload only
+        traffic_src = None
+        # PMC counters cannot be read inside this run: the figure is the committed rocprofv3
+        # FETCH_SIZE/WRITE_SIZE summary of the same kernel on the default N=1 workload
         if world == 1 and (G, n) == (8, 100_000_000) and os.path.exists(PROFILE_SUMMARY):
             try:
                 traffic = json.load(open(PROFILE_SUMMARY)).get("hbm_bytes_per_launch")
+                traffic_src = os.path.relpath(PROFILE_SUMMARY, ROOT) + " (rocprofv3 PMC passes, not this run)"
             except Exception:
                 traffic = None
         out = {
@@ -294,11 +350,16 @@ def main():
                 "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                 "traffic": traffic,
+                "traffic_source": traffic_src,
                 "bytes_per_launch": bytes_dom / max(launches, 1),
                 "avg_launch_ms": ms_dom / max(launches, 1),
+                "timing": "HIP events around each launch on the context's stream, in K profiled steps run "
+                          "after the timed region",
             },
             "phase_ms_per_step": {k: round(v / args.steps, 3) for k, v in phase.items()},
         }
+        if mums_c3 is not None:
+            out["mums_c3"] = mums_c3
         if not args.no_mums:
             try:
                 out["mums"] = run_mums(local, dev, 0.01)

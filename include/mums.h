@@ -135,6 +135,9 @@ int  mums_result_count(mums_ctx* ctx, uint64_t* count, uint32_t* seq_count);
 /* lengths[count]; starts[count * seq_count] row-major (match-major). */
 int  mums_result_copy(mums_ctx* ctx, uint64_t* lengths, int64_t* starts);
 
+/* MemHash::MemTableCount (MemHash.h:100; mem_table_count, MemHash.cpp:245): entries
+ * inserted per hash bucket of the last FindMatches; counts[table_size]. */
+int  mums_mem_table_count(mums_ctx* ctx, uint32_t* counts, uint32_t table_size);
 /* MemCount / MemCollisionCount (MemHash.h:94-97) + per-phase device timings. */
 int  mums_get_stats(mums_ctx* ctx, mums_stats* out);
 /* Record HIP events around each dominant-kernel launch (adds a few us per run). */
@@ -150,6 +153,8 @@ uint32_t mums_default_seed_weight(uint64_t avg_len);
 /* GetDnaSeedMer for every position of genome g after mums_find_stage(>=SEEDS):
  * out[p] = canonical key (SortedMerList.cpp:764-769, 64-bit left-aligned form). */
 int  mums_copy_seed_keys(mums_ctx* ctx, uint32_t genome, uint64_t* out, uint64_t cap);
+/* Same for positions [first, first + count) only (sampling genomes of billions of bases). */
+int  mums_copy_seed_keys_range(mums_ctx* ctx, uint32_t genome, uint64_t first, uint64_t count, uint64_t* out);
 /* MemorySML::Create (MemorySML.cpp:45-60): SML positions of genome g sorted by
  * full key, ties by ascending position. */
 int  mums_build_sml(mums_ctx* ctx, uint32_t genome, uint32_t* positions, uint64_t cap);

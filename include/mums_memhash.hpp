@@ -113,6 +113,62 @@ public:
     // MemCount / MemCollisionCount (MemHash.h:94-97)
     uint64_t MemCount() const { return stats().mem_count; }
     uint64_t MemCollisionCount() const { return stats().collision_count; }
+    // MemHash::MemTableCount (MemHash.h:100): entries inserted per hash bucket
+    void MemTableCount(std::vector<uint32_t>& table_count) const {
+        table_count.assign(table_size_, 0);
+        check(mums_mem_table_count(ctx_, table_count.data(), table_size_));
+    }
+    // MemHash::PrintDistribution (MemHash.cpp:253-264): bucket, entries, bases per line
+    void PrintDistribution(std::ostream& os) const {
+        std::vector<uint32_t> cnt;
+        MemTableCount(cnt);
+        MatchList ml;
+        GetMatchList(ml);
+        uint64_t e = 0;
+        for (uint32_t i = 0; i < cnt.size(); ++i) {
+            uint64_t bases = 0;
+            for (uint32_t k = 0; k < cnt[i]; ++k) bases += ml[e++].length;
+            os << i << '\t' << cnt[i] << '\t' << bases << '\n';
+        }
+    }
+    // MemHash::WriteFile (MemHash.cpp:301-324): header + every entry, bucket-major
+    void WriteFile(std::ostream& os, const std::vector<std::string>& names = {},
+                   const std::vector<uint64_t>& lengths = {}) const {
+        MatchList ml;
+        GetMatchList(ml);
+        const size_t G = ml.empty() ? lengths.size() : ml[0].starts.size();
+        os << "FormatVersion" << '\t' << 1 << "\n";
+        os << "SequenceCount" << '\t' << G << "\n";
+        for (size_t g = 0; g < G; ++g) {
+            const std::string nm = g < names.size() && !names[g].empty() ? names[g] : "null";
+            os << "Sequence" << g << "File" << '\t' << nm << "\n";
+            os << "Sequence" << g << "Length" << '\t' << (g < lengths.size() ? lengths[g] : 0) << "\n";
+        }
+        os << "MatchCount" << '\t' << MemCount() << std::endl;
+        for (const Match& m : ml) os << m << "\n";
+    }
+    // MemHash::FindMatchesFromPosition (MemHash.cpp:117-127)
+    virtual void FindMatchesFromPosition(MatchList& ml, const std::vector<uint64_t>& start_points) {
+        for (const auto& s : ml.seq_table) AddSequence(s);
+        check(mums_set_start_points(ctx_, start_points.data(), (uint32_t)start_points.size()));
+        const int rc = mums_find(ctx_);
+        (void)mums_set_start_points(ctx_, nullptr, 0);
+        check(rc);
+        GetMatchList(ml);
+    }
+    // MatchFinder::SetOffsetLog (MatchFinder.cpp:152-162): the lines the offset stream
+    // received during the last find (start points after every MER_REPEAT_LIMIT restart)
+    void WriteOffsetLog(std::ostream& os) const {
+        uint64_t rows = 0;
+        uint32_t G = 0;
+        check(mums_get_offset_log(ctx_, nullptr, 0, &rows, &G));
+        std::vector<uint64_t> v(rows * G);
+        if (rows) check(mums_get_offset_log(ctx_, v.data(), rows, &rows, &G));
+        for (uint64_t r = 0; r < rows; ++r) {
+            for (uint32_t g = 0; g < G; ++g) os << (g ? "\t" : "") << v[r * G + g];
+            os << std::endl;
+        }
+    }
     mums_stats stats() const {
         mums_stats s{};
         check(mums_get_stats(ctx_, &s));

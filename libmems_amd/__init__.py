@@ -92,7 +92,7 @@ EXPORTED_SYMBOLS = [
     "mums_shard_packed_info", "mums_shard_packed_copy", "mums_shard_find", "mums_set_parallel_compat",
     "mums_seed_occurrence", "mums_multiplicity_filter", "mums_length_filter", "mums_write_sml",
     "mums_add_genome_sml", "mums_set_pairwise", "mums_shard_slice", "mums_set_start_points",
-    "mums_get_offset_log",
+    "mums_get_offset_log", "mums_copy_seed_keys_range", "mums_mem_table_count",
 ]
 
 _lib: Optional[ctypes.CDLL] = None
@@ -158,6 +158,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mums_set_pairwise.argtypes = [vp, i32]
     lib.mums_shard_slice.argtypes = [vp, u32, vp, u32, u64, u64]
     lib.mums_set_start_points.argtypes = [vp, vp, u32]
+    lib.mums_copy_seed_keys_range.argtypes = [vp, u32, u64, u64, vp]
+    lib.mums_mem_table_count.argtypes = [vp, vp, u32]
     lib.mums_get_offset_log.argtypes = [vp, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(u32)]
     _lib = lib
     return lib
@@ -354,6 +356,39 @@ class MemHash:
     def MemCollisionCount(self) -> int:
         return int(self.stats()["collision_count"])
 
+    def MemTableCount(self) -> np.ndarray:
+        """MemHash::MemTableCount (MemHash.h:100): entries inserted per hash bucket."""
+        T = getattr(self, "_ts", 40000)
+        out = np.zeros(T, dtype=np.uint32)
+        self._check(self._lib.mums_mem_table_count(self._ctx, out.ctypes.data, T))
+        return out
+
+    def PrintDistribution(self, ml: Optional["MatchList"] = None) -> str:
+        """MemHash::PrintDistribution (MemHash.cpp:253-264): per bucket `i<TAB>count<TAB>bases`."""
+        counts = self.MemTableCount()
+        if ml is None:
+            ml = self.GetMatchList()
+        ends = np.cumsum(counts.astype(np.int64))
+        csum = np.concatenate([[0], np.cumsum(ml.lengths.astype(np.int64))])
+        bases = csum[ends] - csum[ends - counts.astype(np.int64)]
+        return "".join(f"{i}\t{int(c)}\t{int(b)}\n" for i, (c, b) in enumerate(zip(counts, bases)))
+
+    def WriteFile(self, ml: Optional["MatchList"] = None, names: Optional[Sequence[str]] = None,
+                  lengths: Optional[Sequence[int]] = None) -> str:
+        """MemHash::WriteFile (MemHash.cpp:301-324) text: header, then every entry bucket-major."""
+        if ml is None:
+            ml = self.GetMatchList()
+        G = ml.starts.shape[1] if len(ml) else len(lengths or [])
+        names = list(names) if names is not None else ["null"] * G
+        lengths = list(lengths) if lengths is not None else [0] * G
+        out = ["FormatVersion\t1\n", f"SequenceCount\t{G}\n"]
+        for g in range(G):
+            out.append(f"Sequence{g}File\t{names[g] or 'null'}\n")
+            out.append(f"Sequence{g}Length\t{lengths[g]}\n")
+        out.append(f"MatchCount\t{self.MemCount()}\n")
+        out.append(ml.text())
+        return "".join(out)
+
     def Probes(self):
         """Accepted probes of the last seed stage in AddHashEntry order: (buckets u32[P],
         ref_index u64[P]) -- hash bucket and smallest global seed-mer index of the group."""
@@ -369,6 +404,12 @@ class MemHash:
         out = np.zeros(max(m, 1), dtype=np.uint64)
         self._check(self._lib.mums_copy_seed_keys(self._ctx, genome, out.ctypes.data, m))
         return out[:m]
+
+    def SeedKeysRange(self, genome: int, first: int, count: int) -> np.ndarray:
+        """GetDnaSeedMer of positions [first, first + count) of one genome."""
+        out = np.zeros(count, dtype=np.uint64)
+        self._check(self._lib.mums_copy_seed_keys_range(self._ctx, genome, first, count, out.ctypes.data))
+        return out
 
     def SortedMerList(self, genome: int, m: int) -> np.ndarray:
         out = np.zeros(max(m, 1), dtype=np.uint32)

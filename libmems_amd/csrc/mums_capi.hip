@@ -1222,6 +1222,19 @@ int mums_result_copy(mums_ctx* ctx, uint64_t* lengths, int64_t* starts) {
     return MUMS_OK;
 }
 
+int mums_mem_table_count(mums_ctx* ctx, uint32_t* counts, uint32_t table_size) {
+    if (check_ctx(ctx) || !counts) return MUMS_E_INVALID;
+    if (ctx->stage_done < MUMS_STAGE_ALL) return fail(ctx, MUMS_E_INVALID, "no completed FindMatches on this context");
+    if (table_size != ctx->table_size) return fail(ctx, MUMS_E_INVALID, "table_size differs from the context's");
+    HIPCHK(hipSetDevice(ctx->device));
+    if (ctx->P == 0 && ctx->M == 0) {   // nothing hashed (the table buffers may be unset)
+        std::fill(counts, counts + table_size, 0u);
+        return MUMS_OK;
+    }
+    HIPCHK(hipMemcpy(counts, ctx->tsize.p, (size_t)table_size * 4, hipMemcpyDeviceToHost));
+    return MUMS_OK;
+}
+
 int mums_get_stats(mums_ctx* ctx, mums_stats* out) {
     if (check_ctx(ctx) || !out) return MUMS_E_INVALID;
     *out = ctx->st;
@@ -1249,6 +1262,24 @@ int mums_copy_seed_keys(mums_ctx* ctx, uint32_t genome, uint64_t* out, uint64_t 
                                  ctx->keybuf.as<uint64_t>(), ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     HIPCHK(hipMemcpy(out, ctx->keybuf.p, m * 8, hipMemcpyDeviceToHost));
+    return MUMS_OK;
+}
+
+int mums_copy_seed_keys_range(mums_ctx* ctx, uint32_t genome, uint64_t first, uint64_t count, uint64_t* out) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (ctx->stage_done < MUMS_STAGE_SEEDS) return fail(ctx, MUMS_E_INVALID, "keys not computed yet");
+    if (genome >= ctx->genomes.size()) return fail(ctx, MUMS_E_INVALID, "genome index out of range");
+    const uint64_t m = ctx->gt.m[genome];
+    if (first > m || count > m - first) return fail(ctx, MUMS_E_INVALID, "position range outside the genome's SML");
+    if (count == 0) return MUMS_OK;
+    HIPCHK(hipSetDevice(ctx->device));
+    // keys of positions [first & ~15, first + count) from the word holding position first
+    const uint64_t a = first & ~15ull, mm = first + count - a;
+    HIPCHK(ctx->keybuf.ensure(mm * 8));
+    HIPCHK(launch_keys_of_genome(ctx->ss, ctx->packed.as<uint32_t>() + ctx->gt.woff[genome] + a / 16, mm,
+                                 ctx->keybuf.as<uint64_t>(), ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipMemcpy(out, ctx->keybuf.as<uint64_t>() + (first - a), count * 8, hipMemcpyDeviceToHost));
     return MUMS_OK;
 }
 

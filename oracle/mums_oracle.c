@@ -470,6 +470,7 @@ typedef struct {
     uint32_t* plog_bucket; uint64_t* plog_ref; uint64_t plog_cap;
     int64_t* scratch;         /* G starts of the probe under construction */
     idmer_t* cm; idmer_t* hl; uint64_t cm_cap;   /* SearchRange's cur_match + hash list */
+    int64_t* rec; uint64_t rec_n, rec_cap;       /* OpenMP driver: AddHashEntry calls recorded as rows */
 } memhash_t;
 
 static uint32_t pool_add(memhash_t* h, const mhe_t* src) {
@@ -512,6 +513,17 @@ static void add_hash_entry(memhash_t* h, mhe_t* p) {
     uint32_t bi = (uint32_t)(((p->offset % T) + T) % T);
     bucket_t* b = &h->buckets[bi];
     ++h->probes;
+    if (h->rec_cap) {   /* record mode (oracle_find_matches_omp): the call as a row {starts, offset} */
+        const uint64_t W = (uint64_t)h->x.G + 1;
+        if (h->rec_n == h->rec_cap) {
+            h->rec_cap *= 2;
+            h->rec = (int64_t*)realloc(h->rec, h->rec_cap * W * sizeof(int64_t));
+        }
+        memcpy(h->rec + h->rec_n * W, p->s, (size_t)h->x.G * sizeof(int64_t));
+        h->rec[h->rec_n * W + (W - 1)] = p->offset;
+        ++h->rec_n;
+        return;
+    }
     if (h->seeds_only) {
         h->bucket_sum += bi;
         /* probe log (checking aid): the probe's identity = global index of its first start */
@@ -1002,6 +1014,227 @@ done:
 /* AddHashEntry replay of given probes (test aid for the sharded FindMatches): rows of
  * G+1 int64 {signed starts after SetDirection, offset} in AddHashEntry order; each is
  * looked up, extended and inserted exactly as in oracle_find_matches. */
+/* ------------------------------------------------------------------------- */
+/* OpenMP CPU path (the bench's CPU baseline on the host cores; TEST/BASELINE   */
+/* INFRASTRUCTURE).  Same result as oracle_find_matches, bit for bit:           */
+/*   1. per-genome keys + SortedMerList in parallel (MemorySML::Create per      */
+/*      genome, MemorySML.cpp:45-60; the reference builds them one by one,      */
+/*      MatchList.h:421);                                                        */
+/*   2. the G-way merge (SearchRange, MatchFinder.cpp:172-340) split into key   */
+/*      ranges cut at masked-key boundaries, one range per task; every          */
+/*      AddHashEntry call is recorded as a row, in key order per range;         */
+/*   3. rows grouped by hash bucket (stable), then the buckets replayed in      */
+/*      parallel: AddHashEntry (MemHash.cpp:209-251) only ever touches its own  */
+/*      bucket, and each bucket sees its calls in key order, so the bucket-     */
+/*      major MatchList (MemHash.h:182-203) equals the serial one.              */
+/* An input whose merge restarts (a group above MER_REPEAT_LIMIT), start points,*/
+/* or the ParallelMemHash compat mode run the serial path instead.              */
+/* ------------------------------------------------------------------------- */
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+static uint64_t lower_bound_masked(const bmer_t* v, uint64_t n, uint64_t mask, uint64_t q) {
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        uint64_t mid = lo + (hi - lo) / 2;
+        if ((v[mid].key & mask) < q) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+oracle_result* oracle_find_matches_omp(int G, const char* const* seqs, const uint64_t* lens,
+                                       const oracle_params* prm, int threads) {
+    if (G < 1 || G > 64) return NULL;
+    int serial_only = prm->parallel_compat || prm->start_points;
+    if (serial_only) return oracle_find_matches(G, seqs, lens, prm);
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#endif
+    oracle_result* res = (oracle_result*)calloc(1, sizeof(oracle_result));
+    res->G = G;
+    sml_ctx* ctx = (sml_ctx*)calloc((size_t)G, sizeof(sml_ctx));
+    uint32_t** words = (uint32_t**)calloc((size_t)G, sizeof(uint32_t*));
+    uint64_t** keys = (uint64_t**)calloc((size_t)G, sizeof(uint64_t*));
+    bmer_t** sml = (bmer_t**)calloc((size_t)G, sizeof(bmer_t*));
+    uint64_t* m = (uint64_t*)calloc((size_t)G, sizeof(uint64_t));
+    int bad = 0, fallback = 0;
+    #pragma omp parallel for schedule(dynamic, 1) reduction(|:bad)
+    for (int g = 0; g < G; ++g) {
+        if (sml_init(&ctx[g], seqs[g], lens[g], prm->seed, &words[g])) { bad = 1; continue; }
+        m[g] = sml_length(lens[g], ctx[g].L);
+        keys[g] = (uint64_t*)malloc((m[g] ? m[g] : 1) * sizeof(uint64_t));
+        for (uint64_t q = 0; q < m[g]; ++q) keys[g][q] = get_dna_seed_mer(&ctx[g], q);
+        sml[g] = build_sml(&ctx[g], keys[g], m[g]);
+    }
+    if (bad) { res->count = 0; goto done; }
+    for (int g = 0; g < G; ++g) res->seedmers += m[g];
+    {
+        const int L = ctx[0].L;
+        const uint64_t mask = ctx[0].seed_mask;
+        const uint32_t T = prm->table_size ? prm->table_size : 40000;
+        uint64_t* gbase = (uint64_t*)calloc((size_t)G + 1, sizeof(uint64_t));
+        for (int g = 0; g < G; ++g) gbase[g + 1] = gbase[g] + m[g];
+        memhash_t base;
+        memset(&base, 0, sizeof(base));
+        base.x.G = G;
+        base.x.L = L;
+        base.x.seed_mask = mask;
+        base.x.keys = (const uint64_t**)keys;
+        base.x.n = lens;
+        base.x.gnseqi_end = prm->gnseqi_end_neg1 ? (int64_t)-1 : INT64_MAX;
+        base.table_size = T;
+        base.gbase = gbase;
+        /* key ranges: splitters = masked keys at quantiles of the longest SML */
+        int big = 0;
+        for (int g = 1; g < G; ++g) if (m[g] > m[big]) big = g;
+        const int R = (int)(m[big] / 65536 + 1 < 4096 ? m[big] / 65536 + 1 : 4096);
+        uint64_t* split = (uint64_t*)malloc((size_t)(R + 1) * sizeof(uint64_t));
+        split[0] = 0;
+        for (int r = 1; r < R; ++r) split[r] = sml[big][(uint64_t)r * m[big] / (uint64_t)R].key & mask;
+        uint64_t* rlo = (uint64_t*)malloc((size_t)(R + 1) * (size_t)G * sizeof(uint64_t));
+        #pragma omp parallel for schedule(static)
+        for (int r = 0; r <= R; ++r)
+            for (int g = 0; g < G; ++g)
+                rlo[(uint64_t)r * G + g] = (r == R) ? m[g] : (r == 0 ? 0 : lower_bound_masked(sml[g], m[g], mask, split[r]));
+        int64_t** rrows = (int64_t**)calloc((size_t)R, sizeof(int64_t*));
+        uint64_t* rn = (uint64_t*)calloc((size_t)R, sizeof(uint64_t));
+        uint64_t maxg = 0, restarts = 0;
+        #pragma omp parallel for schedule(dynamic, 1) reduction(max:maxg) reduction(+:restarts)
+        for (int r = 0; r < R; ++r) {
+            memhash_t h = base;
+            h.rec_cap = 1024;
+            h.rec = (int64_t*)malloc(h.rec_cap * (size_t)(G + 1) * sizeof(int64_t));
+            h.scratch = (int64_t*)malloc((size_t)G * sizeof(int64_t));
+            oracle_result lr;
+            memset(&lr, 0, sizeof(lr));
+            uint64_t sp[64], sl[64];
+            for (int g = 0; g < G; ++g) {
+                sp[g] = rlo[(uint64_t)r * G + g];
+                sl[g] = rlo[(uint64_t)(r + 1) * G + g] - sp[g];
+            }
+            if (!search_range_lit(&h, prm, G, sml, m, lens, sp, sl, &lr)) restarts += 1;
+            if (lr.max_group > maxg) maxg = lr.max_group;
+            rrows[r] = h.rec;
+            rn[r] = h.rec_n;
+            free(h.scratch); free(h.cm); free(h.hl);
+        }
+        if (restarts || maxg > MER_REPEAT_LIMIT) fallback = 1;   /* the merge would restart: serial */
+        uint64_t P = 0;
+        for (int r = 0; r < R; ++r) P += rn[r];
+        const uint64_t W = (uint64_t)G + 1;
+        /* stable grouping of the rows (key order) by hash bucket */
+        uint32_t* rb = NULL;
+        uint64_t* boff = NULL;
+        uint64_t* order = NULL;
+        if (!fallback) {
+            int64_t** rowp = (int64_t**)malloc((P ? P : 1) * sizeof(int64_t*));
+            rb = (uint32_t*)malloc((P ? P : 1) * sizeof(uint32_t));
+            uint64_t k = 0;
+            for (int r = 0; r < R; ++r)
+                for (uint64_t i = 0; i < rn[r]; ++i, ++k) {
+                    rowp[k] = rrows[r] + i * W;
+                    const int64_t off = rowp[k][G];
+                    rb[k] = (uint32_t)(((off % (int64_t)T) + (int64_t)T) % (int64_t)T);
+                }
+            res->probes = P;
+            res->max_group = maxg;
+            if (prm->seeds_only) {   /* the AddHashEntry call log, key order */
+                res->plog_bucket = (uint32_t*)malloc((P ? P : 1) * sizeof(uint32_t));
+                res->plog_ref = (uint64_t*)malloc((P ? P : 1) * sizeof(uint64_t));
+                #pragma omp parallel for schedule(static)
+                for (uint64_t i = 0; i < P; ++i) {
+                    int f = 0;
+                    while (rowp[i][f] == 0) ++f;
+                    const int64_t s0 = rowp[i][f] < 0 ? -rowp[i][f] : rowp[i][f];
+                    res->plog_bucket[i] = rb[i];
+                    res->plog_ref[i] = gbase[f] + (uint64_t)(s0 - 1);
+                }
+            } else {
+                boff = (uint64_t*)calloc((size_t)T + 1, sizeof(uint64_t));
+                for (uint64_t i = 0; i < P; ++i) boff[rb[i] + 1]++;
+                for (uint32_t b = 0; b < T; ++b) boff[b + 1] += boff[b];
+                order = (uint64_t*)malloc((P ? P : 1) * sizeof(uint64_t));
+                uint64_t* fill = (uint64_t*)malloc(((size_t)T + 1) * sizeof(uint64_t));
+                memcpy(fill, boff, ((size_t)T + 1) * sizeof(uint64_t));
+                for (uint64_t i = 0; i < P; ++i) order[fill[rb[i]]++] = i;
+                free(fill);
+                bucket_t* buckets = (bucket_t*)calloc(T, sizeof(bucket_t));
+                int nth = 1;
+#ifdef _OPENMP
+                nth = omp_get_max_threads();
+#endif
+                memhash_t* th = (memhash_t*)calloc((size_t)nth, sizeof(memhash_t));
+                int* owner = (int*)calloc(T, sizeof(int));
+                #pragma omp parallel
+                {
+                    int tid = 0;
+#ifdef _OPENMP
+                    tid = omp_get_thread_num();
+#endif
+                    memhash_t* h = &th[tid];
+                    *h = base;
+                    h->buckets = buckets;
+                    int64_t* sv = (int64_t*)malloc((size_t)G * sizeof(int64_t));
+                    #pragma omp for schedule(dynamic, 16)
+                    for (uint32_t b = 0; b < T; ++b) {
+                        owner[b] = tid;
+                        for (uint64_t j = boff[b]; j < boff[b + 1]; ++j) {
+                            const int64_t* row = rowp[order[j]];
+                            mhe_t pr;
+                            memcpy(sv, row, (size_t)G * sizeof(int64_t));
+                            pr.s = sv;
+                            pr.len = L;
+                            pr.mersize = L;
+                            calc_offset(&pr, G);
+                            add_hash_entry(h, &pr);
+                        }
+                    }
+                    free(sv);
+                }
+                uint64_t M = 0, coll = 0;
+                for (int t = 0; t < nth; ++t) { M += th[t].mem_count; coll += th[t].collisions; }
+                res->count = M;
+                res->mem_count = M;
+                res->collision_count = coll;
+                res->lengths = (uint64_t*)malloc((M ? M : 1) * sizeof(uint64_t));
+                res->starts = (int64_t*)malloc((M ? M : 1) * (size_t)G * sizeof(int64_t));
+                uint64_t o = 0;
+                for (uint32_t b = 0; b < T; ++b) {
+                    const memhash_t* h = &th[owner[b]];
+                    for (uint32_t k2 = 0; k2 < buckets[b].n; ++k2) {
+                        const mhe_t* e = &h->pool[buckets[b].v[k2]];
+                        res->lengths[o] = (uint64_t)e->len;
+                        memcpy(res->starts + o * (uint64_t)G, e->s, (size_t)G * sizeof(int64_t));
+                        ++o;
+                    }
+                    free(buckets[b].v);
+                }
+                for (int t = 0; t < nth; ++t) { free(th[t].pool); free(th[t].spool); }
+                free(th); free(owner); free(buckets);
+            }
+            free(rowp);
+        }
+        for (int r = 0; r < R; ++r) free(rrows[r]);
+        free(rrows); free(rn); free(rlo); free(split); free(rb); free(boff); free(order); free(gbase);
+    }
+done:
+    for (int g = 0; g < G; ++g) { free(words[g]); free(keys[g]); free(sml[g]); }
+    free(ctx); free(words); free(keys); free(sml); free(m);
+    if (bad) { oracle_result_free(res); return NULL; }
+    if (fallback) { oracle_result_free(res); return oracle_find_matches(G, seqs, lens, prm); }
+    return res;
+}
+
+int oracle_omp_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+
 oracle_result* oracle_replay_rows(int G, const char* const* seqs, const uint64_t* lens, const oracle_params* prm,
                                   const int64_t* rows, uint64_t nrows) {
     if (G < 1 || G > 64) return NULL;

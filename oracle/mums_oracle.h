@@ -82,6 +82,13 @@ uint64_t oracle_result_chunks(const oracle_result* r);     /* compat: chunks sea
 uint64_t oracle_result_restarts(const oracle_result* r);   /* MER_REPEAT_LIMIT restarts */
 int      oracle_result_offset_log(const oracle_result* r, uint64_t* out); /* restarts x G start points */
 void     oracle_result_free(oracle_result* r);
+/* OpenMP driver of the same restatement (the bench's CPU baseline on the host cores):
+ * per-genome SMLs in parallel, the merge split by key range, the hash buckets replayed
+ * in parallel; bit-identical to oracle_find_matches (falls back to it for restarting
+ * merges, start points and the compat mode).  threads <= 0: the OpenMP default. */
+oracle_result* oracle_find_matches_omp(int G, const char* const* seqs, const uint64_t* lens,
+                                       const oracle_params* prm, int threads);
+int      oracle_omp_threads(void);
 /* AddHashEntry replay of probe rows {starts[G], offset} (sharded FindMatches checks). */
 oracle_result* oracle_replay_rows(int G, const char* const* seqs, const uint64_t* lens, const oracle_params* prm,
                                   const int64_t* rows, uint64_t nrows);

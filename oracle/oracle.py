@@ -62,6 +62,10 @@ def lib() -> ctypes.CDLL:
         L.oracle_find_matches.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(u64),
                                           ctypes.POINTER(_Params)]
         L.oracle_find_matches.restype = vp
+        L.oracle_find_matches_omp.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(u64),
+                                              ctypes.POINTER(_Params), ctypes.c_int]
+        L.oracle_find_matches_omp.restype = vp
+        L.oracle_omp_threads.restype = ctypes.c_int
         for f in ("count", "mem_count", "collision_count", "max_group", "probe_count", "seedmers", "chunks", "restarts"):
             fn = getattr(L, f"oracle_result_{f}")
             fn.argtypes = [vp]
@@ -127,11 +131,13 @@ def find_matches(seqs: Sequence[bytes], seed: int, repeat_tol: int = 0, enum_tol
                  table_size: int = 40000, masked: bool = False, seq_mask: int = 0,
                  gnseqi_end_neg1: bool = False, seeds_only: bool = False, parallel_compat: bool = False,
                  chunk_size: int = 0, pairwise: bool = False,
-                 start_points: Sequence[int] | None = None) -> Tuple[np.ndarray, np.ndarray, dict]:
+                 start_points: Sequence[int] | None = None,
+                 omp_threads: int | None = None) -> Tuple[np.ndarray, np.ndarray, dict]:
     """MemHash::FindMatches restated; returns (lengths[M], starts[M,G], counters).
     parallel_compat: ParallelMemHash::FindMatches instead (ParallelMemHash.cpp:42-121),
     chunk_size = its CHUNK_SIZE (0 = 200000).  start_points: FindMatchesFromPosition
-    (MemHash.cpp:117-127) start SML index per genome."""
+    (MemHash.cpp:117-127) start SML index per genome.  omp_threads: run the OpenMP driver
+    (oracle_find_matches_omp, same result) on that many threads (0 = OpenMP default)."""
     G = len(seqs)
     arr = (ctypes.c_char_p * G)(*seqs)
     lens = (ctypes.c_uint64 * G)(*[len(s) for s in seqs])
@@ -142,7 +148,10 @@ def find_matches(seqs: Sequence[bytes], seed: int, repeat_tol: int = 0, enum_tol
                   int(seeds_only), int(parallel_compat), chunk_size, int(pairwise),
                   ctypes.cast(sp, ctypes.c_void_p) if sp is not None else None)
     L = lib()
-    r = L.oracle_find_matches(G, arr, lens, ctypes.byref(prm))
+    if omp_threads is None:
+        r = L.oracle_find_matches(G, arr, lens, ctypes.byref(prm))
+    else:
+        r = L.oracle_find_matches_omp(G, arr, lens, ctypes.byref(prm), int(omp_threads))
     if not r:
         raise ValueError("oracle rejected input")
     try:
@@ -192,7 +201,7 @@ def replay_rows(seqs: Sequence[bytes], seed: int, rows: np.ndarray, table_size: 
 
 
 def seed_probes(seqs: Sequence[bytes], seed: int, table_size: int = 40000, parallel_compat: bool = False,
-                chunk_size: int = 0) -> Tuple[np.ndarray, np.ndarray, dict]:
+                chunk_size: int = 0, omp_threads: int | None = None) -> Tuple[np.ndarray, np.ndarray, dict]:
     """Seed stage only (keys, SMLs, G-way merge, acceptance, probes): the AddHashEntry calls
     in order as (bucket[P], ref[P]) with ref = global seed-mer index of the probe's first
     start (genome bases = cumulative SMLLength), plus the counters."""
@@ -201,7 +210,10 @@ def seed_probes(seqs: Sequence[bytes], seed: int, table_size: int = 40000, paral
     lens = (ctypes.c_uint64 * G)(*[len(s) for s in seqs])
     prm = _Params(seed, 0, 1, table_size, 0, 0, 0, 1, int(parallel_compat), chunk_size)
     L = lib()
-    r = L.oracle_find_matches(G, arr, lens, ctypes.byref(prm))
+    if omp_threads is None:
+        r = L.oracle_find_matches(G, arr, lens, ctypes.byref(prm))
+    else:
+        r = L.oracle_find_matches_omp(G, arr, lens, ctypes.byref(prm), int(omp_threads))
     if not r:
         raise ValueError("oracle rejected input")
     try:

@@ -1,0 +1,58 @@
+"""Large-input known answers of the CPU oracle, recorded once in this container (the GPU
+box checks the HIP path against them without re-running the oracle for minutes):
+
+  c3: BASELINE config 3, 8 x 100 Mbp related (p = 0.01, genome 2 reverse-complemented,
+      SURVEY.md Appendix C generator, seed 12345), default seed weight 19 (0x7b974ef),
+      MemHash::FindMatches -> match count, md5 of the MatchList text, MemCount,
+      collisions, AddHashEntry calls (probes), largest seed group, restarts.
+  c5s: BASELINE config 5 scaled to 2 x 50 Mbp (w19), same record.
+
+    python tests/golden/make_large_golden.py [c3] [c5s]   (c3: about 15 minutes, ~25 GB RAM)
+"""
+import hashlib
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+from oracle import oracle  # noqa: E402
+
+CASES = {
+    "c3": dict(G=8, n=100_000_000, p=0.01, gen_seed=12345, w=19),
+    # BASELINE config 5 scaled to 2 x 50 Mbp: the GPU runs it in the chunked mode (forced)
+    "c5s": dict(G=2, n=50_000_000, p=0.01, gen_seed=12345, w=19),
+}
+OUT = os.path.join(HERE, "large_cases.json")
+
+
+def run(name):
+    c = CASES[name]
+    t0 = time.time()
+    seqs = oracle.generate(c["G"], c["n"], c["p"], c["gen_seed"])
+    seed = oracle.get_seed(c["w"])
+    lengths, starts, st = oracle.find_matches(seqs, seed)
+    del seqs
+    txt = oracle.match_text(lengths, starts)
+    rec = dict(c, seed=seed, matches=int(len(lengths)), md5=hashlib.md5(txt.encode()).hexdigest(),
+               mem_count=int(st["mem_count"]), collisions=int(st["collision_count"]), probes=int(st["probes"]),
+               max_group=int(st["max_group"]), restarts=int(st["restarts"]), seedmers=int(st["seedmers"]),
+               first_line=txt.split("\n", 1)[0], oracle_seconds=round(time.time() - t0, 1))
+    return rec
+
+
+def main():
+    names = sys.argv[1:] or list(CASES)
+    have = json.load(open(OUT)) if os.path.exists(OUT) else {}
+    for name in names:
+        rec = run(name)
+        have[name] = rec
+        print(name, json.dumps(rec))
+        with open(OUT, "w") as f:
+            json.dump(have, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,128 @@
+"""BASELINE configs 3 and 5 at full size on the GPU.
+
+C3 (8 x 100 Mbp, w19): the whole FindMatches against the oracle's known answer recorded in
+this container (tests/golden/large_cases.json, tests/golden/make_large_golden.py): match
+count, md5 of the MatchList text, MemCount, collisions, AddHashEntry calls.
+C5 (2 x 3 Gbp, w19, chunked mode, > 2^32 seed-mers): the seed stage at full size, checked
+by size-independent properties (seed-mer count, probe / group counts invariant under 16 vs
+32 key chunks and the streaming layout, sampled keys = oracle keys), and a scaled 2 x 50 Mbp
+C5 FindMatches through the chunked mode against the oracle's recorded answer."""
+import hashlib
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+_LARGE_PATH = os.path.join(GOLDEN, "large_cases.json")
+LARGE = json.load(open(_LARGE_PATH)) if os.path.exists(_LARGE_PATH) else {}
+
+
+def case(name):
+    if name not in LARGE:
+        pytest.skip(f"{name} known answer not recorded (tests/golden/make_large_golden.py)")
+    return LARGE[name]
+
+
+def md5_text(ml):
+    return hashlib.md5(ml.text().encode()).hexdigest()
+
+
+def test_c3_findmatches_known_answer(gpu_lib, oracle_mod):
+    import torch
+    c = case("c3")
+    seqs = oracle_mod.generate(c["G"], c["n"], c["p"], c["gen_seed"])
+    dev = [torch.frombuffer(bytearray(s), dtype=torch.uint8).cuda() for s in seqs]
+    del seqs
+    with gpu_lib.MemHash(0) as mh:
+        mh.SetSeed(c["seed"])
+        ml = mh.FindMatches(dev)
+        st = mh.stats()
+    assert st["seedmers"] == c["seedmers"]
+    assert st["probes"] == c["probes"]
+    assert len(ml) == c["matches"] and st["mem_count"] == c["mem_count"]
+    assert st["collision_count"] == c["collisions"]
+    assert st["restarts"] == c["restarts"]
+    assert md5_text(ml) == c["md5"]
+
+
+def test_c5_scaled_findmatches_chunked(gpu_lib, oracle_mod):
+    c = case("c5s")
+    seqs = oracle_mod.generate(c["G"], c["n"], c["p"], c["gen_seed"])
+    os.environ["MUMS_DEV_CHUNK_RECORDS"] = str(16_000_000)   # 2 x 50 Mbp in >= 8 key chunks
+    try:
+        with gpu_lib.MemHash(0) as mh:
+            mh.SetSeed(c["seed"])
+            ml = mh.FindMatches(seqs)
+            st = mh.stats()
+    finally:
+        os.environ.pop("MUMS_DEV_CHUNK_RECORDS", None)
+    assert st["chunks"] >= 8
+    assert st["probes"] == c["probes"]
+    assert len(ml) == c["matches"] and st["collision_count"] == c["collisions"]
+    assert md5_text(ml) == c["md5"]
+
+
+def synth_pair(n, p, seed, dev):
+    import torch
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(seed)
+    lut = torch.tensor(list(b"ACGT"), dtype=torch.uint8, device=dev)
+    a = torch.empty(n, dtype=torch.uint8, device=dev)
+    b = torch.empty(n, dtype=torch.uint8, device=dev)
+    step = 1 << 28
+    for o in range(0, n, step):
+        k = min(step, n - o)
+        x = lut[torch.randint(0, 4, (k,), generator=gen, device=dev, dtype=torch.uint8).long()]
+        a[o:o + k] = x
+        mut = torch.rand(k, generator=gen, device=dev) < p
+        sub = lut[torch.randint(0, 4, (k,), generator=gen, device=dev, dtype=torch.uint8).long()]
+        b[o:o + k] = torch.where(mut, sub, x)
+    torch.cuda.synchronize()
+    return a, b
+
+
+def test_c5_full_seed_stage(gpu_lib, oracle_mod):
+    import torch
+    n = 3_000_000_000
+    dev = torch.device("cuda", 0)
+    a, b = synth_pair(n, 0.01, 2024, dev)
+    seed = oracle_mod.get_seed(19)
+    L = 27
+    m = n - L + 1
+    counts = {}
+    with gpu_lib.MemHash(0) as mh:
+        mh.SetSeed(seed)
+        mh.AddSequence(a)
+        mh.AddSequence(b)
+        for cap in (None, 200_000_000):   # default chunks, then twice as many (or more)
+            if cap:
+                os.environ["MUMS_DEV_CHUNK_RECORDS"] = str(cap)
+            try:
+                mh.FindStage(gpu_lib.STAGE_SEEDS)
+            finally:
+                os.environ.pop("MUMS_DEV_CHUNK_RECORDS", None)
+            st = mh.stats()
+            counts[cap] = (st["chunks"], st["probes"], st["groups"], st["seedmers"])
+        # sampled windows: GPU keys == oracle keys of the same bases
+        rng = random.Random(5)
+        for g, t in ((0, a), (1, b)):
+            for _ in range(3):
+                s0 = rng.randrange(0, m - 4000)
+                ref = oracle_mod.seed_keys(bytes(t[s0:s0 + 4000 + L - 1].cpu().numpy()), seed)
+                got = mh.SeedKeysRange(g, s0, 4000)
+                assert np.array_equal(got, ref)
+        # the last window of each genome
+        for g, t in ((0, a), (1, b)):
+            ref = oracle_mod.seed_keys(bytes(t[m - 100:].cpu().numpy()), seed)
+            assert np.array_equal(mh.SeedKeysRange(g, m - 100, 100), ref)
+    c0, c1 = counts[None], counts[200_000_000]
+    assert c0[3] == c1[3] == 2 * m
+    assert c1[0] > c0[0] >= 8
+    assert c0[1:3] == c1[1:3]
+    assert c0[1] > 0.9 * m   # related genomes: nearly every position is a shared seed

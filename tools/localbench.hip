@@ -1,6 +1,6 @@
 // Development harness: LDS local sort of pre-split sub-buckets (2^msd equal ranges of
 // random 32-bit keys whose top msd bits are the range id), 4 passes.
-#include "../libmems_amd/csrc/local_sort.hip"
+#include "proto/local_sort.hip"
 #include <cstdio>
 #include <vector>
 #include <random>

@@ -3,8 +3,8 @@
 // scatter's output shape).  Checks final order (key, then index) inside every bucket.
 #include "../libmems_amd/csrc/scan.hip"
 #include "../libmems_amd/csrc/radix_seg.hip"
-#include "../libmems_amd/csrc/msd_pass.hip"
-#include "../libmems_amd/csrc/local_sort.hip"
+#include "proto/msd_pass.hip"
+#include "proto/local_sort.hip"
 #include <cstdio>
 #include <vector>
 #include <random>

@@ -6,7 +6,7 @@
 // through LDS (wave64 ballot match-any ranking, per-wave digit counters), and
 // writes the sorted range once: 16 HBM bytes per record for the whole tail of the
 // sort instead of 16 per pass.
-#include "mums_internal.h"
+#include "../../libmems_amd/csrc/mums_internal.h"
 
 namespace mums {
 

@@ -8,7 +8,7 @@
 // consecutive tiles of a bucket, interleaved claim order), with D = 2^kBits digits:
 // every thread owns D/256 consecutive digits of the scan and the look-back.
 // HBM bytes per record: 8 (histogram read) + 8 + 8 (the pass).
-#include "mums_internal.h"
+#include "../../libmems_amd/csrc/mums_internal.h"
 
 namespace mums {
 
