@@ -125,4 +125,6 @@ def test_c5_full_seed_stage(gpu_lib, oracle_mod):
     assert c0[3] == c1[3] == 2 * m
     assert c1[0] > c0[0] >= 8
     assert c0[1:3] == c1[1:3]
-    assert c0[1] > 0.9 * m   # related genomes: nearly every position is a shared seed
+    # related genomes (p = 0.01): a position is a shared unique seed when its 19 care bases
+    # are unmutated, 0.99^19 = 0.83 of the positions
+    assert c0[1] > 0.8 * m
