@@ -13,10 +13,10 @@
 //   3. chain_link_kernel  : neighbours on one line are in one chain iff a chain of
 //                           hits (gaps <= L) joins them: gap <= L, else a walk of
 //                           the hit columns between them; segment ends walk on to
-//                           the chain's end (left walks in chain_left_kernel)
+//                           the chain's end (left walks in chain_left_kernel).  Walks
+//                           test 64 columns per step with packed-word XORs (hit_word)
 //   4. chain_walk_kernel  : walks longer than a per-lane budget, one workgroup each
-//                           (L-jumps speculated across 256 lanes, as ExtendMatch's
-//                           directions 0/1, then the furthest hit within L)
+//                           (one 64-column hit word per lane, scanned in walk order)
 //   5. chain_seg / chain_entry kernels: segment ids (scan), the extended entry of
 //                           every chain and chain_of[probe].
 // The replay (replay.hip) then inserts chain entries without extending anything.
@@ -33,9 +33,9 @@ namespace mums {
 namespace {
 
 #ifndef MUMS_WALK_BUDGET
-#define MUMS_WALK_BUDGET 48   // measured: 24 / 48 / 96 / 384 -> chains 6.0 / 5.6 / 6.1 / 8.5 ms (related 4 x 10 Mbp)
+#define MUMS_WALK_BUDGET 16
 #endif
-constexpr int kWalkBudget = MUMS_WALK_BUDGET;   // hit evaluations per lane before a walk goes to a workgroup
+constexpr int kWalkBudget = MUMS_WALK_BUDGET;   // 64-column hit words per lane before a walk goes to a workgroup
 
 struct WalkItem {
     uint32_t j;      // position in line order
@@ -143,48 +143,186 @@ __device__ __forceinline__ bool hit_lane(int64_t c, const Mhe<MG>& P, const Geno
     return ok;
 }
 
-// Greedy walk along the chain from hit column cur in direction dir: repeatedly move
-// to the furthest hit within L columns.  state 0: the chain ends at the returned
-// column; 1: reached `stop`; 2: budget spent (returned column = progress so far).
-template <int MG>
-__device__ int64_t walk_lane(int dir, int64_t cur, int64_t stop, int budget, int L, const Mhe<MG>& P,
-                             const GenomeTable& gt, int64_t clo, int64_t chi, const uint32_t* __restrict__ packed,
-                             const SeedSpec& ss, int* state) {
-    for (;;) {
-        if (dir > 0 ? cur >= stop : cur <= stop) { *state = 1; return cur; }
-        if (budget <= 0) { *state = 2; return cur; }
-        int d = L;
-        for (; d >= 1; --d) {
-            --budget;
-            if (hit_lane<MG>(cur + dir * (int64_t)d, P, gt, clo, chi, packed, ss)) break;
-        }
-        if (d == 0) { *state = 0; return cur; }
-        cur += dir * (int64_t)d;
+// ---- bit-parallel hit words -----------------------------------------------------------
+// For a palindromic care set (every rank-0 pattern of SeedMasks.h) the
+// canonical-key test of hit_lane reduces to base comparisons along the line (A.9): a
+// forward component hits at column c iff its care bases equal the reference's, a reverse
+// component iff its reverse-complemented window's care bases do (and, for even w only,
+// the window is not its own reverse complement: then both parities are 0 and the strand
+// test of hit_lane fails).  So 64 columns are tested at once: per component the 96 bases
+// under the 64 windows are XORed with the reference's (2 bits per base, reverse
+// components reverse-complemented word-wise), OR-ed into one mismatch mask, and a column
+// hits iff no care offset of its window sees a mismatch.
+
+// 96 bases (3 x 32, first base in bits 63-62) from base position p of the genome at word
+// gw of the packed array; words outside [0, nwords) read as 0 (masked by the caller)
+__device__ __forceinline__ void bases96(const uint32_t* __restrict__ W, uint64_t nwords, uint64_t gw, int64_t p,
+                                        uint64_t c[3]) {
+    const int64_t wi = (int64_t)gw + (p >> 4);
+    const int sh = 2 * (int)(p & 15);
+    uint64_t w[7];
+    #pragma unroll
+    for (int i = 0; i < 7; ++i) {
+        const int64_t k = wi + i;
+        w[i] = (k >= 0 && (uint64_t)k < nwords) ? W[k] : 0u;
+    }
+    #pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const uint64_t hi = (w[2 * k] << 32) | w[2 * k + 1];
+        const uint64_t lo = w[2 * k + 2];
+        c[k] = (hi << sh) | ((lo << sh) >> 32);
     }
 }
 
-__device__ __forceinline__ int wg_first_true(bool pred, int* red) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t b = __ballot(pred);
-    if (lane == 0) red[wv] = b ? wv * 64 + (__ffsll((long long)b) - 1) : kBlock;
-    __syncthreads();
-    int r = red[0];
-    #pragma unroll
-    for (int w = 1; w < kBlock / 64; ++w) r = min(r, red[w]);
-    __syncthreads();
-    return r;
+// reverse complement of 32 packed bases
+__device__ __forceinline__ uint64_t rc32(uint64_t x) {
+    x = __builtin_bitreverse64(x);
+    x = ((x >> 1) & 0x5555555555555555ull) | ((x & 0x5555555555555555ull) << 1);
+    return ~x;
 }
 
-__device__ __forceinline__ int wg_last_true(bool pred, int* red) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t b = __ballot(pred);
-    if (lane == 0) red[wv] = b ? wv * 64 + 63 - __clzll((long long)b) : -1;
-    __syncthreads();
-    int r = red[0];
+// 2-bit XOR word of 32 bases -> 32-bit mismatch mask, base i at bit i
+__device__ __forceinline__ uint32_t mism32(uint64_t x) {
+    x = (x | (x >> 1)) & 0x5555555555555555ull;
+    x = (x | (x >> 1)) & 0x3333333333333333ull;
+    x = (x | (x >> 2)) & 0x0f0f0f0f0f0f0f0full;
+    x = (x | (x >> 4)) & 0x00ff00ff00ff00ffull;
+    x = (x | (x >> 8)) & 0x0000ffff0000ffffull;
+    x = (x | (x >> 16)) & 0x00000000ffffffffull;
+    return __builtin_bitreverse32((uint32_t)x);
+}
+
+struct LineSpec {
+    uint64_t care;     // bit k: offset k of the window is a care position
+    int L;
+    int bitpar;        // 1: palindromic care set (hit words by base comparison)
+    int even_w;        // even weight: self-reverse-complement windows need hit_lane
+    uint64_t nwords;   // packed words (bounds of the loads)
+};
+
+__device__ __forceinline__ LineSpec line_spec(const SeedSpec& ss, const GenomeTable& gt) {
+    LineSpec ls;
+    const uint64_t pat = ss.pattern >> __builtin_ctzll(ss.pattern);
+    const uint64_t rev = __builtin_bitreverse64(pat) >> (64 - ss.L);
+    ls.care = rev;   // bit k <-> pattern bit L-1-k
+    ls.L = ss.L;
+    ls.bitpar = rev == pat;
+    ls.even_w = !(ss.w & 1);
+    ls.nwords = gt.woff[gt.G];
+    return ls;
+}
+
+// hit bits of columns c0 .. c0+63 (bit i = column c0 + i) of the line of P
+template <int MG>
+__device__ uint64_t hit_word(int64_t c0, const Mhe<MG>& P, const GenomeTable& gt, int64_t clo, int64_t chi,
+                             const uint32_t* __restrict__ packed, const SeedSpec& ss, const LineSpec& ls) {
+    if (c0 > chi || c0 + 63 < clo) return 0;
+    uint64_t valid = ~0ull;
+    if (c0 < clo) valid &= ~0ull << (clo - c0);
+    if (c0 + 63 > chi) valid &= ~0ull >> (c0 + 63 - chi);
+    const int ref = first_start(P);
+    const int64_t sref = start_at(P, ref);
+    if (!ls.bitpar || sref <= 0) {   // generic: canonical keys column by column
+        uint64_t h = 0;
+        for (int i = 0; i < 64; ++i)
+            if ((valid >> i) & 1) h |= (uint64_t)hit_lane<MG>(c0 + i, P, gt, clo, chi, packed, ss) << i;
+        return h;
+    }
+    uint64_t R[3];
+    bases96(packed, ls.nwords, gt.woff[ref], sref - 1 + c0, R);
+    uint64_t acc0 = 0, acc1 = 0, acc2 = 0;
+    bool rev = false;
     #pragma unroll
-    for (int w = 1; w < kBlock / 64; ++w) r = max(r, red[w]);
-    __syncthreads();
-    return r;
+    for (int g = 0; g < MG; ++g) {
+        const int64_t s = P.s[g];
+        if (g < gt.G && g != ref && s != 0) {
+            uint64_t C[3];
+            if (s > 0) {
+                bases96(packed, ls.nwords, gt.woff[g], s - 1 + c0, C);
+                acc0 |= R[0] ^ C[0];
+                acc1 |= R[1] ^ C[1];
+                acc2 |= R[2] ^ C[2];
+            } else {   // column t <-> complement of base |s| + L - 2 - c0 - t
+                bases96(packed, ls.nwords, gt.woff[g], -s + ls.L - 2 - c0 - 95, C);
+                acc0 |= R[0] ^ rc32(C[2]);
+                acc1 |= R[1] ^ rc32(C[1]);
+                acc2 |= R[2] ^ rc32(C[0]);
+                rev = true;
+            }
+        }
+    }
+    const uint64_t lo = (uint64_t)mism32(acc0) | ((uint64_t)mism32(acc1) << 32);
+    const uint64_t hi = mism32(acc2);
+    uint64_t any = 0;
+    for (uint64_t cm = ls.care; cm; cm &= cm - 1) {
+        const int k = __builtin_ctzll(cm);
+        any |= k ? ((lo >> k) | (hi << (64 - k))) : lo;
+    }
+    uint64_t h = ~any & valid;
+    if (rev && ls.even_w) {   // drop self-reverse-complement windows (exact test)
+        for (uint64_t t = h; t; t &= t - 1) {
+            const int i = __builtin_ctzll(t);
+            if (!hit_lane<MG>(c0 + i, P, gt, clo, chi, packed, ss)) h &= ~(1ull << i);
+        }
+    }
+    return h;
+}
+
+// 64 hit bits in walk order: bit i = column from + dir * i
+template <int MG>
+__device__ __forceinline__ uint64_t hit_word_dir(int dir, int64_t from, const Mhe<MG>& P, const GenomeTable& gt,
+                                                 int64_t clo, int64_t chi, const uint32_t* __restrict__ packed,
+                                                 const SeedSpec& ss, const LineSpec& ls) {
+    if (dir > 0) return hit_word<MG>(from, P, gt, clo, chi, packed, ss, ls);
+    return __builtin_bitreverse64(hit_word<MG>(from - 63, P, gt, clo, chi, packed, ss, ls));
+}
+
+// One 64-column word of a chain walk.  Walk offsets u >= 0 (column = start + dir * u);
+// *last = offset of the last chain hit so far, the word covers offsets u0 .. u0+63.
+// Returns true when the chain ends (L consecutive misses after *last),
+// with *last its final hit; else *last = the word's last hit.
+__device__ __forceinline__ bool scan_word(uint64_t H, int64_t u0, int64_t* last, int L) {
+    const int64_t gap = u0 - *last - 1;   // misses since the last hit
+    if (H == 0) return true;             // 64 >= L misses
+    const int f = __builtin_ctzll(H);
+    if (gap + f >= L) return true;
+    // bit i of a: offsets i .. i+L-1 of this word all miss (runs into the next word are
+    // found there through gap)
+    uint64_t a = ~H;
+    int len = 1;
+    while (2 * len <= L) { a &= a >> len; len *= 2; }
+    if (len < L) a &= a >> (L - len);
+    if (a) {
+        const int r0 = __builtin_ctzll(a);   // > f: a run needs L misses, f < L
+        const uint64_t below = H & ((1ull << r0) - 1);
+        *last = u0 + (63 - __builtin_clzll(below));
+        return true;
+    }
+    *last = u0 + (63 - __builtin_clzll(H));
+    return false;
+}
+
+// Chain walk from hit column cur in direction dir, one word (64 columns) per step.
+// state 0: the chain ends at the returned column; 1: the chain reaches `stop` (returned:
+// a chain hit at or past it); 2: budget spent (returned: the last hit reached).
+template <int MG>
+__device__ int64_t walk_lane(int dir, int64_t cur, int64_t stop, int budget, const Mhe<MG>& P, const GenomeTable& gt,
+                             int64_t clo, int64_t chi, const uint32_t* __restrict__ packed, const SeedSpec& ss,
+                             const LineSpec& ls, int* state) {
+    int64_t last = 0, u0 = 1;
+    for (;;) {
+        const int64_t col = cur + dir * last;
+        if (dir > 0 ? col >= stop : col <= stop) { *state = 1; return col; }
+        if (budget-- <= 0) { *state = 2; return col; }
+        const uint64_t H = hit_word_dir<MG>(dir, cur + dir * u0, P, gt, clo, chi, packed, ss, ls);
+        const bool broke = scan_word(H, u0, &last, ls.L);
+        u0 += 64;
+        if (broke) {
+            const int64_t c = cur + dir * last;
+            *state = (dir > 0 ? c >= stop : c <= stop) ? 1 : 0;
+            return c;
+        }
+    }
 }
 
 // ---- kernels ------------------------------------------------------------------------
@@ -213,6 +351,7 @@ __global__ __launch_bounds__(kBlock) void chain_link_kernel(View v, const uint64
     const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (j >= P) return;
     const int L = ss.L;
+    const LineSpec ls = line_spec(ss, gt);
     Mhe<MG> A, B;
     probe_of<MG, View>(v, probe_info, ord[j], gt, mp, L, A);
     bool same = false;
@@ -226,7 +365,7 @@ __global__ __launch_bounds__(kBlock) void chain_link_kernel(View v, const uint64
     int state;
     if (same) {
         const int64_t stop = start_at(B, first_start(B)) - xa - L;
-        const int64_t c = walk_lane<MG>(+1, 0, stop, kWalkBudget, L, A, gt, clo, chi, packed, ss, &state);
+        const int64_t c = walk_lane<MG>(+1, 0, stop, kWalkBudget, A, gt, clo, chi, packed, ss, ls, &state);
         if (state == 1) {
             link[j] = 1;
         } else if (state == 0) {
@@ -239,7 +378,7 @@ __global__ __launch_bounds__(kBlock) void chain_link_kernel(View v, const uint64
         }
     } else {
         link[j] = 0;
-        const int64_t c = walk_lane<MG>(+1, 0, INT64_MAX, kWalkBudget, L, A, gt, clo, chi, packed, ss, &state);
+        const int64_t c = walk_lane<MG>(+1, 0, INT64_MAX, kWalkBudget, A, gt, clo, chi, packed, ss, ls, &state);
         if (state == 0) {
             rcol[j] = xa + c;
         } else {
@@ -261,13 +400,14 @@ __global__ __launch_bounds__(kBlock) void chain_left_kernel(View v, const uint64
     if (j >= P) return;
     if (j > 0 && link[j - 1]) return;
     const int L = ss.L;
+    const LineSpec ls = line_spec(ss, gt);
     Mhe<MG> A;
     probe_of<MG, View>(v, probe_info, ord[j], gt, mp, L, A);
     const int64_t xa = start_at(A, first_start(A));
     int64_t clo, chi;
     frame_bounds<MG>(A, gt, &clo, &chi);
     int state;
-    const int64_t c = walk_lane<MG>(-1, 0, INT64_MIN, kWalkBudget, L, A, gt, clo, chi, packed, ss, &state);
+    const int64_t c = walk_lane<MG>(-1, 0, INT64_MIN, kWalkBudget, A, gt, clo, chi, packed, ss, ls, &state);
     if (state == 0) {
         lcol[j] = xa + c;
     } else {
@@ -276,17 +416,11 @@ __global__ __launch_bounds__(kBlock) void chain_left_kernel(View v, const uint64
     }
 }
 
-// Long walks, one workgroup per item (grid-stride over the queue).  Each iteration
-// evaluates the 1024 columns after the current chain end (4 per lane, one 64-column
-// ballot word per wave and sub-step) and one lane scans the 16 words for the first
-// run of >= L columns without a hit: the chain ends at the last hit before it (the
-// maximal chain of hits with gaps <= L); without such a run the walk
-// continues from the last hit of the window.
-#ifndef MUMS_WALK_CPL
-#define MUMS_WALK_CPL 4
-#endif
-constexpr int kWalkCols = MUMS_WALK_CPL * kBlock;   // columns per workgroup step (per lane: MUMS_WALK_CPL)
-
+// Long walks, one workgroup per item (grid-stride over the queue).  Each step evaluates
+// the kBlock words (64 columns each) after the chain's last hit, one word per lane, and
+// one lane scans them in walk order for the first run of L misses (scan_word): the chain
+// ends at the last hit before it; else the walk continues from the last
+// hit of the step.
 template <int MG, typename View>
 __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64_t* __restrict__ probe_info,
                                                             GenomeTable gt, MatchParams mp, SeedSpec ss,
@@ -296,11 +430,12 @@ __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64
                                                             const unsigned int* __restrict__ qcount,
                                                             uint8_t* __restrict__ link, int64_t* __restrict__ rcol,
                                                             int64_t* __restrict__ lcol) {
-    __shared__ uint64_t words[kWalkCols / 64];
-    __shared__ int64_t s_adv;
-    __shared__ int s_broke;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    __shared__ uint64_t words[kBlock];
+    __shared__ int64_t s_last;
+    __shared__ int s_done;
+    const int tid = threadIdx.x;
     const int L = ss.L;
+    const LineSpec ls = line_spec(ss, gt);
     const unsigned nq = *qcount;
     for (unsigned qi = blockIdx.x; qi < nq; qi += gridDim.x) {
         const WalkItem it = queue[qi];
@@ -310,66 +445,41 @@ __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64
         int64_t clo, chi;
         frame_bounds<MG>(A, gt, &clo, &chi);
         const int dir = it.kind == 2 ? -1 : +1;
-        int64_t cur = it.cur;
-        bool reached = false;
-        for (;;) {
-            if (dir > 0 ? cur >= it.stop : cur <= it.stop) { reached = true; break; }
-            #pragma unroll
-            for (int r = 0; r < kWalkCols / kBlock; ++r) {   // column offsets 1 + 256 r + tid
-                const int64_t k = 1 + (int64_t)r * kBlock + tid;
-                const uint64_t m = __ballot(hit_lane<MG>(cur + dir * k, A, gt, clo, chi, packed, ss));
-                if (lane == 0) words[r * (kBlock / 64) + wv] = m;
-            }
+        const int64_t cur = it.cur;   // walk offsets u from here: column = cur + dir * u
+        const int64_t stopu = dir > 0 ? (it.stop == INT64_MAX ? INT64_MAX : it.stop - cur)
+                                      : (it.stop == INT64_MIN ? INT64_MAX : cur - it.stop);
+        int64_t last = 0, u0 = 1;
+        bool reached = last >= stopu;
+        while (!reached) {
+            words[tid] = hit_word_dir<MG>(dir, cur + dir * (u0 + 64 * (int64_t)tid), A, gt, clo, chi, packed, ss, ls);
             __syncthreads();
             if (tid == 0) {
-                int64_t last = 0;   // offset of the last reachable hit (0 = cur)
-                int carry = 0;      // columns without a hit since it
-                int broke = 0;
-                for (int wi = 0; wi < kWalkCols / 64 && !broke; ++wi) {
-                    const uint64_t x = words[wi];
-                    if (x == 0) {
-                        carry += 64;
-                        broke = carry >= L;
-                        continue;
-                    }
-                    const int f = __builtin_ctzll(x);
-                    if (carry + f >= L) { broke = 1; break; }
-                    // bit i of a: columns i .. i+L-1 of this word all miss
-                    uint64_t a = ~x;
-                    int len = 1;
-                    while (2 * len <= L) { a &= a >> len; len *= 2; }
-                    if (len < L) a &= a >> (L - len);
-                    if (a) {
-                        const int r0 = __builtin_ctzll(a);
-                        const uint64_t below = x & ((1ull << r0) - 1);
-                        last = (int64_t)wi * 64 + (63 - __builtin_clzll(below)) + 1;
-                        broke = 1;
-                        break;
-                    }
-                    const int hb = 63 - __builtin_clzll(x);
-                    last = (int64_t)wi * 64 + hb + 1;
-                    carry = 63 - hb;
+                int64_t lst = last;
+                int done = 0;
+                for (int k = 0; k < kBlock && !done; ++k) {
+                    done = scan_word(words[k], u0 + 64 * (int64_t)k, &lst, L) ? 1 : 0;
+                    if (lst >= stopu) done = 2;
                 }
-                s_adv = last;
-                s_broke = broke;
+                s_last = lst;
+                s_done = done;
             }
             __syncthreads();
-            cur += dir * s_adv;
-            const int broke = s_broke;
+            last = s_last;
+            const int done = s_done;
             __syncthreads();
-            if (broke) {
-                reached = dir > 0 ? cur >= it.stop : cur <= it.stop;
-                break;
-            }
+            u0 += 64 * (int64_t)kBlock;
+            reached = last >= stopu;
+            if (done) break;
         }
         if (tid == 0) {
+            const int64_t c = cur + dir * last;
             if (it.kind == 0) {
                 link[it.j] = reached ? 1 : 0;
-                if (!reached) rcol[it.j] = xa + cur;
+                if (!reached) rcol[it.j] = xa + c;
             } else if (it.kind == 1) {
-                rcol[it.j] = xa + cur;
+                rcol[it.j] = xa + c;
             } else {
-                lcol[it.j] = xa + cur;
+                lcol[it.j] = xa + c;
             }
         }
         __syncthreads();

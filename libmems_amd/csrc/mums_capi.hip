@@ -340,9 +340,9 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
     ctx->M = ctx->hc.nmatches;
     HIPCHK(ctx->out_len.ensure((ctx->M + 1) * 8));
     HIPCHK(ctx->out_s.ensure((ctx->M + 1) * (size_t)G * 8));
-    HIPCHK(launch_emit(ctx->tsize.as<uint32_t>(), ctx->obase.as<uint32_t>(), ctx->bstart.as<uint32_t>(),
-                       ctx->tbl.as<uint32_t>(), ctx->pool.as<int64_t>(), G, Tb, ctx->out_len.as<uint64_t>(),
-                       ctx->out_s.as<int64_t>(), st));
+    HIPCHK(launch_emit(ctx->obase.as<uint32_t>(), ctx->bstart.as<uint32_t>(), ctx->tbl.as<uint32_t>(),
+                       ctx->pool.as<int64_t>(), G, Tb, ctx->M, ctx->out_len.as<uint64_t>(), ctx->out_s.as<int64_t>(),
+                       st));
     HIPCHK(hipEventRecord(ctx->ev[EV_OUTPUT], st));
     ctx->stage_done = MUMS_STAGE_ALL;
     return MUMS_OK;

@@ -224,9 +224,8 @@ template <int MG, typename View>
 hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const GenomeTable& gt, const MatchParams& mp,
                          const SeedSpec& ss, const uint32_t* packed, void* d_chain_tmp, void* d_scan_tmp,
                          void* d_radix_tmp, uint32_t* chain_of, int64_t* pool, uint32_t* d_nchains, hipStream_t st);
-hipError_t launch_emit(const uint32_t* tsize, const uint32_t* obase, const uint32_t* bstart, const uint32_t* tbl,
-                       const int64_t* pool, int G, uint32_t table_size, uint64_t* out_len, int64_t* out_s,
-                       hipStream_t st);
+hipError_t launch_emit(const uint32_t* obase, const uint32_t* bstart, const uint32_t* tbl, const int64_t* pool, int G,
+                       uint32_t table_size, uint64_t M, uint64_t* out_len, int64_t* out_s, hipStream_t st);
 
 // sml_tools.hip: SeedOccurrenceList and MatchList filters
 size_t occ_tmp_bytes(uint64_t m);

@@ -475,23 +475,29 @@ __global__ void bucket_ranges_kernel(const uint32_t* __restrict__ sb, uint64_t P
 }
 
 // MemHash::GetMatchList (MemHash.h:182-203): bucket-major, vector order
-__global__ __launch_bounds__(kBlock) void emit_kernel(const uint32_t* __restrict__ tsize,
-                                                      const uint32_t* __restrict__ obase,
+// MatchList output (GetMatchList, MemHash.h:182-203): output row o belongs to the bucket
+// b with obase[b] <= o < obase[b] + tsize[b] (last bucket whose exclusive output base is
+// <= o); one row per thread, so a bucket holding most entries (the main diagonal of
+// related genomes) is written by the whole grid.
+__global__ __launch_bounds__(kBlock) void emit_kernel(const uint32_t* __restrict__ obase,
                                                       const uint32_t* __restrict__ bstart,
                                                       const uint32_t* __restrict__ tbl,
-                                                      const int64_t* __restrict__ pool, int G,
-                                                      uint64_t* __restrict__ out_len, int64_t* __restrict__ out_s) {
-    const uint32_t b = blockIdx.x;
-    const uint32_t n = tsize[b];
-    if (n == 0) return;
-    const uint64_t o = obase[b];
-    const uint32_t beg = bstart[b];
-    for (uint32_t k = threadIdx.x; k < n; k += kBlock) {
-        const uint32_t id = tbl[beg + k];
-        const int64_t* e = pool + (uint64_t)id * (uint64_t)(G + 2);
-        out_len[o + k] = (uint64_t)e[0];
-        for (int g = 0; g < G; ++g) out_s[(o + k) * (uint64_t)G + g] = e[2 + g];
+                                                      const int64_t* __restrict__ pool, int G, uint32_t table_size,
+                                                      uint64_t M, uint64_t* __restrict__ out_len,
+                                                      int64_t* __restrict__ out_s) {
+    const uint64_t o = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (o >= M) return;
+    uint32_t lo = 0, n = table_size;   // upper_bound(obase, o) - 1
+    while (n > 0) {
+        const uint32_t h = n >> 1;
+        if ((uint64_t)obase[lo + h] <= o) { lo += h + 1; n -= h + 1; }
+        else n = h;
     }
+    const uint32_t b = lo - 1;
+    const uint32_t id = tbl[bstart[b] + (uint32_t)(o - obase[b])];
+    const int64_t* e = pool + (uint64_t)id * (uint64_t)(G + 2);
+    out_len[o] = (uint64_t)e[0];
+    for (int g = 0; g < G; ++g) out_s[o * (uint64_t)G + g] = e[2 + g];
 }
 
 }  // namespace
@@ -589,11 +595,11 @@ hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, i
     return hipGetLastError();
 }
 
-hipError_t launch_emit(const uint32_t* tsize, const uint32_t* obase, const uint32_t* bstart, const uint32_t* tbl,
-                       const int64_t* pool, int G, uint32_t table_size, uint64_t* out_len, int64_t* out_s,
-                       hipStream_t st) {
-    hipLaunchKernelGGL(emit_kernel, dim3(table_size), dim3(kBlock), 0, st, tsize, obase, bstart, tbl, pool, G,
-                       out_len, out_s);
+hipError_t launch_emit(const uint32_t* obase, const uint32_t* bstart, const uint32_t* tbl, const int64_t* pool, int G,
+                       uint32_t table_size, uint64_t M, uint64_t* out_len, int64_t* out_s, hipStream_t st) {
+    if (M == 0) return hipSuccess;
+    hipLaunchKernelGGL(emit_kernel, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, obase, bstart,
+                       tbl, pool, G, table_size, M, out_len, out_s);
     return hipGetLastError();
 }
 
