@@ -15,8 +15,8 @@
 //                           the hit columns between them; segment ends walk on to
 //                           the chain's end (left walks in chain_left_kernel).  Walks
 //                           test 64 columns per step with packed-word XORs (hit_word)
-//   4. chain_walk_kernel  : walks longer than a per-lane budget, one workgroup each
-//                           (one 64-column hit word per lane, scanned in walk order)
+//   4. chain_walk_kernel  : walks longer than a per-lane budget, one wave each
+//                           (one 64-column hit word per lane, break found by ballot)
 //   5. chain_seg / chain_entry kernels: segment ids (scan), the extended entry of
 //                           every chain and chain_of[probe].
 // The replay (replay.hip) then inserts chain entries without extending anything.
@@ -33,7 +33,7 @@ namespace mums {
 namespace {
 
 #ifndef MUMS_WALK_BUDGET
-#define MUMS_WALK_BUDGET 16
+#define MUMS_WALK_BUDGET 2
 #endif
 constexpr int kWalkBudget = MUMS_WALK_BUDGET;   // 64-column hit words per lane before a walk goes to a workgroup
 
@@ -416,11 +416,12 @@ __global__ __launch_bounds__(kBlock) void chain_left_kernel(View v, const uint64
     }
 }
 
-// Long walks, one workgroup per item (grid-stride over the queue).  Each step evaluates
-// the kBlock words (64 columns each) after the chain's last hit, one word per lane, and
-// one lane scans them in walk order for the first run of L misses (scan_word): the chain
-// ends at the last hit before it; else the walk continues from the last
-// hit of the step.
+// Long walks, one wave per item (grid-stride over the queue).  Each step evaluates the
+// 64 words (64 columns each) after the chain's last hit, one word per lane; the chain
+// ends at the first lane whose word holds a run of L misses after a hit, or whose first
+// hit lies L or more columns after the previous lane's last hit (the
+// maximal chain of hits with gaps <= L).  A ballot finds that lane, shuffles fetch the
+// last hit before the break.
 template <int MG, typename View>
 __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64_t* __restrict__ probe_info,
                                                             GenomeTable gt, MatchParams mp, SeedSpec ss,
@@ -430,14 +431,12 @@ __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64
                                                             const unsigned int* __restrict__ qcount,
                                                             uint8_t* __restrict__ link, int64_t* __restrict__ rcol,
                                                             int64_t* __restrict__ lcol) {
-    __shared__ uint64_t words[kBlock];
-    __shared__ int64_t s_last;
-    __shared__ int s_done;
-    const int tid = threadIdx.x;
+    const int lane = threadIdx.x & 63;
     const int L = ss.L;
     const LineSpec ls = line_spec(ss, gt);
     const unsigned nq = *qcount;
-    for (unsigned qi = blockIdx.x; qi < nq; qi += gridDim.x) {
+    const unsigned nwaves = gridDim.x * (kBlock / 64);
+    for (unsigned qi = (blockIdx.x * kBlock + threadIdx.x) >> 6; qi < nq; qi += nwaves) {
         const WalkItem it = queue[qi];
         Mhe<MG> A;
         probe_of<MG, View>(v, probe_info, ord[it.j], gt, mp, L, A);
@@ -451,27 +450,37 @@ __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64
         int64_t last = 0, u0 = 1;
         bool reached = last >= stopu;
         while (!reached) {
-            words[tid] = hit_word_dir<MG>(dir, cur + dir * (u0 + 64 * (int64_t)tid), A, gt, clo, chi, packed, ss, ls);
-            __syncthreads();
-            if (tid == 0) {
-                int64_t lst = last;
-                int done = 0;
-                for (int k = 0; k < kBlock && !done; ++k) {
-                    done = scan_word(words[k], u0 + 64 * (int64_t)k, &lst, L) ? 1 : 0;
-                    if (lst >= stopu) done = 2;
-                }
-                s_last = lst;
-                s_done = done;
+            const uint64_t H = hit_word_dir<MG>(dir, cur + dir * (u0 + 64 * (int64_t)lane), A, gt, clo, chi, packed,
+                                                ss, ls);
+            const int f = H ? __builtin_ctzll(H) : 64;
+            const int hb = H ? 63 - __builtin_clzll(H) : -1;
+            int rend = -1;   // last hit before a run of L misses inside the word
+            if (H) {
+                uint64_t a = ~H;
+                int len = 1;
+                while (2 * len <= L) { a &= a >> len; len *= 2; }
+                if (len < L) a &= a >> (L - len);
+                if (a) rend = 63 - __builtin_clzll(H & ((1ull << __builtin_ctzll(a)) - 1));
             }
-            __syncthreads();
-            last = s_last;
-            const int done = s_done;
-            __syncthreads();
-            u0 += 64 * (int64_t)kBlock;
+            const int prev_hb = __shfl_up(hb, 1);
+            const int64_t miss = lane == 0 ? (u0 - last - 1) + f : (int64_t)(63 - prev_hb) + f;
+            const bool brk_in = H == 0 || miss >= L;
+            const uint64_t bm = __ballot(brk_in || rend >= 0);
+            if (bm) {
+                const int k = __builtin_ctzll(bm);
+                const int kin = __shfl(brk_in ? 1 : 0, k);
+                const int hprev = __shfl(hb, k > 0 ? k - 1 : 0);
+                const int rk = __shfl(rend, k);
+                if (kin) last = k == 0 ? last : u0 + 64 * (int64_t)(k - 1) + hprev;
+                else last = u0 + 64 * (int64_t)k + rk;
+                reached = last >= stopu;
+                break;
+            }
+            last = u0 + 64 * 63 + __shfl(hb, 63);
+            u0 += 64 * 64;
             reached = last >= stopu;
-            if (done) break;
         }
-        if (tid == 0) {
+        if (lane == 0) {
             const int64_t c = cur + dir * last;
             if (it.kind == 0) {
                 link[it.j] = reached ? 1 : 0;
@@ -482,7 +491,6 @@ __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64
                 lcol[it.j] = xa + c;
             }
         }
-        __syncthreads();
     }
 }
 
@@ -543,10 +551,11 @@ inline unsigned grid_of(uint64_t n) { return (unsigned)((n + kBlock - 1) / kBloc
 
 }  // namespace
 
-size_t chain_tmp_bytes(uint64_t P) {
+size_t chain_tmp_bytes(uint64_t P, uint32_t Tb) {
     // lkey, sort A/B keys (3 x 8) + vals A/B (2 x 4) + link (1) + rcol, lcol, seg_r (3 x 8)
-    // + seg (4) + queue (24) + padding
-    return P * (24 + 8 + 1 + 24 + 4 + sizeof(WalkItem)) + 64 * 16;
+    // + seg (4) + queue (24) + padding.  The replay reuses it: per chain <= 76 B, then the
+    // big-bucket scratch (count 4 + scan 4 + slot 16 per probe, + 4 per bucket)
+    return P * (24 + 8 + 1 + 24 + 4 + sizeof(WalkItem) + 16 + 24) + (uint64_t)Tb * 4 + 64 * 64;
 }
 
 // Chain labelling of the P probes (key order): chain_of[k] = chain of probe k;

@@ -312,7 +312,7 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
     // summaries, their compacted copies, keep-flag scan, compacted bucket ranges (replay.hip)
     HIPCHK(ctx->summ.ensure((ctx->P + 1) * 64 + (ctx->P + 64) * 4 + ((size_t)Tb + 64) * 8 +
                             scan_tmp_bytes(ctx->P + 2) + 4096));
-    HIPCHK(ctx->chain_tmp.ensure(chain_tmp_bytes(ctx->P + 1)));
+    HIPCHK(ctx->chain_tmp.ensure(chain_tmp_bytes(ctx->P + 1, Tb)));
     HIPCHK(ctx->radix_tmp.ensure(radix_tmp_bytes(ctx->P + 1)));
     HIPCHK(ctx->tmp.ensure(std::max(scan_tmp_bytes(ctx->P + 1), scan_tmp_bytes(Tb))));
     HIPCHK(hipMemsetAsync(&dc->max_bucket, 0, 4, st));
@@ -337,6 +337,7 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
     HIPCHK(exclusive_scan_u32(ctx->obase.as<uint32_t>(), Tb, ctx->tmp.p, &dc->nmatches, st));
     HIPCHK(hipMemcpyAsync(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    if (ctx->hc.err & 4u) return fail(ctx, MUMS_E_HIP, "bucket replay: an insert broke the rank order (internal error)");
     ctx->M = ctx->hc.nmatches;
     HIPCHK(ctx->out_len.ensure((ctx->M + 1) * 8));
     HIPCHK(ctx->out_s.ensure((ctx->M + 1) * (size_t)G * 8));

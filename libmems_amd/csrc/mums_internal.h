@@ -219,7 +219,7 @@ hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, i
                          uint32_t nch, void* d_tmp, void* d_radix_tmp, uint32_t lds_cap, uint32_t* tsize, void* ctr,
                          uint64_t* dbg, hipStream_t st);
 // chains.hip: chain labelling of the probes (key order) before the replay
-size_t chain_tmp_bytes(uint64_t P);
+size_t chain_tmp_bytes(uint64_t P, uint32_t Tb);
 template <int MG, typename View>
 hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const GenomeTable& gt, const MatchParams& mp,
                          const SeedSpec& ss, const uint32_t* packed, void* d_chain_tmp, void* d_scan_tmp,

@@ -20,6 +20,10 @@
 // registers; per round every unconsumed lane runs its lower_bound against the
 // current vector, the workgroup takes the first non-colliding probe (ballot),
 // inserts its chain entry with a one-barrier LDS shift and goes on after it.
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
 #include "match_device.h"
 #include "seed_device.h"
 
@@ -74,6 +78,25 @@ __device__ __forceinline__ int slot_equiv(const uint4 X, uint32_t vmask, int64_t
 
 // std::lower_bound (libstdc++: half = len >> 1, middle = first + half) over slots
 // tb[0..t); full(id) = MheCompare(entry id, V) for the rare undecided slots
+template <typename Acc, typename Full>
+__device__ __forceinline__ uint32_t lower_bound_acc(Acc&& at, uint32_t t, uint32_t vmask, int64_t vs, int64_t vl,
+                                                   uint32_t vcid, Full&& full) {
+    uint32_t first = 0, len = t;
+    while (len > 0) {
+        const uint32_t half = len >> 1, mid = first + half;
+        const uint4 X = at(mid);
+        int r = slot_cmp(X, vmask, vs, vl, vcid);
+        if (r == 2) r = full(X.x) ? 1 : 0;
+        if (r) {
+            first = mid + 1;
+            len = len - half - 1;
+        } else {
+            len = half;
+        }
+    }
+    return first;
+}
+
 template <typename Full>
 __device__ __forceinline__ uint32_t lower_bound_slots(const uint4* tb, uint32_t t, uint32_t vmask, int64_t vs,
                                                      int64_t vl, uint32_t vcid, Full&& full) {
@@ -185,22 +208,32 @@ __global__ __launch_bounds__(kBlock) void chain_next_kernel(const uint32_t* __re
 // first-genome start) and is partitioned with respect to such a probe.
 // summ_b[q] = {chain entry's first-genome start, its length, its rank | tie}: the slot
 // an insert of this probe's chain writes, and its order among the bucket's chains.
+// per chain {entry's first-genome start, its length, its rank, next_s}: one 16-B record
+// the probe pass gathers (instead of the G + 2 int64 pool entry per probe)
+__global__ __launch_bounds__(kBlock) void chain_sb_kernel(const int64_t* __restrict__ pool, uint32_t nch, int G,
+                                                          const uint32_t* __restrict__ rank,
+                                                          const uint32_t* __restrict__ next_s,
+                                                          uint4* __restrict__ chain_sb) {
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    if (c >= nch) return;
+    const int64_t* e = pool + (uint64_t)c * (uint64_t)(G + 2);
+    int64_t es = 0;
+    for (int g = G - 1; g >= 0; --g) es = e[2 + g] != 0 ? e[2 + g] : es;
+    chain_sb[c] = make_uint4((uint32_t)es, (uint32_t)e[0], rank[c], next_s[c]);
+}
+
 __global__ __launch_bounds__(kBlock) void probe_flags_kernel(uint4* __restrict__ summ, uint4* __restrict__ summ_b,
                                                              uint64_t P, const uint32_t* __restrict__ first_pos,
-                                                             const uint32_t* __restrict__ next_s,
-                                                             const uint32_t* __restrict__ rank,
-                                                             const int64_t* __restrict__ pool, int G) {
+                                                             const uint4* __restrict__ chain_sb) {
     const uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (q >= P) return;
     uint4 r = summ[q];
+    const uint4 cs = chain_sb[r.z];
     const bool first = first_pos[r.z] == (uint32_t)q;
-    const bool susp = !first && r.y >= next_s[r.z];
+    const bool susp = !first && r.y >= cs.w;
     r.w |= (first ? 0x80000000u : 0u) | (susp ? 0x40000000u : 0u);
     summ[q] = r;
-    const int64_t* e = pool + (uint64_t)r.z * (uint64_t)(G + 2);
-    int64_t es = 0;
-    for (int g = G - 1; g >= 0; --g) es = e[2 + g] != 0 ? e[2 + g] : es;
-    summ_b[q] = make_uint4((uint32_t)es, (uint32_t)e[0], rank[r.z], 0u);
+    summ_b[q] = make_uint4(cs.x, cs.y, cs.z, 0u);
 }
 
 // the probe of stream group k (AddHashEntry's argument), built on the rare slow path
@@ -420,6 +453,226 @@ __global__ __launch_bounds__(RB) void replay_kernel(
     }
 }
 
+// Big buckets with few exact-search probes (the main diagonal of related genomes: 10^6
+// chain-first inserts and a handful of suspicious probes).  The vector is always sorted by
+// chain rank, duplicates adjacent, so it is held as a copy count per rank
+// of the bucket, cnt[r]: a run of chain-first probes only sets its ranks' counts, and
+// before each suspicious probe an exclusive scan E of the counts gives the virtual vector
+// V[i] = slot of the rank r with E[r] <= i < E[r + 1], on which that probe runs the exact
+// libstdc++ lower_bound of AddHashEntry (MemHash.cpp:215-247).  An insert must land
+// between its rank's neighbours (else the bucket is flagged: DevCounters.err bit 2).
+// Buckets with tied chains or more than kBigSlow suspicious probes stay on replay_kernel;
+// handled buckets get cend = cbeg so that replay_kernel skips them.
+constexpr uint32_t kBigBucket = 4096;   // compacted probes above which a bucket may come here
+                                        // (MUMS_DEV_BIG_BUCKET overrides it: tests)
+constexpr int kBigSlow = 2048;          // suspicious probes per bucket (LDS list)
+constexpr int kBigRB = 1024;
+
+__device__ __forceinline__ uint32_t blk_scan_excl(uint32_t v, uint32_t* red, uint32_t* total) {
+    // exclusive block scan over kBigRB lanes (wave scans + wave totals in LDS)
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t x = v;
+    #pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) red[wv] = x;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+    for (int w = 0; w < kBigRB / 64; ++w) {
+        const uint32_t r = red[w];
+        base += w < wv ? r : 0u;
+        tot += r;
+    }
+    __syncthreads();
+    *total = tot;
+    return base + x - v;
+}
+
+// E[0..R] = exclusive scan of cnt[0..R); returns E[R].  Tiles of kBigIPT * kBigRB counts
+// are loaded coalesced into LDS (tile), scanned as kBigIPT consecutive counts per lane and
+// written back coalesced.
+constexpr int kBigIPT = 8;
+__device__ uint32_t scan_counts(const uint32_t* __restrict__ cnt, uint32_t* __restrict__ E, uint32_t R, uint32_t* red,
+                                uint32_t* tile) {
+    const uint32_t tid = threadIdx.x;
+    constexpr uint32_t T = kBigIPT * kBigRB;
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < R; base += T) {
+        #pragma unroll
+        for (int k = 0; k < kBigIPT; ++k) {
+            const uint32_t i = base + k * kBigRB + tid;
+            tile[k * kBigRB + tid] = i < R ? cnt[i] : 0u;
+        }
+        __syncthreads();
+        uint32_t v[kBigIPT], sum = 0;
+        #pragma unroll
+        for (int k = 0; k < kBigIPT; ++k) {
+            v[k] = tile[tid * kBigIPT + k];
+            sum += v[k];
+        }
+        uint32_t tot;
+        uint32_t run = carry + blk_scan_excl(sum, red, &tot);   // barriers inside: tile reads are done
+        #pragma unroll
+        for (int k = 0; k < kBigIPT; ++k) {
+            tile[tid * kBigIPT + k] = run;
+            run += v[k];
+        }
+        __syncthreads();
+        #pragma unroll
+        for (int k = 0; k < kBigIPT; ++k) {
+            const uint32_t i = base + k * kBigRB + tid;
+            if (i < R) E[i] = tile[k * kBigRB + tid];
+        }
+        carry += tot;
+        __syncthreads();
+    }
+    if (tid == 0) E[R] = carry;
+    __syncthreads();
+    return carry;
+}
+
+template <int MG, typename View>
+__global__ __launch_bounds__(kBigRB) void replay_big_kernel(
+    View v, GenomeTable gt, MatchParams mp, int L, const uint64_t* __restrict__ probe_info,
+    const uint4* __restrict__ summ, const uint4* __restrict__ summ_b, const uint32_t* __restrict__ cbeg,
+    uint32_t* __restrict__ cend, const uint32_t* __restrict__ obase, uint32_t* __restrict__ tbl,
+    const int64_t* __restrict__ pool, const uint4* __restrict__ chain_sb, uint32_t* __restrict__ scr_cnt,
+    uint32_t* __restrict__ scr_e, uint4* __restrict__ scr_slot, uint32_t* __restrict__ tsize, DevCounters* ctr, uint32_t big_min) {
+    __shared__ uint32_t slow[kBigSlow], slow_sorted[kBigSlow];
+    __shared__ uint32_t red[kBigRB / 64];
+    __shared__ uint32_t s_ns, s_bad, s_rmin, s_rmax;
+    __shared__ uint32_t tile[kBigIPT * kBigRB];
+    const uint32_t b = blockIdx.x, tid = threadIdx.x;
+    const uint32_t beg = cbeg[b], K = cend[b] - beg;
+    if (K <= big_min) return;
+    if (tid == 0) { s_ns = 0; s_bad = 0; s_rmin = 0xFFFFFFFFu; s_rmax = 0; }
+    __syncthreads();
+    uint32_t rmin = 0xFFFFFFFFu, rmax = 0;
+    for (uint32_t k = tid; k < K; k += kBigRB) {
+        const uint4 a = summ[beg + k], c = summ_b[beg + k];
+        if (c.z & 0x80000000u) s_bad = 1;                     // tied chains: exact order unknown
+        if (a.w & 0x80000000u) {
+            rmin = min(rmin, c.z);
+            rmax = max(rmax, c.z);
+        } else {
+            const uint32_t q = atomicAdd(&s_ns, 1u);
+            if (q < (uint32_t)kBigSlow) slow[q] = k;
+        }
+    }
+    atomicMin(&s_rmin, rmin);
+    atomicMax(&s_rmax, rmax);
+    __syncthreads();
+    const uint32_t S = s_ns;
+    if (s_bad || S > (uint32_t)kBigSlow || s_rmin > s_rmax) return;
+    const uint32_t r0 = s_rmin, R = s_rmax - s_rmin + 1;
+    for (uint32_t i = tid; i < S; i += kBigRB) {   // ascending probe order
+        const uint32_t x = slow[i];
+        uint32_t rk = 0;
+        for (uint32_t j = 0; j < S; ++j) rk += slow[j] < x ? 1u : 0u;
+        slow_sorted[rk] = x;
+    }
+    uint32_t* cnt = scr_cnt + beg;
+    uint32_t* E = scr_e + beg + b;   // R + 1 entries per bucket
+    uint4* sbr = scr_slot + beg;
+    for (uint32_t r = tid; r < R; r += kBigRB) cnt[r] = 0;
+    __syncthreads();
+    for (uint32_t k = tid; k < K; k += kBigRB) {      // slot of every chain, by rank
+        const uint4 a = summ[beg + k];
+        if (a.w & 0x80000000u) {
+            const uint4 c = summ_b[beg + k];
+            if (c.z - r0 < R) sbr[c.z - r0] = make_uint4(a.z, a.x, c.x, c.y);
+        }
+    }
+    __syncthreads();
+    const int G = gt.G;
+    unsigned long long coll = 0;
+    uint32_t k0 = 0;
+    for (uint32_t si = 0; si <= S; ++si) {
+        const uint32_t j = si < S ? slow_sorted[si] : K;
+        for (uint32_t k = k0 + tid; k < j; k += kBigRB) {   // chain-first run: one copy each
+            const uint4 a = summ[beg + k];
+            if (a.w & 0x80000000u) cnt[(summ_b[beg + k].z) - r0] = 1u;
+        }
+        __syncthreads();
+        if (j == K) break;
+        const uint32_t t = scan_counts(cnt, E, R, red, tile);
+        if (tid == 0) {
+            auto at = [&](uint32_t i) -> uint4 {   // V[i]: rank r with E[r] <= i < E[r + 1]
+                uint32_t lo = 0, n = R;
+                while (n > 0) {
+                    const uint32_t h = n >> 1;
+                    if (E[lo + h + 1] <= i) { lo += h + 1; n -= h + 1; } else n = h;
+                }
+                return sbr[lo];
+            };
+            const uint4 me = summ[beg + j], mb = summ_b[beg + j];
+            const uint32_t pmask = me.x, pcid = me.z;
+            const int64_t ps = (int64_t)me.y, pl = L;
+            Mhe<MG> P;
+            bool have = false;
+            auto full = [&](uint32_t xid) -> bool {
+                if (!have) { probe_full<MG, View>(v, gt, mp, L, probe_info, me.w & 0x3FFFFFFFu, P); have = true; }
+                Mhe<MG> X;
+                load_entry<MG>(pool, xid, G, X);
+                return mhe_less(X, P);
+            };
+            const uint32_t lb = lower_bound_acc(at, t, pmask, ps, pl, pcid, full);
+            bool isnew = true;
+            if (lb < t) {
+                const uint4 X = at(lb);
+                int q = slot_equiv(X, pmask, ps, pl, pcid);
+                if (q == 2) {
+                    if (!have) { probe_full<MG, View>(v, gt, mp, L, probe_info, me.w & 0x3FFFFFFFu, P); have = true; }
+                    Mhe<MG> X2;
+                    load_entry<MG>(pool, X.x, G, X2);
+                    q = (mhe_less(X2, P) || mhe_less(P, X2)) ? 0 : 1;
+                }
+                isnew = q == 0;
+            }
+            if (!isnew) {
+                ++coll;
+            } else {   // insert the chain entry at lower_bound of its copy (MemHash.cpp:247)
+                Mhe<MG> Ec;
+                bool hv = false;
+                auto fullc = [&](uint32_t xid) -> bool {
+                    if (!hv) { load_entry<MG>(pool, pcid, G, Ec); hv = true; }
+                    Mhe<MG> X;
+                    load_entry<MG>(pool, xid, G, X);
+                    return mhe_less(X, Ec);
+                };
+                const uint32_t ins = lower_bound_acc(at, t, pmask, (int64_t)mb.x, (int64_t)mb.y, pcid, fullc);
+                const uint32_t rr = mb.z - r0;
+                const uint32_t rl = ins > 0 ? chain_sb[at(ins - 1).x].z - r0 : 0u;
+                const uint32_t rh = ins < t ? chain_sb[at(ins).x].z - r0 : 0xFFFFFFFFu;
+                if (rr < R && rl <= rr && rr <= rh) cnt[rr] += 1u;
+                else s_bad = 2;
+            }
+        }
+        __syncthreads();
+        if (s_bad) break;
+        k0 = j + 1;
+    }
+    if (s_bad) {
+        if (tid == 0) atomicOr(&ctr->err, 4u);
+        return;
+    }
+    const uint32_t t = scan_counts(cnt, E, R, red, tile);
+    const uint32_t ob = obase[b];
+    for (uint32_t r = tid; r < R; r += kBigRB) {
+        const uint32_t e0 = E[r], c = E[r + 1] - e0;
+        const uint32_t id = c ? sbr[r].x : 0u;
+        for (uint32_t d = 0; d < c; ++d) tbl[ob + e0 + d] = id;
+    }
+    if (tid == 0) {
+        tsize[b] = t;
+        atomicAdd(&ctr->collisions, coll);
+        atomicAdd(&ctr->entries, (unsigned long long)t);
+        cend[b] = beg;   // replay_kernel skips it
+    }
+}
+
 // Probes that are neither chain-first nor suspicious (flag bits 31 / 30 clear) collide
 // with their chain entry without touching the vector, so the replay only needs the
 // others: keep flags -> exclusive scan -> compacted summaries and bucket ranges; the
@@ -474,7 +727,6 @@ __global__ void bucket_ranges_kernel(const uint32_t* __restrict__ sb, uint64_t P
     }
 }
 
-// MemHash::GetMatchList (MemHash.h:182-203): bucket-major, vector order
 // MatchList output (GetMatchList, MemHash.h:182-203): output row o belongs to the bucket
 // b with obase[b] <= o < obase[b] + tsize[b] (last bucket whose exclusive output base is
 // <= o); one row per thread, so a bucket holding most entries (the main diagonal of
@@ -532,6 +784,7 @@ hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, i
     uint32_t* first_pos = (uint32_t*)carve((size_t)nch * 4);
     uint32_t* next_s = (uint32_t*)carve((size_t)nch * 4);
     uint32_t* rank = (uint32_t*)carve((size_t)nch * 4);
+    uint4* chain_sb = (uint4*)carve((size_t)nch * 16);
     uint4* summ_b = (uint4*)summ + (P + 1);
     const unsigned pgrid = (unsigned)((P + kBlock - 1) / kBlock), cgrid = (nch + kBlock - 1) / kBlock;
     hipError_t e = hipMemsetAsync(first_pos, 0xFF, (size_t)nch * 4, st);
@@ -558,8 +811,10 @@ hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, i
     const uint32_t* ord = buf2 ? vin : vout;
     hipLaunchKernelGGL(chain_next_kernel, dim3(cgrid), dim3(kBlock), 0, st, ord, key_s, key_b, nch, next_s, rank);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(chain_sb_kernel, dim3(cgrid), dim3(kBlock), 0, st, pool, nch, gt.G, rank, next_s, chain_sb);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(probe_flags_kernel, dim3(pgrid), dim3(kBlock), 0, st, (uint4*)summ, summ_b, P, first_pos,
-                       next_s, rank, pool, gt.G);
+                       chain_sb);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // the replay reads only chain-first / suspicious probes (summ buffer: 2 more uint4
     // arrays, the scanned keep flags and the compacted bucket ranges after the originals)
@@ -577,6 +832,42 @@ hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, i
     hipLaunchKernelGGL(compact_ranges_kernel, dim3((mp.table_size + kBlock - 1) / kBlock), dim3(kBlock), 0, st,
                        bstart, bend, pos, mp.table_size, P, cbeg, cend, (DevCounters*)ctr);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (getenv("MUMS_DEV_REPLAY_STATS")) {   // development: what keeps the big buckets off the fast path
+        const uint32_t Tb = mp.table_size;
+        std::vector<uint32_t> hb(Tb), he(Tb);
+        (void)hipMemcpyAsync(hb.data(), cbeg, Tb * 4, hipMemcpyDeviceToHost, st);
+        (void)hipMemcpyAsync(he.data(), cend, Tb * 4, hipMemcpyDeviceToHost, st);
+        (void)hipStreamSynchronize(st);
+        for (uint32_t b = 0; b < Tb; ++b) {
+            const uint32_t K = he[b] - hb[b];
+            if (K < 20000) continue;
+            std::vector<uint4> a(K), c(K);
+            (void)hipMemcpy(a.data(), summ_c + hb[b], K * 16, hipMemcpyDeviceToHost);
+            (void)hipMemcpy(c.data(), summ_bc + hb[b], K * 16, hipMemcpyDeviceToHost);
+            uint32_t nfirst = 0, nsusp = 0, ntie = 0, rmin = ~0u, rmax = 0;
+            long first_slow = -1;
+            for (uint32_t k = 0; k < K; ++k) {
+                const bool f = a[k].w & 0x80000000u, su = a[k].w & 0x40000000u, ti = c[k].z & 0x80000000u;
+                nfirst += f; nsusp += su; ntie += ti;
+                if ((!f || su || ti) && first_slow < 0) first_slow = k;
+                rmin = std::min(rmin, c[k].z & 0x7FFFFFFFu); rmax = std::max(rmax, c[k].z & 0x7FFFFFFFu);
+            }
+            fprintf(stderr, "bucket %u: K %u first %u susp %u tied %u rank span %u first slow at %ld\n", b, K, nfirst,
+                    nsusp, ntie, rmax - rmin + 1, first_slow);
+        }
+    }
+    // big buckets with few suspicious probes: rank counts (replay_big_kernel), first
+    {
+        const char* bm_env = getenv("MUMS_DEV_BIG_BUCKET");
+        const uint32_t big_min = bm_env ? (uint32_t)atoi(bm_env) : kBigBucket;
+        uint32_t* scr_cnt = (uint32_t*)carve((P + 1) * 4);
+        uint32_t* scr_e = (uint32_t*)carve((P + 1 + mp.table_size + 1) * 4);
+        uint4* scr_slot = (uint4*)carve((P + 1) * 16);
+        hipLaunchKernelGGL((replay_big_kernel<MG, View>), dim3(mp.table_size), dim3(kBigRB), 0, st, v, gt, mp, L,
+                           probe_info, (const uint4*)summ_c, (const uint4*)summ_bc, cbeg, cend, bstart, tbl, pool,
+                           (const uint4*)chain_sb, scr_cnt, scr_e, scr_slot, tsize, (DevCounters*)ctr, big_min);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     // buckets of <= 64 probes: one wave each; the rest: one big workgroup each
     constexpr uint32_t kSmall = 64;
     hipLaunchKernelGGL((replay_kernel<MG, 64, View>), dim3(mp.table_size), dim3(64), kSmall * sizeof(uint4), st, v, gt,
