@@ -95,6 +95,14 @@ oracle_result* oracle_replay_rows(int G, const char* const* seqs, const uint64_t
 
 /* ---- synthetic genomes (SURVEY.md Appendix C generator) ---- */
 /* fills G buffers of n bytes each (caller allocates G*n bytes, genome-major) */
+/* EliminateOverlaps (Aligner.cpp:62-176) over a MatchList {len, starts[G]}; returns the
+   new count, *len_out / *s_out malloc'd (free with oracle_free) -- eliminate_overlaps.c */
+uint64_t oracle_eliminate_overlaps(int G, uint64_t M, const uint64_t* len_in, const int64_t* s_in,
+                                   uint64_t** len_out, int64_t** s_out);
+/* libstdc++ std::sort of ids by key[id] (SingleStartComparator order); depth override for tests */
+void     oracle_std_sort_ids(uint32_t* ids, uint64_t n, const uint64_t* key);
+void     oracle_std_sort_depth_override(int depth);
+void     oracle_free(void* p);
 void     oracle_generate(int G, uint64_t n, double p, uint64_t rng_seed, char* out);
 
 #ifdef __cplusplus

@@ -233,3 +233,40 @@ def match_text(lengths: np.ndarray, starts: np.ndarray) -> str:
         return ""
     arr = np.concatenate([lengths.astype(np.int64)[:, None], starts], axis=1)
     return "".join("\t".join(map(str, row)) + "\n" for row in arr.tolist())
+
+
+def eliminate_overlaps(lengths: np.ndarray, starts: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    """EliminateOverlaps (Aligner.cpp:62-176) of a MatchList (lengths [M], starts [M, G])."""
+    L = lib()
+    u64 = ctypes.c_uint64
+    L.oracle_eliminate_overlaps.argtypes = [ctypes.c_int, u64, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.POINTER(ctypes.POINTER(u64)),
+                                            ctypes.POINTER(ctypes.POINTER(ctypes.c_int64))]
+    L.oracle_eliminate_overlaps.restype = u64
+    L.oracle_free.argtypes = [ctypes.c_void_p]
+    lengths = np.ascontiguousarray(lengths, dtype=np.uint64)
+    starts = np.ascontiguousarray(starts, dtype=np.int64)
+    M, G = starts.shape
+    lo = ctypes.POINTER(u64)()
+    so = ctypes.POINTER(ctypes.c_int64)()
+    n = L.oracle_eliminate_overlaps(G, M, lengths.ctypes.data, starts.ctypes.data, ctypes.byref(lo), ctypes.byref(so))
+    out_l = np.ctypeslib.as_array(lo, shape=(max(n, 1),))[:n].copy()
+    out_s = np.ctypeslib.as_array(so, shape=(max(n, 1) * G,))[:n * G].reshape(n, G).copy()
+    L.oracle_free(ctypes.cast(lo, ctypes.c_void_p))
+    L.oracle_free(ctypes.cast(so, ctypes.c_void_p))
+    return out_l, out_s
+
+
+def std_sort_ids(keys: np.ndarray, depth: int = -1) -> np.ndarray:
+    """libstdc++ std::sort of ids 0..n-1 by keys[id] (restated), optional depth override."""
+    L = lib()
+    L.oracle_std_sort_ids.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+    L.oracle_std_sort_depth_override.argtypes = [ctypes.c_int]
+    keys = np.ascontiguousarray(keys, dtype=np.uint64)
+    ids = np.arange(len(keys), dtype=np.uint32)
+    L.oracle_std_sort_depth_override(depth)
+    try:
+        L.oracle_std_sort_ids(ids.ctypes.data, len(keys), keys.ctypes.data)
+    finally:
+        L.oracle_std_sort_depth_override(-1)
+    return ids
