@@ -174,6 +174,20 @@ int  mums_write_sml(mums_ctx* ctx, uint32_t genome, const char* path, const char
  * genome of the context; *seed_out = the file's seed pattern (may be NULL). */
 int  mums_add_genome_sml(mums_ctx* ctx, const char* path, uint64_t* seed_out);
 int  mums_length_filter(mums_ctx* ctx, uint64_t min_length);
+/* EliminateOverlaps (libMems/Aligner.cpp:62-176, declared Aligner.h:239) on the context's
+ * MatchList in place: per genome, std::sort by SingleStartComparator (AbstractMatch.h:324-351,
+ * libstdc++ tie order reproduced), crop / delete the smaller of every overlapping pair,
+ * append the cut-off overlaps without that genome (multiplicity > 1).  Same result and
+ * order as the reference on the same MatchList. */
+int  mums_eliminate_overlaps(mums_ctx* ctx);
+/* The caller's MatchList (count x seq_count signed starts, NO_MATCH = 0, lengths) becomes
+ * the context's result, for mums_eliminate_overlaps / the filters on lists that did not
+ * come from this context's FindMatches (Aligner.cpp:920 gap_list, :1580 mlist). */
+int  mums_load_matches(mums_ctx* ctx, uint32_t seq_count, uint64_t count, const uint64_t* lengths,
+                       const int64_t* starts);
+/* Test entry point: ids[0..n) = the permutation libstdc++ std::sort leaves on keys with
+ * operator< (depth_override >= 0 forces the introsort depth limit; -1 = 2*lg(n)). */
+int  mums_debug_std_sort(mums_ctx* ctx, const uint64_t* keys, uint64_t n, int depth_override, uint32_t* ids);
 
 /* ---- sharded seed stage across GPUs -----------------------
  * Replaces the single-process G-way merge of MatchFinder::SearchRange

@@ -180,6 +180,14 @@ public:
     // the device copy of the last MatchList before GetMatchList
     void MultiplicityFilter(unsigned mult) { check(mums_multiplicity_filter(ctx_, mult)); }
     void LengthFilter(uint64_t length) { check(mums_length_filter(ctx_, length)); }
+    // EliminateOverlaps (Aligner.cpp:62-176) of the last MatchList, on the device
+    void EliminateOverlaps() { check(mums_eliminate_overlaps(ctx_)); }
+    // a caller's MatchList (M x G starts + lengths) as the current result, e.g. to run
+    // EliminateOverlaps / the filters on a list the caller assembled
+    void LoadMatches(const std::vector<uint64_t>& lengths, const std::vector<int64_t>& starts, uint32_t G) {
+        if (starts.size() != lengths.size() * G) throw InvalidData("starts must be M x G");
+        check(mums_load_matches(ctx_, G, lengths.size(), lengths.data(), starts.data()));
+    }
     // SeedOccurrenceList::construct + getFrequency (SeedOccurrenceList.h:22-67) for genome g
     std::vector<float> SeedOccurrence(uint32_t genome, uint64_t length) const {
         std::vector<float> f(length);

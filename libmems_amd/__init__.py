@@ -92,7 +92,8 @@ EXPORTED_SYMBOLS = [
     "mums_shard_packed_info", "mums_shard_packed_copy", "mums_shard_find", "mums_set_parallel_compat",
     "mums_seed_occurrence", "mums_multiplicity_filter", "mums_length_filter", "mums_write_sml",
     "mums_add_genome_sml", "mums_set_pairwise", "mums_shard_slice", "mums_set_start_points",
-    "mums_get_offset_log", "mums_copy_seed_keys_range", "mums_mem_table_count",
+    "mums_get_offset_log", "mums_copy_seed_keys_range", "mums_mem_table_count", "mums_eliminate_overlaps",
+    "mums_load_matches", "mums_debug_std_sort",
 ]
 
 _lib: Optional[ctypes.CDLL] = None
@@ -161,6 +162,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mums_copy_seed_keys_range.argtypes = [vp, u32, u64, u64, vp]
     lib.mums_mem_table_count.argtypes = [vp, vp, u32]
     lib.mums_get_offset_log.argtypes = [vp, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(u32)]
+    lib.mums_eliminate_overlaps.argtypes = [vp]
+    lib.mums_load_matches.argtypes = [vp, u32, u64, vp, vp]
+    lib.mums_debug_std_sort.argtypes = [vp, vp, u64, ctypes.c_int, vp]
     _lib = lib
     return lib
 
@@ -439,6 +443,31 @@ class MemHash:
 
     def LengthFilter(self, length: int) -> None:
         self._check(self._lib.mums_length_filter(self._ctx, length))
+
+    def EliminateOverlaps(self) -> None:
+        """EliminateOverlaps (Aligner.cpp:62-176) of the current MatchList, on the GPU."""
+        self._check(self._lib.mums_eliminate_overlaps(self._ctx))
+
+    def LoadMatches(self, ml: "MatchList") -> None:
+        """Make a MatchList (e.g. one the caller edited) this object's current result."""
+        lengths = np.ascontiguousarray(ml.lengths, dtype=np.uint64)
+        starts = np.ascontiguousarray(ml.starts, dtype=np.int64)
+        M, G = starts.shape
+        self._check(self._lib.mums_load_matches(self._ctx, G, M, lengths.ctypes.data, starts.ctypes.data))
+
+    def _debug_std_sort(self, keys: np.ndarray, depth: int = -1) -> np.ndarray:
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        ids = np.zeros(len(keys), dtype=np.uint32)
+        self._check(self._lib.mums_debug_std_sort(self._ctx, keys.ctypes.data, len(keys), depth, ids.ctypes.data))
+        return ids
+
+
+def EliminateOverlaps(ml: "MatchList", device: int = 0) -> "MatchList":
+    """EliminateOverlaps (Aligner.cpp:62) of a MatchList on the GPU; returns the new list."""
+    with MemHash(device) as mh:
+        mh.LoadMatches(ml)
+        mh.EliminateOverlaps()
+        return mh.GetMatchList()
 
 
 class MaskedMemHash(MemHash):

@@ -85,6 +85,7 @@ struct mums_ctx {
     // one genome's SML / seed frequencies (sml_tools.hip) and filtered MatchLists
     DevBuf smlk0, smlkA, smlkB, smlvA, smlvB, smltmp, flen, fs;
     DevBuf rowsall;          // chunked mode: probe rows of all chunks
+    EoWork eo;               // EliminateOverlaps work arrays (overlaps.hip)
     // MER_REPEAT_LIMIT restart / FindMatchesFromPosition (restart.hip)
     std::vector<uint64_t> start_points;   // per genome SML start index (empty = all 0)
     DevBuf rsbuf, rsplan, rsbst;
@@ -1485,6 +1486,61 @@ int mums_multiplicity_filter(mums_ctx* ctx, uint32_t mult) {
 }
 
 int mums_length_filter(mums_ctx* ctx, uint64_t min_len) { return match_filter(ctx, 0, min_len); }
+
+// EliminateOverlaps (Aligner.cpp:62-176) on the context's MatchList, in place
+int mums_eliminate_overlaps(mums_ctx* ctx) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (ctx->stage_done < MUMS_STAGE_ALL) return fail(ctx, MUMS_E_INVALID, "no completed FindMatches on this context");
+    if (ctx->M >= 0xFFFFFFF0ull) return fail(ctx, MUMS_E_UNSUPPORTED, "EliminateOverlaps of more than 2^32 matches");
+    HIPCHK(hipSetDevice(ctx->device));
+    const int G = ctx->gt.G;
+    uint64_t n = 0;
+    HIPCHK(eliminate_overlaps_device(ctx->eo, ctx->out_len.as<uint64_t>(), ctx->out_s.as<int64_t>(), ctx->M, G, &n,
+                                     ctx->stream));
+    HIPCHK(ctx->flen.ensure((n + 1) * 8));
+    HIPCHK(ctx->fs.ensure((n + 1) * (size_t)G * 8 + 8));
+    HIPCHK(eo_gather(ctx->eo, G, ctx->flen.as<uint64_t>(), ctx->fs.as<int64_t>(), ctx->stream));
+    std::swap(ctx->out_len, ctx->flen);
+    std::swap(ctx->out_s, ctx->fs);
+    ctx->M = n;
+    return MUMS_OK;
+}
+
+// a caller's MatchList becomes the context's result (filters / EliminateOverlaps input)
+int mums_load_matches(mums_ctx* ctx, uint32_t seq_count, uint64_t count, const uint64_t* lengths,
+                      const int64_t* starts) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (seq_count == 0 || (count && (!lengths || !starts))) return fail(ctx, MUMS_E_INVALID, "bad MatchList");
+    if (!ctx->genomes.empty() && seq_count != ctx->genomes.size())
+        return fail(ctx, MUMS_E_INVALID, "MatchList sequence count differs from the context's genomes");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(ctx->out_len.ensure((count + 1) * 8));
+    HIPCHK(ctx->out_s.ensure((count + 1) * (size_t)seq_count * 8 + 8));
+    if (count) {
+        HIPCHK(hipMemcpy(ctx->out_len.p, lengths, count * 8, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(ctx->out_s.p, starts, count * (size_t)seq_count * 8, hipMemcpyHostToDevice));
+    }
+    ctx->gt.G = (int)seq_count;
+    ctx->M = count;
+    ctx->P = 0;
+    ctx->stage_done = MUMS_STAGE_ALL;
+    return MUMS_OK;
+}
+
+// test entry point: the device replay of libstdc++ std::sort (overlaps.hip) on host keys
+int mums_debug_std_sort(mums_ctx* ctx, const uint64_t* keys, uint64_t n, int depth_override, uint32_t* ids) {
+    if (check_ctx(ctx) || (n && (!keys || !ids))) return MUMS_E_INVALID;
+    if (n >= 0xFFFFFFF0ull) return fail(ctx, MUMS_E_UNSUPPORTED, "n >= 2^32");
+    if (n == 0) return MUMS_OK;
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(ctx->flen.ensure(n * 8 + 8));
+    HIPCHK(ctx->fs.ensure(n * 4 + 8));
+    HIPCHK(hipMemcpy(ctx->flen.p, keys, n * 8, hipMemcpyHostToDevice));
+    HIPCHK(eo_sort_ids(ctx->eo, ctx->flen.as<uint64_t>(), (uint32_t)n, depth_override, ctx->fs.as<uint32_t>(),
+                       ctx->stream));
+    HIPCHK(hipMemcpy(ids, ctx->fs.p, n * 4, hipMemcpyDeviceToHost));
+    return MUMS_OK;
+}
 
 // ---- sharded seed stage -------------------------------------------
 

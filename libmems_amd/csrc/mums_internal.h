@@ -219,6 +219,29 @@ hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, i
                          uint32_t nch, void* d_tmp, void* d_radix_tmp, uint32_t lds_cap, uint32_t* tsize, void* ctr,
                          uint64_t* dbg, hipStream_t st);
 // chains.hip: chain labelling of the probes (key order) before the replay
+// overlaps.hip: EliminateOverlaps (Aligner.cpp:62-176) on a device MatchList
+struct EoWork {
+    void *K = nullptr, *V = nullptr, *V2 = nullptr, *fl = nullptr, *fr = nullptr, *Lpos = nullptr, *Rpos = nullptr;
+    void *bound = nullptr, *segA = nullptr, *segB = nullptr, *act = nullptr, *heap = nullptr, *piv = nullptr;
+    void *nsw = nullptr, *scratch = nullptr, *plen = nullptr, *ps = nullptr, *nm_key = nullptr, *nm_id = nullptr;
+    void *nk2 = nullptr, *nv2 = nullptr, *nk3 = nullptr, *nv3 = nullptr, *radix = nullptr, *ctr = nullptr;
+    uint64_t cap_n = 0, cap_pool = 0, cap_new = 0, pool_n = 0, n_final = 0;
+    unsigned long long hbuf[8] = {};
+    EoWork() = default;
+    EoWork(const EoWork&) = delete;
+    EoWork& operator=(const EoWork&) = delete;
+    ~EoWork();
+    void release();
+};
+// the result stays in w (pool + ids) until eo_gather writes it out (*M_out matches)
+hipError_t eliminate_overlaps_device(EoWork& w, const uint64_t* d_len, const int64_t* d_s, uint64_t M, int G,
+                                     uint64_t* M_out, hipStream_t st);
+hipError_t eo_gather(EoWork& w, int G, uint64_t* d_len_out, int64_t* d_s_out, hipStream_t st);
+// libstdc++ std::sort replay of ids 0..n-1 by d_keys (test entry point); depth_override >= 0
+// forces __introsort_loop's depth limit
+hipError_t eo_sort_ids(EoWork& w, const uint64_t* d_keys, uint32_t n, int depth_override, uint32_t* d_ids_out,
+                       hipStream_t st);
+
 size_t chain_tmp_bytes(uint64_t P, uint32_t Tb);
 template <int MG, typename View>
 hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const GenomeTable& gt, const MatchParams& mp,
