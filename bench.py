@@ -31,7 +31,7 @@ import torch  # noqa: E402  (loaded before libmums_hip.so: one HIP runtime per p
 import torch.distributed as dist  # noqa: E402
 
 import libmems_amd as lm  # noqa: E402
-from libmems_amd.shard import HipShardEngine, ShardedSeedStage, genome_blocks, genome_slices  # noqa: E402
+from libmems_amd.shard import AbiShardStage, HipShardEngine, ShardedSeedStage, genome_blocks, genome_slices  # noqa: E402
 
 METRIC = "seed-mers/sec sorted+matched (+ MUMs/sec) at 1/2/4/8 MI355X; HBM GB/s vs roofline"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
@@ -178,6 +178,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-mums", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, default) or gloo (rehearsal)")
+    ap.add_argument("--exchange", choices=("abi", "torch"), default="abi",
+                    help="abi (default): the C ABI runs the sharded step with its own RCCL communicator "
+                         "(mums_shard_run; torch.distributed = gloo control plane); torch: records move by "
+                         "torch.distributed all_to_all (shard.py)")
+    ap.add_argument("--force-shard", action="store_true", help="run the sharded path even on one GPU")
     ap.add_argument("--device", type=int, default=None, help="force one HIP device for every rank (rehearsal)")
     ap.add_argument("--workload", choices=("c3", "c5"), default="c3",
                     help="c3 (default, the metric's config): 8 x 100 Mbp; c5: 2 x 3 Gbp (chunked mode on 1 GPU, "
@@ -195,6 +200,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0")) if args.device is None else args.device
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    sharded = world > 1 or args.force_shard
+    if args.exchange == "abi":   # the data moves by the library's RCCL communicator
+        args.dist_backend = "gloo"
     if world > 1:
         # RCCL ("nccl" on ROCm) over xGMI: the key-range all-to-all of the sharded seed stage
         if args.dist_backend == "nccl":
@@ -210,7 +218,7 @@ def main():
     bytes_dom = 0
     launches = 0
     exch_bytes = 0
-    if world == 1:
+    if not sharded:
         mh = lm.MemHash(local)
         mh.SetSeed(seed)
         for s in genomes:
@@ -224,7 +232,7 @@ def main():
         mine = [genomes[g][b0:min(n, b1 + L - 1)]]
         eng = HipShardEngine(local, seed, [n] * G, g, mine, slice_of=(g, b0, b1))
         genomes = mine   # views into genome g keep its storage alive
-        stage = ShardedSeedStage(eng)
+        stage = AbiShardStage(eng, local) if args.exchange == "abi" else ShardedSeedStage(eng)
         mh = eng.mh
         run = stage.run
         stats = eng.stats
@@ -235,7 +243,7 @@ def main():
         del genomes
         genomes = mine
         eng = HipShardEngine(local, seed, [n] * G, first, genomes)
-        stage = ShardedSeedStage(eng)
+        stage = AbiShardStage(eng, local) if args.exchange == "abi" else ShardedSeedStage(eng)
         mh = eng.mh
         run = stage.run
         stats = eng.stats
@@ -300,6 +308,8 @@ def main():
     seedmers_rank = st["seedmers"]
     key_bytes = st["key_bytes"]
     probes = st["probes"]
+    if sharded and hasattr(stage, "close"):
+        stage.close()
     mh.close()
     del genomes
 
@@ -338,9 +348,12 @@ def main():
                        "seedmers_rank0": seedmers_rank, "probes_rank0": probes,
                        "parallelism": (f"genome-sharded x{world}: "
                                        f"{'position slice' if args.workload == 'c5' else 'genome block'} per rank, "
-                                       f"{'RCCL' if args.dist_backend == 'nccl' else args.dist_backend} all-to-all of key "
-                                       f"ranges ({exch_bytes / max(args.steps, 1) / 1e9:.2f} GB/step sent by rank 0), "
-                                       f"merge per key range") if world > 1 else "1 GPU"},
+                                       + (f"RCCL all-to-allv of key ranges inside libmums_hip.so (mums_shard_run, "
+                                          f"ncclCommInitRank communicator), merge per key range"
+                                          if args.exchange == "abi" else
+                                          f"{'RCCL' if args.dist_backend == 'nccl' else args.dist_backend} all-to-all "
+                                          f"of key ranges ({exch_bytes / max(args.steps, 1) / 1e9:.2f} GB/step sent by "
+                                          f"rank 0), merge per key range")) if world > 1 else "1 GPU"},
             "roofline": {
                 "bound": "hbm",
                 "kernel": f"seg_onesweep_kernel (segmented onesweep LSD pass over packed 8-B seed records, "

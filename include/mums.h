@@ -248,6 +248,31 @@ int  mums_shard_packed_copy(mums_ctx* ctx, uint32_t* d_dst);
 int  mums_shard_find(mums_ctx* ctx, const int64_t* d_rows, uint64_t nrows, const uint32_t* d_packed_all);
 int  mums_probe_copy(mums_ctx* ctx, uint32_t* buckets, uint64_t* ref_index, uint64_t capacity);
 
+/* ---- multi-GPU MemHash through the ABI ----------
+ * One communicator per rank: RCCL over xGMI for one process per GPU
+ * (mums_comm_unique_id on rank 0, broadcast by the caller, mums_comm_init_rank on every
+ * rank) or for one process driving several GPUs (mums_comm_init_all, then one host
+ * thread per device); mums_comm_init_local: ranks that are threads of this process,
+ * host-staged (testing the orchestration on one GPU).  mums_shard_run(ctx, comm, stage)
+ * runs the whole sharded pipeline of a rank whose context was set up with
+ * mums_shard_layout / mums_shard_slice and its genomes: keys, all-gather of bucket counts,
+ * key ranges (mums_shard_key_ranges), all-to-allv of the records, merge; with
+ * MUMS_STAGE_ALL also the probe rows' all-to-allv, the packed genomes' all-gather and the
+ * chain labelling + replay of this rank's hash buckets (results via mums_result_*, the
+ * ranks' lists in rank order = the bucket-major MatchList). */
+typedef struct mums_comm mums_comm;
+int  mums_comm_unique_id(void* id, uint64_t bytes);   /* ncclGetUniqueId, 128 bytes */
+int  mums_comm_init_rank(mums_comm** comm, int device, int world, int rank, const void* id);
+int  mums_comm_init_all(mums_comm** comms, int ndev, const int* devices);
+int  mums_comm_init_local(mums_comm** comms, int nranks, const int* devices);
+void mums_comm_destroy(mums_comm* comm);
+const char* mums_comm_last_error(mums_comm* comm);
+/* the balanced contiguous key (or hash-bucket) ranges of the exchange: rank r gets
+ * [first[r], first[r] + count[r]) (host only, no device needed) */
+int  mums_shard_key_ranges(const uint64_t* totals, uint32_t nbuckets, uint32_t world, uint32_t* first,
+                           uint32_t* count);
+int  mums_shard_run(mums_ctx* ctx, mums_comm* comm, int stage);
+
 int  mums_abi_version(void);
 
 #ifdef __cplusplus

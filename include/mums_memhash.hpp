@@ -11,9 +11,11 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
 #include <ostream>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "mums.h"
@@ -229,6 +231,74 @@ public:
 class PairwiseMatchFinder : public MemHash {
 public:
     explicit PairwiseMatchFinder(int device = 0) : MemHash(device) { check(mums_set_pairwise(ctx_, 1)); }
+};
+
+// MemHash::FindMatches over several GPUs of this process:
+// genome block per device, RCCL communicators from ncclCommInitAll (or the host-staged
+// in-process communicator: local = true), one thread per device running mums_shard_run.
+// The MatchList is the devices' bucket ranges concatenated = MemHash's bucket-major list.
+class ShardedMemHash {
+public:
+    explicit ShardedMemHash(std::vector<int> devices, bool local = false) : devices_(std::move(devices)) {
+        comms_.assign(devices_.size(), nullptr);
+        const int rc = local ? mums_comm_init_local(comms_.data(), (int)devices_.size(), devices_.data())
+                             : mums_comm_init_all(comms_.data(), (int)devices_.size(), devices_.data());
+        if (rc != MUMS_OK) throw InvalidData("communicator init failed (RCCL)");
+    }
+    ~ShardedMemHash() {
+        ranks_.clear();
+        for (mums_comm* c : comms_) mums_comm_destroy(c);
+    }
+    ShardedMemHash(const ShardedMemHash&) = delete;
+    ShardedMemHash& operator=(const ShardedMemHash&) = delete;
+    void SetSeed(uint64_t pattern) { seed_ = pattern; }
+    void SetTableSize(uint32_t n) { table_size_ = n; }
+    bool AddSequence(const std::string& seq) {
+        seqs_.push_back(seq);
+        return true;
+    }
+    void FindMatches(MatchList& ml) {
+        const size_t W = devices_.size(), G = seqs_.size();
+        std::vector<uint64_t> lens(G);
+        for (size_t g = 0; g < G; ++g) lens[g] = seqs_[g].size();
+        ranks_.clear();
+        size_t g0 = 0;
+        for (size_t r = 0; r < W; ++r) {   // genome_blocks: earlier ranks take the remainder
+            const size_t cnt = G / W + (r < G % W ? 1 : 0);
+            auto mh = std::make_unique<MemHash>(devices_[r]);
+            mh->SetTableSize(table_size_);
+            mh->SetSeed(seed_);
+            for (size_t g = g0; g < g0 + cnt; ++g) mh->AddSequence(seqs_[g]);
+            if (mums_shard_layout(mh->handle(), (uint32_t)G, (uint32_t)g0, lens.data()) != MUMS_OK)
+                throw InvalidData(mums_last_error(mh->handle()));
+            ranks_.push_back(std::move(mh));
+            g0 += cnt;
+        }
+        std::vector<int> rc(W, MUMS_OK);
+        std::vector<std::thread> th;
+        for (size_t r = 0; r < W; ++r)
+            th.emplace_back([&, r] { rc[r] = mums_shard_run(ranks_[r]->handle(), comms_[r], MUMS_STAGE_ALL); });
+        for (auto& t : th) t.join();
+        for (size_t r = 0; r < W; ++r)
+            if (rc[r] != MUMS_OK)
+                throw InvalidData(std::string("rank ") + std::to_string(r) + ": " + mums_last_error(ranks_[r]->handle()) +
+                                  " " + mums_comm_last_error(comms_[r]));
+        ml.clear();
+        for (size_t r = 0; r < W; ++r) {
+            MatchList part;
+            ranks_[r]->GetMatchList(part);
+            ml.insert(ml.end(), part.begin(), part.end());
+        }
+    }
+    const MemHash& rank(size_t r) const { return *ranks_[r]; }
+
+private:
+    std::vector<int> devices_;
+    std::vector<mums_comm*> comms_;
+    std::vector<std::unique_ptr<MemHash>> ranks_;
+    std::vector<std::string> seqs_;
+    uint64_t seed_ = 0;
+    uint32_t table_size_ = 40000;
 };
 
 }  // namespace mums

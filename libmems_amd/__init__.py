@@ -93,7 +93,8 @@ EXPORTED_SYMBOLS = [
     "mums_seed_occurrence", "mums_multiplicity_filter", "mums_length_filter", "mums_write_sml",
     "mums_add_genome_sml", "mums_set_pairwise", "mums_shard_slice", "mums_set_start_points",
     "mums_get_offset_log", "mums_copy_seed_keys_range", "mums_mem_table_count", "mums_eliminate_overlaps",
-    "mums_load_matches", "mums_debug_std_sort",
+    "mums_load_matches", "mums_debug_std_sort", "mums_comm_unique_id", "mums_comm_init_rank", "mums_comm_init_all",
+    "mums_comm_init_local", "mums_comm_destroy", "mums_comm_last_error", "mums_shard_key_ranges", "mums_shard_run",
 ]
 
 _lib: Optional[ctypes.CDLL] = None
@@ -165,6 +166,16 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mums_eliminate_overlaps.argtypes = [vp]
     lib.mums_load_matches.argtypes = [vp, u32, u64, vp, vp]
     lib.mums_debug_std_sort.argtypes = [vp, vp, u64, ctypes.c_int, vp]
+    lib.mums_comm_unique_id.argtypes = [vp, u64]
+    lib.mums_comm_init_rank.argtypes = [ctypes.POINTER(vp), ctypes.c_int, ctypes.c_int, ctypes.c_int, vp]
+    lib.mums_comm_init_all.argtypes = [ctypes.POINTER(vp), ctypes.c_int, vp]
+    lib.mums_comm_init_local.argtypes = [ctypes.POINTER(vp), ctypes.c_int, vp]
+    lib.mums_comm_destroy.argtypes = [vp]
+    lib.mums_comm_destroy.restype = None
+    lib.mums_comm_last_error.argtypes = [vp]
+    lib.mums_comm_last_error.restype = ctypes.c_char_p
+    lib.mums_shard_key_ranges.argtypes = [vp, u32, u32, vp, vp]
+    lib.mums_shard_run.argtypes = [vp, vp, ctypes.c_int]
     _lib = lib
     return lib
 
@@ -462,6 +473,112 @@ class MemHash:
         return ids
 
 
+def shard_key_ranges(totals, world: int):
+    """The C ABI's key / bucket range cut (mums_shard_key_ranges): [(first, count)] per rank."""
+    lib = load_library()
+    t = np.ascontiguousarray(totals, dtype=np.uint64)
+    f = np.zeros(world, dtype=np.uint32)
+    c = np.zeros(world, dtype=np.uint32)
+    rc = lib.mums_shard_key_ranges(t.ctypes.data, len(t), world, f.ctypes.data, c.ctypes.data)
+    if rc != MUMS_OK:
+        raise MumsError(rc, "mums_shard_key_ranges")
+    return [(int(a), int(b)) for a, b in zip(f, c)]
+
+
+class ShardedMemHash:
+    """MemHash over several ranks in ONE process through the C ABI (mums_shard_run): one
+    context per rank holding a contiguous genome block, one communicator per rank (RCCL
+    over xGMI from mums_comm_init_all, or the host-staged in-process communicator with
+    comm="local"), one host thread per rank.  The ranks' MatchLists in rank order are the
+    bucket-major MatchList of MemHash::FindMatches (DESIGN.md §6)."""
+
+    def __init__(self, devices: Sequence[int], comm: str = "rccl", table_size: int = 40000):
+        self._lib = load_library()
+        self.devices = list(devices)
+        self.world = len(self.devices)
+        self.comm_kind = comm
+        self.table_size = table_size
+        self.seed = 0
+        self.seqs: List[bytes] = []
+        self.ranks: List[MemHash] = []
+        self.stats_per_rank: List[dict] = []
+        comms = (ctypes.c_void_p * self.world)()
+        devs = (ctypes.c_int * self.world)(*self.devices)
+        init = self._lib.mums_comm_init_all if comm == "rccl" else self._lib.mums_comm_init_local
+        rc = init(comms, self.world, devs)
+        if rc != MUMS_OK:
+            raise MumsError(rc, f"mums_comm_init ({comm}) failed")
+        self._comms = [comms[r] for r in range(self.world)]
+
+    def SetSeed(self, seed: int) -> None:
+        self.seed = seed
+
+    def AddSequence(self, seq) -> None:
+        self.seqs.append(seq.encode() if isinstance(seq, str) else bytes(seq))
+
+    def FindMatches(self, sequences: Optional[Sequence] = None, stage: int = STAGE_ALL) -> MatchList:
+        import threading
+        if sequences is not None:
+            for s in sequences:
+                self.AddSequence(s)
+        G = len(self.seqs)
+        lens = (ctypes.c_uint64 * G)(*[len(s) for s in self.seqs])
+        base, rem = divmod(G, self.world)
+        for mh in self.ranks:
+            mh.close()
+        self.ranks = []
+        g0 = 0
+        for r, dev in enumerate(self.devices):
+            cnt = base + (1 if r < rem else 0)
+            mh = MemHash(dev)
+            mh.SetTableSize(self.table_size)
+            mh.SetSeed(self.seed)
+            for s in self.seqs[g0:g0 + cnt]:
+                mh.AddSequence(s)
+            mh._check(self._lib.mums_shard_layout(mh._ctx, G, g0, lens))
+            self.ranks.append(mh)
+            g0 += cnt
+        errs: List[Optional[BaseException]] = [None] * self.world
+
+        def run(r: int) -> None:
+            try:
+                rc = self._lib.mums_shard_run(self.ranks[r]._ctx, self._comms[r], stage)
+                if rc != MUMS_OK:
+                    msg = self._lib.mums_last_error(self.ranks[r]._ctx).decode() or \
+                        self._lib.mums_comm_last_error(self._comms[r]).decode()
+                    raise MumsError(rc, f"rank {r}: {msg}")
+            except BaseException as e:  # noqa: BLE001 -- reported below
+                errs[r] = e
+
+        th = [threading.Thread(target=run, args=(r,)) for r in range(self.world)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        for e in errs:
+            if e is not None:
+                raise e
+        self.stats_per_rank = [mh.stats() for mh in self.ranks]
+        if stage != STAGE_ALL:
+            return MatchList(np.zeros(0, dtype=np.uint64), np.zeros((0, G), dtype=np.int64))
+        parts = [mh.GetMatchList() for mh in self.ranks]
+        return MatchList(np.concatenate([p.lengths for p in parts]), np.concatenate([p.starts for p in parts]))
+
+    def close(self) -> None:
+        for mh in self.ranks:
+            mh.close()
+        self.ranks = []
+        for c in self._comms:
+            self._lib.mums_comm_destroy(c)
+        self._comms = []
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
 def EliminateOverlaps(ml: "MatchList", device: int = 0) -> "MatchList":
     """EliminateOverlaps (Aligner.cpp:62) of a MatchList on the GPU; returns the new list."""
     with MemHash(device) as mh:
@@ -504,5 +621,6 @@ class PairwiseMatchFinder(MemHash):
 
 __all__ = [
     "MemHash", "MaskedMemHash", "ParallelMemHash", "PairwiseMatchFinder", "MatchList", "MumsError", "GapInSequence", "getSeed", "getSeedLength",
-    "getSeedWeight", "getDefaultSeedWeight", "load_library", "EXPORTED_SYMBOLS", "STAGE_SEEDS", "STAGE_ALL",
+    "getSeedWeight", "getDefaultSeedWeight", "load_library", "EXPORTED_SYMBOLS", "STAGE_SEEDS", "STAGE_ALL", "ShardedMemHash",
+    "shard_key_ranges", "EliminateOverlaps",
 ]

@@ -1487,6 +1487,17 @@ int mums_multiplicity_filter(mums_ctx* ctx, uint32_t mult) {
 
 int mums_length_filter(mums_ctx* ctx, uint64_t min_len) { return match_filter(ctx, 0, min_len); }
 
+extern "C++" {
+hipStream_t mums::ctx_stream(mums_ctx* ctx) { return ctx->stream; }
+int mums::ctx_device(mums_ctx* ctx) { return ctx->device; }
+int mums::ctx_table_genomes(mums_ctx* ctx, uint32_t* table_size, uint32_t* genomes) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    *table_size = ctx->table_size;
+    *genomes = (uint32_t)ctx->gt.G;
+    return MUMS_OK;
+}
+}
+
 // EliminateOverlaps (Aligner.cpp:62-176) on the context's MatchList, in place
 int mums_eliminate_overlaps(mums_ctx* ctx) {
     if (check_ctx(ctx)) return MUMS_E_INVALID;

@@ -219,6 +219,14 @@ hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, i
                          uint32_t nch, void* d_tmp, void* d_radix_tmp, uint32_t lds_cap, uint32_t* tsize, void* ctr,
                          uint64_t* dbg, hipStream_t st);
 // chains.hip: chain labelling of the probes (key order) before the replay
+// context accessors for the multi-GPU orchestration (shard_comm.hip; mums_capi.hip)
+}  // namespace mums
+struct mums_ctx;
+namespace mums {
+hipStream_t ctx_stream(mums_ctx* ctx);
+int ctx_device(mums_ctx* ctx);
+int ctx_table_genomes(mums_ctx* ctx, uint32_t* table_size, uint32_t* genomes);
+
 // overlaps.hip: EliminateOverlaps (Aligner.cpp:62-176) on a device MatchList
 struct EoWork {
     void *K = nullptr, *V = nullptr, *V2 = nullptr, *fl = nullptr, *fr = nullptr, *Lpos = nullptr, *Rpos = nullptr;

@@ -1,0 +1,379 @@
+// shard_comm.hip -- multi-GPU MemHash behind the C ABI.
+//
+// One context per rank (mums_shard_layout / mums_shard_slice + its genomes), one
+// communicator per rank.  mums_shard_run drives the sharded seed stage and FindMatches
+// with the rank's collectives issued on the context's stream:
+//   1. keys     : mums_shard_keys -> 8-B records bucketed by the top B key bits;
+//   2. counts   : all-gather of the per-bucket record counts; the buckets are cut into
+//                 world contiguous key ranges of balanced record counts (key_ranges);
+//   3. exchange : one all-to-allv moves every key range to its owner rank, sources in
+//                 rank order (= global seed-mer index order);
+//   4. merge    : mums_shard_merge -> this key range's probes in AddHashEntry order;
+//   5. buckets  : all-gather of per-hash-bucket probe counts, bucket ranges per rank;
+//   6. rows     : mums_shard_probe_rows + all-to-allv of the probe rows;
+//   7. genomes  : all-gather(v) of the 2-bit packed genomes (chain walks read any genome);
+//   8. find     : mums_shard_find -> this rank's buckets of the bucket-major MatchList.
+// Communicators: RCCL (ncclCommInitRank for one process per GPU, ncclCommInitAll for one
+// process driving several GPUs from one thread per device; all-to-allv = grouped
+// ncclSend/ncclRecv over xGMI) or an in-process host-staged communicator for ranks that
+// are threads of one process (tests of the orchestration on a single GPU).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/mums.h"
+#include "mums_internal.h"
+
+struct mums_comm {
+    int world = 1, rank = 0, device = 0;
+    std::string err;
+    virtual ~mums_comm() = default;
+    // host arrays: recv[world][n] = every rank's send[n]
+    virtual int allgather_u64(const uint64_t* send, size_t n, uint64_t* recv, hipStream_t st) = 0;
+    // device buffers, byte counts per peer; send / recv blocks in rank order
+    virtual int alltoallv(const void* d_send, const uint64_t* send_bytes, void* d_recv, const uint64_t* recv_bytes,
+                          hipStream_t st) = 0;
+    // device DevBufs for the run (kept across runs)
+    struct Buf {
+        void* p = nullptr;
+        size_t cap = 0;
+        int ensure(size_t bytes) {
+            if (bytes <= cap) return 0;
+            if (p) (void)hipFree(p);
+            p = nullptr;
+            cap = 0;
+            const size_t want = bytes + (bytes >> 4) + 4096;
+            if (hipMalloc(&p, want) != hipSuccess) return -1;
+            cap = want;
+            return 0;
+        }
+        ~Buf() {
+            if (p) (void)hipFree(p);
+        }
+    } rec, recv, rows, rrows, packed, packed_all;
+};
+
+namespace {
+
+int comm_fail(mums_comm* c, const std::string& m) {
+    c->err = m;
+    return MUMS_E_HIP;
+}
+
+// ---- RCCL ---------------------------------------------------------------------------
+struct RcclComm : mums_comm {
+    ncclComm_t nc = nullptr;
+    Buf scratch;
+    ~RcclComm() override {
+        if (nc) (void)ncclCommDestroy(nc);
+    }
+    int allgather_u64(const uint64_t* send, size_t n, uint64_t* recv, hipStream_t st) override {
+        if (scratch.ensure((world + 1) * n * 8 + 64)) return comm_fail(this, "allgather buffer");
+        uint64_t* d = (uint64_t*)scratch.p;
+        if (hipMemcpyAsync(d + (size_t)world * n, send, n * 8, hipMemcpyHostToDevice, st) != hipSuccess)
+            return comm_fail(this, "allgather H2D");
+        ncclResult_t r = ncclAllGather(d + (size_t)world * n, d, n, ncclUint64, nc, st);
+        if (r != ncclSuccess) return comm_fail(this, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+        if (hipMemcpyAsync(recv, d, (size_t)world * n * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return comm_fail(this, "allgather D2H");
+        return MUMS_OK;
+    }
+    int alltoallv(const void* d_send, const uint64_t* sb, void* d_recv, const uint64_t* rb, hipStream_t st) override {
+        uint64_t so = 0, ro = 0;
+        std::vector<uint64_t> soff(world), roff(world);
+        for (int r = 0; r < world; ++r) {
+            soff[r] = so;
+            roff[r] = ro;
+            so += sb[r];
+            ro += rb[r];
+        }
+        if (sb[rank] != rb[rank]) return comm_fail(this, "alltoallv: self counts differ");
+        if (sb[rank] && hipMemcpyAsync((char*)d_recv + roff[rank], (const char*)d_send + soff[rank], sb[rank],
+                                       hipMemcpyDeviceToDevice, st) != hipSuccess)
+            return comm_fail(this, "alltoallv self copy");
+        ncclResult_t r = ncclGroupStart();
+        for (int p = 0; p < world && r == ncclSuccess; ++p) {
+            if (p == rank) continue;
+            if (sb[p]) r = ncclSend((const char*)d_send + soff[p], sb[p], ncclChar, p, nc, st);
+            if (r == ncclSuccess && rb[p]) r = ncclRecv((char*)d_recv + roff[p], rb[p], ncclChar, p, nc, st);
+        }
+        const ncclResult_t r2 = ncclGroupEnd();
+        if (r != ncclSuccess || r2 != ncclSuccess)
+            return comm_fail(this, std::string("RCCL all-to-allv: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+        return MUMS_OK;
+    }
+};
+
+// ---- in-process ranks (threads), host-staged ----------------------------------------
+struct LocalShared {
+    int world;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t generation = 0;
+    std::vector<std::vector<uint64_t>> host;          // per rank
+    std::vector<const void*> dsend;
+    std::vector<std::vector<uint64_t>> sbytes;
+    explicit LocalShared(int w) : world(w), host(w), dsend(w), sbytes(w) {}
+    void barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        const uint64_t gen = generation;
+        if (++arrived == world) {
+            arrived = 0;
+            ++generation;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return generation != gen; });
+        }
+    }
+};
+
+struct LocalComm : mums_comm {
+    std::shared_ptr<LocalShared> sh;
+    int allgather_u64(const uint64_t* send, size_t n, uint64_t* recv, hipStream_t) override {
+        sh->host[rank].assign(send, send + n);
+        sh->barrier();
+        for (int r = 0; r < world; ++r) std::memcpy(recv + (size_t)r * n, sh->host[r].data(), n * 8);
+        sh->barrier();
+        return MUMS_OK;
+    }
+    int alltoallv(const void* d_send, const uint64_t* sb, void* d_recv, const uint64_t* rb, hipStream_t st) override {
+        if (hipStreamSynchronize(st) != hipSuccess) return comm_fail(this, "stream sync");
+        sh->dsend[rank] = d_send;
+        sh->sbytes[rank].assign(sb, sb + world);
+        sh->barrier();
+        uint64_t ro = 0;
+        int rc = MUMS_OK;
+        for (int s = 0; s < world; ++s) {   // source s's block for this rank
+            uint64_t so = 0;
+            for (int p = 0; p < rank; ++p) so += sh->sbytes[s][p];
+            const uint64_t nb = sh->sbytes[s][rank];
+            if (nb != rb[s]) rc = comm_fail(this, "alltoallv: counts differ");
+            else if (nb && hipMemcpy((char*)d_recv + ro, (const char*)sh->dsend[s] + so, nb, hipMemcpyDefault) !=
+                               hipSuccess)
+                rc = comm_fail(this, "alltoallv copy");
+            ro += nb;
+        }
+        sh->barrier();   // sources stay valid until every rank has copied
+        return rc;
+    }
+};
+
+// key_ranges (libmems_amd/shard.py): boundary r at the first bucket whose prefix sum
+// reaches ceil(total * r / world)
+void key_ranges(const std::vector<uint64_t>& tot, int world, std::vector<uint32_t>& first,
+                std::vector<uint32_t>& count) {
+    const uint32_t nb = (uint32_t)tot.size();
+    std::vector<uint64_t> cum(nb + 1, 0);
+    for (uint32_t b = 0; b < nb; ++b) cum[b + 1] = cum[b] + tot[b];
+    const uint64_t total = cum[nb];
+    std::vector<uint32_t> bounds{0};
+    for (int r = 1; r < world; ++r) {
+        const unsigned __int128 t = ((unsigned __int128)total * (unsigned)r + (unsigned)world - 1) / (unsigned)world;
+        const uint64_t target = (uint64_t)t;
+        const uint32_t b = (uint32_t)(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
+        bounds.push_back(std::min(std::max(b, bounds.back()), nb));
+    }
+    bounds.push_back(nb);
+    first.assign(world, 0);
+    count.assign(world, 0);
+    for (int r = 0; r < world; ++r) {
+        first[r] = bounds[r];
+        count[r] = bounds[r + 1] - bounds[r];
+    }
+}
+
+#define RC(x)                        \
+    do {                             \
+        const int rc_ = (x);         \
+        if (rc_ != MUMS_OK) return rc_; \
+    } while (0)
+
+}  // namespace
+
+extern "C" {
+
+int mums_comm_unique_id(void* id, uint64_t bytes) {
+    if (!id || bytes < sizeof(ncclUniqueId)) return MUMS_E_INVALID;
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return MUMS_E_HIP;
+    std::memcpy(id, &u, sizeof(u));
+    return MUMS_OK;
+}
+
+int mums_comm_init_rank(mums_comm** out, int device, int world, int rank, const void* id) {
+    if (!out || !id || world < 1 || rank < 0 || rank >= world) return MUMS_E_INVALID;
+    *out = nullptr;
+    if (hipSetDevice(device) != hipSuccess) return MUMS_E_NODEVICE;
+    auto* c = new RcclComm();
+    c->world = world;
+    c->rank = rank;
+    c->device = device;
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    if (ncclCommInitRank(&c->nc, world, u, rank) != ncclSuccess) {
+        delete c;
+        return MUMS_E_HIP;
+    }
+    *out = c;
+    return MUMS_OK;
+}
+
+int mums_comm_init_all(mums_comm** out, int ndev, const int* devices) {
+    if (!out || ndev < 1 || !devices) return MUMS_E_INVALID;
+    std::vector<ncclComm_t> nc(ndev);
+    if (ncclCommInitAll(nc.data(), ndev, devices) != ncclSuccess) return MUMS_E_HIP;
+    for (int r = 0; r < ndev; ++r) {
+        auto* c = new RcclComm();
+        c->world = ndev;
+        c->rank = r;
+        c->device = devices[r];
+        c->nc = nc[r];
+        out[r] = c;
+    }
+    return MUMS_OK;
+}
+
+int mums_comm_init_local(mums_comm** out, int nranks, const int* devices) {
+    if (!out || nranks < 1 || !devices) return MUMS_E_INVALID;
+    auto sh = std::make_shared<LocalShared>(nranks);
+    for (int r = 0; r < nranks; ++r) {
+        auto* c = new LocalComm();
+        c->world = nranks;
+        c->rank = r;
+        c->device = devices[r];
+        c->sh = sh;
+        out[r] = c;
+    }
+    return MUMS_OK;
+}
+
+void mums_comm_destroy(mums_comm* c) { delete c; }
+
+const char* mums_comm_last_error(mums_comm* c) { return c ? c->err.c_str() : "null communicator"; }
+
+int mums_shard_key_ranges(const uint64_t* totals, uint32_t nbuckets, uint32_t world, uint32_t* first,
+                          uint32_t* count) {
+    if (!totals || !first || !count || world < 1) return MUMS_E_INVALID;
+    std::vector<uint32_t> f, n;
+    key_ranges(std::vector<uint64_t>(totals, totals + nbuckets), (int)world, f, n);
+    std::copy(f.begin(), f.end(), first);
+    std::copy(n.begin(), n.end(), count);
+    return MUMS_OK;
+}
+
+int mums_shard_run(mums_ctx* ctx, mums_comm* comm, int stage) {
+    if (!ctx || !comm) return MUMS_E_INVALID;
+    const int W = comm->world, R = comm->rank;
+    hipStream_t st = mums::ctx_stream(ctx);
+    if (hipSetDevice(mums::ctx_device(ctx)) != hipSuccess) return MUMS_E_NODEVICE;
+    // 1-4: sharded seed stage
+    uint32_t B = 0;
+    uint64_t n_local = 0;
+    RC(mums_shard_msd_bits(ctx, &B, &n_local));
+    const uint32_t nb = 1u << B;
+    if (comm->rec.ensure((n_local + 1) * 8)) return MUMS_E_HIP;
+    std::vector<uint64_t> counts(nb), C((size_t)W * nb);
+    RC(mums_shard_keys(ctx, (uint64_t*)comm->rec.p, n_local + 1, counts.data()));
+    RC(comm->allgather_u64(counts.data(), nb, C.data(), st));
+    std::vector<uint64_t> tot(nb, 0);
+    for (int r = 0; r < W; ++r)
+        for (uint32_t b = 0; b < nb; ++b) tot[b] += C[(size_t)r * nb + b];
+    std::vector<uint32_t> kf, kn;
+    key_ranges(tot, W, kf, kn);
+    const uint32_t first = kf[R], cnt = kn[R];
+    std::vector<uint64_t> sub((size_t)W * cnt);
+    for (int r = 0; r < W; ++r)
+        for (uint32_t b = 0; b < cnt; ++b) sub[(size_t)r * cnt + b] = C[(size_t)r * nb + first + b];
+    const uint64_t* merged = (const uint64_t*)comm->rec.p;
+    if (W > 1) {
+        std::vector<uint64_t> sb(W, 0), rb(W, 0);
+        for (int p = 0; p < W; ++p)
+            for (uint32_t b = kf[p]; b < kf[p] + kn[p]; ++b) sb[p] += 8 * C[(size_t)R * nb + b];
+        for (int s = 0; s < W; ++s)
+            for (uint32_t b = 0; b < cnt; ++b) rb[s] += 8 * sub[(size_t)s * cnt + b];
+        uint64_t rtot = 0;
+        for (int s = 0; s < W; ++s) rtot += rb[s];
+        if (comm->recv.ensure(rtot + 8)) return MUMS_E_HIP;
+        RC(comm->alltoallv(comm->rec.p, sb.data(), comm->recv.p, rb.data(), st));
+        merged = (const uint64_t*)comm->recv.p;
+    }
+    if (hipStreamSynchronize(st) != hipSuccess) return MUMS_E_HIP;
+    RC(mums_shard_merge(ctx, merged, (uint32_t)W, first, cnt, sub.data()));
+    if (stage != MUMS_STAGE_ALL) return MUMS_OK;
+    // 5-8: sharded FindMatches
+    uint32_t T = 0, G = 0;
+    RC(mums::ctx_table_genomes(ctx, &T, &G));
+    std::vector<uint64_t> bc(T), BC((size_t)W * T);
+    RC(mums_shard_bucket_counts(ctx, bc.data()));
+    RC(comm->allgather_u64(bc.data(), T, BC.data(), st));
+    std::vector<uint64_t> btot(T, 0);
+    for (int r = 0; r < W; ++r)
+        for (uint32_t b = 0; b < T; ++b) btot[b] += BC[(size_t)r * T + b];
+    std::vector<uint32_t> bf, bn;
+    key_ranges(btot, W, bf, bn);
+    std::vector<uint32_t> bounds(bf.begin(), bf.end());
+    bounds.push_back(T);
+    uint64_t P = 0;
+    RC(mums_probe_count(ctx, &P));
+    const uint64_t rowb = 8ull * (G + 1);
+    if (comm->rows.ensure((P + 1) * rowb)) return MUMS_E_HIP;
+    std::vector<uint64_t> send(W), S((size_t)W * W);
+    RC(mums_shard_probe_rows(ctx, (uint32_t)W, bounds.data(), (int64_t*)comm->rows.p, P + 1, send.data()));
+    RC(comm->allgather_u64(send.data(), W, S.data(), st));
+    const int64_t* rows = (const int64_t*)comm->rows.p;
+    uint64_t nrows = P;
+    if (W > 1) {
+        std::vector<uint64_t> sb(W), rb(W);
+        nrows = 0;
+        for (int p = 0; p < W; ++p) {
+            sb[p] = send[p] * rowb;
+            rb[p] = S[(size_t)p * W + R] * rowb;
+            nrows += S[(size_t)p * W + R];
+        }
+        if (comm->rrows.ensure((nrows + 1) * rowb)) return MUMS_E_HIP;
+        RC(comm->alltoallv(comm->rows.p, sb.data(), comm->rrows.p, rb.data(), st));
+        rows = (const int64_t*)comm->rrows.p;
+    }
+    uint64_t woff = 0, nw = 0, total = 0;
+    RC(mums_shard_packed_info(ctx, &woff, &nw, &total));
+    if (comm->packed_all.ensure((total + 1) * 4) || comm->packed.ensure((nw + 1) * 4)) return MUMS_E_HIP;
+    if (hipMemsetAsync(comm->packed_all.p, 0, (total + 1) * 4, st) != hipSuccess) return MUMS_E_HIP;
+    if (W == 1) {
+        RC(mums_shard_packed_copy(ctx, (uint32_t*)comm->packed_all.p + woff));
+    } else {   // all-gather(v) of the packed slices as an all-to-allv with one block per peer
+        RC(mums_shard_packed_copy(ctx, (uint32_t*)comm->packed.p));
+        std::vector<uint64_t> meta{woff, nw}, M((size_t)2 * W);
+        RC(comm->allgather_u64(meta.data(), 2, M.data(), st));
+        // every rank sends its slice to every rank; received blocks land in rank order,
+        // which is word-offset order (genome blocks / slices ascend with the rank)
+        std::vector<uint64_t> sb(W, nw * 4), rb(W);
+        uint64_t o = 0;
+        bool ordered = true;
+        for (int p = 0; p < W; ++p) {
+            rb[p] = M[(size_t)2 * p + 1] * 4;
+            ordered = ordered && M[(size_t)2 * p] == o;
+            o += M[(size_t)2 * p + 1];
+        }
+        if (!ordered) return comm_fail(comm, "packed slices are not in rank order");
+        // the send buffer is the slice repeated per peer (all-to-allv sends disjoint blocks)
+        if (comm->rec.ensure((size_t)W * nw * 4 + 8)) return MUMS_E_HIP;
+        for (int p = 0; p < W; ++p)
+            if (nw && hipMemcpyAsync((uint32_t*)comm->rec.p + (size_t)p * nw, comm->packed.p, nw * 4,
+                                     hipMemcpyDeviceToDevice, st) != hipSuccess)
+                return MUMS_E_HIP;
+        RC(comm->alltoallv(comm->rec.p, sb.data(), comm->packed_all.p, rb.data(), st));
+    }
+    if (hipStreamSynchronize(st) != hipSuccess) return MUMS_E_HIP;
+    return mums_shard_find(ctx, rows, nrows, (const uint32_t*)comm->packed_all.p);
+}
+
+}  // extern "C"

@@ -294,4 +294,41 @@ class ShardedFindMatches:
         return full
 
 
-__all__ = ["key_ranges", "genome_blocks", "HipShardEngine", "ShardedSeedStage", "ShardedFindMatches"]
+class AbiShardStage:
+    """The sharded pipeline of one rank run by the C ABI itself (mums_shard_run,
+    shard_comm.hip): RCCL communicator from ncclCommInitRank, its unique id broadcast over
+    the default process group (any backend: only the 128-byte id and the control travel
+    there).  stage = STAGE_SEEDS (steps 1-4) or STAGE_ALL (1-8)."""
+
+    def __init__(self, engine, device: int, stage: int = 1, group: Optional[dist.ProcessGroup] = None):
+        self.engine = engine
+        self.stage = stage
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        lib = engine.mh._lib
+        uid = ctypes.create_string_buffer(128)
+        if self.rank == 0:
+            engine.mh._check(lib.mums_comm_unique_id(uid, 128))
+        obj = [bytes(uid.raw)]
+        if self.world > 1:
+            dist.broadcast_object_list(obj, src=0, group=group)
+        self.comm = ctypes.c_void_p()
+        rc = lib.mums_comm_init_rank(ctypes.byref(self.comm), device, self.world, self.rank, obj[0])
+        if rc != 0:
+            raise RuntimeError(f"mums_comm_init_rank failed ({rc})")
+        self.last_exchange_bytes = 0
+
+    def run(self) -> None:
+        lib = self.engine.mh._lib
+        rc = lib.mums_shard_run(self.engine.mh._ctx, self.comm, self.stage)
+        if rc != 0:
+            raise RuntimeError(f"mums_shard_run: {lib.mums_last_error(self.engine.mh._ctx).decode()} / "
+                               f"{lib.mums_comm_last_error(self.comm).decode()}")
+
+    def close(self) -> None:
+        if self.comm:
+            self.engine.mh._lib.mums_comm_destroy(self.comm)
+            self.comm = ctypes.c_void_p()
+
+
+__all__ = ["key_ranges", "genome_blocks", "HipShardEngine", "ShardedSeedStage", "ShardedFindMatches", "AbiShardStage"]

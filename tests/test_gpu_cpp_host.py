@@ -27,3 +27,15 @@ def test_cpp_host_known_answers(tool, case):
     out = subprocess.run(args, check=True, capture_output=True, timeout=300).stdout
     assert out.count(b"\n") == case["matches"]
     assert hashlib.md5(out).hexdigest() == case["md5"]
+
+
+@pytest.mark.parametrize("ranks", ["--gpus 1", "--local 2", "--local 3"])
+@pytest.mark.parametrize("case", [c for c in CASES if c["mode"] == "MemHash" and c["n"] <= 10_000_000],
+                         ids=lambda c: f"G{c['G']}_n{c['n']}_p{c['p']}")
+def test_cpp_sharded_known_answers(tool, case, ranks):
+    """mums::ShardedMemHash (one thread per rank, mums_shard_run; --gpus: RCCL communicators
+    from ncclCommInitAll, --local: ranks sharing device 0) = the reference's known answers."""
+    args = [tool] + ranks.split() + ["gen", str(case["G"]), str(case["n"]), str(case["w"]), str(case["p"])]
+    out = subprocess.run(args, check=True, capture_output=True, timeout=300).stdout
+    assert out.count(b"\n") == case["matches"]
+    assert hashlib.md5(out).hexdigest() == case["md5"]

@@ -1,0 +1,42 @@
+"""Multi-GPU MemHash through the C ABI (mums_shard_run, shard_comm.hip): the whole sharded
+pipeline (keys, count all-gather, key ranges, record all-to-allv, merge, bucket ranges, row
+all-to-allv, packed all-gather, chains + replay) with ranks as threads of one process.
+On the one-GPU test box the ranks share device 0: the host-staged in-process communicator
+covers 1-4 ranks, RCCL (ncclCommInitAll) covers one rank.  Results = the oracle's
+MemHash::FindMatches bit for bit."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def run(gpu_lib, oracle_mod, G, n, w, p, world, comm, table_size=40000):
+    seqs = oracle_mod.generate(G, n, p, 500 + G * 11 + world)
+    seed = oracle_mod.get_seed(w)
+    lengths, starts, st = oracle_mod.find_matches(seqs, seed, table_size=table_size)
+    with gpu_lib.ShardedMemHash([0] * world, comm=comm, table_size=table_size) as sh:
+        sh.SetSeed(seed)
+        ml = sh.FindMatches(seqs)
+        coll = sum(s["collision_count"] for s in sh.stats_per_rank)
+    assert len(ml) == len(lengths)
+    assert np.array_equal(ml.lengths, lengths) and np.array_equal(ml.starts, starts)
+    assert coll == st["collision_count"]
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4])
+@pytest.mark.parametrize("G,n,w,p", [(4, 300_000, 15, 0.02), (5, 200_000, 13, 0.05), (3, 500_000, 17, 1.0)])
+def test_shard_run_local_comm(gpu_lib, oracle_mod, world, G, n, w, p):
+    run(gpu_lib, oracle_mod, G, n, w, p, world, "local")
+
+
+def test_shard_run_local_comm_small_table(gpu_lib, oracle_mod):
+    run(gpu_lib, oracle_mod, 4, 200_000, 15, 0.03, 3, "local", table_size=7)
+
+
+def test_shard_run_more_ranks_than_genomes(gpu_lib, oracle_mod):
+    run(gpu_lib, oracle_mod, 2, 300_000, 15, 0.02, 3, "local")
+
+
+@pytest.mark.parametrize("G,n,w,p", [(4, 300_000, 15, 0.02), (8, 200_000, 19, 0.01)])
+def test_shard_run_rccl_one_rank(gpu_lib, oracle_mod, G, n, w, p):
+    run(gpu_lib, oracle_mod, G, n, w, p, 1, "rccl")

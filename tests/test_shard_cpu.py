@@ -158,3 +158,16 @@ def test_genome_slices_cover_every_position_in_order():
         assert all(parts[i][1] == parts[i + 1][0] for i in range(len(parts) - 1))
     with pytest.raises(ValueError):
         genome_slices(lens, L, 3)
+
+
+def test_abi_key_ranges_match_python():
+    """mums_shard_key_ranges (C ABI, host only) = shard.key_ranges for the same totals."""
+    import libmems_amd as lm
+    from libmems_amd.shard import key_ranges
+    rng = np.random.default_rng(3)
+    for nb in (1, 7, 128, 40000):
+        for world in (1, 2, 3, 8):
+            t = rng.integers(0, 1000, size=nb).astype(np.uint64)
+            if nb > 10:
+                t[rng.integers(0, nb, size=nb // 2)] = 0
+            assert lm.shard_key_ranges(t, world) == key_ranges(t, world)

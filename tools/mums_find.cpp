@@ -46,8 +46,16 @@ static std::string read_seq(const std::string& path) {
 }
 
 int main(int argc, char** argv) {
+    int gpus = 0;        // --gpus N: ShardedMemHash over devices 0..N-1 (RCCL); --local N: one GPU, N ranks
+    bool local = false;
+    if (argc > 2 && (std::string(argv[1]) == "--gpus" || std::string(argv[1]) == "--local")) {
+        local = std::string(argv[1]) == "--local";
+        gpus = atoi(argv[2]);
+        argv += 2;
+        argc -= 2;
+    }
     if (argc < 3) {
-        std::cerr << "usage: mums_find gen G n weight p [mask] | files weight f1 f2 ...\n";
+        std::cerr << "usage: mums_find [--gpus N | --local N] gen G n weight p [mask] | files weight f1 f2 ...\n";
         return 2;
     }
     std::string mode = argv[1];
@@ -64,6 +72,28 @@ int main(int argc, char** argv) {
     } else {
         weight = atoi(argv[2]);
         for (int i = 3; i < argc; ++i) seqs.push_back(read_seq(argv[i]));
+    }
+    if (gpus > 0) {
+        try {
+            std::vector<int> devs(gpus, 0);
+            for (int r = 0; r < gpus; ++r) devs[r] = local ? 0 : r;
+            mums::ShardedMemHash sh(devs, local);
+            sh.SetSeed(weight ? (uint64_t)mums_get_seed(weight, 0) : 0);
+            for (const auto& s : seqs) sh.AddSequence(s);
+            mums::MatchList ml;
+            auto t0 = std::chrono::steady_clock::now();
+            sh.FindMatches(ml);
+            auto t1 = std::chrono::steady_clock::now();
+            std::ostringstream os;
+            for (const auto& m : ml) os << m << '\n';
+            std::cout << os.str();
+            std::cerr << "matches " << ml.size() << " ranks " << gpus << " ms "
+                      << std::chrono::duration<double, std::milli>(t1 - t0).count() << "\n";
+        } catch (const std::exception& e) {
+            std::cerr << "error: " << e.what() << "\n";
+            return 1;
+        }
+        return 0;
     }
     try {
         mums::MaskedMemHash mh(0);   // mask 0 behaves exactly like MemHash
