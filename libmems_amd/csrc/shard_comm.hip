@@ -21,6 +21,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <condition_variable>
 #include <cstring>
 #include <memory>
@@ -77,13 +79,20 @@ struct RcclComm : mums_comm {
     int allgather_u64(const uint64_t* send, size_t n, uint64_t* recv, hipStream_t st) override {
         if (scratch.ensure((world + 1) * n * 8 + 64)) return comm_fail(this, "allgather buffer");
         uint64_t* d = (uint64_t*)scratch.p;
-        if (hipMemcpyAsync(d + (size_t)world * n, send, n * 8, hipMemcpyHostToDevice, st) != hipSuccess)
+        if (hipMemcpy(d + (size_t)world * n, send, n * 8, hipMemcpyHostToDevice) != hipSuccess)
             return comm_fail(this, "allgather H2D");
         ncclResult_t r = ncclAllGather(d + (size_t)world * n, d, n, ncclUint64, nc, st);
         if (r != ncclSuccess) return comm_fail(this, std::string("ncclAllGather: ") + ncclGetErrorString(r));
-        if (hipMemcpyAsync(recv, d, (size_t)world * n * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess)
+        if (hipStreamSynchronize(st) != hipSuccess ||
+            hipMemcpy(recv, d, (size_t)world * n * 8, hipMemcpyDeviceToHost) != hipSuccess)
             return comm_fail(this, "allgather D2H");
+        if (getenv("MUMS_DEV_COMM_DEBUG")) {
+            uint64_t a = 0, b = 0;
+            for (size_t i = 0; i < n; ++i) a += send[i] * (i + 1);
+            for (size_t i = 0; i < n; ++i) b += recv[(size_t)rank * n + i] * (i + 1);
+            fprintf(stderr, "rank %d allgather n %zu send %lu recv-own %lu\n", rank, n, (unsigned long)a,
+                    (unsigned long)b);
+        }
         return MUMS_OK;
     }
     int alltoallv(const void* d_send, const uint64_t* sb, void* d_recv, const uint64_t* rb, hipStream_t st) override {

@@ -4,6 +4,8 @@
 // the MatchList text (UngappedLocalAlignment.h:200-206), one match per line.
 //   mums_find gen G n weight p [mask]        (mask > 0 selects MaskedMemHash)
 //   mums_find files weight f1 f2 ...
+#include <unistd.h>
+
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -77,7 +79,15 @@ int main(int argc, char** argv) {
         try {
             std::vector<int> devs(gpus, 0);
             for (int r = 0; r < gpus; ++r) devs[r] = local ? 0 : r;
+            // RCCL prints its version banner on stdout during communicator setup: keep the
+            // MatchList alone on stdout
+            std::fflush(stdout);
+            const int saved = dup(1);
+            dup2(2, 1);
             mums::ShardedMemHash sh(devs, local);
+            std::fflush(stdout);
+            dup2(saved, 1);
+            close(saved);
             sh.SetSeed(weight ? (uint64_t)mums_get_seed(weight, 0) : 0);
             for (const auto& s : seqs) sh.AddSequence(s);
             mums::MatchList ml;
