@@ -35,7 +35,10 @@ namespace {
 #ifndef MUMS_WALK_BUDGET
 #define MUMS_WALK_BUDGET 2
 #endif
-constexpr int kWalkBudget = MUMS_WALK_BUDGET;   // 64-column hit words per lane before a walk goes to a workgroup
+constexpr int kWalkBudget = MUMS_WALK_BUDGET;
+#ifndef MUMS_HIT_BATCH
+#define MUMS_HIT_BATCH 4   // components whose window loads are in flight together (hit_word)
+#endif   // 64-column hit words per lane before a walk goes to a workgroup
 
 struct WalkItem {
     uint32_t j;      // position in line order
@@ -228,22 +231,53 @@ __device__ uint64_t hit_word(int64_t c0, const Mhe<MG>& P, const GenomeTable& gt
             if ((valid >> i) & 1) h |= (uint64_t)hit_lane<MG>(c0 + i, P, gt, clo, chi, packed, ss) << i;
         return h;
     }
-    uint64_t R[3];
-    bases96(packed, ls.nwords, gt.woff[ref], sref - 1 + c0, R);
+    // per batch of (up to) 8 components: every window load is issued before the first
+    // use, so a word costs one memory round trip per batch, not one per genome
+    uint64_t R[3] = {0, 0, 0};
     uint64_t acc0 = 0, acc1 = 0, acc2 = 0;
     bool rev = false;
+    constexpr int kBatch = MG < MUMS_HIT_BATCH ? MG : MUMS_HIT_BATCH;
     #pragma unroll
-    for (int g = 0; g < MG; ++g) {
-        const int64_t s = P.s[g];
-        if (g < gt.G && g != ref && s != 0) {
+    for (int g0 = 0; g0 < MG; g0 += kBatch) {
+        uint32_t w[kBatch][7];
+        int sh[kBatch];
+        #pragma unroll
+        for (int k = 0; k < kBatch; ++k) {
+            const int g = g0 + k;
+            const int64_t s = P.s[g];
+            sh[k] = 0;
+            if (g < gt.G && s != 0) {
+                const int64_t p = s > 0 ? s - 1 + c0 : -s + ls.L - 2 - c0 - 95;
+                const int64_t wi = (int64_t)gt.woff[g] + (p >> 4);
+                sh[k] = 2 * (int)(p & 15);
+                #pragma unroll
+                for (int i = 0; i < 7; ++i) {
+                    const int64_t q = wi + i;
+                    w[k][i] = (q >= 0 && (uint64_t)q < ls.nwords) ? packed[q] : 0u;
+                }
+            }
+        }
+        #pragma unroll
+        for (int k = 0; k < kBatch; ++k) {
+            const int g = g0 + k;
+            const int64_t s = P.s[g];
+            if (!(g < gt.G && s != 0)) continue;
             uint64_t C[3];
-            if (s > 0) {
-                bases96(packed, ls.nwords, gt.woff[g], s - 1 + c0, C);
+            #pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const uint64_t hi = ((uint64_t)w[k][2 * j] << 32) | w[k][2 * j + 1];
+                const uint64_t lo = w[k][2 * j + 2];
+                C[j] = (hi << sh[k]) | ((lo << sh[k]) >> 32);
+            }
+            if (g == ref) {
+                R[0] = C[0];
+                R[1] = C[1];
+                R[2] = C[2];
+            } else if (s > 0) {
                 acc0 |= R[0] ^ C[0];
                 acc1 |= R[1] ^ C[1];
                 acc2 |= R[2] ^ C[2];
             } else {   // column t <-> complement of base |s| + L - 2 - c0 - t
-                bases96(packed, ls.nwords, gt.woff[g], -s + ls.L - 2 - c0 - 95, C);
                 acc0 |= R[0] ^ rc32(C[2]);
                 acc1 |= R[1] ^ rc32(C[1]);
                 acc2 |= R[2] ^ rc32(C[0]);
@@ -353,10 +387,10 @@ __global__ __launch_bounds__(kBlock) void chain_link_kernel(View v, const uint64
     const int L = ss.L;
     const LineSpec ls = line_spec(ss, gt);
     Mhe<MG> A, B;
-    probe_of<MG, View>(v, probe_info, ord[j], gt, mp, L, A);
+    probe_of<MG, View>(v, probe_info, j, gt, mp, L, A);
     bool same = false;
     if (j + 1 < P) {
-        probe_of<MG, View>(v, probe_info, ord[j + 1], gt, mp, L, B);
+        probe_of<MG, View>(v, probe_info, j + 1, gt, mp, L, B);
         same = same_line<MG>(A, B);
     }
     const int64_t xa = start_at(A, first_start(A));
@@ -402,7 +436,7 @@ __global__ __launch_bounds__(kBlock) void chain_left_kernel(View v, const uint64
     const int L = ss.L;
     const LineSpec ls = line_spec(ss, gt);
     Mhe<MG> A;
-    probe_of<MG, View>(v, probe_info, ord[j], gt, mp, L, A);
+    probe_of<MG, View>(v, probe_info, j, gt, mp, L, A);
     const int64_t xa = start_at(A, first_start(A));
     int64_t clo, chi;
     frame_bounds<MG>(A, gt, &clo, &chi);
@@ -430,7 +464,7 @@ __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64
                                                             const WalkItem* __restrict__ queue,
                                                             const unsigned int* __restrict__ qcount,
                                                             uint8_t* __restrict__ link, int64_t* __restrict__ rcol,
-                                                            int64_t* __restrict__ lcol) {
+                                                            int64_t* __restrict__ lcol, unsigned int* __restrict__ dbg) {
     const int lane = threadIdx.x & 63;
     const int L = ss.L;
     const LineSpec ls = line_spec(ss, gt);
@@ -439,7 +473,7 @@ __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64
     for (unsigned qi = (blockIdx.x * kBlock + threadIdx.x) >> 6; qi < nq; qi += nwaves) {
         const WalkItem it = queue[qi];
         Mhe<MG> A;
-        probe_of<MG, View>(v, probe_info, ord[it.j], gt, mp, L, A);
+        probe_of<MG, View>(v, probe_info, it.j, gt, mp, L, A);
         const int64_t xa = start_at(A, first_start(A));
         int64_t clo, chi;
         frame_bounds<MG>(A, gt, &clo, &chi);
@@ -449,7 +483,9 @@ __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64
                                       : (it.stop == INT64_MIN ? INT64_MAX : cur - it.stop);
         int64_t last = 0, u0 = 1;
         bool reached = last >= stopu;
+        unsigned steps = 0;
         while (!reached) {
+            ++steps;
             const uint64_t H = hit_word_dir<MG>(dir, cur + dir * (u0 + 64 * (int64_t)lane), A, gt, clo, chi, packed,
                                                 ss, ls);
             const int f = H ? __builtin_ctzll(H) : 64;
@@ -479,6 +515,13 @@ __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64
             last = u0 + 64 * 63 + __shfl(hb, 63);
             u0 += 64 * 64;
             reached = last >= stopu;
+        }
+        if (lane == 0 && dbg) {   // development: walk length histogram (MUMS_DEV_CHAIN_DEBUG)
+            atomicAdd(&dbg[0], steps > 1 ? 1u : 0u);
+            atomicAdd(&dbg[1], steps > 16 ? 1u : 0u);
+            atomicAdd(&dbg[2], steps > 256 ? 1u : 0u);
+            atomicMax(&dbg[3], steps);
+            atomicAdd(&dbg[4], steps);
         }
         if (lane == 0) {
             const int64_t c = cur + dir * last;
@@ -532,7 +575,7 @@ __global__ __launch_bounds__(kBlock) void chain_entry_kernel(View v, const uint6
     if (j > 0 && link[j - 1]) return;
     const uint32_t s = seg_excl[j];
     Mhe<MG> A;
-    probe_of<MG, View>(v, probe_info, ord[j], gt, mp, L, A);
+    probe_of<MG, View>(v, probe_info, j, gt, mp, L, A);
     const int64_t xa = start_at(A, first_start(A));
     const int64_t cmin = lcol[j] - xa, cmax = seg_r[s] - xa;
     int64_t* e = pool + (uint64_t)s * (uint64_t)(gt.G + 2);
@@ -551,11 +594,12 @@ inline unsigned grid_of(uint64_t n) { return (unsigned)((n + kBlock - 1) / kBloc
 
 }  // namespace
 
-size_t chain_tmp_bytes(uint64_t P, uint32_t Tb) {
+size_t chain_tmp_bytes(uint64_t P, uint32_t Tb, int G) {
     // lkey, sort A/B keys (3 x 8) + vals A/B (2 x 4) + link (1) + rcol, lcol, seg_r (3 x 8)
     // + seg (4) + queue (24) + padding.  The replay reuses it: per chain <= 76 B, then the
     // big-bucket scratch (count 4 + scan 4 + slot 16 per probe, + 4 per bucket)
-    return P * (24 + 8 + 1 + 24 + 4 + sizeof(WalkItem) + 16 + 24) + (uint64_t)Tb * 4 + 64 * 64;
+    // + the probe rows in line order ((G + 1) x 8)
+    return P * (24 + 8 + 1 + 24 + 4 + sizeof(WalkItem) + 16 + 24 + 8 * (uint64_t)(G + 1)) + (uint64_t)Tb * 4 + 64 * 64;
 }
 
 // Chain labelling of the P probes (key order): chain_of[k] = chain of probe k;
@@ -583,6 +627,7 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
     uint32_t* seg = (uint32_t*)carve(P * 4);
     WalkItem* queue = (WalkItem*)carve(P * sizeof(WalkItem));
     unsigned int* qcount = (unsigned int*)carve(64);
+    int64_t* rows_line = (int64_t*)carve(P * (uint64_t)(gt.G + 1) * 8);
     hipError_t e;
     const unsigned grid = grid_of(P);
     hipLaunchKernelGGL((chain_key_kernel<MG, View>), dim3(grid), dim3(kBlock), 0, st, v, probe_info, P, gt, mp, ss.L,
@@ -591,24 +636,31 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
     int buf = 0;
     if ((e = radix_sort<uint64_t>(lkey, nullptr, P, 64, kA, vA, kB, vB, d_radix_tmp, &buf, st)) != hipSuccess) return e;
     const uint32_t* ord = buf ? vB : vA;
+    // the rows in line order: the link / walk / entry kernels then read row j, not row ord[j]
+    if ((e = launch_gather_rows(v.rows, ord, P, gt.G, rows_line, st)) != hipSuccess) return e;
+    View vl = v;
+    vl.rows = rows_line;
     const unsigned walk_grid = 2048;
     for (int pass = 0; pass < 2; ++pass) {
         if ((e = hipMemsetAsync(qcount, 0, 4, st)) != hipSuccess) return e;
         if (pass == 0)
-            hipLaunchKernelGGL((chain_link_kernel<MG, View>), dim3(grid), dim3(kBlock), 0, st, v, probe_info, P, gt,
+            hipLaunchKernelGGL((chain_link_kernel<MG, View>), dim3(grid), dim3(kBlock), 0, st, vl, probe_info, P, gt,
                                mp, ss, ord, packed, link, rcol, queue, qcount);
         else
-            hipLaunchKernelGGL((chain_left_kernel<MG, View>), dim3(grid), dim3(kBlock), 0, st, v, probe_info, P, gt,
+            hipLaunchKernelGGL((chain_left_kernel<MG, View>), dim3(grid), dim3(kBlock), 0, st, vl, probe_info, P, gt,
                                mp, ss, ord, packed, link, lcol, queue, qcount);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-        hipLaunchKernelGGL((chain_walk_kernel<MG, View>), dim3(walk_grid), dim3(kBlock), 0, st, v, probe_info, gt, mp,
-                           ss, ord, packed, queue, qcount, link, rcol, lcol);
+        const bool cdbg = getenv("MUMS_DEV_CHAIN_DEBUG") != nullptr;
+        if (cdbg && (e = hipMemsetAsync(qcount + 4, 0, 32, st)) != hipSuccess) return e;
+        hipLaunchKernelGGL((chain_walk_kernel<MG, View>), dim3(walk_grid), dim3(kBlock), 0, st, vl, probe_info, gt, mp,
+                           ss, ord, packed, queue, qcount, link, rcol, lcol, cdbg ? qcount + 4 : nullptr);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-        if (getenv("MUMS_DEV_CHAIN_DEBUG")) {   // development: long-walk queue sizes
-            unsigned hq = 0;
-            (void)hipMemcpyAsync(&hq, qcount, 4, hipMemcpyDeviceToHost, st);
+        if (cdbg) {   // development: long-walk queue sizes and wave-step histogram
+            unsigned hq[9] = {};
+            (void)hipMemcpyAsync(hq, qcount, 36, hipMemcpyDeviceToHost, st);
             (void)hipStreamSynchronize(st);
-            fprintf(stderr, "chains: pass %d long walks %u of %lu probes\n", pass, hq, (unsigned long)P);
+            fprintf(stderr, "chains: pass %d long walks %u of %lu probes; steps >1: %u >16: %u >256: %u max %u total %u\n",
+                    pass, hq[0], (unsigned long)P, hq[4], hq[5], hq[6], hq[7], hq[8]);
         }
     }
     hipLaunchKernelGGL(chain_flag_kernel, dim3(grid), dim3(kBlock), 0, st, link, P, seg);
@@ -616,7 +668,7 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
     if ((e = exclusive_scan_u32(seg, P, d_scan_tmp, d_nchains, st)) != hipSuccess) return e;
     hipLaunchKernelGGL(chain_seg_kernel, dim3(grid), dim3(kBlock), 0, st, link, ord, seg, P, rcol, chain_of, seg_r);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL((chain_entry_kernel<MG, View>), dim3(grid), dim3(kBlock), 0, st, v, probe_info, P, gt, mp, ss.L,
+    hipLaunchKernelGGL((chain_entry_kernel<MG, View>), dim3(grid), dim3(kBlock), 0, st, vl, probe_info, P, gt, mp, ss.L,
                        ord, link, seg, lcol, seg_r, pool);
     return hipGetLastError();
 }

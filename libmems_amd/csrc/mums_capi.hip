@@ -313,7 +313,7 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
     // summaries, their compacted copies, keep-flag scan, compacted bucket ranges (replay.hip)
     HIPCHK(ctx->summ.ensure((ctx->P + 1) * 64 + (ctx->P + 64) * 4 + ((size_t)Tb + 64) * 8 +
                             scan_tmp_bytes(ctx->P + 2) + 4096));
-    HIPCHK(ctx->chain_tmp.ensure(chain_tmp_bytes(ctx->P + 1, Tb)));
+    HIPCHK(ctx->chain_tmp.ensure(chain_tmp_bytes(ctx->P + 1, Tb, G)));
     HIPCHK(ctx->radix_tmp.ensure(radix_tmp_bytes(ctx->P + 1)));
     HIPCHK(ctx->tmp.ensure(std::max(scan_tmp_bytes(ctx->P + 1), scan_tmp_bytes(Tb))));
     HIPCHK(hipMemsetAsync(&dc->max_bucket, 0, 4, st));

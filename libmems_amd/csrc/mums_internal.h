@@ -250,7 +250,7 @@ hipError_t eo_gather(EoWork& w, int G, uint64_t* d_len_out, int64_t* d_s_out, hi
 hipError_t eo_sort_ids(EoWork& w, const uint64_t* d_keys, uint32_t n, int depth_override, uint32_t* d_ids_out,
                        hipStream_t st);
 
-size_t chain_tmp_bytes(uint64_t P, uint32_t Tb);
+size_t chain_tmp_bytes(uint64_t P, uint32_t Tb, int G);
 template <int MG, typename View>
 hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const GenomeTable& gt, const MatchParams& mp,
                          const SeedSpec& ss, const uint32_t* packed, void* d_chain_tmp, void* d_scan_tmp,

@@ -830,9 +830,9 @@ hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key
         hipLaunchKernelGGL(seg_dbase_kernel, dim3((unsigned)(nb * npass)), dim3(kBlock), 0, st, ghist, d_bstart,
                            npass, dbase, -1);
 #if MUMS_SORT_PERSIST
-    // resident blocks of the persistent pass: occupancy x CUs
-    static uint64_t persist_grid = 0;
-    if (persist_grid == 0) {
+    // resident blocks of the persistent pass: occupancy x CUs of the current device
+    uint64_t persist_grid = 0;
+    {
         int dev = 0, cus = 0, per = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
