@@ -15,7 +15,7 @@
 //                           the hit columns between them; segment ends walk on to
 //                           the chain's end (left walks in chain_left_kernel).  Walks
 //                           test 64 columns per step with packed-word XORs (hit_word)
-//   4. chain_walk_kernel  : walks longer than a per-lane budget, one wave each
+//   4. chain_walk_kernel  : walks longer than a per-lane budget, a group of 16 lanes each
 //                           (one 64-column hit word per lane, break found by ballot)
 //   5. chain_seg / chain_entry kernels: segment ids (scan), the extended entry of
 //                           every chain and chain_of[probe].
@@ -450,12 +450,20 @@ __global__ __launch_bounds__(kBlock) void chain_left_kernel(View v, const uint64
     }
 }
 
-// Long walks, one wave per item (grid-stride over the queue).  Each step evaluates the
-// 64 words (64 columns each) after the chain's last hit, one word per lane; the chain
-// ends at the first lane whose word holds a run of L misses after a hit, or whose first
-// hit lies L or more columns after the previous lane's last hit (the
-// maximal chain of hits with gaps <= L).  A ballot finds that lane, shuffles fetch the
-// last hit before the break.
+// Long walks, one group of kWalkGroup lanes per item (grid-stride over the queue; a wave
+// walks 64 / kWalkGroup items at once: most queued walks end within a few words, so more
+// items in flight hide more load latency than wider steps would).  Each step evaluates the
+// kWalkGroup words (64 columns each) after the chain's last hit, one word per lane; the
+// chain ends at the first lane whose word holds a run of L misses after a hit, or whose
+// first hit lies L or more columns after the previous lane's last hit (the
+// maximal chain of hits with gaps <= L).  A ballot finds that lane, shuffles inside the
+// group fetch the last hit before the break.
+#ifndef MUMS_WALK_GROUP
+#define MUMS_WALK_GROUP 16
+#endif
+constexpr int kWalkGroup = MUMS_WALK_GROUP;
+static_assert(kWalkGroup >= 2 && kWalkGroup <= 64 && (kWalkGroup & (kWalkGroup - 1)) == 0, "group: power of 2");
+
 template <int MG, typename View>
 __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64_t* __restrict__ probe_info,
                                                             GenomeTable gt, MatchParams mp, SeedSpec ss,
@@ -465,12 +473,14 @@ __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64
                                                             const unsigned int* __restrict__ qcount,
                                                             uint8_t* __restrict__ link, int64_t* __restrict__ rcol,
                                                             int64_t* __restrict__ lcol, unsigned int* __restrict__ dbg) {
-    const int lane = threadIdx.x & 63;
+    constexpr int GS = kWalkGroup;
+    const int lane = threadIdx.x & 63, gl = lane & (GS - 1), gsh = lane & ~(GS - 1);
+    const uint64_t gmask = GS == 64 ? ~0ull : ((1ull << GS) - 1);
     const int L = ss.L;
     const LineSpec ls = line_spec(ss, gt);
     const unsigned nq = *qcount;
-    const unsigned nwaves = gridDim.x * (kBlock / 64);
-    for (unsigned qi = (blockIdx.x * kBlock + threadIdx.x) >> 6; qi < nq; qi += nwaves) {
+    const unsigned ngroups = gridDim.x * (kBlock / GS);
+    for (unsigned qi = (blockIdx.x * kBlock + threadIdx.x) / GS; qi < nq; qi += ngroups) {
         const WalkItem it = queue[qi];
         Mhe<MG> A;
         probe_of<MG, View>(v, probe_info, it.j, gt, mp, L, A);
@@ -486,7 +496,7 @@ __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64
         unsigned steps = 0;
         while (!reached) {
             ++steps;
-            const uint64_t H = hit_word_dir<MG>(dir, cur + dir * (u0 + 64 * (int64_t)lane), A, gt, clo, chi, packed,
+            const uint64_t H = hit_word_dir<MG>(dir, cur + dir * (u0 + 64 * (int64_t)gl), A, gt, clo, chi, packed,
                                                 ss, ls);
             const int f = H ? __builtin_ctzll(H) : 64;
             const int hb = H ? 63 - __builtin_clzll(H) : -1;
@@ -498,32 +508,32 @@ __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64
                 if (len < L) a &= a >> (L - len);
                 if (a) rend = 63 - __builtin_clzll(H & ((1ull << __builtin_ctzll(a)) - 1));
             }
-            const int prev_hb = __shfl_up(hb, 1);
-            const int64_t miss = lane == 0 ? (u0 - last - 1) + f : (int64_t)(63 - prev_hb) + f;
+            const int prev_hb = __shfl_up(hb, 1, GS);
+            const int64_t miss = gl == 0 ? (u0 - last - 1) + f : (int64_t)(63 - prev_hb) + f;
             const bool brk_in = H == 0 || miss >= L;
-            const uint64_t bm = __ballot(brk_in || rend >= 0);
+            const uint64_t bm = (__ballot(brk_in || rend >= 0) >> gsh) & gmask;
             if (bm) {
                 const int k = __builtin_ctzll(bm);
-                const int kin = __shfl(brk_in ? 1 : 0, k);
-                const int hprev = __shfl(hb, k > 0 ? k - 1 : 0);
-                const int rk = __shfl(rend, k);
+                const int kin = __shfl(brk_in ? 1 : 0, k, GS);
+                const int hprev = __shfl(hb, k > 0 ? k - 1 : 0, GS);
+                const int rk = __shfl(rend, k, GS);
                 if (kin) last = k == 0 ? last : u0 + 64 * (int64_t)(k - 1) + hprev;
                 else last = u0 + 64 * (int64_t)k + rk;
                 reached = last >= stopu;
                 break;
             }
-            last = u0 + 64 * 63 + __shfl(hb, 63);
-            u0 += 64 * 64;
+            last = u0 + 64 * (GS - 1) + __shfl(hb, GS - 1, GS);
+            u0 += 64 * GS;
             reached = last >= stopu;
         }
-        if (lane == 0 && dbg) {   // development: walk length histogram (MUMS_DEV_CHAIN_DEBUG)
+        if (gl == 0 && dbg) {   // development: walk length histogram (MUMS_DEV_CHAIN_DEBUG)
             atomicAdd(&dbg[0], steps > 1 ? 1u : 0u);
             atomicAdd(&dbg[1], steps > 16 ? 1u : 0u);
             atomicAdd(&dbg[2], steps > 256 ? 1u : 0u);
             atomicMax(&dbg[3], steps);
             atomicAdd(&dbg[4], steps);
         }
-        if (lane == 0) {
+        if (gl == 0) {
             const int64_t c = cur + dir * last;
             if (it.kind == 0) {
                 link[it.j] = reached ? 1 : 0;

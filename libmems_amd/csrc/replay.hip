@@ -20,6 +20,7 @@
 // registers; per round every unconsumed lane runs its lower_bound against the
 // current vector, the workgroup takes the first non-colliding probe (ballot),
 // inserts its chain entry with a one-barrier LDS shift and goes on after it.
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -673,6 +674,157 @@ __global__ __launch_bounds__(kBigRB) void replay_big_kernel(
     }
 }
 
+// Grid path of the big-bucket replay (host-driven, one bucket at a time): the same rank
+// counts as replay_big_kernel, but every pass over the bucket's probes or ranks is a grid
+// launch, the counts' scan is the device-wide scan, and only the exact lower_bound of each
+// suspicious probe runs on one lane.  For buckets with few suspicious probes (<= kGridSlow).
+constexpr uint32_t kGridSlow = 512;
+
+// info: [0] min rank, [1] max rank, [2] tied, [3] suspicious count, [4] error, [5] collisions
+__global__ __launch_bounds__(kBlock) void bigg_classify_kernel(const uint4* __restrict__ summ,
+                                                               const uint4* __restrict__ summ_b, uint32_t beg,
+                                                               uint32_t K, uint32_t* __restrict__ info,
+                                                               uint32_t* __restrict__ slow, uint32_t cap) {
+    __shared__ uint32_t s_min[kBlock / 64], s_max[kBlock / 64], s_tie;
+    const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_tie = 0;
+    uint32_t rmin = 0xFFFFFFFFu, rmax = 0;
+    if (k < K) {
+        const uint4 a = summ[beg + k], c = summ_b[beg + k];
+        if (c.z & 0x80000000u) s_tie = 1;
+        if (a.w & 0x80000000u) {
+            rmin = c.z;
+            rmax = c.z;
+        } else {
+            const uint32_t q = atomicAdd(&info[3], 1u);
+            if (q < cap) slow[q] = k;
+        }
+    }
+    #pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+        rmin = min(rmin, (uint32_t)__shfl_xor((int)rmin, d));
+        rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, d));
+    }
+    if (lane == 0) { s_min[wv] = rmin; s_max[wv] = rmax; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kBlock / 64; ++w) { rmin = min(rmin, s_min[w]); rmax = max(rmax, s_max[w]); }
+        rmin = min(rmin, s_min[0]);
+        rmax = max(rmax, s_max[0]);
+        if (rmin != 0xFFFFFFFFu) atomicMin(&info[0], rmin);
+        atomicMax(&info[1], rmax);
+        if (s_tie) atomicOr(&info[2], 1u);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void bigg_slots_kernel(const uint4* __restrict__ summ,
+                                                            const uint4* __restrict__ summ_b, uint32_t beg, uint32_t K,
+                                                            uint32_t r0, uint32_t R, uint4* __restrict__ sbr) {
+    const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
+    if (k >= K) return;
+    const uint4 a = summ[beg + k];
+    if (a.w & 0x80000000u) {
+        const uint4 c = summ_b[beg + k];
+        if (c.z - r0 < R) sbr[c.z - r0] = make_uint4(a.z, a.x, c.x, c.y);
+    }
+}
+
+// chain-first probes [k0, k1) of the bucket: one copy of their chain each
+__global__ __launch_bounds__(kBlock) void bigg_fill_kernel(const uint4* __restrict__ summ,
+                                                           const uint4* __restrict__ summ_b, uint32_t beg, uint32_t k0,
+                                                           uint32_t k1, uint32_t r0, uint32_t* __restrict__ cnt) {
+    const uint32_t k = k0 + blockIdx.x * kBlock + threadIdx.x;
+    if (k >= k1) return;
+    if (summ[beg + k].w & 0x80000000u) cnt[summ_b[beg + k].z - r0] = 1u;
+}
+
+// suspicious probe j against the virtual vector V[i] = sbr[r], E[r] <= i < E[r + 1]
+template <int MG, typename View>
+__global__ void bigg_slow_kernel(View v, GenomeTable gt, MatchParams mp, int L, const uint64_t* __restrict__ probe_info,
+                                 const uint4* __restrict__ summ, const uint4* __restrict__ summ_b, uint32_t beg,
+                                 uint32_t j, uint32_t r0, uint32_t R, const uint32_t* __restrict__ E,
+                                 const uint4* __restrict__ sbr, const uint4* __restrict__ chain_sb,
+                                 const int64_t* __restrict__ pool, uint32_t* __restrict__ cnt,
+                                 uint32_t* __restrict__ info) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    const int G = gt.G;
+    const uint32_t t = E[R];
+    auto at = [&](uint32_t i) -> uint4 {
+        uint32_t lo = 0, n = R;
+        while (n > 0) {
+            const uint32_t h = n >> 1;
+            if (E[lo + h + 1] <= i) { lo += h + 1; n -= h + 1; } else n = h;
+        }
+        return sbr[lo];
+    };
+    const uint4 me = summ[beg + j], mb = summ_b[beg + j];
+    const uint32_t pmask = me.x, pcid = me.z;
+    const int64_t ps = (int64_t)me.y, pl = L;
+    Mhe<MG> P;
+    bool have = false;
+    auto full = [&](uint32_t xid) -> bool {
+        if (!have) { probe_full<MG, View>(v, gt, mp, L, probe_info, me.w & 0x3FFFFFFFu, P); have = true; }
+        Mhe<MG> X;
+        load_entry<MG>(pool, xid, G, X);
+        return mhe_less(X, P);
+    };
+    const uint32_t lb = lower_bound_acc(at, t, pmask, ps, pl, pcid, full);
+    bool isnew = true;
+    if (lb < t) {
+        const uint4 X = at(lb);
+        int q = slot_equiv(X, pmask, ps, pl, pcid);
+        if (q == 2) {
+            if (!have) { probe_full<MG, View>(v, gt, mp, L, probe_info, me.w & 0x3FFFFFFFu, P); have = true; }
+            Mhe<MG> X2;
+            load_entry<MG>(pool, X.x, G, X2);
+            q = (mhe_less(X2, P) || mhe_less(P, X2)) ? 0 : 1;
+        }
+        isnew = q == 0;
+    }
+    if (!isnew) {
+        info[5] += 1u;
+        return;
+    }
+    Mhe<MG> Ec;
+    bool hv = false;
+    auto fullc = [&](uint32_t xid) -> bool {
+        if (!hv) { load_entry<MG>(pool, pcid, G, Ec); hv = true; }
+        Mhe<MG> X;
+        load_entry<MG>(pool, xid, G, X);
+        return mhe_less(X, Ec);
+    };
+    const uint32_t ins = lower_bound_acc(at, t, pmask, (int64_t)mb.x, (int64_t)mb.y, pcid, fullc);
+    const uint32_t rr = mb.z - r0;
+    const uint32_t rl = ins > 0 ? chain_sb[at(ins - 1).x].z - r0 : 0u;
+    const uint32_t rh = ins < t ? chain_sb[at(ins).x].z - r0 : 0xFFFFFFFFu;
+    if (rr < R && rl <= rr && rr <= rh) cnt[rr] += 1u;
+    else info[4] = 1u;
+}
+
+__global__ __launch_bounds__(kBlock) void bigg_out_kernel(const uint32_t* __restrict__ E, uint32_t R,
+                                                          const uint4* __restrict__ sbr,
+                                                          const uint32_t* __restrict__ obase, uint32_t b,
+                                                          uint32_t* __restrict__ tbl) {
+    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
+    if (r >= R) return;
+    const uint32_t ob = obase[b];
+    const uint32_t e0 = E[r], c = E[r + 1] - e0;
+    for (uint32_t d = 0; d < c; ++d) tbl[ob + e0 + d] = sbr[r].x;
+}
+
+__global__ void bigg_finish_kernel(const uint32_t* __restrict__ E, uint32_t R, const uint32_t* __restrict__ info,
+                                   uint32_t b, uint32_t* __restrict__ tsize, uint32_t* __restrict__ cend, uint32_t beg,
+                                   DevCounters* ctr) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    const uint32_t t = E[R];
+    tsize[b] = t;
+    atomicAdd(&ctr->entries, (unsigned long long)t);
+    atomicAdd(&ctr->collisions, (unsigned long long)info[5]);
+    if (info[4]) atomicOr(&ctr->err, 4u);
+    cend[b] = beg;   // replay_kernel / replay_big_kernel skip it
+}
+
 // Probes that are neither chain-first nor suspicious (flag bits 31 / 30 clear) collide
 // with their chain entry without touching the vector, so the replay only needs the
 // others: keep flags -> exclusive scan -> compacted summaries and bucket ranges; the
@@ -863,6 +1015,62 @@ hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, i
         uint32_t* scr_cnt = (uint32_t*)carve((P + 1) * 4);
         uint32_t* scr_e = (uint32_t*)carve((P + 1 + mp.table_size + 1) * 4);
         uint4* scr_slot = (uint4*)carve((P + 1) * 16);
+        uint32_t* ginfo = (uint32_t*)carve(64);
+        uint32_t* gslow = (uint32_t*)carve((kGridSlow + 1) * 4);
+        // grid path first, for the big buckets with few suspicious probes (host-driven)
+        std::vector<uint32_t> hb(mp.table_size), he(mp.table_size);
+        if ((e = hipMemcpyAsync(hb.data(), cbeg, mp.table_size * 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+        if ((e = hipMemcpyAsync(he.data(), cend, mp.table_size * 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+        for (uint32_t b = 0; b < mp.table_size; ++b) {
+            const uint32_t beg = hb[b], K = he[b] - hb[b];
+            if (K <= big_min) continue;
+            uint32_t hinfo[8] = {0xFFFFFFFFu, 0, 0, 0, 0, 0, 0, 0};
+            if ((e = hipMemcpyAsync(ginfo, hinfo, 32, hipMemcpyHostToDevice, st)) != hipSuccess) return e;
+            hipLaunchKernelGGL(bigg_classify_kernel, dim3((K + kBlock - 1) / kBlock), dim3(kBlock), 0, st,
+                               (const uint4*)summ_c, (const uint4*)summ_bc, beg, K, ginfo, gslow, kGridSlow);
+            if ((e = hipMemcpyAsync(hinfo, ginfo, 32, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+            if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+            const uint32_t S = hinfo[3];
+            if (hinfo[2] || S > kGridSlow || hinfo[0] > hinfo[1]) continue;   // left to the kernels below
+            const uint32_t r0 = hinfo[0], R = hinfo[1] - hinfo[0] + 1;
+            std::vector<uint32_t> hs(S);
+            if (S) {
+                if ((e = hipMemcpy(hs.data(), gslow, S * 4, hipMemcpyDeviceToHost)) != hipSuccess) return e;
+                std::sort(hs.begin(), hs.end());
+            }
+            uint32_t* cnt = scr_cnt;
+            uint32_t* E = scr_e;
+            uint4* sbr = scr_slot;
+            if ((e = hipMemsetAsync(cnt, 0, (size_t)R * 4, st)) != hipSuccess) return e;
+            hipLaunchKernelGGL(bigg_slots_kernel, dim3((K + kBlock - 1) / kBlock), dim3(kBlock), 0, st,
+                               (const uint4*)summ_c, (const uint4*)summ_bc, beg, K, r0, R, sbr);
+            auto scan = [&]() -> hipError_t {
+                hipError_t x = hipMemcpyAsync(E, cnt, (size_t)R * 4, hipMemcpyDeviceToDevice, st);
+                if (x == hipSuccess) x = hipMemsetAsync(E + R, 0, 4, st);
+                if (x == hipSuccess) x = exclusive_scan_u32(E, (uint64_t)R + 1, stmp, nullptr, st);
+                return x;
+            };
+            uint32_t k0 = 0;
+            for (uint32_t si = 0; si <= S; ++si) {
+                const uint32_t j = si < S ? hs[si] : K;
+                if (j > k0)
+                    hipLaunchKernelGGL(bigg_fill_kernel, dim3((j - k0 + kBlock - 1) / kBlock), dim3(kBlock), 0, st,
+                                       (const uint4*)summ_c, (const uint4*)summ_bc, beg, k0, j, r0, cnt);
+                if (j == K) break;
+                if ((e = scan()) != hipSuccess) return e;
+                hipLaunchKernelGGL((bigg_slow_kernel<MG, View>), dim3(1), dim3(64), 0, st, v, gt, mp, L, probe_info,
+                                   (const uint4*)summ_c, (const uint4*)summ_bc, beg, j, r0, R, (const uint32_t*)E,
+                                   (const uint4*)sbr, (const uint4*)chain_sb, pool, cnt, ginfo);
+                k0 = j + 1;
+            }
+            if ((e = scan()) != hipSuccess) return e;
+            hipLaunchKernelGGL(bigg_out_kernel, dim3((R + kBlock - 1) / kBlock), dim3(kBlock), 0, st, (const uint32_t*)E,
+                               R, (const uint4*)sbr, bstart, b, tbl);
+            hipLaunchKernelGGL(bigg_finish_kernel, dim3(1), dim3(64), 0, st, (const uint32_t*)E, R, ginfo, b, tsize,
+                               cend, beg, (DevCounters*)ctr);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
         hipLaunchKernelGGL((replay_big_kernel<MG, View>), dim3(mp.table_size), dim3(kBigRB), 0, st, v, gt, mp, L,
                            probe_info, (const uint4*)summ_c, (const uint4*)summ_bc, cbeg, cend, bstart, tbl, pool,
                            (const uint4*)chain_sb, scr_cnt, scr_e, scr_slot, tsize, (DevCounters*)ctr, big_min);
