@@ -297,11 +297,26 @@ def main():
                 torch.cuda.synchronize()
                 best = min(best, time.perf_counter() - t1)
             sm = mh.stats()
+            # one more FindMatches with HIP events around the dominant kernel's launches
+            # (chain_walk_kernel) for its live duration and the roofline of the MUMs/s path
+            mh.SetProfiling(True)
+            mh.CreateMatches()
+            sp = mh.stats()
+            mh.SetProfiling(False)
+            walk_ms = sp["ms_chain_walks"]
+            walk_gbs = sp["chain_walk_bytes"] / (walk_ms * 1e-3) / 1e9 if walk_ms > 0 else None
             mums_c3 = {"mums_per_s": sm["mem_count"] / best, "matches": sm["mem_count"], "ms": best * 1e3,
                        "probes": sm["probes"], "chains": sm["chains"], "collisions": sm["collision_count"],
                        "workload": f"BASELINE config 3: {G} x {n // 10**6} Mbp related p=0.01, w19, full FindMatches",
                        "phase_ms": {k: round(sm[k], 3) for k in ("ms_keys", "ms_sort", "ms_groups", "ms_buckets",
-                                                                  "ms_chains", "ms_replay", "ms_output")}}
+                                                                  "ms_chains", "ms_replay", "ms_output")},
+                       "roofline": {"bound": "hbm", "kernel": "chain_walk_kernel (2 launches per FindMatches)",
+                                    "achieved": walk_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                    "frac": walk_gbs / HBM_PEAK_GBS if walk_gbs else None,
+                                    "bytes": sp["chain_walk_bytes"], "ms": walk_ms, "walks": sp["chain_walks"],
+                                    "hit_words": sp["chain_walk_words"],
+                                    "model": "28-B packed window per 64-column hit word and present component + "
+                                             "per walk the probe row ((G+1) x 8 B) and its 24-B queue item"}}
         except Exception as e:  # report, never hide
             mums_c3 = {"error": str(e)}
     seedmers_total = sum(max(n - lm.getSeedLength(seed) + 1, 0) for _ in range(G))

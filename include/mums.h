@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MUMS_ABI_VERSION 4
+#define MUMS_ABI_VERSION 5
 
 enum mums_status {
     MUMS_OK = 0,
@@ -73,6 +73,14 @@ typedef struct mums_stats {
     uint64_t chains;            /* seed chains among the probes                                        */
     uint64_t chunks;            /* ParallelMemHash compat: SML chunks searched (ParallelMemHash.cpp:75-83) */
     uint64_t restarts;          /* MER_REPEAT_LIMIT restarts of the merge (MatchFinder.cpp:253-277)      */
+    /* FindMatches' dominant kernel, chain_walk_kernel (ABI 5): HIP events around its launches
+     * (mums_set_profiling), the 64-column hit words it evaluated, the walks it finished and
+     * its algorithmic bytes: 28-B packed windows per word and present component + per walk
+     * the probe row ((G + 1) x 8 B) and the queue item (24 B). */
+    double   ms_chain_walks;
+    uint64_t chain_walk_words;
+    uint64_t chain_walks;
+    uint64_t chain_walk_bytes;
 } mums_stats;
 
 /* MemHash::MemHash (MemHash.cpp:33-49); device = HIP ordinal. */

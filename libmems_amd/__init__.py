@@ -79,6 +79,10 @@ class _Stats(ctypes.Structure):
         ("chains", ctypes.c_uint64),
         ("chunks", ctypes.c_uint64),
         ("restarts", ctypes.c_uint64),
+        ("ms_chain_walks", ctypes.c_double),
+        ("chain_walk_words", ctypes.c_uint64),
+        ("chain_walks", ctypes.c_uint64),
+        ("chain_walk_bytes", ctypes.c_uint64),
     ]
 
 

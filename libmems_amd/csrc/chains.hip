@@ -472,8 +472,10 @@ __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64
                                                             const WalkItem* __restrict__ queue,
                                                             const unsigned int* __restrict__ qcount,
                                                             uint8_t* __restrict__ link, int64_t* __restrict__ rcol,
-                                                            int64_t* __restrict__ lcol, unsigned int* __restrict__ dbg) {
+                                                            int64_t* __restrict__ lcol, unsigned int* __restrict__ dbg,
+                                                            DevCounters* __restrict__ ctr) {
     constexpr int GS = kWalkGroup;
+    unsigned long long my_words = 0, my_items = 0, my_wins = 0;
     const int lane = threadIdx.x & 63, gl = lane & (GS - 1), gsh = lane & ~(GS - 1);
     const uint64_t gmask = GS == 64 ? ~0ull : ((1ull << GS) - 1);
     const int L = ss.L;
@@ -526,6 +528,12 @@ __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64
             u0 += 64 * GS;
             reached = last >= stopu;
         }
+        my_words += (unsigned long long)steps * GS;
+        ++my_items;
+        int npres = 0;
+        #pragma unroll
+        for (int g = 0; g < MG; ++g) npres += (g < gt.G && A.s[g] != 0) ? 1 : 0;
+        my_wins += (unsigned long long)steps * GS * npres;
         if (gl == 0 && dbg) {   // development: walk length histogram (MUMS_DEV_CHAIN_DEBUG)
             atomicAdd(&dbg[0], steps > 1 ? 1u : 0u);
             atomicAdd(&dbg[1], steps > 16 ? 1u : 0u);
@@ -544,6 +552,11 @@ __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64
                 lcol[it.j] = xa + c;
             }
         }
+    }
+    if (ctr && gl == 0 && my_items) {   // words / walks of this group (the roofline's byte count)
+        atomicAdd(&ctr->walk_words, my_words);
+        atomicAdd(&ctr->walk_items, my_items);
+        atomicAdd(&ctr->walk_wins, my_wins);
     }
 }
 
@@ -617,7 +630,8 @@ size_t chain_tmp_bytes(uint64_t P, uint32_t Tb, int G) {
 template <int MG, typename View>
 hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const GenomeTable& gt, const MatchParams& mp,
                          const SeedSpec& ss, const uint32_t* packed, void* d_chain_tmp, void* d_scan_tmp,
-                         void* d_radix_tmp, uint32_t* chain_of, int64_t* pool, uint32_t* d_nchains, hipStream_t st) {
+                         void* d_radix_tmp, uint32_t* chain_of, int64_t* pool, uint32_t* d_nchains, hipStream_t st,
+                         void* ctr, hipEvent_t* ev_walk) {
     if (P == 0) return hipSuccess;
     char* p = (char*)d_chain_tmp;
     auto carve = [&](size_t bytes) {
@@ -662,8 +676,11 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
         if ((e = hipGetLastError()) != hipSuccess) return e;
         const bool cdbg = getenv("MUMS_DEV_CHAIN_DEBUG") != nullptr;
         if (cdbg && (e = hipMemsetAsync(qcount + 4, 0, 32, st)) != hipSuccess) return e;
+        if (ev_walk) (void)hipEventRecord(ev_walk[2 * pass], st);
         hipLaunchKernelGGL((chain_walk_kernel<MG, View>), dim3(walk_grid), dim3(kBlock), 0, st, vl, probe_info, gt, mp,
-                           ss, ord, packed, queue, qcount, link, rcol, lcol, cdbg ? qcount + 4 : nullptr);
+                           ss, ord, packed, queue, qcount, link, rcol, lcol, cdbg ? qcount + 4 : nullptr,
+                           (DevCounters*)ctr);
+        if (ev_walk) (void)hipEventRecord(ev_walk[2 * pass + 1], st);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (cdbg) {   // development: long-walk queue sizes and wave-step histogram
             unsigned hq[9] = {};
@@ -686,7 +703,7 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
 #define MUMS_INST_CHAINS(MG, V)                                                                                   \
     template hipError_t launch_chains<MG, V>(V, const uint64_t*, uint64_t, const GenomeTable&, const MatchParams&, \
                                              const SeedSpec&, const uint32_t*, void*, void*, void*, uint32_t*,     \
-                                             int64_t*, uint32_t*, hipStream_t);
+                                             int64_t*, uint32_t*, hipStream_t, void*, hipEvent_t*);
 MUMS_INST_CHAINS(4, MatProbes)
 MUMS_INST_CHAINS(8, MatProbes)
 MUMS_INST_CHAINS(16, MatProbes)

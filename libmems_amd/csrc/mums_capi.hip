@@ -93,7 +93,9 @@ struct mums_ctx {
     std::vector<uint64_t> offset_log;     // start points after every restart (R x G)
     hipEvent_t ev[EV_COUNT] = {};
     bool profiling = false;
+    bool walk_events = false;    // ev_walk recorded by the last FindMatches
     hipEvent_t ev_ds[16] = {};   // 2 per radix pass (<= 8 passes)
+    hipEvent_t ev_walk[4] = {};  // around the 2 chain_walk_kernel launches (chains.hip)
 
     // sharded seed stage: this context owns genomes [shard_first,
     // shard_first + genomes.size()) of a problem whose genome lengths are shard_len
@@ -228,7 +230,9 @@ int find_rows(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const MatchPar
         return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^30 seed probes in one FindMatches");
     HIPCHK((launch_chains<MG, MatProbes>(v, nullptr, P, ctx->gt, mp, ctx->ss, packed,
                                     ctx->chain_tmp.p, ctx->tmp.p, ctx->radix_tmp.p, ctx->chain_of.as<uint32_t>(),
-                                    ctx->pool.as<int64_t>(), &dc->nchains, st)));
+                                    ctx->pool.as<int64_t>(), &dc->nchains, st, dc,
+                                    ctx->profiling ? ctx->ev_walk : nullptr)));
+    ctx->walk_events = ctx->profiling;
     HIPCHK(hipEventRecord(ctx->ev[EV_CHAINS], st));
     HIPCHK(hipMemcpyAsync(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -529,6 +533,15 @@ void fill_stats(mums_ctx* ctx, uint64_t n) {
         s.chains = ctx->hc.nchains;
         s.ms_output = el(EV_REPLAY, EV_OUTPUT);
         s.ms_total = el(EV_START, EV_OUTPUT);
+        s.chain_walk_words = ctx->hc.walk_words;
+        s.chain_walks = ctx->hc.walk_items;
+        s.chain_walk_bytes = ctx->hc.walk_wins * 28 + ctx->hc.walk_items * (uint64_t)(8 * (ctx->gt.G + 1) + 24);
+        if (ctx->walk_events && ctx->P > 0)
+            for (int p = 0; p < 2; ++p) {
+                float ms = 0.f;
+                (void)hipEventElapsedTime(&ms, ctx->ev_walk[2 * p], ctx->ev_walk[2 * p + 1]);
+                s.ms_chain_walks += ms;
+            }
     } else {
         s.ms_total = el(EV_START, EV_BUCKETS);
     }
@@ -1052,6 +1065,7 @@ int mums_ctx_create(int device, mums_ctx** out) {
     if (e != hipSuccess) { delete ctx; return MUMS_E_HIP; }
     ctx->own_stream = true;
     for (int i = 0; i < EV_COUNT; ++i) (void)hipEventCreate(&ctx->ev[i]);
+    for (int i = 0; i < 4; ++i) (void)hipEventCreate(&ctx->ev_walk[i]);
     *out = ctx;
     return MUMS_OK;
 }
@@ -1066,12 +1080,15 @@ int mums_ctx_destroy(mums_ctx* ctx) {
                       &ctx->pbuf, &ctx->keybuf, &ctx->mstart, &ctx->chain_tmp, &ctx->chain_of,
                       &ctx->radix_tmp, &ctx->spill, &ctx->summ, &ctx->dbgbuf, &ctx->mprobe, &ctx->rowtmp,
                       &ctx->cval, &ctx->ctab, &ctx->smlk0, &ctx->smlkA, &ctx->smlkB, &ctx->smlvA,
-                      &ctx->smlvB, &ctx->smltmp, &ctx->flen, &ctx->fs, &ctx->rowsall};
+                      &ctx->smlvB, &ctx->smltmp, &ctx->flen, &ctx->fs, &ctx->rowsall, &ctx->rsbuf,
+                      &ctx->rsplan, &ctx->rsbst};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i < EV_COUNT; ++i)
         if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
     for (int i = 0; i < 16; ++i)
         if (ctx->ev_ds[i]) (void)hipEventDestroy(ctx->ev_ds[i]);
+    for (int i = 0; i < 4; ++i)
+        if (ctx->ev_walk[i]) (void)hipEventDestroy(ctx->ev_walk[i]);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return MUMS_OK;

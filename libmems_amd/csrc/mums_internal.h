@@ -86,6 +86,9 @@ struct DevCounters {
     uint32_t nchains;                 // seed chains among the probes (chains.hip)
     uint32_t max_bucket;              // probes in the fullest hash bucket
     uint32_t pad;
+    unsigned long long walk_words;    // 64-column hit words evaluated by chain_walk_kernel
+    unsigned long long walk_items;    // walks chain_walk_kernel finished
+    unsigned long long walk_wins;     // 28-B packed windows those words loaded (present components)
 };
 
 // A tile of the segmented (per-MSD-bucket) sort/group passes.  Tiles never
@@ -254,7 +257,8 @@ size_t chain_tmp_bytes(uint64_t P, uint32_t Tb, int G);
 template <int MG, typename View>
 hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const GenomeTable& gt, const MatchParams& mp,
                          const SeedSpec& ss, const uint32_t* packed, void* d_chain_tmp, void* d_scan_tmp,
-                         void* d_radix_tmp, uint32_t* chain_of, int64_t* pool, uint32_t* d_nchains, hipStream_t st);
+                         void* d_radix_tmp, uint32_t* chain_of, int64_t* pool, uint32_t* d_nchains, hipStream_t st,
+                         void* ctr = nullptr, hipEvent_t* ev_walk = nullptr);
 hipError_t launch_emit(const uint32_t* obase, const uint32_t* bstart, const uint32_t* tbl, const int64_t* pool, int G,
                        uint32_t table_size, uint64_t M, uint64_t* out_len, int64_t* out_s, hipStream_t st);
 
