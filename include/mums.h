@@ -182,6 +182,13 @@ int  mums_write_sml(mums_ctx* ctx, uint32_t genome, const char* path, const char
  * genome of the context; *seed_out = the file's seed pattern (may be NULL). */
 int  mums_add_genome_sml(mums_ctx* ctx, const char* path, uint64_t* seed_out);
 int  mums_length_filter(mums_ctx* ctx, uint64_t min_length);
+/* MemHash::SetMatchLog (MemHash.h:149): the reference writes every inserted entry to the
+ * log stream as it inserts it (MemHash.cpp:238-241: `len\ts0\t...` per line, the order of
+ * the AddHashEntry calls that inserted them).  Enable before mums_find; afterwards
+ * mums_match_log_copy returns those entries in that order (*count first: lengths / starts
+ * NULL); MemHash / MaskedMemHash / PairwiseMatchFinder paths, not ParallelMemHash compat. */
+int  mums_set_match_log(mums_ctx* ctx, int enable);
+int  mums_match_log_copy(mums_ctx* ctx, uint64_t* lengths, int64_t* starts, uint64_t capacity, uint64_t* count);
 /* EliminateOverlaps (libMems/Aligner.cpp:62-176, declared Aligner.h:239) on the context's
  * MatchList in place: per genome, std::sort by SingleStartComparator (AbstractMatch.h:324-351,
  * libstdc++ tie order reproduced), crop / delete the smaller of every overlapping pair,

@@ -88,11 +88,13 @@ public:
     virtual void FindMatches(MatchList& ml) {
         for (const auto& s : ml.seq_table) AddSequence(s);
         check(mums_find(ctx_));
+        write_match_log();
         GetMatchList(ml);
     }
     // MemHash::CreateMatches (MemHash.cpp:104-107)
     virtual bool CreateMatches() {
         check(mums_find(ctx_));
+        write_match_log();
         return true;
     }
     // MemHash::GetMatchList (MemHash.h:182-203): clears the list first
@@ -182,6 +184,12 @@ public:
     // the device copy of the last MatchList before GetMatchList
     void MultiplicityFilter(unsigned mult) { check(mums_multiplicity_filter(ctx_, mult)); }
     void LengthFilter(uint64_t length) { check(mums_length_filter(ctx_, length)); }
+    // MemHash::SetMatchLog (MemHash.h:149): every inserted entry of the next FindMatches is
+    // written to *log in insertion order (MemHash.cpp:238-241), one `len<TAB>starts` line each
+    void SetMatchLog(std::ostream* log) {
+        match_log_ = log;
+        check(mums_set_match_log(ctx_, log != nullptr));
+    }
     // EliminateOverlaps (Aligner.cpp:62-176) of the last MatchList, on the device
     void EliminateOverlaps() { check(mums_eliminate_overlaps(ctx_)); }
     // a caller's MatchList (M x G starts + lengths) as the current result, e.g. to run
@@ -205,6 +213,24 @@ protected:
         throw InvalidData(msg);
     }
     void push_params() { check(mums_set_params(ctx_, repeat_tol_, enum_tol_, table_size_)); }
+    void write_match_log() const {
+        if (!match_log_) return;
+        uint64_t n = 0;
+        uint32_t G = 0;
+        uint64_t count = 0;
+        check(mums_match_log_copy(ctx_, nullptr, nullptr, 0, &n));
+        check(mums_result_count(ctx_, &count, &G));
+        std::vector<uint64_t> len(n);
+        std::vector<int64_t> st(n * G);
+        if (n) check(mums_match_log_copy(ctx_, len.data(), st.data(), n, &n));
+        for (uint64_t i = 0; i < n; ++i) {
+            (*match_log_) << len[i];
+            for (uint32_t g = 0; g < G; ++g) (*match_log_) << '\t' << st[i * G + g];
+            (*match_log_) << '\n';
+        }
+        match_log_->flush();
+    }
+    std::ostream* match_log_ = nullptr;
     mums_ctx* ctx_ = nullptr;
     uint32_t repeat_tol_ = 0, enum_tol_ = 1, table_size_ = 40000;
 };

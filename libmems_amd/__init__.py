@@ -99,6 +99,7 @@ EXPORTED_SYMBOLS = [
     "mums_get_offset_log", "mums_copy_seed_keys_range", "mums_mem_table_count", "mums_eliminate_overlaps",
     "mums_load_matches", "mums_debug_std_sort", "mums_comm_unique_id", "mums_comm_init_rank", "mums_comm_init_all",
     "mums_comm_init_local", "mums_comm_destroy", "mums_comm_last_error", "mums_shard_key_ranges", "mums_shard_run",
+    "mums_set_match_log", "mums_match_log_copy",
 ]
 
 _lib: Optional[ctypes.CDLL] = None
@@ -180,6 +181,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mums_comm_last_error.restype = ctypes.c_char_p
     lib.mums_shard_key_ranges.argtypes = [vp, u32, u32, vp, vp]
     lib.mums_shard_run.argtypes = [vp, vp, ctypes.c_int]
+    lib.mums_set_match_log.argtypes = [vp, i32]
+    lib.mums_match_log_copy.argtypes = [vp, vp, vp, u64, ctypes.POINTER(u64)]
     _lib = lib
     return lib
 
@@ -458,6 +461,24 @@ class MemHash:
 
     def LengthFilter(self, length: int) -> None:
         self._check(self._lib.mums_length_filter(self._ctx, length))
+
+    def SetMatchLog(self, enable: bool = True) -> None:
+        """MemHash::SetMatchLog (MemHash.h:149): record every inserted entry of the next FindMatches."""
+        self._check(self._lib.mums_set_match_log(self._ctx, int(bool(enable))))
+
+    def MatchLog(self) -> "MatchList":
+        """The entries the match log stream received (MemHash.cpp:238-241), in insertion order."""
+        n = ctypes.c_uint64()
+        self._check(self._lib.mums_match_log_copy(self._ctx, None, None, 0, ctypes.byref(n)))
+        g = ctypes.c_uint32()
+        cnt = ctypes.c_uint64()
+        self._check(self._lib.mums_result_count(self._ctx, ctypes.byref(cnt), ctypes.byref(g)))
+        lengths = np.zeros(n.value, dtype=np.uint64)
+        starts = np.zeros((n.value, g.value), dtype=np.int64)
+        if n.value:
+            self._check(self._lib.mums_match_log_copy(self._ctx, lengths.ctypes.data, starts.ctypes.data, n.value,
+                                                      ctypes.byref(n)))
+        return MatchList(lengths, starts)
 
     def EliminateOverlaps(self) -> None:
         """EliminateOverlaps (Aligner.cpp:62-176) of the current MatchList, on the GPU."""

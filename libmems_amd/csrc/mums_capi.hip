@@ -86,6 +86,9 @@ struct mums_ctx {
     DevBuf smlk0, smlkA, smlkB, smlvA, smlvB, smltmp, flen, fs;
     DevBuf rowsall;          // chunked mode: probe rows of all chunks
     EoWork eo;               // EliminateOverlaps work arrays (overlaps.hip)
+    bool match_log = false;  // MemHash::SetMatchLog: record the inserts (replay.hip)
+    uint64_t log_n = 0;
+    DevBuf logA, logB, logvA, logvB;
     // MER_REPEAT_LIMIT restart / FindMatchesFromPosition (restart.hip)
     std::vector<uint64_t> start_points;   // per genome SML start index (empty = all 0)
     DevBuf rsbuf, rsplan, rsbst;
@@ -242,13 +245,35 @@ int find_rows(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const MatchPar
         HIPCHK(hipMemsetAsync(ctx->dbgbuf.p, 0, (size_t)ctx->table_size * 64, st));
         dbg = ctx->dbgbuf.as<uint64_t>();
     }
+    uint64_t* mlog = nullptr;
+    ctx->log_n = 0;
+    if (ctx->match_log && !ctx->pcompat) {
+        HIPCHK(ctx->logA.ensure((P + 1) * 8));
+        HIPCHK(ctx->logB.ensure((P + 1) * 8));
+        mlog = ctx->logB.as<uint64_t>();   // unsorted events; sorted into logA
+    }
     // the fullest bucket's vector in LDS when it fits (it holds <= its probes)
     const uint32_t lds_cap = std::max<uint32_t>(64, std::min<uint32_t>(ctx->hc.max_bucket, kReplayLdsIds));
     HIPCHK((launch_replay<MG, MatProbes>(v, ctx->gt, mp, ctx->L, nullptr, ctx->sorted_ids, P,
                                     ctx->bstart.as<uint32_t>(), ctx->bend.as<uint32_t>(), ctx->tbl.as<uint32_t>(),
                                     ctx->spill.p, ctx->summ.p, ctx->pool.as<int64_t>(), ctx->chain_of.as<uint32_t>(),
                                     ctx->hc.nchains, ctx->chain_tmp.p, ctx->radix_tmp.p, lds_cap,
-                                    ctx->tsize.as<uint32_t>(), ctx->counters.p, dbg, st)));
+                                    ctx->tsize.as<uint32_t>(), ctx->counters.p, dbg, st,
+                                    mlog)));
+    if (mlog) {   // the inserts in AddHashEntry call order (probe index << 32 | chain)
+        HIPCHK(hipMemcpyAsync(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        const uint64_t n = ctx->hc.log_n;
+        HIPCHK(ctx->logB.ensure((n + 1) * 8));
+        HIPCHK(ctx->logvA.ensure((n + 1) * 4));
+        HIPCHK(ctx->logvB.ensure((n + 1) * 4));
+        int buf = 0;
+        if (n) HIPCHK(radix_sort<uint64_t>(mlog, nullptr, n, 64, ctx->logA.as<uint64_t>(), ctx->logvA.as<uint32_t>(),
+                                           ctx->logB.as<uint64_t>(), ctx->logvB.as<uint32_t>(), ctx->radix_tmp.p, &buf,
+                                           st));
+        if (buf) std::swap(ctx->logA, ctx->logB);   // sorted events in logA
+        ctx->log_n = n;
+    }
     if (dbg) {   // development instrumentation: the slowest buckets of the replay
         std::vector<uint64_t> h((size_t)ctx->table_size * 8);
         HIPCHK(hipMemcpyAsync(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost, st));
@@ -1513,6 +1538,37 @@ int mums::ctx_table_genomes(mums_ctx* ctx, uint32_t* table_size, uint32_t* genom
     *genomes = (uint32_t)ctx->gt.G;
     return MUMS_OK;
 }
+}
+
+// MemHash::SetMatchLog (MemHash.h:149; written at MemHash.cpp:238-241)
+int mums_set_match_log(mums_ctx* ctx, int enable) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    ctx->match_log = enable != 0;
+    return MUMS_OK;
+}
+
+int mums_match_log_copy(mums_ctx* ctx, uint64_t* lengths, int64_t* starts, uint64_t capacity, uint64_t* count) {
+    if (check_ctx(ctx) || !count) return MUMS_E_INVALID;
+    if (ctx->stage_done < MUMS_STAGE_ALL) return fail(ctx, MUMS_E_INVALID, "no completed FindMatches on this context");
+    if (!ctx->match_log || ctx->pcompat)
+        return fail(ctx, MUMS_E_INVALID, "the match log was not enabled for this FindMatches (mums_set_match_log)");
+    *count = ctx->log_n;
+    if (!lengths && !starts) return MUMS_OK;
+    if (capacity < ctx->log_n) return fail(ctx, MUMS_E_INVALID, "match log capacity too small");
+    if (ctx->log_n == 0) return MUMS_OK;
+    HIPCHK(hipSetDevice(ctx->device));
+    const int G = ctx->gt.G;
+    std::vector<uint64_t> ev(ctx->log_n);
+    HIPCHK(hipMemcpy(ev.data(), ctx->logA.p, ctx->log_n * 8, hipMemcpyDeviceToHost));
+    std::vector<int64_t> e(G + 2);
+    for (uint64_t i = 0; i < ctx->log_n; ++i) {   // pool entry of the inserted chain
+        const uint64_t cid = ev[i] & 0xFFFFFFFFull;
+        HIPCHK(hipMemcpy(e.data(), ctx->pool.as<int64_t>() + cid * (uint64_t)(G + 2), (G + 2) * 8,
+                         hipMemcpyDeviceToHost));
+        if (lengths) lengths[i] = (uint64_t)e[0];
+        if (starts) std::copy(e.begin() + 2, e.end(), starts + i * (uint64_t)G);
+    }
+    return MUMS_OK;
 }
 
 // EliminateOverlaps (Aligner.cpp:62-176) on the context's MatchList, in place

@@ -89,6 +89,7 @@ struct DevCounters {
     unsigned long long walk_words;    // 64-column hit words evaluated by chain_walk_kernel
     unsigned long long walk_items;    // walks chain_walk_kernel finished
     unsigned long long walk_wins;     // 28-B packed windows those words loaded (present components)
+    unsigned long long log_n;         // insertion events recorded for SetMatchLog (replay.hip)
 };
 
 // A tile of the segmented (per-MSD-bucket) sort/group passes.  Tiles never
@@ -220,7 +221,7 @@ hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, i
                          const uint32_t* sorted_ids, uint64_t P, const uint32_t* bstart, const uint32_t* bend,
                          uint32_t* tbl, void* spill, void* summ, const int64_t* pool, const uint32_t* chain_of,
                          uint32_t nch, void* d_tmp, void* d_radix_tmp, uint32_t lds_cap, uint32_t* tsize, void* ctr,
-                         uint64_t* dbg, hipStream_t st);
+                         uint64_t* dbg, hipStream_t st, uint64_t* mlog = nullptr);
 // chains.hip: chain labelling of the probes (key order) before the replay
 // context accessors for the multi-GPU orchestration (shard_comm.hip; mums_capi.hip)
 }  // namespace mums

@@ -32,6 +32,12 @@ namespace mums {
 
 namespace {
 
+// MemHash::SetMatchLog (MemHash.h:149, written at MemHash.cpp:238-241): every insert, as
+// (AddHashEntry call = probe index in key order, chain), sorted by the call afterwards
+__device__ __forceinline__ void log_insert(uint64_t* mlog, DevCounters* ctr, uint32_t probe, uint32_t cid) {
+    if (mlog) mlog[atomicAdd(&ctr->log_n, 1ull)] = ((uint64_t)probe << 32) | cid;
+}
+
 template <int RB>
 __device__ __forceinline__ int block_first_true(bool pred, int* red) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -332,7 +338,8 @@ __global__ __launch_bounds__(RB) void replay_kernel(
     const uint4* __restrict__ summ, const uint4* __restrict__ summ_b, const uint32_t* __restrict__ bstart,
     const uint32_t* __restrict__ bend, const uint32_t* __restrict__ obase,
     uint32_t* __restrict__ tbl, uint4* __restrict__ spill, const int64_t* __restrict__ pool, uint32_t lds_cap,
-    uint32_t* __restrict__ tsize, DevCounters* ctr, uint64_t* __restrict__ dbg, uint32_t kmin, uint32_t kmax) {
+    uint32_t* __restrict__ tsize, DevCounters* ctr, uint64_t* __restrict__ dbg, uint32_t kmin, uint32_t kmax,
+    uint64_t* __restrict__ mlog) {
     extern __shared__ uint4 s_tab[];
     __shared__ int red[RB / 64];
     __shared__ uint32_t s_ins, s_rank;
@@ -372,8 +379,10 @@ __global__ __launch_bounds__(RB) void replay_kernel(
         __syncthreads();
         if (s_ok && s_rmax - s_rmin + 1u == K_b) {
             const uint32_t r0 = s_rmin;
-            for (uint32_t k = tid; k < K_b; k += RB)
+            for (uint32_t k = tid; k < K_b; k += RB) {
                 tbl[ob + ((summ_b[beg + k].z & 0x7FFFFFFFu) - r0)] = summ[beg + k].z;
+                log_insert(mlog, ctr, summ[beg + k].w & 0x3FFFFFFFu, summ[beg + k].z);
+            }
             if (tid == 0) {
                 tsize[b] = K_b;
                 atomicAdd(&ctr->entries, (unsigned long long)K_b);
@@ -423,6 +432,7 @@ __global__ __launch_bounds__(RB) void replay_kernel(
                                    : insert_pos<MG>(spill + ob, t, me.z, me.x, (int64_t)mb.x, (int64_t)mb.y, pool, G);
                 s_rank = mb.z & 0x7FFFFFFFu;
                 s_new = make_uint4(me.z, me.x, mb.x, mb.y);
+                log_insert(mlog, ctr, me.w & 0x3FFFFFFFu, me.z);
             }
             if (in_lds && t + 1 > lds_cap) {   // spill the vector to the bucket's global slice
                 for (uint32_t k = tid; k < t; k += RB) spill[ob + k] = s_tab[k];
@@ -540,7 +550,8 @@ __global__ __launch_bounds__(kBigRB) void replay_big_kernel(
     const uint4* __restrict__ summ, const uint4* __restrict__ summ_b, const uint32_t* __restrict__ cbeg,
     uint32_t* __restrict__ cend, const uint32_t* __restrict__ obase, uint32_t* __restrict__ tbl,
     const int64_t* __restrict__ pool, const uint4* __restrict__ chain_sb, uint32_t* __restrict__ scr_cnt,
-    uint32_t* __restrict__ scr_e, uint4* __restrict__ scr_slot, uint32_t* __restrict__ tsize, DevCounters* ctr, uint32_t big_min) {
+    uint32_t* __restrict__ scr_e, uint4* __restrict__ scr_slot, uint32_t* __restrict__ tsize, DevCounters* ctr, uint32_t big_min,
+    uint64_t* __restrict__ mlog) {
     __shared__ uint32_t slow[kBigSlow], slow_sorted[kBigSlow];
     __shared__ uint32_t red[kBigRB / 64];
     __shared__ uint32_t s_ns, s_bad, s_rmin, s_rmax;
@@ -594,7 +605,10 @@ __global__ __launch_bounds__(kBigRB) void replay_big_kernel(
         const uint32_t j = si < S ? slow_sorted[si] : K;
         for (uint32_t k = k0 + tid; k < j; k += kBigRB) {   // chain-first run: one copy each
             const uint4 a = summ[beg + k];
-            if (a.w & 0x80000000u) cnt[(summ_b[beg + k].z) - r0] = 1u;
+            if (a.w & 0x80000000u) {
+                cnt[(summ_b[beg + k].z) - r0] = 1u;
+                log_insert(mlog, ctr, a.w & 0x3FFFFFFFu, a.z);
+            }
         }
         __syncthreads();
         if (j == K) break;
@@ -647,8 +661,12 @@ __global__ __launch_bounds__(kBigRB) void replay_big_kernel(
                 const uint32_t rr = mb.z - r0;
                 const uint32_t rl = ins > 0 ? chain_sb[at(ins - 1).x].z - r0 : 0u;
                 const uint32_t rh = ins < t ? chain_sb[at(ins).x].z - r0 : 0xFFFFFFFFu;
-                if (rr < R && rl <= rr && rr <= rh) cnt[rr] += 1u;
-                else s_bad = 2;
+                if (rr < R && rl <= rr && rr <= rh) {
+                    cnt[rr] += 1u;
+                    log_insert(mlog, ctr, me.w & 0x3FFFFFFFu, pcid);
+                } else {
+                    s_bad = 2;
+                }
             }
         }
         __syncthreads();
@@ -733,10 +751,15 @@ __global__ __launch_bounds__(kBlock) void bigg_slots_kernel(const uint4* __restr
 // chain-first probes [k0, k1) of the bucket: one copy of their chain each
 __global__ __launch_bounds__(kBlock) void bigg_fill_kernel(const uint4* __restrict__ summ,
                                                            const uint4* __restrict__ summ_b, uint32_t beg, uint32_t k0,
-                                                           uint32_t k1, uint32_t r0, uint32_t* __restrict__ cnt) {
+                                                           uint32_t k1, uint32_t r0, uint32_t* __restrict__ cnt,
+                                                           uint64_t* __restrict__ mlog, DevCounters* ctr) {
     const uint32_t k = k0 + blockIdx.x * kBlock + threadIdx.x;
     if (k >= k1) return;
-    if (summ[beg + k].w & 0x80000000u) cnt[summ_b[beg + k].z - r0] = 1u;
+    const uint4 a = summ[beg + k];
+    if (a.w & 0x80000000u) {
+        cnt[summ_b[beg + k].z - r0] = 1u;
+        log_insert(mlog, ctr, a.w & 0x3FFFFFFFu, a.z);
+    }
 }
 
 // suspicious probe j against the virtual vector V[i] = sbr[r], E[r] <= i < E[r + 1]
@@ -746,7 +769,7 @@ __global__ void bigg_slow_kernel(View v, GenomeTable gt, MatchParams mp, int L, 
                                  uint32_t j, uint32_t r0, uint32_t R, const uint32_t* __restrict__ E,
                                  const uint4* __restrict__ sbr, const uint4* __restrict__ chain_sb,
                                  const int64_t* __restrict__ pool, uint32_t* __restrict__ cnt,
-                                 uint32_t* __restrict__ info) {
+                                 uint32_t* __restrict__ info, uint64_t* __restrict__ mlog, DevCounters* ctr) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     const int G = gt.G;
     const uint32_t t = E[R];
@@ -798,8 +821,12 @@ __global__ void bigg_slow_kernel(View v, GenomeTable gt, MatchParams mp, int L, 
     const uint32_t rr = mb.z - r0;
     const uint32_t rl = ins > 0 ? chain_sb[at(ins - 1).x].z - r0 : 0u;
     const uint32_t rh = ins < t ? chain_sb[at(ins).x].z - r0 : 0xFFFFFFFFu;
-    if (rr < R && rl <= rr && rr <= rh) cnt[rr] += 1u;
-    else info[4] = 1u;
+    if (rr < R && rl <= rr && rr <= rh) {
+        cnt[rr] += 1u;
+        log_insert(mlog, ctr, me.w & 0x3FFFFFFFu, pcid);
+    } else {
+        info[4] = 1u;
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void bigg_out_kernel(const uint32_t* __restrict__ E, uint32_t R,
@@ -919,7 +946,7 @@ hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, i
                          const uint32_t* sorted_ids, uint64_t P, const uint32_t* bstart, const uint32_t* bend,
                          uint32_t* tbl, void* spill, void* summ, const int64_t* pool, const uint32_t* chain_of,
                          uint32_t nch, void* d_tmp, void* d_radix_tmp, uint32_t lds_cap, uint32_t* tsize, void* ctr,
-                         uint64_t* dbg, hipStream_t st) {
+                         uint64_t* dbg, hipStream_t st, uint64_t* mlog) {
     char* p = (char*)d_tmp;
     auto carve = [&](size_t bytes) {
         char* r = p;
@@ -1056,12 +1083,14 @@ hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, i
                 const uint32_t j = si < S ? hs[si] : K;
                 if (j > k0)
                     hipLaunchKernelGGL(bigg_fill_kernel, dim3((j - k0 + kBlock - 1) / kBlock), dim3(kBlock), 0, st,
-                                       (const uint4*)summ_c, (const uint4*)summ_bc, beg, k0, j, r0, cnt);
+                                       (const uint4*)summ_c, (const uint4*)summ_bc, beg, k0, j, r0, cnt, mlog,
+                                       (DevCounters*)ctr);
                 if (j == K) break;
                 if ((e = scan()) != hipSuccess) return e;
                 hipLaunchKernelGGL((bigg_slow_kernel<MG, View>), dim3(1), dim3(64), 0, st, v, gt, mp, L, probe_info,
                                    (const uint4*)summ_c, (const uint4*)summ_bc, beg, j, r0, R, (const uint32_t*)E,
-                                   (const uint4*)sbr, (const uint4*)chain_sb, pool, cnt, ginfo);
+                                   (const uint4*)sbr, (const uint4*)chain_sb, pool, cnt, ginfo, mlog,
+                                   (DevCounters*)ctr);
                 k0 = j + 1;
             }
             if ((e = scan()) != hipSuccess) return e;
@@ -1073,14 +1102,14 @@ hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, i
         }
         hipLaunchKernelGGL((replay_big_kernel<MG, View>), dim3(mp.table_size), dim3(kBigRB), 0, st, v, gt, mp, L,
                            probe_info, (const uint4*)summ_c, (const uint4*)summ_bc, cbeg, cend, bstart, tbl, pool,
-                           (const uint4*)chain_sb, scr_cnt, scr_e, scr_slot, tsize, (DevCounters*)ctr, big_min);
+                           (const uint4*)chain_sb, scr_cnt, scr_e, scr_slot, tsize, (DevCounters*)ctr, big_min, mlog);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     // buckets of <= 64 probes: one wave each; the rest: one big workgroup each
     constexpr uint32_t kSmall = 64;
     hipLaunchKernelGGL((replay_kernel<MG, 64, View>), dim3(mp.table_size), dim3(64), kSmall * sizeof(uint4), st, v, gt,
                        mp, L, probe_info, (const uint4*)summ_c, (const uint4*)summ_bc, cbeg, cend, bstart, tbl,
-                       (uint4*)spill, pool, kSmall, tsize, (DevCounters*)ctr, dbg, 0u, kSmall);
+                       (uint4*)spill, pool, kSmall, tsize, (DevCounters*)ctr, dbg, 0u, kSmall, mlog);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (lds_cap <= kSmall) return hipSuccess;   // lds_cap = min(fullest bucket, LDS slots)
     constexpr int RB = replay_block<MG>();
@@ -1090,7 +1119,7 @@ hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, i
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((replay_kernel<MG, RB, View>), dim3(mp.table_size), dim3(RB), lds, st, v, gt, mp, L, probe_info,
                        (const uint4*)summ_c, (const uint4*)summ_bc, cbeg, cend, bstart, tbl, (uint4*)spill, pool,
-                       lds_cap, tsize, (DevCounters*)ctr, dbg, kSmall, 0xFFFFFFFFu);
+                       lds_cap, tsize, (DevCounters*)ctr, dbg, kSmall, 0xFFFFFFFFu, mlog);
     return hipGetLastError();
 }
 
@@ -1106,7 +1135,8 @@ hipError_t launch_emit(const uint32_t* obase, const uint32_t* bstart, const uint
     template hipError_t launch_replay<MG, V>(V, const GenomeTable&, const MatchParams&, int, const uint64_t*,      \
                                              const uint32_t*, uint64_t, const uint32_t*, const uint32_t*,          \
                                              uint32_t*, void*, void*, const int64_t*, const uint32_t*, uint32_t,   \
-                                             void*, void*, uint32_t, uint32_t*, void*, uint64_t*, hipStream_t);
+                                             void*, void*, uint32_t, uint32_t*, void*, uint64_t*, hipStream_t,    \
+                                             uint64_t*);
 MUMS_INST_REPLAY(4, MatProbes)
 MUMS_INST_REPLAY(8, MatProbes)
 MUMS_INST_REPLAY(16, MatProbes)

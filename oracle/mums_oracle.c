@@ -453,6 +453,8 @@ struct oracle_result {
     uint64_t mem_count, collision_count, max_group, probes, seedmers, chunks, restarts;
     uint64_t* offlog;         /* start points after every restart (SetOffsetLog, MatchFinder.cpp:152-162) */
     int offlog_g;
+    uint64_t* mlog_len;       /* SetMatchLog (MemHash.cpp:238-241): inserted entries in insertion order */
+    int64_t* mlog_s;
     uint32_t* plog_bucket;    /* seeds_only: per AddHashEntry call, its bucket ... */
     uint64_t* plog_ref;       /* ... and the global seed-mer index of the probe's first start */
 };
@@ -1000,6 +1002,14 @@ oracle_result* oracle_find_matches(int G, const char* const* seqs, const uint64_
         res->mem_count = h.mem_count;
         res->collision_count = h.collisions;
         res->probes = h.probes;
+        if (!prm->parallel_compat && h.pool_n == h.mem_count) {   /* pool ids = insertion order */
+            res->mlog_len = (uint64_t*)malloc((h.pool_n ? h.pool_n : 1) * sizeof(uint64_t));
+            res->mlog_s = (int64_t*)malloc((h.pool_n ? h.pool_n : 1) * (size_t)G * sizeof(int64_t));
+            for (uint64_t k = 0; k < h.pool_n; ++k) {
+                res->mlog_len[k] = (uint64_t)h.pool[k].len;
+                memcpy(res->mlog_s + k * (uint64_t)G, h.pool[k].s, (size_t)G * sizeof(int64_t));
+            }
+        }
         free(h.buckets); free(h.pool); free(h.spool); free(gbase); free(h.cm); free(h.hl);
         res->plog_bucket = h.plog_bucket;
         res->plog_ref = h.plog_ref;
@@ -1318,6 +1328,13 @@ uint64_t oracle_result_seedmers(const oracle_result* r) { return r ? r->seedmers
 uint64_t oracle_result_chunks(const oracle_result* r) { return r ? r->chunks : 0; }
 uint64_t oracle_result_restarts(const oracle_result* r) { return r ? r->restarts : 0; }
 /* rows = restarts, G entries each; returns 0 */
+int oracle_result_match_log(const oracle_result* r, uint64_t* lengths, int64_t* starts) {
+    if (!r->mlog_len) return -1;
+    if (lengths) memcpy(lengths, r->mlog_len, r->mem_count * sizeof(uint64_t));
+    if (starts) memcpy(starts, r->mlog_s, r->mem_count * (size_t)r->G * sizeof(int64_t));
+    return 0;
+}
+
 int oracle_result_offset_log(const oracle_result* r, uint64_t* out) {
     if (!r) return -1;
     if (r->offlog && r->restarts) memcpy(out, r->offlog, (size_t)r->restarts * (size_t)r->offlog_g * sizeof(uint64_t));
@@ -1325,7 +1342,8 @@ int oracle_result_offset_log(const oracle_result* r, uint64_t* out) {
 }
 void     oracle_result_free(oracle_result* r) {
     if (!r) return;
-    free(r->lengths); free(r->starts); free(r->plog_bucket); free(r->plog_ref); free(r->offlog); free(r);
+    free(r->lengths); free(r->starts); free(r->plog_bucket); free(r->plog_ref); free(r->offlog);
+    free(r->mlog_len); free(r->mlog_s); free(r);
 }
 
 /* ------------------------------------------------------------------------- */

@@ -168,6 +168,11 @@ def find_matches(seqs: Sequence[bytes], seed: int, repeat_tol: int = 0, enum_tol
         if stats["restarts"] and not parallel_compat:
             L.oracle_result_offset_log(r, offlog.ctypes.data)
         stats["offset_log"] = offlog
+        L.oracle_result_match_log.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        ml_len = np.zeros(int(stats["mem_count"]), dtype=np.uint64)
+        ml_s = np.zeros((int(stats["mem_count"]), G), dtype=np.int64)
+        if L.oracle_result_match_log(r, ml_len.ctypes.data, ml_s.ctypes.data) == 0:
+            stats["match_log"] = (ml_len, ml_s)   # SetMatchLog: inserted entries in insertion order
     finally:
         L.oracle_result_free(r)
     return lengths, starts, stats
