@@ -615,6 +615,123 @@ __global__ __launch_bounds__(kBlock) void chain_entry_kernel(View v, const uint6
 
 inline unsigned grid_of(uint64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
+// --- chunked FindMatches: chains labelled per slice of the probes ---------------------
+// launch_chains on a slice of the probes gives every probe its true chain entry (walks
+// read the genomes, not the other probes), but a chain whose probes fall into several
+// slices gets one entry per slice.  The replay needs one id per chain (its chain-first
+// probe, its rank among the bucket's chains), so the per-slice entries are merged by
+// content: hash sort, then the first equal entry of each equal-hash run is the chain.
+
+__global__ __launch_bounds__(kBlock) void add_offset_kernel(uint32_t* __restrict__ a, uint64_t n, uint32_t off) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) a[i] += off;
+}
+
+__global__ __launch_bounds__(kBlock) void entry_hash_kernel(const int64_t* __restrict__ pool, uint64_t n, int G,
+                                                            uint64_t* __restrict__ key) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const int64_t* e = pool + i * (uint64_t)(G + 2);
+    uint64_t h = 0x243f6a8885a308d3ull;
+    for (int g = 0; g < G + 2; ++g) h = mix64(h ^ (uint64_t)e[g] ^ ((uint64_t)g << 58));
+    key[i] = h;
+}
+
+__device__ __forceinline__ bool same_entry(const int64_t* __restrict__ a, const int64_t* __restrict__ b, int W) {
+    for (int g = 0; g < W; ++g)
+        if (a[g] != b[g]) return false;
+    return true;
+}
+
+// sorted position i: rep[i] = first position of its equal-hash run holding an equal
+// entry (i itself when none), isrep[i] = rep[i] == i
+__global__ __launch_bounds__(kBlock) void entry_rep_kernel(const int64_t* __restrict__ pool, const uint64_t* __restrict__ key,
+                                                           const uint32_t* __restrict__ ord, uint64_t n, int G,
+                                                           uint32_t* __restrict__ rep, uint32_t* __restrict__ isrep) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t c = ord[i];
+    const uint64_t h = key[c];
+    const int W = G + 2;
+    const int64_t* ec = pool + (uint64_t)c * W;
+    uint64_t r0 = i;
+    while (r0 > 0 && key[ord[r0 - 1]] == h) --r0;
+    uint64_t r = i;
+    for (uint64_t j = r0; j < i; ++j)
+        if (same_entry(pool + (uint64_t)ord[j] * W, ec, W)) { r = j; break; }
+    rep[i] = (uint32_t)r;
+    isrep[i] = r == i ? 1u : 0u;
+}
+
+// gmap[local chain] = merged chain id; the merged pool holds each chain's entry once
+__global__ __launch_bounds__(kBlock) void entry_map_kernel(const int64_t* __restrict__ pool, const uint32_t* __restrict__ ord,
+                                                           const uint32_t* __restrict__ rep, const uint32_t* __restrict__ gid,
+                                                           uint64_t n, int G, uint32_t* __restrict__ gmap,
+                                                           int64_t* __restrict__ pool_out) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t c = ord[i], r = rep[i], g = gid[r];
+    gmap[c] = g;
+    if (r == (uint32_t)i) {
+        const int W = G + 2;
+        for (int w = 0; w < W; ++w) pool_out[(uint64_t)g * W + w] = pool[(uint64_t)c * W + w];
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void chain_remap_kernel(uint32_t* __restrict__ chain_of, uint64_t P,
+                                                             const uint32_t* __restrict__ gmap) {
+    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k < P) chain_of[k] = gmap[chain_of[k]];
+}
+
+}  // namespace
+
+hipError_t launch_add_offset(uint32_t* a, uint64_t n, uint32_t off, hipStream_t st) {
+    if (n == 0 || off == 0) return hipSuccess;
+    hipLaunchKernelGGL(add_offset_kernel, dim3(grid_of(n)), dim3(kBlock), 0, st, a, n, off);
+    return hipGetLastError();
+}
+
+size_t chain_merge_tmp_bytes(uint64_t n) { return (n + 64) * (8 * 3 + 4 * 5) + 8 * 256; }
+
+hipError_t launch_chain_merge(const int64_t* pool_loc, uint64_t n, int G, uint32_t* chain_of, uint64_t P,
+                              int64_t* pool_out, void* d_tmp, void* d_radix_tmp, void* d_scan_tmp, uint32_t* d_nchains,
+                              hipStream_t st) {
+    if (n == 0) return hipMemsetAsync(d_nchains, 0, 4, st);
+    char* p = (char*)d_tmp;
+    auto carve = [&](size_t bytes) {
+        char* r = p;
+        p += (bytes + 255) & ~(size_t)255;
+        return (void*)r;
+    };
+    uint64_t* key = (uint64_t*)carve(n * 8);
+    uint64_t* kA = (uint64_t*)carve(n * 8);
+    uint64_t* kB = (uint64_t*)carve(n * 8);
+    uint32_t* vA = (uint32_t*)carve(n * 4);
+    uint32_t* vB = (uint32_t*)carve(n * 4);
+    uint32_t* rep = (uint32_t*)carve(n * 4);
+    uint32_t* gid = (uint32_t*)carve(n * 4);
+    uint32_t* gmap = (uint32_t*)carve(n * 4);
+    const unsigned grid = grid_of(n);
+    hipLaunchKernelGGL(entry_hash_kernel, dim3(grid), dim3(kBlock), 0, st, pool_loc, n, G, key);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    int buf = 0;
+    if ((e = radix_sort<uint64_t>(key, nullptr, n, 64, kA, vA, kB, vB, d_radix_tmp, &buf, st)) != hipSuccess) return e;
+    const uint32_t* ord = buf ? vB : vA;
+    hipLaunchKernelGGL(entry_rep_kernel, dim3(grid), dim3(kBlock), 0, st, pool_loc, (const uint64_t*)key, ord, n, G, rep,
+                       gid);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = exclusive_scan_u32(gid, n, d_scan_tmp, d_nchains, st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(entry_map_kernel, dim3(grid), dim3(kBlock), 0, st, pool_loc, ord, (const uint32_t*)rep,
+                       (const uint32_t*)gid, n, G, gmap, pool_out);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(chain_remap_kernel, dim3(grid_of(P)), dim3(kBlock), 0, st, chain_of, P, (const uint32_t*)gmap);
+    return hipGetLastError();
+}
+
+namespace {
+
 }  // namespace
 
 size_t chain_tmp_bytes(uint64_t P, uint32_t Tb, int G) {

@@ -85,6 +85,10 @@ struct mums_ctx {
     // one genome's SML / seed frequencies (sml_tools.hip) and filtered MatchLists
     DevBuf smlk0, smlkA, smlkB, smlvA, smlvB, smltmp, flen, fs;
     DevBuf rowsall;          // chunked mode: probe rows of all chunks
+    DevBuf pool_loc, cbuf;   // chunked FindMatches: per-slice chain entries, compacted probes
+    DevBuf sids;             // chunked FindMatches: the bucket order (its sort scratch released)
+    uint32_t* emit_tbl = nullptr;          // bucket vectors / slice bases of the last replay
+    const uint32_t* emit_base = nullptr;   // (chunked: compacted, in cbuf; else tbl / bstart)
     EoWork eo;               // EliminateOverlaps work arrays (overlaps.hip)
     bool match_log = false;  // MemHash::SetMatchLog: record the inserts (replay.hip)
     uint64_t log_n = 0;
@@ -229,8 +233,6 @@ template <int MG>
 int find_rows(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const MatchParams& mp, hipStream_t st) {
     DevCounters* dc = ctx->counters.as<DevCounters>();
     const uint64_t P = ctx->P;
-    if (P >= (1ull << 30))   // probe ids share a word with two replay flags (replay.hip)
-        return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^30 seed probes in one FindMatches");
     HIPCHK((launch_chains<MG, MatProbes>(v, nullptr, P, ctx->gt, mp, ctx->ss, packed,
                                     ctx->chain_tmp.p, ctx->tmp.p, ctx->radix_tmp.p, ctx->chain_of.as<uint32_t>(),
                                     ctx->pool.as<int64_t>(), &dc->nchains, st, dc,
@@ -291,8 +293,105 @@ int find_rows(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const MatchPar
     return MUMS_OK;
 }
 
+// FindMatches above find_chunk() probes (BASELINE config 5: 2.5e9): chains labelled per
+// slice of find_chunk() probes (key order) into per-slice entries, merged by content
+// (chains.hip), then the replay in chunks of the bucket order (launch_replay_chunked).
+// Per-probe memory: rows, chain_of, tbl, spill, the bucket order and one keep flag.
+uint64_t find_chunk() {
+    uint64_t c = 1ull << 28;
+    if (const char* e = getenv("MUMS_DEV_FIND_CHUNK")) c = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
+    return c;
+}
+
+void* devbuf_alloc(void* b, size_t bytes) {
+    DevBuf* d = (DevBuf*)b;
+    return d->ensure(bytes) == hipSuccess ? d->p : nullptr;
+}
+
+template <int MG>
+int find_rows_chunked(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const MatchParams& mp, hipStream_t st) {
+    DevCounters* dc = ctx->counters.as<DevCounters>();
+    const uint64_t P = ctx->P, C = find_chunk();
+    const int G = ctx->gt.G;
+    const size_t W = (size_t)(G + 2) * 8;
+    uint32_t* chain_of = ctx->chain_of.as<uint32_t>();
+    uint64_t nloc = 0;
+    for (uint64_t k0 = 0; k0 < P; k0 += C) {
+        const uint64_t n = std::min(C, P - k0);
+        if (ctx->pool_loc.cap < (nloc + n + 1) * W) {   // grow, keeping the entries so far
+            DevBuf nb;
+            HIPCHK(nb.ensure(std::max((nloc + n + 1) * W, ctx->pool_loc.cap + ctx->pool_loc.cap / 4)));
+            if (nloc) HIPCHK(hipMemcpyAsync(nb.p, ctx->pool_loc.p, nloc * W, hipMemcpyDeviceToDevice, st));
+            HIPCHK(hipStreamSynchronize(st));
+            ctx->pool_loc.release();
+            ctx->pool_loc = nb;
+        }
+        MatProbes vc = v;
+        vc.rows = v.rows + k0 * (uint64_t)(G + 1);
+        HIPCHK((launch_chains<MG, MatProbes>(vc, nullptr, n, ctx->gt, mp, ctx->ss, packed, ctx->chain_tmp.p, ctx->tmp.p,
+                                        ctx->radix_tmp.p, chain_of + k0,
+                                        ctx->pool_loc.as<int64_t>() + nloc * (uint64_t)(G + 2), &dc->nchains, st, dc,
+                                        nullptr)));
+        uint32_t nc = 0;
+        HIPCHK(hipMemcpyAsync(&nc, &dc->nchains, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        if (nloc + nc >= (1ull << 31)) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^31 seed chains in one FindMatches");
+        HIPCHK(launch_add_offset(chain_of + k0, n, (uint32_t)nloc, st));
+        nloc += nc;
+    }
+    HIPCHK(ctx->chain_tmp.ensure(chain_merge_tmp_bytes(nloc)));
+    HIPCHK(ctx->pool.ensure((nloc + 1) * W));
+    HIPCHK(ctx->radix_tmp.ensure(radix_tmp_bytes(nloc + 1)));
+    HIPCHK(launch_chain_merge(ctx->pool_loc.as<int64_t>(), nloc, G, chain_of, P, ctx->pool.as<int64_t>(),
+                              ctx->chain_tmp.p, ctx->radix_tmp.p, ctx->tmp.p, &dc->nchains, st));
+    ctx->walk_events = false;
+    HIPCHK(hipEventRecord(ctx->ev[EV_CHAINS], st));
+    HIPCHK(hipMemcpyAsync(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    ctx->pool_loc.release();
+    const uint64_t nch = ctx->hc.nchains;
+    HIPCHK(ctx->chain_tmp.ensure(nch * 96 + 64 * 256));   // the replay's chain keys / ranks
+    HIPCHK(ctx->radix_tmp.ensure(radix_tmp_bytes(nch + 1)));
+    uint64_t* mlog = nullptr;
+    ctx->log_n = 0;
+    if (ctx->match_log && !ctx->pcompat) {
+        HIPCHK(ctx->logA.ensure((P + 1) * 8));
+        HIPCHK(ctx->logB.ensure((P + 1) * 8));
+        mlog = ctx->logB.as<uint64_t>();
+    }
+    const uint64_t qc = std::min<uint64_t>(C, 1ull << 26);
+    uint4* qbuf = ctx->summ.as<uint4>();
+    uint32_t* pos = (uint32_t*)(qbuf + 2 * qc);
+    const uint32_t lds_cap = std::max<uint32_t>(64, std::min<uint32_t>(ctx->hc.max_bucket, kReplayLdsIds));
+    HIPCHK((launch_replay_chunked<MG, MatProbes>(v, ctx->gt, mp, ctx->L, ctx->sorted_ids, P, ctx->bstart.as<uint32_t>(),
+                                            ctx->bend.as<uint32_t>(), &ctx->emit_tbl, &ctx->emit_base,
+                                            ctx->pool.as<int64_t>(), chain_of, (uint32_t)nch, ctx->chain_tmp.p,
+                                            ctx->radix_tmp.p, lds_cap, ctx->tsize.as<uint32_t>(), ctx->counters.p, st,
+                                            mlog, qc, qbuf, pos, ctx->tmp.p, devbuf_alloc, &ctx->cbuf)));
+    if (mlog) {
+        HIPCHK(hipMemcpyAsync(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        const uint64_t n = ctx->hc.log_n;
+        HIPCHK(ctx->logvA.ensure((n + 1) * 4));
+        HIPCHK(ctx->logvB.ensure((n + 1) * 4));
+        int buf = 0;
+        if (n) HIPCHK(radix_sort<uint64_t>(mlog, nullptr, n, 64, ctx->logA.as<uint64_t>(), ctx->logvA.as<uint32_t>(),
+                                           ctx->logB.as<uint64_t>(), ctx->logvB.as<uint32_t>(), ctx->radix_tmp.p, &buf,
+                                           st));
+        if (buf) std::swap(ctx->logA, ctx->logB);
+        ctx->log_n = n;
+    }
+    return MUMS_OK;
+}
+
 int find_rows_dispatch(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const MatchParams& mp, hipStream_t st) {
     const int G = ctx->gt.G;
+    if (ctx->P > find_chunk()) {
+        if (G <= 4) return find_rows_chunked<4>(ctx, v, packed, mp, st);
+        if (G <= 8) return find_rows_chunked<8>(ctx, v, packed, mp, st);
+        if (G <= 16) return find_rows_chunked<16>(ctx, v, packed, mp, st);
+        return find_rows_chunked<32>(ctx, v, packed, mp, st);
+    }
     if (G <= 4) return find_rows<4>(ctx, v, packed, mp, st);
     if (G <= 8) return find_rows<8>(ctx, v, packed, mp, st);
     if (G <= 16) return find_rows<16>(ctx, v, packed, mp, st);
@@ -301,11 +400,13 @@ int find_rows_dispatch(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const
 
 // the probes of the seed stage as rows (one build_probe each) in ctx->mprobe
 template <typename View>
-int materialize_dispatch(mums_ctx* ctx, View sv, const MatchParams& mp, hipStream_t st) {
+int materialize_dispatch(mums_ctx* ctx, View sv, const MatchParams& mp, hipStream_t st, int64_t* rows = nullptr) {
     const int G = ctx->gt.G;
     const uint64_t P = ctx->P;
-    HIPCHK(ctx->mprobe.ensure((P + 1) * (size_t)(G + 1) * 8));
-    int64_t* rows = ctx->mprobe.as<int64_t>();
+    if (!rows) {   // into ctx->mprobe, else into the caller's (P + 1) rows
+        HIPCHK(ctx->mprobe.ensure((P + 1) * (size_t)(G + 1) * 8));
+        rows = ctx->mprobe.as<int64_t>();
+    }
     if (G <= 4) HIPCHK((launch_materialize<4, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st)));
     else if (G <= 8) HIPCHK((launch_materialize<8, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st)));
     else if (G <= 16) HIPCHK((launch_materialize<16, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st)));
@@ -335,14 +436,22 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
     HIPCHK(ctx->bend.ensure((size_t)Tb * 4));
     HIPCHK(ctx->tsize.ensure((size_t)Tb * 4));
     HIPCHK(ctx->obase.ensure((size_t)Tb * 4 + 64));
-    HIPCHK(ctx->pool.ensure((ctx->P + 1) * (size_t)(G + 2) * 8));
-    HIPCHK(ctx->tbl.ensure((ctx->P + 1) * 4));
+    if (ctx->P >= (1ull << 32) - 64) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed probes in one FindMatches");
+    const bool chunked = ctx->P > find_chunk() && !ctx->pcompat;
     HIPCHK(ctx->chain_of.ensure((ctx->P + 1) * 4));
-    HIPCHK(ctx->spill.ensure((ctx->P + 1) * 16));
-    // summaries, their compacted copies, keep-flag scan, compacted bucket ranges (replay.hip)
-    HIPCHK(ctx->summ.ensure((ctx->P + 1) * 64 + (ctx->P + 64) * 4 + ((size_t)Tb + 64) * 8 +
-                            scan_tmp_bytes(ctx->P + 2) + 4096));
-    HIPCHK(ctx->chain_tmp.ensure(chain_tmp_bytes(ctx->P + 1, Tb, G)));
+    if (chunked) {   // find_rows_chunked: chains per slice, replay summaries per chunk + keep flags
+        const uint64_t C = find_chunk(), qc = std::min<uint64_t>(C, 1ull << 26);
+        for (DevBuf* b : {&ctx->pool, &ctx->cbuf, &ctx->tbl, &ctx->spill}) b->release();
+        HIPCHK(ctx->summ.ensure(qc * 32 + (ctx->P + 64) * 4 + 4096));
+    } else {
+        HIPCHK(ctx->tbl.ensure((ctx->P + 1) * 4));
+        HIPCHK(ctx->spill.ensure((ctx->P + 1) * 16));
+        HIPCHK(ctx->pool.ensure((ctx->P + 1) * (size_t)(G + 2) * 8));
+        // summaries, their compacted copies, keep-flag scan, compacted bucket ranges (replay.hip)
+        HIPCHK(ctx->summ.ensure((ctx->P + 1) * 64 + (ctx->P + 64) * 4 + ((size_t)Tb + 64) * 8 +
+                                scan_tmp_bytes(ctx->P + 2) + 4096));
+        HIPCHK(ctx->chain_tmp.ensure(chain_tmp_bytes(ctx->P + 1, Tb, G)));
+    }
     HIPCHK(ctx->radix_tmp.ensure(radix_tmp_bytes(ctx->P + 1)));
     HIPCHK(ctx->tmp.ensure(std::max(scan_tmp_bytes(ctx->P + 1), scan_tmp_bytes(Tb))));
     HIPCHK(hipMemsetAsync(&dc->max_bucket, 0, 4, st));
@@ -351,11 +460,28 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
     HIPCHK(hipMemsetAsync(ctx->tsize.p, 0, (size_t)Tb * 4, st));
     HIPCHK(launch_bucket_ranges(ctx->sorted_buckets, ctx->P, ctx->bstart.as<uint32_t>(), ctx->bend.as<uint32_t>(),
                                 &dc->max_bucket, st));
+    ctx->emit_tbl = ctx->tbl.as<uint32_t>();
+    ctx->emit_base = ctx->bstart.as<uint32_t>();
     if (ctx->P == 0) HIPCHK(hipEventRecord(ctx->ev[EV_CHAINS], st));
     if (ctx->P > 0) {
         MatProbes v{};
         int rc = rows(&v);
         if (rc) return rc;
+        if (chunked) {   // the rows hold all FindMatches reads: keep the bucket order, free the rest
+            HIPCHK(ctx->sids.ensure((ctx->P + 64) * 4));
+            HIPCHK(hipMemcpyAsync(ctx->sids.p, ctx->sorted_ids, ctx->P * 4, hipMemcpyDeviceToDevice, st));
+            HIPCHK(hipStreamSynchronize(st));
+            ctx->sorted_ids = ctx->sids.as<uint32_t>();
+            ctx->sorted_buckets = nullptr;
+            ctx->probe_info = nullptr;
+            ctx->sorted_rec = nullptr;
+            ctx->sorted_key = nullptr;
+            ctx->sorted_idx = nullptr;
+            for (DevBuf* b : {&ctx->recA, &ctx->recB, &ctx->pbuf, &ctx->tiles, &ctx->rowtmp, &ctx->kA, &ctx->kB,
+                              &ctx->vA, &ctx->vB, &ctx->ckey, &ctx->mprobe})
+                if (!(b->p && (char*)v.rows >= (char*)b->p && (char*)v.rows < (char*)b->p + b->cap)) b->release();
+            HIPCHK(ctx->chain_tmp.ensure(chain_tmp_bytes(find_chunk() + 1, Tb, G)));
+        }
         rc = find_rows_dispatch(ctx, v, packed, mp, st);
         if (rc) return rc;
         if (ctx->pcompat)   // ParallelMemHash::MergeTable (ParallelMemHash.cpp:105-121)
@@ -371,7 +497,7 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
     ctx->M = ctx->hc.nmatches;
     HIPCHK(ctx->out_len.ensure((ctx->M + 1) * 8));
     HIPCHK(ctx->out_s.ensure((ctx->M + 1) * (size_t)G * 8));
-    HIPCHK(launch_emit(ctx->obase.as<uint32_t>(), ctx->bstart.as<uint32_t>(), ctx->tbl.as<uint32_t>(),
+    HIPCHK(launch_emit(ctx->obase.as<uint32_t>(), ctx->emit_base, ctx->emit_tbl,
                        ctx->pool.as<int64_t>(), G, Tb, ctx->M, ctx->out_len.as<uint64_t>(), ctx->out_s.as<int64_t>(),
                        st));
     HIPCHK(hipEventRecord(ctx->ev[EV_OUTPUT], st));
@@ -1106,7 +1232,8 @@ int mums_ctx_destroy(mums_ctx* ctx) {
                       &ctx->radix_tmp, &ctx->spill, &ctx->summ, &ctx->dbgbuf, &ctx->mprobe, &ctx->rowtmp,
                       &ctx->cval, &ctx->ctab, &ctx->smlk0, &ctx->smlkA, &ctx->smlkB, &ctx->smlvA,
                       &ctx->smlvB, &ctx->smltmp, &ctx->flen, &ctx->fs, &ctx->rowsall, &ctx->rsbuf,
-                      &ctx->rsplan, &ctx->rsbst};
+                      &ctx->rsplan, &ctx->rsbst, &ctx->pool_loc, &ctx->cbuf, &ctx->sids,
+                      &ctx->logA, &ctx->logB, &ctx->logvA, &ctx->logvB};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i < EV_COUNT; ++i)
         if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
@@ -1837,6 +1964,8 @@ int mums_probe_copy(mums_ctx* ctx, uint32_t* buckets, uint64_t* ref_index, uint6
         return fail(ctx, MUMS_E_UNSUPPORTED, "probe export after a chunked shard merge");
     if (capacity < ctx->P) return fail(ctx, MUMS_E_INVALID, "output buffer too small");
     if (!ctx->packed_path) return fail(ctx, MUMS_E_UNSUPPORTED, "probe export needs the packed-record path");
+    if (ctx->P && (!ctx->probe_info || !ctx->sorted_rec))
+        return fail(ctx, MUMS_E_UNSUPPORTED, "probe export after a chunked run (> 2^32 seed-mers)");
     const uint64_t P = ctx->P, N = ctx->N;
     if (P == 0) return MUMS_OK;
     HIPCHK(hipSetDevice(ctx->device));
@@ -2172,21 +2301,23 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
         groups += ctx->hc.ngroups;
         const uint64_t Pc = ctx->P;
         if (stage >= MUMS_STAGE_ALL && Pc) {
-            if (P_total + Pc >= (1ull << 30))
-                return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^30 seed probes in one FindMatches");
-            rc = materialize_dispatch<RecViewT<33>>(ctx, RecViewT<33>{ctx->sorted_rec}, mp, st);
-            if (rc) return rc;
+            if (P_total + Pc >= (1ull << 32) - 64)   // probe ids are 32-bit (bucket order, chains)
+                return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed probes in one FindMatches");
             const size_t W = (size_t)(G + 1) * 8;
             if (ctx->rowsall.cap < (P_total + Pc + 1) * W) {   // grow, keeping the rows so far
+                // sized for the chunks to come at this chunk's rate (+10 %): one growth
+                // at 2 x 3 Gbp instead of a doubling that would not fit next to the records
+                const uint64_t est = (uint64_t)((double)(P_total + Pc) * nch / (c + 1) * 1.1) + 1;
                 DevBuf nb;
-                HIPCHK(nb.ensure((P_total + Pc + 1) * W * 2));
+                HIPCHK(nb.ensure(std::max(P_total + Pc + 1, est) * W));
                 if (P_total) HIPCHK(hipMemcpyAsync(nb.p, ctx->rowsall.p, P_total * W, hipMemcpyDeviceToDevice, st));
                 HIPCHK(hipStreamSynchronize(st));
                 ctx->rowsall.release();
                 ctx->rowsall = nb;
             }
-            HIPCHK(hipMemcpyAsync((char*)ctx->rowsall.p + P_total * W, ctx->mprobe.p, Pc * W,
-                                  hipMemcpyDeviceToDevice, st));
+            rc = materialize_dispatch<RecViewT<33>>(ctx, RecViewT<33>{ctx->sorted_rec}, mp, st,
+                                                    (int64_t*)((char*)ctx->rowsall.p + P_total * W));
+            if (rc) return rc;
         }
         P_total += Pc;
     }
@@ -2196,6 +2327,12 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
         int tbits = 1;
         while (tbits < 32 && ((uint64_t)1 << tbits) < (uint64_t)ctx->table_size) ++tbits;
         ctx->probe_info = nullptr;
+        if (P_total > find_chunk()) {   // the rows hold everything FindMatches reads: free the records
+            HIPCHK(hipStreamSynchronize(st));
+            for (DevBuf* b : {&ctx->recA, &ctx->recB, &ctx->pbuf, &ctx->mprobe, &ctx->tiles}) b->release();
+            ctx->sorted_rec = nullptr;
+            ctx->probe_info = nullptr;
+        }
         if (P_total) {
             HIPCHK(ctx->rowtmp.ensure((P_total + 64) * 16 + 8192));
             uint32_t* bkt = (uint32_t*)ctx->rowtmp.p;

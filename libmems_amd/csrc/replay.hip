@@ -135,17 +135,18 @@ __device__ __forceinline__ uint32_t mask_of(const Mhe<MG>& m, int G) {
 template <int MG, typename View>
 __global__ __launch_bounds__(kBlock) void probe_summary_kernel(View v, GenomeTable gt, MatchParams mp, int L,
                                                                const uint64_t* __restrict__ probe_info,
-                                                               const uint32_t* __restrict__ ids, uint64_t P,
-                                                               const uint32_t* __restrict__ chain_of,
-                                                               uint4* __restrict__ summ,
+                                                               const uint32_t* __restrict__ ids, uint64_t q0,
+                                                               uint64_t q1, const uint32_t* __restrict__ chain_of,
+                                                               uint4* __restrict__ summ, uint4* __restrict__ summ_b,
                                                                uint32_t* __restrict__ first_pos) {
-    const uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (q >= P) return;
+    const uint64_t q = q0 + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (q >= q1) return;
     const uint32_t k = ids[q];
     Mhe<MG> Q;
     load_probe<MG>(v, k, gt.G, L, Q);
     const uint32_t cid = chain_of[k];
-    summ[q] = make_uint4(mask_of<MG>(Q, gt.G), (uint32_t)start_at(Q, first_start(Q)), cid, k);
+    summ[q - q0] = make_uint4(mask_of<MG>(Q, gt.G), (uint32_t)start_at(Q, first_start(Q)), cid, 0u);
+    summ_b[q - q0] = make_uint4(0u, 0u, 0u, k);   // .w: the probe (AddHashEntry call) index
     // probes run in ascending q, so the plain read filters nearly every later atomic
     if ((uint32_t)q < __hip_atomic_load(&first_pos[cid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
         atomicMin(&first_pos[cid], (uint32_t)q);
@@ -230,17 +231,18 @@ __global__ __launch_bounds__(kBlock) void chain_sb_kernel(const int64_t* __restr
 }
 
 __global__ __launch_bounds__(kBlock) void probe_flags_kernel(uint4* __restrict__ summ, uint4* __restrict__ summ_b,
-                                                             uint64_t P, const uint32_t* __restrict__ first_pos,
+                                                             uint64_t n, uint64_t q0,
+                                                             const uint32_t* __restrict__ first_pos,
                                                              const uint4* __restrict__ chain_sb) {
-    const uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (q >= P) return;
-    uint4 r = summ[q];
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    uint4 r = summ[i];
     const uint4 cs = chain_sb[r.z];
-    const bool first = first_pos[r.z] == (uint32_t)q;
+    const bool first = first_pos[r.z] == (uint32_t)(q0 + i);
     const bool susp = !first && r.y >= cs.w;
     r.w |= (first ? 0x80000000u : 0u) | (susp ? 0x40000000u : 0u);
-    summ[q] = r;
-    summ_b[q] = make_uint4(cs.x, cs.y, cs.z, 0u);
+    summ[i] = r;
+    summ_b[i] = make_uint4(cs.x, cs.y, cs.z, summ_b[i].w);
 }
 
 // the probe of stream group k (AddHashEntry's argument), built on the rare slow path
@@ -255,7 +257,7 @@ __device__ __noinline__ void probe_full(const View& v, const GenomeTable& gt, co
 // whose probe is not a collision (RB if none).  tb is an LDS or a global slot array.
 template <int MG, int RB, typename View>
 __device__ __forceinline__ int round_first(const uint4* tb, uint32_t t, uint32_t done, uint32_t c, uint4 me,
-                                           const View& v, const GenomeTable& gt, const MatchParams& mp, int L,
+                                           uint4 mb, const View& v, const GenomeTable& gt, const MatchParams& mp, int L,
                                            const uint64_t* __restrict__ probe_info,
                                            const int64_t* __restrict__ pool, int* red) {
     const uint32_t tid = threadIdx.x;
@@ -269,7 +271,7 @@ __device__ __forceinline__ int round_first(const uint4* tb, uint32_t t, uint32_t
         Mhe<MG> P;
         bool have = false;
         auto full = [&](uint32_t xid) -> bool {
-            if (!have) { probe_full<MG, View>(v, gt, mp, L, probe_info, me.w & 0x3FFFFFFFu, P); have = true; }
+            if (!have) { probe_full<MG, View>(v, gt, mp, L, probe_info, mb.w, P); have = true; }
             Mhe<MG> E;
             load_entry<MG>(pool, xid, G, E);
             return mhe_less(E, P);
@@ -279,7 +281,7 @@ __device__ __forceinline__ int round_first(const uint4* tb, uint32_t t, uint32_t
             const uint4 X = tb[lb];
             int q = slot_equiv(X, pmask, ps, pl, pcid);
             if (q == 2) {
-                if (!have) { probe_full<MG, View>(v, gt, mp, L, probe_info, me.w & 0x3FFFFFFFu, P); have = true; }
+                if (!have) { probe_full<MG, View>(v, gt, mp, L, probe_info, mb.w, P); have = true; }
                 Mhe<MG> E;
                 load_entry<MG>(pool, X.x, G, E);
                 q = (mhe_less(E, P) || mhe_less(P, E)) ? 0 : 1;
@@ -381,7 +383,7 @@ __global__ __launch_bounds__(RB) void replay_kernel(
             const uint32_t r0 = s_rmin;
             for (uint32_t k = tid; k < K_b; k += RB) {
                 tbl[ob + ((summ_b[beg + k].z & 0x7FFFFFFFu) - r0)] = summ[beg + k].z;
-                log_insert(mlog, ctr, summ[beg + k].w & 0x3FFFFFFFu, summ[beg + k].z);
+                log_insert(mlog, ctr, summ_b[beg + k].w, summ[beg + k].z);
             }
             if (tid == 0) {
                 tsize[b] = K_b;
@@ -416,8 +418,8 @@ __global__ __launch_bounds__(RB) void replay_kernel(
         while (done < c) {
             if (dbg) { t0 = wall_clock64(); ++n_round; }
             const int first = in_lds
-                ? round_first<MG, RB, View>(s_tab, t, done, c, me, v, gt, mp, L, probe_info, pool, red)
-                : round_first<MG, RB, View>(spill + ob, t, done, c, me, v, gt, mp, L, probe_info, pool, red);
+                ? round_first<MG, RB, View>(s_tab, t, done, c, me, mb, v, gt, mp, L, probe_info, pool, red)
+                : round_first<MG, RB, View>(spill + ob, t, done, c, me, mb, v, gt, mp, L, probe_info, pool, red);
             if (dbg) { const uint64_t t1 = wall_clock64(); c_round += t1 - t0; t0 = t1; }
             if (first == RB) {
                 coll += c - done;
@@ -432,7 +434,7 @@ __global__ __launch_bounds__(RB) void replay_kernel(
                                    : insert_pos<MG>(spill + ob, t, me.z, me.x, (int64_t)mb.x, (int64_t)mb.y, pool, G);
                 s_rank = mb.z & 0x7FFFFFFFu;
                 s_new = make_uint4(me.z, me.x, mb.x, mb.y);
-                log_insert(mlog, ctr, me.w & 0x3FFFFFFFu, me.z);
+                log_insert(mlog, ctr, mb.w, me.z);
             }
             if (in_lds && t + 1 > lds_cap) {   // spill the vector to the bucket's global slice
                 for (uint32_t k = tid; k < t; k += RB) spill[ob + k] = s_tab[k];
@@ -607,7 +609,7 @@ __global__ __launch_bounds__(kBigRB) void replay_big_kernel(
             const uint4 a = summ[beg + k];
             if (a.w & 0x80000000u) {
                 cnt[(summ_b[beg + k].z) - r0] = 1u;
-                log_insert(mlog, ctr, a.w & 0x3FFFFFFFu, a.z);
+                log_insert(mlog, ctr, summ_b[beg + k].w, a.z);
             }
         }
         __syncthreads();
@@ -628,7 +630,7 @@ __global__ __launch_bounds__(kBigRB) void replay_big_kernel(
             Mhe<MG> P;
             bool have = false;
             auto full = [&](uint32_t xid) -> bool {
-                if (!have) { probe_full<MG, View>(v, gt, mp, L, probe_info, me.w & 0x3FFFFFFFu, P); have = true; }
+                if (!have) { probe_full<MG, View>(v, gt, mp, L, probe_info, mb.w, P); have = true; }
                 Mhe<MG> X;
                 load_entry<MG>(pool, xid, G, X);
                 return mhe_less(X, P);
@@ -639,7 +641,7 @@ __global__ __launch_bounds__(kBigRB) void replay_big_kernel(
                 const uint4 X = at(lb);
                 int q = slot_equiv(X, pmask, ps, pl, pcid);
                 if (q == 2) {
-                    if (!have) { probe_full<MG, View>(v, gt, mp, L, probe_info, me.w & 0x3FFFFFFFu, P); have = true; }
+                    if (!have) { probe_full<MG, View>(v, gt, mp, L, probe_info, mb.w, P); have = true; }
                     Mhe<MG> X2;
                     load_entry<MG>(pool, X.x, G, X2);
                     q = (mhe_less(X2, P) || mhe_less(P, X2)) ? 0 : 1;
@@ -663,7 +665,7 @@ __global__ __launch_bounds__(kBigRB) void replay_big_kernel(
                 const uint32_t rh = ins < t ? chain_sb[at(ins).x].z - r0 : 0xFFFFFFFFu;
                 if (rr < R && rl <= rr && rr <= rh) {
                     cnt[rr] += 1u;
-                    log_insert(mlog, ctr, me.w & 0x3FFFFFFFu, pcid);
+                    log_insert(mlog, ctr, mb.w, pcid);
                 } else {
                     s_bad = 2;
                 }
@@ -758,7 +760,7 @@ __global__ __launch_bounds__(kBlock) void bigg_fill_kernel(const uint4* __restri
     const uint4 a = summ[beg + k];
     if (a.w & 0x80000000u) {
         cnt[summ_b[beg + k].z - r0] = 1u;
-        log_insert(mlog, ctr, a.w & 0x3FFFFFFFu, a.z);
+        log_insert(mlog, ctr, summ_b[beg + k].w, a.z);
     }
 }
 
@@ -787,7 +789,7 @@ __global__ void bigg_slow_kernel(View v, GenomeTable gt, MatchParams mp, int L, 
     Mhe<MG> P;
     bool have = false;
     auto full = [&](uint32_t xid) -> bool {
-        if (!have) { probe_full<MG, View>(v, gt, mp, L, probe_info, me.w & 0x3FFFFFFFu, P); have = true; }
+        if (!have) { probe_full<MG, View>(v, gt, mp, L, probe_info, mb.w, P); have = true; }
         Mhe<MG> X;
         load_entry<MG>(pool, xid, G, X);
         return mhe_less(X, P);
@@ -798,7 +800,7 @@ __global__ void bigg_slow_kernel(View v, GenomeTable gt, MatchParams mp, int L, 
         const uint4 X = at(lb);
         int q = slot_equiv(X, pmask, ps, pl, pcid);
         if (q == 2) {
-            if (!have) { probe_full<MG, View>(v, gt, mp, L, probe_info, me.w & 0x3FFFFFFFu, P); have = true; }
+            if (!have) { probe_full<MG, View>(v, gt, mp, L, probe_info, mb.w, P); have = true; }
             Mhe<MG> X2;
             load_entry<MG>(pool, X.x, G, X2);
             q = (mhe_less(X2, P) || mhe_less(P, X2)) ? 0 : 1;
@@ -823,7 +825,7 @@ __global__ void bigg_slow_kernel(View v, GenomeTable gt, MatchParams mp, int L, 
     const uint32_t rh = ins < t ? chain_sb[at(ins).x].z - r0 : 0xFFFFFFFFu;
     if (rr < R && rl <= rr && rr <= rh) {
         cnt[rr] += 1u;
-        log_insert(mlog, ctr, me.w & 0x3FFFFFFFu, pcid);
+        log_insert(mlog, ctr, mb.w, pcid);
     } else {
         info[4] = 1u;
     }
@@ -850,6 +852,27 @@ __global__ void bigg_finish_kernel(const uint32_t* __restrict__ E, uint32_t R, c
     atomicAdd(&ctr->collisions, (unsigned long long)info[5]);
     if (info[4]) atomicOr(&ctr->err, 4u);
     cend[b] = beg;   // replay_kernel / replay_big_kernel skip it
+}
+
+// chunked FindMatches (probes beyond one pass of per-probe arrays): the keep flags of
+// bucket-ordered probes [q0, q0 + n) into the global flag array, then their compaction
+__global__ __launch_bounds__(kBlock) void keep_chunk_kernel(const uint4* __restrict__ summ, uint64_t n, uint64_t q0,
+                                                            uint32_t* __restrict__ keep) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) keep[q0 + i] = (summ[i].w & 0xC0000000u) ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(kBlock) void compact_chunk_kernel(const uint4* __restrict__ summ,
+                                                               const uint4* __restrict__ summ_b, uint64_t n,
+                                                               uint64_t q0, const uint32_t* __restrict__ pos,
+                                                               uint4* __restrict__ sc, uint4* __restrict__ sbc) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint4 x = summ[i];
+    if (x.w & 0xC0000000u) {
+        sc[pos[q0 + i]] = x;
+        sbc[pos[q0 + i]] = summ_b[i];
+    }
 }
 
 // Probes that are neither chain-first nor suspicious (flag bits 31 / 30 clear) collide
@@ -941,107 +964,29 @@ hipError_t launch_bucket_ranges(const uint32_t* sb, uint64_t P, uint32_t* bstart
     return hipGetLastError();
 }
 
+// The replay over the compacted probes (chain-first / suspicious, bucket-major, cbeg /
+// cend per bucket): big buckets by rank counts (grid path, then one workgroup), then the
+// per-bucket rounds.  scr: scratch of replay_scratch_bytes(scr_n) for scr_n compacted probes.
 template <int MG, typename View>
-hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, int L, const uint64_t* probe_info,
-                         const uint32_t* sorted_ids, uint64_t P, const uint32_t* bstart, const uint32_t* bend,
-                         uint32_t* tbl, void* spill, void* summ, const int64_t* pool, const uint32_t* chain_of,
-                         uint32_t nch, void* d_tmp, void* d_radix_tmp, uint32_t lds_cap, uint32_t* tsize, void* ctr,
-                         uint64_t* dbg, hipStream_t st, uint64_t* mlog) {
-    char* p = (char*)d_tmp;
+hipError_t replay_tail(View v, const GenomeTable& gt, const MatchParams& mp, int L, const uint64_t* probe_info,
+                       const uint4* summ_c, const uint4* summ_bc, uint32_t* cbeg, uint32_t* cend,
+                       const uint32_t* bstart, uint32_t* tbl, void* spill, const int64_t* pool,
+                       const uint4* chain_sb, uint64_t scr_n, void* scr, void* stmp, uint32_t lds_cap,
+                       uint32_t* tsize, void* ctr, uint64_t* dbg, hipStream_t st, uint64_t* mlog) {
+    hipError_t e = hipSuccess;
+    char* p = (char*)scr;
     auto carve = [&](size_t bytes) {
         char* r = p;
         p += (bytes + 255) & ~(size_t)255;
         return (void*)r;
     };
-    uint64_t* key_s = (uint64_t*)carve((size_t)nch * 8);
-    uint64_t* key_b = (uint64_t*)carve((size_t)nch * 8);
-    uint64_t* key_g = (uint64_t*)carve((size_t)nch * 8);
-    uint64_t* kA = (uint64_t*)carve((size_t)nch * 8);
-    uint64_t* kB = (uint64_t*)carve((size_t)nch * 8);
-    uint32_t* vA = (uint32_t*)carve((size_t)nch * 4);
-    uint32_t* vB = (uint32_t*)carve((size_t)nch * 4);
-    uint32_t* first_pos = (uint32_t*)carve((size_t)nch * 4);
-    uint32_t* next_s = (uint32_t*)carve((size_t)nch * 4);
-    uint32_t* rank = (uint32_t*)carve((size_t)nch * 4);
-    uint4* chain_sb = (uint4*)carve((size_t)nch * 16);
-    uint4* summ_b = (uint4*)summ + (P + 1);
-    const unsigned pgrid = (unsigned)((P + kBlock - 1) / kBlock), cgrid = (nch + kBlock - 1) / kBlock;
-    hipError_t e = hipMemsetAsync(first_pos, 0xFF, (size_t)nch * 4, st);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((probe_summary_kernel<MG, View>), dim3(pgrid), dim3(kBlock), 0, st, v, gt, mp, L, probe_info,
-                       sorted_ids, P, chain_of, (uint4*)summ, first_pos);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    // chains in (bucket, mask, first start) order -> next_s per chain
-    hipLaunchKernelGGL(chain_keys_kernel, dim3(cgrid), dim3(kBlock), 0, st, pool, nch, gt.G, mp.table_size,
-                       1.0 / (double)mp.table_size, key_s, key_b);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    int buf = 0;
-    if ((e = radix_sort<uint64_t>(key_s, nullptr, nch, 32, kA, vA, kB, vB, d_radix_tmp, &buf, st)) != hipSuccess)
-        return e;
-    const uint32_t* ord1 = buf ? vB : vA;
-    hipLaunchKernelGGL(gather_u64_kernel, dim3(cgrid), dim3(kBlock), 0, st, key_b, ord1, nch, key_g);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    uint32_t* vin = buf ? vB : vA;
-    uint32_t* vout = buf ? vA : vB;
-    int buf2 = 0;
-    // pass 0 reads vin and writes vout; later passes ping-pong between vout and vin
-    if ((e = radix_sort<uint64_t>(key_g, vin, nch, 64, kA, vout, kB, vin, d_radix_tmp, &buf2, st)) != hipSuccess)
-        return e;
-    const uint32_t* ord = buf2 ? vin : vout;
-    hipLaunchKernelGGL(chain_next_kernel, dim3(cgrid), dim3(kBlock), 0, st, ord, key_s, key_b, nch, next_s, rank);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(chain_sb_kernel, dim3(cgrid), dim3(kBlock), 0, st, pool, nch, gt.G, rank, next_s, chain_sb);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(probe_flags_kernel, dim3(pgrid), dim3(kBlock), 0, st, (uint4*)summ, summ_b, P, first_pos,
-                       chain_sb);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    // the replay reads only chain-first / suspicious probes (summ buffer: 2 more uint4
-    // arrays, the scanned keep flags and the compacted bucket ranges after the originals)
-    uint4* summ_c = summ_b + (P + 1);
-    uint4* summ_bc = summ_c + (P + 1);
-    uint32_t* pos = (uint32_t*)(summ_bc + (P + 1));
-    uint32_t* cbeg = pos + (P + 64);
-    uint32_t* cend = cbeg + mp.table_size + 64;
-    void* stmp = (void*)(((uintptr_t)(cend + mp.table_size + 64) + 255) & ~(uintptr_t)255);
-    hipLaunchKernelGGL(keep_flags_kernel, dim3((unsigned)((P + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
-                       (const uint4*)summ, P, pos);
-    if ((e = exclusive_scan_u32(pos, P + 1, stmp, nullptr, st)) != hipSuccess) return e;
-    hipLaunchKernelGGL(compact_summ_kernel, dim3(pgrid), dim3(kBlock), 0, st, (const uint4*)summ,
-                       (const uint4*)summ_b, pos, P, summ_c, summ_bc);
-    hipLaunchKernelGGL(compact_ranges_kernel, dim3((mp.table_size + kBlock - 1) / kBlock), dim3(kBlock), 0, st,
-                       bstart, bend, pos, mp.table_size, P, cbeg, cend, (DevCounters*)ctr);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (getenv("MUMS_DEV_REPLAY_STATS")) {   // development: what keeps the big buckets off the fast path
-        const uint32_t Tb = mp.table_size;
-        std::vector<uint32_t> hb(Tb), he(Tb);
-        (void)hipMemcpyAsync(hb.data(), cbeg, Tb * 4, hipMemcpyDeviceToHost, st);
-        (void)hipMemcpyAsync(he.data(), cend, Tb * 4, hipMemcpyDeviceToHost, st);
-        (void)hipStreamSynchronize(st);
-        for (uint32_t b = 0; b < Tb; ++b) {
-            const uint32_t K = he[b] - hb[b];
-            if (K < 20000) continue;
-            std::vector<uint4> a(K), c(K);
-            (void)hipMemcpy(a.data(), summ_c + hb[b], K * 16, hipMemcpyDeviceToHost);
-            (void)hipMemcpy(c.data(), summ_bc + hb[b], K * 16, hipMemcpyDeviceToHost);
-            uint32_t nfirst = 0, nsusp = 0, ntie = 0, rmin = ~0u, rmax = 0;
-            long first_slow = -1;
-            for (uint32_t k = 0; k < K; ++k) {
-                const bool f = a[k].w & 0x80000000u, su = a[k].w & 0x40000000u, ti = c[k].z & 0x80000000u;
-                nfirst += f; nsusp += su; ntie += ti;
-                if ((!f || su || ti) && first_slow < 0) first_slow = k;
-                rmin = std::min(rmin, c[k].z & 0x7FFFFFFFu); rmax = std::max(rmax, c[k].z & 0x7FFFFFFFu);
-            }
-            fprintf(stderr, "bucket %u: K %u first %u susp %u tied %u rank span %u first slow at %ld\n", b, K, nfirst,
-                    nsusp, ntie, rmax - rmin + 1, first_slow);
-        }
-    }
     // big buckets with few suspicious probes: rank counts (replay_big_kernel), first
     {
         const char* bm_env = getenv("MUMS_DEV_BIG_BUCKET");
         const uint32_t big_min = bm_env ? (uint32_t)atoi(bm_env) : kBigBucket;
-        uint32_t* scr_cnt = (uint32_t*)carve((P + 1) * 4);
-        uint32_t* scr_e = (uint32_t*)carve((P + 1 + mp.table_size + 1) * 4);
-        uint4* scr_slot = (uint4*)carve((P + 1) * 16);
+        uint32_t* scr_cnt = (uint32_t*)carve((scr_n + 1) * 4);
+        uint32_t* scr_e = (uint32_t*)carve((scr_n + 1 + mp.table_size + 1) * 4);
+        uint4* scr_slot = (uint4*)carve((scr_n + 1) * 16);
         uint32_t* ginfo = (uint32_t*)carve(64);
         uint32_t* gslow = (uint32_t*)carve((kGridSlow + 1) * 4);
         // grid path first, for the big buckets with few suspicious probes (host-driven)
@@ -1123,6 +1068,210 @@ hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, i
     return hipGetLastError();
 }
 
+size_t replay_scratch_bytes(uint64_t n, uint32_t table_size) {
+    return (n + 1) * 4 + (n + 2 + (uint64_t)table_size) * 4 + (n + 1) * 16 + 64 + (kGridSlow + 1) * 4 + 5 * 256;
+}
+
+template <int MG, typename View>
+hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, int L, const uint64_t* probe_info,
+                         const uint32_t* sorted_ids, uint64_t P, const uint32_t* bstart, const uint32_t* bend,
+                         uint32_t* tbl, void* spill, void* summ, const int64_t* pool, const uint32_t* chain_of,
+                         uint32_t nch, void* d_tmp, void* d_radix_tmp, uint32_t lds_cap, uint32_t* tsize, void* ctr,
+                         uint64_t* dbg, hipStream_t st, uint64_t* mlog) {
+    char* p = (char*)d_tmp;
+    auto carve = [&](size_t bytes) {
+        char* r = p;
+        p += (bytes + 255) & ~(size_t)255;
+        return (void*)r;
+    };
+    uint64_t* key_s = (uint64_t*)carve((size_t)nch * 8);
+    uint64_t* key_b = (uint64_t*)carve((size_t)nch * 8);
+    uint64_t* key_g = (uint64_t*)carve((size_t)nch * 8);
+    uint64_t* kA = (uint64_t*)carve((size_t)nch * 8);
+    uint64_t* kB = (uint64_t*)carve((size_t)nch * 8);
+    uint32_t* vA = (uint32_t*)carve((size_t)nch * 4);
+    uint32_t* vB = (uint32_t*)carve((size_t)nch * 4);
+    uint32_t* first_pos = (uint32_t*)carve((size_t)nch * 4);
+    uint32_t* next_s = (uint32_t*)carve((size_t)nch * 4);
+    uint32_t* rank = (uint32_t*)carve((size_t)nch * 4);
+    uint4* chain_sb = (uint4*)carve((size_t)nch * 16);
+    uint4* summ_b = (uint4*)summ + (P + 1);
+    const unsigned pgrid = (unsigned)((P + kBlock - 1) / kBlock), cgrid = (nch + kBlock - 1) / kBlock;
+    hipError_t e = hipMemsetAsync(first_pos, 0xFF, (size_t)nch * 4, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((probe_summary_kernel<MG, View>), dim3(pgrid), dim3(kBlock), 0, st, v, gt, mp, L, probe_info,
+                       sorted_ids, (uint64_t)0, P, chain_of, (uint4*)summ, summ_b, first_pos);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // chains in (bucket, mask, first start) order -> next_s per chain
+    hipLaunchKernelGGL(chain_keys_kernel, dim3(cgrid), dim3(kBlock), 0, st, pool, nch, gt.G, mp.table_size,
+                       1.0 / (double)mp.table_size, key_s, key_b);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    int buf = 0;
+    if ((e = radix_sort<uint64_t>(key_s, nullptr, nch, 32, kA, vA, kB, vB, d_radix_tmp, &buf, st)) != hipSuccess)
+        return e;
+    const uint32_t* ord1 = buf ? vB : vA;
+    hipLaunchKernelGGL(gather_u64_kernel, dim3(cgrid), dim3(kBlock), 0, st, key_b, ord1, nch, key_g);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    uint32_t* vin = buf ? vB : vA;
+    uint32_t* vout = buf ? vA : vB;
+    int buf2 = 0;
+    // pass 0 reads vin and writes vout; later passes ping-pong between vout and vin
+    if ((e = radix_sort<uint64_t>(key_g, vin, nch, 64, kA, vout, kB, vin, d_radix_tmp, &buf2, st)) != hipSuccess)
+        return e;
+    const uint32_t* ord = buf2 ? vin : vout;
+    hipLaunchKernelGGL(chain_next_kernel, dim3(cgrid), dim3(kBlock), 0, st, ord, key_s, key_b, nch, next_s, rank);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(chain_sb_kernel, dim3(cgrid), dim3(kBlock), 0, st, pool, nch, gt.G, rank, next_s, chain_sb);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(probe_flags_kernel, dim3(pgrid), dim3(kBlock), 0, st, (uint4*)summ, summ_b, P, (uint64_t)0,
+                       first_pos, chain_sb);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // the replay reads only chain-first / suspicious probes (summ buffer: 2 more uint4
+    // arrays, the scanned keep flags and the compacted bucket ranges after the originals)
+    uint4* summ_c = summ_b + (P + 1);
+    uint4* summ_bc = summ_c + (P + 1);
+    uint32_t* pos = (uint32_t*)(summ_bc + (P + 1));
+    uint32_t* cbeg = pos + (P + 64);
+    uint32_t* cend = cbeg + mp.table_size + 64;
+    void* stmp = (void*)(((uintptr_t)(cend + mp.table_size + 64) + 255) & ~(uintptr_t)255);
+    hipLaunchKernelGGL(keep_flags_kernel, dim3((unsigned)((P + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+                       (const uint4*)summ, P, pos);
+    if ((e = exclusive_scan_u32(pos, P + 1, stmp, nullptr, st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(compact_summ_kernel, dim3(pgrid), dim3(kBlock), 0, st, (const uint4*)summ,
+                       (const uint4*)summ_b, pos, P, summ_c, summ_bc);
+    hipLaunchKernelGGL(compact_ranges_kernel, dim3((mp.table_size + kBlock - 1) / kBlock), dim3(kBlock), 0, st,
+                       bstart, bend, pos, mp.table_size, P, cbeg, cend, (DevCounters*)ctr);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (getenv("MUMS_DEV_REPLAY_STATS")) {   // development: what keeps the big buckets off the fast path
+        const uint32_t Tb = mp.table_size;
+        std::vector<uint32_t> hb(Tb), he(Tb);
+        (void)hipMemcpyAsync(hb.data(), cbeg, Tb * 4, hipMemcpyDeviceToHost, st);
+        (void)hipMemcpyAsync(he.data(), cend, Tb * 4, hipMemcpyDeviceToHost, st);
+        (void)hipStreamSynchronize(st);
+        for (uint32_t b = 0; b < Tb; ++b) {
+            const uint32_t K = he[b] - hb[b];
+            if (K < 20000) continue;
+            std::vector<uint4> a(K), c(K);
+            (void)hipMemcpy(a.data(), summ_c + hb[b], K * 16, hipMemcpyDeviceToHost);
+            (void)hipMemcpy(c.data(), summ_bc + hb[b], K * 16, hipMemcpyDeviceToHost);
+            uint32_t nfirst = 0, nsusp = 0, ntie = 0, rmin = ~0u, rmax = 0;
+            long first_slow = -1;
+            for (uint32_t k = 0; k < K; ++k) {
+                const bool f = a[k].w & 0x80000000u, su = a[k].w & 0x40000000u, ti = c[k].z & 0x80000000u;
+                nfirst += f; nsusp += su; ntie += ti;
+                if ((!f || su || ti) && first_slow < 0) first_slow = k;
+                rmin = std::min(rmin, c[k].z & 0x7FFFFFFFu); rmax = std::max(rmax, c[k].z & 0x7FFFFFFFu);
+            }
+            fprintf(stderr, "bucket %u: K %u first %u susp %u tied %u rank span %u first slow at %ld\n", b, K, nfirst,
+                    nsusp, ntie, rmax - rmin + 1, first_slow);
+        }
+    }
+    return replay_tail<MG, View>(v, gt, mp, L, probe_info, summ_c, summ_bc, cbeg, cend, bstart, tbl, spill, pool,
+                                 chain_sb, P, carve(replay_scratch_bytes(P, mp.table_size)), stmp, lds_cap, tsize,
+                                 ctr, dbg, st, mlog);
+}
+
+// FindMatches replay when the per-probe arrays of launch_replay do not fit (BASELINE
+// config 5: 2.5e9 probes): the probes are visited in bucket order in chunks of qc, twice
+// -- once for the chain-first positions and the keep flags, once to compact the kept
+// ones -- so only the compacted probes (chain-first or suspicious) and one flag word per
+// probe stay resident.  Same kernels, same result as launch_replay.
+template <int MG, typename View>
+hipError_t launch_replay_chunked(View v, const GenomeTable& gt, const MatchParams& mp, int L,
+                                 const uint32_t* sorted_ids, uint64_t P, const uint32_t* bstart, const uint32_t* bend,
+                                 uint32_t** tbl_out, const uint32_t** base_out, const int64_t* pool,
+                                 const uint32_t* chain_of, uint32_t nch, void* d_tmp, void* d_radix_tmp,
+                                 uint32_t lds_cap, uint32_t* tsize, void* ctr, hipStream_t st, uint64_t* mlog,
+                                 uint64_t qc, void* qbuf, uint32_t* pos, void* d_scan_tmp,
+                                 void* (*alloc)(void*, size_t), void* alloc_ctx) {
+    char* p = (char*)d_tmp;
+    auto carve = [&](size_t bytes) {
+        char* r = p;
+        p += (bytes + 255) & ~(size_t)255;
+        return (void*)r;
+    };
+    uint64_t* key_s = (uint64_t*)carve((size_t)nch * 8);
+    uint64_t* key_b = (uint64_t*)carve((size_t)nch * 8);
+    uint64_t* key_g = (uint64_t*)carve((size_t)nch * 8);
+    uint64_t* kA = (uint64_t*)carve((size_t)nch * 8);
+    uint64_t* kB = (uint64_t*)carve((size_t)nch * 8);
+    uint32_t* vA = (uint32_t*)carve((size_t)nch * 4);
+    uint32_t* vB = (uint32_t*)carve((size_t)nch * 4);
+    uint32_t* first_pos = (uint32_t*)carve((size_t)nch * 4);
+    uint32_t* next_s = (uint32_t*)carve((size_t)nch * 4);
+    uint32_t* rank = (uint32_t*)carve((size_t)nch * 4);
+    uint4* chain_sb = (uint4*)carve((size_t)nch * 16);
+    uint4* qs = (uint4*)qbuf;          // one chunk's summaries
+    uint4* qsb = qs + qc;
+    const unsigned cgrid = (nch + kBlock - 1) / kBlock;
+    hipError_t e = hipMemsetAsync(first_pos, 0xFF, (size_t)nch * 4, st);
+    if (e != hipSuccess) return e;
+    auto summaries = [&](uint64_t q0, uint64_t n) {
+        hipLaunchKernelGGL((probe_summary_kernel<MG, View>), dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock),
+                           0, st, v, gt, mp, L, nullptr, sorted_ids, q0, q0 + n, chain_of, qs, qsb, first_pos);
+    };
+    for (uint64_t q0 = 0; q0 < P; q0 += qc) summaries(q0, std::min(qc, P - q0));   // chain-first positions
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(chain_keys_kernel, dim3(cgrid), dim3(kBlock), 0, st, pool, nch, gt.G, mp.table_size,
+                       1.0 / (double)mp.table_size, key_s, key_b);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    int buf = 0;
+    if ((e = radix_sort<uint64_t>(key_s, nullptr, nch, 32, kA, vA, kB, vB, d_radix_tmp, &buf, st)) != hipSuccess)
+        return e;
+    const uint32_t* ord1 = buf ? vB : vA;
+    hipLaunchKernelGGL(gather_u64_kernel, dim3(cgrid), dim3(kBlock), 0, st, key_b, ord1, nch, key_g);
+    uint32_t* vin = buf ? vB : vA;
+    uint32_t* vout = buf ? vA : vB;
+    int buf2 = 0;
+    if ((e = radix_sort<uint64_t>(key_g, vin, nch, 64, kA, vout, kB, vin, d_radix_tmp, &buf2, st)) != hipSuccess)
+        return e;
+    const uint32_t* ord = buf2 ? vin : vout;
+    hipLaunchKernelGGL(chain_next_kernel, dim3(cgrid), dim3(kBlock), 0, st, ord, key_s, key_b, nch, next_s, rank);
+    hipLaunchKernelGGL(chain_sb_kernel, dim3(cgrid), dim3(kBlock), 0, st, pool, nch, gt.G, rank, next_s, chain_sb);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // pass 1: keep flags; pass 2: compaction into Kc slots
+    for (uint64_t q0 = 0; q0 < P; q0 += qc) {
+        const uint64_t n = std::min(qc, P - q0);
+        const unsigned g = (unsigned)((n + kBlock - 1) / kBlock);
+        summaries(q0, n);
+        hipLaunchKernelGGL(probe_flags_kernel, dim3(g), dim3(kBlock), 0, st, qs, qsb, n, q0, first_pos, chain_sb);
+        hipLaunchKernelGGL(keep_chunk_kernel, dim3(g), dim3(kBlock), 0, st, (const uint4*)qs, n, q0, pos);
+    }
+    if ((e = hipMemsetAsync(pos + P, 0, 4, st)) != hipSuccess) return e;
+    if ((e = exclusive_scan_u32(pos, P + 1, d_scan_tmp, nullptr, st)) != hipSuccess) return e;
+    uint32_t Kc = 0;
+    if ((e = hipMemcpyAsync(&Kc, pos + P, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+    const uint32_t Tb = mp.table_size;
+    // compacted probes, their bucket ranges, and the bucket vectors: a bucket ends with at
+    // most one entry per compacted probe, so tbl / spill slices start at cbeg too
+    char* cb = (char*)alloc(alloc_ctx, ((uint64_t)Kc + 1) * 52 + ((uint64_t)Tb + 64) * 8 +
+                                           replay_scratch_bytes(Kc, Tb) + 4096);
+    if (!cb) return hipErrorOutOfMemory;
+    uint4* summ_c = (uint4*)cb;
+    uint4* summ_bc = summ_c + (Kc + 1);
+    uint4* spill = summ_bc + (Kc + 1);
+    uint32_t* tbl = (uint32_t*)(spill + (Kc + 1));
+    uint32_t* cbeg = tbl + Kc + 1;
+    uint32_t* cend = cbeg + Tb + 32;
+    void* scr = (void*)(((uintptr_t)(cend + Tb + 32) + 255) & ~(uintptr_t)255);
+    *tbl_out = tbl;
+    *base_out = cbeg;
+    for (uint64_t q0 = 0; q0 < P; q0 += qc) {
+        const uint64_t n = std::min(qc, P - q0);
+        const unsigned g = (unsigned)((n + kBlock - 1) / kBlock);
+        summaries(q0, n);
+        hipLaunchKernelGGL(probe_flags_kernel, dim3(g), dim3(kBlock), 0, st, qs, qsb, n, q0, first_pos, chain_sb);
+        hipLaunchKernelGGL(compact_chunk_kernel, dim3(g), dim3(kBlock), 0, st, (const uint4*)qs, (const uint4*)qsb, n,
+                           q0, (const uint32_t*)pos, summ_c, summ_bc);
+    }
+    hipLaunchKernelGGL(compact_ranges_kernel, dim3((Tb + kBlock - 1) / kBlock), dim3(kBlock), 0, st, bstart, bend, pos,
+                       Tb, P, cbeg, cend, (DevCounters*)ctr);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    return replay_tail<MG, View>(v, gt, mp, L, nullptr, summ_c, summ_bc, cbeg, cend, cbeg, tbl, spill, pool, chain_sb,
+                                 Kc, scr, d_scan_tmp, lds_cap, tsize, ctr, nullptr, st, mlog);
+}
+
 hipError_t launch_emit(const uint32_t* obase, const uint32_t* bstart, const uint32_t* tbl, const int64_t* pool, int G,
                        uint32_t table_size, uint64_t M, uint64_t* out_len, int64_t* out_s, hipStream_t st) {
     if (M == 0) return hipSuccess;
@@ -1137,6 +1286,17 @@ hipError_t launch_emit(const uint32_t* obase, const uint32_t* bstart, const uint
                                              uint32_t*, void*, void*, const int64_t*, const uint32_t*, uint32_t,   \
                                              void*, void*, uint32_t, uint32_t*, void*, uint64_t*, hipStream_t,    \
                                              uint64_t*);
+#define MUMS_INST_REPLAY_CHUNKED(MG, V)                                                                           \
+    template hipError_t launch_replay_chunked<MG, V>(V, const GenomeTable&, const MatchParams&, int, const uint32_t*, \
+                                                     uint64_t, const uint32_t*, const uint32_t*, uint32_t**,        \
+                                                     const uint32_t**, const int64_t*, const uint32_t*, uint32_t,   \
+                                                     void*, void*, uint32_t, uint32_t*, void*, hipStream_t,         \
+                                                     uint64_t*, uint64_t, void*, uint32_t*, void*,                  \
+                                                     void* (*)(void*, size_t), void*);
+MUMS_INST_REPLAY_CHUNKED(4, MatProbes)
+MUMS_INST_REPLAY_CHUNKED(8, MatProbes)
+MUMS_INST_REPLAY_CHUNKED(16, MatProbes)
+MUMS_INST_REPLAY_CHUNKED(32, MatProbes)
 MUMS_INST_REPLAY(4, MatProbes)
 MUMS_INST_REPLAY(8, MatProbes)
 MUMS_INST_REPLAY(16, MatProbes)

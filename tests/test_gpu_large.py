@@ -51,17 +51,19 @@ def test_c3_findmatches_known_answer(gpu_lib, oracle_mod):
     assert md5_text(ml) == c["md5"]
 
 
-def test_c5_scaled_findmatches_chunked(gpu_lib, oracle_mod):
+@pytest.mark.parametrize("find_chunk", [None, 5_000_000], ids=["one_pass", "sliced"])
+def test_c5_scaled_findmatches_chunked(gpu_lib, oracle_mod, monkeypatch, find_chunk):
+    """Chunked seed stage; FindMatches in one pass, then in 9 slices of 5e6 probes (the
+    path the full 2 x 3 Gbp run takes with 2^28-probe slices)."""
     c = case("c5s")
     seqs = oracle_mod.generate(c["G"], c["n"], c["p"], c["gen_seed"])
-    os.environ["MUMS_DEV_CHUNK_RECORDS"] = str(16_000_000)   # 2 x 50 Mbp in >= 8 key chunks
-    try:
-        with gpu_lib.MemHash(0) as mh:
-            mh.SetSeed(c["seed"])
-            ml = mh.FindMatches(seqs)
-            st = mh.stats()
-    finally:
-        os.environ.pop("MUMS_DEV_CHUNK_RECORDS", None)
+    monkeypatch.setenv("MUMS_DEV_CHUNK_RECORDS", str(16_000_000))   # 2 x 50 Mbp in >= 8 key chunks
+    if find_chunk:
+        monkeypatch.setenv("MUMS_DEV_FIND_CHUNK", str(find_chunk))
+    with gpu_lib.MemHash(0) as mh:
+        mh.SetSeed(c["seed"])
+        ml = mh.FindMatches(seqs)
+        st = mh.stats()
     assert st["chunks"] >= 8
     assert st["probes"] == c["probes"]
     assert len(ml) == c["matches"] and st["collision_count"] == c["collisions"]
@@ -128,3 +130,50 @@ def test_c5_full_seed_stage(gpu_lib, oracle_mod):
     # related genomes (p = 0.01): a position is a shared unique seed when its 19 care bases
     # are unmutated, 0.99^19 = 0.83 of the positions
     assert c0[1] > 0.8 * m
+
+
+def test_c5_full_findmatches(gpu_lib, oracle_mod):
+    """BASELINE config 5 end to end on one GPU: 2 x 3 Gbp related (p = 0.01), w19, chunked
+    seed stage (> 2^32 seed-mers) and FindMatches in 2^28-probe slices (2.5e9 AddHashEntry
+    calls).  Size-independent checks: every call either inserted an entry or collided
+    (probes = MemCount + collisions); the MatchList is unchanged with half-size slices;
+    sampled matches begin and end with a seed hit (care positions equal in both genomes)."""
+    import torch
+    n = 3_000_000_000
+    dev = torch.device("cuda", 0)
+    a, b = synth_pair(n, 0.01, 2024, dev)
+    seed = oracle_mod.get_seed(19)
+    res = {}
+    with gpu_lib.MemHash(0) as mh:
+        mh.SetSeed(seed)
+        mh.AddSequence(a)
+        mh.AddSequence(b)
+        for chunk in (None, 1 << 27):
+            if chunk:
+                os.environ["MUMS_DEV_FIND_CHUNK"] = str(chunk)
+            try:
+                mh.CreateMatches()
+            finally:
+                os.environ.pop("MUMS_DEV_FIND_CHUNK", None)
+            ml = mh.GetMatchList()
+            res[chunk] = (ml, mh.stats())
+    ml, st = res[None]
+    ml2, st2 = res[1 << 27]
+    assert st["seedmers"] == 2 * (n - 26)
+    assert st["probes"] > (1 << 31)                   # beyond the former 2^30 limit
+    assert st["probes"] == st["mem_count"] + st["collision_count"]
+    assert len(ml) > 0 and np.array_equal(ml.lengths, ml2.lengths) and np.array_equal(ml.starts, ml2.starts)
+    assert st["chains"] == st2["chains"]
+    # sampled forward entries: the care positions of the first and last seed windows
+    # agree in both genomes (an entry is a chain of seed hits)
+    L = 27
+    care = [k for k in range(L) if (seed >> (L - 1 - k)) & 1]
+    fwd = np.nonzero((ml.starts > 0).all(axis=1))[0]
+    assert len(fwd) > 0
+    rng = random.Random(9)
+    for i in rng.sample(list(fwd), min(200, len(fwd))):
+        s0, s1, ln = int(ml.starts[i, 0]) - 1, int(ml.starts[i, 1]) - 1, int(ml.lengths[i])
+        for d in (0, ln - L):
+            x = a[s0 + d:s0 + d + L].cpu().numpy()
+            y = b[s1 + d:s1 + d + L].cpu().numpy()
+            assert all(x[k] == y[k] for k in care)

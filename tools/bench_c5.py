@@ -3,7 +3,8 @@
 MemHash seed stage ("sorted+matched") in the chunked mode (> 2^32 seed-mers per context,
 libmems_amd/csrc/chunked.hip).  Reports seed-mers/s and, as size-independent parity
 checks, that a finer chunking (MUMS_DEV_CHUNK_RECORDS) gives the same probe and group
-counts, and that the run is repeatable.
+counts, and that the run is repeatable.  Then the whole FindMatches (2.5e9 AddHashEntry
+calls: chains per 2^28-probe slice, replay in chunks of the bucket order) timed likewise.
 
     python tools/bench_c5.py [--length 3000000000] [--steps 2]
 """
@@ -44,6 +45,7 @@ def main():
     ap.add_argument("--length", type=int, default=3_000_000_000)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--fine-cap", type=int, default=400_000_000)
+    ap.add_argument("--find-steps", type=int, default=2)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     t0 = time.perf_counter()
@@ -71,6 +73,15 @@ def main():
         mh.FindStage(lm.STAGE_SEEDS)
         fine = mh.stats()
         os.environ.pop("MUMS_DEV_CHUNK_RECORDS")
+        fts = []
+        for _ in range(args.find_steps):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            mh.CreateMatches()
+            torch.cuda.synchronize()
+            fts.append(time.perf_counter() - t1)
+            print(f"FindMatches {fts[-1] * 1e3:.1f} ms", flush=True)
+        fst = mh.stats() if fts else None
     dt = min(ts)
     out.update({
         "seedmers": st["seedmers"], "seedmers_per_s": st["seedmers"] / dt, "ms_per_step": dt * 1e3,
@@ -79,6 +90,13 @@ def main():
         "finer_chunking": {"chunks": fine["chunks"], "probes": fine["probes"], "groups": fine["groups"],
                            "same_counts": (fine["probes"], fine["groups"]) == (st["probes"], st["groups"])},
     })
+    if fst:
+        fd = min(fts)
+        out["findmatches"] = {
+            "ms": fd * 1e3, "matches": fst["mem_count"], "mums_per_s": fst["mem_count"] / fd, "probes": fst["probes"],
+            "chains": fst["chains"], "mem_count": fst["mem_count"], "collisions": fst["collision_count"],
+            "phase_ms": {k: round(fst[k], 2) for k in fst if k.startswith("ms_")},
+        }
     print(json.dumps(out), flush=True)
     if not out["finer_chunking"]["same_counts"]:
         sys.exit(3)
