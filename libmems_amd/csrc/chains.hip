@@ -825,5 +825,6 @@ MUMS_INST_CHAINS(4, MatProbes)
 MUMS_INST_CHAINS(8, MatProbes)
 MUMS_INST_CHAINS(16, MatProbes)
 MUMS_INST_CHAINS(32, MatProbes)
+MUMS_INST_CHAINS(64, MatProbes)
 
 }  // namespace mums

@@ -466,10 +466,12 @@ MUMS_INST_PROBE(4, PairView<uint32_t>)
 MUMS_INST_PROBE(8, PairView<uint32_t>)
 MUMS_INST_PROBE(16, PairView<uint32_t>)
 MUMS_INST_PROBE(32, PairView<uint32_t>)
+MUMS_INST_PROBE(64, PairView<uint32_t>)
 MUMS_INST_PROBE(4, PairView<uint64_t>)
 MUMS_INST_PROBE(8, PairView<uint64_t>)
 MUMS_INST_PROBE(16, PairView<uint64_t>)
 MUMS_INST_PROBE(32, PairView<uint64_t>)
+MUMS_INST_PROBE(64, PairView<uint64_t>)
 #define MUMS_INST_MAT(MG, V)                                                                                      \
     template hipError_t launch_materialize<MG, V>(V, const uint64_t*, uint64_t, const GenomeTable&,                \
                                                   const MatchParams&, int, int64_t*, hipStream_t);
@@ -477,26 +479,32 @@ MUMS_INST_MAT(4, PairView<uint32_t>)
 MUMS_INST_MAT(8, PairView<uint32_t>)
 MUMS_INST_MAT(16, PairView<uint32_t>)
 MUMS_INST_MAT(32, PairView<uint32_t>)
+MUMS_INST_MAT(64, PairView<uint32_t>)
 MUMS_INST_MAT(4, PairView<uint64_t>)
 MUMS_INST_MAT(8, PairView<uint64_t>)
 MUMS_INST_MAT(16, PairView<uint64_t>)
 MUMS_INST_MAT(32, PairView<uint64_t>)
+MUMS_INST_MAT(64, PairView<uint64_t>)
 MUMS_INST_MAT(4, RecView)
 MUMS_INST_MAT(8, RecView)
 MUMS_INST_MAT(16, RecView)
 MUMS_INST_MAT(32, RecView)
+MUMS_INST_MAT(64, RecView)
 MUMS_INST_PROBE(4, RecView)
 MUMS_INST_PROBE(8, RecView)
 MUMS_INST_PROBE(16, RecView)
 MUMS_INST_PROBE(32, RecView)
+MUMS_INST_PROBE(64, RecView)
 // chunked mode (> 2^32 seed-mers): 33-bit record indices
 MUMS_INST_MAT(4, RecViewT<33>)
 MUMS_INST_MAT(8, RecViewT<33>)
 MUMS_INST_MAT(16, RecViewT<33>)
 MUMS_INST_MAT(32, RecViewT<33>)
+MUMS_INST_MAT(64, RecViewT<33>)
 MUMS_INST_PROBE(4, RecViewT<33>)
 MUMS_INST_PROBE(8, RecViewT<33>)
 MUMS_INST_PROBE(16, RecViewT<33>)
 MUMS_INST_PROBE(32, RecViewT<33>)
+MUMS_INST_PROBE(64, RecViewT<33>)
 
 }  // namespace mums

@@ -208,6 +208,17 @@ __device__ __forceinline__ int genome_of_mg(const GenomeTable& gt, uint64_t i) {
     return g;
 }
 
+// genome presence bits of a probe (bit g = genome g): 32 bits up to 32 genomes, else 64
+template <int MG>
+using MaskT = typename std::conditional<(MG > 32), uint64_t, uint32_t>::type;
+
+// MaskedMemHash's match number (MaskedMemHash.cpp:51-58): genome 0 is the top of G bits
+template <typename M>
+__device__ __forceinline__ uint64_t match_number_of(M mask, uint32_t G) {
+    if constexpr (sizeof(M) == 8) return __builtin_bitreverse64(mask) >> (64 - G);
+    else return (uint64_t)(__builtin_bitreverse32(mask) >> (32 - G));
+}
+
 // Fast path of build_probe for the MemHash defaults repeat_tol = 0, enum_tol = 1
 // (MemHash.h:31-32): accept iff >= 2 records and no genome twice; the probe offset
 // (CalculateOffset, MatchHashEntry.cpp:141-160, after SetDirection) is summed
@@ -238,7 +249,7 @@ __device__ __forceinline__ bool probe_offset_batch(const RecFields (&r)[MG + 1],
     }
     *gsize = cnt;
     if (cnt < 2) return false;
-    uint32_t mask = 0;
+    MaskT<MG> mask = 0;
     bool dup = false;
     int gref = 64;
     int64_t sref = 0;
@@ -250,7 +261,7 @@ __device__ __forceinline__ bool probe_offset_batch(const RecFields (&r)[MG + 1],
         if ((uint32_t)k < cnt) {
             const int g = gk[k];
             dup = dup || ((mask >> g) & 1u);
-            mask |= 1u << g;
+            mask |= (MaskT<MG>)1 << g;
             if (g < gref) {
                 gref = g;
                 sref = (int64_t)(r[k].idx - gt.base[g]) + 1;
@@ -269,7 +280,7 @@ __device__ __forceinline__ bool probe_offset_batch(const RecFields (&r)[MG + 1],
     }
     *offset = off;
     if (mp.masked) {
-        const uint64_t match_number = (uint64_t)(__builtin_bitreverse32(mask) >> (32 - G));
+        const uint64_t match_number = match_number_of(mask, G);
         return mp.seq_mask == 0 || match_number == mp.seq_mask;
     }
     return true;
@@ -314,7 +325,8 @@ __device__ __forceinline__ bool probe_fast_raw(const uint64_t (&x)[MG + 1], cons
         cnt += run ? 1u : 0u;
     }
     *gsize = cnt;
-    uint32_t mask = 0, gref = 64, pref = 0;
+    MaskT<MG> mask = 0;
+    uint32_t gref = 64, pref = 0;
     // 32-bit starts and bases for 32-bit record indices; 64-bit in the chunked mode
     using IdxT = typename std::conditional<(IB > 32), uint64_t, uint32_t>::type;
     IdxT sref = 0;
@@ -337,7 +349,7 @@ __device__ __forceinline__ bool probe_fast_raw(const uint64_t (&x)[MG + 1], cons
         sk[k] = idx - b + 1u;   // 1-based start in genome g
         const bool in = (uint32_t)k < cnt;
         dup = dup || (in && ((mask >> g) & 1u));
-        mask |= in ? (1u << g) : 0u;
+        mask |= in ? ((MaskT<MG>)1 << g) : (MaskT<MG>)0;
         const bool better = in && g < gref;
         gref = better ? g : gref;
         sref = better ? sk[k] : sref;
@@ -354,7 +366,7 @@ __device__ __forceinline__ bool probe_fast_raw(const uint64_t (&x)[MG + 1], cons
     *offset = off;
     const bool accept = cnt >= 2 && cnt <= G && !dup;
     if (mp.masked) {
-        const uint64_t match_number = (uint64_t)(__builtin_bitreverse32(mask) >> (32 - G));
+        const uint64_t match_number = match_number_of(mask, G);
         return accept && (mp.seq_mask == 0 || match_number == mp.seq_mask);
     }
     return accept;

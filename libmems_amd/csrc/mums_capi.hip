@@ -224,7 +224,8 @@ int groups_dispatch(mums_ctx* ctx, View v, const SegTile* tiles, uint64_t ntiles
     if (G <= 4) return run_groups<4, View>(ctx, v, tiles, ntiles, mp, pi, pb, si, sb, st);
     if (G <= 8) return run_groups<8, View>(ctx, v, tiles, ntiles, mp, pi, pb, si, sb, st);
     if (G <= 16) return run_groups<16, View>(ctx, v, tiles, ntiles, mp, pi, pb, si, sb, st);
-    return run_groups<32, View>(ctx, v, tiles, ntiles, mp, pi, pb, si, sb, st);
+    if (G <= 32) return run_groups<32, View>(ctx, v, tiles, ntiles, mp, pi, pb, si, sb, st);
+    return run_groups<64, View>(ctx, v, tiles, ntiles, mp, pi, pb, si, sb, st);
 }
 
 // chain labelling (chains.hip) then the per-bucket replay (replay.hip) of the P probe
@@ -390,12 +391,14 @@ int find_rows_dispatch(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const
         if (G <= 4) return find_rows_chunked<4>(ctx, v, packed, mp, st);
         if (G <= 8) return find_rows_chunked<8>(ctx, v, packed, mp, st);
         if (G <= 16) return find_rows_chunked<16>(ctx, v, packed, mp, st);
-        return find_rows_chunked<32>(ctx, v, packed, mp, st);
+        if (G <= 32) return find_rows_chunked<32>(ctx, v, packed, mp, st);
+        return find_rows_chunked<64>(ctx, v, packed, mp, st);
     }
     if (G <= 4) return find_rows<4>(ctx, v, packed, mp, st);
     if (G <= 8) return find_rows<8>(ctx, v, packed, mp, st);
     if (G <= 16) return find_rows<16>(ctx, v, packed, mp, st);
-    return find_rows<32>(ctx, v, packed, mp, st);
+    if (G <= 32) return find_rows<32>(ctx, v, packed, mp, st);
+    return find_rows<64>(ctx, v, packed, mp, st);
 }
 
 // the probes of the seed stage as rows (one build_probe each) in ctx->mprobe
@@ -410,7 +413,8 @@ int materialize_dispatch(mums_ctx* ctx, View sv, const MatchParams& mp, hipStrea
     if (G <= 4) HIPCHK((launch_materialize<4, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st)));
     else if (G <= 8) HIPCHK((launch_materialize<8, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st)));
     else if (G <= 16) HIPCHK((launch_materialize<16, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st)));
-    else HIPCHK((launch_materialize<32, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st)));
+    else if (G <= 32) HIPCHK((launch_materialize<32, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st)));
+    else HIPCHK((launch_materialize<64, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st)));
     return MUMS_OK;
 }
 
@@ -1282,7 +1286,7 @@ int mums_add_genome(mums_ctx* ctx, const char* ascii, uint64_t n) {
     if (check_ctx(ctx)) return MUMS_E_INVALID;
     if (!ascii && n) return fail(ctx, MUMS_E_INVALID, "Null gnSequence pointer");  // MatchFinder.cpp:63-65
     if (ctx->genomes.size() >= (size_t)kMaxG)
-        return fail(ctx, MUMS_E_UNSUPPORTED, "more than 32 genomes per context");
+        return fail(ctx, MUMS_E_UNSUPPORTED, "more than 64 genomes per context");
     HIPCHK(hipSetDevice(ctx->device));
     char* d = nullptr;
     HIPCHK(hipMalloc(&d, n + 16));
@@ -1296,7 +1300,7 @@ int mums_add_genome_device(mums_ctx* ctx, const void* d_ascii, uint64_t n) {
     if (check_ctx(ctx)) return MUMS_E_INVALID;
     if (!d_ascii && n) return fail(ctx, MUMS_E_INVALID, "Null gnSequence pointer");
     if (ctx->genomes.size() >= (size_t)kMaxG)
-        return fail(ctx, MUMS_E_UNSUPPORTED, "more than 32 genomes per context");
+        return fail(ctx, MUMS_E_UNSUPPORTED, "more than 64 genomes per context");
     ctx->genomes.push_back({(const char*)d_ascii, n, false});
     ctx->stage_done = 0;
     return MUMS_OK;
@@ -1333,6 +1337,8 @@ int mums_find_stage(mums_ctx* ctx, int stage) {
         return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed-mers: only MemHash / MaskedMemHash, enum_tol <= 1");
     if (ctx->pcompat && ctx->enum_tol > 1)
         return fail(ctx, MUMS_E_UNSUPPORTED, "ParallelMemHash compat with enumeration tolerance > 1");
+    if (ctx->genomes.size() > (size_t)kPairMaxG && (ctx->pairwise || ctx->pcompat || ctx->enum_tol > 1))
+        return fail(ctx, MUMS_E_UNSUPPORTED, "more than 32 genomes: only MemHash / MaskedMemHash, enum_tol <= 1");
     if (have_start_points(ctx) && (big || ctx->pcompat))
         return fail(ctx, MUMS_E_UNSUPPORTED, "start points (FindMatchesFromPosition) in the chunked / compat modes");
     if (ctx->pairwise || ctx->enum_tol > 1) return run_pipeline_pairwise(ctx, stage);
@@ -1595,7 +1601,7 @@ int mums_add_genome_sml(mums_ctx* ctx, const char* path, uint64_t* seed_out) {
     if (check_ctx(ctx)) return MUMS_E_INVALID;
     if (!path) return fail(ctx, MUMS_E_INVALID, "null path");
     if (ctx->genomes.size() >= (size_t)kMaxG)
-        return fail(ctx, MUMS_E_UNSUPPORTED, "more than 32 genomes per context");
+        return fail(ctx, MUMS_E_UNSUPPORTED, "more than 64 genomes per context");
     FILE* f = fopen(path, "rb");
     if (!f) return fail(ctx, MUMS_E_INVALID, "Unable to open file.");   // FileSML.cpp:51
     SmlHeaderV5 h;
@@ -1757,7 +1763,7 @@ int mums_debug_std_sort(mums_ctx* ctx, const uint64_t* keys, uint64_t n, int dep
 
 int mums_shard_layout(mums_ctx* ctx, uint32_t genomes_total, uint32_t first_genome, const uint64_t* lengths) {
     if (check_ctx(ctx)) return MUMS_E_INVALID;
-    if (genomes_total > (uint32_t)kMaxG) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 32 genomes");
+    if (genomes_total > (uint32_t)kMaxG) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 64 genomes");
     if (first_genome > genomes_total || (genomes_total && !lengths))
         return fail(ctx, MUMS_E_INVALID, "bad shard layout");
     ctx->shard = true;
@@ -1771,7 +1777,7 @@ int mums_shard_layout(mums_ctx* ctx, uint32_t genomes_total, uint32_t first_geno
 int mums_shard_slice(mums_ctx* ctx, uint32_t genomes_total, const uint64_t* lengths, uint32_t genome,
                      uint64_t pos_begin, uint64_t pos_end) {
     if (check_ctx(ctx)) return MUMS_E_INVALID;
-    if (genomes_total > (uint32_t)kMaxG) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 32 genomes");
+    if (genomes_total > (uint32_t)kMaxG) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 64 genomes");
     if (genome >= genomes_total || !lengths || pos_begin > pos_end) return fail(ctx, MUMS_E_INVALID, "bad slice");
     ctx->shard = true;
     ctx->slice = true;

@@ -24,7 +24,8 @@
 
 namespace mums {
 
-constexpr int kMaxG = 32;            // genomes per context (register arrays in the replay)
+constexpr int kMaxG = 64;            // genomes per context (MaskedMemHash's 64-bit match number)
+constexpr int kPairMaxG = 32;        // PairwiseMatchFinder / enum_tol > 1 / ParallelMemHash compat paths
 constexpr int kRepeatLimit = 1000;   // MER_REPEAT_LIMIT, MatchFinder.cpp:166
 constexpr int kBlock = 256;          // threads per workgroup (4 waves of 64)
 #ifndef MUMS_SEED_TILE
@@ -126,7 +127,7 @@ __device__ __forceinline__ uint32_t wave_match_rank(uint32_t dg, bool valid, uin
     return __builtin_amdgcn_mbcnt_hi(ph, __builtin_amdgcn_mbcnt_lo(pl, 0u));
 }
 
-// genome of a global seed-mer index (G <= 32: linear scan is cheapest)
+// genome of a global seed-mer index (G <= 64: a linear scan is cheapest)
 __device__ __forceinline__ int genome_of(const GenomeTable& gt, uint64_t i) {
     int g = 0;
     #pragma unroll 1

@@ -72,8 +72,8 @@ __global__ void pw_emit_kernel(View v, uint64_t N, GenomeTable gt, int L, const 
     const int G = gt.G;
     uint32_t size = 0;
     const uint32_t u = pw_unique(v, i, N, gt, &size);
-    int64_t s[kMaxG];
-    uint32_t par[kMaxG];
+    int64_t s[kPairMaxG];
+    uint32_t par[kPairMaxG];
     const uint64_t k0 = v.gkey(i);
     for (uint64_t j = i; j < N && v.gkey(j) == k0; ++j) {
         const RecFields r = v.get(j);
@@ -109,11 +109,11 @@ constexpr int kEnumMax = 8;   // enum_tol bound of the GPU path (per-genome reco
 // pos[g][i] / par[g][i] their positions and strand parities.
 template <typename View>
 __device__ bool en_collect(const View& v, uint64_t h, uint64_t N, const GenomeTable& gt, const MatchParams& mp,
-                           uint32_t (&c)[kMaxG], uint32_t (&pos)[kMaxG][kEnumMax], uint8_t (&par)[kMaxG][kEnumMax],
+                           uint32_t (&c)[kPairMaxG], uint32_t (&pos)[kPairMaxG][kEnumMax], uint8_t (&par)[kPairMaxG][kEnumMax],
                            uint32_t* size) {
     const uint64_t k0 = v.gkey(h);
-    uint32_t tally[kMaxG];
-    for (int g = 0; g < kMaxG; ++g) { tally[g] = 0; c[g] = 0; }
+    uint32_t tally[kPairMaxG];
+    for (int g = 0; g < kPairMaxG; ++g) { tally[g] = 0; c[g] = 0; }
     uint32_t n = 0;
     bool ok = true;
     // stream order inside a group = (parity, genome, position): restricted to one genome
@@ -137,7 +137,7 @@ __device__ bool en_collect(const View& v, uint64_t h, uint64_t N, const GenomeTa
 // AddHashEntry calls of a group: the odometer's combinations (one record per present
 // genome), or the single HashMatch of a two-record list; HashMatch / MaskedMemHash::
 // HashMatch decide whether each combination is added (same genome set for all of them).
-__device__ __forceinline__ uint32_t en_calls(const uint32_t (&c)[kMaxG], int G, const MatchParams& mp, bool* two) {
+__device__ __forceinline__ uint32_t en_calls(const uint32_t (&c)[kPairMaxG], int G, const MatchParams& mp, bool* two) {
     uint32_t total = 0, nid = 0, combos = 1;
     uint64_t mn = 0;
     for (int g = 0; g < G; ++g) {
@@ -160,8 +160,8 @@ __global__ void en_count_kernel(View v, uint64_t N, GenomeTable gt, MatchParams 
     if (i >= N) return;
     uint32_t k = 0;
     if (pw_head(v, i)) {
-        uint32_t c[kMaxG], pos[kMaxG][kEnumMax], size = 0;
-        uint8_t par[kMaxG][kEnumMax];
+        uint32_t c[kPairMaxG], pos[kPairMaxG][kEnumMax], size = 0;
+        uint8_t par[kPairMaxG][kEnumMax];
         const bool ok = en_collect(v, i, N, gt, mp, c, pos, par, &size);
         if (size > (uint32_t)kRepeatLimit) atomicAdd(&ctr->repeat_limit, 1ull);
         bool two;
@@ -177,15 +177,15 @@ __global__ void en_emit_kernel(View v, uint64_t N, GenomeTable gt, MatchParams m
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N || ncalls[i] == 0) return;
     const int G = gt.G;
-    uint32_t c[kMaxG], pos[kMaxG][kEnumMax], size = 0;
-    uint8_t par[kMaxG][kEnumMax];
+    uint32_t c[kPairMaxG], pos[kPairMaxG][kEnumMax], size = 0;
+    uint8_t par[kPairMaxG][kEnumMax];
     (void)en_collect(v, i, N, gt, mp, c, pos, par, &size);
     bool two;
     const uint32_t K = en_calls(c, G, mp, &two);
     uint64_t o = off[i];
     for (uint32_t t = 0; t < K; ++t) {
-        int64_t sv[kMaxG];
-        uint32_t pv[kMaxG];
+        int64_t sv[kPairMaxG];
+        uint32_t pv[kPairMaxG];
         for (int g = 0; g < G; ++g) { sv[g] = 0; pv[g] = 0; }
         if (two) {   // HashMatch of the two listed records (MatchFinder.cpp:344-347)
             for (int g = 0; g < G; ++g)

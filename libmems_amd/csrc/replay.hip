@@ -51,22 +51,21 @@ __device__ __forceinline__ int block_first_true(bool pred, int* red) {
     return r;
 }
 
-// A vector slot: {pool id, presence mask (bit g = genome g), first-genome start, length}.
-// The slot decides MheCompare (MatchHashEntry.h:121-143) without the entry unless one
-// first-genome span can contain the other:
+// A vector slot: {pool id, block key, first-genome start, length}.  The block key orders
+// presence masks (bit g = genome g) as MheCompare does -- FirstStart index descending,
+// then the first genome present in only one: absent first -- i.e. as bitreverse(mask):
+// bitreverse32(mask) itself up to 32 genomes, its dense rank among the chains' masks
+// beyond (block_keys).  The slot decides MheCompare (MatchHashEntry.h:121-143) without
+// the entry unless one first-genome span can contain the other:
 //   * X is V's own chain entry (same pool id): X contains V -> equivalent
-//   * masks differ: FirstStart index, then the first genome present in only one
+//   * masks differ: block key order
 //   * same mask, V starts before X: only V can contain X (needs X's span inside V's)
 //   * same mask, V starts after X : only X can contain V (needs V's span inside X's)
 // with no containment possible, strict_start_lessthan_ptr is decided by the first
 // genome's (positive) start.  Returns 0 / 1 (X < V false / true), 2 = needs the entries.
 __device__ __forceinline__ int slot_cmp(const uint4 X, uint32_t vmask, int64_t vs, int64_t vl, uint32_t vcid) {
     if (X.x == vcid) return 0;
-    if (X.y != vmask) {
-        const int fa = __builtin_ctz(X.y), fb = __builtin_ctz(vmask);
-        if (fa != fb) return fa > fb ? 1 : 0;
-        return ((X.y >> __builtin_ctz(X.y ^ vmask)) & 1u) == 0u ? 1 : 0;
-    }
+    if (X.y != vmask) return X.y < vmask ? 1 : 0;
     const int64_t xs = (int64_t)X.z, xl = (int64_t)X.w;
     if (vs < xs) return (xs + xl > vs + vl) ? 0 : 2;
     if (vs > xs) return (vs + vl > xs + xl) ? 1 : 2;
@@ -123,12 +122,44 @@ __device__ __forceinline__ uint32_t lower_bound_slots(const uint4* tb, uint32_t 
     return first;
 }
 
+// block key of a probe: bitreverse32(presence mask) up to 32 genomes, else its chain's
+// dense rank (bkey, from block_keys)
 template <int MG>
-__device__ __forceinline__ uint32_t mask_of(const Mhe<MG>& m, int G) {
-    uint32_t k = 0;
-    #pragma unroll
-    for (int g = 0; g < MG; ++g) k |= (g < G && m.s[g] != 0) ? (1u << g) : 0u;
-    return k;
+__device__ __forceinline__ uint32_t block_key(const Mhe<MG>& m, int G, const uint32_t* __restrict__ bkey,
+                                              uint32_t cid) {
+    if constexpr (MG > 32) {
+        return bkey[cid];
+    } else {
+        uint32_t k = 0;
+        #pragma unroll
+        for (int g = 0; g < MG; ++g) k |= (g < G && m.s[g] != 0) ? (1u << g) : 0u;
+        return __builtin_bitreverse32(k);
+    }
+}
+
+// more than 32 genomes: bitreverse64(presence mask) of every chain entry, then each
+// chain's dense rank among them (block_keys)
+__global__ __launch_bounds__(kBlock) void chain_bmask_kernel(const int64_t* __restrict__ pool, uint32_t nch, int G,
+                                                             uint64_t* __restrict__ out) {
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    if (c >= nch) return;
+    const int64_t* e = pool + (uint64_t)c * (uint64_t)(G + 2);
+    uint64_t m = 0;
+    for (int g = 0; g < G; ++g) m |= e[2 + g] != 0 ? (1ull << g) : 0ull;
+    out[c] = __builtin_bitreverse64(m);
+}
+
+__global__ __launch_bounds__(kBlock) void dense_step_kernel(const uint64_t* __restrict__ skey, uint32_t n,
+                                                            uint32_t* __restrict__ step) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) step[i] = (i + 1 < n && skey[i + 1] != skey[i]) ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(kBlock) void dense_scatter_kernel(const uint32_t* __restrict__ ord,
+                                                               const uint32_t* __restrict__ rank, uint32_t n,
+                                                               uint32_t* __restrict__ bkey) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) bkey[ord[i]] = rank[i];
 }
 
 // per probe in bucket order: {presence mask, first-genome start, chain id, probe id | flags}
@@ -138,25 +169,26 @@ __global__ __launch_bounds__(kBlock) void probe_summary_kernel(View v, GenomeTab
                                                                const uint32_t* __restrict__ ids, uint64_t q0,
                                                                uint64_t q1, const uint32_t* __restrict__ chain_of,
                                                                uint4* __restrict__ summ, uint4* __restrict__ summ_b,
-                                                               uint32_t* __restrict__ first_pos) {
+                                                               uint32_t* __restrict__ first_pos,
+                                                               const uint32_t* __restrict__ bkey) {
     const uint64_t q = q0 + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (q >= q1) return;
     const uint32_t k = ids[q];
     Mhe<MG> Q;
     load_probe<MG>(v, k, gt.G, L, Q);
     const uint32_t cid = chain_of[k];
-    summ[q - q0] = make_uint4(mask_of<MG>(Q, gt.G), (uint32_t)start_at(Q, first_start(Q)), cid, 0u);
+    summ[q - q0] = make_uint4(block_key<MG>(Q, gt.G, bkey, cid), (uint32_t)start_at(Q, first_start(Q)), cid, 0u);
     summ_b[q - q0] = make_uint4(0u, 0u, 0u, k);   // .w: the probe (AddHashEntry call) index
     // probes run in ascending q, so the plain read filters nearly every later atomic
     if ((uint32_t)q < __hip_atomic_load(&first_pos[cid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
         atomicMin(&first_pos[cid], (uint32_t)q);
 }
 
-// Sort keys of the chain entries: (hash bucket, block) and first-genome start, where the
-// block key bitreverse(presence mask) orders blocks as MheCompare does (FirstStart
-// index descending, then the first genome present in only one: absent first).
+// Sort keys of the chain entries: (hash bucket, block key) and first-genome start (the
+// block key orders blocks as MheCompare does, see slot_cmp).
 __global__ __launch_bounds__(kBlock) void chain_keys_kernel(const int64_t* __restrict__ pool, uint32_t nch, int G,
                                                             uint32_t table_size, double inv_t,
+                                                            const uint32_t* __restrict__ bkey,
                                                             uint64_t* __restrict__ key_s, uint64_t* __restrict__ key_b) {
     const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
     if (c >= nch) return;
@@ -165,10 +197,10 @@ __global__ __launch_bounds__(kBlock) void chain_keys_kernel(const int64_t* __res
     int64_t s0 = 0;
     for (int g = G - 1; g >= 0; --g) {
         const int64_t sg = e[2 + g];
-        if (sg != 0) { m |= 1u << g; s0 = sg; }
+        if (sg != 0) { m |= g < 32 ? 1u << g : 0u; s0 = sg; }
     }
     key_s[c] = (uint64_t)s0;
-    key_b[c] = ((uint64_t)bucket_of_fast(e[1], table_size, inv_t) << 32) | __builtin_bitreverse32(m);
+    key_b[c] = ((uint64_t)bucket_of_fast(e[1], table_size, inv_t) << 32) | (bkey ? bkey[c] : __builtin_bitreverse32(m));
 }
 
 __global__ __launch_bounds__(kBlock) void gather_u64_kernel(const uint64_t* __restrict__ src,
@@ -1068,6 +1100,27 @@ hipError_t replay_tail(View v, const GenomeTable& gt, const MatchParams& mp, int
     return hipGetLastError();
 }
 
+// G > 32: bkey[c] = dense rank of bitreverse64(mask of chain c) (kA..vB: sort buffers
+// of nch, step: nch words, stmp: scan scratch); nullptr for G <= 32
+uint32_t* block_keys(const int64_t* pool, uint32_t nch, int G, uint64_t* bm, uint64_t* kA, uint32_t* vA, uint64_t* kB,
+                     uint32_t* vB, uint32_t* step, uint32_t* bkey, void* d_radix_tmp, void* stmp, hipStream_t st,
+                     hipError_t* err) {
+    *err = hipSuccess;
+    if (G <= 32 || nch == 0) return nullptr;
+    const unsigned cgrid = (nch + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(chain_bmask_kernel, dim3(cgrid), dim3(kBlock), 0, st, pool, nch, G, bm);
+    int buf = 0;
+    if ((*err = radix_sort<uint64_t>(bm, nullptr, nch, 64, kA, vA, kB, vB, d_radix_tmp, &buf, st)) != hipSuccess)
+        return nullptr;
+    const uint64_t* sk = buf ? kB : kA;
+    const uint32_t* ord = buf ? vB : vA;
+    hipLaunchKernelGGL(dense_step_kernel, dim3(cgrid), dim3(kBlock), 0, st, sk, nch, step);
+    if ((*err = exclusive_scan_u32(step, nch, stmp, nullptr, st)) != hipSuccess) return nullptr;
+    hipLaunchKernelGGL(dense_scatter_kernel, dim3(cgrid), dim3(kBlock), 0, st, ord, (const uint32_t*)step, nch, bkey);
+    *err = hipGetLastError();
+    return bkey;
+}
+
 size_t replay_scratch_bytes(uint64_t n, uint32_t table_size) {
     return (n + 1) * 4 + (n + 2 + (uint64_t)table_size) * 4 + (n + 1) * 16 + 64 + (kGridSlow + 1) * 4 + 5 * 256;
 }
@@ -1095,16 +1148,22 @@ hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, i
     uint32_t* next_s = (uint32_t*)carve((size_t)nch * 4);
     uint32_t* rank = (uint32_t*)carve((size_t)nch * 4);
     uint4* chain_sb = (uint4*)carve((size_t)nch * 16);
+    uint32_t* bkey_buf = (uint32_t*)carve((size_t)nch * 4);
     uint4* summ_b = (uint4*)summ + (P + 1);
     const unsigned pgrid = (unsigned)((P + kBlock - 1) / kBlock), cgrid = (nch + kBlock - 1) / kBlock;
-    hipError_t e = hipMemsetAsync(first_pos, 0xFF, (size_t)nch * 4, st);
+    hipError_t e = hipSuccess;
+    void* stmp0 = (void*)(((uintptr_t)((uint32_t*)(summ_b + 3 * (P + 1)) + (P + 64) + 2 * (mp.table_size + 64)) + 255) &
+                          ~(uintptr_t)255);   // = stmp below, free until then
+    const uint32_t* bkey = block_keys(pool, nch, gt.G, key_g, kA, vA, kB, vB, next_s, bkey_buf, d_radix_tmp, stmp0,
+                                      st, &e);
     if (e != hipSuccess) return e;
+    if ((e = hipMemsetAsync(first_pos, 0xFF, (size_t)nch * 4, st)) != hipSuccess) return e;
     hipLaunchKernelGGL((probe_summary_kernel<MG, View>), dim3(pgrid), dim3(kBlock), 0, st, v, gt, mp, L, probe_info,
-                       sorted_ids, (uint64_t)0, P, chain_of, (uint4*)summ, summ_b, first_pos);
+                       sorted_ids, (uint64_t)0, P, chain_of, (uint4*)summ, summ_b, first_pos, bkey);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    // chains in (bucket, mask, first start) order -> next_s per chain
+    // chains in (bucket, block, first start) order -> next_s per chain
     hipLaunchKernelGGL(chain_keys_kernel, dim3(cgrid), dim3(kBlock), 0, st, pool, nch, gt.G, mp.table_size,
-                       1.0 / (double)mp.table_size, key_s, key_b);
+                       1.0 / (double)mp.table_size, bkey, key_s, key_b);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     int buf = 0;
     if ((e = radix_sort<uint64_t>(key_s, nullptr, nch, 32, kA, vA, kB, vB, d_radix_tmp, &buf, st)) != hipSuccess)
@@ -1201,19 +1260,23 @@ hipError_t launch_replay_chunked(View v, const GenomeTable& gt, const MatchParam
     uint32_t* next_s = (uint32_t*)carve((size_t)nch * 4);
     uint32_t* rank = (uint32_t*)carve((size_t)nch * 4);
     uint4* chain_sb = (uint4*)carve((size_t)nch * 16);
+    uint32_t* bkey_buf = (uint32_t*)carve((size_t)nch * 4);
     uint4* qs = (uint4*)qbuf;          // one chunk's summaries
     uint4* qsb = qs + qc;
     const unsigned cgrid = (nch + kBlock - 1) / kBlock;
-    hipError_t e = hipMemsetAsync(first_pos, 0xFF, (size_t)nch * 4, st);
+    hipError_t e = hipSuccess;
+    const uint32_t* bkey = block_keys(pool, nch, gt.G, key_g, kA, vA, kB, vB, next_s, bkey_buf, d_radix_tmp, d_scan_tmp,
+                                      st, &e);
     if (e != hipSuccess) return e;
+    if ((e = hipMemsetAsync(first_pos, 0xFF, (size_t)nch * 4, st)) != hipSuccess) return e;
     auto summaries = [&](uint64_t q0, uint64_t n) {
         hipLaunchKernelGGL((probe_summary_kernel<MG, View>), dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock),
-                           0, st, v, gt, mp, L, nullptr, sorted_ids, q0, q0 + n, chain_of, qs, qsb, first_pos);
+                           0, st, v, gt, mp, L, nullptr, sorted_ids, q0, q0 + n, chain_of, qs, qsb, first_pos, bkey);
     };
     for (uint64_t q0 = 0; q0 < P; q0 += qc) summaries(q0, std::min(qc, P - q0));   // chain-first positions
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(chain_keys_kernel, dim3(cgrid), dim3(kBlock), 0, st, pool, nch, gt.G, mp.table_size,
-                       1.0 / (double)mp.table_size, key_s, key_b);
+                       1.0 / (double)mp.table_size, bkey, key_s, key_b);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     int buf = 0;
     if ((e = radix_sort<uint64_t>(key_s, nullptr, nch, 32, kA, vA, kB, vB, d_radix_tmp, &buf, st)) != hipSuccess)
@@ -1297,9 +1360,11 @@ MUMS_INST_REPLAY_CHUNKED(4, MatProbes)
 MUMS_INST_REPLAY_CHUNKED(8, MatProbes)
 MUMS_INST_REPLAY_CHUNKED(16, MatProbes)
 MUMS_INST_REPLAY_CHUNKED(32, MatProbes)
+MUMS_INST_REPLAY_CHUNKED(64, MatProbes)
 MUMS_INST_REPLAY(4, MatProbes)
 MUMS_INST_REPLAY(8, MatProbes)
 MUMS_INST_REPLAY(16, MatProbes)
 MUMS_INST_REPLAY(32, MatProbes)
+MUMS_INST_REPLAY(64, MatProbes)
 
 }  // namespace mums
