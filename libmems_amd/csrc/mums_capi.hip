@@ -32,9 +32,10 @@ namespace {
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
+    bool borrowed = false;   // a view into another DevBuf's dead contents (not ours to free)
     hipError_t ensure(size_t bytes) {
         if (bytes <= cap) return hipSuccess;
-        if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
+        release();
         size_t want = bytes + (bytes >> 4) + 4096;
         hipError_t e = hipMalloc(&p, want);
         if (e == hipSuccess) cap = want;
@@ -42,9 +43,24 @@ struct DevBuf {
         return e;
     }
     void release() {
-        if (p) (void)hipFree(p);
+        if (p && !borrowed) (void)hipFree(p);
         p = nullptr;
         cap = 0;
+        borrowed = false;
+    }
+    // borrow [off, off + bytes) of `host` when it has room (host's contents are dead):
+    // hipMalloc / hipFree of tens of GB cost about a second each at BASELINE config 5
+    bool borrow(const DevBuf& host, size_t off, size_t bytes) {
+        off = (off + 255) & ~(size_t)255;
+        if (!host.p || off + bytes > host.cap) return false;
+        release();
+        p = (char*)host.p + off;
+        cap = host.cap - off;
+        borrowed = true;
+        return true;
+    }
+    void drop_view() {
+        if (borrowed) release();
     }
     template <typename T> T* as() const { return (T*)p; }
 };
@@ -349,7 +365,6 @@ int find_rows_chunked(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const 
     HIPCHK(hipEventRecord(ctx->ev[EV_CHAINS], st));
     HIPCHK(hipMemcpyAsync(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    ctx->pool_loc.release();
     const uint64_t nch = ctx->hc.nchains;
     HIPCHK(ctx->chain_tmp.ensure(nch * 96 + 64 * 256));   // the replay's chain keys / ranks
     HIPCHK(ctx->radix_tmp.ensure(radix_tmp_bytes(nch + 1)));
@@ -445,8 +460,8 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
     HIPCHK(ctx->chain_of.ensure((ctx->P + 1) * 4));
     if (chunked) {   // find_rows_chunked: chains per slice, replay summaries per chunk + keep flags
         const uint64_t C = find_chunk(), qc = std::min<uint64_t>(C, 1ull << 26);
-        for (DevBuf* b : {&ctx->pool, &ctx->cbuf, &ctx->tbl, &ctx->spill}) b->release();
-        HIPCHK(ctx->summ.ensure(qc * 32 + (ctx->P + 64) * 4 + 4096));
+        (void)qc;
+        for (DevBuf* b : {&ctx->pool, &ctx->tbl, &ctx->spill}) b->release();
     } else {
         HIPCHK(ctx->tbl.ensure((ctx->P + 1) * 4));
         HIPCHK(ctx->spill.ensure((ctx->P + 1) * 16));
@@ -471,9 +486,25 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
         MatProbes v{};
         int rc = rows(&v);
         if (rc) return rc;
-        if (chunked) {   // the rows hold all FindMatches reads: keep the bucket order, free the rest
-            HIPCHK(ctx->sids.ensure((ctx->P + 64) * 4));
-            HIPCHK(hipMemcpyAsync(ctx->sids.p, ctx->sorted_ids, ctx->P * 4, hipMemcpyDeviceToDevice, st));
+        if (chunked) {   // the rows hold all FindMatches reads: keep the bucket order only
+            // the dead records (recA / recB, when the packed path sized them) are the arena
+            // of the sliced FindMatches: bucket order and summaries in recB, chain scratch
+            // in recA; buffers that do not fit there are allocated (and the rest freed)
+            const bool arena = ctx->packed_path;
+            const uint32_t* ids = ctx->sorted_ids;
+            const size_t ids_b = (ctx->P + 64) * 4;
+            const uint64_t qc = std::min<uint64_t>(find_chunk(), 1ull << 26);
+            const size_t summ_b = qc * 32 + (ctx->P + 64) * 4 + 4096;
+            // (in rowtmp, itself in recB, the sorted ids lie above 2 x ids_b: no overlap)
+            bool in_b = arena && ctx->sids.borrow(ctx->recB, 0, ids_b);
+            if (in_b && (const char*)ids < (const char*)ctx->recB.p + ids_b &&
+                (const char*)ids + ids_b > (const char*)ctx->recB.p)
+                in_b = false;
+            if (!in_b) {
+                ctx->sids.drop_view();
+                HIPCHK(ctx->sids.ensure(ids_b));
+            }
+            HIPCHK(hipMemcpyAsync(ctx->sids.p, ids, ctx->P * 4, hipMemcpyDeviceToDevice, st));
             HIPCHK(hipStreamSynchronize(st));
             ctx->sorted_ids = ctx->sids.as<uint32_t>();
             ctx->sorted_buckets = nullptr;
@@ -481,10 +512,17 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
             ctx->sorted_rec = nullptr;
             ctx->sorted_key = nullptr;
             ctx->sorted_idx = nullptr;
-            for (DevBuf* b : {&ctx->recA, &ctx->recB, &ctx->pbuf, &ctx->tiles, &ctx->rowtmp, &ctx->kA, &ctx->kB,
-                              &ctx->vA, &ctx->vB, &ctx->ckey, &ctx->mprobe})
+            ctx->rowtmp.drop_view();
+            if (!(in_b && ctx->summ.borrow(ctx->recB, ids_b, summ_b))) HIPCHK(ctx->summ.ensure(summ_b));
+            if (!(arena && ctx->chain_tmp.borrow(ctx->recA, 0, chain_tmp_bytes(find_chunk() + 1, Tb, G))))
+                HIPCHK(ctx->chain_tmp.ensure(chain_tmp_bytes(find_chunk() + 1, Tb, G)));
+            for (DevBuf* b : {&ctx->pbuf, &ctx->tiles, &ctx->rowtmp, &ctx->kA, &ctx->kB, &ctx->vA, &ctx->vB,
+                              &ctx->ckey, &ctx->mprobe})
                 if (!(b->p && (char*)v.rows >= (char*)b->p && (char*)v.rows < (char*)b->p + b->cap)) b->release();
-            HIPCHK(ctx->chain_tmp.ensure(chain_tmp_bytes(find_chunk() + 1, Tb, G)));
+            if (!arena) {
+                ctx->recA.release();
+                ctx->recB.release();
+            }
         }
         rc = find_rows_dispatch(ctx, v, packed, mp, st);
         if (rc) return rc;
@@ -579,7 +617,13 @@ int keys_stage(mums_ctx* ctx, const GenomeTable& lgt, uint32_t T, int B, uint64_
 }
 
 // Workspace of the merge stage for n records in 2^mb buckets of key_bits key bits.
+// the records are about to be written: end the views borrowed from them (sliced FindMatches)
+void records_live(mums_ctx* ctx) {
+    for (DevBuf* b : {&ctx->rowtmp, &ctx->sids, &ctx->summ, &ctx->chain_tmp}) b->drop_view();
+}
+
 int ensure_merge_space(mums_ctx* ctx, uint64_t n, int mb, int key_bits, ProbeSpace* ps) {
+    records_live(ctx);
     const uint64_t ub = seg_tiles_upper(n, mb);
     HIPCHK(ctx->recA.ensure(n * 8 + 64));
     HIPCHK(ctx->recB.ensure(n * 8 + 64));
@@ -957,6 +1001,7 @@ int run_pipeline(mums_ctx* ctx, int stage) {
 // Seed pattern (default from the mean genome length, MatchList.h:351-357; checks of
 // SortedMerList::Create :788-798) and the global genome table for genome lengths lens.
 int prepare_run(mums_ctx* ctx, const std::vector<uint64_t>& lens) {
+    records_live(ctx);
     ctx->stage_done = 0;
     ctx->restarts = 0;
     ctx->offset_log.clear();
@@ -2333,11 +2378,12 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
         int tbits = 1;
         while (tbits < 32 && ((uint64_t)1 << tbits) < (uint64_t)ctx->table_size) ++tbits;
         ctx->probe_info = nullptr;
-        if (P_total > find_chunk()) {   // the rows hold everything FindMatches reads: free the records
+        if (P_total > find_chunk()) {   // the rows hold everything FindMatches reads: the records are dead
             HIPCHK(hipStreamSynchronize(st));
-            for (DevBuf* b : {&ctx->recA, &ctx->recB, &ctx->pbuf, &ctx->mprobe, &ctx->tiles}) b->release();
+            for (DevBuf* b : {&ctx->pbuf, &ctx->mprobe, &ctx->tiles}) b->release();
             ctx->sorted_rec = nullptr;
             ctx->probe_info = nullptr;
+            (void)ctx->rowtmp.borrow(ctx->recB, 0, (P_total + 64) * 16 + 8192);   // sliced FindMatches arena
         }
         if (P_total) {
             HIPCHK(ctx->rowtmp.ensure((P_total + 64) * 16 + 8192));

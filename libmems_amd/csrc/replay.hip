@@ -1036,6 +1036,9 @@ hipError_t replay_tail(View v, const GenomeTable& gt, const MatchParams& mp, int
             if ((e = hipMemcpyAsync(hinfo, ginfo, 32, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
             if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
             const uint32_t S = hinfo[3];
+            if (getenv("MUMS_DEV_REPLAY_STATS"))
+                fprintf(stderr, "grid path bucket %u: K %u flags %u slow %u ranks %u..%u\n", b, K, hinfo[2], S, hinfo[0],
+                        hinfo[1]);
             if (hinfo[2] || S > kGridSlow || hinfo[0] > hinfo[1]) continue;   // left to the kernels below
             const uint32_t r0 = hinfo[0], R = hinfo[1] - hinfo[0] + 1;
             std::vector<uint32_t> hs(S);
