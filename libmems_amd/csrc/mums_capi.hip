@@ -490,7 +490,11 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
             // the dead records (recA / recB, when the packed path sized them) are the arena
             // of the sliced FindMatches: bucket order and summaries in recB, chain scratch
             // in recA; buffers that do not fit there are allocated (and the rest freed)
-            const bool arena = ctx->packed_path;
+            auto inside = [](const DevBuf& b, const void* q) {
+                return b.p && (const char*)q >= (const char*)b.p && (const char*)q < (const char*)b.p + b.cap;
+            };
+            const bool arena = ctx->packed_path && !inside(ctx->recA, v.rows) && !inside(ctx->recB, v.rows) &&
+                               !inside(ctx->recA, packed) && !inside(ctx->recB, packed);
             const uint32_t* ids = ctx->sorted_ids;
             const size_t ids_b = (ctx->P + 64) * 4;
             const uint64_t qc = std::min<uint64_t>(find_chunk(), 1ull << 26);
@@ -2169,7 +2173,7 @@ int run_pipeline_pairwise(mums_ctx* ctx, int stage) {
     }
     HIPCHK(hipEventRecord(ctx->ev[EV_GROUPS], st));
     const uint64_t P = ctx->P;
-    if (P >= (1ull << 30)) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^30 seed probes in one FindMatches");
+    if (P >= (1ull << 32) - 64) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed probes in one FindMatches");
     ctx->probe_info = nullptr;
     int tbits = 1;
     while (tbits < 32 && ((uint64_t)1 << tbits) < (uint64_t)ctx->table_size) ++tbits;
@@ -2512,7 +2516,7 @@ int mums_shard_find(mums_ctx* ctx, const int64_t* d_rows, uint64_t nrows, const 
     int rc = shard_seeds_done(ctx);
     if (rc) return rc;
     if (nrows && (!d_rows || !d_packed_all)) return fail(ctx, MUMS_E_INVALID, "null rows / packed genomes");
-    if (nrows >= (1ull << 30)) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^30 seed probes on one rank");
+    if (nrows >= (1ull << 32) - 64) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed probes on one rank");
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
     uint64_t words = 0;
