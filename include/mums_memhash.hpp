@@ -265,7 +265,10 @@ public:
 // The MatchList is the devices' bucket ranges concatenated = MemHash's bucket-major list.
 class ShardedMemHash {
 public:
-    explicit ShardedMemHash(std::vector<int> devices, bool local = false) : devices_(std::move(devices)) {
+    // slices = false: a contiguous genome block per rank; true: every genome cut into
+    // world / G position slices on 64-base bounds (BASELINE config 5: 2 x 3 Gbp over 8 GPUs)
+    explicit ShardedMemHash(std::vector<int> devices, bool local = false, bool slices = false)
+        : devices_(std::move(devices)), slices_(slices) {
         comms_.assign(devices_.size(), nullptr);
         const int rc = local ? mums_comm_init_local(comms_.data(), (int)devices_.size(), devices_.data())
                              : mums_comm_init_all(comms_.data(), (int)devices_.size(), devices_.data());
@@ -288,8 +291,29 @@ public:
         std::vector<uint64_t> lens(G);
         for (size_t g = 0; g < G; ++g) lens[g] = seqs_[g].size();
         ranks_.clear();
+        if (slices_) {   // shard.genome_slices
+            if (G == 0 || W % G) throw InvalidData("position slices need a rank count that is a multiple of G");
+            uint64_t seed = seed_, total = 0;
+            for (uint64_t n : lens) total += n;
+            if (!seed) seed = mums_get_seed((int)mums_default_seed_weight(total / G), 0);
+            const int L = seed ? 64 - __builtin_clzll(seed) - __builtin_ctzll(seed) : 0;
+            const size_t k = W / G;
+            for (size_t r = 0; r < W; ++r) {
+                const size_t g = r / k, j = r % k;
+                const uint64_t m = lens[g] >= (uint64_t)L ? lens[g] - L + 1 : 0;
+                auto cut = [&](size_t q) { return q == 0 ? 0 : q == k ? m : (m * q / k) / 64 * 64; };
+                const uint64_t b0 = cut(j), b1 = std::max(b0, cut(j + 1));
+                auto mh = std::make_unique<MemHash>(devices_[r]);
+                mh->SetTableSize(table_size_);
+                mh->SetSeed(seed);
+                mh->AddSequence(b1 > b0 ? seqs_[g].substr(b0, std::min<uint64_t>(lens[g], b1 + L - 1) - b0) : "");
+                if (mums_shard_slice(mh->handle(), (uint32_t)G, lens.data(), (uint32_t)g, b0, b1) != MUMS_OK)
+                    throw InvalidData(mums_last_error(mh->handle()));
+                ranks_.push_back(std::move(mh));
+            }
+        }
         size_t g0 = 0;
-        for (size_t r = 0; r < W; ++r) {   // genome_blocks: earlier ranks take the remainder
+        for (size_t r = 0; r < (slices_ ? 0 : W); ++r) {   // genome_blocks: earlier ranks take the remainder
             const size_t cnt = G / W + (r < G % W ? 1 : 0);
             auto mh = std::make_unique<MemHash>(devices_[r]);
             mh->SetTableSize(table_size_);
@@ -320,6 +344,7 @@ public:
 
 private:
     std::vector<int> devices_;
+    bool slices_ = false;
     std::vector<mums_comm*> comms_;
     std::vector<std::unique_ptr<MemHash>> ranks_;
     std::vector<std::string> seqs_;

@@ -517,7 +517,12 @@ class ShardedMemHash:
     comm="local"), one host thread per rank.  The ranks' MatchLists in rank order are the
     bucket-major MatchList of MemHash::FindMatches (DESIGN.md §6)."""
 
-    def __init__(self, devices: Sequence[int], comm: str = "rccl", table_size: int = 40000):
+    def __init__(self, devices: Sequence[int], comm: str = "rccl", table_size: int = 40000, layout: str = "blocks"):
+        """layout "blocks": a contiguous genome block per rank; "slices": every genome cut into
+        world / G position slices (BASELINE config 5: two 3 Gbp genomes over 8 GPUs)."""
+        if layout not in ("blocks", "slices"):
+            raise ValueError("layout: 'blocks' or 'slices'")
+        self.layout = layout
         self._lib = load_library()
         self.devices = list(devices)
         self.world = len(self.devices)
@@ -552,8 +557,19 @@ class ShardedMemHash:
         for mh in self.ranks:
             mh.close()
         self.ranks = []
+        if self.layout == "slices":
+            from .shard import genome_slices
+            seed = self.seed or getSeed(getDefaultSeedWeight(sum(len(s) for s in self.seqs) // max(G, 1)))
+            L = getSeedLength(seed)
+            for r, (g, b0, b1) in enumerate(genome_slices([len(s) for s in self.seqs], L, self.world)):
+                mh = MemHash(self.devices[r])
+                mh.SetTableSize(self.table_size)
+                mh.SetSeed(seed)
+                mh.AddSequence(self.seqs[g][b0:min(len(self.seqs[g]), b1 + L - 1)] if b1 > b0 else b"")
+                mh._check(self._lib.mums_shard_slice(mh._ctx, G, lens, g, b0, b1))
+                self.ranks.append(mh)
         g0 = 0
-        for r, dev in enumerate(self.devices):
+        for r, dev in enumerate(self.devices if self.layout == "blocks" else []):
             cnt = base + (1 if r < rem else 0)
             mh = MemHash(dev)
             mh.SetTableSize(self.table_size)

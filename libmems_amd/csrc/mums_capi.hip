@@ -2488,15 +2488,32 @@ int mums_shard_probe_rows(mums_ctx* ctx, uint32_t nranks, const uint32_t* bounds
 int mums_shard_packed_info(mums_ctx* ctx, uint64_t* word_offset, uint64_t* nwords, uint64_t* total_words) {
     int rc = shard_seeds_done(ctx);
     if (rc) return rc;
-    if (ctx->slice)
-        return fail(ctx, MUMS_E_UNSUPPORTED, "sharded FindMatches needs whole genomes per rank (slices: seed stage)");
     GenomeTable g = ctx->gt;
     uint64_t total = 0;
     (void)layout_packed(g, &total);
+    if (total_words) *total_words = total;
+    if (ctx->slice) {
+        // a position slice's packed words are those of bases [begin, end) of its genome
+        // (16 bases a word; the genome's last slice also holds the tail and pad words):
+        // word-exact only for slices starting on a 64-base boundary (shard.genome_slices)
+        const uint32_t gi = ctx->slice_genome;
+        const uint64_t b0 = ctx->slice_begin, b1 = ctx->slice_end;
+        const bool last = b1 >= ctx->gt.m[gi];
+        if (b0 % 64 || (!last && b1 % 64))
+            return fail(ctx, MUMS_E_UNSUPPORTED, "sharded FindMatches on position slices needs 64-base slice bounds");
+        const uint64_t w0 = g.woff[gi] + b0 / 16;
+        const uint64_t w1 = last ? g.woff[gi + 1] : g.woff[gi] + b1 / 16;
+        GenomeTable lt = ctx->lgt;
+        uint64_t local = 0;
+        (void)layout_packed(lt, &local);
+        if (w1 - w0 > local) return fail(ctx, MUMS_E_INVALID, "slice ASCII shorter than its packed words");
+        if (word_offset) *word_offset = w0;
+        if (nwords) *nwords = w1 - w0;
+        return MUMS_OK;
+    }
     const uint32_t nl = (uint32_t)ctx->genomes.size();
     if (word_offset) *word_offset = g.woff[ctx->shard_first];
     if (nwords) *nwords = g.woff[ctx->shard_first + nl] - g.woff[ctx->shard_first];
-    if (total_words) *total_words = total;
     return MUMS_OK;
 }
 

@@ -63,8 +63,10 @@ def genome_blocks(G: int, world: int) -> List[Tuple[int, int]]:
 def genome_slices(lengths: Sequence[int], L: int, world: int) -> List[Tuple[int, int, int]]:
     """Position-sharded layout (BASELINE config 5: each 3 Gbp genome over world/G ranks):
     rank r owns SML positions [begin, end) of genome g = r // (world / G), the genome's
-    SMLLength cut into world / G equal ranges.  Rank order = genome-major, position order =
-    global seed-mer index order, as the exchange requires."""
+    SMLLength cut into world / G near-equal ranges whose inner bounds fall on 64-base
+    boundaries (a slice's 2-bit packed words are then exactly the genome's words for its
+    bases: the FindMatches all-gather of the packed genomes).  Rank order = genome-major,
+    position order = global seed-mer index order, as the exchange requires."""
     G = len(lengths)
     if G == 0 or world % G:
         raise ValueError("position sharding needs world_size to be a multiple of the genome count")
@@ -72,8 +74,9 @@ def genome_slices(lengths: Sequence[int], L: int, world: int) -> List[Tuple[int,
     out = []
     for g, n in enumerate(lengths):
         m = max(int(n) - L + 1, 0)
+        cut = [0] + [(m * j // k) // 64 * 64 for j in range(1, k)] + [m]
         for j in range(k):
-            out.append((g, m * j // k, m * (j + 1) // k))
+            out.append((g, cut[j], max(cut[j], cut[j + 1])))
     return out
 
 

@@ -1,9 +1,10 @@
 """TEST INFRASTRUCTURE: one rank of the sharded FindMatches on the HIP engine.
 
 Launched by tests/test_gpu_shard.py as
-    python -m torch.distributed.run --nproc-per-node R ... tests/gpu_shard_find_worker.py OUTDIR G n p w T
-Every rank runs its genome block on cuda:0 (one GPU on the test box; exchanges over
-gloo) and saves its part of the MatchList (its hash-bucket range, bucket-major).
+    python -m torch.distributed.run --nproc-per-node R ... tests/gpu_shard_find_worker.py OUTDIR G n p w T [slices]
+Every rank runs its genome block (or, with "slices", its genome position slice) on cuda:0
+(one GPU on the test box; exchanges over gloo) and saves its part of the MatchList (its
+hash-bucket range, bucket-major).
 """
 import os
 import sys
@@ -15,7 +16,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from libmems_amd.shard import HipShardEngine, ShardedFindMatches, genome_blocks  # noqa: E402
+from libmems_amd.shard import HipShardEngine, ShardedFindMatches, genome_blocks, genome_slices  # noqa: E402
 from oracle import oracle  # noqa: E402
 
 
@@ -26,10 +27,19 @@ def main():
     rank, world = dist.get_rank(), dist.get_world_size()
     seqs = oracle.generate(G, n, p, 4242 + G)
     seed = oracle.get_seed(w)
-    first, count = genome_blocks(G, world)[rank]
     dev = torch.device("cuda", 0)
-    local = [torch.frombuffer(bytearray(s), dtype=torch.uint8).to(dev) for s in seqs[first:first + count]]
-    eng = HipShardEngine(0, seed, [len(s) for s in seqs], first, local, table_size=T)
+    lens = [len(s) for s in seqs]
+    if len(sys.argv) > 7 and sys.argv[7] == "slices":
+        L = oracle.lib().oracle_seed_length(seed)
+        g, b0, b1 = genome_slices(lens, L, world)[rank]
+        part = seqs[g][b0:min(lens[g], b1 + L - 1)] if b1 > b0 else b""
+        local = [torch.frombuffer(bytearray(part), dtype=torch.uint8).to(dev)] if part else \
+            [torch.zeros(0, dtype=torch.uint8, device=dev)]
+        eng = HipShardEngine(0, seed, lens, g, local, table_size=T, slice_of=(g, b0, b1))
+    else:
+        first, count = genome_blocks(G, world)[rank]
+        local = [torch.frombuffer(bytearray(s), dtype=torch.uint8).to(dev) for s in seqs[first:first + count]]
+        eng = HipShardEngine(0, seed, lens, first, local, table_size=T)
     ml = ShardedFindMatches(eng).run()
     st = eng.stats()
     np.save(os.path.join(outdir, f"len{rank}.npy"), ml.lengths)

@@ -103,17 +103,26 @@ def test_sharded_slices_chunked_merge_gpu(oracle_mod, G, n, p, w, world):
     assert sum(int(x[1]) for x in s) == st["probes"]
 
 
-@pytest.mark.parametrize("G,n,p,w,world,T", [(4, 300_000, 0.02, 15, 2, 40000), (3, 200_000, 0.05, 19, 3, 40000),
-                                               (5, 100_000, 1.0, 15, 2, 40000), (4, 200_000, 0.01, 15, 3, 7)])
-def test_sharded_find_matches_gpu(oracle_mod, G, n, p, w, world, T):
+@pytest.mark.parametrize("G,n,p,w,world,T,slices", [(4, 300_000, 0.02, 15, 2, 40000, False),
+                                                      (3, 200_000, 0.05, 19, 3, 40000, False),
+                                                      (5, 100_000, 1.0, 15, 2, 40000, False),
+                                                      (4, 200_000, 0.01, 15, 3, 7, False),
+                                                      (2, 300_000, 0.02, 19, 4, 40000, True),
+                                                      (2, 200_001, 0.03, 15, 6, 7, True),
+                                                      (3, 150_000, 0.02, 17, 3, 40000, True)])
+def test_sharded_find_matches_gpu(oracle_mod, G, n, p, w, world, T, slices):
     """Sharded FindMatches (probe rows to bucket owners, packed-genome allgather, per-rank
-    replay): the ranks' MatchLists in rank order = the oracle's MatchList, bit for bit."""
+    replay): the ranks' MatchLists in rank order = the oracle's MatchList, bit for bit --
+    with genome blocks per rank, or position slices (BASELINE config 5 layout: the packed
+    slices all-gathered into the whole genomes for the chain walks)."""
     seqs = oracle_mod.generate(G, n, p, 4242 + G)
     ref_len, ref_st, ref_stats = oracle_mod.find_matches(seqs, oracle_mod.get_seed(w), table_size=T)
     with tempfile.TemporaryDirectory() as d:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
                "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
                os.path.join(ROOT, "tests", "gpu_shard_find_worker.py"), d, str(G), str(n), str(p), str(w), str(T)]
+        if slices:
+            cmd.append("slices")
         env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
         res = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
         assert res.returncode == 0, res.stderr[-3000:]

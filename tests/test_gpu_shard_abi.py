@@ -10,11 +10,11 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def run(gpu_lib, oracle_mod, G, n, w, p, world, comm, table_size=40000):
+def run(gpu_lib, oracle_mod, G, n, w, p, world, comm, table_size=40000, layout="blocks"):
     seqs = oracle_mod.generate(G, n, p, 500 + G * 11 + world)
     seed = oracle_mod.get_seed(w)
     lengths, starts, st = oracle_mod.find_matches(seqs, seed, table_size=table_size)
-    with gpu_lib.ShardedMemHash([0] * world, comm=comm, table_size=table_size) as sh:
+    with gpu_lib.ShardedMemHash([0] * world, comm=comm, table_size=table_size, layout=layout) as sh:
         sh.SetSeed(seed)
         ml = sh.FindMatches(seqs)
         coll = sum(s["collision_count"] for s in sh.stats_per_rank)
@@ -40,3 +40,11 @@ def test_shard_run_more_ranks_than_genomes(gpu_lib, oracle_mod):
 @pytest.mark.parametrize("G,n,w,p", [(4, 300_000, 15, 0.02), (8, 200_000, 19, 0.01)])
 def test_shard_run_rccl_one_rank(gpu_lib, oracle_mod, G, n, w, p):
     run(gpu_lib, oracle_mod, G, n, w, p, 1, "rccl")
+
+
+@pytest.mark.parametrize("G,n,w,p,world,table_size", [(2, 300_000, 19, 0.02, 2, 40000), (2, 250_000, 15, 0.03, 4, 40000),
+                                                      (3, 200_000, 17, 0.02, 3, 7), (2, 100_003, 13, 0.05, 6, 40000)])
+def test_shard_run_position_slices(gpu_lib, oracle_mod, G, n, w, p, world, table_size):
+    """BASELINE config 5 layout through the ABI: every genome cut into world / G position
+    slices; FindMatches all-gathers the packed slices into the whole genomes."""
+    run(gpu_lib, oracle_mod, G, n, w, p, world, "local", table_size=table_size, layout="slices")

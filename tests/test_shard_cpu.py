@@ -156,6 +156,8 @@ def test_genome_slices_cover_every_position_in_order():
         parts = [(b0, b1) for gg, b0, b1 in sl if gg == g]
         assert parts[0][0] == 0 and parts[-1][1] == n - L + 1
         assert all(parts[i][1] == parts[i + 1][0] for i in range(len(parts) - 1))
+        assert all(b0 % 64 == 0 for b0, _ in parts)   # packed words of a slice = the genome's
+        assert all(abs((b1 - b0) - (n - L + 1) / 4) < 64 for b0, b1 in parts)
     with pytest.raises(ValueError):
         genome_slices(lens, L, 3)
 

@@ -49,15 +49,20 @@ static std::string read_seq(const std::string& path) {
 
 int main(int argc, char** argv) {
     int gpus = 0;        // --gpus N: ShardedMemHash over devices 0..N-1 (RCCL); --local N: one GPU, N ranks
-    bool local = false;
+    bool local = false, slices = false;   // --slices: position slices per rank (else genome blocks)
     if (argc > 2 && (std::string(argv[1]) == "--gpus" || std::string(argv[1]) == "--local")) {
         local = std::string(argv[1]) == "--local";
         gpus = atoi(argv[2]);
         argv += 2;
         argc -= 2;
+        if (argc > 1 && std::string(argv[1]) == "--slices") {
+            slices = true;
+            ++argv;
+            --argc;
+        }
     }
     if (argc < 3) {
-        std::cerr << "usage: mums_find [--gpus N | --local N] gen G n weight p [mask] | files weight f1 f2 ...\n";
+        std::cerr << "usage: mums_find [--gpus N | --local N] [--slices] gen G n weight p [mask] | files weight f1 f2 ...\n";
         return 2;
     }
     std::string mode = argv[1];
@@ -84,7 +89,7 @@ int main(int argc, char** argv) {
             std::fflush(stdout);
             const int saved = dup(1);
             dup2(2, 1);
-            mums::ShardedMemHash sh(devs, local);
+            mums::ShardedMemHash sh(devs, local, slices);
             std::fflush(stdout);
             dup2(saved, 1);
             close(saved);
