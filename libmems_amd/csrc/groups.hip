@@ -30,6 +30,16 @@ namespace {
 constexpr int kGTile = kSegTile;
 constexpr int kGRounds = kGTile / kBlock;
 constexpr int kSlots = kGTile / 2;
+// packed-record probe stage: kGSplit workgroups per sort tile (half the LDS per block,
+// twice the blocks per CU to hide the record loads behind the other blocks' probe work)
+#ifndef MUMS_GROUP_SPLIT
+#define MUMS_GROUP_SPLIT 2
+#endif
+constexpr int kGSplit = MUMS_GROUP_SPLIT;
+constexpr int kGSub = kGTile / kGSplit;
+constexpr int kGSubRounds = kGSub / kBlock;
+constexpr int kSubSlots = kGSub / 2;
+static_assert(kGSub % kBlock == 0 && kGSubRounds * (kBlock / 64) <= 64, "probe sub-tile");
 
 __device__ __forceinline__ uint32_t blk_excl_scan(uint32_t v, uint32_t* s_w, uint32_t* total) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -182,23 +192,25 @@ __global__ __launch_bounds__(kBlock) void probe_tile_rec_kernel(const uint64_t* 
                                                                 uint64_t* __restrict__ slot_info,
                                                                 uint32_t* __restrict__ slot_bucket,
                                                                 DevCounters* __restrict__ ctr) {
-    __shared__ uint64_t srec[kGTile];
-    __shared__ uint16_t heads[kSlots];     // heads of groups of >= 2 records (<= kGTile / 2)
+    constexpr int kGRounds = kGSubRounds;   // this block's part of the tile
+    __shared__ uint64_t srec[kGSub];
+    __shared__ uint16_t heads[kSubSlots];  // heads of groups of >= 2 records (<= kGSub / 2)
     __shared__ uint32_t wcnt[kGRounds * (kBlock / 64)];
     __shared__ uint32_t s_w[kBlock / 64];
     __shared__ uint32_t s_red[2];
     __shared__ uint64_t s_prev, s_next;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const SegTile td = tiles[blockIdx.x];
-    if (td.count == 0) {
+    const SegTile td = tiles[blockIdx.x / kGSplit];
+    const uint32_t part0 = (blockIdx.x % kGSplit) * (uint32_t)kGSub;
+    if (td.count <= part0) {
         if (threadIdx.x == 0) {
             tile_count[blockIdx.x] = 0;
             tile_count[gridDim.x + 32 + blockIdx.x] = 0;
         }
         return;
     }
-    const uint64_t tile0 = td.start;
-    const uint32_t cnt = td.count;
+    const uint64_t tile0 = td.start + part0;
+    const uint32_t cnt = td.count - part0 < (uint32_t)kGSub ? td.count - part0 : (uint32_t)kGSub;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 
     // 1) stage the tile (lane-contiguous, coalesced) + the records just before and after
@@ -242,16 +254,16 @@ __global__ __launch_bounds__(kBlock) void probe_tile_rec_kernel(const uint64_t* 
         if (lane == 0) wcnt[r * (kBlock / 64) + wv] = (uint32_t)__popcll(bal);
     }
     __syncthreads();
-    if (wv == 0) {   // exclusive scan of the kGRounds x waves counts (one wave, 64 entries)
-        static_assert(kGRounds * (kBlock / 64) == 64, "one entry per lane");
-        const uint32_t c0 = wcnt[lane];
+    if (wv == 0) {   // exclusive scan of the kGRounds x waves counts (one wave, <= 64 entries)
+        constexpr int kE = kGRounds * (kBlock / 64);
+        const uint32_t c0 = lane < kE ? wcnt[lane] : 0u;
         uint32_t inc = c0;
         #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
             const uint32_t t = __shfl_up(inc, d, 64);
             if (lane >= d) inc += t;
         }
-        wcnt[lane] = inc - c0;
+        if (lane < kE) wcnt[lane] = inc - c0;
         if (lane == 63) s_red[0] = inc;
     }
     __syncthreads();
@@ -268,7 +280,7 @@ __global__ __launch_bounds__(kBlock) void probe_tile_rec_kernel(const uint64_t* 
     const TileRecViewT<IB> v{(lds_u64*)srec, rec, tile0, cnt};
     const bool fast = mp.repeat_tol == 0 && mp.enum_tol == 1;
     const double inv_t = 1.0 / (double)mp.table_size;
-    const uint64_t sb = (uint64_t)blockIdx.x * kSlots;
+    const uint64_t sb = (uint64_t)blockIdx.x * kSubSlots;
     uint32_t nrep = 0, base = 0;
     for (uint32_t c = 0; c < H; c += kBlock) {
         const uint32_t j = c + threadIdx.x;
@@ -330,10 +342,11 @@ __global__ __launch_bounds__(kBlock) void probe_compact_kernel(const uint32_t* _
                                                                const uint64_t* __restrict__ slot_info,
                                                                const uint32_t* __restrict__ slot_bucket,
                                                                uint64_t* __restrict__ probe_info,
-                                                               uint32_t* __restrict__ probe_bucket) {
+                                                               uint32_t* __restrict__ probe_bucket,
+                                                               uint32_t slots_per_block) {
     const uint32_t n = tile_count[blockIdx.x];
     const uint64_t o = tile_off[blockIdx.x];
-    const uint64_t sb = (uint64_t)blockIdx.x * kSlots;
+    const uint64_t sb = (uint64_t)blockIdx.x * slots_per_block;
     for (uint32_t k = threadIdx.x; k < n; k += kBlock) {
         probe_info[o + k] = slot_info[sb + k];
         probe_bucket[o + k] = slot_bucket[sb + k];
@@ -401,6 +414,7 @@ __global__ __launch_bounds__(kBlock) void gather_rows_kernel(const int64_t* __re
 }  // namespace
 
 uint64_t group_slot_count(uint64_t ntiles) { return ntiles * kSlots; }
+uint64_t group_blocks(uint64_t ntiles, bool packed) { return packed ? ntiles * kGSplit : ntiles; }
 
 template <int MG, typename View>
 hipError_t launch_materialize(View v, const uint64_t* probe_info, uint64_t P, const GenomeTable& gt,
@@ -441,7 +455,7 @@ hipError_t launch_probe_tiles(View v, const SegTile* tiles, uint64_t ntiles, uin
                               uint32_t* slot_bucket, void* counters, hipStream_t st) {
     if (ntiles == 0) return hipSuccess;
     if constexpr (RecIB<View>::value > 0)
-        hipLaunchKernelGGL((probe_tile_rec_kernel<MG, RecIB<View>::value>), dim3((unsigned)ntiles), dim3(kBlock), 0, st, v.rec,
+        hipLaunchKernelGGL((probe_tile_rec_kernel<MG, RecIB<View>::value>), dim3((unsigned)(ntiles * kGSplit)), dim3(kBlock), 0, st, v.rec,
                            tiles, gt, mp, L, tile_count, slot_info, slot_bucket, (DevCounters*)counters);
     else
         hipLaunchKernelGGL((probe_tile_kernel<MG, View>), dim3((unsigned)ntiles), dim3(kBlock), 0, st, v, tiles, N, gt,
@@ -449,12 +463,12 @@ hipError_t launch_probe_tiles(View v, const SegTile* tiles, uint64_t ntiles, uin
     return hipGetLastError();
 }
 
-hipError_t launch_probe_compact(uint64_t ntiles, const uint32_t* tile_count, const uint32_t* tile_off,
+hipError_t launch_probe_compact(uint64_t nblocks, const uint32_t* tile_count, const uint32_t* tile_off,
                                 const uint64_t* slot_info, const uint32_t* slot_bucket, uint64_t* probe_info,
-                                uint32_t* probe_bucket, hipStream_t st) {
-    if (ntiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(probe_compact_kernel, dim3((unsigned)ntiles), dim3(kBlock), 0, st, tile_count, tile_off,
-                       slot_info, slot_bucket, probe_info, probe_bucket);
+                                uint32_t* probe_bucket, hipStream_t st, bool packed) {
+    if (nblocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(probe_compact_kernel, dim3((unsigned)nblocks), dim3(kBlock), 0, st, tile_count, tile_off,
+                       slot_info, slot_bucket, probe_info, probe_bucket, (uint32_t)(packed ? kSubSlots : kSlots));
     return hipGetLastError();
 }
 

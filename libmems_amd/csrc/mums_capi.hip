@@ -220,16 +220,19 @@ template <int MG, typename View>
 int run_groups(mums_ctx* ctx, View v, const SegTile* tiles, uint64_t ntiles, const MatchParams& mp,
                uint64_t* probe_info, uint32_t* probe_bucket, uint64_t* slot_info, uint32_t* slot_bucket,
                hipStream_t st) {
-    uint32_t* counts = ctx->partials.as<uint32_t>();          // [ntiles] probes, then [ntiles] groups
-    uint32_t* gcounts = counts + ntiles + 32;
-    uint32_t* offs = gcounts + ntiles + 32;
+    // one count per probe-stage workgroup: [nb] probes, then [nb] groups, then offsets
+    const bool packed = RecIB<View>::value > 0;
+    const uint64_t nb = group_blocks(ntiles, packed);
+    uint32_t* counts = ctx->partials.as<uint32_t>();
+    uint32_t* gcounts = counts + nb + 32;
+    uint32_t* offs = gcounts + nb + 32;
     DevCounters* dc = ctx->counters.as<DevCounters>();
     HIPCHK((launch_probe_tiles<MG, View>(v, tiles, ntiles, ctx->N, ctx->gt, mp, ctx->L, counts, slot_info, slot_bucket,
                                          dc, st)));
-    HIPCHK(exclusive_scan_u32(gcounts, ntiles, ctx->tmp.p, &dc->ngroups, st));
-    HIPCHK(hipMemcpyAsync(offs, counts, ntiles * 4, hipMemcpyDeviceToDevice, st));
-    HIPCHK(exclusive_scan_u32(offs, ntiles, ctx->tmp.p, &dc->nprobes, st));
-    HIPCHK(launch_probe_compact(ntiles, counts, offs, slot_info, slot_bucket, probe_info, probe_bucket, st));
+    HIPCHK(exclusive_scan_u32(gcounts, nb, ctx->tmp.p, &dc->ngroups, st));
+    HIPCHK(hipMemcpyAsync(offs, counts, nb * 4, hipMemcpyDeviceToDevice, st));
+    HIPCHK(exclusive_scan_u32(offs, nb, ctx->tmp.p, &dc->nprobes, st));
+    HIPCHK(launch_probe_compact(nb, counts, offs, slot_info, slot_bucket, probe_info, probe_bucket, st, packed));
     return MUMS_OK;
 }
 
@@ -565,7 +568,7 @@ struct ProbeSpace {
 int ensure_probe_space(mums_ctx* ctx, uint64_t N, uint64_t ntiles_groups, ProbeSpace* ps) {
     const uint64_t pcap = N / 2 + 1;
     const uint64_t nslots = group_slot_count(ntiles_groups);
-    HIPCHK(ctx->partials.ensure((3 * ntiles_groups + 128) * 4));
+    HIPCHK(ctx->partials.ensure((3 * group_blocks(ntiles_groups, true) + 128) * 4));
     HIPCHK(ctx->pbuf.ensure(pcap * (8 + 4 * 4) + nslots * 12 + 256));
     char* pb = (char*)ctx->pbuf.p;
     ps->probe_info = (uint64_t*)pb;

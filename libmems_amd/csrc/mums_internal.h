@@ -195,13 +195,15 @@ hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key
 
 // groups.hip
 uint64_t group_slot_count(uint64_t ntiles);
+// probe-stage workgroups (= tile_count entries) for ntiles tiles (packed records: split tiles)
+uint64_t group_blocks(uint64_t ntiles, bool packed);
 template <int MG, typename View>
 hipError_t launch_probe_tiles(View v, const SegTile* tiles, uint64_t ntiles, uint64_t N, const GenomeTable& gt,
                               const MatchParams& mp, int L, uint32_t* tile_count, uint64_t* slot_info,
                               uint32_t* slot_bucket, void* counters, hipStream_t st);
-hipError_t launch_probe_compact(uint64_t ntiles, const uint32_t* tile_count, const uint32_t* tile_off,
+hipError_t launch_probe_compact(uint64_t nblocks, const uint32_t* tile_count, const uint32_t* tile_off,
                                 const uint64_t* slot_info, const uint32_t* slot_bucket, uint64_t* probe_info,
-                                uint32_t* probe_bucket, hipStream_t st);
+                                uint32_t* probe_bucket, hipStream_t st, bool packed);
 // probes (key order) -> materialized rows (MatProbes, match_device.h)
 template <int MG, typename View>
 hipError_t launch_materialize(View v, const uint64_t* probe_info, uint64_t P, const GenomeTable& gt,
