@@ -145,6 +145,7 @@ struct mums_ctx {
     uint64_t pattern = 0, N = 0, P = 0, M = 0;
     int sorted_buf = 0;
     int sort_passes = 0;
+    bool parity_masked = false;   // sorted_rec ordered by the masked key only (seg_parity_fix restores)
     const uint64_t* sorted_rec = nullptr;   // packed path
     const void* sorted_key = nullptr;       // pair path
     const uint32_t* sorted_idx = nullptr;
@@ -659,14 +660,19 @@ int merge_stage(mums_ctx* ctx, uint64_t n, int mb, int key_bits, const MatchPara
     int buf = 0;
     if (ib != 32 && !(n < (1ull << 30) && key_bits <= 32))
         return fail(ctx, MUMS_E_UNSUPPORTED, "33-bit records need < 2^30 records per merge");
-    if (ctx->use_onesweep && n < (1ull << 30) && key_bits <= 32)
+    // default tolerances: a masked-key group's probe does not depend on its records' order
+    const bool mask_parity = mp.repeat_tol == 0 && mp.enum_tol == 1;
+    ctx->parity_masked = false;
+    if (ctx->use_onesweep && n < (1ull << 30) && key_bits <= 32) {
         HIPCHK(seg_onesweep_sort(rA, rB, n, key_bits, mb, bstart, ctx->tmp.p, &dc->err, &buf, st,
-                                 prof ? ctx->ev_ds : nullptr, ib));
-    else
+                                 prof ? ctx->ev_ds : nullptr, ib, mask_parity));
+        ctx->parity_masked = mask_parity && seg_onesweep_launches(key_bits) < (key_bits + 7) / 8;
+    } else
         HIPCHK(seg_radix_sort(rA, rB, n, key_bits, tiles, ub, ctx->tmp.p, &buf, st, prof ? ctx->ev_ds : nullptr));
     ctx->sorted_buf = buf;
     ctx->sorted_rec = buf ? rB : rA;
-    ctx->sort_passes = (key_bits + 7) / 8;
+    ctx->sort_passes = (ctx->use_onesweep && n < (1ull << 30) && key_bits <= 32) ? seg_onesweep_launches(key_bits)
+                                                                                : (key_bits + 7) / 8;
     HIPCHK(hipEventRecord(ctx->ev[EV_SORT], st));
     if (ib == 33)
         return groups_dispatch<RecViewT<33>>(ctx, RecViewT<33>{ctx->sorted_rec}, tiles, ub, mp, ps.probe_info,
@@ -683,6 +689,7 @@ int finish_seeds(mums_ctx* ctx, const ProbeSpace& ps, hipStream_t st) {
     HIPCHK(hipStreamSynchronize(st));
     if (ctx->hc.err & 1u) return fail(ctx, MUMS_E_GAP, "Gap in genome sequence ('-' encountered)");
     if (ctx->hc.err & 2u) return fail(ctx, MUMS_E_HIP, "sort look-back timed out (internal error)");
+    if (ctx->hc.err & 16u) return fail(ctx, MUMS_E_HIP, "sort segment fix-up list overflow (internal error)");
     ctx->P = ctx->hc.nprobes;
     ctx->probe_info = ps.probe_info;
     HIPCHK(hipEventRecord(ctx->ev[EV_GROUPS], st));
@@ -848,6 +855,11 @@ int restart_stage(mums_ctx* ctx, const MatchParams& mp, const ProbeSpace& ps, hi
         s.B = B;
         s.kbits = 2 * ctx->w + 1;
         uint64_t* dst = ctx->sorted_buf ? ctx->recA.as<uint64_t>() : ctx->recB.as<uint64_t>();
+        if (ctx->parity_masked) {   // the restart replays SearchRange over the exact SML order
+            HIPCHK(seg_parity_fix(const_cast<uint64_t*>(ctx->sorted_rec), dst, N, s.kbits - B, B, ctx->mstart.as<uint32_t>(), ctx->tmp.p,
+                                  &dc->err, st));
+            ctx->parity_masked = false;
+        }
         HIPCHK(ctx->rsbst.ensure(((1ull << B) + 64) * 4));
         rc = restart_fixup(ctx, s, N, dst, nullptr, ctx->rsbst.as<uint32_t>(), &nl, &changed, st);
         if (rc || !changed) return rc;
@@ -2310,7 +2322,7 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
         (void)hipEventElapsedTime(&ms, ctx->ev[a], ctx->ev[b]);
         return (double)ms;
     };
-    const int npass = (31 + 7) / 8;
+    const int npass = seg_onesweep_launches(31);
     for (uint32_t c = 0; c < nch; ++c) {
         const uint32_t dlo = c * nbc;
         uint64_t n_c = 0;
@@ -2332,7 +2344,7 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
         HIPCHK(build_seg_tiles_from_starts(bstart, mb, n_c, tiles, &dc->ntiles, ctx->tmp.p, st));
         int buf = 0;
         HIPCHK(seg_onesweep_sort(rA, rB, n_c, 31, mb, bstart, ctx->tmp.p, &dc->err, &buf, st,
-                                 prof ? ctx->ev_ds : nullptr, 33));
+                                 prof ? ctx->ev_ds : nullptr, 33, mp.repeat_tol == 0 && mp.enum_tol == 1));
         ctx->sorted_buf = buf;
         ctx->sorted_rec = buf ? rB : rA;
         HIPCHK(hipEventRecord(ctx->ev[EV_SORT], st));

@@ -191,7 +191,16 @@ size_t onesweep_tmp_bytes(uint64_t n, int msd_bits, int key_bits);
 // key_shift: first key bit of the records (32; 33 in the chunked mode)
 hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key_bits, int msd_bits,
                              const uint32_t* d_bstart, void* d_tmp, uint32_t* d_err, int* out_buf, hipStream_t st,
-                             hipEvent_t* ev_ds = nullptr, int key_shift = 32);
+                             hipEvent_t* ev_ds = nullptr, int key_shift = 32, bool mask_parity = false);
+// mask_parity: the segment fix-up leaves key bit 0 (the parity / orientation bit) out of
+// the last digit, so equal masked keys keep index order; seg_parity_fix then sorts every
+// masked-key group of such a stream by that bit (d_tmp: seg_parity_fix_tmp_bytes(n))
+size_t seg_parity_fix_tmp_bytes(uint64_t n);
+hipError_t seg_parity_fix(uint64_t* rec, uint64_t* scratch, uint64_t n, int key_bits, int msd_bits,
+                          const uint32_t* d_bstart, void* d_tmp, uint32_t* d_err, hipStream_t st, int key_shift = 32);
+// onesweep launches of seg_onesweep_sort for key_bits (the lowest digit of a >= 2-digit
+// key is finished by the segment fix-up unless MUMS_DEV_SEGFIX=0)
+int seg_onesweep_launches(int key_bits);
 
 // groups.hip
 uint64_t group_slot_count(uint64_t ntiles);

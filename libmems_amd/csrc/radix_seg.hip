@@ -13,6 +13,8 @@
 // ranking, LDS reorder, digit-run-contiguous stores).
 // HBM bytes per record per pass: upsweep 8, downsweep 8 + 8.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 
 #include "mums_internal.h"
 
@@ -706,7 +708,322 @@ __global__ __launch_bounds__(OB) __attribute__((amdgpu_waves_per_eu(4))) void se
     }
 }
 
+// ---------------------------------------------------------------------------------
+// Segment fix-up: the last step of the onesweep sort, in place of the pass over the
+// lowest key digit.  After the passes over the higher digits the stream is sorted by
+// (bucket, key bits above the lowest digit) and, inside such a "segment", by global
+// index.  Stable-sorting every segment by its lowest digit completes the order
+// (= the full LSD sort's).  A segment is mostly the copies of ONE seed key in the G
+// genomes; it needs work only when it holds several keys whose digits decrease
+// somewhere ("dirty").  So the step is one coalesced read of the stream plus sparse
+// in-place writes, instead of a 16-B/record pass.
+//
+// The digit compared is (x >> dshift) & dmask and the segment prefix (x >> pshift) &
+// pmask.  Under the default tolerances (repeat_tol 0, enum_tol 1) the probe of a masked
+// key group does not depend on the order of its records (one record per genome), so the
+// parity bit (key bit 0: the seed's orientation) is left out of the digit: the stream is
+// then ordered by the masked key, the grouping key of SearchRange, and only segments
+// holding two masked keys out of order are dirty.  seg_parity_fix restores the exact
+// order (parity digit inside each masked-key group) for consumers that need it.
+//
+// A block owns the segments starting in its tile and sees kSfX records past the tile.
+// Per window position the segment starts and the dirty pairs are ballot bitmaps in LDS;
+// the lane holding the first dirty pair of an owned segment finds the segment's bounds
+// in the bitmaps and lists its records; then one lane per listed record computes its
+// stable rank inside the segment (segments of <= 64 records) and stores it.  Longer
+// dirty segments and the owned segment running past the window go to the big list
+// (segfix_big_kernel).  Writes stay inside owned segments, and other blocks read only
+// the prefix of those records (the same for every record of a segment), so the
+// in-place rewrite races with nothing.
+constexpr int kSfTile = 2048;
+constexpr int kSfX = 64;
+constexpr int kSfIPT = (kSfTile + kSfX + 2 + kBlock - 1) / kBlock;   // window slots per thread (strided)
+constexpr int kSfW = kSfIPT * kBlock;                               // window [t0 - 1, t1 + kSfX + 1) fits
+constexpr int kSfWords = kSfW / 64;
+constexpr int kSfReg = 16;    // dirty segments up to this size are ranked in registers
+constexpr int kSfLds = 64;    // dirty segments up to this size are sorted in the block; longer: segfix_big_kernel
+
+struct SfMode {
+    int dshift;
+    uint32_t dmask;
+    int pshift;
+    uint64_t pmask;
+};
+__device__ __forceinline__ uint64_t sf_prefix(uint64_t x, const SfMode& md) { return (x >> md.pshift) & md.pmask; }
+__device__ __forceinline__ uint32_t sf_digit(uint64_t x, const SfMode& md) { return (uint32_t)(x >> md.dshift) & md.dmask; }
+
+__device__ __forceinline__ void sf_push_big(uint32_t p, uint32_t* big_list, uint32_t* big_count, uint32_t cap,
+                                            uint32_t* err) {
+    const uint32_t i = atomicAdd(big_count, 1u);
+    if (i < cap) big_list[i] = p;
+    else atomicOr(err, 16u);
+}
+
+// start of the segment holding window slot r: the highest start bit <= r
+__device__ __forceinline__ int sf_seg_start(const uint64_t* smask, const int16_t* lastw, int r) {
+    const int wi = r >> 6, bi = r & 63;
+    const uint64_t sm = smask[wi] & (bi == 63 ? ~0ull : ((2ull << bi) - 1));
+    return sm ? wi * 64 + 63 - __builtin_clzll(sm) : (int)lastw[wi - 1];   // word 0 holds slot 0's start
+}
+
+__global__ __launch_bounds__(kBlock) void segfix_tile_kernel(uint64_t* rec, uint32_t n, SfMode md,
+                                                             const uint32_t* __restrict__ bstart, int nb,
+                                                             uint32_t* __restrict__ big_list,
+                                                             uint32_t* __restrict__ big_count, uint32_t cap,
+                                                             uint32_t* err, int force_big,
+                                                             unsigned long long* dbg) {
+    __shared__ uint64_t w[kSfW];
+    __shared__ uint64_t smask[kSfWords];   // segment starts (bucket starts first)
+    __shared__ uint64_t dmask[kSfWords];   // dirty pairs (position r: pair (r - 1, r))
+    __shared__ uint64_t sdirty[kSfWords];  // at a segment start: the segment holds a dirty pair
+    __shared__ int16_t lastw[kSfWords], nextw[kSfWords];
+    __shared__ uint32_t jobs[kSfW / 2];    // dirty owned segments (>= 2 records each)
+    __shared__ uint32_t s_njobs;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t t0 = blockIdx.x * kSfTile;
+    const uint32_t t1 = min(t0 + (uint32_t)kSfTile, n);
+    const uint32_t wbeg = t0 ? t0 - 1 : 0;
+    const uint32_t wload = min(t1 + (uint32_t)kSfX + 1, n);
+    const int wn = (int)(wload - wbeg);
+    const long long c0 = clock64();
+    const uint32_t bsv = tid <= nb ? bstart[tid] : 0u;   // issued with the record loads
+    {
+        uint64_t x[kSfIPT];   // all loads in flight before the first LDS store
+        #pragma unroll
+        for (int k = 0; k < kSfIPT; ++k) {
+            const int r = tid + k * kBlock;
+            x[k] = rec[wbeg + (uint32_t)(r < wn ? r : wn - 1)];
+        }
+        if (tid < kSfWords) { smask[tid] = 0; sdirty[tid] = 0; }
+        if (tid == 0) s_njobs = 0;
+        #pragma unroll
+        for (int k = 0; k < kSfIPT; ++k) w[tid + k * kBlock] = x[k];
+    }
+    __syncthreads();
+    const long long c1 = clock64();
+    if (tid <= nb && bsv > wbeg && bsv < wload) atomicOr(&smask[(bsv - wbeg) >> 6], 1ull << ((bsv - wbeg) & 63));
+    for (int b = tid + kBlock; b <= nb; b += kBlock) {
+        const uint32_t p = bstart[b];
+        if (p > wbeg && p < wload) atomicOr(&smask[(p - wbeg) >> 6], 1ull << ((p - wbeg) & 63));
+    }
+    __syncthreads();
+    // slot r = k * 256 + wv * 64 + lane: bitmap word k * 4 + wv, bit lane
+    uint32_t dk = 0;
+    #pragma unroll
+    for (int k = 0; k < kSfIPT; ++k) {
+        const int r = tid + k * kBlock;
+        bool st = false, dirty = false;
+        if (r < wn) {
+            st = r == 0 || ((smask[r >> 6] >> (r & 63)) & 1ull);
+            if (!st) {
+                const uint64_t x = w[r], y = w[r - 1];
+                st = sf_prefix(x, md) != sf_prefix(y, md);
+                dirty = !st && sf_digit(x, md) < sf_digit(y, md);
+            }
+        }
+        const uint64_t sb = __ballot(st), db = __ballot(dirty);
+        dk |= (dirty ? 1u : 0u) << k;
+        if (lane == 0) { smask[k * 4 + wv] = sb; dmask[k * 4 + wv] = db; }   // after every read of word k*4+wv
+    }
+    __syncthreads();
+    const long long c2 = clock64();
+    if (dbg && tid == 0) {
+        atomicAdd(dbg, (unsigned long long)(c1 - c0));
+        atomicAdd(dbg + 1, (unsigned long long)(c2 - c1));
+    }
+    // per bitmap word: the last segment start at or before its end (prefix max) and the
+    // first one at or after its beginning (suffix min): segment bounds in O(1) per slot
+    if (wv == 0) {
+        int ls = -1, fs = kSfW;
+        if (lane < kSfWords) {
+            const uint64_t sm = smask[lane];
+            if (sm) { ls = lane * 64 + 63 - __builtin_clzll(sm); fs = lane * 64 + __builtin_ctzll(sm); }
+        }
+        #pragma unroll
+        for (int dd = 1; dd < 64; dd <<= 1) {
+            const int a = __shfl_up(ls, dd, 64), c = __shfl_down(fs, dd, 64);
+            if (lane >= dd) ls = max(ls, a);
+            if (lane + dd < 64) fs = min(fs, c);
+        }
+        if (lane < kSfWords) { lastw[lane] = (int16_t)ls; nextw[lane] = (int16_t)fs; }
+        const int q = __shfl(ls, kSfWords - 1, 64);   // the window's last segment start
+        if (tid == 0 && wload < n) {   // ... whose segment runs past the window
+            const uint32_t p = wbeg + (uint32_t)q;
+            if (p >= t0 && p < t1) sf_push_big(p, big_list, big_count, cap, err);
+        }
+    }
+    __syncthreads();
+    // a dirty pair marks its segment's start
+    #pragma unroll 1
+    for (int k = 0; k < kSfIPT; ++k) {
+        if (!((dk >> k) & 1u)) continue;
+        const int r = tid + k * kBlock;
+        const int s = sf_seg_start(smask, lastw, r);
+        atomicOr(&sdirty[s >> 6], 1ull << (s & 63));
+    }
+    __syncthreads();
+    // owned dirty segments -> jobs (the lane at the segment start), big ones -> big list
+    #pragma unroll 1
+    for (int k = 0; k < kSfIPT; ++k) {
+        const int r = tid + k * kBlock;
+        const int wi = k * (kBlock / 64) + wv;   // uniform in the wave
+        if (!__ballot(r < wn)) break;
+        const uint64_t sm = smask[wi];
+        const uint64_t smb = sm & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
+        const int s = smb ? wi * 64 + 63 - __builtin_clzll(smb) : (int)lastw[wi > 0 ? wi - 1 : 0];
+        if (r >= wn || !((sdirty[s >> 6] >> (s & 63)) & 1ull)) continue;
+        const uint32_t ps = wbeg + (uint32_t)s;
+        if (ps < t0 || ps >= t1) continue;   // not owned
+        const uint64_t sa = lane == 63 ? 0ull : (sm & (~0ull << (lane + 1)));
+        int e = sa ? wi * 64 + __builtin_ctzll(sa) : (wi + 1 < kSfWords ? (int)nextw[wi + 1] : kSfW);
+        if (e >= wn) {
+            if (wload < n) continue;   // open: the big kernel sorts it
+            e = wn;                    // the stream's last segment
+        }
+        const int m = e - s;
+        if (m > kSfLds || (force_big == 1 && (ps & 63u) == 0u)) {   // force_big: test knob
+            if (r == s) sf_push_big(ps, big_list, big_count, cap, err);
+            continue;
+        }
+        if (r == s) {   // one job per segment: (start << 7 | size)
+            if (dbg) { atomicAdd(dbg + 2, 1ull); atomicAdd(dbg + 3, (unsigned long long)m); }
+            jobs[atomicAdd(&s_njobs, 1u)] = ((uint32_t)s << 7) | (uint32_t)m;
+        }
+    }
+    __syncthreads();
+    // one lane per dirty segment: up to kSfReg records ranked in registers, longer ones
+    // (<= kSfLds) from LDS
+    const uint32_t nj = force_big == 3 ? 0u : s_njobs;
+    for (uint32_t j = tid; j < nj; j += kBlock) {
+        const int s = (int)(jobs[j] >> 7), m = (int)(jobs[j] & 127u);
+        const uint32_t ps = wbeg + (uint32_t)s;
+        if (m <= kSfReg) {
+            uint64_t y[kSfReg];
+            uint32_t d[kSfReg];
+            #pragma unroll
+            for (int u = 0; u < kSfReg; ++u) {
+                y[u] = w[min(s + u, kSfW - 1)];
+                d[u] = u < m ? sf_digit(y[u], md) : 0xFFFFFFFFu;   // past the end: never smaller
+            }
+            #pragma unroll
+            for (int i = 0; i < kSfReg; ++i) {
+                uint32_t rank = 0;
+                #pragma unroll
+                for (int u = 0; u < kSfReg; ++u)
+                    rank += (d[u] < d[i] || (d[u] == d[i] && u < i)) ? 1u : 0u;
+                if (i < m && force_big != 2) rec[ps + rank] = y[i];
+            }
+        } else {
+            for (int i = 0; i < m; ++i) {
+                const uint64_t x = w[s + i];
+                const uint32_t di = sf_digit(x, md);
+                uint32_t rank = 0;
+                for (int u = 0; u < m; ++u) {
+                    const uint32_t du = sf_digit(w[s + u], md);
+                    rank += (du < di || (du == di && u < i)) ? 1u : 0u;
+                }
+                if (force_big != 2) rec[ps + rank] = x;
+            }
+        }
+    }
+}
+
+// Big-list segments (long repeats, N runs, and the segment running past a window): one
+// block per segment finds its end, checks whether it is dirty, and if so sorts it stably
+// by the digit through the scratch buffer (the sort's free ping-pong buffer).
+__global__ __launch_bounds__(kBlock) void segfix_big_kernel(uint64_t* rec, uint64_t* scratch, uint32_t n, SfMode md,
+                                                            const uint32_t* __restrict__ bstart, int nb,
+                                                            const uint32_t* __restrict__ big_list,
+                                                            const uint32_t* __restrict__ big_count, uint32_t cap) {
+    __shared__ uint32_t base[256];
+    __shared__ uint32_t wc[kBlock / 64][256];
+    __shared__ uint32_t s_e, s_dirty;
+    const int tid = threadIdx.x, wv = tid >> 6;
+    const uint32_t cnt = min(*big_count, cap);
+    for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
+        const uint32_t s = big_list[k];
+        // end of the bucket holding s: first bucket start > s (bstart[nb] = n)
+        int lo = 0, hi = nb;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (bstart[mid] > s) hi = mid;
+            else lo = mid + 1;
+        }
+        const uint32_t bend = min(bstart[lo], n);
+        if (tid == 0) { s_e = bend; s_dirty = 0; }
+        base[tid] = 0;
+        __syncthreads();
+        const uint64_t ps = sf_prefix(rec[s], md);
+        for (uint32_t q0 = s + 1; q0 < bend; q0 += kBlock) {
+            const uint32_t q = q0 + tid;
+            if (q < bend && sf_prefix(rec[q], md) != ps) atomicMin(&s_e, q);
+            __syncthreads();
+            if (s_e < q0 + kBlock) break;   // uniform: read after the barrier (later minima are larger)
+        }
+        const uint32_t e = s_e;
+        for (uint32_t q = s + 1 + tid; q < e; q += kBlock)
+            if (sf_digit(rec[q], md) < sf_digit(rec[q - 1], md)) s_dirty = 1u;
+        __syncthreads();
+        if (!s_dirty) continue;   // uniform
+        for (uint32_t q = s + tid; q < e; q += kBlock) atomicAdd(&base[sf_digit(rec[q], md)], 1u);
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t acc = s;
+            for (int d = 0; d < 256; ++d) { const uint32_t c = base[d]; base[d] = acc; acc += c; }
+        }
+        __syncthreads();
+        for (uint32_t c = s; c < e; c += kBlock) {
+            const uint32_t q = c + tid;
+            const bool valid = q < e;
+            const uint64_t x = valid ? rec[q] : 0ull;
+            const uint32_t d = sf_digit(x, md);
+            #pragma unroll
+            for (int w = 0; w < kBlock / 64; ++w) wc[w][tid] = 0;
+            __syncthreads();
+            uint32_t tot;
+            const uint32_t rk = wave_match_rank<8>(d, valid, &tot);
+            if (valid && rk == 0) wc[wv][d] = tot;
+            __syncthreads();
+            if (valid) {
+                uint32_t pre = 0;
+                #pragma unroll
+                for (int w = 0; w < kBlock / 64; ++w) pre += (w < wv) ? wc[w][d] : 0u;
+                scratch[base[d] + pre + rk] = x;
+            }
+            __syncthreads();
+            uint32_t add = 0;
+            #pragma unroll
+            for (int w = 0; w < kBlock / 64; ++w) add += wc[w][tid];
+            base[tid] += add;
+            __syncthreads();
+        }
+        __threadfence();
+        __syncthreads();
+        for (uint32_t q = s + tid; q < e; q += kBlock) rec[q] = scratch[q];
+        __syncthreads();
+    }
+}
+
 }  // namespace
+
+// MUMS_DEV_SEGFIX=1: the lowest digit of a sort of >= 2 digits is finished by the segment
+// fix-up instead of an onesweep pass (=2: every dirty segment through segfix_big_kernel,
+// for tests).  Off by default: on BASELINE config 3 the fix-up costs what the pass it
+// replaces costs.
+bool seg_segfix_enabled() {
+    const char* e = getenv("MUMS_DEV_SEGFIX");
+    return e && (e[0] == '1' || e[0] == '2' || e[0] == '3' || e[0] == '4');
+}
+
+static int seg_segfix_force_big() {   // 1: forced big path; 2 / 3: timing experiments (results wrong)
+    const char* e = getenv("MUMS_DEV_SEGFIX");
+    return (e && e[0] == '2') ? 1 : (e && e[0] == '3') ? 2 : (e && e[0] == '4') ? 3 : 0;
+}
+
+int seg_onesweep_launches(int key_bits) {
+    const int npass = (key_bits + 7) / 8;
+    return (npass >= 2 && seg_segfix_enabled()) ? npass - 1 : npass;
+}
 
 uint64_t seg_tiles_upper(uint64_t n, int msd_bits, uint32_t tile) { return (n + tile - 1) / tile + (1ull << msd_bits) + 1; }
 
@@ -789,21 +1106,77 @@ hipError_t build_seg_tiles(const uint32_t* d_hist_scanned, uint32_t T, int msd_b
 
 // d_tmp layout: status [npass][ub][256] | ghist [nb][npass][256] | dbase [nb][npass][256]
 // | counters [npass] (all zeroed per sort) | sort tiles [ub] | tile-build scratch
+// scratch of build_seg_tiles_from_starts (tfirst + scan), rounded to 256 B
+static size_t seg_build_tmp_bytes(uint64_t nb) { return ((nb + 128) * 4 + scan_tmp_bytes(nb + 1) + 4096 + 255) & ~(size_t)255; }
+
+// big-list capacity of the segment fix-up: <= 1 open segment per tile, < n / 64 dirty
+// segments of more than kSfLds records, + the forced test entries (starts at multiples of 64)
+static uint64_t segfix_cap(uint64_t n) { return n / 32 + 2 * ((n + kSfTile - 1) / kSfTile + 2); }
+
 size_t onesweep_tmp_bytes(uint64_t n, int msd_bits, int key_bits) {
     const uint64_t ub = seg_tiles_upper(n, msd_bits, kSortTile);
     const int npass = (key_bits + 7) / 8;
     const uint64_t nb = 1ull << msd_bits;
     return (ub * kDigits * (uint64_t)npass + 2 * nb * npass * kDigits + 64 + 64) * 4 + ub * sizeof(SegTile) + 256 +
-           (nb + 128) * 4 + scan_tmp_bytes(nb + 1) + 4096;
+           seg_build_tmp_bytes(nb) + segfix_cap(n) * 4 + 256;   // + the segment fix-up's big list
+}
+
+// segment fix-up launches: big_count[0..1] zeroed by the caller, big_list in d_list
+static hipError_t launch_segfix(uint64_t* rec, uint64_t* scratch, uint64_t n, const SfMode& md, const uint32_t* d_bstart,
+                                int nb, uint32_t* big_count, void* d_list, uint32_t* d_err, hipStream_t st) {
+    const uint64_t tiles = (n + kSfTile - 1) / kSfTile;
+    const uint32_t cap = (uint32_t)segfix_cap(n);
+    uint32_t* big_list = (uint32_t*)d_list;
+    unsigned long long* dbg = nullptr;
+    const bool stats = getenv("MUMS_DEV_SEGFIX_STATS") != nullptr;
+    if (stats) {   // development: per-phase cycles and job counts
+        dbg = (unsigned long long*)(big_count + 2);   // 8-aligned (big_count = counters + 48 or d_tmp)
+        (void)hipMemsetAsync(dbg, 0, 32, st);
+    }
+    hipLaunchKernelGGL(segfix_tile_kernel, dim3((unsigned)tiles), dim3(kBlock), 0, st, rec, (uint32_t)n, md, d_bstart,
+                       nb, big_list, big_count, cap, d_err, seg_segfix_force_big(), dbg);
+    hipLaunchKernelGGL(segfix_big_kernel, dim3(256), dim3(kBlock), 0, st, rec, scratch, (uint32_t)n, md, d_bstart, nb,
+                       big_list, big_count, cap);
+    if (stats) {   // development: big-list length per fix-up
+        uint32_t hc[2] = {0, 0};
+        unsigned long long hd[4] = {0, 0, 0, 0};
+        (void)hipMemcpyAsync(hc, big_count, 8, hipMemcpyDeviceToHost, st);
+        (void)hipMemcpyAsync(hd, dbg, 32, hipMemcpyDeviceToHost, st);
+        (void)hipStreamSynchronize(st);
+        fprintf(stderr, "segfix: n=%llu tiles=%llu dmask=%u big=%u forced=%u cyc/block load=%.0f flags=%.0f jobs=%llu job_recs=%llu\n",
+                (unsigned long long)n, (unsigned long long)tiles, md.dmask, hc[0], hc[1], hd[0] / (double)tiles,
+                hd[1] / (double)tiles, hd[2], hd[3]);
+    }
+    return hipGetLastError();
+}
+
+size_t seg_parity_fix_tmp_bytes(uint64_t n) { return 256 + segfix_cap(n) * 4 + 256; }
+
+hipError_t seg_parity_fix(uint64_t* rec, uint64_t* scratch, uint64_t n, int key_bits, int msd_bits,
+                          const uint32_t* d_bstart, void* d_tmp, uint32_t* d_err, hipStream_t st, int key_shift) {
+    if (n == 0 || key_bits < 2) return hipSuccess;
+    SfMode md;
+    md.dshift = key_shift;
+    md.dmask = 1u;
+    md.pshift = key_shift + 1;
+    md.pmask = (1ull << (key_bits - 1)) - 1;
+    uint32_t* big_count = (uint32_t*)d_tmp;
+    hipError_t e = hipMemsetAsync(big_count, 0, 64, st);
+    if (e != hipSuccess) return e;
+    return launch_segfix(rec, scratch, n, md, d_bstart, 1 << msd_bits, big_count, (char*)d_tmp + 256, d_err, st);
 }
 
 hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key_bits, int msd_bits,
                              const uint32_t* d_bstart, void* d_tmp, uint32_t* d_err, int* out_buf, hipStream_t st,
-                             hipEvent_t* ev_ds, int key_shift) {
-    const int npass = (key_bits + 7) / 8;
+                             hipEvent_t* ev_ds, int key_shift, bool mask_parity) {
+    const int nkd = (key_bits + 7) / 8;                  // key digits
+    const bool segfix = nkd >= 2 && seg_segfix_enabled();
+    const int npass = segfix ? nkd - 1 : nkd;            // onesweep launches (digits above the lowest)
+    const int digit_shift = key_shift;                   // the lowest digit
+    if (segfix) key_shift += 8;
     *out_buf = npass % 2;
     if (n == 0 || npass == 0) return hipSuccess;
-    if (npass > 4) return hipErrorInvalidValue;
+    if (nkd > 4) return hipErrorInvalidValue;
     const uint64_t nb = 1ull << msd_bits;
     const uint64_t ub = seg_tiles_upper(n, msd_bits, kSortTile);
     uint32_t* status = (uint32_t*)d_tmp;                       // [npass][ub][256]
@@ -865,6 +1238,18 @@ hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key
         uint64_t* t = src;
         src = dst;
         dst = t;
+    }
+    if (segfix) {   // src holds the stream sorted above the lowest digit; dst is free scratch
+        if (ev_ds) (void)hipEventRecord(ev_ds[2 * npass], st);
+        SfMode md;
+        md.dshift = mask_parity ? digit_shift + 1 : digit_shift;
+        md.dmask = mask_parity ? 0x7Fu : 0xFFu;
+        md.pshift = digit_shift + 8;
+        md.pmask = (1ull << (key_bits - 8)) - 1;
+        e = launch_segfix(src, dst, n, md, d_bstart, (int)nb, counters + 48, (char*)btmp + seg_build_tmp_bytes(nb),
+                          d_err, st);
+        if (e != hipSuccess) return e;
+        if (ev_ds) (void)hipEventRecord(ev_ds[2 * npass + 1], st);
     }
     return hipSuccess;
 }
