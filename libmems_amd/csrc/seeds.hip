@@ -347,6 +347,40 @@ __global__ void keys_of_genome_kernel(SeedSpec ss, const uint32_t* __restrict__ 
                       : k;                                          // ckey = v << 1 | parity (same order)
 }
 
+
+// Patterns with compiled-in run tables: ranks 0-2 of getSeed(11..19) (SeedMasks.h; the
+// default weights of genomes up to ~2 Gbp and ProgressiveAligner's seed families,
+// ProgressiveAligner.cpp:619-625).  Any other pattern takes its run table from the kernel
+// argument (SeedSpec); the output is the same.
+#if MUMS_FEW_STATIC_SEEDS   // A/B build: only the BASELINE seeds compiled in
+constexpr uint64_t kStaticSeeds[] = {kSeedW19, kSeedW15};
+#else
+constexpr uint64_t kStaticSeeds[] = {
+    kSeedW19, 0x7d6735full, 0x1edd74full,                 // w19
+    0x3E6B59Full, 0x3EB335Full, 0x7B3566Full,             // w18
+    0x6dbedbull,                                          // w17
+    0xf599afull, 0xEE5A77ull, 0x7CD59Full,                // w16
+    kSeedW15, 0x7b2a6full, 0x79aacfull,                   // w15
+    0x1e6acfull, 0xF59AFull, 0x3D4CAFull,                 // w14
+    0x792a4full, 0x1d64d7ull, 0x1d3597ull,                // w13
+    0x7954full, 0x3D32Full, 0x768B7ull,                   // w12 (rank 0 = w11's)
+    0x75257ull, 0x1c9527ull,                              // w11 ranks 1-2
+};
+#endif
+constexpr int kNumStaticSeeds = (int)(sizeof(kStaticSeeds) / sizeof(kStaticSeeds[0]));
+
+// calls f(std::integral_constant<uint64_t, PAT>) with PAT = pattern when it is compiled in,
+// else PAT = 0 (run table from the argument)
+template <int I = 0, class F>
+void with_static_seed(uint64_t pattern, F&& f) {
+    if constexpr (I == kNumStaticSeeds) {
+        f(std::integral_constant<uint64_t, 0>{});
+    } else {
+        if (pattern == kStaticSeeds[I]) f(std::integral_constant<uint64_t, kStaticSeeds[I]>{});
+        else with_static_seed<I + 1>(pattern, f);
+    }
+}
+
 }  // namespace
 
 hipError_t launch_seed_pack(const SeedSpec& ss, const GenomeTable& gt, const char* const* d_ascii,
@@ -363,13 +397,11 @@ hipError_t launch_seed_pack(const SeedSpec& ss, const GenomeTable& gt, const cha
             hipLaunchKernelGGL((seed_pack_kernel<0, uint32_t>), dim3(ntiles), dim3(kBlock), 0, st, ss, gt, ap,
                                d_packed, (uint32_t*)d_ckey, 0, d_hist, ntiles, d_err);
     } else {
-#define MUMS_PACK1(PAT)                                                                                  \
-    hipLaunchKernelGGL((seed_pack_kernel<1, uint64_t, PAT>), dim3(ntiles), dim3(kBlock), 0, st, ss, gt, ap, d_packed, \
-                       (uint64_t*)nullptr, msd_bits, d_hist, ntiles, d_err)
-        if (ss.pattern == kSeedW19) MUMS_PACK1(kSeedW19);
-        else if (ss.pattern == kSeedW15) MUMS_PACK1(kSeedW15);
-        else MUMS_PACK1(0);
-#undef MUMS_PACK1
+        with_static_seed(ss.pattern, [&](auto pc) {
+            constexpr uint64_t PAT = decltype(pc)::value;
+            hipLaunchKernelGGL((seed_pack_kernel<1, uint64_t, PAT>), dim3(ntiles), dim3(kBlock), 0, st, ss, gt, ap,
+                               d_packed, (uint64_t*)nullptr, msd_bits, d_hist, ntiles, d_err);
+        });
     }
     return hipGetLastError();
 }
@@ -377,27 +409,20 @@ hipError_t launch_seed_pack(const SeedSpec& ss, const GenomeTable& gt, const cha
 hipError_t launch_seed_scatter(const SeedSpec& ss, const GenomeTable& gt, const uint32_t* d_packed, int msd_bits,
                                const uint32_t* d_hist_scanned, uint32_t ntiles, uint64_t* d_rec, hipStream_t st) {
     if (ntiles == 0) return hipSuccess;
-    const uint64_t pat = (ss.pattern == kSeedW19 || ss.pattern == kSeedW15) ? ss.pattern : 0;
-#define MUMS_SCATTER(PAT)                                                                                         \
-    do {                                                                                                          \
-        if (msd_bits == 0)                                                                                        \
-            hipLaunchKernelGGL(seed_scatter_flat_kernel<PAT>, dim3(ntiles), dim3(kBlock), 0, st, ss, gt, d_packed, \
-                               d_rec);                                                                            \
-        else                                                                                                      \
-            hipLaunchKernelGGL((seed_scatter_kernel<256, PAT>), dim3(ntiles), dim3(kBlock), 0, st, ss, gt,         \
-                               d_packed, msd_bits, d_hist_scanned, ntiles, d_rec);                                \
-    } while (0)
     if (msd_bits > 8) {
         hipLaunchKernelGGL((seed_scatter_kernel<(1 << kMaxMsdBits), 0>), dim3(ntiles), dim3(kBlock), 0, st, ss, gt,
                            d_packed, msd_bits, d_hist_scanned, ntiles, d_rec);
-    } else if (pat == kSeedW19) {
-        MUMS_SCATTER(kSeedW19);
-    } else if (pat == kSeedW15) {
-        MUMS_SCATTER(kSeedW15);
-    } else {
-        MUMS_SCATTER(0);
+        return hipGetLastError();
     }
-#undef MUMS_SCATTER
+    with_static_seed(ss.pattern, [&](auto pc) {
+        constexpr uint64_t PAT = decltype(pc)::value;
+        if (msd_bits == 0)
+            hipLaunchKernelGGL(seed_scatter_flat_kernel<PAT>, dim3(ntiles), dim3(kBlock), 0, st, ss, gt, d_packed,
+                               d_rec);
+        else
+            hipLaunchKernelGGL((seed_scatter_kernel<256, PAT>), dim3(ntiles), dim3(kBlock), 0, st, ss, gt, d_packed,
+                               msd_bits, d_hist_scanned, ntiles, d_rec);
+    });
     return hipGetLastError();
 }
 
@@ -408,12 +433,15 @@ hipError_t launch_seed_scatter_chunk(const SeedSpec& ss, const GenomeTable& gt, 
                                      uint64_t* d_rec, hipStream_t st, const uint64_t* d_cbase, int mb) {
     if (ntiles == 0) return hipSuccess;
     if (2 * ss.w + 1 - msd_bits != 64 - 33 || msd_bits > 8 || (nbc == 0 && !d_cbase)) return hipErrorInvalidValue;
-#define MUMS_SCATTER_C(PAT)                                                                                      \
-    hipLaunchKernelGGL((seed_scatter_kernel<256, PAT, 33, true>), dim3(ntiles), dim3(kBlock), 0, st, ss, gt,     \
-                       d_packed, msd_bits, d_hist_slice, ntiles, d_rec, dlo, nbc, d_cbase, mb)
-    if (ss.pattern == kSeedW19) MUMS_SCATTER_C(kSeedW19);
-    else MUMS_SCATTER_C(0);
-#undef MUMS_SCATTER_C
+    // chunked contexts hold > 2^32 seed-mers: w 16-19 (compiled-in tables for the w19 seeds)
+    const uint64_t pat = (ss.pattern == kSeedW19 || ss.pattern == 0x7d6735full || ss.pattern == 0x1edd74full)
+                             ? ss.pattern : 0;
+    with_static_seed(pat, [&](auto pc) {
+        constexpr uint64_t PAT = decltype(pc)::value;
+        if constexpr (PAT == 0 || seed_runs(PAT).w == 19)
+            hipLaunchKernelGGL((seed_scatter_kernel<256, PAT, 33, true>), dim3(ntiles), dim3(kBlock), 0, st, ss, gt,
+                               d_packed, msd_bits, d_hist_slice, ntiles, d_rec, dlo, nbc, d_cbase, mb);
+    });
     return hipGetLastError();
 }
 

@@ -101,6 +101,18 @@ def test_oracle_parity_shapes(gpu_lib, oracle_mod, G, n, w, rank, p, extra):
     assert st["mem_count"] == ref[2]["mem_count"]
 
 
+# every pattern with a compiled-in run table (seeds.hip kStaticSeeds: ranks 0-2 of
+# getSeed(11..19)) against the oracle; the seed stage of these takes the static kernels
+@pytest.mark.parametrize("w,rank", [(w, r) for w in range(11, 20) for r in range(3)])
+def test_compiled_seed_patterns(gpu_lib, oracle_mod, w, rank):
+    seqs = oracle_mod.generate(3, 60_000, 0.02, 500 + 3 * w + rank)
+    seed = oracle_mod.get_seed(w, rank)
+    ref = oracle_mod.find_matches(seqs, seed)
+    ml, st = gpu_find(gpu_lib, seqs, seed)
+    assert_same(ml, ref)
+    assert st["collision_count"] == ref[2]["collision_count"]
+
+
 def _mutate(rng, s: bytes, alphabet=b"ACGTNRYKMacgtn") -> bytes:
     b = bytearray(s)
     for _ in range(len(b) // 50):
