@@ -37,7 +37,7 @@ from libmems_amd.shard import AbiShardStage, HipShardEngine, ShardedSeedStage, g
 METRIC = "seed-mers/sec sorted+matched (+ MUMs/sec) at 1/2/4/8 MI355X; HBM GB/s vs roofline"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
 # the newest round's PMC summary of the dominant kernel (tools/round_evidence.sh + summarize_profile.py)
-_SUMMARIES = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_dominant_kernel.json")))
+_SUMMARIES = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]*_dominant_kernel.json")))
 PROFILE_SUMMARY = _SUMMARIES[-1] if _SUMMARIES else os.path.join(ROOT, "profiles", "r01_dominant_kernel.json")
 
 
