@@ -23,6 +23,7 @@
 #include <string.h>
 
 #include "mums_oracle.h"
+#include "std_sort.h"
 
 typedef struct {
     int G;
@@ -42,142 +43,11 @@ static int64_t pool_add(pool_t* p) {
 
 static int64_t labs64(int64_t x) { return x < 0 ? -x : x; }
 
-/* ---- libstdc++ std::sort over ids, comp(a, b) = key[a] < key[b] ------------------- */
-static const uint64_t* g_key;   /* key per id (single-threaded test code) */
+/* ---- libstdc++ std::sort over ids, comp(a, b) = key[a] < key[b] (std_sort.h) ----------- */
 static int depth_override = -1;
-#define LT(a, b) (g_key[(a)] < g_key[(b)])
-
-static void swap_u32(uint32_t* a, uint32_t* b) { uint32_t t = *a; *a = *b; *b = t; }
-
-static void move_median_to_first(uint32_t* result, uint32_t* a, uint32_t* b, uint32_t* c) {
-    if (LT(*a, *b)) {
-        if (LT(*b, *c)) swap_u32(result, b);
-        else if (LT(*a, *c)) swap_u32(result, c);
-        else swap_u32(result, a);
-    } else if (LT(*a, *c)) swap_u32(result, a);
-    else if (LT(*b, *c)) swap_u32(result, c);
-    else swap_u32(result, b);
-}
-
-static uint32_t* unguarded_partition(uint32_t* first, uint32_t* last, uint32_t* pivot) {
-    for (;;) {
-        while (LT(*first, *pivot)) ++first;
-        --last;
-        while (LT(*pivot, *last)) --last;
-        if (!(first < last)) return first;
-        swap_u32(first, last);
-        ++first;
-    }
-}
-
-/* stl_heap.h: __push_heap / __adjust_heap / __pop_heap / make_heap / sort_heap */
-static void push_heap(uint32_t* first, int64_t hole, int64_t top, uint32_t value) {
-    int64_t parent = (hole - 1) / 2;
-    while (hole > top && LT(first[parent], value)) {
-        first[hole] = first[parent];
-        hole = parent;
-        parent = (hole - 1) / 2;
-    }
-    first[hole] = value;
-}
-
-static void adjust_heap(uint32_t* first, int64_t hole, int64_t len, uint32_t value) {
-    const int64_t top = hole;
-    int64_t child = hole;
-    while (child < (len - 1) / 2) {
-        child = 2 * (child + 1);
-        if (LT(first[child], first[child - 1])) child--;
-        first[hole] = first[child];
-        hole = child;
-    }
-    if ((len & 1) == 0 && child == (len - 2) / 2) {
-        child = 2 * (child + 1);
-        first[hole] = first[child - 1];
-        hole = child - 1;
-    }
-    push_heap(first, hole, top, value);
-}
-
-static void make_heap(uint32_t* first, uint32_t* last) {
-    const int64_t len = last - first;
-    if (len < 2) return;
-    int64_t parent = (len - 2) / 2;
-    for (;;) {
-        uint32_t value = first[parent];
-        adjust_heap(first, parent, len, value);
-        if (parent == 0) return;
-        parent--;
-    }
-}
-
-static void pop_heap(uint32_t* first, uint32_t* last, uint32_t* result) {
-    uint32_t value = *result;
-    *result = *first;
-    adjust_heap(first, 0, last - first, value);
-}
-
-static void partial_sort_all(uint32_t* first, uint32_t* last) {
-    /* __partial_sort(first, last, last): __heap_select (make_heap; no element after
-     * middle = last) then __sort_heap */
-    make_heap(first, last);
-    while (last - first > 1) {
-        --last;
-        pop_heap(first, last, last);
-    }
-}
-
-static void introsort_loop(uint32_t* first, uint32_t* last, int64_t depth_limit) {
-    while (last - first > 16) {
-        if (depth_limit == 0) {
-            partial_sort_all(first, last);
-            return;
-        }
-        --depth_limit;
-        uint32_t* mid = first + (last - first) / 2;
-        move_median_to_first(first, first + 1, mid, last - 1);
-        uint32_t* cut = unguarded_partition(first + 1, last, first);
-        introsort_loop(cut, last, depth_limit);
-        last = cut;
-    }
-}
-
-static void unguarded_linear_insert(uint32_t* last) {
-    uint32_t val = *last;
-    uint32_t* next = last - 1;
-    while (LT(val, *next)) {
-        *last = *next;
-        last = next;
-        --next;
-    }
-    *last = val;
-}
-
-static void insertion_sort(uint32_t* first, uint32_t* last) {
-    if (first == last) return;
-    for (uint32_t* i = first + 1; i != last; ++i) {
-        if (LT(*i, *first)) {
-            uint32_t val = *i;
-            memmove(first + 1, first, (size_t)(i - first) * sizeof(uint32_t));
-            *first = val;
-        } else {
-            unguarded_linear_insert(i);
-        }
-    }
-}
-
-static int lg64(uint64_t n) { return 63 - __builtin_clzll(n); }
 
 void oracle_std_sort_ids(uint32_t* ids, uint64_t n, const uint64_t* key) {
-    if (n == 0) return;
-    g_key = key;
-    const int64_t depth = depth_override >= 0 ? depth_override : 2 * (int64_t)lg64(n);
-    introsort_loop(ids, ids + n, depth);
-    if (n > 16) {
-        insertion_sort(ids, ids + 16);
-        for (uint32_t* i = ids + 16; i != ids + n; ++i) unguarded_linear_insert(i);
-    } else {
-        insertion_sort(ids, ids + n);
-    }
+    ss_std_sort(key, ids, n, depth_override >= 0 ? depth_override : -1);
 }
 
 void oracle_std_sort_depth_override(int depth) { depth_override = depth; }

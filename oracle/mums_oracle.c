@@ -13,6 +13,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "std_sort.h"
+
 /* ------------------------------------------------------------------------- */
 /* Seed pattern table: SeedMasks.h:44-260 (low words; the high words are 0). */
 /* Rows are weights 0..31, columns seed ranks 0..5; 0 = "no seed".           */
@@ -193,9 +195,20 @@ int oracle_seed_keys(const char* seq, uint64_t n, uint64_t seed, uint64_t* out) 
     return 0;
 }
 
-/* MemorySML::Create: MemorySML.cpp:45-60 (std::sort by key, unstable; here   */
-/* ties are broken by position so the order is deterministic).               */
+/* MemorySML::Create: MemorySML.cpp:45-60 -- std::sort(bmer, bmer_lessthan) of the      */
+/* {position, mer} array FillDnaSeedSML / FillSML fill in position order                 */
+/* (SortedMerList.cpp:771-783).  bmer_lessthan compares the mer only (SortedMerList.h:   */
+/* 311-314), so equal mers stay in the order libstdc++'s introsort leaves them: restated */
+/* in std_sort.h (the comparisons and moves depend on the keys alone, so sorting the     */
+/* position ids by key[id] gives the same permutation as sorting the bmer structs).      */
+/* Rule 1 (default) = that order; rule 0 = ties by position (the order of a stable sort, */
+/* kept only so tests can count the inputs on which the two differ).                      */
 typedef struct { uint64_t key; uint32_t pos; } bmer_t;
+
+static int g_sml_tie_rule = 1;
+
+void oracle_set_sml_tie_rule(int rule) { g_sml_tie_rule = rule; }
+int oracle_get_sml_tie_rule(void) { return g_sml_tie_rule; }
 
 static int bmer_cmp(const void* a, const void* b) {
     const bmer_t* x = (const bmer_t*)a; const bmer_t* y = (const bmer_t*)b;
@@ -205,9 +218,17 @@ static int bmer_cmp(const void* a, const void* b) {
 
 static bmer_t* build_sml(const sml_ctx* c, const uint64_t* keys, uint64_t m) {
     bmer_t* v = (bmer_t*)malloc((m ? m : 1) * sizeof(bmer_t));
-    for (uint64_t p = 0; p < m; ++p) { v[p].key = keys[p]; v[p].pos = (uint32_t)p; }
-    qsort(v, m, sizeof(bmer_t), bmer_cmp);
     (void)c;
+    if (g_sml_tie_rule == 0) {
+        for (uint64_t p = 0; p < m; ++p) { v[p].key = keys[p]; v[p].pos = (uint32_t)p; }
+        qsort(v, m, sizeof(bmer_t), bmer_cmp);
+        return v;
+    }
+    uint32_t* ids = (uint32_t*)malloc((m ? m : 1) * sizeof(uint32_t));
+    for (uint64_t p = 0; p < m; ++p) ids[p] = (uint32_t)p;
+    ss_std_sort(keys, ids, m, -1);
+    for (uint64_t i = 0; i < m; ++i) { v[i].key = keys[ids[i]]; v[i].pos = ids[i]; }
+    free(ids);
     return v;
 }
 

@@ -103,6 +103,12 @@ uint64_t oracle_eliminate_overlaps(int G, uint64_t M, const uint64_t* len_in, co
 /* libstdc++ std::sort of ids by key[id] (SingleStartComparator order); depth override for tests */
 void     oracle_std_sort_ids(uint32_t* ids, uint64_t n, const uint64_t* key);
 void     oracle_std_sort_depth_override(int depth);
+/* SML tie order: 1 = libstdc++ std::sort (the reference, default), 0 = by position */
+void     oracle_set_sml_tie_rule(int rule);
+int      oracle_get_sml_tie_rule(void);
+/* SML tie order: 1 = libstdc++ std::sort (the reference, default), 0 = by position */
+void     oracle_set_sml_tie_rule(int rule);
+int      oracle_get_sml_tie_rule(void);
 void     oracle_free(void* p);
 void     oracle_generate(int G, uint64_t n, double p, uint64_t rng_seed, char* out);
 

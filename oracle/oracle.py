@@ -7,6 +7,7 @@ Parity pinning: SURVEY.md Appendix C known-answer md5s (tests/test_oracle_pinnin
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import subprocess
@@ -76,8 +77,24 @@ def lib() -> ctypes.CDLL:
         L.oracle_result_offset_log.argtypes = [vp, vp]
         L.oracle_result_free.argtypes = [vp]
         L.oracle_generate.argtypes = [ctypes.c_int, u64, ctypes.c_double, u64, ctypes.c_char_p]
+        L.oracle_set_sml_tie_rule.argtypes = [ctypes.c_int]
+        L.oracle_get_sml_tie_rule.restype = ctypes.c_int
         _lib = L
     return _lib
+
+
+@contextlib.contextmanager
+def sml_tie_rule(rule: str):
+    """Order of equal seed mers in the oracle's SortedMerLists: "std" (libstdc++ std::sort,
+    MemorySML.cpp:54 -- the reference and the default) or "position" (a stable sort's
+    order, kept only to count the inputs on which the two rules differ)."""
+    L = lib()
+    old = L.oracle_get_sml_tie_rule()
+    L.oracle_set_sml_tie_rule({"std": 1, "position": 0}[rule])
+    try:
+        yield
+    finally:
+        L.oracle_set_sml_tie_rule(old)
 
 
 def get_seed(weight: int, rank: int = 0) -> int:
