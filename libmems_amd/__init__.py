@@ -532,6 +532,7 @@ class ShardedMemHash:
         self.seqs: List[bytes] = []
         self.ranks: List[MemHash] = []
         self.stats_per_rank: List[dict] = []
+        self.rank_status: List[int] = []
         comms = (ctypes.c_void_p * self.world)()
         devs = (ctypes.c_int * self.world)(*self.devices)
         init = self._lib.mums_comm_init_all if comm == "rccl" else self._lib.mums_comm_init_local
@@ -580,10 +581,12 @@ class ShardedMemHash:
             self.ranks.append(mh)
             g0 += cnt
         errs: List[Optional[BaseException]] = [None] * self.world
+        self.rank_status = [MUMS_OK] * self.world   # every rank's mums_shard_run status
 
         def run(r: int) -> None:
             try:
                 rc = self._lib.mums_shard_run(self.ranks[r]._ctx, self._comms[r], stage)
+                self.rank_status[r] = rc
                 if rc != MUMS_OK:
                     msg = self._lib.mums_last_error(self.ranks[r]._ctx).decode() or \
                         self._lib.mums_comm_last_error(self._comms[r]).decode()

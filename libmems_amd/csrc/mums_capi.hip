@@ -55,7 +55,7 @@ struct DevBuf {
         if (!host.p || off + bytes > host.cap) return false;
         release();
         p = (char*)host.p + off;
-        cap = host.cap - off;
+        cap = bytes;   // a larger ensure() reallocates instead of growing into the host
         borrowed = true;
         return true;
     }
@@ -112,6 +112,9 @@ struct mums_ctx {
     // MER_REPEAT_LIMIT restart / FindMatchesFromPosition (restart.hip)
     std::vector<uint64_t> start_points;   // per genome SML start index (empty = all 0)
     DevBuf rsbuf, rsplan, rsbst;
+    DevBuf tiebuf;                        // SML tie order (smlsort.hip)
+    bool ties_fixed = false;              // the stream holds every run of equal keys in std::sort order
+    uint64_t tie_slots = 0;               // slots of the runs replayed by the last run (stats)
     uint64_t restarts = 0;
     std::vector<uint64_t> offset_log;     // start points after every restart (R x G)
     hipEvent_t ev[EV_COUNT] = {};
@@ -644,6 +647,9 @@ int ensure_merge_space(mums_ctx* ctx, uint64_t n, int mb, int key_bits, ProbeSpa
     return ensure_probe_space(ctx, n, ub, ps);
 }
 
+int tie_fix_stream(mums_ctx* ctx, const RsStream& s, uint64_t n, hipStream_t st);
+bool wants_tie_order(const mums_ctx* ctx);
+
 // Merge stage (rows A5-A9): n records in recA, bucket-major over 2^mb buckets whose starts
 // are in ctx->mstart -> stable sort on record key bits [32, 32 + key_bits) inside every
 // bucket (the merged SortedMerList stream) -> equal-key groups -> accepted probes in key order.
@@ -674,6 +680,16 @@ int merge_stage(mums_ctx* ctx, uint64_t n, int mb, int key_bits, const MatchPara
     ctx->sort_passes = (ctx->use_onesweep && n < (1ull << 30) && key_bits <= 32) ? seg_onesweep_launches(key_bits)
                                                                                 : (key_bits + 7) / 8;
     HIPCHK(hipEventRecord(ctx->ev[EV_SORT], st));
+    if (wants_tie_order(ctx) && ib == 32 && !ctx->shard) {
+        RsStream s{};
+        s.kind = 0;
+        s.rec = ctx->sorted_rec;
+        s.bstart = bstart;
+        s.B = mb;
+        s.kbits = 2 * ctx->w + 1;
+        const int rc = tie_fix_stream(ctx, s, n, st);
+        if (rc) return rc;
+    }
     if (ib == 33)
         return groups_dispatch<RecViewT<33>>(ctx, RecViewT<33>{ctx->sorted_rec}, tiles, ub, mp, ps.probe_info,
                                              ps.probe_bucket, ps.slot_info, ps.slot_bucket, st);
@@ -766,6 +782,55 @@ bool have_start_points(const mums_ctx* ctx) {
     return false;
 }
 
+// The std::sort order of equal seed mers (MemorySML::Create, MemorySML.cpp:54) for the runs
+// that matter (smlsort.hip): every run (d_sp == nullptr) or the runs the start points d_sp
+// (rows x G SML indices) fall into.  ck: genome-major sorted keys over the slot space (=
+// global seed-mer indices); the keys in position order come from ckf (per stream record)
+// scattered by the record's global index (rec: packed records, else idx).  On return *tw
+// holds the ids at the flagged slots in std::sort order; *flagged = 0 when nothing matters.
+int tie_order(mums_ctx* ctx, uint64_t n, const uint64_t* ck, const uint64_t* ckf, const uint64_t* rec,
+              const uint32_t* idx, const uint64_t* const* d_sp, const uint64_t* rows, int nsp, TieWs* tw,
+              uint64_t* flagged, hipStream_t st) {
+    const GenomeTable& gt = ctx->gt;
+    *flagged = 0;
+    if (n >= 0xFFFFFFF0ull) return fail(ctx, MUMS_E_UNSUPPORTED, "SortedMerList tie order above 2^32 seed-mers");
+    HIPCHK(ctx->tiebuf.ensure(tie_ws_bytes(n, gt.G)));
+    *tw = tie_ws_layout(ctx->tiebuf.p, n, gt.G);
+    HIPCHK(tie_set_genomes(*tw, gt.base, gt.m, st));
+    HIPCHK(tie_clear_flags(*tw, st));
+    if (nsp == 0) HIPCHK(tie_mark_all(*tw, ck, st));
+    for (int k = 0; k < nsp; ++k) HIPCHK(tie_mark_starts(*tw, ck, d_sp[k], rows[k], st));
+    HIPCHK(tie_prepare(*tw, flagged, st));
+    if (*flagged == 0) return MUMS_OK;
+    HIPCHK(tie_scatter_keys(*tw, ckf, rec, idx, st));
+    HIPCHK(tie_replay(*tw, st));
+    ctx->tie_slots += *flagged;
+    return MUMS_OK;
+}
+
+// Every run of equal keys of the merged stream s (n records) in std::sort order: repeat /
+// enumeration tolerance hash the first copies of a genome in SML order (MemHash.cpp:139-162,
+// MatchFinder.cpp:342-393).  Rewrites the ids of the stream in place.
+int tie_fix_stream(mums_ctx* ctx, const RsStream& s, uint64_t n, hipStream_t st) {
+    HIPCHK(ctx->rsbuf.ensure(restart_ws_bytes(n, ctx->gt.G)));
+    const RestartWs w = restart_ws_layout(ctx->rsbuf.p, n, ctx->gt.G);
+    HIPCHK(launch_restart_smls(s, n, ctx->gt, w, st));
+    TieWs tw{};
+    uint64_t flagged = 0;
+    int rc = tie_order(ctx, n, w.ck, w.ckf, s.kind == 0 ? s.rec : nullptr, s.kind == 0 ? nullptr : s.idx, nullptr,
+                       nullptr, 0, &tw, &flagged, st);
+    if (rc) return rc;
+    if (flagged)
+        HIPCHK(tie_writeback(tw, s.kind == 0 ? const_cast<uint64_t*>(s.rec) : nullptr,
+                             s.kind == 0 ? nullptr : const_cast<uint32_t*>(s.idx), w.inv, st));
+    ctx->ties_fixed = true;
+    return MUMS_OK;
+}
+
+// repeat / enumeration tolerance see the order of a genome's copies (PairwiseMatchFinder
+// hashes single-copy genomes only)
+bool wants_tie_order(const mums_ctx* ctx) { return !ctx->pairwise && (ctx->repeat_tol > 0 || ctx->enum_tol > 1); }
+
 // MER_REPEAT_LIMIT restart (MatchFinder.cpp:253-277) and FindMatchSeeds start points
 // (MemHash.cpp:117-127) on the merged stream s of n records (restart.hip): plan the
 // restarts, then compact the live records in order into dst (records / keys + dst_idx;
@@ -825,6 +890,20 @@ int restart_fixup(mums_ctx* ctx, const RsStream& s, uint64_t n, void* dst_a, uin
     ctx->offset_log.assign(po.nrestarts * Gu, 0);
     if (po.nrestarts) HIPCHK(hipMemcpy(ctx->offset_log.data(), d_rS, po.nrestarts * Gu * 8, hipMemcpyDeviceToHost));
     if (po.nrestarts == 0 && !have_start_points(ctx)) return MUMS_OK;
+    if (!ctx->ties_fixed) {
+        // a start point inside a run of equal keys: which copies live depends on the SML's
+        // std::sort order of that run (GetBreakpoint's FindMer + 1, MatchFinder.cpp:113-121)
+        const uint64_t* sps[2] = {d_S0, d_rS};
+        const uint64_t rws[2] = {1, po.nrestarts};
+        TieWs tw{};
+        uint64_t flagged = 0;
+        int rc = tie_order(ctx, n, w.ck, w.ckf, s.kind == 0 ? s.rec : nullptr, s.kind == 0 ? nullptr : s.idx, sps,
+                           rws, 2, &tw, &flagged, st);
+        if (rc) return rc;
+        if (flagged)
+            HIPCHK(tie_writeback(tw, s.kind == 0 ? const_cast<uint64_t*>(s.rec) : nullptr,
+                                 s.kind == 0 ? nullptr : const_cast<uint32_t*>(s.idx), w.inv, st));
+    }
     uint32_t* d_total = (uint32_t*)d_cnt;
     HIPCHK(launch_restart_compact(s, n, G, w, d_rkey, po.nrestarts, d_rS, d_S0, dst_a, dst_idx, dst_bstart, d_total,
                                   st));
@@ -984,6 +1063,14 @@ int run_pipeline(mums_ctx* ctx, int stage) {
         ctx->sorted_idx = buf ? ctx->vB.as<uint32_t>() : ctx->vA.as<uint32_t>();
         ctx->sort_passes = (kbits + 7) / 8;
         HIPCHK(hipEventRecord(ctx->ev[EV_SORT], st));
+        if (wants_tie_order(ctx)) {
+            RsStream s{};
+            s.kind = ctx->key64 ? 2 : 1;
+            s.key = ctx->sorted_key;
+            s.idx = ctx->sorted_idx;
+            rc = tie_fix_stream(ctx, s, N, st);
+            if (rc) return rc;
+        }
         if (ctx->key64)
             rc = groups_dispatch<PairView<uint64_t>>(ctx, PairView<uint64_t>{(const uint64_t*)ctx->sorted_key,
                                                                              ctx->sorted_idx},
@@ -1022,6 +1109,8 @@ int run_pipeline(mums_ctx* ctx, int stage) {
 int prepare_run(mums_ctx* ctx, const std::vector<uint64_t>& lens) {
     records_live(ctx);
     ctx->stage_done = 0;
+    ctx->ties_fixed = false;
+    ctx->tie_slots = 0;
     ctx->restarts = 0;
     ctx->offset_log.clear();
     ctx->M = ctx->P = 0;
@@ -1153,6 +1242,18 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
                                                          "(overlapping chunk ranges) not reproduced");
     }
     ctx->nchunks = nch;
+    if (N) {   // SML order of the runs the chunk starts fall into (all runs under repeat tolerance)
+        const uint64_t* sps[1] = {cs};
+        const uint64_t rws[1] = {nch};
+        TieWs tw{};
+        uint64_t flagged = 0;
+        const bool all = wants_tie_order(ctx);
+        rc = tie_order(ctx, N, sk, sk, nullptr, sv, all ? nullptr : sps, all ? nullptr : rws, all ? 0 : 1, &tw,
+                       &flagged, st);
+        if (rc) return rc;
+        if (flagged) HIPCHK(tie_slots_out(tw, const_cast<uint32_t*>(sv), st));
+        ctx->ties_fixed = all;
+    }
     int cbits = 0;
     while (((uint64_t)1 << cbits) < (uint64_t)nch) ++cbits;
     if (kbits + cbits > 64) return fail(ctx, MUMS_E_UNSUPPORTED, "ParallelMemHash compat: too many chunks");
@@ -1229,6 +1330,9 @@ int prepare_shard(mums_ctx* ctx) {
     if (rc) return rc;
     if (ctx->enum_tol > 1)
         return fail(ctx, MUMS_E_UNSUPPORTED, "sharded mode: enumeration tolerance > 1 runs single-GPU only");
+    if (ctx->repeat_tol > 0)   // the first copies of a genome follow its whole SML's std::sort order
+        return fail(ctx, MUMS_E_UNSUPPORTED, "sharded mode: repeat tolerance > 0 runs single-GPU only (SortedMerList "
+                                             "tie order)");
     if (2 * ctx->w + 1 > 32 + kMaxMsdBits)
         return fail(ctx, MUMS_E_UNSUPPORTED, "sharded mode needs 2w+1 <= 43 (packed records)");
     GenomeTable& l = ctx->lgt;
@@ -1545,6 +1649,22 @@ int genome_sml(mums_ctx* ctx, uint32_t genome, const uint64_t** sk, const uint32
     }
     *sk = buf ? ctx->smlkB.as<uint64_t>() : ctx->smlkA.as<uint64_t>();
     *sv = buf ? ctx->smlvB.as<uint32_t>() : ctx->smlvA.as<uint32_t>();
+    if (m > 1) {   // equal mers in std::sort order (MemorySML.cpp:54; smlsort.hip)
+        if (m >= 0xFFFFFFF0ull) return fail(ctx, MUMS_E_UNSUPPORTED, "SortedMerList of more than 2^32 seed-mers");
+        HIPCHK(ctx->tiebuf.ensure(tie_ws_bytes(m, 1)));
+        const TieWs tw = tie_ws_layout(ctx->tiebuf.p, m, 1);
+        const uint64_t b0 = 0;
+        HIPCHK(tie_set_genomes(tw, &b0, &m, st));
+        HIPCHK(tie_clear_flags(tw, st));
+        HIPCHK(tie_mark_all(tw, *sk, st));
+        uint64_t flagged = 0;
+        HIPCHK(tie_prepare(tw, &flagged, st));
+        if (flagged) {
+            HIPCHK(hipMemcpyAsync(tw.K, ctx->smlk0.p, m * 8, hipMemcpyDeviceToDevice, st));
+            HIPCHK(tie_replay(tw, st));
+            HIPCHK(tie_slots_out(tw, const_cast<uint32_t*>(*sv), st));
+        }
+    }
     return MUMS_OK;
 }
 
@@ -2160,6 +2280,14 @@ int run_pipeline_pairwise(mums_ctx* ctx, int stage) {
     ctx->sorted_idx = buf ? ctx->vB.as<uint32_t>() : ctx->vA.as<uint32_t>();
     ctx->sort_passes = (kbits + 7) / 8;
     HIPCHK(hipEventRecord(ctx->ev[EV_SORT], st));
+    if (wants_tie_order(ctx)) {   // the odometer runs over the copies in SML order
+        RsStream s{};
+        s.kind = ctx->key64 ? 2 : 1;
+        s.key = ctx->sorted_key;
+        s.idx = ctx->sorted_idx;
+        const int r0 = tie_fix_stream(ctx, s, N, st);
+        if (r0) return r0;
+    }
     int rc = ctx->key64 ? pairwise_rows<uint64_t>(ctx, N, st) : pairwise_rows<uint32_t>(ctx, N, st);
     if (rc) return rc;
     HIPCHK(hipMemcpy(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost));
@@ -2230,6 +2358,9 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
     if (B < 1 || B > 8)
         return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed-mers (chunked mode) needs seed weight 16-19");
     if (N >= (1ull << 33)) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^33 seed-mers per context");
+    if (wants_tie_order(ctx))   // the first copies of a genome follow its SML's std::sort order (smlsort.hip)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "repeat tolerance above 2^32 seed-mers (chunked mode): the SortedMerList "
+                                             "tie order is replayed in a single context only");
     ctx->packed_path = true;
     ctx->key64 = true;
     ctx->msd_bits = B;

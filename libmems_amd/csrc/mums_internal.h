@@ -373,4 +373,44 @@ hipError_t launch_restart_compact(const RsStream& s, uint64_t n, int G, const Re
                                   uint64_t R, const uint64_t* d_rS, const uint64_t* d_S0, void* dst_a, uint32_t* dst_idx,
                                   uint32_t* dst_bstart, uint32_t* d_total, hipStream_t st);
 
+// smlsort.hip: the std::sort order of equal seed mers in every SortedMerList
+// (MemorySML.cpp:54) for flagged runs.  Slot space = genome-major SML slots (= global
+// seed-mer indices); flags: pf[t] = 1 when sorted slots t, t + 1 form a pair of a run that
+// matters.  Usage: tie_set_genomes, tie_clear_flags, tie_mark_all / tie_mark_starts, K filled
+// with the keys in position order (tie_scatter_keys), tie_prepare, tie_replay, then tie_writeback /
+// tie_slots_out.
+struct TieWs {
+    uint64_t n;
+    int G;
+    uint64_t smax;                 // segment capacity per level
+    uint32_t* pf;                  // pair flags (n + 1)
+    uint32_t* ts;                  // exclusive scan of the slot flags (n + 1)
+    uint64_t* K;                   // keys at the slots
+    uint32_t* V;                   // seed-mer ids at the slots
+    uint32_t *fl, *fr, *Lpos, *Rpos;
+    uint8_t* bound;                // partition / genome bounds (leaf pass)
+    void *segA, *segB, *heap;
+    uint32_t *act, *off, *nsw, *ctr;
+    uint64_t* piv;
+    uint64_t *dbase, *dm;          // G + 1 slot bases, SML lengths
+    void* tmp;
+    size_t bytes;
+};
+TieWs tie_ws_layout(void* base, uint64_t n, int G);
+size_t tie_ws_bytes(uint64_t n, int G);
+hipError_t tie_set_genomes(const TieWs& w, const uint64_t* base, const uint64_t* m, hipStream_t st);
+hipError_t tie_clear_flags(const TieWs& w, hipStream_t st);
+hipError_t tie_mark_all(const TieWs& w, const uint64_t* ck, hipStream_t st);
+// d_sp: rows x G start points (SML indices per genome)
+hipError_t tie_mark_starts(const TieWs& w, const uint64_t* ck, const uint64_t* d_sp, uint64_t rows, hipStream_t st);
+// K[global index of stream record j] = ckf[j] (rec: packed records, else idx)
+hipError_t tie_scatter_keys(const TieWs& w, const uint64_t* ckf, const uint64_t* rec, const uint32_t* idx,
+                            hipStream_t st);
+// slot flags scanned; *flagged = slots of flagged runs (0: nothing to replay)
+hipError_t tie_prepare(const TieWs& w, uint64_t* flagged, hipStream_t st);
+hipError_t tie_replay(const TieWs& w, hipStream_t st);
+// stream record j of a flagged run takes the id at its SML slot inv[j] (rec or idx)
+hipError_t tie_writeback(const TieWs& w, uint64_t* rec, uint32_t* idx, const uint32_t* inv, hipStream_t st);
+hipError_t tie_slots_out(const TieWs& w, uint32_t* out, hipStream_t st);
+
 }  // namespace mums

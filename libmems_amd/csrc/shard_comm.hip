@@ -69,6 +69,15 @@ int comm_fail(mums_comm* c, const std::string& m) {
     return MUMS_E_HIP;
 }
 
+// exclusive prefix sums of per-peer byte counts: the block offsets of an all-to-allv's send
+// or receive buffer (blocks in rank order).  Shared by both communicators, so the in-process
+// one (tested on one GPU) checks the same arithmetic the RCCL one runs.
+std::vector<uint64_t> block_offsets(const uint64_t* bytes, int world) {
+    std::vector<uint64_t> off(world + 1, 0);
+    for (int r = 0; r < world; ++r) off[r + 1] = off[r] + bytes[r];
+    return off;
+}
+
 // ---- RCCL ---------------------------------------------------------------------------
 struct RcclComm : mums_comm {
     ncclComm_t nc = nullptr;
@@ -96,14 +105,7 @@ struct RcclComm : mums_comm {
         return MUMS_OK;
     }
     int alltoallv(const void* d_send, const uint64_t* sb, void* d_recv, const uint64_t* rb, hipStream_t st) override {
-        uint64_t so = 0, ro = 0;
-        std::vector<uint64_t> soff(world), roff(world);
-        for (int r = 0; r < world; ++r) {
-            soff[r] = so;
-            roff[r] = ro;
-            so += sb[r];
-            ro += rb[r];
-        }
+        const std::vector<uint64_t> soff = block_offsets(sb, world), roff = block_offsets(rb, world);
         if (sb[rank] != rb[rank]) return comm_fail(this, "alltoallv: self counts differ");
         if (sb[rank] && hipMemcpyAsync((char*)d_recv + roff[rank], (const char*)d_send + soff[rank], sb[rank],
                                        hipMemcpyDeviceToDevice, st) != hipSuccess)
@@ -159,17 +161,15 @@ struct LocalComm : mums_comm {
         sh->dsend[rank] = d_send;
         sh->sbytes[rank].assign(sb, sb + world);
         sh->barrier();
-        uint64_t ro = 0;
+        const std::vector<uint64_t> roff = block_offsets(rb, world);
         int rc = MUMS_OK;
         for (int s = 0; s < world; ++s) {   // source s's block for this rank
-            uint64_t so = 0;
-            for (int p = 0; p < rank; ++p) so += sh->sbytes[s][p];
+            const uint64_t so = block_offsets(sh->sbytes[s].data(), world)[rank];
             const uint64_t nb = sh->sbytes[s][rank];
             if (nb != rb[s]) rc = comm_fail(this, "alltoallv: counts differ");
-            else if (nb && hipMemcpy((char*)d_recv + ro, (const char*)sh->dsend[s] + so, nb, hipMemcpyDefault) !=
+            else if (nb && hipMemcpy((char*)d_recv + roff[s], (const char*)sh->dsend[s] + so, nb, hipMemcpyDefault) !=
                                hipSuccess)
                 rc = comm_fail(this, "alltoallv copy");
-            ro += nb;
         }
         sh->barrier();   // sources stay valid until every rank has copied
         return rc;
@@ -205,6 +205,28 @@ void key_ranges(const std::vector<uint64_t>& tot, int world, std::vector<uint32_
         const int rc_ = (x);         \
         if (rc_ != MUMS_OK) return rc_; \
     } while (0)
+
+// Every rank's status after a local step, before the next collective: a failure on any rank
+// (e.g. mums_shard_merge refusing an input on the rank owning that key range) ends every
+// rank with the lowest failing rank's code instead of leaving the others blocked in the
+// collective.  Ranks that did not fail name the failing rank in mums_comm_last_error.
+int agree(mums_comm* c, int rc, hipStream_t st) {
+    if (c->world == 1) return rc;
+    const uint64_t mine = (uint64_t)(uint32_t)rc;
+    std::vector<uint64_t> all(c->world, 0);
+    const int r2 = c->allgather_u64(&mine, 1, all.data(), st);
+    if (r2 != MUMS_OK) return rc != MUMS_OK ? rc : r2;
+    for (int r = 0; r < c->world; ++r) {
+        const int code = (int)(int32_t)(uint32_t)all[r];
+        if (code == MUMS_OK) continue;
+        if (r != c->rank) c->err = "rank " + std::to_string(r) + " failed (status " + std::to_string(code) + ")";
+        return code;
+    }
+    return MUMS_OK;
+}
+
+// a local step's status: OK, or the step's code (allocation failures as MUMS_E_NOMEM)
+#define AGREE(x) RC(agree(comm, (x), st))
 
 }  // namespace
 
@@ -283,15 +305,18 @@ int mums_shard_run(mums_ctx* ctx, mums_comm* comm, int stage) {
     if (!ctx || !comm) return MUMS_E_INVALID;
     const int W = comm->world, R = comm->rank;
     hipStream_t st = mums::ctx_stream(ctx);
-    if (hipSetDevice(mums::ctx_device(ctx)) != hipSuccess) return MUMS_E_NODEVICE;
-    // 1-4: sharded seed stage
+    int rc = hipSetDevice(mums::ctx_device(ctx)) != hipSuccess ? MUMS_E_NODEVICE : MUMS_OK;
+    // 1-4: sharded seed stage.  Every local step's status is agreed on before the next
+    // collective (agree), so one rank's failure never leaves the others waiting in it.
     uint32_t B = 0;
     uint64_t n_local = 0;
-    RC(mums_shard_msd_bits(ctx, &B, &n_local));
+    if (rc == MUMS_OK) rc = mums_shard_msd_bits(ctx, &B, &n_local);
     const uint32_t nb = 1u << B;
-    if (comm->rec.ensure((n_local + 1) * 8)) return MUMS_E_HIP;
-    std::vector<uint64_t> counts(nb), C((size_t)W * nb);
-    RC(mums_shard_keys(ctx, (uint64_t*)comm->rec.p, n_local + 1, counts.data()));
+    std::vector<uint64_t> counts(nb, 0), C;
+    if (rc == MUMS_OK && comm->rec.ensure((n_local + 1) * 8)) rc = MUMS_E_NOMEM;
+    if (rc == MUMS_OK) rc = mums_shard_keys(ctx, (uint64_t*)comm->rec.p, n_local + 1, counts.data());
+    AGREE(rc);
+    C.assign((size_t)W * nb, 0);
     RC(comm->allgather_u64(counts.data(), nb, C.data(), st));
     std::vector<uint64_t> tot(nb, 0);
     for (int r = 0; r < W; ++r)
@@ -311,18 +336,19 @@ int mums_shard_run(mums_ctx* ctx, mums_comm* comm, int stage) {
             for (uint32_t b = 0; b < cnt; ++b) rb[s] += 8 * sub[(size_t)s * cnt + b];
         uint64_t rtot = 0;
         for (int s = 0; s < W; ++s) rtot += rb[s];
-        if (comm->recv.ensure(rtot + 8)) return MUMS_E_HIP;
+        AGREE(comm->recv.ensure(rtot + 8) ? MUMS_E_NOMEM : MUMS_OK);
         RC(comm->alltoallv(comm->rec.p, sb.data(), comm->recv.p, rb.data(), st));
         merged = (const uint64_t*)comm->recv.p;
     }
-    if (hipStreamSynchronize(st) != hipSuccess) return MUMS_E_HIP;
-    RC(mums_shard_merge(ctx, merged, (uint32_t)W, first, cnt, sub.data()));
+    rc = hipStreamSynchronize(st) != hipSuccess ? MUMS_E_HIP : MUMS_OK;
+    if (rc == MUMS_OK) rc = mums_shard_merge(ctx, merged, (uint32_t)W, first, cnt, sub.data());
+    AGREE(rc);
     if (stage != MUMS_STAGE_ALL) return MUMS_OK;
     // 5-8: sharded FindMatches
     uint32_t T = 0, G = 0;
     RC(mums::ctx_table_genomes(ctx, &T, &G));
-    std::vector<uint64_t> bc(T), BC((size_t)W * T);
-    RC(mums_shard_bucket_counts(ctx, bc.data()));
+    std::vector<uint64_t> bc(T, 0), BC((size_t)W * T);
+    AGREE(mums_shard_bucket_counts(ctx, bc.data()));
     RC(comm->allgather_u64(bc.data(), T, BC.data(), st));
     std::vector<uint64_t> btot(T, 0);
     for (int r = 0; r < W; ++r)
@@ -332,11 +358,13 @@ int mums_shard_run(mums_ctx* ctx, mums_comm* comm, int stage) {
     std::vector<uint32_t> bounds(bf.begin(), bf.end());
     bounds.push_back(T);
     uint64_t P = 0;
-    RC(mums_probe_count(ctx, &P));
     const uint64_t rowb = 8ull * (G + 1);
-    if (comm->rows.ensure((P + 1) * rowb)) return MUMS_E_HIP;
-    std::vector<uint64_t> send(W), S((size_t)W * W);
-    RC(mums_shard_probe_rows(ctx, (uint32_t)W, bounds.data(), (int64_t*)comm->rows.p, P + 1, send.data()));
+    std::vector<uint64_t> send(W, 0), S((size_t)W * W);
+    rc = mums_probe_count(ctx, &P);
+    if (rc == MUMS_OK && comm->rows.ensure((P + 1) * rowb)) rc = MUMS_E_NOMEM;
+    if (rc == MUMS_OK)
+        rc = mums_shard_probe_rows(ctx, (uint32_t)W, bounds.data(), (int64_t*)comm->rows.p, P + 1, send.data());
+    AGREE(rc);
     RC(comm->allgather_u64(send.data(), W, S.data(), st));
     const int64_t* rows = (const int64_t*)comm->rows.p;
     uint64_t nrows = P;
@@ -348,18 +376,20 @@ int mums_shard_run(mums_ctx* ctx, mums_comm* comm, int stage) {
             rb[p] = S[(size_t)p * W + R] * rowb;
             nrows += S[(size_t)p * W + R];
         }
-        if (comm->rrows.ensure((nrows + 1) * rowb)) return MUMS_E_HIP;
+        AGREE(comm->rrows.ensure((nrows + 1) * rowb) ? MUMS_E_NOMEM : MUMS_OK);
         RC(comm->alltoallv(comm->rows.p, sb.data(), comm->rrows.p, rb.data(), st));
         rows = (const int64_t*)comm->rrows.p;
     }
     uint64_t woff = 0, nw = 0, total = 0;
-    RC(mums_shard_packed_info(ctx, &woff, &nw, &total));
-    if (comm->packed_all.ensure((total + 1) * 4) || comm->packed.ensure((nw + 1) * 4)) return MUMS_E_HIP;
-    if (hipMemsetAsync(comm->packed_all.p, 0, (total + 1) * 4, st) != hipSuccess) return MUMS_E_HIP;
-    if (W == 1) {
-        RC(mums_shard_packed_copy(ctx, (uint32_t*)comm->packed_all.p + woff));
-    } else {   // all-gather(v) of the packed slices as an all-to-allv with one block per peer
-        RC(mums_shard_packed_copy(ctx, (uint32_t*)comm->packed.p));
+    rc = mums_shard_packed_info(ctx, &woff, &nw, &total);
+    if (rc == MUMS_OK && (comm->packed_all.ensure((total + 1) * 4) || comm->packed.ensure((nw + 1) * 4)))
+        rc = MUMS_E_NOMEM;
+    if (rc == MUMS_OK && hipMemsetAsync(comm->packed_all.p, 0, (total + 1) * 4, st) != hipSuccess) rc = MUMS_E_HIP;
+    if (rc == MUMS_OK)
+        rc = mums_shard_packed_copy(ctx, W == 1 ? (uint32_t*)comm->packed_all.p + woff : (uint32_t*)comm->packed.p);
+    if (rc == MUMS_OK && W > 1 && comm->rec.ensure((size_t)W * nw * 4 + 8)) rc = MUMS_E_NOMEM;
+    AGREE(rc);
+    if (W > 1) {   // all-gather(v) of the packed slices as an all-to-allv with one block per peer
         std::vector<uint64_t> meta{woff, nw}, M((size_t)2 * W);
         RC(comm->allgather_u64(meta.data(), 2, M.data(), st));
         // every rank sends its slice to every rank; received blocks land in rank order,
@@ -372,17 +402,19 @@ int mums_shard_run(mums_ctx* ctx, mums_comm* comm, int stage) {
             ordered = ordered && M[(size_t)2 * p] == o;
             o += M[(size_t)2 * p + 1];
         }
-        if (!ordered) return comm_fail(comm, "packed slices are not in rank order");
+        if (!ordered) return comm_fail(comm, "packed slices are not in rank order");   // the same on every rank
         // the send buffer is the slice repeated per peer (all-to-allv sends disjoint blocks)
-        if (comm->rec.ensure((size_t)W * nw * 4 + 8)) return MUMS_E_HIP;
-        for (int p = 0; p < W; ++p)
+        rc = MUMS_OK;
+        for (int p = 0; p < W && rc == MUMS_OK; ++p)
             if (nw && hipMemcpyAsync((uint32_t*)comm->rec.p + (size_t)p * nw, comm->packed.p, nw * 4,
                                      hipMemcpyDeviceToDevice, st) != hipSuccess)
-                return MUMS_E_HIP;
+                rc = MUMS_E_HIP;
+        AGREE(rc);
         RC(comm->alltoallv(comm->rec.p, sb.data(), comm->packed_all.p, rb.data(), st));
     }
-    if (hipStreamSynchronize(st) != hipSuccess) return MUMS_E_HIP;
-    return mums_shard_find(ctx, rows, nrows, (const uint32_t*)comm->packed_all.p);
+    rc = hipStreamSynchronize(st) != hipSuccess ? MUMS_E_HIP : MUMS_OK;
+    if (rc == MUMS_OK) rc = mums_shard_find(ctx, rows, nrows, (const uint32_t*)comm->packed_all.p);
+    return agree(comm, rc, st);
 }
 
 }  // extern "C"

@@ -21,8 +21,10 @@ SO = os.path.join(BUILD, "libeo_model.so")
 @pytest.fixture(scope="module")
 def model():
     os.makedirs(BUILD, exist_ok=True)
-    subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", SO, os.path.join(ROOT, "tests", "eo_model.cpp")],
+    tmp = f"{SO}.{os.getpid()}"   # build aside, then rename: parallel workers never load a partial file
+    subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", tmp, os.path.join(ROOT, "tests", "eo_model.cpp")],
                    check=True)
+    os.replace(tmp, SO)
     L = ctypes.CDLL(SO)
     L.model_std_sort.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int]
     L.model_eliminate_overlaps.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,

@@ -24,8 +24,10 @@ def model():
     os.makedirs(BUILD, exist_ok=True)
     src = os.path.join(ROOT, "tests", "restart_model.cpp")
     odir = os.path.join(ROOT, "oracle", "build")
-    subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", SO, src, f"-L{odir}", "-lmums_oracle",
+    tmp = f"{SO}.{os.getpid()}"   # build aside, then rename: parallel workers never load a partial file
+    subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", tmp, src, f"-L{odir}", "-lmums_oracle",
                     f"-Wl,-rpath,{odir}"], check=True)
+    os.replace(tmp, SO)
     L = ctypes.CDLL(SO)
     L.restart_model_check.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_uint64),
                                       ctypes.c_uint64, ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]

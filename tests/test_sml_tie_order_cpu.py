@@ -31,9 +31,11 @@ def model():
     oracle.lib()
     os.makedirs(BUILD, exist_ok=True)
     odir = os.path.join(ROOT, "oracle", "build")
-    subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", SO,
+    tmp = f"{SO}.{os.getpid()}"   # build aside, then rename: parallel workers never load a partial file
+    subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", tmp,
                     os.path.join(ROOT, "tests", "sml_sort_model.cpp"), f"-L{odir}", "-lmums_oracle",
                     f"-Wl,-rpath,{odir}"], check=True)
+    os.replace(tmp, SO)
     L = ctypes.CDLL(SO)
     L.model_sml_positions.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]
     L.model_sml_positions.restype = ctypes.c_int64
