@@ -322,6 +322,40 @@ def main():
                                              "per walk the probe row ((G+1) x 8 B) and its 24-B queue item"}}
         except Exception as e:  # report, never hide
             mums_c3 = {"error": str(e)}
+    elif sharded and args.workload == "c3" and not args.no_mums and hasattr(stage, "run_find"):
+        # MUMs/s of the sharded FindMatches (mums_shard_run, all 8 steps: keys, record
+        # all-to-allv, merge, bucket ranges, row all-to-allv, packed all-gather, chains + replay)
+        # on the same split C3 input: total matches over the ranks / max-over-ranks time
+        try:
+            stage.run_find()   # warm
+            best = float("inf")
+            for _ in range(2):
+                barrier()
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                stage.run_find()
+                torch.cuda.synchronize()
+                barrier()
+                best = min(best, time.perf_counter() - t1)
+            sm = stats()
+            red = torch.tensor([best, float(sm["mem_count"]), float(sm["probes"]), float(sm["collision_count"])],
+                               dtype=torch.float64)
+            tmx = red[:1].clone()
+            if world > 1:
+                dist.all_reduce(tmx, op=dist.ReduceOp.MAX)
+                dist.all_reduce(red, op=dist.ReduceOp.SUM)
+            best = float(tmx.item())
+            matches = int(red[1].item())
+            mums_c3 = {"mums_per_s": matches / best, "matches": matches, "ms": best * 1e3,
+                       "probes": int(red[2].item()), "collisions": int(red[3].item()),
+                       "workload": f"BASELINE config 3: {G} x {n // 10**6} Mbp related p=0.01, w19, full FindMatches "
+                                   f"sharded over {world} rank(s) (mums_shard_run)",
+                       "rank0_phase_ms": {k: round(sm[k], 3) for k in ("ms_chains", "ms_replay", "ms_output")},
+                       "exchange": ("RCCL communicator inside libmums_hip.so (ncclCommInitRank): grouped "
+                                    "ncclSend/ncclRecv all-to-allv, ncclAllGather of counts" if args.exchange == "abi"
+                                    else f"torch.distributed {args.dist_backend} all_to_all (shard.py)")}
+        except Exception as e:  # report, never hide
+            mums_c3 = {"error": str(e)}
     seedmers_total = sum(max(n - lm.getSeedLength(seed) + 1, 0) for _ in range(G))
     seedmers_rank = st["seedmers"]
     key_bytes = st["key_bytes"]

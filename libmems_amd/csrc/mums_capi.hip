@@ -1507,6 +1507,8 @@ int mums_find_stage(mums_ctx* ctx, int stage) {
         return fail(ctx, MUMS_E_UNSUPPORTED, "ParallelMemHash compat with enumeration tolerance > 1");
     if (ctx->genomes.size() > (size_t)kPairMaxG && (ctx->pairwise || ctx->pcompat || ctx->enum_tol > 1))
         return fail(ctx, MUMS_E_UNSUPPORTED, "more than 32 genomes: only MemHash / MaskedMemHash, enum_tol <= 1");
+    if (!ctx->start_points.empty() && ctx->start_points.size() != ctx->genomes.size())   // MatchFinder.cpp:197-199
+        return fail(ctx, MUMS_E_INVALID, "start points: one per sequence required");
     if (have_start_points(ctx) && (big || ctx->pcompat))
         return fail(ctx, MUMS_E_UNSUPPORTED, "start points (FindMatchesFromPosition) in the chunked / compat modes");
     if (ctx->pairwise || ctx->enum_tol > 1) return run_pipeline_pairwise(ctx, stage);
@@ -2038,6 +2040,8 @@ int mums_shard_merge(mums_ctx* ctx, const uint64_t* d_records, uint32_t nsources
     const int B = ctx->msd_bits;
     if (nsources == 0 || (uint64_t)first_bucket + nbuckets > (1ull << B) || (nbuckets && !counts))
         return fail(ctx, MUMS_E_INVALID, "bad shard merge arguments");
+    if (have_start_points(ctx))
+        return fail(ctx, MUMS_E_UNSUPPORTED, "start points (FindMatchesFromPosition) in the sharded mode");
     hipStream_t st = ctx->stream;
     // chunk table: received source-major (each source's buckets in order) -> bucket-major
     std::vector<uint64_t> tot(nbuckets, 0), chunks;

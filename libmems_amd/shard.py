@@ -192,6 +192,12 @@ class ShardedSeedStage:
         dist.all_gather(parts, t, group=self.group)
         return torch.stack(parts).cpu().numpy()
 
+    def run_find(self) -> None:
+        """Steps 1-8 (ShardedFindMatches over the same process group)."""
+        if getattr(self, "_find", None) is None:
+            self._find = ShardedFindMatches(self.engine, self.group)
+        self._find.run()
+
     def run(self) -> None:
         eng = self.engine
         B, n_local = eng.msd_bits()
@@ -324,6 +330,14 @@ class AbiShardStage:
     def run(self) -> None:
         lib = self.engine.mh._lib
         rc = lib.mums_shard_run(self.engine.mh._ctx, self.comm, self.stage)
+        if rc != 0:
+            raise RuntimeError(f"mums_shard_run: {lib.mums_last_error(self.engine.mh._ctx).decode()} / "
+                               f"{lib.mums_comm_last_error(self.comm).decode()}")
+
+    def run_find(self) -> None:
+        """The whole sharded FindMatches (steps 1-8): this rank's buckets of the MatchList."""
+        lib = self.engine.mh._lib
+        rc = lib.mums_shard_run(self.engine.mh._ctx, self.comm, 2)   # MUMS_STAGE_ALL
         if rc != 0:
             raise RuntimeError(f"mums_shard_run: {lib.mums_last_error(self.engine.mh._ctx).decode()} / "
                                f"{lib.mums_comm_last_error(self.comm).decode()}")

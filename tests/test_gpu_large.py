@@ -164,16 +164,51 @@ def test_c5_full_findmatches(gpu_lib, oracle_mod):
     assert st["probes"] == st["mem_count"] + st["collision_count"]
     assert len(ml) > 0 and np.array_equal(ml.lengths, ml2.lengths) and np.array_equal(ml.starts, ml2.starts)
     assert st["chains"] == st2["chains"]
-    # sampled forward entries: the care positions of the first and last seed windows
-    # agree in both genomes (an entry is a chain of seed hits)
+    # sampled forward and reverse entries are maximal seed chains: hits at the
+    # first and last column, none within L columns before the first or after the last
     L = 27
     care = [k for k in range(L) if (seed >> (L - 1 - k)) & 1]
+    a_h, b_h = a.cpu().numpy(), b.cpu().numpy()
     fwd = np.nonzero((ml.starts > 0).all(axis=1))[0]
-    assert len(fwd) > 0
+    rev = np.nonzero((ml.starts[:, 0] > 0) & (ml.starts[:, 1] < 0))[0]
+    assert len(fwd) > 0 and len(rev) > 0
     rng = random.Random(9)
-    for i in rng.sample(list(fwd), min(200, len(fwd))):
-        s0, s1, ln = int(ml.starts[i, 0]) - 1, int(ml.starts[i, 1]) - 1, int(ml.lengths[i])
-        for d in (0, ln - L):
-            x = a[s0 + d:s0 + d + L].cpu().numpy()
-            y = b[s1 + d:s1 + d + L].cpu().numpy()
-            assert all(x[k] == y[k] for k in care)
+    picks = rng.sample(list(fwd), min(200, len(fwd))) + rng.sample(list(rev), min(100, len(rev)))
+    for i in picks:
+        s0, s1, ln = int(ml.starts[i, 0]), int(ml.starts[i, 1]), int(ml.lengths[i])
+        assert is_maximal_chain((a_h, b_h), (s0, s1), ln, L, care), (i, s0, s1, ln)
+    # the check itself rejects a truncated entry
+    i = picks[0]
+    s0, s1, ln = int(ml.starts[i, 0]), int(ml.starts[i, 1]), int(ml.lengths[i])
+    assert not is_maximal_chain((a_h, b_h), (s0, s1 if s1 > 0 else s1 - 1), ln - 1, L, care)
+
+
+_COMP = np.zeros(256, dtype=np.uint8)
+for _x, _y in zip(b"ACGTacgt", b"TGCAtgca"):
+    _COMP[_x] = _y
+
+
+def column_chars(seq, s, ln, c0, c1, pad):
+    """Characters of alignment columns c0..c1 of a component: start s > 0 reads
+    base s - 1 + c, s < 0 the complement of base |s| - 1 + ln - 1 - c; outside -> pad."""
+    cols = np.arange(c0, c1 + 1)
+    pos = (s - 1 + cols) if s > 0 else (-s - 1 + ln - 1 - cols)
+    ok = (pos >= 0) & (pos < len(seq))
+    out = np.full(len(cols), pad, dtype=np.int16)
+    v = seq[pos[ok]]
+    out[ok] = v if s > 0 else _COMP[v]
+    return out
+
+
+def is_maximal_chain(seqs, starts, ln, L, care):
+    """hit(0) and hit(ln - L), and no hit column in [-L, -1] or [ln - L + 1, ln] (a hit within
+    L of the chain's ends would have extended it, MatchFinder.h:218-374)."""
+    c0, c1 = -L, ln
+    x = [column_chars(sq, st, ln, c0, c1 + L - 1, pad=-1 - g) for g, (sq, st) in enumerate(zip(seqs, starts))]
+
+    def hit(c):
+        return all(x[0][c - c0 + k] == x[1][c - c0 + k] for k in care)
+
+    if not (hit(0) and hit(ln - L)):
+        return False
+    return not any(hit(c) for c in list(range(-L, 0)) + list(range(ln - L + 1, ln + 1)))

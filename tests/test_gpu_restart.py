@@ -112,3 +112,14 @@ def test_no_restart_path_untouched(gpu_lib, oracle_mod):
     seqs = oracle_mod.generate(3, 100_000, 0.02, 5)
     st, ref = check(gpu_lib, oracle_mod, seqs, need_restart=False)
     assert st["repeat_limit_groups"] == 0 and st["restarts"] == 0 and ref["restarts"] == 0
+
+
+def test_start_points_count_must_match(gpu_lib, oracle_mod):
+    # MatchFinder::FindMatchSeeds throws InvalidData unless there is one start point per
+    # sequence (MatchFinder.cpp:197-199)
+    seqs = oracle_mod.generate(3, 20_000, 0.02, 9)
+    with gpu_lib.MemHash(0) as mh:
+        mh.SetSeed(oracle_mod.get_seed(15))
+        with pytest.raises(gpu_lib.MumsError) as ei:
+            mh.FindMatchesFromPosition(seqs, [5, 7])
+        assert ei.value.code == gpu_lib.MUMS_E_INVALID
