@@ -33,9 +33,9 @@ namespace mums {
 namespace {
 
 #ifndef MUMS_WALK_BUDGET
-#define MUMS_WALK_BUDGET 2
+#define MUMS_WALK_BUDGET 4
 #endif
-constexpr int kWalkBudget = MUMS_WALK_BUDGET;
+constexpr int kWalkBudget = MUMS_WALK_BUDGET;   // words per lane in chain_walk_short_kernel
 #ifndef MUMS_HIT_BATCH
 #define MUMS_HIT_BATCH 4   // components whose window loads are in flight together (hit_word)
 #endif   // 64-column hit words per lane before a walk goes to a workgroup
@@ -374,79 +374,135 @@ __global__ __launch_bounds__(kBlock) void chain_key_kernel(View v, const uint64_
     lkey[k] = ((uint64_t)line_hash<MG>(Q, gt.G) << 32) | (x & 0xFFFFFFFFull);
 }
 
+// Block-wide append of the items whose want bit is set (kIPT per thread): one atomic per
+// workgroup -- a single queue counter hit by every wave serialises in the L2 atomic unit.
+constexpr int kLinkIPT = 8;
+
+template <int kIPT>
+__device__ __forceinline__ void block_push(uint32_t want, const WalkItem (&it)[kIPT], WalkItem* __restrict__ queue,
+                                           unsigned int* __restrict__ qcount) {
+    __shared__ uint32_t s_w[kBlock / 64 + 1];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t n = (uint32_t)__builtin_popcount(want);
+    uint32_t x = n;
+    #pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    __syncthreads();   // s_w may still be read by the previous call's threads
+    if (lane == 63) s_w[wv] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) {
+            const uint32_t c = s_w[w];
+            s_w[w] = tot;
+            tot += c;
+        }
+        s_w[kBlock / 64] = tot ? atomicAdd(qcount, tot) : 0u;
+    }
+    __syncthreads();
+    uint32_t o = s_w[kBlock / 64] + s_w[wv] + x - n;
+    #pragma unroll
+    for (int i = 0; i < kIPT; ++i)
+        if ((want >> i) & 1u) queue[o++] = it[i];
+}
+
+// Neighbours in line order: same line and gap <= L -> linked without a walk; every other
+// probe queues a walk (bridge to the next probe, or its chain's right end).  The walks run
+// compacted in chain_walk_short_kernel (no lane of a wave idles behind them).
 template <int MG, typename View>
 __global__ __launch_bounds__(kBlock) void chain_link_kernel(View v, const uint64_t* __restrict__ probe_info, uint64_t P,
                                                             GenomeTable gt, MatchParams mp, SeedSpec ss,
-                                                            const uint32_t* __restrict__ ord,
-                                                            const uint32_t* __restrict__ packed,
-                                                            uint8_t* __restrict__ link, int64_t* __restrict__ rcol,
-                                                            WalkItem* __restrict__ queue,
+                                                            uint8_t* __restrict__ link, WalkItem* __restrict__ queue,
                                                             unsigned int* __restrict__ qcount) {
-    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (j >= P) return;
     const int L = ss.L;
-    const LineSpec ls = line_spec(ss, gt);
-    Mhe<MG> A, B;
-    probe_of<MG, View>(v, probe_info, j, gt, mp, L, A);
-    bool same = false;
-    if (j + 1 < P) {
-        probe_of<MG, View>(v, probe_info, j + 1, gt, mp, L, B);
-        same = same_line<MG>(A, B);
-    }
-    const int64_t xa = start_at(A, first_start(A));
-    int64_t clo, chi;
-    frame_bounds<MG>(A, gt, &clo, &chi);
-    int state;
-    if (same) {
-        const int64_t stop = start_at(B, first_start(B)) - xa - L;
-        const int64_t c = walk_lane<MG>(+1, 0, stop, kWalkBudget, A, gt, clo, chi, packed, ss, ls, &state);
-        if (state == 1) {
-            link[j] = 1;
-        } else if (state == 0) {
-            link[j] = 0;
-            rcol[j] = xa + c;
-        } else {
-            link[j] = 0;
-            const unsigned q = atomicAdd(qcount, 1u);
-            queue[q] = WalkItem{(uint32_t)j, 0, c, stop};
+    uint32_t want = 0;
+    WalkItem it[kLinkIPT];
+    #pragma unroll
+    for (int i = 0; i < kLinkIPT; ++i) {
+        const uint64_t j = (uint64_t)blockIdx.x * (kBlock * kLinkIPT) + (uint64_t)i * kBlock + threadIdx.x;
+        it[i] = WalkItem{(uint32_t)j, 1, 0, INT64_MAX};
+        if (j >= P) continue;
+        Mhe<MG> A, B;
+        probe_of<MG, View>(v, probe_info, j, gt, mp, L, A);
+        bool same = false;
+        if (j + 1 < P) {
+            probe_of<MG, View>(v, probe_info, j + 1, gt, mp, L, B);
+            same = same_line<MG>(A, B);
         }
-    } else {
-        link[j] = 0;
-        const int64_t c = walk_lane<MG>(+1, 0, INT64_MAX, kWalkBudget, A, gt, clo, chi, packed, ss, ls, &state);
-        if (state == 0) {
-            rcol[j] = xa + c;
+        uint8_t lk = 0;
+        if (same) {
+            const int64_t stop = start_at(B, first_start(B)) - start_at(A, first_start(A)) - L;
+            if (stop <= 0) lk = 1;
+            else { it[i].kind = 0; it[i].stop = stop; want |= 1u << i; }
         } else {
-            const unsigned q = atomicAdd(qcount, 1u);
-            queue[q] = WalkItem{(uint32_t)j, 1, c, INT64_MAX};
+            want |= 1u << i;
         }
+        link[j] = lk;
     }
+    block_push<kLinkIPT>(want, it, queue, qcount);
 }
 
-template <int MG, typename View>
-__global__ __launch_bounds__(kBlock) void chain_left_kernel(View v, const uint64_t* __restrict__ probe_info, uint64_t P,
-                                                            GenomeTable gt, MatchParams mp, SeedSpec ss,
-                                                            const uint32_t* __restrict__ ord,
-                                                            const uint32_t* __restrict__ packed,
-                                                            const uint8_t* __restrict__ link,
-                                                            int64_t* __restrict__ lcol, WalkItem* __restrict__ queue,
+// segment starts (first probe, or the previous probe not linked) walk left to the chain start
+__global__ __launch_bounds__(kBlock) void chain_left_kernel(uint64_t P, const uint8_t* __restrict__ link,
+                                                            WalkItem* __restrict__ queue,
                                                             unsigned int* __restrict__ qcount) {
-    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (j >= P) return;
-    if (j > 0 && link[j - 1]) return;
+    uint32_t want = 0;
+    WalkItem it[kLinkIPT];
+    #pragma unroll
+    for (int i = 0; i < kLinkIPT; ++i) {
+        const uint64_t j = (uint64_t)blockIdx.x * (kBlock * kLinkIPT) + (uint64_t)i * kBlock + threadIdx.x;
+        it[i] = WalkItem{(uint32_t)j, 2, 0, INT64_MIN};
+        if (j < P && (j == 0 || !link[j - 1])) want |= 1u << i;
+    }
+    block_push<kLinkIPT>(want, it, queue, qcount);
+}
+
+// Queued walks, one lane per item, up to kWalkBudget 64-column words each (most chain ends
+// lie within a few words); the rest go on to chain_walk_kernel's lane groups.
+template <int MG, typename View>
+__global__ __launch_bounds__(kBlock) void chain_walk_short_kernel(View v, const uint64_t* __restrict__ probe_info,
+                                                                  GenomeTable gt, MatchParams mp, SeedSpec ss,
+                                                                  const uint32_t* __restrict__ packed,
+                                                                  const WalkItem* __restrict__ queue,
+                                                                  const unsigned int* __restrict__ qcount,
+                                                                  uint8_t* __restrict__ link, int64_t* __restrict__ rcol,
+                                                                  int64_t* __restrict__ lcol, WalkItem* __restrict__ lq,
+                                                                  unsigned int* __restrict__ lqcount) {
     const int L = ss.L;
     const LineSpec ls = line_spec(ss, gt);
-    Mhe<MG> A;
-    probe_of<MG, View>(v, probe_info, j, gt, mp, L, A);
-    const int64_t xa = start_at(A, first_start(A));
-    int64_t clo, chi;
-    frame_bounds<MG>(A, gt, &clo, &chi);
-    int state;
-    const int64_t c = walk_lane<MG>(-1, 0, INT64_MIN, kWalkBudget, A, gt, clo, chi, packed, ss, ls, &state);
-    if (state == 0) {
-        lcol[j] = xa + c;
-    } else {
-        const unsigned q = atomicAdd(qcount, 1u);
-        queue[q] = WalkItem{(uint32_t)j, 2, c, INT64_MIN};
+    const unsigned nq = *qcount;
+    const unsigned stride = gridDim.x * kBlock;
+    // block-uniform trip count: block_push synchronises the workgroup
+    for (unsigned q0 = blockIdx.x * kBlock; q0 < nq; q0 += stride) {
+        const unsigned q = q0 + threadIdx.x;
+        uint32_t want = 0;
+        WalkItem nx[1] = {WalkItem{}};
+        if (q < nq) {
+            const WalkItem it = queue[q];
+            Mhe<MG> A;
+            probe_of<MG, View>(v, probe_info, it.j, gt, mp, L, A);
+            const int64_t xa = start_at(A, first_start(A));
+            int64_t clo, chi;
+            frame_bounds<MG>(A, gt, &clo, &chi);
+            const int dir = it.kind == 2 ? -1 : +1;
+            int state;
+            const int64_t c = walk_lane<MG>(dir, it.cur, it.stop, kWalkBudget, A, gt, clo, chi, packed, ss, ls, &state);
+            if (state == 2) {
+                nx[0] = WalkItem{it.j, it.kind, c, it.stop};
+                want = 1;
+            } else if (it.kind == 0) {
+                link[it.j] = state == 1 ? 1 : 0;
+                if (state == 0) rcol[it.j] = xa + c;
+            } else if (it.kind == 1) {
+                rcol[it.j] = xa + c;
+            } else {
+                lcol[it.j] = xa + c;
+            }
+        }
+        block_push<1>(want, nx, lq, lqcount);
     }
 }
 
@@ -736,10 +792,10 @@ namespace {
 
 size_t chain_tmp_bytes(uint64_t P, uint32_t Tb, int G) {
     // lkey, sort A/B keys (3 x 8) + vals A/B (2 x 4) + link (1) + rcol, lcol, seg_r (3 x 8)
-    // + seg (4) + queue (24) + padding.  The replay reuses it: per chain <= 76 B, then the
+    // + seg (4) + queues (2 x 24) + padding.  The replay reuses it: per chain <= 76 B, then the
     // big-bucket scratch (count 4 + scan 4 + slot 16 per probe, + 4 per bucket)
     // + the probe rows in line order ((G + 1) x 8)
-    return P * (24 + 8 + 1 + 24 + 4 + sizeof(WalkItem) + 16 + 24 + 8 * (uint64_t)(G + 1)) + (uint64_t)Tb * 4 + 64 * 64;
+    return P * (24 + 8 + 1 + 24 + 4 + 2 * sizeof(WalkItem) + 16 + 24 + 8 * (uint64_t)(G + 1)) + (uint64_t)Tb * 4 + 64 * 64;
 }
 
 // Chain labelling of the P probes (key order): chain_of[k] = chain of probe k;
@@ -767,6 +823,7 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
     int64_t* seg_r = (int64_t*)carve(P * 8);
     uint32_t* seg = (uint32_t*)carve(P * 4);
     WalkItem* queue = (WalkItem*)carve(P * sizeof(WalkItem));
+    WalkItem* queue_long = (WalkItem*)carve(P * sizeof(WalkItem));
     unsigned int* qcount = (unsigned int*)carve(64);
     int64_t* rows_line = (int64_t*)carve(P * (uint64_t)(gt.G + 1) * 8);
     hipError_t e;
@@ -781,30 +838,37 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
     if ((e = launch_gather_rows(v.rows, ord, P, gt.G, rows_line, st)) != hipSuccess) return e;
     View vl = v;
     vl.rows = rows_line;
-    const unsigned walk_grid = 2048;
+    const unsigned walk_grid = 2048, short_grid = 8192;
+    unsigned int* qshort = qcount;      // chain_link / chain_left -> chain_walk_short_kernel
+    unsigned int* qlong = qcount + 1;   // chain_walk_short_kernel -> chain_walk_kernel
+    const bool cdbg = getenv("MUMS_DEV_CHAIN_DEBUG") != nullptr;
     for (int pass = 0; pass < 2; ++pass) {
-        if ((e = hipMemsetAsync(qcount, 0, 4, st)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(qcount, 0, 8, st)) != hipSuccess) return e;
+        const unsigned lgrid = (unsigned)((P + kBlock * kLinkIPT - 1) / (kBlock * kLinkIPT));
         if (pass == 0)
-            hipLaunchKernelGGL((chain_link_kernel<MG, View>), dim3(grid), dim3(kBlock), 0, st, vl, probe_info, P, gt,
-                               mp, ss, ord, packed, link, rcol, queue, qcount);
+            hipLaunchKernelGGL((chain_link_kernel<MG, View>), dim3(lgrid), dim3(kBlock), 0, st, vl, probe_info, P, gt,
+                               mp, ss, link, queue, qshort);
         else
-            hipLaunchKernelGGL((chain_left_kernel<MG, View>), dim3(grid), dim3(kBlock), 0, st, vl, probe_info, P, gt,
-                               mp, ss, ord, packed, link, lcol, queue, qcount);
+            hipLaunchKernelGGL(chain_left_kernel, dim3(lgrid), dim3(kBlock), 0, st, P, (const uint8_t*)link, queue,
+                               qshort);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-        const bool cdbg = getenv("MUMS_DEV_CHAIN_DEBUG") != nullptr;
+        hipLaunchKernelGGL((chain_walk_short_kernel<MG, View>), dim3(short_grid), dim3(kBlock), 0, st, vl, probe_info,
+                           gt, mp, ss, packed, (const WalkItem*)queue, (const unsigned int*)qshort, link, rcol, lcol,
+                           queue_long, qlong);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
         if (cdbg && (e = hipMemsetAsync(qcount + 4, 0, 32, st)) != hipSuccess) return e;
         if (ev_walk) (void)hipEventRecord(ev_walk[2 * pass], st);
         hipLaunchKernelGGL((chain_walk_kernel<MG, View>), dim3(walk_grid), dim3(kBlock), 0, st, vl, probe_info, gt, mp,
-                           ss, ord, packed, queue, qcount, link, rcol, lcol, cdbg ? qcount + 4 : nullptr,
-                           (DevCounters*)ctr);
+                           ss, ord, packed, (const WalkItem*)queue_long, (const unsigned int*)qlong, link, rcol, lcol,
+                           cdbg ? qcount + 4 : nullptr, (DevCounters*)ctr);
         if (ev_walk) (void)hipEventRecord(ev_walk[2 * pass + 1], st);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-        if (cdbg) {   // development: long-walk queue sizes and wave-step histogram
+        if (cdbg) {   // development: walk queue sizes and the long walks' step histogram
             unsigned hq[9] = {};
             (void)hipMemcpyAsync(hq, qcount, 36, hipMemcpyDeviceToHost, st);
             (void)hipStreamSynchronize(st);
-            fprintf(stderr, "chains: pass %d long walks %u of %lu probes; steps >1: %u >16: %u >256: %u max %u total %u\n",
-                    pass, hq[0], (unsigned long)P, hq[4], hq[5], hq[6], hq[7], hq[8]);
+            fprintf(stderr, "chains: pass %d walks %u, long %u of %lu probes; steps >1: %u >16: %u >256: %u max %u "
+                    "total %u\n", pass, hq[0], hq[1], (unsigned long)P, hq[4], hq[5], hq[6], hq[7], hq[8]);
         }
     }
     hipLaunchKernelGGL(chain_flag_kernel, dim3(grid), dim3(kBlock), 0, st, link, P, seg);

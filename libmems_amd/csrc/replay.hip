@@ -858,6 +858,7 @@ __global__ void bigg_slow_kernel(View v, GenomeTable gt, MatchParams mp, int L, 
     if (rr < R && rl <= rr && rr <= rh) {
         cnt[rr] += 1u;
         log_insert(mlog, ctr, mb.w, pcid);
+        info[6] = 1u;   // inserted (the closed-form path counts it as a duplicate)
     } else {
         info[4] = 1u;
     }
@@ -884,6 +885,196 @@ __global__ void bigg_finish_kernel(const uint32_t* __restrict__ E, uint32_t R, c
     atomicAdd(&ctr->collisions, (unsigned long long)info[5]);
     if (info[4]) atomicOr(&ctr->err, 4u);
     cend[b] = beg;   // replay_kernel / replay_big_kernel skip it
+}
+
+// ---- closed-form path for big buckets with many suspicious probes -----------------------
+// BASELINE config 5's main diagonal: 4.2e4 chain-first inserts and 1.9e6 suspicious probes in
+// one bucket.  Between two inserts every suspicious probe V (of chain A, rank a) meets a vector
+// whose MheCompare pattern is fixed by counts alone: entries of ranks < a are less than V
+// (earlier block, or same block and start < A's), A's copies are equivalent (A contains V),
+// ranks in (a, x] (same block, start in (A.start, V.start)) are less (no other chain contains
+// V: containment needs the same line, MatchHashEntry.cpp:164-200, and chains of one line are
+// disjoint), ranks after x are not less.  So with pA / dA / nC inserted entries of those three
+// groups and t in all, lower_bound (MemHash.cpp:215) is the libstdc++ recurrence over
+//   T^pA F^dA T^nC F^(t - pA - dA - nC)
+// and V collides iff it lands on A's copies; else a copy of A goes in front of A's copies
+// (its own lower_bound: T^pA then F).  Ranks with start == V.start (other genomes decide the
+// order) make a probe "exact": it runs the rank-count path (bigg_slow_kernel) at its time.
+// The counts come from the chain-first insert times (prefix tables over the firsts in time
+// order) plus the duplicate inserts found so far; rounds find the earliest probe that is
+// not a collision, apply it, and go on from there.
+constexpr uint32_t kQW = 10;   // words per query record
+
+// ff[k] = chain-first flag of bucket probe k (ff[K] = 0); ft[rank] = its time; logs the inserts
+__global__ __launch_bounds__(kBlock) void bigq_first_kernel(const uint4* __restrict__ summ,
+                                                            const uint4* __restrict__ summ_b, uint32_t beg, uint32_t K,
+                                                            uint32_t r0, uint32_t* __restrict__ ff,
+                                                            uint32_t* __restrict__ sf, uint32_t* __restrict__ ft,
+                                                            uint64_t* __restrict__ mlog, DevCounters* ctr) {
+    const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
+    if (k > K) return;
+    if (k == K) { ff[K] = 0; sf[K] = 0; return; }
+    const uint4 a = summ[beg + k];
+    const bool first = (a.w & 0x80000000u) != 0u;
+    ff[k] = first ? 1u : 0u;
+    sf[k] = first ? 0u : 1u;
+    if (first) {
+        const uint4 c = summ_b[beg + k];
+        ft[(c.z & 0x7FFFFFFFu) - r0] = k;
+        log_insert(mlog, ctr, c.w, a.z);
+    }
+}
+
+// after the scans: fr[i] = rank of the i-th chain-first probe (time order), fi[rank] = i
+__global__ __launch_bounds__(kBlock) void bigq_fr_kernel(const uint4* __restrict__ summ, const uint4* __restrict__ summ_b,
+                                                         uint32_t beg, uint32_t K, uint32_t r0,
+                                                         const uint32_t* __restrict__ fpos, uint32_t* __restrict__ fr,
+                                                         uint32_t* __restrict__ fi) {
+    const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
+    if (k >= K || !(summ[beg + k].w & 0x80000000u)) return;
+    const uint32_t r = (summ_b[beg + k].z & 0x7FFFFFFFu) - r0, i = fpos[k];
+    fr[i] = r;
+    fi[r] = i;
+}
+
+// PT[blk][r] = chain-first probes among the first blk * bs (time order) with rank < r: one
+// workgroup per row, exclusive scan of the indicator over r with a carry
+__global__ __launch_bounds__(kBigRB) void bigq_table_kernel(const uint32_t* __restrict__ fi, uint32_t R, uint32_t bs,
+                                                            uint32_t* __restrict__ PT) {
+    __shared__ uint32_t red[kBigRB / 64];
+    const uint32_t blk = blockIdx.x, lim = blk * bs;
+    uint32_t* row = PT + (uint64_t)blk * (R + 1);
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < R; base += kBigRB) {
+        const uint32_t r = base + threadIdx.x;
+        const uint32_t v = (r < R && fi[r] < lim) ? 1u : 0u;
+        uint32_t tot;
+        const uint32_t ex = blk_scan_excl(v, red, &tot);
+        if (r < R) row[r] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) row[R] = carry;
+}
+
+// first rank r in [0, R) with (block key, start) of sbr[r] >= (m, s)
+__device__ __forceinline__ uint32_t rank_lb(const uint4* __restrict__ sbr, uint32_t R, uint32_t m, uint64_t s) {
+    uint32_t lo = 0, n = R;
+    while (n > 0) {
+        const uint32_t h = n >> 1;
+        const uint4 X = sbr[lo + h];
+        const bool less = X.y < m || (X.y == m && (uint64_t)X.z < s);
+        if (less) { lo += h + 1; n -= h + 1; } else n = h;
+    }
+    return lo;
+}
+
+// one query per suspicious probe, in time order (spos = exclusive scan of the flags):
+// Q[q] = {time, a, x, xe, pA, dA, nC, eq, t, status}
+__global__ __launch_bounds__(kBlock) void bigq_query_kernel(const uint4* __restrict__ summ,
+                                                            const uint4* __restrict__ summ_b, uint32_t beg, uint32_t K,
+                                                            uint32_t r0, uint32_t R, const uint4* __restrict__ sbr,
+                                                            const uint32_t* __restrict__ fpos,
+                                                            const uint32_t* __restrict__ spos,
+                                                            const uint32_t* __restrict__ fr,
+                                                            const uint32_t* __restrict__ PT, uint32_t bs,
+                                                            uint32_t* __restrict__ Q) {
+    const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
+    if (k >= K) return;
+    const uint4 me = summ[beg + k];
+    if (me.w & 0x80000000u) return;
+    const uint4 mb = summ_b[beg + k];
+    const uint32_t a = (mb.z & 0x7FFFFFFFu) - r0;
+    const uint32_t x = rank_lb(sbr, R, me.x, (uint64_t)me.y) - 1u;          // start < V.start
+    const uint32_t xe = rank_lb(sbr, R, me.x, (uint64_t)me.y + 1u) - 1u;    // start <= V.start
+    const uint32_t kq = fpos[k];   // chain-first inserts before V
+    const uint32_t blk = kq / bs;
+    const uint32_t* row = PT + (uint64_t)blk * (R + 1);
+    uint32_t c_a = row[a], c_a1 = row[a + 1], c_x1 = row[x + 1], c_xe1 = row[xe + 1];
+    for (uint32_t i = blk * bs; i < kq; ++i) {
+        const uint32_t r = fr[i];
+        c_a += r < a;
+        c_a1 += r < a + 1;
+        c_x1 += r < x + 1;
+        c_xe1 += r < xe + 1;
+    }
+    uint32_t* q = Q + (uint64_t)spos[k] * kQW;
+    q[0] = k;
+    q[1] = a;
+    q[2] = x;
+    q[3] = xe;
+    q[4] = c_a;                       // pA
+    q[5] = c_a1 - c_a;                // dA (A's first insert precedes V)
+    q[6] = c_x1 - c_a1;               // nC
+    q[7] = c_xe1 - c_x1;              // eq
+    q[8] = kq;                        // t
+    q[9] = 0;
+}
+
+// libstdc++ __lower_bound over the pattern T^pA F^dA T^nC F^...
+__device__ __forceinline__ uint32_t lb_pattern(uint32_t t, uint32_t pA, uint32_t dA, uint32_t nC) {
+    const uint32_t e1 = pA + dA, e2 = e1 + nC;
+    uint32_t first = 0, len = t;
+    while (len > 0) {
+        const uint32_t half = len >> 1, mid = first + half;
+        if (mid < pA || (mid >= e1 && mid < e2)) {
+            first = mid + 1;
+            len = len - half - 1;
+        } else {
+            len = half;
+        }
+    }
+    return first;
+}
+
+// one round over the queries [q0, S): apply the last insert (rank da at time dt) to the
+// later queries, classify (0 collision, 1 insert, 2 exact) and find the earliest non-collision
+__global__ __launch_bounds__(kBlock) void bigq_round_kernel(uint32_t* __restrict__ Q, uint32_t S, uint32_t q0,
+                                                            uint32_t has, uint32_t da, uint32_t dt,
+                                                            uint32_t* __restrict__ best) {
+    const uint32_t i = q0 + blockIdx.x * kBlock + threadIdx.x;
+    if (i >= S) return;
+    uint32_t* q = Q + (uint64_t)i * kQW;
+    const uint32_t a = q[1], x = q[2], xe = q[3];
+    uint32_t pA = q[4], dA = q[5], nC = q[6], eq = q[7], t = q[8];
+    if (has && q[0] > dt) {
+        pA += da < a;
+        dA += da == a;
+        nC += (da > a && da <= x);
+        eq += (da > x && da <= xe);
+        t += 1;
+        q[4] = pA; q[5] = dA; q[6] = nC; q[7] = eq; q[8] = t;
+    }
+    uint32_t st = 2;
+    if (eq == 0) {
+        const uint32_t lb = lb_pattern(t, pA, dA, nC);
+        st = (lb >= pA && lb < pA + dA) ? 0u : 1u;
+    }
+    q[9] = st;
+    if (st) atomicMin(best, i);
+}
+
+// counts of the virtual vector at time tau: chain-first inserts before tau + duplicates
+__global__ __launch_bounds__(kBlock) void bigq_cnt_kernel(const uint32_t* __restrict__ ft,
+                                                          const uint32_t* __restrict__ dup, uint32_t R, uint32_t tau,
+                                                          uint32_t* __restrict__ cnt) {
+    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
+    if (r < R) cnt[r] = (ft[r] < tau ? 1u : 0u) + dup[r];
+}
+
+// a duplicate insert of rank da (probe at bucket time k): counted, logged unless the exact
+// path logged it
+__global__ void bigq_dup_kernel(uint32_t* __restrict__ dup, uint32_t da, const uint4* __restrict__ summ,
+                                const uint4* __restrict__ summ_b, uint32_t beg, uint32_t k, int log,
+                                uint64_t* __restrict__ mlog, DevCounters* ctr) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    dup[da] += 1u;
+    if (log) log_insert(mlog, ctr, summ_b[beg + k].w, summ[beg + k].z);
+}
+
+__global__ __launch_bounds__(kBlock) void bigq_final_kernel(const uint32_t* __restrict__ dup, uint32_t R,
+                                                            uint32_t* __restrict__ cnt) {
+    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
+    if (r < R) cnt[r] = 1u + dup[r];
 }
 
 // chunked FindMatches (probes beyond one pass of per-probe arrays): the keep flags of
@@ -996,6 +1187,124 @@ hipError_t launch_bucket_ranges(const uint32_t* sb, uint64_t P, uint32_t* bstart
     return hipGetLastError();
 }
 
+// Closed-form replay of one big bucket (probes [beg, beg + K), S suspicious, chain ranks
+// r0 .. r0 + R - 1, no tied chains): see bigq_round_kernel.  Scratch is allocated here (the
+// path runs for a handful of buckets per FindMatches).
+template <int MG, typename View>
+hipError_t bigq_bucket(View v, const GenomeTable& gt, const MatchParams& mp, int L, const uint64_t* probe_info,
+                       const uint4* summ, const uint4* summ_b, uint32_t beg, uint32_t K, uint32_t S, uint32_t r0,
+                       uint32_t R, uint32_t b, uint32_t* cend, const uint32_t* bstart, uint32_t* tbl,
+                       const int64_t* pool, const uint4* chain_sb, uint32_t* info, void* stmp, uint32_t* tsize,
+                       void* ctr, hipStream_t st, uint64_t* mlog) {
+    const uint32_t F = K - S;
+    const uint32_t bs = std::max<uint32_t>(256u, (F + 255u) / 256u);
+    const uint32_t NB = F / bs + 1;
+    const size_t words = 3ull * (K + 1) + 5ull * (R + 1) + (size_t)F + 1 + (size_t)NB * (R + 1) +
+                         (size_t)S * kQW + 64;
+    size_t stmp_need = scan_tmp_bytes((uint64_t)std::max(K, R) + 1);
+    char* base = nullptr;
+    hipError_t e = hipMalloc(&base, words * 4 + 16 * (size_t)(R + 1) + stmp_need + 4096);
+    if (e != hipSuccess) return e;
+    char* p = base;
+    auto carve = [&](size_t bytes) {
+        char* r = p;
+        p += (bytes + 255) & ~(size_t)255;
+        return (void*)r;
+    };
+    uint32_t* ff = (uint32_t*)carve((K + 1) * 4ull);     // first flags -> fpos
+    uint32_t* sf = (uint32_t*)carve((K + 1) * 4ull);     // suspicious flags -> spos
+    uint32_t* ft = (uint32_t*)carve((R + 1) * 4ull);     // time of each rank's first insert
+    uint32_t* fi = (uint32_t*)carve((R + 1) * 4ull);     // index of each rank's first among the firsts
+    uint32_t* dup = (uint32_t*)carve((R + 1) * 4ull);    // duplicate inserts per rank
+    uint32_t* cnt = (uint32_t*)carve((R + 1) * 4ull);
+    uint32_t* E = (uint32_t*)carve((R + 1) * 4ull);
+    uint32_t* fr = (uint32_t*)carve((F + 1) * 4ull);
+    uint32_t* PT = (uint32_t*)carve((size_t)NB * (R + 1) * 4);
+    uint32_t* Q = (uint32_t*)carve((size_t)S * kQW * 4 + 4);
+    uint32_t* best = (uint32_t*)carve(64);
+    uint4* sbr = (uint4*)carve((R + 1) * 16ull);
+    void* tmp = carve(stmp_need);
+    (void)stmp;
+    auto done = [&](hipError_t x) {
+        (void)hipStreamSynchronize(st);
+        (void)hipFree(base);
+        return x;
+    };
+    auto grid = [](uint64_t n) { return dim3((unsigned)((n + kBlock - 1) / kBlock)); };
+    if ((e = hipMemsetAsync(dup, 0, (R + 1) * 4ull, st)) != hipSuccess) return done(e);
+    hipLaunchKernelGGL(bigg_slots_kernel, grid(K), dim3(kBlock), 0, st, summ, summ_b, beg, K, r0, R, sbr);
+    hipLaunchKernelGGL(bigq_first_kernel, grid(K + 1), dim3(kBlock), 0, st, summ, summ_b, beg, K, r0, ff, sf, ft, mlog,
+                       (DevCounters*)ctr);
+    if ((e = hipGetLastError()) != hipSuccess) return done(e);
+    if ((e = exclusive_scan_u32(ff, (uint64_t)K + 1, tmp, nullptr, st)) != hipSuccess) return done(e);
+    if ((e = exclusive_scan_u32(sf, (uint64_t)K + 1, tmp, nullptr, st)) != hipSuccess) return done(e);
+    hipLaunchKernelGGL(bigq_fr_kernel, grid(K), dim3(kBlock), 0, st, summ, summ_b, beg, K, r0, (const uint32_t*)ff, fr,
+                       fi);
+    hipLaunchKernelGGL(bigq_table_kernel, dim3(NB), dim3(kBigRB), 0, st, (const uint32_t*)fi, R, bs, PT);
+    hipLaunchKernelGGL(bigq_query_kernel, grid(K), dim3(kBlock), 0, st, summ, summ_b, beg, K, r0, R,
+                       (const uint4*)sbr, (const uint32_t*)ff, (const uint32_t*)sf, (const uint32_t*)fr,
+                       (const uint32_t*)PT, bs, Q);
+    if ((e = hipGetLastError()) != hipSuccess) return done(e);
+    uint32_t q0 = 0, has = 0, da = 0, dt = 0, ndup = 0;
+    std::vector<uint32_t> hq(kQW);
+    const bool stats = getenv("MUMS_DEV_REPLAY_STATS") != nullptr;
+    uint32_t nexact = 0, rounds = 0;
+    while (q0 < S) {
+        const uint32_t inf = 0xFFFFFFFFu;
+        if ((e = hipMemcpyAsync(best, &inf, 4, hipMemcpyHostToDevice, st)) != hipSuccess) return done(e);
+        hipLaunchKernelGGL(bigq_round_kernel, grid(S - q0), dim3(kBlock), 0, st, Q, S, q0, has, da, dt, best);
+        if ((e = hipGetLastError()) != hipSuccess) return done(e);
+        uint32_t m = inf;
+        if ((e = hipMemcpyAsync(&m, best, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return done(e);
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return done(e);
+        ++rounds;
+        if (m == inf) break;
+        if ((e = hipMemcpy(hq.data(), Q + (size_t)m * kQW, kQW * 4, hipMemcpyDeviceToHost)) != hipSuccess) return done(e);
+        const uint32_t k = hq[0], a = hq[1];
+        bool inserted = hq[9] == 1;
+        if (hq[9] == 2) {   // exact lower_bound on the rank counts at this probe's time
+            ++nexact;
+            hipLaunchKernelGGL(bigq_cnt_kernel, grid(R), dim3(kBlock), 0, st, (const uint32_t*)ft,
+                               (const uint32_t*)dup, R, k, cnt);
+            if ((e = hipMemcpyAsync(E, cnt, (size_t)R * 4, hipMemcpyDeviceToDevice, st)) != hipSuccess) return done(e);
+            if ((e = hipMemsetAsync(E + R, 0, 4, st)) != hipSuccess) return done(e);
+            if ((e = exclusive_scan_u32(E, (uint64_t)R + 1, tmp, nullptr, st)) != hipSuccess) return done(e);
+            if ((e = hipMemsetAsync(info + 6, 0, 4, st)) != hipSuccess) return done(e);
+            hipLaunchKernelGGL((bigg_slow_kernel<MG, View>), dim3(1), dim3(64), 0, st, v, gt, mp, L, probe_info, summ,
+                               summ_b, beg, k, r0, R, (const uint32_t*)E, (const uint4*)sbr, chain_sb, pool, cnt, info,
+                               mlog, (DevCounters*)ctr);
+            uint32_t ins = 0;
+            if ((e = hipMemcpyAsync(&ins, info + 6, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return done(e);
+            if ((e = hipStreamSynchronize(st)) != hipSuccess) return done(e);
+            inserted = ins != 0;
+        }
+        has = 0;
+        if (inserted) {
+            hipLaunchKernelGGL(bigq_dup_kernel, dim3(1), dim3(64), 0, st, dup, a, summ, summ_b, beg, k,
+                               hq[9] == 1 ? 1 : 0, mlog, (DevCounters*)ctr);
+            has = 1;
+            da = a;
+            dt = k;
+            ++ndup;
+        }
+        q0 = m + 1;
+    }
+    if (stats)
+        fprintf(stderr, "closed-form bucket %u: K %u suspicious %u ranks %u duplicates %u exact %u rounds %u\n", b, K, S,
+                R, ndup, nexact, rounds);
+    hipLaunchKernelGGL(bigq_final_kernel, grid(R), dim3(kBlock), 0, st, (const uint32_t*)dup, R, cnt);
+    if ((e = hipMemcpyAsync(E, cnt, (size_t)R * 4, hipMemcpyDeviceToDevice, st)) != hipSuccess) return done(e);
+    if ((e = hipMemsetAsync(E + R, 0, 4, st)) != hipSuccess) return done(e);
+    if ((e = exclusive_scan_u32(E, (uint64_t)R + 1, tmp, nullptr, st)) != hipSuccess) return done(e);
+    const uint32_t coll = S - ndup;   // every other suspicious probe collided
+    if ((e = hipMemcpyAsync(info + 5, &coll, 4, hipMemcpyHostToDevice, st)) != hipSuccess) return done(e);
+    hipLaunchKernelGGL(bigg_out_kernel, grid(R), dim3(kBlock), 0, st, (const uint32_t*)E, R, (const uint4*)sbr, bstart,
+                       b, tbl);
+    hipLaunchKernelGGL(bigg_finish_kernel, dim3(1), dim3(64), 0, st, (const uint32_t*)E, R, (const uint32_t*)info, b,
+                       tsize, cend, beg, (DevCounters*)ctr);
+    return done(hipGetLastError());
+}
+
 // The replay over the compacted probes (chain-first / suspicious, bucket-major, cbeg /
 // cend per bucket): big buckets by rank counts (grid path, then one workgroup), then the
 // per-bucket rounds.  scr: scratch of replay_scratch_bytes(scr_n) for scr_n compacted probes.
@@ -1016,6 +1325,8 @@ hipError_t replay_tail(View v, const GenomeTable& gt, const MatchParams& mp, int
     {
         const char* bm_env = getenv("MUMS_DEV_BIG_BUCKET");
         const uint32_t big_min = bm_env ? (uint32_t)atoi(bm_env) : kBigBucket;
+        const char* gs_env = getenv("MUMS_DEV_GRID_SLOW");   // tests: force the closed-form path
+        const uint32_t grid_slow = gs_env ? (uint32_t)atoi(gs_env) : kGridSlow;
         uint32_t* scr_cnt = (uint32_t*)carve((scr_n + 1) * 4);
         uint32_t* scr_e = (uint32_t*)carve((scr_n + 1 + mp.table_size + 1) * 4);
         uint4* scr_slot = (uint4*)carve((scr_n + 1) * 16);
@@ -1039,7 +1350,14 @@ hipError_t replay_tail(View v, const GenomeTable& gt, const MatchParams& mp, int
             if (getenv("MUMS_DEV_REPLAY_STATS"))
                 fprintf(stderr, "grid path bucket %u: K %u flags %u slow %u ranks %u..%u\n", b, K, hinfo[2], S, hinfo[0],
                         hinfo[1]);
-            if (hinfo[2] || S > kGridSlow || hinfo[0] > hinfo[1]) continue;   // left to the kernels below
+            if (hinfo[2] || hinfo[0] > hinfo[1]) continue;   // tied chains: left to the kernels below
+            if (S > grid_slow) {   // many suspicious probes: closed form (bigq_*)
+                if ((e = bigq_bucket<MG, View>(v, gt, mp, L, probe_info, summ_c, summ_bc, beg, K, S, hinfo[0],
+                                               hinfo[1] - hinfo[0] + 1, b, cend, bstart, tbl, pool, chain_sb, ginfo,
+                                               stmp, tsize, ctr, st, mlog)) != hipSuccess)
+                    return e;
+                continue;
+            }
             const uint32_t r0 = hinfo[0], R = hinfo[1] - hinfo[0] + 1;
             std::vector<uint32_t> hs(S);
             if (S) {
