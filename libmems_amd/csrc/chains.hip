@@ -33,7 +33,7 @@ namespace mums {
 namespace {
 
 #ifndef MUMS_WALK_BUDGET
-#define MUMS_WALK_BUDGET 4
+#define MUMS_WALK_BUDGET 8
 #endif
 constexpr int kWalkBudget = MUMS_WALK_BUDGET;   // words per lane in chain_walk_short_kernel
 #ifndef MUMS_HIT_BATCH
@@ -624,18 +624,32 @@ __global__ __launch_bounds__(kBlock) void chain_flag_kernel(const uint8_t* __res
     seg[j] = (j == 0 || !link[j - 1]) ? 1u : 0u;
 }
 
+// chain of every probe; fk[chain] = its first probe in key order (kbase + the least ord[j]
+// of the segment: a segmented min over the wave, one atomicMin per segment and wave)
 __global__ __launch_bounds__(kBlock) void chain_seg_kernel(const uint8_t* __restrict__ link,
                                                            const uint32_t* __restrict__ ord,
                                                            const uint32_t* __restrict__ seg_excl, uint64_t P,
                                                            const int64_t* __restrict__ rcol,
                                                            uint32_t* __restrict__ chain_of,
-                                                           int64_t* __restrict__ seg_r) {
+                                                           int64_t* __restrict__ seg_r, uint32_t* __restrict__ fk,
+                                                           uint32_t kbase) {
     const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (j >= P) return;
-    const uint32_t f = (j == 0 || !link[j - 1]) ? 1u : 0u;
-    const uint32_t s = seg_excl[j] + f - 1u;
-    chain_of[ord[j]] = s;
-    if (!link[j]) seg_r[s] = rcol[j];
+    const int lane = threadIdx.x & 63;
+    uint32_t s = 0xFFFFFFFFu, m = 0xFFFFFFFFu;
+    if (j < P) {
+        const uint32_t f = (j == 0 || !link[j - 1]) ? 1u : 0u;
+        s = seg_excl[j] + f - 1u;
+        m = ord[j];
+        chain_of[m] = s;
+        if (!link[j]) seg_r[s] = rcol[j];
+    }
+    #pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {   // segments are contiguous: equal s at distance d spans them
+        const uint32_t om = __shfl_up(m, d, 64), os = __shfl_up(s, d, 64);
+        if (lane >= d && os == s) m = min(m, om);
+    }
+    const uint32_t ns = __shfl_down(s, 1, 64);
+    if (j < P && (lane == 63 || ns != s)) atomicMin(&fk[s], kbase + m);
 }
 
 // the extended entry of every chain (ExtendMatch write-back, MatchFinder.h:218-374;
@@ -723,11 +737,14 @@ __global__ __launch_bounds__(kBlock) void entry_rep_kernel(const int64_t* __rest
 __global__ __launch_bounds__(kBlock) void entry_map_kernel(const int64_t* __restrict__ pool, const uint32_t* __restrict__ ord,
                                                            const uint32_t* __restrict__ rep, const uint32_t* __restrict__ gid,
                                                            uint64_t n, int G, uint32_t* __restrict__ gmap,
-                                                           int64_t* __restrict__ pool_out) {
+                                                           int64_t* __restrict__ pool_out,
+                                                           const uint32_t* __restrict__ fk_loc,
+                                                           uint32_t* __restrict__ fk_out) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const uint32_t c = ord[i], r = rep[i], g = gid[r];
     gmap[c] = g;
+    atomicMin(&fk_out[g], fk_loc[c]);   // the merged chain's first probe: the earliest slice's
     if (r == (uint32_t)i) {
         const int W = G + 2;
         for (int w = 0; w < W; ++w) pool_out[(uint64_t)g * W + w] = pool[(uint64_t)c * W + w];
@@ -752,7 +769,7 @@ size_t chain_merge_tmp_bytes(uint64_t n) { return (n + 64) * (8 * 3 + 4 * 5) + 8
 
 hipError_t launch_chain_merge(const int64_t* pool_loc, uint64_t n, int G, uint32_t* chain_of, uint64_t P,
                               int64_t* pool_out, void* d_tmp, void* d_radix_tmp, void* d_scan_tmp, uint32_t* d_nchains,
-                              hipStream_t st) {
+                              hipStream_t st, const uint32_t* fk_loc, uint32_t* fk_out) {
     if (n == 0) return hipMemsetAsync(d_nchains, 0, 4, st);
     char* p = (char*)d_tmp;
     auto carve = [&](size_t bytes) {
@@ -779,8 +796,9 @@ hipError_t launch_chain_merge(const int64_t* pool_loc, uint64_t n, int G, uint32
                        gid);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = exclusive_scan_u32(gid, n, d_scan_tmp, d_nchains, st)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(fk_out, 0xFF, n * 4, st)) != hipSuccess) return e;
     hipLaunchKernelGGL(entry_map_kernel, dim3(grid), dim3(kBlock), 0, st, pool_loc, ord, (const uint32_t*)rep,
-                       (const uint32_t*)gid, n, G, gmap, pool_out);
+                       (const uint32_t*)gid, n, G, gmap, pool_out, fk_loc, fk_out);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(chain_remap_kernel, dim3(grid_of(P)), dim3(kBlock), 0, st, chain_of, P, (const uint32_t*)gmap);
     return hipGetLastError();
@@ -795,7 +813,7 @@ size_t chain_tmp_bytes(uint64_t P, uint32_t Tb, int G) {
     // + seg (4) + queues (2 x 24) + padding.  The replay reuses it: per chain <= 76 B, then the
     // big-bucket scratch (count 4 + scan 4 + slot 16 per probe, + 4 per bucket)
     // + the probe rows in line order ((G + 1) x 8)
-    return P * (24 + 8 + 1 + 24 + 4 + 2 * sizeof(WalkItem) + 16 + 24 + 8 * (uint64_t)(G + 1)) + (uint64_t)Tb * 4 + 64 * 64;
+    return P * (24 + 8 + 1 + 24 + 4 + 2 * sizeof(WalkItem) + 32 + 24 + 8 * (uint64_t)(G + 1)) + (uint64_t)Tb * 4 + 64 * 64;
 }
 
 // Chain labelling of the P probes (key order): chain_of[k] = chain of probe k;
@@ -804,7 +822,7 @@ template <int MG, typename View>
 hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const GenomeTable& gt, const MatchParams& mp,
                          const SeedSpec& ss, const uint32_t* packed, void* d_chain_tmp, void* d_scan_tmp,
                          void* d_radix_tmp, uint32_t* chain_of, int64_t* pool, uint32_t* d_nchains, hipStream_t st,
-                         void* ctr, hipEvent_t* ev_walk) {
+                         void* ctr, hipEvent_t* ev_walk, uint32_t* fk, uint32_t kbase) {
     if (P == 0) return hipSuccess;
     char* p = (char*)d_chain_tmp;
     auto carve = [&](size_t bytes) {
@@ -874,7 +892,9 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
     hipLaunchKernelGGL(chain_flag_kernel, dim3(grid), dim3(kBlock), 0, st, link, P, seg);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = exclusive_scan_u32(seg, P, d_scan_tmp, d_nchains, st)) != hipSuccess) return e;
-    hipLaunchKernelGGL(chain_seg_kernel, dim3(grid), dim3(kBlock), 0, st, link, ord, seg, P, rcol, chain_of, seg_r);
+    if ((e = hipMemsetAsync(fk, 0xFF, P * 4, st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(chain_seg_kernel, dim3(grid), dim3(kBlock), 0, st, link, ord, seg, P, rcol, chain_of, seg_r, fk,
+                       kbase);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL((chain_entry_kernel<MG, View>), dim3(grid), dim3(kBlock), 0, st, vl, probe_info, P, gt, mp, ss.L,
                        ord, link, seg, lcol, seg_r, pool);
@@ -884,7 +904,8 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
 #define MUMS_INST_CHAINS(MG, V)                                                                                   \
     template hipError_t launch_chains<MG, V>(V, const uint64_t*, uint64_t, const GenomeTable&, const MatchParams&, \
                                              const SeedSpec&, const uint32_t*, void*, void*, void*, uint32_t*,     \
-                                             int64_t*, uint32_t*, hipStream_t, void*, hipEvent_t*);
+                                             int64_t*, uint32_t*, hipStream_t, void*, hipEvent_t*, uint32_t*,    \
+                                             uint32_t);
 MUMS_INST_CHAINS(4, MatProbes)
 MUMS_INST_CHAINS(8, MatProbes)
 MUMS_INST_CHAINS(16, MatProbes)

@@ -91,6 +91,7 @@ struct mums_ctx {
     DevBuf packed, recA, recB, hist, tiles, ckey, kA, kB, vA, vB, tmp, partials, counters;
     DevBuf bstart, bend, tsize, obase, pool, tbl, out_len, out_s, pbuf, keybuf, mstart;
     DevBuf chain_tmp, chain_of, radix_tmp, spill, summ, dbgbuf, mprobe, rowtmp;
+    DevBuf fk, fkloc;        // each chain's first probe in key order (merged / per slice)
     bool use_onesweep = true;
     // ParallelMemHash chunk-compat mode (compat.hip): chunk = CHUNK_SIZE, ParallelMemHash.cpp:51
     bool pcompat = false;
@@ -251,16 +252,22 @@ int groups_dispatch(mums_ctx* ctx, View v, const SegTile* tiles, uint64_t ntiles
     return run_groups<64, View>(ctx, v, tiles, ntiles, mp, pi, pb, si, sb, st);
 }
 
+void* devbuf_alloc(void* b, size_t bytes) {
+    DevBuf* d = (DevBuf*)b;
+    return d->ensure(bytes) == hipSuccess ? d->p : nullptr;
+}
+
 // chain labelling (chains.hip) then the per-bucket replay (replay.hip) of the P probe
 // rows v (key order), bucket-sorted as ctx->sorted_ids; packed = all genomes (gt layout)
 template <int MG>
 int find_rows(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const MatchParams& mp, hipStream_t st) {
     DevCounters* dc = ctx->counters.as<DevCounters>();
     const uint64_t P = ctx->P;
+    HIPCHK(ctx->fk.ensure((P + 1) * 4));
     HIPCHK((launch_chains<MG, MatProbes>(v, nullptr, P, ctx->gt, mp, ctx->ss, packed,
                                     ctx->chain_tmp.p, ctx->tmp.p, ctx->radix_tmp.p, ctx->chain_of.as<uint32_t>(),
                                     ctx->pool.as<int64_t>(), &dc->nchains, st, dc,
-                                    ctx->profiling ? ctx->ev_walk : nullptr)));
+                                    ctx->profiling ? ctx->ev_walk : nullptr, ctx->fk.as<uint32_t>(), 0u)));
     ctx->walk_events = ctx->profiling;
     HIPCHK(hipEventRecord(ctx->ev[EV_CHAINS], st));
     HIPCHK(hipMemcpyAsync(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
@@ -280,12 +287,11 @@ int find_rows(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const MatchPar
     }
     // the fullest bucket's vector in LDS when it fits (it holds <= its probes)
     const uint32_t lds_cap = std::max<uint32_t>(64, std::min<uint32_t>(ctx->hc.max_bucket, kReplayLdsIds));
-    HIPCHK((launch_replay<MG, MatProbes>(v, ctx->gt, mp, ctx->L, nullptr, ctx->sorted_ids, P,
-                                    ctx->bstart.as<uint32_t>(), ctx->bend.as<uint32_t>(), ctx->tbl.as<uint32_t>(),
-                                    ctx->spill.p, ctx->summ.p, ctx->pool.as<int64_t>(), ctx->chain_of.as<uint32_t>(),
-                                    ctx->hc.nchains, ctx->chain_tmp.p, ctx->radix_tmp.p, lds_cap,
-                                    ctx->tsize.as<uint32_t>(), ctx->counters.p, dbg, st,
-                                    mlog)));
+    HIPCHK((launch_replay_kept<MG, MatProbes>(v, ctx->gt, mp, ctx->L, P, ctx->pool.as<int64_t>(),
+                                         ctx->chain_of.as<uint32_t>(), ctx->fk.as<uint32_t>(), ctx->hc.nchains,
+                                         ctx->chain_tmp.p, ctx->radix_tmp.p, ctx->tmp.p, lds_cap,
+                                         ctx->tsize.as<uint32_t>(), ctx->counters.p, dbg, st, mlog, &ctx->emit_tbl,
+                                         &ctx->emit_base, devbuf_alloc, &ctx->cbuf)));
     if (mlog) {   // the inserts in AddHashEntry call order (probe index << 32 | chain)
         HIPCHK(hipMemcpyAsync(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
@@ -319,17 +325,12 @@ int find_rows(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const MatchPar
 
 // FindMatches above find_chunk() probes (BASELINE config 5: 2.5e9): chains labelled per
 // slice of find_chunk() probes (key order) into per-slice entries, merged by content
-// (chains.hip), then the replay in chunks of the bucket order (launch_replay_chunked).
+// (chains.hip), then the replay of the kept probes (launch_replay_kept).
 // Per-probe memory: rows, chain_of, tbl, spill, the bucket order and one keep flag.
 uint64_t find_chunk() {
     uint64_t c = 1ull << 28;
     if (const char* e = getenv("MUMS_DEV_FIND_CHUNK")) c = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
     return c;
-}
-
-void* devbuf_alloc(void* b, size_t bytes) {
-    DevBuf* d = (DevBuf*)b;
-    return d->ensure(bytes) == hipSuccess ? d->p : nullptr;
 }
 
 template <int MG>
@@ -350,12 +351,20 @@ int find_rows_chunked(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const 
             ctx->pool_loc.release();
             ctx->pool_loc = nb;
         }
+        if (ctx->fkloc.cap < (nloc + n + 1) * 4) {
+            DevBuf nb;
+            HIPCHK(nb.ensure(std::max((nloc + n + 1) * 4, ctx->fkloc.cap + ctx->fkloc.cap / 4)));
+            if (nloc) HIPCHK(hipMemcpyAsync(nb.p, ctx->fkloc.p, nloc * 4, hipMemcpyDeviceToDevice, st));
+            HIPCHK(hipStreamSynchronize(st));
+            ctx->fkloc.release();
+            ctx->fkloc = nb;
+        }
         MatProbes vc = v;
         vc.rows = v.rows + k0 * (uint64_t)(G + 1);
         HIPCHK((launch_chains<MG, MatProbes>(vc, nullptr, n, ctx->gt, mp, ctx->ss, packed, ctx->chain_tmp.p, ctx->tmp.p,
                                         ctx->radix_tmp.p, chain_of + k0,
                                         ctx->pool_loc.as<int64_t>() + nloc * (uint64_t)(G + 2), &dc->nchains, st, dc,
-                                        nullptr)));
+                                        nullptr, ctx->fkloc.as<uint32_t>() + nloc, (uint32_t)k0)));
         uint32_t nc = 0;
         HIPCHK(hipMemcpyAsync(&nc, &dc->nchains, 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
@@ -366,14 +375,16 @@ int find_rows_chunked(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const 
     HIPCHK(ctx->chain_tmp.ensure(chain_merge_tmp_bytes(nloc)));
     HIPCHK(ctx->pool.ensure((nloc + 1) * W));
     HIPCHK(ctx->radix_tmp.ensure(radix_tmp_bytes(nloc + 1)));
+    HIPCHK(ctx->fk.ensure((nloc + 1) * 4));
     HIPCHK(launch_chain_merge(ctx->pool_loc.as<int64_t>(), nloc, G, chain_of, P, ctx->pool.as<int64_t>(),
-                              ctx->chain_tmp.p, ctx->radix_tmp.p, ctx->tmp.p, &dc->nchains, st));
+                              ctx->chain_tmp.p, ctx->radix_tmp.p, ctx->tmp.p, &dc->nchains, st,
+                              ctx->fkloc.as<uint32_t>(), ctx->fk.as<uint32_t>()));
     ctx->walk_events = false;
     HIPCHK(hipEventRecord(ctx->ev[EV_CHAINS], st));
     HIPCHK(hipMemcpyAsync(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     const uint64_t nch = ctx->hc.nchains;
-    HIPCHK(ctx->chain_tmp.ensure(nch * 96 + 64 * 256));   // the replay's chain keys / ranks
+    HIPCHK(ctx->chain_tmp.ensure(nch * 112 + 64 * 256));   // the replay's chain keys / ranks
     HIPCHK(ctx->radix_tmp.ensure(radix_tmp_bytes(nch + 1)));
     uint64_t* mlog = nullptr;
     ctx->log_n = 0;
@@ -382,15 +393,11 @@ int find_rows_chunked(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const 
         HIPCHK(ctx->logB.ensure((P + 1) * 8));
         mlog = ctx->logB.as<uint64_t>();
     }
-    const uint64_t qc = std::min<uint64_t>(C, 1ull << 26);
-    uint4* qbuf = ctx->summ.as<uint4>();
-    uint32_t* pos = (uint32_t*)(qbuf + 2 * qc);
     const uint32_t lds_cap = std::max<uint32_t>(64, std::min<uint32_t>(ctx->hc.max_bucket, kReplayLdsIds));
-    HIPCHK((launch_replay_chunked<MG, MatProbes>(v, ctx->gt, mp, ctx->L, ctx->sorted_ids, P, ctx->bstart.as<uint32_t>(),
-                                            ctx->bend.as<uint32_t>(), &ctx->emit_tbl, &ctx->emit_base,
-                                            ctx->pool.as<int64_t>(), chain_of, (uint32_t)nch, ctx->chain_tmp.p,
-                                            ctx->radix_tmp.p, lds_cap, ctx->tsize.as<uint32_t>(), ctx->counters.p, st,
-                                            mlog, qc, qbuf, pos, ctx->tmp.p, devbuf_alloc, &ctx->cbuf)));
+    HIPCHK((launch_replay_kept<MG, MatProbes>(v, ctx->gt, mp, ctx->L, P, ctx->pool.as<int64_t>(), chain_of,
+                                         ctx->fk.as<uint32_t>(), (uint32_t)nch, ctx->chain_tmp.p, ctx->radix_tmp.p,
+                                         ctx->tmp.p, lds_cap, ctx->tsize.as<uint32_t>(), ctx->counters.p, nullptr, st,
+                                         mlog, &ctx->emit_tbl, &ctx->emit_base, devbuf_alloc, &ctx->cbuf)));
     if (mlog) {
         HIPCHK(hipMemcpyAsync(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
@@ -465,17 +472,13 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
     if (ctx->P >= (1ull << 32) - 64) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed probes in one FindMatches");
     const bool chunked = ctx->P > find_chunk() && !ctx->pcompat;
     HIPCHK(ctx->chain_of.ensure((ctx->P + 1) * 4));
-    if (chunked) {   // find_rows_chunked: chains per slice, replay summaries per chunk + keep flags
-        const uint64_t C = find_chunk(), qc = std::min<uint64_t>(C, 1ull << 26);
-        (void)qc;
-        for (DevBuf* b : {&ctx->pool, &ctx->tbl, &ctx->spill}) b->release();
+    // the replay keeps only the chain-first / suspicious probes (launch_replay_kept): its
+    // summaries, bucket vectors and spill live in ctx->cbuf, sized by their count
+    for (DevBuf* b : {&ctx->tbl, &ctx->spill, &ctx->summ}) b->release();
+    if (chunked) {   // find_rows_chunked: chains per slice, merged
+        ctx->pool.release();
     } else {
-        HIPCHK(ctx->tbl.ensure((ctx->P + 1) * 4));
-        HIPCHK(ctx->spill.ensure((ctx->P + 1) * 16));
         HIPCHK(ctx->pool.ensure((ctx->P + 1) * (size_t)(G + 2) * 8));
-        // summaries, their compacted copies, keep-flag scan, compacted bucket ranges (replay.hip)
-        HIPCHK(ctx->summ.ensure((ctx->P + 1) * 64 + (ctx->P + 64) * 4 + ((size_t)Tb + 64) * 8 +
-                                scan_tmp_bytes(ctx->P + 2) + 4096));
         HIPCHK(ctx->chain_tmp.ensure(chain_tmp_bytes(ctx->P + 1, Tb, G)));
     }
     HIPCHK(ctx->radix_tmp.ensure(radix_tmp_bytes(ctx->P + 1)));
@@ -502,29 +505,13 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
             };
             const bool arena = ctx->packed_path && !inside(ctx->recA, v.rows) && !inside(ctx->recB, v.rows) &&
                                !inside(ctx->recA, packed) && !inside(ctx->recB, packed);
-            const uint32_t* ids = ctx->sorted_ids;
-            const size_t ids_b = (ctx->P + 64) * 4;
-            const uint64_t qc = std::min<uint64_t>(find_chunk(), 1ull << 26);
-            const size_t summ_b = qc * 32 + (ctx->P + 64) * 4 + 4096;
-            // (in rowtmp, itself in recB, the sorted ids lie above 2 x ids_b: no overlap)
-            bool in_b = arena && ctx->sids.borrow(ctx->recB, 0, ids_b);
-            if (in_b && (const char*)ids < (const char*)ctx->recB.p + ids_b &&
-                (const char*)ids + ids_b > (const char*)ctx->recB.p)
-                in_b = false;
-            if (!in_b) {
-                ctx->sids.drop_view();
-                HIPCHK(ctx->sids.ensure(ids_b));
-            }
-            HIPCHK(hipMemcpyAsync(ctx->sids.p, ids, ctx->P * 4, hipMemcpyDeviceToDevice, st));
-            HIPCHK(hipStreamSynchronize(st));
-            ctx->sorted_ids = ctx->sids.as<uint32_t>();
+            ctx->sorted_ids = nullptr;   // the replay needs no bucket order of all probes
             ctx->sorted_buckets = nullptr;
             ctx->probe_info = nullptr;
             ctx->sorted_rec = nullptr;
             ctx->sorted_key = nullptr;
             ctx->sorted_idx = nullptr;
             ctx->rowtmp.drop_view();
-            if (!(in_b && ctx->summ.borrow(ctx->recB, ids_b, summ_b))) HIPCHK(ctx->summ.ensure(summ_b));
             if (!(arena && ctx->chain_tmp.borrow(ctx->recA, 0, chain_tmp_bytes(find_chunk() + 1, Tb, G))))
                 HIPCHK(ctx->chain_tmp.ensure(chain_tmp_bytes(find_chunk() + 1, Tb, G)));
             for (DevBuf* b : {&ctx->pbuf, &ctx->tiles, &ctx->rowtmp, &ctx->kA, &ctx->kB, &ctx->vA, &ctx->vB,
@@ -538,7 +525,7 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
         rc = find_rows_dispatch(ctx, v, packed, mp, st);
         if (rc) return rc;
         if (ctx->pcompat)   // ParallelMemHash::MergeTable (ParallelMemHash.cpp:105-121)
-            HIPCHK(launch_compat_merge(ctx->tsize.as<uint32_t>(), ctx->bstart.as<uint32_t>(), ctx->tbl.as<uint32_t>(),
+            HIPCHK(launch_compat_merge(ctx->tsize.as<uint32_t>(), ctx->emit_base, ctx->emit_tbl,
                                        ctx->pool.as<int64_t>(), G, Tb, &dc->collisions, st));
     }
     HIPCHK(hipEventRecord(ctx->ev[EV_REPLAY], st));

@@ -228,24 +228,15 @@ hipError_t launch_flat_tiles(uint64_t N, SegTile* d_tiles, hipStream_t st);
 // replay.hip
 hipError_t launch_bucket_ranges(const uint32_t* sb, uint64_t P, uint32_t* bstart, uint32_t* bend, uint32_t* d_max,
                                 hipStream_t st);
+// the replay from the probes in key order (rows v, chain_of, fk = each chain's first probe):
+// kept probes (chain-first / suspicious) bucket-sorted, summarised and replayed; the bucket
+// vectors in *tbl_out at bases *base_out (allocated through alloc)
 template <int MG, typename View>
-hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, int L, const uint64_t* probe_info,
-                         const uint32_t* sorted_ids, uint64_t P, const uint32_t* bstart, const uint32_t* bend,
-                         uint32_t* tbl, void* spill, void* summ, const int64_t* pool, const uint32_t* chain_of,
-                         uint32_t nch, void* d_tmp, void* d_radix_tmp, uint32_t lds_cap, uint32_t* tsize, void* ctr,
-                         uint64_t* dbg, hipStream_t st, uint64_t* mlog = nullptr);
-// the replay of probes too many for launch_replay's per-probe arrays, in chunks of qc
-// probes of the bucket order (qbuf: 32 B x qc, pos: P + 1 flags; alloc(alloc_ctx, bytes)
-// returns a device buffer for the compacted probes, and the bucket vectors: *tbl_out,
-// bucket b's slice at (*base_out)[b], for launch_emit)
-template <int MG, typename View>
-hipError_t launch_replay_chunked(View v, const GenomeTable& gt, const MatchParams& mp, int L,
-                                 const uint32_t* sorted_ids, uint64_t P, const uint32_t* bstart, const uint32_t* bend,
-                                 uint32_t** tbl_out, const uint32_t** base_out, const int64_t* pool,
-                                 const uint32_t* chain_of, uint32_t nch, void* d_tmp, void* d_radix_tmp,
-                                 uint32_t lds_cap, uint32_t* tsize, void* ctr, hipStream_t st, uint64_t* mlog,
-                                 uint64_t qc, void* qbuf, uint32_t* pos, void* d_scan_tmp,
-                                 void* (*alloc)(void*, size_t), void* alloc_ctx);
+hipError_t launch_replay_kept(View v, const GenomeTable& gt, const MatchParams& mp, int L, uint64_t P,
+                              const int64_t* pool, const uint32_t* chain_of, const uint32_t* fk, uint32_t nch,
+                              void* d_tmp, void* d_radix_tmp, void* d_scan_tmp, uint32_t lds_cap, uint32_t* tsize,
+                              void* ctr, uint64_t* dbg, hipStream_t st, uint64_t* mlog, uint32_t** tbl_out,
+                              const uint32_t** base_out, void* (*alloc)(void*, size_t), void* alloc_ctx);
 // chains.hip: chain labelling of the probes (key order) before the replay
 // context accessors for the multi-GPU orchestration (shard_comm.hip; mums_capi.hip)
 }  // namespace mums
@@ -283,14 +274,15 @@ size_t chain_tmp_bytes(uint64_t P, uint32_t Tb, int G);
 // per-slice chain entries merged by content (chain_of remapped, *d_nchains = merged count)
 hipError_t launch_add_offset(uint32_t* a, uint64_t n, uint32_t off, hipStream_t st);
 size_t chain_merge_tmp_bytes(uint64_t n);
+// fk_out[merged chain] = min of fk_loc over its per-slice chains
 hipError_t launch_chain_merge(const int64_t* pool_loc, uint64_t n, int G, uint32_t* chain_of, uint64_t P,
                               int64_t* pool_out, void* d_tmp, void* d_radix_tmp, void* d_scan_tmp, uint32_t* d_nchains,
-                              hipStream_t st);
+                              hipStream_t st, const uint32_t* fk_loc, uint32_t* fk_out);
 template <int MG, typename View>
 hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const GenomeTable& gt, const MatchParams& mp,
                          const SeedSpec& ss, const uint32_t* packed, void* d_chain_tmp, void* d_scan_tmp,
                          void* d_radix_tmp, uint32_t* chain_of, int64_t* pool, uint32_t* d_nchains, hipStream_t st,
-                         void* ctr = nullptr, hipEvent_t* ev_walk = nullptr);
+                         void* ctr, hipEvent_t* ev_walk, uint32_t* fk, uint32_t kbase);
 hipError_t launch_emit(const uint32_t* obase, const uint32_t* bstart, const uint32_t* tbl, const int64_t* pool, int G,
                        uint32_t table_size, uint64_t M, uint64_t* out_len, int64_t* out_s, hipStream_t st);
 

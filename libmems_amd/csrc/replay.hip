@@ -162,28 +162,6 @@ __global__ __launch_bounds__(kBlock) void dense_scatter_kernel(const uint32_t* _
     if (i < n) bkey[ord[i]] = rank[i];
 }
 
-// per probe in bucket order: {presence mask, first-genome start, chain id, probe id | flags}
-template <int MG, typename View>
-__global__ __launch_bounds__(kBlock) void probe_summary_kernel(View v, GenomeTable gt, MatchParams mp, int L,
-                                                               const uint64_t* __restrict__ probe_info,
-                                                               const uint32_t* __restrict__ ids, uint64_t q0,
-                                                               uint64_t q1, const uint32_t* __restrict__ chain_of,
-                                                               uint4* __restrict__ summ, uint4* __restrict__ summ_b,
-                                                               uint32_t* __restrict__ first_pos,
-                                                               const uint32_t* __restrict__ bkey) {
-    const uint64_t q = q0 + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (q >= q1) return;
-    const uint32_t k = ids[q];
-    Mhe<MG> Q;
-    load_probe<MG>(v, k, gt.G, L, Q);
-    const uint32_t cid = chain_of[k];
-    summ[q - q0] = make_uint4(block_key<MG>(Q, gt.G, bkey, cid), (uint32_t)start_at(Q, first_start(Q)), cid, 0u);
-    summ_b[q - q0] = make_uint4(0u, 0u, 0u, k);   // .w: the probe (AddHashEntry call) index
-    // probes run in ascending q, so the plain read filters nearly every later atomic
-    if ((uint32_t)q < __hip_atomic_load(&first_pos[cid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-        atomicMin(&first_pos[cid], (uint32_t)q);
-}
-
 // Sort keys of the chain entries: (hash bucket, block key) and first-genome start (the
 // block key orders blocks as MheCompare does, see slot_cmp).
 __global__ __launch_bounds__(kBlock) void chain_keys_kernel(const int64_t* __restrict__ pool, uint32_t nch, int G,
@@ -260,21 +238,6 @@ __global__ __launch_bounds__(kBlock) void chain_sb_kernel(const int64_t* __restr
     int64_t es = 0;
     for (int g = G - 1; g >= 0; --g) es = e[2 + g] != 0 ? e[2 + g] : es;
     chain_sb[c] = make_uint4((uint32_t)es, (uint32_t)e[0], rank[c], next_s[c]);
-}
-
-__global__ __launch_bounds__(kBlock) void probe_flags_kernel(uint4* __restrict__ summ, uint4* __restrict__ summ_b,
-                                                             uint64_t n, uint64_t q0,
-                                                             const uint32_t* __restrict__ first_pos,
-                                                             const uint4* __restrict__ chain_sb) {
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    uint4 r = summ[i];
-    const uint4 cs = chain_sb[r.z];
-    const bool first = first_pos[r.z] == (uint32_t)(q0 + i);
-    const bool susp = !first && r.y >= cs.w;
-    r.w |= (first ? 0x80000000u : 0u) | (susp ? 0x40000000u : 0u);
-    summ[i] = r;
-    summ_b[i] = make_uint4(cs.x, cs.y, cs.z, summ_b[i].w);
 }
 
 // the probe of stream group k (AddHashEntry's argument), built on the rare slow path
@@ -1077,63 +1040,6 @@ __global__ __launch_bounds__(kBlock) void bigq_final_kernel(const uint32_t* __re
     if (r < R) cnt[r] = 1u + dup[r];
 }
 
-// chunked FindMatches (probes beyond one pass of per-probe arrays): the keep flags of
-// bucket-ordered probes [q0, q0 + n) into the global flag array, then their compaction
-__global__ __launch_bounds__(kBlock) void keep_chunk_kernel(const uint4* __restrict__ summ, uint64_t n, uint64_t q0,
-                                                            uint32_t* __restrict__ keep) {
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < n) keep[q0 + i] = (summ[i].w & 0xC0000000u) ? 1u : 0u;
-}
-
-__global__ __launch_bounds__(kBlock) void compact_chunk_kernel(const uint4* __restrict__ summ,
-                                                               const uint4* __restrict__ summ_b, uint64_t n,
-                                                               uint64_t q0, const uint32_t* __restrict__ pos,
-                                                               uint4* __restrict__ sc, uint4* __restrict__ sbc) {
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    const uint4 x = summ[i];
-    if (x.w & 0xC0000000u) {
-        sc[pos[q0 + i]] = x;
-        sbc[pos[q0 + i]] = summ_b[i];
-    }
-}
-
-// Probes that are neither chain-first nor suspicious (flag bits 31 / 30 clear) collide
-// with their chain entry without touching the vector, so the replay only needs the
-// others: keep flags -> exclusive scan -> compacted summaries and bucket ranges; the
-// dropped probes are counted as collisions (MemHash::m_collision_count) up front.
-__global__ __launch_bounds__(kBlock) void keep_flags_kernel(const uint4* __restrict__ summ, uint64_t P,
-                                                            uint32_t* __restrict__ keep) {
-    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (k <= P) keep[k] = (k < P && (summ[k].w & 0xC0000000u)) ? 1u : 0u;
-}
-
-__global__ __launch_bounds__(kBlock) void compact_summ_kernel(const uint4* __restrict__ summ,
-                                                              const uint4* __restrict__ summ_b,
-                                                              const uint32_t* __restrict__ pos, uint64_t P,
-                                                              uint4* __restrict__ sc, uint4* __restrict__ sbc) {
-    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (k >= P) return;
-    const uint4 x = summ[k];
-    if (x.w & 0xC0000000u) {
-        sc[pos[k]] = x;
-        sbc[pos[k]] = summ_b[k];
-    }
-}
-
-__global__ __launch_bounds__(kBlock) void compact_ranges_kernel(const uint32_t* __restrict__ bstart,
-                                                                const uint32_t* __restrict__ bend,
-                                                                const uint32_t* __restrict__ pos, uint32_t Tb,
-                                                                uint64_t P, uint32_t* __restrict__ cbeg,
-                                                                uint32_t* __restrict__ cend,
-                                                                DevCounters* __restrict__ ctr) {
-    const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
-    if (b == 0) atomicAdd(&ctr->collisions, (unsigned long long)(P - pos[P]));
-    if (b >= Tb) return;
-    cbeg[b] = pos[bstart[b]];
-    cend[b] = pos[bend[b]];
-}
-
 __global__ void bucket_ranges_kernel(const uint32_t* __restrict__ sb, uint64_t P, uint32_t* __restrict__ bstart,
                                      uint32_t* __restrict__ bend, uint32_t* __restrict__ d_max) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1446,124 +1352,134 @@ size_t replay_scratch_bytes(uint64_t n, uint32_t table_size) {
     return (n + 1) * 4 + (n + 2 + (uint64_t)table_size) * 4 + (n + 1) * 16 + 64 + (kGridSlow + 1) * 4 + 5 * 256;
 }
 
-template <int MG, typename View>
-hipError_t launch_replay(View v, const GenomeTable& gt, const MatchParams& mp, int L, const uint64_t* probe_info,
-                         const uint32_t* sorted_ids, uint64_t P, const uint32_t* bstart, const uint32_t* bend,
-                         uint32_t* tbl, void* spill, void* summ, const int64_t* pool, const uint32_t* chain_of,
-                         uint32_t nch, void* d_tmp, void* d_radix_tmp, uint32_t lds_cap, uint32_t* tsize, void* ctr,
-                         uint64_t* dbg, hipStream_t st, uint64_t* mlog) {
-    char* p = (char*)d_tmp;
-    auto carve = [&](size_t bytes) {
-        char* r = p;
-        p += (bytes + 255) & ~(size_t)255;
-        return (void*)r;
-    };
-    uint64_t* key_s = (uint64_t*)carve((size_t)nch * 8);
-    uint64_t* key_b = (uint64_t*)carve((size_t)nch * 8);
-    uint64_t* key_g = (uint64_t*)carve((size_t)nch * 8);
-    uint64_t* kA = (uint64_t*)carve((size_t)nch * 8);
-    uint64_t* kB = (uint64_t*)carve((size_t)nch * 8);
-    uint32_t* vA = (uint32_t*)carve((size_t)nch * 4);
-    uint32_t* vB = (uint32_t*)carve((size_t)nch * 4);
-    uint32_t* first_pos = (uint32_t*)carve((size_t)nch * 4);
-    uint32_t* next_s = (uint32_t*)carve((size_t)nch * 4);
-    uint32_t* rank = (uint32_t*)carve((size_t)nch * 4);
-    uint4* chain_sb = (uint4*)carve((size_t)nch * 16);
-    uint32_t* bkey_buf = (uint32_t*)carve((size_t)nch * 4);
-    uint4* summ_b = (uint4*)summ + (P + 1);
-    const unsigned pgrid = (unsigned)((P + kBlock - 1) / kBlock), cgrid = (nch + kBlock - 1) / kBlock;
-    hipError_t e = hipSuccess;
-    void* stmp0 = (void*)(((uintptr_t)((uint32_t*)(summ_b + 3 * (P + 1)) + (P + 64) + 2 * (mp.table_size + 64)) + 255) &
-                          ~(uintptr_t)255);   // = stmp below, free until then
-    const uint32_t* bkey = block_keys(pool, nch, gt.G, key_g, kA, vA, kB, vB, next_s, bkey_buf, d_radix_tmp, stmp0,
-                                      st, &e);
-    if (e != hipSuccess) return e;
-    if ((e = hipMemsetAsync(first_pos, 0xFF, (size_t)nch * 4, st)) != hipSuccess) return e;
-    hipLaunchKernelGGL((probe_summary_kernel<MG, View>), dim3(pgrid), dim3(kBlock), 0, st, v, gt, mp, L, probe_info,
-                       sorted_ids, (uint64_t)0, P, chain_of, (uint4*)summ, summ_b, first_pos, bkey);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    // chains in (bucket, block, first start) order -> next_s per chain
-    hipLaunchKernelGGL(chain_keys_kernel, dim3(cgrid), dim3(kBlock), 0, st, pool, nch, gt.G, mp.table_size,
-                       1.0 / (double)mp.table_size, bkey, key_s, key_b);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    int buf = 0;
-    if ((e = radix_sort<uint64_t>(key_s, nullptr, nch, 32, kA, vA, kB, vB, d_radix_tmp, &buf, st)) != hipSuccess)
-        return e;
-    const uint32_t* ord1 = buf ? vB : vA;
-    hipLaunchKernelGGL(gather_u64_kernel, dim3(cgrid), dim3(kBlock), 0, st, key_b, ord1, nch, key_g);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    uint32_t* vin = buf ? vB : vA;
-    uint32_t* vout = buf ? vA : vB;
-    int buf2 = 0;
-    // pass 0 reads vin and writes vout; later passes ping-pong between vout and vin
-    if ((e = radix_sort<uint64_t>(key_g, vin, nch, 64, kA, vout, kB, vin, d_radix_tmp, &buf2, st)) != hipSuccess)
-        return e;
-    const uint32_t* ord = buf2 ? vin : vout;
-    hipLaunchKernelGGL(chain_next_kernel, dim3(cgrid), dim3(kBlock), 0, st, ord, key_s, key_b, nch, next_s, rank);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(chain_sb_kernel, dim3(cgrid), dim3(kBlock), 0, st, pool, nch, gt.G, rank, next_s, chain_sb);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(probe_flags_kernel, dim3(pgrid), dim3(kBlock), 0, st, (uint4*)summ, summ_b, P, (uint64_t)0,
-                       first_pos, chain_sb);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    // the replay reads only chain-first / suspicious probes (summ buffer: 2 more uint4
-    // arrays, the scanned keep flags and the compacted bucket ranges after the originals)
-    uint4* summ_c = summ_b + (P + 1);
-    uint4* summ_bc = summ_c + (P + 1);
-    uint32_t* pos = (uint32_t*)(summ_bc + (P + 1));
-    uint32_t* cbeg = pos + (P + 64);
-    uint32_t* cend = cbeg + mp.table_size + 64;
-    void* stmp = (void*)(((uintptr_t)(cend + mp.table_size + 64) + 255) & ~(uintptr_t)255);
-    hipLaunchKernelGGL(keep_flags_kernel, dim3((unsigned)((P + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
-                       (const uint4*)summ, P, pos);
-    if ((e = exclusive_scan_u32(pos, P + 1, stmp, nullptr, st)) != hipSuccess) return e;
-    hipLaunchKernelGGL(compact_summ_kernel, dim3(pgrid), dim3(kBlock), 0, st, (const uint4*)summ,
-                       (const uint4*)summ_b, pos, P, summ_c, summ_bc);
-    hipLaunchKernelGGL(compact_ranges_kernel, dim3((mp.table_size + kBlock - 1) / kBlock), dim3(kBlock), 0, st,
-                       bstart, bend, pos, mp.table_size, P, cbeg, cend, (DevCounters*)ctr);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (getenv("MUMS_DEV_REPLAY_STATS")) {   // development: what keeps the big buckets off the fast path
-        const uint32_t Tb = mp.table_size;
-        std::vector<uint32_t> hb(Tb), he(Tb);
-        (void)hipMemcpyAsync(hb.data(), cbeg, Tb * 4, hipMemcpyDeviceToHost, st);
-        (void)hipMemcpyAsync(he.data(), cend, Tb * 4, hipMemcpyDeviceToHost, st);
-        (void)hipStreamSynchronize(st);
-        for (uint32_t b = 0; b < Tb; ++b) {
-            const uint32_t K = he[b] - hb[b];
-            if (K < 20000) continue;
-            std::vector<uint4> a(K), c(K);
-            (void)hipMemcpy(a.data(), summ_c + hb[b], K * 16, hipMemcpyDeviceToHost);
-            (void)hipMemcpy(c.data(), summ_bc + hb[b], K * 16, hipMemcpyDeviceToHost);
-            uint32_t nfirst = 0, nsusp = 0, ntie = 0, rmin = ~0u, rmax = 0;
-            long first_slow = -1;
-            for (uint32_t k = 0; k < K; ++k) {
-                const bool f = a[k].w & 0x80000000u, su = a[k].w & 0x40000000u, ti = c[k].z & 0x80000000u;
-                nfirst += f; nsusp += su; ntie += ti;
-                if ((!f || su || ti) && first_slow < 0) first_slow = k;
-                rmin = std::min(rmin, c[k].z & 0x7FFFFFFFu); rmax = std::max(rmax, c[k].z & 0x7FFFFFFFu);
-            }
-            fprintf(stderr, "bucket %u: K %u first %u susp %u tied %u rank span %u first slow at %ld\n", b, K, nfirst,
-                    nsusp, ntie, rmax - rmin + 1, first_slow);
-        }
+// ---- the replay from the probes in key order ------------------------------------------
+// Only two kinds of AddHashEntry call can touch a bucket vector: the chain's first probe in
+// key order (= in its bucket's order: the bucket partition is stable)
+// inserts the chain, and a suspicious probe (another chain of the bucket and block starts in
+// [chain start, probe start]) runs the exact search; every other probe collides with its
+// chain's entry.  Both tests need only the probe's chain and first-genome start, so one pass
+// over the probes in key order keeps those (first: fk[chain] == k, from chains.hip; suspicious:
+// start >= next_s of the chain), and the bucket order, the summaries and the replay work on
+// the kept probes alone -- no per-probe pass in bucket order.
+constexpr int kKeepIPT = 8;
+
+__device__ __forceinline__ uint32_t row_first_start(const int64_t* __restrict__ rows, uint64_t k, int G) {
+    const int64_t* r = rows + k * (uint64_t)(G + 1);
+    for (int g = 0; g < G; ++g) {
+        const int64_t x = r[g];
+        if (x != 0) return (uint32_t)x;   // forward by SetDirection: the first present genome's start > 0
     }
-    return replay_tail<MG, View>(v, gt, mp, L, probe_info, summ_c, summ_bc, cbeg, cend, bstart, tbl, spill, pool,
-                                 chain_sb, P, carve(replay_scratch_bytes(P, mp.table_size)), stmp, lds_cap, tsize,
-                                 ctr, dbg, st, mlog);
+    return 0u;
 }
 
-// FindMatches replay when the per-probe arrays of launch_replay do not fit (BASELINE
-// config 5: 2.5e9 probes): the probes are visited in bucket order in chunks of qc, twice
-// -- once for the chain-first positions and the keep flags, once to compact the kept
-// ones -- so only the compacted probes (chain-first or suspicious) and one flag word per
-// probe stay resident.  Same kernels, same result as launch_replay.
+// per chain, what the keep test reads: {first probe (key order), next_s, hash bucket, 0}
+__global__ __launch_bounds__(kBlock) void chain_keep_kernel(const uint32_t* __restrict__ fk,
+                                                            const uint32_t* __restrict__ next_s,
+                                                            const uint64_t* __restrict__ key_b, uint32_t nch,
+                                                            uint4* __restrict__ ck) {
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    if (c < nch) ck[c] = make_uint4(fk[c], next_s[c], (uint32_t)(key_b[c] >> 32), 0u);
+}
+
+// kept probe k (chain-first or suspicious) -> *key = bucket << 32 | k
+__device__ __forceinline__ bool keep_probe(const int64_t* __restrict__ rows, uint64_t k, int G,
+                                           const uint32_t* __restrict__ chain_of, const uint4* __restrict__ ck,
+                                           uint64_t* key) {
+    const uint4 c = ck[chain_of[k]];
+    const bool first = c.x == (uint32_t)k;
+    bool keep = first;
+    if (!first) keep = row_first_start(rows, k, G) >= c.y;
+    *key = ((uint64_t)c.z << 32) | k;
+    return keep;
+}
+
+// the kept keys, one pass: per block an offset from one atomic (the order is restored by
+// the sort that follows: the key holds the probe index)
+__global__ __launch_bounds__(kBlock) void keep_fill_kernel(const int64_t* __restrict__ rows, uint64_t P, int G,
+                                                           const uint32_t* __restrict__ chain_of,
+                                                           const uint4* __restrict__ ck,
+                                                           unsigned int* __restrict__ nkept, uint64_t cap,
+                                                           uint64_t* __restrict__ kept) {
+    __shared__ uint32_t s_w[kBlock / 64 + 1];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint64_t keys[kKeepIPT];
+    uint32_t want = 0;
+    #pragma unroll
+    for (int i = 0; i < kKeepIPT; ++i) {
+        const uint64_t k = (uint64_t)blockIdx.x * (kBlock * kKeepIPT) + (uint64_t)i * kBlock + threadIdx.x;
+        keys[i] = 0;
+        if (k < P && keep_probe(rows, k, G, chain_of, ck, &keys[i])) want |= 1u << i;
+    }
+    const uint32_t n = (uint32_t)__builtin_popcount(want);
+    uint32_t x = n;
+    #pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) s_w[wv] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) {
+            const uint32_t c = s_w[w];
+            s_w[w] = tot;
+            tot += c;
+        }
+        s_w[kBlock / 64] = tot ? atomicAdd(nkept, tot) : 0u;
+    }
+    __syncthreads();
+    uint64_t o = (uint64_t)s_w[kBlock / 64] + s_w[wv] + x - n;
+    #pragma unroll
+    for (int i = 0; i < kKeepIPT; ++i)
+        if ((want >> i) & 1u) {
+            if (o < cap) kept[o] = keys[i];
+            ++o;
+        }
+}
+
+// summaries of the kept probes in bucket order (sorted keys): {block key, first-genome start,
+// chain id, flags (bit 31 chain-first, bit 30 suspicious)}, {chain entry's start, its length,
+// its rank | tie, probe index}
 template <int MG, typename View>
-hipError_t launch_replay_chunked(View v, const GenomeTable& gt, const MatchParams& mp, int L,
-                                 const uint32_t* sorted_ids, uint64_t P, const uint32_t* bstart, const uint32_t* bend,
-                                 uint32_t** tbl_out, const uint32_t** base_out, const int64_t* pool,
-                                 const uint32_t* chain_of, uint32_t nch, void* d_tmp, void* d_radix_tmp,
-                                 uint32_t lds_cap, uint32_t* tsize, void* ctr, hipStream_t st, uint64_t* mlog,
-                                 uint64_t qc, void* qbuf, uint32_t* pos, void* d_scan_tmp,
-                                 void* (*alloc)(void*, size_t), void* alloc_ctx) {
+__global__ __launch_bounds__(kBlock) void kept_summary_kernel(View v, GenomeTable gt, int L,
+                                                              const uint64_t* __restrict__ skey, uint32_t Kc,
+                                                              const uint32_t* __restrict__ chain_of,
+                                                              const uint32_t* __restrict__ fk,
+                                                              const uint4* __restrict__ chain_sb,
+                                                              const uint32_t* __restrict__ bkey,
+                                                              uint4* __restrict__ summ, uint4* __restrict__ summ_b) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= Kc) return;
+    const uint32_t k = (uint32_t)skey[i];
+    Mhe<MG> Q;
+    load_probe<MG>(v, k, gt.G, L, Q);
+    const uint32_t cid = chain_of[k];
+    const uint4 cs = chain_sb[cid];
+    const bool first = fk[cid] == k;
+    summ[i] = make_uint4(block_key<MG>(Q, gt.G, bkey, cid), (uint32_t)start_at(Q, first_start(Q)), cid,
+                         first ? 0x80000000u : 0x40000000u);
+    summ_b[i] = make_uint4(cs.x, cs.y, cs.z, k);
+}
+
+// bucket ranges of the sorted kept keys (cbeg / cend zeroed before)
+__global__ __launch_bounds__(kBlock) void kept_ranges_kernel(const uint64_t* __restrict__ skey, uint32_t Kc,
+                                                             uint32_t* __restrict__ cbeg, uint32_t* __restrict__ cend,
+                                                             uint64_t P, DevCounters* __restrict__ ctr) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i == 0) atomicAdd(&ctr->collisions, (unsigned long long)(P - Kc));   // the dropped probes collide
+    if (i >= Kc) return;
+    const uint32_t b = (uint32_t)(skey[i] >> 32);
+    if (i == 0 || (uint32_t)(skey[i - 1] >> 32) != b) cbeg[b] = i;
+    if (i + 1 == Kc || (uint32_t)(skey[i + 1] >> 32) != b) cend[b] = i + 1;
+}
+
+template <int MG, typename View>
+hipError_t launch_replay_kept(View v, const GenomeTable& gt, const MatchParams& mp, int L, uint64_t P,
+                              const int64_t* pool, const uint32_t* chain_of, const uint32_t* fk, uint32_t nch,
+                              void* d_tmp, void* d_radix_tmp, void* d_scan_tmp, uint32_t lds_cap, uint32_t* tsize,
+                              void* ctr, uint64_t* dbg, hipStream_t st, uint64_t* mlog, uint32_t** tbl_out,
+                              const uint32_t** base_out, void* (*alloc)(void*, size_t), void* alloc_ctx) {
     char* p = (char*)d_tmp;
     auto carve = [&](size_t bytes) {
         char* r = p;
@@ -1577,25 +1493,19 @@ hipError_t launch_replay_chunked(View v, const GenomeTable& gt, const MatchParam
     uint64_t* kB = (uint64_t*)carve((size_t)nch * 8);
     uint32_t* vA = (uint32_t*)carve((size_t)nch * 4);
     uint32_t* vB = (uint32_t*)carve((size_t)nch * 4);
-    uint32_t* first_pos = (uint32_t*)carve((size_t)nch * 4);
     uint32_t* next_s = (uint32_t*)carve((size_t)nch * 4);
     uint32_t* rank = (uint32_t*)carve((size_t)nch * 4);
     uint4* chain_sb = (uint4*)carve((size_t)nch * 16);
     uint32_t* bkey_buf = (uint32_t*)carve((size_t)nch * 4);
-    uint4* qs = (uint4*)qbuf;          // one chunk's summaries
-    uint4* qsb = qs + qc;
+    const uint64_t nblk = (P + kBlock * kKeepIPT - 1) / (kBlock * kKeepIPT);
+    unsigned int* nkept = (unsigned int*)carve(64);
+    uint4* ckeep = (uint4*)carve((size_t)nch * 16);
     const unsigned cgrid = (nch + kBlock - 1) / kBlock;
     hipError_t e = hipSuccess;
-    const uint32_t* bkey = block_keys(pool, nch, gt.G, key_g, kA, vA, kB, vB, next_s, bkey_buf, d_radix_tmp, d_scan_tmp,
-                                      st, &e);
+    const uint32_t* bkey = block_keys(pool, nch, gt.G, key_g, kA, vA, kB, vB, next_s, bkey_buf, d_radix_tmp,
+                                      d_scan_tmp, st, &e);
     if (e != hipSuccess) return e;
-    if ((e = hipMemsetAsync(first_pos, 0xFF, (size_t)nch * 4, st)) != hipSuccess) return e;
-    auto summaries = [&](uint64_t q0, uint64_t n) {
-        hipLaunchKernelGGL((probe_summary_kernel<MG, View>), dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock),
-                           0, st, v, gt, mp, L, nullptr, sorted_ids, q0, q0 + n, chain_of, qs, qsb, first_pos, bkey);
-    };
-    for (uint64_t q0 = 0; q0 < P; q0 += qc) summaries(q0, std::min(qc, P - q0));   // chain-first positions
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // chains in (bucket, block, first start) order -> rank, next_s per chain
     hipLaunchKernelGGL(chain_keys_kernel, dim3(cgrid), dim3(kBlock), 0, st, pool, nch, gt.G, mp.table_size,
                        1.0 / (double)mp.table_size, bkey, key_s, key_b);
     if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -1612,48 +1522,70 @@ hipError_t launch_replay_chunked(View v, const GenomeTable& gt, const MatchParam
     const uint32_t* ord = buf2 ? vin : vout;
     hipLaunchKernelGGL(chain_next_kernel, dim3(cgrid), dim3(kBlock), 0, st, ord, key_s, key_b, nch, next_s, rank);
     hipLaunchKernelGGL(chain_sb_kernel, dim3(cgrid), dim3(kBlock), 0, st, pool, nch, gt.G, rank, next_s, chain_sb);
+    hipLaunchKernelGGL(chain_keep_kernel, dim3(cgrid), dim3(kBlock), 0, st, fk, (const uint32_t*)next_s,
+                       (const uint64_t*)key_b, nch, ckeep);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    // pass 1: keep flags; pass 2: compaction into Kc slots
-    for (uint64_t q0 = 0; q0 < P; q0 += qc) {
-        const uint64_t n = std::min(qc, P - q0);
-        const unsigned g = (unsigned)((n + kBlock - 1) / kBlock);
-        summaries(q0, n);
-        hipLaunchKernelGGL(probe_flags_kernel, dim3(g), dim3(kBlock), 0, st, qs, qsb, n, q0, first_pos, chain_sb);
-        hipLaunchKernelGGL(keep_chunk_kernel, dim3(g), dim3(kBlock), 0, st, (const uint4*)qs, n, q0, pos);
-    }
-    if ((e = hipMemsetAsync(pos + P, 0, 4, st)) != hipSuccess) return e;
-    if ((e = exclusive_scan_u32(pos, P + 1, d_scan_tmp, nullptr, st)) != hipSuccess) return e;
-    uint32_t Kc = 0;
-    if ((e = hipMemcpyAsync(&Kc, pos + P, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
-    if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+    // the kept probes, one pass into a buffer of a guessed capacity (again, exactly sized,
+    // when the guess was short)
+    const int G = gt.G;
     const uint32_t Tb = mp.table_size;
-    // compacted probes, their bucket ranges, and the bucket vectors: a bucket ends with at
-    // most one entry per compacted probe, so tbl / spill slices start at cbeg too
-    char* cb = (char*)alloc(alloc_ctx, ((uint64_t)Kc + 1) * 52 + ((uint64_t)Tb + 64) * 8 +
-                                           replay_scratch_bytes(Kc, Tb) + 4096);
-    if (!cb) return hipErrorOutOfMemory;
-    uint4* summ_c = (uint4*)cb;
-    uint4* summ_bc = summ_c + (Kc + 1);
-    uint4* spill = summ_bc + (Kc + 1);
-    uint32_t* tbl = (uint32_t*)(spill + (Kc + 1));
-    uint32_t* cbeg = tbl + Kc + 1;
-    uint32_t* cend = cbeg + Tb + 32;
-    void* scr = (void*)(((uintptr_t)(cend + Tb + 32) + 255) & ~(uintptr_t)255);
+    int tbits = 1;
+    while (tbits < 32 && ((uint64_t)1 << tbits) < (uint64_t)Tb) ++tbits;
+    uint64_t cap = std::min<uint64_t>(P, (uint64_t)nch * 2 + (P >> 6) + 4096);
+    uint32_t Kc = 0;
+    char* cb = nullptr;
+    uint64_t* kept = nullptr;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        const uint64_t K1 = cap + 1;
+        const size_t rtmp = radix_tmp_bytes(K1);
+        cb = (char*)alloc(alloc_ctx, K1 * (8 * 3 + 4 * 2 + 16 * 3 + 4) + ((uint64_t)Tb + 64) * 8 + rtmp +
+                                         replay_scratch_bytes(cap, Tb) + 16 * 256);
+        if (!cb) return hipErrorOutOfMemory;
+        kept = (uint64_t*)cb;
+        if ((e = hipMemsetAsync(nkept, 0, 4, st)) != hipSuccess) return e;
+        hipLaunchKernelGGL(keep_fill_kernel, dim3((unsigned)nblk), dim3(kBlock), 0, st, v.rows, P, G, chain_of,
+                           (const uint4*)ckeep, nkept, cap, kept);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if ((e = hipMemcpyAsync(&Kc, nkept, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+        if (Kc <= cap) break;
+        cap = Kc;
+    }
+    const uint64_t K1 = (uint64_t)cap + 1;
+    const size_t rtmp = radix_tmp_bytes(K1);
+    p = cb;
+    carve(K1 * 8);   // kept
+    uint64_t* sA = (uint64_t*)carve(K1 * 8);
+    uint64_t* sB = (uint64_t*)carve(K1 * 8);
+    uint32_t* iA = (uint32_t*)carve(K1 * 4);
+    uint32_t* iB = (uint32_t*)carve(K1 * 4);
+    uint4* summ_c = (uint4*)carve(K1 * 16);
+    uint4* summ_bc = (uint4*)carve(K1 * 16);
+    uint4* spill = (uint4*)carve(K1 * 16);
+    uint32_t* tbl = (uint32_t*)carve(K1 * 4);
+    uint32_t* cbeg = (uint32_t*)carve(((uint64_t)Tb + 32) * 4);
+    uint32_t* cend = (uint32_t*)carve(((uint64_t)Tb + 32) * 4);
+    void* rt = carve(rtmp);
+    void* scr = carve(replay_scratch_bytes(cap, Tb));
     *tbl_out = tbl;
     *base_out = cbeg;
-    for (uint64_t q0 = 0; q0 < P; q0 += qc) {
-        const uint64_t n = std::min(qc, P - q0);
-        const unsigned g = (unsigned)((n + kBlock - 1) / kBlock);
-        summaries(q0, n);
-        hipLaunchKernelGGL(probe_flags_kernel, dim3(g), dim3(kBlock), 0, st, qs, qsb, n, q0, first_pos, chain_sb);
-        hipLaunchKernelGGL(compact_chunk_kernel, dim3(g), dim3(kBlock), 0, st, (const uint4*)qs, (const uint4*)qsb, n,
-                           q0, (const uint32_t*)pos, summ_c, summ_bc);
+    const uint64_t* skey = kept;
+    if (Kc > 1) {
+        int b3 = 0;
+        if ((e = radix_sort<uint64_t>(kept, nullptr, Kc, 32 + tbits, sA, iA, sB, iB, rt, &b3, st)) != hipSuccess)
+            return e;
+        skey = b3 ? sB : sA;
     }
-    hipLaunchKernelGGL(compact_ranges_kernel, dim3((Tb + kBlock - 1) / kBlock), dim3(kBlock), 0, st, bstart, bend, pos,
-                       Tb, P, cbeg, cend, (DevCounters*)ctr);
+    if ((e = hipMemsetAsync(cbeg, 0, ((uint64_t)Tb + 32) * 4, st)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(cend, 0, ((uint64_t)Tb + 32) * 4, st)) != hipSuccess) return e;
+    const unsigned kgrid = (unsigned)((Kc + 1 + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL((kept_summary_kernel<MG, View>), dim3(kgrid), dim3(kBlock), 0, st, v, gt, L, skey, Kc, chain_of,
+                       fk, (const uint4*)chain_sb, bkey, summ_c, summ_bc);
+    hipLaunchKernelGGL(kept_ranges_kernel, dim3(kgrid), dim3(kBlock), 0, st, skey, Kc, cbeg, cend, P,
+                       (DevCounters*)ctr);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     return replay_tail<MG, View>(v, gt, mp, L, nullptr, summ_c, summ_bc, cbeg, cend, cbeg, tbl, spill, pool, chain_sb,
-                                 Kc, scr, d_scan_tmp, lds_cap, tsize, ctr, nullptr, st, mlog);
+                                 Kc, scr, d_scan_tmp, lds_cap, tsize, ctr, dbg, st, mlog);
 }
 
 hipError_t launch_emit(const uint32_t* obase, const uint32_t* bstart, const uint32_t* tbl, const int64_t* pool, int G,
@@ -1664,28 +1596,16 @@ hipError_t launch_emit(const uint32_t* obase, const uint32_t* bstart, const uint
     return hipGetLastError();
 }
 
-#define MUMS_INST_REPLAY(MG, V)                                                                                   \
-    template hipError_t launch_replay<MG, V>(V, const GenomeTable&, const MatchParams&, int, const uint64_t*,      \
-                                             const uint32_t*, uint64_t, const uint32_t*, const uint32_t*,          \
-                                             uint32_t*, void*, void*, const int64_t*, const uint32_t*, uint32_t,   \
-                                             void*, void*, uint32_t, uint32_t*, void*, uint64_t*, hipStream_t,    \
-                                             uint64_t*);
-#define MUMS_INST_REPLAY_CHUNKED(MG, V)                                                                           \
-    template hipError_t launch_replay_chunked<MG, V>(V, const GenomeTable&, const MatchParams&, int, const uint32_t*, \
-                                                     uint64_t, const uint32_t*, const uint32_t*, uint32_t**,        \
-                                                     const uint32_t**, const int64_t*, const uint32_t*, uint32_t,   \
-                                                     void*, void*, uint32_t, uint32_t*, void*, hipStream_t,         \
-                                                     uint64_t*, uint64_t, void*, uint32_t*, void*,                  \
-                                                     void* (*)(void*, size_t), void*);
-MUMS_INST_REPLAY_CHUNKED(4, MatProbes)
-MUMS_INST_REPLAY_CHUNKED(8, MatProbes)
-MUMS_INST_REPLAY_CHUNKED(16, MatProbes)
-MUMS_INST_REPLAY_CHUNKED(32, MatProbes)
-MUMS_INST_REPLAY_CHUNKED(64, MatProbes)
-MUMS_INST_REPLAY(4, MatProbes)
-MUMS_INST_REPLAY(8, MatProbes)
-MUMS_INST_REPLAY(16, MatProbes)
-MUMS_INST_REPLAY(32, MatProbes)
-MUMS_INST_REPLAY(64, MatProbes)
+#define MUMS_INST_REPLAY_KEPT(MG, V)                                                                              \
+    template hipError_t launch_replay_kept<MG, V>(V, const GenomeTable&, const MatchParams&, int, uint64_t,           \
+                                                  const int64_t*, const uint32_t*, const uint32_t*, uint32_t, void*,  \
+                                                  void*, void*, uint32_t, uint32_t*, void*, uint64_t*, hipStream_t,   \
+                                                  uint64_t*, uint32_t**, const uint32_t**, void* (*)(void*, size_t),  \
+                                                  void*);
+MUMS_INST_REPLAY_KEPT(4, MatProbes)
+MUMS_INST_REPLAY_KEPT(8, MatProbes)
+MUMS_INST_REPLAY_KEPT(16, MatProbes)
+MUMS_INST_REPLAY_KEPT(32, MatProbes)
+MUMS_INST_REPLAY_KEPT(64, MatProbes)
 
 }  // namespace mums

@@ -1,7 +1,8 @@
 """MemHash::SetMatchLog (MemHash.h:149; MemHash.cpp:238-241): the entries the log stream
 receives, in insertion (AddHashEntry call) order, = the oracle's inserts in its call order,
 on every replay path (per-bucket rounds, the whole-bucket fast path, the big-bucket rank
-counts with suspicious probes, forced onto small buckets by MUMS_DEV_BIG_BUCKET)."""
+counts with suspicious probes and their closed-form rounds, forced onto small buckets by
+MUMS_DEV_BIG_BUCKET / MUMS_DEV_GRID_SLOW)."""
 import numpy as np
 import pytest
 
@@ -10,10 +11,13 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("G,n,w,p,table_size,big", [(3, 200_000, 15, 0.03, 40000, None), (4, 1_000_000, 15, 0.01, 40000, None),
                                                    (4, 1_000_000, 15, 0.01, 40000, "8"), (5, 300_000, 13, 0.02, 7, None),
-                                                   (4, 500_000, 15, 1.0, 40000, None), (3, 400_000, 11, 0.05, 1, "8")])
+                                                   (4, 500_000, 15, 1.0, 40000, None), (3, 400_000, 11, 0.05, 1, "8"),
+                                                   (4, 1_000_000, 15, 0.01, 40000, "8+closed")])
 def test_match_log_order(gpu_lib, oracle_mod, monkeypatch, G, n, w, p, table_size, big):
     if big:
-        monkeypatch.setenv("MUMS_DEV_BIG_BUCKET", big)
+        monkeypatch.setenv("MUMS_DEV_BIG_BUCKET", big.split("+")[0])
+        if big.endswith("+closed"):   # the closed-form big-bucket rounds (bigq_*)
+            monkeypatch.setenv("MUMS_DEV_GRID_SLOW", "0")
     seqs = oracle_mod.generate(G, n, p, 31 + G + w)
     seed = oracle_mod.get_seed(w)
     _, _, st = oracle_mod.find_matches(seqs, seed, table_size=table_size)

@@ -1,5 +1,6 @@
 """The big-bucket replay (replay_big_kernel: chain-rank counts + exact lower_bound for the
-suspicious probes) forced onto small buckets (MUMS_DEV_BIG_BUCKET), bit-exact against the
+suspicious probes; the closed-form rounds of bigq_* for buckets with many suspicious probes)
+forced onto small buckets (MUMS_DEV_BIG_BUCKET, MUMS_DEV_GRID_SLOW), bit-exact against the
 reference known answers (incl. the 4 x 10 Mbp related case whose main-diagonal bucket holds
 the duplicated entry of SURVEY.md §0.4) and the oracle on varied shapes."""
 import hashlib
@@ -15,9 +16,11 @@ pytestmark = pytest.mark.gpu
 CASES = [c for c in json.load(open(os.path.join(GOLDEN, "appendix_c.json")))["cases"] if c["mode"] != "ParallelMemHash"]
 
 
-@pytest.fixture
-def force_big(monkeypatch):
+@pytest.fixture(params=["rank_counts", "closed_form"])
+def force_big(monkeypatch, request):
     monkeypatch.setenv("MUMS_DEV_BIG_BUCKET", "8")
+    if request.param == "closed_form":   # every untied big bucket through bigq_* (replay.hip)
+        monkeypatch.setenv("MUMS_DEV_GRID_SLOW", "0")
 
 
 @pytest.mark.parametrize("case", CASES, ids=lambda c: f"G{c['G']}_n{c['n']}_p{c['p']}_{c['mode']}")
