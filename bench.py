@@ -313,13 +313,16 @@ def main():
                        "workload": f"BASELINE config 3: {G} x {n // 10**6} Mbp related p=0.01, w19, full FindMatches",
                        "phase_ms": {k: round(sm[k], 3) for k in ("ms_keys", "ms_sort", "ms_groups", "ms_buckets",
                                                                   "ms_chains", "ms_replay", "ms_output")},
-                       "roofline": {"bound": "hbm", "kernel": "chain_walk_kernel (2 launches per FindMatches)",
+                       "roofline": {"bound": "hbm", "kernel": "chain_walk_kernel (2 launches per FindMatches, the "
+                                                              "long walks)",
                                     "achieved": walk_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                     "frac": walk_gbs / HBM_PEAK_GBS if walk_gbs else None,
                                     "bytes": sp["chain_walk_bytes"], "ms": walk_ms, "walks": sp["chain_walks"],
                                     "hit_words": sp["chain_walk_words"],
-                                    "model": "28-B packed window per 64-column hit word and present component + "
-                                             "per walk the probe row ((G+1) x 8 B) and its 24-B queue item"}}
+                                    "model": "REQUESTED bytes, not HBM traffic: 28-B packed window per 64-column hit "
+                                             "word and present component + per walk the probe row ((G+1) x 8 B) and its "
+                                             "24-B queue item; much of the 200 MB packed genome is served from L2 / MALL "
+                                             "(PMC FETCH_SIZE of the kernel: profiles/r02_pmc_chains.txt)"}}
         except Exception as e:  # report, never hide
             mums_c3 = {"error": str(e)}
     elif sharded and args.workload == "c3" and not args.no_mums and hasattr(stage, "run_find"):

@@ -866,7 +866,7 @@ __global__ void bigg_finish_kernel(const uint32_t* __restrict__ E, uint32_t R, c
 // The counts come from the chain-first insert times (prefix tables over the firsts in time
 // order) plus the duplicate inserts found so far; rounds find the earliest probe that is
 // not a collision, apply it, and go on from there.
-constexpr uint32_t kQW = 10;   // words per query record
+constexpr uint32_t kQW = 11;   // words per query record
 
 // ff[k] = chain-first flag of bucket probe k (ff[K] = 0); ft[rank] = its time; logs the inserts
 __global__ __launch_bounds__(kBlock) void bigq_first_kernel(const uint4* __restrict__ summ,
@@ -932,7 +932,7 @@ __device__ __forceinline__ uint32_t rank_lb(const uint4* __restrict__ sbr, uint3
 }
 
 // one query per suspicious probe, in time order (spos = exclusive scan of the flags):
-// Q[q] = {time, a, x, xe, pA, dA, nC, eq, t, status}
+// Q[q] = {time, a, x, xe, pA, dA, nC, eq, t, status, duplicates applied}
 __global__ __launch_bounds__(kBlock) void bigq_query_kernel(const uint4* __restrict__ summ,
                                                             const uint4* __restrict__ summ_b, uint32_t beg, uint32_t K,
                                                             uint32_t r0, uint32_t R, const uint4* __restrict__ sbr,
@@ -971,6 +971,7 @@ __global__ __launch_bounds__(kBlock) void bigq_query_kernel(const uint4* __restr
     q[7] = c_xe1 - c_x1;              // eq
     q[8] = kq;                        // t
     q[9] = 0;
+    q[10] = 0;
 }
 
 // libstdc++ __lower_bound over the pattern T^pA F^dA T^nC F^...
@@ -989,23 +990,28 @@ __device__ __forceinline__ uint32_t lb_pattern(uint32_t t, uint32_t pA, uint32_t
     return first;
 }
 
-// one round over the queries [q0, S): apply the last insert (rank da at time dt) to the
-// later queries, classify (0 collision, 1 insert, 2 exact) and find the earliest non-collision
-__global__ __launch_bounds__(kBlock) void bigq_round_kernel(uint32_t* __restrict__ Q, uint32_t S, uint32_t q0,
-                                                            uint32_t has, uint32_t da, uint32_t dt,
+// one round over the window [q0, q1) of the queries: bring each up to date with the
+// duplicate inserts so far (all of them precede the window: dups[], their ranks in order),
+// classify (0 collision, 1 insert, 2 exact) and find the earliest non-collision
+__global__ __launch_bounds__(kBlock) void bigq_round_kernel(uint32_t* __restrict__ Q, uint32_t q0, uint32_t q1,
+                                                            const uint32_t* __restrict__ dups, uint32_t nd,
                                                             uint32_t* __restrict__ best) {
     const uint32_t i = q0 + blockIdx.x * kBlock + threadIdx.x;
-    if (i >= S) return;
+    if (i >= q1) return;
     uint32_t* q = Q + (uint64_t)i * kQW;
     const uint32_t a = q[1], x = q[2], xe = q[3];
     uint32_t pA = q[4], dA = q[5], nC = q[6], eq = q[7], t = q[8];
-    if (has && q[0] > dt) {
-        pA += da < a;
-        dA += da == a;
-        nC += (da > a && da <= x);
-        eq += (da > x && da <= xe);
-        t += 1;
-        q[4] = pA; q[5] = dA; q[6] = nC; q[7] = eq; q[8] = t;
+    const uint32_t done = q[10];
+    if (done < nd) {
+        for (uint32_t d = done; d < nd; ++d) {
+            const uint32_t da = dups[d];
+            pA += da < a;
+            dA += da == a;
+            nC += (da > a && da <= x);
+            eq += (da > x && da <= xe);
+        }
+        t += nd - done;
+        q[4] = pA; q[5] = dA; q[6] = nC; q[7] = eq; q[8] = t; q[10] = nd;
     }
     uint32_t st = 2;
     if (eq == 0) {
@@ -1026,11 +1032,12 @@ __global__ __launch_bounds__(kBlock) void bigq_cnt_kernel(const uint32_t* __rest
 
 // a duplicate insert of rank da (probe at bucket time k): counted, logged unless the exact
 // path logged it
-__global__ void bigq_dup_kernel(uint32_t* __restrict__ dup, uint32_t da, const uint4* __restrict__ summ,
-                                const uint4* __restrict__ summ_b, uint32_t beg, uint32_t k, int log,
-                                uint64_t* __restrict__ mlog, DevCounters* ctr) {
+__global__ void bigq_dup_kernel(uint32_t* __restrict__ dup, uint32_t* __restrict__ dups, uint32_t nd, uint32_t da,
+                                const uint4* __restrict__ summ, const uint4* __restrict__ summ_b, uint32_t beg,
+                                uint32_t k, int log, uint64_t* __restrict__ mlog, DevCounters* ctr) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     dup[da] += 1u;
+    dups[nd] = da;
     if (log) log_insert(mlog, ctr, summ_b[beg + k].w, summ[beg + k].z);
 }
 
@@ -1106,7 +1113,7 @@ hipError_t bigq_bucket(View v, const GenomeTable& gt, const MatchParams& mp, int
     const uint32_t bs = std::max<uint32_t>(256u, (F + 255u) / 256u);
     const uint32_t NB = F / bs + 1;
     const size_t words = 3ull * (K + 1) + 5ull * (R + 1) + (size_t)F + 1 + (size_t)NB * (R + 1) +
-                         (size_t)S * kQW + 64;
+                         (size_t)S * (kQW + 1) + 64 + 64 * 8;
     size_t stmp_need = scan_tmp_bytes((uint64_t)std::max(K, R) + 1);
     char* base = nullptr;
     hipError_t e = hipMalloc(&base, words * 4 + 16 * (size_t)(R + 1) + stmp_need + 4096);
@@ -1122,6 +1129,7 @@ hipError_t bigq_bucket(View v, const GenomeTable& gt, const MatchParams& mp, int
     uint32_t* ft = (uint32_t*)carve((R + 1) * 4ull);     // time of each rank's first insert
     uint32_t* fi = (uint32_t*)carve((R + 1) * 4ull);     // index of each rank's first among the firsts
     uint32_t* dup = (uint32_t*)carve((R + 1) * 4ull);    // duplicate inserts per rank
+    uint32_t* dups = (uint32_t*)carve((S + 1) * 4ull);   // their ranks, in insert order
     uint32_t* cnt = (uint32_t*)carve((R + 1) * 4ull);
     uint32_t* E = (uint32_t*)carve((R + 1) * 4ull);
     uint32_t* fr = (uint32_t*)carve((F + 1) * 4ull);
@@ -1151,20 +1159,30 @@ hipError_t bigq_bucket(View v, const GenomeTable& gt, const MatchParams& mp, int
                        (const uint4*)sbr, (const uint32_t*)ff, (const uint32_t*)sf, (const uint32_t*)fr,
                        (const uint32_t*)PT, bs, Q);
     if ((e = hipGetLastError()) != hipSuccess) return done(e);
-    uint32_t q0 = 0, has = 0, da = 0, dt = 0, ndup = 0;
+    // rounds over a window of the queries: it doubles while no event turns up in it
+    uint32_t q0 = 0, ndup = 0;
+    constexpr uint32_t kWin0 = 32768;
+    uint32_t win = kWin0;
     std::vector<uint32_t> hq(kQW);
     const bool stats = getenv("MUMS_DEV_REPLAY_STATS") != nullptr;
     uint32_t nexact = 0, rounds = 0;
     while (q0 < S) {
         const uint32_t inf = 0xFFFFFFFFu;
+        const uint32_t q1 = (uint32_t)std::min<uint64_t>(S, (uint64_t)q0 + win);
         if ((e = hipMemcpyAsync(best, &inf, 4, hipMemcpyHostToDevice, st)) != hipSuccess) return done(e);
-        hipLaunchKernelGGL(bigq_round_kernel, grid(S - q0), dim3(kBlock), 0, st, Q, S, q0, has, da, dt, best);
+        hipLaunchKernelGGL(bigq_round_kernel, grid(q1 - q0), dim3(kBlock), 0, st, Q, q0, q1, (const uint32_t*)dups,
+                           ndup, best);
         if ((e = hipGetLastError()) != hipSuccess) return done(e);
         uint32_t m = inf;
         if ((e = hipMemcpyAsync(&m, best, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return done(e);
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return done(e);
         ++rounds;
-        if (m == inf) break;
+        if (m == inf) {   // every query of the window collides
+            q0 = q1;
+            win = std::min<uint32_t>(win * 2, 1u << 30);
+            continue;
+        }
+        win = kWin0;
         if ((e = hipMemcpy(hq.data(), Q + (size_t)m * kQW, kQW * 4, hipMemcpyDeviceToHost)) != hipSuccess) return done(e);
         const uint32_t k = hq[0], a = hq[1];
         bool inserted = hq[9] == 1;
@@ -1184,13 +1202,9 @@ hipError_t bigq_bucket(View v, const GenomeTable& gt, const MatchParams& mp, int
             if ((e = hipStreamSynchronize(st)) != hipSuccess) return done(e);
             inserted = ins != 0;
         }
-        has = 0;
         if (inserted) {
-            hipLaunchKernelGGL(bigq_dup_kernel, dim3(1), dim3(64), 0, st, dup, a, summ, summ_b, beg, k,
+            hipLaunchKernelGGL(bigq_dup_kernel, dim3(1), dim3(64), 0, st, dup, dups, ndup, a, summ, summ_b, beg, k,
                                hq[9] == 1 ? 1 : 0, mlog, (DevCounters*)ctr);
-            has = 1;
-            da = a;
-            dt = k;
             ++ndup;
         }
         q0 = m + 1;
