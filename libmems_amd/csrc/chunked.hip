@@ -9,6 +9,8 @@
 // chunk and the probes come out in the reference's AddHashEntry order.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "mums_internal.h"
 
 namespace mums {
@@ -37,6 +39,295 @@ hipError_t launch_digit_totals(const uint32_t* hist, uint32_t ndigits, uint32_t 
     if (ndigits == 0) return hipSuccess;
     hipLaunchKernelGGL(digit_totals_kernel, dim3(ndigits), dim3(256), 0, st, hist, T, out);
     return hipGetLastError();
+}
+
+}  // namespace mums
+
+// ---- MER_REPEAT_LIMIT restarts and start points in the chunked mode ------------------
+// MatchFinder::SearchRange's restart (MatchFinder.cpp:253-277) needs every genome's
+// SortedMerList: its plan (restart_plan.h) reads SML keys by index, and a record lives iff
+// its SML index reaches the start point of its key's phase.  With all chunks resident and
+// sorted, the merged stream is one sorted array of N records; a stable partition by genome
+// gives the G SMLs as full keys (ck, genome-major, 64-bit slots = global seed-mer indices),
+// and a record's SML index is its rank among its genome's records in stream order, counted
+// per block of kCrBlk records (per-genome block counts, scanned).
+namespace mums {
+namespace {
+
+constexpr uint32_t kCrBlk = 4096;   // records per rank block (kBlock threads x 16 rounds)
+
+__device__ __forceinline__ uint64_t cr_key(const CrStream& s, uint64_t j) {
+    uint32_t lo = 0, n = s.nd;   // digit of j: digits whose end <= j
+    while (n > 0) {
+        const uint32_t h = n >> 1;
+        if (s.dstart[lo + h + 1] <= j) { lo += h + 1; n -= h + 1; } else n = h;
+    }
+    return ((uint64_t)lo << 31) | (s.rec[j] >> 33);
+}
+
+__device__ __forceinline__ uint64_t cr_idx(const CrStream& s, uint64_t j) { return s.rec[j] & ((1ull << 33) - 1); }
+
+// per-block genome counts: gcnt[g * (nblk + 1) + b]
+__global__ __launch_bounds__(kBlock) void cr_count_kernel(CrStream s, GenomeTable gt, uint64_t nblk,
+                                                          uint32_t* __restrict__ gcnt) {
+    __shared__ uint32_t c[kMaxG];
+    const uint64_t b = blockIdx.x;
+    if (threadIdx.x < kMaxG) c[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t r = threadIdx.x; r < kCrBlk; r += kBlock) {
+        const uint64_t j = b * kCrBlk + r;
+        if (j < s.N) atomicAdd(&c[genome_of(gt, cr_idx(s, j))], 1u);
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < gt.G) gcnt[(uint64_t)threadIdx.x * (nblk + 1) + b] = c[threadIdx.x];
+}
+
+// f(j, g, sml index) for every record of block b, in stream order per genome (stable)
+template <typename F>
+__device__ __forceinline__ void cr_block_ranks(const CrStream& s, const GenomeTable& gt, uint64_t b,
+                                               const uint32_t* __restrict__ gscan, uint64_t nblk, F&& f) {
+    __shared__ uint32_t base[kMaxG];
+    __shared__ uint32_t wcnt[kBlock / 64][kMaxG];
+    const int tid = threadIdx.x, wv = tid >> 6;
+    if (tid < gt.G) base[tid] = gscan[(uint64_t)tid * (nblk + 1) + b];
+    for (uint32_t r0 = 0; r0 < kCrBlk; r0 += kBlock) {
+        for (int i = tid; i < (kBlock / 64) * kMaxG; i += kBlock) (&wcnt[0][0])[i] = 0;
+        __syncthreads();
+        const uint64_t j = b * kCrBlk + r0 + tid;
+        const bool valid = j < s.N;
+        const uint32_t g = valid ? (uint32_t)genome_of(gt, cr_idx(s, j)) : 0u;
+        uint32_t tot;
+        const uint32_t rk = wave_match_rank<6>(g, valid, &tot);
+        if (valid && rk == 0) wcnt[wv][g] = tot;
+        __syncthreads();
+        if (valid) {
+            uint32_t o = base[g] + rk;
+            for (int w = 0; w < wv; ++w) o += wcnt[w][g];
+            f(j, (int)g, (uint64_t)o);
+        }
+        __syncthreads();
+        if (tid < gt.G) {
+            uint32_t t = 0;
+            for (int w = 0; w < kBlock / 64; ++w) t += wcnt[w][tid];
+            base[tid] += t;
+        }
+    }
+}
+
+// the G SortedMerLists as full keys: ck[base_g + sml index] = ckey
+__global__ __launch_bounds__(kBlock) void cr_ck_kernel(CrStream s, GenomeTable gt, const uint32_t* __restrict__ gscan,
+                                                       uint64_t nblk, uint64_t* __restrict__ ck) {
+    cr_block_ranks(s, gt, blockIdx.x, gscan, nblk,
+                   [&](uint64_t j, int g, uint64_t i) { ck[gt.base[g] + i] = cr_key(s, j); });
+}
+
+// masked keys with more than MER_REPEAT_LIMIT records: such a run holds a multiple of 1000,
+// so only those positions look for their run's bounds (galloping) -- the first multiple
+// of 1000 inside the run reports its key
+__device__ __forceinline__ uint64_t cr_run_edge(const CrStream& s, uint64_t m, uint64_t v, int dir) {
+    // last position from m in direction dir whose masked key is v
+    uint64_t good = m, step = 1;
+    for (;;) {
+        const bool in = dir < 0 ? good >= step : good + step < s.N;
+        if (!in) break;
+        const uint64_t q = dir < 0 ? good - step : good + step;
+        if ((cr_key(s, q) >> 1) != v) break;
+        good = q;
+        step <<= 1;
+    }
+    uint64_t lo = dir < 0 ? (good >= step ? good - step + 1 : 0) : good, hi = dir < 0 ? good : std::min(good + step, s.N);
+    if (dir < 0) {   // first position in [lo, good] with key v
+        while (lo < hi) {
+            const uint64_t mid = lo + (hi - lo) / 2;
+            if ((cr_key(s, mid) >> 1) == v) hi = mid; else lo = mid + 1;
+        }
+        return lo;
+    }
+    while (hi - lo > 1) {   // last position in [good, hi) with key v
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if ((cr_key(s, mid) >> 1) == v) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(kBlock) void cr_cand_kernel(CrStream s, uint64_t* __restrict__ list,
+                                                         unsigned long long* __restrict__ cnt, uint64_t cap) {
+    const uint64_t m = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * restart::kRepeatLimit;
+    if (m >= s.N) return;
+    const uint64_t v = cr_key(s, m) >> 1;
+    const uint64_t a = cr_run_edge(s, m, v, -1);
+    if (m >= a + restart::kRepeatLimit) return;   // an earlier multiple of 1000 lies in the run
+    const uint64_t b = cr_run_edge(s, m, v, +1);
+    if (b - a + 1 <= restart::kRepeatLimit) return;
+    const unsigned long long k = atomicAdd(cnt, 1ull);
+    if (k < cap) list[k] = v;
+}
+
+// live[j - lo] for the records [lo, hi) of one chunk: SML index >= its phase's start point
+__global__ __launch_bounds__(kBlock) void cr_live_kernel(CrStream s, GenomeTable gt, const uint32_t* __restrict__ gscan,
+                                                         uint64_t nblk, uint64_t b0, uint64_t lo, uint64_t hi,
+                                                         const uint64_t* __restrict__ rkey, uint64_t R,
+                                                         const uint64_t* __restrict__ rS,
+                                                         const uint64_t* __restrict__ S0, uint32_t* __restrict__ live) {
+    const int G = gt.G;
+    cr_block_ranks(s, gt, b0 + blockIdx.x, gscan, nblk, [&](uint64_t j, int g, uint64_t i) {
+        if (j < lo || j >= hi) return;
+        const uint64_t v = cr_key(s, j) >> 1;
+        uint64_t a = 0, n = R;   // phase = restart keys <= v
+        while (n > 0) {
+            const uint64_t h = n >> 1;
+            if (rkey[a + h] <= v) { a += h + 1; n -= h + 1; } else n = h;
+        }
+        const uint64_t sp = a == 0 ? S0[g] : rS[(a - 1) * (uint64_t)G + g];
+        live[j - lo] = i >= sp ? 1u : 0u;
+    });
+}
+
+// straddled runs: start point s of genome g inside a run of equal keys -> {g, lo, hi}
+__global__ __launch_bounds__(kBlock) void cr_runs_kernel(const uint64_t* __restrict__ ck, GenomeTable gt,
+                                                         const uint64_t* __restrict__ sp, uint64_t rows,
+                                                         uint64_t* __restrict__ runs, unsigned long long* __restrict__ nr,
+                                                         uint64_t cap) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int G = gt.G;
+    if (i >= rows * (uint64_t)G) return;
+    const int g = (int)(i % (uint64_t)G);
+    const uint64_t s = sp[i], m = gt.m[g];
+    if (s == 0 || s >= m) return;
+    const uint64_t* a = ck + gt.base[g];
+    const uint64_t k = a[s];
+    if (a[s - 1] != k) return;
+    uint64_t lo = s - 1, hi = s + 1;
+    while (lo > 0 && a[lo - 1] == k) --lo;
+    while (hi < m && a[hi] == k) ++hi;
+    const unsigned long long q = atomicAdd(nr, 1ull);
+    if (q < cap) {
+        runs[3 * q] = (uint64_t)g;
+        runs[3 * q + 1] = lo;
+        runs[3 * q + 2] = hi;
+    }
+}
+
+// K[pos] = key of genome g's seed-mer pos (the tie replay's position order)
+__global__ __launch_bounds__(kBlock) void cr_kpos_kernel(CrStream s, GenomeTable gt, int g, uint64_t* __restrict__ K) {
+    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= s.N) return;
+    const uint64_t gi = cr_idx(s, j);
+    if (genome_of(gt, gi) != g) return;
+    K[gi - gt.base[g]] = cr_key(s, j);
+}
+
+// the records of a straddled run of genome g (slots [lo, hi), key ck) take the ids of the
+// std::sort order (V: positions at the slots); one lane per run
+__global__ void cr_tie_write_kernel(CrStream s, GenomeTable gt, int g, const uint64_t* __restrict__ runs, uint64_t nrun,
+                                    const uint64_t* __restrict__ ck, const uint32_t* __restrict__ V,
+                                    uint64_t* __restrict__ rec) {
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nrun || (int)runs[3 * q] != g) return;
+    const uint64_t lo = runs[3 * q + 1], hi = runs[3 * q + 2];
+    const uint64_t key = ck[gt.base[g] + lo];
+    uint64_t a = 0, n = s.N;   // first stream record with key >= key
+    while (n > 0) {
+        const uint64_t h = n >> 1;
+        if (cr_key(s, a + h) < key) { a += h + 1; n -= h + 1; } else n = h;
+    }
+    uint64_t r = 0;
+    for (uint64_t j = a; j < s.N && r < hi - lo && cr_key(s, j) == key; ++j) {
+        if (genome_of(gt, cr_idx(s, j)) != g) continue;
+        const uint64_t gi = gt.base[g] + V[lo + r];
+        rec[j] = (rec[j] & ~((1ull << 33) - 1)) | gi;
+        ++r;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void cr_compact_kernel(const T* __restrict__ src, const uint32_t* __restrict__ live,
+                                                            const uint32_t* __restrict__ pos, uint64_t n,
+                                                            T* __restrict__ dst) {
+    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j < n && live[j]) dst[pos[j]] = src[j];
+}
+
+inline dim3 cr_grid(uint64_t n) { return dim3((unsigned)((n + kBlock - 1) / kBlock)); }
+
+}  // namespace
+
+uint64_t cr_blocks(uint64_t N) { return (N + kCrBlk - 1) / kCrBlk; }
+
+hipError_t launch_cr_counts(const CrStream& s, const GenomeTable& gt, uint32_t* gcnt, void* d_scan_tmp,
+                            hipStream_t st) {
+    const uint64_t nblk = cr_blocks(s.N);
+    hipError_t e = hipMemsetAsync(gcnt, 0, (size_t)gt.G * (nblk + 1) * 4, st);
+    if (e != hipSuccess || nblk == 0) return e;
+    hipLaunchKernelGGL(cr_count_kernel, dim3((unsigned)nblk), dim3(kBlock), 0, st, s, gt, nblk, gcnt);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    for (int g = 0; g < gt.G; ++g)
+        if ((e = exclusive_scan_u32(gcnt + (uint64_t)g * (nblk + 1), nblk + 1, d_scan_tmp, nullptr, st)) != hipSuccess)
+            return e;
+    return hipSuccess;
+}
+
+hipError_t launch_cr_ck(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, uint64_t* ck, hipStream_t st) {
+    const uint64_t nblk = cr_blocks(s.N);
+    if (nblk == 0) return hipSuccess;
+    hipLaunchKernelGGL(cr_ck_kernel, dim3((unsigned)nblk), dim3(kBlock), 0, st, s, gt, gscan, nblk, ck);
+    return hipGetLastError();
+}
+
+hipError_t launch_cr_cands(const CrStream& s, uint64_t* list, unsigned long long* cnt, uint64_t cap, hipStream_t st) {
+    hipError_t e = hipMemsetAsync(cnt, 0, 8, st);
+    if (e != hipSuccess || s.N == 0) return e;
+    hipLaunchKernelGGL(cr_cand_kernel, cr_grid((s.N + restart::kRepeatLimit - 1) / restart::kRepeatLimit), dim3(kBlock),
+                       0, st, s, list, cnt, cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_cr_runs(const uint64_t* ck, const GenomeTable& gt, const uint64_t* sp, uint64_t rows, uint64_t* runs,
+                          unsigned long long* nr, uint64_t cap, hipStream_t st) {
+    if (rows == 0) return hipSuccess;
+    hipLaunchKernelGGL(cr_runs_kernel, cr_grid(rows * (uint64_t)gt.G), dim3(kBlock), 0, st, ck, gt, sp, rows, runs, nr,
+                       cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_cr_kpos(const CrStream& s, const GenomeTable& gt, int g, uint64_t* K, hipStream_t st) {
+    if (s.N == 0) return hipSuccess;
+    hipLaunchKernelGGL(cr_kpos_kernel, cr_grid(s.N), dim3(kBlock), 0, st, s, gt, g, K);
+    return hipGetLastError();
+}
+
+hipError_t launch_cr_tie_write(const CrStream& s, const GenomeTable& gt, int g, const uint64_t* runs, uint64_t nrun,
+                               const uint64_t* ck, const uint32_t* V, uint64_t* rec, hipStream_t st) {
+    if (nrun == 0) return hipSuccess;
+    hipLaunchKernelGGL(cr_tie_write_kernel, dim3((unsigned)((nrun + 63) / 64)), dim3(64), 0, st, s, gt, g, runs, nrun,
+                       ck, V, rec);
+    return hipGetLastError();
+}
+
+// live records of chunk [lo, hi) compacted (order kept) into dst; *d_total = how many;
+// bucket starts (chunk-relative, nb + 1) mapped through the scan into dst_bstart
+hipError_t launch_cr_live_compact(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, uint64_t lo,
+                                  uint64_t hi, const uint64_t* rkey, uint64_t R, const uint64_t* rS, const uint64_t* S0,
+                                  uint32_t* live, uint32_t* pos, void* d_scan_tmp, uint64_t* dst,
+                                  const uint32_t* bstart, uint32_t nb, uint32_t* dst_bstart, uint32_t* d_total,
+                                  hipStream_t st) {
+    const uint64_t n = hi - lo;
+    const uint64_t nblk = cr_blocks(s.N);
+    const uint64_t b0 = lo / kCrBlk, b1 = (hi + kCrBlk - 1) / kCrBlk;
+    hipError_t e = hipMemsetAsync(live + n, 0, 4, st);
+    if (e != hipSuccess) return e;
+    if (n) {
+        hipLaunchKernelGGL(cr_live_kernel, dim3((unsigned)(b1 - b0)), dim3(kBlock), 0, st, s, gt, gscan, nblk, b0, lo,
+                           hi, rkey, R, rS, S0, live);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    if ((e = hipMemcpyAsync(pos, live, (n + 1) * 4, hipMemcpyDeviceToDevice, st)) != hipSuccess) return e;
+    if ((e = exclusive_scan_u32(pos, n + 1, d_scan_tmp, d_total, st)) != hipSuccess) return e;
+    if (n) {
+        hipLaunchKernelGGL(cr_compact_kernel<uint64_t>, cr_grid(n), dim3(kBlock), 0, st, s.rec + lo, live, pos, n, dst);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    return launch_map_starts(bstart, nb, pos, dst_bstart, st);
 }
 
 }  // namespace mums

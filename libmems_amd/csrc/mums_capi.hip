@@ -114,6 +114,8 @@ struct mums_ctx {
     std::vector<uint64_t> start_points;   // per genome SML start index (empty = all 0)
     DevBuf rsbuf, rsplan, rsbst;
     DevBuf tiebuf;                        // SML tie order (smlsort.hip)
+    DevBuf crbuf, crcnt, crlive, crruns;  // chunked-mode restarts (chunked.hip)
+    uint64_t cr_cands = 0;                // groups above MER_REPEAT_LIMIT (chunked restart)
     bool ties_fixed = false;              // the stream holds every run of equal keys in std::sort order
     uint64_t tie_slots = 0;               // slots of the runs replayed by the last run (stats)
     uint64_t restarts = 0;
@@ -1392,7 +1394,8 @@ int mums_ctx_destroy(mums_ctx* ctx) {
                       &ctx->cval, &ctx->ctab, &ctx->smlk0, &ctx->smlkA, &ctx->smlkB, &ctx->smlvA,
                       &ctx->smlvB, &ctx->smltmp, &ctx->flen, &ctx->fs, &ctx->rowsall, &ctx->rsbuf,
                       &ctx->rsplan, &ctx->rsbst, &ctx->pool_loc, &ctx->cbuf, &ctx->sids,
-                      &ctx->logA, &ctx->logB, &ctx->logvA, &ctx->logvB};
+                      &ctx->logA, &ctx->logB, &ctx->logvA, &ctx->logvB, &ctx->tiebuf, &ctx->fk, &ctx->fkloc,
+                      &ctx->crbuf, &ctx->crcnt, &ctx->crlive, &ctx->crruns};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i < EV_COUNT; ++i)
         if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
@@ -1496,8 +1499,8 @@ int mums_find_stage(mums_ctx* ctx, int stage) {
         return fail(ctx, MUMS_E_UNSUPPORTED, "more than 32 genomes: only MemHash / MaskedMemHash, enum_tol <= 1");
     if (!ctx->start_points.empty() && ctx->start_points.size() != ctx->genomes.size())   // MatchFinder.cpp:197-199
         return fail(ctx, MUMS_E_INVALID, "start points: one per sequence required");
-    if (have_start_points(ctx) && (big || ctx->pcompat))
-        return fail(ctx, MUMS_E_UNSUPPORTED, "start points (FindMatchesFromPosition) in the chunked / compat modes");
+    if (have_start_points(ctx) && ctx->pcompat)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "start points (FindMatchesFromPosition) in the ParallelMemHash compat mode");
     if (ctx->pairwise || ctx->enum_tol > 1) return run_pipeline_pairwise(ctx, stage);
     if (ctx->pcompat) return run_pipeline_compat(ctx, stage);
     return big ? run_pipeline_chunked(ctx, stage) : run_pipeline(ctx, stage);
@@ -2338,6 +2341,170 @@ int run_pipeline_pairwise(mums_ctx* ctx, int stage) {
 // global indices; the 2w+1-31 MSD digits are cut into power-of-two chunks of < 2^30
 // records and every chunk runs scatter -> onesweep -> groups -> probe buckets [-> rows]
 // on its own, in key order; the FindMatches tail then replays all chunks' rows.
+// MER_REPEAT_LIMIT restarts / start points of the chunked mode (MatchFinder.cpp:253-277,
+// MemHash.cpp:117-127): all chunks resident and sorted in buffer sbuf.  Candidates (groups
+// above 1000 records) from the whole stream; if any (or start points): the G SortedMerLists
+// as full keys in the other record buffer, the restart plan (restart_plan.h), the std::sort
+// order of the runs a start point falls into (smlsort.hip, one genome at a time), then each
+// chunk's live records compacted into the other buffer: *live_rec, n_live[c], the chunks'
+// bucket starts in ctx->rsbst.  *live_rec stays null when every record lives.
+int chunked_restart(mums_ctx* ctx, int sbuf, const std::vector<uint64_t>& dstart, const std::vector<uint64_t>& cbase,
+                    uint32_t* hist, uint32_t T, uint32_t nbc, int mb, uint32_t nch, std::vector<uint64_t>& n_live,
+                    uint64_t** live_rec, hipStream_t st) {
+    const GenomeTable& gt = ctx->gt;
+    const int G = gt.G;
+    const uint64_t Gu = (uint64_t)G;
+    const uint64_t N = ctx->N;
+    const uint32_t nd = (uint32_t)dstart.size() - 1;
+    uint64_t* srec = sbuf ? ctx->recB.as<uint64_t>() : ctx->recA.as<uint64_t>();
+    uint64_t* other = sbuf ? ctx->recA.as<uint64_t>() : ctx->recB.as<uint64_t>();
+    *live_rec = nullptr;
+    ctx->restarts = 0;
+    ctx->offset_log.clear();
+    const uint64_t ccap = N / (restart::kRepeatLimit + 1) + 16;   // candidates: runs of > 1000 records
+    HIPCHK(ctx->crbuf.ensure((nd + 1) * 8 + 64 + ccap * 8 + 4096));
+    uint64_t* d_dstart = ctx->crbuf.as<uint64_t>();
+    unsigned long long* d_cnt = (unsigned long long*)(d_dstart + nd + 1);
+    uint64_t* d_list = (uint64_t*)(d_cnt + 8);
+    HIPCHK(hipMemcpyAsync(d_dstart, dstart.data(), (nd + 1) * 8, hipMemcpyHostToDevice, st));
+    const CrStream s{srec, d_dstart, nd, N};
+    HIPCHK(launch_cr_cands(s, d_list, d_cnt, ccap, st));
+    unsigned long long C = 0;
+    HIPCHK(hipMemcpyAsync(&C, d_cnt, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    ctx->cr_cands = C;
+    if (C == 0 && !have_start_points(ctx)) return MUMS_OK;
+    if (C > ccap) return fail(ctx, MUMS_E_HIP, "chunked restart: candidate list overflow (internal error)");
+    if (seg_onesweep_launches(31) < 4)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "chunked restart with the segment fix-up sort (MUMS_DEV_SEGFIX)");
+    std::vector<uint64_t> cand(C);
+    if (C) {
+        HIPCHK(hipMemcpy(cand.data(), d_list, C * 8, hipMemcpyDeviceToHost));
+        std::sort(cand.begin(), cand.end());
+        HIPCHK(hipMemcpyAsync(d_list, cand.data(), C * 8, hipMemcpyHostToDevice, st));
+    }
+    // per-genome block counts and the SMLs (full keys) in the other buffer
+    const uint64_t nblk = cr_blocks(N);
+    HIPCHK(ctx->crcnt.ensure(Gu * (nblk + 1) * 4 + 256));
+    HIPCHK(ctx->tmp.ensure(std::max(ctx->tmp.cap, scan_tmp_bytes(nblk + 2))));
+    uint32_t* gscan = ctx->crcnt.as<uint32_t>();
+    HIPCHK(launch_cr_counts(s, gt, gscan, ctx->tmp.p, st));
+    uint64_t* ck = other;
+    HIPCHK(launch_cr_ck(s, gt, gscan, ck, st));
+    // the plan (restart.hip's kernels over the SMLs)
+    std::vector<uint64_t> S0(G, 0), hm(G + 1, 0), hb(G + 1, 0);
+    for (int g = 0; g < G && g < (int)ctx->start_points.size(); ++g) S0[g] = ctx->start_points[g];
+    for (int g = 0; g < G; ++g) {
+        hm[g] = gt.m[g];
+        hb[g] = gt.base[g];
+    }
+    const uint64_t cap = C + 16;
+    const size_t plan_words = cap + 1 + 3 * cap * Gu + (cap + 1) / 2 + 2 * Gu + 16 + cap + cap * Gu + 2 * (Gu + 1);
+    HIPCHK(ctx->rsplan.ensure(plan_words * 8 + sizeof(restart::PlanOut) + 4096));
+    uint64_t* p_list = ctx->rsplan.as<uint64_t>();
+    uint64_t* d_pre = p_list + cap + 1;
+    uint64_t* d_S = d_pre + 3 * cap * Gu + (cap + 1) / 2;
+    uint64_t* d_S0 = d_S + Gu;
+    restart::PlanOut* d_out = (restart::PlanOut*)(d_S0 + Gu);
+    uint64_t* d_rkey = d_S0 + Gu + 16;
+    uint64_t* d_rS = d_rkey + cap;
+    uint64_t* d_dm = d_rS + cap * Gu;
+    uint64_t* d_db = d_dm + Gu + 1;
+    if (C) HIPCHK(hipMemcpyAsync(p_list, d_list, C * 8, hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_dm, hm.data(), (Gu + 1) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_db, hb.data(), (Gu + 1) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_S, S0.data(), Gu * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_S0, S0.data(), Gu * 8, hipMemcpyHostToDevice, st));
+    restart::PlanOut po{};
+    po.cap = C;
+    po.rkey = d_rkey;
+    po.rS = d_rS;
+    po.status = restart::kPlanOk;
+    HIPCHK(hipMemcpyAsync(d_out, &po, sizeof(po), hipMemcpyHostToDevice, st));
+    RestartWs w{};
+    w.dm = d_dm;
+    w.dbase = d_db;
+    w.ck = ck;
+    HIPCHK(launch_restart_plan(w, G, p_list, C, d_pre, d_S, d_out, st));
+    HIPCHK(hipMemcpyAsync(&po, d_out, sizeof(po), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (po.status != restart::kPlanOk) return fail(ctx, MUMS_E_HIP, "restart plan table full (internal error)");
+    const uint64_t R = po.nrestarts;
+    ctx->restarts = R;
+    ctx->offset_log.assign(R * Gu, 0);
+    if (R) HIPCHK(hipMemcpy(ctx->offset_log.data(), d_rS, R * Gu * 8, hipMemcpyDeviceToHost));
+    if (R == 0 && !have_start_points(ctx)) return MUMS_OK;
+    // start points inside runs of equal keys: those runs in std::sort order (MemorySML.cpp:54)
+    const uint64_t rcap = (R + 1) * Gu + 16;
+    HIPCHK(ctx->crruns.ensure(rcap * 24 + (R + 1) * 8 + 256));
+    uint64_t* d_runs = ctx->crruns.as<uint64_t>();
+    uint64_t* d_sp = d_runs + 3 * rcap;   // genome g's start points, one per row
+    HIPCHK(hipMemsetAsync(d_cnt, 0, 8, st));
+    HIPCHK(launch_cr_runs(ck, gt, d_S0, 1, d_runs, d_cnt, rcap, st));
+    HIPCHK(launch_cr_runs(ck, gt, d_rS, R, d_runs, d_cnt, rcap, st));
+    unsigned long long nruns = 0;
+    HIPCHK(hipMemcpyAsync(&nruns, d_cnt, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (nruns > rcap) return fail(ctx, MUMS_E_HIP, "chunked restart: run list overflow (internal error)");
+    if (nruns) {
+        std::vector<uint64_t> hr(3 * nruns);
+        HIPCHK(hipMemcpy(hr.data(), d_runs, 3 * nruns * 8, hipMemcpyDeviceToHost));
+        for (int g = 0; g < G; ++g) {
+            bool any = false;
+            for (uint64_t q = 0; q < nruns; ++q) any = any || (int)hr[3 * q] == g;
+            if (!any) continue;
+            const uint64_t m = gt.m[g];
+            if (m >= 0xFFFFFFF0ull) return fail(ctx, MUMS_E_UNSUPPORTED, "SortedMerList of more than 2^32 seed-mers");
+            if (ctx->tiebuf.ensure(tie_ws_bytes(m, 1)) != hipSuccess)
+                return fail(ctx, MUMS_E_NOMEM, "chunked restart: no device memory for the SortedMerList tie order "
+                                               "of a genome");
+            const TieWs tw = tie_ws_layout(ctx->tiebuf.p, m, 1);
+            const uint64_t b0 = 0;
+            HIPCHK(tie_set_genomes(tw, &b0, &m, st));
+            HIPCHK(tie_clear_flags(tw, st));
+            std::vector<uint64_t> sp(R + 1);
+            sp[0] = S0[g];
+            for (uint64_t r = 0; r < R; ++r) sp[r + 1] = ctx->offset_log[r * Gu + g];
+            HIPCHK(hipMemcpyAsync(d_sp, sp.data(), (R + 1) * 8, hipMemcpyHostToDevice, st));
+            HIPCHK(hipStreamSynchronize(st));   // (sp is a host temporary)
+            HIPCHK(tie_mark_starts(tw, ck + gt.base[g], d_sp, R + 1, st));
+            uint64_t flagged = 0;
+            HIPCHK(tie_prepare(tw, &flagged, st));
+            if (!flagged) continue;
+            HIPCHK(launch_cr_kpos(s, gt, g, tw.K, st));
+            HIPCHK(tie_replay(tw, st));
+            HIPCHK(launch_cr_tie_write(s, gt, g, d_runs, nruns, ck, tw.V, srec, st));
+            ctx->tie_slots += flagged;
+        }
+        HIPCHK(hipStreamSynchronize(st));
+        ctx->tiebuf.release();
+    }
+    // every chunk's live records (SML index >= the start point of its key's phase),
+    // compacted into the other buffer at the chunk's base (the SMLs there are dead now)
+    uint64_t nmax = 0;
+    for (uint32_t c = 0; c < nch; ++c) nmax = std::max(nmax, cbase[c + 1] - cbase[c]);
+    HIPCHK(ctx->crlive.ensure(2 * (nmax + 64) * 4));
+    HIPCHK(ctx->rsbst.ensure((uint64_t)nch * (nbc + 1) * 4 + 64));
+    HIPCHK(ctx->tmp.ensure(std::max(ctx->tmp.cap, scan_tmp_bytes(nmax + 2))));
+    uint32_t* live = ctx->crlive.as<uint32_t>();
+    uint32_t* pos = live + nmax + 64;
+    uint32_t* d_total = (uint32_t*)d_cnt;
+    for (uint32_t c = 0; c < nch; ++c) {
+        const uint64_t lo = cbase[c], hi = cbase[c + 1];
+        uint32_t* bst = ctx->mstart.as<uint32_t>();
+        HIPCHK(seg_bucket_starts(mb > 0 ? hist + (uint64_t)c * nbc * T : nullptr, T, mb, hi - lo, bst, st));
+        HIPCHK(launch_cr_live_compact(s, gt, gscan, lo, hi, d_rkey, R, d_rS, d_S0, live, pos, ctx->tmp.p, other + lo,
+                                      bst, nbc, ctx->rsbst.as<uint32_t>() + (uint64_t)c * (nbc + 1), d_total, st));
+        uint32_t t = 0;
+        HIPCHK(hipMemcpyAsync(&t, d_total, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        n_live[c] = t;
+    }
+    for (DevBuf* b : {&ctx->crcnt, &ctx->crlive, &ctx->crruns}) b->release();
+    *live_rec = other;
+    return MUMS_OK;
+}
+
 int run_pipeline_chunked(mums_ctx* ctx, int stage) {
     hipStream_t st = ctx->stream;
     const int G = (int)ctx->genomes.size();
@@ -2445,6 +2612,49 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
         return (double)ms;
     };
     const int npass = seg_onesweep_launches(31);
+    // resident layout: every chunk is sorted first (pass 1), so that a MER_REPEAT_LIMIT
+    // restart or start points (chunked_restart) see the whole merged stream; then groups /
+    // probes / rows per chunk in key order (pass 2), on the live records after a restart.
+    // Streaming layout: sort + groups per chunk in one pass (restarts refused).
+    int sbuf = 0;
+    uint64_t* live_rec = nullptr;            // after a restart: compacted chunks (cbase offsets)
+    std::vector<uint64_t> n_live(nch, 0);
+    DevBuf& lbst = ctx->rsbst;               // per chunk: compacted bucket starts (nbc + 1)
+    for (uint32_t c = 0; c < nch && resident; ++c) {
+        const uint32_t dlo = c * nbc;
+        uint64_t n_c = 0;
+        for (uint32_t d = dlo; d < dlo + nbc; ++d) n_c += tot[d];
+        if (n_c == 0) continue;
+        uint32_t* slice = hist + (uint64_t)dlo * T;
+        uint64_t* rA = ctx->recA.as<uint64_t>() + cbase[c];
+        uint64_t* rB = ctx->recB.as<uint64_t>() + cbase[c];
+        HIPCHK(hipEventRecord(ctx->ev[EV_CHAINS], st));
+        uint32_t* bstart = ctx->mstart.as<uint32_t>();
+        HIPCHK(seg_bucket_starts(mb > 0 ? slice : nullptr, T, mb, n_c, bstart, st));
+        SegTile* tiles = ctx->tiles.as<SegTile>();
+        HIPCHK(build_seg_tiles_from_starts(bstart, mb, n_c, tiles, &dc->ntiles, ctx->tmp.p, st));
+        HIPCHK(seg_onesweep_sort(rA, rB, n_c, 31, mb, bstart, ctx->tmp.p, &dc->err, &sbuf, st,
+                                 prof ? ctx->ev_ds : nullptr, 33, mp.repeat_tol == 0 && mp.enum_tol == 1));
+        HIPCHK(hipEventRecord(ctx->ev[EV_SORT], st));
+        HIPCHK(hipEventSynchronize(ctx->ev[EV_SORT]));
+        ms_sort += el(EV_CHAINS, EV_SORT);
+        if (prof)
+            for (int p = 0; p < npass; ++p) {
+                float ms = 0.f;
+                (void)hipEventElapsedTime(&ms, ctx->ev_ds[2 * p], ctx->ev_ds[2 * p + 1]);
+                ms_dom += ms;
+            }
+        dom_bytes += n_c * 16 * (uint64_t)npass;
+        dom_launches += (uint64_t)npass;
+    }
+    if (!resident && have_start_points(ctx))
+        return fail(ctx, MUMS_E_UNSUPPORTED, "start points in the chunked mode without resident records");
+    if (resident) {
+        std::vector<uint64_t> dstart(nd + 1, 0);
+        for (uint32_t d = 0; d < nd; ++d) dstart[d + 1] = dstart[d] + tot[d];
+        rc = chunked_restart(ctx, sbuf, dstart, cbase, hist, T, nbc, mb, nch, n_live, &live_rec, st);
+        if (rc) return rc;
+    }
     for (uint32_t c = 0; c < nch; ++c) {
         const uint32_t dlo = c * nbc;
         uint64_t n_c = 0;
@@ -2455,41 +2665,55 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
         uint64_t* rA = ctx->recA.as<uint64_t>() + o;
         uint64_t* rB = ctx->recB.as<uint64_t>() + o;
         HIPCHK(hipEventRecord(ctx->ev[EV_CHAINS], st));   // chunk start (scatter counts as sort)
+        uint32_t* bstart = ctx->mstart.as<uint32_t>();
         if (!resident) {
             HIPCHK(exclusive_scan_u32(slice, (uint64_t)nbc * T, ctx->tmp.p, nullptr, st));
             HIPCHK(launch_seed_scatter_chunk(ctx->ss, gt, ctx->packed.as<uint32_t>(), B, slice, T, dlo, nbc, rA, st));
         }
-        uint32_t* bstart = ctx->mstart.as<uint32_t>();
-        HIPCHK(seg_bucket_starts(mb > 0 ? slice : nullptr, T, mb, n_c, bstart, st));
+        if (live_rec) {   // the chunk's live records after the restarts
+            n_c = n_live[c];
+            HIPCHK(hipMemcpyAsync(bstart, lbst.as<uint32_t>() + (uint64_t)c * (nbc + 1), (nbc + 1) * 4ull,
+                                  hipMemcpyDeviceToDevice, st));
+        } else {
+            HIPCHK(seg_bucket_starts(mb > 0 ? slice : nullptr, T, mb, n_c, bstart, st));
+        }
         SegTile* tiles = ctx->tiles.as<SegTile>();
         const uint64_t ub = seg_tiles_upper(n_c, mb);
         HIPCHK(build_seg_tiles_from_starts(bstart, mb, n_c, tiles, &dc->ntiles, ctx->tmp.p, st));
-        int buf = 0;
-        HIPCHK(seg_onesweep_sort(rA, rB, n_c, 31, mb, bstart, ctx->tmp.p, &dc->err, &buf, st,
-                                 prof ? ctx->ev_ds : nullptr, 33, mp.repeat_tol == 0 && mp.enum_tol == 1));
-        ctx->sorted_buf = buf;
-        ctx->sorted_rec = buf ? rB : rA;
+        if (!resident) {
+            int buf = 0;
+            HIPCHK(seg_onesweep_sort(rA, rB, n_c, 31, mb, bstart, ctx->tmp.p, &dc->err, &buf, st,
+                                     prof ? ctx->ev_ds : nullptr, 33, mp.repeat_tol == 0 && mp.enum_tol == 1));
+            ctx->sorted_rec = buf ? rB : rA;
+            if (prof)
+                for (int p = 0; p < npass; ++p) {
+                    float ms = 0.f;
+                    (void)hipEventElapsedTime(&ms, ctx->ev_ds[2 * p], ctx->ev_ds[2 * p + 1]);
+                    ms_dom += ms;
+                }
+            dom_bytes += n_c * 16 * (uint64_t)npass;
+            dom_launches += (uint64_t)npass;
+        } else {
+            ctx->sorted_rec = live_rec ? live_rec + o : (sbuf ? rB : rA);
+        }
         HIPCHK(hipEventRecord(ctx->ev[EV_SORT], st));
-        rc = groups_dispatch<RecViewT<33>>(ctx, RecViewT<33>{ctx->sorted_rec}, tiles, ub, mp, ps.probe_info,
-                                           ps.probe_bucket, ps.slot_info, ps.slot_bucket, st);
-        if (rc) return rc;
+        if (n_c) {
+            rc = groups_dispatch<RecViewT<33>>(ctx, RecViewT<33>{ctx->sorted_rec}, tiles, ub, mp, ps.probe_info,
+                                               ps.probe_bucket, ps.slot_info, ps.slot_bucket, st);
+            if (rc) return rc;
+        } else {
+            HIPCHK(hipMemsetAsync(&dc->nprobes, 0, 4, st));
+            HIPCHK(hipMemsetAsync(&dc->ngroups, 0, 4, st));
+        }
         rc = finish_seeds(ctx, ps, st);
         if (rc) return rc;
-        if (ctx->hc.repeat_limit)
-            return fail(ctx, MUMS_E_UNSUPPORTED, "chunked mode: a seed group above MER_REPEAT_LIMIT (the reference's "
-                                                 "SearchRange restart is reproduced below 2^32 seed-mers only)");
+        if (ctx->hc.repeat_limit && !resident)
+            return fail(ctx, MUMS_E_UNSUPPORTED, "chunked mode without resident records: a seed group above "
+                                                 "MER_REPEAT_LIMIT (the SearchRange restart needs all chunks resident)");
         HIPCHK(hipEventSynchronize(ctx->ev[EV_BUCKETS]));
-        ms_sort += el(EV_CHAINS, EV_SORT);
+        if (!resident) ms_sort += el(EV_CHAINS, EV_SORT);
         ms_groups += el(EV_SORT, EV_GROUPS);
         ms_buckets += el(EV_GROUPS, EV_BUCKETS);
-        if (prof)
-            for (int p = 0; p < npass; ++p) {
-                float ms = 0.f;
-                (void)hipEventElapsedTime(&ms, ctx->ev_ds[2 * p], ctx->ev_ds[2 * p + 1]);
-                ms_dom += ms;
-            }
-        dom_bytes += n_c * 16 * (uint64_t)npass;
-        dom_launches += (uint64_t)npass;
         groups += ctx->hc.ngroups;
         const uint64_t Pc = ctx->P;
         if (stage >= MUMS_STAGE_ALL && Pc) {
@@ -2515,6 +2739,10 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
     }
     ctx->P = P_total;
     ctx->stage_done = MUMS_STAGE_SEEDS;
+    if (live_rec) {   // the report counts the groups above MER_REPEAT_LIMIT of the whole stream
+        ctx->hc.repeat_limit = ctx->cr_cands;
+        HIPCHK(hipMemcpy(&dc->repeat_limit, &ctx->cr_cands, 8, hipMemcpyHostToDevice));
+    }
     if (stage >= MUMS_STAGE_ALL) {
         int tbits = 1;
         while (tbits < 32 && ((uint64_t)1 << tbits) < (uint64_t)ctx->table_size) ++tbits;

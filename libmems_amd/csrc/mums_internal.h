@@ -365,6 +365,32 @@ hipError_t launch_restart_compact(const RsStream& s, uint64_t n, int G, const Re
                                   uint64_t R, const uint64_t* d_rS, const uint64_t* d_S0, void* dst_a, uint32_t* dst_idx,
                                   uint32_t* dst_bstart, uint32_t* d_total, hipStream_t st);
 
+// bucket starts through a compaction's exclusive scan: out[b] = pos[bstart[b]], b <= nb
+hipError_t launch_map_starts(const uint32_t* bstart, uint32_t nb, const uint32_t* pos, uint32_t* out, hipStream_t st);
+
+// chunked.hip: MER_REPEAT_LIMIT restarts / start points over the resident chunked stream
+struct CrStream {
+    const uint64_t* rec;       // N sorted records (key_low31 << 33 | index33), all chunks
+    const uint64_t* dstart;    // 2^B + 1 global MSD digit starts
+    uint32_t nd;               // 2^B
+    uint64_t N;
+};
+uint64_t cr_blocks(uint64_t N);
+// gcnt: G x (cr_blocks(N) + 1) per-genome block counts, exclusive-scanned per genome
+hipError_t launch_cr_counts(const CrStream& s, const GenomeTable& gt, uint32_t* gcnt, void* d_scan_tmp, hipStream_t st);
+hipError_t launch_cr_ck(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, uint64_t* ck, hipStream_t st);
+hipError_t launch_cr_cands(const CrStream& s, uint64_t* list, unsigned long long* cnt, uint64_t cap, hipStream_t st);
+hipError_t launch_cr_runs(const uint64_t* ck, const GenomeTable& gt, const uint64_t* sp, uint64_t rows, uint64_t* runs,
+                          unsigned long long* nr, uint64_t cap, hipStream_t st);
+hipError_t launch_cr_kpos(const CrStream& s, const GenomeTable& gt, int g, uint64_t* K, hipStream_t st);
+hipError_t launch_cr_tie_write(const CrStream& s, const GenomeTable& gt, int g, const uint64_t* runs, uint64_t nrun,
+                               const uint64_t* ck, const uint32_t* V, uint64_t* rec, hipStream_t st);
+hipError_t launch_cr_live_compact(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, uint64_t lo,
+                                  uint64_t hi, const uint64_t* rkey, uint64_t R, const uint64_t* rS, const uint64_t* S0,
+                                  uint32_t* live, uint32_t* pos, void* d_scan_tmp, uint64_t* dst,
+                                  const uint32_t* bstart, uint32_t nb, uint32_t* dst_bstart, uint32_t* d_total,
+                                  hipStream_t st);
+
 // smlsort.hip: the std::sort order of equal seed mers in every SortedMerList
 // (MemorySML.cpp:54) for flagged runs.  Slot space = genome-major SML slots (= global
 // seed-mer indices); flags: pf[t] = 1 when sorted slots t, t + 1 form a pair of a run that

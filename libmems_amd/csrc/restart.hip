@@ -255,4 +255,9 @@ hipError_t launch_restart_compact(const RsStream& s, uint64_t n, int G, const Re
     return hipGetLastError();
 }
 
+hipError_t launch_map_starts(const uint32_t* bstart, uint32_t nb, const uint32_t* pos, uint32_t* out, hipStream_t st) {
+    hipLaunchKernelGGL(rs_bstart_kernel, grid_of(nb + 1), dim3(kBlock), 0, st, bstart, nb, pos, out);
+    return hipGetLastError();
+}
+
 }  // namespace mums
