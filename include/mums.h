@@ -234,6 +234,30 @@ int  mums_shard_msd_bits(mums_ctx* ctx, uint32_t* msd_bits, uint64_t* local_reco
 int  mums_shard_keys(mums_ctx* ctx, uint64_t* d_records, uint64_t capacity, uint64_t* bucket_counts);
 int  mums_shard_merge(mums_ctx* ctx, const uint64_t* d_records, uint32_t nsources, uint32_t first_bucket,
                       uint32_t nbuckets, const uint64_t* counts);
+/* ---- sharded MER_REPEAT_LIMIT restart (MatchFinder::SearchRange, MatchFinder.cpp:253-277;
+ * GetBreakpoint, :89-126) and FindMatchesFromPosition start points (MemHash.cpp:117-127;
+ * FindMatchSeeds, MatchFinder.cpp:137-164), between mums_shard_merge and the probe /
+ * FindMatches steps.  A restart moves the start points of every later key, i.e. of records
+ * held by other ranks, and its plan reads whole SortedMerLists (FindMer, the head-order
+ * walk), so one planner rank plans on the whole merged stream:
+ *   1. mums_shard_restart_pending: > 0 when this rank's key range holds a group above
+ *      MER_REPEAT_LIMIT or start points are set (mums_set_start_points: one per genome of
+ *      the shard layout); when any rank reports one, the steps below are required;
+ *   2. mums_shard_stream: this rank's merged stream (device records, count), gathered onto
+ *      the planner in rank order (= key order);
+ *   3. mums_shard_restart_plan (planner): d_stream = the gathered streams (ids of the runs a
+ *      start point falls into are rewritten in place, std::sort order, MemorySML.cpp:54),
+ *      counts = the keys stage's per-rank bucket counts [nranks][2^msd_bits], the key
+ *      ranges; writes one block per rank into d_out (capacity >= 8 * (N + nranks *
+ *      (2^msd_bits + 4)) bytes), block_bytes[r]; the restart log via mums_get_offset_log;
+ *   4. mums_shard_restart_apply (every rank): its block + the planner's restart log ->
+ *      the live records replace the stream and the groups stage runs again. */
+int  mums_shard_restart_pending(mums_ctx* ctx, uint64_t* pending);
+int  mums_shard_stream(mums_ctx* ctx, const void** d_records, uint64_t* n);
+int  mums_shard_restart_plan(mums_ctx* ctx, uint64_t* d_stream, uint32_t nranks, const uint64_t* counts,
+                             const uint32_t* first_bucket, const uint32_t* nbuckets, void* d_out,
+                             uint64_t capacity_bytes, uint64_t* block_bytes);
+int  mums_shard_restart_apply(mums_ctx* ctx, const void* d_block, uint64_t restarts, const uint64_t* offset_log);
 /* Accepted probes of the last seed stage, in AddHashEntry call order
  * (MemHash::EnumerateMatches -> AddHashEntry, MemHash.cpp:139-162, 209-251):
  * hash bucket ((offset % T) + T) % T and the smallest global seed-mer index of

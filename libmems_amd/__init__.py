@@ -99,7 +99,8 @@ EXPORTED_SYMBOLS = [
     "mums_get_offset_log", "mums_copy_seed_keys_range", "mums_mem_table_count", "mums_eliminate_overlaps",
     "mums_load_matches", "mums_debug_std_sort", "mums_comm_unique_id", "mums_comm_init_rank", "mums_comm_init_all",
     "mums_comm_init_local", "mums_comm_destroy", "mums_comm_last_error", "mums_shard_key_ranges", "mums_shard_run",
-    "mums_set_match_log", "mums_match_log_copy",
+    "mums_set_match_log", "mums_match_log_copy", "mums_shard_restart_pending", "mums_shard_stream",
+    "mums_shard_restart_plan", "mums_shard_restart_apply",
 ]
 
 _lib: Optional[ctypes.CDLL] = None
@@ -547,6 +548,21 @@ class ShardedMemHash:
     def AddSequence(self, seq) -> None:
         self.seqs.append(seq.encode() if isinstance(seq, str) else bytes(seq))
 
+    def FindMatchesFromPosition(self, sequences: Optional[Sequence], start_points: Sequence[int],
+                                stage: int = STAGE_ALL) -> MatchList:
+        """MemHash::FindMatchesFromPosition (MemHash.cpp:117-127) over the ranks: every rank gets
+        all G start points; rank 0 plans the restarts on the gathered streams (mums_shard_restart_*)."""
+        self._start_points = np.ascontiguousarray(np.asarray(start_points, dtype=np.uint64))
+        try:
+            return self.FindMatches(sequences, stage)
+        finally:
+            self._start_points = None
+
+    def OffsetLog(self) -> np.ndarray:
+        """Start points after every MER_REPEAT_LIMIT restart of the last find (every rank holds
+        the planner's log)."""
+        return self.ranks[0].OffsetLog() if self.ranks else np.zeros((0, 0), dtype=np.uint64)
+
     def FindMatches(self, sequences: Optional[Sequence] = None, stage: int = STAGE_ALL) -> MatchList:
         import threading
         if sequences is not None:
@@ -580,6 +596,10 @@ class ShardedMemHash:
             mh._check(self._lib.mums_shard_layout(mh._ctx, G, g0, lens))
             self.ranks.append(mh)
             g0 += cnt
+        sp = getattr(self, "_start_points", None)
+        if sp is not None:
+            for mh in self.ranks:
+                mh._check(self._lib.mums_set_start_points(mh._ctx, sp.ctypes.data, len(sp)))
         errs: List[Optional[BaseException]] = [None] * self.world
         self.rank_status = [MUMS_OK] * self.world   # every rank's mums_shard_run status
 

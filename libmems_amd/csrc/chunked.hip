@@ -62,10 +62,10 @@ __device__ __forceinline__ uint64_t cr_key(const CrStream& s, uint64_t j) {
         const uint32_t h = n >> 1;
         if (s.dstart[lo + h + 1] <= j) { lo += h + 1; n -= h + 1; } else n = h;
     }
-    return ((uint64_t)lo << 31) | (s.rec[j] >> 33);
+    return ((uint64_t)lo << s.kb) | ((s.rec[j] >> s.ib) & ((1ull << s.kb) - 1));
 }
 
-__device__ __forceinline__ uint64_t cr_idx(const CrStream& s, uint64_t j) { return s.rec[j] & ((1ull << 33) - 1); }
+__device__ __forceinline__ uint64_t cr_idx(const CrStream& s, uint64_t j) { return s.rec[j] & ((1ull << s.ib) - 1); }
 
 // per-block genome counts: gcnt[g * (nblk + 1) + b]
 __global__ __launch_bounds__(kBlock) void cr_count_kernel(CrStream s, GenomeTable gt, uint64_t nblk,
@@ -235,7 +235,7 @@ __global__ void cr_tie_write_kernel(CrStream s, GenomeTable gt, int g, const uin
     for (uint64_t j = a; j < s.N && r < hi - lo && cr_key(s, j) == key; ++j) {
         if (genome_of(gt, cr_idx(s, j)) != g) continue;
         const uint64_t gi = gt.base[g] + V[lo + r];
-        rec[j] = (rec[j] & ~((1ull << 33) - 1)) | gi;
+        rec[j] = (rec[j] & ~((1ull << s.ib) - 1)) | gi;
         ++r;
     }
 }

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <functional>
 #include <cstddef>
 #include <cstdio>
 #include <cstdlib>
@@ -116,6 +117,10 @@ struct mums_ctx {
     DevBuf tiebuf;                        // SML tie order (smlsort.hip)
     DevBuf crbuf, crcnt, crlive, crruns;  // chunked-mode restarts (chunked.hip)
     uint64_t cr_cands = 0;                // groups above MER_REPEAT_LIMIT (chunked restart)
+    DevBuf crall;                         // sharded restart planner: the whole stream's SMLs
+    bool shard_restart_pending = false;   // mums_shard_merge saw a group above the limit / start points
+    int shard_mb = 0;                     // local bucket bits of the last mums_shard_merge
+    uint64_t shard_n = 0;                 // its records
     bool ties_fixed = false;              // the stream holds every run of equal keys in std::sort order
     uint64_t tie_slots = 0;               // slots of the runs replayed by the last run (stats)
     uint64_t restarts = 0;
@@ -1395,7 +1400,7 @@ int mums_ctx_destroy(mums_ctx* ctx) {
                       &ctx->smlvB, &ctx->smltmp, &ctx->flen, &ctx->fs, &ctx->rowsall, &ctx->rsbuf,
                       &ctx->rsplan, &ctx->rsbst, &ctx->pool_loc, &ctx->cbuf, &ctx->sids,
                       &ctx->logA, &ctx->logB, &ctx->logvA, &ctx->logvB, &ctx->tiebuf, &ctx->fk, &ctx->fkloc,
-                      &ctx->crbuf, &ctx->crcnt, &ctx->crlive, &ctx->crruns};
+                      &ctx->crbuf, &ctx->crcnt, &ctx->crlive, &ctx->crruns, &ctx->crall};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i < EV_COUNT; ++i)
         if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
@@ -2020,6 +2025,34 @@ int mums_shard_keys(mums_ctx* ctx, uint64_t* d_records, uint64_t capacity, uint6
     return MUMS_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// One segment of a whole merged stream (a chunk of the chunked mode, a rank's key range of
+// the sharded mode): records [lo, hi), bucket-major over nb local buckets.
+struct RestartSeg {
+    uint64_t lo, hi;
+    uint32_t nb;
+};
+
+int stream_restart(mums_ctx* ctx, uint64_t* srec, uint64_t* other, const std::vector<uint64_t>& dstart, uint32_t kb,
+                   uint32_t ib, const std::vector<RestartSeg>& segs,
+                   const std::function<int(uint32_t, uint32_t*)>& bst_in, uint32_t* d_bst_out,
+                   std::vector<uint64_t>& n_live, bool* live_out, hipStream_t st);
+
+// stats of a sharded merge over n records: the regroup copy counts as sort, the keys stage
+// is mums_shard_keys' (owned genomes)
+void shard_merge_stats(mums_ctx* ctx, uint64_t n) {
+    fill_stats(ctx, n);
+    float rg = 0.f;
+    (void)hipEventElapsedTime(&rg, ctx->ev[EV_START], ctx->ev[EV_KEYS]);
+    ctx->st.ms_sort += rg;
+    ctx->st.ms_keys = ctx->shard_keys_ms;
+}
+}  // namespace
+
+extern "C" {
+
 int mums_shard_merge(mums_ctx* ctx, const uint64_t* d_records, uint32_t nsources, uint32_t first_bucket,
                      uint32_t nbuckets, const uint64_t* counts) {
     if (check_ctx(ctx)) return MUMS_E_INVALID;
@@ -2030,8 +2063,9 @@ int mums_shard_merge(mums_ctx* ctx, const uint64_t* d_records, uint32_t nsources
     const int B = ctx->msd_bits;
     if (nsources == 0 || (uint64_t)first_bucket + nbuckets > (1ull << B) || (nbuckets && !counts))
         return fail(ctx, MUMS_E_INVALID, "bad shard merge arguments");
-    if (have_start_points(ctx))
-        return fail(ctx, MUMS_E_UNSUPPORTED, "start points (FindMatchesFromPosition) in the sharded mode");
+    if (!ctx->start_points.empty() && ctx->start_points.size() != (size_t)ctx->gt.G)   // MatchFinder.cpp:197-199
+        return fail(ctx, MUMS_E_INVALID, "start points: one per sequence (all genomes of the shard layout) required");
+    ctx->shard_restart_pending = false;
     hipStream_t st = ctx->stream;
     // chunk table: received source-major (each source's buckets in order) -> bucket-major
     std::vector<uint64_t> tot(nbuckets, 0), chunks;
@@ -2116,27 +2150,189 @@ int mums_shard_merge(mums_ctx* ctx, const uint64_t* d_records, uint32_t nsources
             b0 = b1;
         }
     }
-    if (ctx->hc.repeat_limit)
-        return fail(ctx, MUMS_E_UNSUPPORTED, "sharded mode: a seed group above MER_REPEAT_LIMIT (the reference's "
-                                             "SearchRange restart is reproduced on one context only)");
+    // a group above MER_REPEAT_LIMIT (or start points): the restart moves start points of
+    // every later key, on every rank -> planned on the whole stream (mums_shard_restart_*)
+    ctx->restarts = 0;
+    ctx->offset_log.clear();
+    ctx->shard_restart_pending = ctx->hc.repeat_limit > 0 || have_start_points(ctx);
+    if (ctx->shard_restart_pending && ctx->merge_chunked)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "sharded mode: a MER_REPEAT_LIMIT restart after a chunked merge (a key "
+                                             "range above 2^30 records)");
+    ctx->shard_mb = mb;
+    ctx->shard_n = n;
     ctx->stage_done = MUMS_STAGE_SEEDS;
     HIPCHK(hipStreamSynchronize(st));
-    fill_stats(ctx, n);
+    shard_merge_stats(ctx, n);
     if (ctx->merge_chunked) {
         ctx->P = P_total;
         ctx->st.probes = P_total;
         ctx->st.groups = groups;
     }
-    float rg = 0.f;
-    (void)hipEventElapsedTime(&rg, ctx->ev[EV_START], ctx->ev[EV_KEYS]);
-    ctx->st.ms_sort += rg;                 // the regroup copy is part of the merge's sort
-    ctx->st.ms_keys = ctx->shard_keys_ms;  // keys stage of the owned genomes (mums_shard_keys)
+    return MUMS_OK;
+}
+
+int mums_shard_restart_pending(mums_ctx* ctx, uint64_t* pending) {
+    if (check_ctx(ctx) || !pending) return MUMS_E_INVALID;
+    if (!ctx->shard || ctx->stage_done < MUMS_STAGE_SEEDS) return fail(ctx, MUMS_E_INVALID, "no sharded merge run");
+    *pending = ctx->shard_restart_pending ? std::max<uint64_t>(ctx->hc.repeat_limit, 1) : 0;
+    return MUMS_OK;
+}
+
+int mums_shard_stream(mums_ctx* ctx, const void** d_records, uint64_t* n) {
+    if (check_ctx(ctx) || !d_records || !n) return MUMS_E_INVALID;
+    if (!ctx->shard || ctx->stage_done < MUMS_STAGE_SEEDS || ctx->merge_chunked)
+        return fail(ctx, MUMS_E_INVALID, "no sharded (one-pass) merge run");
+    *d_records = ctx->sorted_rec;
+    *n = ctx->shard_n;
+    return MUMS_OK;
+}
+
+// The planner (one rank) on the ranks' merged streams gathered in rank order (= key order):
+// MSD digit starts from the keys stage's per-rank bucket counts, one segment per rank, then
+// stream_restart; every rank's block {n_live, nbst, nbst bucket starts, live records}.
+int mums_shard_restart_plan(mums_ctx* ctx, uint64_t* d_stream, uint32_t nranks, const uint64_t* counts,
+                            const uint32_t* first_bucket, const uint32_t* nbuckets, void* d_out,
+                            uint64_t capacity_bytes, uint64_t* block_bytes) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (!have_device()) return fail(ctx, MUMS_E_NODEVICE, "no HIP device");
+    if (!ctx->shard || ctx->stage_done < MUMS_STAGE_SEEDS) return fail(ctx, MUMS_E_INVALID, "no sharded merge run");
+    if (nranks == 0 || !counts || !first_bucket || !nbuckets || !block_bytes || !d_out)
+        return fail(ctx, MUMS_E_INVALID, "bad restart plan arguments");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    const int B = ctx->msd_bits;
+    const uint64_t nb = 1ull << B;
+    std::vector<uint64_t> dstart(nb + 1, 0);
+    for (uint64_t b = 0; b < nb; ++b) {
+        uint64_t t = 0;
+        for (uint32_t r = 0; r < nranks; ++r) t += counts[(uint64_t)r * nb + b];
+        dstart[b + 1] = dstart[b] + t;
+    }
+    const uint64_t N = dstart[nb];
+    std::vector<RestartSeg> segs(nranks);
+    std::vector<int> mbs(nranks);
+    uint64_t need = 0, expect = 0;
+    for (uint32_t r = 0; r < nranks; ++r) {
+        if ((uint64_t)first_bucket[r] + nbuckets[r] > nb || first_bucket[r] != expect)
+            return fail(ctx, MUMS_E_INVALID, "restart plan: key ranges must tile the buckets in rank order");
+        expect = first_bucket[r] + nbuckets[r];
+        mbs[r] = ceil_log2(nbuckets[r]);
+        segs[r] = RestartSeg{dstart[first_bucket[r]], dstart[expect], 1u << mbs[r]};
+        if (segs[r].hi - segs[r].lo >= 0xFFFFFFF0ull) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 records per shard");
+        need += 8 * (2 + (uint64_t)segs[r].nb + 1 + (segs[r].hi - segs[r].lo));
+    }
+    if (expect != nb) return fail(ctx, MUMS_E_INVALID, "restart plan: key ranges must cover every bucket");
+    if (need > capacity_bytes) return fail(ctx, MUMS_E_INVALID, "restart plan: output buffer too small");
+    if (N && !d_stream) return fail(ctx, MUMS_E_INVALID, "null stream");
+    const uint64_t n_own = ctx->N;
+    ctx->N = N;   // stream_restart's stream: the whole merged stream
+    HIPCHK(ctx->crall.ensure((N + 64) * 8));
+    uint64_t nbst = 0;
+    for (const RestartSeg& g : segs) nbst += g.nb + 1;
+    HIPCHK(ctx->rsbst.ensure(nbst * 4 + 64));
+    std::vector<uint64_t> n_live;
+    bool live = false;
+    std::vector<uint32_t> hb;
+    const int kb = 2 * ctx->w + 1 - B;
+    int rc = stream_restart(ctx, d_stream, ctx->crall.as<uint64_t>(), dstart, (uint32_t)kb, (uint32_t)ctx->rec_ib, segs,
+                            [&](uint32_t r, uint32_t* d) -> int {
+        hb.assign(segs[r].nb + 1, (uint32_t)(segs[r].hi - segs[r].lo));
+        for (uint32_t b = 0; b < nbuckets[r]; ++b) hb[b] = (uint32_t)(dstart[first_bucket[r] + b] - segs[r].lo);
+        HIPCHK(hipMemcpy(d, hb.data(), hb.size() * 4, hipMemcpyHostToDevice));
+        return MUMS_OK;
+    }, ctx->rsbst.as<uint32_t>(), n_live, &live, st);
+    ctx->N = n_own;
+    if (rc) return rc;
+    // blocks: header words, bucket starts widened to 64 bits, records
+    const uint64_t* src = live ? ctx->crall.as<uint64_t>() : d_stream;
+    std::vector<uint32_t> all_bst(nbst);
+    if (live) HIPCHK(hipMemcpy(all_bst.data(), ctx->rsbst.p, nbst * 4, hipMemcpyDeviceToHost));
+    uint64_t o = 0, bo = 0;
+    char* out = (char*)d_out;
+    for (uint32_t r = 0; r < nranks; ++r) {
+        const uint64_t nl = live ? n_live[r] : segs[r].hi - segs[r].lo;
+        std::vector<uint64_t> head(2 + segs[r].nb + 1);
+        head[0] = nl;
+        head[1] = segs[r].nb + 1;
+        for (uint64_t b = 0; b <= segs[r].nb; ++b) {
+            uint64_t v;
+            if (live) v = all_bst[bo + b];
+            else v = b < nbuckets[r] ? dstart[first_bucket[r] + b] - segs[r].lo : segs[r].hi - segs[r].lo;
+            head[2 + b] = v;
+        }
+        bo += segs[r].nb + 1;
+        HIPCHK(hipMemcpy(out + o, head.data(), head.size() * 8, hipMemcpyHostToDevice));
+        o += head.size() * 8;
+        if (nl) HIPCHK(hipMemcpyAsync(out + o, src + segs[r].lo, nl * 8, hipMemcpyDeviceToDevice, st));
+        o += nl * 8;
+        block_bytes[r] = 8 * (head.size() + nl);
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    ctx->crall.release();
+    return MUMS_OK;
+}
+
+// Every rank: its block from the planner -> the live records replace the merged stream,
+// the groups stage runs again (as restart_stage does on one context).
+int mums_shard_restart_apply(mums_ctx* ctx, const void* d_block, uint64_t restarts, const uint64_t* offset_log) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (!have_device()) return fail(ctx, MUMS_E_NODEVICE, "no HIP device");
+    if (!ctx->shard || ctx->stage_done < MUMS_STAGE_SEEDS || ctx->merge_chunked)
+        return fail(ctx, MUMS_E_INVALID, "no sharded (one-pass) merge run");
+    if (!d_block || (restarts && !offset_log)) return fail(ctx, MUMS_E_INVALID, "bad restart block");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    const int mb = ctx->shard_mb;
+    uint64_t head[2] = {0, 0};
+    HIPCHK(hipMemcpy(head, d_block, 16, hipMemcpyDeviceToHost));
+    const uint64_t nl = head[0];
+    if (head[1] != (1ull << mb) + 1 || nl > ctx->shard_n)
+        return fail(ctx, MUMS_E_INVALID, "restart block does not match this rank's merge");
+    std::vector<uint64_t> b64(head[1]);
+    HIPCHK(hipMemcpy(b64.data(), (const uint64_t*)d_block + 2, head[1] * 8, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> bst(head[1]);
+    for (uint64_t b = 0; b < head[1]; ++b) bst[b] = (uint32_t)b64[b];
+    const int B = ctx->msd_bits;
+    const int kb = 2 * ctx->w + 1 - B;
+    ProbeSpace ps{};
+    int rc = ensure_merge_space(ctx, ctx->shard_n, mb, kb, &ps);
+    if (rc) return rc;
+    uint64_t* dst = ctx->sorted_buf ? ctx->recA.as<uint64_t>() : ctx->recB.as<uint64_t>();
+    if (nl) HIPCHK(hipMemcpyAsync(dst, (const uint64_t*)d_block + 2 + head[1], nl * 8, hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(ctx->mstart.p, bst.data(), bst.size() * 4, hipMemcpyHostToDevice, st));
+    ctx->sorted_buf ^= 1;
+    ctx->sorted_rec = dst;
+    DevCounters* dc = ctx->counters.as<DevCounters>();
+    const uint64_t rep = ctx->hc.repeat_limit;
+    SegTile* tiles = ctx->tiles.as<SegTile>();
+    HIPCHK(build_seg_tiles_from_starts(ctx->mstart.as<uint32_t>(), mb, nl, tiles, &dc->ntiles, ctx->tmp.p, st));
+    HIPCHK(hipMemsetAsync(&dc->repeat_limit, 0, 8, st));
+    const MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, ctx->masked, ctx->seq_mask};
+    const uint64_t ub = seg_tiles_upper(nl, mb);
+    if (ctx->rec_ib == 33)
+        rc = groups_dispatch<RecViewT<33>>(ctx, RecViewT<33>{dst}, tiles, ub, mp, ps.probe_info, ps.probe_bucket,
+                                           ps.slot_info, ps.slot_bucket, st);
+    else
+        rc = groups_dispatch<RecView>(ctx, RecView{dst}, tiles, ub, mp, ps.probe_info, ps.probe_bucket, ps.slot_info,
+                                      ps.slot_bucket, st);
+    if (rc) return rc;
+    rc = finish_seeds(ctx, ps, st);
+    if (rc) return rc;
+    HIPCHK(hipMemcpy(&dc->repeat_limit, &rep, 8, hipMemcpyHostToDevice));   // the report: the whole range's groups
+    ctx->hc.repeat_limit = rep;
+    ctx->restarts = restarts;
+    ctx->offset_log.assign(offset_log, offset_log + restarts * (uint64_t)ctx->gt.G);
+    ctx->shard_restart_pending = false;
+    HIPCHK(hipStreamSynchronize(st));
+    shard_merge_stats(ctx, ctx->shard_n);
     return MUMS_OK;
 }
 
 int mums_probe_count(mums_ctx* ctx, uint64_t* count) {
     if (check_ctx(ctx) || !count) return MUMS_E_INVALID;
     if (ctx->stage_done < MUMS_STAGE_SEEDS) return fail(ctx, MUMS_E_INVALID, "no seed stage run");
+    if (ctx->shard && ctx->shard_restart_pending)
+        return fail(ctx, MUMS_E_INVALID, "sharded restart pending (mums_shard_restart_plan / _apply)");
     *count = ctx->P;
     return MUMS_OK;
 }
@@ -2146,6 +2342,8 @@ int mums_probe_copy(mums_ctx* ctx, uint32_t* buckets, uint64_t* ref_index, uint6
     if (ctx->stage_done < MUMS_STAGE_SEEDS) return fail(ctx, MUMS_E_INVALID, "no seed stage run");
     if (ctx->shard && ctx->merge_chunked)
         return fail(ctx, MUMS_E_UNSUPPORTED, "probe export after a chunked shard merge");
+    if (ctx->shard && ctx->shard_restart_pending)
+        return fail(ctx, MUMS_E_INVALID, "sharded restart pending (mums_shard_restart_plan / _apply)");
     if (capacity < ctx->P) return fail(ctx, MUMS_E_INVALID, "output buffer too small");
     if (!ctx->packed_path) return fail(ctx, MUMS_E_UNSUPPORTED, "probe export needs the packed-record path");
     if (ctx->P && (!ctx->probe_info || !ctx->sorted_rec))
@@ -2183,6 +2381,8 @@ int shard_seeds_done(mums_ctx* ctx) {
     if (ctx->stage_done < MUMS_STAGE_SEEDS) return fail(ctx, MUMS_E_INVALID, "no sharded seed stage run");
     if (ctx->merge_chunked)
         return fail(ctx, MUMS_E_UNSUPPORTED, "sharded FindMatches after a chunked merge (> 2^30 records per rank)");
+    if (ctx->shard_restart_pending)
+        return fail(ctx, MUMS_E_INVALID, "sharded restart pending (mums_shard_restart_plan / _apply)");
     return MUMS_OK;
 }
 
@@ -2341,24 +2541,27 @@ int run_pipeline_pairwise(mums_ctx* ctx, int stage) {
 // global indices; the 2w+1-31 MSD digits are cut into power-of-two chunks of < 2^30
 // records and every chunk runs scatter -> onesweep -> groups -> probe buckets [-> rows]
 // on its own, in key order; the FindMatches tail then replays all chunks' rows.
-// MER_REPEAT_LIMIT restarts / start points of the chunked mode (MatchFinder.cpp:253-277,
-// MemHash.cpp:117-127): all chunks resident and sorted in buffer sbuf.  Candidates (groups
+// MER_REPEAT_LIMIT restarts / start points (MatchFinder.cpp:253-277, MemHash.cpp:117-127)
+// over a whole merged stream srec of N records (N = ctx->N; key_low << ib | global index,
+// 2^B MSD digits implicit, digit starts dstart), split into segments.  Candidates (groups
 // above 1000 records) from the whole stream; if any (or start points): the G SortedMerLists
-// as full keys in the other record buffer, the restart plan (restart_plan.h), the std::sort
-// order of the runs a start point falls into (smlsort.hip, one genome at a time), then each
-// chunk's live records compacted into the other buffer: *live_rec, n_live[c], the chunks'
-// bucket starts in ctx->rsbst.  *live_rec stays null when every record lives.
-int chunked_restart(mums_ctx* ctx, int sbuf, const std::vector<uint64_t>& dstart, const std::vector<uint64_t>& cbase,
-                    uint32_t* hist, uint32_t T, uint32_t nbc, int mb, uint32_t nch, std::vector<uint64_t>& n_live,
-                    uint64_t** live_rec, hipStream_t st) {
+// as full keys in `other` (N + 64 slots), the restart plan (restart_plan.h), the std::sort
+// order of the runs a start point falls into (smlsort.hip, one genome at a time; the ids of
+// those records in srec are rewritten), then each segment's live records compacted into
+// `other` at the segment's base: n_live[c], its bucket starts (bst_in(c, d) writes the
+// original nb + 1 of them to device memory d) mapped into d_bst_out + sum of earlier (nb + 1).
+// *live = false when every record lives (nothing written).
+int stream_restart(mums_ctx* ctx, uint64_t* srec, uint64_t* other, const std::vector<uint64_t>& dstart, uint32_t kb,
+                   uint32_t ib, const std::vector<RestartSeg>& segs,
+                   const std::function<int(uint32_t, uint32_t*)>& bst_in, uint32_t* d_bst_out,
+                   std::vector<uint64_t>& n_live, bool* live_out, hipStream_t st) {
     const GenomeTable& gt = ctx->gt;
     const int G = gt.G;
     const uint64_t Gu = (uint64_t)G;
     const uint64_t N = ctx->N;
     const uint32_t nd = (uint32_t)dstart.size() - 1;
-    uint64_t* srec = sbuf ? ctx->recB.as<uint64_t>() : ctx->recA.as<uint64_t>();
-    uint64_t* other = sbuf ? ctx->recA.as<uint64_t>() : ctx->recB.as<uint64_t>();
-    *live_rec = nullptr;
+    *live_out = false;
+    n_live.assign(segs.size(), 0);
     ctx->restarts = 0;
     ctx->offset_log.clear();
     const uint64_t ccap = N / (restart::kRepeatLimit + 1) + 16;   // candidates: runs of > 1000 records
@@ -2367,16 +2570,18 @@ int chunked_restart(mums_ctx* ctx, int sbuf, const std::vector<uint64_t>& dstart
     unsigned long long* d_cnt = (unsigned long long*)(d_dstart + nd + 1);
     uint64_t* d_list = (uint64_t*)(d_cnt + 8);
     HIPCHK(hipMemcpyAsync(d_dstart, dstart.data(), (nd + 1) * 8, hipMemcpyHostToDevice, st));
-    const CrStream s{srec, d_dstart, nd, N};
+    CrStream s{srec, d_dstart, nd, N};
+    s.kb = kb;
+    s.ib = ib;
     HIPCHK(launch_cr_cands(s, d_list, d_cnt, ccap, st));
     unsigned long long C = 0;
     HIPCHK(hipMemcpyAsync(&C, d_cnt, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     ctx->cr_cands = C;
     if (C == 0 && !have_start_points(ctx)) return MUMS_OK;
-    if (C > ccap) return fail(ctx, MUMS_E_HIP, "chunked restart: candidate list overflow (internal error)");
-    if (seg_onesweep_launches(31) < 4)
-        return fail(ctx, MUMS_E_UNSUPPORTED, "chunked restart with the segment fix-up sort (MUMS_DEV_SEGFIX)");
+    if (C > ccap) return fail(ctx, MUMS_E_HIP, "restart: candidate list overflow (internal error)");
+    if (ctx->parity_masked || seg_onesweep_launches(kb) < (int)((kb + 7) / 8))
+        return fail(ctx, MUMS_E_UNSUPPORTED, "restart with the segment fix-up sort (MUMS_DEV_SEGFIX)");
     std::vector<uint64_t> cand(C);
     if (C) {
         HIPCHK(hipMemcpy(cand.data(), d_list, C * 8, hipMemcpyDeviceToHost));
@@ -2445,7 +2650,7 @@ int chunked_restart(mums_ctx* ctx, int sbuf, const std::vector<uint64_t>& dstart
     unsigned long long nruns = 0;
     HIPCHK(hipMemcpyAsync(&nruns, d_cnt, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    if (nruns > rcap) return fail(ctx, MUMS_E_HIP, "chunked restart: run list overflow (internal error)");
+    if (nruns > rcap) return fail(ctx, MUMS_E_HIP, "restart: run list overflow (internal error)");
     if (nruns) {
         std::vector<uint64_t> hr(3 * nruns);
         HIPCHK(hipMemcpy(hr.data(), d_runs, 3 * nruns * 8, hipMemcpyDeviceToHost));
@@ -2456,8 +2661,8 @@ int chunked_restart(mums_ctx* ctx, int sbuf, const std::vector<uint64_t>& dstart
             const uint64_t m = gt.m[g];
             if (m >= 0xFFFFFFF0ull) return fail(ctx, MUMS_E_UNSUPPORTED, "SortedMerList of more than 2^32 seed-mers");
             if (ctx->tiebuf.ensure(tie_ws_bytes(m, 1)) != hipSuccess)
-                return fail(ctx, MUMS_E_NOMEM, "chunked restart: no device memory for the SortedMerList tie order "
-                                               "of a genome");
+                return fail(ctx, MUMS_E_NOMEM, "restart: no device memory for the SortedMerList tie order of a "
+                                               "genome");
             const TieWs tw = tie_ws_layout(ctx->tiebuf.p, m, 1);
             const uint64_t b0 = 0;
             HIPCHK(tie_set_genomes(tw, &b0, &m, st));
@@ -2479,29 +2684,55 @@ int chunked_restart(mums_ctx* ctx, int sbuf, const std::vector<uint64_t>& dstart
         HIPCHK(hipStreamSynchronize(st));
         ctx->tiebuf.release();
     }
-    // every chunk's live records (SML index >= the start point of its key's phase),
-    // compacted into the other buffer at the chunk's base (the SMLs there are dead now)
-    uint64_t nmax = 0;
-    for (uint32_t c = 0; c < nch; ++c) nmax = std::max(nmax, cbase[c + 1] - cbase[c]);
-    HIPCHK(ctx->crlive.ensure(2 * (nmax + 64) * 4));
-    HIPCHK(ctx->rsbst.ensure((uint64_t)nch * (nbc + 1) * 4 + 64));
+    // every segment's live records (SML index >= the start point of its key's phase),
+    // compacted into `other` at the segment's base (the SMLs there are dead now)
+    uint64_t nmax = 0, nbmax = 0;
+    for (const RestartSeg& g : segs) {
+        nmax = std::max(nmax, g.hi - g.lo);
+        nbmax = std::max<uint64_t>(nbmax, g.nb);
+    }
+    HIPCHK(ctx->crlive.ensure(2 * (nmax + 64) * 4 + (nbmax + 64) * 4));
     HIPCHK(ctx->tmp.ensure(std::max(ctx->tmp.cap, scan_tmp_bytes(nmax + 2))));
     uint32_t* live = ctx->crlive.as<uint32_t>();
     uint32_t* pos = live + nmax + 64;
+    uint32_t* bst = pos + nmax + 64;
     uint32_t* d_total = (uint32_t*)d_cnt;
-    for (uint32_t c = 0; c < nch; ++c) {
-        const uint64_t lo = cbase[c], hi = cbase[c + 1];
-        uint32_t* bst = ctx->mstart.as<uint32_t>();
-        HIPCHK(seg_bucket_starts(mb > 0 ? hist + (uint64_t)c * nbc * T : nullptr, T, mb, hi - lo, bst, st));
+    uint64_t bo = 0;
+    for (uint32_t c = 0; c < (uint32_t)segs.size(); ++c) {
+        const uint64_t lo = segs[c].lo, hi = segs[c].hi;
+        const int rc = bst_in(c, bst);
+        if (rc) return rc;
         HIPCHK(launch_cr_live_compact(s, gt, gscan, lo, hi, d_rkey, R, d_rS, d_S0, live, pos, ctx->tmp.p, other + lo,
-                                      bst, nbc, ctx->rsbst.as<uint32_t>() + (uint64_t)c * (nbc + 1), d_total, st));
+                                      bst, segs[c].nb, d_bst_out + bo, d_total, st));
+        bo += segs[c].nb + 1;
         uint32_t t = 0;
         HIPCHK(hipMemcpyAsync(&t, d_total, 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         n_live[c] = t;
     }
     for (DevBuf* b : {&ctx->crcnt, &ctx->crlive, &ctx->crruns}) b->release();
-    *live_rec = other;
+    *live_out = true;
+    return MUMS_OK;
+}
+
+// The chunked mode's restart (all chunks resident and sorted in buffer sbuf): live chunks
+// into the other buffer (*live_rec), n_live[c], the chunks' bucket starts in ctx->rsbst.
+int chunked_restart(mums_ctx* ctx, int sbuf, const std::vector<uint64_t>& dstart, const std::vector<uint64_t>& cbase,
+                    uint32_t* hist, uint32_t T, uint32_t nbc, int mb, uint32_t nch, std::vector<uint64_t>& n_live,
+                    uint64_t** live_rec, hipStream_t st) {
+    uint64_t* srec = sbuf ? ctx->recB.as<uint64_t>() : ctx->recA.as<uint64_t>();
+    uint64_t* other = sbuf ? ctx->recA.as<uint64_t>() : ctx->recB.as<uint64_t>();
+    *live_rec = nullptr;
+    std::vector<RestartSeg> segs(nch);
+    for (uint32_t c = 0; c < nch; ++c) segs[c] = RestartSeg{cbase[c], cbase[c + 1], nbc};
+    HIPCHK(ctx->rsbst.ensure((uint64_t)nch * (nbc + 1) * 4 + 64));
+    bool live = false;
+    const int rc = stream_restart(ctx, srec, other, dstart, 31, 33, segs, [&](uint32_t c, uint32_t* d) -> int {
+        HIPCHK(seg_bucket_starts(mb > 0 ? hist + (uint64_t)c * nbc * T : nullptr, T, mb, cbase[c + 1] - cbase[c], d, st));
+        return MUMS_OK;
+    }, ctx->rsbst.as<uint32_t>(), n_live, &live, st);
+    if (rc) return rc;
+    if (live) *live_rec = other;
     return MUMS_OK;
 }
 
@@ -2522,6 +2753,7 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
     ctx->packed_path = true;
     ctx->key64 = true;
     ctx->msd_bits = B;
+    ctx->parity_masked = false;
     uint64_t words = 0;
     const uint32_t T = layout_packed(gt, &words);
     HIPCHK(ctx->packed.ensure(words * 4 + 64));

@@ -370,10 +370,11 @@ hipError_t launch_map_starts(const uint32_t* bstart, uint32_t nb, const uint32_t
 
 // chunked.hip: MER_REPEAT_LIMIT restarts / start points over the resident chunked stream
 struct CrStream {
-    const uint64_t* rec;       // N sorted records (key_low31 << 33 | index33), all chunks
+    const uint64_t* rec;       // N sorted records (key_low << ib | index), MSD digit implicit
     const uint64_t* dstart;    // 2^B + 1 global MSD digit starts
     uint32_t nd;               // 2^B
     uint64_t N;
+    uint32_t kb = 31, ib = 33; // key bits / index bits per record (chunked mode: 31 / 33)
 };
 uint64_t cr_blocks(uint64_t N);
 // gcnt: G x (cr_blocks(N) + 1) per-genome block counts, exclusive-scanned per genome

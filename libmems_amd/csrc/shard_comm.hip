@@ -9,6 +9,8 @@
 //   3. exchange : one all-to-allv moves every key range to its owner rank, sources in
 //                 rank order (= global seed-mer index order);
 //   4. merge    : mums_shard_merge -> this key range's probes in AddHashEntry order;
+//      (4b. a MER_REPEAT_LIMIT restart or start points: streams gathered on rank 0, which
+//      plans and returns every rank's live records; mums_shard_restart_*)
 //   5. buckets  : all-gather of per-hash-bucket probe counts, bucket ranges per rank;
 //   6. rows     : mums_shard_probe_rows + all-to-allv of the probe rows;
 //   7. genomes  : all-gather(v) of the 2-bit packed genomes (chain walks read any genome);
@@ -228,6 +230,66 @@ int agree(mums_comm* c, int rc, hipStream_t st) {
 // a local step's status: OK, or the step's code (allocation failures as MUMS_E_NOMEM)
 #define AGREE(x) RC(agree(comm, (x), st))
 
+// 4b. MER_REPEAT_LIMIT restarts / start points (MatchFinder.cpp:253-277, MemHash.cpp:117-127):
+// a restart moves the start points of every later key (records of other ranks) and its plan
+// reads whole SortedMerLists, so the merged streams are gathered in rank order (= key order)
+// onto rank 0, which plans, fixes the std::sort tie order of the runs the start points fall
+// into and compacts every rank's live records; the blocks go back in one all-to-allv and
+// every rank runs its groups stage again.  C: the keys stage's per-rank bucket counts.
+int shard_restart(mums_ctx* ctx, mums_comm* comm, const std::vector<uint64_t>& C, const std::vector<uint32_t>& kf,
+                  const std::vector<uint32_t>& kn, uint32_t nb, hipStream_t st) {
+    const int W = comm->world, R = comm->rank;
+    const void* d_stream = nullptr;
+    uint64_t n = 0;
+    AGREE(mums_shard_stream(ctx, &d_stream, &n));
+    std::vector<uint64_t> NN(W);
+    RC(comm->allgather_u64(&n, 1, NN.data(), st));
+    uint64_t N = 0;
+    for (int r = 0; r < W; ++r) N += NN[r];
+    std::vector<uint64_t> sb(W, 0), rb(W, 0);
+    sb[0] = n * 8;
+    if (R == 0)
+        for (int r = 0; r < W; ++r) rb[r] = NN[r] * 8;
+    const uint64_t out_cap = 8 * (N + (uint64_t)W * (nb + 4));
+    AGREE(R == 0 && (comm->recv.ensure(N * 8 + 8) || comm->rows.ensure(out_cap)) ? MUMS_E_NOMEM : MUMS_OK);
+    RC(comm->alltoallv(d_stream, sb.data(), comm->recv.p, rb.data(), st));
+    std::vector<uint64_t> bb(W, 0);
+    int rc = hipStreamSynchronize(st) != hipSuccess ? MUMS_E_HIP : MUMS_OK;
+    if (rc == MUMS_OK && R == 0)
+        rc = mums_shard_restart_plan(ctx, (uint64_t*)comm->recv.p, (uint32_t)W, C.data(), kf.data(), kn.data(),
+                                     comm->rows.p, out_cap, bb.data());
+    uint64_t rows = 0;
+    uint32_t G = 0;
+    if (rc == MUMS_OK) rc = mums_get_offset_log(ctx, nullptr, 0, &rows, &G);
+    AGREE(rc);
+    // rank 0's restart count and block sizes, then its offset log
+    std::vector<uint64_t> meta(1 + W, 0), M((size_t)W * (1 + W));
+    if (R == 0) {
+        meta[0] = rows;
+        for (int r = 0; r < W; ++r) meta[1 + r] = bb[r];
+    }
+    RC(comm->allgather_u64(meta.data(), meta.size(), M.data(), st));
+    const uint64_t nres = M[0];
+    std::vector<uint64_t> log(nres * G, 0);
+    if (nres * G) {
+        std::vector<uint64_t> mine(nres * G, 0), L((size_t)W * nres * G);
+        if (R == 0) rc = mums_get_offset_log(ctx, mine.data(), nres, &rows, &G);
+        AGREE(rc);
+        RC(comm->allgather_u64(mine.data(), mine.size(), L.data(), st));
+        std::copy(L.begin(), L.begin() + nres * G, log.begin());
+    }
+    std::fill(sb.begin(), sb.end(), 0);
+    std::fill(rb.begin(), rb.end(), 0);
+    if (R == 0)
+        for (int r = 0; r < W; ++r) sb[r] = M[1 + r];
+    rb[0] = M[1 + R];
+    AGREE(comm->rrows.ensure(rb[0] + 8) ? MUMS_E_NOMEM : MUMS_OK);
+    RC(comm->alltoallv(comm->rows.p, sb.data(), comm->rrows.p, rb.data(), st));
+    rc = hipStreamSynchronize(st) != hipSuccess ? MUMS_E_HIP : MUMS_OK;
+    if (rc == MUMS_OK) rc = mums_shard_restart_apply(ctx, comm->rrows.p, nres, log.data());
+    return agree(comm, rc, st);
+}
+
 }  // namespace
 
 extern "C" {
@@ -343,6 +405,15 @@ int mums_shard_run(mums_ctx* ctx, mums_comm* comm, int stage) {
     rc = hipStreamSynchronize(st) != hipSuccess ? MUMS_E_HIP : MUMS_OK;
     if (rc == MUMS_OK) rc = mums_shard_merge(ctx, merged, (uint32_t)W, first, cnt, sub.data());
     AGREE(rc);
+    {   // 4b: restarts, when any rank's key range holds a group above MER_REPEAT_LIMIT
+        uint64_t pend = 0;
+        AGREE(mums_shard_restart_pending(ctx, &pend));
+        std::vector<uint64_t> PEND(W);
+        RC(comm->allgather_u64(&pend, 1, PEND.data(), st));
+        bool any = false;
+        for (int r = 0; r < W; ++r) any = any || PEND[r] != 0;
+        if (any) RC(shard_restart(ctx, comm, C, kf, kn, nb, st));
+    }
     if (stage != MUMS_STAGE_ALL) return MUMS_OK;
     // 5-8: sharded FindMatches
     uint32_t T = 0, G = 0;

@@ -1,0 +1,106 @@
+"""GPU parity of MER_REPEAT_LIMIT restarts (MatchFinder.cpp:253-277) and FindMatchesFromPosition
+start points (MemHash.cpp:117-127) in the sharded mode (mums_shard_run, shard_comm.hip): the
+ranks' merged streams are gathered onto rank 0, which plans the restarts on the whole stream
+(restart_plan.h), fixes the std::sort order of the runs a start point falls into
+(MemorySML.cpp:54) and sends every rank its live records (mums_shard_restart_*).
+
+Ranks are threads of one process over the host-staged communicator (one GPU); genome blocks
+and position slices.  MatchList, collisions (summed over ranks), restarts and the offset log
+must equal the oracle's."""
+import os
+
+import numpy as np
+import pytest
+
+from tests import repeat_inputs, tie_inputs
+
+pytestmark = pytest.mark.gpu
+
+
+def check(lm, oracle_mod, seqs, world, w=15, layout="blocks", start_points=None, table_size=40000):
+    if layout == "slices":   # world / G position slices per genome
+        world = len(seqs) * (1 if world <= len(seqs) else 2)
+    seed = oracle_mod.get_seed(w)
+    ref_len, ref_starts, ref = oracle_mod.find_matches(seqs, seed, start_points=start_points, table_size=table_size)
+    with lm.ShardedMemHash([0] * world, comm="local", layout=layout, table_size=table_size) as sh:
+        sh.SetSeed(seed)
+        if start_points is None:
+            ml = sh.FindMatches(seqs)
+        else:
+            ml = sh.FindMatchesFromPosition(seqs, start_points)
+        stats = sh.stats_per_rank
+        offlog = sh.OffsetLog()
+    assert all(s["restarts"] == ref["restarts"] for s in stats), ([s["restarts"] for s in stats], ref["restarts"])
+    assert np.array_equal(offlog, ref["offset_log"])
+    assert len(ml) == len(ref_len), (len(ml), len(ref_len))
+    assert np.array_equal(ml.lengths, ref_len) and np.array_equal(ml.starts, ref_starts)
+    assert sum(s["collision_count"] for s in stats) == ref["collision_count"]
+    return ref
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("layout", ["blocks", "slices"])
+def test_n_gapped(gpu_lib, oracle_mod, world, layout):
+    seqs = repeat_inputs.n_gapped(G=3, n=200_000, gaps=((40_000, 3000), (120_000, 3000)), shift=500, seed=1)
+    ref = check(gpu_lib, oracle_mod, seqs, world, layout=layout)
+    assert ref["restarts"] > 0
+
+
+@pytest.mark.parametrize("tandem", [False, True])
+@pytest.mark.parametrize("world", [2, 4])
+def test_high_copy(gpu_lib, oracle_mod, tandem, world):
+    seqs = repeat_inputs.high_copy(G=3, n=60_000, copies=2000, tandem=tandem, seed=2)
+    check(gpu_lib, oracle_mod, seqs, world)
+
+
+def test_runs_across_buffer_boundaries(gpu_lib, oracle_mod):
+    seqs = repeat_inputs.n_gapped(G=4, n=90_000, gaps=((2_000, 25_000), (60_000, 10_022)), shift=1_300, seed=13)
+    check(gpu_lib, oracle_mod, seqs, 3, w=17, layout="slices")
+
+
+@pytest.mark.parametrize("seed", list(range(0, 10)) + [95, 106])
+def test_mixed_repeats_fuzz(gpu_lib, oracle_mod, seed):
+    check(gpu_lib, oracle_mod, repeat_inputs.mixed_repeats(seed), 2 + seed % 3,
+          layout="slices" if seed % 2 else "blocks")
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_multi_gap_ties(gpu_lib, oracle_mod, seed):
+    # restarts at the "A...AC" gap keys: start points inside runs of equal full keys
+    check(gpu_lib, oracle_mod, tie_inputs.multi_gap(seed=seed), 2 + seed % 3, w=15 + 2 * (seed % 3))
+
+
+def test_small_table(gpu_lib, oracle_mod):
+    seqs = repeat_inputs.n_gapped(G=4, n=80_000, gaps=((10_000, 3000), (50_000, 1800)), shift=300, seed=19)
+    check(gpu_lib, oracle_mod, seqs, 3, w=19, table_size=7)
+
+
+@pytest.mark.parametrize("sp", [[0, 0, 0], [1000, 25_000, 7], [50_000, 0, 59_000]])
+def test_start_points_plain(gpu_lib, oracle_mod, sp):
+    seqs = oracle_mod.generate(3, 60_000, 0.02, 777)
+    check(gpu_lib, oracle_mod, seqs, 3, start_points=sp)
+
+
+@pytest.mark.parametrize("sp", [[1000, 25_000, 7], [3, 9_999, 10_001, 40_000]])
+@pytest.mark.parametrize("layout", ["blocks", "slices"])
+def test_start_points_with_restarts(gpu_lib, oracle_mod, sp, layout):
+    seqs = repeat_inputs.n_gapped(G=len(sp), n=90_000, gaps=((2_000, 25_000), (60_000, 4_000)), shift=1_300,
+                                  seed=31)
+    check(gpu_lib, oracle_mod, seqs, 2, start_points=sp, layout=layout)
+
+
+@pytest.mark.parametrize("sd", range(4))
+def test_start_points_in_duplicate_runs(gpu_lib, oracle_mod, sd):
+    rng = np.random.default_rng(200 + sd)
+    seqs = tie_inputs.dup_block(seed=80 + sd)
+    sp = [int(rng.integers(0, 30_000)), int(rng.integers(1, 50_000)), 0]
+    check(gpu_lib, oracle_mod, seqs, 2 + sd % 3, start_points=sp)
+
+
+def test_start_point_count_must_match(gpu_lib, oracle_mod):
+    seqs = oracle_mod.generate(3, 20_000, 0.02, 9)
+    with gpu_lib.ShardedMemHash([0] * 2, comm="local") as sh:
+        sh.SetSeed(oracle_mod.get_seed(15))
+        with pytest.raises(gpu_lib.MumsError):
+            sh.FindMatchesFromPosition(seqs, [5, 7])
+        assert sh.rank_status == [gpu_lib.MUMS_E_INVALID] * 2
