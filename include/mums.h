@@ -304,6 +304,18 @@ int  mums_comm_unique_id(void* id, uint64_t bytes);   /* ncclGetUniqueId, 128 by
 int  mums_comm_init_rank(mums_comm** comm, int device, int world, int rank, const void* id);
 int  mums_comm_init_all(mums_comm** comms, int ndev, const int* devices);
 int  mums_comm_init_local(mums_comm** comms, int nranks, const int* devices);
+/* The caller's own transport (MPI, gloo, a job launcher's sockets ...): two host-side
+ * collectives, called on every rank in the same order; return 0 on success.  Device data
+ * is staged through host memory by the library.
+ *   allgather_u64: recv[r * n + i] = rank r's send[i]
+ *   alltoallv    : send holds one byte block per peer in rank order (send_bytes[p] bytes
+ *                  for peer p), recv the blocks from every peer in rank order (recv_bytes[p]) */
+typedef struct mums_comm_ops {
+    int (*allgather_u64)(void* user, const uint64_t* send, uint64_t n, uint64_t* recv);
+    int (*alltoallv)(void* user, const void* send, const uint64_t* send_bytes, void* recv,
+                     const uint64_t* recv_bytes);
+} mums_comm_ops;
+int  mums_comm_init_host(mums_comm** comm, int device, int world, int rank, const mums_comm_ops* ops, void* user);
 void mums_comm_destroy(mums_comm* comm);
 const char* mums_comm_last_error(mums_comm* comm);
 /* the balanced contiguous key (or hash-bucket) ranges of the exchange: rank r gets

@@ -100,8 +100,18 @@ EXPORTED_SYMBOLS = [
     "mums_load_matches", "mums_debug_std_sort", "mums_comm_unique_id", "mums_comm_init_rank", "mums_comm_init_all",
     "mums_comm_init_local", "mums_comm_destroy", "mums_comm_last_error", "mums_shard_key_ranges", "mums_shard_run",
     "mums_set_match_log", "mums_match_log_copy", "mums_shard_restart_pending", "mums_shard_stream",
-    "mums_shard_restart_plan", "mums_shard_restart_apply",
+    "mums_shard_restart_plan", "mums_shard_restart_apply", "mums_comm_init_host",
 ]
+
+# mums_comm_ops (include/mums.h): the caller's transport as two host callbacks
+COMM_ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint64,
+                                     ctypes.POINTER(ctypes.c_uint64))
+COMM_ALLTOALLV_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                                     ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64))
+
+
+class MumsCommOps(ctypes.Structure):
+    _fields_ = [("allgather_u64", COMM_ALLGATHER_FN), ("alltoallv", COMM_ALLTOALLV_FN)]
 
 _lib: Optional[ctypes.CDLL] = None
 
@@ -176,6 +186,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mums_comm_init_rank.argtypes = [ctypes.POINTER(vp), ctypes.c_int, ctypes.c_int, ctypes.c_int, vp]
     lib.mums_comm_init_all.argtypes = [ctypes.POINTER(vp), ctypes.c_int, vp]
     lib.mums_comm_init_local.argtypes = [ctypes.POINTER(vp), ctypes.c_int, vp]
+    lib.mums_comm_init_host.argtypes = [ctypes.POINTER(vp), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.POINTER(MumsCommOps), vp]
     lib.mums_comm_destroy.argtypes = [vp]
     lib.mums_comm_destroy.restype = None
     lib.mums_comm_last_error.argtypes = [vp]

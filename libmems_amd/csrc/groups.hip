@@ -373,18 +373,40 @@ template <int MG, typename View>
 __global__ __launch_bounds__(kBlock) void probe_materialize_kernel(View v, const uint64_t* __restrict__ probe_info,
                                                                    uint64_t P, GenomeTable gt, MatchParams mp, int L,
                                                                    int64_t* __restrict__ rows) {
-    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (k >= P) return;
-    const uint64_t info = probe_info[k];
-    const uint64_t h = info & 0xFFFFFFFFull;
+    const uint64_t k0 = (uint64_t)blockIdx.x * kBlock;
+    const uint64_t k = k0 + threadIdx.x;
+    const int W = gt.G + 1;
     Mhe<MG> Q;
-    uint32_t gs;
-    build_probe<MG, View>(v, h, h + ((info >> 32) & 0xFFFFull), gt, mp, L, Q, &gs);
-    int64_t* row = rows + k * (uint64_t)(gt.G + 1);
-    #pragma unroll
-    for (int g = 0; g < MG; ++g)
-        if (g < gt.G) row[g] = Q.s[g];
-    row[gt.G] = Q.offset;
+    if (k < P) {
+        const uint64_t info = probe_info[k];
+        const uint64_t h = info & 0xFFFFFFFFull;
+        uint32_t gs;
+        build_probe<MG, View>(v, h, h + ((info >> 32) & 0xFFFFull), gt, mp, L, Q, &gs);
+    }
+    if constexpr (MG <= 16) {
+        // the block's rows are one contiguous range: staged in LDS, stored with consecutive
+        // lanes on consecutive words (one lane per row would touch a 128-B line per lane and
+        // word: W x 64 lines per store instruction)
+        __shared__ int64_t srow[kBlock * (MG + 1)];
+        if (k < P) {
+            int64_t* r = srow + threadIdx.x * W;
+            #pragma unroll
+            for (int g = 0; g < MG; ++g)
+                if (g < gt.G) r[g] = Q.s[g];
+            r[gt.G] = Q.offset;
+        }
+        __syncthreads();
+        const uint64_t nk = P - k0 < (uint64_t)kBlock ? P - k0 : (uint64_t)kBlock;
+        int64_t* out = rows + k0 * (uint64_t)W;
+        for (uint32_t i = threadIdx.x; i < nk * (uint64_t)W; i += kBlock) out[i] = srow[i];
+    } else {
+        if (k >= P) return;
+        int64_t* row = rows + k * (uint64_t)W;
+        #pragma unroll
+        for (int g = 0; g < MG; ++g)
+            if (g < gt.G) row[g] = Q.s[g];
+        row[gt.G] = Q.offset;
+    }
 }
 
 // bucket (MemHash.cpp:213) of every row; dest = owning rank of that bucket when bounds

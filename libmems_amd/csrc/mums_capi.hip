@@ -93,6 +93,8 @@ struct mums_ctx {
     DevBuf bstart, bend, tsize, obase, pool, tbl, out_len, out_s, pbuf, keybuf, mstart;
     DevBuf chain_tmp, chain_of, radix_tmp, spill, summ, dbgbuf, mprobe, rowtmp;
     DevBuf fk, fkloc;        // each chain's first probe in key order (merged / per slice)
+    DevBuf side, bst8;       // keys wider than 32 + 8 bits: side bytes, 8-bit bucket starts (msdsplit.hip)
+    DevBuf cbst;             // chunked mode, w20-21: every chunk's bucket starts after the split
     bool use_onesweep = true;
     // ParallelMemHash chunk-compat mode (compat.hip): chunk = CHUNK_SIZE, ParallelMemHash.cpp:51
     bool pcompat = false;
@@ -600,12 +602,30 @@ uint32_t layout_packed(GenomeTable& t, uint64_t* words) {
 // bases are GLOBAL seed-mer indices), histogram the top B key bits per tile, then scatter
 // the (ckey_low << 32 | global index) records stably into their MSD buckets in out.
 // Bucket starts -> bstart[0 .. 2^B] (device).
+// side > 0 (keys wider than 32 + 8 bits, w20-21): the scatter runs on the top 8 bits into
+// scratch (ctx->recB) with the next `side` key bits in ctx->side, and msd_split partitions
+// the 256 buckets into the 2^B buckets of out.
 int keys_stage(mums_ctx* ctx, const GenomeTable& lgt, uint32_t T, int B, uint64_t n, uint64_t* out, uint32_t* bstart,
-               hipStream_t st, int ib = 32) {
+               hipStream_t st, int ib = 32, int side = 0) {
     DevCounters* dc = ctx->counters.as<DevCounters>();
     std::vector<const char*> ptrs(lgt.G);
     for (int g = 0; g < lgt.G; ++g) ptrs[g] = ctx->genomes[g].d_ptr;
     uint32_t* hist = ctx->hist.as<uint32_t>();
+    if (side > 0) {
+        if (ib != 32 || B != 8 + side || out == ctx->recB.as<uint64_t>()) return fail(ctx, MUMS_E_INVALID, "msd split");
+        HIPCHK(ctx->side.ensure(n + 64));
+        HIPCHK(ctx->bst8.ensure((256 + 64) * 4));
+        HIPCHK(ctx->tmp.ensure(std::max(ctx->tmp.cap, msd_split_tmp_bytes(n, 8))));
+        HIPCHK(launch_seed_pack(ctx->ss, lgt, ptrs.data(), ctx->packed.as<uint32_t>(), 1, true, nullptr, 8, hist, T,
+                                &dc->err, st));
+        HIPCHK(exclusive_scan_u32(hist, (uint64_t)T << 8, ctx->tmp.p, nullptr, st));
+        HIPCHK(launch_seed_scatter(ctx->ss, lgt, ctx->packed.as<uint32_t>(), 8, hist, T, ctx->recB.as<uint64_t>(), st,
+                                   ctx->side.as<uint8_t>(), side));
+        HIPCHK(seg_bucket_starts(hist, T, 8, n, ctx->bst8.as<uint32_t>(), st));
+        HIPCHK(msd_split(ctx->recB.as<uint64_t>(), ctx->side.as<uint8_t>(), out, n, 8, side, ctx->bst8.as<uint32_t>(),
+                         bstart, ctx->tmp.p, st));
+        return MUMS_OK;
+    }
     HIPCHK(launch_seed_pack(ctx->ss, lgt, ptrs.data(), ctx->packed.as<uint32_t>(), 1, true, nullptr, B, hist, T,
                             &dc->err, st));
     if (B > 0) HIPCHK(exclusive_scan_u32(hist, (uint64_t)T << B, ctx->tmp.p, nullptr, st));
@@ -998,6 +1018,10 @@ int run_pipeline(mums_ctx* ctx, int stage) {
     if (const char* e = getenv("MUMS_DEV_MSD_BITS"))   // development knob (sort layout experiments)
         if (ctx->packed_path) ctx->msd_bits = std::min(kMaxMsdBits, std::max(ctx->msd_bits, atoi(e)));
     const int B = ctx->msd_bits;
+    // keys wider than 32 + 8 bits: an 8-bit scatter + side bytes + msd_split (msdsplit.hip)
+    // instead of a 2^B-digit scatter (write runs of ~2 records per tile at w21)
+    const int side = (ctx->packed_path && B > 8 && !getenv("MUMS_DEV_MSD_BITS") && !getenv("MUMS_DEV_NO_SPLIT"))
+                         ? B - 8 : 0;
     const size_t kb = ctx->key64 ? 8 : 4;
     ProbeSpace ps{};
     if (ctx->packed_path) {
@@ -1029,7 +1053,7 @@ int run_pipeline(mums_ctx* ctx, int stage) {
 
     int rc = MUMS_OK;
     if (ctx->packed_path) {
-        rc = keys_stage(ctx, gt, T, B, N, ctx->recA.as<uint64_t>(), ctx->mstart.as<uint32_t>(), st);
+        rc = keys_stage(ctx, gt, T, B, N, ctx->recA.as<uint64_t>(), ctx->mstart.as<uint32_t>(), st, 32, side);
         if (rc) return rc;
         HIPCHK(hipEventRecord(ctx->ev[EV_KEYS], st));
         rc = merge_stage(ctx, N, B, kbits - B, mp, ps, st);
@@ -2718,8 +2742,8 @@ int stream_restart(mums_ctx* ctx, uint64_t* srec, uint64_t* other, const std::ve
 // The chunked mode's restart (all chunks resident and sorted in buffer sbuf): live chunks
 // into the other buffer (*live_rec), n_live[c], the chunks' bucket starts in ctx->rsbst.
 int chunked_restart(mums_ctx* ctx, int sbuf, const std::vector<uint64_t>& dstart, const std::vector<uint64_t>& cbase,
-                    uint32_t* hist, uint32_t T, uint32_t nbc, int mb, uint32_t nch, std::vector<uint64_t>& n_live,
-                    uint64_t** live_rec, hipStream_t st) {
+                    uint32_t nbc, uint32_t nch, std::vector<uint64_t>& n_live, uint64_t** live_rec,
+                    const std::function<int(uint32_t, uint64_t, uint32_t*)>& chunk_starts, hipStream_t st) {
     uint64_t* srec = sbuf ? ctx->recB.as<uint64_t>() : ctx->recA.as<uint64_t>();
     uint64_t* other = sbuf ? ctx->recA.as<uint64_t>() : ctx->recB.as<uint64_t>();
     *live_rec = nullptr;
@@ -2728,8 +2752,7 @@ int chunked_restart(mums_ctx* ctx, int sbuf, const std::vector<uint64_t>& dstart
     HIPCHK(ctx->rsbst.ensure((uint64_t)nch * (nbc + 1) * 4 + 64));
     bool live = false;
     const int rc = stream_restart(ctx, srec, other, dstart, 31, 33, segs, [&](uint32_t c, uint32_t* d) -> int {
-        HIPCHK(seg_bucket_starts(mb > 0 ? hist + (uint64_t)c * nbc * T : nullptr, T, mb, cbase[c + 1] - cbase[c], d, st));
-        return MUMS_OK;
+        return chunk_starts(c, cbase[c + 1] - cbase[c], d);
     }, ctx->rsbst.as<uint32_t>(), n_live, &live, st);
     if (rc) return rc;
     if (live) *live_rec = other;
@@ -2743,16 +2766,21 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
     MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, ctx->masked, ctx->seq_mask};
     GenomeTable& gt = ctx->gt;
     const int kbits = 2 * ctx->w + 1;
-    const int B = kbits - 31;   // MSD digit bits: the record keeps 31 key bits + 33 index bits
-    if (B < 1 || B > 8)
-        return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed-mers (chunked mode) needs seed weight 16-19");
+    // implicit digit bits: the record keeps 31 key bits + 33 index bits.  Above 8 of them
+    // (w20-21, the default seed of genomes above ~1.07 Gbp) the scatter splits by the top 8
+    // and keeps the next S in side bytes; msd_split refines every chunk (msdsplit.hip).
+    const int Bt = kbits - 31;
+    const int S = Bt > 8 ? Bt - 8 : 0;
+    const int B = Bt - S;       // scatter (MSD) digit bits
+    if (Bt < 1 || Bt > 12)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed-mers (chunked mode) needs seed weight 16-21");
     if (N >= (1ull << 33)) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^33 seed-mers per context");
     if (wants_tie_order(ctx))   // the first copies of a genome follow its SML's std::sort order (smlsort.hip)
         return fail(ctx, MUMS_E_UNSUPPORTED, "repeat tolerance above 2^32 seed-mers (chunked mode): the SortedMerList "
                                              "tie order is replayed in a single context only");
     ctx->packed_path = true;
     ctx->key64 = true;
-    ctx->msd_bits = B;
+    ctx->msd_bits = Bt;
     ctx->parity_masked = false;
     uint64_t words = 0;
     const uint32_t T = layout_packed(gt, &words);
@@ -2794,18 +2822,21 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
         if (ok) break;
     }
     if (cb > B) return fail(ctx, MUMS_E_UNSUPPORTED, "chunked mode: one MSD digit holds more seed-mers than a chunk (2^30)");
-    const int mb = B - cb;
-    const uint32_t nbc = 1u << mb, nch = 1u << cb;
+    const int mb8 = B - cb;                               // scatter digits per chunk: 2^mb8
+    const uint32_t nbc8 = 1u << mb8, nch = 1u << cb;
+    const int mb = mb8 + S;                               // sort buckets per chunk (after the split)
+    const uint32_t nbc = 1u << mb;
     uint64_t nmax = 0;
     for (uint32_t c = 0; c < nch; ++c) {
         uint64_t sum = 0;
-        for (uint32_t d = c * nbc; d < (c + 1) * nbc; ++d) sum += tot[d];
+        for (uint32_t d = c * nbc8; d < (c + 1) * nbc8; ++d) sum += tot[d];
         nmax = std::max(nmax, sum);
     }
     ProbeSpace ps{};
     int rc = ensure_merge_space(ctx, nmax + 1, mb, 31, &ps);
     if (rc) return rc;
-    HIPCHK(ctx->tmp.ensure(std::max(ctx->tmp.cap, scan_tmp_bytes((uint64_t)nbc * T + 1))));
+    HIPCHK(ctx->tmp.ensure(std::max(ctx->tmp.cap, scan_tmp_bytes((uint64_t)nbc8 * T + 1))));
+    if (S) HIPCHK(ctx->tmp.ensure(std::max(ctx->tmp.cap, msd_split_tmp_bytes(nmax + 1, mb8))));
     // resident layout (the 288 GB of HBM hold all 2 x N records): every chunk's slice of
     // the MSD histogram scanned on its own, ONE scatter of all records to their chunk
     // (64-bit chunk bases), then each chunk sorted / grouped in place.  Otherwise (or
@@ -2814,15 +2845,19 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
     std::vector<uint64_t> cbase(nch + 1, 0);
     for (uint32_t c = 0; c < nch; ++c) {
         uint64_t sum = 0;
-        for (uint32_t d = c * nbc; d < (c + 1) * nbc; ++d) sum += tot[d];
+        for (uint32_t d = c * nbc8; d < (c + 1) * nbc8; ++d) sum += tot[d];
         cbase[c + 1] = cbase[c] + sum;
     }
     bool resident = getenv("MUMS_DEV_CHUNK_STREAM") == nullptr;
+    if (S && !resident)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "seed weight 20-21 in the chunked mode needs the resident layout");
     if (resident) {
         size_t fr = 0, total_mem = 0;
         HIPCHK(hipMemGetInfo(&fr, &total_mem));
-        const uint64_t need = 2 * (N + 64) * 8;
-        resident = need + (uint64_t)(1ull << 30) < (uint64_t)fr + ctx->recA.cap + ctx->recB.cap;
+        const uint64_t need = 2 * (N + 64) * 8 + (S ? N + 64 : 0);
+        resident = need + (uint64_t)(1ull << 30) < (uint64_t)fr + ctx->recA.cap + ctx->recB.cap + ctx->side.cap;
+        if (S && !resident)
+            return fail(ctx, MUMS_E_NOMEM, "seed weight 20-21 in the chunked mode: records and side bytes do not fit");
     }
     if (resident) {
         HIPCHK(ctx->recA.ensure((N + 64) * 8));
@@ -2831,10 +2866,23 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
         uint64_t* d_cbase = ctx->ctab.as<uint64_t>() + nd;
         HIPCHK(hipMemcpyAsync(d_cbase, cbase.data(), nch * 8, hipMemcpyHostToDevice, st));
         for (uint32_t c = 0; c < nch; ++c)
-            HIPCHK(exclusive_scan_u32(hist + (uint64_t)c * nbc * T, (uint64_t)nbc * T, ctx->tmp.p, nullptr, st));
+            HIPCHK(exclusive_scan_u32(hist + (uint64_t)c * nbc8 * T, (uint64_t)nbc8 * T, ctx->tmp.p, nullptr, st));
+        if (S) {
+            HIPCHK(ctx->side.ensure(N + 64));
+            HIPCHK(ctx->cbst.ensure((uint64_t)nch * (nbc + 1) * 4 + (nbc8 + 64) * 4 + 64));
+        }
         HIPCHK(launch_seed_scatter_chunk(ctx->ss, gt, ctx->packed.as<uint32_t>(), B, hist, T, 0, 0,
-                                         ctx->recA.as<uint64_t>(), st, d_cbase, mb));
+                                         ctx->recA.as<uint64_t>(), st, d_cbase, mb8, S ? ctx->side.as<uint8_t>() : nullptr,
+                                         S));
     }
+    // the sort buckets of chunk c: from its slice of the MSD histogram, or (S > 0) the split's
+    // starts kept in ctx->cbst
+    uint32_t* cbst = S ? ctx->cbst.as<uint32_t>() : nullptr;
+    auto chunk_starts = [&](uint32_t c, uint64_t n_c, uint32_t* d) -> int {
+        if (S) HIPCHK(hipMemcpyAsync(d, cbst + (uint64_t)c * (nbc + 1), (nbc + 1) * 4ull, hipMemcpyDeviceToDevice, st));
+        else HIPCHK(seg_bucket_starts(mb > 0 ? hist + (uint64_t)c * nbc * T : nullptr, T, mb, n_c, d, st));
+        return MUMS_OK;
+    };
     uint64_t P_total = 0, groups = 0;
     double ms_sort = 0, ms_groups = 0, ms_buckets = 0, ms_dom = 0;
     uint64_t dom_bytes = 0, dom_launches = 0;
@@ -2853,20 +2901,31 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
     std::vector<uint64_t> n_live(nch, 0);
     DevBuf& lbst = ctx->rsbst;               // per chunk: compacted bucket starts (nbc + 1)
     for (uint32_t c = 0; c < nch && resident; ++c) {
-        const uint32_t dlo = c * nbc;
+        const uint32_t dlo = c * nbc8;
         uint64_t n_c = 0;
-        for (uint32_t d = dlo; d < dlo + nbc; ++d) n_c += tot[d];
-        if (n_c == 0) continue;
-        uint32_t* slice = hist + (uint64_t)dlo * T;
+        for (uint32_t d = dlo; d < dlo + nbc8; ++d) n_c += tot[d];
         uint64_t* rA = ctx->recA.as<uint64_t>() + cbase[c];
         uint64_t* rB = ctx->recB.as<uint64_t>() + cbase[c];
-        HIPCHK(hipEventRecord(ctx->ev[EV_CHAINS], st));
         uint32_t* bstart = ctx->mstart.as<uint32_t>();
-        HIPCHK(seg_bucket_starts(mb > 0 ? slice : nullptr, T, mb, n_c, bstart, st));
+        if (S) {   // chunk c's 2^mb8 scatter buckets split by the side digits: rA -> rB
+            uint32_t* bst8 = ctx->cbst.as<uint32_t>() + (uint64_t)nch * (nbc + 1);
+            uint32_t* out = cbst + (uint64_t)c * (nbc + 1);
+            HIPCHK(seg_bucket_starts(mb8 > 0 ? hist + (uint64_t)dlo * T : nullptr, T, mb8, n_c, bst8, st));
+            if (n_c) HIPCHK(msd_split(rA, ctx->side.as<uint8_t>() + cbase[c], rB, n_c, mb8, S, bst8, out, ctx->tmp.p, st));
+            else HIPCHK(hipMemsetAsync(out, 0, (nbc + 1) * 4ull, st));
+        }
+        if (n_c == 0) continue;
+        HIPCHK(hipEventRecord(ctx->ev[EV_CHAINS], st));
+        rc = chunk_starts(c, n_c, bstart);
+        if (rc) return rc;
         SegTile* tiles = ctx->tiles.as<SegTile>();
         HIPCHK(build_seg_tiles_from_starts(bstart, mb, n_c, tiles, &dc->ntiles, ctx->tmp.p, st));
-        HIPCHK(seg_onesweep_sort(rA, rB, n_c, 31, mb, bstart, ctx->tmp.p, &dc->err, &sbuf, st,
+        // the sort reads the split's output (rB) when S > 0; sbuf names the buffer holding
+        // the sorted chunk (0: recA, 1: recB) either way
+        int sb = 0;
+        HIPCHK(seg_onesweep_sort(S ? rB : rA, S ? rA : rB, n_c, 31, mb, bstart, ctx->tmp.p, &dc->err, &sb, st,
                                  prof ? ctx->ev_ds : nullptr, 33, mp.repeat_tol == 0 && mp.enum_tol == 1));
+        sbuf = S ? 1 - sb : sb;
         HIPCHK(hipEventRecord(ctx->ev[EV_SORT], st));
         HIPCHK(hipEventSynchronize(ctx->ev[EV_SORT]));
         ms_sort += el(EV_CHAINS, EV_SORT);
@@ -2882,15 +2941,25 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
     if (!resident && have_start_points(ctx))
         return fail(ctx, MUMS_E_UNSUPPORTED, "start points in the chunked mode without resident records");
     if (resident) {
-        std::vector<uint64_t> dstart(nd + 1, 0);
-        for (uint32_t d = 0; d < nd; ++d) dstart[d + 1] = dstart[d] + tot[d];
-        rc = chunked_restart(ctx, sbuf, dstart, cbase, hist, T, nbc, mb, nch, n_live, &live_rec, st);
+        // global starts of the 2^Bt implicit digits (the restart's full keys)
+        std::vector<uint64_t> dstart((1ull << Bt) + 1, 0);
+        if (S) {
+            std::vector<uint32_t> hb((uint64_t)nch * (nbc + 1));
+            HIPCHK(hipMemcpyAsync(hb.data(), cbst, hb.size() * 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            for (uint32_t c = 0; c < nch; ++c)
+                for (uint32_t j = 0; j < nbc; ++j) dstart[(uint64_t)c * nbc + j] = cbase[c] + hb[(uint64_t)c * (nbc + 1) + j];
+            dstart[1ull << Bt] = N;
+        } else {
+            for (uint32_t d = 0; d < nd; ++d) dstart[d + 1] = dstart[d] + tot[d];
+        }
+        rc = chunked_restart(ctx, sbuf, dstart, cbase, nbc, nch, n_live, &live_rec, chunk_starts, st);
         if (rc) return rc;
     }
     for (uint32_t c = 0; c < nch; ++c) {
-        const uint32_t dlo = c * nbc;
+        const uint32_t dlo = c * nbc8;
         uint64_t n_c = 0;
-        for (uint32_t d = dlo; d < dlo + nbc; ++d) n_c += tot[d];
+        for (uint32_t d = dlo; d < dlo + nbc8; ++d) n_c += tot[d];
         if (n_c == 0) continue;
         uint32_t* slice = hist + (uint64_t)dlo * T;
         const uint64_t o = resident ? cbase[c] : 0;
@@ -2899,15 +2968,16 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
         HIPCHK(hipEventRecord(ctx->ev[EV_CHAINS], st));   // chunk start (scatter counts as sort)
         uint32_t* bstart = ctx->mstart.as<uint32_t>();
         if (!resident) {
-            HIPCHK(exclusive_scan_u32(slice, (uint64_t)nbc * T, ctx->tmp.p, nullptr, st));
-            HIPCHK(launch_seed_scatter_chunk(ctx->ss, gt, ctx->packed.as<uint32_t>(), B, slice, T, dlo, nbc, rA, st));
+            HIPCHK(exclusive_scan_u32(slice, (uint64_t)nbc8 * T, ctx->tmp.p, nullptr, st));
+            HIPCHK(launch_seed_scatter_chunk(ctx->ss, gt, ctx->packed.as<uint32_t>(), B, slice, T, dlo, nbc8, rA, st));
         }
         if (live_rec) {   // the chunk's live records after the restarts
             n_c = n_live[c];
             HIPCHK(hipMemcpyAsync(bstart, lbst.as<uint32_t>() + (uint64_t)c * (nbc + 1), (nbc + 1) * 4ull,
                                   hipMemcpyDeviceToDevice, st));
         } else {
-            HIPCHK(seg_bucket_starts(mb > 0 ? slice : nullptr, T, mb, n_c, bstart, st));
+            rc = chunk_starts(c, n_c, bstart);
+            if (rc) return rc;
         }
         SegTile* tiles = ctx->tiles.as<SegTile>();
         const uint64_t ub = seg_tiles_upper(n_c, mb);

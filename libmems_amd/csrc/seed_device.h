@@ -116,6 +116,7 @@ __device__ __forceinline__ uint32_t ckey_top_static(uint64_t mer) {
 // the patterns with compiled-in run tables (getSeed(15), getSeed(19): SeedMasks.h)
 constexpr uint64_t kSeedW15 = 0x7ac9afull;
 constexpr uint64_t kSeedW19 = 0x7b974efull;
+constexpr uint64_t kSeedW21 = 0x7ddaddfull;   // getSeed(21): default weight of genomes above ~1.07 Gbp
 
 __device__ __forceinline__ uint64_t window_at(const uint32_t* __restrict__ W, uint64_t p) {
     const uint64_t wi = p >> 4;

@@ -125,7 +125,10 @@ __global__ __launch_bounds__(kBlock) void seed_pack_kernel(SeedSpec ss, GenomeTa
     const uint64_t base = gt.base[g];
     const int klow = 2 * ss.w + 1 - msd_bits;
     if constexpr (kMode == 1 && PAT != 0 && kStaticMsd<PAT> >= 1 && kStaticMsd<PAT> <= kMaxMsdBits) {
-        if (msd_bits == kStaticMsd<PAT>) {   // the default split: top digit only
+        // the default split: top digit only; keys wider than 32 + 8 bits split by their top
+        // 8 bits first (msdsplit.hip)
+        constexpr int kTop = kStaticMsd<PAT> > 8 ? 8 : kStaticMsd<PAT>;
+        if (msd_bits == kTop) {
             #pragma unroll 4
             for (int j = 0; j < kPerThread; ++j) {
                 const int q = tid + j * kBlock;
@@ -134,7 +137,7 @@ __global__ __launch_bounds__(kBlock) void seed_pack_kernel(SeedSpec ss, GenomeTa
                 const int wi = q >> 4, sh = 2 * (q & 15);
                 const uint64_t hi = ((uint64_t)words[wi] << 32) | words[wi + 1];
                 const uint64_t lo = words[wi + 2];
-                atomicAdd(&bh[ckey_top_static<PAT, kStaticMsd<PAT>>((hi << sh) | ((lo << sh) >> 32))], 1u);
+                atomicAdd(&bh[ckey_top_static<PAT, kTop>((hi << sh) | ((lo << sh) >> 32))], 1u);
             }
             __syncthreads();
             for (int i = tid; i < nb; i += kBlock) hist[(uint64_t)i * T + t] = bh[i];
@@ -167,19 +170,23 @@ __global__ __launch_bounds__(kBlock) void seed_pack_kernel(SeedSpec ss, GenomeTa
 // cannot reach it: its LDS alone allows two blocks per CU)
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Wpass-failed"
-template <int kMaxDig, uint64_t PAT = 0, int IB = 32, bool kChunk = false>
+// kSide: the key has side_bits (<= 4) bits between the record's 64 - IB key bits and the
+// msd_bits MSD digit; they go to side[] at the record's position (msdsplit.hip splits the
+// buckets by them)
+template <int kMaxDig, uint64_t PAT = 0, int IB = 32, bool kChunk = false, int kSide = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void seed_scatter_kernel(SeedSpec ss, GenomeTable gt,
                                                               const uint32_t* __restrict__ packed, int msd_bits,
                                                               const uint32_t* __restrict__ hist, uint32_t T,
                                                               uint64_t* __restrict__ rec, uint32_t dlo = 0,
                                                               uint32_t nbc = 0,
                                                               const uint64_t* __restrict__ cbase = nullptr,
-                                                              int mb = 0) {
+                                                              int mb = 0, uint8_t* __restrict__ side = nullptr,
+                                                              int side_bits = 0) {
     // LDS (<= 40 KB at kMaxDig 256, four blocks per CU): the packed words alias the
     // record staging area (read only before the records are placed), wave digit
     // offsets are 16-bit (<= kTile) and fold in the block-local digit starts, and gofs
     // folds in minus those starts (u32 arithmetic: the sum is < 2^32).
-    using DigT = typename std::conditional<(kMaxDig <= 256), uint8_t, uint16_t>::type;
+    using DigT = typename std::conditional<(kMaxDig <= 256 && kSide == 0), uint8_t, uint16_t>::type;
     __shared__ uint64_t srec[kTile];
     __shared__ DigT sdig[kTile];
     __shared__ uint16_t wcnt[kWaves][kMaxDig];
@@ -200,7 +207,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     const int nd = (kChunk && !all_chunks) ? (int)nbc : (1 << msd_bits);
     if (kChunk && tid == 0) s_kept = 0;
     const int klow = 2 * ss.w + 1 - msd_bits;
-    const uint64_t lmask = (klow >= 64) ? ~0ull : ((1ull << klow) - 1);   // klow <= 64 - IB
+    const uint64_t lmask = (klow >= 64) ? ~0ull : ((1ull << klow) - 1);   // klow <= 64 - IB + kSide
     const uint64_t pw = packed_words(gt.n[g]);
     const uint32_t* W = packed + gt.woff[g];
     for (int k = tid; k < kTileWords; k += kBlock) {
@@ -230,7 +237,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             valid = valid && d < nbc;
             d = valid ? d : 0u;
         }
-        r_key[r] = (uint32_t)(kv & lmask);
+        r_key[r] = (uint32_t)(kv & lmask);   // the record keeps the low 64 - IB bits
         uint32_t tot;
         // digits are < 2^msd_bits <= kMaxDig: the unused high bits rank as equal
         const uint32_t rk = wave_match_rank<(kMaxDig > 256 ? kMaxMsdBits : 8)>(d, valid, &tot);
@@ -238,6 +245,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         if (valid) old = wcnt[wv][d];
         if (valid && rk == 0) wcnt[wv][d] = (uint16_t)(old + tot);
         r_pk[r] = valid ? (((old + rk) << 16) | d) : 0xFFFFFFFFu;
+        if constexpr (kSide > 0)   // rank < 2^12: bits 28-31 are free (d < 256 here)
+            if (valid) r_pk[r] |= ((uint32_t)(kv >> (64 - IB)) & ((1u << side_bits) - 1)) << 28;
     }
     __syncthreads();
     // per-digit wave offsets + block-local digit starts (each thread owns nd/256 digits)
@@ -285,9 +294,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         const uint32_t pk = r_pk[r];
         if (pk != 0xFFFFFFFFu) {
             const uint32_t d = pk & 0xFFFFu;
-            const uint32_t lp = (uint32_t)wcnt[wv][d] + (pk >> 16);
+            const uint32_t lp = (uint32_t)wcnt[wv][d] + ((pk >> 16) & (kSide > 0 ? 0xFFFu : 0xFFFFu));
             srec[lp] = ((uint64_t)r_key[r] << IB) | (base + p0 + (uint64_t)(q0 + r * 64 + lane));
-            sdig[lp] = (DigT)d;
+            sdig[lp] = (DigT)(kSide > 0 ? (d | ((pk >> 28) << 8)) : d);   // + the side digit
         }
     }
     __syncthreads();
@@ -296,9 +305,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     for (int r = 0; r < kPerThread; ++r) {
         const uint32_t s = tid + r * kBlock;
         if (s < cnt) {
-            const uint32_t d = sdig[s];
+            const uint32_t dd = sdig[s];
+            const uint32_t d = kSide > 0 ? (dd & 0xFFu) : dd;
             const uint64_t b = (kChunk && all_chunks) ? cbase[d >> mb] : 0ull;
-            rec[b + (uint64_t)(uint32_t)(gofs[d] + s)] = srec[s];
+            const uint64_t o = b + (uint64_t)(uint32_t)(gofs[d] + s);
+            rec[o] = srec[s];
+            if constexpr (kSide > 0) side[o] = (uint8_t)(dd >> 8);   // run order, like the records
         }
     }
 }
@@ -356,6 +368,7 @@ __global__ void keys_of_genome_kernel(SeedSpec ss, const uint32_t* __restrict__ 
 constexpr uint64_t kStaticSeeds[] = {kSeedW19, kSeedW15};
 #else
 constexpr uint64_t kStaticSeeds[] = {
+    kSeedW21,                                             // w21 (3 Gbp genomes' default)
     kSeedW19, 0x7d6735full, 0x1edd74full,                 // w19
     0x3E6B59Full, 0x3EB335Full, 0x7B3566Full,             // w18
     0x6dbedbull,                                          // w17
@@ -407,8 +420,24 @@ hipError_t launch_seed_pack(const SeedSpec& ss, const GenomeTable& gt, const cha
 }
 
 hipError_t launch_seed_scatter(const SeedSpec& ss, const GenomeTable& gt, const uint32_t* d_packed, int msd_bits,
-                               const uint32_t* d_hist_scanned, uint32_t ntiles, uint64_t* d_rec, hipStream_t st) {
+                               const uint32_t* d_hist_scanned, uint32_t ntiles, uint64_t* d_rec, hipStream_t st,
+                               uint8_t* d_side, int side_bits) {
     if (ntiles == 0) return hipSuccess;
+    if (side_bits > 0) {   // 8 MSD bits + side_bits in side[] (msdsplit.hip)
+        if (msd_bits != 8 || side_bits > 4 || 2 * ss.w + 1 != 32 + 8 + side_bits) return hipErrorInvalidValue;
+        with_static_seed(ss.pattern, [&](auto pc) {
+            constexpr uint64_t PAT = decltype(pc)::value;
+            if constexpr (PAT == 0 || 2 * seed_runs(PAT).w + 1 > 40)
+                hipLaunchKernelGGL((seed_scatter_kernel<256, PAT, 32, false, 1>), dim3(ntiles), dim3(kBlock), 0, st,
+                                   ss, gt, d_packed, msd_bits, d_hist_scanned, ntiles, d_rec, 0u, 0u,
+                                   (const uint64_t*)nullptr, 0, d_side, side_bits);
+            else
+                hipLaunchKernelGGL((seed_scatter_kernel<256, 0, 32, false, 1>), dim3(ntiles), dim3(kBlock), 0, st,
+                                   ss, gt, d_packed, msd_bits, d_hist_scanned, ntiles, d_rec, 0u, 0u,
+                                   (const uint64_t*)nullptr, 0, d_side, side_bits);
+        });
+        return hipGetLastError();
+    }
     if (msd_bits > 8) {
         hipLaunchKernelGGL((seed_scatter_kernel<(1 << kMaxMsdBits), 0>), dim3(ntiles), dim3(kBlock), 0, st, ss, gt,
                            d_packed, msd_bits, d_hist_scanned, ntiles, d_rec);
@@ -430,8 +459,22 @@ hipError_t launch_seed_scatter(const SeedSpec& ss, const GenomeTable& gt, const 
 // (requires 2w+1 - msd_bits == 31); hist_slice = the scanned histogram rows of those digits
 hipError_t launch_seed_scatter_chunk(const SeedSpec& ss, const GenomeTable& gt, const uint32_t* d_packed, int msd_bits,
                                      const uint32_t* d_hist_slice, uint32_t ntiles, uint32_t dlo, uint32_t nbc,
-                                     uint64_t* d_rec, hipStream_t st, const uint64_t* d_cbase, int mb) {
+                                     uint64_t* d_rec, hipStream_t st, const uint64_t* d_cbase, int mb, uint8_t* d_side,
+                                     int side_bits) {
     if (ntiles == 0) return hipSuccess;
+    if (side_bits > 0) {   // w20-21: 8 MSD bits + side_bits in side[] (msdsplit.hip), every chunk at once
+        if (msd_bits != 8 || side_bits > 4 || 2 * ss.w + 1 != 31 + 8 + side_bits || !d_cbase)
+            return hipErrorInvalidValue;
+        const uint64_t pat = ss.pattern == kSeedW21 ? ss.pattern : 0;
+        with_static_seed(pat, [&](auto pc) {
+            constexpr uint64_t PAT = decltype(pc)::value;
+            if constexpr (PAT == 0 || PAT == kSeedW21)
+                hipLaunchKernelGGL((seed_scatter_kernel<256, PAT, 33, true, 1>), dim3(ntiles), dim3(kBlock), 0, st,
+                                   ss, gt, d_packed, msd_bits, d_hist_slice, ntiles, d_rec, dlo, nbc, d_cbase, mb,
+                                   d_side, side_bits);
+        });
+        return hipGetLastError();
+    }
     if (2 * ss.w + 1 - msd_bits != 64 - 33 || msd_bits > 8 || (nbc == 0 && !d_cbase)) return hipErrorInvalidValue;
     // chunked contexts hold > 2^32 seed-mers: w 16-19 (compiled-in tables for the w19 seeds)
     const uint64_t pat = (ss.pattern == kSeedW19 || ss.pattern == 0x7d6735full || ss.pattern == 0x1edd74full)

@@ -17,8 +17,9 @@
 //   8. find     : mums_shard_find -> this rank's buckets of the bucket-major MatchList.
 // Communicators: RCCL (ncclCommInitRank for one process per GPU, ncclCommInitAll for one
 // process driving several GPUs from one thread per device; all-to-allv = grouped
-// ncclSend/ncclRecv over xGMI) or an in-process host-staged communicator for ranks that
-// are threads of one process (tests of the orchestration on a single GPU).
+// ncclSend/ncclRecv over xGMI), an in-process host-staged communicator for ranks that
+// are threads of one process (tests of the orchestration on a single GPU), or the
+// caller's own transport through two host callbacks (mums_comm_init_host: MPI, gloo, ...).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -29,6 +30,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -175,6 +177,38 @@ struct LocalComm : mums_comm {
         }
         sh->barrier();   // sources stay valid until every rank has copied
         return rc;
+    }
+};
+
+// ---- the caller's transport (mums_comm_ops), host-staged ------------------------------
+// Every collective of mums_shard_run goes through two host callbacks, so a caller whose
+// ranks already talk over MPI, gloo or a job launcher's sockets runs the sharded pipeline
+// without RCCL (and ranks that are processes sharing one GPU can run it: RCCL refuses two
+// ranks on one device).
+struct HostComm : mums_comm {
+    mums_comm_ops ops{};
+    void* user = nullptr;
+    std::vector<char> hs, hr;   // host staging of the all-to-allv
+    int allgather_u64(const uint64_t* send, size_t n, uint64_t* recv, hipStream_t) override {
+        if (ops.allgather_u64(user, send, n, recv) != 0) return comm_fail(this, "host allgather callback failed");
+        return MUMS_OK;
+    }
+    int alltoallv(const void* d_send, const uint64_t* sb, void* d_recv, const uint64_t* rb, hipStream_t st) override {
+        const std::vector<uint64_t> soff = block_offsets(sb, world), roff = block_offsets(rb, world);
+        if (sb[rank] != rb[rank]) return comm_fail(this, "alltoallv: self counts differ");
+        try {
+            hs.resize(soff[world] + 1);
+            hr.resize(roff[world] + 1);
+        } catch (const std::bad_alloc&) {
+            return comm_fail(this, "alltoallv: host staging allocation");
+        }
+        if (hipStreamSynchronize(st) != hipSuccess ||
+            (soff[world] && hipMemcpy(hs.data(), d_send, soff[world], hipMemcpyDeviceToHost) != hipSuccess))
+            return comm_fail(this, "alltoallv D2H");
+        if (ops.alltoallv(user, hs.data(), sb, hr.data(), rb) != 0) return comm_fail(this, "host alltoallv callback failed");
+        if (roff[world] && hipMemcpy(d_recv, hr.data(), roff[world], hipMemcpyHostToDevice) != hipSuccess)
+            return comm_fail(this, "alltoallv H2D");
+        return MUMS_OK;
     }
 };
 
@@ -346,6 +380,19 @@ int mums_comm_init_local(mums_comm** out, int nranks, const int* devices) {
         c->sh = sh;
         out[r] = c;
     }
+    return MUMS_OK;
+}
+
+int mums_comm_init_host(mums_comm** out, int device, int world, int rank, const mums_comm_ops* ops, void* user) {
+    if (!out || !ops || !ops->allgather_u64 || !ops->alltoallv || world < 1 || rank < 0 || rank >= world)
+        return MUMS_E_INVALID;
+    auto* c = new HostComm();
+    c->world = world;
+    c->rank = rank;
+    c->device = device;
+    c->ops = *ops;
+    c->user = user;
+    *out = c;
     return MUMS_OK;
 }
 

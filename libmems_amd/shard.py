@@ -303,18 +303,66 @@ class ShardedFindMatches:
         return full
 
 
+def host_comm_ops(group: Optional[dist.ProcessGroup] = None):
+    """mums_comm_ops over torch.distributed on host tensors (gloo): the C ABI stages device
+    data through host memory and calls these for its all-gather and all-to-allv.  Returns
+    the ops struct (keep it alive as long as the communicator)."""
+    import libmems_amd as lm
+
+    world = dist.get_world_size(group)
+
+    def allgather(_user, send, n, recv):
+        try:
+            src = torch.from_numpy(np.ctypeslib.as_array(send, shape=(n,)).astype(np.int64))
+            outs = [torch.empty(n, dtype=torch.int64) for _ in range(world)]
+            dist.all_gather(outs, src, group=group)
+            dst = np.ctypeslib.as_array(recv, shape=(world * n,))
+            for r in range(world):
+                dst[r * n:(r + 1) * n] = outs[r].numpy().view(np.uint64)
+            return 0
+        except Exception:   # a failed collective is reported through the status code
+            return 1
+
+    def alltoallv(_user, send, send_bytes, recv, recv_bytes):
+        try:
+            sb = [int(send_bytes[p]) for p in range(world)]
+            rb = [int(recv_bytes[p]) for p in range(world)]
+            src = torch.frombuffer((ctypes.c_char * max(sum(sb), 1)).from_address(send), dtype=torch.uint8)[:sum(sb)]
+            out = torch.empty(sum(rb), dtype=torch.uint8)
+            dist.all_to_all_single(out, src.clone(), rb, sb, group=group)
+            if sum(rb):
+                ctypes.memmove(recv, out.data_ptr(), sum(rb))
+            return 0
+        except Exception:
+            return 1
+
+    return lm.MumsCommOps(lm.COMM_ALLGATHER_FN(allgather), lm.COMM_ALLTOALLV_FN(alltoallv))
+
+
 class AbiShardStage:
     """The sharded pipeline of one rank run by the C ABI itself (mums_shard_run,
-    shard_comm.hip): RCCL communicator from ncclCommInitRank, its unique id broadcast over
-    the default process group (any backend: only the 128-byte id and the control travel
-    there).  stage = STAGE_SEEDS (steps 1-4) or STAGE_ALL (1-8)."""
+    shard_comm.hip).  comm="rccl": RCCL communicator from ncclCommInitRank, its unique id
+    broadcast over the default process group (any backend: only the 128-byte id and the
+    control travel there); comm="host": the process group itself carries the collectives
+    (mums_comm_init_host with host_comm_ops, e.g. gloo; ranks may share one GPU).
+    stage = STAGE_SEEDS (steps 1-4) or STAGE_ALL (1-8)."""
 
-    def __init__(self, engine, device: int, stage: int = 1, group: Optional[dist.ProcessGroup] = None):
+    def __init__(self, engine, device: int, stage: int = 1, group: Optional[dist.ProcessGroup] = None,
+                 comm: str = "rccl"):
         self.engine = engine
         self.stage = stage
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         lib = engine.mh._lib
+        self.last_exchange_bytes = 0
+        if comm == "host":
+            self._ops = host_comm_ops(group)
+            self.comm = ctypes.c_void_p()
+            rc = lib.mums_comm_init_host(ctypes.byref(self.comm), device, self.world, self.rank,
+                                         ctypes.byref(self._ops), None)
+            if rc != 0:
+                raise RuntimeError(f"mums_comm_init_host failed ({rc})")
+            return
         uid = ctypes.create_string_buffer(128)
         if self.rank == 0:
             engine.mh._check(lib.mums_comm_unique_id(uid, 128))
@@ -348,4 +396,5 @@ class AbiShardStage:
             self.comm = ctypes.c_void_p()
 
 
-__all__ = ["key_ranges", "genome_blocks", "HipShardEngine", "ShardedSeedStage", "ShardedFindMatches", "AbiShardStage"]
+__all__ = ["key_ranges", "genome_blocks", "HipShardEngine", "ShardedSeedStage", "ShardedFindMatches", "AbiShardStage",
+           "host_comm_ops"]

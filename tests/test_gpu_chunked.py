@@ -28,7 +28,12 @@ def force_chunks():
                                                        (3, 300000, 0.02, 19, 60000, 7, 0),
                                                        (3, 200000, 1.0, 17, 80000, 0, 0),
                                                        (3, 300000, 0.02, 19, 100000, 0, 1),
-                                                       (4, 200000, 0.03, 17, 120000, 7, 1)])
+                                                       (4, 200000, 0.03, 17, 120000, 7, 1),
+                                                       # w20-21 (msd_split of every chunk): 12 / 10 implicit bits
+                                                       (3, 300000, 0.02, 21, 100000, 0, 0),
+                                                       (2, 1000000, 0.01, 21, 300000, 0, 0),
+                                                       (4, 200000, 0.03, 20, 120000, 7, 0),
+                                                       (3, 200000, 1.0, 21, 50000, 0, 0)])
 def test_chunked_vs_oracle(gpu_lib, oracle_mod, force_chunks, G, n, p, w, cap, masked, stream):
     seqs = oracle_mod.generate(G, n, p, 99 + G)
     seed = oracle_mod.get_seed(w)
@@ -63,3 +68,13 @@ def test_chunked_seed_stage_counts(gpu_lib, oracle_mod, force_chunks):
         got = mh.stats()
     assert got["chunks"] >= 8
     assert (got["probes"], got["groups"], got["seedmers"]) == (ref["probes"], ref["groups"], ref["seedmers"])
+
+
+def test_chunked_w21_streaming_layout_refused(gpu_lib, oracle_mod, force_chunks):
+    """w20-21 keep side bytes next to the resident records: the streaming layout refuses them."""
+    seqs = oracle_mod.generate(2, 200000, 0.02, 5)
+    force_chunks(100000, stream=True)
+    with gpu_lib.MemHash(0) as mh:
+        mh.SetSeed(oracle_mod.get_seed(21))
+        with pytest.raises(gpu_lib.MumsError, match="resident"):
+            mh.FindMatches(seqs)

@@ -68,7 +68,7 @@ def check(lm, oracle_mod, force_chunks, seqs, w, chunks=4, cls="MemHash", mask=0
 
 
 @pytest.mark.parametrize("cls,mask", [("MemHash", 0), ("MaskedMemHash", 7)])
-@pytest.mark.parametrize("w", [16, 19])
+@pytest.mark.parametrize("w", [16, 19, 21])
 def test_n_gapped(gpu_lib, oracle_mod, force_chunks, cls, mask, w):
     seqs = repeat_inputs.n_gapped(G=3, n=200_000, gaps=((40_000, 3000), (120_000, 3000)), shift=500, seed=1)
     st, ref = check(gpu_lib, oracle_mod, force_chunks, seqs, w, cls=cls, mask=mask)
@@ -108,6 +108,13 @@ def test_start_points_with_restarts(gpu_lib, oracle_mod, force_chunks, sp):
     seqs = repeat_inputs.n_gapped(G=len(sp), n=90_000, gaps=((2_000, 25_000), (60_000, 4_000)), shift=1_300,
                                   seed=31)
     check(gpu_lib, oracle_mod, force_chunks, seqs, 19, start_points=sp)
+
+
+@pytest.mark.parametrize("w", [20, 21])
+def test_w2x_start_points_with_restarts(gpu_lib, oracle_mod, force_chunks, w):
+    """w20-21: the full keys of the restart plan take their top bits from the split buckets."""
+    seqs = repeat_inputs.n_gapped(G=3, n=90_000, gaps=((2_000, 25_000), (60_000, 4_000)), shift=1_300, seed=33)
+    check(gpu_lib, oracle_mod, force_chunks, seqs, w, start_points=[1000, 25_000, 7])
 
 
 @pytest.mark.parametrize("sd", range(4))

@@ -132,3 +132,39 @@ def test_sharded_find_matches_gpu(oracle_mod, G, n, p, w, world, T, slices):
     assert len(lens) == len(ref_len)
     assert (lens == ref_len).all() and (sts == ref_st).all()
     assert int(stats[0]) == ref_stats["mem_count"] and int(stats[1]) == ref_stats["collision_count"]
+
+
+@pytest.mark.parametrize("G,n,p,w,world,T,flags", [(4, 300_000, 0.02, 15, 2, 40000, ("abi",)),
+                                                     (3, 200_000, 0.05, 19, 3, 7, ("abi",)),
+                                                     (2, 300_000, 0.02, 19, 4, 40000, ("abi", "slices")),
+                                                     (3, 200_000, 0.01, 15, 2, 40000, ("abi", "gapped")),
+                                                     (2, 240_000, 0.01, 19, 4, 40000, ("abi", "slices", "gapped"))])
+def test_sharded_abi_multiprocess_gpu(oracle_mod, G, n, p, w, world, T, flags):
+    """mums_shard_run (the C++ orchestration of shard_comm.hip: agreement on every rank's
+    status, record and row all-to-allv, packed all-gather, restart planning on rank 0) with
+    ranks that are separate processes sharing cuda:0, their collectives carried by a gloo
+    process group through mums_comm_init_host.  RCCL refuses two ranks on one GPU, so this
+    is the multi-process path the one-GPU box can run; the ranks' MatchLists in rank order
+    = the oracle's, bit for bit (N-gapped inputs: restarts planned over all ranks)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gsfw", os.path.join(ROOT, "tests", "gpu_shard_find_worker.py"))
+    gsfw = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gsfw)
+    seqs = gsfw.genomes(G, n, p, flags)
+    ref_len, ref_st, ref_stats = oracle_mod.find_matches(seqs, oracle_mod.get_seed(w), table_size=T)
+    with tempfile.TemporaryDirectory() as d:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+               "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+               os.path.join(ROOT, "tests", "gpu_shard_find_worker.py"), d, str(G), str(n), str(p), str(w), str(T),
+               *flags]
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        res = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+        assert res.returncode == 0, res.stderr[-3000:]
+        lens = np.concatenate([np.load(os.path.join(d, f"len{r}.npy")) for r in range(world)])
+        sts = np.concatenate([np.load(os.path.join(d, f"st{r}.npy")).reshape(-1, G) for r in range(world)])
+        stats = sum(np.load(os.path.join(d, f"stats{r}.npy")) for r in range(world))
+    if "gapped" in flags:
+        assert ref_stats["restarts"] > 0
+    assert len(lens) == len(ref_len)
+    assert (lens == ref_len).all() and (sts == ref_st).all()
+    assert int(stats[0]) == ref_stats["mem_count"] and int(stats[1]) == ref_stats["collision_count"]

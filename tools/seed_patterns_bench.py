@@ -25,7 +25,7 @@ from bench import synth_genomes  # noqa: E402
 
 # (weight, rank): getSeed(19) is the bench's; ranks 1-2 are ProgressiveAligner's
 # seed families (ProgressiveAligner.cpp:619-625); w11-w17 the default weights of
-# smaller genomes; w21+ take the (key, index) pair path.
+# smaller genomes; w21 (genomes above ~1.07 Gbp) the 8-bit scatter + msd_split.
 PATTERNS = [(19, 0), (19, 1), (19, 2), (18, 0), (17, 0), (16, 0), (15, 0), (15, 1), (13, 0), (11, 0), (21, 0)]
 
 
@@ -36,12 +36,14 @@ def main():
     ap.add_argument("--length", type=int, default=100_000_000)
     ap.add_argument("--lib", default=None, help="A/B: another build of libmums_hip.so")
     ap.add_argument("--tag", default="")
+    ap.add_argument("--patterns", default="", help="subset, e.g. 21:0,19:0")
     args = ap.parse_args()
+    pats = [tuple(int(x) for x in p.split(":")) for p in args.patterns.split(",")] if args.patterns else PATTERNS
     if args.lib:
         lm.load_library(os.path.join(ROOT, args.lib))
     dev = torch.device("cuda", 0)
     genomes = synth_genomes(args.genomes, args.length, 0.01, 12345, dev)
-    for w, r in PATTERNS:
+    for w, r in pats:
         pat = lm.getSeed(w, r)
         with lm.MemHash(0) as mh:
             mh.SetSeed(pat)
