@@ -197,7 +197,8 @@ hipError_t launch_compat_merge(uint32_t* tsize, const uint32_t* bstart, uint32_t
     if (G <= 4) hipLaunchKernelGGL(compat_merge_kernel<4>, grid, blk, 0, st, tsize, bstart, tbl, pool, G, Tb, collisions);
     else if (G <= 8) hipLaunchKernelGGL(compat_merge_kernel<8>, grid, blk, 0, st, tsize, bstart, tbl, pool, G, Tb, collisions);
     else if (G <= 16) hipLaunchKernelGGL(compat_merge_kernel<16>, grid, blk, 0, st, tsize, bstart, tbl, pool, G, Tb, collisions);
-    else hipLaunchKernelGGL(compat_merge_kernel<32>, grid, blk, 0, st, tsize, bstart, tbl, pool, G, Tb, collisions);
+    else if (G <= 32) hipLaunchKernelGGL(compat_merge_kernel<32>, grid, blk, 0, st, tsize, bstart, tbl, pool, G, Tb, collisions);
+    else hipLaunchKernelGGL(compat_merge_kernel<64>, grid, blk, 0, st, tsize, bstart, tbl, pool, G, Tb, collisions);
     return hipGetLastError();
 }
 

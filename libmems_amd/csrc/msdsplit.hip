@@ -12,7 +12,7 @@
 // the 2^(8+S) buckets the segmented LSD sort runs in (bucket = parent << S | side).
 //
 //   split_count_kernel  : per 4096-record tile of a parent bucket, counts of its 2^S side
-//                         digits (reads 1 B per record);
+//                         digits (reads 1 B per record, byte-packed per-lane counters);
 //   one exclusive scan  : hist[tfirst_b * 2^S + d * ntb_b + tb] -> output offsets (the
 //                         order bucket-major, digit-major, tile-minor is the output order);
 //   split_scatter_kernel: wave64 match-any rank on the side digit, LDS reorder,
@@ -51,21 +51,38 @@ __global__ __launch_bounds__(kBlock) void split_count_kernel(const uint8_t* __re
             for (uint32_t k = 0; k < valid; ++k) w4[k >> 2] |= (uint32_t)side[a0 + k] << (8 * (k & 3));
         }
     }
-    // nibble counters: digit v of byte k adds 1 << 4v to acc[k / 8] (<= 8 per nibble)
-    uint64_t acc0 = 0, acc1 = 0;
+    // per-lane counts of the 16 digit values in byte fields (<= 16 each): c[v / 4] byte v % 4
+    uint32_t c[4] = {0, 0, 0, 0};
     #pragma unroll
     for (int k = 0; k < 16; ++k) {
         const uint32_t v = (w4[k >> 2] >> (8 * (k & 3))) & 15u;
-        const uint64_t inc = (uint32_t)k < valid ? (1ull << (4 * v)) : 0ull;
-        if (k < 8) acc0 += inc;
-        else acc1 += inc;
+        const uint32_t inc = (uint32_t)k < valid ? 1u << (8 * (v & 3)) : 0u;
+        c[0] += (v >> 2) == 0 ? inc : 0u;
+        c[1] += (v >> 2) == 1 ? inc : 0u;
+        c[2] += (v >> 2) == 2 ? inc : 0u;
+        c[3] += (v >> 2) == 3 ? inc : 0u;
+    }
+    // wave sum: 8 lanes in byte fields (<= 128), then 16-bit fields (<= 1024)
+    #pragma unroll
+    for (int o = 1; o <= 4; o <<= 1)
+        #pragma unroll
+        for (int i = 0; i < 4; ++i) c[i] += __shfl_xor(c[i], o, 64);
+    uint32_t h16[8];
+    #pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        h16[2 * i] = c[i] & 0x00FF00FFu;            // values 4i, 4i + 2
+        h16[2 * i + 1] = (c[i] >> 8) & 0x00FF00FFu; // values 4i + 1, 4i + 3
     }
     #pragma unroll
-    for (int v = 0; v < kMaxSide; ++v) {
-        uint32_t c = (uint32_t)((acc0 >> (4 * v)) & 15u) + (uint32_t)((acc1 >> (4 * v)) & 15u);
+    for (int o = 8; o <= 32; o <<= 1)
         #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
-        if (lane == 0) h[wv][v] = c;
+        for (int i = 0; i < 8; ++i) h16[i] += __shfl_xor(h16[i], o, 64);
+    if (lane < kMaxSide) {   // lane v picks value v: byte v % 4 of c[v / 4]
+        const uint32_t i = (uint32_t)lane >> 2, j = (uint32_t)lane & 3u;
+        uint32_t x = 0;
+        #pragma unroll
+        for (int q = 0; q < 8; ++q) x = (q == (int)(2 * i + (j & 1))) ? h16[q] : x;
+        h[wv][lane] = (j >> 1) ? (x >> 16) : (x & 0xFFFFu);
     }
     __syncthreads();
     if (tid < nd) {

@@ -1524,12 +1524,15 @@ int mums_find_stage(mums_ctx* ctx, int stage) {
         return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed-mers: only MemHash / MaskedMemHash, enum_tol <= 1");
     if (ctx->pcompat && ctx->enum_tol > 1)
         return fail(ctx, MUMS_E_UNSUPPORTED, "ParallelMemHash compat with enumeration tolerance > 1");
-    if (ctx->genomes.size() > (size_t)kPairMaxG && (ctx->pairwise || ctx->pcompat || ctx->enum_tol > 1))
-        return fail(ctx, MUMS_E_UNSUPPORTED, "more than 32 genomes: only MemHash / MaskedMemHash, enum_tol <= 1");
     if (!ctx->start_points.empty() && ctx->start_points.size() != ctx->genomes.size())   // MatchFinder.cpp:197-199
         return fail(ctx, MUMS_E_INVALID, "start points: one per sequence required");
     if (have_start_points(ctx) && ctx->pcompat)
-        return fail(ctx, MUMS_E_UNSUPPORTED, "start points (FindMatchesFromPosition) in the ParallelMemHash compat mode");
+        // ParallelMemHash has no FindMatchesFromPosition of its own: the inherited MemHash one
+        // (MemHash.cpp:117-127) runs SearchRange into ParallelMemHash::AddHashEntry's thread
+        // table (ParallelMemHash.cpp:123-127), which only FindMatches sizes (:85-86) and merges:
+        // undefined behaviour in the reference, refused here
+        return fail(ctx, MUMS_E_UNSUPPORTED, "start points (FindMatchesFromPosition) in the ParallelMemHash compat mode: "
+                                             "the reference hashes them into an unsized thread table");
     if (ctx->pairwise || ctx->enum_tol > 1) return run_pipeline_pairwise(ctx, stage);
     if (ctx->pcompat) return run_pipeline_compat(ctx, stage);
     return big ? run_pipeline_chunked(ctx, stage) : run_pipeline(ctx, stage);

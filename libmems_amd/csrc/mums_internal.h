@@ -25,7 +25,6 @@
 namespace mums {
 
 constexpr int kMaxG = 64;            // genomes per context (MaskedMemHash's 64-bit match number)
-constexpr int kPairMaxG = 32;        // PairwiseMatchFinder / enum_tol > 1 / ParallelMemHash compat paths
 constexpr int kRepeatLimit = 1000;   // MER_REPEAT_LIMIT, MatchFinder.cpp:166
 constexpr int kBlock = 256;          // threads per workgroup (4 waves of 64)
 #ifndef MUMS_SEED_TILE
@@ -125,42 +124,6 @@ __device__ __forceinline__ uint32_t wave_match_rank(uint32_t dg, bool valid, uin
     }
     *peers_out = (uint32_t)__builtin_popcount(pl) + (uint32_t)__builtin_popcount(ph);
     return __builtin_amdgcn_mbcnt_hi(ph, __builtin_amdgcn_mbcnt_lo(pl, 0u));
-}
-
-// wave_match_rank over two elements per lane in index order (lane l holds elements 2l, 2l + 1):
-// *r0 / *r1 = valid elements before each with the same digit, *t0 / *t1 = valid elements
-// of the wave with that digit.  Per digit bit: two ballots and four masks per half.
-template <int kBits>
-__device__ __forceinline__ void wave_match_rank_pair(uint32_t d0, uint32_t d1, bool v0, bool v1, uint32_t* r0,
-                                                     uint32_t* r1, uint32_t* t0, uint32_t* t1) {
-    const uint64_t b0 = __ballot(v0), b1 = __ballot(v1);
-    uint32_t p00l = (uint32_t)b0, p00h = (uint32_t)(b0 >> 32);   // lanes whose element 0 equals my d0
-    uint32_t p10l = (uint32_t)b1, p10h = (uint32_t)(b1 >> 32);   // lanes whose element 1 equals my d0
-    uint32_t p01l = p00l, p01h = p00h;                             // lanes whose element 0 equals my d1
-    uint32_t p11l = p10l, p11h = p10h;                             // lanes whose element 1 equals my d1
-    #pragma unroll
-    for (int b = 0; b < kBits; ++b) {
-        const uint32_t m0 = (uint32_t)__builtin_amdgcn_sbfe((int32_t)d0, b, 1);
-        const uint32_t m1 = (uint32_t)__builtin_amdgcn_sbfe((int32_t)d1, b, 1);
-        const uint64_t x0 = __ballot(m0 != 0u), x1 = __ballot(m1 != 0u);
-        const uint32_t x0l = (uint32_t)x0, x0h = (uint32_t)(x0 >> 32), x1l = (uint32_t)x1, x1h = (uint32_t)(x1 >> 32);
-        p00l = __builtin_amdgcn_bitop3_b32(p00l, x0l, m0, 0x90);
-        p00h = __builtin_amdgcn_bitop3_b32(p00h, x0h, m0, 0x90);
-        p10l = __builtin_amdgcn_bitop3_b32(p10l, x1l, m0, 0x90);
-        p10h = __builtin_amdgcn_bitop3_b32(p10h, x1h, m0, 0x90);
-        p01l = __builtin_amdgcn_bitop3_b32(p01l, x0l, m1, 0x90);
-        p01h = __builtin_amdgcn_bitop3_b32(p01h, x0h, m1, 0x90);
-        p11l = __builtin_amdgcn_bitop3_b32(p11l, x1l, m1, 0x90);
-        p11h = __builtin_amdgcn_bitop3_b32(p11h, x1h, m1, 0x90);
-    }
-    *t0 = (uint32_t)(__builtin_popcount(p00l) + __builtin_popcount(p00h) + __builtin_popcount(p10l) +
-                     __builtin_popcount(p10h));
-    *t1 = (uint32_t)(__builtin_popcount(p01l) + __builtin_popcount(p01h) + __builtin_popcount(p11l) +
-                     __builtin_popcount(p11h));
-    *r0 = __builtin_amdgcn_mbcnt_hi(p00h, __builtin_amdgcn_mbcnt_lo(p00l, 0u)) +
-          __builtin_amdgcn_mbcnt_hi(p10h, __builtin_amdgcn_mbcnt_lo(p10l, 0u));
-    *r1 = __builtin_amdgcn_mbcnt_hi(p01h, __builtin_amdgcn_mbcnt_lo(p01l, 0u)) +
-          __builtin_amdgcn_mbcnt_hi(p11h, __builtin_amdgcn_mbcnt_lo(p11l, 0u)) + ((v0 && d0 == d1) ? 1u : 0u);
 }
 
 // genome of a global seed-mer index (G <= 64: a linear scan is cheapest)

@@ -17,6 +17,8 @@
 #include "mums_internal.h"
 #include "seed_device.h"
 
+#include <type_traits>
+
 namespace mums {
 namespace {
 
@@ -27,14 +29,18 @@ __device__ __forceinline__ bool pw_head(const View& v, uint64_t i) {
 
 // genomes present exactly once in the group starting at head h; *size = group size
 // (walk stops past MER_REPEAT_LIMIT: SearchRange skips such groups, MatchFinder.cpp:215)
-template <typename View>
-__device__ __forceinline__ uint32_t pw_unique(const View& v, uint64_t h, uint64_t N, const GenomeTable& gt,
-                                              uint32_t* size) {
+template <int MG>
+using PwMask = typename std::conditional<(MG > 32), uint64_t, uint32_t>::type;
+
+template <int MG, typename View>
+__device__ __forceinline__ PwMask<MG> pw_unique(const View& v, uint64_t h, uint64_t N, const GenomeTable& gt,
+                                                uint32_t* size) {
     const uint64_t k0 = v.gkey(h);
-    uint32_t seen = 0, dup = 0, n = 0;
+    PwMask<MG> seen = 0, dup = 0;
+    uint32_t n = 0;
     for (uint64_t j = h; j < N && v.gkey(j) == k0; ++j) {
         ++n;
-        const uint32_t b = 1u << genome_of(gt, v.gidx(j));
+        const PwMask<MG> b = (PwMask<MG>)1 << genome_of(gt, v.gidx(j));
         dup |= seen & b;
         seen |= b;
     }
@@ -42,7 +48,7 @@ __device__ __forceinline__ uint32_t pw_unique(const View& v, uint64_t h, uint64_
     return seen & ~dup;
 }
 
-template <typename View>
+template <int MG, typename View>
 __global__ void pw_count_kernel(View v, uint64_t N, GenomeTable gt, uint32_t* __restrict__ npairs,
                                 DevCounters* __restrict__ ctr) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -50,8 +56,8 @@ __global__ void pw_count_kernel(View v, uint64_t N, GenomeTable gt, uint32_t* __
     uint32_t c = 0;
     if (pw_head(v, i)) {
         uint32_t size = 0;
-        const uint32_t u = pw_unique(v, i, N, gt, &size);
-        const uint32_t k = (uint32_t)__builtin_popcount(u);
+        const PwMask<MG> u = pw_unique<MG>(v, i, N, gt, &size);
+        const uint32_t k = (uint32_t)__builtin_popcountll((uint64_t)u);
         // a group above MER_REPEAT_LIMIT that survived the restart fix-up (restart.hip) is
         // enumerated like any other (SearchRange hands it to EnumerateMatches, :242-246)
         if (size > (uint32_t)kRepeatLimit) atomicAdd(&ctr->repeat_limit, 1ull);
@@ -64,30 +70,30 @@ __global__ void pw_count_kernel(View v, uint64_t N, GenomeTable gt, uint32_t* __
 // MemHash::HashMatch (MemHash.cpp:167-187): starts pos+1, SetDirection (:189-203: the
 // lower genome is the reference, the other is negated when its strand parity differs),
 // CalculateOffset (MatchHashEntry.cpp:141-160).
-template <typename View>
+template <int MG, typename View>
 __global__ void pw_emit_kernel(View v, uint64_t N, GenomeTable gt, int L, const uint32_t* __restrict__ npairs,
                                const uint32_t* __restrict__ off, int64_t* __restrict__ rows) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N || npairs[i] == 0) return;
     const int G = gt.G;
     uint32_t size = 0;
-    const uint32_t u = pw_unique(v, i, N, gt, &size);
-    int64_t s[kPairMaxG];
-    uint32_t par[kPairMaxG];
+    const PwMask<MG> u = pw_unique<MG>(v, i, N, gt, &size);
+    int64_t s[MG];
+    uint32_t par[MG];
     const uint64_t k0 = v.gkey(i);
     for (uint64_t j = i; j < N && v.gkey(j) == k0; ++j) {
         const RecFields r = v.get(j);
         const int g = genome_of(gt, r.idx);
-        if ((u >> g) & 1u) {
+        if ((u >> g) & 1) {
             s[g] = (int64_t)(r.idx - gt.base[g]) + 1;
             par[g] = r.par;
         }
     }
     uint64_t o = off[i];
     for (int a = 0; a < G; ++a) {
-        if (!((u >> a) & 1u)) continue;
+        if (!((u >> a) & 1)) continue;
         for (int b = a + 1; b < G; ++b) {
-            if (!((u >> b) & 1u)) continue;
+            if (!((u >> b) & 1)) continue;
             int64_t* row = rows + o * (uint64_t)(G + 1);
             for (int g = 0; g < G; ++g) row[g] = 0;
             const int64_t sb = (par[b] != par[a]) ? -s[b] : s[b];
@@ -107,13 +113,13 @@ constexpr int kEnumMax = 8;   // enum_tol bound of the GPU path (per-genome reco
 // repeat_tol + 1 records (groups above MER_REPEAT_LIMIT reach here only when the
 // reference's merge hands them over whole: restart.hip).  c[g] = kept records of g,
 // pos[g][i] / par[g][i] their positions and strand parities.
-template <typename View>
+template <int MG, typename View>
 __device__ bool en_collect(const View& v, uint64_t h, uint64_t N, const GenomeTable& gt, const MatchParams& mp,
-                           uint32_t (&c)[kPairMaxG], uint32_t (&pos)[kPairMaxG][kEnumMax], uint8_t (&par)[kPairMaxG][kEnumMax],
+                           uint32_t (&c)[MG], uint32_t (&pos)[MG][kEnumMax], uint8_t (&par)[MG][kEnumMax],
                            uint32_t* size) {
     const uint64_t k0 = v.gkey(h);
-    uint32_t tally[kPairMaxG];
-    for (int g = 0; g < kPairMaxG; ++g) { tally[g] = 0; c[g] = 0; }
+    uint32_t tally[MG];
+    for (int g = 0; g < MG; ++g) { tally[g] = 0; c[g] = 0; }
     uint32_t n = 0;
     bool ok = true;
     // stream order inside a group = (parity, genome, position): restricted to one genome
@@ -137,7 +143,8 @@ __device__ bool en_collect(const View& v, uint64_t h, uint64_t N, const GenomeTa
 // AddHashEntry calls of a group: the odometer's combinations (one record per present
 // genome), or the single HashMatch of a two-record list; HashMatch / MaskedMemHash::
 // HashMatch decide whether each combination is added (same genome set for all of them).
-__device__ __forceinline__ uint32_t en_calls(const uint32_t (&c)[kPairMaxG], int G, const MatchParams& mp, bool* two) {
+template <int MG>
+__device__ __forceinline__ uint32_t en_calls(const uint32_t (&c)[MG], int G, const MatchParams& mp, bool* two) {
     uint32_t total = 0, nid = 0, combos = 1;
     uint64_t mn = 0;
     for (int g = 0; g < G; ++g) {
@@ -153,39 +160,39 @@ __device__ __forceinline__ uint32_t en_calls(const uint32_t (&c)[kPairMaxG], int
     return (total == 2) ? 1u : combos;
 }
 
-template <typename View>
+template <int MG, typename View>
 __global__ void en_count_kernel(View v, uint64_t N, GenomeTable gt, MatchParams mp, uint32_t* __restrict__ ncalls,
                                 DevCounters* __restrict__ ctr) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N) return;
     uint32_t k = 0;
     if (pw_head(v, i)) {
-        uint32_t c[kPairMaxG], pos[kPairMaxG][kEnumMax], size = 0;
-        uint8_t par[kPairMaxG][kEnumMax];
-        const bool ok = en_collect(v, i, N, gt, mp, c, pos, par, &size);
+        uint32_t c[MG], pos[MG][kEnumMax], size = 0;
+        uint8_t par[MG][kEnumMax];
+        const bool ok = en_collect<MG>(v, i, N, gt, mp, c, pos, par, &size);
         if (size > (uint32_t)kRepeatLimit) atomicAdd(&ctr->repeat_limit, 1ull);
         bool two;
-        if (ok && size >= 2) k = en_calls(c, gt.G, mp, &two);
+        if (ok && size >= 2) k = en_calls<MG>(c, gt.G, mp, &two);
     }
     ncalls[i] = k;
 }
 
-template <typename View>
+template <int MG, typename View>
 __global__ void en_emit_kernel(View v, uint64_t N, GenomeTable gt, MatchParams mp, int L,
                                const uint32_t* __restrict__ ncalls, const uint32_t* __restrict__ off,
                                int64_t* __restrict__ rows) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N || ncalls[i] == 0) return;
     const int G = gt.G;
-    uint32_t c[kPairMaxG], pos[kPairMaxG][kEnumMax], size = 0;
-    uint8_t par[kPairMaxG][kEnumMax];
-    (void)en_collect(v, i, N, gt, mp, c, pos, par, &size);
+    uint32_t c[MG], pos[MG][kEnumMax], size = 0;
+    uint8_t par[MG][kEnumMax];
+    (void)en_collect<MG>(v, i, N, gt, mp, c, pos, par, &size);
     bool two;
-    const uint32_t K = en_calls(c, G, mp, &two);
+    const uint32_t K = en_calls<MG>(c, G, mp, &two);
     uint64_t o = off[i];
     for (uint32_t t = 0; t < K; ++t) {
-        int64_t sv[kPairMaxG];
-        uint32_t pv[kPairMaxG];
+        int64_t sv[MG];
+        uint32_t pv[MG];
         for (int g = 0; g < G; ++g) { sv[g] = 0; pv[g] = 0; }
         if (two) {   // HashMatch of the two listed records (MatchFinder.cpp:344-347)
             for (int g = 0; g < G; ++g)
@@ -224,7 +231,10 @@ template <typename View>
 hipError_t launch_pairwise_count(View v, uint64_t N, const GenomeTable& gt, uint32_t* npairs, void* ctr,
                                  hipStream_t st) {
     if (N == 0) return hipSuccess;
-    hipLaunchKernelGGL(pw_count_kernel<View>, grid_of(N), dim3(256), 0, st, v, N, gt, npairs, (DevCounters*)ctr);
+    if (gt.G > 32)
+        hipLaunchKernelGGL((pw_count_kernel<64, View>), grid_of(N), dim3(256), 0, st, v, N, gt, npairs, (DevCounters*)ctr);
+    else
+        hipLaunchKernelGGL((pw_count_kernel<32, View>), grid_of(N), dim3(256), 0, st, v, N, gt, npairs, (DevCounters*)ctr);
     return hipGetLastError();
 }
 
@@ -232,7 +242,10 @@ template <typename View>
 hipError_t launch_pairwise_emit(View v, uint64_t N, const GenomeTable& gt, int L, const uint32_t* npairs,
                                 const uint32_t* off, int64_t* rows, hipStream_t st) {
     if (N == 0) return hipSuccess;
-    hipLaunchKernelGGL(pw_emit_kernel<View>, grid_of(N), dim3(256), 0, st, v, N, gt, L, npairs, off, rows);
+    if (gt.G > 32)
+        hipLaunchKernelGGL((pw_emit_kernel<64, View>), grid_of(N), dim3(256), 0, st, v, N, gt, L, npairs, off, rows);
+    else
+        hipLaunchKernelGGL((pw_emit_kernel<32, View>), grid_of(N), dim3(256), 0, st, v, N, gt, L, npairs, off, rows);
     return hipGetLastError();
 }
 
@@ -240,7 +253,10 @@ template <typename View>
 hipError_t launch_enum_count(View v, uint64_t N, const GenomeTable& gt, const MatchParams& mp, uint32_t* ncalls,
                              void* ctr, hipStream_t st) {
     if (N == 0) return hipSuccess;
-    hipLaunchKernelGGL(en_count_kernel<View>, grid_of(N), dim3(256), 0, st, v, N, gt, mp, ncalls, (DevCounters*)ctr);
+    if (gt.G > 32)
+        hipLaunchKernelGGL((en_count_kernel<64, View>), grid_of(N), dim3(256), 0, st, v, N, gt, mp, ncalls, (DevCounters*)ctr);
+    else
+        hipLaunchKernelGGL((en_count_kernel<32, View>), grid_of(N), dim3(256), 0, st, v, N, gt, mp, ncalls, (DevCounters*)ctr);
     return hipGetLastError();
 }
 
@@ -248,7 +264,10 @@ template <typename View>
 hipError_t launch_enum_emit(View v, uint64_t N, const GenomeTable& gt, const MatchParams& mp, int L,
                             const uint32_t* ncalls, const uint32_t* off, int64_t* rows, hipStream_t st) {
     if (N == 0) return hipSuccess;
-    hipLaunchKernelGGL(en_emit_kernel<View>, grid_of(N), dim3(256), 0, st, v, N, gt, mp, L, ncalls, off, rows);
+    if (gt.G > 32)
+        hipLaunchKernelGGL((en_emit_kernel<64, View>), grid_of(N), dim3(256), 0, st, v, N, gt, mp, L, ncalls, off, rows);
+    else
+        hipLaunchKernelGGL((en_emit_kernel<32, View>), grid_of(N), dim3(256), 0, st, v, N, gt, mp, L, ncalls, off, rows);
     return hipGetLastError();
 }
 

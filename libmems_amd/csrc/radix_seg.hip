@@ -52,9 +52,7 @@ constexpr int kSortTile = MUMS_SORT_TILE;      // records per onesweep tile (lon
 #ifndef MUMS_LOOKBACK
 #define MUMS_LOOKBACK 4
 #endif
-#ifndef MUMS_OS_PAIR
-#define MUMS_OS_PAIR 0      // 1: two consecutive records per lane and load (16 B), ranked as a pair
-#endif
+
 constexpr int kLookback = MUMS_LOOKBACK;       // predecessor statuses fetched per look-back step
 inline uint64_t ub_status(uint64_t ub, int npass) { return ub * kDigits * (uint64_t)npass; }
 
@@ -387,26 +385,7 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
     const uint32_t q0 = wv * (kT / kW);
     uint64_t key[kIPT];
     uint32_t rank[kIPT];
-    // record r of this lane: q0 + r * 64 + lane, or with MUMS_OS_PAIR the pair layout
-    // q0 + (r / 2) * 128 + 2 * lane + r % 2 (one 16-B load per pair)
-    auto qof = [&](int r) -> uint32_t {
-        return MUMS_OS_PAIR ? q0 + (uint32_t)(r >> 1) * 128u + 2u * (uint32_t)lane + (uint32_t)(r & 1)
-                            : q0 + (uint32_t)r * 64u + (uint32_t)lane;
-    };
-#if MUMS_OS_PAIR
-    #pragma unroll
-    for (int r = 0; r < kIPT; r += 2) {
-        const uint32_t q = qof(r);
-        if (q + 1 < d.count) {
-            const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(rin + d.start + q);   // 8-B aligned: dwordx4
-            key[r] = v.x;
-            key[r + 1] = v.y;
-        } else {
-            key[r] = q < d.count ? rin[d.start + q] : 0ull;
-            key[r + 1] = 0ull;
-        }
-    }
-#else
+    auto qof = [&](int r) -> uint32_t { return q0 + (uint32_t)r * 64u + (uint32_t)lane; };
     #pragma unroll
     for (int r = 0; r < kIPT; ++r) {
         const uint32_t q = qof(r);
@@ -416,7 +395,6 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
         key[r] = q < d.count ? rin[d.start + q] : 0ull;
 #endif
     }
-#endif
 #if !MUMS_OS_LATEPUB
     // publish this tile's per-digit counts as soon as the keys are in: successors'
     // look-backs then rarely find an unpublished predecessor.
@@ -437,24 +415,6 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
             if (q < d.count) atomicAdd(&hnext[(uint32_t)(key[r] >> (shift + 8)) & 0xFFu], 1u);
         }
     }
-#if MUMS_OS_PAIR
-    #pragma unroll
-    for (int r = 0; r < kIPT; r += 2) {
-        const uint32_t q = qof(r);
-        const bool v0 = q < d.count, v1 = q + 1 < d.count;
-        const uint32_t d0 = (uint32_t)(key[r] >> shift) & 0xFFu, d1 = (uint32_t)(key[r + 1] >> shift) & 0xFFu;
-        uint32_t t0, t1;
-        uint32_t rk0, rk1;
-        wave_match_rank_pair<8>(d0, d1, v0, v1, &rk0, &rk1, &t0, &t1);
-        uint32_t o0 = 0, o1 = 0;
-        if (v0) o0 = wcnt[wv][d0];
-        if (v1) o1 = wcnt[wv][d1];
-        if (v0 && rk0 == 0) wcnt[wv][d0] = o0 + t0;
-        if (v1 && rk1 == 0) wcnt[wv][d1] = o1 + t1;
-        rank[r] = o0 + rk0;
-        rank[r + 1] = o1 + rk1;
-    }
-#else
     #pragma unroll
     for (int r = 0; r < kIPT; ++r) {
         const uint32_t q = qof(r);
@@ -467,7 +427,6 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
         if (valid && rk == 0) wcnt[wv][dg] = old + tot;
         rank[r] = old + rk;
     }
-#endif
     __syncthreads();
     uint32_t v = 0, acc = 0;
     if (tid < kDigits) {

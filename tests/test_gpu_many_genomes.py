@@ -1,8 +1,9 @@
 """More than 32 genomes per context (up to 64, MaskedMemHash's 64-bit match number,
 MaskedMemHash.cpp:51-58): MemHash and MaskedMemHash FindMatches on 33-64 related genomes
 against the oracle, incl. the 64-bit masks (all genomes, all but one), the sliced
-FindMatches, and the refusal of the paths that stay at 32 (PairwiseMatchFinder,
-enumeration tolerance > 1, ParallelMemHash compat)."""
+FindMatches, and the paths with their own kernels (PairwiseMatchFinder, enumeration
+tolerance > 1: 64-bit genome masks above 32 genomes; ParallelMemHash compat: 64-genome
+MergeTable)."""
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -64,10 +65,35 @@ def test_many_genomes_sliced_findmatches(gpu_lib, oracle_mod, monkeypatch):
     check(ml, st, ref)
 
 
-def test_more_than_32_genomes_refused_on_32_genome_paths(gpu_lib, oracle_mod):
-    seqs = oracle_mod.generate(33, 5000, 0.01, 3)
-    with gpu_lib.MemHash(0) as mh:
-        mh.SetSeed(oracle_mod.get_seed(11))
-        mh.SetEnumerationTolerance(2)
-        with pytest.raises(gpu_lib.MumsError):
-            mh.FindMatches(seqs)
+@pytest.mark.parametrize("G,n,p,w,kind", [(40, 3000, 0.01, 13, "pairwise"), (64, 1500, 0.005, 11, "pairwise"),
+                                           (36, 20000, 0.01, 13, "enum2"), (36, 20000, 1.0, 13, "enum3_rep1"),
+                                           (40, 30000, 0.01, 13, "compat")])
+def test_more_than_32_genomes_other_finders(gpu_lib, oracle_mod, G, n, p, w, kind):
+    seqs = oracle_mod.generate(G, n, p, 1300 + G)
+    seed = oracle_mod.get_seed(w)
+    kw, cls, setup = {}, gpu_lib.MemHash, {}
+    if kind == "pairwise":
+        kw, cls = dict(pairwise=True), gpu_lib.PairwiseMatchFinder
+    elif kind == "enum2":
+        kw = setup = dict(enum_tol=2)
+    elif kind == "enum3_rep1":
+        kw = setup = dict(enum_tol=3, repeat_tol=1)
+    else:
+        kw, cls = dict(parallel_compat=True, chunk_size=20000), None
+    ref = oracle_mod.find_matches(seqs, seed, **kw)
+    assert len(ref[0]) > 0
+    mh = gpu_lib.ParallelMemHash(0, chunk_size=20000) if cls is None else cls(0)
+    with mh:
+        mh.SetSeed(seed)
+        if "enum_tol" in setup:
+            mh.SetEnumerationTolerance(setup["enum_tol"])
+        if "repeat_tol" in setup:
+            mh.SetRepeatTolerance(setup["repeat_tol"])
+        ml = mh.FindMatches(seqs)
+        st = mh.stats()
+    lengths, starts, ost = ref
+    assert len(ml) == len(lengths)
+    assert (ml.lengths == lengths).all() and (ml.starts == starts).all()
+    assert st["mem_count"] == ost["mem_count"]
+    if kind != "compat":   # ParallelMemHash's collision counter is bumped by every OpenMP thread unguarded
+        assert st["collision_count"] == ost["collision_count"]   # (MemHash.cpp:218 via ParallelMemHash.cpp:114,126): not a defined output

@@ -173,3 +173,48 @@ def test_abi_key_ranges_match_python():
             if nb > 10:
                 t[rng.integers(0, nb, size=nb // 2)] = 0
             assert lm.shard_key_ranges(t, world) == key_ranges(t, world)
+
+
+def _host_ops_worker(rank, world, port, outdir):
+    """Calls the mums_comm_ops callbacks of host_comm_ops through their C function pointers,
+    as shard_comm.hip's HostComm does, on host buffers."""
+    import ctypes
+
+    import torch.distributed as dist
+    from libmems_amd.shard import host_comm_ops
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ops = host_comm_ops()
+    # all-gather: rank r sends [r, r + 2^63, 7]
+    send = np.array([rank, (1 << 63) + rank, 7], dtype=np.uint64)
+    recv = np.zeros(3 * world, dtype=np.uint64)
+    u64p = ctypes.POINTER(ctypes.c_uint64)
+    rc1 = ops.allgather_u64(None, send.ctypes.data_as(u64p), 3, recv.ctypes.data_as(u64p))
+    # all-to-allv: rank r sends (p + 1) * (r + 1) bytes of value 16 r + p to peer p
+    sb = np.array([(p + 1) * (rank + 1) for p in range(world)], dtype=np.uint64)
+    rb = np.array([(rank + 1) * (s + 1) for s in range(world)], dtype=np.uint64)
+    sbuf = np.concatenate([np.full(int(sb[p]), 16 * rank + p, dtype=np.uint8) for p in range(world)])
+    rbuf = np.zeros(int(rb.sum()), dtype=np.uint8)
+    rc2 = ops.alltoallv(None, sbuf.ctypes.data, sb.ctypes.data_as(u64p), rbuf.ctypes.data, rb.ctypes.data_as(u64p))
+    np.save(os.path.join(outdir, f"ag{rank}.npy"), recv)
+    np.save(os.path.join(outdir, f"a2a{rank}.npy"), rbuf)
+    np.save(os.path.join(outdir, f"rc{rank}.npy"), np.array([rc1, rc2]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_host_comm_ops_gloo(world):
+    """The transport mums_comm_init_host hands to mums_shard_run (shard.host_comm_ops over gloo):
+    all-gather and all-to-allv blocks in rank order, exercised through the C callback types."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_host_ops_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        for r in range(world):
+            assert (np.load(os.path.join(d, f"rc{r}.npy")) == 0).all()
+            ag = np.load(os.path.join(d, f"ag{r}.npy"))
+            exp = np.concatenate([np.array([s, (1 << 63) + s, 7], dtype=np.uint64) for s in range(world)])
+            assert (ag == exp).all()
+            a2a = np.load(os.path.join(d, f"a2a{r}.npy"))
+            exp2 = np.concatenate([np.full((r + 1) * (s + 1), 16 * s + r, dtype=np.uint8) for s in range(world)])
+            assert (a2a == exp2).all()

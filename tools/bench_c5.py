@@ -40,9 +40,26 @@ def synth_pair(n: int, p: float, seed: int, dev):
     return a, b
 
 
+def add_gaps(a, b, gaps: int, seed: int):
+    """N runs as in assembled mammalian genomes: `gaps` runs of 5-60 kbp per genome at random
+    positions (N encodes as A: each run is one seed group of tens of thousands of records,
+    a MER_REPEAT_LIMIT restart, MatchFinder.cpp:253-277)."""
+    g = torch.Generator()
+    g.manual_seed(seed)
+    n = a.numel()
+    for t in (a, b):
+        pos = torch.randint(0, n - 60_000, (gaps,), generator=g).tolist()
+        ln = torch.randint(5_000, 60_000, (gaps,), generator=g).tolist()
+        for p0, l0 in zip(pos, ln):
+            t[p0:p0 + l0] = ord("N")
+    torch.cuda.synchronize()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--length", type=int, default=3_000_000_000)
+    ap.add_argument("--weight", type=int, default=19, help="seed weight (21 = getDefaultSeedWeight of 3 Gbp genomes)")
+    ap.add_argument("--gaps", type=int, default=0, help="N runs per genome (restarts)")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--fine-cap", type=int, default=400_000_000)
     ap.add_argument("--find-steps", type=int, default=2)
@@ -50,12 +67,15 @@ def main():
     dev = torch.device("cuda", 0)
     t0 = time.perf_counter()
     a, b = synth_pair(args.length, 0.01, 2024, dev)
+    if args.gaps:
+        add_gaps(a, b, args.gaps, 77)
     gen_s = time.perf_counter() - t0
     print(f"generated 2 x {args.length} bp in {gen_s:.1f} s", flush=True)
-    out = {"config": "BASELINE config 5 shape on 1 GPU: 2 x %d bp related p=0.01, w19 (0x7b974ef), MemHash seed stage"
-                     % args.length}
+    out = {"config": "BASELINE config 5 shape on 1 GPU: 2 x %d bp related p=0.01, w%d (%s)%s, MemHash seed stage"
+                     % (args.length, args.weight, hex(lm.getSeed(args.weight)),
+                        f", {args.gaps} N runs of 5-60 kbp per genome" if args.gaps else "")}
     with lm.MemHash(0) as mh:
-        mh.SetSeed(lm.getSeed(19))
+        mh.SetSeed(lm.getSeed(args.weight))
         mh.AddSequence(a)
         mh.AddSequence(b)
         mh.FindStage(lm.STAGE_SEEDS)   # warm
@@ -95,6 +115,7 @@ def main():
         out["findmatches"] = {
             "ms": fd * 1e3, "matches": fst["mem_count"], "mums_per_s": fst["mem_count"] / fd, "probes": fst["probes"],
             "chains": fst["chains"], "mem_count": fst["mem_count"], "collisions": fst["collision_count"],
+            "restarts": fst.get("restarts"), "repeat_limit_groups": fst.get("repeat_limit_groups"),
             "phase_ms": {k: round(fst[k], 2) for k in fst if k.startswith("ms_")},
         }
     print(json.dumps(out), flush=True)

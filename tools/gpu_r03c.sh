@@ -5,7 +5,7 @@ T=${1:-r03c}
 OUT=gpurun_out/$T
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_shard.py -k abi_multiprocess -m gpu -q -x -rf --timeout 300 \
+timeout -k 10 500 python -u -m pytest tests/test_gpu_pairwise.py tests/test_gpu_enumerate.py tests/test_gpu_compat.py tests/test_gpu_shard.py -k "abi_multiprocess or pairwise or enum or compat or Pairwise or Parallel" -m gpu -q -x -rf --timeout 300 \
   --timeout-method thread > $OUT/pytest_mp.log 2>&1 || { echo "pytest mp failed"; tail -30 $OUT/pytest_mp.log; exit 11; }
 tail -1 $OUT/pytest_mp.log
 bash tools/gpu_quick.sh ${T}_quick || exit 12
