@@ -221,6 +221,7 @@ def main():
     bytes_dom = 0
     launches = 0
     exch_bytes = 0
+    abi_err = None
     if not sharded:
         mh = lm.MemHash(local)
         mh.SetSeed(seed)
@@ -246,16 +247,49 @@ def main():
         del genomes
         genomes = mine
         eng = HipShardEngine(local, seed, [n] * G, first, genomes)
-        stage = AbiShardStage(eng, local) if args.exchange == "abi" else ShardedSeedStage(eng)
+        if args.exchange == "abi":
+            try:
+                stage = AbiShardStage(eng, local)
+            except Exception as e:  # agreed on below: every rank falls back together
+                stage, abi_err = None, e
+        else:
+            stage = ShardedSeedStage(eng)
         mh = eng.mh
-        run = stage.run
+        run = stage.run if stage is not None else None
         stats = eng.stats
+    fallback = None
+    if sharded and world > 1 and args.exchange == "abi":
+        # the library's own RCCL communicator has only run with one rank on the one-GPU test
+        # boxes: if its first step fails on any rank, every rank (agreed over the gloo control
+        # group) continues with the torch.distributed RCCL exchange of shard.py instead, and
+        # the line says so
+        ok = 1
+        try:
+            if stage is None:
+                raise RuntimeError(f"communicator: {abi_err}")
+            stage.run()
+        except Exception as e:  # report, never hide
+            ok = 0
+            fallback = f"mums_shard_run failed on rank {rank}: {e}"
+            print(fallback, file=sys.stderr, flush=True)
+        flag = torch.tensor([ok], dtype=torch.int64)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if int(flag.item()) == 0:
+            if fallback is None:
+                fallback = "mums_shard_run failed on another rank"
+            nccl = dist.new_group(backend="nccl")
+            if stage is not None:
+                stage.close()
+            stage = ShardedSeedStage(eng, group=nccl)
+            run = stage.run
+            args.exchange = "torch"
+            args.dist_backend = "nccl"
     for _ in range(args.warmup):
         run()
 
     def barrier():
         if world > 1:
-            if args.dist_backend == "nccl":
+            if args.dist_backend == "nccl" and fallback is None:
                 dist.barrier(device_ids=[local])
             else:
                 dist.barrier()
@@ -271,7 +305,8 @@ def main():
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
-    tmax = torch.tensor([dt], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
+    tmax = torch.tensor([dt], dtype=torch.float64, device=dev if (args.dist_backend == "nccl" and fallback is None)
+                        else "cpu")
     if world > 1:
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     dt = float(tmax.item())
@@ -428,6 +463,8 @@ def main():
         }
         if mums_c3 is not None:
             out["mums_c3"] = mums_c3
+        if fallback is not None:
+            out["exchange_fallback"] = fallback + " -> torch.distributed RCCL all_to_all (libmems_amd/shard.py)"
         if not args.no_mums:
             try:
                 out["mums"] = run_mums(local, dev, 0.01)

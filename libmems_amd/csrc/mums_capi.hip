@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <functional>
 #include <cstddef>
 #include <cstdio>
@@ -2578,10 +2579,26 @@ int run_pipeline_pairwise(mums_ctx* ctx, int stage) {
 // `other` at the segment's base: n_live[c], its bucket starts (bst_in(c, d) writes the
 // original nb + 1 of them to device memory d) mapped into d_bst_out + sum of earlier (nb + 1).
 // *live = false when every record lives (nothing written).
+// development: MUMS_DEV_RESTART_TIMING prints the wall time of every restart phase
+struct PhaseClock {
+    bool on;
+    hipStream_t st;
+    std::chrono::steady_clock::time_point t0;
+    PhaseClock(hipStream_t s) : on(getenv("MUMS_DEV_RESTART_TIMING") != nullptr), st(s), t0(std::chrono::steady_clock::now()) {}
+    void mark(const char* what) {
+        if (!on) return;
+        (void)hipStreamSynchronize(st);
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "restart phase %-28s %9.1f ms\n", what, std::chrono::duration<double, std::milli>(t - t0).count());
+        t0 = t;
+    }
+};
+
 int stream_restart(mums_ctx* ctx, uint64_t* srec, uint64_t* other, const std::vector<uint64_t>& dstart, uint32_t kb,
                    uint32_t ib, const std::vector<RestartSeg>& segs,
                    const std::function<int(uint32_t, uint32_t*)>& bst_in, uint32_t* d_bst_out,
                    std::vector<uint64_t>& n_live, bool* live_out, hipStream_t st) {
+    PhaseClock pc(st);
     const GenomeTable& gt = ctx->gt;
     const int G = gt.G;
     const uint64_t Gu = (uint64_t)G;
@@ -2605,6 +2622,7 @@ int stream_restart(mums_ctx* ctx, uint64_t* srec, uint64_t* other, const std::ve
     HIPCHK(hipMemcpyAsync(&C, d_cnt, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     ctx->cr_cands = C;
+    pc.mark("candidates");
     if (C == 0 && !have_start_points(ctx)) return MUMS_OK;
     if (C > ccap) return fail(ctx, MUMS_E_HIP, "restart: candidate list overflow (internal error)");
     if (ctx->parity_masked || seg_onesweep_launches(kb) < (int)((kb + 7) / 8))
@@ -2623,6 +2641,7 @@ int stream_restart(mums_ctx* ctx, uint64_t* srec, uint64_t* other, const std::ve
     HIPCHK(launch_cr_counts(s, gt, gscan, ctx->tmp.p, st));
     uint64_t* ck = other;
     HIPCHK(launch_cr_ck(s, gt, gscan, ck, st));
+    pc.mark("SMLs (counts, keys)");
     // the plan (restart.hip's kernels over the SMLs)
     std::vector<uint64_t> S0(G, 0), hm(G + 1, 0), hb(G + 1, 0);
     for (int g = 0; g < G && g < (int)ctx->start_points.size(); ++g) S0[g] = ctx->start_points[g];
@@ -2665,6 +2684,7 @@ int stream_restart(mums_ctx* ctx, uint64_t* srec, uint64_t* other, const std::ve
     ctx->restarts = R;
     ctx->offset_log.assign(R * Gu, 0);
     if (R) HIPCHK(hipMemcpy(ctx->offset_log.data(), d_rS, R * Gu * 8, hipMemcpyDeviceToHost));
+    pc.mark("plan");
     if (R == 0 && !have_start_points(ctx)) return MUMS_OK;
     // start points inside runs of equal keys: those runs in std::sort order (MemorySML.cpp:54)
     const uint64_t rcap = (R + 1) * Gu + 16;
@@ -2707,6 +2727,9 @@ int stream_restart(mums_ctx* ctx, uint64_t* srec, uint64_t* other, const std::ve
             HIPCHK(tie_replay(tw, st));
             HIPCHK(launch_cr_tie_write(s, gt, g, d_runs, nruns, ck, tw.V, srec, st));
             ctx->tie_slots += flagged;
+            if (pc.on) fprintf(stderr, "restart genome %d: %lu flagged slots, %lu runs\n", g, (unsigned long)flagged,
+                               (unsigned long)nruns);
+            pc.mark("tie order of one genome");
         }
         HIPCHK(hipStreamSynchronize(st));
         ctx->tiebuf.release();
@@ -2737,6 +2760,7 @@ int stream_restart(mums_ctx* ctx, uint64_t* srec, uint64_t* other, const std::ve
         HIPCHK(hipStreamSynchronize(st));
         n_live[c] = t;
     }
+    pc.mark("live compaction");
     for (DevBuf* b : {&ctx->crcnt, &ctx->crlive, &ctx->crruns}) b->release();
     *live_out = true;
     return MUMS_OK;
