@@ -2579,6 +2579,18 @@ int run_pipeline_pairwise(mums_ctx* ctx, int stage) {
 // `other` at the segment's base: n_live[c], its bucket starts (bst_in(c, d) writes the
 // original nb + 1 of them to device memory d) mapped into d_bst_out + sum of earlier (nb + 1).
 // *live = false when every record lives (nothing written).
+// the FindMatches tail's buffers (rows, chains, replay, MatchList) hold nothing the seed stage
+// reads: freed when a seed-stage allocation does not fit beside them
+void release_find_buffers(mums_ctx* ctx) {
+    for (DevBuf* b : {&ctx->rowsall, &ctx->rowtmp, &ctx->sids, &ctx->summ, &ctx->chain_tmp, &ctx->chain_of, &ctx->pool,
+                      &ctx->pool_loc, &ctx->cbuf, &ctx->spill, &ctx->tbl, &ctx->fk, &ctx->fkloc, &ctx->mprobe,
+                      &ctx->out_len, &ctx->out_s})
+        b->release();
+    ctx->emit_tbl = nullptr;
+    ctx->emit_base = nullptr;
+    ctx->M = 0;
+}
+
 // development: MUMS_DEV_RESTART_TIMING prints the wall time of every restart phase
 struct PhaseClock {
     bool on;
@@ -2707,9 +2719,17 @@ int stream_restart(mums_ctx* ctx, uint64_t* srec, uint64_t* other, const std::ve
             if (!any) continue;
             const uint64_t m = gt.m[g];
             if (m >= 0xFFFFFFF0ull) return fail(ctx, MUMS_E_UNSUPPORTED, "SortedMerList of more than 2^32 seed-mers");
-            if (ctx->tiebuf.ensure(tie_ws_bytes(m, 1)) != hipSuccess)
-                return fail(ctx, MUMS_E_NOMEM, "restart: no device memory for the SortedMerList tie order of a "
-                                               "genome");
+            if (ctx->tiebuf.ensure(tie_ws_bytes(m, 1)) != hipSuccess) {
+                // the previous FindMatches' tail buffers are dead during the seed stage: free them
+                // and try again (2 x 3 Gbp: ~135 GB of tie workspace beside 96 GB of records)
+                (void)hipGetLastError();
+                HIPCHK(hipStreamSynchronize(st));
+                release_find_buffers(ctx);
+                if (ctx->tiebuf.ensure(tie_ws_bytes(m, 1)) != hipSuccess)
+                    return fail(ctx, MUMS_E_NOMEM, "restart: no device memory for the SortedMerList tie order of a "
+                                                   "genome");
+            }
+            pc.mark("tie workspace");
             const TieWs tw = tie_ws_layout(ctx->tiebuf.p, m, 1);
             const uint64_t b0 = 0;
             HIPCHK(tie_set_genomes(tw, &b0, &m, st));
@@ -2722,9 +2742,12 @@ int stream_restart(mums_ctx* ctx, uint64_t* srec, uint64_t* other, const std::ve
             HIPCHK(tie_mark_starts(tw, ck + gt.base[g], d_sp, R + 1, st));
             uint64_t flagged = 0;
             HIPCHK(tie_prepare(tw, &flagged, st));
+            pc.mark("tie flags");
             if (!flagged) continue;
             HIPCHK(launch_cr_kpos(s, gt, g, tw.K, st));
+            pc.mark("tie keys in position order");
             HIPCHK(tie_replay(tw, st));
+            pc.mark("tie replay");
             HIPCHK(launch_cr_tie_write(s, gt, g, d_runs, nruns, ck, tw.V, srec, st));
             ctx->tie_slots += flagged;
             if (pc.on) fprintf(stderr, "restart genome %d: %lu flagged slots, %lu runs\n", g, (unsigned long)flagged,

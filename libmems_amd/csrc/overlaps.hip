@@ -108,7 +108,8 @@ __global__ void rank_kernel(const SortSeg* __restrict__ segs, uint32_t S, uint32
 // pair k swaps iff L_k < R_k (a prefix of k); nswap[s] = K
 __global__ void swap_kernel(uint64_t* K, uint32_t* V, const SortSeg* __restrict__ segs, uint32_t S, uint32_t n,
                             const uint32_t* __restrict__ fl, const uint32_t* __restrict__ fr,
-                            const uint32_t* __restrict__ Rpos, uint32_t* __restrict__ nswap) {
+                            const uint32_t* __restrict__ Lpos, const uint32_t* __restrict__ Rpos,
+                            uint32_t* __restrict__ nswap) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n || fl[i + 1] == fl[i]) return;
     const int s = seg_of(segs, S, i);
@@ -120,7 +121,10 @@ __global__ void swap_kernel(uint64_t* K, uint32_t* V, const SortSeg* __restrict_
     const uint32_t j = Rpos[g.f + 1 + k];
     if (!(i < j)) return;
     swap_kv(K, V, i, j);
-    atomicAdd(&nswap[s], 1u);
+    // the swapping pairs are a prefix: its last pair writes the count (no per-swap atomic
+    // on one counter, which serialises large segments)
+    const uint32_t cntL = fl[g.l] - fl[g.f + 1];
+    if (k + 1 >= cntL || k + 1 >= cntR || !(Lpos[g.f + 1 + k + 1] < Rpos[g.f + 1 + k + 1])) nswap[s] = k + 1;
 }
 
 // cut = min(L_{K+1}, R_K) (R_0 = l); children [f, cut), [cut, l) at depth d - 1 into
@@ -488,7 +492,7 @@ static hipError_t std_sort_device(EoWork& w, uint32_t n, int depth_override, hip
         hipLaunchKernelGGL(rank_kernel, dim3(grid_of(n)), dim3(kBlock), 0, st, segA, S, n, fl, fr, (uint32_t*)w.Lpos,
                            (uint32_t*)w.Rpos);
         EOCHK(hipMemsetAsync(nsw, 0, (size_t)S * 4, st));
-        hipLaunchKernelGGL(swap_kernel, dim3(grid_of(n)), dim3(kBlock), 0, st, K, V, segA, S, n, fl, fr,
+        hipLaunchKernelGGL(swap_kernel, dim3(grid_of(n)), dim3(kBlock), 0, st, K, V, segA, S, n, fl, fr, (const uint32_t*)w.Lpos,
                            (const uint32_t*)w.Rpos, nsw);
         hipLaunchKernelGGL(cut_kernel, dim3(grid_of(S)), dim3(kBlock), 0, st, segA, S, fl, (const uint32_t*)w.Lpos,
                            (const uint32_t*)w.Rpos, nsw, segB, act, (SortSeg*)w.heap, d_nheap, bound);

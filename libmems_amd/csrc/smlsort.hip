@@ -29,6 +29,8 @@
 //     final insertion sort (it never moves an element across a partition boundary).
 // The oracle restates std::sort in oracle/std_sort.h, pinned to the real std::sort.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "mums_internal.h"
@@ -202,8 +204,8 @@ __global__ void rank_kernel(const TieSeg* __restrict__ segs, const uint32_t* __r
 // pair k swaps iff L_k < R_k (a prefix of k); nswap[s] = K
 __global__ void swap_kernel(uint64_t* K, uint32_t* V, const TieSeg* __restrict__ segs,
                             const uint32_t* __restrict__ off, uint32_t S, uint32_t A, const uint32_t* __restrict__ fl,
-                            const uint32_t* __restrict__ fr, const uint32_t* __restrict__ Rpos,
-                            uint32_t* __restrict__ nswap) {
+                            const uint32_t* __restrict__ fr, const uint32_t* __restrict__ Lpos,
+                            const uint32_t* __restrict__ Rpos, uint32_t* __restrict__ nswap) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= A || fl[t + 1] == fl[t]) return;
     const uint32_t s = seg_of(off, S, t);
@@ -215,7 +217,11 @@ __global__ void swap_kernel(uint64_t* K, uint32_t* V, const TieSeg* __restrict__
     const uint32_t j = Rpos[b + k];
     if (!(i < j)) return;
     swap_kv(K, V, i, j);
-    atomicAdd(&nswap[s], 1u);
+    // the swapping pairs are a prefix (L_k rises, R_k falls): its last pair writes the count.
+    // (One atomic per swap on the segment's counter serialised 1.5e9 swaps of a 3 Gbp SML:
+    // 28 s per restart at BASELINE config 5.)
+    const uint32_t cntL = fl[e] - fl[b];
+    if (k + 1 >= cntL || k + 1 >= cntR || !(Lpos[b + k + 1] < Rpos[b + k + 1])) nswap[s] = k + 1;
 }
 
 // cut = min(L_{K+1}, R_K) (R_0 = l); children [f, cut), [cut, l) at depth d - 1 into
@@ -461,6 +467,9 @@ hipError_t tie_replay(const TieWs& w, hipStream_t st) {
                        heap, d_nheap, w.bound);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     uint32_t n2 = (uint32_t)w.G;
+    const bool dbg = getenv("MUMS_DEV_RESTART_TIMING") != nullptr;   // development: levels and sizes
+    int level = 0;
+    uint64_t a_sum = 0;
     for (;;) {
         // compact the kept children of the last level into segA, their partition sizes into off
         if ((e = exclusive_scan_u32(w.act, (uint64_t)n2 + 1, w.tmp, d_nact, st)) != hipSuccess) return e;
@@ -477,6 +486,9 @@ hipError_t tie_replay(const TieWs& w, hipStream_t st) {
         hipLaunchKernelGGL(median_kernel, dim3(grid_of(S)), dim3(kBlock), 0, st, w.K, w.V, segA, S, w.piv);
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
         const uint32_t A = hc[1];
+        a_sum += A;
+        if (dbg && (level < 8 || (level % 8) == 0)) fprintf(stderr, "tie replay level %d: %u segments, %u elements\n", level, S, A);
+        ++level;
         hipLaunchKernelGGL(classify_kernel, dim3(grid_of((uint64_t)A + 1)), dim3(kBlock), 0, st, w.K, segA, w.off, S,
                            w.piv, A, w.fl, w.fr);
         if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -486,7 +498,7 @@ hipError_t tie_replay(const TieWs& w, hipStream_t st) {
                            w.Rpos);
         if ((e = hipMemsetAsync(w.nsw, 0, (size_t)S * 4, st)) != hipSuccess) return e;
         hipLaunchKernelGGL(swap_kernel, dim3(grid_of(A)), dim3(kBlock), 0, st, w.K, w.V, segA, w.off, S, A, w.fl, w.fr,
-                           w.Rpos, w.nsw);
+                           w.Lpos, w.Rpos, w.nsw);
         hipLaunchKernelGGL(cut_kernel, dim3(grid_of(S)), dim3(kBlock), 0, st, segA, w.off, S, w.fl, w.Lpos, w.Rpos,
                            w.nsw, w.ts, segB, w.act, heap, d_nheap, w.bound);
         if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -494,6 +506,8 @@ hipError_t tie_replay(const TieWs& w, hipStream_t st) {
     }
     if ((e = hipMemcpyAsync(hc + 2, d_nheap, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+    if (dbg) fprintf(stderr, "tie replay: %d levels, %lu elements partitioned, %u heap segments\n", level,
+                     (unsigned long)a_sum, hc[2]);
     if (hc[2] > 0) {
         hipLaunchKernelGGL(heap_kernel, dim3(grid_of(hc[2])), dim3(kBlock), 0, st, w.K, w.V, heap, hc[2]);
         if ((e = hipGetLastError()) != hipSuccess) return e;
