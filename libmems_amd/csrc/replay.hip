@@ -1376,6 +1376,7 @@ size_t replay_scratch_bytes(uint64_t n, uint32_t table_size) {
 // start >= next_s of the chain), and the bucket order, the summaries and the replay work on
 // the kept probes alone -- no per-probe pass in bucket order.
 constexpr int kKeepIPT = 8;
+constexpr int kKeepStageW = 17;   // rows of up to 16 genomes are staged through LDS in keep_fill_kernel
 
 __device__ __forceinline__ uint32_t row_first_start(const int64_t* __restrict__ rows, uint64_t k, int G) {
     const int64_t* r = rows + k * (uint64_t)(G + 1);
@@ -1415,14 +1416,41 @@ __global__ __launch_bounds__(kBlock) void keep_fill_kernel(const int64_t* __rest
                                                            unsigned int* __restrict__ nkept, uint64_t cap,
                                                            uint64_t* __restrict__ kept) {
     __shared__ uint32_t s_w[kBlock / 64 + 1];
+    __shared__ int64_t srow[kBlock * kKeepStageW];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint64_t keys[kKeepIPT];
     uint32_t want = 0;
+    const int W = G + 1;
+    const bool staged = W <= kKeepStageW;   // uniform
     #pragma unroll
     for (int i = 0; i < kKeepIPT; ++i) {
-        const uint64_t k = (uint64_t)blockIdx.x * (kBlock * kKeepIPT) + (uint64_t)i * kBlock + threadIdx.x;
+        const uint64_t k0 = (uint64_t)blockIdx.x * (kBlock * kKeepIPT) + (uint64_t)i * kBlock;
+        const uint64_t k = k0 + threadIdx.x;
         keys[i] = 0;
-        if (k < P && keep_probe(rows, k, G, chain_of, ck, &keys[i])) want |= 1u << i;
+        if (staged) {
+            // the round's rows are one contiguous range: read it with consecutive lanes on
+            // consecutive words (one lane per row touches a 128-B line per lane)
+            if (k0 < P) {
+                const uint64_t nk = P - k0 < (uint64_t)kBlock ? P - k0 : (uint64_t)kBlock;
+                const int64_t* src = rows + k0 * (uint64_t)W;
+                for (uint32_t j = threadIdx.x; j < nk * (uint64_t)W; j += kBlock) srow[j] = src[j];
+            }
+            __syncthreads();
+            if (k < P) {
+                const uint4 c = ck[chain_of[k]];
+                bool keep = c.x == (uint32_t)k;
+                if (!keep) {
+                    uint32_t fs = 0;
+                    for (int g = 0; g < G && fs == 0; ++g) fs = (uint32_t)srow[threadIdx.x * W + g];
+                    keep = fs >= c.y;
+                }
+                keys[i] = ((uint64_t)c.z << 32) | k;
+                if (keep) want |= 1u << i;
+            }
+            __syncthreads();
+        } else if (k < P && keep_probe(rows, k, G, chain_of, ck, &keys[i])) {
+            want |= 1u << i;
+        }
     }
     const uint32_t n = (uint32_t)__builtin_popcount(want);
     uint32_t x = n;

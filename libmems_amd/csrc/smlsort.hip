@@ -370,11 +370,11 @@ TieWs tie_ws_layout(void* base, uint64_t n, int G) {
     w.n = n;
     w.G = G;
     w.smax = smax;
-    w.pf = (uint32_t*)take(n1 * 4);
     w.ts = (uint32_t*)take(n1 * 4);
     w.K = (uint64_t*)take(n1 * 8);
     w.V = (uint32_t*)take(n1 * 4);
     w.fl = (uint32_t*)take(n1 * 4);
+    w.pf = w.fl;   // the pair flags are dead once tie_prepare has scanned them into ts
     w.fr = (uint32_t*)take(n1 * 4);
     w.Lpos = (uint32_t*)take(n1 * 4);
     w.Rpos = (uint32_t*)take(n1 * 4);

@@ -7,7 +7,7 @@ OUT=gpurun_out/${1:-pmc_chains}
 mkdir -p $OUT
 export TMPDIR=/tmp
 CMD="python3 tools/c3_mums.py 1"
-RE="chain_walk|chain_link|chain_left|replay_big|bigg_|gather_rows|probe_materialize"
+RE="chain_|replay|bigg_|bigq_|gather_rows|probe_materialize|keep_fill|kept_summary"
 i=0
 for SET in "FETCH_SIZE" "WRITE_SIZE" \
            "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM_RD" \
