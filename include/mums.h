@@ -189,6 +189,14 @@ int  mums_length_filter(mums_ctx* ctx, uint64_t min_length);
  * NULL); MemHash / MaskedMemHash / PairwiseMatchFinder paths, not ParallelMemHash compat. */
 int  mums_set_match_log(mums_ctx* ctx, int enable);
 int  mums_match_log_copy(mums_ctx* ctx, uint64_t* lengths, int64_t* starts, uint64_t capacity, uint64_t* count);
+/* MatchFinder::LogProgress (MatchFinder.h:80, MatchFinder.cpp:55-56,296-309): the reference
+ * writes "N%.." to the log stream each time its merge crosses a whole percent of the mers
+ * (counted per 10 000-mer buffer refill, a newline every ten).  Enable before mums_find; the
+ * seed stage then restates that text (MER_REPEAT_LIMIT restarts and start points included;
+ * single context and chunked mode with packed records, i.e. seed weight <= 21) and
+ * mums_progress_log_copy returns it (*length = its size; text NUL-terminated, may be NULL). */
+int  mums_set_progress_log(mums_ctx* ctx, int enable);
+int  mums_progress_log_copy(mums_ctx* ctx, char* text, uint64_t capacity, uint64_t* length);
 /* EliminateOverlaps (libMems/Aligner.cpp:62-176, declared Aligner.h:239) on the context's
  * MatchList in place: per genome, std::sort by SingleStartComparator (AbstractMatch.h:324-351,
  * libstdc++ tie order reproduced), crop / delete the smaller of every overlapping pair,

@@ -89,12 +89,14 @@ public:
         for (const auto& s : ml.seq_table) AddSequence(s);
         check(mums_find(ctx_));
         write_match_log();
+        write_progress();
         GetMatchList(ml);
     }
     // MemHash::CreateMatches (MemHash.cpp:104-107)
     virtual bool CreateMatches() {
         check(mums_find(ctx_));
         write_match_log();
+        write_progress();
         return true;
     }
     // MemHash::GetMatchList (MemHash.h:182-203): clears the list first
@@ -190,6 +192,12 @@ public:
         match_log_ = log;
         check(mums_set_match_log(ctx_, log != nullptr));
     }
+    // MatchFinder::LogProgress (MatchFinder.cpp:55-56): the merge's progress text ("N%.." per
+    // whole percent, MatchFinder.cpp:296-309) is written to *os after every FindMatches
+    void LogProgress(std::ostream* os) {
+        progress_ = os;
+        check(mums_set_progress_log(ctx_, os != nullptr));
+    }
     // EliminateOverlaps (Aligner.cpp:62-176) of the last MatchList, on the device
     void EliminateOverlaps() { check(mums_eliminate_overlaps(ctx_)); }
     // a caller's MatchList (M x G starts + lengths) as the current result, e.g. to run
@@ -230,7 +238,18 @@ protected:
         }
         match_log_->flush();
     }
+    void write_progress() const {
+        if (!progress_) return;
+        uint64_t n = 0;
+        check(mums_progress_log_copy(ctx_, nullptr, 0, &n));
+        std::string t(n + 1, '\0');
+        check(mums_progress_log_copy(ctx_, &t[0], n + 1, &n));
+        t.resize(n);
+        (*progress_) << t;
+        progress_->flush();
+    }
     std::ostream* match_log_ = nullptr;
+    std::ostream* progress_ = nullptr;
     mums_ctx* ctx_ = nullptr;
     uint32_t repeat_tol_ = 0, enum_tol_ = 1, table_size_ = 40000;
 };

@@ -100,7 +100,8 @@ EXPORTED_SYMBOLS = [
     "mums_load_matches", "mums_debug_std_sort", "mums_comm_unique_id", "mums_comm_init_rank", "mums_comm_init_all",
     "mums_comm_init_local", "mums_comm_destroy", "mums_comm_last_error", "mums_shard_key_ranges", "mums_shard_run",
     "mums_set_match_log", "mums_match_log_copy", "mums_shard_restart_pending", "mums_shard_stream",
-    "mums_shard_restart_plan", "mums_shard_restart_apply", "mums_comm_init_host",
+    "mums_shard_restart_plan", "mums_shard_restart_apply", "mums_comm_init_host", "mums_set_progress_log",
+    "mums_progress_log_copy",
 ]
 
 # mums_comm_ops (include/mums.h): the caller's transport as two host callbacks
@@ -195,6 +196,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mums_shard_key_ranges.argtypes = [vp, u32, u32, vp, vp]
     lib.mums_shard_run.argtypes = [vp, vp, ctypes.c_int]
     lib.mums_set_match_log.argtypes = [vp, i32]
+    lib.mums_set_progress_log.argtypes = [vp, i32]
+    lib.mums_progress_log_copy.argtypes = [vp, ctypes.c_char_p, u64, ctypes.POINTER(u64)]
     lib.mums_match_log_copy.argtypes = [vp, vp, vp, u64, ctypes.POINTER(u64)]
     _lib = lib
     return lib
@@ -492,6 +495,19 @@ class MemHash:
             self._check(self._lib.mums_match_log_copy(self._ctx, lengths.ctypes.data, starts.ctypes.data, n.value,
                                                       ctypes.byref(n)))
         return MatchList(lengths, starts)
+
+    def LogProgress(self, enable: bool = True) -> None:
+        """MatchFinder::LogProgress (MatchFinder.cpp:55-56): restate the progress text of the
+        next FindMatches' merge (ProgressLog())."""
+        self._check(self._lib.mums_set_progress_log(self._ctx, int(bool(enable))))
+
+    def ProgressLog(self) -> str:
+        """The text the reference's log stream receives ("N%.." per whole percent, MatchFinder.cpp:296-309)."""
+        n = ctypes.c_uint64()
+        self._check(self._lib.mums_progress_log_copy(self._ctx, None, 0, ctypes.byref(n)))
+        buf = ctypes.create_string_buffer(n.value + 1)
+        self._check(self._lib.mums_progress_log_copy(self._ctx, buf, n.value + 1, ctypes.byref(n)))
+        return buf.value.decode()
 
     def EliminateOverlaps(self) -> None:
         """EliminateOverlaps (Aligner.cpp:62-176) of the current MatchList, on the GPU."""

@@ -240,6 +240,33 @@ __global__ void cr_tie_write_kernel(CrStream s, GenomeTable gt, int g, const uin
     }
 }
 
+// LogProgress: the masked key of the e-th record of genome g in stream order (= its SML
+// index e) for every query q = g << 56 | e: the block holding it from the genome's block
+// prefix counts, then a walk over that block's records
+__global__ __launch_bounds__(kBlock) void cr_query_kernel(CrStream s, GenomeTable gt, const uint32_t* __restrict__ gscan,
+                                                          uint64_t nblk, const uint64_t* __restrict__ q, uint64_t nq,
+                                                          uint64_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= nq) return;
+    const int g = (int)(q[i] >> 56);
+    const uint64_t e = q[i] & ((1ull << 56) - 1);
+    const uint32_t* c = gscan + (uint64_t)g * (nblk + 1);   // exclusive prefix counts per block
+    uint64_t lo = 0, n = nblk;                              // last block b with c[b] <= e
+    while (n > 0) {
+        const uint64_t h = n >> 1;
+        if (c[lo + h] <= e) { lo += h + 1; n -= h + 1; } else n = h;
+    }
+    const uint64_t b = lo - 1;
+    uint64_t r = e - c[b];
+    uint64_t key = ~0ull;
+    for (uint64_t j = b * kCrBlk; j < s.N && j < (b + 1) * kCrBlk; ++j) {
+        if (genome_of(gt, cr_idx(s, j)) != g) continue;
+        if (r == 0) { key = cr_key(s, j) >> 1; break; }
+        --r;
+    }
+    out[i] = key;
+}
+
 template <typename T>
 __global__ __launch_bounds__(kBlock) void cr_compact_kernel(const T* __restrict__ src, const uint32_t* __restrict__ live,
                                                             const uint32_t* __restrict__ pos, uint64_t n,
@@ -293,6 +320,13 @@ hipError_t launch_cr_runs(const uint64_t* ck, const GenomeTable& gt, const uint6
 hipError_t launch_cr_kpos(const CrStream& s, const GenomeTable& gt, int g, uint64_t* K, hipStream_t st) {
     if (s.N == 0) return hipSuccess;
     hipLaunchKernelGGL(cr_kpos_kernel, cr_grid(s.N), dim3(kBlock), 0, st, s, gt, g, K);
+    return hipGetLastError();
+}
+
+hipError_t launch_cr_query(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, const uint64_t* q, uint64_t nq,
+                           uint64_t* out, hipStream_t st) {
+    if (nq == 0) return hipSuccess;
+    hipLaunchKernelGGL(cr_query_kernel, cr_grid(nq), dim3(kBlock), 0, st, s, gt, gscan, cr_blocks(s.N), q, nq, out);
     return hipGetLastError();
 }
 

@@ -128,6 +128,9 @@ struct mums_ctx {
     uint64_t tie_slots = 0;               // slots of the runs replayed by the last run (stats)
     uint64_t restarts = 0;
     std::vector<uint64_t> offset_log;     // start points after every restart (R x G)
+    std::vector<uint64_t> consumed_log;   // consumed SML positions at every restart (R x G, restart plan)
+    bool progress_on = false;             // MatchFinder::LogProgress: restate the progress text
+    std::string progress;                 // its text for the last seed stage
     hipEvent_t ev[EV_COUNT] = {};
     bool profiling = false;
     bool walk_events = false;    // ev_walk recorded by the last FindMatches
@@ -846,6 +849,8 @@ int tie_fix_stream(mums_ctx* ctx, const RsStream& s, uint64_t n, hipStream_t st)
 // hashes single-copy genomes only)
 bool wants_tie_order(const mums_ctx* ctx) { return !ctx->pairwise && (ctx->repeat_tol > 0 || ctx->enum_tol > 1); }
 
+int progress_packed(mums_ctx* ctx, const uint64_t* rec, const uint32_t* bstart, int B, uint64_t n, hipStream_t st);
+
 // MER_REPEAT_LIMIT restart (MatchFinder.cpp:253-277) and FindMatchSeeds start points
 // (MemHash.cpp:117-127) on the merged stream s of n records (restart.hip): plan the
 // restarts, then compact the live records in order into dst (records / keys + dst_idx;
@@ -868,7 +873,7 @@ int restart_fixup(mums_ctx* ctx, const RsStream& s, uint64_t n, void* dst_a, uin
     // candidates: one per group above MER_REPEAT_LIMIT (counted by the groups stage)
     const uint64_t cap = ctx->hc.repeat_limit + 16;
     const uint64_t Gu = (uint64_t)G;
-    const size_t plan_words = cap + 1 + 3 * cap * Gu + (cap + 1) / 2 + 2 * Gu + 16 + cap + cap * Gu;
+    const size_t plan_words = cap + 1 + 3 * cap * Gu + (cap + 1) / 2 + 2 * Gu + 16 + cap + 2 * cap * Gu;
     HIPCHK(ctx->rsplan.ensure(plan_words * 8 + sizeof(restart::PlanOut) + 256));
     uint64_t* d_list = ctx->rsplan.as<uint64_t>();
     unsigned long long* d_cnt = (unsigned long long*)(d_list + cap);
@@ -878,6 +883,7 @@ int restart_fixup(mums_ctx* ctx, const RsStream& s, uint64_t n, void* dst_a, uin
     restart::PlanOut* d_out = (restart::PlanOut*)(d_S0 + Gu);
     uint64_t* d_rkey = d_S0 + Gu + 16;
     uint64_t* d_rS = d_rkey + cap;
+    uint64_t* d_rC = d_rS + cap * Gu;
     HIPCHK(launch_restart_cands(w, n, d_list, d_cnt, cap, st));
     unsigned long long C = 0;
     HIPCHK(hipMemcpyAsync(&C, d_cnt, 8, hipMemcpyDeviceToHost, st));
@@ -895,6 +901,7 @@ int restart_fixup(mums_ctx* ctx, const RsStream& s, uint64_t n, void* dst_a, uin
     po.cap = C;
     po.rkey = d_rkey;
     po.rS = d_rS;
+    po.rC = d_rC;
     po.status = restart::kPlanOk;
     HIPCHK(hipMemcpyAsync(d_out, &po, sizeof(po), hipMemcpyHostToDevice, st));
     HIPCHK(launch_restart_plan(w, G, d_list, C, d_pre, d_S, d_out, st));
@@ -904,6 +911,12 @@ int restart_fixup(mums_ctx* ctx, const RsStream& s, uint64_t n, void* dst_a, uin
     ctx->restarts = po.nrestarts;
     ctx->offset_log.assign(po.nrestarts * Gu, 0);
     if (po.nrestarts) HIPCHK(hipMemcpy(ctx->offset_log.data(), d_rS, po.nrestarts * Gu * 8, hipMemcpyDeviceToHost));
+    ctx->consumed_log.assign(po.nrestarts * Gu, 0);
+    if (po.nrestarts) HIPCHK(hipMemcpy(ctx->consumed_log.data(), d_rC, po.nrestarts * Gu * 8, hipMemcpyDeviceToHost));
+    if (ctx->progress_on && s.kind == 0) {   // the stream is still whole here (compaction below)
+        const int rc = progress_packed(ctx, s.rec, s.bstart, s.B, n, st);
+        if (rc) return rc;
+    }
     if (po.nrestarts == 0 && !have_start_points(ctx)) return MUMS_OK;
     if (!ctx->ties_fixed) {
         // a start point inside a run of equal keys: which copies live depends on the SML's
@@ -933,7 +946,14 @@ int restart_fixup(mums_ctx* ctx, const RsStream& s, uint64_t n, void* dst_a, uin
 // run_pipeline's restart stage: after the groups stage saw a group above MER_REPEAT_LIMIT
 // (or with start points), fix the stream up and run the groups stage again on it.
 int restart_stage(mums_ctx* ctx, const MatchParams& mp, const ProbeSpace& ps, hipStream_t st) {
-    if (!ctx->hc.repeat_limit && !have_start_points(ctx)) return MUMS_OK;
+    ctx->progress.clear();
+    ctx->consumed_log.clear();
+    if (!ctx->hc.repeat_limit && !have_start_points(ctx)) {
+        ctx->restarts = 0;
+        if (ctx->progress_on && ctx->packed_path)
+            return progress_packed(ctx, ctx->sorted_rec, ctx->mstart.as<uint32_t>(), ctx->msd_bits, ctx->N, st);
+        return MUMS_OK;
+    }
     DevCounters* dc = ctx->counters.as<DevCounters>();
     const uint64_t rep = ctx->hc.repeat_limit;
     const uint64_t N = ctx->N;
@@ -1883,6 +1903,24 @@ int mums::ctx_table_genomes(mums_ctx* ctx, uint32_t* table_size, uint32_t* genom
 }
 
 // MemHash::SetMatchLog (MemHash.h:149; written at MemHash.cpp:238-241)
+int mums_set_progress_log(mums_ctx* ctx, int enable) {
+    if (!ctx) return MUMS_E_INVALID;
+    ctx->progress_on = enable != 0;
+    ctx->progress.clear();
+    return MUMS_OK;
+}
+
+int mums_progress_log_copy(mums_ctx* ctx, char* text, uint64_t capacity, uint64_t* length) {
+    if (!ctx) return MUMS_E_INVALID;
+    if (length) *length = ctx->progress.size();
+    if (text && capacity) {
+        const uint64_t k = std::min<uint64_t>(capacity - 1, ctx->progress.size());
+        std::memcpy(text, ctx->progress.data(), k);
+        text[k] = 0;
+    }
+    return MUMS_OK;
+}
+
 int mums_set_match_log(mums_ctx* ctx, int enable) {
     if (check_ctx(ctx)) return MUMS_E_INVALID;
     ctx->match_log = enable != 0;
@@ -2606,6 +2644,107 @@ struct PhaseClock {
     }
 };
 
+// MatchFinder::LogProgress (MatchFinder.cpp:55-56, 137-164, 296-309): the text the reference
+// writes while its merge runs.  Every MER_BUFFER_SIZE (10 000) mers read per genome from the
+// phase's start point form a buffer; exhausting one adds its size to mers_processed and prints
+// the whole percent when it changed ("N%.."), a newline when the tens digit changed.  A buffer
+// is exhausted when the merge consumes its last mer, i.e. at that mer's masked key; in a phase
+// that ends in a restart only the buffers ending at or before the plan's consumed positions
+// were exhausted (restart_plan.h).  Events are ordered by masked key, ties by genome (the
+// text can differ from the reference's only where two buffers of unequal size end in one seed
+// group and a percent boundary falls between them).  s = the whole merged stream.
+int progress_log(mums_ctx* ctx, const CrStream& s, const uint32_t* gscan, hipStream_t st) {
+    ctx->progress.clear();
+    const GenomeTable& gt = ctx->gt;
+    const int G = gt.G;
+    const uint64_t Gu = (uint64_t)G;
+    constexpr uint64_t kBuf = restart::kMerBuffer;
+    const uint64_t R = ctx->restarts;
+    if (R && ctx->consumed_log.size() != R * Gu) return fail(ctx, MUMS_E_HIP, "progress: restart plan without consumed positions");
+    struct Ev { uint64_t phase, g, size; };
+    std::vector<Ev> ev;
+    std::vector<uint64_t> q;
+    std::vector<uint64_t> S(Gu, 0), total_sp(R + 1, 0);
+    uint64_t total = 0;
+    for (int g = 0; g < G; ++g) total += gt.m[g];
+    for (uint64_t p = 0; p <= R; ++p) {
+        for (int g = 0; g < G; ++g) {
+            S[g] = p == 0 ? (g < (int)ctx->start_points.size() ? ctx->start_points[g] : 0) : ctx->offset_log[(p - 1) * Gu + g];
+            total_sp[p] += S[g];
+            const uint64_t m = gt.m[g];
+            const uint64_t cons = p < R ? ctx->consumed_log[p * Gu + g] : m;
+            for (uint64_t a = S[g]; a < m; a += kBuf) {
+                const uint64_t e = std::min(a + kBuf, m);
+                if (e > cons) break;
+                ev.push_back(Ev{p, (uint64_t)g, e - a});
+                q.push_back(((uint64_t)g << 56) | (e - 1));
+            }
+        }
+    }
+    std::vector<uint64_t> key(q.size(), 0);
+    if (!q.empty()) {
+        const uint64_t nblk = cr_blocks(s.N);
+        if (!gscan) {
+            HIPCHK(ctx->crcnt.ensure(Gu * (nblk + 1) * 4 + 256));
+            HIPCHK(ctx->tmp.ensure(std::max(ctx->tmp.cap, scan_tmp_bytes(nblk + 2))));
+            HIPCHK(launch_cr_counts(s, gt, ctx->crcnt.as<uint32_t>(), ctx->tmp.p, st));
+            gscan = ctx->crcnt.as<uint32_t>();
+        }
+        DevBuf qb;
+        HIPCHK(qb.ensure(q.size() * 16 + 64));
+        uint64_t* d_q = qb.as<uint64_t>();
+        HIPCHK(hipMemcpyAsync(d_q, q.data(), q.size() * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(launch_cr_query(s, gt, gscan, d_q, q.size(), d_q + q.size(), st));
+        HIPCHK(hipMemcpyAsync(key.data(), d_q + q.size(), q.size() * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+    }
+    std::vector<uint64_t> ord(ev.size());
+    for (uint64_t i = 0; i < ord.size(); ++i) ord[i] = i;
+    std::stable_sort(ord.begin(), ord.end(), [&](uint64_t a, uint64_t b) {
+        if (ev[a].phase != ev[b].phase) return ev[a].phase < ev[b].phase;
+        return key[a] < key[b];
+    });
+    double m_progress = -1;   // MatchFinder.cpp:143; kept across restarts
+    uint64_t processed = 0;
+    uint64_t phase = ~0ull;
+    char b[32];
+    for (uint64_t i : ord) {
+        if (ev[i].phase != phase) {
+            phase = ev[i].phase;
+            processed = total_sp[phase];   // :147 / :150-158
+        }
+        processed += ev[i].size;
+        const double old = m_progress;
+        m_progress = ((double)processed / (double)total) * 100.0;   // PROGRESS_GRANULARITY 100
+        if ((int)old != (int)m_progress) {
+            snprintf(b, sizeof b, "%d%%..", (int)((m_progress / 100.0) * 100));
+            ctx->progress += b;
+        }
+        if (((int)old / 10) != ((int)m_progress / 10)) ctx->progress += "\n";
+    }
+    return MUMS_OK;
+}
+
+// the single-context packed stream (records key_low << 32 | index, 2^B MSD buckets starting at
+// the device u32 bucket starts bstart) as a CrStream for progress_log
+int progress_packed(mums_ctx* ctx, const uint64_t* rec, const uint32_t* bstart, int B, uint64_t n, hipStream_t st) {
+    const uint64_t nd = 1ull << B;
+    std::vector<uint32_t> h32(nd + 1);
+    HIPCHK(hipMemcpyAsync(h32.data(), bstart, (nd + 1) * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    std::vector<uint64_t> h64(nd + 1);
+    for (uint64_t d = 0; d <= nd; ++d) h64[d] = B ? h32[d] : (d ? n : 0);
+    DevBuf db;
+    HIPCHK(db.ensure((nd + 1) * 8 + 64));
+    HIPCHK(hipMemcpyAsync(db.p, h64.data(), (nd + 1) * 8, hipMemcpyHostToDevice, st));
+    CrStream s{rec, db.as<uint64_t>(), (uint32_t)nd, n};
+    s.kb = (uint32_t)(2 * ctx->w + 1 - B);
+    s.ib = 32;
+    const int rc = progress_log(ctx, s, nullptr, st);
+    HIPCHK(hipStreamSynchronize(st));   // db and the query buffer are freed on return
+    return rc;
+}
+
 int stream_restart(mums_ctx* ctx, uint64_t* srec, uint64_t* other, const std::vector<uint64_t>& dstart, uint32_t kb,
                    uint32_t ib, const std::vector<RestartSeg>& segs,
                    const std::function<int(uint32_t, uint32_t*)>& bst_in, uint32_t* d_bst_out,
@@ -2635,7 +2774,8 @@ int stream_restart(mums_ctx* ctx, uint64_t* srec, uint64_t* other, const std::ve
     HIPCHK(hipStreamSynchronize(st));
     ctx->cr_cands = C;
     pc.mark("candidates");
-    if (C == 0 && !have_start_points(ctx)) return MUMS_OK;
+    ctx->consumed_log.clear();
+    if (C == 0 && !have_start_points(ctx)) return ctx->progress_on ? progress_log(ctx, s, nullptr, st) : MUMS_OK;
     if (C > ccap) return fail(ctx, MUMS_E_HIP, "restart: candidate list overflow (internal error)");
     if (ctx->parity_masked || seg_onesweep_launches(kb) < (int)((kb + 7) / 8))
         return fail(ctx, MUMS_E_UNSUPPORTED, "restart with the segment fix-up sort (MUMS_DEV_SEGFIX)");
@@ -2662,7 +2802,7 @@ int stream_restart(mums_ctx* ctx, uint64_t* srec, uint64_t* other, const std::ve
         hb[g] = gt.base[g];
     }
     const uint64_t cap = C + 16;
-    const size_t plan_words = cap + 1 + 3 * cap * Gu + (cap + 1) / 2 + 2 * Gu + 16 + cap + cap * Gu + 2 * (Gu + 1);
+    const size_t plan_words = cap + 1 + 3 * cap * Gu + (cap + 1) / 2 + 2 * Gu + 16 + cap + 2 * cap * Gu + 2 * (Gu + 1);
     HIPCHK(ctx->rsplan.ensure(plan_words * 8 + sizeof(restart::PlanOut) + 4096));
     uint64_t* p_list = ctx->rsplan.as<uint64_t>();
     uint64_t* d_pre = p_list + cap + 1;
@@ -2673,6 +2813,7 @@ int stream_restart(mums_ctx* ctx, uint64_t* srec, uint64_t* other, const std::ve
     uint64_t* d_rS = d_rkey + cap;
     uint64_t* d_dm = d_rS + cap * Gu;
     uint64_t* d_db = d_dm + Gu + 1;
+    uint64_t* d_rC = d_db + Gu + 1;
     if (C) HIPCHK(hipMemcpyAsync(p_list, d_list, C * 8, hipMemcpyDeviceToDevice, st));
     HIPCHK(hipMemcpyAsync(d_dm, hm.data(), (Gu + 1) * 8, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(d_db, hb.data(), (Gu + 1) * 8, hipMemcpyHostToDevice, st));
@@ -2682,6 +2823,7 @@ int stream_restart(mums_ctx* ctx, uint64_t* srec, uint64_t* other, const std::ve
     po.cap = C;
     po.rkey = d_rkey;
     po.rS = d_rS;
+    po.rC = d_rC;
     po.status = restart::kPlanOk;
     HIPCHK(hipMemcpyAsync(d_out, &po, sizeof(po), hipMemcpyHostToDevice, st));
     RestartWs w{};
@@ -2696,7 +2838,13 @@ int stream_restart(mums_ctx* ctx, uint64_t* srec, uint64_t* other, const std::ve
     ctx->restarts = R;
     ctx->offset_log.assign(R * Gu, 0);
     if (R) HIPCHK(hipMemcpy(ctx->offset_log.data(), d_rS, R * Gu * 8, hipMemcpyDeviceToHost));
+    ctx->consumed_log.assign(R * Gu, 0);
+    if (R) HIPCHK(hipMemcpy(ctx->consumed_log.data(), d_rC, R * Gu * 8, hipMemcpyDeviceToHost));
     pc.mark("plan");
+    if (ctx->progress_on) {   // the stream is still whole here (compaction below)
+        const int rc = progress_log(ctx, s, gscan, st);
+        if (rc) return rc;
+    }
     if (R == 0 && !have_start_points(ctx)) return MUMS_OK;
     // start points inside runs of equal keys: those runs in std::sort order (MemorySML.cpp:54)
     const uint64_t rcap = (R + 1) * Gu + 16;

@@ -388,6 +388,9 @@ uint64_t cr_blocks(uint64_t N);
 // gcnt: G x (cr_blocks(N) + 1) per-genome block counts, exclusive-scanned per genome
 hipError_t launch_cr_counts(const CrStream& s, const GenomeTable& gt, uint32_t* gcnt, void* d_scan_tmp, hipStream_t st);
 hipError_t launch_cr_ck(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, uint64_t* ck, hipStream_t st);
+// masked key of genome g's SML index e for every query g << 56 | e (gscan from launch_cr_counts)
+hipError_t launch_cr_query(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, const uint64_t* q, uint64_t nq,
+                           uint64_t* out, hipStream_t st);
 hipError_t launch_cr_cands(const CrStream& s, uint64_t* list, unsigned long long* cnt, uint64_t cap, hipStream_t st);
 hipError_t launch_cr_runs(const uint64_t* ck, const GenomeTable& gt, const uint64_t* sp, uint64_t rows, uint64_t* runs,
                           unsigned long long* nr, uint64_t cap, hipStream_t st);

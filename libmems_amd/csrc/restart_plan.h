@@ -239,6 +239,7 @@ struct PlanOut {
     uint64_t walk_steps;     // distinct keys walked for head orders (diagnostic)
     uint64_t checked;        // candidates with more than 1000 live records
     int status;
+    uint64_t* rC;            // optional: consumed SML position of every genome at restart r: rC[r * G + g]
 };
 
 // Consume the candidates (groups of > 1000 records, ascending masked keys cand[c], with
@@ -290,6 +291,8 @@ MUMS_HD inline void restart_plan(const PlanData& d, const uint64_t* cand, uint64
         const int s = cseq[c];
         const uint64_t* bp = cbp + c * (uint64_t)G;
         uint64_t* ns = out->rS + out->nrestarts * (uint64_t)G;
+        if (out->rC)   // LogProgress: buffers of that phase ending at or before these positions were exhausted
+            for (int g = 0; g < G; ++g) out->rC[out->nrestarts * (uint64_t)G + g] = consumed[g];
         for (int g = 0; g < G; ++g) {
             uint64_t v = s < G ? bp[g] : S[g];
             if (v < consumed[g]) v = consumed[g];   // don't allow it to move backwards (:271-272)

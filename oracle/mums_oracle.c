@@ -478,7 +478,37 @@ struct oracle_result {
     int64_t* mlog_s;
     uint32_t* plog_bucket;    /* seeds_only: per AddHashEntry call, its bucket ... */
     uint64_t* plog_ref;       /* ... and the global seed-mer index of the probe's first start */
+    /* LogProgress (MatchFinder.cpp:55-56, 137-164, 296-309): the text a log stream receives */
+    int prog_on;
+    double m_progress;
+    uint64_t mers_processed, total_mers;
+    char* prog;
+    size_t prog_n, prog_cap;
 };
+
+static void prog_append(oracle_result* res, const char* t) {
+    const size_t k = strlen(t);
+    if (res->prog_n + k + 1 > res->prog_cap) {
+        res->prog_cap = (res->prog_n + k + 1) * 2 + 64;
+        res->prog = (char*)realloc(res->prog, res->prog_cap);
+    }
+    memcpy(res->prog + res->prog_n, t, k + 1);
+    res->prog_n += k;
+}
+
+/* a buffer of `size` mers exhausted (MatchFinder.cpp:297-309, PROGRESS_GRANULARITY 100) */
+static void prog_event(oracle_result* res, uint64_t size) {
+    if (!res->prog_on) return;
+    res->mers_processed += size;
+    const double old = res->m_progress;
+    res->m_progress = ((double)res->mers_processed / (double)res->total_mers) * 100.0;
+    if ((int)old != (int)res->m_progress) {
+        char b[32];
+        snprintf(b, sizeof b, "%d%%..", (int)((res->m_progress / 100.0) * 100));
+        prog_append(res, b);
+    }
+    if (((int)old / 10) != ((int)res->m_progress / 10)) prog_append(res, "\n");
+}
 
 typedef struct {
     ext_ctx x;
@@ -781,6 +811,7 @@ static int search_range_lit(memhash_t* h, const oracle_params* prm, int G, bmer_
             if (merI == vn[cur]) exhausted = 1;
         }
         if (exhausted) {
+            prog_event(res, vn[cur]);   /* mers_processed += mer_vector[cur_id].size() */
             mer_baseindex[cur] += (uint32_t)vn[cur];
             uint32_t rs = MER_BUFFER_SIZE;
             if ((uint64_t)MER_BUFFER_SIZE + mer_baseindex[cur] > search_len[cur])
@@ -817,7 +848,18 @@ static void find_match_seeds(memhash_t* h, const oracle_params* prm, int G, bmer
                              const uint64_t* lens, const uint64_t* start_offsets, oracle_result* res) {
     uint64_t sp[64], sl[64];
     for (int g = 0; g < G; ++g) { sp[g] = start_offsets ? start_offsets[g] : 0; sl[g] = UINT64_MAX; }
+    /* progress counters (MatchFinder.cpp:141-148): total = the SML lengths, processed = the start offsets */
+    res->prog_on = 1;
+    res->mers_processed = 0;
+    res->total_mers = 0;
+    res->m_progress = -1;
+    for (int g = 0; g < G; ++g) {
+        res->total_mers += m[g];
+        res->mers_processed += sp[g];
+    }
     while (!search_range_lit(h, prm, G, sml, m, lens, sp, sl, res)) {
+        res->mers_processed = 0;   /* :150-158 */
+        for (int g = 0; g < G; ++g) res->mers_processed += sp[g];
         /* the offset stream line of this restart (MatchFinder.cpp:152-162) */
         res->offlog = (uint64_t*)realloc(res->offlog, (size_t)res->restarts * (size_t)G * sizeof(uint64_t));
         memcpy(res->offlog + (res->restarts - 1) * (uint64_t)G, sp, (size_t)G * sizeof(uint64_t));
@@ -1361,8 +1403,12 @@ int oracle_result_offset_log(const oracle_result* r, uint64_t* out) {
     if (r->offlog && r->restarts) memcpy(out, r->offlog, (size_t)r->restarts * (size_t)r->offlog_g * sizeof(uint64_t));
     return 0;
 }
+/* LogProgress text of the last FindMatches ("" unless the serial MemHash path ran) */
+const char* oracle_result_progress(const oracle_result* r) { return (r && r->prog) ? r->prog : ""; }
+
 void     oracle_result_free(oracle_result* r) {
     if (!r) return;
+    free(r->prog);
     free(r->lengths); free(r->starts); free(r->plog_bucket); free(r->plog_ref); free(r->offlog);
     free(r->mlog_len); free(r->mlog_s); free(r);
 }

@@ -185,6 +185,9 @@ def find_matches(seqs: Sequence[bytes], seed: int, repeat_tol: int = 0, enum_tol
         if stats["restarts"] and not parallel_compat:
             L.oracle_result_offset_log(r, offlog.ctypes.data)
         stats["offset_log"] = offlog
+        L.oracle_result_progress.restype = ctypes.c_char_p
+        L.oracle_result_progress.argtypes = [ctypes.c_void_p]
+        stats["progress"] = (L.oracle_result_progress(r) or b"").decode()
         L.oracle_result_match_log.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         ml_len = np.zeros(int(stats["mem_count"]), dtype=np.uint64)
         ml_s = np.zeros((int(stats["mem_count"]), G), dtype=np.int64)
