@@ -849,7 +849,8 @@ int tie_fix_stream(mums_ctx* ctx, const RsStream& s, uint64_t n, hipStream_t st)
 // hashes single-copy genomes only)
 bool wants_tie_order(const mums_ctx* ctx) { return !ctx->pairwise && (ctx->repeat_tol > 0 || ctx->enum_tol > 1); }
 
-int progress_packed(mums_ctx* ctx, const uint64_t* rec, const uint32_t* bstart, int B, uint64_t n, hipStream_t st);
+int progress_packed(mums_ctx* ctx, const uint64_t* rec, const uint32_t* bstart, int B, uint64_t n, hipStream_t st,
+                    const RestartWs* pw = nullptr, uint64_t* ck_build = nullptr);
 
 // MER_REPEAT_LIMIT restart (MatchFinder.cpp:253-277) and FindMatchSeeds start points
 // (MemHash.cpp:117-127) on the merged stream s of n records (restart.hip): plan the
@@ -914,7 +915,7 @@ int restart_fixup(mums_ctx* ctx, const RsStream& s, uint64_t n, void* dst_a, uin
     ctx->consumed_log.assign(po.nrestarts * Gu, 0);
     if (po.nrestarts) HIPCHK(hipMemcpy(ctx->consumed_log.data(), d_rC, po.nrestarts * Gu * 8, hipMemcpyDeviceToHost));
     if (ctx->progress_on && s.kind == 0) {   // the stream is still whole here (compaction below)
-        const int rc = progress_packed(ctx, s.rec, s.bstart, s.B, n, st);
+        const int rc = progress_packed(ctx, s.rec, s.bstart, s.B, n, st, &w);
         if (rc) return rc;
     }
     if (po.nrestarts == 0 && !have_start_points(ctx)) return MUMS_OK;
@@ -951,7 +952,8 @@ int restart_stage(mums_ctx* ctx, const MatchParams& mp, const ProbeSpace& ps, hi
     if (!ctx->hc.repeat_limit && !have_start_points(ctx)) {
         ctx->restarts = 0;
         if (ctx->progress_on && ctx->packed_path)
-            return progress_packed(ctx, ctx->sorted_rec, ctx->mstart.as<uint32_t>(), ctx->msd_bits, ctx->N, st);
+            return progress_packed(ctx, ctx->sorted_rec, ctx->mstart.as<uint32_t>(), ctx->msd_bits, ctx->N, st, nullptr,
+                                   ctx->sorted_buf ? ctx->recA.as<uint64_t>() : ctx->recB.as<uint64_t>());
         return MUMS_OK;
     }
     DevCounters* dc = ctx->counters.as<DevCounters>();
@@ -2650,10 +2652,12 @@ struct PhaseClock {
 // the whole percent when it changed ("N%.."), a newline when the tens digit changed.  A buffer
 // is exhausted when the merge consumes its last mer, i.e. at that mer's masked key; in a phase
 // that ends in a restart only the buffers ending at or before the plan's consumed positions
-// were exhausted (restart_plan.h).  Events are ordered by masked key, ties by genome (the
-// text can differ from the reference's only where two buffers of unequal size end in one seed
-// group and a percent boundary falls between them).  s = the whole merged stream.
-int progress_log(mums_ctx* ctx, const CrStream& s, const uint32_t* gscan, hipStream_t st) {
+// were exhausted (restart_plan.h).  Events are ordered by masked key; inside one seed group
+// holding buffer ends of several genomes with unequal sizes, the genomes' runs go in the
+// merge's head order (restart_plan.h head_order over the genome-major SML keys: pw->ck, else
+// built into ck_build, N slots).  s = the whole merged stream.
+int progress_log(mums_ctx* ctx, const CrStream& s, const uint32_t* gscan, hipStream_t st,
+                 const RestartWs* pw = nullptr, uint64_t* ck_build = nullptr) {
     ctx->progress.clear();
     const GenomeTable& gt = ctx->gt;
     const int G = gt.G;
@@ -2704,6 +2708,75 @@ int progress_log(mums_ctx* ctx, const CrStream& s, const uint32_t* gscan, hipStr
         if (ev[a].phase != ev[b].phase) return ev[a].phase < ev[b].phase;
         return key[a] < key[b];
     });
+    std::vector<std::pair<uint64_t, uint64_t>> groups;   // [begin, end) in ord
+    std::vector<uint64_t> gk, gu;
+    std::vector<uint32_t> gp;
+    for (uint64_t i = 0; i < ord.size();) {
+        uint64_t j = i + 1;
+        while (j < ord.size() && ev[ord[j]].phase == ev[ord[i]].phase && key[ord[j]] == key[ord[i]]) ++j;
+        uint64_t U = 0;
+        bool uneq = false;
+        for (uint64_t k = i; k < j; ++k) {
+            U |= 1ull << ev[ord[k]].g;
+            uneq = uneq || ev[ord[k]].size != ev[ord[i]].size;
+        }
+        if ((U & (U - 1)) && uneq) {
+            groups.push_back({i, j});
+            gk.push_back(key[ord[i]]);
+            gu.push_back(U);
+            gp.push_back((uint32_t)ev[ord[i]].phase);
+        }
+        i = j;
+    }
+    if (!groups.empty() && (pw || ck_build)) {
+        const uint64_t ng = groups.size();
+        DevBuf aux;
+        HIPCHK(aux.ensure(((R + 1) * Gu + 2 * ng + 2 * (Gu + 1)) * 8 + ng * 4 + ng * Gu * 4 + 1024));
+        uint64_t* d_S = aux.as<uint64_t>();
+        uint64_t* d_gk = d_S + (R + 1) * Gu;
+        uint64_t* d_gu = d_gk + ng;
+        uint64_t* d_dm = d_gu + ng;
+        uint64_t* d_db = d_dm + Gu + 1;
+        uint32_t* d_gp = (uint32_t*)(d_db + Gu + 1);
+        int* d_ord = (int*)(d_gp + ng);
+        RestartWs w{};
+        if (pw) {
+            w = *pw;
+        } else {   // gscan was built above (the queries are nonempty when groups exist)
+            HIPCHK(launch_cr_ck(s, gt, gscan, ck_build, st));
+            std::vector<uint64_t> hm(Gu + 1, 0), hb(Gu + 1, 0);
+            for (int g = 0; g < G; ++g) {
+                hm[g] = gt.m[g];
+                hb[g] = gt.base[g];
+            }
+            HIPCHK(hipMemcpyAsync(d_dm, hm.data(), (Gu + 1) * 8, hipMemcpyHostToDevice, st));
+            HIPCHK(hipMemcpyAsync(d_db, hb.data(), (Gu + 1) * 8, hipMemcpyHostToDevice, st));
+            HIPCHK(hipStreamSynchronize(st));
+            w.ck = ck_build;
+            w.dm = d_dm;
+            w.dbase = d_db;
+        }
+        std::vector<uint64_t> Sall((R + 1) * Gu, 0);
+        for (uint64_t p = 0; p <= R; ++p)
+            for (int g = 0; g < G; ++g)
+                Sall[p * Gu + g] = p == 0 ? (g < (int)ctx->start_points.size() ? ctx->start_points[g] : 0)
+                                          : ctx->offset_log[(p - 1) * Gu + g];
+        HIPCHK(hipMemcpyAsync(d_S, Sall.data(), Sall.size() * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(d_gk, gk.data(), ng * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(d_gu, gu.data(), ng * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(d_gp, gp.data(), ng * 4, hipMemcpyHostToDevice, st));
+        HIPCHK(launch_tie_heads(w, G, d_gk, d_gu, d_gp, d_S, ng, d_ord, st));
+        std::vector<int> ho(ng * Gu);
+        HIPCHK(hipMemcpyAsync(ho.data(), d_ord, ho.size() * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        std::vector<int> rank(Gu);
+        for (uint64_t x = 0; x < ng; ++x) {
+            std::fill(rank.begin(), rank.end(), G);
+            for (int k = 0; k < G && ho[x * Gu + k] >= 0; ++k) rank[ho[x * Gu + k]] = k;
+            std::stable_sort(ord.begin() + groups[x].first, ord.begin() + groups[x].second,
+                             [&](uint64_t a, uint64_t b) { return rank[ev[a].g] < rank[ev[b].g]; });
+        }
+    }
     double m_progress = -1;   // MatchFinder.cpp:143; kept across restarts
     uint64_t processed = 0;
     uint64_t phase = ~0ull;
@@ -2727,7 +2800,8 @@ int progress_log(mums_ctx* ctx, const CrStream& s, const uint32_t* gscan, hipStr
 
 // the single-context packed stream (records key_low << 32 | index, 2^B MSD buckets starting at
 // the device u32 bucket starts bstart) as a CrStream for progress_log
-int progress_packed(mums_ctx* ctx, const uint64_t* rec, const uint32_t* bstart, int B, uint64_t n, hipStream_t st) {
+int progress_packed(mums_ctx* ctx, const uint64_t* rec, const uint32_t* bstart, int B, uint64_t n, hipStream_t st,
+                    const RestartWs* pw, uint64_t* ck_build) {
     const uint64_t nd = 1ull << B;
     std::vector<uint32_t> h32(nd + 1);
     HIPCHK(hipMemcpyAsync(h32.data(), bstart, (nd + 1) * 4, hipMemcpyDeviceToHost, st));
@@ -2740,7 +2814,7 @@ int progress_packed(mums_ctx* ctx, const uint64_t* rec, const uint32_t* bstart, 
     CrStream s{rec, db.as<uint64_t>(), (uint32_t)nd, n};
     s.kb = (uint32_t)(2 * ctx->w + 1 - B);
     s.ib = 32;
-    const int rc = progress_log(ctx, s, nullptr, st);
+    const int rc = progress_log(ctx, s, nullptr, st, pw, ck_build);
     HIPCHK(hipStreamSynchronize(st));   // db and the query buffer are freed on return
     return rc;
 }
@@ -2775,7 +2849,7 @@ int stream_restart(mums_ctx* ctx, uint64_t* srec, uint64_t* other, const std::ve
     ctx->cr_cands = C;
     pc.mark("candidates");
     ctx->consumed_log.clear();
-    if (C == 0 && !have_start_points(ctx)) return ctx->progress_on ? progress_log(ctx, s, nullptr, st) : MUMS_OK;
+    if (C == 0 && !have_start_points(ctx)) return ctx->progress_on ? progress_log(ctx, s, nullptr, st, nullptr, other) : MUMS_OK;
     if (C > ccap) return fail(ctx, MUMS_E_HIP, "restart: candidate list overflow (internal error)");
     if (ctx->parity_masked || seg_onesweep_launches(kb) < (int)((kb + 7) / 8))
         return fail(ctx, MUMS_E_UNSUPPORTED, "restart with the segment fix-up sort (MUMS_DEV_SEGFIX)");
@@ -2842,7 +2916,7 @@ int stream_restart(mums_ctx* ctx, uint64_t* srec, uint64_t* other, const std::ve
     if (R) HIPCHK(hipMemcpy(ctx->consumed_log.data(), d_rC, R * Gu * 8, hipMemcpyDeviceToHost));
     pc.mark("plan");
     if (ctx->progress_on) {   // the stream is still whole here (compaction below)
-        const int rc = progress_log(ctx, s, gscan, st);
+        const int rc = progress_log(ctx, s, gscan, st, &w);
         if (rc) return rc;
     }
     if (R == 0 && !have_start_points(ctx)) return MUMS_OK;

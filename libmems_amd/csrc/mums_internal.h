@@ -369,6 +369,10 @@ hipError_t launch_restart_plan(const RestartWs& w, int G, const uint64_t* d_cand
                                uint64_t* d_S, restart::PlanOut* d_out, hipStream_t st);
 // live records (SML index >= start point of their key's phase) compacted in order into
 // dst (records, or keys + dst_idx); kind 0 also writes the new bucket starts
+// LogProgress tie groups (w.ck / w.dm / w.dbase): ord[i * G ..] = head order of the genomes
+// gu[i] at masked key gk[i] in phase gp[i] (start points Sall[gp * G ..]), -1 padded
+hipError_t launch_tie_heads(const RestartWs& w, int G, const uint64_t* gk, const uint64_t* gu, const uint32_t* gp,
+                            const uint64_t* Sall, uint64_t ng, int* ord, hipStream_t st);
 hipError_t launch_restart_compact(const RsStream& s, uint64_t n, int G, const RestartWs& w, const uint64_t* d_rkey,
                                   uint64_t R, const uint64_t* d_rS, const uint64_t* d_S0, void* dst_a, uint32_t* dst_idx,
                                   uint32_t* dst_bstart, uint32_t* d_total, hipStream_t st);

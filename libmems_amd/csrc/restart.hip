@@ -222,6 +222,37 @@ hipError_t launch_restart_plan(const RestartWs& w, int G, const uint64_t* d_cand
     return hipGetLastError();
 }
 
+// LogProgress tie groups: the head order (restart_plan.h head_order) of the genomes U of a
+// group at masked key K in the SearchRange call whose start points are S (phase p)
+__global__ void tie_heads_kernel(PlanData d, const uint64_t* __restrict__ gk, const uint64_t* __restrict__ gu,
+                                 const uint32_t* __restrict__ gp, const uint64_t* __restrict__ Sall, uint64_t ng,
+                                 int* __restrict__ ord) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ng) return;
+    const int G = d.G;
+    const uint64_t* S = Sall + (uint64_t)gp[i] * G;
+    uint64_t a[restart::kMaxGenomes];
+    for (int g = 0; g < G; ++g) {
+        a[g] = 0;
+        if ((gu[i] >> g) & 1) {
+            const uint64_t lb = restart::lower_bound_u64(d.ck + d.base[g], d.m[g], gk[i] << 1);
+            a[g] = lb > S[g] ? lb : S[g];
+        }
+    }
+    uint64_t steps = 0;
+    int* o = ord + i * (uint64_t)G;
+    const int n = restart::head_order(d, gu[i], a, S, o, &steps);
+    for (int k = n; k < G; ++k) o[k] = -1;
+}
+
+hipError_t launch_tie_heads(const RestartWs& w, int G, const uint64_t* gk, const uint64_t* gu, const uint32_t* gp,
+                            const uint64_t* Sall, uint64_t ng, int* ord, hipStream_t st) {
+    if (ng == 0) return hipSuccess;
+    const PlanData d{G, w.dm, w.dbase, w.ck};
+    hipLaunchKernelGGL(tie_heads_kernel, grid_of(ng), dim3(kBlock), 0, st, d, gk, gu, gp, Sall, ng, ord);
+    return hipGetLastError();
+}
+
 hipError_t launch_restart_compact(const RsStream& s, uint64_t n, int G, const RestartWs& w, const uint64_t* d_rkey,
                                   uint64_t R, const uint64_t* d_rS, const uint64_t* d_S0, void* dst_a, uint32_t* dst_idx,
                                   uint32_t* dst_bstart, uint32_t* d_total, hipStream_t st) {

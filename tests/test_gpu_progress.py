@@ -45,7 +45,7 @@ def test_progress_masked(gpu_lib, oracle_mod):
     check(gpu_lib, oracle_mod, oracle_mod.generate(4, 400_000, 0.02, 3), 15, "MaskedMemHash", 0b1011)
 
 
-@pytest.mark.parametrize("sp", [[0, 0, 0], [1000, 25_000, 7], [150_000, 0, 190_000]])
+@pytest.mark.parametrize("sp", [[0, 0, 0], [1000, 25_000, 7], [150_000, 0, 190_000], [9_990, 19_990, 29_990]])
 def test_progress_start_points(gpu_lib, oracle_mod, sp):
     check(gpu_lib, oracle_mod, oracle_mod.generate(3, 200_000, 0.02, 777), 15, start_points=sp)
 
