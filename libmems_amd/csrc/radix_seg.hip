@@ -27,10 +27,10 @@ constexpr int kRounds = kTile / kBlock;  // 16
 constexpr int kWaves = kBlock / 64;
 constexpr int kDigits = 256;
 #ifndef MUMS_SORT_BLOCK
-#define MUMS_SORT_BLOCK 512
+#define MUMS_SORT_BLOCK 768
 #endif
 #ifndef MUMS_SORT_TILE
-#define MUMS_SORT_TILE 8192
+#define MUMS_SORT_TILE 9216
 #endif
 #ifndef MUMS_SORT_NT
 #define MUMS_SORT_NT 0      // bit 0: non-temporal record loads, bit 1: non-temporal stores
@@ -353,7 +353,9 @@ __device__ __forceinline__ void onesweep_load(const uint64_t* __restrict__ rin, 
 // order = tiles[c].order, see claim_order_kernel), so every tile it waits on was
 // claimed earlier by a resident block.  OB threads x kIPT records per tile; the first
 // 256 threads also own one digit each for the look-back and the digit starts.
-template <int OB, int kIPT>
+// kAlias: the per-wave digit counts live in the record exchange buffer (every lane folds
+// its slot base into its ranks before the exchange), so a tile costs kT * 8 B + 4 KB of LDS.
+template <int OB, int kIPT, bool kAlias = false>
 __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __restrict__ rin,
                                                           uint64_t* __restrict__ rout,
                                                           const SegTile* __restrict__ tiles, uint32_t nclaims,
@@ -364,8 +366,10 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
     constexpr int kT = kIPT * OB;
     constexpr int kW = OB / 64;
     static_assert(OB >= kDigits, "one thread per digit");
+    static_assert(!kAlias || kW * kDigits * 4 <= kT * 8, "counts fit in the exchange buffer");
     __shared__ uint64_t srec[kT];
-    __shared__ uint32_t wcnt[kW][kDigits];
+    __shared__ uint32_t wcnt_own[kAlias ? 1 : kW][kDigits];
+    uint32_t (*wcnt)[kDigits] = kAlias ? reinterpret_cast<uint32_t (*)[kDigits]>(srec) : wcnt_own;
     __shared__ uint32_t lstart[kDigits];
     __shared__ uint32_t gofs[kDigits];
     __shared__ uint32_t s_w[kDigits / 64];
@@ -503,6 +507,21 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
 #endif
     }
     __syncthreads();
+    if constexpr (kAlias) {   // slots first: the exchange overwrites the counts
+        #pragma unroll
+        for (int r = 0; r < kIPT; ++r) {
+            const uint32_t dg = (uint32_t)(key[r] >> shift) & 0xFFu;
+#if MUMS_OS_FUSED
+            rank[r] += wcnt[wv][dg];
+#else
+            rank[r] += lstart[dg] + wcnt[wv][dg];
+#endif
+        }
+        __syncthreads();
+        #pragma unroll
+        for (int r = 0; r < kIPT; ++r)
+            if (qof(r) < d.count) srec[rank[r]] = key[r];
+    } else {
     #pragma unroll
     for (int r = 0; r < kIPT; ++r) {
         const uint32_t q = qof(r);
@@ -514,6 +533,7 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
             srec[lstart[dg] + wcnt[wv][dg] + rank[r]] = key[r];
 #endif
         }
+    }
     }
     __syncthreads();
     #pragma unroll
@@ -1115,8 +1135,30 @@ static size_t seg_build_tmp_bytes(uint64_t nb) { return ((nb + 128) * 4 + scan_t
 // segments of more than kSfLds records, + the forced test entries (starts at multiples of 64)
 static uint64_t segfix_cap(uint64_t n) { return n / 32 + 2 * ((n + kSfTile - 1) / kSfTile + 2); }
 
+// development A/B of the onesweep block shape (MUMS_DEV_OS_VARIANT, read once):
+// 0 = <768 threads, 12 records> (9216-record tiles, the per-wave counts aliased into the
+// exchange buffer: 76 KB, two blocks and 24 waves per CU, 79 VGPRs), 1-6 and 8 aliased too:
+// 1 <512, 16> (8192), 2 <512, 12> and 3 <384, 16> (6144-record tiles, 52 KB: three blocks per
+// CU), 4 <256, 16> and 5 <512, 8> (4096, 36 KB: four per CU), 6 <1024, 8> (8192, 32 waves per
+// CU), 8 <640, 14> (8960); 7 = the round-2 shape <512, 16> with the counts in their own LDS
+// (8192, 78 KB).  Measured on C3 in one call: 0 is 2.5 % faster per pass than 7 and 1;
+// 6144- and 4096-record tiles (more blocks per CU) are 6-14 % slower: the digit runs a tile
+// stores get shorter.
+static int os_variant() {
+    static const int v = [] {
+        const char* e = getenv("MUMS_DEV_OS_VARIANT");
+        const int x = e ? atoi(e) : 0;
+        return x >= 0 && x <= 8 ? x : 0;
+    }();
+    return v;
+}
+static int os_tile() {
+    static const int t[9] = {kSortTile, 8192, 6144, 6144, 4096, 4096, 8192, 8192, 8960};
+    return MUMS_SORT_PERSIST ? kSortTile : t[os_variant()];
+}
+
 size_t onesweep_tmp_bytes(uint64_t n, int msd_bits, int key_bits) {
-    const uint64_t ub = seg_tiles_upper(n, msd_bits, kSortTile);
+    const uint64_t ub = seg_tiles_upper(n, msd_bits, os_tile());
     const int npass = (key_bits + 7) / 8;
     const uint64_t nb = 1ull << msd_bits;
     return (ub * kDigits * (uint64_t)npass + 2 * nb * npass * kDigits + 64 + 64) * 4 + ub * sizeof(SegTile) + 256 +
@@ -1180,7 +1222,8 @@ hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key
     if (n == 0 || npass == 0) return hipSuccess;
     if (nkd > 4) return hipErrorInvalidValue;
     const uint64_t nb = 1ull << msd_bits;
-    const uint64_t ub = seg_tiles_upper(n, msd_bits, kSortTile);
+    const int tile = os_tile();
+    const uint64_t ub = seg_tiles_upper(n, msd_bits, tile);
     uint32_t* status = (uint32_t*)d_tmp;                       // [npass][ub][256]
     uint32_t* ghist = status + ub_status(ub, npass);           // [nb][npass][256]
     uint32_t* dbase = ghist + nb * npass * kDigits;            // [nb][npass][256]
@@ -1190,7 +1233,7 @@ hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key
     void* btmp = (void*)((char*)stiles + ((ub * sizeof(SegTile) + 255) & ~(size_t)255));
     hipError_t e = hipMemsetAsync(status, 0, zero_bytes, st);
     if (e != hipSuccess) return e;
-    e = build_seg_tiles_from_starts(d_bstart, msd_bits, n, stiles, counters + 32, btmp, st, kSortTile);
+    e = build_seg_tiles_from_starts(d_bstart, msd_bits, n, stiles, counters + 32, btmp, st, tile);
     if (e != hipSuccess) return e;
     const unsigned gblocks = (unsigned)((ub + kGhistTilesPerBlock - 1) / kGhistTilesPerBlock);
     // the histogram read counts digit 0 only when every later pass's digits are
@@ -1226,10 +1269,26 @@ hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key
                            stiles, (uint32_t)ub, key_shift + 8 * p, p, npass, dbase,
                            status + (uint64_t)p * ub * kDigits, counters + p, d_err);
 #else
-        hipLaunchKernelGGL((seg_onesweep_kernel<kSortBlock, kSortTile / kSortBlock>), dim3((unsigned)ub),
-                           dim3(kSortBlock), 0, st, src, dst, stiles, (uint32_t)ub, key_shift + 8 * p, p, npass,
-                           dbase, status + (uint64_t)p * ub * kDigits, counters + p, d_err,
-                           (nexthist && p + 1 < npass) ? ghist : (uint32_t*)nullptr);
+        {
+            uint32_t* gn = (nexthist && p + 1 < npass) ? ghist : (uint32_t*)nullptr;
+            uint32_t* sp = status + (uint64_t)p * ub * kDigits;
+            const int sh = key_shift + 8 * p;
+#define MUMS_OS_LAUNCH(OB, IPT, AL)                                                                               \
+    hipLaunchKernelGGL((seg_onesweep_kernel<OB, IPT, AL>), dim3((unsigned)ub), dim3(OB), 0, st, src, dst, stiles, \
+                       (uint32_t)ub, sh, p, npass, dbase, sp, counters + p, d_err, gn)
+            switch (os_variant()) {
+            case 1: MUMS_OS_LAUNCH(512, 16, true); break;
+            case 2: MUMS_OS_LAUNCH(512, 12, true); break;
+            case 3: MUMS_OS_LAUNCH(384, 16, true); break;
+            case 4: MUMS_OS_LAUNCH(256, 16, true); break;
+            case 5: MUMS_OS_LAUNCH(512, 8, true); break;
+            case 6: MUMS_OS_LAUNCH(1024, 8, true); break;
+            case 7: MUMS_OS_LAUNCH(512, 16, false); break;
+            case 8: MUMS_OS_LAUNCH(640, 14, true); break;
+            default: MUMS_OS_LAUNCH(kSortBlock, kSortTile / kSortBlock, true); break;
+            }
+#undef MUMS_OS_LAUNCH
+        }
 #endif
         e = hipGetLastError();
         if (e != hipSuccess) return e;
