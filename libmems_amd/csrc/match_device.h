@@ -331,10 +331,12 @@ __device__ __forceinline__ bool probe_fast_raw(const uint64_t (&x)[MG + 1], cons
     using IdxT = typename std::conditional<(IB > 32), uint64_t, uint32_t>::type;
     IdxT sref = 0;
     bool dup = false;
-    uint32_t gk[MG + 1];
-    IdxT sk[MG + 1];
+    // record MG only bounds the run: an accepted probe has cnt <= G <= MG records, so it is
+    // never a member (cnt = MG + 1 is rejected below whatever mask, dup and off hold)
+    uint32_t gk[MG];
+    IdxT sk[MG];
     #pragma unroll
-    for (int k = 0; k <= MG; ++k) {
+    for (int k = 0; k < MG; ++k) {
         const IdxT idx = (IdxT)(x[k] & ((1ull << IB) - 1));
         uint32_t g = 0;
         IdxT b = 0;
@@ -357,7 +359,7 @@ __device__ __forceinline__ bool probe_fast_raw(const uint64_t (&x)[MG + 1], cons
     }
     int64_t off = 0;
     #pragma unroll
-    for (int k = 0; k <= MG; ++k) {
+    for (int k = 0; k < MG; ++k) {
         const bool use = (uint32_t)k < cnt && gk[k] != gref;
         const int64_t sv = (int64_t)sk[k], sr = (int64_t)sref;
         const int64_t term = (((uint32_t)(x[k] >> IB) & 1u) != pref) ? (-sv - sr - (int64_t)L) : (sv - sr);

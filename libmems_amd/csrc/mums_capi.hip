@@ -2946,7 +2946,9 @@ int stream_restart(mums_ctx* ctx, uint64_t* srec, uint64_t* other, const std::ve
                 // and try again (2 x 3 Gbp: ~135 GB of tie workspace beside 96 GB of records)
                 (void)hipGetLastError();
                 HIPCHK(hipStreamSynchronize(st));
+                pc.mark("tie workspace (first try)");
                 release_find_buffers(ctx);
+                pc.mark("FindMatches buffers freed");
                 if (ctx->tiebuf.ensure(tie_ws_bytes(m, 1)) != hipSuccess)
                     return fail(ctx, MUMS_E_NOMEM, "restart: no device memory for the SortedMerList tie order of a "
                                                    "genome");
@@ -2978,6 +2980,7 @@ int stream_restart(mums_ctx* ctx, uint64_t* srec, uint64_t* other, const std::ve
         }
         HIPCHK(hipStreamSynchronize(st));
         ctx->tiebuf.release();
+        pc.mark("tie workspace freed");
     }
     // every segment's live records (SML index >= the start point of its key's phase),
     // compacted into `other` at the segment's base (the SMLs there are dead now)

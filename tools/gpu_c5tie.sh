@@ -1,0 +1,7 @@
+#!/bin/bash
+# restart-phase timing of the N-gapped config-5 FindMatches at w21 (tie workspace split)
+set -o pipefail
+T=${1:-r03p}
+mkdir -p gpurun_out/$T
+MUMS_DEV_RESTART_TIMING=1 timeout -k 10 500 python -u tools/bench_c5.py --weight 21 --gaps 100 --steps 1 --find-steps 2 > gpurun_out/$T/c5_w21_gaps.log 2>&1 || { tail -20 gpurun_out/$T/c5_w21_gaps.log; exit 31; }
+grep -v "tie replay level" gpurun_out/$T/c5_w21_gaps.log | grep -E "restart phase|FindMatches" | tail -30
