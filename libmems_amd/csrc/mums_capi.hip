@@ -126,6 +126,9 @@ struct mums_ctx {
     uint64_t shard_n = 0;                 // its records
     bool ties_fixed = false;              // the stream holds every run of equal keys in std::sort order
     uint64_t tie_slots = 0;               // slots of the runs replayed by the last run (stats)
+    // seed-stage-only chunked runs keep the tie workspace between calls when memory allows:
+    // its hipMalloc is 3-4 s at 2 x 3 Gbp (135 GB), the replay itself 0.15 s
+    bool keep_tiebuf = false;
     uint64_t restarts = 0;
     std::vector<uint64_t> offset_log;     // start points after every restart (R x G)
     std::vector<uint64_t> consumed_log;   // consumed SML positions at every restart (R x G, restart plan)
@@ -2631,6 +2634,9 @@ void release_find_buffers(mums_ctx* ctx) {
     ctx->M = 0;
 }
 
+// free device memory left beside a kept tie workspace (the chunk loop's buffers)
+constexpr size_t kKeepTieFree = 24ull << 30;
+
 // development: MUMS_DEV_RESTART_TIMING prints the wall time of every restart phase
 struct PhaseClock {
     bool on;
@@ -2979,7 +2985,9 @@ int stream_restart(mums_ctx* ctx, uint64_t* srec, uint64_t* other, const std::ve
             pc.mark("tie order of one genome");
         }
         HIPCHK(hipStreamSynchronize(st));
-        ctx->tiebuf.release();
+        size_t free_b = 0, total_b = 0;
+        if (!(ctx->keep_tiebuf && hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b >= kKeepTieFree))
+            ctx->tiebuf.release();
         pc.mark("tie workspace freed");
     }
     // every segment's live records (SML index >= the start point of its key's phase),
@@ -3228,7 +3236,9 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
         } else {
             for (uint32_t d = 0; d < nd; ++d) dstart[d + 1] = dstart[d] + tot[d];
         }
+        ctx->keep_tiebuf = stage < MUMS_STAGE_ALL;   // FindMatches needs the memory for its tail
         rc = chunked_restart(ctx, sbuf, dstart, cbase, nbc, nch, n_live, &live_rec, chunk_starts, st);
+        ctx->keep_tiebuf = false;
         if (rc) return rc;
     }
     for (uint32_t c = 0; c < nch; ++c) {
