@@ -132,3 +132,26 @@ def test_streaming_layout_refuses_start_points(gpu_lib, oracle_mod, force_chunks
     with pytest.raises(gpu_lib.MumsError) as ei:
         run_gpu(gpu_lib, seqs, oracle_mod.get_seed(17), start_points=[5, 6, 7])
     assert ei.value.code == gpu_lib.MUMS_E_UNSUPPORTED
+
+
+def test_tie_workspace_kept_across_seed_stage_calls(gpu_lib, oracle_mod, force_chunks):
+    """Seed-stage-only chunked runs keep the tie workspace (keep_tiebuf, mums_capi.hip); the
+    FindMatches calls after them reuse it: the same MatchList as the oracle every time."""
+    seqs = repeat_inputs.n_gapped(G=3, n=200_000, gaps=((40_000, 3000), (120_000, 3000)), shift=500, seed=1)
+    seed = oracle_mod.get_seed(19)
+    ref_len, ref_starts, ref = oracle_mod.find_matches(seqs, seed)
+    assert ref["restarts"] > 0
+    force_chunks(sum(len(s) for s in seqs) // 2 + 20_000)
+    with gpu_lib.MemHash(0) as mh:
+        mh.SetSeed(seed)
+        for s in seqs:
+            mh.AddSequence(s)
+        for _ in range(2):
+            mh.FindStage(gpu_lib.STAGE_SEEDS)
+        for _ in range(2):
+            ml = mh.FindMatches()
+            st = mh.stats()
+            assert st["chunks"] >= 2 and st["restarts"] == ref["restarts"]
+            assert (ml.lengths == ref_len).all() and (ml.starts == ref_starts).all()
+        mh.FindStage(gpu_lib.STAGE_SEEDS)
+        assert (mh.FindMatches().starts == ref_starts).all()
