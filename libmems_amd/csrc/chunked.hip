@@ -111,6 +111,7 @@ __device__ __forceinline__ void cr_block_ranks(const CrStream& s, const GenomeTa
             for (int w = 0; w < kBlock / 64; ++w) t += wcnt[w][tid];
             base[tid] += t;
         }
+        __syncthreads();   // wcnt is read above before the next round zeroes it
     }
 }
 

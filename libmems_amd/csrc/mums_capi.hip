@@ -129,6 +129,7 @@ struct mums_ctx {
     // seed-stage-only chunked runs keep the tie workspace between calls when memory allows:
     // its hipMalloc is 3-4 s at 2 x 3 Gbp (135 GB), the replay itself 0.15 s
     bool keep_tiebuf = false;
+    bool tiebuf_kept = false;             // the last chunked seed-stage-only call kept tiebuf
     uint64_t restarts = 0;
     std::vector<uint64_t> offset_log;     // start points after every restart (R x G)
     std::vector<uint64_t> consumed_log;   // consumed SML positions at every restart (R x G, restart plan)
@@ -1559,6 +1560,10 @@ int mums_find_stage(mums_ctx* ctx, int stage) {
         // undefined behaviour in the reference, refused here
         return fail(ctx, MUMS_E_UNSUPPORTED, "start points (FindMatchesFromPosition) in the ParallelMemHash compat mode: "
                                              "the reference hashes them into an unsized thread table");
+    // the chunked mode may keep its (config-5-sized) tie workspace between seed-stage-only
+    // calls; any other pipeline sizes its own
+    if (!big && ctx->tiebuf_kept) ctx->tiebuf.release();
+    ctx->tiebuf_kept = false;
     if (ctx->pairwise || ctx->enum_tol > 1) return run_pipeline_pairwise(ctx, stage);
     if (ctx->pcompat) return run_pipeline_compat(ctx, stage);
     return big ? run_pipeline_chunked(ctx, stage) : run_pipeline(ctx, stage);
@@ -2296,11 +2301,11 @@ int mums_shard_restart_plan(mums_ctx* ctx, uint64_t* d_stream, uint32_t nranks, 
     if (need > capacity_bytes) return fail(ctx, MUMS_E_INVALID, "restart plan: output buffer too small");
     if (N && !d_stream) return fail(ctx, MUMS_E_INVALID, "null stream");
     const uint64_t n_own = ctx->N;
-    ctx->N = N;   // stream_restart's stream: the whole merged stream
     HIPCHK(ctx->crall.ensure((N + 64) * 8));
     uint64_t nbst = 0;
     for (const RestartSeg& g : segs) nbst += g.nb + 1;
     HIPCHK(ctx->rsbst.ensure(nbst * 4 + 64));
+    ctx->N = N;   // stream_restart's stream: the whole merged stream (restored below)
     std::vector<uint64_t> n_live;
     bool live = false;
     std::vector<uint32_t> hb;
@@ -2676,7 +2681,7 @@ int progress_log(mums_ctx* ctx, const CrStream& s, const uint32_t* gscan, hipStr
     std::vector<uint64_t> q;
     std::vector<uint64_t> S(Gu, 0), total_sp(R + 1, 0);
     uint64_t total = 0;
-    for (int g = 0; g < G; ++g) total += gt.m[g];
+    for (int g = 0; g < G; ++g) total += gt.n[g];   // MatchFinder.cpp:146: SortedMerList::Length() = seq_len
     for (uint64_t p = 0; p <= R; ++p) {
         for (int g = 0; g < G; ++g) {
             S[g] = p == 0 ? (g < (int)ctx->start_points.size() ? ctx->start_points[g] : 0) : ctx->offset_log[(p - 1) * Gu + g];
@@ -2988,6 +2993,8 @@ int stream_restart(mums_ctx* ctx, uint64_t* srec, uint64_t* other, const std::ve
         size_t free_b = 0, total_b = 0;
         if (!(ctx->keep_tiebuf && hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b >= kKeepTieFree))
             ctx->tiebuf.release();
+        else
+            ctx->tiebuf_kept = true;
         pc.mark("tie workspace freed");
     }
     // every segment's live records (SML index >= the start point of its key's phase),
@@ -3241,6 +3248,9 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
         ctx->keep_tiebuf = false;
         if (rc) return rc;
     }
+    // a workspace kept by an earlier seed-stage-only call and not reused above (no restart,
+    // no tie run) must not stay beside the FindMatches tail
+    if (stage == MUMS_STAGE_ALL) ctx->tiebuf.release();
     for (uint32_t c = 0; c < nch; ++c) {
         const uint32_t dlo = c * nbc8;
         uint64_t n_c = 0;

@@ -195,6 +195,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     __shared__ uint32_t s_kept;
     static_assert(kTileWords * 4 <= kTile * 8, "words alias srec");
     static_assert(kTile <= 65535, "16-bit wave digit offsets");
+    static_assert(kSide == 0 || kTile <= 4096, "side digits sit in bits 28-31 above a 12-bit rank");
     uint32_t* words = reinterpret_cast<uint32_t*>(srec);
     const uint32_t t = blockIdx.x;
     const int g = tile_genome(gt, t);

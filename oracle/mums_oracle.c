@@ -848,13 +848,14 @@ static void find_match_seeds(memhash_t* h, const oracle_params* prm, int G, bmer
                              const uint64_t* lens, const uint64_t* start_offsets, oracle_result* res) {
     uint64_t sp[64], sl[64];
     for (int g = 0; g < G; ++g) { sp[g] = start_offsets ? start_offsets[g] : 0; sl[g] = UINT64_MAX; }
-    /* progress counters (MatchFinder.cpp:141-148): total = the SML lengths, processed = the start offsets */
+    /* progress counters (MatchFinder.cpp:141-148): total = sar_table[i]->Length(), the sequence lengths
+       (header.length = seq_len, SortedMerList.cpp:814 -- not SMLLength), processed = the start offsets */
     res->prog_on = 1;
     res->mers_processed = 0;
     res->total_mers = 0;
     res->m_progress = -1;
     for (int g = 0; g < G; ++g) {
-        res->total_mers += m[g];
+        res->total_mers += lens[g];
         res->mers_processed += sp[g];
     }
     while (!search_range_lit(h, prm, G, sml, m, lens, sp, sl, res)) {

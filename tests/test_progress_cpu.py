@@ -56,7 +56,7 @@ def model_text(seqs, seed, start_points=None) -> str:
         sml = oracle.build_sml(s, seed)
         masked.append(keys[sml] >> np.uint64(1) if len(sml) else keys)
         m = len(sml)
-        total += m
+        total += len(s)   # Length() = sequence length (MatchFinder.cpp:146, SortedMerList.cpp:814)
         for a in range(sp[g], m, 10_000):
             e = min(a + 10_000, m)
             ev.append((int(masked[g][e - 1]), g, e - a))
@@ -107,5 +107,19 @@ def test_progress_text_shape():
     _, _, ref = oracle.find_matches(seqs, oracle.get_seed(15))
     t = ref["progress"]
     vals = [int(x) for x in t.replace("\n", "").split("%..") if x]
-    assert vals == sorted(vals) and vals[0] == 0 and vals[-1] == 100
-    assert t.count("\n") == 10 and t.endswith("100%..\n")
+    # total = sequence lengths (MatchFinder.cpp:146): a linear genome's last L-1 positions
+    # hold no mer, so the text stops at 99%
+    assert vals == sorted(vals) and vals[0] == 0 and vals[-1] == 99
+    assert t.count("\n") == 9 and t.endswith("90%..\n" + "".join(f"{v}%.." for v in range(91, 100)))
+
+
+def test_progress_total_is_sequence_length():
+    """MatchFinder.cpp:146 sums SortedMerList::Length() = header.length = seq_len
+    (SortedMerList.cpp:814), not SMLLength = n - L + 1: on linear sequences the
+    processed / total ratio ends below 1, so the text never prints a final 100%."""
+    seqs = oracle.generate(2, 30_000, 0.01, 7)
+    seed = oracle.get_seed(15)
+    _, _, ref = oracle.find_matches(seqs, seed)
+    assert ref["restarts"] == 0
+    assert "100%" not in ref["progress"] and "99%.." in ref["progress"]
+    assert model_text(seqs, seed) == ref["progress"]
