@@ -315,6 +315,11 @@ class MemHash:
             self._keepalive.append(seq)
             self._check(self._lib.mums_add_genome_device(self._ctx, ctypes.c_void_p(seq.data_ptr()), seq.numel()))
             return
+        if hasattr(seq, "data_ptr") and hasattr(seq, "is_pinned") and seq.is_contiguous() and seq.element_size() == 1:
+            # a host torch uint8 tensor (e.g. pinned): copied by the library straight from its storage
+            self._check(self._lib.mums_add_genome(self._ctx, ctypes.c_char_p(seq.data_ptr()) if seq.numel() else None,
+                                                  seq.numel()))
+            return
         if isinstance(seq, str):
             seq = seq.encode()
         b = bytes(seq)

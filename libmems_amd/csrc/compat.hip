@@ -18,11 +18,15 @@
 //   2. compat_breaks_kernel   chunk starts on the longest SML (sequential walk)
 //   3. compat_find_kernel     FindMer (bsearch) of each break mer in the other SMLs
 //   4. compat_chunk_keys      chunk of every record -> key2
-//   5. compat_merge_kernel    MergeTable: re-add each bucket's entries in vector order
+//   5. compat_cand / fire /   MER_REPEAT_LIMIT inside a chunk: SearchRange returns false and
+//      drop kernels           ParallelMemHash.cpp:97 ignores it, so the rest of that chunk is
+//                             never searched -- its records from the firing group on are dropped
+//   6. compat_merge_kernel    MergeTable: re-add each bucket's entries in vector order
 #include <hip/hip_runtime.h>
 
 #include "match_device.h"
 #include "mums_internal.h"
+#include "restart_plan.h"
 
 namespace mums {
 namespace {
@@ -102,10 +106,12 @@ __global__ void compat_find_kernel(const uint64_t* __restrict__ sk, GenomeTable 
     cs[(uint64_t)k * G + g] = cur;
 }
 
-// chunk of SML index r of genome g = last k with cs[k][g] <= r (cs[0][g] = 0)
+// chunk of SML index r of genome g = last k with cs[k][g] <= r (cs[0][g] = 0); ck (optional)
+// keeps the genome-major SMLs' keys without the genome bits for the truncation plan
 __global__ void compat_chunk_keys_kernel(const uint64_t* __restrict__ sk, const uint32_t* __restrict__ sv, uint64_t N,
                                          GenomeTable gt, int kbits, const uint64_t* __restrict__ cs, uint32_t nch,
-                                         uint64_t* __restrict__ key2, uint32_t* __restrict__ val2) {
+                                         uint64_t* __restrict__ key2, uint32_t* __restrict__ val2,
+                                         uint64_t* __restrict__ ck) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= N) return;
     const uint64_t kmask = (kbits >= 64) ? ~0ull : ((1ull << kbits) - 1);
@@ -121,6 +127,108 @@ __global__ void compat_chunk_keys_kernel(const uint64_t* __restrict__ sk, const 
     }
     key2[j] = ((uint64_t)lo << kbits) | (x & kmask);
     val2[j] = sv[j];
+    if (ck) ck[j] = x & kmask;
+}
+
+// MER_REPEAT_LIMIT inside a chunk.  Candidates: (chunk, masked key) groups of more than
+// 1000 records in the chunk-major stream -- the stream index of every such group's first
+// record (key2 >> 1 = chunk, masked key).
+__global__ void compat_cand_kernel(const uint64_t* __restrict__ key2, uint64_t N, uint64_t* __restrict__ list,
+                                   unsigned long long* __restrict__ cnt, uint64_t cap) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= N) return;
+    const uint64_t v = key2[j] >> 1;
+    if (j > 0 && (key2[j - 1] >> 1) == v) return;
+    const uint64_t e = j + restart::kRepeatLimit;
+    if (e >= N || (key2[e] >> 1) != v) return;
+    const unsigned long long k = atomicAdd(cnt, 1ull);
+    if (k < cap) list[k] = j;
+}
+
+// Per candidate: does SearchRange's check (MatchFinder.cpp:253) fire on this group inside its
+// chunk?  The chunk's SearchRange (ParallelMemHash.cpp:97) reads genome g from
+// S = cs[i][g] for search_len = cs[i+1][g] - cs[i][g] records (the last chunk: to the SML's
+// end) in MER_BUFFER_SIZE buffers from S; the group is collected genome run by genome run
+// in the head order of restart_plan.h, and the check precedes every collection step.
+// out[c] = 1 when it fires; cend[c] = stream index of the chunk's end (first record of
+// chunk i + 1).
+__global__ void compat_fire_kernel(restart::PlanData d, const uint64_t* __restrict__ key2, uint64_t N, int kbits,
+                                   const uint64_t* __restrict__ cand, uint64_t C, const uint64_t* __restrict__ cs,
+                                   uint32_t nch, uint32_t* __restrict__ out, uint64_t* __restrict__ cend) {
+    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const int G = d.G;
+    const uint64_t j = cand[c];
+    const uint64_t x2 = key2[j];
+    const uint32_t i = (uint32_t)(x2 >> kbits);
+    const uint64_t K = (x2 & ((1ull << kbits) - 1)) >> 1;
+    uint64_t S[restart::kMaxGenomes], a[restart::kMaxGenomes], b[restart::kMaxGenomes], E[restart::kMaxGenomes];
+    uint64_t U = 0;
+    for (int g = 0; g < G; ++g) {
+        const uint64_t m = d.m[g];
+        S[g] = cs[(uint64_t)i * G + g];
+        E[g] = i + 1 < nch ? cs[(uint64_t)(i + 1) * G + g] : m;
+        if (S[g] > m) S[g] = m;
+        if (E[g] > m) E[g] = m;
+        if (E[g] < S[g]) E[g] = S[g];
+        const uint64_t* ag = d.ck + d.base[g];
+        const uint64_t lo = restart::lower_bound_u64(ag, m, K << 1), hi = restart::lower_bound_u64(ag, m, (K + 1) << 1);
+        a[g] = lo < S[g] ? S[g] : (lo > E[g] ? E[g] : lo);
+        b[g] = hi < S[g] ? S[g] : (hi > E[g] ? E[g] : hi);
+        if (b[g] > a[g]) U |= 1ull << g;
+    }
+    int ord[restart::kMaxGenomes];
+    uint64_t steps = 0;
+    const int n = restart::head_order(d, U, a, S, ord, &steps);
+    uint64_t cum = 0;
+    bool fired = false;
+    for (int k = 0; k < n && !fired; ++k) {
+        const int g = ord[k];
+        uint64_t x = a[g];
+        while (x < b[g]) {
+            if (cum > restart::kRepeatLimit) { fired = true; break; }
+            const uint64_t nb = S[g] + ((x - S[g]) / restart::kMerBuffer + 1) * restart::kMerBuffer;
+            const uint64_t y = b[g] < nb ? b[g] : nb;
+            cum += y - x;
+            x = y;
+        }
+        // a run ending on a buffer boundary with more of the chunk to read: the refilled
+        // head still carries K for one more iteration
+        if (!fired && (b[g] - S[g]) % restart::kMerBuffer == 0 && b[g] < E[g] && cum > restart::kRepeatLimit)
+            fired = true;
+    }
+    out[c] = fired ? 1u : 0u;
+    const uint64_t nxt = (uint64_t)(i + 1) << kbits;
+    uint64_t lo = j, hi = N;   // first stream index with key2 >= nxt
+    while (lo < hi) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if (key2[mid] < nxt) lo = mid + 1;
+        else hi = mid;
+    }
+    cend[c] = lo;
+}
+
+// drop the stream ranges [rlo[r], rhi[r]) (sorted, disjoint; rpre[r] = records dropped
+// before range r), order kept
+__global__ void compat_drop_kernel(const uint64_t* __restrict__ k_in, const uint32_t* __restrict__ v_in, uint64_t N,
+                                   const uint64_t* __restrict__ rlo, const uint64_t* __restrict__ rhi,
+                                   const uint64_t* __restrict__ rpre, uint32_t R, uint64_t* __restrict__ k_out,
+                                   uint32_t* __restrict__ v_out) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= N) return;
+    uint32_t lo = 0, hi = R;   // ranges starting at or before j
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (rlo[mid] <= j) lo = mid + 1;
+        else hi = mid;
+    }
+    uint64_t drop = 0;
+    if (lo > 0) {
+        if (j < rhi[lo - 1]) return;
+        drop = rpre[lo - 1] + (rhi[lo - 1] - rlo[lo - 1]);
+    }
+    k_out[j - drop] = k_in[j];
+    v_out[j - drop] = v_in[j];
 }
 
 // MergeTable (ParallelMemHash.cpp:105-121): every entry of the thread table is re-added
@@ -184,10 +292,36 @@ hipError_t launch_compat_find(const uint64_t* sk, const GenomeTable& gt, uint64_
 
 hipError_t launch_compat_chunk_keys(const uint64_t* sk, const uint32_t* sv, uint64_t N, const GenomeTable& gt,
                                     int kbits, const uint64_t* cs, uint32_t nch, uint64_t* key2, uint32_t* val2,
-                                    hipStream_t st) {
+                                    uint64_t* ck, hipStream_t st) {
     if (N == 0) return hipSuccess;
     hipLaunchKernelGGL(compat_chunk_keys_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, sk, sv, N, gt,
-                       kbits, cs, nch, key2, val2);
+                       kbits, cs, nch, key2, val2, ck);
+    return hipGetLastError();
+}
+
+hipError_t launch_compat_cands(const uint64_t* key2, uint64_t N, uint64_t* list, unsigned long long* cnt, uint64_t cap,
+                               hipStream_t st) {
+    hipError_t e = hipMemsetAsync(cnt, 0, 8, st);
+    if (e != hipSuccess || N == 0) return e;
+    hipLaunchKernelGGL(compat_cand_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, key2, N, list, cnt, cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_compat_fire(const restart::PlanData& d, const uint64_t* key2, uint64_t N, int kbits,
+                              const uint64_t* cand, uint64_t C, const uint64_t* cs, uint32_t nch, uint32_t* out,
+                              uint64_t* cend, hipStream_t st) {
+    if (C == 0) return hipSuccess;
+    hipLaunchKernelGGL(compat_fire_kernel, dim3((unsigned)((C + 63) / 64)), dim3(64), 0, st, d, key2, N, kbits, cand, C,
+                       cs, nch, out, cend);
+    return hipGetLastError();
+}
+
+hipError_t launch_compat_drop(const uint64_t* k_in, const uint32_t* v_in, uint64_t N, const uint64_t* rlo,
+                              const uint64_t* rhi, const uint64_t* rpre, uint32_t R, uint64_t* k_out, uint32_t* v_out,
+                              hipStream_t st) {
+    if (N == 0) return hipSuccess;
+    hipLaunchKernelGGL(compat_drop_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, k_in, v_in, N, rlo, rhi,
+                       rpre, R, k_out, v_out);
     return hipGetLastError();
 }
 

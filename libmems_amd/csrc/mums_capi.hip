@@ -1200,6 +1200,83 @@ int prepare_run(mums_ctx* ctx, const std::vector<uint64_t>& lens) {
 // pair path; one sort of (genome, ckey) gives the G SortedMerLists, the chunk starts
 // follow GetBreakpoint, and a second sort of (chunk, ckey) yields the chunk-major probe
 // order; groups / probes / chains / replay are the serial kernels, then MergeTable.
+// ParallelMemHash chunks with a seed group above MER_REPEAT_LIMIT (ParallelMemHash.cpp:97-100):
+// the chunk's SearchRange returns false at the group (MatchFinder.cpp:253-277), the return
+// value is ignored and MergeTable still runs, so the chunk keeps exactly the AddHashEntry
+// calls before that group and the later chunks are unaffected.  On the chunk-major stream
+// (sorted_key / sorted_idx, N records) every (chunk, masked key) group of more than 1000
+// records is a candidate; compat_fire_kernel decides per candidate whether the check fires
+// inside its chunk (restart_plan.h head order, buffers from the chunk start); the first
+// firing group of a chunk drops the stream from its first record to the chunk's end.
+// ctx->crall holds the genome-major SML keys.  *n_live = records kept.
+int compat_truncate(mums_ctx* ctx, uint32_t nch, const uint64_t* cs, int kbits, uint64_t* n_live, hipStream_t st) {
+    const GenomeTable& gt = ctx->gt;
+    const int G = gt.G;
+    const uint64_t N = ctx->N;
+    *n_live = N;
+    ctx->restarts = 0;
+    const uint64_t cap = N / (restart::kRepeatLimit + 1) + 16;
+    const uint64_t words = cap * 3 + 2 * (uint64_t)(G + 1) + 16 + 3 * ((uint64_t)nch + 1);
+    HIPCHK(ctx->rsplan.ensure(words * 8 + 256));
+    uint64_t* d_list = ctx->rsplan.as<uint64_t>();
+    uint64_t* d_cend = d_list + cap;
+    uint32_t* d_fire = (uint32_t*)(d_cend + cap);
+    uint64_t* d_dm = d_list + 3 * cap;   // (d_fire takes cap/2 words of that third block)
+    uint64_t* d_db = d_dm + G + 1;
+    unsigned long long* d_cnt = (unsigned long long*)(d_db + G + 1);
+    uint64_t* d_rng = d_db + G + 1 + 16;
+    const uint64_t* key2 = (const uint64_t*)ctx->sorted_key;
+    HIPCHK(launch_compat_cands(key2, N, d_list, d_cnt, cap, st));
+    unsigned long long C = 0;
+    HIPCHK(hipMemcpyAsync(&C, d_cnt, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (C > cap) return fail(ctx, MUMS_E_HIP, "compat: candidate list overflow (internal error)");
+    if (C == 0) return MUMS_OK;
+    std::vector<uint64_t> cand(C);
+    HIPCHK(hipMemcpy(cand.data(), d_list, C * 8, hipMemcpyDeviceToHost));
+    std::sort(cand.begin(), cand.end());
+    std::vector<uint64_t> hm(G + 1, 0), hb(G + 1, 0);
+    for (int g = 0; g < G; ++g) { hm[g] = gt.m[g]; hb[g] = gt.base[g]; }
+    HIPCHK(hipMemcpyAsync(d_list, cand.data(), C * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_dm, hm.data(), (G + 1) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_db, hb.data(), (G + 1) * 8, hipMemcpyHostToDevice, st));
+    const restart::PlanData d{G, d_dm, d_db, ctx->crall.as<uint64_t>()};
+    HIPCHK(launch_compat_fire(d, key2, N, kbits, d_list, C, cs, nch, d_fire, d_cend, st));
+    std::vector<uint32_t> fire(C);
+    std::vector<uint64_t> cend(C);
+    HIPCHK(hipMemcpyAsync(fire.data(), d_fire, C * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(cend.data(), d_cend, C * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    // candidates are in stream order = (chunk, key) order: the first firing one of a chunk cuts it
+    std::vector<uint64_t> rlo, rhi, rpre;
+    uint64_t dropped = 0;
+    for (uint64_t c = 0; c < C; ++c) {
+        if (!fire[c] || (!rhi.empty() && cand[c] < rhi.back())) continue;   // chunk already cut
+        rlo.push_back(cand[c]);
+        rhi.push_back(cend[c]);
+        rpre.push_back(dropped);
+        dropped += cend[c] - cand[c];
+    }
+    ctx->restarts = rlo.size();
+    if (rlo.empty()) return MUMS_OK;
+    const uint32_t R = (uint32_t)rlo.size();
+    uint64_t* d_rlo = d_rng;
+    uint64_t* d_rhi = d_rlo + R;
+    uint64_t* d_rpre = d_rhi + R;
+    HIPCHK(hipMemcpyAsync(d_rlo, rlo.data(), R * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_rhi, rhi.data(), R * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_rpre, rpre.data(), R * 8, hipMemcpyHostToDevice, st));
+    uint64_t* k_out = ctx->sorted_buf ? ctx->kA.as<uint64_t>() : ctx->kB.as<uint64_t>();
+    uint32_t* v_out = ctx->sorted_buf ? ctx->vA.as<uint32_t>() : ctx->vB.as<uint32_t>();
+    HIPCHK(launch_compat_drop(key2, ctx->sorted_idx, N, d_rlo, d_rhi, d_rpre, R, k_out, v_out, st));
+    HIPCHK(hipStreamSynchronize(st));   // (rlo / rhi / rpre are host temporaries)
+    ctx->sorted_buf ^= 1;
+    ctx->sorted_key = k_out;
+    ctx->sorted_idx = v_out;
+    *n_live = N - dropped;
+    return MUMS_OK;
+}
+
 int run_pipeline_compat(mums_ctx* ctx, int stage) {
     hipStream_t st = ctx->stream;
     const int G = (int)ctx->genomes.size();
@@ -1302,8 +1379,11 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
     int cbits = 0;
     while (((uint64_t)1 << cbits) < (uint64_t)nch) ++cbits;
     if (kbits + cbits > 64) return fail(ctx, MUMS_E_UNSUPPORTED, "ParallelMemHash compat: too many chunks");
+    // the genome-major SMLs' keys (genome bits off) survive the second sort for the
+    // MER_REPEAT_LIMIT plan below
+    HIPCHK(ctx->crall.ensure(N * 8 + 64));
     HIPCHK(launch_compat_chunk_keys(sk, sv, N, gt, kbits, cs, nch, ctx->ckey.as<uint64_t>(), ctx->cval.as<uint32_t>(),
-                                    st));
+                                    ctx->crall.as<uint64_t>(), st));
     HIPCHK(radix_sort<uint64_t>(ctx->ckey.as<uint64_t>(), ctx->cval.as<uint32_t>(), N, kbits + cbits,
                                 ctx->kA.as<uint64_t>(), ctx->vA.as<uint32_t>(), ctx->kB.as<uint64_t>(),
                                 ctx->vB.as<uint32_t>(), ctx->tmp.p, &buf, st));
@@ -1311,18 +1391,18 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
     ctx->sorted_key = buf ? ctx->kB.p : ctx->kA.p;
     ctx->sorted_idx = buf ? ctx->vB.as<uint32_t>() : ctx->vA.as<uint32_t>();
     ctx->sort_passes = (kbits + cbits + 7) / 8;
+    uint64_t n_live = N;
+    rc = compat_truncate(ctx, nch, cs, kbits, &n_live, st);
+    if (rc) return rc;
     HIPCHK(hipEventRecord(ctx->ev[EV_SORT], st));
     SegTile* tiles = ctx->tiles.as<SegTile>();
-    HIPCHK(launch_flat_tiles(N, tiles, st));
+    HIPCHK(launch_flat_tiles(n_live, tiles, st));
     rc = groups_dispatch<PairView<uint64_t>>(
-        ctx, PairView<uint64_t>{(const uint64_t*)ctx->sorted_key, ctx->sorted_idx}, tiles, ntiles_groups, mp,
-        ps.probe_info, ps.probe_bucket, ps.slot_info, ps.slot_bucket, st);
+        ctx, PairView<uint64_t>{(const uint64_t*)ctx->sorted_key, ctx->sorted_idx}, tiles,
+        (n_live + kSegTile - 1) / kSegTile, mp, ps.probe_info, ps.probe_bucket, ps.slot_info, ps.slot_bucket, st);
     if (rc) return rc;
     rc = finish_seeds(ctx, ps, st);
     if (rc) return rc;
-    if (ctx->hc.repeat_limit)
-        return fail(ctx, MUMS_E_UNSUPPORTED, "ParallelMemHash compat: a seed group above MER_REPEAT_LIMIT ends its "
-                                             "chunk in the reference (SearchRange's ignored return) - not reproduced");
     ctx->stage_done = MUMS_STAGE_SEEDS;
     if (stage >= MUMS_STAGE_ALL) {
         rc = find_tail(ctx, mp, ctx->packed.as<uint32_t>(), [&](MatProbes* v) {

@@ -333,7 +333,15 @@ hipError_t launch_compat_find(const uint64_t* sk, const GenomeTable& gt, uint64_
                               const uint64_t* bm, uint32_t nch, hipStream_t st);
 hipError_t launch_compat_chunk_keys(const uint64_t* sk, const uint32_t* sv, uint64_t N, const GenomeTable& gt,
                                     int kbits, const uint64_t* cs, uint32_t nch, uint64_t* key2, uint32_t* val2,
-                                    hipStream_t st);
+                                    uint64_t* ck, hipStream_t st);
+hipError_t launch_compat_cands(const uint64_t* key2, uint64_t N, uint64_t* list, unsigned long long* cnt, uint64_t cap,
+                               hipStream_t st);
+hipError_t launch_compat_fire(const restart::PlanData& d, const uint64_t* key2, uint64_t N, int kbits,
+                              const uint64_t* cand, uint64_t C, const uint64_t* cs, uint32_t nch, uint32_t* out,
+                              uint64_t* cend, hipStream_t st);
+hipError_t launch_compat_drop(const uint64_t* k_in, const uint32_t* v_in, uint64_t N, const uint64_t* rlo,
+                              const uint64_t* rhi, const uint64_t* rpre, uint32_t R, uint64_t* k_out, uint32_t* v_out,
+                              hipStream_t st);
 hipError_t launch_compat_merge(uint32_t* tsize, const uint32_t* bstart, uint32_t* tbl, const int64_t* pool, int G,
                                uint32_t Tb, unsigned long long* collisions, hipStream_t st);
 

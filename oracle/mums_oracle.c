@@ -971,6 +971,9 @@ static int parallel_compat_search(memhash_t* h, const oracle_params* prm, int G,
         }
         if (get_breakpoint(mx, cs[(nch - 1) * G + mx] + chunk, G, sml, m, lens, h->x.L, h->x.seed_mask,
                            cs + nch * G)) { free(cs); return -1; }
+        /* a masked-key group at least a chunk long: GetBreakpoint returns the same start   */
+        /* again and the reference's loop (:75-83) never ends -- reported, not replayed     */
+        if (cs[nch * G + mx] <= cs[(nch - 1) * G + mx]) { free(cs); return -1; }
         ++nch;
     }
     const uint32_t T = h->table_size;

@@ -74,3 +74,36 @@ def test_parallel_single_chunk_equals_serial(gpu_lib, oracle_mod):
     serial = oracle_mod.match_text(lengths, starts).splitlines()
     dedup = [l for i, l in enumerate(serial) if i == 0 or serial[i - 1] != l]
     assert ml.text().splitlines() == dedup
+
+
+LARGE = json.load(open(os.path.join(GOLDEN, "large_cases.json")))
+
+
+def test_parallel_ngaps_known_answer(gpu_lib, oracle_mod):
+    """BASELINE config 2's shape (4 x 10 Mbp related, w15) with 20 N runs per genome under
+    ParallelMemHash (chunk 200 000): the chunk holding the all-A seed group (> 1000 records)
+    is cut there (SearchRange returns false, ParallelMemHash.cpp:97 ignores it) -- the
+    oracle's recorded answer (tests/golden/make_large_golden.py pc_ngaps)."""
+    from tests import tie_inputs
+    c = LARGE["pc_ngaps"]
+    seqs = tie_inputs.multi_gap(G=c["G"], n=c["n"], ngaps=c["ngaps"], gap=(900, 3200), p=c["p"], seed=c["gen_seed"])
+    ml, st = gpu_parallel(gpu_lib, seqs, c["seed"], c["chunk_size"])
+    assert st["chunks"] == c["chunks"] and st["restarts"] == c["restarts"]
+    assert len(ml) == c["matches"]
+    assert hashlib.md5(ml.text().encode()).hexdigest() == c["md5"]
+
+
+@pytest.mark.parametrize("copies,tandem,chunk,w", [(1500, False, 7000, 15), (2500, False, 20_000, 13),
+                                                   (2000, True, 50_000, 15), (1200, False, 3000, 11)])
+def test_parallel_repeat_limit_cuts_vs_oracle(gpu_lib, oracle_mod, copies, tandem, chunk, w):
+    """High-copy repeats: seed groups above MER_REPEAT_LIMIT inside many chunks, each chunk cut
+    at its first firing group (buffers of 10 000 from the chunk start, head order)."""
+    from tests import repeat_inputs
+    seqs = repeat_inputs.high_copy(G=4, n=300_000, copies=copies, tandem=tandem, seed=copies + chunk)
+    seed = oracle_mod.get_seed(w)
+    lengths, starts, ost = oracle_mod.find_matches(seqs, seed, parallel_compat=True, chunk_size=chunk)
+    assert ost["restarts"] > 0
+    ml, st = gpu_parallel(gpu_lib, seqs, seed, chunk)
+    assert st["chunks"] == ost["chunks"] and st["restarts"] == ost["restarts"]
+    assert len(ml) == len(lengths)
+    assert (ml.lengths == lengths).all() and (ml.starts == starts).all()

@@ -46,17 +46,15 @@ def test_tie_inputs_vs_std_sort_oracle(gpu_lib, oracle_mod, name):
     with oracle_mod.sml_tie_rule("std"):
         ref_len, ref_starts, ref = oracle_mod.find_matches(seqs, oracle_mod.get_seed(opts.get("w", 15)),
                                                            **tie_inputs.oracle_kwargs(opts))
-    if compat and ref["restarts"] > 0:
-        # a group above MER_REPEAT_LIMIT ends a ParallelMemHash chunk (SearchRange's ignored
-        # return, ParallelMemHash.cpp:97): refused by the compat mode, loudly
-        with pytest.raises(gpu_lib.MumsError) as ei:
-            run_case(gpu_lib, seqs, opts)
-        assert ei.value.code == gpu_lib.MUMS_E_UNSUPPORTED
-        return
     ml, st, offlog = run_case(gpu_lib, seqs, opts)
     assert len(ml) == len(ref_len), (len(ml), len(ref_len))
     assert (ml.lengths == ref_len).all() and (ml.starts == ref_starts).all()
-    if not compat:   # (the compat mode's collision count is not the thread tables' sum)
+    if compat:
+        # a group above MER_REPEAT_LIMIT ends its ParallelMemHash chunk (SearchRange's ignored
+        # return, ParallelMemHash.cpp:97): one cut chunk per oracle restart
+        assert st["restarts"] == ref["restarts"]
+        assert st["chunks"] == ref["chunks"]
+    else:   # (the compat mode's collision count is not the thread tables' sum)
         assert st["collision_count"] == ref["collision_count"]
         assert st["restarts"] == ref["restarts"]
         assert np.array_equal(offlog, ref["offset_log"])

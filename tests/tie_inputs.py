@@ -121,6 +121,20 @@ def _cases():
                                         dict(w=13, repeat_tol=2, enum_tol=3))
         c[f"tandem_compat_{sd}"] = (lambda sd=sd: tandem_blocks(G=3, n=50_000, copies=200, seed=40 + sd),
                                     dict(w=13, cls="ParallelMemHash", chunk_size=3000))
+    # ParallelMemHash chunks holding a seed group above MER_REPEAT_LIMIT: the chunk's SearchRange
+    # returns false at the group and ParallelMemHash.cpp:97 ignores it (the chunk is cut there)
+    for sd, chunk in enumerate((20_000, 25_000, 40_000)):
+        c[f"multi_gap_compat_{sd}"] = (lambda sd=sd: multi_gap(G=3, n=100_000, ngaps=5, seed=200 + sd),
+                                       dict(w=15, cls="ParallelMemHash", chunk_size=chunk))
+    c["multi_gap_compat_G5"] = (lambda: multi_gap(G=5, n=80_000, ngaps=4, seed=210),
+                                dict(w=13, cls="ParallelMemHash", chunk_size=15_000))
+    c["n_gapped_compat_buffers"] = (lambda: repeat_inputs.n_gapped(G=4, n=90_000, gaps=((2_000, 25_000), (60_000, 10_022)),
+                                                                   shift=1_300, seed=13),
+                                    dict(w=15, cls="ParallelMemHash", chunk_size=45_000))
+    c["high_copy_compat"] = (lambda: repeat_inputs.high_copy(G=3, n=60_000, copies=2000, seed=2),
+                             dict(w=15, cls="ParallelMemHash", chunk_size=5000))
+    c["high_copy_tandem_compat"] = (lambda: repeat_inputs.high_copy(G=3, n=60_000, copies=2000, tandem=True, seed=2),
+                                    dict(w=15, cls="ParallelMemHash", chunk_size=20_000))
     c["multi_gap_pairwise"] = (lambda: multi_gap(G=3, n=60_000, ngaps=4, seed=16), dict(w=15, cls="PairwiseMatchFinder"))
     for sd in range(4):
         rng = np.random.default_rng(100 + sd)
