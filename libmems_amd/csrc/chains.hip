@@ -22,6 +22,7 @@
 // The replay (replay.hip) then inserts chain entries without extending anything.
 // A 32-bit line-hash collision only splits runs of a line: every probe still gets
 // its true chain ends (a segment end always walks to the real end of its chain).
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 
@@ -47,40 +48,12 @@ struct WalkItem {
     int64_t stop;    // bridge: done once cur >= stop
 };
 
-__device__ __forceinline__ uint64_t mix64(uint64_t x) {
-    x ^= x >> 30;
-    x *= 0xbf58476d1ce4e5b9ull;
-    x ^= x >> 27;
-    x *= 0x94d049bb133111ebull;
-    x ^= x >> 31;
-    return x;
-}
 
 // probe of sorted-stream group k (the AddHashEntry argument), see build_probe
 template <int MG, typename View>
 __device__ __forceinline__ void probe_of(const View& v, const uint64_t* __restrict__ /*probe_info*/, uint32_t k,
                                          const GenomeTable& gt, const MatchParams& /*mp*/, int L, Mhe<MG>& P) {
     load_probe<MG>(v, k, gt.G, L, P);
-}
-
-// line invariants: reference start x = s_ref (> 0); per other component the
-// diagonal s_g - s_ref (forward) or |s_g| + s_ref (reverse)
-template <int MG>
-__device__ __forceinline__ uint32_t line_hash(const Mhe<MG>& P, int G) {
-    const int ref = first_start(P);
-    const int64_t x = start_at(P, ref);
-    uint64_t h = 0x9e3779b97f4a7c15ull ^ (uint64_t)ref;
-    #pragma unroll
-    for (int g = 0; g < MG; ++g) {
-        if (g < G && g > ref && P.s[g] != 0) {
-            const int64_t s = P.s[g];
-            const uint64_t d = s > 0 ? (uint64_t)(s - x) : (uint64_t)(-s + x) ^ 0x8000000000000000ull;
-            h = mix64(h ^ d ^ ((uint64_t)g << 56));
-        } else {
-            h = mix64(h ^ ((uint64_t)g << 48));
-        }
-    }
-    return (uint32_t)(h >> 32);
 }
 
 template <int MG>
@@ -683,6 +656,29 @@ __global__ __launch_bounds__(kBlock) void chain_entry_kernel(View v, const uint6
     }
 }
 
+// ---- line order: (line hash, reference start) by two stable onesweep sorts -------------
+// of packed 8-B records (radix_seg.hip): first (x << 32 | k) by x, then
+// (hash << 32 | position after the first sort) by hash; ord[j] = the probe at line position j
+__global__ __launch_bounds__(kBlock) void line_rec1_kernel(const uint64_t* __restrict__ lkey, uint64_t P,
+                                                           uint64_t* __restrict__ rec) {
+    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k < P) rec[k] = (lkey[k] << 32) | k;
+}
+
+__global__ __launch_bounds__(kBlock) void line_rec2_kernel(const uint64_t* __restrict__ lkey,
+                                                           const uint64_t* __restrict__ s1, uint64_t P,
+                                                           uint64_t* __restrict__ rec) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < P) rec[i] = (lkey[(uint32_t)s1[i]] & 0xFFFFFFFF00000000ull) | i;
+}
+
+__global__ __launch_bounds__(kBlock) void line_ord_kernel(const uint64_t* __restrict__ s1,
+                                                          const uint64_t* __restrict__ s2, uint64_t P,
+                                                          uint32_t* __restrict__ ord) {
+    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j < P) ord[j] = (uint32_t)s1[(uint32_t)s2[j]];
+}
+
 inline unsigned grid_of(uint64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
 // --- chunked FindMatches: chains labelled per slice of the probes ---------------------
@@ -816,47 +812,91 @@ size_t chain_tmp_bytes(uint64_t P, uint32_t Tb, int G) {
     return P * (24 + 8 + 1 + 24 + 4 + 2 * sizeof(WalkItem) + 32 + 24 + 8 * (uint64_t)(G + 1)) + (uint64_t)Tb * 4 + 64 * 64;
 }
 
-// Chain labelling of the P probes (key order): chain_of[k] = chain of probe k;
-// pool[c] = extended entry of chain c; *d_nchains (device) = number of chains.
-template <int MG, typename View>
-hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const GenomeTable& gt, const MatchParams& mp,
-                         const SeedSpec& ss, const uint32_t* packed, void* d_chain_tmp, void* d_scan_tmp,
-                         void* d_radix_tmp, uint32_t* chain_of, int64_t* pool, uint32_t* d_nchains, hipStream_t st,
-                         void* ctr, hipEvent_t* ev_walk, uint32_t* fk, uint32_t kbase) {
-    if (P == 0) return hipSuccess;
+namespace {
+
+// launch_chains' scratch in d_chain_tmp (rows_line only when the rows are gathered there)
+struct ChainWs {
+    uint64_t *lkey, *kA, *kB;
+    uint32_t *vA, *vB;
+    uint8_t* link;
+    int64_t *rcol, *lcol, *seg_r;
+    uint32_t* seg;
+    WalkItem *queue, *queue_long;
+    unsigned int* qcount;
+    int64_t* rows_line;
+    uint32_t* bst;   // {0, P}: the one bucket of the line sort
+};
+
+ChainWs chain_ws(void* d_chain_tmp, uint64_t P, int G, bool with_rows) {
     char* p = (char*)d_chain_tmp;
     auto carve = [&](size_t bytes) {
         char* r = p;
         p += (bytes + 255) & ~(size_t)255;
         return (void*)r;
     };
-    uint64_t* lkey = (uint64_t*)carve(P * 8);
-    uint64_t* kA = (uint64_t*)carve(P * 8);
-    uint64_t* kB = (uint64_t*)carve(P * 8);
-    uint32_t* vA = (uint32_t*)carve(P * 4);
-    uint32_t* vB = (uint32_t*)carve(P * 4);
-    uint8_t* link = (uint8_t*)carve(P);
-    int64_t* rcol = (int64_t*)carve(P * 8);
-    int64_t* lcol = (int64_t*)carve(P * 8);
-    int64_t* seg_r = (int64_t*)carve(P * 8);
-    uint32_t* seg = (uint32_t*)carve(P * 4);
-    WalkItem* queue = (WalkItem*)carve(P * sizeof(WalkItem));
-    WalkItem* queue_long = (WalkItem*)carve(P * sizeof(WalkItem));
-    unsigned int* qcount = (unsigned int*)carve(64);
-    int64_t* rows_line = (int64_t*)carve(P * (uint64_t)(gt.G + 1) * 8);
+    ChainWs w;
+    w.lkey = (uint64_t*)carve(P * 8);
+    w.kA = (uint64_t*)carve(P * 8);
+    w.kB = (uint64_t*)carve(P * 8);
+    w.vA = (uint32_t*)carve(P * 4);
+    w.vB = (uint32_t*)carve(P * 4);
+    w.link = (uint8_t*)carve(P);
+    w.rcol = (int64_t*)carve(P * 8);
+    w.lcol = (int64_t*)carve(P * 8);
+    w.seg_r = (int64_t*)carve(P * 8);
+    w.seg = (uint32_t*)carve(P * 4);
+    w.queue = (WalkItem*)carve(P * sizeof(WalkItem));
+    w.queue_long = (WalkItem*)carve(P * sizeof(WalkItem));
+    w.qcount = (unsigned int*)carve(64);
+    w.bst = (uint32_t*)carve(64);
+    w.rows_line = with_rows ? (int64_t*)carve(P * (uint64_t)(G + 1) * 8) : nullptr;
+    return w;
+}
+
+// line order of the P probes from w.lkey (hash << 32 | x): ord[j] (in w.vA) = the probe at
+// line position j.  Two stable onesweep sorts of packed records (by x on xbits bits, then
+// by hash) instead of eight 8-bit passes over 12-B (key, value) pairs.  lkey is consumed.
+hipError_t line_sort(const ChainWs& w, uint64_t P, int xbits, void* d_tmp, uint32_t* d_err, hipStream_t st,
+                     const uint32_t** ord_out) {
+    hipError_t e;
+    const uint32_t hb[2] = {0u, (uint32_t)P};
+    if ((e = hipMemcpyAsync(w.bst, hb, 8, hipMemcpyHostToDevice, st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(line_rec1_kernel, dim3(grid_of(P)), dim3(kBlock), 0, st, w.lkey, P, w.kA);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    int b1 = 0;
+    if ((e = seg_onesweep_sort(w.kA, w.kB, P, xbits, 0, w.bst, d_tmp, d_err, &b1, st)) != hipSuccess) return e;
+    const uint64_t* s1 = b1 ? w.kB : w.kA;
+    uint64_t* r2 = b1 ? w.kA : w.kB;
+    hipLaunchKernelGGL(line_rec2_kernel, dim3(grid_of(P)), dim3(kBlock), 0, st, w.lkey, s1, P, r2);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    int b2 = 0;
+    if ((e = seg_onesweep_sort(r2, w.lkey, P, 32, 0, w.bst, d_tmp, d_err, &b2, st)) != hipSuccess) return e;
+    const uint64_t* s2 = b2 ? w.lkey : r2;
+    hipLaunchKernelGGL(line_ord_kernel, dim3(grid_of(P)), dim3(kBlock), 0, st, s1, s2, P, w.vA);
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;   // (hb is a host temporary)
+    *ord_out = w.vA;
+    return hipGetLastError();
+}
+
+int x_bits(const GenomeTable& gt) {
+    uint64_t mx = 1;
+    for (int g = 0; g < gt.G; ++g) mx = gt.n[g] + 2 > mx ? gt.n[g] + 2 : mx;
+    int b = 1;
+    while (b < 32 && (1ull << b) < mx) ++b;
+    return b;
+}
+
+// after the line sort (ord = probe of line position j, vl.rows = the rows in line order):
+// links, walks, segment ids, chain_of and the chain entries
+template <int MG>
+hipError_t chains_core(MatProbes vl, const ChainWs& w, const uint32_t* ord, uint64_t P, const GenomeTable& gt,
+                       const MatchParams& mp, const SeedSpec& ss, const uint32_t* packed, void* d_scan_tmp,
+                       uint32_t* chain_of, int64_t* pool, uint32_t* d_nchains, hipStream_t st, void* ctr,
+                       hipEvent_t* ev_walk, uint32_t* fk, uint32_t kbase) {
     hipError_t e;
     const unsigned grid = grid_of(P);
-    hipLaunchKernelGGL((chain_key_kernel<MG, View>), dim3(grid), dim3(kBlock), 0, st, v, probe_info, P, gt, mp, ss.L,
-                       lkey);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    int buf = 0;
-    if ((e = radix_sort<uint64_t>(lkey, nullptr, P, 64, kA, vA, kB, vB, d_radix_tmp, &buf, st)) != hipSuccess) return e;
-    const uint32_t* ord = buf ? vB : vA;
-    // the rows in line order: the link / walk / entry kernels then read row j, not row ord[j]
-    if ((e = launch_gather_rows(v.rows, ord, P, gt.G, rows_line, st)) != hipSuccess) return e;
-    View vl = v;
-    vl.rows = rows_line;
     const unsigned walk_grid = 2048, short_grid = 8192;
+    unsigned int* qcount = w.qcount;
     unsigned int* qshort = qcount;      // chain_link / chain_left -> chain_walk_short_kernel
     unsigned int* qlong = qcount + 1;   // chain_walk_short_kernel -> chain_walk_kernel
     const bool cdbg = getenv("MUMS_DEV_CHAIN_DEBUG") != nullptr;
@@ -864,21 +904,21 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
         if ((e = hipMemsetAsync(qcount, 0, 8, st)) != hipSuccess) return e;
         const unsigned lgrid = (unsigned)((P + kBlock * kLinkIPT - 1) / (kBlock * kLinkIPT));
         if (pass == 0)
-            hipLaunchKernelGGL((chain_link_kernel<MG, View>), dim3(lgrid), dim3(kBlock), 0, st, vl, probe_info, P, gt,
-                               mp, ss, link, queue, qshort);
+            hipLaunchKernelGGL((chain_link_kernel<MG, MatProbes>), dim3(lgrid), dim3(kBlock), 0, st, vl, nullptr, P, gt,
+                               mp, ss, w.link, w.queue, qshort);
         else
-            hipLaunchKernelGGL(chain_left_kernel, dim3(lgrid), dim3(kBlock), 0, st, P, (const uint8_t*)link, queue,
+            hipLaunchKernelGGL(chain_left_kernel, dim3(lgrid), dim3(kBlock), 0, st, P, (const uint8_t*)w.link, w.queue,
                                qshort);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-        hipLaunchKernelGGL((chain_walk_short_kernel<MG, View>), dim3(short_grid), dim3(kBlock), 0, st, vl, probe_info,
-                           gt, mp, ss, packed, (const WalkItem*)queue, (const unsigned int*)qshort, link, rcol, lcol,
-                           queue_long, qlong);
+        hipLaunchKernelGGL((chain_walk_short_kernel<MG, MatProbes>), dim3(short_grid), dim3(kBlock), 0, st, vl, nullptr,
+                           gt, mp, ss, packed, (const WalkItem*)w.queue, (const unsigned int*)qshort, w.link, w.rcol,
+                           w.lcol, w.queue_long, qlong);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (cdbg && (e = hipMemsetAsync(qcount + 4, 0, 32, st)) != hipSuccess) return e;
         if (ev_walk) (void)hipEventRecord(ev_walk[2 * pass], st);
-        hipLaunchKernelGGL((chain_walk_kernel<MG, View>), dim3(walk_grid), dim3(kBlock), 0, st, vl, probe_info, gt, mp,
-                           ss, ord, packed, (const WalkItem*)queue_long, (const unsigned int*)qlong, link, rcol, lcol,
-                           cdbg ? qcount + 4 : nullptr, (DevCounters*)ctr);
+        hipLaunchKernelGGL((chain_walk_kernel<MG, MatProbes>), dim3(walk_grid), dim3(kBlock), 0, st, vl, nullptr, gt, mp,
+                           ss, ord, packed, (const WalkItem*)w.queue_long, (const unsigned int*)qlong, w.link, w.rcol,
+                           w.lcol, cdbg ? qcount + 4 : nullptr, (DevCounters*)ctr);
         if (ev_walk) (void)hipEventRecord(ev_walk[2 * pass + 1], st);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (cdbg) {   // development: walk queue sizes and the long walks' step histogram
@@ -889,23 +929,69 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
                     "total %u\n", pass, hq[0], hq[1], (unsigned long)P, hq[4], hq[5], hq[6], hq[7], hq[8]);
         }
     }
-    hipLaunchKernelGGL(chain_flag_kernel, dim3(grid), dim3(kBlock), 0, st, link, P, seg);
+    hipLaunchKernelGGL(chain_flag_kernel, dim3(grid), dim3(kBlock), 0, st, w.link, P, w.seg);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if ((e = exclusive_scan_u32(seg, P, d_scan_tmp, d_nchains, st)) != hipSuccess) return e;
+    if ((e = exclusive_scan_u32(w.seg, P, d_scan_tmp, d_nchains, st)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(fk, 0xFF, P * 4, st)) != hipSuccess) return e;
-    hipLaunchKernelGGL(chain_seg_kernel, dim3(grid), dim3(kBlock), 0, st, link, ord, seg, P, rcol, chain_of, seg_r, fk,
-                       kbase);
+    hipLaunchKernelGGL(chain_seg_kernel, dim3(grid), dim3(kBlock), 0, st, w.link, ord, w.seg, P, w.rcol, chain_of,
+                       w.seg_r, fk, kbase);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL((chain_entry_kernel<MG, View>), dim3(grid), dim3(kBlock), 0, st, vl, probe_info, P, gt, mp, ss.L,
-                       ord, link, seg, lcol, seg_r, pool);
+    hipLaunchKernelGGL((chain_entry_kernel<MG, MatProbes>), dim3(grid), dim3(kBlock), 0, st, vl, nullptr, P, gt, mp,
+                       ss.L, ord, w.link, w.seg, w.lcol, w.seg_r, pool);
     return hipGetLastError();
+}
+
+// the line order: onesweep records when the reference starts fit 32 bits and P < 2^30
+// (MUMS_DEV_LINE_RADIX: the 64-bit pair sort), else 64-bit (key, value) radix passes
+hipError_t line_order(const ChainWs& w, uint64_t P, const GenomeTable& gt, void* d_tmp, void* ctr, hipStream_t st,
+                      const uint32_t** ord) {
+    static const bool pairs = getenv("MUMS_DEV_LINE_RADIX") != nullptr;
+    uint64_t mx = 0;
+    for (int g = 0; g < gt.G; ++g) mx = gt.n[g] > mx ? gt.n[g] : mx;
+    if (!pairs && ctr && P < (1ull << 30) && mx + 2 < (1ull << 32))
+        return line_sort(w, P, x_bits(gt), d_tmp, &((DevCounters*)ctr)->err, st, ord);
+    int buf = 0;
+    hipError_t e = radix_sort<uint64_t>(w.lkey, nullptr, P, 64, w.kA, w.vA, w.kB, w.vB, d_tmp, &buf, st);
+    *ord = buf ? w.vB : w.vA;
+    return e;
+}
+
+}  // namespace
+
+uint64_t* chain_lkey_slot(void* d_chain_tmp, uint64_t P, int G) { return chain_ws(d_chain_tmp, P, G, true).lkey; }
+
+size_t chain_radix_tmp_bytes(uint64_t P) { return std::max(radix_tmp_bytes(P), onesweep_tmp_bytes(P, 0, 32)); }
+
+// Chain labelling of the P probes (key order): chain_of[k] = chain of probe k;
+// pool[c] = extended entry of chain c; *d_nchains (device) = number of chains.
+template <int MG, typename View>
+hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const GenomeTable& gt, const MatchParams& mp,
+                         const SeedSpec& ss, const uint32_t* packed, void* d_chain_tmp, void* d_scan_tmp,
+                         void* d_radix_tmp, uint32_t* chain_of, int64_t* pool, uint32_t* d_nchains, hipStream_t st,
+                         void* ctr, hipEvent_t* ev_walk, uint32_t* fk, uint32_t kbase, bool lkey_ready) {
+    if (P == 0) return hipSuccess;
+    const ChainWs w = chain_ws(d_chain_tmp, P, gt.G, true);
+    hipError_t e;
+    if (!lkey_ready) {   // else written by the materialize pass (chain_lkey_slot)
+        hipLaunchKernelGGL((chain_key_kernel<MG, View>), dim3(grid_of(P)), dim3(kBlock), 0, st, v, probe_info, P, gt,
+                           mp, ss.L, w.lkey);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    const uint32_t* ord = nullptr;
+    if ((e = line_order(w, P, gt, d_radix_tmp, ctr, st, &ord)) != hipSuccess) return e;
+    // the rows in line order: the link / walk / entry kernels then read row j, not row ord[j]
+    if ((e = launch_gather_rows(v.rows, ord, P, gt.G, w.rows_line, st)) != hipSuccess) return e;
+    MatProbes vl{};
+    vl.rows = w.rows_line;
+    return chains_core<MG>(vl, w, ord, P, gt, mp, ss, packed, d_scan_tmp, chain_of, pool, d_nchains, st, ctr, ev_walk,
+                           fk, kbase);
 }
 
 #define MUMS_INST_CHAINS(MG, V)                                                                                   \
     template hipError_t launch_chains<MG, V>(V, const uint64_t*, uint64_t, const GenomeTable&, const MatchParams&, \
                                              const SeedSpec&, const uint32_t*, void*, void*, void*, uint32_t*,     \
                                              int64_t*, uint32_t*, hipStream_t, void*, hipEvent_t*, uint32_t*,    \
-                                             uint32_t);
+                                             uint32_t, bool);
 MUMS_INST_CHAINS(4, MatProbes)
 MUMS_INST_CHAINS(8, MatProbes)
 MUMS_INST_CHAINS(16, MatProbes)

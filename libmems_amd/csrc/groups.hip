@@ -368,11 +368,16 @@ __global__ void flat_tiles_kernel(uint64_t N, uint64_t nt, SegTile* __restrict__
     tiles[t] = d;
 }
 
-// probe k (key order) -> MatProbes row k: build_probe once per probe for the replay
+// probe k (key order) -> MatProbes row k: build_probe once per probe for the replay.
+// Packed records under the default tolerances load the group (<= G records, size in
+// probe_info) as one batch of independent loads (probe_row_fast).  lkey / fsk (optional):
+// the chain labelling's line key (chains.hip) and the first-genome start of probe k, so
+// neither re-reads the rows.
 template <int MG, typename View>
 __global__ __launch_bounds__(kBlock) void probe_materialize_kernel(View v, const uint64_t* __restrict__ probe_info,
                                                                    uint64_t P, GenomeTable gt, MatchParams mp, int L,
-                                                                   int64_t* __restrict__ rows) {
+                                                                   int64_t* __restrict__ rows, uint64_t* __restrict__ lkey,
+                                                                   uint32_t* __restrict__ fsk) {
     const uint64_t k0 = (uint64_t)blockIdx.x * kBlock;
     const uint64_t k = k0 + threadIdx.x;
     const int W = gt.G + 1;
@@ -380,8 +385,26 @@ __global__ __launch_bounds__(kBlock) void probe_materialize_kernel(View v, const
     if (k < P) {
         const uint64_t info = probe_info[k];
         const uint64_t h = info & 0xFFFFFFFFull;
-        uint32_t gs;
-        build_probe<MG, View>(v, h, h + ((info >> 32) & 0xFFFFull), gt, mp, L, Q, &gs);
+        const uint32_t gsz = (uint32_t)((info >> 32) & 0xFFFFull);
+        bool done = false;
+        if constexpr (RecIB<View>::value > 0) {
+            if (mp.repeat_tol == 0 && mp.enum_tol == 1 && gsz <= (uint32_t)MG) {
+                uint64_t x[MG];
+                #pragma unroll
+                for (int q = 0; q < MG; ++q) x[q] = (uint32_t)q < gsz ? v.rec[h + q] : ~0ull;
+                probe_row_fast<MG, RecIB<View>::value>(x, gsz, gt, L, Q);
+                done = true;
+            }
+        }
+        if (!done) {
+            uint32_t gs;
+            build_probe<MG, View>(v, h, h + gsz, gt, mp, L, Q, &gs);
+        }
+        if (lkey) {
+            const uint64_t xs = (uint64_t)start_at(Q, first_start(Q));
+            lkey[k] = ((uint64_t)line_hash<MG>(Q, gt.G) << 32) | (xs & 0xFFFFFFFFull);
+            fsk[k] = (uint32_t)xs;
+        }
     }
     if constexpr (MG <= 16) {
         // the block's rows are one contiguous range: staged in LDS, stored with consecutive
@@ -424,13 +447,30 @@ __global__ __launch_bounds__(kBlock) void row_bucket_kernel(const int64_t* __res
     out[k] = r;
 }
 
-__global__ __launch_bounds__(kBlock) void gather_rows_kernel(const int64_t* __restrict__ src,
-                                                             const uint32_t* __restrict__ perm, uint64_t P, int W,
-                                                             int64_t* __restrict__ dst) {
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= P * (uint64_t)W) return;
-    const uint64_t k = i / (uint64_t)W, c = i - k * (uint64_t)W;
-    dst[i] = src[(uint64_t)perm[k] * W + c];
+// the same with kGatherIPT elements per thread, all loads in flight together (consecutive
+// lanes stay on consecutive words: a row is read by W neighbouring lanes)
+constexpr int kGatherIPT = 8;
+__global__ __launch_bounds__(kBlock) void gather_rows_ilp_kernel(const int64_t* __restrict__ src,
+                                                                 const uint32_t* __restrict__ perm, uint64_t n, uint32_t W,
+                                                                 int64_t* __restrict__ dst) {
+    const uint64_t e0 = (uint64_t)blockIdx.x * (kBlock * kGatherIPT) + threadIdx.x;
+    uint64_t k = e0 / W;
+    uint32_t c = (uint32_t)(e0 - k * W);
+    const uint32_t dk = kBlock / W, dc = kBlock % W;
+    int64_t x[kGatherIPT];
+    #pragma unroll
+    for (int i = 0; i < kGatherIPT; ++i) {
+        const uint64_t e = e0 + (uint64_t)i * kBlock;
+        x[i] = e < n ? src[(uint64_t)perm[k] * W + c] : 0;
+        k += dk;
+        c += dc;
+        if (c >= W) { c -= W; ++k; }
+    }
+    #pragma unroll
+    for (int i = 0; i < kGatherIPT; ++i) {
+        const uint64_t e = e0 + (uint64_t)i * kBlock;
+        if (e < n) dst[e] = x[i];
+    }
 }
 
 }  // namespace
@@ -440,10 +480,11 @@ uint64_t group_blocks(uint64_t ntiles, bool packed) { return packed ? ntiles * k
 
 template <int MG, typename View>
 hipError_t launch_materialize(View v, const uint64_t* probe_info, uint64_t P, const GenomeTable& gt,
-                              const MatchParams& mp, int L, int64_t* rows, hipStream_t st) {
+                              const MatchParams& mp, int L, int64_t* rows, hipStream_t st, uint64_t* lkey,
+                              uint32_t* fsk) {
     if (P == 0) return hipSuccess;
     hipLaunchKernelGGL((probe_materialize_kernel<MG, View>), dim3((unsigned)((P + kBlock - 1) / kBlock)), dim3(kBlock),
-                       0, st, v, probe_info, P, gt, mp, L, rows);
+                       0, st, v, probe_info, P, gt, mp, L, rows, lkey, fsk);
     return hipGetLastError();
 }
 
@@ -459,8 +500,9 @@ hipError_t launch_gather_rows(const int64_t* src, const uint32_t* perm, uint64_t
                               hipStream_t st) {
     if (P == 0) return hipSuccess;
     const uint64_t n = P * (uint64_t)(G + 1);
-    hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, src, perm,
-                       P, G + 1, dst);
+    const uint64_t per = (uint64_t)kBlock * kGatherIPT;
+    hipLaunchKernelGGL(gather_rows_ilp_kernel, dim3((unsigned)((n + per - 1) / per)), dim3(kBlock), 0, st, src, perm, n,
+                       (uint32_t)(G + 1), dst);
     return hipGetLastError();
 }
 
@@ -510,7 +552,8 @@ MUMS_INST_PROBE(32, PairView<uint64_t>)
 MUMS_INST_PROBE(64, PairView<uint64_t>)
 #define MUMS_INST_MAT(MG, V)                                                                                      \
     template hipError_t launch_materialize<MG, V>(V, const uint64_t*, uint64_t, const GenomeTable&,                \
-                                                  const MatchParams&, int, int64_t*, hipStream_t);
+                                                  const MatchParams&, int, int64_t*, hipStream_t, uint64_t*,      \
+                                                  uint32_t*);
 MUMS_INST_MAT(4, PairView<uint32_t>)
 MUMS_INST_MAT(8, PairView<uint32_t>)
 MUMS_INST_MAT(16, PairView<uint32_t>)

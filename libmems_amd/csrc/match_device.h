@@ -374,13 +374,100 @@ __device__ __forceinline__ bool probe_fast_raw(const uint64_t (&x)[MG + 1], cons
     return accept;
 }
 
+// The probe (starts after SetDirection, CalculateOffset) of an accepted default-tolerance
+// group of cnt (<= G) records x[0 .. cnt) -- packed records (key << IB+1 | parity << IB | index);
+// the parity bit is part of the sort key, so the reference genome (the smallest present) is
+// found, not assumed first.  All loads are the caller's one batch; the same row as build_probe.
+template <int MG, int IB = 32>
+__device__ __forceinline__ void probe_row_fast(const uint64_t (&x)[MG], uint32_t cnt, const GenomeTable& gt, int L,
+                                               Mhe<MG>& P) {
+    using IdxT = typename std::conditional<(IB > 32), uint64_t, uint32_t>::type;
+    const uint32_t G = (uint32_t)gt.G;
+    int64_t st[MG];
+    uint32_t gk[MG], pk[MG];
+    #pragma unroll
+    for (int k = 0; k < MG; ++k) {
+        const IdxT idx = (IdxT)(x[k] & ((1ull << IB) - 1));
+        uint32_t g = 0;
+        IdxT b = 0;
+        #pragma unroll
+        for (int j = 1; j < MG; ++j) {
+            const IdxT bj = (IdxT)gt.base[j];
+            const bool ge = (uint32_t)j < G && idx >= bj;
+            g = ge ? (uint32_t)j : g;
+            b = ge ? bj : b;
+        }
+        gk[k] = (uint32_t)k < cnt ? g : 0xFFu;
+        pk[k] = (uint32_t)(x[k] >> IB) & 1u;
+        st[k] = (int64_t)(idx - b) + 1;
+    }
+    uint32_t gref = 0xFFu, ref_par = 0;
+    int64_t sref = 0;
+    #pragma unroll
+    for (int k = 0; k < MG; ++k) {
+        const bool better = gk[k] < gref;   // (records past cnt carry 0xFF)
+        gref = better ? gk[k] : gref;
+        ref_par = better ? pk[k] : ref_par;
+        sref = better ? st[k] : sref;
+    }
+    int64_t off = 0;
+    #pragma unroll
+    for (int k = 0; k < MG; ++k) {
+        const bool other = gk[k] != gref && gk[k] != 0xFFu;
+        const bool rev = other && pk[k] != ref_par;
+        st[k] = rev ? -st[k] : st[k];
+        off += other ? (st[k] - sref - (rev ? (int64_t)L : 0)) : 0;
+    }
+    P.len = L;
+    P.mersize = L;
+    P.offset = off;
+    #pragma unroll
+    for (int g = 0; g < MG; ++g) {
+        int64_t v = 0;
+        #pragma unroll
+        for (int k = 0; k < MG; ++k) v = gk[k] == (uint32_t)g ? st[k] : v;
+        P.s[g] = v;
+    }
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+    x ^= x >> 30;
+    x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27;
+    x *= 0x94d049bb133111ebull;
+    x ^= x >> 31;
+    return x;
+}
+
+// line invariants: reference start x = s_ref (> 0); per other component the
+// diagonal s_g - s_ref (forward) or |s_g| + s_ref (reverse)
+template <int MG>
+__device__ __forceinline__ uint32_t line_hash(const Mhe<MG>& P, int G) {
+    const int ref = first_start(P);
+    const int64_t x = start_at(P, ref);
+    uint64_t h = 0x9e3779b97f4a7c15ull ^ (uint64_t)ref;
+    #pragma unroll
+    for (int g = 0; g < MG; ++g) {
+        if (g < G && g > ref && P.s[g] != 0) {
+            const int64_t s = P.s[g];
+            const uint64_t d = s > 0 ? (uint64_t)(s - x) : (uint64_t)(-s + x) ^ 0x8000000000000000ull;
+            h = mix64(h ^ d ^ ((uint64_t)g << 56));
+        } else {
+            h = mix64(h ^ ((uint64_t)g << 48));
+        }
+    }
+    return (uint32_t)(h >> 32);
+}
+
+
 // Materialized probes: the AddHashEntry arguments of the seed stage in key order, one
 // row of G+1 int64 per probe: the signed 1-based starts (after SetDirection) and the
 // CalculateOffset value.  The chain labelling and the replay read probes only through
 // this (one contiguous row per probe instead of G+1 gathers from the record stream);
 // the sharded FindMatches ships the same rows between ranks.
 struct MatProbes {
-    const int64_t* rows;   // [P][G + 1]
+    const int64_t* rows;           // [P][G + 1]
+    const uint32_t* fs = nullptr;  // optional: probe k's first-genome start (the replay's keep test)
 };
 
 template <int MG>

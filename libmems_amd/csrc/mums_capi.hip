@@ -103,6 +103,8 @@ struct mums_ctx {
     uint64_t chunk_size = 200000;
     uint32_t nchunks = 0;
     DevBuf cval, ctab;
+    DevBuf fsk;              // FindMatches: first-genome start of each probe (key order)
+    bool fused_keys = false; // materialize_seeds also writes the line keys and fsk (find_tail)
     // one genome's SML / seed frequencies (sml_tools.hip) and filtered MatchLists
     DevBuf smlk0, smlkA, smlkB, smlvA, smlvB, smltmp, flen, fs;
     DevBuf rowsall;          // chunked mode: probe rows of all chunks
@@ -277,6 +279,10 @@ void* devbuf_alloc(void* b, size_t bytes) {
 // chain labelling (chains.hip) then the per-bucket replay (replay.hip) of the P probe
 // rows v (key order), bucket-sorted as ctx->sorted_ids; packed = all genomes (gt layout)
 template <int MG>
+int find_replay(mums_ctx* ctx, MatProbes v, const MatchParams& mp, hipStream_t st);
+
+// v.fs set: the materialize pass also wrote the line keys (chain_lkey_slot) and first starts
+template <int MG>
 int find_rows(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const MatchParams& mp, hipStream_t st) {
     DevCounters* dc = ctx->counters.as<DevCounters>();
     const uint64_t P = ctx->P;
@@ -284,7 +290,15 @@ int find_rows(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const MatchPar
     HIPCHK((launch_chains<MG, MatProbes>(v, nullptr, P, ctx->gt, mp, ctx->ss, packed,
                                     ctx->chain_tmp.p, ctx->tmp.p, ctx->radix_tmp.p, ctx->chain_of.as<uint32_t>(),
                                     ctx->pool.as<int64_t>(), &dc->nchains, st, dc,
-                                    ctx->profiling ? ctx->ev_walk : nullptr, ctx->fk.as<uint32_t>(), 0u)));
+                                    ctx->profiling ? ctx->ev_walk : nullptr, ctx->fk.as<uint32_t>(), 0u,
+                                    v.fs != nullptr)));
+    return find_replay<MG>(ctx, v, mp, st);
+}
+
+template <int MG>
+int find_replay(mums_ctx* ctx, MatProbes v, const MatchParams& mp, hipStream_t st) {
+    DevCounters* dc = ctx->counters.as<DevCounters>();
+    const uint64_t P = ctx->P;
     ctx->walk_events = ctx->profiling;
     HIPCHK(hipEventRecord(ctx->ev[EV_CHAINS], st));
     HIPCHK(hipMemcpyAsync(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
@@ -456,11 +470,13 @@ int materialize_dispatch(mums_ctx* ctx, View sv, const MatchParams& mp, hipStrea
         HIPCHK(ctx->mprobe.ensure((P + 1) * (size_t)(G + 1) * 8));
         rows = ctx->mprobe.as<int64_t>();
     }
-    if (G <= 4) HIPCHK((launch_materialize<4, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st)));
-    else if (G <= 8) HIPCHK((launch_materialize<8, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st)));
-    else if (G <= 16) HIPCHK((launch_materialize<16, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st)));
-    else if (G <= 32) HIPCHK((launch_materialize<32, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st)));
-    else HIPCHK((launch_materialize<64, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st)));
+    uint64_t* lk = ctx->fused_keys ? chain_lkey_slot(ctx->chain_tmp.p, P, G) : nullptr;
+    uint32_t* fs = ctx->fused_keys ? ctx->fsk.as<uint32_t>() : nullptr;
+    if (G <= 4) HIPCHK((launch_materialize<4, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st, lk, fs)));
+    else if (G <= 8) HIPCHK((launch_materialize<8, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st, lk, fs)));
+    else if (G <= 16) HIPCHK((launch_materialize<16, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st, lk, fs)));
+    else if (G <= 32) HIPCHK((launch_materialize<32, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st, lk, fs)));
+    else HIPCHK((launch_materialize<64, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st, lk, fs)));
     return MUMS_OK;
 }
 
@@ -477,8 +493,11 @@ int materialize_seeds(mums_ctx* ctx, const MatchParams& mp, hipStream_t st) {
 
 // FindMatches after the bucket sort (ctx->P probes, ctx->sorted_ids / sorted_buckets):
 // workspace, bucket ranges, [rows()] materialize, chains + replay, MatchList (A10-A12)
+// stream_rows: rows() is materialize_seeds (the seed stage's probes from its merged stream):
+// in the single-pass path it also writes the line keys and first starts (ctx->fused_keys)
 template <typename Rows>
-int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows&& rows, hipStream_t st) {
+int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows&& rows, hipStream_t st,
+              bool stream_rows = false) {
     DevCounters* dc = ctx->counters.as<DevCounters>();
     const int G = ctx->gt.G;
     const uint32_t Tb = ctx->table_size;
@@ -498,7 +517,8 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
         HIPCHK(ctx->pool.ensure((ctx->P + 1) * (size_t)(G + 2) * 8));
         HIPCHK(ctx->chain_tmp.ensure(chain_tmp_bytes(ctx->P + 1, Tb, G)));
     }
-    HIPCHK(ctx->radix_tmp.ensure(radix_tmp_bytes(ctx->P + 1)));
+    HIPCHK(ctx->radix_tmp.ensure(std::max(radix_tmp_bytes(ctx->P + 1),
+                                          chain_radix_tmp_bytes(std::min<uint64_t>(ctx->P, find_chunk()) + 1))));
     HIPCHK(ctx->tmp.ensure(std::max(scan_tmp_bytes(ctx->P + 1), scan_tmp_bytes(Tb))));
     HIPCHK(hipMemsetAsync(&dc->max_bucket, 0, 4, st));
     HIPCHK(hipMemsetAsync(ctx->bstart.p, 0, (size_t)Tb * 4, st));
@@ -511,8 +531,13 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
     if (ctx->P == 0) HIPCHK(hipEventRecord(ctx->ev[EV_CHAINS], st));
     if (ctx->P > 0) {
         MatProbes v{};
+        // the seed stage's own probes, one pass: rows plus line keys and first starts
+        ctx->fused_keys = stream_rows && !chunked;
+        if (ctx->fused_keys) HIPCHK(ctx->fsk.ensure((ctx->P + 1) * 4));
         int rc = rows(&v);
+        ctx->fused_keys = false;
         if (rc) return rc;
+        if (stream_rows && !chunked) v.fs = ctx->fsk.as<uint32_t>();
         if (chunked) {   // the rows hold all FindMatches reads: keep the bucket order only
             // the dead records (recA / recB, when the packed path sized them) are the arena
             // of the sliced FindMatches: bucket order and summaries in recB, chain scratch
@@ -1139,7 +1164,7 @@ int run_pipeline(mums_ctx* ctx, int stage) {
             const int r = materialize_seeds(ctx, mp, st);
             v->rows = ctx->mprobe.as<int64_t>();
             return r;
-        }, st);
+        }, st, true);
         if (rc) return rc;
     }
     HIPCHK(hipStreamSynchronize(st));
@@ -1409,7 +1434,7 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
             const int r = materialize_seeds(ctx, mp, st);
             v->rows = ctx->mprobe.as<int64_t>();
             return r;
-        }, st);
+        }, st, true);
         if (rc) return rc;
     }
     HIPCHK(hipStreamSynchronize(st));
@@ -1531,7 +1556,7 @@ int mums_ctx_destroy(mums_ctx* ctx) {
                       &ctx->smlvB, &ctx->smltmp, &ctx->flen, &ctx->fs, &ctx->rowsall, &ctx->rsbuf,
                       &ctx->rsplan, &ctx->rsbst, &ctx->pool_loc, &ctx->cbuf, &ctx->sids,
                       &ctx->logA, &ctx->logB, &ctx->logvA, &ctx->logvB, &ctx->tiebuf, &ctx->fk, &ctx->fkloc,
-                      &ctx->crbuf, &ctx->crcnt, &ctx->crlive, &ctx->crruns, &ctx->crall};
+                      &ctx->crbuf, &ctx->crcnt, &ctx->crlive, &ctx->crruns, &ctx->crall, &ctx->fsk};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i < EV_COUNT; ++i)
         if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);

@@ -223,8 +223,10 @@ hipError_t launch_probe_compact(uint64_t nblocks, const uint32_t* tile_count, co
                                 uint32_t* probe_bucket, hipStream_t st, bool packed);
 // probes (key order) -> materialized rows (MatProbes, match_device.h)
 template <int MG, typename View>
+// lkey / fsk (optional): each probe's line key (chain_lkey_slot) and first-genome start
 hipError_t launch_materialize(View v, const uint64_t* probe_info, uint64_t P, const GenomeTable& gt,
-                              const MatchParams& mp, int L, int64_t* rows, hipStream_t st);
+                              const MatchParams& mp, int L, int64_t* rows, hipStream_t st, uint64_t* lkey = nullptr,
+                              uint32_t* fsk = nullptr);
 // hash bucket of every row (d_bounds == nullptr) or its owning rank (bucket ranges)
 hipError_t launch_row_buckets(const int64_t* rows, uint64_t P, int G, uint32_t table_size, const uint32_t* d_bounds,
                               uint32_t nranks, uint32_t* out, hipStream_t st);
@@ -286,11 +288,16 @@ size_t chain_merge_tmp_bytes(uint64_t n);
 hipError_t launch_chain_merge(const int64_t* pool_loc, uint64_t n, int G, uint32_t* chain_of, uint64_t P,
                               int64_t* pool_out, void* d_tmp, void* d_radix_tmp, void* d_scan_tmp, uint32_t* d_nchains,
                               hipStream_t st, const uint32_t* fk_loc, uint32_t* fk_out);
+// radix scratch of launch_chains / launch_chains_stream for P probes (the line sort)
+size_t chain_radix_tmp_bytes(uint64_t P);
 template <int MG, typename View>
 hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const GenomeTable& gt, const MatchParams& mp,
                          const SeedSpec& ss, const uint32_t* packed, void* d_chain_tmp, void* d_scan_tmp,
                          void* d_radix_tmp, uint32_t* chain_of, int64_t* pool, uint32_t* d_nchains, hipStream_t st,
-                         void* ctr, hipEvent_t* ev_walk, uint32_t* fk, uint32_t kbase);
+                         void* ctr, hipEvent_t* ev_walk, uint32_t* fk, uint32_t kbase, bool lkey_ready = false);
+// where launch_chains(d_chain_tmp, P probes, G) reads the line keys from: a producer that
+// writes them there (launch_materialize) lets launch_chains skip its key pass (lkey_ready)
+uint64_t* chain_lkey_slot(void* d_chain_tmp, uint64_t P, int G);
 hipError_t launch_emit(const uint32_t* obase, const uint32_t* bstart, const uint32_t* tbl, const int64_t* pool, int G,
                        uint32_t table_size, uint64_t M, uint64_t* out_len, int64_t* out_s, hipStream_t st);
 

@@ -52,6 +52,9 @@ constexpr int kSortTile = MUMS_SORT_TILE;      // records per onesweep tile (lon
 #ifndef MUMS_LOOKBACK
 #define MUMS_LOOKBACK 4
 #endif
+#ifndef MUMS_OS_CTILES
+#define MUMS_OS_CTILES 0    // 1: descriptors copied into claim order (one load per claim): measured 1.3 % slower per pass
+#endif
 
 constexpr int kLookback = MUMS_LOOKBACK;       // predecessor statuses fetched per look-back step
 inline uint64_t ub_status(uint64_t ub, int npass) { return ub * kDigits * (uint64_t)npass; }
@@ -145,6 +148,18 @@ __global__ __launch_bounds__(256) void claim_order_kernel(const uint32_t* __rest
         pos += (n < k ? n : k) + ((uint32_t)b < d.bucket && n > k ? 1u : 0u);
     }
     tiles[pos].order = (uint32_t)t;
+}
+
+// ctiles[c] = the descriptor of the c-th claimed tile (ctiles[c].order = its tile index): a
+// claiming block then reads its tile with one load after the claim
+__global__ __launch_bounds__(256) void claim_tiles_kernel(const SegTile* __restrict__ tiles, uint64_t ub,
+                                                          SegTile* __restrict__ ctiles) {
+    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= ub) return;
+    const uint32_t t = tiles[c].order;
+    SegTile d = tiles[t];
+    d.order = t;
+    ctiles[c] = d;
 }
 
 __global__ __launch_bounds__(kBlock) void seg_upsweep(const uint64_t* __restrict__ rec, const SegTile* __restrict__ tiles,
@@ -383,8 +398,13 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
     __syncthreads();
     const uint32_t c = __builtin_amdgcn_readfirstlane(s_tile);   // uniform: scalar descriptor loads
     if (c >= nclaims) return;
+#if MUMS_OS_CTILES
+    const SegTile d = tiles[c];   // claim-ordered copy (claim_tiles_kernel)
+    const uint32_t t = __builtin_amdgcn_readfirstlane(d.order);
+#else
     const uint32_t t = __builtin_amdgcn_readfirstlane(tiles[c].order);
     const SegTile d = tiles[t];
+#endif
     if (d.count == 0) return;
     const uint32_t q0 = wv * (kT / kW);
     uint64_t key[kIPT];
@@ -1161,8 +1181,8 @@ size_t onesweep_tmp_bytes(uint64_t n, int msd_bits, int key_bits) {
     const uint64_t ub = seg_tiles_upper(n, msd_bits, os_tile());
     const int npass = (key_bits + 7) / 8;
     const uint64_t nb = 1ull << msd_bits;
-    return (ub * kDigits * (uint64_t)npass + 2 * nb * npass * kDigits + 64 + 64) * 4 + ub * sizeof(SegTile) + 256 +
-           seg_build_tmp_bytes(nb) + segfix_cap(n) * 4 + 256;   // + the segment fix-up's big list
+    return (ub * kDigits * (uint64_t)npass + 2 * nb * npass * kDigits + 64 + 64) * 4 + 2 * (ub * sizeof(SegTile) + 256) +
+           seg_build_tmp_bytes(nb) + segfix_cap(n) * 4 + 256;   // + the claim-ordered copy, the fix-up's big list
 }
 
 // segment fix-up launches: big_count[0..1] zeroed by the caller, big_list in d_list
@@ -1230,11 +1250,18 @@ hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key
     uint32_t* counters = dbase + nb * npass * kDigits;         // [npass] + ntiles
     const size_t zero_bytes = ((uint64_t)(counters - status) + 64) * 4;
     SegTile* stiles = (SegTile*)((char*)d_tmp + ((zero_bytes + 255) & ~(size_t)255));
-    void* btmp = (void*)((char*)stiles + ((ub * sizeof(SegTile) + 255) & ~(size_t)255));
+    SegTile* ctiles = (SegTile*)((char*)stiles + ((ub * sizeof(SegTile) + 255) & ~(size_t)255));
+    void* btmp = (void*)((char*)ctiles + ((ub * sizeof(SegTile) + 255) & ~(size_t)255));
     hipError_t e = hipMemsetAsync(status, 0, zero_bytes, st);
     if (e != hipSuccess) return e;
     e = build_seg_tiles_from_starts(d_bstart, msd_bits, n, stiles, counters + 32, btmp, st, tile);
     if (e != hipSuccess) return e;
+#if MUMS_OS_CTILES
+    hipLaunchKernelGGL(claim_tiles_kernel, dim3((unsigned)((ub + 255) / 256)), dim3(256), 0, st, stiles, ub, ctiles);
+    const SegTile* otiles = ctiles;   // what the onesweep launches read
+#else
+    const SegTile* otiles = stiles;
+#endif
     const unsigned gblocks = (unsigned)((ub + kGhistTilesPerBlock - 1) / kGhistTilesPerBlock);
     // the histogram read counts digit 0 only when every later pass's digits are
     // counted by the pass before it (MUMS_OS_NEXTHIST, plain onesweep kernel)
@@ -1274,7 +1301,7 @@ hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key
             uint32_t* sp = status + (uint64_t)p * ub * kDigits;
             const int sh = key_shift + 8 * p;
 #define MUMS_OS_LAUNCH(OB, IPT, AL)                                                                               \
-    hipLaunchKernelGGL((seg_onesweep_kernel<OB, IPT, AL>), dim3((unsigned)ub), dim3(OB), 0, st, src, dst, stiles, \
+    hipLaunchKernelGGL((seg_onesweep_kernel<OB, IPT, AL>), dim3((unsigned)ub), dim3(OB), 0, st, src, dst, otiles, \
                        (uint32_t)ub, sh, p, npass, dbase, sp, counters + p, d_err, gn)
             switch (os_variant()) {
             case 1: MUMS_OS_LAUNCH(512, 16, true); break;

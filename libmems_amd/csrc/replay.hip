@@ -1414,7 +1414,8 @@ __global__ __launch_bounds__(kBlock) void keep_fill_kernel(const int64_t* __rest
                                                            const uint32_t* __restrict__ chain_of,
                                                            const uint4* __restrict__ ck,
                                                            unsigned int* __restrict__ nkept, uint64_t cap,
-                                                           uint64_t* __restrict__ kept) {
+                                                           uint64_t* __restrict__ kept,
+                                                           const uint32_t* __restrict__ fsk) {
     __shared__ uint32_t s_w[kBlock / 64 + 1];
     __shared__ int64_t srow[kBlock * kKeepStageW];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1427,7 +1428,14 @@ __global__ __launch_bounds__(kBlock) void keep_fill_kernel(const int64_t* __rest
         const uint64_t k0 = (uint64_t)blockIdx.x * (kBlock * kKeepIPT) + (uint64_t)i * kBlock;
         const uint64_t k = k0 + threadIdx.x;
         keys[i] = 0;
-        if (staged) {
+        if (fsk) {   // first-genome starts in key order (rows stored in line order)
+            if (k < P) {
+                const uint4 c = ck[chain_of[k]];
+                const bool keep = c.x == (uint32_t)k || fsk[k] >= c.y;
+                keys[i] = ((uint64_t)c.z << 32) | k;
+                if (keep) want |= 1u << i;
+            }
+        } else if (staged) {
             // the round's rows are one contiguous range: read it with consecutive lanes on
             // consecutive words (one lane per row touches a 128-B line per lane)
             if (k0 < P) {
@@ -1586,7 +1594,7 @@ hipError_t launch_replay_kept(View v, const GenomeTable& gt, const MatchParams& 
         kept = (uint64_t*)cb;
         if ((e = hipMemsetAsync(nkept, 0, 4, st)) != hipSuccess) return e;
         hipLaunchKernelGGL(keep_fill_kernel, dim3((unsigned)nblk), dim3(kBlock), 0, st, v.rows, P, G, chain_of,
-                           (const uint4*)ckeep, nkept, cap, kept);
+                           (const uint4*)ckeep, nkept, cap, kept, v.fs);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if ((e = hipMemcpyAsync(&Kc, nkept, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
