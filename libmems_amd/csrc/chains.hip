@@ -859,8 +859,7 @@ ChainWs chain_ws(void* d_chain_tmp, uint64_t P, int G, bool with_rows) {
 hipError_t line_sort(const ChainWs& w, uint64_t P, int xbits, void* d_tmp, uint32_t* d_err, hipStream_t st,
                      const uint32_t** ord_out) {
     hipError_t e;
-    const uint32_t hb[2] = {0u, (uint32_t)P};
-    if ((e = hipMemcpyAsync(w.bst, hb, 8, hipMemcpyHostToDevice, st)) != hipSuccess) return e;
+    if ((e = seg_bucket_starts(nullptr, 0, 0, P, w.bst, st)) != hipSuccess) return e;
     hipLaunchKernelGGL(line_rec1_kernel, dim3(grid_of(P)), dim3(kBlock), 0, st, w.lkey, P, w.kA);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     int b1 = 0;
@@ -873,7 +872,6 @@ hipError_t line_sort(const ChainWs& w, uint64_t P, int xbits, void* d_tmp, uint3
     if ((e = seg_onesweep_sort(r2, w.lkey, P, 32, 0, w.bst, d_tmp, d_err, &b2, st)) != hipSuccess) return e;
     const uint64_t* s2 = b2 ? w.lkey : r2;
     hipLaunchKernelGGL(line_ord_kernel, dim3(grid_of(P)), dim3(kBlock), 0, st, s1, s2, P, w.vA);
-    if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;   // (hb is a host temporary)
     *ord_out = w.vA;
     return hipGetLastError();
 }

@@ -473,7 +473,37 @@ __global__ __launch_bounds__(kBlock) void gather_rows_ilp_kernel(const int64_t* 
     }
 }
 
+// the probes' bucket partition as packed records (bucket << 32 | probe) for the onesweep
+// sort, and back to the two arrays the consumers read
+__global__ __launch_bounds__(kBlock) void bucket_rec_kernel(const uint32_t* __restrict__ b, uint64_t P,
+                                                            uint64_t* __restrict__ rec) {
+    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k < P) rec[k] = ((uint64_t)b[k] << 32) | k;
+}
+
+__global__ __launch_bounds__(kBlock) void bucket_split_kernel(const uint64_t* __restrict__ rec, uint64_t P,
+                                                              uint32_t* __restrict__ b, uint32_t* __restrict__ ids) {
+    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= P) return;
+    const uint64_t r = rec[k];
+    b[k] = (uint32_t)(r >> 32);
+    ids[k] = (uint32_t)r;
+}
+
 }  // namespace
+
+hipError_t launch_bucket_records(const uint32_t* b, uint64_t P, uint64_t* rec, hipStream_t st) {
+    if (P == 0) return hipSuccess;
+    hipLaunchKernelGGL(bucket_rec_kernel, dim3((unsigned)((P + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, b, P, rec);
+    return hipGetLastError();
+}
+
+hipError_t launch_bucket_split(const uint64_t* rec, uint64_t P, uint32_t* b, uint32_t* ids, hipStream_t st) {
+    if (P == 0) return hipSuccess;
+    hipLaunchKernelGGL(bucket_split_kernel, dim3((unsigned)((P + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, rec, P, b,
+                       ids);
+    return hipGetLastError();
+}
 
 uint64_t group_slot_count(uint64_t ntiles) { return ntiles * kSlots; }
 uint64_t group_blocks(uint64_t ntiles, bool packed) { return packed ? ntiles * kGSplit : ntiles; }

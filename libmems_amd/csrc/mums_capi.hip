@@ -104,6 +104,7 @@ struct mums_ctx {
     uint32_t nchunks = 0;
     DevBuf cval, ctab;
     DevBuf fsk;              // FindMatches: first-genome start of each probe (key order)
+    DevBuf bst2;             // {0, P}: the one bucket of the probes' onesweep bucket sort
     bool fused_keys = false; // materialize_seeds also writes the line keys and fsk (find_tail)
     // one genome's SML / seed frequencies (sml_tools.hip) and filtered MatchLists
     DevBuf smlk0, smlkA, smlkB, smlvA, smlvB, smltmp, flen, fs;
@@ -125,12 +126,13 @@ struct mums_ctx {
     DevBuf crall;                         // sharded restart planner: the whole stream's SMLs
     bool shard_restart_pending = false;   // mums_shard_merge saw a group above the limit / start points
     int shard_mb = 0;                     // local bucket bits of the last mums_shard_merge
+    int shard_side = 0;                   // 33-bit records at w20-21: side bits split below the 8-bit scatter
     uint64_t shard_n = 0;                 // its records
     bool ties_fixed = false;              // the stream holds every run of equal keys in std::sort order
     uint64_t tie_slots = 0;               // slots of the runs replayed by the last run (stats)
     // seed-stage-only chunked runs keep the tie workspace between calls when memory allows:
     // its hipMalloc is 3-4 s at 2 x 3 Gbp (135 GB), the replay itself 0.15 s
-    bool keep_tiebuf = false;
+    int keep_tiebuf = 0;                  // 1: keep when memory stays free beside it, 2: keep (the tail lives inside)
     bool tiebuf_kept = false;             // the last chunked seed-stage-only call kept tiebuf
     uint64_t restarts = 0;
     std::vector<uint64_t> offset_log;     // start points after every restart (R x G)
@@ -182,6 +184,9 @@ struct mums_ctx {
 };
 
 namespace {
+
+void release_tiebuf(mums_ctx* ctx);
+hipError_t tiebuf_ensure(mums_ctx* ctx, size_t bytes);
 
 int fail(mums_ctx* c, int code, const std::string& msg) {
     if (c) c->err = msg;
@@ -554,8 +559,13 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
             ctx->sorted_key = nullptr;
             ctx->sorted_idx = nullptr;
             ctx->rowtmp.drop_view();
-            if (!(arena && ctx->chain_tmp.borrow(ctx->recA, 0, chain_tmp_bytes(find_chunk() + 1, Tb, G))))
-                HIPCHK(ctx->chain_tmp.ensure(chain_tmp_bytes(find_chunk() + 1, Tb, G)));
+            const size_t cbytes = chain_tmp_bytes(find_chunk() + 1, Tb, G);
+            // a kept tie workspace holding the rows (run_pipeline_chunked) holds the chain
+            // scratch behind them
+            const bool in_tie = ctx->rowsall.borrowed && ctx->tiebuf.p && ctx->rowsall.p == ctx->tiebuf.p &&
+                                ctx->chain_tmp.borrow(ctx->tiebuf, ctx->rowsall.cap, cbytes);
+            if (!in_tie && !(arena && ctx->chain_tmp.borrow(ctx->recA, 0, cbytes)))
+                HIPCHK(ctx->chain_tmp.ensure(cbytes));
             for (DevBuf* b : {&ctx->pbuf, &ctx->tiles, &ctx->rowtmp, &ctx->kA, &ctx->kB, &ctx->vA, &ctx->vB,
                               &ctx->ckey, &ctx->mprobe})
                 if (!(b->p && (char*)v.rows >= (char*)b->p && (char*)v.rows < (char*)b->p + b->cap)) b->release();
@@ -599,7 +609,7 @@ struct ProbeSpace {
 };
 
 int ensure_probe_space(mums_ctx* ctx, uint64_t N, uint64_t ntiles_groups, ProbeSpace* ps) {
-    const uint64_t pcap = N / 2 + 1;
+    const uint64_t pcap = (N / 2 + 2) & ~1ull;   // even: bucketB is 8-B aligned (finish_seeds)
     const uint64_t nslots = group_slot_count(ntiles_groups);
     HIPCHK(ctx->partials.ensure((3 * group_blocks(ntiles_groups, true) + 128) * 4));
     HIPCHK(ctx->pbuf.ensure(pcap * (8 + 4 * 4) + nslots * 12 + 256));
@@ -645,15 +655,25 @@ int keys_stage(mums_ctx* ctx, const GenomeTable& lgt, uint32_t T, int B, uint64_
     for (int g = 0; g < lgt.G; ++g) ptrs[g] = ctx->genomes[g].d_ptr;
     uint32_t* hist = ctx->hist.as<uint32_t>();
     if (side > 0) {
-        if (ib != 32 || B != 8 + side || out == ctx->recB.as<uint64_t>()) return fail(ctx, MUMS_E_INVALID, "msd split");
+        if (B != 8 + side || out == ctx->recB.as<uint64_t>() || (ib != 32 && ib != 33))
+            return fail(ctx, MUMS_E_INVALID, "msd split");
         HIPCHK(ctx->side.ensure(n + 64));
         HIPCHK(ctx->bst8.ensure((256 + 64) * 4));
+        HIPCHK(ctx->recB.ensure(n * 8 + 64));
         HIPCHK(ctx->tmp.ensure(std::max(ctx->tmp.cap, msd_split_tmp_bytes(n, 8))));
         HIPCHK(launch_seed_pack(ctx->ss, lgt, ptrs.data(), ctx->packed.as<uint32_t>(), 1, true, nullptr, 8, hist, T,
                                 &dc->err, st));
         HIPCHK(exclusive_scan_u32(hist, (uint64_t)T << 8, ctx->tmp.p, nullptr, st));
-        HIPCHK(launch_seed_scatter(ctx->ss, lgt, ctx->packed.as<uint32_t>(), 8, hist, T, ctx->recB.as<uint64_t>(), st,
-                                   ctx->side.as<uint8_t>(), side));
+        if (ib == 32) {
+            HIPCHK(launch_seed_scatter(ctx->ss, lgt, ctx->packed.as<uint32_t>(), 8, hist, T, ctx->recB.as<uint64_t>(),
+                                       st, ctx->side.as<uint8_t>(), side));
+        } else {   // 33-bit indices (sharded above 2^32 seed-mers, w20-21): chunked.hip's scatter, one chunk
+            HIPCHK(ctx->ctab.ensure(64));
+            HIPCHK(hipMemsetAsync(ctx->ctab.p, 0, 64, st));
+            HIPCHK(launch_seed_scatter_chunk(ctx->ss, lgt, ctx->packed.as<uint32_t>(), 8, hist, T, 0, 0,
+                                             ctx->recB.as<uint64_t>(), st, ctx->ctab.as<uint64_t>(), 8,
+                                             ctx->side.as<uint8_t>(), side));
+        }
         HIPCHK(seg_bucket_starts(hist, T, 8, n, ctx->bst8.as<uint32_t>(), st));
         HIPCHK(msd_split(ctx->recB.as<uint64_t>(), ctx->side.as<uint8_t>(), out, n, 8, side, ctx->bst8.as<uint32_t>(),
                          bstart, ctx->tmp.p, st));
@@ -758,11 +778,33 @@ int finish_seeds(mums_ctx* ctx, const ProbeSpace& ps, hipStream_t st) {
     HIPCHK(hipEventRecord(ctx->ev[EV_GROUPS], st));
     int tbits = 1;
     while (tbits < 32 && ((uint64_t)1 << tbits) < (uint64_t)ctx->table_size) ++tbits;
-    int pout = 0;
-    HIPCHK(radix_sort<uint32_t>(ps.probe_bucket, nullptr, ctx->P, tbits, ps.bucketB, ps.idsA, ps.probe_bucket,
-                                ps.idsB, ctx->tmp.p, &pout, st));
-    ctx->sorted_buckets = pout ? ps.probe_bucket : ps.bucketB;
-    ctx->sorted_ids = pout ? ps.idsB : ps.idsA;
+    const uint64_t P = ctx->P;
+    // the onesweep variant (MUMS_DEV_BUCKET_ONESWEEP) moves packed 8-B records: 2.36 vs 1.56 ms
+    // on C3's 1e8 probes (u32 keys and ids in the radix passes move fewer bytes)
+    static const bool radix = getenv("MUMS_DEV_BUCKET_ONESWEEP") == nullptr;
+    // (the seed sort's scratch holds the onesweep workspace: ctx->tmp is not regrown here, other
+    // stages may hold pointers into it)
+    if (!radix && P >= 4096 && P < (1ull << 30) && ps.slot_info + P <= (const uint64_t*)ps.probe_bucket &&
+        ctx->tmp.cap >= onesweep_tmp_bytes(P, 0, tbits)) {
+        // one onesweep sort of packed (bucket << 32 | probe) records: the dead slot array and
+        // [bucketB, idsA] are the ping-pong pair, the sorted partition lands in probe_bucket / idsB
+        uint64_t* rA = ps.slot_info;
+        uint64_t* rB = (uint64_t*)ps.bucketB;
+        HIPCHK(ctx->bst2.ensure(64));
+        HIPCHK(launch_bucket_records(ps.probe_bucket, P, rA, st));
+        HIPCHK(seg_bucket_starts(nullptr, 0, 0, P, ctx->bst2.as<uint32_t>(), st));
+        int ob = 0;
+        HIPCHK(seg_onesweep_sort(rA, rB, P, tbits, 0, ctx->bst2.as<uint32_t>(), ctx->tmp.p, &dc->err, &ob, st));
+        HIPCHK(launch_bucket_split(ob ? rB : rA, P, ps.probe_bucket, ps.idsB, st));
+        ctx->sorted_buckets = ps.probe_bucket;
+        ctx->sorted_ids = ps.idsB;
+    } else {
+        int pout = 0;
+        HIPCHK(radix_sort<uint32_t>(ps.probe_bucket, nullptr, P, tbits, ps.bucketB, ps.idsA, ps.probe_bucket,
+                                    ps.idsB, ctx->tmp.p, &pout, st));
+        ctx->sorted_buckets = pout ? ps.probe_bucket : ps.bucketB;
+        ctx->sorted_ids = pout ? ps.idsB : ps.idsA;
+    }
     HIPCHK(hipEventRecord(ctx->ev[EV_BUCKETS], st));
     return MUMS_OK;
 }
@@ -841,7 +883,7 @@ int tie_order(mums_ctx* ctx, uint64_t n, const uint64_t* ck, const uint64_t* ckf
     const GenomeTable& gt = ctx->gt;
     *flagged = 0;
     if (n >= 0xFFFFFFF0ull) return fail(ctx, MUMS_E_UNSUPPORTED, "SortedMerList tie order above 2^32 seed-mers");
-    HIPCHK(ctx->tiebuf.ensure(tie_ws_bytes(n, gt.G)));
+    HIPCHK(tiebuf_ensure(ctx, tie_ws_bytes(n, gt.G)));
     *tw = tie_ws_layout(ctx->tiebuf.p, n, gt.G);
     HIPCHK(tie_set_genomes(*tw, gt.base, gt.m, st));
     HIPCHK(tie_clear_flags(*tw, st));
@@ -1515,8 +1557,15 @@ int prepare_shard(mums_ctx* ctx) {
     // then holds 2w+1-B = 31 bits: w19 with B = 8)
     const bool big = ctx->gt.base[ctx->gt.G] >= 0xFFFFFFF0ull || getenv("MUMS_DEV_SHARD_IB33") != nullptr;
     ctx->rec_ib = big ? 33 : 32;
-    if (big && (2 * ctx->w + 1 - ctx->msd_bits != 31 || ctx->msd_bits > 8))
-        return fail(ctx, MUMS_E_UNSUPPORTED, "sharded mode above 2^32 seed-mers needs seed weight 19");
+    ctx->shard_side = 0;
+    if (big && 2 * ctx->w + 1 - 31 > 8 && 2 * ctx->w + 1 - 31 <= 12) {
+        // w20-21 (getDefaultSeedWeight of 3 Gbp genomes, SeedMasks.h:389-401): 31 key bits in
+        // the record, 8 MSD bits scattered + 2-4 side bits split before the exchange (msdsplit.hip)
+        ctx->msd_bits = 2 * ctx->w + 1 - 31;
+        ctx->shard_side = ctx->msd_bits - 8;
+    } else if (big && (2 * ctx->w + 1 - ctx->msd_bits != 31 || ctx->msd_bits > 8)) {
+        return fail(ctx, MUMS_E_UNSUPPORTED, "sharded mode above 2^32 seed-mers needs seed weight 19-21");
+    }
     return MUMS_OK;
 }
 
@@ -1556,7 +1605,7 @@ int mums_ctx_destroy(mums_ctx* ctx) {
                       &ctx->smlvB, &ctx->smltmp, &ctx->flen, &ctx->fs, &ctx->rowsall, &ctx->rsbuf,
                       &ctx->rsplan, &ctx->rsbst, &ctx->pool_loc, &ctx->cbuf, &ctx->sids,
                       &ctx->logA, &ctx->logB, &ctx->logvA, &ctx->logvB, &ctx->tiebuf, &ctx->fk, &ctx->fkloc,
-                      &ctx->crbuf, &ctx->crcnt, &ctx->crlive, &ctx->crruns, &ctx->crall, &ctx->fsk};
+                      &ctx->crbuf, &ctx->crcnt, &ctx->crlive, &ctx->crruns, &ctx->crall, &ctx->fsk, &ctx->bst2};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i < EV_COUNT; ++i)
         if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
@@ -1667,8 +1716,7 @@ int mums_find_stage(mums_ctx* ctx, int stage) {
                                              "the reference hashes them into an unsized thread table");
     // the chunked mode may keep its (config-5-sized) tie workspace between seed-stage-only
     // calls; any other pipeline sizes its own
-    if (!big && ctx->tiebuf_kept) ctx->tiebuf.release();
-    ctx->tiebuf_kept = false;
+    if (!big && ctx->tiebuf_kept) release_tiebuf(ctx);
     if (ctx->pairwise || ctx->enum_tol > 1) return run_pipeline_pairwise(ctx, stage);
     if (ctx->pcompat) return run_pipeline_compat(ctx, stage);
     return big ? run_pipeline_chunked(ctx, stage) : run_pipeline(ctx, stage);
@@ -1811,7 +1859,7 @@ int genome_sml(mums_ctx* ctx, uint32_t genome, const uint64_t** sk, const uint32
     *sv = buf ? ctx->smlvB.as<uint32_t>() : ctx->smlvA.as<uint32_t>();
     if (m > 1) {   // equal mers in std::sort order (MemorySML.cpp:54; smlsort.hip)
         if (m >= 0xFFFFFFF0ull) return fail(ctx, MUMS_E_UNSUPPORTED, "SortedMerList of more than 2^32 seed-mers");
-        HIPCHK(ctx->tiebuf.ensure(tie_ws_bytes(m, 1)));
+        HIPCHK(tiebuf_ensure(ctx, tie_ws_bytes(m, 1)));
         const TieWs tw = tie_ws_layout(ctx->tiebuf.p, m, 1);
         const uint64_t b0 = 0;
         HIPCHK(tie_set_genomes(tw, &b0, &m, st));
@@ -2191,7 +2239,7 @@ int mums_shard_keys(mums_ctx* ctx, uint64_t* d_records, uint64_t capacity, uint6
     HIPCHK(hipMemsetAsync(dc, 0, sizeof(DevCounters), st));
     std::vector<uint32_t> hs(nb + 1, 0);
     if (l.G > 0 && n > 0) {
-        rc = keys_stage(ctx, l, T, B, n, d_records, ctx->mstart.as<uint32_t>(), st, ctx->rec_ib);
+        rc = keys_stage(ctx, l, T, B, n, d_records, ctx->mstart.as<uint32_t>(), st, ctx->rec_ib, ctx->shard_side);
         if (rc) return rc;
         HIPCHK(hipMemcpyAsync(hs.data(), ctx->mstart.p, (nb + 1) * 4, hipMemcpyDeviceToHost, st));
     }
@@ -2744,6 +2792,24 @@ void release_find_buffers(mums_ctx* ctx) {
     ctx->M = 0;
 }
 
+// the tie workspace, and the views the chunked FindMatches keeps inside it (rows, chain scratch)
+void release_tiebuf(mums_ctx* ctx) {
+    auto inside = [&](const DevBuf& b) {
+        return b.borrowed && ctx->tiebuf.p && (const char*)b.p >= (const char*)ctx->tiebuf.p &&
+               (const char*)b.p < (const char*)ctx->tiebuf.p + ctx->tiebuf.cap;
+    };
+    for (DevBuf* b : {&ctx->rowsall, &ctx->chain_tmp})
+        if (inside(*b)) b->release();
+    ctx->tiebuf.release();
+    ctx->tiebuf_kept = false;
+}
+
+// tiebuf.ensure that first drops the views inside the workspace when it must reallocate
+hipError_t tiebuf_ensure(mums_ctx* ctx, size_t bytes) {
+    if (bytes > ctx->tiebuf.cap) release_tiebuf(ctx);
+    return ctx->tiebuf.ensure(bytes);
+}
+
 // free device memory left beside a kept tie workspace (the chunk loop's buffers)
 constexpr size_t kKeepTieFree = 24ull << 30;
 
@@ -3057,7 +3123,7 @@ int stream_restart(mums_ctx* ctx, uint64_t* srec, uint64_t* other, const std::ve
             if (!any) continue;
             const uint64_t m = gt.m[g];
             if (m >= 0xFFFFFFF0ull) return fail(ctx, MUMS_E_UNSUPPORTED, "SortedMerList of more than 2^32 seed-mers");
-            if (ctx->tiebuf.ensure(tie_ws_bytes(m, 1)) != hipSuccess) {
+            if (tiebuf_ensure(ctx, tie_ws_bytes(m, 1)) != hipSuccess) {
                 // the previous FindMatches' tail buffers are dead during the seed stage: free them
                 // and try again (2 x 3 Gbp: ~135 GB of tie workspace beside 96 GB of records)
                 (void)hipGetLastError();
@@ -3065,7 +3131,7 @@ int stream_restart(mums_ctx* ctx, uint64_t* srec, uint64_t* other, const std::ve
                 pc.mark("tie workspace (first try)");
                 release_find_buffers(ctx);
                 pc.mark("FindMatches buffers freed");
-                if (ctx->tiebuf.ensure(tie_ws_bytes(m, 1)) != hipSuccess)
+                if (tiebuf_ensure(ctx, tie_ws_bytes(m, 1)) != hipSuccess)
                     return fail(ctx, MUMS_E_NOMEM, "restart: no device memory for the SortedMerList tie order of a "
                                                    "genome");
             }
@@ -3096,8 +3162,9 @@ int stream_restart(mums_ctx* ctx, uint64_t* srec, uint64_t* other, const std::ve
         }
         HIPCHK(hipStreamSynchronize(st));
         size_t free_b = 0, total_b = 0;
-        if (!(ctx->keep_tiebuf && hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b >= kKeepTieFree))
-            ctx->tiebuf.release();
+        if (!(ctx->keep_tiebuf == 2 ||
+              (ctx->keep_tiebuf == 1 && hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b >= kKeepTieFree)))
+            release_tiebuf(ctx);
         else
             ctx->tiebuf_kept = true;
         pc.mark("tie workspace freed");
@@ -3348,14 +3415,18 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
         } else {
             for (uint32_t d = 0; d < nd; ++d) dstart[d + 1] = dstart[d] + tot[d];
         }
-        ctx->keep_tiebuf = stage < MUMS_STAGE_ALL;   // FindMatches needs the memory for its tail
+        // the tie workspace (135 GB at 2 x 3 Gbp; its hipMalloc alone is 3-4 s) stays allocated
+        // between calls: a FindMatches call's rows and chain scratch live inside it (below)
+        ctx->keep_tiebuf = stage < MUMS_STAGE_ALL ? 1 : 2;
         rc = chunked_restart(ctx, sbuf, dstart, cbase, nbc, nch, n_live, &live_rec, chunk_starts, st);
-        ctx->keep_tiebuf = false;
+        ctx->keep_tiebuf = 0;
         if (rc) return rc;
     }
-    // a workspace kept by an earlier seed-stage-only call and not reused above (no restart,
-    // no tie run) must not stay beside the FindMatches tail
-    if (stage == MUMS_STAGE_ALL) ctx->tiebuf.release();
+    // FindMatches: a kept tie workspace is the arena of the probe rows and the sliced chain
+    // scratch when both fit in it; else it is released so the tail can allocate them
+    const size_t Wrow = (size_t)(G + 1) * 8;
+    const size_t chain_need = chain_tmp_bytes(find_chunk() + 1, ctx->table_size, G) + 4096;
+    if (stage == MUMS_STAGE_ALL && ctx->tiebuf.p && ctx->tiebuf.cap < chain_need + (N / 4) * Wrow) release_tiebuf(ctx);
     for (uint32_t c = 0; c < nch; ++c) {
         const uint32_t dlo = c * nbc8;
         uint64_t n_c = 0;
@@ -3426,8 +3497,26 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
                 // sized for the chunks to come at this chunk's rate (+10 %): one growth
                 // at 2 x 3 Gbp instead of a doubling that would not fit next to the records
                 const uint64_t est = (uint64_t)((double)(P_total + Pc) * nch / (c + 1) * 1.1) + 1;
+                const size_t want = std::max(P_total + Pc + 1, est) * W;
                 DevBuf nb;
-                HIPCHK(nb.ensure(std::max(P_total + Pc + 1, est) * W));
+                // (inside the kept workspace: all the room the chain scratch leaves, whatever the
+                // skewed first-chunk estimate says; outgrowing it moves the rows out below)
+                const bool in_tie = !ctx->rowsall.borrowed && ctx->tiebuf.p &&
+                                    ctx->tiebuf.cap > chain_need + (P_total + Pc + 1) * W &&
+                                    nb.borrow(ctx->tiebuf, 0, ctx->tiebuf.cap - chain_need);
+                if (!in_tie && ctx->tiebuf.p) {   // the rows outgrow the kept workspace: give it up
+                    HIPCHK(hipStreamSynchronize(st));
+                    if (ctx->rowsall.borrowed) {   // (rows so far inside it: moved out first)
+                        DevBuf keep;
+                        HIPCHK(keep.ensure(P_total * W + 64));
+                        if (P_total) HIPCHK(hipMemcpyAsync(keep.p, ctx->rowsall.p, P_total * W, hipMemcpyDeviceToDevice, st));
+                        HIPCHK(hipStreamSynchronize(st));
+                        ctx->rowsall.release();
+                        ctx->rowsall = keep;
+                    }
+                    release_tiebuf(ctx);
+                }
+                if (!in_tie) HIPCHK(nb.ensure(want));
                 if (P_total) HIPCHK(hipMemcpyAsync(nb.p, ctx->rowsall.p, P_total * W, hipMemcpyDeviceToDevice, st));
                 HIPCHK(hipStreamSynchronize(st));
                 ctx->rowsall.release();

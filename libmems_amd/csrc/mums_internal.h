@@ -37,6 +37,7 @@ constexpr int kSeedTile = MUMS_SEED_TILE;  // positions per key-kernel workgroup
 constexpr int kSegTile = MUMS_SEG_TILE; // records per sort / group tile
 constexpr int kLocalIPT = 16;        // records per lane of the LDS-resident local sort (local_sort.hip)
 constexpr int kMaxMsdBits = 11;      // packed path: 2w+1 <= 32 + 11
+constexpr int kMaxSegBucketBits = 12; // segmented sorts: buckets of a merge (sharded 33-bit records at w21: 12 MSD bits)
 
 // Per-run constants shared by the kernels (passed by value).
 constexpr int kMaxSeedRuns = 16;     // runs of care positions in a seed of length <= 32
@@ -221,6 +222,9 @@ hipError_t launch_probe_tiles(View v, const SegTile* tiles, uint64_t ntiles, uin
 hipError_t launch_probe_compact(uint64_t nblocks, const uint32_t* tile_count, const uint32_t* tile_off,
                                 const uint64_t* slot_info, const uint32_t* slot_bucket, uint64_t* probe_info,
                                 uint32_t* probe_bucket, hipStream_t st, bool packed);
+// the bucket partition of the probes as packed records (bucket << 32 | probe) and back
+hipError_t launch_bucket_records(const uint32_t* b, uint64_t P, uint64_t* rec, hipStream_t st);
+hipError_t launch_bucket_split(const uint64_t* rec, uint64_t P, uint32_t* b, uint32_t* ids, hipStream_t st);
 // probes (key order) -> materialized rows (MatProbes, match_device.h)
 template <int MG, typename View>
 // lkey / fsk (optional): each probe's line key (chain_lkey_slot) and first-genome start

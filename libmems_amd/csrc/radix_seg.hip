@@ -133,7 +133,7 @@ __global__ void tiles_kernel(const uint32_t* __restrict__ bstart, const uint32_t
 // pos(k, b) = sum_b' min(ntb_b', k) + #{b' < b : ntb_b' > k}.
 __global__ __launch_bounds__(256) void claim_order_kernel(const uint32_t* __restrict__ tfirst, int nb, uint64_t ub,
                                                           SegTile* __restrict__ tiles) {
-    __shared__ uint32_t s_n[1 << kMaxMsdBits];
+    __shared__ uint32_t s_n[1 << kMaxSegBucketBits];
     for (int b = threadIdx.x; b < nb; b += blockDim.x) s_n[b] = tfirst[b + 1] - tfirst[b];
     __syncthreads();
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -59,7 +59,8 @@ def test_sharded_seed_stage_gpu(oracle_mod, G, n, p, w, world):
 
 @pytest.mark.parametrize("G,n,p,w,world,ib33", [(2, 300_000, 0.02, 19, 4, False), (2, 300_000, 0.02, 19, 4, True),
                                                   (3, 200_000, 0.03, 19, 6, True), (2, 400_000, 0.01, 15, 2, False),
-                                                  (2, 250_000, 0.05, 17, 8, False)])
+                                                  (2, 250_000, 0.05, 17, 8, False), (2, 300_000, 0.02, 21, 2, True),
+                                                  (2, 300_000, 0.02, 21, 8, True), (3, 200_000, 0.03, 20, 6, True)])
 def test_sharded_slices_gpu(oracle_mod, G, n, p, w, world, ib33):
     """Position-sharded seed stage (BASELINE config 5 layout: every genome cut into
     world/G position slices), optionally with the 33-bit records of the > 2^32 seed-mer

@@ -64,3 +64,15 @@ def test_shard_run_failure_is_collective(gpu_lib, oracle_mod, world, monkeypatch
         with pytest.raises(gpu_lib.MumsError):
             sh.FindMatches(seqs)
         assert sh.rank_status == [gpu_lib.MUMS_E_UNSUPPORTED] * world, sh.rank_status
+
+
+@pytest.mark.parametrize("G,n,w,p,world,layout", [(2, 300_000, 21, 0.02, 2, "slices"), (2, 250_000, 21, 0.03, 4, "slices"),
+                                                  (2, 200_000, 21, 0.02, 8, "slices"), (3, 200_000, 21, 0.02, 3, "blocks"),
+                                                  (4, 150_000, 20, 0.02, 2, "blocks"), (2, 200_000, 20, 0.05, 4, "slices")])
+def test_shard_run_ib33_wide_seeds(gpu_lib, oracle_mod, G, n, w, p, world, layout, monkeypatch):
+    """Above 2^32 seed-mers (forced small: MUMS_DEV_SHARD_IB33) the records carry 33-bit indices
+    and 31 key bits, so the default seed of 3 Gbp genomes (w21, getDefaultSeedWeight,
+    SeedMasks.h:389-401) has 12 MSD bits: 8 scattered, 4 as side bytes split before the
+    exchange (msdsplit.hip).  FindMatches over 2-8 ranks = the oracle's MatchList."""
+    monkeypatch.setenv("MUMS_DEV_SHARD_IB33", "1")
+    run(gpu_lib, oracle_mod, G, n, w, p, world, "local", layout=layout)
