@@ -266,6 +266,40 @@ int  mums_shard_restart_plan(mums_ctx* ctx, uint64_t* d_stream, uint32_t nranks,
                              const uint32_t* first_bucket, const uint32_t* nbuckets, void* d_out,
                              uint64_t capacity_bytes, uint64_t* block_bytes);
 int  mums_shard_restart_apply(mums_ctx* ctx, const void* d_block, uint64_t restarts, const uint64_t* offset_log);
+/* The same restart planned where the records are (mums_shard_run's default; the gathered
+ * plan above stays the fallback).  Rank r holds SML indices [off_r[g], off_r[g] + n_r[g])
+ * of every genome g (off_r = the counts of lower ranks), so every SML read of the plan
+ * (restart_plan.h) is answered locally, with the last key of genome g below the range and
+ * the first above it as neighbours; a read beyond those flags the plan undecidable.
+ *   1. mums_shard_restart_counts: this rank's SML parts (local genome-major keys), info =
+ *      [n[G], first key[G], last key[G], status] (status 1: use the gathered plan);
+ *   2. mums_shard_restart_prepare: every rank's info (all-gathered, rank order) -> offsets,
+ *      neighbours, the per-candidate precompute (cand_precompute); S0 = the start points;
+ *   3. mums_shard_restart_step, one rank after the other: the plan over this rank's
+ *      candidates with the running start points S (in/out), its restart count and the
+ *      undecidable flag (any rank: every rank falls back before anything is changed);
+ *      mums_shard_restart_log copies its restarts (keys, start points R x G);
+ *   4. mums_shard_restart_runs: the runs of equal keys that the start points of every phase
+ *      (S0 + all ranks' restarts, in key order) fall into on this rank, {g, lo, hi} global;
+ *   5. mums_shard_restart_ties (rank g % world for genome g): std::sort order of genome g's
+ *      runs (smlsort.hip) from the all-gathered packed genomes; the positions of run q's
+ *      slots to d_out + vofs[q];
+ *   6. mums_shard_restart_finish: this rank's runs take those positions as ids; the live
+ *      records (SML index >= its phase's start point) replace the stream, groups again.
+ * mums_shard_restart_info: [path (1 local plan, 2 gathered plan), candidates, restarts,
+ * device bytes the restart allocated on this rank]. */
+int  mums_shard_restart_counts(mums_ctx* ctx, uint64_t* info);
+int  mums_shard_restart_prepare(mums_ctx* ctx, uint32_t nranks, uint32_t rank, const uint64_t* all_info,
+                                uint64_t* S0);
+int  mums_shard_restart_step(mums_ctx* ctx, uint64_t* S, uint64_t* restarts, uint64_t* undecidable);
+int  mums_shard_restart_log(mums_ctx* ctx, uint64_t* rkey, uint64_t* rS);
+int  mums_shard_restart_runs(mums_ctx* ctx, uint64_t restarts, const uint64_t* rkey, const uint64_t* rS,
+                             uint64_t* runs, uint64_t capacity, uint64_t* nruns);
+int  mums_shard_restart_ties(mums_ctx* ctx, const uint32_t* d_packed_all, const uint64_t* runs, uint64_t nruns,
+                             const uint64_t* vofs, uint32_t* d_out);
+int  mums_shard_restart_finish(mums_ctx* ctx, uint64_t restarts, const uint64_t* rkey, const uint64_t* rS,
+                               const uint64_t* runs, uint64_t nruns, const uint32_t* d_pos, const uint64_t* vofs);
+int  mums_shard_restart_info(mums_ctx* ctx, uint64_t* info);
 /* Accepted probes of the last seed stage, in AddHashEntry call order
  * (MemHash::EnumerateMatches -> AddHashEntry, MemHash.cpp:139-162, 209-251):
  * hash bucket ((offset % T) + T) % T and the smallest global seed-mer index of

@@ -101,7 +101,9 @@ EXPORTED_SYMBOLS = [
     "mums_comm_init_local", "mums_comm_destroy", "mums_comm_last_error", "mums_shard_key_ranges", "mums_shard_run",
     "mums_set_match_log", "mums_match_log_copy", "mums_shard_restart_pending", "mums_shard_stream",
     "mums_shard_restart_plan", "mums_shard_restart_apply", "mums_comm_init_host", "mums_set_progress_log",
-    "mums_progress_log_copy",
+    "mums_progress_log_copy", "mums_shard_restart_counts", "mums_shard_restart_prepare", "mums_shard_restart_step",
+    "mums_shard_restart_log", "mums_shard_restart_runs", "mums_shard_restart_ties", "mums_shard_restart_finish",
+    "mums_shard_restart_info",
 ]
 
 # mums_comm_ops (include/mums.h): the caller's transport as two host callbacks
@@ -584,7 +586,8 @@ class ShardedMemHash:
     def FindMatchesFromPosition(self, sequences: Optional[Sequence], start_points: Sequence[int],
                                 stage: int = STAGE_ALL) -> MatchList:
         """MemHash::FindMatchesFromPosition (MemHash.cpp:117-127) over the ranks: every rank gets
-        all G start points; rank 0 plans the restarts on the gathered streams (mums_shard_restart_*)."""
+        all G start points; the restarts are planned on the ranks' own SML parts
+        (mums_shard_restart_counts .. _finish; the gathered plan as the fallback)."""
         self._start_points = np.ascontiguousarray(np.asarray(start_points, dtype=np.uint64))
         try:
             return self.FindMatches(sequences, stage)
@@ -656,6 +659,12 @@ class ShardedMemHash:
             if e is not None:
                 raise e
         self.stats_per_rank = [mh.stats() for mh in self.ranks]
+        self.restart_info = []   # per rank: path (0 none, 1 local plan, 2 gathered), candidates, restarts, bytes
+        for mh in self.ranks:
+            ri = np.zeros(4, dtype=np.uint64)
+            mh._check(self._lib.mums_shard_restart_info(mh._ctx, ri.ctypes.data))
+            self.restart_info.append({"path": int(ri[0]), "candidates": int(ri[1]), "restarts": int(ri[2]),
+                                      "bytes": int(ri[3])})
         if stage != STAGE_ALL:
             return MatchList(np.zeros(0, dtype=np.uint64), np.zeros((0, G), dtype=np.int64))
         parts = [mh.GetMatchList() for mh in self.ranks]

@@ -116,10 +116,14 @@ __device__ __forceinline__ void cr_block_ranks(const CrStream& s, const GenomeTa
 }
 
 // the G SortedMerLists as full keys: ck[base_g + sml index] = ckey
+// (lbase: the genome-major bases of a stream holding part of every SML -- a sharded rank's
+// key range; nullptr: gt.base)
 __global__ __launch_bounds__(kBlock) void cr_ck_kernel(CrStream s, GenomeTable gt, const uint32_t* __restrict__ gscan,
-                                                       uint64_t nblk, uint64_t* __restrict__ ck) {
-    cr_block_ranks(s, gt, blockIdx.x, gscan, nblk,
-                   [&](uint64_t j, int g, uint64_t i) { ck[gt.base[g] + i] = cr_key(s, j); });
+                                                       uint64_t nblk, const uint64_t* __restrict__ lbase,
+                                                       uint64_t* __restrict__ ck) {
+    cr_block_ranks(s, gt, blockIdx.x, gscan, nblk, [&](uint64_t j, int g, uint64_t i) {
+        ck[(lbase ? lbase[g] : gt.base[g]) + i] = cr_key(s, j);
+    });
 }
 
 // masked keys with more than MER_REPEAT_LIMIT records: such a run holds a multiple of 1000,
@@ -169,10 +173,12 @@ __global__ __launch_bounds__(kBlock) void cr_live_kernel(CrStream s, GenomeTable
                                                          uint64_t nblk, uint64_t b0, uint64_t lo, uint64_t hi,
                                                          const uint64_t* __restrict__ rkey, uint64_t R,
                                                          const uint64_t* __restrict__ rS,
-                                                         const uint64_t* __restrict__ S0, uint32_t* __restrict__ live) {
+                                                         const uint64_t* __restrict__ S0, const uint64_t* __restrict__ goff,
+                                                         uint32_t* __restrict__ live) {
     const int G = gt.G;
     cr_block_ranks(s, gt, b0 + blockIdx.x, gscan, nblk, [&](uint64_t j, int g, uint64_t i) {
         if (j < lo || j >= hi) return;
+        if (goff) i += goff[g];   // a sharded rank: SML indices below its key range
         const uint64_t v = cr_key(s, j) >> 1;
         uint64_t a = 0, n = R;   // phase = restart keys <= v
         while (n > 0) {
@@ -206,6 +212,61 @@ __global__ __launch_bounds__(kBlock) void cr_runs_kernel(const uint64_t* __restr
         runs[3 * q] = (uint64_t)g;
         runs[3 * q + 1] = lo;
         runs[3 * q + 2] = hi;
+    }
+}
+
+// A sharded rank's straddled runs: it holds SML indices [goff[g], goff[g] + gn[g]) of genome
+// g at ck[lbase[g] ..]; a start point strictly inside that range (its predecessor is held
+// too, so a run of equal full keys can straddle it) -> {g, lo, hi} in global SML indices
+__global__ __launch_bounds__(kBlock) void cr_druns_kernel(const uint64_t* __restrict__ ck, int G,
+                                                          const uint64_t* __restrict__ lbase,
+                                                          const uint64_t* __restrict__ goff,
+                                                          const uint64_t* __restrict__ gn,
+                                                          const uint64_t* __restrict__ sp, uint64_t rows,
+                                                          uint64_t* __restrict__ runs,
+                                                          unsigned long long* __restrict__ nr, uint64_t cap) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= rows * (uint64_t)G) return;
+    const int g = (int)(i % (uint64_t)G);
+    const uint64_t o = goff[g], n = gn[g], s = sp[i];
+    if (s <= o || s - o >= n) return;
+    const uint64_t* a = ck + lbase[g];
+    const uint64_t ls = s - o, k = a[ls];
+    if (a[ls - 1] != k) return;
+    uint64_t lo = ls - 1, hi = ls + 1;
+    while (lo > 0 && a[lo - 1] == k) --lo;
+    while (hi < n && a[hi] == k) ++hi;
+    const unsigned long long q = atomicAdd(nr, 1ull);
+    if (q < cap) {
+        runs[3 * q] = (uint64_t)g;
+        runs[3 * q + 1] = o + lo;
+        runs[3 * q + 2] = o + hi;
+    }
+}
+
+// A sharded rank's straddled run q (genome g, global slots [lo, hi)): its records, in stream
+// order, take the ids of the std::sort order, V[vofs[q] + r] (positions in the genome),
+// computed on the rank that replayed genome g's sort; one lane per run
+__global__ void cr_dtie_write_kernel(CrStream s, GenomeTable gt, const uint64_t* __restrict__ runs, uint64_t nrun,
+                                     const uint64_t* __restrict__ ck, const uint64_t* __restrict__ lbase,
+                                     const uint64_t* __restrict__ goff, const uint32_t* __restrict__ V,
+                                     const uint64_t* __restrict__ vofs, uint64_t* __restrict__ rec) {
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nrun) return;
+    const int g = (int)runs[3 * q];
+    const uint64_t lo = runs[3 * q + 1], hi = runs[3 * q + 2];
+    const uint64_t key = ck[lbase[g] + (lo - goff[g])];
+    uint64_t a = 0, n = s.N;   // first stream record with key >= key
+    while (n > 0) {
+        const uint64_t h = n >> 1;
+        if (cr_key(s, a + h) < key) { a += h + 1; n -= h + 1; } else n = h;
+    }
+    const uint32_t* v = V + vofs[q];
+    uint64_t r = 0;
+    for (uint64_t j = a; j < s.N && r < hi - lo && cr_key(s, j) == key; ++j) {
+        if (genome_of(gt, cr_idx(s, j)) != g) continue;
+        rec[j] = (rec[j] & ~((1ull << s.ib) - 1)) | (gt.base[g] + v[r]);
+        ++r;
     }
 }
 
@@ -295,10 +356,11 @@ hipError_t launch_cr_counts(const CrStream& s, const GenomeTable& gt, uint32_t* 
     return hipSuccess;
 }
 
-hipError_t launch_cr_ck(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, uint64_t* ck, hipStream_t st) {
+hipError_t launch_cr_ck(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, uint64_t* ck, hipStream_t st,
+                        const uint64_t* lbase) {
     const uint64_t nblk = cr_blocks(s.N);
     if (nblk == 0) return hipSuccess;
-    hipLaunchKernelGGL(cr_ck_kernel, dim3((unsigned)nblk), dim3(kBlock), 0, st, s, gt, gscan, nblk, ck);
+    hipLaunchKernelGGL(cr_ck_kernel, dim3((unsigned)nblk), dim3(kBlock), 0, st, s, gt, gscan, nblk, lbase, ck);
     return hipGetLastError();
 }
 
@@ -315,6 +377,24 @@ hipError_t launch_cr_runs(const uint64_t* ck, const GenomeTable& gt, const uint6
     if (rows == 0) return hipSuccess;
     hipLaunchKernelGGL(cr_runs_kernel, cr_grid(rows * (uint64_t)gt.G), dim3(kBlock), 0, st, ck, gt, sp, rows, runs, nr,
                        cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_cr_druns(const uint64_t* ck, int G, const uint64_t* lbase, const uint64_t* goff, const uint64_t* gn,
+                           const uint64_t* sp, uint64_t rows, uint64_t* runs, unsigned long long* nr, uint64_t cap,
+                           hipStream_t st) {
+    if (rows == 0) return hipSuccess;
+    hipLaunchKernelGGL(cr_druns_kernel, cr_grid(rows * (uint64_t)G), dim3(kBlock), 0, st, ck, G, lbase, goff, gn, sp,
+                       rows, runs, nr, cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_cr_dtie_write(const CrStream& s, const GenomeTable& gt, const uint64_t* runs, uint64_t nrun,
+                                const uint64_t* ck, const uint64_t* lbase, const uint64_t* goff, const uint32_t* V,
+                                const uint64_t* vofs, uint64_t* rec, hipStream_t st) {
+    if (nrun == 0) return hipSuccess;
+    hipLaunchKernelGGL(cr_dtie_write_kernel, dim3((unsigned)((nrun + 63) / 64)), dim3(64), 0, st, s, gt, runs, nrun,
+                       ck, lbase, goff, V, vofs, rec);
     return hipGetLastError();
 }
 
@@ -345,7 +425,7 @@ hipError_t launch_cr_live_compact(const CrStream& s, const GenomeTable& gt, cons
                                   uint64_t hi, const uint64_t* rkey, uint64_t R, const uint64_t* rS, const uint64_t* S0,
                                   uint32_t* live, uint32_t* pos, void* d_scan_tmp, uint64_t* dst,
                                   const uint32_t* bstart, uint32_t nb, uint32_t* dst_bstart, uint32_t* d_total,
-                                  hipStream_t st) {
+                                  hipStream_t st, const uint64_t* goff) {
     const uint64_t n = hi - lo;
     const uint64_t nblk = cr_blocks(s.N);
     const uint64_t b0 = lo / kCrBlk, b1 = (hi + kCrBlk - 1) / kCrBlk;
@@ -353,7 +433,7 @@ hipError_t launch_cr_live_compact(const CrStream& s, const GenomeTable& gt, cons
     if (e != hipSuccess) return e;
     if (n) {
         hipLaunchKernelGGL(cr_live_kernel, dim3((unsigned)(b1 - b0)), dim3(kBlock), 0, st, s, gt, gscan, nblk, b0, lo,
-                           hi, rkey, R, rS, S0, live);
+                           hi, rkey, R, rS, S0, goff, live);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if ((e = hipMemcpyAsync(pos, live, (n + 1) * 4, hipMemcpyDeviceToDevice, st)) != hipSuccess) return e;

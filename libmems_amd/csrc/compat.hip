@@ -171,8 +171,7 @@ __global__ void compat_fire_kernel(restart::PlanData d, const uint64_t* __restri
         if (S[g] > m) S[g] = m;
         if (E[g] > m) E[g] = m;
         if (E[g] < S[g]) E[g] = S[g];
-        const uint64_t* ag = d.ck + d.base[g];
-        const uint64_t lo = restart::lower_bound_u64(ag, m, K << 1), hi = restart::lower_bound_u64(ag, m, (K + 1) << 1);
+        const uint64_t lo = restart::lower_bound_g(d, g, 0, m, K << 1), hi = restart::lower_bound_g(d, g, 0, m, (K + 1) << 1);
         a[g] = lo < S[g] ? S[g] : (lo > E[g] ? E[g] : lo);
         b[g] = hi < S[g] ? S[g] : (hi > E[g] ? E[g] : hi);
         if (b[g] > a[g]) U |= 1ull << g;

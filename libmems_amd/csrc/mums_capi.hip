@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <functional>
 #include <cstddef>
@@ -128,6 +129,15 @@ struct mums_ctx {
     int shard_mb = 0;                     // local bucket bits of the last mums_shard_merge
     int shard_side = 0;                   // 33-bit records at w20-21: side bits split below the 8-bit scatter
     uint64_t shard_n = 0;                 // its records
+    uint32_t shard_kfirst = 0, shard_kcount = 0;   // its key range (first MSD bucket, buckets)
+    std::vector<uint32_t> shard_bst;      // its local bucket starts (2^shard_mb + 1)
+    // the restart planned where the records are (mums_shard_restart_counts .. _finish)
+    DevBuf dsarr;                         // PlanData arrays (m, lbase, off, n, prv, nxt), S0, flags
+    bool ds_ready = false;
+    uint64_t ds_C = 0;                    // this rank's candidates (groups above MER_REPEAT_LIMIT)
+    std::vector<uint64_t> ds_n, ds_off;   // SML indices [off, off + n) of every genome held here
+    std::vector<uint64_t> ds_rkey, ds_rS; // this rank's restarts (last step)
+    uint64_t rs_info[4] = {0, 0, 0, 0};   // mums_shard_restart_info
     bool ties_fixed = false;              // the stream holds every run of equal keys in std::sort order
     uint64_t tie_slots = 0;               // slots of the runs replayed by the last run (stats)
     // seed-stage-only chunked runs keep the tie workspace between calls when memory allows:
@@ -187,6 +197,8 @@ namespace {
 
 void release_tiebuf(mums_ctx* ctx);
 hipError_t tiebuf_ensure(mums_ctx* ctx, size_t bytes);
+void release_find_buffers(mums_ctx* ctx);
+void note_rs_bytes(mums_ctx* ctx);
 
 int fail(mums_ctx* c, int code, const std::string& msg) {
     if (c) c->err = msg;
@@ -1605,7 +1617,8 @@ int mums_ctx_destroy(mums_ctx* ctx) {
                       &ctx->smlvB, &ctx->smltmp, &ctx->flen, &ctx->fs, &ctx->rowsall, &ctx->rsbuf,
                       &ctx->rsplan, &ctx->rsbst, &ctx->pool_loc, &ctx->cbuf, &ctx->sids,
                       &ctx->logA, &ctx->logB, &ctx->logvA, &ctx->logvB, &ctx->tiebuf, &ctx->fk, &ctx->fkloc,
-                      &ctx->crbuf, &ctx->crcnt, &ctx->crlive, &ctx->crruns, &ctx->crall, &ctx->fsk, &ctx->bst2};
+                      &ctx->crbuf, &ctx->crcnt, &ctx->crlive, &ctx->crruns, &ctx->crall, &ctx->fsk, &ctx->bst2,
+                      &ctx->side, &ctx->bst8, &ctx->cbst, &ctx->dsarr};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i < EV_COUNT; ++i)
         if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
@@ -2278,6 +2291,40 @@ void shard_merge_stats(mums_ctx* ctx, uint64_t n) {
     ctx->st.ms_sort += rg;
     ctx->st.ms_keys = ctx->shard_keys_ms;
 }
+// the groups stage again over the nl live records at dst (bucket starts bst, 2^shard_mb + 1):
+// the end of a sharded restart (mums_shard_restart_apply / _finish)
+int shard_regroup(mums_ctx* ctx, uint64_t* dst, uint64_t nl, const std::vector<uint32_t>& bst, const ProbeSpace& ps,
+                  uint64_t restarts, const uint64_t* offset_log, hipStream_t st) {
+    const int mb = ctx->shard_mb;
+    HIPCHK(hipMemcpyAsync(ctx->mstart.p, bst.data(), bst.size() * 4, hipMemcpyHostToDevice, st));
+    ctx->sorted_buf ^= 1;
+    ctx->sorted_rec = dst;
+    DevCounters* dc = ctx->counters.as<DevCounters>();
+    const uint64_t rep = ctx->hc.repeat_limit;
+    SegTile* tiles = ctx->tiles.as<SegTile>();
+    HIPCHK(build_seg_tiles_from_starts(ctx->mstart.as<uint32_t>(), mb, nl, tiles, &dc->ntiles, ctx->tmp.p, st));
+    HIPCHK(hipMemsetAsync(&dc->repeat_limit, 0, 8, st));
+    const MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, ctx->masked, ctx->seq_mask};
+    const uint64_t ub = seg_tiles_upper(nl, mb);
+    int rc;
+    if (ctx->rec_ib == 33)
+        rc = groups_dispatch<RecViewT<33>>(ctx, RecViewT<33>{dst}, tiles, ub, mp, ps.probe_info, ps.probe_bucket,
+                                           ps.slot_info, ps.slot_bucket, st);
+    else
+        rc = groups_dispatch<RecView>(ctx, RecView{dst}, tiles, ub, mp, ps.probe_info, ps.probe_bucket, ps.slot_info,
+                                      ps.slot_bucket, st);
+    if (rc) return rc;
+    rc = finish_seeds(ctx, ps, st);
+    if (rc) return rc;
+    HIPCHK(hipMemcpy(&dc->repeat_limit, &rep, 8, hipMemcpyHostToDevice));   // the report: the whole range's groups
+    ctx->hc.repeat_limit = rep;
+    ctx->restarts = restarts;
+    ctx->offset_log.assign(offset_log, offset_log + restarts * (uint64_t)ctx->gt.G);
+    ctx->shard_restart_pending = false;
+    HIPCHK(hipStreamSynchronize(st));
+    shard_merge_stats(ctx, ctx->shard_n);
+    return MUMS_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -2389,6 +2436,10 @@ int mums_shard_merge(mums_ctx* ctx, const uint64_t* d_records, uint32_t nsources
                                              "range above 2^30 records)");
     ctx->shard_mb = mb;
     ctx->shard_n = n;
+    ctx->shard_kfirst = first_bucket;
+    ctx->shard_kcount = nbuckets;
+    ctx->shard_bst = bst;
+    ctx->ds_ready = false;
     ctx->stage_done = MUMS_STAGE_SEEDS;
     HIPCHK(hipStreamSynchronize(st));
     shard_merge_stats(ctx, n);
@@ -2497,6 +2548,7 @@ int mums_shard_restart_plan(mums_ctx* ctx, uint64_t* d_stream, uint32_t nranks, 
         block_bytes[r] = 8 * (head.size() + nl);
     }
     HIPCHK(hipStreamSynchronize(st));
+    note_rs_bytes(ctx);
     ctx->crall.release();
     return MUMS_OK;
 }
@@ -2528,32 +2580,432 @@ int mums_shard_restart_apply(mums_ctx* ctx, const void* d_block, uint64_t restar
     if (rc) return rc;
     uint64_t* dst = ctx->sorted_buf ? ctx->recA.as<uint64_t>() : ctx->recB.as<uint64_t>();
     if (nl) HIPCHK(hipMemcpyAsync(dst, (const uint64_t*)d_block + 2 + head[1], nl * 8, hipMemcpyDeviceToDevice, st));
-    HIPCHK(hipMemcpyAsync(ctx->mstart.p, bst.data(), bst.size() * 4, hipMemcpyHostToDevice, st));
-    ctx->sorted_buf ^= 1;
-    ctx->sorted_rec = dst;
-    DevCounters* dc = ctx->counters.as<DevCounters>();
-    const uint64_t rep = ctx->hc.repeat_limit;
-    SegTile* tiles = ctx->tiles.as<SegTile>();
-    HIPCHK(build_seg_tiles_from_starts(ctx->mstart.as<uint32_t>(), mb, nl, tiles, &dc->ntiles, ctx->tmp.p, st));
-    HIPCHK(hipMemsetAsync(&dc->repeat_limit, 0, 8, st));
-    const MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, ctx->masked, ctx->seq_mask};
-    const uint64_t ub = seg_tiles_upper(nl, mb);
-    if (ctx->rec_ib == 33)
-        rc = groups_dispatch<RecViewT<33>>(ctx, RecViewT<33>{dst}, tiles, ub, mp, ps.probe_info, ps.probe_bucket,
-                                           ps.slot_info, ps.slot_bucket, st);
-    else
-        rc = groups_dispatch<RecView>(ctx, RecView{dst}, tiles, ub, mp, ps.probe_info, ps.probe_bucket, ps.slot_info,
-                                      ps.slot_bucket, st);
-    if (rc) return rc;
-    rc = finish_seeds(ctx, ps, st);
-    if (rc) return rc;
-    HIPCHK(hipMemcpy(&dc->repeat_limit, &rep, 8, hipMemcpyHostToDevice));   // the report: the whole range's groups
-    ctx->hc.repeat_limit = rep;
-    ctx->restarts = restarts;
-    ctx->offset_log.assign(offset_log, offset_log + restarts * (uint64_t)ctx->gt.G);
-    ctx->shard_restart_pending = false;
+    ctx->rs_info[0] = 2;
+    ctx->rs_info[2] = restarts;
+    return shard_regroup(ctx, dst, nl, bst, ps, restarts, offset_log, st);
+}
+
+// ---- the restart planned where the records are (mums_shard_restart_counts .. _finish) ----
+// Rank r's merged stream holds every genome's SML indices [off_r[g], off_r[g] + n_r[g]) (the
+// key ranges ascend with the rank), so its part of genome g's SortedMerList is its records
+// of genome g in stream order.  Those parts answer the plan's reads (PlanData's distributed
+// form); the restarts of lower ranks arrive as the running start points.
+
+int mums_shard_restart_counts(mums_ctx* ctx, uint64_t* info) {
+    if (check_ctx(ctx) || !info) return MUMS_E_INVALID;
+    if (!have_device()) return fail(ctx, MUMS_E_NODEVICE, "no HIP device");
+    if (!ctx->shard || ctx->stage_done < MUMS_STAGE_SEEDS || ctx->merge_chunked)
+        return fail(ctx, MUMS_E_INVALID, "no sharded (one-pass) merge run");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    const GenomeTable& gt = ctx->gt;
+    const int G = gt.G;
+    const uint64_t Gu = (uint64_t)G, n = ctx->shard_n;
+    const int B = ctx->msd_bits;
+    const uint32_t kb = (uint32_t)(2 * ctx->w + 1 - B);
+    std::fill(info, info + 3 * Gu + 1, 0ull);
+    ctx->ds_ready = false;
+    ctx->rs_info[0] = ctx->rs_info[1] = ctx->rs_info[2] = ctx->rs_info[3] = 0;
+    if (ctx->parity_masked || seg_onesweep_launches(kb) < (int)((kb + 7) / 8))
+        return fail(ctx, MUMS_E_UNSUPPORTED, "restart with the segment fix-up sort (MUMS_DEV_SEGFIX)");
+    const char* force = getenv("MUMS_DEV_SHARD_RESTART");
+    if (ctx->progress_on || (force && !strcmp(force, "gather"))) {   // LogProgress needs the whole stream
+        info[3 * Gu] = 1;
+        return MUMS_OK;
+    }
+    // the local stream: 2^B global digit starts around this rank's buckets
+    const uint64_t nd = 1ull << B;
+    std::vector<uint64_t> dstart(nd + 1, 0);
+    for (uint64_t d = 0; d <= nd; ++d) {
+        if (d < ctx->shard_kfirst) dstart[d] = 0;
+        else if (d - ctx->shard_kfirst <= ctx->shard_kcount) dstart[d] = ctx->shard_bst[d - ctx->shard_kfirst];
+        else dstart[d] = n;
+    }
+    const uint64_t ccap = n / (restart::kRepeatLimit + 1) + 16;
+    HIPCHK(ctx->crbuf.ensure((nd + 1) * 8 + 64 + ccap * 8 + 4096));
+    uint64_t* d_dstart = ctx->crbuf.as<uint64_t>();
+    unsigned long long* d_cnt = (unsigned long long*)(d_dstart + nd + 1);
+    uint64_t* d_list = (uint64_t*)(d_cnt + 8);
+    HIPCHK(hipMemcpyAsync(d_dstart, dstart.data(), (nd + 1) * 8, hipMemcpyHostToDevice, st));
+    CrStream s{ctx->sorted_rec, d_dstart, (uint32_t)nd, n};
+    s.kb = kb;
+    s.ib = (uint32_t)ctx->rec_ib;
+    HIPCHK(launch_cr_cands(s, d_list, d_cnt, ccap, st));
+    unsigned long long C = 0;
+    HIPCHK(hipMemcpyAsync(&C, d_cnt, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    shard_merge_stats(ctx, ctx->shard_n);
+    if (C > ccap) return fail(ctx, MUMS_E_HIP, "restart: candidate list overflow (internal error)");
+    if (C) {
+        std::vector<uint64_t> cand(C);
+        HIPCHK(hipMemcpy(cand.data(), d_list, C * 8, hipMemcpyDeviceToHost));
+        std::sort(cand.begin(), cand.end());
+        HIPCHK(hipMemcpy(d_list, cand.data(), C * 8, hipMemcpyHostToDevice));
+    }
+    ctx->ds_C = C;
+    // per-genome block counts, this rank's part of every SML (full keys, genome-major)
+    const uint64_t nblk = cr_blocks(n);
+    HIPCHK(ctx->crcnt.ensure(Gu * (nblk + 1) * 4 + 256));
+    HIPCHK(ctx->tmp.ensure(std::max(ctx->tmp.cap, scan_tmp_bytes(nblk + 2))));
+    uint32_t* gscan = ctx->crcnt.as<uint32_t>();
+    HIPCHK(launch_cr_counts(s, gt, gscan, ctx->tmp.p, st));
+    std::vector<uint32_t> tot(Gu, 0);
+    for (int g = 0; g < G; ++g)
+        HIPCHK(hipMemcpyAsync(&tot[g], gscan + (uint64_t)g * (nblk + 1) + nblk, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    ctx->ds_n.assign(Gu, 0);
+    std::vector<uint64_t> lbase(Gu + 1, 0);
+    for (int g = 0; g < G; ++g) {
+        ctx->ds_n[g] = tot[g];
+        lbase[g + 1] = lbase[g] + tot[g];
+    }
+    if (lbase[G] != n) return fail(ctx, MUMS_E_HIP, "restart: genome counts differ from the stream (internal error)");
+    HIPCHK(ctx->dsarr.ensure(8 * (8 * (Gu + 1) + 64)));
+    uint64_t* d_lbase = ctx->dsarr.as<uint64_t>() + (Gu + 1);
+    HIPCHK(hipMemcpyAsync(d_lbase, lbase.data(), (Gu + 1) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx->crall.ensure((n + 64) * 8));
+    uint64_t* ck = ctx->crall.as<uint64_t>();
+    HIPCHK(launch_cr_ck(s, gt, gscan, ck, st, d_lbase));
+    for (int g = 0; g < G; ++g) {
+        info[g] = tot[g];
+        info[Gu + g] = ~0ull;
+        if (!tot[g]) continue;
+        HIPCHK(hipMemcpyAsync(&info[Gu + g], ck + lbase[g], 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(&info[2 * Gu + g], ck + lbase[g + 1] - 1, 8, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    ctx->rs_info[1] = C;
+    return MUMS_OK;
+}
+
+}  // extern "C"
+
+namespace {
+// device arrays of the distributed plan in ctx->dsarr (G + 1 words each)
+struct DsArrays {
+    uint64_t *dm, *lbase, *off, *n, *prv, *nxt, *S0;
+    unsigned* bad;
+};
+DsArrays ds_arrays(mums_ctx* ctx) {
+    const uint64_t W = (uint64_t)ctx->gt.G + 1;
+    uint64_t* b = ctx->dsarr.as<uint64_t>();
+    return DsArrays{b, b + W, b + 2 * W, b + 3 * W, b + 4 * W, b + 5 * W, b + 6 * W, (unsigned*)(b + 7 * W)};
+}
+restart::PlanData ds_plan_data(mums_ctx* ctx, const DsArrays& a) {
+    restart::PlanData d{ctx->gt.G, a.dm, a.lbase, ctx->crall.as<uint64_t>()};
+    d.off = a.off;
+    d.n = a.n;
+    d.prv = a.prv;
+    d.nxt = a.nxt;
+    const int sh = 2 * ctx->w + 1 - ctx->msd_bits;
+    const uint64_t end = (uint64_t)ctx->shard_kfirst + ctx->shard_kcount;
+    d.key_lo = (uint64_t)ctx->shard_kfirst << sh;
+    d.key_hi = end >= (1ull << ctx->msd_bits) ? ~0ull : end << sh;
+    d.bad = a.bad;
+    return d;
+}
+// plan workspace in ctx->rsplan: [pre 3 C G + C/2][cbad C/2 + 1][S G][PlanOut][rkey C][rS C G]
+struct DsPlan {
+    uint64_t* pre;
+    unsigned* cbad;
+    uint64_t* S;
+    restart::PlanOut* out;
+    uint64_t *rkey, *rS;
+};
+DsPlan ds_plan(mums_ctx* ctx, uint64_t cap) {
+    const uint64_t Gu = (uint64_t)ctx->gt.G;
+    uint64_t* p = ctx->rsplan.as<uint64_t>();
+    DsPlan w{};
+    w.pre = p;
+    p += 3 * cap * Gu + (cap + 1) / 2 + 1;
+    w.cbad = (unsigned*)p;
+    p += (cap + 1) / 2 + 1;
+    w.S = p;
+    p += Gu + 1;
+    w.out = (restart::PlanOut*)p;
+    p += (sizeof(restart::PlanOut) + 7) / 8 + 1;
+    w.rkey = p;
+    p += cap;
+    w.rS = p;
+    return w;
+}
+size_t ds_plan_bytes(uint64_t cap, uint64_t Gu) {
+    return 8 * (3 * cap * Gu + (cap + 1) + 4 + Gu + 1 + (sizeof(restart::PlanOut) + 7) / 8 + 1 + cap + cap * Gu) + 4096;
+}
+// the restart's own device buffers (mums_shard_restart_info; the tie replay's workspace, O(the
+// genome) on the rank replaying it, is not counted)
+void note_rs_bytes(mums_ctx* ctx) {
+    uint64_t b = 0;
+    for (const DevBuf* x : {&ctx->crall, &ctx->crcnt, &ctx->crlive, &ctx->crruns, &ctx->rsplan, &ctx->crbuf,
+                            &ctx->rsbst, &ctx->dsarr})
+        b += x->cap;
+    ctx->rs_info[3] = std::max<uint64_t>(ctx->rs_info[3], b);
+}
+}  // namespace
+
+extern "C" {
+
+int mums_shard_restart_prepare(mums_ctx* ctx, uint32_t nranks, uint32_t rank, const uint64_t* all_info, uint64_t* S0) {
+    if (check_ctx(ctx) || !all_info || !S0 || rank >= nranks) return MUMS_E_INVALID;
+    if (ctx->ds_n.size() != (size_t)ctx->gt.G || !ctx->crall.p)
+        return fail(ctx, MUMS_E_INVALID, "mums_shard_restart_counts first");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    const GenomeTable& gt = ctx->gt;
+    const int G = gt.G;
+    const uint64_t Gu = (uint64_t)G, rowlen = 3 * Gu + 1;
+    std::vector<uint64_t> hm(Gu + 1, 0), off(Gu + 1, 0), hn(Gu + 1, 0), prv(Gu + 1, 0), nxt(Gu + 1, ~0ull),
+        s0(Gu + 1, 0);
+    for (int g = 0; g < G; ++g) {
+        hm[g] = gt.m[g];
+        uint64_t t = 0;
+        for (uint32_t r = 0; r < nranks; ++r) {
+            const uint64_t* row = all_info + (uint64_t)r * rowlen;
+            if (r < rank) off[g] += row[g];
+            t += row[g];
+            if (r < rank && row[g]) prv[g] = row[2 * Gu + g];
+        }
+        for (uint32_t r = nranks; r-- > rank + 1;) {
+            const uint64_t* row = all_info + (uint64_t)r * rowlen;
+            if (row[g]) nxt[g] = row[Gu + g];
+        }
+        if (t != gt.m[g] || all_info[(uint64_t)rank * rowlen + g] != ctx->ds_n[g])
+            return fail(ctx, MUMS_E_INVALID, "restart: the ranks' SML counts do not add up to the genome");
+        hn[g] = ctx->ds_n[g];
+        s0[g] = g < (int)ctx->start_points.size() ? ctx->start_points[g] : 0;
+        S0[g] = s0[g];
+    }
+    ctx->ds_off.assign(off.begin(), off.begin() + Gu);
+    const DsArrays a = ds_arrays(ctx);
+    HIPCHK(hipMemcpyAsync(a.dm, hm.data(), (Gu + 1) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(a.off, off.data(), (Gu + 1) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(a.n, hn.data(), (Gu + 1) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(a.prv, prv.data(), (Gu + 1) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(a.nxt, nxt.data(), (Gu + 1) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(a.S0, s0.data(), (Gu + 1) * 8, hipMemcpyHostToDevice, st));
+    const uint64_t C = ctx->ds_C, cap = C + 16;
+    HIPCHK(ctx->rsplan.ensure(ds_plan_bytes(cap, Gu)));
+    const DsPlan w = ds_plan(ctx, cap);
+    const uint64_t nd = 1ull << ctx->msd_bits;
+    const uint64_t* d_list = (const uint64_t*)((unsigned long long*)(ctx->crbuf.as<uint64_t>() + nd + 1) + 8);
+    HIPCHK(launch_restart_dpre(ds_plan_data(ctx, a), d_list, C, w.pre, w.cbad, st));
+    HIPCHK(hipStreamSynchronize(st));
+    ctx->ds_ready = true;
+    note_rs_bytes(ctx);
+    return MUMS_OK;
+}
+
+int mums_shard_restart_step(mums_ctx* ctx, uint64_t* S, uint64_t* restarts, uint64_t* undecidable) {
+    if (check_ctx(ctx) || !S || !restarts || !undecidable) return MUMS_E_INVALID;
+    if (!ctx->ds_ready) return fail(ctx, MUMS_E_INVALID, "mums_shard_restart_prepare first");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    const uint64_t Gu = (uint64_t)ctx->gt.G, C = ctx->ds_C, cap = C + 16;
+    *restarts = 0;
+    *undecidable = 0;
+    ctx->ds_rkey.clear();
+    ctx->ds_rS.clear();
+    if (C == 0) return MUMS_OK;   // the start points pass through
+    const DsArrays a = ds_arrays(ctx);
+    const DsPlan w = ds_plan(ctx, cap);
+    restart::PlanOut po{};
+    po.cap = C;
+    po.rkey = w.rkey;
+    po.rS = w.rS;
+    po.status = restart::kPlanOk;
+    const unsigned zero = 0;
+    HIPCHK(hipMemcpyAsync(w.S, S, Gu * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(w.out, &po, sizeof(po), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(a.bad, &zero, 4, hipMemcpyHostToDevice, st));
+    const uint64_t nd = 1ull << ctx->msd_bits;
+    const uint64_t* d_list = (const uint64_t*)((unsigned long long*)(ctx->crbuf.as<uint64_t>() + nd + 1) + 8);
+    HIPCHK(launch_restart_dplan(ds_plan_data(ctx, a), d_list, C, w.pre, w.cbad, w.S, w.out, st));
+    unsigned bad = 0;
+    HIPCHK(hipMemcpyAsync(&po, w.out, sizeof(po), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&bad, a.bad, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(S, w.S, Gu * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (po.status != restart::kPlanOk) return fail(ctx, MUMS_E_HIP, "restart plan table full (internal error)");
+    const uint64_t R = po.nrestarts;
+    ctx->ds_rkey.assign(R, 0);
+    ctx->ds_rS.assign(R * Gu, 0);
+    if (R) {
+        HIPCHK(hipMemcpy(ctx->ds_rkey.data(), w.rkey, R * 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(ctx->ds_rS.data(), w.rS, R * Gu * 8, hipMemcpyDeviceToHost));
+    }
+    *restarts = R;
+    *undecidable = bad ? 1 : 0;
+    return MUMS_OK;
+}
+
+int mums_shard_restart_log(mums_ctx* ctx, uint64_t* rkey, uint64_t* rS) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (!ctx->ds_rkey.empty() && (!rkey || !rS)) return MUMS_E_INVALID;
+    std::copy(ctx->ds_rkey.begin(), ctx->ds_rkey.end(), rkey);
+    std::copy(ctx->ds_rS.begin(), ctx->ds_rS.end(), rS);
+    return MUMS_OK;
+}
+
+int mums_shard_restart_runs(mums_ctx* ctx, uint64_t R, const uint64_t* rkey, const uint64_t* rS, uint64_t* runs,
+                            uint64_t capacity, uint64_t* nruns) {
+    if (check_ctx(ctx) || !nruns || (R && (!rkey || !rS)) || (capacity && !runs)) return MUMS_E_INVALID;
+    if (!ctx->ds_ready) return fail(ctx, MUMS_E_INVALID, "mums_shard_restart_prepare first");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    const uint64_t Gu = (uint64_t)ctx->gt.G, rows = R + 1, rcap = rows * Gu + 16;
+    HIPCHK(ctx->crruns.ensure(rcap * 24 + rows * Gu * 8 + 256));
+    uint64_t* d_runs = ctx->crruns.as<uint64_t>();
+    uint64_t* d_sp = d_runs + 3 * rcap;
+    unsigned long long* d_cnt = (unsigned long long*)(d_sp + rows * Gu);
+    const DsArrays a = ds_arrays(ctx);
+    HIPCHK(hipMemcpyAsync(d_sp, a.S0, Gu * 8, hipMemcpyDeviceToDevice, st));
+    if (R) HIPCHK(hipMemcpyAsync(d_sp + Gu, rS, R * Gu * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(d_cnt, 0, 8, st));
+    HIPCHK(launch_cr_druns(ctx->crall.as<uint64_t>(), ctx->gt.G, a.lbase, a.off, a.n, d_sp, rows, d_runs, d_cnt, rcap,
+                           st));
+    unsigned long long nr = 0;
+    HIPCHK(hipMemcpyAsync(&nr, d_cnt, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));   // (rS is the caller's host array)
+    if (nr > rcap) return fail(ctx, MUMS_E_HIP, "restart: run list overflow (internal error)");
+    std::vector<std::array<uint64_t, 3>> v(nr);
+    if (nr) HIPCHK(hipMemcpy(v.data(), d_runs, nr * 24, hipMemcpyDeviceToHost));
+    std::sort(v.begin(), v.end());
+    v.erase(std::unique(v.begin(), v.end()), v.end());
+    *nruns = v.size();
+    for (uint64_t q = 0; q < v.size() && q < capacity / 3; ++q)
+        for (int k = 0; k < 3; ++k) runs[3 * q + k] = v[q][k];
+    return v.size() * 3 > capacity ? fail(ctx, MUMS_E_INVALID, "run buffer too small") : MUMS_OK;
+}
+
+int mums_shard_restart_ties(mums_ctx* ctx, const uint32_t* d_packed_all, const uint64_t* runs, uint64_t nruns,
+                            const uint64_t* vofs, uint32_t* d_out) {
+    if (check_ctx(ctx) || (nruns && (!d_packed_all || !runs || !vofs || !d_out))) return MUMS_E_INVALID;
+    if (!ctx->shard || ctx->stage_done < MUMS_STAGE_SEEDS) return fail(ctx, MUMS_E_INVALID, "no sharded merge run");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    const GenomeTable& gt = ctx->gt;
+    for (int g = 0; g < gt.G; ++g) {
+        bool any = false;
+        for (uint64_t q = 0; q < nruns; ++q) any = any || (int)runs[3 * q] == g;
+        if (!any) continue;
+        const uint64_t m = gt.m[g];
+        if (m >= 0xFFFFFFF0ull) return fail(ctx, MUMS_E_UNSUPPORTED, "SortedMerList of more than 2^32 seed-mers");
+        for (uint64_t q = 0; q < nruns; ++q)
+            if ((int)runs[3 * q] == g && (runs[3 * q + 1] >= runs[3 * q + 2] || runs[3 * q + 2] > m))
+                return fail(ctx, MUMS_E_INVALID, "restart: bad run");
+        if (tiebuf_ensure(ctx, tie_ws_bytes(m, 1)) != hipSuccess) {
+            (void)hipGetLastError();
+            HIPCHK(hipStreamSynchronize(st));
+            release_find_buffers(ctx);   // the previous FindMatches' tail buffers are dead here
+            if (tiebuf_ensure(ctx, tie_ws_bytes(m, 1)) != hipSuccess)
+                return fail(ctx, MUMS_E_NOMEM, "restart: no device memory for the SortedMerList tie order of a genome");
+        }
+        note_rs_bytes(ctx);
+        const TieWs tw = tie_ws_layout(ctx->tiebuf.p, m, 1);
+        const uint64_t b0 = 0;
+        HIPCHK(tie_set_genomes(tw, &b0, &m, st));
+        HIPCHK(tie_clear_flags(tw, st));
+        for (uint64_t q = 0; q < nruns; ++q) {   // pair flags of every run: slots [lo, hi - 1)
+            if ((int)runs[3 * q] != g) continue;
+            const uint64_t lo = runs[3 * q + 1], hi = runs[3 * q + 2];
+            if (hi - lo >= 2) HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(tw.pf + lo), 1u, hi - 1 - lo, st));
+        }
+        uint64_t flagged = 0;
+        HIPCHK(tie_prepare(tw, &flagged, st));
+        if (flagged) {
+            HIPCHK(launch_keys_of_genome(ctx->ss, d_packed_all + gt.woff[g], m, tw.K, st, false));
+            HIPCHK(tie_replay(tw, st));
+            ctx->tie_slots += flagged;
+        }
+        for (uint64_t q = 0; q < nruns; ++q) {
+            if ((int)runs[3 * q] != g) continue;
+            const uint64_t lo = runs[3 * q + 1], hi = runs[3 * q + 2];
+            HIPCHK(hipMemcpyAsync(d_out + vofs[q], tw.V + lo, (hi - lo) * 4, hipMemcpyDeviceToDevice, st));
+        }
+        HIPCHK(hipStreamSynchronize(st));
+    }
+    if (nruns) {
+        HIPCHK(hipStreamSynchronize(st));
+        release_tiebuf(ctx);
+    }
+    return MUMS_OK;
+}
+
+int mums_shard_restart_finish(mums_ctx* ctx, uint64_t R, const uint64_t* rkey, const uint64_t* rS,
+                              const uint64_t* runs, uint64_t nruns, const uint32_t* d_pos, const uint64_t* vofs) {
+    if (check_ctx(ctx) || (R && (!rkey || !rS)) || (nruns && (!runs || !d_pos || !vofs))) return MUMS_E_INVALID;
+    if (!ctx->ds_ready) return fail(ctx, MUMS_E_INVALID, "mums_shard_restart_prepare first");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    const GenomeTable& gt = ctx->gt;
+    const uint64_t Gu = (uint64_t)gt.G, n = ctx->shard_n;
+    const int B = ctx->msd_bits, mb = ctx->shard_mb;
+    const int kb = 2 * ctx->w + 1 - B;
+    ctx->rs_info[0] = 1;
+    ctx->rs_info[2] = R;
+    auto done = [&]() {
+        for (DevBuf* b : {&ctx->crall, &ctx->crcnt, &ctx->crlive, &ctx->crruns, &ctx->rsplan, &ctx->crbuf})
+            b->release();
+        ctx->ds_ready = false;
+    };
+    if (R == 0 && !have_start_points(ctx)) {   // nothing moves: the stream and its groups stand
+        note_rs_bytes(ctx);
+        done();
+        ctx->restarts = 0;
+        ctx->offset_log.clear();
+        ctx->shard_restart_pending = false;
+        return MUMS_OK;
+    }
+    const uint64_t nd = 1ull << B;
+    CrStream s{ctx->sorted_rec, ctx->crbuf.as<uint64_t>(), (uint32_t)nd, n};
+    s.kb = (uint32_t)kb;
+    s.ib = (uint32_t)ctx->rec_ib;
+    const DsArrays a = ds_arrays(ctx);
+    // device copies: runs + offsets, restart keys, start points of every phase
+    const uint64_t words = 3 * nruns + nruns + R + R * Gu + 64;
+    HIPCHK(ctx->crruns.ensure(words * 8 + 256));
+    uint64_t* d_runs = ctx->crruns.as<uint64_t>();
+    uint64_t* d_vofs = d_runs + 3 * nruns;
+    uint64_t* d_rkey = d_vofs + nruns;
+    uint64_t* d_rS = d_rkey + R;
+    if (nruns) {
+        HIPCHK(hipMemcpyAsync(d_runs, runs, 3 * nruns * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(d_vofs, vofs, nruns * 8, hipMemcpyHostToDevice, st));
+    }
+    if (R) {
+        HIPCHK(hipMemcpyAsync(d_rkey, rkey, R * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(d_rS, rS, R * Gu * 8, hipMemcpyHostToDevice, st));
+    }
+    HIPCHK(launch_cr_dtie_write(s, gt, d_runs, nruns, ctx->crall.as<uint64_t>(), a.lbase, a.off, d_pos, d_vofs,
+                                const_cast<uint64_t*>(ctx->sorted_rec), st));
+    ProbeSpace ps{};
+    int rc = ensure_merge_space(ctx, n, mb, kb, &ps);
+    if (rc) return rc;
+    uint64_t* dst = ctx->sorted_buf ? ctx->recA.as<uint64_t>() : ctx->recB.as<uint64_t>();
+    const uint32_t nb = 1u << mb;
+    HIPCHK(ctx->crlive.ensure(2 * (n + 64) * 4 + 2 * (nb + 64) * 4 + 64));
+    HIPCHK(ctx->tmp.ensure(std::max(ctx->tmp.cap, scan_tmp_bytes(n + 2))));
+    uint32_t* live = ctx->crlive.as<uint32_t>();
+    uint32_t* pos = live + n + 64;
+    uint32_t* bst_in = pos + n + 64;
+    uint32_t* bst_out = bst_in + nb + 64;
+    uint32_t* d_total = bst_out + nb + 64;
+    HIPCHK(hipMemcpyAsync(bst_in, ctx->shard_bst.data(), (nb + 1) * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(launch_cr_live_compact(s, gt, ctx->crcnt.as<uint32_t>(), 0, n, d_rkey, R, d_rS, a.S0, live, pos,
+                                  ctx->tmp.p, dst, bst_in, nb, bst_out, d_total, st, a.off));
+    uint32_t nl = 0;
+    std::vector<uint32_t> bst(nb + 1);
+    HIPCHK(hipMemcpyAsync(&nl, d_total, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(bst.data(), bst_out, (nb + 1) * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    note_rs_bytes(ctx);
+    done();
+    std::vector<uint64_t> log(rS, rS + R * Gu);
+    return shard_regroup(ctx, dst, nl, bst, ps, R, log.data(), st);
+}
+
+int mums_shard_restart_info(mums_ctx* ctx, uint64_t* info) {
+    if (check_ctx(ctx) || !info) return MUMS_E_INVALID;
+    std::copy(ctx->rs_info, ctx->rs_info + 4, info);
     return MUMS_OK;
 }
 
@@ -2604,13 +3056,14 @@ int mums_probe_copy(mums_ctx* ctx, uint32_t* buckets, uint64_t* ref_index, uint6
 
 namespace {
 
-int shard_seeds_done(mums_ctx* ctx) {
+// (pending_ok: the packed genomes, which the restart's tie replay reads too)
+int shard_seeds_done(mums_ctx* ctx, bool pending_ok = false) {
     if (check_ctx(ctx)) return MUMS_E_INVALID;
     if (!ctx->shard) return fail(ctx, MUMS_E_INVALID, "not a sharded context (mums_shard_layout)");
     if (ctx->stage_done < MUMS_STAGE_SEEDS) return fail(ctx, MUMS_E_INVALID, "no sharded seed stage run");
     if (ctx->merge_chunked)
         return fail(ctx, MUMS_E_UNSUPPORTED, "sharded FindMatches after a chunked merge (> 2^30 records per rank)");
-    if (ctx->shard_restart_pending)
+    if (ctx->shard_restart_pending && !pending_ok)
         return fail(ctx, MUMS_E_INVALID, "sharded restart pending (mums_shard_restart_plan / _apply)");
     return MUMS_OK;
 }
@@ -3642,7 +4095,7 @@ int mums_shard_probe_rows(mums_ctx* ctx, uint32_t nranks, const uint32_t* bounds
 }
 
 int mums_shard_packed_info(mums_ctx* ctx, uint64_t* word_offset, uint64_t* nwords, uint64_t* total_words) {
-    int rc = shard_seeds_done(ctx);
+    int rc = shard_seeds_done(ctx, true);
     if (rc) return rc;
     GenomeTable g = ctx->gt;
     uint64_t total = 0;

@@ -386,6 +386,11 @@ hipError_t launch_restart_cands(const RestartWs& w, uint64_t n, uint64_t* d_list
 // d_pre: 3 * C * G uint64 + C int; d_S: G start points in / last phase's out
 hipError_t launch_restart_plan(const RestartWs& w, int G, const uint64_t* d_cand, uint64_t C, uint64_t* d_pre,
                                uint64_t* d_S, restart::PlanOut* d_out, hipStream_t st);
+// the sharded mode's distributed plan (PlanData with off / n / prv / nxt; cbad: C flags)
+hipError_t launch_restart_dpre(const restart::PlanData& d, const uint64_t* d_cand, uint64_t C, uint64_t* d_pre,
+                               unsigned* cbad, hipStream_t st);
+hipError_t launch_restart_dplan(const restart::PlanData& d, const uint64_t* d_cand, uint64_t C, const uint64_t* d_pre,
+                                const unsigned* cbad, uint64_t* d_S, restart::PlanOut* d_out, hipStream_t st);
 // live records (SML index >= start point of their key's phase) compacted in order into
 // dst (records, or keys + dst_idx); kind 0 also writes the new bucket starts
 // LogProgress tie groups (w.ck / w.dm / w.dbase): ord[i * G ..] = head order of the genomes
@@ -410,7 +415,8 @@ struct CrStream {
 uint64_t cr_blocks(uint64_t N);
 // gcnt: G x (cr_blocks(N) + 1) per-genome block counts, exclusive-scanned per genome
 hipError_t launch_cr_counts(const CrStream& s, const GenomeTable& gt, uint32_t* gcnt, void* d_scan_tmp, hipStream_t st);
-hipError_t launch_cr_ck(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, uint64_t* ck, hipStream_t st);
+hipError_t launch_cr_ck(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, uint64_t* ck, hipStream_t st,
+                        const uint64_t* lbase = nullptr);
 // masked key of genome g's SML index e for every query g << 56 | e (gscan from launch_cr_counts)
 hipError_t launch_cr_query(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, const uint64_t* q, uint64_t nq,
                            uint64_t* out, hipStream_t st);
@@ -418,13 +424,22 @@ hipError_t launch_cr_cands(const CrStream& s, uint64_t* list, unsigned long long
 hipError_t launch_cr_runs(const uint64_t* ck, const GenomeTable& gt, const uint64_t* sp, uint64_t rows, uint64_t* runs,
                           unsigned long long* nr, uint64_t cap, hipStream_t st);
 hipError_t launch_cr_kpos(const CrStream& s, const GenomeTable& gt, int g, uint64_t* K, hipStream_t st);
+// a sharded rank's part of every SML (global indices [goff[g], goff[g] + gn[g]) at ck[lbase[g] ..]):
+// straddled runs {g, lo, hi} (global indices) of the start points sp (rows x G), and the id
+// rewrite of its runs from V[vofs[q] ..]
+hipError_t launch_cr_druns(const uint64_t* ck, int G, const uint64_t* lbase, const uint64_t* goff, const uint64_t* gn,
+                           const uint64_t* sp, uint64_t rows, uint64_t* runs, unsigned long long* nr, uint64_t cap,
+                           hipStream_t st);
+hipError_t launch_cr_dtie_write(const CrStream& s, const GenomeTable& gt, const uint64_t* runs, uint64_t nrun,
+                                const uint64_t* ck, const uint64_t* lbase, const uint64_t* goff, const uint32_t* V,
+                                const uint64_t* vofs, uint64_t* rec, hipStream_t st);
 hipError_t launch_cr_tie_write(const CrStream& s, const GenomeTable& gt, int g, const uint64_t* runs, uint64_t nrun,
                                const uint64_t* ck, const uint32_t* V, uint64_t* rec, hipStream_t st);
 hipError_t launch_cr_live_compact(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, uint64_t lo,
                                   uint64_t hi, const uint64_t* rkey, uint64_t R, const uint64_t* rS, const uint64_t* S0,
                                   uint32_t* live, uint32_t* pos, void* d_scan_tmp, uint64_t* dst,
                                   const uint32_t* bstart, uint32_t nb, uint32_t* dst_bstart, uint32_t* d_total,
-                                  hipStream_t st);
+                                  hipStream_t st, const uint64_t* goff = nullptr);
 
 // smlsort.hip: the std::sort order of equal seed mers in every SortedMerList
 // (MemorySML.cpp:54) for flagged runs.  Slot space = genome-major SML slots (= global

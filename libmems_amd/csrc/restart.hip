@@ -88,10 +88,15 @@ __global__ void rs_cand_kernel(const uint64_t* __restrict__ ckf, uint64_t n, uin
 }
 
 __global__ void rs_pre_kernel(PlanData d, const uint64_t* __restrict__ cand, uint64_t C, uint64_t* __restrict__ clo,
-                              uint64_t* __restrict__ chi, uint64_t* __restrict__ cbp, int* __restrict__ cseq) {
+                              uint64_t* __restrict__ chi, uint64_t* __restrict__ cbp, int* __restrict__ cseq,
+                              unsigned* __restrict__ cbad) {
     const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
     const uint64_t G = (uint64_t)d.G;
+    if (cbad) {   // distributed: flags per candidate (restart_plan reads them when one fires)
+        cbad[c] = 0u;
+        d.bad = cbad + c;
+    }
     restart::cand_precompute(d, cand[c], clo + c * G, chi + c * G, cbp + c * G, cseq + c);
 }
 
@@ -100,10 +105,10 @@ __global__ void rs_pre_kernel(PlanData d, const uint64_t* __restrict__ cand, uin
 __global__ void rs_plan_kernel(PlanData d, const uint64_t* __restrict__ cand, uint64_t C,
                                const uint64_t* __restrict__ clo, const uint64_t* __restrict__ chi,
                                const uint64_t* __restrict__ cbp, const int* __restrict__ cseq, uint64_t* S,
-                               PlanOut* out) {
+                               PlanOut* out, const unsigned* __restrict__ cbad) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     PlanOut o = *out;
-    restart::restart_plan(d, cand, C, clo, chi, cbp, cseq, S, &o);
+    restart::restart_plan(d, cand, C, clo, chi, cbp, cseq, S, &o, cbad);
     *out = o;
 }
 
@@ -215,10 +220,35 @@ hipError_t launch_restart_plan(const RestartWs& w, int G, const uint64_t* d_cand
     uint64_t* chi = clo + C * (uint64_t)G;
     uint64_t* cbp = chi + C * (uint64_t)G;
     int* cseq = (int*)(cbp + C * (uint64_t)G);
-    hipLaunchKernelGGL(rs_pre_kernel, grid_of(C), dim3(kBlock), 0, st, d, d_cand, C, clo, chi, cbp, cseq);
+    hipLaunchKernelGGL(rs_pre_kernel, grid_of(C), dim3(kBlock), 0, st, d, d_cand, C, clo, chi, cbp, cseq, nullptr);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(rs_plan_kernel, dim3(1), dim3(64), 0, st, d, d_cand, C, clo, chi, cbp, cseq, d_S, d_out);
+    hipLaunchKernelGGL(rs_plan_kernel, dim3(1), dim3(64), 0, st, d, d_cand, C, clo, chi, cbp, cseq, d_S, d_out,
+                       nullptr);
+    return hipGetLastError();
+}
+
+// the sharded mode's plan (restart_plan.h PlanData with off / n / prv / nxt): candidate
+// precompute on every rank at once, then the plan one rank after the other (running S)
+hipError_t launch_restart_dpre(const PlanData& d, const uint64_t* d_cand, uint64_t C, uint64_t* d_pre, unsigned* cbad,
+                               hipStream_t st) {
+    if (C == 0) return hipSuccess;
+    uint64_t* clo = d_pre;
+    uint64_t* chi = clo + C * (uint64_t)d.G;
+    uint64_t* cbp = chi + C * (uint64_t)d.G;
+    int* cseq = (int*)(cbp + C * (uint64_t)d.G);
+    hipLaunchKernelGGL(rs_pre_kernel, grid_of(C), dim3(kBlock), 0, st, d, d_cand, C, clo, chi, cbp, cseq, cbad);
+    return hipGetLastError();
+}
+
+hipError_t launch_restart_dplan(const PlanData& d, const uint64_t* d_cand, uint64_t C, const uint64_t* d_pre,
+                                const unsigned* cbad, uint64_t* d_S, PlanOut* d_out, hipStream_t st) {
+    if (C == 0) return hipSuccess;
+    const uint64_t* clo = d_pre;
+    const uint64_t* chi = clo + C * (uint64_t)d.G;
+    const uint64_t* cbp = chi + C * (uint64_t)d.G;
+    const int* cseq = (const int*)(cbp + C * (uint64_t)d.G);
+    hipLaunchKernelGGL(rs_plan_kernel, dim3(1), dim3(64), 0, st, d, d_cand, C, clo, chi, cbp, cseq, d_S, d_out, cbad);
     return hipGetLastError();
 }
 
@@ -235,7 +265,7 @@ __global__ void tie_heads_kernel(PlanData d, const uint64_t* __restrict__ gk, co
     for (int g = 0; g < G; ++g) {
         a[g] = 0;
         if ((gu[i] >> g) & 1) {
-            const uint64_t lb = restart::lower_bound_u64(d.ck + d.base[g], d.m[g], gk[i] << 1);
+            const uint64_t lb = restart::lower_bound_g(d, g, 0, d.m[g], gk[i] << 1);
             a[g] = lb > S[g] ? lb : S[g];
         }
     }

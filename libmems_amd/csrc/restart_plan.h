@@ -49,13 +49,55 @@ constexpr int kMaxGenomes = 64;
 constexpr uint64_t kRepeatLimit = 1000;   // MER_REPEAT_LIMIT, MatchFinder.cpp:166
 constexpr uint64_t kMerBuffer = 10000;    // MER_BUFFER_SIZE, MatchFinder.cpp:175
 
-// per-genome sorted mer lists: genome g's SML = ck[base[g] .. base[g] + m[g])
+// per-genome sorted mer lists: genome g's SML = ck[base[g] .. base[g] + m[g]).
+// Distributed (off != nullptr, the sharded mode): this rank holds genome g's SML indices
+// [off[g], off[g] + n[g]) at ck[base[g] ..], the records of its key range [key_lo, key_hi)
+// (full keys; both bounds even: a masked key never straddles two ranks).  Of the other
+// indices it knows the keys next to its range: prv[g] at off[g] - 1 (the last key of genome g
+// on a lower rank) and nxt[g] at off[g] + n[g] (the first on a higher one).  kc() answers every
+// index -- below the range with prv[g] (an upper bound), above it with nxt[g] (a lower bound):
+// exact at the two neighbours, and comparing like the real key against any query in
+// [key_lo, key_hi] -- what the binary searches need.  kx() needs the real key: outside
+// [off[g] - 1, off[g] + n[g]] it flags *bad (the plan is then made on the gathered streams).
 struct PlanData {
     int G;
     const uint64_t* m;
     const uint64_t* base;
     const uint64_t* ck;
+    const uint64_t* off = nullptr;
+    const uint64_t* n = nullptr;
+    const uint64_t* prv = nullptr;
+    const uint64_t* nxt = nullptr;
+    uint64_t key_lo = 0, key_hi = ~0ull;
+    unsigned* bad = nullptr;
+    MUMS_HD void flag() const {
+        if (bad) *bad = 1u;
+    }
+    MUMS_HD uint64_t kc(int g, uint64_t i) const {
+        if (!off) return ck[base[g] + i];
+        if (i < off[g]) return prv[g];
+        if (i - off[g] >= n[g]) return nxt[g];
+        return ck[base[g] + (i - off[g])];
+    }
+    MUMS_HD uint64_t kx(int g, uint64_t i) const {
+        if (off && (i + 1 < off[g] || i > off[g] + n[g])) flag();
+        return kc(g, i);
+    }
+    // a query key the stand-ins cannot answer (beyond this rank's key range)
+    MUMS_HD void need(uint64_t q) const {
+        if (off && q >= key_hi) flag();
+    }
 };
+
+// first index i in [lo, hi) of genome g's SML with key >= x (i = hi if none)
+MUMS_HD inline uint64_t lower_bound_g(const PlanData& d, int g, uint64_t lo, uint64_t hi, uint64_t x) {
+    while (lo < hi) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if (d.kc(g, mid) < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
 
 // first index i in a[0, n) with a[i] >= x
 MUMS_HD inline uint64_t lower_bound_u64(const uint64_t* a, uint64_t n, uint64_t x) {
@@ -69,10 +111,10 @@ MUMS_HD inline uint64_t lower_bound_u64(const uint64_t* a, uint64_t n, uint64_t 
 }
 
 // SortedMerList::bsearch (SortedMerList.cpp:380-394), recursion unrolled, unsigned
-MUMS_HD inline uint64_t ref_bsearch(const uint64_t* a, uint64_t q, uint64_t start, uint64_t end) {
+MUMS_HD inline uint64_t ref_bsearch(const PlanData& d, int g, uint64_t q, uint64_t start, uint64_t end) {
     for (;;) {
         const uint64_t middle = (start + end) / 2;
-        const uint64_t k = a[middle];
+        const uint64_t k = d.kc(g, middle);
         if (k == q) return middle;
         if (k < q && middle < end) start = middle + 1;
         else if (k > q && start < middle) end = middle - 1;
@@ -80,12 +122,14 @@ MUMS_HD inline uint64_t ref_bsearch(const uint64_t* a, uint64_t q, uint64_t star
     }
 }
 
-// SortedMerList::FindMer (SortedMerList.cpp:170-179) on an SML of m records (m = 0 <=>
-// sequence shorter than the seed: early return, *result untouched).
-MUMS_HD inline bool ref_find_mer(const uint64_t* a, uint64_t m, uint64_t q, uint64_t* result) {
+// SortedMerList::FindMer (SortedMerList.cpp:170-179) on genome g's SML of m records (m = 0
+// <=> sequence shorter than the seed: early return, *result untouched).
+MUMS_HD inline bool ref_find_mer(const PlanData& d, int g, uint64_t q, uint64_t* result) {
+    const uint64_t m = d.m[g];
     if (m == 0) return false;
-    *result = ref_bsearch(a, q, 0, m - 1);
-    return a[*result] == q;
+    d.need(q);
+    *result = ref_bsearch(d, g, q, 0, m - 1);
+    return d.kc(g, *result) == q;   // (a stand-in never equals a query of this key range)
 }
 
 // Per candidate key v (masked, i.e. ckey >> 1): the run [lo, hi) of v in every SML and
@@ -95,43 +139,43 @@ MUMS_HD inline void cand_precompute(const PlanData& d, uint64_t v, uint64_t* lo,
                                     int* seq_out) {
     const int G = d.G;
     for (int g = 0; g < G; ++g) {
-        const uint64_t* a = d.ck + d.base[g];
-        lo[g] = lower_bound_u64(a, d.m[g], v << 1);
-        hi[g] = lower_bound_u64(a, d.m[g], (v + 1) << 1);
+        lo[g] = lower_bound_g(d, g, 0, d.m[g], v << 1);
+        hi[g] = lower_bound_g(d, g, 0, d.m[g], (v + 1) << 1);
         bp[g] = 0;
     }
     const uint64_t next = (v + 1) << 1;   // next_mer = K + (~mer_mask + 1), forward parity
     uint64_t next_pos = 0;
     int s = 0;
     for (; s < G; ++s) {
-        if (!ref_find_mer(d.ck + d.base[s], d.m[s], next, &next_pos)) ++next_pos;
+        if (!ref_find_mer(d, s, next, &next_pos)) ++next_pos;
         if (next_pos < d.m[s]) break;
     }
     *seq_out = s;
     if (s >= G) return;
-    const uint64_t* as = d.ck + d.base[s];
-    const uint64_t brk = as[next_pos];
-    const uint64_t start = lower_bound_u64(as, next_pos + 1, (brk >> 1) << 1);   // backward loop :104-112
+    const uint64_t brk = d.kx(s, next_pos);
+    const uint64_t start = lower_bound_g(d, s, 0, next_pos + 1, (brk >> 1) << 1);   // backward loop :104-112
     for (int i = 0; i < G; ++i) {
         if (i == s) { bp[i] = start; continue; }
         uint64_t cur = 0;   // the reference's uninitialised cur_start (only for empty SMLs)
-        const uint64_t* ai = d.ck + d.base[i];
-        if (ref_find_mer(ai, d.m[i], brk, &cur)) {
+        if (ref_find_mer(d, i, brk, &cur)) {
             // (matchmer.mer & mer_mask) == (break_mer.mer && mer_mask): true only for the
             // all-A key hit by a zero break key; the loop then runs down to -1
-            const bool runs = (ai[cur] >> 1) == 0 && brk == 0;
+            const bool runs = (d.kx(i, cur) >> 1) == 0 && brk == 0;
             cur = runs ? 0 : cur + 1;
         }
         bp[i] = cur;
     }
 }
 
-// first index of the masked-key run containing p (a[p] >> 1 == X), galloping backwards
-MUMS_HD inline uint64_t run_start_back(const uint64_t* a, uint64_t p, uint64_t X) {
+// first index of genome g's masked-key run containing p (key >> 1 == X), galloping backwards
+// (a masked-key run of this rank's key range ends at its lower edge: kc's stand-in there is
+// smaller; the run of prv[g] at off[g] - 1 lies on a lower rank)
+MUMS_HD inline uint64_t run_start_back(const PlanData& d, int g, uint64_t p, uint64_t X) {
+    if (d.off && p < d.off[g] && p > 0) d.flag();
     uint64_t good = p, step = 1;
     int64_t bad = -1;
     for (;;) {
-        if (good >= step && (a[good - step] >> 1) == X) {
+        if (good >= step && (d.kc(g, good - step) >> 1) == X) {
             good -= step;
             step <<= 1;
         } else {
@@ -142,7 +186,7 @@ MUMS_HD inline uint64_t run_start_back(const uint64_t* a, uint64_t p, uint64_t X
     uint64_t lo = (uint64_t)(bad + 1), hi = good;
     while (lo < hi) {
         const uint64_t mid = lo + (hi - lo) / 2;
-        if ((a[mid] >> 1) < X) lo = mid + 1;
+        if ((d.kc(g, mid) >> 1) < X) lo = mid + 1;
         else hi = mid;
     }
     return lo;
@@ -185,12 +229,12 @@ MUMS_HD inline int head_order(const PlanData& d, uint64_t U, const uint64_t* a, 
         bool any = false;
         for (int g = 0; g < G; ++g) {
             if (!((active >> g) & 1)) continue;
-            const uint64_t x = d.ck[d.base[g] + p[g]] >> 1;
+            const uint64_t x = d.kx(g, p[g]) >> 1;
             if (!any || x > X) { X = x; any = true; }
         }
         uint64_t pres = 0;
         for (int g = 0; g < G; ++g)
-            if (((active >> g) & 1) && (d.ck[d.base[g] + p[g]] >> 1) == X) pres |= 1ull << g;
+            if (((active >> g) & 1) && (d.kx(g, p[g]) >> 1) == X) pres |= 1ull << g;
         ++*walk_steps;
         // fold the key into the classes (in order)
         OrderClass nc[kMaxGenomes];
@@ -209,8 +253,7 @@ MUMS_HD inline int head_order(const PlanData& d, uint64_t U, const uint64_t* a, 
         // step the holders back past their run of X
         for (int g = 0; g < G; ++g) {
             if (!((pres >> g) & 1)) continue;
-            const uint64_t* ag = d.ck + d.base[g];
-            const uint64_t st = run_start_back(ag, p[g], X);
+            const uint64_t st = run_start_back(d, g, p[g], X);
             if (st > S[g]) p[g] = st - 1;
             else active &= ~(1ull << g);
         }
@@ -245,9 +288,11 @@ struct PlanOut {
 // Consume the candidates (groups of > 1000 records, ascending masked keys cand[c], with
 // cand_precompute results clo / chi / cbp [c * G + g] and cseq[c]) in key order with the
 // running start points S (in: the FindMatchSeeds start offsets; out: the last phase's).
+// cbad (distributed): cand_precompute needed a key of another rank for candidate c -- its
+// restart target is unknown, so firing it flags d.bad.
 MUMS_HD inline void restart_plan(const PlanData& d, const uint64_t* cand, uint64_t C, const uint64_t* clo,
                                  const uint64_t* chi, const uint64_t* cbp, const int* cseq, uint64_t* S,
-                                 PlanOut* out) {
+                                 PlanOut* out, const unsigned* cbad = nullptr) {
     const int G = d.G;
     for (uint64_t c = 0; c < C; ++c) {
         const uint64_t* lo = clo + c * (uint64_t)G;
@@ -287,6 +332,7 @@ MUMS_HD inline void restart_plan(const PlanData& d, const uint64_t* cand, uint64
             if (!fired && (b[g] - S[g]) % kMerBuffer == 0 && b[g] < d.m[g] && cum > kRepeatLimit) fired = true;
         }
         if (!fired) continue;
+        if (cbad && cbad[c]) d.flag();
         if (out->nrestarts >= out->cap) { out->status = kPlanTableFull; return; }
         const int s = cseq[c];
         const uint64_t* bp = cbp + c * (uint64_t)G;

@@ -64,6 +64,7 @@ struct mums_comm {
             if (p) (void)hipFree(p);
         }
     } rec, recv, rows, rrows, packed, packed_all;
+    bool packed_done = false;   // packed_all holds this run's genomes (gather_packed)
 };
 
 namespace {
@@ -264,6 +265,179 @@ int agree(mums_comm* c, int rc, hipStream_t st) {
 // a local step's status: OK, or the step's code (allocation failures as MUMS_E_NOMEM)
 #define AGREE(x) RC(agree(comm, (x), st))
 
+// 7. all-gather(v) of the 2-bit packed genomes into comm->packed_all, genome g at its word
+// offset (FindMatches' chain walks, the restart's tie replay read any genome); once per run
+int gather_packed(mums_ctx* ctx, mums_comm* comm, hipStream_t st) {
+    const int W = comm->world;
+    int rc = MUMS_OK;
+    uint64_t woff = 0, nw = 0, total = 0;
+    rc = mums_shard_packed_info(ctx, &woff, &nw, &total);
+    if (rc == MUMS_OK && (comm->packed_all.ensure((total + 1) * 4) || comm->packed.ensure((nw + 1) * 4)))
+        rc = MUMS_E_NOMEM;
+    if (rc == MUMS_OK && hipMemsetAsync(comm->packed_all.p, 0, (total + 1) * 4, st) != hipSuccess) rc = MUMS_E_HIP;
+    if (rc == MUMS_OK)
+        rc = mums_shard_packed_copy(ctx, W == 1 ? (uint32_t*)comm->packed_all.p + woff : (uint32_t*)comm->packed.p);
+    if (rc == MUMS_OK && W > 1 && comm->rec.ensure((size_t)W * nw * 4 + 8)) rc = MUMS_E_NOMEM;
+    AGREE(rc);
+    if (W > 1) {   // all-gather(v) of the packed slices as an all-to-allv with one block per peer
+        std::vector<uint64_t> meta{woff, nw}, M((size_t)2 * W);
+        RC(comm->allgather_u64(meta.data(), 2, M.data(), st));
+        // every rank sends its slice to every rank; received blocks land in rank order,
+        // which is word-offset order (genome blocks / slices ascend with the rank)
+        std::vector<uint64_t> sb(W, nw * 4), rb(W);
+        uint64_t o = 0;
+        bool ordered = true;
+        for (int p = 0; p < W; ++p) {
+            rb[p] = M[(size_t)2 * p + 1] * 4;
+            ordered = ordered && M[(size_t)2 * p] == o;
+            o += M[(size_t)2 * p + 1];
+        }
+        if (!ordered) return comm_fail(comm, "packed slices are not in rank order");   // the same on every rank
+        // the send buffer is the slice repeated per peer (all-to-allv sends disjoint blocks)
+        rc = MUMS_OK;
+        for (int p = 0; p < W && rc == MUMS_OK; ++p)
+            if (nw && hipMemcpyAsync((uint32_t*)comm->rec.p + (size_t)p * nw, comm->packed.p, nw * 4,
+                                     hipMemcpyDeviceToDevice, st) != hipSuccess)
+                rc = MUMS_E_HIP;
+        AGREE(rc);
+        RC(comm->alltoallv(comm->rec.p, sb.data(), comm->packed_all.p, rb.data(), st));
+    }
+    comm->packed_done = true;
+    return MUMS_OK;
+}
+
+// 4b (default). The restart planned where the records are (mums_shard_restart_counts ..
+// _finish): rank r holds SML indices [off_r[g], off_r[g] + n_r[g]) of every genome, so the
+// plan runs on the ranks' own SML parts -- candidate precompute everywhere at once, then the
+// plan rank after rank with the running start points (G words per step).  Straddled runs
+// get their std::sort order on rank g % world from the all-gathered packed genomes; every
+// rank compacts its own live records.  Nothing is gathered: rank 0 holds O(its records).
+// *done = false (nothing changed) when any rank's plan needs a key beyond its neighbours.
+int shard_restart_local(mums_ctx* ctx, mums_comm* comm, hipStream_t st, bool* done) {
+    *done = false;
+    const int W = comm->world, R = comm->rank;
+    const bool dbg = getenv("MUMS_DEV_SHARD_RESTART_DEBUG") != nullptr;
+    uint32_t T = 0, G = 0;
+    RC(mums::ctx_table_genomes(ctx, &T, &G));
+    const uint64_t Gu = G, row = 3 * Gu + 2;   // mums_shard_restart_counts' info + candidates
+    std::vector<uint64_t> info(row, 0), ALL((size_t)W * row), ri(4, 0);
+    int rc = mums_shard_restart_counts(ctx, info.data());
+    if (rc == MUMS_OK) rc = mums_shard_restart_info(ctx, ri.data());
+    info[3 * Gu + 1] = ri[1];
+    AGREE(rc);
+    RC(comm->allgather_u64(info.data(), row, ALL.data(), st));
+    std::vector<uint64_t> flat((size_t)W * (row - 1));   // rows of 3G + 1 for _prepare
+    for (int r = 0; r < W; ++r) {
+        if (ALL[(size_t)r * row + 3 * Gu]) return MUMS_OK;   // a rank asks for the gathered plan
+        std::copy(ALL.begin() + (size_t)r * row, ALL.begin() + (size_t)r * row + row - 1,
+                  flat.begin() + (size_t)r * (row - 1));
+    }
+    if (dbg)
+        fprintf(stderr, "rank %d: restart counts ok, candidates %lu\n", R, (unsigned long)info[3 * Gu + 1]);
+    std::vector<uint64_t> S(Gu, 0);
+    AGREE(mums_shard_restart_prepare(ctx, (uint32_t)W, (uint32_t)R, flat.data(), S.data()));
+    // the plan, rank after rank: [status, restarts, undecidable, S]
+    std::vector<uint64_t> msg(3 + Gu), M((size_t)W * (3 + Gu)), Rn(W, 0);
+    for (int r = 0; r < W; ++r) {
+        if (ALL[(size_t)r * row + 3 * Gu + 1] == 0) continue;   // no candidates: S passes through
+        std::fill(msg.begin(), msg.end(), 0);
+        if (r == R) {
+            std::copy(S.begin(), S.end(), msg.begin() + 3);
+            uint64_t nr = 0, und = 0;
+            const int src = mums_shard_restart_step(ctx, msg.data() + 3, &nr, &und);
+            msg[0] = (uint64_t)(uint32_t)src;
+            msg[1] = nr;
+            msg[2] = und;
+        }
+        RC(comm->allgather_u64(msg.data(), msg.size(), M.data(), st));
+        const uint64_t* m = M.data() + (size_t)r * (3 + Gu);
+        const int code = (int)(int32_t)(uint32_t)m[0];
+        if (code != MUMS_OK) {
+            if (r != R) comm->err = "rank " + std::to_string(r) + " failed (status " + std::to_string(code) + ")";
+            return code;
+        }
+        if (dbg) fprintf(stderr, "rank %d: plan step of rank %d: %lu restarts, undecidable %lu\n", R, r,
+                         (unsigned long)m[1], (unsigned long)m[2]);
+        if (m[2]) return MUMS_OK;   // undecidable on rank r: the gathered plan (nothing changed yet)
+        Rn[r] = m[1];
+        std::copy(m + 3, m + 3 + Gu, S.begin());
+    }
+    // every rank's restarts in rank order (= key order)
+    uint64_t Rt = 0, Rmax = 0;
+    for (int r = 0; r < W; ++r) {
+        Rt += Rn[r];
+        Rmax = std::max(Rmax, Rn[r]);
+    }
+    std::vector<uint64_t> rkey(Rt), rS(Rt * Gu);
+    if (Rt) {
+        const uint64_t blk = Rmax * (1 + Gu);
+        std::vector<uint64_t> mine(blk, 0), L((size_t)W * blk);
+        rc = Rn[R] ? mums_shard_restart_log(ctx, mine.data(), mine.data() + Rmax) : MUMS_OK;
+        AGREE(rc);
+        RC(comm->allgather_u64(mine.data(), blk, L.data(), st));
+        uint64_t o = 0;
+        for (int r = 0; r < W; ++r) {
+            const uint64_t* b = L.data() + (size_t)r * blk;
+            for (uint64_t k = 0; k < Rn[r]; ++k, ++o) {
+                rkey[o] = b[k];
+                std::copy(b + Rmax + k * Gu, b + Rmax + (k + 1) * Gu, rS.begin() + o * Gu);
+            }
+        }
+    }
+    // the runs of equal keys the start points of every phase fall into, on their owner ranks
+    const uint64_t cap = 3 * (Rt + 1) * Gu;
+    std::vector<uint64_t> runs(cap + 3, 0);
+    uint64_t nr = 0;
+    AGREE(mums_shard_restart_runs(ctx, Rt, rkey.data(), rS.data(), runs.data(), cap, &nr));
+    std::vector<uint64_t> NR(W);
+    RC(comm->allgather_u64(&nr, 1, NR.data(), st));
+    if (dbg) fprintf(stderr, "rank %d: %lu restarts in all, %lu straddled runs here\n", R, (unsigned long)Rt, (unsigned long)nr);
+    uint64_t NRmax = 0, NRt = 0;
+    for (int r = 0; r < W; ++r) {
+        NRmax = std::max(NRmax, NR[r]);
+        NRt += NR[r];
+    }
+    std::vector<uint64_t> vofs(nr, 0);
+    if (NRt) {
+        std::vector<uint64_t> AR((size_t)W * 3 * NRmax);
+        runs.resize(std::max<uint64_t>(3 * NRmax, 3));
+        RC(comm->allgather_u64(runs.data(), 3 * NRmax, AR.data(), st));
+        RC(gather_packed(ctx, comm, st));
+        // rank g % W replays genome g; its send block for rank p: p's runs of those genomes
+        std::vector<uint64_t> sb(W, 0), rb(W, 0), des, dofs;
+        uint64_t so = 0;
+        for (int p = 0; p < W; ++p)
+            for (uint64_t q = 0; q < NR[p]; ++q) {
+                const uint64_t* x = AR.data() + (size_t)p * 3 * NRmax + 3 * q;
+                if ((int)(x[0] % (uint64_t)W) != R) continue;
+                des.insert(des.end(), x, x + 3);
+                dofs.push_back(so);
+                so += x[2] - x[1];
+                sb[p] += 4 * (x[2] - x[1]);
+            }
+        uint64_t ro = 0;
+        for (int d = 0; d < W; ++d)
+            for (uint64_t q = 0; q < nr; ++q) {
+                const uint64_t* x = runs.data() + 3 * q;
+                if ((int)(x[0] % (uint64_t)W) != d) continue;
+                vofs[q] = ro;
+                ro += x[2] - x[1];
+                rb[d] += 4 * (x[2] - x[1]);
+            }
+        AGREE(comm->rows.ensure(so * 4 + 8) || comm->rrows.ensure(ro * 4 + 8) ? MUMS_E_NOMEM : MUMS_OK);
+        AGREE(mums_shard_restart_ties(ctx, (const uint32_t*)comm->packed_all.p, des.data(), dofs.size(), dofs.data(),
+                                      (uint32_t*)comm->rows.p));
+        RC(comm->alltoallv(comm->rows.p, sb.data(), comm->rrows.p, rb.data(), st));
+    }
+    rc = hipStreamSynchronize(st) != hipSuccess ? MUMS_E_HIP : MUMS_OK;
+    if (rc == MUMS_OK)
+        rc = mums_shard_restart_finish(ctx, Rt, rkey.data(), rS.data(), runs.data(), nr,
+                                       nr ? (const uint32_t*)comm->rrows.p : nullptr, vofs.data());
+    *done = true;
+    if (dbg) fprintf(stderr, "rank %d: restart finish rc %d (%s)\n", R, rc, rc ? mums_last_error(ctx) : "");
+    return agree(comm, rc, st);
+}
+
 // 4b. MER_REPEAT_LIMIT restarts / start points (MatchFinder.cpp:253-277, MemHash.cpp:117-127):
 // a restart moves the start points of every later key (records of other ranks) and its plan
 // reads whole SortedMerLists, so the merged streams are gathered in rank order (= key order)
@@ -415,6 +589,7 @@ int mums_shard_run(mums_ctx* ctx, mums_comm* comm, int stage) {
     const int W = comm->world, R = comm->rank;
     hipStream_t st = mums::ctx_stream(ctx);
     int rc = hipSetDevice(mums::ctx_device(ctx)) != hipSuccess ? MUMS_E_NODEVICE : MUMS_OK;
+    comm->packed_done = false;
     // 1-4: sharded seed stage.  Every local step's status is agreed on before the next
     // collective (agree), so one rank's failure never leaves the others waiting in it.
     uint32_t B = 0;
@@ -459,7 +634,11 @@ int mums_shard_run(mums_ctx* ctx, mums_comm* comm, int stage) {
         RC(comm->allgather_u64(&pend, 1, PEND.data(), st));
         bool any = false;
         for (int r = 0; r < W; ++r) any = any || PEND[r] != 0;
-        if (any) RC(shard_restart(ctx, comm, C, kf, kn, nb, st));
+        if (any) {
+            bool done = false;
+            RC(shard_restart_local(ctx, comm, st, &done));
+            if (!done) RC(shard_restart(ctx, comm, C, kf, kn, nb, st));
+        }
     }
     if (stage != MUMS_STAGE_ALL) return MUMS_OK;
     // 5-8: sharded FindMatches
@@ -498,38 +677,7 @@ int mums_shard_run(mums_ctx* ctx, mums_comm* comm, int stage) {
         RC(comm->alltoallv(comm->rows.p, sb.data(), comm->rrows.p, rb.data(), st));
         rows = (const int64_t*)comm->rrows.p;
     }
-    uint64_t woff = 0, nw = 0, total = 0;
-    rc = mums_shard_packed_info(ctx, &woff, &nw, &total);
-    if (rc == MUMS_OK && (comm->packed_all.ensure((total + 1) * 4) || comm->packed.ensure((nw + 1) * 4)))
-        rc = MUMS_E_NOMEM;
-    if (rc == MUMS_OK && hipMemsetAsync(comm->packed_all.p, 0, (total + 1) * 4, st) != hipSuccess) rc = MUMS_E_HIP;
-    if (rc == MUMS_OK)
-        rc = mums_shard_packed_copy(ctx, W == 1 ? (uint32_t*)comm->packed_all.p + woff : (uint32_t*)comm->packed.p);
-    if (rc == MUMS_OK && W > 1 && comm->rec.ensure((size_t)W * nw * 4 + 8)) rc = MUMS_E_NOMEM;
-    AGREE(rc);
-    if (W > 1) {   // all-gather(v) of the packed slices as an all-to-allv with one block per peer
-        std::vector<uint64_t> meta{woff, nw}, M((size_t)2 * W);
-        RC(comm->allgather_u64(meta.data(), 2, M.data(), st));
-        // every rank sends its slice to every rank; received blocks land in rank order,
-        // which is word-offset order (genome blocks / slices ascend with the rank)
-        std::vector<uint64_t> sb(W, nw * 4), rb(W);
-        uint64_t o = 0;
-        bool ordered = true;
-        for (int p = 0; p < W; ++p) {
-            rb[p] = M[(size_t)2 * p + 1] * 4;
-            ordered = ordered && M[(size_t)2 * p] == o;
-            o += M[(size_t)2 * p + 1];
-        }
-        if (!ordered) return comm_fail(comm, "packed slices are not in rank order");   // the same on every rank
-        // the send buffer is the slice repeated per peer (all-to-allv sends disjoint blocks)
-        rc = MUMS_OK;
-        for (int p = 0; p < W && rc == MUMS_OK; ++p)
-            if (nw && hipMemcpyAsync((uint32_t*)comm->rec.p + (size_t)p * nw, comm->packed.p, nw * 4,
-                                     hipMemcpyDeviceToDevice, st) != hipSuccess)
-                rc = MUMS_E_HIP;
-        AGREE(rc);
-        RC(comm->alltoallv(comm->rec.p, sb.data(), comm->packed_all.p, rb.data(), st));
-    }
+    if (!comm->packed_done) RC(gather_packed(ctx, comm, st));
     rc = hipStreamSynchronize(st) != hipSuccess ? MUMS_E_HIP : MUMS_OK;
     if (rc == MUMS_OK) rc = mums_shard_find(ctx, rows, nrows, (const uint32_t*)comm->packed_all.p);
     return agree(comm, rc, st);

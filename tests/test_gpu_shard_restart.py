@@ -1,8 +1,10 @@
 """GPU parity of MER_REPEAT_LIMIT restarts (MatchFinder.cpp:253-277) and FindMatchesFromPosition
-start points (MemHash.cpp:117-127) in the sharded mode (mums_shard_run, shard_comm.hip): the
-ranks' merged streams are gathered onto rank 0, which plans the restarts on the whole stream
-(restart_plan.h), fixes the std::sort order of the runs a start point falls into
-(MemorySML.cpp:54) and sends every rank its live records (mums_shard_restart_*).
+start points (MemHash.cpp:117-127) in the sharded mode (mums_shard_run, shard_comm.hip).  By
+default every rank plans on its own part of every SortedMerList (restart_plan.h's distributed
+PlanData, rank after rank with the running start points), the runs a start point falls into
+get their std::sort order (MemorySML.cpp:54) on rank g % world, and every rank compacts its
+own live records (mums_shard_restart_counts .. _finish).  MUMS_DEV_SHARD_RESTART=gather forces
+the fallback: the streams gathered onto rank 0, which plans on the whole stream.
 
 Ranks are threads of one process over the host-staged communicator (one GPU); genome blocks
 and position slices.  MatchList, collisions (summed over ranks), restarts and the offset log
@@ -17,7 +19,10 @@ from tests import repeat_inputs, tie_inputs
 pytestmark = pytest.mark.gpu
 
 
-def check(lm, oracle_mod, seqs, world, w=15, layout="blocks", start_points=None, table_size=40000):
+PATHS = {"local": 0, "gather": 0}   # restarts planned per path (reported by test_zz_path_counts)
+
+
+def check(lm, oracle_mod, seqs, world, w=15, layout="blocks", start_points=None, table_size=40000, info=None):
     if layout == "slices":   # world / G position slices per genome
         world = len(seqs) * (1 if world <= len(seqs) else 2)
     seed = oracle_mod.get_seed(w)
@@ -30,6 +35,15 @@ def check(lm, oracle_mod, seqs, world, w=15, layout="blocks", start_points=None,
             ml = sh.FindMatchesFromPosition(seqs, start_points)
         stats = sh.stats_per_rank
         offlog = sh.OffsetLog()
+        rinfo = sh.restart_info
+    if info is not None:
+        info.extend(rinfo)
+    paths = {i["path"] for i in rinfo}
+    assert len(paths) == 1, rinfo   # every rank took the same path
+    if 1 in paths:
+        PATHS["local"] += 1
+    if 2 in paths:
+        PATHS["gather"] += 1
     assert all(s["restarts"] == ref["restarts"] for s in stats), ([s["restarts"] for s in stats], ref["restarts"])
     assert np.array_equal(offlog, ref["offset_log"])
     assert len(ml) == len(ref_len), (len(ml), len(ref_len))
@@ -104,3 +118,38 @@ def test_start_point_count_must_match(gpu_lib, oracle_mod):
         with pytest.raises(gpu_lib.MumsError):
             sh.FindMatchesFromPosition(seqs, [5, 7])
         assert sh.rank_status == [gpu_lib.MUMS_E_INVALID] * 2
+
+
+@pytest.mark.parametrize("mode", ["local", "gather"])
+@pytest.mark.parametrize("layout", ["blocks", "slices"])
+def test_restart_memory_per_rank(gpu_lib, oracle_mod, monkeypatch, mode, layout):
+    """The default plan allocates O(the rank's records) on every rank (its SML parts, 8 B per
+    record, the live flags and their scan, 8 B per record, plus O(candidates) plan arrays); the
+    gathered fallback allocates the whole stream's SMLs (8 B per seed-mer of every genome) on
+    rank 0."""
+    if mode == "gather":
+        monkeypatch.setenv("MUMS_DEV_SHARD_RESTART", "gather")
+    seqs = repeat_inputs.n_gapped(G=3, n=200_000, gaps=((40_000, 3000), (120_000, 3000)), shift=500, seed=1)
+    info = []
+    ref = check(gpu_lib, oracle_mod, seqs, 4, layout=layout, info=info)
+    assert ref["restarts"] > 0
+    L = gpu_lib.getSeedLength(oracle_mod.get_seed(15))
+    N = sum(len(s) - L + 1 for s in seqs)
+    world = len(info)
+    if mode == "local":
+        assert all(i["path"] == 1 for i in info), info
+        for i in info:   # each rank: about 16 B x N / world (balanced key ranges) + small arrays
+            assert i["bytes"] < 20 * N / world + (4 << 20), (i, N)
+        assert info[0]["bytes"] < 8 * N, (info[0], N)
+    else:
+        assert all(i["path"] == 2 for i in info), info
+        assert info[0]["bytes"] >= 8 * N, (info[0], N)
+        assert all(i["bytes"] == 0 for i in info[1:]), info
+
+
+def test_zz_path_counts(gpu_lib):
+    """Report how many checks above planned locally and how many fell back (a key beyond a
+    rank's neighbours): the fallback must stay the exception."""
+    print("restart paths:", PATHS)
+    if PATHS["local"] + PATHS["gather"] >= 20:
+        assert PATHS["local"] >= PATHS["gather"], PATHS

@@ -101,3 +101,63 @@ def test_runs_across_buffer_boundaries(model, sp):
     seqs = repeat_inputs.n_gapped(G=4, n=90_000, gaps=((2_000, 25_000), (60_000, 10_022)), shift=1_300, seed=13)
     s = check(model, seqs, start_points=sp)
     assert s["oracle_restarts"] >= 1
+
+
+# ---- the sharded mode's plan on the ranks' own SML parts (mums_shard_restart_*) ----------
+DIST = {"cases": 0, "undecidable": 0}
+
+
+def check_dist(L, seqs, world, w=15, B=8, start_points=None):
+    """restart_plan.h's distributed PlanData, rank after rank, must give the whole-stream plan
+    (restart keys and start points of every phase) or flag the case undecidable."""
+    G = len(seqs)
+    arr = (ctypes.c_char_p * G)(*seqs)
+    lens = (ctypes.c_uint64 * G)(*[len(s) for s in seqs])
+    st = np.zeros(5, dtype=np.uint64)
+    sp = None if start_points is None else np.ascontiguousarray(start_points, dtype=np.uint64)
+    L.restart_model_dist.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_uint64),
+                                     ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    rc = L.restart_model_dist(G, arr, lens, oracle.get_seed(w), sp.ctypes.data if sp is not None else None, world, B,
+                              st.ctypes.data)
+    assert rc == 0
+    whole, dist, bad, equal, cands = (int(x) for x in st)
+    DIST["cases"] += 1
+    DIST["undecidable"] += bad
+    if not bad:
+        assert equal == 1, (whole, dist, cands)
+    return whole, bad
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_dist_n_gaps(model, world):
+    whole, bad = check_dist(model, repeat_inputs.n_gapped(G=3, n=200_000, gaps=((40_000, 3000), (120_000, 3000)),
+                                                          shift=500, seed=1), world)
+    assert whole > 0 and not bad
+
+
+@pytest.mark.parametrize("seed", [26, 95, 98, 99, 106] + list(range(0, 24)))
+def test_dist_mixed_repeats_fuzz(model, seed):
+    check_dist(model, repeat_inputs.mixed_repeats(seed), 2 + seed % 7)
+
+
+@pytest.mark.parametrize("sp", [None, [0, 0, 0, 0], [3, 9_999, 10_001, 40_000]])
+@pytest.mark.parametrize("world", [2, 5])
+def test_dist_buffer_boundaries(model, sp, world):
+    seqs = repeat_inputs.n_gapped(G=4, n=90_000, gaps=((2_000, 25_000), (60_000, 10_022)), shift=1_300, seed=13)
+    check_dist(model, seqs, world, start_points=sp)
+
+
+@pytest.mark.parametrize("tandem", [False, True])
+def test_dist_high_copy(model, tandem):
+    check_dist(model, repeat_inputs.high_copy(G=3, n=30_000, copies=2000, tandem=tandem), 4)
+
+
+def test_dist_w19_narrow_buckets(model):
+    check_dist(model, repeat_inputs.high_copy(G=4, n=30_000, copies=1500, unit=90, seed=21), 3, w=19, B=11)
+
+
+def test_dist_zz_mostly_decidable():
+    """The fallback (the gathered plan) stays the exception on these inputs."""
+    print("distributed plans:", DIST)
+    if DIST["cases"] >= 20:
+        assert DIST["undecidable"] * 4 <= DIST["cases"], DIST
