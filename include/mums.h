@@ -300,6 +300,21 @@ int  mums_shard_restart_ties(mums_ctx* ctx, const uint32_t* d_packed_all, const 
 int  mums_shard_restart_finish(mums_ctx* ctx, uint64_t restarts, const uint64_t* rkey, const uint64_t* rS,
                                const uint64_t* runs, uint64_t nruns, const uint32_t* d_pos, const uint64_t* vofs);
 int  mums_shard_restart_info(mums_ctx* ctx, uint64_t* info);
+/* Repeat tolerance in the sharded mode (MemHash.cpp:139-162: the first copies of a genome in
+ * SortedMerList order, so every run of equal keys in std::sort order, MemorySML.cpp:54), run
+ * by mums_shard_run after step 3 above:
+ *   mums_shard_tie_flags: this rank's pair flags of its SML parts (u32 per record: slot i of
+ *     genome g flags i, i + 1 equal), genome g's at d_out + gofs[g];
+ *   mums_shard_tie_replay (rank g % world): genome g's flags from every rank (nparts parts in
+ *     rank order at d_flags + flag_off[r], lens[r] slots) -> the std::sort order replayed on
+ *     the keys of the all-gathered packed genome -> ids (position in the genome, ~0 outside
+ *     every run) of part r at d_out + out_off[r];
+ *   mums_shard_tie_apply: this rank's records take the ids at d_ids + vofs[g] + SML slot. */
+int  mums_shard_tie_flags(mums_ctx* ctx, const uint64_t* gofs, uint32_t* d_out);
+int  mums_shard_tie_replay(mums_ctx* ctx, const uint32_t* d_packed_all, uint32_t genome, uint32_t nparts,
+                           const uint32_t* d_flags, const uint64_t* flag_off, const uint64_t* lens, uint32_t* d_out,
+                           const uint64_t* out_off);
+int  mums_shard_tie_apply(mums_ctx* ctx, const uint32_t* d_ids, const uint64_t* vofs);
 /* Accepted probes of the last seed stage, in AddHashEntry call order
  * (MemHash::EnumerateMatches -> AddHashEntry, MemHash.cpp:139-162, 209-251):
  * hash bucket ((offset % T) + T) % T and the smallest global seed-mer index of

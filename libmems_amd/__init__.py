@@ -103,7 +103,7 @@ EXPORTED_SYMBOLS = [
     "mums_shard_restart_plan", "mums_shard_restart_apply", "mums_comm_init_host", "mums_set_progress_log",
     "mums_progress_log_copy", "mums_shard_restart_counts", "mums_shard_restart_prepare", "mums_shard_restart_step",
     "mums_shard_restart_log", "mums_shard_restart_runs", "mums_shard_restart_ties", "mums_shard_restart_finish",
-    "mums_shard_restart_info",
+    "mums_shard_restart_info", "mums_shard_tie_flags", "mums_shard_tie_replay", "mums_shard_tie_apply",
 ]
 
 # mums_comm_ops (include/mums.h): the caller's transport as two host callbacks
@@ -565,6 +565,7 @@ class ShardedMemHash:
         self.comm_kind = comm
         self.table_size = table_size
         self.seed = 0
+        self.repeat_tol = 0
         self.seqs: List[bytes] = []
         self.ranks: List[MemHash] = []
         self.stats_per_rank: List[dict] = []
@@ -579,6 +580,11 @@ class ShardedMemHash:
 
     def SetSeed(self, seed: int) -> None:
         self.seed = seed
+
+    def SetRepeatTolerance(self, t: int) -> None:
+        """MemHash::SetRepeatTolerance (MemHash.h:125-131) on every rank: the first copies of a
+        genome follow its SortedMerList's std::sort order, replayed on rank g % world."""
+        self.repeat_tol = int(t)
 
     def AddSequence(self, seq) -> None:
         self.seqs.append(seq.encode() if isinstance(seq, str) else bytes(seq))
@@ -617,6 +623,7 @@ class ShardedMemHash:
             for r, (g, b0, b1) in enumerate(genome_slices([len(s) for s in self.seqs], L, self.world)):
                 mh = MemHash(self.devices[r])
                 mh.SetTableSize(self.table_size)
+                mh.SetRepeatTolerance(self.repeat_tol)
                 mh.SetSeed(seed)
                 mh.AddSequence(self.seqs[g][b0:min(len(self.seqs[g]), b1 + L - 1)] if b1 > b0 else b"")
                 mh._check(self._lib.mums_shard_slice(mh._ctx, G, lens, g, b0, b1))
@@ -626,6 +633,7 @@ class ShardedMemHash:
             cnt = base + (1 if r < rem else 0)
             mh = MemHash(dev)
             mh.SetTableSize(self.table_size)
+            mh.SetRepeatTolerance(self.repeat_tol)
             mh.SetSeed(self.seed)
             for s in self.seqs[g0:g0 + cnt]:
                 mh.AddSequence(s)

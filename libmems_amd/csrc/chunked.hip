@@ -270,6 +270,45 @@ __global__ void cr_dtie_write_kernel(CrStream s, GenomeTable gt, const uint64_t*
     }
 }
 
+// Repeat tolerance (every run of equal keys in std::sort order): every record of genome g in
+// a flagged run (the tie replay's scanned slot flags ts) takes the id at its SML slot, V[i]
+// (positions in the genome).  Ids move only inside genome g, so gscan stays valid.
+__global__ __launch_bounds__(kBlock) void cr_tie_all_kernel(CrStream s, GenomeTable gt,
+                                                            const uint32_t* __restrict__ gscan, uint64_t nblk, int g,
+                                                            const uint32_t* __restrict__ ts,
+                                                            const uint32_t* __restrict__ V, uint64_t* rec) {
+    cr_block_ranks(s, gt, blockIdx.x, gscan, nblk, [&](uint64_t j, int gg, uint64_t i) {
+        if (gg != g || ts[i + 1] == ts[i]) return;
+        rec[j] = (rec[j] & ~((1ull << s.ib) - 1)) | (gt.base[g] + V[i]);
+    });
+}
+
+// Sharded repeat tolerance: a rank's pair flags of its SML parts (slot i of genome g flags the
+// pair i, i + 1 of equal full keys; runs never straddle two ranks' key ranges), written at
+// out[gofs[g] + i], and the id rewrite from the replayed order: V[vofs[g] + i] (~0: a slot
+// outside every run keeps its id)
+__global__ __launch_bounds__(kBlock) void cr_pair_flags_kernel(const uint64_t* __restrict__ ck, int G,
+                                                               const uint64_t* __restrict__ lbase,
+                                                               const uint64_t* __restrict__ gofs,
+                                                               uint64_t n, uint32_t* __restrict__ out) {
+    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= n) return;
+    int g = 0;
+    for (int k = 1; k < G; ++k) g += (j >= lbase[k]) ? 1 : 0;
+    const uint64_t i = j - lbase[g];
+    out[gofs[g] + i] = (j + 1 < lbase[g + 1] && ck[j] == ck[j + 1]) ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(kBlock) void cr_tie_vals_kernel(CrStream s, GenomeTable gt,
+                                                             const uint32_t* __restrict__ gscan, uint64_t nblk,
+                                                             const uint64_t* __restrict__ vofs,
+                                                             const uint32_t* __restrict__ V, uint64_t* rec) {
+    cr_block_ranks(s, gt, blockIdx.x, gscan, nblk, [&](uint64_t j, int g, uint64_t i) {
+        const uint32_t v = V[vofs[g] + i];
+        if (v != 0xFFFFFFFFu) rec[j] = (rec[j] & ~((1ull << s.ib) - 1)) | (gt.base[g] + v);
+    });
+}
+
 // K[pos] = key of genome g's seed-mer pos (the tie replay's position order)
 __global__ __launch_bounds__(kBlock) void cr_kpos_kernel(CrStream s, GenomeTable gt, int g, uint64_t* __restrict__ K) {
     const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -395,6 +434,29 @@ hipError_t launch_cr_dtie_write(const CrStream& s, const GenomeTable& gt, const 
     if (nrun == 0) return hipSuccess;
     hipLaunchKernelGGL(cr_dtie_write_kernel, dim3((unsigned)((nrun + 63) / 64)), dim3(64), 0, st, s, gt, runs, nrun,
                        ck, lbase, goff, V, vofs, rec);
+    return hipGetLastError();
+}
+
+hipError_t launch_cr_tie_all(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, int g, const uint32_t* ts,
+                             const uint32_t* V, uint64_t* rec, hipStream_t st) {
+    const uint64_t nblk = cr_blocks(s.N);
+    if (nblk == 0) return hipSuccess;
+    hipLaunchKernelGGL(cr_tie_all_kernel, dim3((unsigned)nblk), dim3(kBlock), 0, st, s, gt, gscan, nblk, g, ts, V, rec);
+    return hipGetLastError();
+}
+
+hipError_t launch_cr_pair_flags(const uint64_t* ck, int G, const uint64_t* lbase, const uint64_t* gofs, uint64_t n,
+                                uint32_t* out, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(cr_pair_flags_kernel, cr_grid(n), dim3(kBlock), 0, st, ck, G, lbase, gofs, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_cr_tie_vals(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, const uint64_t* vofs,
+                              const uint32_t* V, uint64_t* rec, hipStream_t st) {
+    const uint64_t nblk = cr_blocks(s.N);
+    if (nblk == 0) return hipSuccess;
+    hipLaunchKernelGGL(cr_tie_vals_kernel, dim3((unsigned)nblk), dim3(kBlock), 0, st, s, gt, gscan, nblk, vofs, V, rec);
     return hipGetLastError();
 }
 

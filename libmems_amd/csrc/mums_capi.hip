@@ -137,6 +137,7 @@ struct mums_ctx {
     uint64_t ds_C = 0;                    // this rank's candidates (groups above MER_REPEAT_LIMIT)
     std::vector<uint64_t> ds_n, ds_off;   // SML indices [off, off + n) of every genome held here
     std::vector<uint64_t> ds_rkey, ds_rS; // this rank's restarts (last step)
+    bool ds_ties = false;                 // repeat tolerance: every run's ids rewritten (mums_shard_tie_apply)
     uint64_t rs_info[4] = {0, 0, 0, 0};   // mums_shard_restart_info
     bool ties_fixed = false;              // the stream holds every run of equal keys in std::sort order
     uint64_t tie_slots = 0;               // slots of the runs replayed by the last run (stats)
@@ -169,7 +170,8 @@ struct mums_ctx {
     uint32_t slice_genome = 0;
     uint64_t slice_begin = 0, slice_end = 0;
     int rec_ib = 32;          // index bits of the packed records (33: > 2^32 seed-mers)
-    bool merge_chunked = false;   // the last shard merge ran in key chunks (probe exports: last chunk only)
+    bool merge_chunked = false;   // the last shard merge ran in key chunks of < 2^30 records
+    bool shard_rows_built = false;   // chunked merge: every chunk's probe rows in rowsall (shard_chunk_rows)
 
     // state of the last run
     int stage_done = 0;
@@ -1534,9 +1536,6 @@ int prepare_shard(mums_ctx* ctx) {
     if (rc) return rc;
     if (ctx->enum_tol > 1)
         return fail(ctx, MUMS_E_UNSUPPORTED, "sharded mode: enumeration tolerance > 1 runs single-GPU only");
-    if (ctx->repeat_tol > 0)   // the first copies of a genome follow its whole SML's std::sort order
-        return fail(ctx, MUMS_E_UNSUPPORTED, "sharded mode: repeat tolerance > 0 runs single-GPU only (SortedMerList "
-                                             "tie order)");
     if (2 * ctx->w + 1 > 32 + kMaxMsdBits)
         return fail(ctx, MUMS_E_UNSUPPORTED, "sharded mode needs 2w+1 <= 43 (packed records)");
     GenomeTable& l = ctx->lgt;
@@ -2069,6 +2068,7 @@ int mums_length_filter(mums_ctx* ctx, uint64_t min_len) { return match_filter(ct
 
 extern "C++" {
 hipStream_t mums::ctx_stream(mums_ctx* ctx) { return ctx->stream; }
+uint32_t mums::ctx_repeat_tol(mums_ctx* ctx) { return ctx->repeat_tol; }
 int mums::ctx_device(mums_ctx* ctx) { return ctx->device; }
 int mums::ctx_table_genomes(mums_ctx* ctx, uint32_t* table_size, uint32_t* genomes) {
     if (check_ctx(ctx)) return MUMS_E_INVALID;
@@ -2291,16 +2291,132 @@ void shard_merge_stats(mums_ctx* ctx, uint64_t n) {
     ctx->st.ms_sort += rg;
     ctx->st.ms_keys = ctx->shard_keys_ms;
 }
+// The key chunks of a sharded merge above one onesweep merge (2^30 records): runs of
+// consecutive local buckets of < cap records each, in key order ({b0, b1} pairs over the
+// merge's nbuckets real buckets; bst: local bucket starts).  Empty when a bucket alone is
+// too big.
+uint64_t shard_chunk_cap() {
+    uint64_t cap = (1ull << 30) - 4096;
+    if (const char* e = getenv("MUMS_DEV_CHUNK_RECORDS")) cap = std::min<uint64_t>(cap, strtoull(e, nullptr, 10));
+    return cap;
+}
+std::vector<std::pair<uint32_t, uint32_t>> shard_key_chunks(const std::vector<uint32_t>& bst, uint32_t nbuckets,
+                                                            uint64_t cap) {
+    std::vector<std::pair<uint32_t, uint32_t>> out;
+    uint32_t b0 = 0;
+    while (b0 < nbuckets) {
+        uint32_t b1 = b0;
+        while (b1 < nbuckets && (uint64_t)bst[b1 + 1] - bst[b0] < cap) ++b1;
+        if (b1 == b0) return {};
+        out.push_back({b0, b1});
+        b0 = b1;
+    }
+    return out;
+}
+
+// The groups stage of every key chunk of a chunked sharded stream rec (local bucket starts
+// bst) in key order: the seed-stage counts over all chunks (ctx->P = their probes); rows:
+// every chunk's probe rows appended to ctx->rowsall (the sharded FindMatches' input).
+int shard_groups_chunked(mums_ctx* ctx, uint64_t* rec, const std::vector<uint32_t>& bst, const ProbeSpace& ps,
+                         bool rows, hipStream_t st) {
+    const int mb = ctx->shard_mb, G = ctx->gt.G;
+    const uint32_t nbk = 1u << mb;
+    const auto chunks = shard_key_chunks(bst, ctx->shard_kcount, shard_chunk_cap());
+    if (chunks.empty() && ctx->shard_kcount)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "one MSD bucket holds more than 2^30 records");
+    DevCounters* dc = ctx->counters.as<DevCounters>();
+    const MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, ctx->masked, ctx->seq_mask};
+    const size_t W = (size_t)(G + 1) * 8;
+    uint64_t P_total = 0, groups = 0;
+    ctx->fused_keys = false;
+    for (const auto& ch : chunks) {
+        const uint32_t b0 = ch.first, b1 = ch.second;
+        const uint64_t o = bst[b0], nc = (uint64_t)bst[b1] - o;
+        std::vector<uint32_t> sub(nbk + 1);
+        for (uint32_t b = 0; b <= nbk; ++b) sub[b] = b < b0 ? 0u : (b < b1 ? bst[b] - (uint32_t)o : (uint32_t)nc);
+        HIPCHK(hipMemcpyAsync(ctx->mstart.p, sub.data(), sub.size() * 4, hipMemcpyHostToDevice, st));
+        SegTile* tiles = ctx->tiles.as<SegTile>();
+        HIPCHK(build_seg_tiles_from_starts(ctx->mstart.as<uint32_t>(), mb, nc, tiles, &dc->ntiles, ctx->tmp.p, st));
+        const uint64_t ub = seg_tiles_upper(nc, mb);
+        int rc;
+        if (ctx->rec_ib == 33)
+            rc = groups_dispatch<RecViewT<33>>(ctx, RecViewT<33>{rec + o}, tiles, ub, mp, ps.probe_info,
+                                               ps.probe_bucket, ps.slot_info, ps.slot_bucket, st);
+        else
+            rc = groups_dispatch<RecView>(ctx, RecView{rec + o}, tiles, ub, mp, ps.probe_info, ps.probe_bucket,
+                                          ps.slot_info, ps.slot_bucket, st);
+        if (rc) return rc;
+        rc = finish_seeds(ctx, ps, st);
+        if (rc) return rc;
+        const uint64_t Pc = ctx->P;
+        if (rows && Pc) {
+            if (P_total + Pc >= (1ull << 32) - 64)
+                return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed probes on one rank");
+            if (ctx->rowsall.cap < (P_total + Pc + 1) * W) {   // grow, keeping the rows so far
+                DevBuf nb;
+                HIPCHK(nb.ensure((P_total + Pc + 1) * W * 5 / 4));
+                if (P_total) HIPCHK(hipMemcpyAsync(nb.p, ctx->rowsall.p, P_total * W, hipMemcpyDeviceToDevice, st));
+                HIPCHK(hipStreamSynchronize(st));
+                ctx->rowsall.release();
+                ctx->rowsall = nb;
+            }
+            int64_t* dst = ctx->rowsall.as<int64_t>() + P_total * (uint64_t)(G + 1);
+            if (ctx->rec_ib == 33) rc = materialize_dispatch<RecViewT<33>>(ctx, RecViewT<33>{rec + o}, mp, st, dst);
+            else rc = materialize_dispatch<RecView>(ctx, RecView{rec + o}, mp, st, dst);
+            if (rc) return rc;
+        }
+        P_total += Pc;
+        groups += ctx->hc.ngroups;
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    ctx->P = P_total;
+    ctx->st.probes = P_total;
+    ctx->st.groups = groups;
+    ctx->sorted_rec = rec;
+    return MUMS_OK;
+}
+
+// a chunked merge's probe rows for the sharded FindMatches (once per merge / restart)
+int shard_chunk_rows(mums_ctx* ctx, hipStream_t st) {
+    if (!ctx->merge_chunked || ctx->shard_rows_built) return MUMS_OK;
+    ProbeSpace ps{};
+    int rc = ensure_probe_space(ctx, ctx->shard_n, seg_tiles_upper(ctx->shard_n, ctx->shard_mb), &ps);
+    if (rc) return rc;
+    HIPCHK(hipMemsetAsync(ctx->counters.p, 0, sizeof(DevCounters), st));
+    rc = shard_groups_chunked(ctx, const_cast<uint64_t*>(ctx->sorted_rec), ctx->shard_bst, ps, true, st);
+    if (rc) return rc;
+    ctx->shard_rows_built = true;
+    return MUMS_OK;
+}
+
 // the groups stage again over the nl live records at dst (bucket starts bst, 2^shard_mb + 1):
 // the end of a sharded restart (mums_shard_restart_apply / _finish)
 int shard_regroup(mums_ctx* ctx, uint64_t* dst, uint64_t nl, const std::vector<uint32_t>& bst, const ProbeSpace& ps,
                   uint64_t restarts, const uint64_t* offset_log, hipStream_t st) {
     const int mb = ctx->shard_mb;
-    HIPCHK(hipMemcpyAsync(ctx->mstart.p, bst.data(), bst.size() * 4, hipMemcpyHostToDevice, st));
     ctx->sorted_buf ^= 1;
     ctx->sorted_rec = dst;
     DevCounters* dc = ctx->counters.as<DevCounters>();
     const uint64_t rep = ctx->hc.repeat_limit;
+    if (ctx->merge_chunked) {   // the live stream's key chunks (seed-stage counts; rows on export)
+        ctx->shard_bst = bst;
+        ctx->shard_n = nl;
+        ctx->shard_rows_built = false;
+        HIPCHK(hipMemsetAsync(dc, 0, sizeof(DevCounters), st));
+        const int rc = shard_groups_chunked(ctx, dst, bst, ps, false, st);
+        if (rc) return rc;
+        const uint64_t P = ctx->P, groups = ctx->st.groups;
+        ctx->hc.repeat_limit = rep;
+        ctx->restarts = restarts;
+        ctx->offset_log.assign(offset_log, offset_log + restarts * (uint64_t)ctx->gt.G);
+        ctx->shard_restart_pending = false;
+        shard_merge_stats(ctx, nl);
+        ctx->P = P;
+        ctx->st.probes = P;
+        ctx->st.groups = groups;
+        return MUMS_OK;
+    }
+    HIPCHK(hipMemcpyAsync(ctx->mstart.p, bst.data(), bst.size() * 4, hipMemcpyHostToDevice, st));
     SegTile* tiles = ctx->tiles.as<SegTile>();
     HIPCHK(build_seg_tiles_from_starts(ctx->mstart.as<uint32_t>(), mb, nl, tiles, &dc->ntiles, ctx->tmp.p, st));
     HIPCHK(hipMemsetAsync(&dc->repeat_limit, 0, 8, st));
@@ -2425,15 +2541,16 @@ int mums_shard_merge(mums_ctx* ctx, const uint64_t* d_records, uint32_t nsources
             groups += ctx->hc.ngroups;
             b0 = b1;
         }
+        // every chunk sorted in place with the same pass count: the whole range's stream
+        ctx->sorted_rec = ctx->sorted_buf ? ctx->recB.as<uint64_t>() : ctx->recA.as<uint64_t>();
     }
+    ctx->shard_rows_built = false;
     // a group above MER_REPEAT_LIMIT (or start points): the restart moves start points of
     // every later key, on every rank -> planned on the whole stream (mums_shard_restart_*)
     ctx->restarts = 0;
     ctx->offset_log.clear();
-    ctx->shard_restart_pending = ctx->hc.repeat_limit > 0 || have_start_points(ctx);
-    if (ctx->shard_restart_pending && ctx->merge_chunked)
-        return fail(ctx, MUMS_E_UNSUPPORTED, "sharded mode: a MER_REPEAT_LIMIT restart after a chunked merge (a key "
-                                             "range above 2^30 records)");
+    // (repeat tolerance: every run of equal keys in std::sort order, mums_shard_tie_*, first)
+    ctx->shard_restart_pending = ctx->hc.repeat_limit > 0 || have_start_points(ctx) || ctx->repeat_tol > 0;
     ctx->shard_mb = mb;
     ctx->shard_n = n;
     ctx->shard_kfirst = first_bucket;
@@ -2594,8 +2711,7 @@ int mums_shard_restart_apply(mums_ctx* ctx, const void* d_block, uint64_t restar
 int mums_shard_restart_counts(mums_ctx* ctx, uint64_t* info) {
     if (check_ctx(ctx) || !info) return MUMS_E_INVALID;
     if (!have_device()) return fail(ctx, MUMS_E_NODEVICE, "no HIP device");
-    if (!ctx->shard || ctx->stage_done < MUMS_STAGE_SEEDS || ctx->merge_chunked)
-        return fail(ctx, MUMS_E_INVALID, "no sharded (one-pass) merge run");
+    if (!ctx->shard || ctx->stage_done < MUMS_STAGE_SEEDS) return fail(ctx, MUMS_E_INVALID, "no sharded merge run");
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
     const GenomeTable& gt = ctx->gt;
@@ -2610,6 +2726,12 @@ int mums_shard_restart_counts(mums_ctx* ctx, uint64_t* info) {
         return fail(ctx, MUMS_E_UNSUPPORTED, "restart with the segment fix-up sort (MUMS_DEV_SEGFIX)");
     const char* force = getenv("MUMS_DEV_SHARD_RESTART");
     if (ctx->progress_on || (force && !strcmp(force, "gather"))) {   // LogProgress needs the whole stream
+        if (ctx->repeat_tol > 0)
+            return fail(ctx, MUMS_E_UNSUPPORTED, "sharded repeat tolerance: the gathered plan (LogProgress) does not "
+                                                 "order every run of equal keys");
+        if (ctx->merge_chunked)
+            return fail(ctx, MUMS_E_UNSUPPORTED, "sharded restart after a chunked merge: the gathered plan (LogProgress) "
+                                                 "needs one merge per rank");
         info[3 * Gu] = 1;
         return MUMS_OK;
     }
@@ -2659,7 +2781,8 @@ int mums_shard_restart_counts(mums_ctx* ctx, uint64_t* info) {
         lbase[g + 1] = lbase[g] + tot[g];
     }
     if (lbase[G] != n) return fail(ctx, MUMS_E_HIP, "restart: genome counts differ from the stream (internal error)");
-    HIPCHK(ctx->dsarr.ensure(8 * (8 * (Gu + 1) + 64)));
+    HIPCHK(ctx->dsarr.ensure(8 * (10 * (Gu + 1) + 64)));
+    ctx->ds_ties = false;
     uint64_t* d_lbase = ctx->dsarr.as<uint64_t>() + (Gu + 1);
     HIPCHK(hipMemcpyAsync(d_lbase, lbase.data(), (Gu + 1) * 8, hipMemcpyHostToDevice, st));
     HIPCHK(ctx->crall.ensure((n + 64) * 8));
@@ -2947,7 +3070,7 @@ int mums_shard_restart_finish(mums_ctx* ctx, uint64_t R, const uint64_t* rkey, c
             b->release();
         ctx->ds_ready = false;
     };
-    if (R == 0 && !have_start_points(ctx)) {   // nothing moves: the stream and its groups stand
+    if (R == 0 && !have_start_points(ctx) && !ctx->ds_ties) {   // nothing moves: the stream and its groups stand
         note_rs_bytes(ctx);
         done();
         ctx->restarts = 0;
@@ -3001,6 +3124,95 @@ int mums_shard_restart_finish(mums_ctx* ctx, uint64_t R, const uint64_t* rkey, c
     done();
     std::vector<uint64_t> log(rS, rS + R * Gu);
     return shard_regroup(ctx, dst, nl, bst, ps, R, log.data(), st);
+}
+
+// ---- sharded repeat tolerance (MemHash.cpp:139-162): the first copies of a genome in its
+// SortedMerList order need every run of equal keys in std::sort order (MemorySML.cpp:54).
+// The runs lie inside the ranks' SML parts; rank g % world replays genome g's sort from the
+// pair flags of every rank (rank order = SML order) and returns each rank its slots' ids.
+int mums_shard_tie_flags(mums_ctx* ctx, const uint64_t* gofs, uint32_t* d_out) {
+    if (check_ctx(ctx) || !gofs || (ctx->shard_n && !d_out)) return MUMS_E_INVALID;
+    if (!ctx->ds_ready) return fail(ctx, MUMS_E_INVALID, "mums_shard_restart_prepare first");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    const uint64_t W = (uint64_t)ctx->gt.G + 1;
+    uint64_t* d_gofs = ctx->dsarr.as<uint64_t>() + 8 * W;
+    HIPCHK(hipMemcpyAsync(d_gofs, gofs, (W - 1) * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(launch_cr_pair_flags(ctx->crall.as<uint64_t>(), ctx->gt.G, ds_arrays(ctx).lbase, d_gofs, ctx->shard_n, d_out,
+                                st));
+    HIPCHK(hipStreamSynchronize(st));   // (gofs is the caller's host array)
+    return MUMS_OK;
+}
+
+int mums_shard_tie_replay(mums_ctx* ctx, const uint32_t* d_packed_all, uint32_t genome, uint32_t nparts,
+                          const uint32_t* d_flags, const uint64_t* flag_off, const uint64_t* lens, uint32_t* d_out,
+                          const uint64_t* out_off) {
+    if (check_ctx(ctx) || !d_packed_all || !flag_off || !lens || !out_off || !d_flags || !d_out) return MUMS_E_INVALID;
+    if (!ctx->shard || ctx->stage_done < MUMS_STAGE_SEEDS) return fail(ctx, MUMS_E_INVALID, "no sharded merge run");
+    const GenomeTable& gt = ctx->gt;
+    if (genome >= (uint32_t)gt.G) return fail(ctx, MUMS_E_INVALID, "bad genome");
+    const uint64_t m = gt.m[genome];
+    uint64_t tot = 0;
+    for (uint32_t r = 0; r < nparts; ++r) tot += lens[r];
+    if (tot != m) return fail(ctx, MUMS_E_INVALID, "tie replay: the parts do not cover the SortedMerList");
+    if (m >= 0xFFFFFFF0ull) return fail(ctx, MUMS_E_UNSUPPORTED, "SortedMerList of more than 2^32 seed-mers");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    if (m == 0) return MUMS_OK;
+    if (tiebuf_ensure(ctx, tie_ws_bytes(m, 1)) != hipSuccess) {
+        (void)hipGetLastError();
+        HIPCHK(hipStreamSynchronize(st));
+        release_find_buffers(ctx);
+        if (tiebuf_ensure(ctx, tie_ws_bytes(m, 1)) != hipSuccess)
+            return fail(ctx, MUMS_E_NOMEM, "repeat tolerance: no device memory for the SortedMerList tie order");
+    }
+    const TieWs tw = tie_ws_layout(ctx->tiebuf.p, m, 1);
+    const uint64_t b0 = 0;
+    HIPCHK(tie_set_genomes(tw, &b0, &m, st));
+    HIPCHK(tie_clear_flags(tw, st));
+    uint64_t o = 0;
+    for (uint32_t r = 0; r < nparts; ++r) {   // the ranks' pair flags in SML order
+        if (lens[r]) HIPCHK(hipMemcpyAsync(tw.pf + o, d_flags + flag_off[r], lens[r] * 4, hipMemcpyDeviceToDevice, st));
+        o += lens[r];
+    }
+    uint64_t flagged = 0;
+    HIPCHK(tie_prepare(tw, &flagged, st));
+    uint32_t* ids = tw.Lpos;   // (free once the replay is done) ids at the flagged slots, ~0 elsewhere
+    if (flagged) {
+        HIPCHK(launch_keys_of_genome(ctx->ss, d_packed_all + gt.woff[genome], m, tw.K, st, false));
+        HIPCHK(tie_replay(tw, st));
+        HIPCHK(hipMemsetAsync(ids, 0xFF, m * 4, st));
+        HIPCHK(tie_slots_out(tw, ids, st));
+        ctx->tie_slots += flagged;
+    } else {
+        HIPCHK(hipMemsetAsync(ids, 0xFF, m * 4, st));
+    }
+    o = 0;
+    for (uint32_t r = 0; r < nparts; ++r) {
+        if (lens[r]) HIPCHK(hipMemcpyAsync(d_out + out_off[r], ids + o, lens[r] * 4, hipMemcpyDeviceToDevice, st));
+        o += lens[r];
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    return MUMS_OK;
+}
+
+int mums_shard_tie_apply(mums_ctx* ctx, const uint32_t* d_ids, const uint64_t* vofs) {
+    if (check_ctx(ctx) || !vofs || (ctx->shard_n && !d_ids)) return MUMS_E_INVALID;
+    if (!ctx->ds_ready) return fail(ctx, MUMS_E_INVALID, "mums_shard_restart_prepare first");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    const uint64_t W = (uint64_t)ctx->gt.G + 1;
+    uint64_t* d_vofs = ctx->dsarr.as<uint64_t>() + 9 * W;
+    HIPCHK(hipMemcpyAsync(d_vofs, vofs, (W - 1) * 8, hipMemcpyHostToDevice, st));
+    CrStream s{ctx->sorted_rec, ctx->crbuf.as<uint64_t>(), 1u << ctx->msd_bits, ctx->shard_n};
+    s.kb = (uint32_t)(2 * ctx->w + 1 - ctx->msd_bits);
+    s.ib = (uint32_t)ctx->rec_ib;
+    HIPCHK(launch_cr_tie_vals(s, ctx->gt, ctx->crcnt.as<uint32_t>(), d_vofs, d_ids,
+                              const_cast<uint64_t*>(ctx->sorted_rec), st));
+    HIPCHK(hipStreamSynchronize(st));
+    ctx->ds_ties = true;
+    ctx->ties_fixed = true;
+    return MUMS_OK;
 }
 
 int mums_shard_restart_info(mums_ctx* ctx, uint64_t* info) {
@@ -3061,8 +3273,6 @@ int shard_seeds_done(mums_ctx* ctx, bool pending_ok = false) {
     if (check_ctx(ctx)) return MUMS_E_INVALID;
     if (!ctx->shard) return fail(ctx, MUMS_E_INVALID, "not a sharded context (mums_shard_layout)");
     if (ctx->stage_done < MUMS_STAGE_SEEDS) return fail(ctx, MUMS_E_INVALID, "no sharded seed stage run");
-    if (ctx->merge_chunked)
-        return fail(ctx, MUMS_E_UNSUPPORTED, "sharded FindMatches after a chunked merge (> 2^30 records per rank)");
     if (ctx->shard_restart_pending && !pending_ok)
         return fail(ctx, MUMS_E_INVALID, "sharded restart pending (mums_shard_restart_plan / _apply)");
     return MUMS_OK;
@@ -3654,6 +3864,60 @@ int stream_restart(mums_ctx* ctx, uint64_t* srec, uint64_t* other, const std::ve
     return MUMS_OK;
 }
 
+// Repeat tolerance in the chunked mode (MemHash.cpp:139-162: the first copies of a genome
+// in SML order): every run of equal keys of the resident stream (buffer sbuf) takes the
+// std::sort order (smlsort.hip, all runs flagged), one genome after the other; the SMLs
+// (full keys, genome-major) are built in the other buffer.
+int chunked_tie_fix(mums_ctx* ctx, int sbuf, const std::vector<uint64_t>& dstart, hipStream_t st) {
+    uint64_t* srec = sbuf ? ctx->recB.as<uint64_t>() : ctx->recA.as<uint64_t>();
+    uint64_t* ck = sbuf ? ctx->recA.as<uint64_t>() : ctx->recB.as<uint64_t>();
+    const GenomeTable& gt = ctx->gt;
+    const uint64_t N = ctx->N, Gu = (uint64_t)gt.G;
+    const uint32_t nd = (uint32_t)dstart.size() - 1;
+    PhaseClock pc(st);
+    HIPCHK(ctx->crbuf.ensure((nd + 1) * 8 + 4096));
+    uint64_t* d_dstart = ctx->crbuf.as<uint64_t>();
+    HIPCHK(hipMemcpyAsync(d_dstart, dstart.data(), (nd + 1) * 8, hipMemcpyHostToDevice, st));
+    CrStream s{srec, d_dstart, nd, N};
+    s.kb = 31;
+    s.ib = 33;
+    const uint64_t nblk = cr_blocks(N);
+    HIPCHK(ctx->crcnt.ensure(Gu * (nblk + 1) * 4 + 256));
+    HIPCHK(ctx->tmp.ensure(std::max(ctx->tmp.cap, scan_tmp_bytes(nblk + 2))));
+    uint32_t* gscan = ctx->crcnt.as<uint32_t>();
+    HIPCHK(launch_cr_counts(s, gt, gscan, ctx->tmp.p, st));
+    HIPCHK(launch_cr_ck(s, gt, gscan, ck, st));
+    pc.mark("tie order: SMLs");
+    for (int g = 0; g < gt.G; ++g) {
+        const uint64_t m = gt.m[g];
+        if (m < 2) continue;
+        if (m >= 0xFFFFFFF0ull) return fail(ctx, MUMS_E_UNSUPPORTED, "SortedMerList of more than 2^32 seed-mers");
+        if (tiebuf_ensure(ctx, tie_ws_bytes(m, 1)) != hipSuccess) {
+            (void)hipGetLastError();
+            HIPCHK(hipStreamSynchronize(st));
+            release_find_buffers(ctx);
+            if (tiebuf_ensure(ctx, tie_ws_bytes(m, 1)) != hipSuccess)
+                return fail(ctx, MUMS_E_NOMEM, "repeat tolerance: no device memory for the SortedMerList tie order");
+        }
+        const TieWs tw = tie_ws_layout(ctx->tiebuf.p, m, 1);
+        const uint64_t b0 = 0;
+        HIPCHK(tie_set_genomes(tw, &b0, &m, st));
+        HIPCHK(tie_clear_flags(tw, st));
+        HIPCHK(tie_mark_all(tw, ck + gt.base[g], st));
+        uint64_t flagged = 0;
+        HIPCHK(tie_prepare(tw, &flagged, st));
+        if (!flagged) continue;
+        HIPCHK(launch_cr_kpos(s, gt, g, tw.K, st));
+        HIPCHK(tie_replay(tw, st));
+        HIPCHK(launch_cr_tie_all(s, gt, gscan, g, tw.ts, tw.V, srec, st));
+        ctx->tie_slots += flagged;
+        pc.mark("tie order of one genome (all runs)");
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    ctx->ties_fixed = true;
+    return MUMS_OK;
+}
+
 // The chunked mode's restart (all chunks resident and sorted in buffer sbuf): live chunks
 // into the other buffer (*live_rec), n_live[c], the chunks' bucket starts in ctx->rsbst.
 int chunked_restart(mums_ctx* ctx, int sbuf, const std::vector<uint64_t>& dstart, const std::vector<uint64_t>& cbase,
@@ -3690,9 +3954,10 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
     if (Bt < 1 || Bt > 12)
         return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed-mers (chunked mode) needs seed weight 16-21");
     if (N >= (1ull << 33)) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^33 seed-mers per context");
-    if (wants_tie_order(ctx))   // the first copies of a genome follow its SML's std::sort order (smlsort.hip)
-        return fail(ctx, MUMS_E_UNSUPPORTED, "repeat tolerance above 2^32 seed-mers (chunked mode): the SortedMerList "
-                                             "tie order is replayed in a single context only");
+    // repeat tolerance: the first copies of a genome follow its SML's std::sort order, replayed
+    // over the resident stream (chunked_tie_fix)
+    if (wants_tie_order(ctx) && getenv("MUMS_DEV_CHUNK_STREAM"))
+        return fail(ctx, MUMS_E_UNSUPPORTED, "repeat tolerance in the chunked mode needs the resident layout");
     ctx->packed_path = true;
     ctx->key64 = true;
     ctx->msd_bits = Bt;
@@ -3773,6 +4038,8 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
         resident = need + (uint64_t)(1ull << 30) < (uint64_t)fr + ctx->recA.cap + ctx->recB.cap + ctx->side.cap;
         if (S && !resident)
             return fail(ctx, MUMS_E_NOMEM, "seed weight 20-21 in the chunked mode: records and side bytes do not fit");
+        if (wants_tie_order(ctx) && !resident)
+            return fail(ctx, MUMS_E_NOMEM, "repeat tolerance in the chunked mode: the records do not fit resident");
     }
     if (resident) {
         HIPCHK(ctx->recA.ensure((N + 64) * 8));
@@ -3871,6 +4138,11 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
         // the tie workspace (135 GB at 2 x 3 Gbp; its hipMalloc alone is 3-4 s) stays allocated
         // between calls: a FindMatches call's rows and chain scratch live inside it (below)
         ctx->keep_tiebuf = stage < MUMS_STAGE_ALL ? 1 : 2;
+        ctx->ties_fixed = false;
+        if (wants_tie_order(ctx)) {
+            rc = chunked_tie_fix(ctx, sbuf, dstart, st);
+            if (rc) return rc;
+        }
         rc = chunked_restart(ctx, sbuf, dstart, cbase, nbc, nch, n_live, &live_rec, chunk_starts, st);
         ctx->keep_tiebuf = 0;
         if (rc) return rc;
@@ -4039,9 +4311,20 @@ int mums_shard_bucket_counts(mums_ctx* ctx, uint64_t* counts) {
     HIPCHK(hipSetDevice(ctx->device));
     const uint32_t Tb = ctx->table_size;
     std::fill(counts, counts + Tb, 0ull);
-    if (ctx->P == 0) return MUMS_OK;
     hipStream_t st = ctx->stream;
+    rc = shard_chunk_rows(ctx, st);
+    if (rc) return rc;
+    if (ctx->P == 0) return MUMS_OK;
     DevCounters* dc = ctx->counters.as<DevCounters>();
+    if (ctx->merge_chunked) {   // the buckets of every chunk's rows (key order kept per bucket)
+        int tbits = 1;
+        while (tbits < 32 && ((uint64_t)1 << tbits) < (uint64_t)Tb) ++tbits;
+        HIPCHK(ctx->rowtmp.ensure((ctx->P + 64) * 16 + 8192));
+        uint32_t* bkt = (uint32_t*)ctx->rowtmp.p;
+        HIPCHK(launch_row_buckets(ctx->rowsall.as<int64_t>(), ctx->P, ctx->gt.G, Tb, nullptr, 0, bkt, st));
+        rc = sort_row_keys(ctx, bkt, ctx->P, tbits, st);
+        if (rc) return rc;
+    }
     HIPCHK(ctx->bstart.ensure((size_t)Tb * 4));
     HIPCHK(ctx->bend.ensure((size_t)Tb * 4));
     HIPCHK(hipMemsetAsync(ctx->bstart.p, 0, (size_t)Tb * 4, st));
@@ -4073,19 +4356,24 @@ int mums_shard_probe_rows(mums_ctx* ctx, uint32_t nranks, const uint32_t* bounds
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
     MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, ctx->masked, ctx->seq_mask};
-    rc = materialize_seeds(ctx, mp, st);
-    if (rc) return rc;
+    const int64_t* src = ctx->rowsall.as<int64_t>();   // a chunked merge: every chunk's rows
+    if (!ctx->merge_chunked) {
+        rc = materialize_seeds(ctx, mp, st);
+        if (rc) return rc;
+        src = ctx->mprobe.as<int64_t>();
+    } else if (!ctx->shard_rows_built) {
+        return fail(ctx, MUMS_E_INVALID, "mums_shard_bucket_counts first (a chunked merge's rows)");
+    }
     const int G = ctx->gt.G;
     HIPCHK(ctx->rowtmp.ensure((P + 64) * 16 + 8192));
     HIPCHK(ctx->keybuf.ensure((size_t)(nranks + 1) * 8 + 64));
     HIPCHK(hipMemcpyAsync(ctx->keybuf.p, bounds, (size_t)(nranks + 1) * 4, hipMemcpyHostToDevice, st));
     uint32_t* dest = (uint32_t*)ctx->rowtmp.p;
-    HIPCHK(launch_row_buckets(ctx->mprobe.as<int64_t>(), P, G, ctx->table_size, ctx->keybuf.as<uint32_t>(), nranks,
-                              dest, st));
+    HIPCHK(launch_row_buckets(src, P, G, ctx->table_size, ctx->keybuf.as<uint32_t>(), nranks, dest, st));
     rc = sort_row_keys(ctx, dest, P, std::max(1, ceil_log2(nranks)), st);   // stable: key order per rank
     if (rc) return rc;
     const uint32_t* perm = ctx->sorted_ids;
-    HIPCHK(launch_gather_rows(ctx->mprobe.as<int64_t>(), perm, P, G, d_rows, st));
+    HIPCHK(launch_gather_rows(src, perm, P, G, d_rows, st));
     // rows per destination rank = run lengths of the sorted destinations
     std::vector<uint32_t> sd(P);
     HIPCHK(hipMemcpyAsync(sd.data(), ctx->sorted_buckets, P * 4, hipMemcpyDeviceToHost, st));

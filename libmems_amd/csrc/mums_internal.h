@@ -259,6 +259,7 @@ namespace mums {
 hipStream_t ctx_stream(mums_ctx* ctx);
 int ctx_device(mums_ctx* ctx);
 int ctx_table_genomes(mums_ctx* ctx, uint32_t* table_size, uint32_t* genomes);
+uint32_t ctx_repeat_tol(mums_ctx* ctx);
 
 // overlaps.hip: EliminateOverlaps (Aligner.cpp:62-176) on a device MatchList
 struct EoWork {
@@ -424,6 +425,16 @@ hipError_t launch_cr_cands(const CrStream& s, uint64_t* list, unsigned long long
 hipError_t launch_cr_runs(const uint64_t* ck, const GenomeTable& gt, const uint64_t* sp, uint64_t rows, uint64_t* runs,
                           unsigned long long* nr, uint64_t cap, hipStream_t st);
 hipError_t launch_cr_kpos(const CrStream& s, const GenomeTable& gt, int g, uint64_t* K, hipStream_t st);
+// repeat tolerance: genome g's records in flagged runs (tie replay slot flags ts, ids V) take
+// the std::sort order's ids
+// sharded repeat tolerance: pair flags of a rank's SML parts at out[gofs[g] + i]; ids from
+// V[vofs[g] + i] (~0 keeps the id)
+hipError_t launch_cr_pair_flags(const uint64_t* ck, int G, const uint64_t* lbase, const uint64_t* gofs, uint64_t n,
+                                uint32_t* out, hipStream_t st);
+hipError_t launch_cr_tie_vals(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, const uint64_t* vofs,
+                              const uint32_t* V, uint64_t* rec, hipStream_t st);
+hipError_t launch_cr_tie_all(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, int g, const uint32_t* ts,
+                             const uint32_t* V, uint64_t* rec, hipStream_t st);
 // a sharded rank's part of every SML (global indices [goff[g], goff[g] + gn[g]) at ck[lbase[g] ..]):
 // straddled runs {g, lo, hi} (global indices) of the start points sp (rows x G), and the id
 // rewrite of its runs from V[vofs[q] ..]

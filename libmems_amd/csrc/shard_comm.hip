@@ -358,7 +358,13 @@ int shard_restart_local(mums_ctx* ctx, mums_comm* comm, hipStream_t st, bool* do
         }
         if (dbg) fprintf(stderr, "rank %d: plan step of rank %d: %lu restarts, undecidable %lu\n", R, r,
                          (unsigned long)m[1], (unsigned long)m[2]);
-        if (m[2]) return MUMS_OK;   // undecidable on rank r: the gathered plan (nothing changed yet)
+        if (m[2]) {   // undecidable on rank r: the gathered plan (nothing changed yet)
+            if (mums::ctx_repeat_tol(ctx) > 0) {   // (which does not order every run of equal keys)
+                comm->err = "sharded repeat tolerance: a restart plan needs keys beyond a rank's neighbours";
+                return MUMS_E_UNSUPPORTED;
+            }
+            return MUMS_OK;
+        }
         Rn[r] = m[1];
         std::copy(m + 3, m + 3 + Gu, S.begin());
     }
@@ -384,11 +390,53 @@ int shard_restart_local(mums_ctx* ctx, mums_comm* comm, hipStream_t st, bool* do
             }
         }
     }
+    // repeat tolerance: every run of equal keys in std::sort order.  Pair flags go to rank
+    // g % W (blocks in rank order = SML order), which replays genome g's sort and returns each
+    // rank the ids of its slots in the same layout.
+    const bool rtol = mums::ctx_repeat_tol(ctx) > 0;
+    if (rtol) {
+        auto part = [&](int r, uint32_t g) { return ALL[(size_t)r * row + g]; };
+        std::vector<uint64_t> gofs(Gu, 0), sb(W, 0), rb(W, 0);
+        uint64_t o = 0;
+        for (int p = 0; p < W; ++p)   // send: destination-major, genomes ascending
+            for (uint32_t g = (uint32_t)p; g < G; g += (uint32_t)W) {
+                gofs[g] = o;
+                o += part(R, g);
+                sb[p] += 4 * part(R, g);
+            }
+        const uint64_t nloc = o;
+        std::vector<std::vector<uint64_t>> foff(G, std::vector<uint64_t>(W, 0)), lens(G, std::vector<uint64_t>(W, 0));
+        uint64_t ro = 0;
+        for (int r = 0; r < W; ++r)   // receive: source-major, this rank's genomes ascending
+            for (uint32_t g = (uint32_t)R; g < G; g += (uint32_t)W) {
+                foff[g][r] = ro;
+                lens[g][r] = part(r, g);
+                ro += part(r, g);
+                rb[r] += 4 * part(r, g);
+            }
+        AGREE(comm->rows.ensure(nloc * 4 + 8) || comm->rrows.ensure(ro * 4 + 8) || comm->recv.ensure(ro * 4 + 8)
+                  ? MUMS_E_NOMEM : MUMS_OK);
+        AGREE(mums_shard_tie_flags(ctx, gofs.data(), (uint32_t*)comm->rows.p));
+        RC(comm->alltoallv(comm->rows.p, sb.data(), comm->rrows.p, rb.data(), st));
+        RC(gather_packed(ctx, comm, st));
+        rc = hipStreamSynchronize(st) != hipSuccess ? MUMS_E_HIP : MUMS_OK;
+        for (uint32_t g = (uint32_t)R; g < G && rc == MUMS_OK; g += (uint32_t)W)
+            rc = mums_shard_tie_replay(ctx, (const uint32_t*)comm->packed_all.p, g, (uint32_t)W,
+                                       (const uint32_t*)comm->rrows.p, foff[g].data(), lens[g].data(),
+                                       (uint32_t*)comm->recv.p, foff[g].data());
+        AGREE(rc);
+        RC(comm->alltoallv(comm->recv.p, rb.data(), comm->rows.p, sb.data(), st));
+        rc = hipStreamSynchronize(st) != hipSuccess ? MUMS_E_HIP : MUMS_OK;
+        if (rc == MUMS_OK) rc = mums_shard_tie_apply(ctx, (const uint32_t*)comm->rows.p, gofs.data());
+        AGREE(rc);
+        if (dbg) fprintf(stderr, "rank %d: every run of equal keys in std::sort order\n", R);
+    }
     // the runs of equal keys the start points of every phase fall into, on their owner ranks
+    // (all of them are in order already under repeat tolerance)
     const uint64_t cap = 3 * (Rt + 1) * Gu;
     std::vector<uint64_t> runs(cap + 3, 0);
     uint64_t nr = 0;
-    AGREE(mums_shard_restart_runs(ctx, Rt, rkey.data(), rS.data(), runs.data(), cap, &nr));
+    if (!rtol) AGREE(mums_shard_restart_runs(ctx, Rt, rkey.data(), rS.data(), runs.data(), cap, &nr));
     std::vector<uint64_t> NR(W);
     RC(comm->allgather_u64(&nr, 1, NR.data(), st));
     if (dbg) fprintf(stderr, "rank %d: %lu restarts in all, %lu straddled runs here\n", R, (unsigned long)Rt, (unsigned long)nr);

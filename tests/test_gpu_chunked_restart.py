@@ -155,3 +155,51 @@ def test_tie_workspace_kept_across_seed_stage_calls(gpu_lib, oracle_mod, force_c
             assert (ml.lengths == ref_len).all() and (ml.starts == ref_starts).all()
         mh.FindStage(gpu_lib.STAGE_SEEDS)
         assert (mh.FindMatches().starts == ref_starts).all()
+
+
+# repeat tolerance in the chunked mode (MemHash.cpp:139-162): the first copies of a genome in
+# SortedMerList order, i.e. every run of equal keys in std::sort order (chunked_tie_fix)
+RTOL_CASES = {k: v for k, v in tie_inputs.CASES.items()
+              if v[1].get("repeat_tol", 0) > 0 and v[1].get("enum_tol", 1) == 1}
+
+
+@pytest.mark.parametrize("name", sorted(RTOL_CASES))
+@pytest.mark.parametrize("chunks", [3, 8])
+def test_repeat_tolerance_chunked(gpu_lib, oracle_mod, force_chunks, name, chunks):
+    gen, opts = RTOL_CASES[name]
+    seqs = gen()
+    w = max(opts.get("w", 15), 17)   # the chunked mode's weights: 2w + 1 > 32
+    seed = oracle_mod.get_seed(w)
+    with oracle_mod.sml_tie_rule("std"):
+        ref_len, ref_starts, ref = oracle_mod.find_matches(seqs, seed, repeat_tol=opts["repeat_tol"])
+    force_chunks(max(sum(len(s) for s in seqs) // chunks, 4096))
+    with gpu_lib.MemHash(0) as mh:
+        mh.SetSeed(seed)
+        mh.SetRepeatTolerance(opts["repeat_tol"])
+        ml = mh.FindMatches(seqs)
+        st = mh.stats()
+    assert st["chunks"] >= 2
+    assert len(ml) == len(ref_len), (len(ml), len(ref_len))
+    assert (ml.lengths == ref_len).all() and (ml.starts == ref_starts).all()
+    assert st["collision_count"] == ref["collision_count"]
+    assert st["restarts"] == ref["restarts"]
+
+
+@pytest.mark.parametrize("rtol", [1, 3])
+def test_repeat_tolerance_chunked_with_restarts(gpu_lib, oracle_mod, force_chunks, rtol):
+    seqs = repeat_inputs.n_gapped(G=3, n=200_000, gaps=((40_000, 3000), (120_000, 3000)), shift=500, seed=1)
+    seed = oracle_mod.get_seed(17)
+    with oracle_mod.sml_tie_rule("std"):
+        ref_len, ref_starts, ref = oracle_mod.find_matches(seqs, seed, repeat_tol=rtol)
+    assert ref["restarts"] > 0
+    force_chunks(max(sum(len(s) for s in seqs) // 4, 4096))
+    with gpu_lib.MemHash(0) as mh:
+        mh.SetSeed(seed)
+        mh.SetRepeatTolerance(rtol)
+        ml = mh.FindMatches(seqs)
+        st = mh.stats()
+        offlog = mh.OffsetLog()
+    assert st["chunks"] >= 2
+    assert (ml.lengths == ref_len).all() and (ml.starts == ref_starts).all() and len(ml) == len(ref_len)
+    assert st["restarts"] == ref["restarts"] and np.array_equal(offlog, ref["offset_log"])
+    assert st["collision_count"] == ref["collision_count"]

@@ -52,13 +52,13 @@ def test_shard_run_position_slices(gpu_lib, oracle_mod, G, n, w, p, world, table
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_shard_run_failure_is_collective(gpu_lib, oracle_mod, world, monkeypatch):
-    """A rank whose local step fails (here: mums_shard_merge refusing a MER_REPEAT_LIMIT
-    restart after a chunked merge -- forced small -- on the rank owning the repeat group's
-    key range only) must not leave the other ranks blocked in the next collective: every
-    rank returns the same status."""
+    """A rank whose local step fails (here: mums_shard_merge refusing a key chunk, forced
+    small, that one MSD bucket overfills -- on the rank owning the repeat group's bucket only)
+    must not leave the other ranks blocked in the next collective: every rank returns the
+    same status."""
     from tests import repeat_inputs
     seqs = repeat_inputs.high_copy(G=3, n=60_000, copies=2000, tandem=False, seed=2)
-    monkeypatch.setenv("MUMS_DEV_CHUNK_RECORDS", "30000")
+    monkeypatch.setenv("MUMS_DEV_CHUNK_RECORDS", "3000")
     with gpu_lib.ShardedMemHash([0] * world, comm="local") as sh:
         sh.SetSeed(oracle_mod.get_seed(15))
         with pytest.raises(gpu_lib.MumsError):

@@ -22,13 +22,17 @@ pytestmark = pytest.mark.gpu
 PATHS = {"local": 0, "gather": 0}   # restarts planned per path (reported by test_zz_path_counts)
 
 
-def check(lm, oracle_mod, seqs, world, w=15, layout="blocks", start_points=None, table_size=40000, info=None):
+def check(lm, oracle_mod, seqs, world, w=15, layout="blocks", start_points=None, table_size=40000, info=None,
+          repeat_tol=0):
     if layout == "slices":   # world / G position slices per genome
         world = len(seqs) * (1 if world <= len(seqs) else 2)
     seed = oracle_mod.get_seed(w)
-    ref_len, ref_starts, ref = oracle_mod.find_matches(seqs, seed, start_points=start_points, table_size=table_size)
+    with oracle_mod.sml_tie_rule("std"):
+        ref_len, ref_starts, ref = oracle_mod.find_matches(seqs, seed, start_points=start_points,
+                                                           table_size=table_size, repeat_tol=repeat_tol)
     with lm.ShardedMemHash([0] * world, comm="local", layout=layout, table_size=table_size) as sh:
         sh.SetSeed(seed)
+        sh.SetRepeatTolerance(repeat_tol)
         if start_points is None:
             ml = sh.FindMatches(seqs)
         else:
@@ -153,3 +157,57 @@ def test_zz_path_counts(gpu_lib):
     print("restart paths:", PATHS)
     if PATHS["local"] + PATHS["gather"] >= 20:
         assert PATHS["local"] >= PATHS["gather"], PATHS
+
+
+# key ranges above one onesweep merge (2^30 records per rank: config 5 on 2 or 4 GPUs), forced
+# small: mums_shard_merge merges the range in key chunks; the restart plans on the whole local
+# stream, the live records are grouped chunk by chunk, and FindMatches takes every chunk's rows
+@pytest.mark.parametrize("world,layout", [(2, "blocks"), (3, "blocks"), (2, "slices")])
+def test_chunked_merge_restarts(gpu_lib, oracle_mod, monkeypatch, world, layout):
+    seqs = repeat_inputs.n_gapped(G=3, n=200_000, gaps=((40_000, 3000), (120_000, 3000)), shift=500, seed=1)
+    monkeypatch.setenv("MUMS_DEV_CHUNK_RECORDS", str(sum(len(s) for s in seqs) // (3 * world * 2)))
+    ref = check(gpu_lib, oracle_mod, seqs, world, layout=layout)
+    assert ref["restarts"] > 0
+
+
+@pytest.mark.parametrize("sp", [[1000, 25_000, 7], [3, 9_999, 10_001, 40_000]])
+def test_chunked_merge_start_points(gpu_lib, oracle_mod, monkeypatch, sp):
+    seqs = repeat_inputs.n_gapped(G=len(sp), n=90_000, gaps=((2_000, 25_000), (60_000, 4_000)), shift=1_300,
+                                  seed=31)
+    monkeypatch.setenv("MUMS_DEV_CHUNK_RECORDS", str(sum(len(s) for s in seqs) // 8))
+    check(gpu_lib, oracle_mod, seqs, 2, start_points=sp)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_chunked_merge_findmatches(gpu_lib, oracle_mod, monkeypatch, world):
+    seqs = oracle_mod.generate(4, 150_000, 0.02, 71)
+    monkeypatch.setenv("MUMS_DEV_CHUNK_RECORDS", str(sum(len(s) for s in seqs) // (world * 4)))
+    check(gpu_lib, oracle_mod, seqs, world, w=17)
+
+
+# repeat tolerance (MemHash.cpp:139-162) over the ranks: every run of equal keys in std::sort
+# order (mums_shard_tie_*), with and without restarts, one-pass and chunked merges
+RTOL_CASES = {k: v for k, v in tie_inputs.CASES.items()
+              if v[1].get("repeat_tol", 0) > 0 and v[1].get("enum_tol", 1) == 1}
+
+
+@pytest.mark.parametrize("name", sorted(RTOL_CASES))
+@pytest.mark.parametrize("world,layout", [(2, "blocks"), (3, "blocks"), (2, "slices")])
+def test_repeat_tolerance(gpu_lib, oracle_mod, name, world, layout):
+    gen, opts = RTOL_CASES[name]
+    check(gpu_lib, oracle_mod, gen(), world, w=opts.get("w", 15), layout=layout, repeat_tol=opts["repeat_tol"])
+
+
+@pytest.mark.parametrize("rtol", [1, 2])
+@pytest.mark.parametrize("world,layout", [(2, "blocks"), (4, "blocks"), (3, "slices")])
+def test_repeat_tolerance_with_restarts(gpu_lib, oracle_mod, rtol, world, layout):
+    seqs = repeat_inputs.n_gapped(G=3, n=200_000, gaps=((40_000, 3000), (120_000, 3000)), shift=500, seed=1)
+    ref = check(gpu_lib, oracle_mod, seqs, world, layout=layout, repeat_tol=rtol)
+    assert ref["restarts"] > 0
+
+
+@pytest.mark.parametrize("rtol", [1, 3])
+def test_repeat_tolerance_chunked_merge(gpu_lib, oracle_mod, monkeypatch, rtol):
+    seqs = repeat_inputs.n_gapped(G=3, n=200_000, gaps=((40_000, 3000), (120_000, 3000)), shift=500, seed=1)
+    monkeypatch.setenv("MUMS_DEV_CHUNK_RECORDS", str(sum(len(s) for s in seqs) // 12))
+    check(gpu_lib, oracle_mod, seqs, 2, repeat_tol=rtol)
