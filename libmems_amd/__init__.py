@@ -197,6 +197,21 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mums_comm_last_error.restype = ctypes.c_char_p
     lib.mums_shard_key_ranges.argtypes = [vp, u32, u32, vp, vp]
     lib.mums_shard_run.argtypes = [vp, vp, ctypes.c_int]
+    lib.mums_shard_restart_pending.argtypes = [vp, vp]
+    lib.mums_shard_stream.argtypes = [vp, vp, vp]
+    lib.mums_shard_restart_plan.argtypes = [vp, vp, u32, vp, vp, vp, vp, u64, vp]
+    lib.mums_shard_restart_apply.argtypes = [vp, vp, u64, vp]
+    lib.mums_shard_restart_counts.argtypes = [vp, vp]
+    lib.mums_shard_restart_prepare.argtypes = [vp, u32, u32, vp, vp]
+    lib.mums_shard_restart_step.argtypes = [vp, vp, vp, vp]
+    lib.mums_shard_restart_log.argtypes = [vp, vp, vp]
+    lib.mums_shard_restart_runs.argtypes = [vp, u64, vp, vp, vp, u64, vp]
+    lib.mums_shard_restart_ties.argtypes = [vp, vp, vp, u64, vp, vp]
+    lib.mums_shard_restart_finish.argtypes = [vp, u64, vp, vp, vp, u64, vp, vp]
+    lib.mums_shard_restart_info.argtypes = [vp, vp]
+    lib.mums_shard_tie_flags.argtypes = [vp, vp, vp]
+    lib.mums_shard_tie_replay.argtypes = [vp, vp, u32, u32, vp, vp, vp, vp, vp]
+    lib.mums_shard_tie_apply.argtypes = [vp, vp, vp]
     lib.mums_set_match_log.argtypes = [vp, i32]
     lib.mums_set_progress_log.argtypes = [vp, i32]
     lib.mums_progress_log_copy.argtypes = [vp, ctypes.c_char_p, u64, ctypes.POINTER(u64)]

@@ -2854,6 +2854,15 @@ DsPlan ds_plan(mums_ctx* ctx, uint64_t cap) {
 size_t ds_plan_bytes(uint64_t cap, uint64_t Gu) {
     return 8 * (3 * cap * Gu + (cap + 1) + 4 + Gu + 1 + (sizeof(restart::PlanOut) + 7) / 8 + 1 + cap + cap * Gu) + 4096;
 }
+// word offset of genome g in the all-gathered packed genomes (layout_packed over every genome;
+// the context's own packed array holds only its genomes)
+uint64_t all_woff(const GenomeTable& gt, int g) {
+    GenomeTable t = gt;
+    uint64_t words = 0;
+    (void)layout_packed(t, &words);
+    return t.woff[g];
+}
+
 // the restart's own device buffers (mums_shard_restart_info; the tie replay's workspace, O(the
 // genome) on the rank replaying it, is not counted)
 void note_rs_bytes(mums_ctx* ctx) {
@@ -3035,7 +3044,7 @@ int mums_shard_restart_ties(mums_ctx* ctx, const uint32_t* d_packed_all, const u
         uint64_t flagged = 0;
         HIPCHK(tie_prepare(tw, &flagged, st));
         if (flagged) {
-            HIPCHK(launch_keys_of_genome(ctx->ss, d_packed_all + gt.woff[g], m, tw.K, st, false));
+            HIPCHK(launch_keys_of_genome(ctx->ss, d_packed_all + all_woff(gt, g), m, tw.K, st, false));
             HIPCHK(tie_replay(tw, st));
             ctx->tie_slots += flagged;
         }
@@ -3179,7 +3188,7 @@ int mums_shard_tie_replay(mums_ctx* ctx, const uint32_t* d_packed_all, uint32_t 
     HIPCHK(tie_prepare(tw, &flagged, st));
     uint32_t* ids = tw.Lpos;   // (free once the replay is done) ids at the flagged slots, ~0 elsewhere
     if (flagged) {
-        HIPCHK(launch_keys_of_genome(ctx->ss, d_packed_all + gt.woff[genome], m, tw.K, st, false));
+        HIPCHK(launch_keys_of_genome(ctx->ss, d_packed_all + all_woff(gt, (int)genome), m, tw.K, st, false));
         HIPCHK(tie_replay(tw, st));
         HIPCHK(hipMemsetAsync(ids, 0xFF, m * 4, st));
         HIPCHK(tie_slots_out(tw, ids, st));

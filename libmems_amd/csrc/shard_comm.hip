@@ -439,7 +439,13 @@ int shard_restart_local(mums_ctx* ctx, mums_comm* comm, hipStream_t st, bool* do
     if (!rtol) AGREE(mums_shard_restart_runs(ctx, Rt, rkey.data(), rS.data(), runs.data(), cap, &nr));
     std::vector<uint64_t> NR(W);
     RC(comm->allgather_u64(&nr, 1, NR.data(), st));
-    if (dbg) fprintf(stderr, "rank %d: %lu restarts in all, %lu straddled runs here\n", R, (unsigned long)Rt, (unsigned long)nr);
+    if (dbg) {
+        fprintf(stderr, "rank %d: %lu restarts in all, %lu straddled runs here:", R, (unsigned long)Rt, (unsigned long)nr);
+        for (uint64_t q = 0; q < nr && q < 8; ++q)
+            fprintf(stderr, " {%lu %lu %lu}", (unsigned long)runs[3 * q], (unsigned long)runs[3 * q + 1],
+                    (unsigned long)runs[3 * q + 2]);
+        fprintf(stderr, "\n");
+    }
     uint64_t NRmax = 0, NRt = 0;
     for (int r = 0; r < W; ++r) {
         NRmax = std::max(NRmax, NR[r]);

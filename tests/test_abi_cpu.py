@@ -47,3 +47,10 @@ def test_null_context_is_rejected(gpu_lib):
     assert lib.mums_find(None) == -1
     assert lib.mums_set_seed(None, 0x7AC9AF) == -1
     assert lib.mums_ctx_create(0, None) == -1
+
+
+def test_every_entry_point_has_argtypes(gpu_lib):
+    """ctypes passes undeclared arguments as C int: a context pointer would be truncated."""
+    lib = gpu_lib.load_library()
+    missing = [s for s in gpu_lib.EXPORTED_SYMBOLS if s != "mums_abi_version" and getattr(lib, s).argtypes is None]
+    assert not missing, missing
