@@ -301,9 +301,22 @@ public:
     ShardedMemHash& operator=(const ShardedMemHash&) = delete;
     void SetSeed(uint64_t pattern) { seed_ = pattern; }
     void SetTableSize(uint32_t n) { table_size_ = n; }
+    // MemHash::SetRepeatTolerance (MemHash.h:125-131) on every rank
+    void SetRepeatTolerance(uint32_t t) { repeat_tol_ = t; }
     bool AddSequence(const std::string& seq) {
         seqs_.push_back(seq);
         return true;
+    }
+    // MemHash::FindMatchesFromPosition (MemHash.cpp:117-127): all G start points on every rank
+    void FindMatchesFromPosition(MatchList& ml, const std::vector<uint64_t>& start_points) {
+        start_points_ = start_points;
+        try {
+            FindMatches(ml);
+        } catch (...) {
+            start_points_.clear();
+            throw;
+        }
+        start_points_.clear();
     }
     void FindMatches(MatchList& ml) {
         const size_t W = devices_.size(), G = seqs_.size();
@@ -324,6 +337,7 @@ public:
                 const uint64_t b0 = cut(j), b1 = std::max(b0, cut(j + 1));
                 auto mh = std::make_unique<MemHash>(devices_[r]);
                 mh->SetTableSize(table_size_);
+                mh->SetRepeatTolerance(repeat_tol_);
                 mh->SetSeed(seed);
                 mh->AddSequence(b1 > b0 ? seqs_[g].substr(b0, std::min<uint64_t>(lens[g], b1 + L - 1) - b0) : "");
                 if (mums_shard_slice(mh->handle(), (uint32_t)G, lens.data(), (uint32_t)g, b0, b1) != MUMS_OK)
@@ -336,6 +350,7 @@ public:
             const size_t cnt = G / W + (r < G % W ? 1 : 0);
             auto mh = std::make_unique<MemHash>(devices_[r]);
             mh->SetTableSize(table_size_);
+            mh->SetRepeatTolerance(repeat_tol_);
             mh->SetSeed(seed_);
             for (size_t g = g0; g < g0 + cnt; ++g) mh->AddSequence(seqs_[g]);
             if (mums_shard_layout(mh->handle(), (uint32_t)G, (uint32_t)g0, lens.data()) != MUMS_OK)
@@ -343,6 +358,10 @@ public:
             ranks_.push_back(std::move(mh));
             g0 += cnt;
         }
+        if (!start_points_.empty())
+            for (auto& mh : ranks_)
+                if (mums_set_start_points(mh->handle(), start_points_.data(), (uint32_t)start_points_.size()) != MUMS_OK)
+                    throw InvalidData(mums_last_error(mh->handle()));
         std::vector<int> rc(W, MUMS_OK);
         std::vector<std::thread> th;
         for (size_t r = 0; r < W; ++r)
@@ -369,6 +388,8 @@ private:
     std::vector<std::string> seqs_;
     uint64_t seed_ = 0;
     uint32_t table_size_ = 40000;
+    uint32_t repeat_tol_ = 0;
+    std::vector<uint64_t> start_points_;
 };
 
 }  // namespace mums
