@@ -28,6 +28,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402  (loaded before libmums_hip.so: one HIP runtime per process)
 import torch.distributed as dist  # noqa: E402
 
@@ -177,6 +178,9 @@ def run_e2e(mh, genomes, seed, reps: int = 2):
     signed starts, mums_result_copy).  The context is warm (its work buffers sized by the
     runs before), as for a caller that reuses a MemHash; best of `reps`."""
     pinned = [g.cpu().pin_memory() for g in genomes]
+    # the host MatchList lands in caller-owned pinned buffers (like the input), sized by the
+    # warm-up run and reused by the timed ones
+    out = None
     best = None
     for _ in range(reps + 1):   # the first run warms the per-genome allocations
         mh.Clear()
@@ -188,9 +192,14 @@ def run_e2e(mh, genomes, seed, reps: int = 2):
         mh.SetSeed(seed)
         mh.CreateMatches()
         t2 = time.perf_counter()
-        ml = mh.GetMatchList()
+        ml = mh.GetMatchList(out)
         t3 = time.perf_counter()
         r = (t3 - t0, t1 - t0, t2 - t1, t3 - t2, len(ml))
+        if out is None:   # warm-up run: allocate the pinned result buffers
+            n, G = len(ml), len(genomes)
+            out = (torch.empty(n, dtype=torch.int64, pin_memory=True).numpy().view(np.uint64),
+                   torch.empty(n * G, dtype=torch.int64, pin_memory=True).numpy())
+            continue
         if best is None or r[0] < best[0]:
             best = r
     tot, add, find, copy, m = best
@@ -198,7 +207,8 @@ def run_e2e(mh, genomes, seed, reps: int = 2):
     return {"mums_per_s": m / tot, "seedmers_per_s": sm["seedmers"] / tot, "matches": m, "ms": tot * 1e3,
             "ms_add_h2d": add * 1e3, "ms_find": find * 1e3, "ms_result_d2h": copy * 1e3,
             "workload": f"BASELINE config 3 end to end: {len(genomes)} x {genomes[0].numel() // 10**6} Mbp ASCII in "
-                        f"pinned host memory -> host MatchList ({m} matches x {len(genomes)} starts)"}
+                        f"pinned host memory -> host MatchList ({m} matches x {len(genomes)} starts) in caller-owned "
+                        f"pinned buffers"}
 
 
 def main():

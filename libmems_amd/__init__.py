@@ -394,12 +394,23 @@ class MemHash:
     def FindStage(self, stage: int) -> None:
         self._check(self._lib.mums_find_stage(self._ctx, stage))
 
-    def GetMatchList(self) -> MatchList:
+    def GetMatchList(self, out=None) -> MatchList:
+        """MemHash::GetMatchList (MemHash.h:182-203).  out = (lengths, starts): caller-owned
+        host arrays (uint64 [>= count], int64 [>= count * G], e.g. pinned memory reused across
+        calls) that receive the result; the MatchList then views their first rows."""
         cnt = ctypes.c_uint64()
         g = ctypes.c_uint32()
         self._check(self._lib.mums_result_count(self._ctx, ctypes.byref(cnt), ctypes.byref(g)))
-        lengths = np.zeros(cnt.value, dtype=np.uint64)
-        starts = np.zeros((cnt.value, g.value), dtype=np.int64)
+        if out is not None:
+            lb, sb = out
+            if lb.dtype != np.uint64 or sb.dtype != np.int64 or lb.size < cnt.value or sb.size < cnt.value * g.value \
+                    or not (lb.flags.c_contiguous and sb.flags.c_contiguous):
+                raise ValueError("GetMatchList(out): uint64 / int64 contiguous arrays of the result size required")
+            lengths = lb.reshape(-1)[:cnt.value]
+            starts = sb.reshape(-1)[:cnt.value * g.value].reshape(cnt.value, g.value)
+        else:
+            lengths = np.zeros(cnt.value, dtype=np.uint64)
+            starts = np.zeros((cnt.value, g.value), dtype=np.int64)
         if cnt.value:
             self._check(self._lib.mums_result_copy(self._ctx, lengths.ctypes.data, starts.ctypes.data))
         return MatchList(lengths, starts)
