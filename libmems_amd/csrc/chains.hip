@@ -20,8 +20,11 @@
 //   5. chain_seg / chain_entry kernels: segment ids (scan), the extended entry of
 //                           every chain and chain_of[probe].
 // The replay (replay.hip) then inserts chain entries without extending anything.
-// A 32-bit line-hash collision only splits runs of a line: every probe still gets
-// its true chain ends (a segment end always walks to the real end of its chain).
+// A line-hash collision whose two lines interleave in x order splits a chain into two
+// segments with the same extended entry, and the replay then sees it twice: with a 16-bit
+// hash the 4 x 10 Mbp related known answer gains 4 matches (MUMS_LINE_HASH_BITS A/B,
+// round 4).  32 bits: only colliding multi-probe lines whose x ranges overlap do this --
+// none in the test corpus or the C3 known answer; the residual risk is noted in DESIGN.md.
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -347,6 +350,8 @@ __global__ __launch_bounds__(kBlock) void chain_key_kernel(View v, const uint64_
     lkey[k] = ((uint64_t)line_hash<MG>(Q, gt.G) << 32) | (x & 0xFFFFFFFFull);
 }
 
+constexpr uint64_t kCollideScan = 4096;   // probes scanned after a line-hash collision
+
 // Block-wide append of the items whose want bit is set (kIPT per thread): one atomic per
 // workgroup -- a single queue counter hit by every wave serialises in the L2 atomic unit.
 constexpr int kLinkIPT = 8;
@@ -389,9 +394,10 @@ template <int MG, typename View>
 __global__ __launch_bounds__(kBlock) void chain_link_kernel(View v, const uint64_t* __restrict__ probe_info, uint64_t P,
                                                             GenomeTable gt, MatchParams mp, SeedSpec ss,
                                                             uint8_t* __restrict__ link, WalkItem* __restrict__ queue,
-                                                            unsigned int* __restrict__ qcount) {
+                                                            unsigned int* __restrict__ qcount,
+                                                            unsigned int* __restrict__ collide) {
     const int L = ss.L;
-    uint32_t want = 0;
+    uint32_t want = 0, cbits = 0;
     WalkItem it[kLinkIPT];
     #pragma unroll
     for (int i = 0; i < kLinkIPT; ++i) {
@@ -412,8 +418,30 @@ __global__ __launch_bounds__(kBlock) void chain_link_kernel(View v, const uint64
             else { it[i].kind = 0; it[i].stop = stop; want |= 1u << i; }
         } else {
             want |= 1u << i;
+            // a different line with the same line hash (checked below)
+            if (collide && j + 1 < P && line_hash<MG>(A, gt.G) == line_hash<MG>(B, gt.G)) cbits |= 1u << i;
         }
         link[j] = lk;
+    }
+    // a later probe of A's line inside the equal-hash run means two lines interleave (a chain
+    // would split in two segments); looked for over kCollideScan probes, a longer run counts
+    // as interleaved -- the caller then orders the lines exactly
+    while (cbits) {
+        const int i = __builtin_ctz(cbits);
+        cbits &= cbits - 1;
+        const uint64_t j = (uint64_t)blockIdx.x * (kBlock * kLinkIPT) + (uint64_t)i * kBlock + threadIdx.x;
+        Mhe<MG> A;
+        probe_of<MG, View>(v, probe_info, j, gt, mp, L, A);
+        const uint32_t hA = line_hash<MG>(A, gt.G);
+        bool hit = j + 2 < P;
+        for (uint64_t q = j + 2; q < P && q < j + 2 + kCollideScan; ++q) {
+            Mhe<MG> Q;
+            probe_of<MG, View>(v, probe_info, q, gt, mp, L, Q);
+            if (line_hash<MG>(Q, gt.G) != hA) { hit = false; break; }
+            if (same_line<MG>(A, Q)) break;
+            if (q + 1 == P) hit = false;
+        }
+        if (hit) atomicOr(collide, 1u);
     }
     block_push<kLinkIPT>(want, it, queue, qcount);
 }
@@ -869,7 +897,7 @@ hipError_t line_sort(const ChainWs& w, uint64_t P, int xbits, void* d_tmp, uint3
     hipLaunchKernelGGL(line_rec2_kernel, dim3(grid_of(P)), dim3(kBlock), 0, st, w.lkey, s1, P, r2);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     int b2 = 0;
-    if ((e = seg_onesweep_sort(r2, w.lkey, P, 32, 0, w.bst, d_tmp, d_err, &b2, st)) != hipSuccess) return e;
+    if ((e = seg_onesweep_sort(r2, w.lkey, P, kLineHashBits, 0, w.bst, d_tmp, d_err, &b2, st)) != hipSuccess) return e;
     const uint64_t* s2 = b2 ? w.lkey : r2;
     hipLaunchKernelGGL(line_ord_kernel, dim3(grid_of(P)), dim3(kBlock), 0, st, s1, s2, P, w.vA);
     *ord_out = w.vA;
@@ -903,7 +931,7 @@ hipError_t chains_core(MatProbes vl, const ChainWs& w, const uint32_t* ord, uint
         const unsigned lgrid = (unsigned)((P + kBlock * kLinkIPT - 1) / (kBlock * kLinkIPT));
         if (pass == 0)
             hipLaunchKernelGGL((chain_link_kernel<MG, MatProbes>), dim3(lgrid), dim3(kBlock), 0, st, vl, nullptr, P, gt,
-                               mp, ss, w.link, w.queue, qshort);
+                               mp, ss, w.link, w.queue, qshort, qcount + 12);
         else
             hipLaunchKernelGGL(chain_left_kernel, dim3(lgrid), dim3(kBlock), 0, st, P, (const uint8_t*)w.link, w.queue,
                                qshort);
@@ -954,6 +982,47 @@ hipError_t line_order(const ChainWs& w, uint64_t P, const GenomeTable& gt, void*
     return e;
 }
 
+// exact line order (after an interleaving line-hash collision): by x, then stably by the
+// 64-bit line hash (two radix sorts of (key, probe) pairs; rows in key order)
+template <int MG>
+__global__ __launch_bounds__(kBlock) void line_x_kernel(MatProbes v, uint64_t P, int G, uint64_t* __restrict__ out) {
+    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= P) return;
+    Mhe<MG> Q;
+    load_probe<MG>(v, (uint32_t)k, G, 0, Q);
+    out[k] = (uint64_t)start_at(Q, first_start(Q));
+}
+
+template <int MG>
+__global__ __launch_bounds__(kBlock) void line_h64_kernel(MatProbes v, const uint32_t* __restrict__ vk, uint64_t P,
+                                                          int G, uint64_t* __restrict__ out,
+                                                          uint32_t* __restrict__ vcopy) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= P) return;
+    Mhe<MG> Q;
+    load_probe<MG>(v, vk[i], G, 0, Q);
+    out[i] = line_hash64<MG>(Q, G);
+    vcopy[i] = vk[i];
+}
+
+template <int MG>
+hipError_t line_order_exact(MatProbes v, const ChainWs& w, uint64_t P, const GenomeTable& gt, void* d_tmp,
+                            hipStream_t st, const uint32_t** ord) {
+    hipLaunchKernelGGL((line_x_kernel<MG>), dim3(grid_of(P)), dim3(kBlock), 0, st, v, P, gt.G, w.lkey);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    int b1 = 0;
+    if ((e = radix_sort<uint64_t>(w.lkey, nullptr, P, x_bits(gt), w.kA, w.vA, w.kB, w.vB, d_tmp, &b1, st)) != hipSuccess)
+        return e;
+    hipLaunchKernelGGL((line_h64_kernel<MG>), dim3(grid_of(P)), dim3(kBlock), 0, st, v, b1 ? w.vB : w.vA, P, gt.G,
+                       w.lkey, w.seg);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    int b2 = 0;
+    if ((e = radix_sort<uint64_t>(w.lkey, w.seg, P, 64, w.kA, w.vA, w.kB, w.vB, d_tmp, &b2, st)) != hipSuccess) return e;
+    *ord = b2 ? w.vB : w.vA;
+    return hipSuccess;
+}
+
 }  // namespace
 
 uint64_t* chain_lkey_slot(void* d_chain_tmp, uint64_t P, int G) { return chain_ws(d_chain_tmp, P, G, true).lkey; }
@@ -981,6 +1050,22 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
     if ((e = launch_gather_rows(v.rows, ord, P, gt.G, w.rows_line, st)) != hipSuccess) return e;
     MatProbes vl{};
     vl.rows = w.rows_line;
+    if ((e = hipMemsetAsync(w.qcount + 12, 0, 4, st)) != hipSuccess) return e;
+    if ((e = chains_core<MG>(vl, w, ord, P, gt, mp, ss, packed, d_scan_tmp, chain_of, pool, d_nchains, st, ctr, ev_walk,
+                             fk, kbase)) != hipSuccess)
+        return e;
+    // two lines with equal 32-bit line hashes interleaved (a chain split in two segments):
+    // the line order again with the 64-bit hash, and the chains again (rare: colliding
+    // multi-probe lines whose x ranges overlap)
+    unsigned hc = 0;
+    if ((e = hipMemcpyAsync(&hc, w.qcount + 12, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+    if (!hc && !getenv("MUMS_DEV_LINE_EXACT")) return hipSuccess;
+    if (getenv("MUMS_DEV_CHAIN_DEBUG")) fprintf(stderr, "chains: line-hash collision, exact line order\n");
+    MatProbes vk{};
+    vk.rows = v.rows;
+    if ((e = line_order_exact<MG>(vk, w, P, gt, d_radix_tmp, st, &ord)) != hipSuccess) return e;
+    if ((e = launch_gather_rows(v.rows, ord, P, gt.G, w.rows_line, st)) != hipSuccess) return e;
     return chains_core<MG>(vl, w, ord, P, gt, mp, ss, packed, d_scan_tmp, chain_of, pool, d_nchains, st, ctr, ev_walk,
                            fk, kbase);
 }

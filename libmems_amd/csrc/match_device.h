@@ -440,9 +440,15 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
 }
 
 // line invariants: reference start x = s_ref (> 0); per other component the
-// diagonal s_g - s_ref (forward) or |s_g| + s_ref (reverse)
+// diagonal s_g - s_ref (forward) or |s_g| + s_ref (reverse).  kLineHashBits of them key the
+// line order; fewer bits save sort passes (24: -1.4 ms at C3) but a collision that interleaves
+// two chains changes the MatchList (chains.hip), so 32 stays.
+#ifndef MUMS_LINE_HASH_BITS
+#define MUMS_LINE_HASH_BITS 32
+#endif
+constexpr int kLineHashBits = MUMS_LINE_HASH_BITS;
 template <int MG>
-__device__ __forceinline__ uint32_t line_hash(const Mhe<MG>& P, int G) {
+__device__ __forceinline__ uint64_t line_hash64(const Mhe<MG>& P, int G) {
     const int ref = first_start(P);
     const int64_t x = start_at(P, ref);
     uint64_t h = 0x9e3779b97f4a7c15ull ^ (uint64_t)ref;
@@ -456,7 +462,11 @@ __device__ __forceinline__ uint32_t line_hash(const Mhe<MG>& P, int G) {
             h = mix64(h ^ ((uint64_t)g << 48));
         }
     }
-    return (uint32_t)(h >> 32);
+    return h;
+}
+template <int MG>
+__device__ __forceinline__ uint32_t line_hash(const Mhe<MG>& P, int G) {
+    return (uint32_t)(line_hash64<MG>(P, G) >> (64 - kLineHashBits));
 }
 
 

@@ -218,3 +218,15 @@ def test_c3_scale_seed_stage_properties(gpu_lib, oracle_mod):
         ks = mh.SeedKeys(5, m)[sml]
         assert bool(np.all(ks[1:] >= ks[:-1]))
         assert st["probes"] > 0.9 * m   # related genomes: almost every position is a shared seed
+
+
+# ---- the exact line order (64-bit line hash), taken after an interleaving collision of the
+# 32-bit line hash (chains.hip): forced here, it must give the same known answers
+@pytest.mark.parametrize("case", CASES[:4], ids=lambda c: f"G{c['G']}_n{c['n']}_p{c['p']}_{c['mode']}")
+def test_exact_line_order_known_answers(gpu_lib, oracle_mod, case, monkeypatch):
+    monkeypatch.setenv("MUMS_DEV_LINE_EXACT", "1")
+    seqs = oracle_mod.generate(case["G"], case["n"], case["p"], 12345)
+    ml, st = gpu_find(gpu_lib, seqs, oracle_mod.get_seed(case["w"]), masked=case["mode"] == "MaskedMemHash",
+                      mask=case.get("mask", 0))
+    assert len(ml) == case["matches"]
+    assert hashlib.md5(ml.text().encode()).hexdigest() == case["md5"]
