@@ -592,6 +592,7 @@ class ShardedMemHash:
         self.table_size = table_size
         self.seed = 0
         self.repeat_tol = 0
+        self.progress = False
         self.seqs: List[bytes] = []
         self.ranks: List[MemHash] = []
         self.stats_per_rank: List[dict] = []
@@ -611,6 +612,14 @@ class ShardedMemHash:
         """MemHash::SetRepeatTolerance (MemHash.h:125-131) on every rank: the first copies of a
         genome follow its SortedMerList's std::sort order, replayed on rank g % world."""
         self.repeat_tol = int(t)
+
+    def LogProgress(self, enable: bool = True) -> None:
+        """MatchFinder::LogProgress (MatchFinder.cpp:55-56) over the ranks: the text of the whole
+        merge, restated on rank 0 (the restart is then planned on the gathered streams)."""
+        self.progress = bool(enable)
+
+    def ProgressLog(self) -> str:
+        return self.ranks[0].ProgressLog() if self.ranks else ""
 
     def AddSequence(self, seq) -> None:
         self.seqs.append(seq.encode() if isinstance(seq, str) else bytes(seq))
@@ -666,6 +675,8 @@ class ShardedMemHash:
             mh._check(self._lib.mums_shard_layout(mh._ctx, G, g0, lens))
             self.ranks.append(mh)
             g0 += cnt
+        for mh in self.ranks:
+            mh.LogProgress(self.progress)
         sp = getattr(self, "_start_points", None)
         if sp is not None:
             for mh in self.ranks:

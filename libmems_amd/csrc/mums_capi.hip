@@ -2550,7 +2550,9 @@ int mums_shard_merge(mums_ctx* ctx, const uint64_t* d_records, uint32_t nsources
     ctx->restarts = 0;
     ctx->offset_log.clear();
     // (repeat tolerance: every run of equal keys in std::sort order, mums_shard_tie_*, first)
-    ctx->shard_restart_pending = ctx->hc.repeat_limit > 0 || have_start_points(ctx) || ctx->repeat_tol > 0;
+    // (LogProgress: the text is restated by the gathered plan on rank 0, over the whole stream)
+    ctx->shard_restart_pending =
+        ctx->hc.repeat_limit > 0 || have_start_points(ctx) || ctx->repeat_tol > 0 || ctx->progress_on;
     ctx->shard_mb = mb;
     ctx->shard_n = n;
     ctx->shard_kfirst = first_bucket;

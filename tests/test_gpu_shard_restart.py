@@ -212,3 +212,30 @@ def test_repeat_tolerance_chunked_merge(gpu_lib, oracle_mod, monkeypatch, rtol):
     seqs = repeat_inputs.n_gapped(G=3, n=200_000, gaps=((40_000, 3000), (120_000, 3000)), shift=500, seed=1)
     monkeypatch.setenv("MUMS_DEV_CHUNK_RECORDS", str(sum(len(s) for s in seqs) // 12))
     check(gpu_lib, oracle_mod, seqs, 2, repeat_tol=rtol)
+
+
+# MatchFinder::LogProgress (MatchFinder.cpp:55-56, 296-309) over the ranks: the text of the
+# whole merge, restated on rank 0 -- the single context's text (pinned to the oracle's
+# literal SearchRange text by tests/test_gpu_progress.py)
+@pytest.mark.parametrize("world,layout", [(2, "blocks"), (3, "blocks"), (2, "slices")])
+@pytest.mark.parametrize("kind", ["plain", "n_gapped"])
+def test_progress_text(gpu_lib, oracle_mod, world, layout, kind):
+    if kind == "plain":
+        seqs = oracle_mod.generate(3, 120_000, 0.02, 31)
+    else:
+        seqs = repeat_inputs.n_gapped(G=3, n=200_000, gaps=((40_000, 3000), (120_000, 3000)), shift=500, seed=1)
+    seed = oracle_mod.get_seed(15)
+    with gpu_lib.MemHash(0) as mh:
+        mh.SetSeed(seed)
+        mh.LogProgress(True)
+        ref_ml = mh.FindMatches(seqs)
+        ref = mh.ProgressLog()
+    assert ref.endswith("..") and "%" in ref
+    with gpu_lib.ShardedMemHash([0] * (len(seqs) * 2 if layout == "slices" else world), comm="local",
+                                layout=layout) as sh:
+        sh.SetSeed(seed)
+        sh.LogProgress(True)
+        ml = sh.FindMatches(seqs)
+        text = sh.ProgressLog()
+    assert text == ref
+    assert len(ml) == len(ref_ml)
