@@ -270,6 +270,17 @@ __global__ void cr_dtie_write_kernel(CrStream s, GenomeTable gt, const uint64_t*
     }
 }
 
+// LogProgress on genome-major SMLs (the pair path's restart workspace): the masked key of
+// SML index e of genome g for every query g << 56 | e
+__global__ __launch_bounds__(kBlock) void cr_ck_query_kernel(const uint64_t* __restrict__ ck, GenomeTable gt,
+                                                             const uint64_t* __restrict__ q, uint64_t nq,
+                                                             uint64_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= nq) return;
+    const int g = (int)(q[i] >> 56);
+    out[i] = ck[gt.base[g] + (q[i] & ((1ull << 56) - 1))] >> 1;
+}
+
 // Repeat tolerance (every run of equal keys in std::sort order): every record of genome g in
 // a flagged run (the tie replay's scanned slot flags ts) takes the id at its SML slot, V[i]
 // (positions in the genome).  Ids move only inside genome g, so gscan stays valid.
@@ -463,6 +474,13 @@ hipError_t launch_cr_tie_vals(const CrStream& s, const GenomeTable& gt, const ui
 hipError_t launch_cr_kpos(const CrStream& s, const GenomeTable& gt, int g, uint64_t* K, hipStream_t st) {
     if (s.N == 0) return hipSuccess;
     hipLaunchKernelGGL(cr_kpos_kernel, cr_grid(s.N), dim3(kBlock), 0, st, s, gt, g, K);
+    return hipGetLastError();
+}
+
+hipError_t launch_cr_ck_query(const uint64_t* ck, const GenomeTable& gt, const uint64_t* q, uint64_t nq, uint64_t* out,
+                              hipStream_t st) {
+    if (nq == 0) return hipSuccess;
+    hipLaunchKernelGGL(cr_ck_query_kernel, cr_grid(nq), dim3(kBlock), 0, st, ck, gt, q, nq, out);
     return hipGetLastError();
 }
 

@@ -936,6 +936,9 @@ bool wants_tie_order(const mums_ctx* ctx) { return !ctx->pairwise && (ctx->repea
 
 int progress_packed(mums_ctx* ctx, const uint64_t* rec, const uint32_t* bstart, int B, uint64_t n, hipStream_t st,
                     const RestartWs* pw = nullptr, uint64_t* ck_build = nullptr);
+int progress_pairs(mums_ctx* ctx, const RestartWs* pw, hipStream_t st);
+// the pair path's (key, index) stream without a restart: its SMLs built for LogProgress
+int progress_pair_stream(mums_ctx* ctx, const RsStream& s, uint64_t n, hipStream_t st);
 
 // MER_REPEAT_LIMIT restart (MatchFinder.cpp:253-277) and FindMatchSeeds start points
 // (MemHash.cpp:117-127) on the merged stream s of n records (restart.hip): plan the
@@ -999,8 +1002,8 @@ int restart_fixup(mums_ctx* ctx, const RsStream& s, uint64_t n, void* dst_a, uin
     if (po.nrestarts) HIPCHK(hipMemcpy(ctx->offset_log.data(), d_rS, po.nrestarts * Gu * 8, hipMemcpyDeviceToHost));
     ctx->consumed_log.assign(po.nrestarts * Gu, 0);
     if (po.nrestarts) HIPCHK(hipMemcpy(ctx->consumed_log.data(), d_rC, po.nrestarts * Gu * 8, hipMemcpyDeviceToHost));
-    if (ctx->progress_on && s.kind == 0) {   // the stream is still whole here (compaction below)
-        const int rc = progress_packed(ctx, s.rec, s.bstart, s.B, n, st, &w);
+    if (ctx->progress_on) {   // the stream is still whole here (compaction below)
+        const int rc = s.kind == 0 ? progress_packed(ctx, s.rec, s.bstart, s.B, n, st, &w) : progress_pairs(ctx, &w, st);
         if (rc) return rc;
     }
     if (po.nrestarts == 0 && !have_start_points(ctx)) return MUMS_OK;
@@ -1039,6 +1042,13 @@ int restart_stage(mums_ctx* ctx, const MatchParams& mp, const ProbeSpace& ps, hi
         if (ctx->progress_on && ctx->packed_path)
             return progress_packed(ctx, ctx->sorted_rec, ctx->mstart.as<uint32_t>(), ctx->msd_bits, ctx->N, st, nullptr,
                                    ctx->sorted_buf ? ctx->recA.as<uint64_t>() : ctx->recB.as<uint64_t>());
+        if (ctx->progress_on) {   // the pair path (seed weight > 21)
+            RsStream ps{};
+            ps.kind = ctx->key64 ? 2 : 1;
+            ps.key = ctx->sorted_key;
+            ps.idx = ctx->sorted_idx;
+            return progress_pair_stream(ctx, ps, ctx->N, st);
+        }
         return MUMS_OK;
     }
     DevCounters* dc = ctx->counters.as<DevCounters>();
@@ -3410,6 +3420,13 @@ int run_pipeline_pairwise(mums_ctx* ctx, int stage) {
             HIPCHK(hipMemcpy(&dc->repeat_limit, &rep, 8, hipMemcpyHostToDevice));
             HIPCHK(hipMemcpy(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost));
         }
+    } else if (ctx->progress_on) {   // LogProgress without a restart (MatchFinder.cpp:296-309)
+        RsStream s{};
+        s.kind = ctx->key64 ? 2 : 1;
+        s.key = ctx->sorted_key;
+        s.idx = ctx->sorted_idx;
+        rc = progress_pair_stream(ctx, s, N, st);
+        if (rc) return rc;
     }
     HIPCHK(hipEventRecord(ctx->ev[EV_GROUPS], st));
     const uint64_t P = ctx->P;
@@ -3542,7 +3559,16 @@ int progress_log(mums_ctx* ctx, const CrStream& s, const uint32_t* gscan, hipStr
         }
     }
     std::vector<uint64_t> key(q.size(), 0);
-    if (!q.empty()) {
+    if (!q.empty() && !s.rec) {   // no packed stream (the pair path): the SMLs of pw answer
+        if (!pw) return fail(ctx, MUMS_E_HIP, "progress: neither a stream nor SMLs (internal error)");
+        DevBuf qb;
+        HIPCHK(qb.ensure(q.size() * 16 + 64));
+        uint64_t* d_q = qb.as<uint64_t>();
+        HIPCHK(hipMemcpyAsync(d_q, q.data(), q.size() * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(launch_cr_ck_query(pw->ck, gt, d_q, q.size(), d_q + q.size(), st));
+        HIPCHK(hipMemcpyAsync(key.data(), d_q + q.size(), q.size() * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+    } else if (!q.empty()) {
         const uint64_t nblk = cr_blocks(s.N);
         if (!gscan) {
             HIPCHK(ctx->crcnt.ensure(Gu * (nblk + 1) * 4 + 256));
@@ -3672,6 +3698,24 @@ int progress_packed(mums_ctx* ctx, const uint64_t* rec, const uint32_t* bstart, 
     s.ib = 32;
     const int rc = progress_log(ctx, s, nullptr, st, pw, ck_build);
     HIPCHK(hipStreamSynchronize(st));   // db and the query buffer are freed on return
+    return rc;
+}
+
+// the pair path (keys + indices, no packed stream): the SMLs of the restart workspace
+int progress_pairs(mums_ctx* ctx, const RestartWs* pw, hipStream_t st) {
+    CrStream none{nullptr, nullptr, 0, 0};
+    return progress_log(ctx, none, nullptr, st, pw);
+}
+
+int progress_pair_stream(mums_ctx* ctx, const RsStream& s, uint64_t n, hipStream_t st) {
+    HIPCHK(ctx->rsbuf.ensure(restart_ws_bytes(n, ctx->gt.G)));
+    const RestartWs w = restart_ws_layout(ctx->rsbuf.p, n, ctx->gt.G);
+    HIPCHK(launch_restart_smls(s, n, ctx->gt, w, st));
+    ctx->restarts = 0;
+    ctx->offset_log.clear();
+    ctx->consumed_log.clear();
+    const int rc = progress_pairs(ctx, &w, st);
+    HIPCHK(hipStreamSynchronize(st));
     return rc;
 }
 

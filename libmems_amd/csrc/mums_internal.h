@@ -421,6 +421,9 @@ hipError_t launch_cr_ck(const CrStream& s, const GenomeTable& gt, const uint32_t
 // masked key of genome g's SML index e for every query g << 56 | e (gscan from launch_cr_counts)
 hipError_t launch_cr_query(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, const uint64_t* q, uint64_t nq,
                            uint64_t* out, hipStream_t st);
+// the same from genome-major SMLs (ck[base[g] + e])
+hipError_t launch_cr_ck_query(const uint64_t* ck, const GenomeTable& gt, const uint64_t* q, uint64_t nq, uint64_t* out,
+                              hipStream_t st);
 hipError_t launch_cr_cands(const CrStream& s, uint64_t* list, unsigned long long* cnt, uint64_t cap, hipStream_t st);
 hipError_t launch_cr_runs(const uint64_t* ck, const GenomeTable& gt, const uint64_t* sp, uint64_t rows, uint64_t* runs,
                           unsigned long long* nr, uint64_t cap, hipStream_t st);

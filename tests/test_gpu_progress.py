@@ -83,3 +83,26 @@ def test_progress_chunked_mode(gpu_lib, oracle_mod, monkeypatch, gapped):
     _, _, ref = oracle_mod.find_matches(seqs, seed)
     assert st["chunks"] >= 2
     assert text == ref["progress"]
+
+
+@pytest.mark.parametrize("w,gapped", [(23, False), (25, False), (23, True)])
+def test_progress_pair_path(gpu_lib, oracle_mod, w, gapped):
+    """the pair-key path (seed weight > 21): keys restated from the key-order ranks"""
+    seqs = (repeat_inputs.n_gapped(G=3, n=250_000, gaps=((40_000, 3000), (150_000, 3000)), shift=600, seed=5)
+            if gapped else oracle_mod.generate(3, 600_000, 0.01, 23))
+    _, ref = check(gpu_lib, oracle_mod, seqs, w)
+    if gapped:
+        assert ref["restarts"] > 0
+
+
+@pytest.mark.parametrize("w,gapped", [(15, False), (23, False), (15, True)])
+def test_progress_pairwise(gpu_lib, oracle_mod, w, gapped):
+    """PairwiseMatchFinder searches with MatchFinder::FindMatchSeeds (PairwiseMatchFinder.cpp:
+    37-73 only changes how a seed group is hashed), so its text is the same merge's"""
+    seqs = (repeat_inputs.n_gapped(G=3, n=250_000, gaps=((40_000, 3000), (150_000, 3000)), shift=600, seed=6)
+            if gapped else oracle_mod.generate(4, 400_000, 0.02, 41))
+    seed = oracle_mod.get_seed(w)
+    text, st = gpu_progress(gpu_lib, seqs, seed, "PairwiseMatchFinder")
+    _, _, ref = oracle_mod.find_matches(seqs, seed, pairwise=True)
+    assert st["restarts"] == ref["restarts"]
+    assert text == ref["progress"] and text
