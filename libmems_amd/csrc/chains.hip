@@ -707,6 +707,60 @@ __global__ __launch_bounds__(kBlock) void line_ord_kernel(const uint64_t* __rest
     if (j < P) ord[j] = (uint32_t)s1[(uint32_t)s2[j]];
 }
 
+// the rows in line order as LineRows (match_device.h): a block's kBlock rows are loaded
+// element-wise (neighbouring lanes on one row, all loads in flight together) into LDS, then
+// each thread packs one row's starts to int32 and checks that they fit and that the
+// recomputed offset equals the materialized one (*bad |= 1 otherwise: the caller redoes
+// the chains from the 64-bit rows)
+template <int MG>
+__global__ __launch_bounds__(kBlock) void gather_line_rows_kernel(const int64_t* __restrict__ src,
+                                                                  const uint32_t* __restrict__ ord, uint64_t P, int G,
+                                                                  int L, int32_t* __restrict__ dst,
+                                                                  unsigned int* __restrict__ bad) {
+    static_assert(MG % 4 == 0 && MG <= 16, "int4 rows, LDS staging");
+    __shared__ int64_t srow[kBlock * (MG + 1)];
+    __shared__ uint32_t sk[kBlock];
+    const uint64_t j0 = (uint64_t)blockIdx.x * kBlock;
+    const uint32_t nj = P - j0 < (uint64_t)kBlock ? (uint32_t)(P - j0) : (uint32_t)kBlock;
+    const uint32_t W = (uint32_t)G + 1, ne = nj * W;
+    if (threadIdx.x < nj) sk[threadIdx.x] = ord[j0 + threadIdx.x];
+    __syncthreads();
+    uint32_t r = threadIdx.x / W, c = threadIdx.x - r * W;
+    const uint32_t dr = kBlock / W, dc = kBlock % W;
+    int64_t x[MG + 1];
+    #pragma unroll
+    for (int i = 0; i < MG + 1; ++i) {
+        const uint32_t e = threadIdx.x + (uint32_t)i * kBlock;
+        x[i] = e < ne ? src[(uint64_t)sk[r] * W + c] : 0;
+        r += dr;
+        c += dc;
+        if (c >= W) { c -= W; ++r; }
+    }
+    #pragma unroll
+    for (int i = 0; i < MG + 1; ++i) {
+        const uint32_t e = threadIdx.x + (uint32_t)i * kBlock;
+        if (e < ne) srow[e] = x[i];
+    }
+    __syncthreads();
+    if (threadIdx.x >= nj) return;
+    const int64_t* row = srow + threadIdx.x * W;
+    Mhe<MG> Q;
+    bool ok = true;
+    #pragma unroll
+    for (int g = 0; g < MG; ++g) {
+        Q.s[g] = g < G ? row[g] : 0;
+        ok = ok && Q.s[g] == (int64_t)(int32_t)Q.s[g];
+    }
+    ok = ok && probe_offset<MG>(Q, L) == row[G];
+    int32_t* out = dst + (j0 + threadIdx.x) * (uint64_t)line_row_stride(G);
+    #pragma unroll
+    for (int q = 0; q < MG / 4; ++q)
+        if (4 * q < G)
+            *reinterpret_cast<int4*>(out + 4 * q) =
+                make_int4((int32_t)Q.s[4 * q], (int32_t)Q.s[4 * q + 1], (int32_t)Q.s[4 * q + 2], (int32_t)Q.s[4 * q + 3]);
+    if (!ok) atomicOr(bad, 1u);
+}
+
 inline unsigned grid_of(uint64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
 // --- chunked FindMatches: chains labelled per slice of the probes ---------------------
@@ -914,8 +968,8 @@ int x_bits(const GenomeTable& gt) {
 
 // after the line sort (ord = probe of line position j, vl.rows = the rows in line order):
 // links, walks, segment ids, chain_of and the chain entries
-template <int MG>
-hipError_t chains_core(MatProbes vl, const ChainWs& w, const uint32_t* ord, uint64_t P, const GenomeTable& gt,
+template <int MG, typename LV>
+hipError_t chains_core(LV vl, const ChainWs& w, const uint32_t* ord, uint64_t P, const GenomeTable& gt,
                        const MatchParams& mp, const SeedSpec& ss, const uint32_t* packed, void* d_scan_tmp,
                        uint32_t* chain_of, int64_t* pool, uint32_t* d_nchains, hipStream_t st, void* ctr,
                        hipEvent_t* ev_walk, uint32_t* fk, uint32_t kbase) {
@@ -930,19 +984,19 @@ hipError_t chains_core(MatProbes vl, const ChainWs& w, const uint32_t* ord, uint
         if ((e = hipMemsetAsync(qcount, 0, 8, st)) != hipSuccess) return e;
         const unsigned lgrid = (unsigned)((P + kBlock * kLinkIPT - 1) / (kBlock * kLinkIPT));
         if (pass == 0)
-            hipLaunchKernelGGL((chain_link_kernel<MG, MatProbes>), dim3(lgrid), dim3(kBlock), 0, st, vl, nullptr, P, gt,
+            hipLaunchKernelGGL((chain_link_kernel<MG, LV>), dim3(lgrid), dim3(kBlock), 0, st, vl, nullptr, P, gt,
                                mp, ss, w.link, w.queue, qshort, qcount + 12);
         else
             hipLaunchKernelGGL(chain_left_kernel, dim3(lgrid), dim3(kBlock), 0, st, P, (const uint8_t*)w.link, w.queue,
                                qshort);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-        hipLaunchKernelGGL((chain_walk_short_kernel<MG, MatProbes>), dim3(short_grid), dim3(kBlock), 0, st, vl, nullptr,
+        hipLaunchKernelGGL((chain_walk_short_kernel<MG, LV>), dim3(short_grid), dim3(kBlock), 0, st, vl, nullptr,
                            gt, mp, ss, packed, (const WalkItem*)w.queue, (const unsigned int*)qshort, w.link, w.rcol,
                            w.lcol, w.queue_long, qlong);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (cdbg && (e = hipMemsetAsync(qcount + 4, 0, 32, st)) != hipSuccess) return e;
         if (ev_walk) (void)hipEventRecord(ev_walk[2 * pass], st);
-        hipLaunchKernelGGL((chain_walk_kernel<MG, MatProbes>), dim3(walk_grid), dim3(kBlock), 0, st, vl, nullptr, gt, mp,
+        hipLaunchKernelGGL((chain_walk_kernel<MG, LV>), dim3(walk_grid), dim3(kBlock), 0, st, vl, nullptr, gt, mp,
                            ss, ord, packed, (const WalkItem*)w.queue_long, (const unsigned int*)qlong, w.link, w.rcol,
                            w.lcol, cdbg ? qcount + 4 : nullptr, (DevCounters*)ctr);
         if (ev_walk) (void)hipEventRecord(ev_walk[2 * pass + 1], st);
@@ -962,7 +1016,7 @@ hipError_t chains_core(MatProbes vl, const ChainWs& w, const uint32_t* ord, uint
     hipLaunchKernelGGL(chain_seg_kernel, dim3(grid), dim3(kBlock), 0, st, w.link, ord, w.seg, P, w.rcol, chain_of,
                        w.seg_r, fk, kbase);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL((chain_entry_kernel<MG, MatProbes>), dim3(grid), dim3(kBlock), 0, st, vl, nullptr, P, gt, mp,
+    hipLaunchKernelGGL((chain_entry_kernel<MG, LV>), dim3(grid), dim3(kBlock), 0, st, vl, nullptr, P, gt, mp,
                        ss.L, ord, w.link, w.seg, w.lcol, w.seg_r, pool);
     return hipGetLastError();
 }
@@ -1046,28 +1100,52 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
     }
     const uint32_t* ord = nullptr;
     if ((e = line_order(w, P, gt, d_radix_tmp, ctr, st, &ord)) != hipSuccess) return e;
-    // the rows in line order: the link / walk / entry kernels then read row j, not row ord[j]
-    if ((e = launch_gather_rows(v.rows, ord, P, gt.G, w.rows_line, st)) != hipSuccess) return e;
-    MatProbes vl{};
-    vl.rows = w.rows_line;
-    if ((e = hipMemsetAsync(w.qcount + 12, 0, 4, st)) != hipSuccess) return e;
-    if ((e = chains_core<MG>(vl, w, ord, P, gt, mp, ss, packed, d_scan_tmp, chain_of, pool, d_nchains, st, ctr, ev_walk,
-                             fk, kbase)) != hipSuccess)
-        return e;
+    // the rows in line order: the link / walk / entry kernels then read row j, not row ord[j];
+    // as LineRows (int32 starts, 32 B per probe at G = 8) when every start fits 31 bits
+    uint64_t mx = 0;
+    for (int g = 0; g < gt.G; ++g) mx = gt.n[g] > mx ? gt.n[g] : mx;
+    static const bool wide_env = getenv("MUMS_DEV_WIDE_LINE_ROWS") != nullptr;
+    bool narrow = MG % 4 == 0 && MG <= 16 && !wide_env && mx + 2 < (1ull << 31);
+    unsigned int* flags = w.qcount + 12;   // [0] interleaving line-hash collision, [1] a row not narrow
+    auto chains_from = [&](const uint32_t* o) -> hipError_t {
+        hipError_t r;
+        if ((r = hipMemsetAsync(flags, 0, 8, st)) != hipSuccess) return r;
+        if constexpr (MG % 4 == 0 && MG <= 16) {
+            if (narrow) {
+                hipLaunchKernelGGL((gather_line_rows_kernel<MG>), dim3(grid_of(P)), dim3(kBlock), 0, st, v.rows, o, P,
+                                   gt.G, ss.L, (int32_t*)w.rows_line, flags + 1);
+                if ((r = hipGetLastError()) != hipSuccess) return r;
+                LineRows vl{(const int32_t*)w.rows_line, line_row_stride(gt.G), ss.L};
+                return chains_core<MG>(vl, w, o, P, gt, mp, ss, packed, d_scan_tmp, chain_of, pool, d_nchains, st, ctr,
+                                       ev_walk, fk, kbase);
+            }
+        }
+        if ((r = launch_gather_rows(v.rows, o, P, gt.G, w.rows_line, st)) != hipSuccess) return r;
+        MatProbes vl{};
+        vl.rows = w.rows_line;
+        return chains_core<MG>(vl, w, o, P, gt, mp, ss, packed, d_scan_tmp, chain_of, pool, d_nchains, st, ctr, ev_walk,
+                               fk, kbase);
+    };
+    unsigned hf[2] = {0, 0};
+    auto read_flags = [&]() -> hipError_t {
+        hipError_t r;
+        if ((r = hipMemcpyAsync(hf, flags, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return r;
+        return hipStreamSynchronize(st);
+    };
+    if ((e = chains_from(ord)) != hipSuccess || (e = read_flags()) != hipSuccess) return e;
+    if (hf[1]) {   // a start or offset the int32 rows do not restate: the 64-bit rows
+        narrow = false;
+        if ((e = chains_from(ord)) != hipSuccess || (e = read_flags()) != hipSuccess) return e;
+    }
     // two lines with equal 32-bit line hashes interleaved (a chain split in two segments):
     // the line order again with the 64-bit hash, and the chains again (rare: colliding
     // multi-probe lines whose x ranges overlap)
-    unsigned hc = 0;
-    if ((e = hipMemcpyAsync(&hc, w.qcount + 12, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
-    if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
-    if (!hc && !getenv("MUMS_DEV_LINE_EXACT")) return hipSuccess;
+    if (!hf[0] && !getenv("MUMS_DEV_LINE_EXACT")) return hipSuccess;
     if (getenv("MUMS_DEV_CHAIN_DEBUG")) fprintf(stderr, "chains: line-hash collision, exact line order\n");
     MatProbes vk{};
     vk.rows = v.rows;
     if ((e = line_order_exact<MG>(vk, w, P, gt, d_radix_tmp, st, &ord)) != hipSuccess) return e;
-    if ((e = launch_gather_rows(v.rows, ord, P, gt.G, w.rows_line, st)) != hipSuccess) return e;
-    return chains_core<MG>(vl, w, ord, P, gt, mp, ss, packed, d_scan_tmp, chain_of, pool, d_nchains, st, ctr, ev_walk,
-                           fk, kbase);
+    return chains_from(ord);
 }
 
 #define MUMS_INST_CHAINS(MG, V)                                                                                   \

@@ -490,6 +490,52 @@ __device__ __forceinline__ void load_probe(const MatProbes& m, uint64_t k, int G
     for (int g = 0; g < MG; ++g) P.s[g] = (g < G) ? row[g] : 0;
 }
 
+// CalculateOffset of directed starts (the sum build_probe takes, MemHash.cpp:189-203)
+template <int MG>
+__device__ __forceinline__ int64_t probe_offset(const Mhe<MG>& P, int L) {
+    const int ref = first_start(P);
+    const int64_t sref = start_at(P, ref);
+    int64_t off = 0;
+    #pragma unroll
+    for (int g = 0; g < MG; ++g)
+        if (g > ref && P.s[g] != 0) off += P.s[g] - sref - (P.s[g] < 0 ? (int64_t)L : 0);
+    return off;
+}
+
+// The chain kernels' copy of the probe rows in line order when every start fits 31 bits:
+// G int32 starts per row (stride G rounded up to 4, 16-B aligned rows) and the offset
+// recomputed from them -- 32 B per probe instead of 72 at G = 8.  The gather that writes
+// it checks the recomputed offset against the materialized one (launch_gather_line_rows).
+struct LineRows {
+    const int32_t* rows;
+    uint32_t stride;
+    int L;   // seed length of the offset sum
+};
+
+__host__ __device__ inline uint32_t line_row_stride(int G) { return (uint32_t)((G + 3) & ~3); }
+
+template <int MG>
+__device__ __forceinline__ void load_probe(const LineRows& m, uint64_t k, int G, int L, Mhe<MG>& P) {
+    const int32_t* row = m.rows + k * (uint64_t)m.stride;
+    P.len = L;
+    P.mersize = L;
+    if constexpr (MG % 4 == 0) {
+        #pragma unroll
+        for (int q = 0; q < MG / 4; ++q) {
+            int4 v = make_int4(0, 0, 0, 0);
+            if (4 * q < G) v = *reinterpret_cast<const int4*>(row + 4 * q);
+            P.s[4 * q] = v.x;
+            P.s[4 * q + 1] = 4 * q + 1 < G ? v.y : 0;
+            P.s[4 * q + 2] = 4 * q + 2 < G ? v.z : 0;
+            P.s[4 * q + 3] = 4 * q + 3 < G ? v.w : 0;
+        }
+    } else {
+        #pragma unroll
+        for (int g = 0; g < MG; ++g) P.s[g] = (g < G) ? row[g] : 0;
+    }
+    P.offset = probe_offset<MG>(P, m.L);
+}
+
 __device__ __forceinline__ uint32_t bucket_of(int64_t offset, uint32_t table_size) {
     const int64_t T = (int64_t)table_size;
     return (uint32_t)(((offset % T) + T) % T);  // MemHash.cpp:213
