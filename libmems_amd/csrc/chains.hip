@@ -395,7 +395,8 @@ __global__ __launch_bounds__(kBlock) void chain_link_kernel(View v, const uint64
                                                             GenomeTable gt, MatchParams mp, SeedSpec ss,
                                                             uint8_t* __restrict__ link, WalkItem* __restrict__ queue,
                                                             unsigned int* __restrict__ qcount,
-                                                            unsigned int* __restrict__ collide) {
+                                                            unsigned int* __restrict__ collide,
+                                                            uint32_t* __restrict__ fsl) {
     const int L = ss.L;
     uint32_t want = 0, cbits = 0;
     WalkItem it[kLinkIPT];
@@ -406,6 +407,7 @@ __global__ __launch_bounds__(kBlock) void chain_link_kernel(View v, const uint64
         if (j >= P) continue;
         Mhe<MG> A, B;
         probe_of<MG, View>(v, probe_info, j, gt, mp, L, A);
+        if (fsl) fsl[j] = (uint32_t)start_at(A, first_start(A));
         bool same = false;
         if (j + 1 < P) {
             probe_of<MG, View>(v, probe_info, j + 1, gt, mp, L, B);
@@ -633,7 +635,7 @@ __global__ __launch_bounds__(kBlock) void chain_seg_kernel(const uint8_t* __rest
                                                            const int64_t* __restrict__ rcol,
                                                            uint32_t* __restrict__ chain_of,
                                                            int64_t* __restrict__ seg_r, uint32_t* __restrict__ fk,
-                                                           uint32_t kbase) {
+                                                           uint32_t kbase, uint32_t* __restrict__ jl) {
     const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     const int lane = threadIdx.x & 63;
     uint32_t s = 0xFFFFFFFFu, m = 0xFFFFFFFFu;
@@ -641,7 +643,11 @@ __global__ __launch_bounds__(kBlock) void chain_seg_kernel(const uint8_t* __rest
         const uint32_t f = (j == 0 || !link[j - 1]) ? 1u : 0u;
         s = seg_excl[j] + f - 1u;
         m = ord[j];
-        chain_of[m] = s;
+        if (chain_of) chain_of[m] = s;
+        if (jl) {
+            jl[j] = s;
+            jl[P + j] = m;
+        }
         if (!link[j]) seg_r[s] = rcol[j];
     }
     #pragma unroll
@@ -972,7 +978,7 @@ template <int MG, typename LV>
 hipError_t chains_core(LV vl, const ChainWs& w, const uint32_t* ord, uint64_t P, const GenomeTable& gt,
                        const MatchParams& mp, const SeedSpec& ss, const uint32_t* packed, void* d_scan_tmp,
                        uint32_t* chain_of, int64_t* pool, uint32_t* d_nchains, hipStream_t st, void* ctr,
-                       hipEvent_t* ev_walk, uint32_t* fk, uint32_t kbase) {
+                       hipEvent_t* ev_walk, uint32_t* fk, uint32_t kbase, uint32_t* jl) {
     hipError_t e;
     const unsigned grid = grid_of(P);
     const unsigned walk_grid = 2048, short_grid = 8192;
@@ -985,7 +991,7 @@ hipError_t chains_core(LV vl, const ChainWs& w, const uint32_t* ord, uint64_t P,
         const unsigned lgrid = (unsigned)((P + kBlock * kLinkIPT - 1) / (kBlock * kLinkIPT));
         if (pass == 0)
             hipLaunchKernelGGL((chain_link_kernel<MG, LV>), dim3(lgrid), dim3(kBlock), 0, st, vl, nullptr, P, gt,
-                               mp, ss, w.link, w.queue, qshort, qcount + 12);
+                               mp, ss, w.link, w.queue, qshort, qcount + 12, jl ? jl + 2 * P : nullptr);
         else
             hipLaunchKernelGGL(chain_left_kernel, dim3(lgrid), dim3(kBlock), 0, st, P, (const uint8_t*)w.link, w.queue,
                                qshort);
@@ -1014,7 +1020,7 @@ hipError_t chains_core(LV vl, const ChainWs& w, const uint32_t* ord, uint64_t P,
     if ((e = exclusive_scan_u32(w.seg, P, d_scan_tmp, d_nchains, st)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(fk, 0xFF, P * 4, st)) != hipSuccess) return e;
     hipLaunchKernelGGL(chain_seg_kernel, dim3(grid), dim3(kBlock), 0, st, w.link, ord, w.seg, P, w.rcol, chain_of,
-                       w.seg_r, fk, kbase);
+                       w.seg_r, fk, kbase, jl);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL((chain_entry_kernel<MG, LV>), dim3(grid), dim3(kBlock), 0, st, vl, nullptr, P, gt, mp,
                        ss.L, ord, w.link, w.seg, w.lcol, w.seg_r, pool);
@@ -1089,7 +1095,8 @@ template <int MG, typename View>
 hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const GenomeTable& gt, const MatchParams& mp,
                          const SeedSpec& ss, const uint32_t* packed, void* d_chain_tmp, void* d_scan_tmp,
                          void* d_radix_tmp, uint32_t* chain_of, int64_t* pool, uint32_t* d_nchains, hipStream_t st,
-                         void* ctr, hipEvent_t* ev_walk, uint32_t* fk, uint32_t kbase, bool lkey_ready) {
+                         void* ctr, hipEvent_t* ev_walk, uint32_t* fk, uint32_t kbase, bool lkey_ready,
+                         uint32_t* jl) {
     if (P == 0) return hipSuccess;
     const ChainWs w = chain_ws(d_chain_tmp, P, gt.G, true);
     hipError_t e;
@@ -1117,14 +1124,14 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
                 if ((r = hipGetLastError()) != hipSuccess) return r;
                 LineRows vl{(const int32_t*)w.rows_line, line_row_stride(gt.G), ss.L};
                 return chains_core<MG>(vl, w, o, P, gt, mp, ss, packed, d_scan_tmp, chain_of, pool, d_nchains, st, ctr,
-                                       ev_walk, fk, kbase);
+                                       ev_walk, fk, kbase, jl);
             }
         }
         if ((r = launch_gather_rows(v.rows, o, P, gt.G, w.rows_line, st)) != hipSuccess) return r;
         MatProbes vl{};
         vl.rows = w.rows_line;
         return chains_core<MG>(vl, w, o, P, gt, mp, ss, packed, d_scan_tmp, chain_of, pool, d_nchains, st, ctr, ev_walk,
-                               fk, kbase);
+                               fk, kbase, jl);
     };
     unsigned hf[2] = {0, 0};
     auto read_flags = [&]() -> hipError_t {
@@ -1152,7 +1159,7 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
     template hipError_t launch_chains<MG, V>(V, const uint64_t*, uint64_t, const GenomeTable&, const MatchParams&, \
                                              const SeedSpec&, const uint32_t*, void*, void*, void*, uint32_t*,     \
                                              int64_t*, uint32_t*, hipStream_t, void*, hipEvent_t*, uint32_t*,    \
-                                             uint32_t, bool);
+                                             uint32_t, bool, uint32_t*);
 MUMS_INST_CHAINS(4, MatProbes)
 MUMS_INST_CHAINS(8, MatProbes)
 MUMS_INST_CHAINS(16, MatProbes)

@@ -306,11 +306,13 @@ int find_rows(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const MatchPar
     DevCounters* dc = ctx->counters.as<DevCounters>();
     const uint64_t P = ctx->P;
     HIPCHK(ctx->fk.ensure((P + 1) * 4));
+    // chain / probe / first start per line position in ctx->chain_of (3 P words, find_tail):
+    // the replay's keep pass reads them in line order, no per-probe chain id is scattered
     HIPCHK((launch_chains<MG, MatProbes>(v, nullptr, P, ctx->gt, mp, ctx->ss, packed,
-                                    ctx->chain_tmp.p, ctx->tmp.p, ctx->radix_tmp.p, ctx->chain_of.as<uint32_t>(),
+                                    ctx->chain_tmp.p, ctx->tmp.p, ctx->radix_tmp.p, nullptr,
                                     ctx->pool.as<int64_t>(), &dc->nchains, st, dc,
                                     ctx->profiling ? ctx->ev_walk : nullptr, ctx->fk.as<uint32_t>(), 0u,
-                                    v.fs != nullptr)));
+                                    v.fs != nullptr, ctx->chain_of.as<uint32_t>())));
     return find_replay<MG>(ctx, v, mp, st);
 }
 
@@ -337,11 +339,11 @@ int find_replay(mums_ctx* ctx, MatProbes v, const MatchParams& mp, hipStream_t s
     }
     // the fullest bucket's vector in LDS when it fits (it holds <= its probes)
     const uint32_t lds_cap = std::max<uint32_t>(64, std::min<uint32_t>(ctx->hc.max_bucket, kReplayLdsIds));
-    HIPCHK((launch_replay_kept<MG, MatProbes>(v, ctx->gt, mp, ctx->L, P, ctx->pool.as<int64_t>(),
-                                         ctx->chain_of.as<uint32_t>(), ctx->fk.as<uint32_t>(), ctx->hc.nchains,
+    HIPCHK((launch_replay_kept<MG, MatProbes>(v, ctx->gt, mp, ctx->L, P, ctx->pool.as<int64_t>(), nullptr,
+                                         ctx->fk.as<uint32_t>(), ctx->hc.nchains,
                                          ctx->chain_tmp.p, ctx->radix_tmp.p, ctx->tmp.p, lds_cap,
                                          ctx->tsize.as<uint32_t>(), ctx->counters.p, dbg, st, mlog, &ctx->emit_tbl,
-                                         &ctx->emit_base, devbuf_alloc, &ctx->cbuf)));
+                                         &ctx->emit_base, devbuf_alloc, &ctx->cbuf, ctx->chain_of.as<uint32_t>())));
     if (mlog) {   // the inserts in AddHashEntry call order (probe index << 32 | chain)
         HIPCHK(hipMemcpyAsync(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
@@ -526,7 +528,7 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
     HIPCHK(ctx->obase.ensure((size_t)Tb * 4 + 64));
     if (ctx->P >= (1ull << 32) - 64) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed probes in one FindMatches");
     const bool chunked = ctx->P > find_chunk() && !ctx->pcompat;
-    HIPCHK(ctx->chain_of.ensure((ctx->P + 1) * 4));
+    HIPCHK(ctx->chain_of.ensure((ctx->P + 1) * (chunked ? 4 : 12)));   // find_rows: 3 words per line position
     // the replay keeps only the chain-first / suspicious probes (launch_replay_kept): its
     // summaries, bucket vectors and spill live in ctx->cbuf, sized by their count
     for (DevBuf* b : {&ctx->tbl, &ctx->spill, &ctx->summ}) b->release();

@@ -250,7 +250,8 @@ hipError_t launch_replay_kept(View v, const GenomeTable& gt, const MatchParams& 
                               const int64_t* pool, const uint32_t* chain_of, const uint32_t* fk, uint32_t nch,
                               void* d_tmp, void* d_radix_tmp, void* d_scan_tmp, uint32_t lds_cap, uint32_t* tsize,
                               void* ctr, uint64_t* dbg, hipStream_t st, uint64_t* mlog, uint32_t** tbl_out,
-                              const uint32_t** base_out, void* (*alloc)(void*, size_t), void* alloc_ctx);
+                              const uint32_t** base_out, void* (*alloc)(void*, size_t), void* alloc_ctx,
+                              const uint32_t* jl = nullptr);
 // chains.hip: chain labelling of the probes (key order) before the replay
 // context accessors for the multi-GPU orchestration (shard_comm.hip; mums_capi.hip)
 }  // namespace mums
@@ -299,7 +300,11 @@ template <int MG, typename View>
 hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const GenomeTable& gt, const MatchParams& mp,
                          const SeedSpec& ss, const uint32_t* packed, void* d_chain_tmp, void* d_scan_tmp,
                          void* d_radix_tmp, uint32_t* chain_of, int64_t* pool, uint32_t* d_nchains, hipStream_t st,
-                         void* ctr, hipEvent_t* ev_walk, uint32_t* fk, uint32_t kbase, bool lkey_ready = false);
+                         void* ctr, hipEvent_t* ev_walk, uint32_t* fk, uint32_t kbase, bool lkey_ready = false,
+                         uint32_t* jl = nullptr);
+// jl (3 P words, optional): per line position j the chain, the probe (key order) and its
+// first-genome start -- the replay's keep pass then reads them in line order and chain_of
+// (a random scatter) is not written (chain_of may be null)
 // where launch_chains(d_chain_tmp, P probes, G) reads the line keys from: a producer that
 // writes them there (launch_materialize) lets launch_chains skip its key pass (lkey_ready)
 uint64_t* chain_lkey_slot(void* d_chain_tmp, uint64_t P, int G);

@@ -1415,11 +1415,13 @@ __global__ __launch_bounds__(kBlock) void keep_fill_kernel(const int64_t* __rest
                                                            const uint4* __restrict__ ck,
                                                            unsigned int* __restrict__ nkept, uint64_t cap,
                                                            uint64_t* __restrict__ kept,
-                                                           const uint32_t* __restrict__ fsk) {
+                                                           const uint32_t* __restrict__ fsk,
+                                                           uint32_t* __restrict__ kcid) {
     __shared__ uint32_t s_w[kBlock / 64 + 1];
     __shared__ int64_t srow[kBlock * kKeepStageW];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint64_t keys[kKeepIPT];
+    uint32_t cids[kKeepIPT];
     uint32_t want = 0;
     const int W = G + 1;
     const bool staged = W <= kKeepStageW;   // uniform
@@ -1428,9 +1430,10 @@ __global__ __launch_bounds__(kBlock) void keep_fill_kernel(const int64_t* __rest
         const uint64_t k0 = (uint64_t)blockIdx.x * (kBlock * kKeepIPT) + (uint64_t)i * kBlock;
         const uint64_t k = k0 + threadIdx.x;
         keys[i] = 0;
+        cids[i] = k < P ? chain_of[k] : 0u;
         if (fsk) {   // first-genome starts in key order (rows stored in line order)
             if (k < P) {
-                const uint4 c = ck[chain_of[k]];
+                const uint4 c = ck[cids[i]];
                 const bool keep = c.x == (uint32_t)k || fsk[k] >= c.y;
                 keys[i] = ((uint64_t)c.z << 32) | k;
                 if (keep) want |= 1u << i;
@@ -1445,7 +1448,7 @@ __global__ __launch_bounds__(kBlock) void keep_fill_kernel(const int64_t* __rest
             }
             __syncthreads();
             if (k < P) {
-                const uint4 c = ck[chain_of[k]];
+                const uint4 c = ck[cids[i]];
                 bool keep = c.x == (uint32_t)k;
                 if (!keep) {
                     uint32_t fs = 0;
@@ -1483,7 +1486,67 @@ __global__ __launch_bounds__(kBlock) void keep_fill_kernel(const int64_t* __rest
     #pragma unroll
     for (int i = 0; i < kKeepIPT; ++i)
         if ((want >> i) & 1u) {
-            if (o < cap) kept[o] = keys[i];
+            if (o < cap) {
+                kept[o] = keys[i];
+                kcid[o] = cids[i];
+            }
+            ++o;
+        }
+}
+
+// the same from the chains' line-order arrays (launch_chains jl): chain, probe and first
+// start of line position j, read in line order -- the chain summaries ck[s] are read in chain
+// order and no per-probe chain id is gathered
+__global__ __launch_bounds__(kBlock) void keep_fill_line_kernel(const uint32_t* __restrict__ jl, uint64_t P,
+                                                                const uint4* __restrict__ ck,
+                                                                unsigned int* __restrict__ nkept, uint64_t cap,
+                                                                uint64_t* __restrict__ kept,
+                                                                uint32_t* __restrict__ kcid) {
+    __shared__ uint32_t s_w[kBlock / 64 + 1];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint64_t keys[kKeepIPT];
+    uint32_t cids[kKeepIPT];
+    uint32_t want = 0;
+    #pragma unroll
+    for (int i = 0; i < kKeepIPT; ++i) {
+        const uint64_t j = (uint64_t)blockIdx.x * (kBlock * kKeepIPT) + (uint64_t)i * kBlock + threadIdx.x;
+        keys[i] = 0;
+        cids[i] = 0;
+        if (j < P) {
+            const uint32_t s = jl[j], k = jl[P + j];
+            const uint4 c = ck[s];
+            if (c.x == k || jl[2 * P + j] >= c.y) want |= 1u << i;
+            keys[i] = ((uint64_t)c.z << 32) | k;
+            cids[i] = s;
+        }
+    }
+    const uint32_t n = (uint32_t)__builtin_popcount(want);
+    uint32_t x = n;
+    #pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) s_w[wv] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) {
+            const uint32_t c = s_w[w];
+            s_w[w] = tot;
+            tot += c;
+        }
+        s_w[kBlock / 64] = tot ? atomicAdd(nkept, tot) : 0u;
+    }
+    __syncthreads();
+    uint64_t o = (uint64_t)s_w[kBlock / 64] + s_w[wv] + x - n;
+    #pragma unroll
+    for (int i = 0; i < kKeepIPT; ++i)
+        if ((want >> i) & 1u) {
+            if (o < cap) {
+                kept[o] = keys[i];
+                kcid[o] = cids[i];
+            }
             ++o;
         }
 }
@@ -1494,7 +1557,7 @@ __global__ __launch_bounds__(kBlock) void keep_fill_kernel(const int64_t* __rest
 template <int MG, typename View>
 __global__ __launch_bounds__(kBlock) void kept_summary_kernel(View v, GenomeTable gt, int L,
                                                               const uint64_t* __restrict__ skey, uint32_t Kc,
-                                                              const uint32_t* __restrict__ chain_of,
+                                                              const uint32_t* __restrict__ scid,
                                                               const uint32_t* __restrict__ fk,
                                                               const uint4* __restrict__ chain_sb,
                                                               const uint32_t* __restrict__ bkey,
@@ -1504,7 +1567,7 @@ __global__ __launch_bounds__(kBlock) void kept_summary_kernel(View v, GenomeTabl
     const uint32_t k = (uint32_t)skey[i];
     Mhe<MG> Q;
     load_probe<MG>(v, k, gt.G, L, Q);
-    const uint32_t cid = chain_of[k];
+    const uint32_t cid = scid[i];
     const uint4 cs = chain_sb[cid];
     const bool first = fk[cid] == k;
     summ[i] = make_uint4(block_key<MG>(Q, gt.G, bkey, cid), (uint32_t)start_at(Q, first_start(Q)), cid,
@@ -1529,7 +1592,8 @@ hipError_t launch_replay_kept(View v, const GenomeTable& gt, const MatchParams& 
                               const int64_t* pool, const uint32_t* chain_of, const uint32_t* fk, uint32_t nch,
                               void* d_tmp, void* d_radix_tmp, void* d_scan_tmp, uint32_t lds_cap, uint32_t* tsize,
                               void* ctr, uint64_t* dbg, hipStream_t st, uint64_t* mlog, uint32_t** tbl_out,
-                              const uint32_t** base_out, void* (*alloc)(void*, size_t), void* alloc_ctx) {
+                              const uint32_t** base_out, void* (*alloc)(void*, size_t), void* alloc_ctx,
+                              const uint32_t* jl) {
     char* p = (char*)d_tmp;
     auto carve = [&](size_t bytes) {
         char* r = p;
@@ -1588,13 +1652,18 @@ hipError_t launch_replay_kept(View v, const GenomeTable& gt, const MatchParams& 
     for (int attempt = 0; attempt < 2; ++attempt) {
         const uint64_t K1 = cap + 1;
         const size_t rtmp = radix_tmp_bytes(K1);
-        cb = (char*)alloc(alloc_ctx, K1 * (8 * 3 + 4 * 2 + 16 * 3 + 4) + ((uint64_t)Tb + 64) * 8 + rtmp +
+        cb = (char*)alloc(alloc_ctx, K1 * (8 * 3 + 4 * 3 + 16 * 3 + 4) + ((uint64_t)Tb + 64) * 8 + rtmp +
                                          replay_scratch_bytes(cap, Tb) + 16 * 256);
         if (!cb) return hipErrorOutOfMemory;
         kept = (uint64_t*)cb;
+        uint32_t* kcid = (uint32_t*)(cb + ((K1 * 8 + 255) & ~(uint64_t)255));
         if ((e = hipMemsetAsync(nkept, 0, 4, st)) != hipSuccess) return e;
-        hipLaunchKernelGGL(keep_fill_kernel, dim3((unsigned)nblk), dim3(kBlock), 0, st, v.rows, P, G, chain_of,
-                           (const uint4*)ckeep, nkept, cap, kept, v.fs);
+        if (jl)
+            hipLaunchKernelGGL(keep_fill_line_kernel, dim3((unsigned)nblk), dim3(kBlock), 0, st, jl, P,
+                               (const uint4*)ckeep, nkept, cap, kept, kcid);
+        else
+            hipLaunchKernelGGL(keep_fill_kernel, dim3((unsigned)nblk), dim3(kBlock), 0, st, v.rows, P, G, chain_of,
+                               (const uint4*)ckeep, nkept, cap, kept, v.fs, kcid);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if ((e = hipMemcpyAsync(&Kc, nkept, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
@@ -1605,6 +1674,7 @@ hipError_t launch_replay_kept(View v, const GenomeTable& gt, const MatchParams& 
     const size_t rtmp = radix_tmp_bytes(K1);
     p = cb;
     carve(K1 * 8);   // kept
+    uint32_t* kcid = (uint32_t*)carve(K1 * 4);   // their chains
     uint64_t* sA = (uint64_t*)carve(K1 * 8);
     uint64_t* sB = (uint64_t*)carve(K1 * 8);
     uint32_t* iA = (uint32_t*)carve(K1 * 4);
@@ -1620,16 +1690,18 @@ hipError_t launch_replay_kept(View v, const GenomeTable& gt, const MatchParams& 
     *tbl_out = tbl;
     *base_out = cbeg;
     const uint64_t* skey = kept;
+    const uint32_t* scid = kcid;
     if (Kc > 1) {
         int b3 = 0;
-        if ((e = radix_sort<uint64_t>(kept, nullptr, Kc, 32 + tbits, sA, iA, sB, iB, rt, &b3, st)) != hipSuccess)
+        if ((e = radix_sort<uint64_t>(kept, kcid, Kc, 32 + tbits, sA, iA, sB, iB, rt, &b3, st)) != hipSuccess)
             return e;
         skey = b3 ? sB : sA;
+        scid = b3 ? iB : iA;
     }
     if ((e = hipMemsetAsync(cbeg, 0, ((uint64_t)Tb + 32) * 4, st)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(cend, 0, ((uint64_t)Tb + 32) * 4, st)) != hipSuccess) return e;
     const unsigned kgrid = (unsigned)((Kc + 1 + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL((kept_summary_kernel<MG, View>), dim3(kgrid), dim3(kBlock), 0, st, v, gt, L, skey, Kc, chain_of,
+    hipLaunchKernelGGL((kept_summary_kernel<MG, View>), dim3(kgrid), dim3(kBlock), 0, st, v, gt, L, skey, Kc, scid,
                        fk, (const uint4*)chain_sb, bkey, summ_c, summ_bc);
     hipLaunchKernelGGL(kept_ranges_kernel, dim3(kgrid), dim3(kBlock), 0, st, skey, Kc, cbeg, cend, P,
                        (DevCounters*)ctr);
@@ -1651,7 +1723,7 @@ hipError_t launch_emit(const uint32_t* obase, const uint32_t* bstart, const uint
                                                   const int64_t*, const uint32_t*, const uint32_t*, uint32_t, void*,  \
                                                   void*, void*, uint32_t, uint32_t*, void*, uint64_t*, hipStream_t,   \
                                                   uint64_t*, uint32_t**, const uint32_t**, void* (*)(void*, size_t),  \
-                                                  void*);
+                                                  void*, const uint32_t*);
 MUMS_INST_REPLAY_KEPT(4, MatProbes)
 MUMS_INST_REPLAY_KEPT(8, MatProbes)
 MUMS_INST_REPLAY_KEPT(16, MatProbes)
