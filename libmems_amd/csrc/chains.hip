@@ -340,14 +340,19 @@ __device__ int64_t walk_lane(int dir, int64_t cur, int64_t stop, int budget, con
 template <int MG, typename View>
 __global__ __launch_bounds__(kBlock) void chain_key_kernel(View v, const uint64_t* __restrict__ probe_info, uint64_t P,
                                                            GenomeTable gt, MatchParams mp, int L,
-                                                           uint64_t* __restrict__ lkey) {
+                                                           uint64_t* __restrict__ lkey, uint32_t* __restrict__ lhash) {
     const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (k >= P) return;
     Mhe<MG> Q;
     probe_of<MG, View>(v, probe_info, (uint32_t)k, gt, mp, L, Q);
     const int ref = first_start(Q);
     const uint64_t x = (uint64_t)start_at(Q, ref);
-    lkey[k] = ((uint64_t)line_hash<MG>(Q, gt.G) << 32) | (x & 0xFFFFFFFFull);
+    if (lhash) {   // line_sort's first records and the hashes apart (chain_line_slots)
+        lkey[k] = (x << 32) | k;
+        lhash[k] = line_hash<MG>(Q, gt.G);
+    } else {
+        lkey[k] = ((uint64_t)line_hash<MG>(Q, gt.G) << 32) | (x & 0xFFFFFFFFull);
+    }
 }
 
 constexpr uint64_t kCollideScan = 4096;   // probes scanned after a line-hash collision
@@ -691,19 +696,14 @@ __global__ __launch_bounds__(kBlock) void chain_entry_kernel(View v, const uint6
 }
 
 // ---- line order: (line hash, reference start) by two stable onesweep sorts -------------
-// of packed 8-B records (radix_seg.hip): first (x << 32 | k) by x, then
-// (hash << 32 | position after the first sort) by hash; ord[j] = the probe at line position j
-__global__ __launch_bounds__(kBlock) void line_rec1_kernel(const uint64_t* __restrict__ lkey, uint64_t P,
-                                                           uint64_t* __restrict__ rec) {
-    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (k < P) rec[k] = (lkey[k] << 32) | k;
-}
-
-__global__ __launch_bounds__(kBlock) void line_rec2_kernel(const uint64_t* __restrict__ lkey,
+// of packed 8-B records (radix_seg.hip): first (x << 32 | k) by x (written by the probe
+// producer, chain_line_slots), then (hash << 32 | position after the first sort) by hash;
+// ord[j] = the probe at line position j
+__global__ __launch_bounds__(kBlock) void line_rec2_kernel(const uint32_t* __restrict__ lhash,
                                                            const uint64_t* __restrict__ s1, uint64_t P,
                                                            uint64_t* __restrict__ rec) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < P) rec[i] = (lkey[(uint32_t)s1[i]] & 0xFFFFFFFF00000000ull) | i;
+    if (i < P) rec[i] = ((uint64_t)lhash[(uint32_t)s1[i]] << 32) | i;
 }
 
 __global__ __launch_bounds__(kBlock) void line_ord_kernel(const uint64_t* __restrict__ s1,
@@ -941,20 +941,19 @@ ChainWs chain_ws(void* d_chain_tmp, uint64_t P, int G, bool with_rows) {
     return w;
 }
 
-// line order of the P probes from w.lkey (hash << 32 | x): ord[j] (in w.vA) = the probe at
-// line position j.  Two stable onesweep sorts of packed records (by x on xbits bits, then
-// by hash) instead of eight 8-bit passes over 12-B (key, value) pairs.  lkey is consumed.
+// line order of the P probes from the records (x << 32 | k) in w.kA and the line hashes in
+// w.vB: ord[j] (in w.vA) = the probe at line position j.  Two stable onesweep sorts of packed
+// records (by x on xbits bits, then by hash) instead of eight 8-bit passes over 12-B
+// (key, value) pairs.  w.lkey is the second sort's ping-pong buffer.
 hipError_t line_sort(const ChainWs& w, uint64_t P, int xbits, void* d_tmp, uint32_t* d_err, hipStream_t st,
                      const uint32_t** ord_out) {
     hipError_t e;
     if ((e = seg_bucket_starts(nullptr, 0, 0, P, w.bst, st)) != hipSuccess) return e;
-    hipLaunchKernelGGL(line_rec1_kernel, dim3(grid_of(P)), dim3(kBlock), 0, st, w.lkey, P, w.kA);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
     int b1 = 0;
     if ((e = seg_onesweep_sort(w.kA, w.kB, P, xbits, 0, w.bst, d_tmp, d_err, &b1, st)) != hipSuccess) return e;
     const uint64_t* s1 = b1 ? w.kB : w.kA;
     uint64_t* r2 = b1 ? w.kA : w.kB;
-    hipLaunchKernelGGL(line_rec2_kernel, dim3(grid_of(P)), dim3(kBlock), 0, st, w.lkey, s1, P, r2);
+    hipLaunchKernelGGL(line_rec2_kernel, dim3(grid_of(P)), dim3(kBlock), 0, st, (const uint32_t*)w.vB, s1, P, r2);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     int b2 = 0;
     if ((e = seg_onesweep_sort(r2, w.lkey, P, kLineHashBits, 0, w.bst, d_tmp, d_err, &b2, st)) != hipSuccess) return e;
@@ -1027,15 +1026,23 @@ hipError_t chains_core(LV vl, const ChainWs& w, const uint32_t* ord, uint64_t P,
     return hipGetLastError();
 }
 
+}  // namespace
+
 // the line order: onesweep records when the reference starts fit 32 bits and P < 2^30
 // (MUMS_DEV_LINE_RADIX: the 64-bit pair sort), else 64-bit (key, value) radix passes
-hipError_t line_order(const ChainWs& w, uint64_t P, const GenomeTable& gt, void* d_tmp, void* ctr, hipStream_t st,
-                      const uint32_t** ord) {
+bool chain_line_records(uint64_t P, const GenomeTable& gt) {
     static const bool pairs = getenv("MUMS_DEV_LINE_RADIX") != nullptr;
     uint64_t mx = 0;
     for (int g = 0; g < gt.G; ++g) mx = gt.n[g] > mx ? gt.n[g] : mx;
-    if (!pairs && ctr && P < (1ull << 30) && mx + 2 < (1ull << 32))
-        return line_sort(w, P, x_bits(gt), d_tmp, &((DevCounters*)ctr)->err, st, ord);
+    return !pairs && P < (1ull << 30) && mx + 2 < (1ull << 32);
+}
+
+namespace {
+
+hipError_t line_order(const ChainWs& w, uint64_t P, const GenomeTable& gt, void* d_tmp, void* ctr, hipStream_t st,
+                      const uint32_t** ord) {
+    if (chain_line_records(P, gt))
+        return line_sort(w, P, x_bits(gt), d_tmp, ctr ? &((DevCounters*)ctr)->err : w.qcount + 14, st, ord);
     int buf = 0;
     hipError_t e = radix_sort<uint64_t>(w.lkey, nullptr, P, 64, w.kA, w.vA, w.kB, w.vB, d_tmp, &buf, st);
     *ord = buf ? w.vB : w.vA;
@@ -1087,6 +1094,12 @@ hipError_t line_order_exact(MatProbes v, const ChainWs& w, uint64_t P, const Gen
 
 uint64_t* chain_lkey_slot(void* d_chain_tmp, uint64_t P, int G) { return chain_ws(d_chain_tmp, P, G, true).lkey; }
 
+void chain_line_slots(void* d_chain_tmp, uint64_t P, int G, uint64_t** rec, uint32_t** lhash) {
+    const ChainWs w = chain_ws(d_chain_tmp, P, G, true);
+    *rec = w.kA;
+    *lhash = w.vB;
+}
+
 size_t chain_radix_tmp_bytes(uint64_t P) { return std::max(radix_tmp_bytes(P), onesweep_tmp_bytes(P, 0, 32)); }
 
 // Chain labelling of the P probes (key order): chain_of[k] = chain of probe k;
@@ -1101,8 +1114,9 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
     const ChainWs w = chain_ws(d_chain_tmp, P, gt.G, true);
     hipError_t e;
     if (!lkey_ready) {   // else written by the materialize pass (chain_lkey_slot)
+        const bool recs = chain_line_records(P, gt);
         hipLaunchKernelGGL((chain_key_kernel<MG, View>), dim3(grid_of(P)), dim3(kBlock), 0, st, v, probe_info, P, gt,
-                           mp, ss.L, w.lkey);
+                           mp, ss.L, recs ? w.kA : w.lkey, recs ? w.vB : nullptr);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     const uint32_t* ord = nullptr;

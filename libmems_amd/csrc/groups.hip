@@ -377,7 +377,7 @@ template <int MG, typename View>
 __global__ __launch_bounds__(kBlock) void probe_materialize_kernel(View v, const uint64_t* __restrict__ probe_info,
                                                                    uint64_t P, GenomeTable gt, MatchParams mp, int L,
                                                                    int64_t* __restrict__ rows, uint64_t* __restrict__ lkey,
-                                                                   uint32_t* __restrict__ fsk) {
+                                                                   uint32_t* __restrict__ fsk, uint32_t* __restrict__ lhash) {
     const uint64_t k0 = (uint64_t)blockIdx.x * kBlock;
     const uint64_t k = k0 + threadIdx.x;
     const int W = gt.G + 1;
@@ -402,7 +402,12 @@ __global__ __launch_bounds__(kBlock) void probe_materialize_kernel(View v, const
         }
         if (lkey) {
             const uint64_t xs = (uint64_t)start_at(Q, first_start(Q));
-            lkey[k] = ((uint64_t)line_hash<MG>(Q, gt.G) << 32) | (xs & 0xFFFFFFFFull);
+            if (lhash) {   // the line sort's first records (chain_line_slots) and the hashes apart
+                lkey[k] = (xs << 32) | k;
+                lhash[k] = line_hash<MG>(Q, gt.G);
+            } else {
+                lkey[k] = ((uint64_t)line_hash<MG>(Q, gt.G) << 32) | (xs & 0xFFFFFFFFull);
+            }
             fsk[k] = (uint32_t)xs;
         }
     }
@@ -511,10 +516,10 @@ uint64_t group_blocks(uint64_t ntiles, bool packed) { return packed ? ntiles * k
 template <int MG, typename View>
 hipError_t launch_materialize(View v, const uint64_t* probe_info, uint64_t P, const GenomeTable& gt,
                               const MatchParams& mp, int L, int64_t* rows, hipStream_t st, uint64_t* lkey,
-                              uint32_t* fsk) {
+                              uint32_t* fsk, uint32_t* lhash) {
     if (P == 0) return hipSuccess;
     hipLaunchKernelGGL((probe_materialize_kernel<MG, View>), dim3((unsigned)((P + kBlock - 1) / kBlock)), dim3(kBlock),
-                       0, st, v, probe_info, P, gt, mp, L, rows, lkey, fsk);
+                       0, st, v, probe_info, P, gt, mp, L, rows, lkey, fsk, lhash);
     return hipGetLastError();
 }
 
@@ -583,7 +588,7 @@ MUMS_INST_PROBE(64, PairView<uint64_t>)
 #define MUMS_INST_MAT(MG, V)                                                                                      \
     template hipError_t launch_materialize<MG, V>(V, const uint64_t*, uint64_t, const GenomeTable&,                \
                                                   const MatchParams&, int, int64_t*, hipStream_t, uint64_t*,      \
-                                                  uint32_t*);
+                                                  uint32_t*, uint32_t*);
 MUMS_INST_MAT(4, PairView<uint32_t>)
 MUMS_INST_MAT(8, PairView<uint32_t>)
 MUMS_INST_MAT(16, PairView<uint32_t>)

@@ -493,11 +493,13 @@ int materialize_dispatch(mums_ctx* ctx, View sv, const MatchParams& mp, hipStrea
     }
     uint64_t* lk = ctx->fused_keys ? chain_lkey_slot(ctx->chain_tmp.p, P, G) : nullptr;
     uint32_t* fs = ctx->fused_keys ? ctx->fsk.as<uint32_t>() : nullptr;
-    if (G <= 4) HIPCHK((launch_materialize<4, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st, lk, fs)));
-    else if (G <= 8) HIPCHK((launch_materialize<8, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st, lk, fs)));
-    else if (G <= 16) HIPCHK((launch_materialize<16, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st, lk, fs)));
-    else if (G <= 32) HIPCHK((launch_materialize<32, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st, lk, fs)));
-    else HIPCHK((launch_materialize<64, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st, lk, fs)));
+    uint32_t* lh = nullptr;   // the line sort's records and hashes instead of the line keys
+    if (ctx->fused_keys && chain_line_records(P, ctx->gt)) chain_line_slots(ctx->chain_tmp.p, P, G, &lk, &lh);
+    if (G <= 4) HIPCHK((launch_materialize<4, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st, lk, fs, lh)));
+    else if (G <= 8) HIPCHK((launch_materialize<8, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st, lk, fs, lh)));
+    else if (G <= 16) HIPCHK((launch_materialize<16, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st, lk, fs, lh)));
+    else if (G <= 32) HIPCHK((launch_materialize<32, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st, lk, fs, lh)));
+    else HIPCHK((launch_materialize<64, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st, lk, fs, lh)));
     return MUMS_OK;
 }
 

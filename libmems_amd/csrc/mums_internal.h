@@ -227,10 +227,12 @@ hipError_t launch_bucket_records(const uint32_t* b, uint64_t P, uint64_t* rec, h
 hipError_t launch_bucket_split(const uint64_t* rec, uint64_t P, uint32_t* b, uint32_t* ids, hipStream_t st);
 // probes (key order) -> materialized rows (MatProbes, match_device.h)
 template <int MG, typename View>
-// lkey / fsk (optional): each probe's line key (chain_lkey_slot) and first-genome start
+// lkey / fsk (optional): each probe's line key (chain_lkey_slot) and first-genome start;
+// with lhash the line sort's first records (x << 32 | k) go to lkey and the line hashes to
+// lhash (chain_line_slots)
 hipError_t launch_materialize(View v, const uint64_t* probe_info, uint64_t P, const GenomeTable& gt,
                               const MatchParams& mp, int L, int64_t* rows, hipStream_t st, uint64_t* lkey = nullptr,
-                              uint32_t* fsk = nullptr);
+                              uint32_t* fsk = nullptr, uint32_t* lhash = nullptr);
 // hash bucket of every row (d_bounds == nullptr) or its owning rank (bucket ranges)
 hipError_t launch_row_buckets(const int64_t* rows, uint64_t P, int G, uint32_t table_size, const uint32_t* d_bounds,
                               uint32_t nranks, uint32_t* out, hipStream_t st);
@@ -308,6 +310,10 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
 // where launch_chains(d_chain_tmp, P probes, G) reads the line keys from: a producer that
 // writes them there (launch_materialize) lets launch_chains skip its key pass (lkey_ready)
 uint64_t* chain_lkey_slot(void* d_chain_tmp, uint64_t P, int G);
+// whether launch_chains orders the lines by the onesweep records (given DevCounters); then a
+// producer writes (x << 32 | k) and the line hashes into chain_line_slots instead
+bool chain_line_records(uint64_t P, const GenomeTable& gt);
+void chain_line_slots(void* d_chain_tmp, uint64_t P, int G, uint64_t** rec, uint32_t** lhash);
 hipError_t launch_emit(const uint32_t* obase, const uint32_t* bstart, const uint32_t* tbl, const int64_t* pool, int G,
                        uint32_t table_size, uint64_t M, uint64_t* out_len, int64_t* out_s, hipStream_t st);
 
