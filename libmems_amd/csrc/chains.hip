@@ -767,6 +767,23 @@ __global__ __launch_bounds__(kBlock) void gather_line_rows_kernel(const int64_t*
     if (!ok) atomicOr(bad, 1u);
 }
 
+// int32 rows (MatProbes::rows32) in line order: row ord[j] -> row j, S / 4 int4 per row
+__global__ __launch_bounds__(kBlock) void gather_rows32_kernel(const int32_t* __restrict__ src,
+                                                               const uint32_t* __restrict__ ord, uint64_t P,
+                                                               uint32_t S, int32_t* __restrict__ dst) {
+    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= P) return;
+    const int4* a = reinterpret_cast<const int4*>(src + (uint64_t)ord[j] * S);
+    int4* b = reinterpret_cast<int4*>(dst + j * S);
+    if (S == 8) {
+        const int4 x = a[0], y = a[1];
+        b[0] = x;
+        b[1] = y;
+    } else {
+        for (uint32_t q = 0; q < S / 4; ++q) b[q] = a[q];
+    }
+}
+
 inline unsigned grid_of(uint64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
 // --- chunked FindMatches: chains labelled per slice of the probes ---------------------
@@ -1111,6 +1128,7 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
                          void* ctr, hipEvent_t* ev_walk, uint32_t* fk, uint32_t kbase, bool lkey_ready,
                          uint32_t* jl) {
     if (P == 0) return hipSuccess;
+    if (v.rows32 && !(MG % 4 == 0 && MG <= 16)) return hipErrorInvalidValue;   // int32 rows: G <= 16 only
     const ChainWs w = chain_ws(d_chain_tmp, P, gt.G, true);
     hipError_t e;
     if (!lkey_ready) {   // else written by the materialize pass (chain_lkey_slot)
@@ -1132,6 +1150,14 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
         hipError_t r;
         if ((r = hipMemsetAsync(flags, 0, 8, st)) != hipSuccess) return r;
         if constexpr (MG % 4 == 0 && MG <= 16) {
+            if (v.rows32) {   // int32 rows in key order (materialize_dispatch): copied in line order
+                hipLaunchKernelGGL(gather_rows32_kernel, dim3(grid_of(P)), dim3(kBlock), 0, st, v.rows32, o, P,
+                                   v.stride32, (int32_t*)w.rows_line);
+                if ((r = hipGetLastError()) != hipSuccess) return r;
+                LineRows vl{(const int32_t*)w.rows_line, v.stride32, v.L32};
+                return chains_core<MG>(vl, w, o, P, gt, mp, ss, packed, d_scan_tmp, chain_of, pool, d_nchains, st, ctr,
+                                       ev_walk, fk, kbase, jl);
+            }
             if (narrow) {
                 hipLaunchKernelGGL((gather_line_rows_kernel<MG>), dim3(grid_of(P)), dim3(kBlock), 0, st, v.rows, o, P,
                                    gt.G, ss.L, (int32_t*)w.rows_line, flags + 1);
@@ -1163,8 +1189,8 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
     // multi-probe lines whose x ranges overlap)
     if (!hf[0] && !getenv("MUMS_DEV_LINE_EXACT")) return hipSuccess;
     if (getenv("MUMS_DEV_CHAIN_DEBUG")) fprintf(stderr, "chains: line-hash collision, exact line order\n");
-    MatProbes vk{};
-    vk.rows = v.rows;
+    MatProbes vk = v;
+    vk.fs = nullptr;
     if ((e = line_order_exact<MG>(vk, w, P, gt, d_radix_tmp, st, &ord)) != hipSuccess) return e;
     return chains_from(ord);
 }

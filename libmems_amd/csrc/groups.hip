@@ -377,7 +377,8 @@ template <int MG, typename View>
 __global__ __launch_bounds__(kBlock) void probe_materialize_kernel(View v, const uint64_t* __restrict__ probe_info,
                                                                    uint64_t P, GenomeTable gt, MatchParams mp, int L,
                                                                    int64_t* __restrict__ rows, uint64_t* __restrict__ lkey,
-                                                                   uint32_t* __restrict__ fsk, uint32_t* __restrict__ lhash) {
+                                                                   uint32_t* __restrict__ fsk, uint32_t* __restrict__ lhash,
+                                                                   int32_t* __restrict__ rows32) {
     const uint64_t k0 = (uint64_t)blockIdx.x * kBlock;
     const uint64_t k = k0 + threadIdx.x;
     const int W = gt.G + 1;
@@ -409,6 +410,22 @@ __global__ __launch_bounds__(kBlock) void probe_materialize_kernel(View v, const
                 lkey[k] = ((uint64_t)line_hash<MG>(Q, gt.G) << 32) | (xs & 0xFFFFFFFFull);
             }
             fsk[k] = (uint32_t)xs;
+        }
+    }
+    if constexpr (MG % 4 == 0 && MG <= 16) {
+        if (rows32) {   // uniform: int32 starts (MatProbes::rows32); fsk[P] |= 1 when one does not fit
+            if (k >= P) return;
+            bool ok = probe_offset<MG>(Q, L) == Q.offset;
+            #pragma unroll
+            for (int g = 0; g < MG; ++g) ok = ok && Q.s[g] == (int64_t)(int32_t)Q.s[g];
+            int32_t* out = rows32 + k * (uint64_t)line_row_stride(gt.G);
+            #pragma unroll
+            for (int q = 0; q < MG / 4; ++q)
+                if (4 * q < gt.G)
+                    *reinterpret_cast<int4*>(out + 4 * q) = make_int4((int32_t)Q.s[4 * q], (int32_t)Q.s[4 * q + 1],
+                                                                      (int32_t)Q.s[4 * q + 2], (int32_t)Q.s[4 * q + 3]);
+            if (!ok) atomicOr(fsk + P, 1u);
+            return;
         }
     }
     if constexpr (MG <= 16) {
@@ -516,10 +533,10 @@ uint64_t group_blocks(uint64_t ntiles, bool packed) { return packed ? ntiles * k
 template <int MG, typename View>
 hipError_t launch_materialize(View v, const uint64_t* probe_info, uint64_t P, const GenomeTable& gt,
                               const MatchParams& mp, int L, int64_t* rows, hipStream_t st, uint64_t* lkey,
-                              uint32_t* fsk, uint32_t* lhash) {
+                              uint32_t* fsk, uint32_t* lhash, int32_t* rows32) {
     if (P == 0) return hipSuccess;
     hipLaunchKernelGGL((probe_materialize_kernel<MG, View>), dim3((unsigned)((P + kBlock - 1) / kBlock)), dim3(kBlock),
-                       0, st, v, probe_info, P, gt, mp, L, rows, lkey, fsk, lhash);
+                       0, st, v, probe_info, P, gt, mp, L, rows, lkey, fsk, lhash, rows32);
     return hipGetLastError();
 }
 
@@ -588,7 +605,7 @@ MUMS_INST_PROBE(64, PairView<uint64_t>)
 #define MUMS_INST_MAT(MG, V)                                                                                      \
     template hipError_t launch_materialize<MG, V>(V, const uint64_t*, uint64_t, const GenomeTable&,                \
                                                   const MatchParams&, int, int64_t*, hipStream_t, uint64_t*,      \
-                                                  uint32_t*, uint32_t*);
+                                                  uint32_t*, uint32_t*, int32_t*);
 MUMS_INST_MAT(4, PairView<uint32_t>)
 MUMS_INST_MAT(8, PairView<uint32_t>)
 MUMS_INST_MAT(16, PairView<uint32_t>)

@@ -475,20 +475,17 @@ __device__ __forceinline__ uint32_t line_hash(const Mhe<MG>& P, int G) {
 // CalculateOffset value.  The chain labelling and the replay read probes only through
 // this (one contiguous row per probe instead of G+1 gathers from the record stream);
 // the sharded FindMatches ships the same rows between ranks.
+// rows32 (optional, G <= 16, every start below 2^31): the same rows as G int32 starts (stride32
+// = G rounded up to 4) with the offset recomputed from them (probe_offset, seed length L32) --
+// 32 B per probe at G = 8 instead of 72; the materialize pass checked the recomputation.
+// rows is then null.
 struct MatProbes {
     const int64_t* rows;           // [P][G + 1]
     const uint32_t* fs = nullptr;  // optional: probe k's first-genome start (the replay's keep test)
+    const int32_t* rows32 = nullptr;
+    uint32_t stride32 = 0;
+    int L32 = 0;
 };
-
-template <int MG>
-__device__ __forceinline__ void load_probe(const MatProbes& m, uint64_t k, int G, int L, Mhe<MG>& P) {
-    const int64_t* row = m.rows + k * (uint64_t)(G + 1);
-    P.len = L;
-    P.mersize = L;
-    P.offset = row[G];
-    #pragma unroll
-    for (int g = 0; g < MG; ++g) P.s[g] = (g < G) ? row[g] : 0;
-}
 
 // CalculateOffset of directed starts (the sum build_probe takes, MemHash.cpp:189-203)
 template <int MG>
@@ -502,21 +499,11 @@ __device__ __forceinline__ int64_t probe_offset(const Mhe<MG>& P, int L) {
     return off;
 }
 
-// The chain kernels' copy of the probe rows in line order when every start fits 31 bits:
-// G int32 starts per row (stride G rounded up to 4, 16-B aligned rows) and the offset
-// recomputed from them -- 32 B per probe instead of 72 at G = 8.  The gather that writes
-// it checks the recomputed offset against the materialized one (launch_gather_line_rows).
-struct LineRows {
-    const int32_t* rows;
-    uint32_t stride;
-    int L;   // seed length of the offset sum
-};
-
 __host__ __device__ inline uint32_t line_row_stride(int G) { return (uint32_t)((G + 3) & ~3); }
 
+// one row of int32 starts (16-B aligned, stride a multiple of 4)
 template <int MG>
-__device__ __forceinline__ void load_probe(const LineRows& m, uint64_t k, int G, int L, Mhe<MG>& P) {
-    const int32_t* row = m.rows + k * (uint64_t)m.stride;
+__device__ __forceinline__ void load_probe32(const int32_t* __restrict__ row, int G, int L, int Loff, Mhe<MG>& P) {
     P.len = L;
     P.mersize = L;
     if constexpr (MG % 4 == 0) {
@@ -533,7 +520,36 @@ __device__ __forceinline__ void load_probe(const LineRows& m, uint64_t k, int G,
         #pragma unroll
         for (int g = 0; g < MG; ++g) P.s[g] = (g < G) ? row[g] : 0;
     }
-    P.offset = probe_offset<MG>(P, m.L);
+    P.offset = probe_offset<MG>(P, Loff);
+}
+
+template <int MG>
+__device__ __forceinline__ void load_probe(const MatProbes& m, uint64_t k, int G, int L, Mhe<MG>& P) {
+    if (m.rows32) {   // kernel argument: a uniform branch
+        load_probe32<MG>(m.rows32 + k * (uint64_t)m.stride32, G, L, m.L32, P);
+        return;
+    }
+    const int64_t* row = m.rows + k * (uint64_t)(G + 1);
+    P.len = L;
+    P.mersize = L;
+    P.offset = row[G];
+    #pragma unroll
+    for (int g = 0; g < MG; ++g) P.s[g] = (g < G) ? row[g] : 0;
+}
+
+// The chain kernels' copy of the probe rows in line order when every start fits 31 bits:
+// G int32 starts per row (stride G rounded up to 4, 16-B aligned rows) and the offset
+// recomputed from them -- 32 B per probe instead of 72 at G = 8.  The gather that writes
+// it checks the recomputed offset against the materialized one (launch_gather_line_rows).
+struct LineRows {
+    const int32_t* rows;
+    uint32_t stride;
+    int L;   // seed length of the offset sum
+};
+
+template <int MG>
+__device__ __forceinline__ void load_probe(const LineRows& m, uint64_t k, int G, int L, Mhe<MG>& P) {
+    load_probe32<MG>(m.rows + k * (uint64_t)m.stride, G, L, m.L, P);
 }
 
 __device__ __forceinline__ uint32_t bucket_of(int64_t offset, uint32_t table_size) {

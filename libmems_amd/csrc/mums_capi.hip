@@ -107,6 +107,7 @@ struct mums_ctx {
     DevBuf fsk;              // FindMatches: first-genome start of each probe (key order)
     DevBuf bst2;             // {0, P}: the one bucket of the probes' onesweep bucket sort
     bool fused_keys = false; // materialize_seeds also writes the line keys and fsk (find_tail)
+    bool rows_narrow = false; // ctx->mprobe holds int32 rows (MatProbes::rows32; materialize_dispatch)
     // one genome's SML / seed frequencies (sml_tools.hip) and filtered MatchLists
     DevBuf smlk0, smlkA, smlkB, smlvA, smlvB, smltmp, flen, fs;
     DevBuf rowsall;          // chunked mode: probe rows of all chunks
@@ -487,6 +488,12 @@ template <typename View>
 int materialize_dispatch(mums_ctx* ctx, View sv, const MatchParams& mp, hipStream_t st, int64_t* rows = nullptr) {
     const int G = ctx->gt.G;
     const uint64_t P = ctx->P;
+    ctx->rows_narrow = false;
+    // find_tail's own rows (ctx->fused_keys) as int32 starts when every start fits
+    uint64_t mx = 0;
+    for (int g = 0; g < G; ++g) mx = std::max<uint64_t>(mx, ctx->gt.n[g]);
+    static const bool wide_env = getenv("MUMS_DEV_WIDE_ROWS") != nullptr;
+    bool narrow = !rows && ctx->fused_keys && G <= 16 && mx + 2 < (1ull << 31) && !wide_env;
     if (!rows) {   // into ctx->mprobe, else into the caller's (P + 1) rows
         HIPCHK(ctx->mprobe.ensure((P + 1) * (size_t)(G + 1) * 8));
         rows = ctx->mprobe.as<int64_t>();
@@ -495,11 +502,24 @@ int materialize_dispatch(mums_ctx* ctx, View sv, const MatchParams& mp, hipStrea
     uint32_t* fs = ctx->fused_keys ? ctx->fsk.as<uint32_t>() : nullptr;
     uint32_t* lh = nullptr;   // the line sort's records and hashes instead of the line keys
     if (ctx->fused_keys && chain_line_records(P, ctx->gt)) chain_line_slots(ctx->chain_tmp.p, P, G, &lk, &lh);
-    if (G <= 4) HIPCHK((launch_materialize<4, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st, lk, fs, lh)));
-    else if (G <= 8) HIPCHK((launch_materialize<8, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st, lk, fs, lh)));
-    else if (G <= 16) HIPCHK((launch_materialize<16, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st, lk, fs, lh)));
-    else if (G <= 32) HIPCHK((launch_materialize<32, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st, lk, fs, lh)));
-    else HIPCHK((launch_materialize<64, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st, lk, fs, lh)));
+    for (int pass = 0; pass < 2; ++pass) {
+        int32_t* r32 = narrow ? (int32_t*)rows : nullptr;
+        if (narrow) HIPCHK(hipMemsetAsync(fs + P, 0, 4, st));
+        if (G <= 4) HIPCHK((launch_materialize<4, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st, lk, fs, lh, r32)));
+        else if (G <= 8) HIPCHK((launch_materialize<8, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st, lk, fs, lh, r32)));
+        else if (G <= 16) HIPCHK((launch_materialize<16, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st, lk, fs, lh, r32)));
+        else if (G <= 32) HIPCHK((launch_materialize<32, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st, lk, fs, lh)));
+        else HIPCHK((launch_materialize<64, View>(sv, ctx->probe_info, P, ctx->gt, mp, ctx->L, rows, st, lk, fs, lh)));
+        if (!narrow) break;
+        uint32_t bad = 0;
+        HIPCHK(hipMemcpyAsync(&bad, fs + P, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        if (!bad) {
+            ctx->rows_narrow = true;
+            break;
+        }
+        narrow = false;   // a start or offset the int32 rows do not restate: the 64-bit rows
+    }
     return MUMS_OK;
 }
 
@@ -561,6 +581,12 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
         ctx->fused_keys = false;
         if (rc) return rc;
         if (stream_rows && !chunked) v.fs = ctx->fsk.as<uint32_t>();
+        if (stream_rows && !chunked && ctx->rows_narrow) {
+            v.rows32 = (const int32_t*)ctx->mprobe.p;
+            v.stride32 = line_row_stride(G);
+            v.L32 = ctx->L;
+            v.rows = nullptr;
+        }
         if (chunked) {   // the rows hold all FindMatches reads: keep the bucket order only
             // the dead records (recA / recB, when the packed path sized them) are the arena
             // of the sliced FindMatches: bucket order and summaries in recB, chain scratch

@@ -232,7 +232,9 @@ template <int MG, typename View>
 // lhash (chain_line_slots)
 hipError_t launch_materialize(View v, const uint64_t* probe_info, uint64_t P, const GenomeTable& gt,
                               const MatchParams& mp, int L, int64_t* rows, hipStream_t st, uint64_t* lkey = nullptr,
-                              uint32_t* fsk = nullptr, uint32_t* lhash = nullptr);
+                              uint32_t* fsk = nullptr, uint32_t* lhash = nullptr, int32_t* rows32 = nullptr);
+// rows32 (MG a multiple of 4 up to 16, fsk given): the rows as int32 starts instead
+// (MatProbes::rows32); fsk[P] |= 1 when a start or the recomputed offset does not fit
 // hash bucket of every row (d_bounds == nullptr) or its owning rank (bucket ranges)
 hipError_t launch_row_buckets(const int64_t* rows, uint64_t P, int G, uint32_t table_size, const uint32_t* d_bounds,
                               uint32_t nranks, uint32_t* out, hipStream_t st);
