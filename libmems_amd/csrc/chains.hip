@@ -526,9 +526,15 @@ __global__ __launch_bounds__(kBlock) void chain_walk_short_kernel(View v, const 
 #define MUMS_WALK_GROUP 16
 #endif
 constexpr int kWalkGroup = MUMS_WALK_GROUP;
-static_assert(kWalkGroup >= 2 && kWalkGroup <= 64 && (kWalkGroup & (kWalkGroup - 1)) == 0, "group: power of 2");
+#ifndef MUMS_WALK_HANDOFF
+#define MUMS_WALK_HANDOFF 16   // steps of a kWalkGroup-lane walk before it goes to a whole wave (0: never)
+#endif
+constexpr unsigned kWalkHandoff = MUMS_WALK_HANDOFF;
 
-template <int MG, typename View>
+// maxsteps > 0: a walk still going after maxsteps steps is handed on (from its last hit) to
+// xq for the next launch with wider groups -- the few walks of hundreds of steps otherwise
+// set the kernel's duration one step at a time.
+template <int MG, typename View, int GS>
 __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64_t* __restrict__ probe_info,
                                                             GenomeTable gt, MatchParams mp, SeedSpec ss,
                                                             const uint32_t* __restrict__ ord,
@@ -537,8 +543,9 @@ __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64
                                                             const unsigned int* __restrict__ qcount,
                                                             uint8_t* __restrict__ link, int64_t* __restrict__ rcol,
                                                             int64_t* __restrict__ lcol, unsigned int* __restrict__ dbg,
-                                                            DevCounters* __restrict__ ctr) {
-    constexpr int GS = kWalkGroup;
+                                                            DevCounters* __restrict__ ctr, unsigned maxsteps,
+                                                            WalkItem* __restrict__ xq, unsigned int* __restrict__ xqcount) {
+    static_assert(GS >= 2 && GS <= 64 && (GS & (GS - 1)) == 0, "group: power of 2");
     unsigned long long my_words = 0, my_items = 0, my_wins = 0;
     const int lane = threadIdx.x & 63, gl = lane & (GS - 1), gsh = lane & ~(GS - 1);
     const uint64_t gmask = GS == 64 ? ~0ull : ((1ull << GS) - 1);
@@ -559,8 +566,14 @@ __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64
                                       : (it.stop == INT64_MIN ? INT64_MAX : cur - it.stop);
         int64_t last = 0, u0 = 1;
         bool reached = last >= stopu;
+        bool handed = false;
         unsigned steps = 0;
         while (!reached) {
+            if (maxsteps && steps == maxsteps) {   // uniform in the group
+                if (gl == 0) xq[atomicAdd(xqcount, 1u)] = WalkItem{it.j, it.kind, cur + dir * last, it.stop};
+                handed = true;
+                break;
+            }
             ++steps;
             const uint64_t H = hit_word_dir<MG>(dir, cur + dir * (u0 + 64 * (int64_t)gl), A, gt, clo, chi, packed,
                                                 ss, ls);
@@ -605,7 +618,7 @@ __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64
             atomicMax(&dbg[3], steps);
             atomicAdd(&dbg[4], steps);
         }
-        if (gl == 0) {
+        if (gl == 0 && !handed) {
             const int64_t c = cur + dir * last;
             if (it.kind == 0) {
                 link[it.j] = reached ? 1 : 0;
@@ -1003,7 +1016,7 @@ hipError_t chains_core(LV vl, const ChainWs& w, const uint32_t* ord, uint64_t P,
     unsigned int* qlong = qcount + 1;   // chain_walk_short_kernel -> chain_walk_kernel
     const bool cdbg = getenv("MUMS_DEV_CHAIN_DEBUG") != nullptr;
     for (int pass = 0; pass < 2; ++pass) {
-        if ((e = hipMemsetAsync(qcount, 0, 8, st)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(qcount, 0, 12, st)) != hipSuccess) return e;
         const unsigned lgrid = (unsigned)((P + kBlock * kLinkIPT - 1) / (kBlock * kLinkIPT));
         if (pass == 0)
             hipLaunchKernelGGL((chain_link_kernel<MG, LV>), dim3(lgrid), dim3(kBlock), 0, st, vl, nullptr, P, gt,
@@ -1018,17 +1031,26 @@ hipError_t chains_core(LV vl, const ChainWs& w, const uint32_t* ord, uint64_t P,
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (cdbg && (e = hipMemsetAsync(qcount + 4, 0, 32, st)) != hipSuccess) return e;
         if (ev_walk) (void)hipEventRecord(ev_walk[2 * pass], st);
-        hipLaunchKernelGGL((chain_walk_kernel<MG, LV>), dim3(walk_grid), dim3(kBlock), 0, st, vl, nullptr, gt, mp,
-                           ss, ord, packed, (const WalkItem*)w.queue_long, (const unsigned int*)qlong, w.link, w.rcol,
-                           w.lcol, cdbg ? qcount + 4 : nullptr, (DevCounters*)ctr);
+        // the queue of chain_link / chain_left is consumed: it takes the handed-on walks
+        hipLaunchKernelGGL((chain_walk_kernel<MG, LV, kWalkGroup>), dim3(walk_grid), dim3(kBlock), 0, st, vl, nullptr,
+                           gt, mp, ss, ord, packed, (const WalkItem*)w.queue_long, (const unsigned int*)qlong, w.link,
+                           w.rcol, w.lcol, cdbg ? qcount + 4 : nullptr, (DevCounters*)ctr, kWalkHandoff, w.queue,
+                           qcount + 2);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if (kWalkHandoff)
+            hipLaunchKernelGGL((chain_walk_kernel<MG, LV, 64>), dim3(walk_grid), dim3(kBlock), 0, st, vl, nullptr, gt,
+                               mp, ss, ord, packed, (const WalkItem*)w.queue, (const unsigned int*)(qcount + 2),
+                               w.link, w.rcol, w.lcol, cdbg ? qcount + 4 : nullptr, (DevCounters*)ctr, 0u,
+                               (WalkItem*)nullptr, (unsigned int*)nullptr);
         if (ev_walk) (void)hipEventRecord(ev_walk[2 * pass + 1], st);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (cdbg) {   // development: walk queue sizes and the long walks' step histogram
             unsigned hq[9] = {};
             (void)hipMemcpyAsync(hq, qcount, 36, hipMemcpyDeviceToHost, st);
             (void)hipStreamSynchronize(st);
-            fprintf(stderr, "chains: pass %d walks %u, long %u of %lu probes; steps >1: %u >16: %u >256: %u max %u "
-                    "total %u\n", pass, hq[0], hq[1], (unsigned long)P, hq[4], hq[5], hq[6], hq[7], hq[8]);
+            fprintf(stderr, "chains: pass %d walks %u, long %u (to whole waves %u) of %lu probes; steps >1: %u >16: %u "
+                    ">256: %u max %u total %u\n", pass, hq[0], hq[1], hq[2], (unsigned long)P, hq[4], hq[5], hq[6], hq[7],
+                    hq[8]);
         }
     }
     hipLaunchKernelGGL(chain_flag_kernel, dim3(grid), dim3(kBlock), 0, st, w.link, P, w.seg);

@@ -897,7 +897,8 @@ void fill_stats(mums_ctx* ctx, uint64_t n) {
         s.ms_total = el(EV_START, EV_OUTPUT);
         s.chain_walk_words = ctx->hc.walk_words;
         s.chain_walks = ctx->hc.walk_items;
-        s.chain_walk_bytes = ctx->hc.walk_wins * 28 + ctx->hc.walk_items * (uint64_t)(8 * (ctx->gt.G + 1) + 24);
+        const uint64_t row_b = ctx->rows_narrow ? 4ull * line_row_stride(ctx->gt.G) : 8ull * (ctx->gt.G + 1);
+        s.chain_walk_bytes = ctx->hc.walk_wins * 28 + ctx->hc.walk_items * (row_b + 24);
         if (ctx->walk_events && ctx->P > 0)
             for (int p = 0; p < 2; ++p) {
                 float ms = 0.f;
