@@ -172,7 +172,7 @@ def run_mums(device: int, dev: torch.device, p: float = 0.01, reps: int = 3):
                                                         "ms_output")}}
 
 
-WALK_PMC = os.path.join(ROOT, "profiles", "r04t_pmc_chains.txt")
+WALK_PMC = os.path.join(ROOT, "profiles", "r04v_pmc_chains.txt")
 
 
 def walk_counter_traffic(walk_ms):
@@ -180,16 +180,20 @@ def walk_counter_traffic(walk_ms):
     (tools/pmc_chains.sh: FETCH_SIZE + WRITE_SIZE per dispatch, KiB, not this run) over the
     live duration of its two launches: the counter-based roofline next to the requested one."""
     try:
-        per = {}
-        for line in open(WALK_PMC):
-            f = line.split()
-            if len(f) == 3 and f[0].startswith("chain_walk_kernel") and f[1] in ("FETCH_SIZE", "WRITE_SIZE"):
-                per[f[1]] = float(f[2]) * 1024
-        b = 2 * (per["FETCH_SIZE"] + per["WRITE_SIZE"])   # two launches per FindMatches
+        per = {"FETCH_SIZE": 0.0, "WRITE_SIZE": 0.0}
+        seen = 0
+        for line in open(WALK_PMC):   # "<kernel> <counter> <value per dispatch>", kernel names may hold spaces
+            f = line.rsplit(None, 2)
+            if len(f) == 3 and f[0].startswith("chain_walk_kernel") and f[1] in per:
+                per[f[1]] += float(f[2]) * 1024
+                seen += 1
+        if not seen:
+            raise KeyError("chain_walk_kernel")
+        b = 2 * (per["FETCH_SIZE"] + per["WRITE_SIZE"])   # each instance: one launch per pass, two passes
         gbs = b / (walk_ms * 1e-3) / 1e9
         return {"traffic": b, "traffic_achieved": gbs, "traffic_frac": gbs / HBM_PEAK_GBS,
-                "traffic_source": os.path.relpath(WALK_PMC, ROOT) + " (FETCH_SIZE + WRITE_SIZE per dispatch x 2 "
-                                  "launches, rocprofv3 PMC passes, not this run)"}
+                "traffic_source": os.path.relpath(WALK_PMC, ROOT) + " (FETCH_SIZE + WRITE_SIZE per dispatch of "
+                                  "every chain_walk_kernel instance x 2 passes, rocprofv3 PMC passes, not this run)"}
     except (OSError, KeyError, ValueError, ZeroDivisionError):
         return {"traffic": None}
 

@@ -41,7 +41,7 @@ namespace {
 #endif
 constexpr int kWalkBudget = MUMS_WALK_BUDGET;   // words per lane in chain_walk_short_kernel
 #ifndef MUMS_HIT_BATCH
-#define MUMS_HIT_BATCH 4   // components whose window loads are in flight together (hit_word)
+#define MUMS_HIT_BATCH 2   // components whose window loads are in flight together (hit_word; A/B round 4: 1 / 2 / 4 / 8)
 #endif   // 64-column hit words per lane before a walk goes to a workgroup
 
 struct WalkItem {
