@@ -986,7 +986,11 @@ hipError_t line_sort(const ChainWs& w, uint64_t P, int xbits, void* d_tmp, uint3
     hipLaunchKernelGGL(line_rec2_kernel, dim3(grid_of(P)), dim3(kBlock), 0, st, (const uint32_t*)w.vB, s1, P, r2);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     int b2 = 0;
-    if ((e = seg_onesweep_sort(r2, w.lkey, P, kLineHashBits, 0, w.bst, d_tmp, d_err, &b2, st)) != hipSuccess) return e;
+    // the hashes in x order come in runs (a line's probes): run-aware histogram, late publish
+    static const bool runs = !getenv("MUMS_DEV_LINE_NORUNS");
+    if ((e = seg_onesweep_sort(r2, w.lkey, P, kLineHashBits, 0, w.bst, d_tmp, d_err, &b2, st, nullptr, 32, false,
+                               runs)) != hipSuccess)
+        return e;
     const uint64_t* s2 = b2 ? w.lkey : r2;
     hipLaunchKernelGGL(line_ord_kernel, dim3(grid_of(P)), dim3(kBlock), 0, st, s1, s2, P, w.vA);
     *ord_out = w.vA;

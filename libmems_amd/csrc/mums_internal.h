@@ -200,7 +200,10 @@ size_t onesweep_tmp_bytes(uint64_t n, int msd_bits, int key_bits);
 // key_shift: first key bit of the records (32; 33 in the chunked mode)
 hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key_bits, int msd_bits,
                              const uint32_t* d_bstart, void* d_tmp, uint32_t* d_err, int* out_buf, hipStream_t st,
-                             hipEvent_t* ev_ds = nullptr, int key_shift = 32, bool mask_parity = false);
+                             hipEvent_t* ev_ds = nullptr, int key_shift = 32, bool mask_parity = false,
+                             bool key_runs = false);
+// key_runs: the keys come in runs of equal digits (the line sort's hashes in x order): the
+// histogram adds once per run and the passes publish their counts after the ranking
 // mask_parity: the segment fix-up leaves key bit 0 (the parity / orientation bit) out of
 // the last digit, so equal masked keys keep index order; seg_parity_fix then sorts every
 // masked-key group of such a stream by that bit (d_tmp: seg_parity_fix_tmp_bytes(n))

@@ -282,7 +282,7 @@ constexpr int kGhistBatch = MUMS_GHIST_BATCH;   // records per lane loaded as on
 __global__ __launch_bounds__(kBlock) void seg_ghist_kernel(const uint64_t* __restrict__ rec,
                                                            const SegTile* __restrict__ tiles, uint64_t ntiles_ub,
                                                            int npass, uint32_t* __restrict__ ghist, int key_shift,
-                                                           int nh) {
+                                                           int nh, int runs) {
     __shared__ uint32_t h[4][kDigits];
     const int tid = threadIdx.x;
     const uint64_t t0 = (uint64_t)blockIdx.x * kGhistTilesPerBlock;
@@ -314,11 +314,32 @@ __global__ __launch_bounds__(kBlock) void seg_ghist_kernel(const uint64_t* __res
                 const uint32_t q = q0 + u * kBlock + tid;
                 kk[u] = q < d.count ? rec[d.start + q] : 0ull;
             }
-            #pragma unroll
-            for (int u = 0; u < kGhistBatch; ++u) {
-                if (q0 + u * kBlock + tid >= d.count) break;
-                const uint64_t key = kk[u] >> key_shift;
-                for (int p = 0; p < nh; ++p) atomicAdd(&h[p][(uint32_t)(key >> (8 * p)) & 0xFFu], 1u);
+            if (runs) {   // uniform: runs of equal digits in neighbouring lanes add once per run
+                const int lane = tid & 63;
+                #pragma unroll
+                for (int u = 0; u < kGhistBatch; ++u) {
+                    const bool valid = q0 + u * kBlock + tid < d.count;   // a prefix of the wave's lanes
+                    const uint64_t vm = __ballot(valid);
+                    const uint64_t key = kk[u] >> key_shift;
+                    for (int p = 0; p < nh; ++p) {
+                        const uint32_t dg = (uint32_t)(key >> (8 * p)) & 0xFFu;
+                        const uint32_t pd = __shfl_up(dg, 1, 64);
+                        const bool head = valid && (lane == 0 || pd != dg);
+                        const uint64_t hm = __ballot(head);
+                        if (head) {
+                            const uint64_t above = lane == 63 ? 0ull : (hm & (~0ull << (lane + 1)));
+                            const int nxt = above ? __builtin_ctzll(above) : __popcll(vm);
+                            atomicAdd(&h[p][dg], (uint32_t)(nxt - lane));
+                        }
+                    }
+                }
+            } else {
+                #pragma unroll
+                for (int u = 0; u < kGhistBatch; ++u) {
+                    if (q0 + u * kBlock + tid >= d.count) break;
+                    const uint64_t key = kk[u] >> key_shift;
+                    for (int p = 0; p < nh; ++p) atomicAdd(&h[p][(uint32_t)(key >> (8 * p)) & 0xFFu], 1u);
+                }
             }
         }
     }
@@ -370,7 +391,7 @@ __device__ __forceinline__ void onesweep_load(const uint64_t* __restrict__ rin, 
 // 256 threads also own one digit each for the look-back and the digit starts.
 // kAlias: the per-wave digit counts live in the record exchange buffer (every lane folds
 // its slot base into its ranks before the exchange), so a tile costs kT * 8 B + 4 KB of LDS.
-template <int OB, int kIPT, bool kAlias = false>
+template <int OB, int kIPT, bool kAlias = false, bool kLate = false>
 __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __restrict__ rin,
                                                           uint64_t* __restrict__ rout,
                                                           const SegTile* __restrict__ tiles, uint32_t nclaims,
@@ -379,6 +400,7 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
                                                           uint32_t* tile_counter, uint32_t* err,
                                                           uint32_t* __restrict__ ghist_next) {
     constexpr int kT = kIPT * OB;
+    constexpr bool late = MUMS_OS_LATEPUB || kLate;
     constexpr int kW = OB / 64;
     static_assert(OB >= kDigits, "one thread per digit");
     static_assert(!kAlias || kW * kDigits * 4 <= kT * 8, "counts fit in the exchange buffer");
@@ -419,19 +441,21 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
         key[r] = q < d.count ? rin[d.start + q] : 0ull;
 #endif
     }
-#if !MUMS_OS_LATEPUB
-    // publish this tile's per-digit counts as soon as the keys are in: successors'
-    // look-backs then rarely find an unpublished predecessor.
-    #pragma unroll
-    for (int r = 0; r < kIPT; ++r) {
-        const uint32_t q = qof(r);
-        if (q < d.count) atomicAdd(&hcnt[(uint32_t)(key[r] >> shift) & 0xFFu], 1u);
+    if constexpr (!late) {
+        // publish this tile's per-digit counts as soon as the keys are in: successors'
+        // look-backs then rarely find an unpublished predecessor.  (Late: after the ranking,
+        // from its per-wave counts -- for keys in runs of equal digits, whose per-record LDS
+        // atomics here would serialise.)
+        #pragma unroll
+        for (int r = 0; r < kIPT; ++r) {
+            const uint32_t q = qof(r);
+            if (q < d.count) atomicAdd(&hcnt[(uint32_t)(key[r] >> shift) & 0xFFu], 1u);
+        }
+        __syncthreads();
+        if (d.tb != 0 && tid < kDigits)
+            __hip_atomic_store(status + (uint64_t)t * kDigits + tid, kFlagAgg | hcnt[tid], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     }
-    __syncthreads();
-    if (d.tb != 0 && tid < kDigits)
-        __hip_atomic_store(status + (uint64_t)t * kDigits + tid, kFlagAgg | hcnt[tid], __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-#endif
     if (ghist_next) {   // uniform: the next pass's histogram rides on this pass's read
         #pragma unroll
         for (int r = 0; r < kIPT; ++r) {
@@ -459,9 +483,7 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
         for (int w = 0; w < kW; ++w) { const uint32_t x = wcnt[w][dg]; wcnt[w][dg] = acc; acc += x; }
         // look back over the bucket's preceding tiles, then publish the inclusive prefix
         uint32_t* st = status + (uint64_t)t * kDigits + dg;
-#if MUMS_OS_LATEPUB
-        if (d.tb != 0) __hip_atomic_store(st, kFlagAgg | acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
+        if (late && d.tb != 0) __hip_atomic_store(st, kFlagAgg | acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         uint32_t prefix = 0;
         if (d.tb == 0) {
             __hip_atomic_store(st, kFlagInc | acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1232,7 +1254,7 @@ hipError_t seg_parity_fix(uint64_t* rec, uint64_t* scratch, uint64_t n, int key_
 
 hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key_bits, int msd_bits,
                              const uint32_t* d_bstart, void* d_tmp, uint32_t* d_err, int* out_buf, hipStream_t st,
-                             hipEvent_t* ev_ds, int key_shift, bool mask_parity) {
+                             hipEvent_t* ev_ds, int key_shift, bool mask_parity, bool key_runs) {
     const int nkd = (key_bits + 7) / 8;                  // key digits
     const bool segfix = nkd >= 2 && seg_segfix_enabled();
     const int npass = segfix ? nkd - 1 : nkd;            // onesweep launches (digits above the lowest)
@@ -1267,7 +1289,7 @@ hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key
     // counted by the pass before it (MUMS_OS_NEXTHIST, plain onesweep kernel)
     const bool nexthist = MUMS_OS_NEXTHIST && !MUMS_SORT_PERSIST;
     hipLaunchKernelGGL(seg_ghist_kernel, dim3(gblocks), dim3(kBlock), 0, st, recA, stiles, ub, npass, ghist,
-                       key_shift, nexthist ? 1 : npass);
+                       key_shift, nexthist ? 1 : npass, key_runs ? 1 : 0);
     if (nexthist)
         hipLaunchKernelGGL(seg_dbase_kernel, dim3((unsigned)nb), dim3(kBlock), 0, st, ghist, d_bstart, npass, dbase,
                            0);
@@ -1303,6 +1325,11 @@ hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key
 #define MUMS_OS_LAUNCH(OB, IPT, AL)                                                                               \
     hipLaunchKernelGGL((seg_onesweep_kernel<OB, IPT, AL>), dim3((unsigned)ub), dim3(OB), 0, st, src, dst, otiles, \
                        (uint32_t)ub, sh, p, npass, dbase, sp, counters + p, d_err, gn)
+            if (key_runs) {   // equal-digit runs: publish after the ranking (no per-record LDS atomics)
+                hipLaunchKernelGGL((seg_onesweep_kernel<kSortBlock, kSortTile / kSortBlock, true, true>),
+                                   dim3((unsigned)ub), dim3(kSortBlock), 0, st, src, dst, otiles, (uint32_t)ub, sh, p,
+                                   npass, dbase, sp, counters + p, d_err, gn);
+            } else
             switch (os_variant()) {
             case 1: MUMS_OS_LAUNCH(512, 16, true); break;
             case 2: MUMS_OS_LAUNCH(512, 12, true); break;
