@@ -13,6 +13,7 @@
 //               then digit-run-contiguous global stores.
 // HBM bytes per key per pass: upsweep K, downsweep 2(K+V)  (first pass: values
 // are the implicit indices and are not read).
+#include <cstdlib>
 #include "mums_internal.h"
 
 namespace mums {
@@ -26,18 +27,31 @@ constexpr int kDigits = 256;
 
 template <typename K>
 __global__ __launch_bounds__(kBlock) void rs_upsweep(const K* __restrict__ keys, uint64_t n, int shift,
-                                                     uint32_t* __restrict__ hist, uint32_t nblocks) {
+                                                     uint32_t* __restrict__ hist, uint32_t nblocks, int agg) {
     __shared__ uint32_t h[kWaves][kDigits];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (int i = threadIdx.x; i < kWaves * kDigits; i += kBlock) (&h[0][0])[i] = 0;
     __syncthreads();
     const uint64_t b0 = (uint64_t)blockIdx.x * kRTile + (uint64_t)wv * (kRTile / kWaves);
-    #pragma unroll 4
-    for (int r = 0; r < kRounds; ++r) {
-        uint64_t i = b0 + (uint64_t)r * 64 + lane;
-        if (i < n) {
-            uint32_t d = (uint32_t)(keys[i] >> shift) & 0xFFu;
-            atomicAdd(&h[wv][d], 1u);
+    if (agg) {   // uniform: one LDS add per distinct digit of the wave (keys with a hot digit,
+                 // e.g. the probes' hash buckets of related genomes, serialise per-key atomics)
+        #pragma unroll 4
+        for (int r = 0; r < kRounds; ++r) {
+            const uint64_t i = b0 + (uint64_t)r * 64 + lane;
+            const bool valid = i < n;
+            const uint32_t d = valid ? (uint32_t)(keys[i] >> shift) & 0xFFu : 0u;
+            uint32_t tot;
+            const uint32_t rk = wave_match_rank<8>(d, valid, &tot);
+            if (valid && rk == 0) atomicAdd(&h[wv][d], tot);
+        }
+    } else {
+        #pragma unroll 4
+        for (int r = 0; r < kRounds; ++r) {
+            uint64_t i = b0 + (uint64_t)r * 64 + lane;
+            if (i < n) {
+                uint32_t d = (uint32_t)(keys[i] >> shift) & 0xFFu;
+                atomicAdd(&h[wv][d], 1u);
+            }
         }
     }
     __syncthreads();
@@ -161,7 +175,8 @@ hipError_t radix_sort(const K* keys_in, const uint32_t* vals_in, uint64_t n, int
         K* kdst = (p % 2 == 0) ? kA : kB;
         uint32_t* vdst = (p % 2 == 0) ? vA : vB;
         const int shift = 8 * p;
-        hipLaunchKernelGGL(rs_upsweep<K>, dim3(nb), dim3(kBlock), 0, st, ksrc, n, shift, hist, nb);
+        static const bool agg = getenv("MUMS_DEV_RS_AGG") != nullptr;   // opt-in until measured
+        hipLaunchKernelGGL(rs_upsweep<K>, dim3(nb), dim3(kBlock), 0, st, ksrc, n, shift, hist, nb, agg ? 1 : 0);
         hipError_t e = exclusive_scan_u32(hist, (uint64_t)kDigits * nb, stmp, nullptr, st);
         if (e != hipSuccess) return e;
         if (ev_ds) (void)hipEventRecord(ev_ds[2 * p], st);
