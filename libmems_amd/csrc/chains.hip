@@ -28,6 +28,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 #include "match_device.h"
 #include "seed_device.h"
@@ -987,7 +988,7 @@ hipError_t line_sort(const ChainWs& w, uint64_t P, int xbits, void* d_tmp, uint3
     if ((e = hipGetLastError()) != hipSuccess) return e;
     int b2 = 0;
     // the hashes in x order come in runs (a line's probes): run-aware histogram, late publish
-    static const bool runs = !getenv("MUMS_DEV_LINE_NORUNS");
+    const bool runs = !getenv("MUMS_DEV_LINE_NORUNS");   // read per call (tests toggle it)
     if ((e = seg_onesweep_sort(r2, w.lkey, P, kLineHashBits, 0, w.bst, d_tmp, d_err, &b2, st, nullptr, 32, false,
                                runs)) != hipSuccess)
         return e;
@@ -1074,7 +1075,7 @@ hipError_t chains_core(LV vl, const ChainWs& w, const uint32_t* ord, uint64_t P,
 // the line order: onesweep records when the reference starts fit 32 bits and P < 2^30
 // (MUMS_DEV_LINE_RADIX: the 64-bit pair sort), else 64-bit (key, value) radix passes
 bool chain_line_records(uint64_t P, const GenomeTable& gt) {
-    static const bool pairs = getenv("MUMS_DEV_LINE_RADIX") != nullptr;
+    const bool pairs = getenv("MUMS_DEV_LINE_RADIX") != nullptr;
     uint64_t mx = 0;
     for (int g = 0; g < gt.G; ++g) mx = gt.n[g] > mx ? gt.n[g] : mx;
     return !pairs && P < (1ull << 30) && mx + 2 < (1ull << 32);
@@ -1169,7 +1170,10 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
     // as LineRows (int32 starts, 32 B per probe at G = 8) when every start fits 31 bits
     uint64_t mx = 0;
     for (int g = 0; g < gt.G; ++g) mx = gt.n[g] > mx ? gt.n[g] : mx;
-    static const bool wide_env = getenv("MUMS_DEV_WIDE_LINE_ROWS") != nullptr;
+    // test hooks, read per call: "1" the 64-bit rows, "retry" the int32 rows flagged bad once
+    const char* wide_sw = getenv("MUMS_DEV_WIDE_LINE_ROWS");
+    const bool force_retry = wide_sw && !strcmp(wide_sw, "retry");
+    const bool wide_env = wide_sw && !force_retry;
     bool narrow = MG % 4 == 0 && MG <= 16 && !wide_env && mx + 2 < (1ull << 31);
     unsigned int* flags = w.qcount + 12;   // [0] interleaving line-hash collision, [1] a row not narrow
     auto chains_from = [&](const uint32_t* o) -> hipError_t {
@@ -1206,6 +1210,7 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
         return hipStreamSynchronize(st);
     };
     if ((e = chains_from(ord)) != hipSuccess || (e = read_flags()) != hipSuccess) return e;
+    if (force_retry && narrow && !v.rows32) hf[1] = 1;
     if (hf[1]) {   // a start or offset the int32 rows do not restate: the 64-bit rows
         narrow = false;
         if ((e = chains_from(ord)) != hipSuccess || (e = read_flags()) != hipSuccess) return e;

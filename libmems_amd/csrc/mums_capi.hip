@@ -467,9 +467,14 @@ int find_rows_chunked(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const 
     return MUMS_OK;
 }
 
-int find_rows_dispatch(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const MatchParams& mp, hipStream_t st) {
+// chunked: find_tail's decision (P > find_chunk()), made once per call so the rows it
+// materialized (64-bit rows for the sliced path, int32 rows only in the one-pass path)
+// are the ones the chain kernels read
+int find_rows_dispatch(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const MatchParams& mp, hipStream_t st,
+                       bool chunked) {
     const int G = ctx->gt.G;
-    if (ctx->P > find_chunk()) {
+    if (chunked) {
+        if (!v.rows) return fail(ctx, MUMS_E_HIP, "sliced FindMatches needs 64-bit probe rows (internal error)");
         if (G <= 4) return find_rows_chunked<4>(ctx, v, packed, mp, st);
         if (G <= 8) return find_rows_chunked<8>(ctx, v, packed, mp, st);
         if (G <= 16) return find_rows_chunked<16>(ctx, v, packed, mp, st);
@@ -492,8 +497,9 @@ int materialize_dispatch(mums_ctx* ctx, View sv, const MatchParams& mp, hipStrea
     // find_tail's own rows (ctx->fused_keys) as int32 starts when every start fits
     uint64_t mx = 0;
     for (int g = 0; g < G; ++g) mx = std::max<uint64_t>(mx, ctx->gt.n[g]);
-    static const bool wide_env = getenv("MUMS_DEV_WIDE_ROWS") != nullptr;
-    bool narrow = !rows && ctx->fused_keys && G <= 16 && mx + 2 < (1ull << 31) && !wide_env;
+    const char* wide_sw = getenv("MUMS_DEV_WIDE_ROWS");   // "1": 64-bit rows; "retry": the int32 rows flagged bad
+    const bool force_retry = wide_sw && !strcmp(wide_sw, "retry");
+    bool narrow = !rows && ctx->fused_keys && G <= 16 && mx + 2 < (1ull << 31) && (!wide_sw || force_retry);
     if (!rows) {   // into ctx->mprobe, else into the caller's (P + 1) rows
         HIPCHK(ctx->mprobe.ensure((P + 1) * (size_t)(G + 1) * 8));
         rows = ctx->mprobe.as<int64_t>();
@@ -514,6 +520,7 @@ int materialize_dispatch(mums_ctx* ctx, View sv, const MatchParams& mp, hipStrea
         uint32_t bad = 0;
         HIPCHK(hipMemcpyAsync(&bad, fs + P, 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
+        if (force_retry) bad = 1;
         if (!bad) {
             ctx->rows_narrow = true;
             break;
@@ -549,7 +556,8 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
     HIPCHK(ctx->tsize.ensure((size_t)Tb * 4));
     HIPCHK(ctx->obase.ensure((size_t)Tb * 4 + 64));
     if (ctx->P >= (1ull << 32) - 64) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed probes in one FindMatches");
-    const bool chunked = ctx->P > find_chunk() && !ctx->pcompat;
+    const uint64_t fchunk = find_chunk();   // read once: the env switch may change between calls
+    const bool chunked = ctx->P > fchunk;
     HIPCHK(ctx->chain_of.ensure((ctx->P + 1) * (chunked ? 4 : 12)));   // find_rows: 3 words per line position
     // the replay keeps only the chain-first / suspicious probes (launch_replay_kept): its
     // summaries, bucket vectors and spill live in ctx->cbuf, sized by their count
@@ -618,7 +626,7 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
                 ctx->recB.release();
             }
         }
-        rc = find_rows_dispatch(ctx, v, packed, mp, st);
+        rc = find_rows_dispatch(ctx, v, packed, mp, st, chunked);
         if (rc) return rc;
         if (ctx->pcompat)   // ParallelMemHash::MergeTable (ParallelMemHash.cpp:105-121)
             HIPCHK(launch_compat_merge(ctx->tsize.as<uint32_t>(), ctx->emit_base, ctx->emit_tbl,
@@ -825,7 +833,7 @@ int finish_seeds(mums_ctx* ctx, const ProbeSpace& ps, hipStream_t st) {
     const uint64_t P = ctx->P;
     // the onesweep variant (MUMS_DEV_BUCKET_ONESWEEP) moves packed 8-B records: 2.36 vs 1.56 ms
     // on C3's 1e8 probes (u32 keys and ids in the radix passes move fewer bytes)
-    static const bool radix = getenv("MUMS_DEV_BUCKET_ONESWEEP") == nullptr;
+    const bool radix = getenv("MUMS_DEV_BUCKET_ONESWEEP") == nullptr;
     // (the seed sort's scratch holds the onesweep workspace: ctx->tmp is not regrown here, other
     // stages may hold pointers into it)
     if (!radix && P >= 4096 && P < (1ull << 30) && ps.slot_info + P <= (const uint64_t*)ps.probe_bucket &&
@@ -1577,6 +1585,12 @@ int prepare_shard(mums_ctx* ctx) {
     if (rc) return rc;
     if (ctx->enum_tol > 1)
         return fail(ctx, MUMS_E_UNSUPPORTED, "sharded mode: enumeration tolerance > 1 runs single-GPU only");
+    // the sharded merge / find build MemHash's MatchParams: a ParallelMemHash compat or
+    // PairwiseMatchFinder context would silently get MemHash's MatchList
+    if (ctx->pcompat)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "sharded mode: ParallelMemHash compat runs single-GPU only");
+    if (ctx->pairwise)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "sharded mode: PairwiseMatchFinder runs single-GPU only");
     if (2 * ctx->w + 1 > 32 + kMaxMsdBits)
         return fail(ctx, MUMS_E_UNSUPPORTED, "sharded mode needs 2w+1 <= 43 (packed records)");
     GenomeTable& l = ctx->lgt;
@@ -2110,6 +2124,7 @@ int mums_length_filter(mums_ctx* ctx, uint64_t min_len) { return match_filter(ct
 extern "C++" {
 hipStream_t mums::ctx_stream(mums_ctx* ctx) { return ctx->stream; }
 uint32_t mums::ctx_repeat_tol(mums_ctx* ctx) { return ctx->repeat_tol; }
+bool mums::ctx_merge_chunked(mums_ctx* ctx) { return ctx->merge_chunked; }
 int mums::ctx_device(mums_ctx* ctx) { return ctx->device; }
 int mums::ctx_table_genomes(mums_ctx* ctx, uint32_t* table_size, uint32_t* genomes) {
     if (check_ctx(ctx)) return MUMS_E_INVALID;
@@ -3009,6 +3024,9 @@ int mums_shard_restart_step(mums_ctx* ctx, uint64_t* S, uint64_t* restarts, uint
     }
     *restarts = R;
     *undecidable = bad ? 1 : 0;
+    // test hook: the step reports an undecidable plan (a read beyond the rank's neighbours)
+    const char* force = getenv("MUMS_DEV_SHARD_RESTART");
+    if (force && !strcmp(force, "undecidable")) *undecidable = 1;
     return MUMS_OK;
 }
 

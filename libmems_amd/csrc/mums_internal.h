@@ -268,6 +268,7 @@ hipStream_t ctx_stream(mums_ctx* ctx);
 int ctx_device(mums_ctx* ctx);
 int ctx_table_genomes(mums_ctx* ctx, uint32_t* table_size, uint32_t* genomes);
 uint32_t ctx_repeat_tol(mums_ctx* ctx);
+bool ctx_merge_chunked(mums_ctx* ctx);   // the last shard merge ran in key chunks
 
 // overlaps.hip: EliminateOverlaps (Aligner.cpp:62-176) on a device MatchList
 struct EoWork {

@@ -175,7 +175,7 @@ hipError_t radix_sort(const K* keys_in, const uint32_t* vals_in, uint64_t n, int
         K* kdst = (p % 2 == 0) ? kA : kB;
         uint32_t* vdst = (p % 2 == 0) ? vA : vB;
         const int shift = 8 * p;
-        static const bool agg = !getenv("MUMS_DEV_RS_NOAGG");   // A/B round 4: bucket sort 1.56 -> 1.34 ms
+        const bool agg = !getenv("MUMS_DEV_RS_NOAGG");   // A/B round 4: bucket sort 1.56 -> 1.34 ms
         hipLaunchKernelGGL(rs_upsweep<K>, dim3(nb), dim3(kBlock), 0, st, ksrc, n, shift, hist, nb, agg ? 1 : 0);
         hipError_t e = exclusive_scan_u32(hist, (uint64_t)kDigits * nb, stmp, nullptr, st);
         if (e != hipSuccess) return e;

@@ -691,7 +691,16 @@ int mums_shard_run(mums_ctx* ctx, mums_comm* comm, int stage) {
         if (any) {
             bool done = false;
             RC(shard_restart_local(ctx, comm, st, &done));
-            if (!done) RC(shard_restart(ctx, comm, C, kf, kn, nb, st));
+            if (!done) {   // the gathered plan reads one merged stream per rank
+                int rcg = MUMS_OK;
+                if (mums::ctx_merge_chunked(ctx)) {
+                    comm->err = "sharded restart after a key-chunked merge: a restart plan needs keys beyond a "
+                                "rank's neighbours (the gathered plan needs one-pass merges)";
+                    rcg = MUMS_E_UNSUPPORTED;
+                }
+                AGREE(rcg);
+                RC(shard_restart(ctx, comm, C, kf, kn, nb, st));
+            }
         }
     }
     if (stage != MUMS_STAGE_ALL) return MUMS_OK;

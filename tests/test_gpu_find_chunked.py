@@ -99,3 +99,31 @@ def test_find_chunked_reuse(gpu_lib, oracle_mod, find_chunk):
                 os.environ.pop("MUMS_DEV_FIND_CHUNK", None)
             ml = mh.GetMatchList()
             assert (ml.lengths == lengths).all() and (ml.starts == starts).all()
+
+
+PCOMPAT = json.load(open(os.path.join(GOLDEN, "appendix_c.json")))["parallel_compat"]
+
+
+@pytest.mark.parametrize("chunk", [1_000_003, 77_777])
+def test_find_chunked_parallel_compat(gpu_lib, oracle_mod, find_chunk, chunk):
+    """ParallelMemHash compat through the sliced FindMatches (its chunk-major stream, 64-bit
+    rows per slice, MergeTable on the merged chain pool): the reference md5 fa9dea6f... of
+    4 x 10 Mbp, and a small shape against the oracle."""
+    case = PCOMPAT[0]
+    seqs = oracle_mod.generate(case["G"], case["n"], case["p"], 12345)
+    find_chunk(chunk)
+    with gpu_lib.ParallelMemHash(0, case["chunk_size"]) as mh:
+        mh.SetSeed(oracle_mod.get_seed(case["w"]))
+        ml = mh.FindMatches(seqs)
+        st = mh.stats()
+    assert st["probes"] > chunk
+    assert st["chunks"] == case["chunks"] and len(ml) == case["matches"]
+    assert hashlib.md5(ml.text().encode()).hexdigest() == case["md5"]
+    seqs = oracle_mod.generate(3, 300_000, 0.03, 2)
+    seed = oracle_mod.get_seed(15)
+    lengths, starts, _ = oracle_mod.find_matches(seqs, seed, parallel_compat=True, chunk_size=3000)
+    find_chunk(max(1, chunk // 100))
+    with gpu_lib.ParallelMemHash(0, 3000) as mh:
+        mh.SetSeed(seed)
+        ml = mh.FindMatches(seqs)
+    assert (ml.lengths == lengths).all() and (ml.starts == starts).all()

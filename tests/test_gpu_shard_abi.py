@@ -76,3 +76,32 @@ def test_shard_run_ib33_wide_seeds(gpu_lib, oracle_mod, G, n, w, p, world, layou
     exchange (msdsplit.hip).  FindMatches over 2-8 ranks = the oracle's MatchList."""
     monkeypatch.setenv("MUMS_DEV_SHARD_IB33", "1")
     run(gpu_lib, oracle_mod, G, n, w, p, world, "local", layout=layout)
+
+
+@pytest.mark.parametrize("mode", ["parallel_compat", "pairwise"])
+def test_shard_run_refuses_single_gpu_modes(gpu_lib, oracle_mod, mode):
+    """mums_shard_run builds MemHash's MatchParams: a ParallelMemHash compat or a
+    PairwiseMatchFinder context is refused (MUMS_E_UNSUPPORTED), never answered with
+    MemHash's MatchList."""
+    import ctypes
+    lib = gpu_lib.load_library()
+    seqs = oracle_mod.generate(2, 20_000, 0.02, 5)
+    comms = (ctypes.c_void_p * 1)()
+    devs = (ctypes.c_int * 1)(0)
+    assert lib.mums_comm_init_local(comms, 1, devs) == gpu_lib.MUMS_OK
+    try:
+        with gpu_lib.MemHash(0) as mh:
+            mh.SetSeed(oracle_mod.get_seed(15))
+            for s in seqs:
+                mh.AddSequence(s)
+            if mode == "parallel_compat":
+                mh._check(lib.mums_set_parallel_compat(mh._ctx, 1, 3000))
+            else:
+                mh._check(lib.mums_set_pairwise(mh._ctx, 1))
+            lens = (ctypes.c_uint64 * 2)(*[len(s) for s in seqs])
+            mh._check(lib.mums_shard_layout(mh._ctx, 2, 0, lens))
+            rc = lib.mums_shard_run(mh._ctx, comms[0], gpu_lib.STAGE_ALL)
+            assert rc == gpu_lib.MUMS_E_UNSUPPORTED
+            assert "single-GPU" in lib.mums_last_error(mh._ctx).decode()
+    finally:
+        lib.mums_comm_destroy(comms[0])

@@ -239,3 +239,27 @@ def test_progress_text(gpu_lib, oracle_mod, world, layout, kind):
         text = sh.ProgressLog()
     assert text == ref
     assert len(ml) == len(ref_ml)
+
+
+def test_chunked_merge_gathered_plan_refused(gpu_lib, oracle_mod, monkeypatch):
+    """A key-chunked merge whose local restart plan is undecidable (forced by the test hook; on
+    real inputs a plan that needs keys beyond a rank's neighbours) ends every rank with
+    MUMS_E_UNSUPPORTED and a message saying why, not the gathered plan's INVALID."""
+    seqs = repeat_inputs.n_gapped(G=3, n=200_000, gaps=((40_000, 3000), (120_000, 3000)), shift=500, seed=1)
+    monkeypatch.setenv("MUMS_DEV_CHUNK_RECORDS", str(sum(len(s) for s in seqs) // 12))
+    monkeypatch.setenv("MUMS_DEV_SHARD_RESTART", "undecidable")
+    with gpu_lib.ShardedMemHash([0] * 2, comm="local", table_size=40000) as sh:
+        sh.SetSeed(oracle_mod.get_seed(15))
+        with pytest.raises(gpu_lib.MumsError, match="key-chunked merge"):
+            sh.FindMatches(seqs)
+        assert sh.rank_status == [gpu_lib.MUMS_E_UNSUPPORTED] * 2
+
+
+def test_undecidable_plan_falls_back_to_gathered(gpu_lib, oracle_mod, monkeypatch):
+    """One-pass merges: an undecidable local plan falls back to the gathered plan, which gives
+    the oracle's MatchList."""
+    monkeypatch.setenv("MUMS_DEV_SHARD_RESTART", "undecidable")
+    seqs = repeat_inputs.n_gapped(G=3, n=200_000, gaps=((40_000, 3000), (120_000, 3000)), shift=500, seed=1)
+    info = []
+    ref = check(gpu_lib, oracle_mod, seqs, 2, info=info)
+    assert ref["restarts"] > 0 and all(i["path"] == 2 for i in info), info
