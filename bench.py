@@ -198,6 +198,32 @@ def walk_counter_traffic(walk_ms):
         return {"traffic": None}
 
 
+def run_compat(device: int, genomes, seed, reps: int = 2):
+    """ParallelMemHash (ParallelMemHash.cpp:42-121, CHUNK_SIZE 200 000) on the metric's config:
+    the patched OpenMP reference's MatchList (chunked search, MergeTable), full FindMatches
+    from the resident genomes; best of `reps` after a warm run."""
+    with lm.ParallelMemHash(device, 200_000) as mh:
+        mh.SetSeed(seed)
+        for s in genomes:
+            mh.AddSequence(s)
+        mh.CreateMatches()   # warm
+        dt = float("inf")
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            mh.CreateMatches()
+            torch.cuda.synchronize()
+            dt = min(dt, time.perf_counter() - t0)
+        st = mh.stats()
+    return {"mums_per_s": st["mem_count"] / dt, "matches": st["mem_count"], "ms": dt * 1e3,
+            "chunks": st["chunks"], "probes": st["probes"], "restarts": st["restarts"],
+            "workload": f"BASELINE config 3 ({len(genomes)} x {genomes[0].numel() // 10**6} Mbp related, w19) under "
+                        f"ParallelMemHash compat (chunks of 200 000 mers of the longest SML, MergeTable), full "
+                        f"FindMatches",
+            "phase_ms": {k: round(st[k], 3) for k in ("ms_keys", "ms_sort", "ms_groups", "ms_buckets", "ms_chains",
+                                                        "ms_replay", "ms_output")}}
+
+
 def run_e2e(mh, genomes, seed, reps: int = 2):
     """End to end on the metric's config: host ASCII in pinned memory ->
     AddSequence (H2D copy into the context) -> FindMatches -> host MatchList (lengths +
@@ -390,6 +416,7 @@ def main():
     mh.SetProfiling(False)
     mums_c3 = None
     e2e_c3 = None
+    compat_c3 = None
     if world == 1 and args.workload == "c3" and not args.no_mums:
         # MUMs/s on the metric's own config: full FindMatches of the resident C3 genomes
         try:
@@ -431,6 +458,10 @@ def main():
             e2e_c3 = run_e2e(mh, genomes, seed)
         except Exception as e:  # report, never hide
             e2e_c3 = {"error": str(e)}
+        try:
+            compat_c3 = run_compat(local, genomes, seed)
+        except Exception as e:  # report, never hide
+            compat_c3 = {"error": str(e)}
     elif sharded and args.workload == "c3" and not args.no_mums and hasattr(stage, "run_find"):
         # MUMs/s of the sharded FindMatches (mums_shard_run, all 8 steps: keys, record
         # all-to-allv, merge, bucket ranges, row all-to-allv, packed all-gather, chains + replay)
@@ -536,6 +567,8 @@ def main():
             out["mums_c3"] = mums_c3
         if e2e_c3 is not None:
             out["e2e_c3"] = e2e_c3
+        if compat_c3 is not None:
+            out["mums_c3_compat"] = compat_c3
         if fallback is not None:
             out["exchange_fallback"] = fallback + " -> torch.distributed RCCL all_to_all (libmems_amd/shard.py)"
         if not args.no_mums:

@@ -117,6 +117,11 @@ int  mums_set_pairwise(mums_ctx* ctx, int enable);
 int  mums_add_genome(mums_ctx* ctx, const char* ascii, uint64_t n);
 /* Same for a device-resident ASCII genome (not copied; must outlive the find). */
 int  mums_add_genome_device(mums_ctx* ctx, const void* d_ascii, uint64_t n);
+/* The device copy of genome g this context holds (its ASCII in HBM, n bases): a deferred
+ * SortedMerList (SortedMerList::Create, SortedMerList.cpp:786-824, recorded but not built;
+ * mums::HipSML in mums_memhash.hpp) hands its genome to a MemHash context this way, through
+ * mums_add_genome_device, without a host copy.  Valid until the context is cleared. */
+int  mums_genome_device(mums_ctx* ctx, uint32_t genome, const void** d_ascii, uint64_t* n);
 /* MemHash::Clear / ClearSequences (MemHash.cpp:80-93): drops genomes and results. */
 int  mums_clear(mums_ctx* ctx);
 
@@ -132,8 +137,8 @@ int  mums_set_start_points(mums_ctx* ctx, const uint64_t* start_points, uint32_t
 int  mums_get_offset_log(mums_ctx* ctx, uint64_t* out, uint64_t cap_rows, uint64_t* rows, uint32_t* seq_count);
 /* MemHash::FindMatches(MatchList&) (MemHash.cpp:109-115) / CreateMatches (:104-107).
  * SearchRange's MER_REPEAT_LIMIT restart (MatchFinder.cpp:253-277) is reproduced
- * (mums_stats.restarts); the chunked (> 2^32 seed-mers) and sharded modes refuse an
- * input that has a seed group above MER_REPEAT_LIMIT (MUMS_E_UNSUPPORTED). */
+ * (mums_stats.restarts) in the single-context, chunked (> 2^32 seed-mers) and sharded
+ * modes. */
 int  mums_find(mums_ctx* ctx);
 /* Run only up to a stage (benchmarks); MUMS_STAGE_ALL == mums_find. */
 int  mums_find_stage(mums_ctx* ctx, int stage);
@@ -164,7 +169,7 @@ int  mums_copy_seed_keys(mums_ctx* ctx, uint32_t genome, uint64_t* out, uint64_t
 /* Same for positions [first, first + count) only (sampling genomes of billions of bases). */
 int  mums_copy_seed_keys_range(mums_ctx* ctx, uint32_t genome, uint64_t first, uint64_t count, uint64_t* out);
 /* MemorySML::Create (MemorySML.cpp:45-60): SML positions of genome g sorted by
- * full key, ties by ascending position. */
+ * full key, equal keys in libstdc++ std::sort(bmer_lessthan) order. */
 int  mums_build_sml(mums_ctx* ctx, uint32_t genome, uint32_t* positions, uint64_t cap);
 /* SeedOccurrenceList::construct (SeedOccurrenceList.h:22-61) + smoothFrequencies
  * (:71-87) over genome's SortedMerList: freq[p] (float32, n entries) = mean masked-key
@@ -342,6 +347,28 @@ int  mums_shard_probe_rows(mums_ctx* ctx, uint32_t nranks, const uint32_t* bound
 int  mums_shard_packed_info(mums_ctx* ctx, uint64_t* word_offset, uint64_t* nwords, uint64_t* total_words);
 int  mums_shard_packed_copy(mums_ctx* ctx, uint32_t* d_dst);
 int  mums_shard_find(mums_ctx* ctx, const int64_t* d_rows, uint64_t nrows, const uint32_t* d_packed_all);
+/* The same FindMatches with the chains labelled where the probes are (mums_shard_run's
+ * default): on related genomes most probes share one hash bucket (the main
+ * diagonal's offset, MemHash.cpp:213), so the bucket owner would label nearly every chain.
+ *   mums_shard_chain_label: after the merge (and restarts) the rank labels the chains of its
+ *     own probes (its key range, key order; MatchFinder::ExtendMatch, MatchFinder.h:218-374)
+ *     against the all-gathered packed genomes; *nchains = chain entries labelled.
+ *   mums_shard_chain_export: rows (as mums_shard_probe_rows) + per row its chain entry's index
+ *     inside the destination's entry block (d_tags) + the entries (G + 2 int64 each, d_entries)
+ *     with their first probe's index inside the destination's row block (d_first), grouped by
+ *     destination rank (row_counts / entry_counts per rank; a chain goes where its bucket does).
+ *   mums_shard_find_labelled: on the bucket owner, the received blocks in source-rank order
+ *     (src_rows / src_entries: the blocks' sizes); equal entries from several ranks merge, then
+ *     the replay and the MatchList of the owned buckets.
+ *   mums_shard_chain_info: info[4] = {probes labelled, chains, label time in us, 0}. */
+int  mums_shard_chain_label(mums_ctx* ctx, const uint32_t* d_packed_all, uint64_t* nchains);
+int  mums_shard_chain_export(mums_ctx* ctx, uint32_t nranks, const uint32_t* bounds, int64_t* d_rows, uint32_t* d_tags,
+                             uint64_t capacity_rows, int64_t* d_entries, uint32_t* d_first, uint64_t capacity_entries,
+                             uint64_t* row_counts, uint64_t* entry_counts);
+int  mums_shard_find_labelled(mums_ctx* ctx, const int64_t* d_rows, const uint32_t* d_tags, uint64_t nrows,
+                              const int64_t* d_entries, const uint32_t* d_first, uint64_t nentries, uint32_t nsrc,
+                              const uint64_t* src_rows, const uint64_t* src_entries, const uint32_t* d_packed_all);
+int  mums_shard_chain_info(mums_ctx* ctx, uint64_t* info);
 int  mums_probe_copy(mums_ctx* ctx, uint32_t* buckets, uint64_t* ref_index, uint64_t capacity);
 
 /* ---- multi-GPU MemHash through the ABI ----------

@@ -47,13 +47,173 @@ inline std::ostream& operator<<(std::ostream& os, const Match& m) {
     return os;
 }
 
+// bmer (SortedMerList.h:43-46): an SML entry, position + its seed mer (GetSeedMer)
+struct bmer {
+    uint32_t position;
+    uint64_t mer;
+};
+
+// DNAMemorySML (DNAMemorySML.h:27-51, MemorySML.h:26-54) with SortedMerList construction
+// deferred to the GPU.  The reference builds every SML on the CPU before FindMatches
+// (MemorySML::Create: FillDnaSeedSML + std::sort, MemorySML.cpp:45-60; called by
+// GenericMatchList::CreateMemorySMLs, MatchList.h:409-435, and Aligner.cpp:1181-1184), and
+// MemHash's merge then reads them.  Here Create only records the seed pattern and the
+// lengths and copies the ASCII into HBM (its own one-genome context); MemHash::FindMatches
+// takes the genome from there (mums_genome_device -> mums_add_genome_device) and builds
+// keys and the sorted order on the device with everything else.  The few other readers
+// (Read / operator[] / FindMer / GetSeedMer: SeedOccurrenceList, FindAll callers) materialise
+// the SML on first use from the GPU (mums_build_sml: std::sort(bmer_lessthan) order,
+// mums_copy_seed_keys: GetDnaSeedMer) -- no host key or sort work on any path.
+class HipSML {
+public:
+    explicit HipSML(int device = 0) : device_(device) {}
+    virtual ~HipSML() { if (ctx_) mums_ctx_destroy(ctx_); }
+    HipSML(const HipSML&) = delete;
+    HipSML& operator=(const HipSML&) = delete;
+
+    // SortedMerList::Create (SortedMerList.cpp:786-824) + MemorySML::Create (MemorySML.cpp:45-60),
+    // the sort deferred: header fields and the sequence only
+    virtual void Create(const std::string& seq, uint64_t seed) {
+        Clear();
+        const uint32_t L = seed ? 64 - __builtin_clzll(seed) - __builtin_ctzll(seed) : 0;
+        if (L > 32) throw InvalidData("Mer size is too large");     // SortedMerList.cpp:794-795 (64 / 2 bits)
+        if (L == 0) throw InvalidData("Can't have 0 seed length");  // :797-798
+        if (!ctx_ && mums_ctx_create(device_, &ctx_) != MUMS_OK)
+            throw InvalidData("mums_ctx_create failed (no HIP device?)");
+        check(mums_set_seed(ctx_, seed));
+        check(mums_add_genome(ctx_, seq.data(), seq.size()));
+        seed_ = seed;
+        seed_length_ = L;
+        length_ = seq.size();
+    }
+    // MemorySML::Clear (MemorySML.cpp:40-43)
+    virtual void Clear() {
+        if (ctx_) check(mums_clear(ctx_));
+        positions_.clear();
+        keys_.clear();
+        materialized_ = false;
+        seed_ = 0;
+        seed_length_ = 0;
+        length_ = 0;
+    }
+    uint64_t Seed() const { return seed_; }                                          // SortedMerList.cpp:251-253
+    uint32_t SeedLength() const { return seed_length_; }
+    uint32_t SeedWeight() const { return (uint32_t)__builtin_popcountll(seed_); }     // getSeedWeight
+    uint64_t Length() const { return length_; }                                      // SortedMerList.cpp:284-286
+    // SortedMerList::SMLLength (SortedMerList.cpp:288-295), linear sequences
+    uint64_t SMLLength() const { return length_ < seed_length_ ? 0 : length_ - seed_length_ + 1; }
+    bool IsCircular() const { return false; }
+
+    // MemorySML::Read (MemorySML.cpp:62-82)
+    virtual bool Read(std::vector<bmer>& readVector, uint64_t size, uint64_t offset = 0) {
+        materialize();
+        readVector.clear();
+        if (offset > positions_.size()) return false;
+        uint64_t last_mer = offset + size;
+        bool success = true;
+        if (last_mer > positions_.size()) {
+            last_mer = positions_.size();
+            success = false;
+        }
+        for (uint64_t i = offset; i < last_mer; ++i) readVector.push_back(at(i));
+        return success;
+    }
+    // MemorySML::operator[] (MemorySML.cpp:88-94)
+    virtual bmer operator[](uint64_t index) {
+        materialize();
+        if (index >= positions_.size()) throw InvalidData("SML index out of range");
+        return at(index);
+    }
+    // DNAMemorySML::GetSeedMer = SortedMerList::GetDnaSeedMer (SortedMerList.cpp:726-783)
+    virtual uint64_t GetSeedMer(uint64_t offset) {
+        materialize();
+        if (offset >= keys_.size()) throw InvalidData("SML offset out of range");
+        return keys_[offset];
+    }
+    // SortedMerList::FindMer (SortedMerList.cpp:170-179) with bsearch (:380-394)
+    virtual bool FindMer(uint64_t query_mer, uint64_t& result) {
+        uint64_t last_pos = Length();
+        if (last_pos == 0 || last_pos < seed_length_) return false;
+        last_pos -= seed_length_;
+        result = bsearch(query_mer, 0, last_pos);
+        return (*this)[result].mer == query_mer;
+    }
+    bool Materialized() const { return materialized_; }
+    mums_ctx* handle() const { return ctx_; }
+    int device() const { return device_; }
+    // SMLs materialised by any HipSML of this process (a drop-in FindMatches makes none)
+    static uint64_t& Materializations() {
+        static uint64_t n = 0;
+        return n;
+    }
+
+protected:
+    void check(int rc) const {
+        if (rc == MUMS_OK) return;
+        std::string msg = ctx_ ? mums_last_error(ctx_) : "no context";
+        if (rc == MUMS_E_GAP) throw GapInSequence(msg);
+        throw InvalidData(msg);
+    }
+    bmer at(uint64_t i) const { return bmer{positions_[i], keys_[positions_[i]]}; }
+    uint64_t bsearch(uint64_t q, uint64_t start, uint64_t end) {
+        const uint64_t middle = (start + end) / 2;
+        const uint64_t mid = (*this)[middle].mer;
+        if (mid == q) return middle;
+        if (mid < q && middle < end) return bsearch(q, middle + 1, end);
+        if (mid > q && start < middle) return bsearch(q, start, middle - 1);
+        return middle;   // where it would be if it existed
+    }
+    void materialize() {
+        if (materialized_) return;
+        if (!ctx_) throw InvalidData("SML not created");
+        const uint64_t m = SMLLength();
+        check(mums_find_stage(ctx_, MUMS_STAGE_SEEDS));
+        positions_.assign(m, 0);
+        keys_.assign(m, 0);
+        if (m) {
+            check(mums_build_sml(ctx_, 0, positions_.data(), m));
+            check(mums_copy_seed_keys(ctx_, 0, keys_.data(), m));
+        }
+        materialized_ = true;
+        ++Materializations();
+    }
+    int device_ = 0;
+    mums_ctx* ctx_ = nullptr;
+    uint64_t seed_ = 0, length_ = 0;
+    uint32_t seed_length_ = 0;
+    bool materialized_ = false;
+    std::vector<uint32_t> positions_;   // SML order
+    std::vector<uint64_t> keys_;        // GetSeedMer per sequence position
+};
+
 struct MatchList : std::vector<Match> {
-    std::vector<std::string> seq_table;   // genomes in AddSequence order (MatchList.h:107)
+    std::vector<std::string> seq_table;   // genomes in AddSequence order (MatchList.h:110)
+    // the SortedMerList of each sequence (MatchList.h:109); shared by copies of the list
+    // as the reference's raw pointers are
+    std::vector<std::shared_ptr<HipSML>> sml_table;
+    // GenericMatchList::GetDefaultMerSize (MatchList.h:351-357)
+    uint32_t GetDefaultMerSize() const {
+        uint64_t total = 0;
+        for (const auto& s : seq_table) total += s.size();
+        return mums_default_seed_weight(seq_table.empty() ? 0 : total / seq_table.size());
+    }
+    // GenericMatchList::CreateMemorySMLs (MatchList.h:409-435) with deferred SMLs: one
+    // HipSML::Create per sequence (no keys, no sort: FindMatches builds them on the device)
+    void CreateMemorySMLs(uint32_t mer_size = 0, int seed_rank = 0, int device = 0) {
+        if (mer_size == 0) mer_size = GetDefaultMerSize();
+        const uint64_t default_seed = (uint64_t)mums_get_seed((int)mer_size, seed_rank);
+        sml_table.clear();
+        for (const auto& s : seq_table) {
+            auto sml = std::make_shared<HipSML>(device);
+            sml->Create(s, default_seed);
+            sml_table.push_back(std::move(sml));
+        }
+    }
 };
 
 class MemHash {
 public:
-    explicit MemHash(int device = 0) {
+    explicit MemHash(int device = 0) : device_(device) {
         int rc = mums_ctx_create(device, &ctx_);
         if (rc != MUMS_OK) throw InvalidData("mums_ctx_create failed (no HIP device?)");
     }
@@ -83,10 +243,26 @@ public:
         check(mums_add_genome_device(ctx_, d_ascii, n));
         return true;
     }
+    // MatchFinder::AddSequence(SortedMerList*, gnSequence*) (MatchFinder.cpp:59-87): the merge
+    // reads the SML's seed pattern; the genome is the deferred SML's device copy (no host copy)
+    virtual bool AddSequence(HipSML* sml, const std::string* seq = nullptr) {
+        (void)seq;   // the reference keeps it for ExtendMatch only; the device reads the SML's copy
+        if (!sml) throw InvalidData("Null SortedMerList pointer");
+        if (!sml->handle()) throw InvalidData("SortedMerList not created");
+        if (sml->device() != device_) throw InvalidData("SortedMerList lives on another device");
+        const void* d = nullptr;
+        uint64_t n = 0;
+        if (mums_genome_device(sml->handle(), 0, &d, &n) != MUMS_OK) throw InvalidData(mums_last_error(sml->handle()));
+        check(mums_set_seed(ctx_, sml->Seed()));
+        check(mums_add_genome_device(ctx_, d, n));
+        return true;
+    }
 
-    // MemHash::FindMatches (MemHash.cpp:109-115): adds ml.seq_table, finds, fills ml
+    // MemHash::FindMatches (MemHash.cpp:109-115): adds ml's sequences -- through its
+    // SortedMerLists when it has them (MemHash.cpp:117-127 passes ml.sml_table[i]), else the
+    // seq_table ASCII -- finds, fills ml
     virtual void FindMatches(MatchList& ml) {
-        for (const auto& s : ml.seq_table) AddSequence(s);
+        add_list(ml);
         check(mums_find(ctx_));
         write_match_log();
         write_progress();
@@ -155,7 +331,7 @@ public:
     }
     // MemHash::FindMatchesFromPosition (MemHash.cpp:117-127)
     virtual void FindMatchesFromPosition(MatchList& ml, const std::vector<uint64_t>& start_points) {
-        for (const auto& s : ml.seq_table) AddSequence(s);
+        add_list(ml);
         check(mums_set_start_points(ctx_, start_points.data(), (uint32_t)start_points.size()));
         const int rc = mums_find(ctx_);
         (void)mums_set_start_points(ctx_, nullptr, 0);
@@ -221,6 +397,16 @@ protected:
         throw InvalidData(msg);
     }
     void push_params() { check(mums_set_params(ctx_, repeat_tol_, enum_tol_, table_size_)); }
+    void add_list(MatchList& ml) {
+        if (ml.sml_table.empty()) {
+            for (const auto& s : ml.seq_table) AddSequence(s);
+            return;
+        }
+        if (!ml.seq_table.empty() && ml.seq_table.size() != ml.sml_table.size())
+            throw InvalidData("one SortedMerList per sequence required");
+        for (size_t i = 0; i < ml.sml_table.size(); ++i)
+            AddSequence(ml.sml_table[i].get(), i < ml.seq_table.size() ? &ml.seq_table[i] : nullptr);
+    }
     void write_match_log() const {
         if (!match_log_) return;
         uint64_t n = 0;
@@ -251,6 +437,7 @@ protected:
     std::ostream* match_log_ = nullptr;
     std::ostream* progress_ = nullptr;
     mums_ctx* ctx_ = nullptr;
+    int device_ = 0;
     uint32_t repeat_tol_ = 0, enum_tol_ = 1, table_size_ = 40000;
 };
 

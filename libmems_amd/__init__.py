@@ -104,6 +104,8 @@ EXPORTED_SYMBOLS = [
     "mums_progress_log_copy", "mums_shard_restart_counts", "mums_shard_restart_prepare", "mums_shard_restart_step",
     "mums_shard_restart_log", "mums_shard_restart_runs", "mums_shard_restart_ties", "mums_shard_restart_finish",
     "mums_shard_restart_info", "mums_shard_tie_flags", "mums_shard_tie_replay", "mums_shard_tie_apply",
+    "mums_genome_device", "mums_shard_chain_label", "mums_shard_chain_export", "mums_shard_find_labelled",
+    "mums_shard_chain_info",
 ]
 
 # mums_comm_ops (include/mums.h): the caller's transport as two host callbacks
@@ -144,6 +146,11 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mums_set_mask.argtypes = [vp, i32, u64]
     lib.mums_add_genome.argtypes = [vp, ctypes.c_char_p, u64]
     lib.mums_add_genome_device.argtypes = [vp, vp, u64]
+    lib.mums_genome_device.argtypes = [vp, u32, ctypes.POINTER(vp), ctypes.POINTER(u64)]
+    lib.mums_shard_chain_label.argtypes = [vp, vp, vp]
+    lib.mums_shard_chain_export.argtypes = [vp, u32, vp, vp, vp, u64, vp, vp, u64, vp, vp]
+    lib.mums_shard_find_labelled.argtypes = [vp, vp, vp, u64, vp, vp, u64, u32, vp, vp, vp]
+    lib.mums_shard_chain_info.argtypes = [vp, vp]
     lib.mums_clear.argtypes = [vp]
     lib.mums_find.argtypes = [vp]
     lib.mums_find_stage.argtypes = [vp, i32]
@@ -710,6 +717,13 @@ class ShardedMemHash:
             mh._check(self._lib.mums_shard_restart_info(mh._ctx, ri.ctypes.data))
             self.restart_info.append({"path": int(ri[0]), "candidates": int(ri[1]), "restarts": int(ri[2]),
                                       "bytes": int(ri[3])})
+        # per rank: the probes whose chains it labelled (its own key range), the chain entries
+        # and the labelling's device time (mums_shard_chain_info)
+        self.chain_info = []
+        for mh in self.ranks:
+            ci = np.zeros(4, dtype=np.uint64)
+            mh._check(self._lib.mums_shard_chain_info(mh._ctx, ci.ctypes.data))
+            self.chain_info.append({"probes": int(ci[0]), "chains": int(ci[1]), "ms": int(ci[2]) / 1000.0})
         if stage != STAGE_ALL:
             return MatchList(np.zeros(0, dtype=np.uint64), np.zeros((0, G), dtype=np.int64))
         parts = [mh.GetMatchList() for mh in self.ranks]

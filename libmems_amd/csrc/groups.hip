@@ -512,7 +512,82 @@ __global__ __launch_bounds__(kBlock) void bucket_split_kernel(const uint64_t* __
     ids[k] = (uint32_t)r;
 }
 
+// ---- sharded FindMatches: chains labelled where the probes are (mums_shard_chain_*) -----
+// cdest[c] = destination rank of chain c = the rank owning its first probe's bucket (all
+// probes of a chain share one line, hence one offset and one bucket, MemHash.cpp:213)
+__global__ __launch_bounds__(kBlock) void chain_dest_kernel(const uint32_t* __restrict__ fk, uint64_t nch,
+                                                            const uint32_t* __restrict__ pdest,
+                                                            uint32_t* __restrict__ cdest) {
+    const uint64_t c = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (c < nch) cdest[c] = pdest[fk[c]];
+}
+
+__global__ __launch_bounds__(kBlock) void inverse_perm_kernel(const uint32_t* __restrict__ perm, uint64_t n,
+                                                              uint32_t* __restrict__ inv) {
+    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k < n) inv[perm[k]] = (uint32_t)k;
+}
+
+// the k-th exported row's chain: its entry's index inside the destination's entry block
+__global__ __launch_bounds__(kBlock) void chain_tag_kernel(const uint32_t* __restrict__ chain_of,
+                                                           const uint32_t* __restrict__ perm,
+                                                           const uint32_t* __restrict__ sdest, uint64_t P,
+                                                           const uint32_t* __restrict__ cinv,
+                                                           const uint32_t* __restrict__ cstart,
+                                                           uint32_t* __restrict__ tags) {
+    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k < P) tags[k] = cinv[chain_of[perm[k]]] - cstart[sdest[k]];
+}
+
+// the k-th exported entry: chain cperm[k] (G + 2 words) and its first probe's index inside
+// the destination's row block
+__global__ __launch_bounds__(kBlock) void chain_entry_out_kernel(const int64_t* __restrict__ pool,
+                                                                 const uint32_t* __restrict__ fk,
+                                                                 const uint32_t* __restrict__ cperm,
+                                                                 const uint32_t* __restrict__ scdest, uint64_t nch,
+                                                                 int G, const uint32_t* __restrict__ pinv,
+                                                                 const uint32_t* __restrict__ rstart,
+                                                                 int64_t* __restrict__ eout, uint32_t* __restrict__ fout) {
+    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= nch) return;
+    const uint32_t c = cperm[k];
+    const uint64_t W = (uint64_t)(G + 2);
+    for (uint64_t w = 0; w < W; ++w) eout[k * W + w] = pool[(uint64_t)c * W + w];
+    fout[k] = pinv[fk[c]] - rstart[scdest[k]];
+}
+
 }  // namespace
+
+hipError_t launch_chain_dest(const uint32_t* fk, uint64_t nch, const uint32_t* pdest, uint32_t* cdest, hipStream_t st) {
+    if (nch == 0) return hipSuccess;
+    hipLaunchKernelGGL(chain_dest_kernel, dim3((unsigned)((nch + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, fk, nch,
+                       pdest, cdest);
+    return hipGetLastError();
+}
+
+hipError_t launch_inverse_perm(const uint32_t* perm, uint64_t n, uint32_t* inv, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(inverse_perm_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, perm, n,
+                       inv);
+    return hipGetLastError();
+}
+
+hipError_t launch_chain_tags(const uint32_t* chain_of, const uint32_t* perm, const uint32_t* sdest, uint64_t P,
+                             const uint32_t* cinv, const uint32_t* cstart, uint32_t* tags, hipStream_t st) {
+    if (P == 0) return hipSuccess;
+    hipLaunchKernelGGL(chain_tag_kernel, dim3((unsigned)((P + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, chain_of,
+                       perm, sdest, P, cinv, cstart, tags);
+    return hipGetLastError();
+}
+
+hipError_t launch_chain_entries_out(const int64_t* pool, const uint32_t* fk, const uint32_t* cperm,
+                                    const uint32_t* scdest, uint64_t nch, int G, const uint32_t* pinv,
+                                    const uint32_t* rstart, int64_t* eout, uint32_t* fout, hipStream_t st) {
+    if (nch == 0) return hipSuccess;
+    hipLaunchKernelGGL(chain_entry_out_kernel, dim3((unsigned)((nch + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+                       pool, fk, cperm, scdest, nch, G, pinv, rstart, eout, fout);
+    return hipGetLastError();
+}
 
 hipError_t launch_bucket_records(const uint32_t* b, uint64_t P, uint64_t* rec, hipStream_t st) {
     if (P == 0) return hipSuccess;

@@ -100,6 +100,11 @@ struct mums_ctx {
     bool use_onesweep = true;
     // ParallelMemHash chunk-compat mode (compat.hip): chunk = CHUNK_SIZE, ParallelMemHash.cpp:51
     bool pcompat = false;
+    bool prelabelled = false;   // find_tail: chain_of / pool_loc / fkloc hold the ranks' chain labels
+    uint64_t prelab_n = 0;      // entries in pool_loc
+    const int64_t* lab_rows = nullptr;   // sharded: the rank's own probe rows the labels refer to
+    uint64_t lab_nch = 0;                // sharded: chains labelled among them
+    double lab_ms = 0;                   // sharded: device time of the labelling
     bool pairwise = false;   // PairwiseMatchFinder (pairwise.hip)
     uint64_t chunk_size = 200000;
     uint32_t nchunks = 0;
@@ -113,6 +118,7 @@ struct mums_ctx {
     DevBuf rowsall;          // chunked mode: probe rows of all chunks
     DevBuf pool_loc, cbuf;   // chunked FindMatches: per-slice chain entries, compacted probes
     DevBuf sids;             // chunked FindMatches: the bucket order (its sort scratch released)
+    DevBuf labx;             // sharded chain export scratch (mums_shard_chain_export)
     uint32_t* emit_tbl = nullptr;          // bucket vectors / slice bases of the last replay
     const uint32_t* emit_base = nullptr;   // (chunked: compacted, in cbuf; else tbl / bstart)
     EoWork eo;               // EliminateOverlaps work arrays (overlaps.hip)
@@ -386,8 +392,13 @@ uint64_t find_chunk() {
     return c;
 }
 
+// Chains of the P probe rows v (key order) labelled slice by slice (find_chunk() probes
+// each, key order) into per-slice entries: ctx->pool_loc (*nloc_out x (G + 2) words),
+// ctx->fkloc (each entry's first probe, global index) and ctx->chain_of (probe -> entry).
+// A chain whose probes fall into k slices has k equal entries (merge_slices).
 template <int MG>
-int find_rows_chunked(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const MatchParams& mp, hipStream_t st) {
+int label_slices(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const MatchParams& mp, hipStream_t st,
+                 uint64_t* nloc_out) {
     DevCounters* dc = ctx->counters.as<DevCounters>();
     const uint64_t P = ctx->P, C = find_chunk();
     const int G = ctx->gt.G;
@@ -425,6 +436,20 @@ int find_rows_chunked(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const 
         HIPCHK(launch_add_offset(chain_of + k0, n, (uint32_t)nloc, st));
         nloc += nc;
     }
+    *nloc_out = nloc;
+    return MUMS_OK;
+}
+
+// The nloc per-slice (or per-rank) entries in ctx->pool_loc / ctx->fkloc merged by content
+// into ctx->pool / ctx->fk (chain_of remapped; *nch_out merged chains), then the replay of
+// the kept probes (launch_replay_kept) and the match log.
+template <int MG>
+int replay_merged(mums_ctx* ctx, MatProbes v, const MatchParams& mp, hipStream_t st, uint64_t nloc) {
+    DevCounters* dc = ctx->counters.as<DevCounters>();
+    const uint64_t P = ctx->P;
+    const int G = ctx->gt.G;
+    const size_t W = (size_t)(G + 2) * 8;
+    uint32_t* chain_of = ctx->chain_of.as<uint32_t>();
     HIPCHK(ctx->chain_tmp.ensure(chain_merge_tmp_bytes(nloc)));
     HIPCHK(ctx->pool.ensure((nloc + 1) * W));
     HIPCHK(ctx->radix_tmp.ensure(radix_tmp_bytes(nloc + 1)));
@@ -465,6 +490,15 @@ int find_rows_chunked(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const 
         ctx->log_n = n;
     }
     return MUMS_OK;
+}
+
+template <int MG>
+int find_rows_chunked(mums_ctx* ctx, MatProbes v, const uint32_t* packed, const MatchParams& mp, hipStream_t st) {
+    if (ctx->prelabelled) return replay_merged<MG>(ctx, v, mp, st, ctx->prelab_n);   // chains labelled by the ranks
+    uint64_t nloc = 0;
+    int rc = label_slices<MG>(ctx, v, packed, mp, st, &nloc);
+    if (rc) return rc;
+    return replay_merged<MG>(ctx, v, mp, st, nloc);
 }
 
 // chunked: find_tail's decision (P > find_chunk()), made once per call so the rows it
@@ -557,7 +591,9 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
     HIPCHK(ctx->obase.ensure((size_t)Tb * 4 + 64));
     if (ctx->P >= (1ull << 32) - 64) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed probes in one FindMatches");
     const uint64_t fchunk = find_chunk();   // read once: the env switch may change between calls
-    const bool chunked = ctx->P > fchunk;
+    // prelabelled (sharded FindMatches): the ranks labelled the chains of their own probes;
+    // their entries are merged and replayed like the slices of the sliced path
+    const bool chunked = ctx->P > fchunk || ctx->prelabelled;
     HIPCHK(ctx->chain_of.ensure((ctx->P + 1) * (chunked ? 4 : 12)));   // find_rows: 3 words per line position
     // the replay keeps only the chain-first / suspicious probes (launch_replay_kept): its
     // summaries, bucket vectors and spill live in ctx->cbuf, sized by their count
@@ -611,7 +647,9 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
             ctx->sorted_key = nullptr;
             ctx->sorted_idx = nullptr;
             ctx->rowtmp.drop_view();
-            const size_t cbytes = chain_tmp_bytes(find_chunk() + 1, Tb, G);
+            // (prelabelled: only the merge of the received entries; the replay sizes its own)
+            const size_t cbytes = ctx->prelabelled ? chain_merge_tmp_bytes(ctx->prelab_n + 1)
+                                                   : chain_tmp_bytes(std::min<uint64_t>(ctx->P, fchunk) + 1, Tb, G);
             // a kept tie workspace holding the rows (run_pipeline_chunked) holds the chain
             // scratch behind them
             const bool in_tie = ctx->rowsall.borrowed && ctx->tiebuf.p && ctx->rowsall.p == ctx->tiebuf.p &&
@@ -788,7 +826,14 @@ int merge_stage(mums_ctx* ctx, uint64_t n, int mb, int key_bits, const MatchPara
     // default tolerances: a masked-key group's probe does not depend on its records' order
     const bool mask_parity = mp.repeat_tol == 0 && mp.enum_tol == 1;
     ctx->parity_masked = false;
-    if (ctx->use_onesweep && n < (1ull << 30) && key_bits <= 32) {
+    const bool onesweep = ctx->use_onesweep && n < (1ull << 30) && key_bits <= 32;
+    // three 10-bit passes, parity bit unsorted (radix_wide.hip; 31 key bits with the 8-bit MSD)
+    const bool wide = onesweep && mask_parity && ib == 32 && seg_wide_sort_enabled() && seg_wide_passes(key_bits) <= 3;
+    if (wide) {
+        HIPCHK(seg_onesweep_sort_wide(rA, rB, n, key_bits, mb, bstart, ctx->tmp.p, &dc->err, &buf, st,
+                                      prof ? ctx->ev_ds : nullptr, 32));
+        ctx->parity_masked = true;
+    } else if (onesweep) {
         HIPCHK(seg_onesweep_sort(rA, rB, n, key_bits, mb, bstart, ctx->tmp.p, &dc->err, &buf, st,
                                  prof ? ctx->ev_ds : nullptr, ib, mask_parity));
         ctx->parity_masked = mask_parity && seg_onesweep_launches(key_bits) < (key_bits + 7) / 8;
@@ -796,8 +841,7 @@ int merge_stage(mums_ctx* ctx, uint64_t n, int mb, int key_bits, const MatchPara
         HIPCHK(seg_radix_sort(rA, rB, n, key_bits, tiles, ub, ctx->tmp.p, &buf, st, prof ? ctx->ev_ds : nullptr));
     ctx->sorted_buf = buf;
     ctx->sorted_rec = buf ? rB : rA;
-    ctx->sort_passes = (ctx->use_onesweep && n < (1ull << 30) && key_bits <= 32) ? seg_onesweep_launches(key_bits)
-                                                                                : (key_bits + 7) / 8;
+    ctx->sort_passes = wide ? seg_wide_passes(key_bits) : onesweep ? seg_onesweep_launches(key_bits) : (key_bits + 7) / 8;
     HIPCHK(hipEventRecord(ctx->ev[EV_SORT], st));
     if (wants_tie_order(ctx) && ib == 32 && !ctx->shard) {
         RsStream s{};
@@ -1174,6 +1218,11 @@ int run_pipeline(mums_ctx* ctx, int stage) {
     ctx->msd_bits = ctx->packed_path ? std::max(0, kbits - 32) : 0;
     if (const char* e = getenv("MUMS_DEV_MSD_BITS"))   // development knob (sort layout experiments)
         if (ctx->packed_path) ctx->msd_bits = std::min(kMaxMsdBits, std::max(ctx->msd_bits, atoi(e)));
+    // the three-pass sort (MUMS_DEV_SORT3) sorts 30 bits: the 8-bit MSD scatter leaves 31 key
+    // bits in a w19 record, the parity bit stays unsorted (default tolerances only)
+    if (ctx->packed_path && seg_wide_sort_enabled() && ctx->msd_bits < 8 && kbits - 8 <= 31 && kbits > 8 &&
+        ctx->repeat_tol == 0 && ctx->enum_tol == 1)
+        ctx->msd_bits = 8;
     const int B = ctx->msd_bits;
     // keys wider than 32 + 8 bits: an 8-bit scatter + side bytes + msd_split (msdsplit.hip)
     // instead of a 2^B-digit scatter (write runs of ~2 records per tile at w21)
@@ -1672,7 +1721,7 @@ int mums_ctx_destroy(mums_ctx* ctx) {
                       &ctx->rsplan, &ctx->rsbst, &ctx->pool_loc, &ctx->cbuf, &ctx->sids,
                       &ctx->logA, &ctx->logB, &ctx->logvA, &ctx->logvB, &ctx->tiebuf, &ctx->fk, &ctx->fkloc,
                       &ctx->crbuf, &ctx->crcnt, &ctx->crlive, &ctx->crruns, &ctx->crall, &ctx->fsk, &ctx->bst2,
-                      &ctx->side, &ctx->bst8, &ctx->cbst, &ctx->dsarr};
+                      &ctx->side, &ctx->bst8, &ctx->cbst, &ctx->dsarr, &ctx->labx};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i < EV_COUNT; ++i)
         if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
@@ -1738,6 +1787,15 @@ int mums_add_genome_device(mums_ctx* ctx, const void* d_ascii, uint64_t n) {
         return fail(ctx, MUMS_E_UNSUPPORTED, "more than 64 genomes per context");
     ctx->genomes.push_back({(const char*)d_ascii, n, false});
     ctx->stage_done = 0;
+    return MUMS_OK;
+}
+
+int mums_genome_device(mums_ctx* ctx, uint32_t genome, const void** d_ascii, uint64_t* n) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (!d_ascii || !n) return fail(ctx, MUMS_E_INVALID, "null output pointer");
+    if (genome >= ctx->genomes.size()) return fail(ctx, MUMS_E_INVALID, "genome index out of range");
+    *d_ascii = ctx->genomes[genome].d_ptr;
+    *n = ctx->genomes[genome].n;
     return MUMS_OK;
 }
 
@@ -4486,6 +4544,173 @@ int mums_shard_probe_rows(mums_ctx* ctx, uint32_t nranks, const uint32_t* bounds
     return MUMS_OK;
 }
 
+// ---- sharded FindMatches with the chains labelled where the probes are -----
+// On related genomes ~95 % of the probes share one hash bucket (the main diagonal's offset,
+// MemHash.cpp:213), so labelling chains on the bucket owner left one rank with the chain
+// stage.  Instead every rank labels the chains of ITS probes (its seed-stage key range, key
+// order) against the all-gathered packed genomes -- the line sort, links and walks divide
+// like the seed stage -- and ships each chain's entry with the rows to the bucket owner
+// (all probes of a chain share its bucket).  The owner merges equal entries (a chain whose
+// probes sit on several ranks is labelled by each of them) and replays its buckets.
+int mums_shard_chain_label(mums_ctx* ctx, const uint32_t* d_packed_all, uint64_t* nchains) {
+    int rc = shard_seeds_done(ctx);
+    if (rc) return rc;
+    if (ctx->P && !d_packed_all) return fail(ctx, MUMS_E_INVALID, "null packed genomes");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    const MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, ctx->masked, ctx->seq_mask};
+    rc = shard_chunk_rows(ctx, st);   // a chunked merge: every chunk's rows
+    if (rc) return rc;
+    const uint64_t P = ctx->P;
+    const int G = ctx->gt.G;
+    const int64_t* src = ctx->rowsall.as<int64_t>();
+    if (!ctx->merge_chunked) {
+        rc = materialize_seeds(ctx, mp, st);
+        if (rc) return rc;
+        src = ctx->mprobe.as<int64_t>();
+    }
+    ctx->lab_rows = src;
+    ctx->lab_nch = 0;
+    ctx->lab_ms = 0;
+    if (nchains) *nchains = 0;
+    if (P == 0) return MUMS_OK;
+    if (P >= (1ull << 32) - 64) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed probes on one rank");
+    const uint64_t C = std::min<uint64_t>(P, find_chunk());
+    HIPCHK(ctx->chain_of.ensure((P + 1) * 4));
+    HIPCHK(ctx->chain_tmp.ensure(chain_tmp_bytes(C + 1, ctx->table_size, G)));
+    HIPCHK(ctx->radix_tmp.ensure(chain_radix_tmp_bytes(C + 1)));
+    HIPCHK(ctx->tmp.ensure(scan_tmp_bytes(C + 1)));
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, st));
+    MatProbes v{};
+    v.rows = src;
+    uint64_t nloc = 0;
+    if (G <= 4) rc = label_slices<4>(ctx, v, d_packed_all, mp, st, &nloc);
+    else if (G <= 8) rc = label_slices<8>(ctx, v, d_packed_all, mp, st, &nloc);
+    else if (G <= 16) rc = label_slices<16>(ctx, v, d_packed_all, mp, st, &nloc);
+    else if (G <= 32) rc = label_slices<32>(ctx, v, d_packed_all, mp, st, &nloc);
+    else rc = label_slices<64>(ctx, v, d_packed_all, mp, st, &nloc);
+    if (rc == MUMS_OK && P > C) {   // several slices: their equal entries merged here already
+        DevCounters* dc = ctx->counters.as<DevCounters>();
+        const size_t W = (size_t)(G + 2) * 8;
+        HIPCHK(ctx->chain_tmp.ensure(chain_merge_tmp_bytes(nloc)));
+        HIPCHK(ctx->pool.ensure((nloc + 1) * W));
+        HIPCHK(ctx->radix_tmp.ensure(radix_tmp_bytes(nloc + 1)));
+        HIPCHK(ctx->fk.ensure((nloc + 1) * 4));
+        HIPCHK(launch_chain_merge(ctx->pool_loc.as<int64_t>(), nloc, G, ctx->chain_of.as<uint32_t>(), P,
+                                  ctx->pool.as<int64_t>(), ctx->chain_tmp.p, ctx->radix_tmp.p, ctx->tmp.p, &dc->nchains,
+                                  st, ctx->fkloc.as<uint32_t>(), ctx->fk.as<uint32_t>()));
+        uint32_t nc = 0;
+        HIPCHK(hipMemcpyAsync(&nc, &dc->nchains, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        std::swap(ctx->pool, ctx->pool_loc);
+        std::swap(ctx->fk, ctx->fkloc);
+        nloc = nc;
+    }
+    HIPCHK(hipEventRecord(e1, st));
+    HIPCHK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (rc) return rc;
+    ctx->lab_nch = nloc;
+    ctx->lab_ms = ms;
+    if (nchains) *nchains = nloc;
+    return MUMS_OK;
+}
+
+int mums_shard_chain_export(mums_ctx* ctx, uint32_t nranks, const uint32_t* bounds, int64_t* d_rows, uint32_t* d_tags,
+                            uint64_t capacity_rows, int64_t* d_entries, uint32_t* d_first, uint64_t capacity_entries,
+                            uint64_t* row_counts, uint64_t* entry_counts) {
+    int rc = shard_seeds_done(ctx);
+    if (rc) return rc;
+    if (nranks == 0 || nranks > 1024 || !bounds || !row_counts || !entry_counts)
+        return fail(ctx, MUMS_E_INVALID, "bad rank bounds");
+    if (bounds[0] != 0 || bounds[nranks] != ctx->table_size)
+        return fail(ctx, MUMS_E_INVALID, "bucket bounds must cover [0, table_size)");
+    for (uint32_t r = 0; r < nranks; ++r)
+        if (bounds[r] > bounds[r + 1]) return fail(ctx, MUMS_E_INVALID, "bucket bounds must not decrease");
+    const uint64_t P = ctx->P, nch = ctx->lab_nch;
+    std::fill(row_counts, row_counts + nranks, 0ull);
+    std::fill(entry_counts, entry_counts + nranks, 0ull);
+    if (P == 0) return MUMS_OK;
+    if (!ctx->lab_rows) return fail(ctx, MUMS_E_INVALID, "mums_shard_chain_label first");
+    if (capacity_rows < P || capacity_entries < nch) return fail(ctx, MUMS_E_INVALID, "export buffer too small");
+    if (!d_rows || !d_tags || (nch && (!d_entries || !d_first))) return fail(ctx, MUMS_E_INVALID, "null export buffer");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    const int G = ctx->gt.G;
+    const int bits = std::max(1, ceil_log2(nranks));
+    // scratch: per probe its destination (4), the inverse row permutation (4); per chain its
+    // destination, the sort's key / id ping-pong and the inverse (6 x 4); rank starts
+    HIPCHK(ctx->rowtmp.ensure((P + 64) * 16 + 8192));
+    HIPCHK(ctx->labx.ensure((P + 64) * 8 + (nch + 64) * 24 + (size_t)(nranks + 1) * 8 + 4096));
+    uint32_t* pdest = ctx->labx.as<uint32_t>();
+    uint32_t* pinv = pdest + (P + 64);
+    uint32_t* cdest = pinv + (P + 64);
+    uint32_t* ckB = cdest + (nch + 64);
+    uint32_t* ciA = ckB + (nch + 64);
+    uint32_t* ciB = ciA + (nch + 64);
+    uint32_t* cinv = ciB + (nch + 64);
+    uint32_t* ckA2 = cinv + (nch + 64);
+    uint32_t* rstart = ckA2 + (nch + 64);
+    uint32_t* cstart = rstart + (nranks + 1);
+    HIPCHK(ctx->keybuf.ensure((size_t)(nranks + 1) * 8 + 64));
+    HIPCHK(hipMemcpyAsync(ctx->keybuf.p, bounds, (size_t)(nranks + 1) * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(launch_row_buckets(ctx->lab_rows, P, G, ctx->table_size, ctx->keybuf.as<uint32_t>(), nranks, pdest, st));
+    // chains: destination of the first probe, stable by destination
+    const uint32_t* scdest = nullptr;
+    const uint32_t* cperm = nullptr;
+    if (nch) {
+        HIPCHK(launch_chain_dest(ctx->fkloc.as<uint32_t>(), nch, pdest, cdest, st));
+        HIPCHK(hipMemcpyAsync(ckA2, cdest, nch * 4, hipMemcpyDeviceToDevice, st));
+        HIPCHK(ctx->radix_tmp.ensure(radix_tmp_bytes(std::max(P, nch) + 1)));
+        int out = 0;
+        HIPCHK(radix_sort<uint32_t>(ckA2, nullptr, nch, bits, ckB, ciA, ckA2, ciB, ctx->radix_tmp.p, &out, st));
+        scdest = out ? ckA2 : ckB;
+        cperm = out ? ciB : ciA;
+        HIPCHK(launch_inverse_perm(cperm, nch, cinv, st));
+    }
+    // rows: stable by destination (key order per destination)
+    uint32_t* dest = (uint32_t*)ctx->rowtmp.p;
+    HIPCHK(hipMemcpyAsync(dest, pdest, P * 4, hipMemcpyDeviceToDevice, st));
+    rc = sort_row_keys(ctx, dest, P, bits, st);
+    if (rc) return rc;
+    const uint32_t* perm = ctx->sorted_ids;
+    const uint32_t* sdest = ctx->sorted_buckets;
+    HIPCHK(launch_inverse_perm(perm, P, pinv, st));
+    HIPCHK(launch_gather_rows(ctx->lab_rows, perm, P, G, d_rows, st));
+    std::vector<uint32_t> sd(P), scd(nch);
+    HIPCHK(hipMemcpyAsync(sd.data(), sdest, P * 4, hipMemcpyDeviceToHost, st));
+    if (nch) HIPCHK(hipMemcpyAsync(scd.data(), scdest, nch * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    for (uint64_t i = 0; i < P; ++i) ++row_counts[sd[i]];
+    for (uint64_t i = 0; i < nch; ++i) ++entry_counts[scd[i]];
+    std::vector<uint32_t> starts(2 * (nranks + 1), 0);
+    for (uint32_t r = 0; r < nranks; ++r) {
+        starts[r + 1] = starts[r] + (uint32_t)row_counts[r];
+        starts[nranks + 1 + r + 1] = starts[nranks + 1 + r] + (uint32_t)entry_counts[r];
+    }
+    HIPCHK(hipMemcpyAsync(rstart, starts.data(), starts.size() * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(launch_chain_tags(ctx->chain_of.as<uint32_t>(), perm, sdest, P, cinv, cstart, d_tags, st));
+    HIPCHK(launch_chain_entries_out(ctx->pool_loc.as<int64_t>(), ctx->fkloc.as<uint32_t>(), cperm, scdest, nch, G,
+                                    pinv, rstart, d_entries, d_first, st));
+    HIPCHK(hipStreamSynchronize(st));   // (starts is a host vector)
+    return MUMS_OK;
+}
+
+int mums_shard_chain_info(mums_ctx* ctx, uint64_t* info) {
+    if (check_ctx(ctx) || !info) return MUMS_E_INVALID;
+    info[0] = ctx->lab_rows ? ctx->P : 0;
+    info[1] = ctx->lab_nch;
+    info[2] = (uint64_t)(ctx->lab_ms * 1000.0 + 0.5);
+    info[3] = 0;
+    return MUMS_OK;
+}
+
 int mums_shard_packed_info(mums_ctx* ctx, uint64_t* word_offset, uint64_t* nwords, uint64_t* total_words) {
     int rc = shard_seeds_done(ctx, true);
     if (rc) return rc;
@@ -4528,6 +4753,52 @@ int mums_shard_packed_copy(mums_ctx* ctx, uint32_t* d_dst) {
     HIPCHK(hipMemcpyAsync(d_dst, ctx->packed.p, n * 4, hipMemcpyDeviceToDevice, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return MUMS_OK;
+}
+
+int mums_shard_find_labelled(mums_ctx* ctx, const int64_t* d_rows, const uint32_t* d_tags, uint64_t nrows,
+                             const int64_t* d_entries, const uint32_t* d_first, uint64_t nentries, uint32_t nsrc,
+                             const uint64_t* src_rows, const uint64_t* src_entries, const uint32_t* d_packed_all) {
+    int rc = shard_seeds_done(ctx);
+    if (rc) return rc;
+    if (nrows && (!d_rows || !d_tags || !d_packed_all || !d_entries || !d_first))
+        return fail(ctx, MUMS_E_INVALID, "null rows / chain labels / packed genomes");
+    if (nrows >= (1ull << 32) - 64) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed probes on one rank");
+    if (nsrc == 0 || !src_rows || !src_entries) return fail(ctx, MUMS_E_INVALID, "no source blocks");
+    uint64_t sr = 0, se = 0;
+    for (uint32_t s = 0; s < nsrc; ++s) {
+        sr += src_rows[s];
+        se += src_entries[s];
+    }
+    if (sr != nrows || se != nentries) return fail(ctx, MUMS_E_INVALID, "source blocks do not add up");
+    if (nentries > nrows) return fail(ctx, MUMS_E_INVALID, "more chains than probes");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    const int G = ctx->gt.G;
+    // the labels, rebased: a row's entry index past the entry blocks of the sources before it,
+    // an entry's first probe past their row blocks
+    HIPCHK(ctx->chain_of.ensure((nrows + 1) * 4));
+    HIPCHK(ctx->pool_loc.ensure((nentries + 1) * (size_t)(G + 2) * 8));
+    HIPCHK(ctx->fkloc.ensure((nentries + 1) * 4));
+    if (nrows) HIPCHK(hipMemcpyAsync(ctx->chain_of.p, d_tags, nrows * 4, hipMemcpyDeviceToDevice, st));
+    if (nentries) {
+        HIPCHK(hipMemcpyAsync(ctx->pool_loc.p, d_entries, nentries * (size_t)(G + 2) * 8, hipMemcpyDeviceToDevice, st));
+        HIPCHK(hipMemcpyAsync(ctx->fkloc.p, d_first, nentries * 4, hipMemcpyDeviceToDevice, st));
+    }
+    uint64_t ro = 0, eo = 0;
+    for (uint32_t s = 0; s < nsrc; ++s) {
+        if (s) {
+            HIPCHK(launch_add_offset(ctx->chain_of.as<uint32_t>() + ro, src_rows[s], (uint32_t)eo, st));
+            HIPCHK(launch_add_offset(ctx->fkloc.as<uint32_t>() + eo, src_entries[s], (uint32_t)ro, st));
+        }
+        ro += src_rows[s];
+        eo += src_entries[s];
+    }
+    ctx->prelabelled = true;
+    ctx->prelab_n = nentries;
+    rc = mums_shard_find(ctx, d_rows, nrows, d_packed_all);
+    ctx->prelabelled = false;
+    ctx->prelab_n = 0;
+    return rc;
 }
 
 int mums_shard_find(mums_ctx* ctx, const int64_t* d_rows, uint64_t nrows, const uint32_t* d_packed_all) {

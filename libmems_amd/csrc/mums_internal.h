@@ -213,6 +213,14 @@ hipError_t seg_parity_fix(uint64_t* rec, uint64_t* scratch, uint64_t n, int key_
 // onesweep launches of seg_onesweep_sort for key_bits (the lowest digit of a >= 2-digit
 // key is finished by the segment fix-up unless MUMS_DEV_SEGFIX=0)
 int seg_onesweep_launches(int key_bits);
+// radix_wide.hip (MUMS_DEV_SORT3 > 0): three 10-bit passes over key bits [1, key_bits) with
+// the parity bit left unsorted (default tolerances; the 8-bit MSD scatter leaves 31 key bits)
+bool seg_wide_sort_enabled();
+int seg_wide_passes(int key_bits);
+size_t onesweep_wide_tmp_bytes(uint64_t n, int msd_bits, int key_bits);
+hipError_t seg_onesweep_sort_wide(uint64_t* recA, uint64_t* recB, uint64_t n, int key_bits, int msd_bits,
+                                  const uint32_t* d_bstart, void* d_tmp, uint32_t* d_err, int* out_buf,
+                                  hipStream_t st, hipEvent_t* ev_ds, int key_shift = 32);
 
 // groups.hip
 uint64_t group_slot_count(uint64_t ntiles);
@@ -243,6 +251,17 @@ hipError_t launch_row_buckets(const int64_t* rows, uint64_t P, int G, uint32_t t
                               uint32_t nranks, uint32_t* out, hipStream_t st);
 hipError_t launch_gather_rows(const int64_t* src, const uint32_t* perm, uint64_t P, int G, int64_t* dst,
                               hipStream_t st);
+// sharded FindMatches with chains labelled on the probes' own rank (mums_shard_chain_*):
+// chain destinations (the rank of the chain's first probe), an inverse permutation, every
+// exported row's entry index inside its destination block, and the exported entries with
+// their first probe's index inside the destination's row block
+hipError_t launch_chain_dest(const uint32_t* fk, uint64_t nch, const uint32_t* pdest, uint32_t* cdest, hipStream_t st);
+hipError_t launch_inverse_perm(const uint32_t* perm, uint64_t n, uint32_t* inv, hipStream_t st);
+hipError_t launch_chain_tags(const uint32_t* chain_of, const uint32_t* perm, const uint32_t* sdest, uint64_t P,
+                             const uint32_t* cinv, const uint32_t* cstart, uint32_t* tags, hipStream_t st);
+hipError_t launch_chain_entries_out(const int64_t* pool, const uint32_t* fk, const uint32_t* cperm,
+                                    const uint32_t* scdest, uint64_t nch, int G, const uint32_t* pinv,
+                                    const uint32_t* rstart, int64_t* eout, uint32_t* fout, hipStream_t st);
 // flat tiles over [0, N) for the pair path (one bucket)
 hipError_t launch_flat_tiles(uint64_t N, SegTile* d_tiles, hipStream_t st);
 

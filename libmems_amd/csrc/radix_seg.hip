@@ -1203,8 +1203,10 @@ size_t onesweep_tmp_bytes(uint64_t n, int msd_bits, int key_bits) {
     const uint64_t ub = seg_tiles_upper(n, msd_bits, os_tile());
     const int npass = (key_bits + 7) / 8;
     const uint64_t nb = 1ull << msd_bits;
-    return (ub * kDigits * (uint64_t)npass + 2 * nb * npass * kDigits + 64 + 64) * 4 + 2 * (ub * sizeof(SegTile) + 256) +
-           seg_build_tmp_bytes(nb) + segfix_cap(n) * 4 + 256;   // + the claim-ordered copy, the fix-up's big list
+    const size_t b = (ub * kDigits * (uint64_t)npass + 2 * nb * npass * kDigits + 64 + 64) * 4 +
+                     2 * (ub * sizeof(SegTile) + 256) + seg_build_tmp_bytes(nb) + segfix_cap(n) * 4 +
+                     256;   // + the claim-ordered copy, the fix-up's big list
+    return seg_wide_sort_enabled() ? std::max(b, onesweep_wide_tmp_bytes(n, msd_bits, key_bits)) : b;
 }
 
 // segment fix-up launches: big_count[0..1] zeroed by the caller, big_list in d_list

@@ -63,7 +63,7 @@ struct mums_comm {
         ~Buf() {
             if (p) (void)hipFree(p);
         }
-    } rec, recv, rows, rrows, packed, packed_all;
+    } rec, recv, rows, rrows, packed, packed_all, tags, rtags, ents, rents, efk, refk;
     bool packed_done = false;   // packed_all holds this run's genomes (gather_packed)
 };
 
@@ -719,6 +719,64 @@ int mums_shard_run(mums_ctx* ctx, mums_comm* comm, int stage) {
     bounds.push_back(T);
     uint64_t P = 0;
     const uint64_t rowb = 8ull * (G + 1);
+    // default: chains labelled on the probes' own rank (key ranges balance the line sort and
+    // the walks); MUMS_DEV_SHARD_BUCKET_CHAINS: labelled by the bucket owner (rows only)
+    const bool labelled = getenv("MUMS_DEV_SHARD_BUCKET_CHAINS") == nullptr;
+    if (labelled) {
+        if (!comm->packed_done) RC(gather_packed(ctx, comm, st));
+        uint64_t nch = 0;
+        rc = mums_shard_chain_label(ctx, (const uint32_t*)comm->packed_all.p, &nch);
+        if (rc == MUMS_OK) rc = mums_probe_count(ctx, &P);
+        const uint64_t entb = 8ull * (G + 2);
+        if (rc == MUMS_OK && (comm->rows.ensure((P + 1) * rowb) || comm->tags.ensure((P + 1) * 4) ||
+                              comm->ents.ensure((nch + 1) * entb) || comm->efk.ensure((nch + 1) * 4)))
+            rc = MUMS_E_NOMEM;
+        std::vector<uint64_t> cnt(2 * (size_t)W, 0), CNT((size_t)W * 2 * W);
+        if (rc == MUMS_OK)
+            rc = mums_shard_chain_export(ctx, (uint32_t)W, bounds.data(), (int64_t*)comm->rows.p, (uint32_t*)comm->tags.p,
+                                         P + 1, (int64_t*)comm->ents.p, (uint32_t*)comm->efk.p, nch + 1, cnt.data(),
+                                         cnt.data() + W);
+        AGREE(rc);
+        RC(comm->allgather_u64(cnt.data(), 2 * (size_t)W, CNT.data(), st));
+        // rank s sends CNT[s][R] rows and CNT[s][W + R] entries here
+        std::vector<uint64_t> src_rows(W), src_ents(W);
+        uint64_t nrows = 0, nents = 0;
+        for (int s2 = 0; s2 < W; ++s2) {
+            src_rows[s2] = CNT[(size_t)s2 * 2 * W + R];
+            src_ents[s2] = CNT[(size_t)s2 * 2 * W + W + R];
+            nrows += src_rows[s2];
+            nents += src_ents[s2];
+        }
+        const void *rrows = comm->rows.p, *rtags = comm->tags.p, *rents = comm->ents.p, *refk = comm->efk.p;
+        if (W > 1) {
+            AGREE(comm->rrows.ensure((nrows + 1) * rowb) || comm->rtags.ensure((nrows + 1) * 4) ||
+                          comm->rents.ensure((nents + 1) * entb) || comm->refk.ensure((nents + 1) * 4)
+                      ? MUMS_E_NOMEM
+                      : MUMS_OK);
+            std::vector<uint64_t> sb(W), rb(W);
+            auto xchg = [&](uint64_t unit, int which, const void* sendp, void* recvp) -> int {
+                for (int p = 0; p < W; ++p) {
+                    sb[p] = cnt[(size_t)which * W + p] * unit;
+                    rb[p] = (which ? src_ents[p] : src_rows[p]) * unit;
+                }
+                return comm->alltoallv(sendp, sb.data(), recvp, rb.data(), st);
+            };
+            RC(xchg(rowb, 0, comm->rows.p, comm->rrows.p));
+            RC(xchg(4, 0, comm->tags.p, comm->rtags.p));
+            RC(xchg(entb, 1, comm->ents.p, comm->rents.p));
+            RC(xchg(4, 1, comm->efk.p, comm->refk.p));
+            rrows = comm->rrows.p;
+            rtags = comm->rtags.p;
+            rents = comm->rents.p;
+            refk = comm->refk.p;
+        }
+        rc = hipStreamSynchronize(st) != hipSuccess ? MUMS_E_HIP : MUMS_OK;
+        if (rc == MUMS_OK)
+            rc = mums_shard_find_labelled(ctx, (const int64_t*)rrows, (const uint32_t*)rtags, nrows,
+                                          (const int64_t*)rents, (const uint32_t*)refk, nents, (uint32_t)W,
+                                          src_rows.data(), src_ents.data(), (const uint32_t*)comm->packed_all.p);
+        return agree(comm, rc, st);
+    }
     std::vector<uint64_t> send(W, 0), S((size_t)W * W);
     rc = mums_probe_count(ctx, &P);
     if (rc == MUMS_OK && comm->rows.ensure((P + 1) * rowb)) rc = MUMS_E_NOMEM;

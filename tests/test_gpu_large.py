@@ -33,8 +33,12 @@ def md5_text(ml):
     return hashlib.md5(ml.text().encode()).hexdigest()
 
 
-def test_c3_findmatches_known_answer(gpu_lib, oracle_mod):
+@pytest.mark.parametrize("sort3", [None, "1"], ids=["four_pass", "three_pass"])
+def test_c3_findmatches_known_answer(gpu_lib, oracle_mod, monkeypatch, sort3):
+    """sort3: the three 10-bit passes with the parity bit unsorted (radix_wide.hip)."""
     import torch
+    if sort3:
+        monkeypatch.setenv("MUMS_DEV_SORT3", sort3)
     c = case("c3")
     seqs = oracle_mod.generate(c["G"], c["n"], c["p"], c["gen_seed"])
     dev = [torch.frombuffer(bytearray(s), dtype=torch.uint8).cuda() for s in seqs]

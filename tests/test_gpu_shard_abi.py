@@ -105,3 +105,46 @@ def test_shard_run_refuses_single_gpu_modes(gpu_lib, oracle_mod, mode):
             assert "single-GPU" in lib.mums_last_error(mh._ctx).decode()
     finally:
         lib.mums_comm_destroy(comms[0])
+
+
+def test_shard_chains_labelled_where_the_probes_are(gpu_lib, oracle_mod):
+    """BASELINE config-3 shape at 8 x 10 Mbp (related, w15) over 4 in-process ranks: every
+    rank labels the chains of its own probes (mums_shard_chain_label), the bucket owners merge
+    the entries and replay.  MatchList = the oracle's; the chain stage divides like the seed
+    stage: the largest rank labels <= 1.5 x the mean probe count (by bucket owner one rank
+    would label ~95 %: the related genomes' main diagonal is one hash bucket)."""
+    G, n, w, p, world = 8, 10_000_000, 15, 0.01, 4
+    seqs = oracle_mod.generate(G, n, p, 12345)
+    seed = oracle_mod.get_seed(w)
+    lengths, starts, st = oracle_mod.find_matches(seqs, seed, omp_threads=16)
+    with gpu_lib.ShardedMemHash([0] * world, comm="local") as sh:
+        sh.SetSeed(seed)
+        ml = sh.FindMatches(seqs)
+        coll = sum(s["collision_count"] for s in sh.stats_per_rank)
+        info = sh.chain_info
+        owned = [s["probes"] for s in sh.stats_per_rank]   # rows each bucket owner replayed
+    assert len(ml) == len(lengths)
+    assert np.array_equal(ml.lengths, lengths) and np.array_equal(ml.starts, starts)
+    assert coll == st["collision_count"]
+    lab = [i["probes"] for i in info]
+    assert sum(lab) == sum(owned)
+    mean = sum(lab) / world
+    assert max(lab) <= 1.5 * mean, lab
+    assert max(owned) > 1.5 * mean, owned   # (the bucket owners' rows are as skewed as ever)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_shard_bucket_owner_chains_switch(gpu_lib, oracle_mod, monkeypatch, world):
+    """MUMS_DEV_SHARD_BUCKET_CHAINS: the previous layout (rows only, chains labelled by the
+    bucket owner) still gives the oracle's MatchList."""
+    monkeypatch.setenv("MUMS_DEV_SHARD_BUCKET_CHAINS", "1")
+    run(gpu_lib, oracle_mod, 4, 300_000, 15, 0.02, world, "local")
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_shard_chains_sliced_labels(gpu_lib, oracle_mod, monkeypatch, world):
+    """Ranks with more probes than one labelling slice (MUMS_DEV_FIND_CHUNK, config 5 on 8
+    ranks: 3e8 probes per rank > 2^28): the slices' entries merge on the rank, then again on
+    the bucket owner."""
+    monkeypatch.setenv("MUMS_DEV_FIND_CHUNK", "20000")
+    run(gpu_lib, oracle_mod, 4, 300_000, 15, 0.02, world, "local")

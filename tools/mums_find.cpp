@@ -4,6 +4,11 @@
 // the MatchList text (UngappedLocalAlignment.h:200-206), one match per line.
 //   mums_find gen G n weight p [mask]        (mask > 0 selects MaskedMemHash)
 //   mums_find files weight f1 f2 ...
+//   mums_find sml G n weight p [mask]        the drop-in path of Aligner.cpp:1181-1184 /
+//       CreateMemorySMLs (MatchList.h:409-435): HipSML::Create per genome (deferred), then
+//       MemHash::FindMatches from ml.sml_table; stderr reports the SMLs materialised (0)
+//   mums_find smldump G n weight p g stride  genome g's deferred SML read back: every entry
+//       (position, mer) through operator[], then FindMer of every stride-th entry's mer
 #include <unistd.h>
 
 #include <chrono>
@@ -66,6 +71,58 @@ int main(int argc, char** argv) {
         return 2;
     }
     std::string mode = argv[1];
+    if ((mode == "sml" || mode == "smldump") && argc >= 6) {
+        const int G = atoi(argv[2]);
+        const uint64_t n = strtoull(argv[3], nullptr, 10);
+        const int weight = atoi(argv[4]);
+        const double p = atof(argv[5]);
+        try {
+            mums::MatchList ml;
+            ml.seq_table = generate(G, n, p, 12345);
+            auto t0 = std::chrono::steady_clock::now();
+            ml.CreateMemorySMLs((uint32_t)weight);   // Create per genome: no keys, no sort
+            auto t1 = std::chrono::steady_clock::now();
+            if (mode == "smldump") {
+                const uint32_t g = argc > 6 ? (uint32_t)atoi(argv[6]) : 0;
+                const uint64_t stride = argc > 7 ? strtoull(argv[7], nullptr, 10) : 1000;
+                mums::HipSML& sml = *ml.sml_table.at(g);
+                std::ostringstream os;
+                const uint64_t m = sml.SMLLength();
+                for (uint64_t i = 0; i < m; ++i) {
+                    const mums::bmer b = sml[i];
+                    os << b.position << '\t' << b.mer << '\n';
+                }
+                for (uint64_t i = 0; i < m; i += stride) {   // FindMer (SortedMerList.cpp:170-179)
+                    uint64_t r = 0;
+                    const bool f = sml.FindMer(sml[i].mer, r);
+                    os << "find\t" << i << '\t' << f << '\t' << r << '\n';
+                }
+                std::vector<mums::bmer> rv;   // MemorySML::Read past the end returns false
+                const bool ok = sml.Read(rv, 10, m > 5 ? m - 5 : 0);
+                os << "read\t" << ok << '\t' << rv.size() << '\n';
+                std::cout << os.str();
+                std::cerr << "sml length " << m << " materialized " << mums::HipSML::Materializations() << "\n";
+                return 0;
+            }
+            mums::MaskedMemHash mh(0);
+            const uint64_t mask = argc > 6 ? strtoull(argv[6], nullptr, 0) : 0;
+            if (mask) mh.SetMask(mask);
+            else mums_set_mask(mh.handle(), 0, 0);
+            mh.FindMatches(ml);   // genomes and seed pattern from ml.sml_table
+            auto t2 = std::chrono::steady_clock::now();
+            std::ostringstream os;
+            for (const auto& m : ml) os << m << '\n';
+            std::cout << os.str();
+            std::cerr << "matches " << ml.size() << " create ms "
+                      << std::chrono::duration<double, std::milli>(t1 - t0).count() << " find ms "
+                      << std::chrono::duration<double, std::milli>(t2 - t1).count() << " materialized "
+                      << mums::HipSML::Materializations() << "\n";
+        } catch (const std::exception& e) {
+            std::cerr << "error: " << e.what() << "\n";
+            return 1;
+        }
+        return 0;
+    }
     std::vector<std::string> seqs;
     int weight = 0;
     uint64_t mask = 0;
