@@ -488,8 +488,10 @@ public:
     ShardedMemHash& operator=(const ShardedMemHash&) = delete;
     void SetSeed(uint64_t pattern) { seed_ = pattern; }
     void SetTableSize(uint32_t n) { table_size_ = n; }
-    // MemHash::SetRepeatTolerance (MemHash.h:125-131) on every rank
+    // MemHash::SetRepeatTolerance (MemHash.h:125-131) / SetEnumerationTolerance (:137-144) on
+    // every rank
     void SetRepeatTolerance(uint32_t t) { repeat_tol_ = t; }
+    void SetEnumerationTolerance(uint32_t t) { enum_tol_ = t; }
     bool AddSequence(const std::string& seq) {
         seqs_.push_back(seq);
         return true;
@@ -525,6 +527,7 @@ public:
                 auto mh = std::make_unique<MemHash>(devices_[r]);
                 mh->SetTableSize(table_size_);
                 mh->SetRepeatTolerance(repeat_tol_);
+                mh->SetEnumerationTolerance(enum_tol_);
                 mh->SetSeed(seed);
                 mh->AddSequence(b1 > b0 ? seqs_[g].substr(b0, std::min<uint64_t>(lens[g], b1 + L - 1) - b0) : "");
                 if (mums_shard_slice(mh->handle(), (uint32_t)G, lens.data(), (uint32_t)g, b0, b1) != MUMS_OK)
@@ -538,6 +541,7 @@ public:
             auto mh = std::make_unique<MemHash>(devices_[r]);
             mh->SetTableSize(table_size_);
             mh->SetRepeatTolerance(repeat_tol_);
+            mh->SetEnumerationTolerance(enum_tol_);
             mh->SetSeed(seed_);
             for (size_t g = g0; g < g0 + cnt; ++g) mh->AddSequence(seqs_[g]);
             if (mums_shard_layout(mh->handle(), (uint32_t)G, (uint32_t)g0, lens.data()) != MUMS_OK)
@@ -575,7 +579,7 @@ private:
     std::vector<std::string> seqs_;
     uint64_t seed_ = 0;
     uint32_t table_size_ = 40000;
-    uint32_t repeat_tol_ = 0;
+    uint32_t repeat_tol_ = 0, enum_tol_ = 1;
     std::vector<uint64_t> start_points_;
 };
 

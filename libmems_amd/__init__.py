@@ -599,6 +599,7 @@ class ShardedMemHash:
         self.table_size = table_size
         self.seed = 0
         self.repeat_tol = 0
+        self.enum_tol = 1
         self.progress = False
         self.seqs: List[bytes] = []
         self.ranks: List[MemHash] = []
@@ -619,6 +620,12 @@ class ShardedMemHash:
         """MemHash::SetRepeatTolerance (MemHash.h:125-131) on every rank: the first copies of a
         genome follow its SortedMerList's std::sort order, replayed on rank g % world."""
         self.repeat_tol = int(t)
+
+    def SetEnumerationTolerance(self, t: int) -> None:
+        """MemHash::SetEnumerationTolerance (MemHash.h:137-144) on every rank: each rank
+        enumerates the groups of its key range (MatchFinder.cpp:342-393, the odometer), the
+        first copies in SortedMerList order (replayed like repeat tolerance)."""
+        self.enum_tol = int(t)
 
     def LogProgress(self, enable: bool = True) -> None:
         """MatchFinder::LogProgress (MatchFinder.cpp:55-56) over the ranks: the text of the whole
@@ -666,6 +673,7 @@ class ShardedMemHash:
                 mh = MemHash(self.devices[r])
                 mh.SetTableSize(self.table_size)
                 mh.SetRepeatTolerance(self.repeat_tol)
+                mh.SetEnumerationTolerance(self.enum_tol)
                 mh.SetSeed(seed)
                 mh.AddSequence(self.seqs[g][b0:min(len(self.seqs[g]), b1 + L - 1)] if b1 > b0 else b"")
                 mh._check(self._lib.mums_shard_slice(mh._ctx, G, lens, g, b0, b1))
@@ -676,6 +684,7 @@ class ShardedMemHash:
             mh = MemHash(dev)
             mh.SetTableSize(self.table_size)
             mh.SetRepeatTolerance(self.repeat_tol)
+            mh.SetEnumerationTolerance(self.enum_tol)
             mh.SetSeed(self.seed)
             for s in self.seqs[g0:g0 + cnt]:
                 mh.AddSequence(s)

@@ -1632,8 +1632,8 @@ int prepare_shard(mums_ctx* ctx) {
     }
     int rc = prepare_run(ctx, ctx->shard_len);
     if (rc) return rc;
-    if (ctx->enum_tol > 1)
-        return fail(ctx, MUMS_E_UNSUPPORTED, "sharded mode: enumeration tolerance > 1 runs single-GPU only");
+    if (ctx->enum_tol > 8)   // pairwise.hip kEnumMax
+        return fail(ctx, MUMS_E_UNSUPPORTED, "enumeration tolerance > 8");
     // the sharded merge / find build MemHash's MatchParams: a ParallelMemHash compat or
     // PairwiseMatchFinder context would silently get MemHash's MatchList
     if (ctx->pcompat)
@@ -2183,6 +2183,7 @@ extern "C++" {
 hipStream_t mums::ctx_stream(mums_ctx* ctx) { return ctx->stream; }
 uint32_t mums::ctx_repeat_tol(mums_ctx* ctx) { return ctx->repeat_tol; }
 bool mums::ctx_merge_chunked(mums_ctx* ctx) { return ctx->merge_chunked; }
+bool mums::ctx_tie_all(mums_ctx* ctx) { return wants_tie_order(ctx); }
 int mums::ctx_device(mums_ctx* ctx) { return ctx->device; }
 int mums::ctx_table_genomes(mums_ctx* ctx, uint32_t* table_size, uint32_t* genomes) {
     if (check_ctx(ctx)) return MUMS_E_INVALID;
@@ -2490,9 +2491,56 @@ int shard_groups_chunked(mums_ctx* ctx, uint64_t* rec, const std::vector<uint32_
     return MUMS_OK;
 }
 
+// the sharded FindMatches reads its probe rows from ctx->rowsall (built once per merge /
+// restart) for a chunked merge and under enumeration tolerance > 1
+bool shard_rows_from_all(const mums_ctx* ctx) { return ctx->merge_chunked || ctx->enum_tol > 1; }
+
+// Enumeration tolerance > 1 on a sharded rank (MemHash::EnumerateMatches, MemHash.cpp:139-162 ->
+// MatchFinder::EnumerateMatches' odometer, MatchFinder.cpp:342-393): one probe row per
+// AddHashEntry call of every group of the rank's key range, in key order (pairwise.hip
+// en_count / en_emit over the records as full-key pairs, the run order already the std::sort
+// order: mums_shard_tie_*).  ctx->P = the rows.
+int shard_enum_rows(mums_ctx* ctx, hipStream_t st) {
+    if (ctx->rec_ib != 32)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "sharded enumeration tolerance > 1 above 2^32 seed-mers (33-bit records)");
+    const uint64_t n = ctx->shard_n;
+    const int G = ctx->gt.G;
+    const MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, ctx->masked, ctx->seq_mask};
+    DevCounters* dc = ctx->counters.as<DevCounters>();
+    const uint32_t nb = (uint32_t)ctx->shard_bst.size() - 1;
+    HIPCHK(ctx->ckey.ensure(n * 8 + 64));
+    HIPCHK(ctx->cval.ensure(2 * (n + 64) * 4 + (uint64_t)(nb + 1) * 4));
+    uint32_t* idx = ctx->cval.as<uint32_t>();
+    uint32_t* ncalls = idx + n + 64;
+    uint32_t* d_bst = ncalls + n + 64;
+    HIPCHK(hipMemcpyAsync(d_bst, ctx->shard_bst.data(), (uint64_t)(nb + 1) * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(launch_rec_pairs(ctx->sorted_rec, n, d_bst, nb, ctx->shard_kfirst, 2 * ctx->w + 1 - ctx->msd_bits,
+                            ctx->ckey.as<uint64_t>(), idx, st));
+    const PairView<uint64_t> v{ctx->ckey.as<uint64_t>(), idx};
+    HIPCHK(hipMemsetAsync(&dc->repeat_limit, 0, 8, st));
+    HIPCHK(launch_enum_count<PairView<uint64_t>>(v, n, ctx->gt, mp, ncalls, dc, st));
+    HIPCHK(ctx->tmp.ensure(std::max(ctx->tmp.cap, scan_tmp_bytes(n + 1))));
+    uint32_t* total = &dc->nprobes;
+    HIPCHK(ctx->rowtmp.ensure((n + 64) * 4 + 4096));
+    uint32_t* off = (uint32_t*)ctx->rowtmp.p;
+    HIPCHK(hipMemcpyAsync(off, ncalls, n * 4, hipMemcpyDeviceToDevice, st));
+    HIPCHK(exclusive_scan_u32(off, n, ctx->tmp.p, total, st));
+    uint32_t P = 0;
+    HIPCHK(hipMemcpyAsync(&P, total, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(ctx->rowsall.ensure(((uint64_t)P + 1) * (G + 1) * 8));
+    HIPCHK(launch_enum_emit<PairView<uint64_t>>(v, n, ctx->gt, mp, ctx->L, ncalls, off, ctx->rowsall.as<int64_t>(), st));
+    HIPCHK(hipStreamSynchronize(st));
+    ctx->P = P;
+    ctx->st.probes = P;
+    ctx->shard_rows_built = true;
+    return MUMS_OK;
+}
+
 // a chunked merge's probe rows for the sharded FindMatches (once per merge / restart)
 int shard_chunk_rows(mums_ctx* ctx, hipStream_t st) {
-    if (!ctx->merge_chunked || ctx->shard_rows_built) return MUMS_OK;
+    if (!shard_rows_from_all(ctx) || ctx->shard_rows_built) return MUMS_OK;
+    if (ctx->enum_tol > 1) return shard_enum_rows(ctx, st);
     ProbeSpace ps{};
     int rc = ensure_probe_space(ctx, ctx->shard_n, seg_tiles_upper(ctx->shard_n, ctx->shard_mb), &ps);
     if (rc) return rc;
@@ -2666,7 +2714,7 @@ int mums_shard_merge(mums_ctx* ctx, const uint64_t* d_records, uint32_t nsources
     // (repeat tolerance: every run of equal keys in std::sort order, mums_shard_tie_*, first)
     // (LogProgress: the text is restated by the gathered plan on rank 0, over the whole stream)
     ctx->shard_restart_pending =
-        ctx->hc.repeat_limit > 0 || have_start_points(ctx) || ctx->repeat_tol > 0 || ctx->progress_on;
+        ctx->hc.repeat_limit > 0 || have_start_points(ctx) || wants_tie_order(ctx) || ctx->progress_on;
     ctx->shard_mb = mb;
     ctx->shard_n = n;
     ctx->shard_kfirst = first_bucket;
@@ -2842,9 +2890,9 @@ int mums_shard_restart_counts(mums_ctx* ctx, uint64_t* info) {
         return fail(ctx, MUMS_E_UNSUPPORTED, "restart with the segment fix-up sort (MUMS_DEV_SEGFIX)");
     const char* force = getenv("MUMS_DEV_SHARD_RESTART");
     if (ctx->progress_on || (force && !strcmp(force, "gather"))) {   // LogProgress needs the whole stream
-        if (ctx->repeat_tol > 0)
-            return fail(ctx, MUMS_E_UNSUPPORTED, "sharded repeat tolerance: the gathered plan (LogProgress) does not "
-                                                 "order every run of equal keys");
+        if (wants_tie_order(ctx))
+            return fail(ctx, MUMS_E_UNSUPPORTED, "sharded repeat / enumeration tolerance: the gathered plan (LogProgress) "
+                                                 "does not order every run of equal keys");
         if (ctx->merge_chunked)
             return fail(ctx, MUMS_E_UNSUPPORTED, "sharded restart after a chunked merge: the gathered plan (LogProgress) "
                                                  "needs one merge per rank");
@@ -4478,7 +4526,7 @@ int mums_shard_bucket_counts(mums_ctx* ctx, uint64_t* counts) {
     if (rc) return rc;
     if (ctx->P == 0) return MUMS_OK;
     DevCounters* dc = ctx->counters.as<DevCounters>();
-    if (ctx->merge_chunked) {   // the buckets of every chunk's rows (key order kept per bucket)
+    if (shard_rows_from_all(ctx)) {   // the buckets of every chunk's rows (key order kept per bucket)
         int tbits = 1;
         while (tbits < 32 && ((uint64_t)1 << tbits) < (uint64_t)Tb) ++tbits;
         HIPCHK(ctx->rowtmp.ensure((ctx->P + 64) * 16 + 8192));
@@ -4519,7 +4567,7 @@ int mums_shard_probe_rows(mums_ctx* ctx, uint32_t nranks, const uint32_t* bounds
     hipStream_t st = ctx->stream;
     MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, ctx->masked, ctx->seq_mask};
     const int64_t* src = ctx->rowsall.as<int64_t>();   // a chunked merge: every chunk's rows
-    if (!ctx->merge_chunked) {
+    if (!shard_rows_from_all(ctx)) {
         rc = materialize_seeds(ctx, mp, st);
         if (rc) return rc;
         src = ctx->mprobe.as<int64_t>();
@@ -4559,12 +4607,12 @@ int mums_shard_chain_label(mums_ctx* ctx, const uint32_t* d_packed_all, uint64_t
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
     const MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, ctx->masked, ctx->seq_mask};
-    rc = shard_chunk_rows(ctx, st);   // a chunked merge: every chunk's rows
+    rc = shard_chunk_rows(ctx, st);   // a chunked merge / enumeration: every row
     if (rc) return rc;
     const uint64_t P = ctx->P;
     const int G = ctx->gt.G;
     const int64_t* src = ctx->rowsall.as<int64_t>();
-    if (!ctx->merge_chunked) {
+    if (!shard_rows_from_all(ctx)) {
         rc = materialize_seeds(ctx, mp, st);
         if (rc) return rc;
         src = ctx->mprobe.as<int64_t>();
@@ -4575,6 +4623,8 @@ int mums_shard_chain_label(mums_ctx* ctx, const uint32_t* d_packed_all, uint64_t
     if (nchains) *nchains = 0;
     if (P == 0) return MUMS_OK;
     if (P >= (1ull << 32) - 64) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed probes on one rank");
+    uint64_t words = 0;
+    (void)layout_packed(ctx->gt, &words);   // the walks read every genome at its global word offset
     const uint64_t C = std::min<uint64_t>(P, find_chunk());
     HIPCHK(ctx->chain_of.ensure((P + 1) * 4));
     HIPCHK(ctx->chain_tmp.ensure(chain_tmp_bytes(C + 1, ctx->table_size, G)));

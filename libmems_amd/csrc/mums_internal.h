@@ -255,6 +255,10 @@ hipError_t launch_gather_rows(const int64_t* src, const uint32_t* perm, uint64_t
 // chain destinations (the rank of the chain's first probe), an inverse permutation, every
 // exported row's entry index inside its destination block, and the exported entries with
 // their first probe's index inside the destination's row block
+// a sharded rank's merged records (local MSD buckets, starts d_bst[0..nb]) as (full key,
+// 32-bit index) pairs for the group scans of pairwise.hip
+hipError_t launch_rec_pairs(const uint64_t* rec, uint64_t n, const uint32_t* d_bst, uint32_t nb, uint32_t kfirst,
+                            int kb_rec, uint64_t* key, uint32_t* idx, hipStream_t st);
 hipError_t launch_chain_dest(const uint32_t* fk, uint64_t nch, const uint32_t* pdest, uint32_t* cdest, hipStream_t st);
 hipError_t launch_inverse_perm(const uint32_t* perm, uint64_t n, uint32_t* inv, hipStream_t st);
 hipError_t launch_chain_tags(const uint32_t* chain_of, const uint32_t* perm, const uint32_t* sdest, uint64_t P,
@@ -288,6 +292,7 @@ int ctx_device(mums_ctx* ctx);
 int ctx_table_genomes(mums_ctx* ctx, uint32_t* table_size, uint32_t* genomes);
 uint32_t ctx_repeat_tol(mums_ctx* ctx);
 bool ctx_merge_chunked(mums_ctx* ctx);   // the last shard merge ran in key chunks
+bool ctx_tie_all(mums_ctx* ctx);         // every run of equal keys in std::sort order (repeat / enum tol)
 
 // overlaps.hip: EliminateOverlaps (Aligner.cpp:62-176) on a device MatchList
 struct EoWork {

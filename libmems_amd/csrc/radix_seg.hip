@@ -162,6 +162,49 @@ __global__ __launch_bounds__(256) void claim_tiles_kernel(const SegTile* __restr
     ctiles[c] = d;
 }
 
+// XCD-grouped claim queues (MUMS_DEV_OS_XCD, development A/B): bucket b's tiles form queue
+// b % 8, in (tile-in-bucket, bucket) order inside the queue; blocks b and b + 8 share an XCD
+// (round-robin dispatch, MI355X_MICROARCH.md: a speed-only affinity), so a block claims from
+// queue blockIdx % 8 first: consecutive tiles of a bucket -- whose digit runs abut in the
+// output -- run on one XCD and their partial cache lines can merge in its L2.  A block whose
+// queue is empty takes from the next queue: a tile's predecessors precede it in its queue, so
+// they were claimed by running blocks (forward progress as in claim_order_kernel).
+// xq[0..7] queue lengths, xq[8..16] queue offsets, xq[32 + off + i] the i-th tile of a queue.
+__global__ __launch_bounds__(256) void xcd_order_kernel(const uint32_t* __restrict__ tfirst, int nb, uint64_t ub,
+                                                        const SegTile* __restrict__ tiles, uint32_t* __restrict__ xq) {
+    __shared__ uint32_t s_n[1 << kMaxSegBucketBits];
+    __shared__ uint32_t s_off[9];
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) s_n[b] = tfirst[b + 1] - tfirst[b];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t o = 0;
+        for (int x = 0; x < 8; ++x) {
+            uint32_t len = 0;
+            for (int b = x; b < nb; b += 8) len += s_n[b];
+            s_off[x] = o;
+            if (blockIdx.x == 0) {
+                xq[x] = len;
+                xq[8 + x] = o;
+            }
+            o += len;
+        }
+        s_off[8] = o;
+        if (blockIdx.x == 0) xq[16] = o;
+    }
+    __syncthreads();
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ub || t >= tfirst[nb]) return;
+    const SegTile d = tiles[t];
+    const uint32_t k = d.tb;
+    const int x = (int)(d.bucket & 7u);
+    uint32_t pos = 0;
+    for (int b = x; b < nb; b += 8) {
+        const uint32_t n = s_n[b];
+        pos += (n < k ? n : k) + ((uint32_t)b < d.bucket && n > k ? 1u : 0u);
+    }
+    xq[32 + s_off[x] + pos] = (uint32_t)t;
+}
+
 __global__ __launch_bounds__(kBlock) void seg_upsweep(const uint64_t* __restrict__ rec, const SegTile* __restrict__ tiles,
                                                       int shift, uint32_t* __restrict__ hist) {
     __shared__ uint32_t h[kWaves][kDigits];
@@ -398,7 +441,8 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
                                                           int shift, int pass, int npass,
                                                           const uint32_t* __restrict__ dbase, uint32_t* status,
                                                           uint32_t* tile_counter, uint32_t* err,
-                                                          uint32_t* __restrict__ ghist_next) {
+                                                          uint32_t* __restrict__ ghist_next,
+                                                          const uint32_t* __restrict__ xq) {
     constexpr int kT = kIPT * OB;
     constexpr bool late = MUMS_OS_LATEPUB || kLate;
     constexpr int kW = OB / 64;
@@ -414,17 +458,33 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
     __shared__ uint32_t hcnt[kDigits];
     __shared__ uint32_t hnext[kDigits];   // next pass's digit counts (ghist_next != null)
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    if (tid == 0) s_tile = atomicAdd(tile_counter, 1u);
+    if (tid == 0) {
+        if (xq) {   // XCD-grouped queues (xcd_order_kernel): s_tile = the tile itself
+            uint32_t tt = 0xFFFFFFFFu;
+            const uint32_t x = blockIdx.x & 7u;
+            for (uint32_t a = 0; a < 8; ++a) {
+                const uint32_t q = (x + a) & 7u;
+                const uint32_t cc = atomicAdd(tile_counter + q, 1u);
+                if (cc < xq[q]) {
+                    tt = xq[32 + xq[8 + q] + cc];
+                    break;
+                }
+            }
+            s_tile = tt;
+        } else {
+            s_tile = atomicAdd(tile_counter, 1u);
+        }
+    }
     for (int i = tid; i < kW * kDigits; i += OB) (&wcnt[0][0])[i] = 0;
     if (tid < kDigits) { hcnt[tid] = 0; hnext[tid] = 0; }
     __syncthreads();
     const uint32_t c = __builtin_amdgcn_readfirstlane(s_tile);   // uniform: scalar descriptor loads
-    if (c >= nclaims) return;
+    if (xq ? c == 0xFFFFFFFFu : c >= nclaims) return;
 #if MUMS_OS_CTILES
     const SegTile d = tiles[c];   // claim-ordered copy (claim_tiles_kernel)
     const uint32_t t = __builtin_amdgcn_readfirstlane(d.order);
 #else
-    const uint32_t t = __builtin_amdgcn_readfirstlane(tiles[c].order);
+    const uint32_t t = xq ? c : __builtin_amdgcn_readfirstlane(tiles[c].order);
     const SegTile d = tiles[t];
 #endif
     if (d.count == 0) return;
@@ -1194,6 +1254,8 @@ static int os_variant() {
     }();
     return v;
 }
+// MUMS_DEV_OS_XCD (read per call): XCD-grouped claim queues, development A/B
+static bool os_xcd() { return getenv("MUMS_DEV_OS_XCD") != nullptr; }
 static int os_tile() {
     static const int t[9] = {kSortTile, 8192, 6144, 6144, 4096, 4096, 8192, 8192, 8960};
     return MUMS_SORT_PERSIST ? kSortTile : t[os_variant()];
@@ -1203,7 +1265,7 @@ size_t onesweep_tmp_bytes(uint64_t n, int msd_bits, int key_bits) {
     const uint64_t ub = seg_tiles_upper(n, msd_bits, os_tile());
     const int npass = (key_bits + 7) / 8;
     const uint64_t nb = 1ull << msd_bits;
-    const size_t b = (ub * kDigits * (uint64_t)npass + 2 * nb * npass * kDigits + 64 + 64) * 4 +
+    const size_t b = (ub * kDigits * (uint64_t)npass + 2 * nb * npass * kDigits + 256 + 64) * 4 +
                      2 * (ub * sizeof(SegTile) + 256) + seg_build_tmp_bytes(nb) + segfix_cap(n) * 4 +
                      256;   // + the claim-ordered copy, the fix-up's big list
     return seg_wide_sort_enabled() ? std::max(b, onesweep_wide_tmp_bytes(n, msd_bits, key_bits)) : b;
@@ -1272,7 +1334,7 @@ hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key
     uint32_t* ghist = status + ub_status(ub, npass);           // [nb][npass][256]
     uint32_t* dbase = ghist + nb * npass * kDigits;            // [nb][npass][256]
     uint32_t* counters = dbase + nb * npass * kDigits;         // [npass] + ntiles
-    const size_t zero_bytes = ((uint64_t)(counters - status) + 64) * 4;
+    const size_t zero_bytes = ((uint64_t)(counters - status) + 256) * 4;   // + the XCD queue counters
     SegTile* stiles = (SegTile*)((char*)d_tmp + ((zero_bytes + 255) & ~(size_t)255));
     SegTile* ctiles = (SegTile*)((char*)stiles + ((ub * sizeof(SegTile) + 255) & ~(size_t)255));
     void* btmp = (void*)((char*)ctiles + ((ub * sizeof(SegTile) + 255) & ~(size_t)255));
@@ -1283,8 +1345,14 @@ hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key
 #if MUMS_OS_CTILES
     hipLaunchKernelGGL(claim_tiles_kernel, dim3((unsigned)((ub + 255) / 256)), dim3(256), 0, st, stiles, ub, ctiles);
     const SegTile* otiles = ctiles;   // what the onesweep launches read
+    uint32_t* xq = nullptr;
 #else
     const SegTile* otiles = stiles;
+    // XCD-grouped claim queues (development A/B): the unused claim-ordered copy's room
+    uint32_t* xq = (os_xcd() && !key_runs && !MUMS_SORT_PERSIST) ? (uint32_t*)ctiles : nullptr;
+    if (xq)
+        hipLaunchKernelGGL(xcd_order_kernel, dim3((unsigned)((ub + 255) / 256)), dim3(256), 0, st,
+                           (const uint32_t*)btmp, (int)nb, ub, stiles, xq);
 #endif
     const unsigned gblocks = (unsigned)((ub + kGhistTilesPerBlock - 1) / kGhistTilesPerBlock);
     // the histogram read counts digit 0 only when every later pass's digits are
@@ -1324,13 +1392,14 @@ hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key
             uint32_t* gn = (nexthist && p + 1 < npass) ? ghist : (uint32_t*)nullptr;
             uint32_t* sp = status + (uint64_t)p * ub * kDigits;
             const int sh = key_shift + 8 * p;
+            uint32_t* tc = xq ? counters + 128 + 8 * p : counters + p;
 #define MUMS_OS_LAUNCH(OB, IPT, AL)                                                                               \
     hipLaunchKernelGGL((seg_onesweep_kernel<OB, IPT, AL>), dim3((unsigned)ub), dim3(OB), 0, st, src, dst, otiles, \
-                       (uint32_t)ub, sh, p, npass, dbase, sp, counters + p, d_err, gn)
+                       (uint32_t)ub, sh, p, npass, dbase, sp, tc, d_err, gn, xq)
             if (key_runs) {   // equal-digit runs: publish after the ranking (no per-record LDS atomics)
                 hipLaunchKernelGGL((seg_onesweep_kernel<kSortBlock, kSortTile / kSortBlock, true, true>),
                                    dim3((unsigned)ub), dim3(kSortBlock), 0, st, src, dst, otiles, (uint32_t)ub, sh, p,
-                                   npass, dbase, sp, counters + p, d_err, gn);
+                                   npass, dbase, sp, counters + p, d_err, gn, (const uint32_t*)nullptr);
             } else
             switch (os_variant()) {
             case 1: MUMS_OS_LAUNCH(512, 16, true); break;

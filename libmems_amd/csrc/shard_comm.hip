@@ -359,7 +359,7 @@ int shard_restart_local(mums_ctx* ctx, mums_comm* comm, hipStream_t st, bool* do
         if (dbg) fprintf(stderr, "rank %d: plan step of rank %d: %lu restarts, undecidable %lu\n", R, r,
                          (unsigned long)m[1], (unsigned long)m[2]);
         if (m[2]) {   // undecidable on rank r: the gathered plan (nothing changed yet)
-            if (mums::ctx_repeat_tol(ctx) > 0) {   // (which does not order every run of equal keys)
+            if (mums::ctx_tie_all(ctx)) {   // (which does not order every run of equal keys)
                 comm->err = "sharded repeat tolerance: a restart plan needs keys beyond a rank's neighbours";
                 return MUMS_E_UNSUPPORTED;
             }
@@ -393,7 +393,7 @@ int shard_restart_local(mums_ctx* ctx, mums_comm* comm, hipStream_t st, bool* do
     // repeat tolerance: every run of equal keys in std::sort order.  Pair flags go to rank
     // g % W (blocks in rank order = SML order), which replays genome g's sort and returns each
     // rank the ids of its slots in the same layout.
-    const bool rtol = mums::ctx_repeat_tol(ctx) > 0;
+    const bool rtol = mums::ctx_tie_all(ctx);   // repeat tolerance or enumeration tolerance > 1
     if (rtol) {
         auto part = [&](int r, uint32_t g) { return ALL[(size_t)r * row + g]; };
         std::vector<uint64_t> gofs(Gu, 0), sb(W, 0), rb(W, 0);

@@ -33,12 +33,14 @@ def md5_text(ml):
     return hashlib.md5(ml.text().encode()).hexdigest()
 
 
-@pytest.mark.parametrize("sort3", [None, "1"], ids=["four_pass", "three_pass"])
-def test_c3_findmatches_known_answer(gpu_lib, oracle_mod, monkeypatch, sort3):
-    """sort3: the three 10-bit passes with the parity bit unsorted (radix_wide.hip)."""
+@pytest.mark.parametrize("variant", [None, ("MUMS_DEV_SORT3", "3"), ("MUMS_DEV_OS_XCD", "1")],
+                         ids=["four_pass", "three_pass", "xcd_queues"])
+def test_c3_findmatches_known_answer(gpu_lib, oracle_mod, monkeypatch, variant):
+    """variant: the three 10-bit passes with the parity bit unsorted (radix_wide.hip), or the
+    XCD-grouped claim queues of the four-pass sort."""
     import torch
-    if sort3:
-        monkeypatch.setenv("MUMS_DEV_SORT3", sort3)
+    if variant:
+        monkeypatch.setenv(*variant)
     c = case("c3")
     seqs = oracle_mod.generate(c["G"], c["n"], c["p"], c["gen_seed"])
     dev = [torch.frombuffer(bytearray(s), dtype=torch.uint8).cuda() for s in seqs]

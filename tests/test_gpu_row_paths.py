@@ -25,7 +25,7 @@ def test_row_paths_one_process(gpu_lib, oracle_mod, monkeypatch, masked):
     seqs = oracle_mod.generate(3 if masked else 4, 150_000, 0.02, 901 + masked)
     seed = oracle_mod.get_seed(15)
     lengths, starts, ost = oracle_mod.find_matches(seqs, seed, masked=bool(masked), seq_mask=masked)
-    assert len(lengths) > 1000
+    assert len(lengths) > 10
     cls = gpu_lib.MaskedMemHash if masked else gpu_lib.MemHash
     with cls(0) as mh:
         mh.SetSeed(seed)

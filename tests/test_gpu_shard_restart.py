@@ -23,16 +23,18 @@ PATHS = {"local": 0, "gather": 0}   # restarts planned per path (reported by tes
 
 
 def check(lm, oracle_mod, seqs, world, w=15, layout="blocks", start_points=None, table_size=40000, info=None,
-          repeat_tol=0):
+          repeat_tol=0, enum_tol=1):
     if layout == "slices":   # world / G position slices per genome
         world = len(seqs) * (1 if world <= len(seqs) else 2)
     seed = oracle_mod.get_seed(w)
     with oracle_mod.sml_tie_rule("std"):
         ref_len, ref_starts, ref = oracle_mod.find_matches(seqs, seed, start_points=start_points,
-                                                           table_size=table_size, repeat_tol=repeat_tol)
+                                                           table_size=table_size, repeat_tol=repeat_tol,
+                                                           enum_tol=enum_tol)
     with lm.ShardedMemHash([0] * world, comm="local", layout=layout, table_size=table_size) as sh:
         sh.SetSeed(seed)
         sh.SetRepeatTolerance(repeat_tol)
+        sh.SetEnumerationTolerance(enum_tol)
         if start_points is None:
             ml = sh.FindMatches(seqs)
         else:
@@ -263,3 +265,29 @@ def test_undecidable_plan_falls_back_to_gathered(gpu_lib, oracle_mod, monkeypatc
     info = []
     ref = check(gpu_lib, oracle_mod, seqs, 2, info=info)
     assert ref["restarts"] > 0 and all(i["path"] == 2 for i in info), info
+
+
+# enumeration tolerance > 1 (MemHash.cpp:139-162, MatchFinder.cpp:342-393) over the ranks: each
+# rank enumerates the groups of its key range, the copies in std::sort order (mums_shard_tie_*)
+ETOL_CASES = {k: v for k, v in tie_inputs.CASES.items()
+              if v[1].get("enum_tol", 1) > 1 and not v[1].get("cls") and v[1].get("w", 15) <= 21}
+
+
+@pytest.mark.parametrize("name", sorted(ETOL_CASES))
+@pytest.mark.parametrize("world,layout", [(2, "blocks"), (3, "slices")])
+def test_enumeration_tolerance(gpu_lib, oracle_mod, name, world, layout):
+    gen, o = ETOL_CASES[name]
+    check(gpu_lib, oracle_mod, gen(), world, w=o.get("w", 15), layout=layout, repeat_tol=o.get("repeat_tol", 0),
+          enum_tol=o["enum_tol"], start_points=o.get("start_points"))
+
+
+@pytest.mark.parametrize("etol,rtol", [(2, 1), (3, 2), (8, 7)])
+def test_enumeration_tolerance_repeats(gpu_lib, oracle_mod, etol, rtol):
+    seqs = repeat_inputs.high_copy(G=3, n=60_000, copies=40, tandem=False, seed=etol)
+    check(gpu_lib, oracle_mod, seqs, 3, repeat_tol=rtol, enum_tol=etol)
+
+
+def test_enumeration_tolerance_with_restarts(gpu_lib, oracle_mod):
+    seqs = repeat_inputs.n_gapped(G=3, n=200_000, gaps=((40_000, 3000), (120_000, 3000)), shift=500, seed=1)
+    ref = check(gpu_lib, oracle_mod, seqs, 2, repeat_tol=1, enum_tol=2)
+    assert ref["restarts"] > 0

@@ -110,3 +110,20 @@ def test_sort3_start_points_and_repeat_tol(gpu_lib, oracle_mod, monkeypatch):
     _vs_oracle(gpu_lib, oracle_mod, seqs, 15, start_points=[3, 9_999, 10_001, 40_000])
     seqs = oracle_mod.generate(3, 200_000, 0.02, 5)
     _vs_oracle(gpu_lib, oracle_mod, seqs, 15, repeat_tol=2)
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"G{c['G']}_n{c['n']}_p{c['p']}_{c['mode']}")
+def test_xcd_claim_queues_known_answers(gpu_lib, oracle_mod, monkeypatch, case):
+    """The four-pass sort with XCD-grouped claim queues (MUMS_DEV_OS_XCD: bucket b's tiles in
+    queue b % 8, blocks claim from queue blockIdx % 8 first, then steal): same MatchList."""
+    monkeypatch.setenv("MUMS_DEV_OS_XCD", "1")
+    seqs = oracle_mod.generate(case["G"], case["n"], case["p"], 12345)
+    masked = case["mode"] == "MaskedMemHash"
+    cls = gpu_lib.MaskedMemHash if masked else gpu_lib.MemHash
+    with cls(0) as mh:
+        mh.SetSeed(oracle_mod.get_seed(case["w"]))
+        if masked:
+            mh.SetMask(case.get("mask", 0))
+        ml = mh.FindMatches(seqs)
+    assert len(ml) == case["matches"]
+    assert hashlib.md5(ml.text().encode()).hexdigest() == case["md5"]
