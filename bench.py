@@ -486,11 +486,22 @@ def main():
                 dist.all_reduce(red, op=dist.ReduceOp.SUM)
             best = float(tmx.item())
             matches = int(red[1].item())
+            # every rank's chain stage: the probes it labelled (its key range) and the time
+            ci = stage.chain_info() if hasattr(stage, "chain_info") else {"probes": 0, "ms": 0.0}
+            per = torch.tensor([[float(ci["probes"]), ci["ms"], float(sm["probes"]), float(sm["ms_replay"])]],
+                               dtype=torch.float64)
+            allr = [torch.zeros_like(per) for _ in range(world)] if world > 1 else [per]
+            if world > 1:
+                dist.all_gather(allr, per)
+            ranks_chain = [{"labelled_probes": int(a[0, 0].item()), "ms_label": round(float(a[0, 1].item()), 3),
+                            "replayed_rows": int(a[0, 2].item()), "ms_replay": round(float(a[0, 3].item()), 3)}
+                           for a in allr]
             mums_c3 = {"mums_per_s": matches / best, "matches": matches, "ms": best * 1e3,
                        "probes": int(red[2].item()), "collisions": int(red[3].item()),
                        "workload": f"BASELINE config 3: {G} x {n // 10**6} Mbp related p=0.01, w19, full FindMatches "
                                    f"sharded over {world} rank(s) (mums_shard_run)",
                        "rank0_phase_ms": {k: round(sm[k], 3) for k in ("ms_chains", "ms_replay", "ms_output")},
+                       "ranks_chain_stage": ranks_chain,
                        "exchange": ("RCCL communicator inside libmums_hip.so (ncclCommInitRank): grouped "
                                     "ncclSend/ncclRecv all-to-allv, ncclAllGather of counts" if args.exchange == "abi"
                                     else f"torch.distributed {args.dist_backend} all_to_all (shard.py)")}

@@ -184,8 +184,8 @@ struct TileRecViewT {
     }
 };
 
-template <int MG, int IB>
-__global__ __launch_bounds__(kBlock) void probe_tile_rec_kernel(const uint64_t* __restrict__ rec,
+template <int MG, int IB, bool kGl = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGl ? 6 : 1))) void probe_tile_rec_kernel(const uint64_t* __restrict__ rec,
                                                                 const SegTile* __restrict__ tiles, GenomeTable gt,
                                                                 MatchParams mp, int L,
                                                                 uint32_t* __restrict__ tile_count,
@@ -199,6 +199,8 @@ __global__ __launch_bounds__(kBlock) void probe_tile_rec_kernel(const uint64_t* 
     __shared__ uint32_t s_w[kBlock / 64];
     __shared__ uint32_t s_red[2];
     __shared__ uint64_t s_prev, s_next;
+    __shared__ uint8_t s_gl[256];
+    __shared__ uint32_t s_gb[kMaxG + 1];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const SegTile td = tiles[blockIdx.x / kGSplit];
     const uint32_t part0 = (blockIdx.x % kGSplit) * (uint32_t)kGSub;
@@ -231,6 +233,13 @@ __global__ __launch_bounds__(kBlock) void probe_tile_rec_kernel(const uint64_t* 
     }
     if (threadIdx.x == 0) s_prev = (tile0 > td.bstart) ? rec[tile0 - 1] : ~0ull;
     if (threadIdx.x == 64) s_next = (tile0 + cnt < td.bend) ? rec[tile0 + cnt] : ~0ull;
+    // the coarse genome lookup in LDS (GenomeTable gl_*; 32-bit indices)
+    constexpr bool use_gl = kGl && IB == 32;   // (the launcher checks gt.gl_n)
+    if constexpr (use_gl) {
+        for (uint32_t i = threadIdx.x; i < gt.gl_n; i += kBlock) s_gl[i] = gt.gl[i];
+        for (int i = threadIdx.x; i <= kMaxG; i += kBlock) s_gb[i] = (uint32_t)gt.base[i];
+    }
+    const GLook glk{(lds_u8c*)s_gl, (lds_u32c*)s_gb, gt.gl_shift, gt.gl_n ? gt.gl_n - 1 : 0};
     __syncthreads();
 
     // 2) group heads in stream order; a head is kept only when its group has >= 2
@@ -306,7 +315,7 @@ __global__ __launch_bounds__(kBlock) void probe_tile_rec_kernel(const uint64_t* 
                     for (int k = 0; k <= MG; ++k)
                         xb[k] = ((uint32_t)k <= (uint32_t)gt.G && h + k < td.bend) ? rec[h + k] : ~0ull;
                 }
-                ok = probe_fast_raw<MG, IB>(xb, gt, mp, L, &off, &gsz);
+                ok = probe_fast_raw<MG, IB, use_gl>(xb, gt, mp, L, &off, &gsz, &glk);
                 if (gsz > (uint32_t)gt.G) {   // oversize group: rejected; count on for the report
                     uint64_t i = h + gsz;
                     const uint32_t k0 = (uint32_t)(xb[0] >> (IB + 1));
@@ -373,7 +382,7 @@ __global__ void flat_tiles_kernel(uint64_t N, uint64_t nt, SegTile* __restrict__
 // probe_info) as one batch of independent loads (probe_row_fast).  lkey / fsk (optional):
 // the chain labelling's line key (chains.hip) and the first-genome start of probe k, so
 // neither re-reads the rows.
-template <int MG, typename View>
+template <int MG, typename View, bool kGl = false>
 __global__ __launch_bounds__(kBlock) void probe_materialize_kernel(View v, const uint64_t* __restrict__ probe_info,
                                                                    uint64_t P, GenomeTable gt, MatchParams mp, int L,
                                                                    int64_t* __restrict__ rows, uint64_t* __restrict__ lkey,
@@ -383,6 +392,15 @@ __global__ __launch_bounds__(kBlock) void probe_materialize_kernel(View v, const
     const uint64_t k = k0 + threadIdx.x;
     const int W = gt.G + 1;
     Mhe<MG> Q;
+    __shared__ uint8_t s_gl[256];
+    __shared__ uint32_t s_gb[kMaxG + 1];
+    constexpr bool use_gl = kGl && RecIB<View>::value == 32;   // (the launcher checks gt.gl_n)
+    if constexpr (use_gl) {   // the coarse genome lookup in LDS (GenomeTable gl_*)
+        for (uint32_t i = threadIdx.x; i < gt.gl_n; i += kBlock) s_gl[i] = gt.gl[i];
+        for (int i = threadIdx.x; i <= kMaxG; i += kBlock) s_gb[i] = (uint32_t)gt.base[i];
+        __syncthreads();
+    }
+    const GLook glk{(lds_u8c*)s_gl, (lds_u32c*)s_gb, gt.gl_shift, gt.gl_n ? gt.gl_n - 1 : 0};
     if (k < P) {
         const uint64_t info = probe_info[k];
         const uint64_t h = info & 0xFFFFFFFFull;
@@ -393,7 +411,7 @@ __global__ __launch_bounds__(kBlock) void probe_materialize_kernel(View v, const
                 uint64_t x[MG];
                 #pragma unroll
                 for (int q = 0; q < MG; ++q) x[q] = (uint32_t)q < gsz ? v.rec[h + q] : ~0ull;
-                probe_row_fast<MG, RecIB<View>::value>(x, gsz, gt, L, Q);
+                probe_row_fast<MG, RecIB<View>::value, use_gl>(x, gsz, gt, L, Q, &glk);
                 done = true;
             }
         }
@@ -638,8 +656,12 @@ hipError_t launch_materialize(View v, const uint64_t* probe_info, uint64_t P, co
                               const MatchParams& mp, int L, int64_t* rows, hipStream_t st, uint64_t* lkey,
                               uint32_t* fsk, uint32_t* lhash, int32_t* rows32) {
     if (P == 0) return hipSuccess;
-    hipLaunchKernelGGL((probe_materialize_kernel<MG, View>), dim3((unsigned)((P + kBlock - 1) / kBlock)), dim3(kBlock),
-                       0, st, v, probe_info, P, gt, mp, L, rows, lkey, fsk, lhash, rows32);
+    if (RecIB<View>::value == 32 && gt.gl_n > 0)   // the coarse genome lookup (GenomeTable gl_*)
+        hipLaunchKernelGGL((probe_materialize_kernel<MG, View, true>), dim3((unsigned)((P + kBlock - 1) / kBlock)),
+                           dim3(kBlock), 0, st, v, probe_info, P, gt, mp, L, rows, lkey, fsk, lhash, rows32);
+    else
+        hipLaunchKernelGGL((probe_materialize_kernel<MG, View>), dim3((unsigned)((P + kBlock - 1) / kBlock)),
+                           dim3(kBlock), 0, st, v, probe_info, P, gt, mp, L, rows, lkey, fsk, lhash, rows32);
     return hipGetLastError();
 }
 
@@ -673,10 +695,16 @@ hipError_t launch_probe_tiles(View v, const SegTile* tiles, uint64_t ntiles, uin
                               const MatchParams& mp, int L, uint32_t* tile_count, uint64_t* slot_info,
                               uint32_t* slot_bucket, void* counters, hipStream_t st) {
     if (ntiles == 0) return hipSuccess;
-    if constexpr (RecIB<View>::value > 0)
-        hipLaunchKernelGGL((probe_tile_rec_kernel<MG, RecIB<View>::value>), dim3((unsigned)(ntiles * kGSplit)), dim3(kBlock), 0, st, v.rec,
-                           tiles, gt, mp, L, tile_count, slot_info, slot_bucket, (DevCounters*)counters);
-    else
+    if constexpr (RecIB<View>::value > 0) {
+        if (RecIB<View>::value == 32 && gt.gl_n > 0)   // the coarse genome lookup (GenomeTable gl_*)
+            hipLaunchKernelGGL((probe_tile_rec_kernel<MG, RecIB<View>::value, true>), dim3((unsigned)(ntiles * kGSplit)),
+                               dim3(kBlock), 0, st, v.rec, tiles, gt, mp, L, tile_count, slot_info, slot_bucket,
+                               (DevCounters*)counters);
+        else
+            hipLaunchKernelGGL((probe_tile_rec_kernel<MG, RecIB<View>::value>), dim3((unsigned)(ntiles * kGSplit)),
+                               dim3(kBlock), 0, st, v.rec, tiles, gt, mp, L, tile_count, slot_info, slot_bucket,
+                               (DevCounters*)counters);
+    } else
         hipLaunchKernelGGL((probe_tile_kernel<MG, View>), dim3((unsigned)ntiles), dim3(kBlock), 0, st, v, tiles, N, gt,
                            mp, L, tile_count, slot_info, slot_bucket, (DevCounters*)counters);
     return hipGetLastError();

@@ -312,9 +312,28 @@ __device__ __forceinline__ uint32_t bucket_of_fast(int64_t offset, uint32_t tabl
 // results as probe_offset_fast.  gsize_batch = equal-key run length inside the batch
 // (the caller walks on when it exceeds G).  Genome and base of each record come from
 // one unrolled compare/select pass over the (32-bit) genome bases.
-template <int MG, int IB = 32>
+// The coarse genome lookup of GenomeTable (gl_*) staged in LDS by the calling kernel: a
+// record's genome and base from two LDS reads instead of G - 1 compares and selects.
+typedef __attribute__((address_space(3))) const uint8_t lds_u8c;
+typedef __attribute__((address_space(3))) const uint32_t lds_u32c;
+struct GLook {
+    lds_u8c* tab;     // gl[], gl_n entries
+    lds_u32c* base;   // base[0 .. kMaxG] as uint32 (N < 2^32)
+    uint32_t shift, last;
+};
+__device__ __forceinline__ void glook(const GLook& l, uint32_t idx, uint32_t* g, uint32_t* b) {
+    const uint32_t s = min(idx >> l.shift, l.last);   // (padding records: idx ~0)
+    const uint32_t t = l.tab[s];
+    const uint32_t b0 = l.base[t], b1 = l.base[t + 1];
+    const bool ge = idx >= b1;
+    *g = t + (ge ? 1u : 0u);
+    *b = ge ? b1 : b0;
+}
+
+template <int MG, int IB = 32, bool kGl = false>
 __device__ __forceinline__ bool probe_fast_raw(const uint64_t (&x)[MG + 1], const GenomeTable& gt,
-                                               const MatchParams& mp, int L, int64_t* offset, uint32_t* gsize) {
+                                               const MatchParams& mp, int L, int64_t* offset, uint32_t* gsize,
+                                               const GLook* glk = nullptr) {
     const uint32_t G = (uint32_t)gt.G;
     const uint32_t k0 = (uint32_t)(x[0] >> (IB + 1));
     uint32_t cnt = 0;
@@ -340,12 +359,18 @@ __device__ __forceinline__ bool probe_fast_raw(const uint64_t (&x)[MG + 1], cons
         const IdxT idx = (IdxT)(x[k] & ((1ull << IB) - 1));
         uint32_t g = 0;
         IdxT b = 0;
-        #pragma unroll
-        for (int j = 1; j < MG; ++j) {
-            const IdxT bj = (IdxT)gt.base[j];
-            const bool ge = (uint32_t)j < G && idx >= bj;
-            g = ge ? (uint32_t)j : g;
-            b = ge ? bj : b;
+        if constexpr (kGl && IB == 32) {
+            uint32_t bb;
+            glook(*glk, (uint32_t)idx, &g, &bb);
+            b = bb;
+        } else {
+            #pragma unroll
+            for (int j = 1; j < MG; ++j) {
+                const IdxT bj = (IdxT)gt.base[j];
+                const bool ge = (uint32_t)j < G && idx >= bj;
+                g = ge ? (uint32_t)j : g;
+                b = ge ? bj : b;
+            }
         }
         gk[k] = g;
         sk[k] = idx - b + 1u;   // 1-based start in genome g
@@ -378,9 +403,9 @@ __device__ __forceinline__ bool probe_fast_raw(const uint64_t (&x)[MG + 1], cons
 // group of cnt (<= G) records x[0 .. cnt) -- packed records (key << IB+1 | parity << IB | index);
 // the parity bit is part of the sort key, so the reference genome (the smallest present) is
 // found, not assumed first.  All loads are the caller's one batch; the same row as build_probe.
-template <int MG, int IB = 32>
+template <int MG, int IB = 32, bool kGl = false>
 __device__ __forceinline__ void probe_row_fast(const uint64_t (&x)[MG], uint32_t cnt, const GenomeTable& gt, int L,
-                                               Mhe<MG>& P) {
+                                               Mhe<MG>& P, const GLook* glk = nullptr) {
     using IdxT = typename std::conditional<(IB > 32), uint64_t, uint32_t>::type;
     const uint32_t G = (uint32_t)gt.G;
     int64_t st[MG];
@@ -390,12 +415,18 @@ __device__ __forceinline__ void probe_row_fast(const uint64_t (&x)[MG], uint32_t
         const IdxT idx = (IdxT)(x[k] & ((1ull << IB) - 1));
         uint32_t g = 0;
         IdxT b = 0;
-        #pragma unroll
-        for (int j = 1; j < MG; ++j) {
-            const IdxT bj = (IdxT)gt.base[j];
-            const bool ge = (uint32_t)j < G && idx >= bj;
-            g = ge ? (uint32_t)j : g;
-            b = ge ? bj : b;
+        if constexpr (kGl && IB == 32) {
+            uint32_t bb;
+            glook(*glk, (uint32_t)idx, &g, &bb);
+            b = bb;
+        } else {
+            #pragma unroll
+            for (int j = 1; j < MG; ++j) {
+                const IdxT bj = (IdxT)gt.base[j];
+                const bool ge = (uint32_t)j < G && idx >= bj;
+                g = ge ? (uint32_t)j : g;
+                b = ge ? bj : b;
+            }
         }
         gk[k] = (uint32_t)k < cnt ? g : 0xFFu;
         pk[k] = (uint32_t)(x[k] >> IB) & 1u;

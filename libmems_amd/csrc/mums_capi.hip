@@ -104,6 +104,7 @@ struct mums_ctx {
     uint64_t prelab_n = 0;      // entries in pool_loc
     const int64_t* lab_rows = nullptr;   // sharded: the rank's own probe rows the labels refer to
     uint64_t lab_nch = 0;                // sharded: chains labelled among them
+    uint64_t lab_p = 0;                  // sharded: probes labelled (the rank's own)
     double lab_ms = 0;                   // sharded: device time of the labelling
     bool pairwise = false;   // PairwiseMatchFinder (pairwise.hip)
     uint64_t chunk_size = 200000;
@@ -132,7 +133,9 @@ struct mums_ctx {
     DevBuf crbuf, crcnt, crlive, crruns;  // chunked-mode restarts (chunked.hip)
     uint64_t cr_cands = 0;                // groups above MER_REPEAT_LIMIT (chunked restart)
     DevBuf crall;                         // sharded restart planner: the whole stream's SMLs
-    bool shard_restart_pending = false;   // mums_shard_merge saw a group above the limit / start points
+    bool shard_restart_pending = false;
+    uint64_t live_n = 0;                   // sharded: the live stream's records (after a restart)
+    std::vector<uint32_t> live_bst;        // and its local bucket starts   // mums_shard_merge saw a group above the limit / start points
     int shard_mb = 0;                     // local bucket bits of the last mums_shard_merge
     int shard_side = 0;                   // 33-bit records at w20-21: side bits split below the 8-bit scatter
     uint64_t shard_n = 0;                 // its records
@@ -1368,6 +1371,7 @@ int prepare_run(mums_ctx* ctx, const std::vector<uint64_t>& lens) {
     }
     gt.base[G] = N;
     for (int g = G + 1; g <= kMaxG; ++g) gt.base[g] = N;
+    genome_lookup_init(gt);
     if (N >= (1ull << 33))
         return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^33 seed-mers per context");
     ctx->N = N;
@@ -2503,17 +2507,17 @@ bool shard_rows_from_all(const mums_ctx* ctx) { return ctx->merge_chunked || ctx
 int shard_enum_rows(mums_ctx* ctx, hipStream_t st) {
     if (ctx->rec_ib != 32)
         return fail(ctx, MUMS_E_UNSUPPORTED, "sharded enumeration tolerance > 1 above 2^32 seed-mers (33-bit records)");
-    const uint64_t n = ctx->shard_n;
+    const uint64_t n = ctx->live_n;   // the live stream (after a restart: its live records)
     const int G = ctx->gt.G;
     const MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, ctx->masked, ctx->seq_mask};
     DevCounters* dc = ctx->counters.as<DevCounters>();
-    const uint32_t nb = (uint32_t)ctx->shard_bst.size() - 1;
+    const uint32_t nb = (uint32_t)ctx->live_bst.size() - 1;
     HIPCHK(ctx->ckey.ensure(n * 8 + 64));
     HIPCHK(ctx->cval.ensure(2 * (n + 64) * 4 + (uint64_t)(nb + 1) * 4));
     uint32_t* idx = ctx->cval.as<uint32_t>();
     uint32_t* ncalls = idx + n + 64;
     uint32_t* d_bst = ncalls + n + 64;
-    HIPCHK(hipMemcpyAsync(d_bst, ctx->shard_bst.data(), (uint64_t)(nb + 1) * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_bst, ctx->live_bst.data(), (uint64_t)(nb + 1) * 4, hipMemcpyHostToDevice, st));
     HIPCHK(launch_rec_pairs(ctx->sorted_rec, n, d_bst, nb, ctx->shard_kfirst, 2 * ctx->w + 1 - ctx->msd_bits,
                             ctx->ckey.as<uint64_t>(), idx, st));
     const PairView<uint64_t> v{ctx->ckey.as<uint64_t>(), idx};
@@ -2563,6 +2567,8 @@ int shard_regroup(mums_ctx* ctx, uint64_t* dst, uint64_t nl, const std::vector<u
     if (ctx->merge_chunked) {   // the live stream's key chunks (seed-stage counts; rows on export)
         ctx->shard_bst = bst;
         ctx->shard_n = nl;
+        ctx->live_n = nl;
+        ctx->live_bst = bst;
         ctx->shard_rows_built = false;
         HIPCHK(hipMemsetAsync(dc, 0, sizeof(DevCounters), st));
         const int rc = shard_groups_chunked(ctx, dst, bst, ps, false, st);
@@ -2579,6 +2585,8 @@ int shard_regroup(mums_ctx* ctx, uint64_t* dst, uint64_t nl, const std::vector<u
         return MUMS_OK;
     }
     HIPCHK(hipMemcpyAsync(ctx->mstart.p, bst.data(), bst.size() * 4, hipMemcpyHostToDevice, st));
+    ctx->live_n = nl;
+    ctx->live_bst = bst;
     SegTile* tiles = ctx->tiles.as<SegTile>();
     HIPCHK(build_seg_tiles_from_starts(ctx->mstart.as<uint32_t>(), mb, nl, tiles, &dc->ntiles, ctx->tmp.p, st));
     HIPCHK(hipMemsetAsync(&dc->repeat_limit, 0, 8, st));
@@ -2720,6 +2728,8 @@ int mums_shard_merge(mums_ctx* ctx, const uint64_t* d_records, uint32_t nsources
     ctx->shard_kfirst = first_bucket;
     ctx->shard_kcount = nbuckets;
     ctx->shard_bst = bst;
+    ctx->live_n = n;
+    ctx->live_bst = bst;
     ctx->ds_ready = false;
     ctx->stage_done = MUMS_STAGE_SEEDS;
     HIPCHK(hipStreamSynchronize(st));
@@ -4619,6 +4629,7 @@ int mums_shard_chain_label(mums_ctx* ctx, const uint32_t* d_packed_all, uint64_t
     }
     ctx->lab_rows = src;
     ctx->lab_nch = 0;
+    ctx->lab_p = P;
     ctx->lab_ms = 0;
     if (nchains) *nchains = 0;
     if (P == 0) return MUMS_OK;
@@ -4754,7 +4765,7 @@ int mums_shard_chain_export(mums_ctx* ctx, uint32_t nranks, const uint32_t* boun
 
 int mums_shard_chain_info(mums_ctx* ctx, uint64_t* info) {
     if (check_ctx(ctx) || !info) return MUMS_E_INVALID;
-    info[0] = ctx->lab_rows ? ctx->P : 0;
+    info[0] = ctx->lab_p;
     info[1] = ctx->lab_nch;
     info[2] = (uint64_t)(ctx->lab_ms * 1000.0 + 0.5);
     info[3] = 0;

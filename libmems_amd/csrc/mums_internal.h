@@ -19,6 +19,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "restart_plan.h"
 
@@ -63,7 +64,37 @@ struct GenomeTable {
     uint64_t base[kMaxG + 1];   // global seed-mer index base; base[G] = N
     uint64_t woff[kMaxG + 1];   // word offset of genome g in the packed array
     uint32_t tfirst[kMaxG + 1]; // first key-kernel tile of genome g (tiles cover n_g bytes)
+    // coarse genome lookup (genome_lookup_init): gl[i >> gl_shift] = the genome of index
+    // i's bucket start; every genome is at least 2^gl_shift seed-mers long, so a bucket meets
+    // at most two genomes and g = gl[.] + (i >= base[gl[.] + 1]).  gl_n = 0: off.
+    uint32_t gl_shift;
+    uint32_t gl_n;
+    uint8_t gl[256];
 };
+
+// the coarse lookup table of gt (bases set; off when a genome is empty or the table would
+// need more than 256 buckets)
+inline void genome_lookup_init(GenomeTable& gt) {
+    gt.gl_n = 0;
+    gt.gl_shift = 0;
+    const uint64_t N = gt.base[gt.G];
+    if (gt.G < 2 || N == 0 || N >= (1ull << 32)) return;
+    if (getenv("MUMS_DEV_NO_GL")) return;   // development A/B: the compare-and-select lookup
+    uint64_t mn = ~0ull;
+    for (int g = 0; g < gt.G; ++g) mn = gt.m[g] < mn ? gt.m[g] : mn;
+    if (mn == 0) return;
+    const int sh = 63 - __builtin_clzll(mn);
+    const uint64_t nb = ((N - 1) >> sh) + 1;
+    if (nb > 256) return;
+    int g = 0;
+    for (uint64_t s = 0; s < nb; ++s) {
+        const uint64_t i = s << sh;
+        while (g + 1 < gt.G && gt.base[g + 1] <= i) ++g;
+        gt.gl[s] = (uint8_t)g;
+    }
+    gt.gl_shift = (uint32_t)sh;
+    gt.gl_n = (uint32_t)nb;
+}
 
 struct MatchParams {
     uint32_t repeat_tol;    // MemHash.h:31

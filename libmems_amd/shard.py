@@ -390,6 +390,14 @@ class AbiShardStage:
             raise RuntimeError(f"mums_shard_run: {lib.mums_last_error(self.engine.mh._ctx).decode()} / "
                                f"{lib.mums_comm_last_error(self.comm).decode()}")
 
+    def chain_info(self) -> dict:
+        """This rank's share of the last sharded FindMatches' chain stage (mums_shard_chain_info):
+        the probes whose chains it labelled (its own key range), the chain entries, the time."""
+        import numpy as np
+        ci = np.zeros(4, dtype=np.uint64)
+        self.engine.mh._check(self.engine.mh._lib.mums_shard_chain_info(self.engine.mh._ctx, ci.ctypes.data))
+        return {"probes": int(ci[0]), "chains": int(ci[1]), "ms": int(ci[2]) / 1000.0}
+
     def close(self) -> None:
         if self.comm:
             self.engine.mh._lib.mums_comm_destroy(self.comm)
