@@ -162,7 +162,7 @@ __global__ __launch_bounds__(256) void claim_tiles_kernel(const SegTile* __restr
     ctiles[c] = d;
 }
 
-// XCD-grouped claim queues (MUMS_DEV_OS_XCD, development A/B): bucket b's tiles form queue
+// XCD-grouped claim queues (default; MUMS_DEV_OS_XCD=0 turns them off): bucket b's tiles form queue
 // b % 8, in (tile-in-bucket, bucket) order inside the queue; blocks b and b + 8 share an XCD
 // (round-robin dispatch, MI355X_MICROARCH.md: a speed-only affinity), so a block claims from
 // queue blockIdx % 8 first: consecutive tiles of a bucket -- whose digit runs abut in the
@@ -1254,8 +1254,12 @@ static int os_variant() {
     }();
     return v;
 }
-// MUMS_DEV_OS_XCD (read per call): XCD-grouped claim queues, development A/B
-static bool os_xcd() { return getenv("MUMS_DEV_OS_XCD") != nullptr; }
+// XCD-grouped claim queues (default since round 5: 3.31 -> 3.04 ms per C3 pass, same box,
+// profiles/r05j_xcd_ab.txt); MUMS_DEV_OS_XCD=0 (read per call) restores the single queue
+static bool os_xcd() {
+    const char* e = getenv("MUMS_DEV_OS_XCD");
+    return !(e && e[0] == '0');
+}
 static int os_tile() {
     static const int t[9] = {kSortTile, 8192, 6144, 6144, 4096, 4096, 8192, 8192, 8960};
     return MUMS_SORT_PERSIST ? kSortTile : t[os_variant()];
@@ -1349,7 +1353,8 @@ hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key
 #else
     const SegTile* otiles = stiles;
     // XCD-grouped claim queues (development A/B): the unused claim-ordered copy's room
-    uint32_t* xq = (os_xcd() && !key_runs && !MUMS_SORT_PERSIST) ? (uint32_t*)ctiles : nullptr;
+    // (fewer than 8 MSD buckets: one queue is all there is)
+    uint32_t* xq = (os_xcd() && nb >= 8 && !MUMS_SORT_PERSIST) ? (uint32_t*)ctiles : nullptr;
     if (xq)
         hipLaunchKernelGGL(xcd_order_kernel, dim3((unsigned)((ub + 255) / 256)), dim3(256), 0, st,
                            (const uint32_t*)btmp, (int)nb, ub, stiles, xq);
@@ -1399,7 +1404,7 @@ hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key
             if (key_runs) {   // equal-digit runs: publish after the ranking (no per-record LDS atomics)
                 hipLaunchKernelGGL((seg_onesweep_kernel<kSortBlock, kSortTile / kSortBlock, true, true>),
                                    dim3((unsigned)ub), dim3(kSortBlock), 0, st, src, dst, otiles, (uint32_t)ub, sh, p,
-                                   npass, dbase, sp, counters + p, d_err, gn, (const uint32_t*)nullptr);
+                                   npass, dbase, sp, tc, d_err, gn, xq);
             } else
             switch (os_variant()) {
             case 1: MUMS_OS_LAUNCH(512, 16, true); break;
