@@ -42,6 +42,14 @@ _SUMMARIES = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]*_domin
 PROFILE_SUMMARY = _SUMMARIES[-1] if _SUMMARIES else os.path.join(ROOT, "profiles", "r01_dominant_kernel.json")
 
 
+_T0 = time.perf_counter()
+
+
+def progress(msg: str) -> None:
+    """Progress line on stderr (the JSON line alone goes to stdout)."""
+    print(f"[bench +{time.perf_counter() - _T0:.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def synth_genomes(G: int, n: int, p: float, seed: int, device: torch.device):
     """Synthetic related genomes on the GPU: genome 0 iid ACGT; genome g>0 = genome 0 with
     per-base substitution rate p; genome 2 reverse-complemented (SURVEY.md 8(d) shape)."""
@@ -272,6 +280,8 @@ def main():
     ap.add_argument("--length", type=int, default=100_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-mums", action="store_true")
+    ap.add_argument("--no-compat", action="store_true",
+                    help="skip the ParallelMemHash compat FindMatches at C3 (mums_c3_compat)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, default) or gloo (rehearsal)")
     ap.add_argument("--exchange", choices=("abi", "torch"), default="abi",
                     help="abi (default): the C ABI runs the sharded step with its own RCCL communicator "
@@ -386,6 +396,7 @@ def main():
             else:
                 dist.barrier()
 
+    progress(f"timed region: {args.steps} steps")
     # timed region: K steps, no per-pass instrumentation events
     barrier()
     torch.cuda.synchronize()
@@ -404,6 +415,7 @@ def main():
     dt = float(tmax.item())
     # after it, the same K steps with HIP events around every sort-pass launch (on the
     # context's stream) for the dominant kernel's live duration and the phase split
+    progress(f"timed region done: {dt / args.steps * 1e3:.3f} ms/step; profiled steps")
     mh.SetProfiling(True)
     for _ in range(args.steps):
         run()
@@ -419,6 +431,7 @@ def main():
     compat_c3 = None
     if world == 1 and args.workload == "c3" and not args.no_mums:
         # MUMs/s on the metric's own config: full FindMatches of the resident C3 genomes
+        progress("C3 FindMatches")
         try:
             mh.CreateMatches()   # warm
             best = float("inf")
@@ -454,14 +467,17 @@ def main():
                                     **walk_counter_traffic(walk_ms)}}
         except Exception as e:  # report, never hide
             mums_c3 = {"error": str(e)}
+        progress("C3 end to end")
         try:
             e2e_c3 = run_e2e(mh, genomes, seed)
         except Exception as e:  # report, never hide
             e2e_c3 = {"error": str(e)}
-        try:
-            compat_c3 = run_compat(local, genomes, seed)
-        except Exception as e:  # report, never hide
-            compat_c3 = {"error": str(e)}
+        if not args.no_compat:
+            progress("C3 ParallelMemHash compat")
+            try:
+                compat_c3 = run_compat(local, genomes, seed)
+            except Exception as e:  # report, never hide
+                compat_c3 = {"error": str(e)}
     elif sharded and args.workload == "c3" and not args.no_mums and hasattr(stage, "run_find"):
         # MUMs/s of the sharded FindMatches (mums_shard_run, all 8 steps: keys, record
         # all-to-allv, merge, bucket ranges, row all-to-allv, packed all-gather, chains + replay)
@@ -583,15 +599,18 @@ def main():
         if fallback is not None:
             out["exchange_fallback"] = fallback + " -> torch.distributed RCCL all_to_all (libmems_amd/shard.py)"
         if not args.no_mums:
+            progress("MUMs/s small configs")
             try:
                 out["mums"] = run_mums(local, dev, 0.01)
                 out["mums_iid"] = run_mums(local, dev, 1.0)
             except Exception as e:  # report, never hide
                 out["mums"] = {"error": str(e)}
         if not args.no_cpu_baseline and world == 1:
+            progress("CPU baselines")
             out["cpu_baseline"] = cpu_baseline()
             if not args.no_mums:
                 out["cpu_baseline_mums"] = cpu_baseline_mums()
+        progress("done")
         print(json.dumps(out), flush=True)
     if world > 1:
         barrier()

@@ -41,6 +41,10 @@ namespace {
 #define MUMS_WALK_BUDGET 8
 #endif
 constexpr int kWalkBudget = MUMS_WALK_BUDGET;   // words per lane in chain_walk_short_kernel
+#ifndef MUMS_WALK_SORT_SHIFT
+#define MUMS_WALK_SORT_SHIFT 11
+#endif
+constexpr int kWalkSortShift = MUMS_WALK_SORT_SHIFT;   // walk order granule: 2^11 columns
 #ifndef MUMS_HIT_BATCH
 #define MUMS_HIT_BATCH 2   // components whose window loads are in flight together (hit_word; A/B round 4: 1 / 2 / 4 / 8)
 #endif   // 64-column hit words per lane before a walk goes to a workgroup
@@ -469,6 +473,25 @@ __global__ __launch_bounds__(kBlock) void chain_left_kernel(uint64_t P, const ui
     block_push<kLinkIPT>(want, it, queue, qcount);
 }
 
+// Walk order by genome position: record (x >> shift) << 32 | q of queue item q, x = the
+// first start of its probe.  A walk reads the packed windows of every component around its
+// probe -- about one 128-B line per genome per walk, lines that the walks of nearby probes
+// (other lines of the same region: the partial tuples around a substitution, the next chain
+// of the diagonal) read too.  In line order those walks are far apart in time and each line
+// is fetched again from HBM; sorted by position they run close together and share L2.
+template <int MG, typename View>
+__global__ __launch_bounds__(kBlock) void walk_key_kernel(View v, GenomeTable gt, MatchParams mp, int L,
+                                                          const WalkItem* __restrict__ queue,
+                                                          const unsigned int* __restrict__ qcount, int shift,
+                                                          uint64_t* __restrict__ rec) {
+    const uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (q >= *qcount) return;
+    Mhe<MG> A;
+    probe_of<MG, View>(v, nullptr, queue[q].j, gt, mp, L, A);
+    const int64_t x = start_at(A, first_start(A));
+    rec[q] = ((uint64_t)(x > 0 ? x : 0) >> shift << 32) | q;
+}
+
 // Queued walks, one lane per item, up to kWalkBudget 64-column words each (most chain ends
 // lie within a few words); the rest go on to chain_walk_kernel's lane groups.
 template <int MG, typename View>
@@ -479,7 +502,8 @@ __global__ __launch_bounds__(kBlock) void chain_walk_short_kernel(View v, const 
                                                                   const unsigned int* __restrict__ qcount,
                                                                   uint8_t* __restrict__ link, int64_t* __restrict__ rcol,
                                                                   int64_t* __restrict__ lcol, WalkItem* __restrict__ lq,
-                                                                  unsigned int* __restrict__ lqcount) {
+                                                                  unsigned int* __restrict__ lqcount,
+                                                                  const uint64_t* __restrict__ order) {
     const int L = ss.L;
     const LineSpec ls = line_spec(ss, gt);
     const unsigned nq = *qcount;
@@ -490,7 +514,7 @@ __global__ __launch_bounds__(kBlock) void chain_walk_short_kernel(View v, const 
         uint32_t want = 0;
         WalkItem nx[1] = {WalkItem{}};
         if (q < nq) {
-            const WalkItem it = queue[q];
+            const WalkItem it = queue[order ? (uint32_t)order[q] : q];
             Mhe<MG> A;
             probe_of<MG, View>(v, probe_info, it.j, gt, mp, L, A);
             const int64_t xa = start_at(A, first_start(A));
@@ -512,6 +536,111 @@ __global__ __launch_bounds__(kBlock) void chain_walk_short_kernel(View v, const 
             }
         }
         block_push<1>(want, nx, lq, lqcount);
+    }
+}
+
+// chain_walk_short_kernel with lane refill.  Walk lengths are heavy-tailed (about one item
+// in five spends the whole budget), so a wave of 64 one-shot lanes nearly always runs
+// kWalkBudget steps for items that mostly end after one or two words.  Here each block owns
+// a contiguous range of the queue, a lane whose walk has ended takes the next item of that
+// range (LDS counter, once kRefillMin lanes of the wave are idle) and every step advances
+// each busy lane by one word.  Results per item are the same as chain_walk_short_kernel's
+// (same walk, same budget); the handed-on items reach lq in another order, which no later
+// step depends on.
+#ifndef MUMS_WALK_REFILL_MIN
+#define MUMS_WALK_REFILL_MIN 16
+#endif
+template <int MG, typename View>
+__global__ __launch_bounds__(kBlock) void chain_walk_refill_kernel(View v, GenomeTable gt, MatchParams mp, SeedSpec ss,
+                                                                   const uint32_t* __restrict__ packed,
+                                                                   const WalkItem* __restrict__ queue,
+                                                                   const unsigned int* __restrict__ qcount,
+                                                                   uint8_t* __restrict__ link, int64_t* __restrict__ rcol,
+                                                                   int64_t* __restrict__ lcol, WalkItem* __restrict__ lq,
+                                                                   unsigned int* __restrict__ lqcount) {
+    const int L = ss.L;
+    const LineSpec ls = line_spec(ss, gt);
+    const unsigned nq = *qcount;
+    const unsigned per = (nq + gridDim.x - 1) / gridDim.x;
+    const unsigned lo = min(nq, blockIdx.x * per), hi = min(nq, lo + per);
+    __shared__ unsigned s_next;
+    if (threadIdx.x == 0) s_next = lo;
+    __syncthreads();
+    if (lo >= hi) return;
+    const int lane = threadIdx.x & 63;
+    const uint64_t below = (1ull << lane) - 1;
+    bool have = false, more = true;   // more: wave-uniform
+    WalkItem it{};
+    Mhe<MG> A;
+    int64_t xa = 0, clo = 0, chi = 0, last = 0, u0 = 1;
+    int budget = 0, dir = 1;
+    for (;;) {
+        const uint64_t idle = __ballot(!have);
+        const unsigned n = (unsigned)__popcll(idle);
+        if (more && n >= (unsigned)MUMS_WALK_REFILL_MIN) {
+            const int lead = __builtin_ctzll(idle);
+            unsigned base = 0;
+            if (lane == lead) base = atomicAdd(&s_next, n);
+            base = __shfl(base, lead);
+            if (base + n >= hi) more = false;
+            if (!have) {
+                const unsigned q = base + (unsigned)__popcll(idle & below);
+                if (q < hi) {
+                    it = queue[q];
+                    probe_of<MG, View>(v, nullptr, it.j, gt, mp, L, A);
+                    xa = start_at(A, first_start(A));
+                    frame_bounds<MG>(A, gt, &clo, &chi);
+                    dir = it.kind == 2 ? -1 : +1;
+                    last = 0;
+                    u0 = 1;
+                    budget = kWalkBudget;
+                    have = true;
+                }
+            }
+        }
+        if (!__any(have)) {
+            if (!more) break;
+            continue;
+        }
+        bool hand_on = false;
+        if (have) {   // one step of walk_lane
+            const int64_t col = it.cur + dir * last;
+            int state = -1;
+            int64_t c = col;
+            if (dir > 0 ? col >= it.stop : col <= it.stop) state = 1;
+            else if (budget-- <= 0) state = 2;
+            else {
+                const uint64_t H = hit_word_dir<MG>(dir, it.cur + dir * u0, A, gt, clo, chi, packed, ss, ls);
+                const bool broke = scan_word(H, u0, &last, L);
+                u0 += 64;
+                if (broke) {
+                    c = it.cur + dir * last;
+                    state = (dir > 0 ? c >= it.stop : c <= it.stop) ? 1 : 0;
+                }
+            }
+            if (state >= 0) {
+                have = false;
+                if (state == 2) {
+                    hand_on = true;
+                    it.cur = c;
+                } else if (it.kind == 0) {
+                    link[it.j] = state == 1 ? 1 : 0;
+                    if (state == 0) rcol[it.j] = xa + c;
+                } else if (it.kind == 1) {
+                    rcol[it.j] = xa + c;
+                } else {
+                    lcol[it.j] = xa + c;
+                }
+            }
+        }
+        const uint64_t hm = __ballot(hand_on);
+        if (hm) {   // wave-aggregated append to the long-walk queue
+            const int lead = __builtin_ctzll(hm);
+            unsigned base = 0;
+            if (lane == lead) base = atomicAdd(lqcount, (unsigned)__popcll(hm));
+            base = __shfl(base, lead);
+            if (hand_on) lq[base + (unsigned)__popcll(hm & below)] = it;
+        }
     }
 }
 
@@ -1011,8 +1140,8 @@ int x_bits(const GenomeTable& gt) {
 template <int MG, typename LV>
 hipError_t chains_core(LV vl, const ChainWs& w, const uint32_t* ord, uint64_t P, const GenomeTable& gt,
                        const MatchParams& mp, const SeedSpec& ss, const uint32_t* packed, void* d_scan_tmp,
-                       uint32_t* chain_of, int64_t* pool, uint32_t* d_nchains, hipStream_t st, void* ctr,
-                       hipEvent_t* ev_walk, uint32_t* fk, uint32_t kbase, uint32_t* jl) {
+                       void* d_radix_tmp, uint32_t* chain_of, int64_t* pool, uint32_t* d_nchains, hipStream_t st,
+                       void* ctr, hipEvent_t* ev_walk, uint32_t* fk, uint32_t kbase, uint32_t* jl) {
     hipError_t e;
     const unsigned grid = grid_of(P);
     const unsigned walk_grid = 2048, short_grid = 8192;
@@ -1020,6 +1149,15 @@ hipError_t chains_core(LV vl, const ChainWs& w, const uint32_t* ord, uint64_t P,
     unsigned int* qshort = qcount;      // chain_link / chain_left -> chain_walk_short_kernel
     unsigned int* qlong = qcount + 1;   // chain_walk_short_kernel -> chain_walk_kernel
     const bool cdbg = getenv("MUMS_DEV_CHAIN_DEBUG") != nullptr;
+    // refilled short-walk lanes (read per call: tests and A/B runs toggle it)
+    const bool refill = getenv("MUMS_DEV_WALK_REFILL") && getenv("MUMS_DEV_WALK_REFILL")[0] == '1';
+    // short walks in genome-position order (walk_key_kernel), MUMS_DEV_WALK_SORT=1: measured
+    // slower at C3 than the queue's line order, kept for A/B runs
+    const char* wsort_env = getenv("MUMS_DEV_WALK_SORT");
+    const bool wsort = !refill && wsort_env && wsort_env[0] == '1' && P < (1ull << 32);
+    const int wshift = kWalkSortShift;
+    const int wbits = std::max(1, x_bits(gt) - wshift);
+    uint32_t* d_err = ctr ? &((DevCounters*)ctr)->err : w.qcount + 14;
     for (int pass = 0; pass < 2; ++pass) {
         if ((e = hipMemsetAsync(qcount, 0, 12, st)) != hipSuccess) return e;
         const unsigned lgrid = (unsigned)((P + kBlock * kLinkIPT - 1) / (kBlock * kLinkIPT));
@@ -1030,9 +1168,31 @@ hipError_t chains_core(LV vl, const ChainWs& w, const uint32_t* ord, uint64_t P,
             hipLaunchKernelGGL(chain_left_kernel, dim3(lgrid), dim3(kBlock), 0, st, P, (const uint8_t*)w.link, w.queue,
                                qshort);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-        hipLaunchKernelGGL((chain_walk_short_kernel<MG, LV>), dim3(short_grid), dim3(kBlock), 0, st, vl, nullptr,
-                           gt, mp, ss, packed, (const WalkItem*)w.queue, (const unsigned int*)qshort, w.link, w.rcol,
-                           w.lcol, w.queue_long, qlong);
+        const uint64_t* order = nullptr;
+        if (wsort) {   // the queue length sizes the sort: read back (one small sync per pass)
+            unsigned nq = 0;
+            if ((e = hipMemcpyAsync(&nq, qshort, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+            if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+            if (nq > 1) {
+                hipLaunchKernelGGL((walk_key_kernel<MG, LV>), dim3(grid_of(nq)), dim3(kBlock), 0, st, vl, gt, mp, ss.L,
+                                   (const WalkItem*)w.queue, (const unsigned int*)qshort, wshift, w.kA);
+                if ((e = hipGetLastError()) != hipSuccess) return e;
+                if ((e = seg_bucket_starts(nullptr, 0, 0, nq, w.bst + 8, st)) != hipSuccess) return e;
+                int ob = 0;
+                if ((e = seg_onesweep_sort(w.kA, w.kB, nq, wbits, 0, w.bst + 8, d_radix_tmp, d_err, &ob, st)) !=
+                    hipSuccess)
+                    return e;
+                order = ob ? w.kB : w.kA;
+            }
+        }
+        if (refill)
+            hipLaunchKernelGGL((chain_walk_refill_kernel<MG, LV>), dim3(short_grid), dim3(kBlock), 0, st, vl, gt, mp,
+                               ss, packed, (const WalkItem*)w.queue, (const unsigned int*)qshort, w.link, w.rcol,
+                               w.lcol, w.queue_long, qlong);
+        else
+            hipLaunchKernelGGL((chain_walk_short_kernel<MG, LV>), dim3(short_grid), dim3(kBlock), 0, st, vl, nullptr,
+                               gt, mp, ss, packed, (const WalkItem*)w.queue, (const unsigned int*)qshort, w.link,
+                               w.rcol, w.lcol, w.queue_long, qlong, order);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (cdbg && (e = hipMemsetAsync(qcount + 4, 0, 32, st)) != hipSuccess) return e;
         if (ev_walk) (void)hipEventRecord(ev_walk[2 * pass], st);
@@ -1185,7 +1345,7 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
                                    v.stride32, (int32_t*)w.rows_line);
                 if ((r = hipGetLastError()) != hipSuccess) return r;
                 LineRows vl{(const int32_t*)w.rows_line, v.stride32, v.L32};
-                return chains_core<MG>(vl, w, o, P, gt, mp, ss, packed, d_scan_tmp, chain_of, pool, d_nchains, st, ctr,
+                return chains_core<MG>(vl, w, o, P, gt, mp, ss, packed, d_scan_tmp, d_radix_tmp, chain_of, pool, d_nchains, st, ctr,
                                        ev_walk, fk, kbase, jl);
             }
             if (narrow) {
@@ -1193,14 +1353,14 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
                                    gt.G, ss.L, (int32_t*)w.rows_line, flags + 1);
                 if ((r = hipGetLastError()) != hipSuccess) return r;
                 LineRows vl{(const int32_t*)w.rows_line, line_row_stride(gt.G), ss.L};
-                return chains_core<MG>(vl, w, o, P, gt, mp, ss, packed, d_scan_tmp, chain_of, pool, d_nchains, st, ctr,
+                return chains_core<MG>(vl, w, o, P, gt, mp, ss, packed, d_scan_tmp, d_radix_tmp, chain_of, pool, d_nchains, st, ctr,
                                        ev_walk, fk, kbase, jl);
             }
         }
         if ((r = launch_gather_rows(v.rows, o, P, gt.G, w.rows_line, st)) != hipSuccess) return r;
         MatProbes vl{};
         vl.rows = w.rows_line;
-        return chains_core<MG>(vl, w, o, P, gt, mp, ss, packed, d_scan_tmp, chain_of, pool, d_nchains, st, ctr, ev_walk,
+        return chains_core<MG>(vl, w, o, P, gt, mp, ss, packed, d_scan_tmp, d_radix_tmp, chain_of, pool, d_nchains, st, ctr, ev_walk,
                                fk, kbase, jl);
     };
     unsigned hf[2] = {0, 0};

@@ -24,6 +24,8 @@
 //   6. compat_merge_kernel    MergeTable: re-add each bucket's entries in vector order
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "match_device.h"
 #include "mums_internal.h"
 #include "restart_plan.h"
@@ -151,10 +153,12 @@ __global__ void compat_cand_kernel(const uint64_t* __restrict__ key2, uint64_t N
 // end) in MER_BUFFER_SIZE buffers from S; the group is collected genome run by genome run
 // in the head order of restart_plan.h, and the check precedes every collection step.
 // out[c] = 1 when it fires; cend[c] = stream index of the chunk's end (first record of
-// chunk i + 1).
+// chunk i + 1); cons (optional, C x (G + 1)): the SML positions the chunk's merge consumed
+// in every genome when the check fired, then the chunk i (LogProgress of a cut chunk).
 __global__ void compat_fire_kernel(restart::PlanData d, const uint64_t* __restrict__ key2, uint64_t N, int kbits,
                                    const uint64_t* __restrict__ cand, uint64_t C, const uint64_t* __restrict__ cs,
-                                   uint32_t nch, uint32_t* __restrict__ out, uint64_t* __restrict__ cend) {
+                                   uint32_t nch, uint32_t* __restrict__ out, uint64_t* __restrict__ cend,
+                                   uint64_t* __restrict__ cons) {
     const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
     const int G = d.G;
@@ -181,6 +185,8 @@ __global__ void compat_fire_kernel(restart::PlanData d, const uint64_t* __restri
     const int n = restart::head_order(d, U, a, S, ord, &steps);
     uint64_t cum = 0;
     bool fired = false;
+    uint64_t cz[restart::kMaxGenomes];   // consumed: every key below K, then the collected runs
+    for (int g = 0; g < G; ++g) cz[g] = a[g];
     for (int k = 0; k < n && !fired; ++k) {
         const int g = ord[k];
         uint64_t x = a[g];
@@ -190,6 +196,7 @@ __global__ void compat_fire_kernel(restart::PlanData d, const uint64_t* __restri
             const uint64_t y = b[g] < nb ? b[g] : nb;
             cum += y - x;
             x = y;
+            cz[g] = x;
         }
         // a run ending on a buffer boundary with more of the chunk to read: the refilled
         // head still carries K for one more iteration
@@ -197,6 +204,10 @@ __global__ void compat_fire_kernel(restart::PlanData d, const uint64_t* __restri
             fired = true;
     }
     out[c] = fired ? 1u : 0u;
+    if (cons) {
+        for (int g = 0; g < G; ++g) cons[c * (uint64_t)(G + 1) + g] = cz[g];
+        cons[c * (uint64_t)(G + 1) + G] = i;
+    }
     const uint64_t nxt = (uint64_t)(i + 1) << kbits;
     uint64_t lo = j, hi = N;   // first stream index with key2 >= nxt
     while (lo < hi) {
@@ -233,38 +244,160 @@ __global__ void compat_drop_kernel(const uint64_t* __restrict__ k_in, const uint
 // MergeTable (ParallelMemHash.cpp:105-121): every entry of the thread table is re-added
 // with AddHashEntry (MemHash.cpp:209-251) into the global table: lower_bound, a
 // collision when equivalent (MheCompare both ways false), else inserted at the
-// lower_bound; entries are already Extended() (:223), so nothing is re-extended.  One
-// thread per bucket, in place: the merged prefix never overtakes the entry being read.
+// lower_bound; entries are already Extended() (:223), so nothing is re-extended.
+//
+// The table was built by the same lower_bound inserts, so nearly every re-add lands at the
+// end of the merged prefix: while that holds the merged bucket IS the table's prefix.  Pass
+// 1 (compat_merge_spec_kernel, one lane per entry of every bucket) checks exactly that:
+// entry j's lower_bound over the table's own prefix [0, j) (std::lower_bound's probes).
+// The first entry of a bucket that would not append -- an equivalent copy (A.10) or an
+// insert inside the prefix -- starts pass 2 (compat_merge_fix_kernel) on that bucket only:
+// the exact sequential merge from there, one workgroup, a batch of entries per round
+// (each lower_bound over the merged prefix followed by the batch's earlier entries; the
+// batch is applied up to its first entry that does not append, which is then dropped or
+// inserted as the serial merge would).  Buckets of one diagonal hold most of a related
+// input's matches (4.5 M at BASELINE config 3), so an in-place serial insertion merge of
+// them is quadratic.
 template <int MG>
-__global__ __launch_bounds__(256) void compat_merge_kernel(uint32_t* __restrict__ tsize,
-                                                           const uint32_t* __restrict__ bstart,
-                                                           uint32_t* __restrict__ tbl,
-                                                           const int64_t* __restrict__ pool, int G, uint32_t Tb,
-                                                           unsigned long long* __restrict__ collisions) {
-    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= Tb) return;
-    const uint32_t n = tsize[b];
-    if (n < 2) return;
-    uint32_t* v = tbl + bstart[b];
-    uint32_t out = 0, dropped = 0;
-    Mhe<MG> e, x;
-    for (uint32_t j = 0; j < n; ++j) {
-        const uint32_t id = v[j];
-        load_entry(pool, id, G, e);
-        const uint32_t it = lower_bound_tbl<MG>(v, out, pool, G, e);
-        if (it != out) {
-            load_entry(pool, v[it], G, x);
-            if (!mhe_less(x, e) && !mhe_less(e, x)) { ++dropped; continue; }
-        }
-        for (uint32_t q = out; q > it; --q) v[q] = v[q - 1];
-        v[it] = id;
-        ++out;
+__global__ __launch_bounds__(256) void compat_merge_spec_kernel(const uint32_t* __restrict__ tsize,
+                                                                const uint32_t* __restrict__ bstart,
+                                                                const uint32_t* __restrict__ tbl,
+                                                                const int64_t* __restrict__ pool, int G, uint32_t Tb,
+                                                                const uint32_t* __restrict__ tscan, uint64_t total,
+                                                                uint32_t* __restrict__ first_fail) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= total) return;
+    uint32_t lo = 0, hi = Tb;   // the bucket: the last b with tscan[b] <= g
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (tscan[mid] <= g) lo = mid;
+        else hi = mid;
     }
-    tsize[b] = out;
-    if (dropped) atomicAdd(collisions, (unsigned long long)dropped);
+    const uint32_t b = lo, j = (uint32_t)(g - tscan[b]);
+    if (j == 0 || j >= tsize[b]) return;
+    const uint32_t* v = tbl + bstart[b];
+    Mhe<MG> e;
+    load_entry(pool, v[j], G, e);
+    if (lower_bound_tbl<MG>(v, j, pool, G, e) != j) atomicMin(&first_fail[b], j);
+}
+
+// lower_bound (std::lower_bound's probes) of e over the merged prefix v[0, out) followed by
+// the batch entries v[j, j + t)
+template <int MG>
+__device__ __forceinline__ uint32_t lower_bound_merge(const uint32_t* v, uint32_t out, uint32_t j, uint32_t t,
+                                                     const int64_t* __restrict__ pool, int G, const Mhe<MG>& e) {
+    uint32_t first = 0, len = out + t;
+    Mhe<MG> x;
+    while (len > 0) {
+        const uint32_t half = len >> 1, mid = first + half;
+        load_entry(pool, mid < out ? v[mid] : v[j + (mid - out)], G, x);
+        if (mhe_less(x, e)) {
+            first = mid + 1;
+            len = len - half - 1;
+        } else {
+            len = half;
+        }
+    }
+    return first;
+}
+
+template <int MG, int kBlk>
+__global__ __launch_bounds__(kBlk) void compat_merge_fix_kernel(uint32_t* __restrict__ tsize,
+                                                               const uint32_t* __restrict__ bstart,
+                                                               uint32_t* __restrict__ tbl,
+                                                               const int64_t* __restrict__ pool, int G,
+                                                               const uint32_t* __restrict__ first_fail,
+                                                               unsigned long long* __restrict__ collisions) {
+    const uint32_t b = blockIdx.x;
+    const uint32_t j0 = first_fail[b];
+    if (j0 == 0xFFFFFFFFu) return;
+    __shared__ uint32_t s_bad, s_res, s_id;
+    const uint32_t n = tsize[b];
+    uint32_t* v = tbl + bstart[b];
+    uint32_t out = j0, j = j0, dropped = 0;   // merged prefix v[0, out); unread entries v[j, n)
+    while (j < n) {   // workgroup-uniform
+        const uint32_t t = threadIdx.x;
+        const uint32_t B = min((uint32_t)kBlk, n - j);
+        if (t == 0) s_bad = B;
+        __syncthreads();
+        uint32_t id = 0, res = 0;
+        if (t < B) {
+            id = v[j + t];
+            Mhe<MG> e;
+            load_entry(pool, id, G, e);
+            res = lower_bound_merge<MG>(v, out, j, t, pool, G, e);
+            if (res != out + t) atomicMin(&s_bad, t);
+        }
+        __syncthreads();
+        const uint32_t bad = s_bad;
+        if (t == bad) {
+            s_res = res;
+            s_id = id;
+        }
+        if (out != j && t < bad) v[out + t] = id;   // (every lane read its entry before the barrier)
+        __syncthreads();
+        out += bad;
+        j += bad;
+        if (bad < B) {   // entry j: its lower_bound res was taken over exactly the merged prefix
+            const uint32_t it = s_res, eid = s_id;
+            Mhe<MG> e, x;
+            load_entry(pool, eid, G, e);
+            bool coll = false;
+            if (it != out) {
+                load_entry(pool, v[it], G, x);
+                coll = !mhe_less(x, e) && !mhe_less(e, x);
+            }
+            if (coll) {
+                ++dropped;
+            } else {   // insert at it: v[it, out) moves up one slot (v[out] <= v[j], read already)
+                for (uint32_t top = out; top > it;) {
+                    const uint32_t low = top - it > (uint32_t)kBlk ? top - kBlk : it;
+                    const uint32_t idx = low + t;
+                    uint32_t tmp = 0;
+                    if (idx < top) tmp = v[idx];
+                    __syncthreads();
+                    if (idx < top) v[idx + 1] = tmp;
+                    __syncthreads();
+                    top = low;
+                }
+                if (t == 0) v[it] = eid;
+                ++out;
+            }
+            ++j;
+            __syncthreads();
+        }
+    }
+    if (threadIdx.x == 0) {
+        tsize[b] = out;
+        if (dropped) atomicAdd(collisions, (unsigned long long)dropped);
+    }
+}
+
+// SetMatchLog in compat mode: the chunk of every probe is nondecreasing in AddHashEntry call
+// order (the chunk-major stream), so the chunks are ranges of probes: pfirst[c] = first probe
+// of chunk c (nch + 1 entries, pfirst[nch] = P).  probe_info low word = the group's first
+// stream record, whose key2 carries the chunk above kbits.
+__global__ void compat_probe_chunk_kernel(const uint64_t* __restrict__ probe_info, uint64_t P,
+                                          const uint64_t* __restrict__ key2, int kbits, uint32_t nch,
+                                          uint32_t* __restrict__ pfirst) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= P) return;
+    const uint64_t c = key2[probe_info[k] & 0xFFFFFFFFull] >> kbits;
+    const int64_t cp = k ? (int64_t)(key2[probe_info[k - 1] & 0xFFFFFFFFull] >> kbits) : -1;
+    for (int64_t x = cp + 1; x <= (int64_t)c && x <= (int64_t)nch; ++x) pfirst[x] = (uint32_t)k;
+    if (k + 1 == P)
+        for (uint64_t x = c + 1; x <= nch; ++x) pfirst[x] = (uint32_t)P;
 }
 
 }  // namespace
+
+hipError_t launch_compat_probe_chunks(const uint64_t* probe_info, uint64_t P, const uint64_t* key2, int kbits,
+                                      uint32_t nch, uint32_t* pfirst, hipStream_t st) {
+    if (P == 0) return hipMemsetAsync(pfirst, 0, ((uint64_t)nch + 1) * 4, st);
+    hipLaunchKernelGGL(compat_probe_chunk_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st, probe_info, P,
+                       key2, kbits, nch, pfirst);
+    return hipGetLastError();
+}
 
 hipError_t launch_genome_keys(uint64_t* ckey, uint64_t N, const GenomeTable& gt, int kbits, hipStream_t st) {
     if (N == 0) return hipSuccess;
@@ -308,10 +441,10 @@ hipError_t launch_compat_cands(const uint64_t* key2, uint64_t N, uint64_t* list,
 
 hipError_t launch_compat_fire(const restart::PlanData& d, const uint64_t* key2, uint64_t N, int kbits,
                               const uint64_t* cand, uint64_t C, const uint64_t* cs, uint32_t nch, uint32_t* out,
-                              uint64_t* cend, hipStream_t st) {
+                              uint64_t* cend, uint64_t* cons, hipStream_t st) {
     if (C == 0) return hipSuccess;
     hipLaunchKernelGGL(compat_fire_kernel, dim3((unsigned)((C + 63) / 64)), dim3(64), 0, st, d, key2, N, kbits, cand, C,
-                       cs, nch, out, cend);
+                       cs, nch, out, cend, cons);
     return hipGetLastError();
 }
 
@@ -324,14 +457,29 @@ hipError_t launch_compat_drop(const uint64_t* k_in, const uint32_t* v_in, uint64
     return hipGetLastError();
 }
 
+// tscan: exclusive scan of tsize (Tb entries), total = its sum; first_fail: Tb words (scratch)
 hipError_t launch_compat_merge(uint32_t* tsize, const uint32_t* bstart, uint32_t* tbl, const int64_t* pool, int G,
-                               uint32_t Tb, unsigned long long* collisions, hipStream_t st) {
-    const dim3 grid((Tb + 255) / 256), blk(256);
-    if (G <= 4) hipLaunchKernelGGL(compat_merge_kernel<4>, grid, blk, 0, st, tsize, bstart, tbl, pool, G, Tb, collisions);
-    else if (G <= 8) hipLaunchKernelGGL(compat_merge_kernel<8>, grid, blk, 0, st, tsize, bstart, tbl, pool, G, Tb, collisions);
-    else if (G <= 16) hipLaunchKernelGGL(compat_merge_kernel<16>, grid, blk, 0, st, tsize, bstart, tbl, pool, G, Tb, collisions);
-    else if (G <= 32) hipLaunchKernelGGL(compat_merge_kernel<32>, grid, blk, 0, st, tsize, bstart, tbl, pool, G, Tb, collisions);
-    else hipLaunchKernelGGL(compat_merge_kernel<64>, grid, blk, 0, st, tsize, bstart, tbl, pool, G, Tb, collisions);
+                               uint32_t Tb, unsigned long long* collisions, const uint32_t* tscan, uint64_t total,
+                               uint32_t* first_fail, hipStream_t st) {
+    // test hook (read per call): every bucket through the exact merge from its first entry
+    const bool all_exact = getenv("MUMS_DEV_COMPAT_MERGE_EXACT") != nullptr;
+    hipError_t e = hipMemsetAsync(first_fail, all_exact ? 0x00 : 0xFF, (size_t)Tb * 4, st);
+    if (e != hipSuccess || total == 0) return e;
+    const dim3 sgrid((unsigned)((total + 255) / 256)), sblk(256);
+#define MUMS_COMPAT_MERGE(MGV, BLK)                                                                                   \
+    do {                                                                                                              \
+        if (!all_exact)                                                                                               \
+            hipLaunchKernelGGL(compat_merge_spec_kernel<MGV>, sgrid, sblk, 0, st, tsize, bstart, tbl, pool, G, Tb,    \
+                               tscan, total, first_fail);                                                             \
+        hipLaunchKernelGGL((compat_merge_fix_kernel<MGV, BLK>), dim3(Tb), dim3(BLK), 0, st, tsize, bstart, tbl, pool, \
+                           G, first_fail, collisions);                                                                \
+    } while (0)
+    if (G <= 4) MUMS_COMPAT_MERGE(4, 1024);
+    else if (G <= 8) MUMS_COMPAT_MERGE(8, 1024);
+    else if (G <= 16) MUMS_COMPAT_MERGE(16, 512);
+    else if (G <= 32) MUMS_COMPAT_MERGE(32, 256);
+    else MUMS_COMPAT_MERGE(64, 256);
+#undef MUMS_COMPAT_MERGE
     return hipGetLastError();
 }
 

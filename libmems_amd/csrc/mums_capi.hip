@@ -93,6 +93,7 @@ struct mums_ctx {
 
     DevBuf packed, recA, recB, hist, tiles, ckey, kA, kB, vA, vB, tmp, partials, counters;
     DevBuf bstart, bend, tsize, obase, pool, tbl, out_len, out_s, pbuf, keybuf, mstart;
+    DevBuf cmerge;   // compat MergeTable: first entry of every bucket that does not append
     DevBuf chain_tmp, chain_of, radix_tmp, spill, summ, dbgbuf, mprobe, rowtmp;
     DevBuf fk, fkloc;        // each chain's first probe in key order (merged / per slice)
     DevBuf side, bst8;       // keys wider than 32 + 8 bits: side bytes, 8-bit bucket starts (msdsplit.hip)
@@ -158,6 +159,10 @@ struct mums_ctx {
     uint64_t restarts = 0;
     std::vector<uint64_t> offset_log;     // start points after every restart (R x G)
     std::vector<uint64_t> consumed_log;   // consumed SML positions at every restart (R x G, restart plan)
+    std::vector<uint32_t> compat_pfirst;  // compat + match log: first probe of every chunk (nch + 1)
+    std::vector<uint32_t> log_ids;        // compat + match log: the logged entries (pool ids) in log order
+    std::vector<uint64_t> compat_cons;    // compat: consumed SML positions of every chunk cut by MER_REPEAT_LIMIT
+                                          // (nch x G, ~0 = not cut), compat_truncate
     bool progress_on = false;             // MatchFinder::LogProgress: restate the progress text
     std::string progress;                 // its text for the last seed stage
     hipEvent_t ev[EV_COUNT] = {};
@@ -342,7 +347,7 @@ int find_replay(mums_ctx* ctx, MatProbes v, const MatchParams& mp, hipStream_t s
     }
     uint64_t* mlog = nullptr;
     ctx->log_n = 0;
-    if (ctx->match_log && !ctx->pcompat) {
+    if (ctx->match_log) {
         HIPCHK(ctx->logA.ensure((P + 1) * 8));
         HIPCHK(ctx->logB.ensure((P + 1) * 8));
         mlog = ctx->logB.as<uint64_t>();   // unsorted events; sorted into logA
@@ -382,6 +387,57 @@ int find_replay(mums_ctx* ctx, MatProbes v, const MatchParams& mp, hipStream_t s
                     (unsigned long)d[3], d[4] / 100.0, d[5] / 100.0, d[6] / 100.0, d[7] / 100.0);
         }
     }
+    return MUMS_OK;
+}
+
+// SetMatchLog under ParallelMemHash (the patched 2-argument AddHashEntry logs every insert,
+// MemHash.cpp:238-241), one OpenMP thread: for every chunk, its SearchRange's
+// inserts into the thread table in call order (the replay's log events of the chunk's
+// probes), then MergeTable's (ParallelMemHash.cpp:105-121): the chunk's new entries that
+// survive the re-add, bucket by bucket in vector order.  An entry can only enter the global
+// table at its own chunk's merge, and the final table holds exactly the surviving entries in
+// that order, so the merge lines of chunk c are the final table's entries created in chunk c.
+int compat_log_order(mums_ctx* ctx, uint32_t Tb, hipStream_t st) {
+    const uint64_t n = ctx->log_n;
+    const uint32_t nch = ctx->compat_pfirst.empty() ? 0 : (uint32_t)ctx->compat_pfirst.size() - 1;
+    std::vector<uint64_t> ev(n);
+    if (n) HIPCHK(hipMemcpyAsync(ev.data(), ctx->logA.p, n * 8, hipMemcpyDeviceToHost, st));
+    std::vector<uint32_t> ts(Tb), tb(Tb);
+    HIPCHK(hipMemcpyAsync(ts.data(), ctx->tsize.p, (size_t)Tb * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(tb.data(), ctx->emit_base, (size_t)Tb * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    uint64_t end = 0;
+    for (uint32_t b = 0; b < Tb; ++b)
+        if (ts[b]) end = std::max<uint64_t>(end, (uint64_t)tb[b] + ts[b]);
+    std::vector<uint32_t> tbl(end);
+    if (end) HIPCHK(hipMemcpy(tbl.data(), ctx->emit_tbl, end * 4, hipMemcpyDeviceToHost));
+    auto chunk_of_probe = [&](uint64_t k) -> uint32_t {
+        if (!nch) return 0;
+        const auto it = std::upper_bound(ctx->compat_pfirst.begin(), ctx->compat_pfirst.end() - 1, (uint32_t)k);
+        return (uint32_t)(it - ctx->compat_pfirst.begin()) - 1;
+    };
+    uint32_t maxid = 0;
+    for (uint64_t i = 0; i < n; ++i) maxid = std::max(maxid, (uint32_t)(ev[i] & 0xFFFFFFFFull));
+    std::vector<uint32_t> made(maxid + 1u, 0);   // chunk that created each pool entry
+    std::vector<std::vector<uint32_t>> lines(std::max<uint32_t>(nch, 1));
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint32_t cid = (uint32_t)(ev[i] & 0xFFFFFFFFull), c = chunk_of_probe(ev[i] >> 32);
+        made[cid] = c;
+        lines[c].push_back(cid);
+    }
+    std::vector<std::vector<uint32_t>> merged(lines.size());
+    for (uint32_t b = 0; b < Tb; ++b)
+        for (uint32_t j = 0; j < ts[b]; ++j) {
+            const uint32_t cid = tbl[(uint64_t)tb[b] + j];
+            if (cid > maxid) return fail(ctx, MUMS_E_HIP, "compat match log: an entry without an insert (internal error)");
+            merged[made[cid]].push_back(cid);
+        }
+    ctx->log_ids.clear();
+    for (size_t c = 0; c < lines.size(); ++c) {
+        ctx->log_ids.insert(ctx->log_ids.end(), lines[c].begin(), lines[c].end());
+        ctx->log_ids.insert(ctx->log_ids.end(), merged[c].begin(), merged[c].end());
+    }
+    ctx->log_n = ctx->log_ids.size();
     return MUMS_OK;
 }
 
@@ -469,7 +525,7 @@ int replay_merged(mums_ctx* ctx, MatProbes v, const MatchParams& mp, hipStream_t
     HIPCHK(ctx->radix_tmp.ensure(radix_tmp_bytes(nch + 1)));
     uint64_t* mlog = nullptr;
     ctx->log_n = 0;
-    if (ctx->match_log && !ctx->pcompat) {
+    if (ctx->match_log) {
         HIPCHK(ctx->logA.ensure((P + 1) * 8));
         HIPCHK(ctx->logB.ensure((P + 1) * 8));
         mlog = ctx->logB.as<uint64_t>();
@@ -669,9 +725,17 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
         }
         rc = find_rows_dispatch(ctx, v, packed, mp, st, chunked);
         if (rc) return rc;
-        if (ctx->pcompat)   // ParallelMemHash::MergeTable (ParallelMemHash.cpp:105-121)
+        if (ctx->pcompat) {   // ParallelMemHash::MergeTable (ParallelMemHash.cpp:105-121)
+            HIPCHK(hipMemcpyAsync(ctx->obase.p, ctx->tsize.p, (size_t)Tb * 4, hipMemcpyDeviceToDevice, st));
+            HIPCHK(exclusive_scan_u32(ctx->obase.as<uint32_t>(), Tb, ctx->tmp.p, &dc->nmatches, st));
+            uint32_t tot = 0;
+            HIPCHK(hipMemcpyAsync(&tot, &dc->nmatches, 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            HIPCHK(ctx->cmerge.ensure((size_t)Tb * 4 + 64));
             HIPCHK(launch_compat_merge(ctx->tsize.as<uint32_t>(), ctx->emit_base, ctx->emit_tbl,
-                                       ctx->pool.as<int64_t>(), G, Tb, &dc->collisions, st));
+                                       ctx->pool.as<int64_t>(), G, Tb, &dc->collisions, ctx->obase.as<uint32_t>(), tot,
+                                       ctx->cmerge.as<uint32_t>(), st));
+        }
     }
     HIPCHK(hipEventRecord(ctx->ev[EV_REPLAY], st));
     HIPCHK(hipMemcpyAsync(ctx->obase.p, ctx->tsize.p, (size_t)Tb * 4, hipMemcpyDeviceToDevice, st));
@@ -686,6 +750,11 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
                        ctx->pool.as<int64_t>(), G, Tb, ctx->M, ctx->out_len.as<uint64_t>(), ctx->out_s.as<int64_t>(),
                        st));
     HIPCHK(hipEventRecord(ctx->ev[EV_OUTPUT], st));
+    ctx->log_ids.clear();
+    if (ctx->match_log && ctx->pcompat) {
+        const int rc = compat_log_order(ctx, Tb, st);
+        if (rc) return rc;
+    }
     ctx->stage_done = MUMS_STAGE_ALL;
     return MUMS_OK;
 }
@@ -1392,6 +1461,8 @@ int prepare_run(mums_ctx* ctx, const std::vector<uint64_t>& lens) {
 // inside its chunk (restart_plan.h head order, buffers from the chunk start); the first
 // firing group of a chunk drops the stream from its first record to the chunk's end.
 // ctx->crall holds the genome-major SML keys.  *n_live = records kept.
+int progress_compat(mums_ctx* ctx, uint32_t nch, const std::vector<uint64_t>& hcs, hipStream_t st);
+
 int compat_truncate(mums_ctx* ctx, uint32_t nch, const uint64_t* cs, int kbits, uint64_t* n_live, hipStream_t st) {
     const GenomeTable& gt = ctx->gt;
     const int G = gt.G;
@@ -1399,7 +1470,7 @@ int compat_truncate(mums_ctx* ctx, uint32_t nch, const uint64_t* cs, int kbits, 
     *n_live = N;
     ctx->restarts = 0;
     const uint64_t cap = N / (restart::kRepeatLimit + 1) + 16;
-    const uint64_t words = cap * 3 + 2 * (uint64_t)(G + 1) + 16 + 3 * ((uint64_t)nch + 1);
+    const uint64_t words = cap * (4 + (uint64_t)G) + 2 * (uint64_t)(G + 1) + 16 + 3 * ((uint64_t)nch + 1);
     HIPCHK(ctx->rsplan.ensure(words * 8 + 256));
     uint64_t* d_list = ctx->rsplan.as<uint64_t>();
     uint64_t* d_cend = d_list + cap;
@@ -1408,6 +1479,8 @@ int compat_truncate(mums_ctx* ctx, uint32_t nch, const uint64_t* cs, int kbits, 
     uint64_t* d_db = d_dm + G + 1;
     unsigned long long* d_cnt = (unsigned long long*)(d_db + G + 1);
     uint64_t* d_rng = d_db + G + 1 + 16;
+    uint64_t* d_cons = d_rng + 3 * ((uint64_t)nch + 1);   // cap x (G + 1)
+    ctx->compat_cons.clear();
     const uint64_t* key2 = (const uint64_t*)ctx->sorted_key;
     HIPCHK(launch_compat_cands(key2, N, d_list, d_cnt, cap, st));
     unsigned long long C = 0;
@@ -1424,17 +1497,21 @@ int compat_truncate(mums_ctx* ctx, uint32_t nch, const uint64_t* cs, int kbits, 
     HIPCHK(hipMemcpyAsync(d_dm, hm.data(), (G + 1) * 8, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(d_db, hb.data(), (G + 1) * 8, hipMemcpyHostToDevice, st));
     const restart::PlanData d{G, d_dm, d_db, ctx->crall.as<uint64_t>()};
-    HIPCHK(launch_compat_fire(d, key2, N, kbits, d_list, C, cs, nch, d_fire, d_cend, st));
+    HIPCHK(launch_compat_fire(d, key2, N, kbits, d_list, C, cs, nch, d_fire, d_cend, d_cons, st));
     std::vector<uint32_t> fire(C);
-    std::vector<uint64_t> cend(C);
+    std::vector<uint64_t> cend(C), cons(C * (uint64_t)(G + 1));
     HIPCHK(hipMemcpyAsync(fire.data(), d_fire, C * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(cend.data(), d_cend, C * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(cons.data(), d_cons, cons.size() * 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     // candidates are in stream order = (chunk, key) order: the first firing one of a chunk cuts it
     std::vector<uint64_t> rlo, rhi, rpre;
     uint64_t dropped = 0;
     for (uint64_t c = 0; c < C; ++c) {
         if (!fire[c] || (!rhi.empty() && cand[c] < rhi.back())) continue;   // chunk already cut
+        if (ctx->compat_cons.empty()) ctx->compat_cons.assign((uint64_t)nch * G, ~0ull);
+        const uint64_t* cz = &cons[c * (uint64_t)(G + 1)];
+        std::copy(cz, cz + G, ctx->compat_cons.begin() + cz[G] * (uint64_t)G);   // the cut chunk's consumption
         rlo.push_back(cand[c]);
         rhi.push_back(cend[c]);
         rpre.push_back(dropped);
@@ -1473,6 +1550,7 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
     ctx->packed_path = false;
     ctx->key64 = true;
     ctx->msd_bits = 0;
+    ctx->progress.clear();
     const uint64_t kmask = (1ull << kbits) - 1;
 
     uint64_t words = 0;
@@ -1522,6 +1600,7 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
     const uint64_t* sk = buf ? ctx->kB.as<uint64_t>() : ctx->kA.as<uint64_t>();
     const uint32_t* sv = buf ? ctx->vB.as<uint32_t>() : ctx->vA.as<uint32_t>();
     uint32_t nch = 1;
+    std::vector<uint64_t> hcs((size_t)G, 0);   // chunk starts (nch x G)
     if (mx >= 0) {
         HIPCHK(launch_compat_breaks(sk, gt, kmask, mx, chunk, cs, bm, cap, d_nch, &dc->err, st));
         uint32_t h[2] = {0, 0};
@@ -1537,7 +1616,7 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
                                                  "(out-of-range SortedMerList::operator[] in the reference)");
         nch = h[0];
         HIPCHK(launch_compat_find(sk, gt, kmask, mx, ctx->L, cs, bm, nch, st));
-        std::vector<uint64_t> hcs((size_t)nch * G);
+        hcs.assign((size_t)nch * G, 0);
         HIPCHK(hipMemcpyAsync(hcs.data(), cs, hcs.size() * 8, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         for (uint32_t k = 1; k < nch; ++k)
@@ -1577,6 +1656,7 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
     uint64_t n_live = N;
     rc = compat_truncate(ctx, nch, cs, kbits, &n_live, st);
     if (rc) return rc;
+    if (ctx->progress_on && (rc = progress_compat(ctx, nch, hcs, st))) return rc;
     HIPCHK(hipEventRecord(ctx->ev[EV_SORT], st));
     SegTile* tiles = ctx->tiles.as<SegTile>();
     HIPCHK(launch_flat_tiles(n_live, tiles, st));
@@ -1586,6 +1666,16 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
     if (rc) return rc;
     rc = finish_seeds(ctx, ps, st);
     if (rc) return rc;
+    ctx->compat_pfirst.clear();
+    if (ctx->match_log) {   // the probes of every chunk (the match log's per-chunk order)
+        DevBuf pf;
+        HIPCHK(pf.ensure(((uint64_t)nch + 1) * 4 + 64));
+        HIPCHK(launch_compat_probe_chunks(ctx->probe_info, ctx->P, (const uint64_t*)ctx->sorted_key, kbits, nch,
+                                          pf.as<uint32_t>(), st));
+        ctx->compat_pfirst.resize((size_t)nch + 1);
+        HIPCHK(hipMemcpyAsync(ctx->compat_pfirst.data(), pf.p, ((uint64_t)nch + 1) * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+    }
     ctx->stage_done = MUMS_STAGE_SEEDS;
     if (stage >= MUMS_STAGE_ALL) {
         rc = find_tail(ctx, mp, ctx->packed.as<uint32_t>(), [&](MatProbes* v) {
@@ -2225,7 +2315,7 @@ int mums_set_match_log(mums_ctx* ctx, int enable) {
 int mums_match_log_copy(mums_ctx* ctx, uint64_t* lengths, int64_t* starts, uint64_t capacity, uint64_t* count) {
     if (check_ctx(ctx) || !count) return MUMS_E_INVALID;
     if (ctx->stage_done < MUMS_STAGE_ALL) return fail(ctx, MUMS_E_INVALID, "no completed FindMatches on this context");
-    if (!ctx->match_log || ctx->pcompat)
+    if (!ctx->match_log)
         return fail(ctx, MUMS_E_INVALID, "the match log was not enabled for this FindMatches (mums_set_match_log)");
     *count = ctx->log_n;
     if (!lengths && !starts) return MUMS_OK;
@@ -2233,15 +2323,21 @@ int mums_match_log_copy(mums_ctx* ctx, uint64_t* lengths, int64_t* starts, uint6
     if (ctx->log_n == 0) return MUMS_OK;
     HIPCHK(hipSetDevice(ctx->device));
     const int G = ctx->gt.G;
-    std::vector<uint64_t> ev(ctx->log_n);
-    HIPCHK(hipMemcpy(ev.data(), ctx->logA.p, ctx->log_n * 8, hipMemcpyDeviceToHost));
-    std::vector<int64_t> e(G + 2);
-    for (uint64_t i = 0; i < ctx->log_n; ++i) {   // pool entry of the inserted chain
-        const uint64_t cid = ev[i] & 0xFFFFFFFFull;
-        HIPCHK(hipMemcpy(e.data(), ctx->pool.as<int64_t>() + cid * (uint64_t)(G + 2), (G + 2) * 8,
-                         hipMemcpyDeviceToHost));
+    std::vector<uint32_t> ids(ctx->log_n);   // pool entries of the inserted chains, in log order
+    if (ctx->pcompat) {
+        ids = ctx->log_ids;
+    } else {
+        std::vector<uint64_t> ev(ctx->log_n);
+        HIPCHK(hipMemcpy(ev.data(), ctx->logA.p, ctx->log_n * 8, hipMemcpyDeviceToHost));
+        for (uint64_t i = 0; i < ctx->log_n; ++i) ids[i] = (uint32_t)(ev[i] & 0xFFFFFFFFull);
+    }
+    const uint64_t nid = (uint64_t)*std::max_element(ids.begin(), ids.end()) + 1;
+    std::vector<int64_t> pool(nid * (uint64_t)(G + 2));   // one copy of the entries referenced
+    HIPCHK(hipMemcpy(pool.data(), ctx->pool.as<int64_t>(), pool.size() * 8, hipMemcpyDeviceToHost));
+    for (uint64_t i = 0; i < ctx->log_n; ++i) {
+        const int64_t* e = &pool[(uint64_t)ids[i] * (G + 2)];
         if (lengths) lengths[i] = (uint64_t)e[0];
-        if (starts) std::copy(e.begin() + 2, e.end(), starts + i * (uint64_t)G);
+        if (starts) std::copy(e + 2, e + 2 + G, starts + i * (uint64_t)G);
     }
     return MUMS_OK;
 }
@@ -3694,6 +3790,16 @@ struct PhaseClock {
 // holding buffer ends of several genomes with unequal sizes, the genomes' runs go in the
 // merge's head order (restart_plan.h head_order over the genome-major SML keys: pw->ck, else
 // built into ck_build, N slots).  s = the whole merged stream.
+struct ProgressEv { uint64_t phase, g, size; };
+
+// the text of buffer-refill events ev (query q[i] = g << 56 | SML index of the buffer's last
+// mer) in nph phases whose start points are Sall (nph x G); base[p] = mers_processed when
+// phase p starts (MatchFinder.cpp:147 / :150-158), or empty: the count carries across phases
+// (ParallelMemHash.cpp:57-61 sets it once for all chunks)
+int progress_text(mums_ctx* ctx, const std::vector<ProgressEv>& ev, const std::vector<uint64_t>& q, uint64_t nph,
+                  const std::vector<uint64_t>& Sall, const std::vector<uint64_t>& base, const CrStream& s,
+                  const uint32_t* gscan, hipStream_t st, const RestartWs* pw, uint64_t* ck_build);
+
 int progress_log(mums_ctx* ctx, const CrStream& s, const uint32_t* gscan, hipStream_t st,
                  const RestartWs* pw = nullptr, uint64_t* ck_build = nullptr) {
     ctx->progress.clear();
@@ -3703,26 +3809,36 @@ int progress_log(mums_ctx* ctx, const CrStream& s, const uint32_t* gscan, hipStr
     constexpr uint64_t kBuf = restart::kMerBuffer;
     const uint64_t R = ctx->restarts;
     if (R && ctx->consumed_log.size() != R * Gu) return fail(ctx, MUMS_E_HIP, "progress: restart plan without consumed positions");
-    struct Ev { uint64_t phase, g, size; };
-    std::vector<Ev> ev;
+    std::vector<ProgressEv> ev;
     std::vector<uint64_t> q;
-    std::vector<uint64_t> S(Gu, 0), total_sp(R + 1, 0);
-    uint64_t total = 0;
-    for (int g = 0; g < G; ++g) total += gt.n[g];   // MatchFinder.cpp:146: SortedMerList::Length() = seq_len
+    std::vector<uint64_t> S(Gu, 0), total_sp(R + 1, 0), Sall((R + 1) * Gu, 0);
     for (uint64_t p = 0; p <= R; ++p) {
         for (int g = 0; g < G; ++g) {
             S[g] = p == 0 ? (g < (int)ctx->start_points.size() ? ctx->start_points[g] : 0) : ctx->offset_log[(p - 1) * Gu + g];
+            Sall[p * Gu + g] = S[g];
             total_sp[p] += S[g];
             const uint64_t m = gt.m[g];
             const uint64_t cons = p < R ? ctx->consumed_log[p * Gu + g] : m;
             for (uint64_t a = S[g]; a < m; a += kBuf) {
                 const uint64_t e = std::min(a + kBuf, m);
                 if (e > cons) break;
-                ev.push_back(Ev{p, (uint64_t)g, e - a});
+                ev.push_back(ProgressEv{p, (uint64_t)g, e - a});
                 q.push_back(((uint64_t)g << 56) | (e - 1));
             }
         }
     }
+    return progress_text(ctx, ev, q, R + 1, Sall, total_sp, s, gscan, st, pw, ck_build);
+}
+
+int progress_text(mums_ctx* ctx, const std::vector<ProgressEv>& ev, const std::vector<uint64_t>& q, uint64_t nph,
+                  const std::vector<uint64_t>& Sall, const std::vector<uint64_t>& base, const CrStream& s,
+                  const uint32_t* gscan, hipStream_t st, const RestartWs* pw, uint64_t* ck_build) {
+    ctx->progress.clear();
+    const GenomeTable& gt = ctx->gt;
+    const int G = gt.G;
+    const uint64_t Gu = (uint64_t)G;
+    uint64_t total = 0;
+    for (int g = 0; g < G; ++g) total += gt.n[g];   // MatchFinder.cpp:146: SortedMerList::Length() = seq_len
     std::vector<uint64_t> key(q.size(), 0);
     if (!q.empty() && !s.rec) {   // no packed stream (the pair path): the SMLs of pw answer
         if (!pw) return fail(ctx, MUMS_E_HIP, "progress: neither a stream nor SMLs (internal error)");
@@ -3778,9 +3894,9 @@ int progress_log(mums_ctx* ctx, const CrStream& s, const uint32_t* gscan, hipStr
     if (!groups.empty() && (pw || ck_build)) {
         const uint64_t ng = groups.size();
         DevBuf aux;
-        HIPCHK(aux.ensure(((R + 1) * Gu + 2 * ng + 2 * (Gu + 1)) * 8 + ng * 4 + ng * Gu * 4 + 1024));
+        HIPCHK(aux.ensure((nph * Gu + 2 * ng + 2 * (Gu + 1)) * 8 + ng * 4 + ng * Gu * 4 + 1024));
         uint64_t* d_S = aux.as<uint64_t>();
-        uint64_t* d_gk = d_S + (R + 1) * Gu;
+        uint64_t* d_gk = d_S + nph * Gu;
         uint64_t* d_gu = d_gk + ng;
         uint64_t* d_dm = d_gu + ng;
         uint64_t* d_db = d_dm + Gu + 1;
@@ -3803,11 +3919,6 @@ int progress_log(mums_ctx* ctx, const CrStream& s, const uint32_t* gscan, hipStr
             w.dm = d_dm;
             w.dbase = d_db;
         }
-        std::vector<uint64_t> Sall((R + 1) * Gu, 0);
-        for (uint64_t p = 0; p <= R; ++p)
-            for (int g = 0; g < G; ++g)
-                Sall[p * Gu + g] = p == 0 ? (g < (int)ctx->start_points.size() ? ctx->start_points[g] : 0)
-                                          : ctx->offset_log[(p - 1) * Gu + g];
         HIPCHK(hipMemcpyAsync(d_S, Sall.data(), Sall.size() * 8, hipMemcpyHostToDevice, st));
         HIPCHK(hipMemcpyAsync(d_gk, gk.data(), ng * 8, hipMemcpyHostToDevice, st));
         HIPCHK(hipMemcpyAsync(d_gu, gu.data(), ng * 8, hipMemcpyHostToDevice, st));
@@ -3831,7 +3942,7 @@ int progress_log(mums_ctx* ctx, const CrStream& s, const uint32_t* gscan, hipStr
     for (uint64_t i : ord) {
         if (ev[i].phase != phase) {
             phase = ev[i].phase;
-            processed = total_sp[phase];   // :147 / :150-158
+            if (!base.empty()) processed = base[phase];   // :147 / :150-158
         }
         processed += ev[i].size;
         const double old = m_progress;
@@ -3843,6 +3954,55 @@ int progress_log(mums_ctx* ctx, const CrStream& s, const uint32_t* gscan, hipStr
         if (((int)old / 10) != ((int)m_progress / 10)) ctx->progress += "\n";
     }
     return MUMS_OK;
+}
+
+// ParallelMemHash LogProgress (ParallelMemHash.cpp:56-61, 86-101) in the schedule of one
+// OpenMP thread: the chunks' SearchRange calls in chunk order, genome g of chunk c read in
+// MER_BUFFER_SIZE buffers from S = hcs[c][g] up to the chunk's search_len (the next chunk's
+// start; the last chunk: the SML end), mers_processed set to 0 once and carried across the
+// chunks.  A chunk cut by MER_REPEAT_LIMIT (compat_truncate) refills only the buffers its
+// merge consumed.  The SML keys are the genome-major ckeys in ctx->crall.
+int progress_compat(mums_ctx* ctx, uint32_t nch, const std::vector<uint64_t>& hcs, hipStream_t st) {
+    const GenomeTable& gt = ctx->gt;
+    const int G = gt.G;
+    const uint64_t Gu = (uint64_t)G;
+    constexpr uint64_t kBuf = restart::kMerBuffer;
+    if (hcs.size() < (uint64_t)nch * Gu) return fail(ctx, MUMS_E_HIP, "progress: chunk starts missing (internal error)");
+    std::vector<ProgressEv> ev;
+    std::vector<uint64_t> q, Sall((uint64_t)nch * Gu, 0);
+    for (uint32_t c = 0; c < nch; ++c) {
+        for (int g = 0; g < G; ++g) {
+            const uint64_t m = gt.m[g];
+            const uint64_t S = std::min(hcs[(uint64_t)c * Gu + g], m);
+            uint64_t E = c + 1 < nch ? std::min(hcs[(uint64_t)(c + 1) * Gu + g], m) : m;
+            if (E < S) E = S;
+            const uint64_t cz = ctx->compat_cons.empty() ? ~0ull : ctx->compat_cons[(uint64_t)c * Gu + g];
+            const uint64_t cons = cz == ~0ull ? E : cz;
+            Sall[(uint64_t)c * Gu + g] = S;
+            for (uint64_t a = S; a < E; a += kBuf) {
+                const uint64_t e = std::min(a + kBuf, E);
+                if (e > cons) break;
+                ev.push_back(ProgressEv{c, (uint64_t)g, e - a});
+                q.push_back(((uint64_t)g << 56) | (e - 1));
+            }
+        }
+    }
+    DevBuf aux;
+    HIPCHK(aux.ensure(2 * (Gu + 1) * 8 + 64));
+    std::vector<uint64_t> hm(2 * (Gu + 1), 0);
+    for (int g = 0; g < G; ++g) {
+        hm[g] = gt.m[g];
+        hm[Gu + 1 + g] = gt.base[g];
+    }
+    HIPCHK(hipMemcpyAsync(aux.p, hm.data(), hm.size() * 8, hipMemcpyHostToDevice, st));
+    RestartWs w{};
+    w.ck = ctx->crall.as<uint64_t>();
+    w.dm = aux.as<uint64_t>();
+    w.dbase = aux.as<uint64_t>() + Gu + 1;
+    const CrStream none{nullptr, nullptr, 0, 0};
+    const int rc = progress_text(ctx, ev, q, nch, Sall, {}, none, nullptr, st, &w, nullptr);
+    HIPCHK(hipStreamSynchronize(st));   // aux is freed on return
+    return rc;
 }
 
 // the single-context packed stream (records key_low << 32 | index, 2^B MSD buckets starting at

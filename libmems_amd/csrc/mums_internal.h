@@ -422,12 +422,15 @@ hipError_t launch_compat_cands(const uint64_t* key2, uint64_t N, uint64_t* list,
                                hipStream_t st);
 hipError_t launch_compat_fire(const restart::PlanData& d, const uint64_t* key2, uint64_t N, int kbits,
                               const uint64_t* cand, uint64_t C, const uint64_t* cs, uint32_t nch, uint32_t* out,
-                              uint64_t* cend, hipStream_t st);
+                              uint64_t* cend, uint64_t* cons, hipStream_t st);
+hipError_t launch_compat_probe_chunks(const uint64_t* probe_info, uint64_t P, const uint64_t* key2, int kbits,
+                                      uint32_t nch, uint32_t* pfirst, hipStream_t st);
 hipError_t launch_compat_drop(const uint64_t* k_in, const uint32_t* v_in, uint64_t N, const uint64_t* rlo,
                               const uint64_t* rhi, const uint64_t* rpre, uint32_t R, uint64_t* k_out, uint32_t* v_out,
                               hipStream_t st);
 hipError_t launch_compat_merge(uint32_t* tsize, const uint32_t* bstart, uint32_t* tbl, const int64_t* pool, int G,
-                               uint32_t Tb, unsigned long long* collisions, hipStream_t st);
+                               uint32_t Tb, unsigned long long* collisions, const uint32_t* tscan, uint64_t total,
+                               uint32_t* first_fail, hipStream_t st);
 
 // restart.hip: MER_REPEAT_LIMIT restart (MatchFinder.cpp:253-277) / start points
 // (MemHash.cpp:117-127) as a fix-up of the merged stream

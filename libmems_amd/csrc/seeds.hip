@@ -168,6 +168,9 @@ __global__ __launch_bounds__(kBlock) void seed_pack_kernel(SeedSpec ss, GenomeTa
 // chunk (hist = all slices, each scanned on its own: 32-bit offsets inside a chunk).
 // four waves per SIMD for the <= 256-digit forms (the 2^11-digit development form
 // cannot reach it: its LDS alone allows two blocks per CU)
+#ifndef MUMS_SCATTER_SWZ
+#define MUMS_SCATTER_SWZ 1
+#endif
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Wpass-failed"
 // kSide: the key has side_bits (<= 4) bits between the record's 64 - IB key bits and the
@@ -197,7 +200,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     static_assert(kTile <= 65535, "16-bit wave digit offsets");
     static_assert(kSide == 0 || kTile <= 4096, "side digits sit in bits 28-31 above a 12-bit rank");
     uint32_t* words = reinterpret_cast<uint32_t*>(srec);
+#if MUMS_SCATTER_SWZ
+    // XCD-grouped tiles (a bijective blockIdx swizzle, cdna_hip_programming.md T1): blocks
+    // b, b + 8, b + 16 ... share an XCD (round-robin dispatch, speed only) and take
+    // consecutive seed tiles, so the digit runs consecutive tiles store into one MSD bucket
+    // -- which abut in the output -- meet in that XCD's L2 and their partial lines merge
+    const uint32_t t = [] {
+        const uint32_t b = blockIdx.x, n = gridDim.x, q = n >> 3, r = n & 7u, x = b & 7u;
+        return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+    }();
+#else
     const uint32_t t = blockIdx.x;
+#endif
     const int g = tile_genome(gt, t);
     const uint32_t x = t - gt.tfirst[g];
     const uint64_t m = gt.m[g];

@@ -476,6 +476,7 @@ struct oracle_result {
     int offlog_g;
     uint64_t* mlog_len;       /* SetMatchLog (MemHash.cpp:238-241): inserted entries in insertion order */
     int64_t* mlog_s;
+    uint64_t mlog_n, mlog_cap;
     uint32_t* plog_bucket;    /* seeds_only: per AddHashEntry call, its bucket ... */
     uint64_t* plog_ref;       /* ... and the global seed-mer index of the probe's first start */
     /* LogProgress (MatchFinder.cpp:55-56, 137-164, 296-309): the text a log stream receives */
@@ -508,6 +509,18 @@ static void prog_event(oracle_result* res, uint64_t size) {
         prog_append(res, b);
     }
     if (((int)old / 10) != ((int)res->m_progress / 10)) prog_append(res, "\n");
+}
+
+/* one SetMatchLog line (MemHash.cpp:238-241): the inserted entry */
+static void mlog_push(oracle_result* res, uint64_t len, const int64_t* st, int G) {
+    if (res->mlog_n == res->mlog_cap) {
+        res->mlog_cap = res->mlog_cap ? res->mlog_cap * 2 : 256;
+        res->mlog_len = (uint64_t*)realloc(res->mlog_len, res->mlog_cap * sizeof(uint64_t));
+        res->mlog_s = (int64_t*)realloc(res->mlog_s, res->mlog_cap * (size_t)G * sizeof(int64_t));
+    }
+    res->mlog_len[res->mlog_n] = len;
+    memcpy(res->mlog_s + res->mlog_n * (uint64_t)G, st, (size_t)G * sizeof(int64_t));
+    ++res->mlog_n;
 }
 
 typedef struct {
@@ -931,13 +944,14 @@ static int get_breakpoint(int sarI, uint64_t startI, int G, bmer_t* const* sml, 
 /* AddHashEntry of SURVEY.md Appendix B.3 as MergeTable calls it,                  */
 /* ParallelMemHash.cpp:105-121): lower_bound, collision if equivalent, else insert;*/
 /* Extended() is set, so no extension (MemHash.cpp:223-224).                        */
-static void merge_entry(memhash_t* h, bucket_t* b, uint32_t id) {
+static void merge_entry(memhash_t* h, bucket_t* b, uint32_t id, oracle_result* res) {
     const mhe_t* e = &h->pool[id];
     uint32_t it = lower_bound_mhe(h, b, e);
     if (it != b->n) {
         const mhe_t* x = &h->pool[b->v[it]];
         if (!mhe_less(x, e, h->x.G) && !mhe_less(e, x, h->x.G)) { ++h->collisions; return; }
     }
+    mlog_push(res, (uint64_t)e->len, e->s, h->x.G);   /* the patched AddHashEntry logs this insert too */
     if (b->n == b->cap) {
         b->cap = b->cap ? b->cap * 2 : 4;
         b->v = (uint32_t*)realloc(b->v, b->cap * sizeof(uint32_t));
@@ -976,6 +990,13 @@ static int parallel_compat_search(memhash_t* h, const oracle_params* prm, int G,
         if (cs[nch * G + mx] <= cs[(nch - 1) * G + mx]) { free(cs); return -1; }
         ++nch;
     }
+    /* progress counters, set once for the whole loop (:56-61); SearchRange never resets them, so
+       with one thread the text is every chunk's buffer refills in chunk order */
+    res->prog_on = 1;
+    res->mers_processed = 0;
+    res->total_mers = 0;
+    res->m_progress = -1;
+    for (int g = 0; g < G; ++g) res->total_mers += lens[g];
     const uint32_t T = h->table_size;
     bucket_t* gb = (bucket_t*)calloc(T, sizeof(bucket_t));   /* global table G */
     uint64_t* lo = (uint64_t*)malloc((size_t)G * sizeof(uint64_t));
@@ -986,10 +1007,13 @@ static int parallel_compat_search(memhash_t* h, const oracle_params* prm, int G,
             /* chunk_lens = next start - start (gnSeqI, wraps) or GNSEQI_END (:91-96) */
             hi[g] = (i + 1 < nch) ? cs[(i + 1) * G + g] - cs[i * G + g] : UINT64_MAX;
         }
+        const uint64_t p0 = h->pool_n;
         (void)search_range_lit(h, prm, G, sml, m, lens, lo, hi, res);   /* return value ignored (:97) */
+        /* match log: the thread-table inserts of this chunk (pool order = AddHashEntry order) ... */
+        for (uint64_t k = p0; k < h->pool_n; ++k) mlog_push(res, (uint64_t)h->pool[k].len, h->pool[k].s, G);
         if (prm->parallel_compat == 2 && i + 1 < nch) continue;   /* checking aid: one deferred merge */
         for (uint32_t bI = 0; bI < T; ++bI)
-            for (uint32_t k = 0; k < h->buckets[bI].n; ++k) merge_entry(h, &gb[bI], h->buckets[bI].v[k]);
+            for (uint32_t k = 0; k < h->buckets[bI].n; ++k) merge_entry(h, &gb[bI], h->buckets[bI].v[k], res);   /* ... then MergeTable's */
         for (uint32_t bI = 0; bI < T; ++bI) {   /* thread table = global table */
             bucket_t* tb = &h->buckets[bI];
             if (tb->cap < gb[bI].n) {
@@ -1070,12 +1094,14 @@ oracle_result* oracle_find_matches(int G, const char* const* seqs, const uint64_
         res->collision_count = h.collisions;
         res->probes = h.probes;
         if (!prm->parallel_compat && h.pool_n == h.mem_count) {   /* pool ids = insertion order */
-            res->mlog_len = (uint64_t*)malloc((h.pool_n ? h.pool_n : 1) * sizeof(uint64_t));
-            res->mlog_s = (int64_t*)malloc((h.pool_n ? h.pool_n : 1) * (size_t)G * sizeof(int64_t));
-            for (uint64_t k = 0; k < h.pool_n; ++k) {
-                res->mlog_len[k] = (uint64_t)h.pool[k].len;
-                memcpy(res->mlog_s + k * (uint64_t)G, h.pool[k].s, (size_t)G * sizeof(int64_t));
-            }
+            for (uint64_t k = 0; k < h.pool_n; ++k) mlog_push(res, (uint64_t)h.pool[k].len, h.pool[k].s, G);
+        } else if (!prm->parallel_compat) {
+            free(res->mlog_len); free(res->mlog_s);
+            res->mlog_len = NULL; res->mlog_s = NULL; res->mlog_n = 0;
+        }
+        if ((prm->parallel_compat || h.pool_n == h.mem_count) && !res->mlog_len) {   /* an empty log */
+            res->mlog_len = (uint64_t*)malloc(sizeof(uint64_t));
+            res->mlog_s = (int64_t*)malloc((size_t)G * sizeof(int64_t));
         }
         free(h.buckets); free(h.pool); free(h.spool); free(gbase); free(h.cm); free(h.hl);
         res->plog_bucket = h.plog_bucket;
@@ -1397,10 +1423,12 @@ uint64_t oracle_result_restarts(const oracle_result* r) { return r ? r->restarts
 /* rows = restarts, G entries each; returns 0 */
 int oracle_result_match_log(const oracle_result* r, uint64_t* lengths, int64_t* starts) {
     if (!r->mlog_len) return -1;
-    if (lengths) memcpy(lengths, r->mlog_len, r->mem_count * sizeof(uint64_t));
-    if (starts) memcpy(starts, r->mlog_s, r->mem_count * (size_t)r->G * sizeof(int64_t));
+    if (lengths) memcpy(lengths, r->mlog_len, r->mlog_n * sizeof(uint64_t));
+    if (starts) memcpy(starts, r->mlog_s, r->mlog_n * (size_t)r->G * sizeof(int64_t));
     return 0;
 }
+/* lines of the match log (MemCount for MemHash; thread-table + MergeTable inserts in compat) */
+uint64_t oracle_result_match_log_count(const oracle_result* r) { return r ? r->mlog_n : 0; }
 
 int oracle_result_offset_log(const oracle_result* r, uint64_t* out) {
     if (!r) return -1;

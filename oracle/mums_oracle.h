@@ -82,6 +82,7 @@ uint64_t oracle_result_chunks(const oracle_result* r);     /* compat: chunks sea
 uint64_t oracle_result_restarts(const oracle_result* r);   /* MER_REPEAT_LIMIT restarts */
 const char* oracle_result_progress(const oracle_result* r); /* LogProgress text (serial MemHash path) */
 int      oracle_result_match_log(const oracle_result* r, uint64_t* lengths, int64_t* starts); /* SetMatchLog order */
+uint64_t oracle_result_match_log_count(const oracle_result* r);   /* its lines */
 int      oracle_result_offset_log(const oracle_result* r, uint64_t* out); /* restarts x G start points */
 void     oracle_result_free(oracle_result* r);
 /* OpenMP driver of the same restatement (the bench's CPU baseline on the host cores):

@@ -189,8 +189,11 @@ def find_matches(seqs: Sequence[bytes], seed: int, repeat_tol: int = 0, enum_tol
         L.oracle_result_progress.argtypes = [ctypes.c_void_p]
         stats["progress"] = (L.oracle_result_progress(r) or b"").decode()
         L.oracle_result_match_log.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
-        ml_len = np.zeros(int(stats["mem_count"]), dtype=np.uint64)
-        ml_s = np.zeros((int(stats["mem_count"]), G), dtype=np.int64)
+        L.oracle_result_match_log_count.restype = ctypes.c_uint64
+        L.oracle_result_match_log_count.argtypes = [ctypes.c_void_p]
+        nlog = int(L.oracle_result_match_log_count(r))
+        ml_len = np.zeros(nlog, dtype=np.uint64)
+        ml_s = np.zeros((nlog, G), dtype=np.int64)
         if L.oracle_result_match_log(r, ml_len.ctypes.data, ml_s.ctypes.data) == 0:
             stats["match_log"] = (ml_len, ml_s)   # SetMatchLog: inserted entries in insertion order
     finally:

@@ -107,3 +107,31 @@ def test_parallel_repeat_limit_cuts_vs_oracle(gpu_lib, oracle_mod, copies, tande
     assert st["chunks"] == ost["chunks"] and st["restarts"] == ost["restarts"]
     assert len(ml) == len(lengths)
     assert (ml.lengths == lengths).all() and (ml.starts == starts).all()
+
+
+@pytest.mark.parametrize("case", ["known"] + [f"small{i}" for i in (0, 1, 4, 7)])
+def test_parallel_merge_exact_pass_everywhere(gpu_lib, oracle_mod, monkeypatch, case):
+    """MergeTable's two passes (compat.hip): the speculative append check, then the exact
+    batched merge from a bucket's first entry that does not append.  The test hook runs every
+    bucket through the exact pass from its first entry; both must give the oracle's list."""
+    if case == "known":
+        c = PCOMPAT[0]
+        seqs = oracle_mod.generate(c["G"], c["n"], c["p"], 12345)
+        w, chunk = c["w"], c["chunk_size"]
+    else:
+        G, n, p, w, chunk, gseed = COMPAT_SMALL[int(case[5:])]
+        seqs = oracle_mod.generate(G, n, p, gseed)
+    seed = oracle_mod.get_seed(w)
+    if case != "known":
+        lengths, starts, ost = oracle_mod.find_matches(seqs, seed, parallel_compat=True, chunk_size=chunk)
+    for exact in (False, True):
+        with monkeypatch.context() as m:
+            if exact:
+                m.setenv("MUMS_DEV_COMPAT_MERGE_EXACT", "1")
+            ml, st = gpu_parallel(gpu_lib, seqs, seed, chunk)
+        if case == "known":   # the patched reference's 15 893 entries, md5 of the text
+            assert len(ml) == c["matches"], exact
+            assert hashlib.md5(ml.text().encode()).hexdigest() == c["md5"], exact
+            continue
+        assert len(ml) == len(lengths), exact
+        assert (ml.lengths == lengths).all() and (ml.starts == starts).all(), exact

@@ -11,9 +11,10 @@ VALS=${VALS:-"0 1"}
 for rep in 1 2; do
   for v in $VALS; do
     if [ "$v" = 0 ]; then unset $VAR; else export $VAR=$v; fi
+    f=$(echo "$v" | tr '/.' '__')
     timeout -k 10 300 python3 -u bench.py --steps 20 --warmup 3 --no-cpu-baseline ${EXTRA_ARGS:---no-mums} \
-      > $OUT/v${v}_r$rep.json 2> $OUT/v${v}_r$rep.err || { echo "variant $v failed"; tail -20 $OUT/v${v}_r$rep.err; exit 11; }
-    python3 - $OUT/v${v}_r$rep.json "$VAR=$v" <<'PY'
+      > $OUT/v${f}_r$rep.json 2> $OUT/v${f}_r$rep.err || { echo "variant $v failed"; tail -20 $OUT/v${f}_r$rep.err; exit 11; }
+    python3 - $OUT/v${f}_r$rep.json "$VAR=$v" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 ph = d.get("phase_ms_per_step", {})
