@@ -191,15 +191,19 @@ int  mums_length_filter(mums_ctx* ctx, uint64_t min_length);
  * log stream as it inserts it (MemHash.cpp:238-241: `len\ts0\t...` per line, the order of
  * the AddHashEntry calls that inserted them).  Enable before mums_find; afterwards
  * mums_match_log_copy returns those entries in that order (*count first: lengths / starts
- * NULL); MemHash / MaskedMemHash / PairwiseMatchFinder paths, not ParallelMemHash compat. */
+ * NULL).  ParallelMemHash compat (the patched 2-argument AddHashEntry of SURVEY.md B.3,
+ * one OpenMP thread): per chunk its thread-table inserts in call order, then MergeTable's
+ * inserts (ParallelMemHash.cpp:105-121) in bucket order -- every entry appears twice. */
 int  mums_set_match_log(mums_ctx* ctx, int enable);
 int  mums_match_log_copy(mums_ctx* ctx, uint64_t* lengths, int64_t* starts, uint64_t capacity, uint64_t* count);
 /* MatchFinder::LogProgress (MatchFinder.h:80, MatchFinder.cpp:55-56,296-309): the reference
  * writes "N%.." to the log stream each time its merge crosses a whole percent of the mers
  * (counted per 10 000-mer buffer refill, a newline every ten).  Enable before mums_find; the
  * seed stage then restates that text (MER_REPEAT_LIMIT restarts and start points included;
- * single context and chunked mode with packed records, i.e. seed weight <= 21) and
- * mums_progress_log_copy returns it (*length = its size; text NUL-terminated, may be NULL). */
+ * single context and chunked mode with packed records, i.e. seed weight <= 21; ParallelMemHash
+ * compat: every chunk's SearchRange in chunk order, the count set once for the whole loop,
+ * ParallelMemHash.cpp:56-61) and mums_progress_log_copy returns it (*length = its size; text
+ * NUL-terminated, may be NULL). */
 int  mums_set_progress_log(mums_ctx* ctx, int enable);
 int  mums_progress_log_copy(mums_ctx* ctx, char* text, uint64_t capacity, uint64_t* length);
 /* EliminateOverlaps (libMems/Aligner.cpp:62-176, declared Aligner.h:239) on the context's

@@ -45,6 +45,16 @@ constexpr int kWalkBudget = MUMS_WALK_BUDGET;   // words per lane in chain_walk_
 #define MUMS_WALK_SORT_SHIFT 11
 #endif
 constexpr int kWalkSortShift = MUMS_WALK_SORT_SHIFT;   // walk order granule: 2^11 columns
+#ifndef MUMS_WALK_SWZ
+#define MUMS_WALK_SWZ 1   // walk kernels: XCD-grouped block order (xcd_grouped_block)
+#endif
+__device__ __forceinline__ unsigned walk_block() {
+#if MUMS_WALK_SWZ
+    return xcd_grouped_block(blockIdx.x, gridDim.x);
+#else
+    return blockIdx.x;
+#endif
+}
 #ifndef MUMS_HIT_BATCH
 #define MUMS_HIT_BATCH 2   // components whose window loads are in flight together (hit_word; A/B round 4: 1 / 2 / 4 / 8)
 #endif   // 64-column hit words per lane before a walk goes to a workgroup
@@ -509,7 +519,7 @@ __global__ __launch_bounds__(kBlock) void chain_walk_short_kernel(View v, const 
     const unsigned nq = *qcount;
     const unsigned stride = gridDim.x * kBlock;
     // block-uniform trip count: block_push synchronises the workgroup
-    for (unsigned q0 = blockIdx.x * kBlock; q0 < nq; q0 += stride) {
+    for (unsigned q0 = walk_block() * kBlock; q0 < nq; q0 += stride) {
         const unsigned q = q0 + threadIdx.x;
         uint32_t want = 0;
         WalkItem nx[1] = {WalkItem{}};
@@ -683,7 +693,7 @@ __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64
     const LineSpec ls = line_spec(ss, gt);
     const unsigned nq = *qcount;
     const unsigned ngroups = gridDim.x * (kBlock / GS);
-    for (unsigned qi = (blockIdx.x * kBlock + threadIdx.x) / GS; qi < nq; qi += ngroups) {
+    for (unsigned qi = (walk_block() * kBlock + threadIdx.x) / GS; qi < nq; qi += ngroups) {
         const WalkItem it = queue[qi];
         Mhe<MG> A;
         probe_of<MG, View>(v, probe_info, it.j, gt, mp, L, A);

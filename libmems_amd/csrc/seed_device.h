@@ -10,6 +10,14 @@
 
 namespace mums {
 
+// XCD-grouped block order (a bijective blockIdx swizzle, cdna_hip_programming.md T1): the
+// dispatcher hands workgroups to the 8 XCDs round-robin, so blocks b, b + 8, b + 16 ...
+// share one L2; they get consecutive work indices (placement is a speed matter only)
+__device__ __forceinline__ uint32_t xcd_grouped_block(uint32_t b, uint32_t n) {
+    const uint32_t q = n >> 3, r = n & 7u, x = b & 7u;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+
 // 2w-bit reverse complement (RevCompMer, SortedMerList.cpp:597-614, on bottom-aligned bits)
 __device__ __forceinline__ uint64_t revcomp2w(uint64_t v, int w) {
     uint64_t x = ~v;

@@ -205,10 +205,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     // b, b + 8, b + 16 ... share an XCD (round-robin dispatch, speed only) and take
     // consecutive seed tiles, so the digit runs consecutive tiles store into one MSD bucket
     // -- which abut in the output -- meet in that XCD's L2 and their partial lines merge
-    const uint32_t t = [] {
-        const uint32_t b = blockIdx.x, n = gridDim.x, q = n >> 3, r = n & 7u, x = b & 7u;
-        return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
-    }();
+    const uint32_t t = xcd_grouped_block(blockIdx.x, gridDim.x);
 #else
     const uint32_t t = blockIdx.x;
 #endif
