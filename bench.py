@@ -180,11 +180,12 @@ def run_mums(device: int, dev: torch.device, p: float = 0.01, reps: int = 3):
                                                         "ms_output")}}
 
 
-WALK_PMC = os.path.join(ROOT, "profiles", "r04v_pmc_chains.txt")
+_WALK_PMCS = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_chains.txt")))
+WALK_PMC = _WALK_PMCS[-1] if _WALK_PMCS else os.path.join(ROOT, "profiles", "r04v_pmc_chains.txt")
 
 
-def walk_counter_traffic(walk_ms):
-    """chain_walk_kernel's HBM-side bytes from the committed rocprofv3 PMC passes
+def walk_counter_traffic(walk_ms, kernel="chain_walk_kernel"):
+    """A walk kernel's HBM-side bytes from the committed rocprofv3 PMC passes
     (tools/pmc_chains.sh: FETCH_SIZE + WRITE_SIZE per dispatch, KiB, not this run) over the
     live duration of its two launches: the counter-based roofline next to the requested one."""
     try:
@@ -192,18 +193,31 @@ def walk_counter_traffic(walk_ms):
         seen = 0
         for line in open(WALK_PMC):   # "<kernel> <counter> <value per dispatch>", kernel names may hold spaces
             f = line.rsplit(None, 2)
-            if len(f) == 3 and f[0].startswith("chain_walk_kernel") and f[1] in per:
+            if len(f) == 3 and f[0].startswith(kernel + "<") and f[1] in per:
                 per[f[1]] += float(f[2]) * 1024
                 seen += 1
         if not seen:
-            raise KeyError("chain_walk_kernel")
+            raise KeyError(kernel)
         b = 2 * (per["FETCH_SIZE"] + per["WRITE_SIZE"])   # each instance: one launch per pass, two passes
         gbs = b / (walk_ms * 1e-3) / 1e9
         return {"traffic": b, "traffic_achieved": gbs, "traffic_frac": gbs / HBM_PEAK_GBS,
-                "traffic_source": os.path.relpath(WALK_PMC, ROOT) + " (FETCH_SIZE + WRITE_SIZE per dispatch of "
-                                  "every chain_walk_kernel instance x 2 passes, rocprofv3 PMC passes, not this run)"}
+                "traffic_source": os.path.relpath(WALK_PMC, ROOT) + f" (FETCH_SIZE + WRITE_SIZE per dispatch of "
+                                  f"every {kernel} instance x 2 passes, rocprofv3 PMC passes, not this run)"}
     except (OSError, KeyError, ValueError, ZeroDivisionError):
         return {"traffic": None}
+
+
+def walk_roofline(kernel, ms, nbytes, walks, words, what):
+    """Requested-bytes roofline of one walk kernel (HIP events around its two launches) with
+    the committed counter bytes beside it."""
+    gbs = nbytes / (ms * 1e-3) / 1e9 if ms > 0 else None
+    return {"bound": "hbm", "kernel": kernel + " (2 launches per FindMatches, " + what + ")",
+            "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS if gbs else None,
+            "bytes": nbytes, "ms": ms, "walks": walks, "hit_words": words,
+            "model": "REQUESTED bytes: 28-B packed window per 64-column hit word and present component + per walk "
+                     "the probe row (int32 starts, 32 B at G=8) and its 24-B queue item; much of the 200 MB packed "
+                     "genome is served from L2 / MALL",
+            **(walk_counter_traffic(ms, kernel) if ms > 0 else {"traffic": None})}
 
 
 def run_compat(device: int, genomes, seed, reps: int = 2):
@@ -448,23 +462,19 @@ def main():
             mh.CreateMatches()
             sp = mh.stats()
             mh.SetProfiling(False)
-            walk_ms = sp["ms_chain_walks"]
-            walk_gbs = sp["chain_walk_bytes"] / (walk_ms * 1e-3) / 1e9 if walk_ms > 0 else None
             mums_c3 = {"mums_per_s": sm["mem_count"] / best, "matches": sm["mem_count"], "ms": best * 1e3,
                        "probes": sm["probes"], "chains": sm["chains"], "collisions": sm["collision_count"],
                        "workload": f"BASELINE config 3: {G} x {n // 10**6} Mbp related p=0.01, w19, full FindMatches",
                        "phase_ms": {k: round(sm[k], 3) for k in ("ms_keys", "ms_sort", "ms_groups", "ms_buckets",
                                                                   "ms_chains", "ms_replay", "ms_output")},
-                       "roofline": {"bound": "hbm", "kernel": "chain_walk_kernel (2 launches per FindMatches, the "
-                                                              "long walks)",
-                                    "achieved": walk_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                    "frac": walk_gbs / HBM_PEAK_GBS if walk_gbs else None,
-                                    "bytes": sp["chain_walk_bytes"], "ms": walk_ms, "walks": sp["chain_walks"],
-                                    "hit_words": sp["chain_walk_words"],
-                                    "model": "REQUESTED bytes: 28-B packed window per 64-column hit word and present "
-                                             "component + per walk the probe row (int32 starts, 32 B at G=8) and its "
-                                             "24-B queue item; much of the 200 MB packed genome is served from L2 / MALL",
-                                    **walk_counter_traffic(walk_ms)}}
+                       # FindMatches' largest kernel, then the lane-group walks it hands on to
+                       "roofline": walk_roofline("chain_walk_short_kernel", sp["ms_short_walks"],
+                                                 sp["short_walk_bytes"], sp["short_walks"], sp["short_walk_words"],
+                                                 "every queued walk, one lane each, up to 8 words"),
+                       "roofline_long_walks": walk_roofline("chain_walk_kernel", sp["ms_chain_walks"],
+                                                            sp["chain_walk_bytes"], sp["chain_walks"],
+                                                            sp["chain_walk_words"],
+                                                            "the walks past 8 words, 16 then 64 lanes each")}
         except Exception as e:  # report, never hide
             mums_c3 = {"error": str(e)}
         progress("C3 end to end")

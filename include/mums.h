@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MUMS_ABI_VERSION 5
+#define MUMS_ABI_VERSION 6
 
 enum mums_status {
     MUMS_OK = 0,
@@ -81,6 +81,12 @@ typedef struct mums_stats {
     uint64_t chain_walk_words;
     uint64_t chain_walks;
     uint64_t chain_walk_bytes;
+    /* the same for chain_walk_short_kernel (ABI 6): every queued walk's first kWalkBudget
+     * words, one lane per walk; the walks it hands on are counted again above. */
+    double   ms_short_walks;
+    uint64_t short_walk_words;
+    uint64_t short_walks;
+    uint64_t short_walk_bytes;
 } mums_stats;
 
 /* MemHash::MemHash (MemHash.cpp:33-49); device = HIP ordinal. */

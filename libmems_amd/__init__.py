@@ -83,6 +83,10 @@ class _Stats(ctypes.Structure):
         ("chain_walk_words", ctypes.c_uint64),
         ("chain_walks", ctypes.c_uint64),
         ("chain_walk_bytes", ctypes.c_uint64),
+        ("ms_short_walks", ctypes.c_double),
+        ("short_walk_words", ctypes.c_uint64),
+        ("short_walks", ctypes.c_uint64),
+        ("short_walk_bytes", ctypes.c_uint64),
     ]
 
 

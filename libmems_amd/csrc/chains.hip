@@ -46,7 +46,7 @@ constexpr int kWalkBudget = MUMS_WALK_BUDGET;   // words per lane in chain_walk_
 #endif
 constexpr int kWalkSortShift = MUMS_WALK_SORT_SHIFT;   // walk order granule: 2^11 columns
 #ifndef MUMS_WALK_SWZ
-#define MUMS_WALK_SWZ 1   // walk kernels: XCD-grouped block order (xcd_grouped_block)
+#define MUMS_WALK_SWZ 0   // 1: walk kernels in XCD-grouped block order (measured slower)
 #endif
 __device__ __forceinline__ unsigned walk_block() {
 #if MUMS_WALK_SWZ
@@ -333,12 +333,13 @@ __device__ __forceinline__ bool scan_word(uint64_t H, int64_t u0, int64_t* last,
 template <int MG>
 __device__ int64_t walk_lane(int dir, int64_t cur, int64_t stop, int budget, const Mhe<MG>& P, const GenomeTable& gt,
                              int64_t clo, int64_t chi, const uint32_t* __restrict__ packed, const SeedSpec& ss,
-                             const LineSpec& ls, int* state) {
+                             const LineSpec& ls, int* state, unsigned* words) {
     int64_t last = 0, u0 = 1;
     for (;;) {
         const int64_t col = cur + dir * last;
         if (dir > 0 ? col >= stop : col <= stop) { *state = 1; return col; }
         if (budget-- <= 0) { *state = 2; return col; }
+        ++*words;
         const uint64_t H = hit_word_dir<MG>(dir, cur + dir * u0, P, gt, clo, chi, packed, ss, ls);
         const bool broke = scan_word(H, u0, &last, ls.L);
         u0 += 64;
@@ -502,6 +503,15 @@ __global__ __launch_bounds__(kBlock) void walk_key_kernel(View v, GenomeTable gt
     rec[q] = ((uint64_t)(x > 0 ? x : 0) >> shift << 32) | q;
 }
 
+// records (j << 32 | i) of the handed-on walks: their line order back (MUMS_DEV_WALK_SORT=2)
+__global__ __launch_bounds__(kBlock) void walk_line_key_kernel(const WalkItem* __restrict__ lq,
+                                                               const unsigned int* __restrict__ lqcount,
+                                                               uint64_t* __restrict__ rec) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= *lqcount) return;
+    rec[i] = ((uint64_t)lq[i].j << 32) | i;
+}
+
 // Queued walks, one lane per item, up to kWalkBudget 64-column words each (most chain ends
 // lie within a few words); the rest go on to chain_walk_kernel's lane groups.
 template <int MG, typename View>
@@ -513,11 +523,13 @@ __global__ __launch_bounds__(kBlock) void chain_walk_short_kernel(View v, const 
                                                                   uint8_t* __restrict__ link, int64_t* __restrict__ rcol,
                                                                   int64_t* __restrict__ lcol, WalkItem* __restrict__ lq,
                                                                   unsigned int* __restrict__ lqcount,
-                                                                  const uint64_t* __restrict__ order) {
+                                                                  const uint64_t* __restrict__ order,
+                                                                  DevCounters* __restrict__ ctr) {
     const int L = ss.L;
     const LineSpec ls = line_spec(ss, gt);
     const unsigned nq = *qcount;
     const unsigned stride = gridDim.x * kBlock;
+    unsigned long long my_words = 0, my_items = 0, my_wins = 0;
     // block-uniform trip count: block_push synchronises the workgroup
     for (unsigned q0 = walk_block() * kBlock; q0 < nq; q0 += stride) {
         const unsigned q = q0 + threadIdx.x;
@@ -532,7 +544,15 @@ __global__ __launch_bounds__(kBlock) void chain_walk_short_kernel(View v, const 
             frame_bounds<MG>(A, gt, &clo, &chi);
             const int dir = it.kind == 2 ? -1 : +1;
             int state;
-            const int64_t c = walk_lane<MG>(dir, it.cur, it.stop, kWalkBudget, A, gt, clo, chi, packed, ss, ls, &state);
+            unsigned nw = 0;
+            const int64_t c = walk_lane<MG>(dir, it.cur, it.stop, kWalkBudget, A, gt, clo, chi, packed, ss, ls, &state,
+                                            &nw);
+            int npres = 0;
+            #pragma unroll
+            for (int g = 0; g < MG; ++g) npres += (g < gt.G && A.s[g] != 0) ? 1 : 0;
+            my_words += nw;
+            my_wins += (unsigned long long)nw * npres;
+            ++my_items;
             if (state == 2) {
                 nx[0] = WalkItem{it.j, it.kind, c, it.stop};
                 want = 1;
@@ -546,6 +566,19 @@ __global__ __launch_bounds__(kBlock) void chain_walk_short_kernel(View v, const 
             }
         }
         block_push<1>(want, nx, lq, lqcount);
+    }
+    if (ctr) {   // words / walks of this wave (the roofline's byte count): one atomic per wave
+        #pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            my_words += __shfl_xor(my_words, d, 64);
+            my_items += __shfl_xor(my_items, d, 64);
+            my_wins += __shfl_xor(my_wins, d, 64);
+        }
+        if ((threadIdx.x & 63) == 0 && my_items) {
+            atomicAdd(&ctr->short_words, my_words);
+            atomicAdd(&ctr->short_items, my_items);
+            atomicAdd(&ctr->short_wins, my_wins);
+        }
     }
 }
 
@@ -684,7 +717,8 @@ __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64
                                                             uint8_t* __restrict__ link, int64_t* __restrict__ rcol,
                                                             int64_t* __restrict__ lcol, unsigned int* __restrict__ dbg,
                                                             DevCounters* __restrict__ ctr, unsigned maxsteps,
-                                                            WalkItem* __restrict__ xq, unsigned int* __restrict__ xqcount) {
+                                                            WalkItem* __restrict__ xq, unsigned int* __restrict__ xqcount,
+                                                            const uint64_t* __restrict__ order) {
     static_assert(GS >= 2 && GS <= 64 && (GS & (GS - 1)) == 0, "group: power of 2");
     unsigned long long my_words = 0, my_items = 0, my_wins = 0;
     const int lane = threadIdx.x & 63, gl = lane & (GS - 1), gsh = lane & ~(GS - 1);
@@ -694,7 +728,7 @@ __global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64
     const unsigned nq = *qcount;
     const unsigned ngroups = gridDim.x * (kBlock / GS);
     for (unsigned qi = (walk_block() * kBlock + threadIdx.x) / GS; qi < nq; qi += ngroups) {
-        const WalkItem it = queue[qi];
+        const WalkItem it = queue[order ? (uint32_t)order[qi] : qi];
         Mhe<MG> A;
         probe_of<MG, View>(v, probe_info, it.j, gt, mp, L, A);
         const int64_t xa = start_at(A, first_start(A));
@@ -1164,7 +1198,10 @@ hipError_t chains_core(LV vl, const ChainWs& w, const uint32_t* ord, uint64_t P,
     // short walks in genome-position order (walk_key_kernel), MUMS_DEV_WALK_SORT=1: measured
     // slower at C3 than the queue's line order, kept for A/B runs
     const char* wsort_env = getenv("MUMS_DEV_WALK_SORT");
-    const bool wsort = !refill && wsort_env && wsort_env[0] == '1' && P < (1ull << 32);
+    const bool wsort = !refill && wsort_env && (wsort_env[0] == '1' || wsort_env[0] == '2') && P < (1ull << 32);
+    const bool wsort_long = wsort && wsort_env[0] == '2';   // and the handed-on walks back in line order
+    int pbits = 1;
+    while (pbits < 32 && (1ull << pbits) < P) ++pbits;
     const int wshift = kWalkSortShift;
     const int wbits = std::max(1, x_bits(gt) - wshift);
     uint32_t* d_err = ctr ? &((DevCounters*)ctr)->err : w.qcount + 14;
@@ -1195,6 +1232,7 @@ hipError_t chains_core(LV vl, const ChainWs& w, const uint32_t* ord, uint64_t P,
                 order = ob ? w.kB : w.kA;
             }
         }
+        if (ev_walk) (void)hipEventRecord(ev_walk[3 * pass], st);   // the short walks start
         if (refill)
             hipLaunchKernelGGL((chain_walk_refill_kernel<MG, LV>), dim3(short_grid), dim3(kBlock), 0, st, vl, gt, mp,
                                ss, packed, (const WalkItem*)w.queue, (const unsigned int*)qshort, w.link, w.rcol,
@@ -1202,22 +1240,41 @@ hipError_t chains_core(LV vl, const ChainWs& w, const uint32_t* ord, uint64_t P,
         else
             hipLaunchKernelGGL((chain_walk_short_kernel<MG, LV>), dim3(short_grid), dim3(kBlock), 0, st, vl, nullptr,
                                gt, mp, ss, packed, (const WalkItem*)w.queue, (const unsigned int*)qshort, w.link,
-                               w.rcol, w.lcol, w.queue_long, qlong, order);
+                               w.rcol, w.lcol, w.queue_long, qlong, order, (DevCounters*)ctr);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (cdbg && (e = hipMemsetAsync(qcount + 4, 0, 32, st)) != hipSuccess) return e;
-        if (ev_walk) (void)hipEventRecord(ev_walk[2 * pass], st);
+        if (ev_walk) (void)hipEventRecord(ev_walk[3 * pass + 1], st);
+        const uint64_t* lorder = nullptr;
+        if (wsort_long && order) {
+            unsigned nl = 0;
+            if ((e = hipMemcpyAsync(&nl, qlong, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+            if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+            if (nl > 1) {
+                uint64_t* ra = order == w.kA ? w.kB : w.kA;   // the short walks' order is consumed
+                uint64_t* rb = order == w.kA ? w.kA : w.kB;
+                hipLaunchKernelGGL(walk_line_key_kernel, dim3(grid_of(nl)), dim3(kBlock), 0, st,
+                                   (const WalkItem*)w.queue_long, (const unsigned int*)qlong, ra);
+                if ((e = hipGetLastError()) != hipSuccess) return e;
+                if ((e = seg_bucket_starts(nullptr, 0, 0, nl, w.bst + 8, st)) != hipSuccess) return e;
+                int ob = 0;
+                if ((e = seg_onesweep_sort(ra, rb, nl, pbits, 0, w.bst + 8, d_radix_tmp, d_err, &ob, st)) !=
+                    hipSuccess)
+                    return e;
+                lorder = ob ? rb : ra;
+            }
+        }
         // the queue of chain_link / chain_left is consumed: it takes the handed-on walks
         hipLaunchKernelGGL((chain_walk_kernel<MG, LV, kWalkGroup>), dim3(walk_grid), dim3(kBlock), 0, st, vl, nullptr,
                            gt, mp, ss, ord, packed, (const WalkItem*)w.queue_long, (const unsigned int*)qlong, w.link,
                            w.rcol, w.lcol, cdbg ? qcount + 4 : nullptr, (DevCounters*)ctr, kWalkHandoff, w.queue,
-                           qcount + 2);
+                           qcount + 2, lorder);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (kWalkHandoff)
             hipLaunchKernelGGL((chain_walk_kernel<MG, LV, 64>), dim3(walk_grid), dim3(kBlock), 0, st, vl, nullptr, gt,
                                mp, ss, ord, packed, (const WalkItem*)w.queue, (const unsigned int*)(qcount + 2),
                                w.link, w.rcol, w.lcol, cdbg ? qcount + 4 : nullptr, (DevCounters*)ctr, 0u,
-                               (WalkItem*)nullptr, (unsigned int*)nullptr);
-        if (ev_walk) (void)hipEventRecord(ev_walk[2 * pass + 1], st);
+                               (WalkItem*)nullptr, (unsigned int*)nullptr, (const uint64_t*)nullptr);
+        if (ev_walk) (void)hipEventRecord(ev_walk[3 * pass + 2], st);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (cdbg) {   // development: walk queue sizes and the long walks' step histogram
             unsigned hq[9] = {};

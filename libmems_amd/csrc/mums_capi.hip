@@ -169,7 +169,7 @@ struct mums_ctx {
     bool profiling = false;
     bool walk_events = false;    // ev_walk recorded by the last FindMatches
     hipEvent_t ev_ds[16] = {};   // 2 per radix pass (<= 8 passes)
-    hipEvent_t ev_walk[4] = {};  // around the 2 chain_walk_kernel launches (chains.hip)
+    hipEvent_t ev_walk[6] = {};  // per walk pass: before the short walks, after them, after the long walks (chains.hip)
 
     // sharded seed stage: this context owns genomes [shard_first,
     // shard_first + genomes.size()) of a problem whose genome lengths are shard_len
@@ -1023,11 +1023,16 @@ void fill_stats(mums_ctx* ctx, uint64_t n) {
         s.chain_walks = ctx->hc.walk_items;
         const uint64_t row_b = ctx->rows_narrow ? 4ull * line_row_stride(ctx->gt.G) : 8ull * (ctx->gt.G + 1);
         s.chain_walk_bytes = ctx->hc.walk_wins * 28 + ctx->hc.walk_items * (row_b + 24);
+        s.short_walk_words = ctx->hc.short_words;
+        s.short_walks = ctx->hc.short_items;
+        s.short_walk_bytes = ctx->hc.short_wins * 28 + ctx->hc.short_items * (row_b + 24);
         if (ctx->walk_events && ctx->P > 0)
             for (int p = 0; p < 2; ++p) {
-                float ms = 0.f;
-                (void)hipEventElapsedTime(&ms, ctx->ev_walk[2 * p], ctx->ev_walk[2 * p + 1]);
+                float ms = 0.f, ms_s = 0.f;
+                (void)hipEventElapsedTime(&ms_s, ctx->ev_walk[3 * p], ctx->ev_walk[3 * p + 1]);
+                (void)hipEventElapsedTime(&ms, ctx->ev_walk[3 * p + 1], ctx->ev_walk[3 * p + 2]);
                 s.ms_chain_walks += ms;
+                s.ms_short_walks += ms_s;
             }
     } else {
         s.ms_total = el(EV_START, EV_BUCKETS);
@@ -1796,7 +1801,7 @@ int mums_ctx_create(int device, mums_ctx** out) {
     if (e != hipSuccess) { delete ctx; return MUMS_E_HIP; }
     ctx->own_stream = true;
     for (int i = 0; i < EV_COUNT; ++i) (void)hipEventCreate(&ctx->ev[i]);
-    for (int i = 0; i < 4; ++i) (void)hipEventCreate(&ctx->ev_walk[i]);
+    for (int i = 0; i < 6; ++i) (void)hipEventCreate(&ctx->ev_walk[i]);
     *out = ctx;
     return MUMS_OK;
 }
@@ -1821,7 +1826,7 @@ int mums_ctx_destroy(mums_ctx* ctx) {
         if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
     for (int i = 0; i < 16; ++i)
         if (ctx->ev_ds[i]) (void)hipEventDestroy(ctx->ev_ds[i]);
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 6; ++i)
         if (ctx->ev_walk[i]) (void)hipEventDestroy(ctx->ev_walk[i]);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;

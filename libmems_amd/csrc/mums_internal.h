@@ -121,6 +121,9 @@ struct DevCounters {
     unsigned long long walk_words;    // 64-column hit words evaluated by chain_walk_kernel
     unsigned long long walk_items;    // walks chain_walk_kernel finished
     unsigned long long walk_wins;     // 28-B packed windows those words loaded (present components)
+    unsigned long long short_words;   // the same for chain_walk_short_kernel (one lane per walk)
+    unsigned long long short_items;   // walks it took from the queue
+    unsigned long long short_wins;
     unsigned long long log_n;         // insertion events recorded for SetMatchLog (replay.hip)
 };
 

@@ -22,7 +22,7 @@ def test_library_exports_every_declared_symbol(gpu_lib):
     for s in syms:
         assert hasattr(lib, s), s
     assert set(syms) == set(gpu_lib.EXPORTED_SYMBOLS)
-    assert lib.mums_abi_version() == 5
+    assert lib.mums_abi_version() == 6
 
 
 def test_seed_helpers_match_oracle(gpu_lib, oracle_mod):

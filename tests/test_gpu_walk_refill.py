@@ -36,7 +36,8 @@ def test_walk_refill_matches_oracle(gpu_lib, oracle_mod, monkeypatch, case):
         for s in seqs:
             mh.AddSequence(s)
         for var in ({}, {"MUMS_DEV_WALK_REFILL": "1"}, {"MUMS_DEV_WALK_REFILL": "1", "MUMS_DEV_FIND_CHUNK": "30000"},
-                    {"MUMS_DEV_WALK_SORT": "1"}, {"MUMS_DEV_WALK_SORT": "1", "MUMS_DEV_FIND_CHUNK": "30000"}):
+                    {"MUMS_DEV_WALK_SORT": "1"}, {"MUMS_DEV_WALK_SORT": "2"},
+                    {"MUMS_DEV_WALK_SORT": "2", "MUMS_DEV_FIND_CHUNK": "30000"}):
             with monkeypatch.context() as m:
                 for k, v in var.items():
                     m.setenv(k, v)
