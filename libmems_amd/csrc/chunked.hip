@@ -126,6 +126,100 @@ __global__ __launch_bounds__(kBlock) void cr_ck_kernel(CrStream s, GenomeTable g
     });
 }
 
+// the G SortedMerLists as (genome << kbits | ckey, global index) pairs, genome-major
+// (ParallelMemHash compat: the SMLs its chunking walks, from the MemHash path's sorted stream)
+__global__ __launch_bounds__(kBlock) void cr_partition_kernel(CrStream s, GenomeTable gt,
+                                                              const uint32_t* __restrict__ gscan, uint64_t nblk,
+                                                              int kbits, uint64_t* __restrict__ sk,
+                                                              uint32_t* __restrict__ sv, uint64_t* __restrict__ ck) {
+    cr_block_ranks(s, gt, blockIdx.x, gscan, nblk, [&](uint64_t j, int g, uint64_t i) {
+        const uint64_t o = gt.base[g] + i, k = cr_key(s, j);
+        sk[o] = ((uint64_t)g << kbits) | k;
+        sv[o] = (uint32_t)cr_idx(s, j);
+        if (ck) ck[o] = k;
+    });
+}
+
+// ParallelMemHash's chunk-major stream as a stable partition of the sorted stream by chunk:
+// a record's chunk is the last chunk whose start in its genome (cs[c * G + g]) is at or
+// below its SML index.  The stream is ordered by (ckey, global index), i.e. inside a chunk by
+// ckey, then genome, then SML order -- the order of the (chunk, ckey) sort of the SMLs when
+// no equal-key run of a genome was reordered into std::sort order (the caller checks).
+// Pass 1 counts (chunk, block) records, chunk-major (cnt[c * (nblk + 1) + b]); after an
+// exclusive scan pass 2 writes key2 = chunk << kbits | ckey and the index at the scanned
+// offset plus the record's stable rank inside its block.
+constexpr uint32_t kCpChunks = 2048;   // chunks of the LDS form (more: the caller's radix sort)
+
+__device__ __forceinline__ uint32_t compat_chunk_at(const uint64_t* __restrict__ cs, uint32_t nch, int G, int g,
+                                                    uint64_t i) {
+    uint32_t lo = 0, n = nch;   // chunks whose start is <= i
+    while (n > 0) {
+        const uint32_t h = n >> 1;
+        if (cs[(uint64_t)(lo + h) * G + g] <= i) { lo += h + 1; n -= h + 1; } else n = h;
+    }
+    return lo ? lo - 1 : 0;
+}
+
+template <bool kWrite>
+__global__ __launch_bounds__(kBlock) void cr_chunk_part_kernel(CrStream s, GenomeTable gt,
+                                                               const uint32_t* __restrict__ gscan, uint64_t nblk,
+                                                               const uint64_t* __restrict__ cs, uint32_t nch, int kbits,
+                                                               uint32_t* __restrict__ cnt, uint64_t* __restrict__ key2,
+                                                               uint32_t* __restrict__ idx) {
+    __shared__ uint32_t gbase[kMaxG];
+    __shared__ uint32_t gw[kBlock / 64][kMaxG];
+    __shared__ uint32_t cbase[kCpChunks];
+    __shared__ uint32_t cw[kBlock / 64][kCpChunks];   // stamp << 16 | count (no per-round zeroing)
+    const uint64_t b = blockIdx.x;
+    const int tid = threadIdx.x, wv = tid >> 6, G = gt.G;
+    if (tid < G) gbase[tid] = gscan[(uint64_t)tid * (nblk + 1) + b];
+    for (uint32_t c = tid; c < nch; c += kBlock) {
+        cbase[c] = kWrite ? cnt[(uint64_t)c * (nblk + 1) + b] : 0u;
+        for (int w = 0; w < kBlock / 64; ++w) cw[w][c] = 0;
+    }
+    uint32_t stamp = 0;
+    for (uint32_t r0 = 0; r0 < kCrBlk; r0 += kBlock) {
+        ++stamp;
+        for (int i = tid; i < (kBlock / 64) * kMaxG; i += kBlock) (&gw[0][0])[i] = 0;
+        __syncthreads();
+        const uint64_t j = b * kCrBlk + r0 + tid;
+        const bool valid = j < s.N;
+        const uint32_t g = valid ? (uint32_t)genome_of(gt, cr_idx(s, j)) : 0u;
+        uint32_t gtot;
+        const uint32_t grk = wave_match_rank<6>(g, valid, &gtot);
+        if (valid && grk == 0) gw[wv][g] = gtot;
+        __syncthreads();
+        uint32_t c = 0;
+        if (valid) {
+            uint32_t o = gbase[g] + grk;
+            for (int w = 0; w < wv; ++w) o += gw[w][g];
+            c = compat_chunk_at(cs, nch, G, (int)g, o);
+        }
+        uint32_t ctot;
+        const uint32_t crk = wave_match_rank<11>(c, valid, &ctot);
+        if (valid && crk == 0) {
+            if (kWrite) cw[wv][c] = (stamp << 16) | ctot;
+            else atomicAdd(&cbase[c], ctot);
+        }
+        __syncthreads();
+        if (kWrite && valid) {
+            uint32_t d = cbase[c] + crk;
+            for (int w = 0; w < wv; ++w) {
+                const uint32_t x = cw[w][c];
+                d += (x >> 16) == (stamp & 0xFFFFu) ? (x & 0xFFFFu) : 0u;
+            }
+            key2[d] = ((uint64_t)c << kbits) | cr_key(s, j);
+            idx[d] = (uint32_t)cr_idx(s, j);
+        }
+        __syncthreads();
+        if (valid && grk == 0) atomicAdd(&gbase[g], gtot);
+        if (kWrite && valid && crk == 0) atomicAdd(&cbase[c], ctot);
+        __syncthreads();
+    }
+    if (!kWrite)
+        for (uint32_t c = tid; c < nch; c += kBlock) cnt[(uint64_t)c * (nblk + 1) + b] = cbase[c];
+}
+
 // masked keys with more than MER_REPEAT_LIMIT records: such a run holds a multiple of 1000,
 // so only those positions look for their run's bounds (galloping) -- the first multiple
 // of 1000 inside the run reports its key
@@ -404,6 +498,39 @@ hipError_t launch_cr_counts(const CrStream& s, const GenomeTable& gt, uint32_t* 
         if ((e = exclusive_scan_u32(gcnt + (uint64_t)g * (nblk + 1), nblk + 1, d_scan_tmp, nullptr, st)) != hipSuccess)
             return e;
     return hipSuccess;
+}
+
+hipError_t launch_cr_partition(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, int kbits, uint64_t* sk,
+                               uint32_t* sv, uint64_t* ck, hipStream_t st) {
+    const uint64_t nblk = cr_blocks(s.N);
+    if (nblk == 0) return hipSuccess;
+    hipLaunchKernelGGL(cr_partition_kernel, dim3((unsigned)nblk), dim3(kBlock), 0, st, s, gt, gscan, nblk, kbits, sk,
+                       sv, ck);
+    return hipGetLastError();
+}
+
+size_t cr_chunk_part_cnt_words(uint64_t N, uint32_t nch) { return (size_t)nch * (cr_blocks(N) + 1); }
+
+bool cr_chunk_part_fits(uint64_t N, uint32_t nch) {
+    return nch <= kCpChunks && cr_chunk_part_cnt_words(N, nch) < (1ull << 31);
+}
+
+hipError_t launch_cr_chunk_part(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, const uint64_t* cs,
+                                uint32_t nch, int kbits, uint32_t* cnt, void* d_scan_tmp, uint64_t* key2, uint32_t* idx,
+                                hipStream_t st) {
+    const uint64_t nblk = cr_blocks(s.N);
+    if (nblk == 0) return hipSuccess;
+    if (!cr_chunk_part_fits(s.N, nch)) return hipErrorInvalidValue;
+    const size_t words = cr_chunk_part_cnt_words(s.N, nch);
+    hipError_t e = hipMemsetAsync(cnt, 0, words * 4, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(cr_chunk_part_kernel<false>, dim3((unsigned)nblk), dim3(kBlock), 0, st, s, gt, gscan, nblk, cs,
+                       nch, kbits, cnt, (uint64_t*)nullptr, (uint32_t*)nullptr);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = exclusive_scan_u32(cnt, words, d_scan_tmp, nullptr, st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(cr_chunk_part_kernel<true>, dim3((unsigned)nblk), dim3(kBlock), 0, st, s, gt, gscan, nblk, cs,
+                       nch, kbits, cnt, key2, idx);
+    return hipGetLastError();
 }
 
 hipError_t launch_cr_ck(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, uint64_t* ck, hipStream_t st,

@@ -1592,18 +1592,62 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
     HIPCHK(hipEventRecord(ctx->ev[EV_START], st));
     HIPCHK(hipMemsetAsync(dc, 0, sizeof(DevCounters), st));
     HIPCHK(hipMemsetAsync(cs, 0, (size_t)cap * G * 8, st));
-    std::vector<const char*> ptrs(G);
-    for (int g = 0; g < G; ++g) ptrs[g] = ctx->genomes[g].d_ptr;
-    HIPCHK(launch_seed_pack(ctx->ss, gt, ptrs.data(), ctx->packed.as<uint32_t>(), 0, true, ctx->ckey.p, 0, nullptr, T,
-                            &dc->err, st));
-    HIPCHK(launch_genome_keys(ctx->ckey.as<uint64_t>(), N, gt, kbits, st));
-    HIPCHK(hipEventRecord(ctx->ev[EV_KEYS], st));
     int buf = 0;
-    HIPCHK(radix_sort<uint64_t>(ctx->ckey.as<uint64_t>(), nullptr, N, kbits + gbits, ctx->kA.as<uint64_t>(),
-                                ctx->vA.as<uint32_t>(), ctx->kB.as<uint64_t>(), ctx->vB.as<uint32_t>(), ctx->tmp.p,
-                                &buf, st));
-    const uint64_t* sk = buf ? ctx->kB.as<uint64_t>() : ctx->kA.as<uint64_t>();
-    const uint32_t* sv = buf ? ctx->vB.as<uint32_t>() : ctx->vA.as<uint32_t>();
+    const uint64_t* sk = nullptr;
+    const uint32_t* sv = nullptr;
+    // the G SortedMerLists, genome-major: from the MemHash path's packed records (scatter into
+    // 2^B MSD buckets + onesweep passes, then a stable partition by genome) where they fit,
+    // else one 64-bit (genome, ckey) radix sort.  MUMS_DEV_COMPAT_RADIX (read per call): the
+    // radix sort always.
+    const int B = std::max(0, kbits - 32);
+    const bool packed_sml = B <= 7 && N > 0 && N < (1ull << 30) && !getenv("MUMS_DEV_COMPAT_RADIX");
+    DevBuf dst;            // the sorted stream's bucket starts (packed_sml)
+    CrStream pstream{};    // the sorted stream (packed_sml): also the source of the chunk-major order
+    HIPCHK(ctx->crall.ensure(N * 8 + 64));
+    if (packed_sml) {
+        HIPCHK(ctx->hist.ensure(((uint64_t)T << B) * 4 + 64));
+        HIPCHK(ctx->recA.ensure(N * 8 + 64));
+        HIPCHK(ctx->recB.ensure(N * 8 + 64));
+        HIPCHK(ctx->mstart.ensure(((1ull << B) + 64) * 4));
+        const uint64_t nblk = cr_blocks(N);
+        HIPCHK(ctx->tmp.ensure(std::max({ctx->tmp.cap, onesweep_tmp_bytes(N, B, kbits - B),
+                                         scan_tmp_bytes((uint64_t)T << B), scan_tmp_bytes(nblk + 2)})));
+        HIPCHK(ctx->crcnt.ensure((uint64_t)G * (nblk + 1) * 4 + 256));
+        int rc0 = keys_stage(ctx, gt, T, B, N, ctx->recA.as<uint64_t>(), ctx->mstart.as<uint32_t>(), st);
+        if (rc0) return rc0;
+        HIPCHK(hipEventRecord(ctx->ev[EV_KEYS], st));
+        int ob = 0;
+        HIPCHK(seg_onesweep_sort(ctx->recA.as<uint64_t>(), ctx->recB.as<uint64_t>(), N, kbits - B, B,
+                                 ctx->mstart.as<uint32_t>(), ctx->tmp.p, &dc->err, &ob, st));
+        const uint64_t nd = 1ull << B;
+        std::vector<uint32_t> h32(nd + 1);
+        HIPCHK(hipMemcpyAsync(h32.data(), ctx->mstart.p, (nd + 1) * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        std::vector<uint64_t> h64(nd + 1);
+        for (uint64_t d = 0; d <= nd; ++d) h64[d] = B ? h32[d] : (d ? N : 0);
+        HIPCHK(dst.ensure((nd + 1) * 8 + 64));
+        HIPCHK(hipMemcpyAsync(dst.p, h64.data(), (nd + 1) * 8, hipMemcpyHostToDevice, st));
+        pstream = CrStream{ob ? ctx->recB.as<uint64_t>() : ctx->recA.as<uint64_t>(), dst.as<uint64_t>(), (uint32_t)nd, N};
+        pstream.kb = (uint32_t)(kbits - B);
+        pstream.ib = 32;
+        HIPCHK(launch_cr_counts(pstream, gt, ctx->crcnt.as<uint32_t>(), ctx->tmp.p, st));
+        HIPCHK(launch_cr_partition(pstream, gt, ctx->crcnt.as<uint32_t>(), kbits, ctx->kA.as<uint64_t>(),
+                                   ctx->vA.as<uint32_t>(), ctx->crall.as<uint64_t>(), st));
+        sk = ctx->kA.as<uint64_t>();
+        sv = ctx->vA.as<uint32_t>();
+    } else {
+        std::vector<const char*> ptrs(G);
+        for (int g = 0; g < G; ++g) ptrs[g] = ctx->genomes[g].d_ptr;
+        HIPCHK(launch_seed_pack(ctx->ss, gt, ptrs.data(), ctx->packed.as<uint32_t>(), 0, true, ctx->ckey.p, 0, nullptr,
+                                T, &dc->err, st));
+        HIPCHK(launch_genome_keys(ctx->ckey.as<uint64_t>(), N, gt, kbits, st));
+        HIPCHK(hipEventRecord(ctx->ev[EV_KEYS], st));
+        HIPCHK(radix_sort<uint64_t>(ctx->ckey.as<uint64_t>(), nullptr, N, kbits + gbits, ctx->kA.as<uint64_t>(),
+                                    ctx->vA.as<uint32_t>(), ctx->kB.as<uint64_t>(), ctx->vB.as<uint32_t>(), ctx->tmp.p,
+                                    &buf, st));
+        sk = buf ? ctx->kB.as<uint64_t>() : ctx->kA.as<uint64_t>();
+        sv = buf ? ctx->vB.as<uint32_t>() : ctx->vA.as<uint32_t>();
+    }
     uint32_t nch = 1;
     std::vector<uint64_t> hcs((size_t)G, 0);   // chunk starts (nch x G)
     if (mx >= 0) {
@@ -1631,6 +1675,7 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
                                                          "(overlapping chunk ranges) not reproduced");
     }
     ctx->nchunks = nch;
+    bool reordered = false;   // an equal-key run of a genome moved into std::sort order
     if (N) {   // SML order of the runs the chunk starts fall into (all runs under repeat tolerance)
         const uint64_t* sps[1] = {cs};
         const uint64_t rws[1] = {nch};
@@ -1641,19 +1686,29 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
                        &flagged, st);
         if (rc) return rc;
         if (flagged) HIPCHK(tie_slots_out(tw, const_cast<uint32_t*>(sv), st));
+        reordered = flagged != 0;
         ctx->ties_fixed = all;
     }
     int cbits = 0;
     while (((uint64_t)1 << cbits) < (uint64_t)nch) ++cbits;
     if (kbits + cbits > 64) return fail(ctx, MUMS_E_UNSUPPORTED, "ParallelMemHash compat: too many chunks");
-    // the genome-major SMLs' keys (genome bits off) survive the second sort for the
-    // MER_REPEAT_LIMIT plan below
-    HIPCHK(ctx->crall.ensure(N * 8 + 64));
-    HIPCHK(launch_compat_chunk_keys(sk, sv, N, gt, kbits, cs, nch, ctx->ckey.as<uint64_t>(), ctx->cval.as<uint32_t>(),
-                                    ctx->crall.as<uint64_t>(), st));
-    HIPCHK(radix_sort<uint64_t>(ctx->ckey.as<uint64_t>(), ctx->cval.as<uint32_t>(), N, kbits + cbits,
-                                ctx->kA.as<uint64_t>(), ctx->vA.as<uint32_t>(), ctx->kB.as<uint64_t>(),
-                                ctx->vB.as<uint32_t>(), ctx->tmp.p, &buf, st));
+    // the chunk-major stream: from the sorted stream by a stable partition by chunk when its
+    // order inside equal keys is the SMLs' (no run reordered), else a (chunk, ckey) radix sort
+    // of the SMLs.  The genome-major SMLs' keys (genome bits off, ctx->crall) survive for the
+    // MER_REPEAT_LIMIT plan below.
+    if (packed_sml && !reordered && cr_chunk_part_fits(N, nch)) {
+        HIPCHK(ctx->ckey.ensure(cr_chunk_part_cnt_words(N, nch) * 4 + 64));   // the (chunk, block) counts
+        HIPCHK(ctx->tmp.ensure(std::max(ctx->tmp.cap, scan_tmp_bytes(cr_chunk_part_cnt_words(N, nch)))));
+        HIPCHK(launch_cr_chunk_part(pstream, gt, ctx->crcnt.as<uint32_t>(), cs, nch, kbits, ctx->ckey.as<uint32_t>(),
+                                    ctx->tmp.p, ctx->kB.as<uint64_t>(), ctx->vB.as<uint32_t>(), st));
+        buf = 1;
+    } else {
+        HIPCHK(launch_compat_chunk_keys(sk, sv, N, gt, kbits, cs, nch, ctx->ckey.as<uint64_t>(),
+                                        ctx->cval.as<uint32_t>(), ctx->crall.as<uint64_t>(), st));
+        HIPCHK(radix_sort<uint64_t>(ctx->ckey.as<uint64_t>(), ctx->cval.as<uint32_t>(), N, kbits + cbits,
+                                    ctx->kA.as<uint64_t>(), ctx->vA.as<uint32_t>(), ctx->kB.as<uint64_t>(),
+                                    ctx->vB.as<uint32_t>(), ctx->tmp.p, &buf, st));
+    }
     ctx->sorted_buf = buf;
     ctx->sorted_key = buf ? ctx->kB.p : ctx->kA.p;
     ctx->sorted_idx = buf ? ctx->vB.as<uint32_t>() : ctx->vA.as<uint32_t>();

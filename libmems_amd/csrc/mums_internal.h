@@ -494,6 +494,17 @@ struct CrStream {
 uint64_t cr_blocks(uint64_t N);
 // gcnt: G x (cr_blocks(N) + 1) per-genome block counts, exclusive-scanned per genome
 hipError_t launch_cr_counts(const CrStream& s, const GenomeTable& gt, uint32_t* gcnt, void* d_scan_tmp, hipStream_t st);
+// the SMLs as (genome << kbits | ckey, index) pairs at gt.base[g] + SML index (compat.hip's input)
+hipError_t launch_cr_partition(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, int kbits, uint64_t* sk,
+                               uint32_t* sv, uint64_t* ck, hipStream_t st);
+// ParallelMemHash's chunk-major stream (key2 = chunk << kbits | ckey, index) as a stable
+// partition of the sorted stream by chunk (cs: nch x G chunk starts); cnt: cr_chunk_part_cnt_words
+// u32 scratch; only when cr_chunk_part_fits
+size_t cr_chunk_part_cnt_words(uint64_t N, uint32_t nch);
+bool cr_chunk_part_fits(uint64_t N, uint32_t nch);
+hipError_t launch_cr_chunk_part(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, const uint64_t* cs,
+                                uint32_t nch, int kbits, uint32_t* cnt, void* d_scan_tmp, uint64_t* key2, uint32_t* idx,
+                                hipStream_t st);
 hipError_t launch_cr_ck(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, uint64_t* ck, hipStream_t st,
                         const uint64_t* lbase = nullptr);
 // masked key of genome g's SML index e for every query g << 56 | e (gscan from launch_cr_counts)

@@ -135,3 +135,27 @@ def test_parallel_merge_exact_pass_everywhere(gpu_lib, oracle_mod, monkeypatch, 
             continue
         assert len(ml) == len(lengths), exact
         assert (ml.lengths == lengths).all() and (ml.starts == starts).all(), exact
+
+
+@pytest.mark.parametrize("idx", [0, 3, 4, 7])
+def test_parallel_sml_builds_agree(gpu_lib, oracle_mod, monkeypatch, idx):
+    """The compat SMLs from the MemHash path's packed onesweep stream (default for 2w+1 <= 39)
+    and from the 64-bit (genome, ckey) radix sort (MUMS_DEV_COMPAT_RADIX, wider seeds) give
+    the oracle's list, progress text and match log."""
+    G, n, p, w, chunk, gseed = COMPAT_SMALL[idx]
+    seqs = oracle_mod.generate(G, n, p, gseed)
+    seed = oracle_mod.get_seed(w)
+    lengths, starts, ost = oracle_mod.find_matches(seqs, seed, parallel_compat=True, chunk_size=chunk)
+    for radix in (False, True):
+        with monkeypatch.context() as m:
+            if radix:
+                m.setenv("MUMS_DEV_COMPAT_RADIX", "1")
+            with gpu_lib.ParallelMemHash(0, chunk) as mh:
+                mh.SetSeed(seed)
+                mh.LogProgress(True)
+                ml = mh.FindMatches(seqs)
+                text = mh.ProgressLog()
+                st = mh.stats()
+        assert st["chunks"] == ost["chunks"], radix
+        assert len(ml) == len(lengths) and (ml.lengths == lengths).all() and (ml.starts == starts).all(), radix
+        assert text == ost["progress"], radix
