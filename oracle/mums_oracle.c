@@ -1001,7 +1001,17 @@ static int parallel_compat_search(memhash_t* h, const oracle_params* prm, int G,
     bucket_t* gb = (bucket_t*)calloc(T, sizeof(bucket_t));   /* global table G */
     uint64_t* lo = (uint64_t*)malloc((size_t)G * sizeof(uint64_t));
     uint64_t* hi = (uint64_t*)malloc((size_t)G * sizeof(uint64_t));
+    /* parallel_compat >= 16: R = parallel_compat - 16 ranks, each searching a contiguous chunk
+       range into tables of its own (thread table and G start empty, never synced), their G
+       tables re-added rank after rank into one at the end (a model of chunk-parallel GPUs) */
+    const uint64_t R = prm->parallel_compat >= 16 ? (uint64_t)(prm->parallel_compat - 16) : 1;
+    bucket_t* gf = R > 1 ? (bucket_t*)calloc(T, sizeof(bucket_t)) : NULL;
+    uint64_t rank = 0;
     for (uint64_t i = 0; i < nch; ++i) {
+        if (gf && i == nch * rank / R) {   /* a new rank's range: fresh tables */
+            for (uint32_t bI = 0; bI < T; ++bI) { h->buckets[bI].n = 0; gb[bI].n = 0; }
+            ++rank;
+        }
         for (int g = 0; g < G; ++g) {
             lo[g] = cs[i * G + g];
             /* chunk_lens = next start - start (gnSeqI, wraps) or GNSEQI_END (:91-96) */
@@ -1023,6 +1033,23 @@ static int parallel_compat_search(memhash_t* h, const oracle_params* prm, int G,
             if (gb[bI].n) memcpy(tb->v, gb[bI].v, gb[bI].n * sizeof(uint32_t));
             tb->n = gb[bI].n;
         }
+        if (gf && (i + 1 == nch || i + 1 == nch * rank / R))   /* the rank's G into the final table */
+            for (uint32_t bI = 0; bI < T; ++bI)
+                for (uint32_t k = 0; k < gb[bI].n; ++k) merge_entry(h, &gf[bI], gb[bI].v[k], res);
+    }
+    if (gf) {
+        for (uint32_t bI = 0; bI < T; ++bI) {
+            free(gb[bI].v);
+            bucket_t* tb = &h->buckets[bI];
+            if (tb->cap < gf[bI].n) {
+                tb->cap = gf[bI].n;
+                tb->v = (uint32_t*)realloc(tb->v, tb->cap * sizeof(uint32_t));
+            }
+            if (gf[bI].n) memcpy(tb->v, gf[bI].v, gf[bI].n * sizeof(uint32_t));
+            tb->n = gf[bI].n;
+        }
+        free(gb);
+        gb = gf;
     }
     uint64_t entries = 0;
     for (uint32_t bI = 0; bI < T; ++bI) { entries += gb[bI].n; free(gb[bI].v); }

@@ -34,3 +34,19 @@ def test_many_chunks_log_covers_the_list(oracle_mod):
     # the text counts every chunk's buffers: the percentages only grow, one line per ten
     pct = [int(t) for t in xc["progress"].replace("\n", "").split("%..") if t]
     assert pct == sorted(pct) and pct[0] == 0
+
+
+@pytest.mark.parametrize("G,n,p,w,chunk,gseed,ranks", [(3, 300_000, 0.03, 15, 3000, 2, 3), (4, 200_000, 0.01, 15, 2000, 3, 8),
+                                                       (3, 200_000, 1.0, 11, 1003, 6, 4), (5, 300_000, 0.02, 17, 4000, 9, 2)])
+def test_chunk_range_ranks_model(oracle_mod, G, n, p, w, chunk, gseed, ranks):
+    """The oracle's model of chunk-parallel ranks (parallel_compat = 16 + ranks: each rank
+    searches a contiguous chunk range into tables of its own, never synced, and the ranks'
+    global tables are re-added rank after rank at the end) gives the one-thread reference's
+    MatchList -- the schedule independence SURVEY.md §8 row A13 reports for 1/4/8 OpenMP
+    threads, the basis of a multi-GPU compat mode."""
+    seqs = oracle_mod.generate(G, n, p, gseed)
+    seed = oracle_mod.get_seed(w)
+    l1, s1, x1 = oracle_mod.find_matches(seqs, seed, parallel_compat=True, chunk_size=chunk)
+    lr, sr, xr = oracle_mod.find_matches(seqs, seed, parallel_compat=16 + ranks, chunk_size=chunk)
+    assert x1["chunks"] == xr["chunks"] > ranks
+    assert np.array_equal(l1, lr) and np.array_equal(s1, sr)
