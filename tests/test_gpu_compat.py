@@ -159,3 +159,15 @@ def test_parallel_sml_builds_agree(gpu_lib, oracle_mod, monkeypatch, idx):
         assert st["chunks"] == ost["chunks"], radix
         assert len(ml) == len(lengths) and (ml.lengths == lengths).all() and (ml.starts == starts).all(), radix
         assert text == ost["progress"], radix
+
+
+@pytest.mark.parametrize("n,chunk", [(300_000, 150), (320_000, 140)])
+def test_parallel_many_chunks(gpu_lib, oracle_mod, n, chunk):
+    """2000 chunks (the chunk partition's LDS counters hold up to 2048) and 2286 (past them:
+    the (chunk, ckey) radix sort) give the oracle's list."""
+    seqs = oracle_mod.generate(3, n, 0.02, 41)
+    seed = oracle_mod.get_seed(15)
+    lengths, starts, ost = oracle_mod.find_matches(seqs, seed, parallel_compat=True, chunk_size=chunk)
+    ml, st = gpu_parallel(gpu_lib, seqs, seed, chunk)
+    assert st["chunks"] == ost["chunks"] > 1500
+    assert len(ml) == len(lengths) and (ml.lengths == lengths).all() and (ml.starts == starts).all()
