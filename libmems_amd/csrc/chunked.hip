@@ -67,6 +67,40 @@ __device__ __forceinline__ uint64_t cr_key(const CrStream& s, uint64_t j) {
 
 __device__ __forceinline__ uint64_t cr_idx(const CrStream& s, uint64_t j) { return s.rec[j] & ((1ull << s.ib) - 1); }
 
+// digit (MSD bucket) of stream position j
+__device__ __forceinline__ uint32_t cr_digit(const CrStream& s, uint64_t j) {
+    uint32_t lo = 0, n = s.nd;
+    while (n > 0) {
+        const uint32_t h = n >> 1;
+        if (s.dstart[lo + h + 1] <= j) { lo += h + 1; n -= h + 1; } else n = h;
+    }
+    return lo;
+}
+
+// cr_key for a position of a block whose first and last records have digits d0 <= d1: no
+// search when they agree (nearly every block: 128 digits over 2e5 blocks at config 3)
+__device__ __forceinline__ uint64_t cr_key_in(const CrStream& s, uint64_t j, uint32_t d0, uint32_t d1) {
+    uint32_t d = d0;
+    if (d1 != d0) {
+        uint32_t lo = d0, n = d1 - d0;   // digits in [d0, d1] whose end <= j
+        while (n > 0) {
+            const uint32_t h = n >> 1;
+            if (s.dstart[lo + h + 1] <= j) { lo += h + 1; n -= h + 1; } else n = h;
+        }
+        d = lo;
+    }
+    return ((uint64_t)d << s.kb) | ((s.rec[j] >> s.ib) & ((1ull << s.kb) - 1));
+}
+
+// the digits of block b's first and last records into LDS (thread 0; callers barrier first)
+__device__ __forceinline__ void cr_block_digits(const CrStream& s, uint64_t b, uint32_t* sd) {
+    if (threadIdx.x == 0) {
+        const uint64_t j0 = b * kCrBlk, j1 = (s.N < j0 + kCrBlk ? s.N : j0 + kCrBlk) - 1;
+        sd[0] = cr_digit(s, j0);
+        sd[1] = cr_digit(s, j1);
+    }
+}
+
 // per-block genome counts: gcnt[g * (nblk + 1) + b]
 __global__ __launch_bounds__(kBlock) void cr_count_kernel(CrStream s, GenomeTable gt, uint64_t nblk,
                                                           uint32_t* __restrict__ gcnt) {
@@ -132,8 +166,10 @@ __global__ __launch_bounds__(kBlock) void cr_partition_kernel(CrStream s, Genome
                                                               const uint32_t* __restrict__ gscan, uint64_t nblk,
                                                               int kbits, uint64_t* __restrict__ sk,
                                                               uint32_t* __restrict__ sv, uint64_t* __restrict__ ck) {
+    __shared__ uint32_t sd[2];
+    cr_block_digits(s, blockIdx.x, sd);   // (cr_block_ranks barriers before its first callback)
     cr_block_ranks(s, gt, blockIdx.x, gscan, nblk, [&](uint64_t j, int g, uint64_t i) {
-        const uint64_t o = gt.base[g] + i, k = cr_key(s, j);
+        const uint64_t o = gt.base[g] + i, k = cr_key_in(s, j, sd[0], sd[1]);
         sk[o] = ((uint64_t)g << kbits) | k;
         sv[o] = (uint32_t)cr_idx(s, j);
         if (ck) ck[o] = k;
@@ -160,6 +196,29 @@ __device__ __forceinline__ uint32_t compat_chunk_at(const uint64_t* __restrict__
     return lo ? lo - 1 : 0;
 }
 
+// (chunk, block) counts without reading the records: block b holds genome g's SML indices
+// [gscan[g][b], gscan[g][b + 1]), chunk c takes [cs[c][g], cs[c + 1][g]) of them
+__global__ __launch_bounds__(kBlock) void cr_chunk_count_kernel(GenomeTable gt, const uint32_t* __restrict__ gscan,
+                                                                uint64_t nblk, const uint64_t* __restrict__ cs,
+                                                                uint32_t nch, uint32_t* __restrict__ cnt) {
+    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int G = gt.G;
+    const uint64_t b = t / G;
+    const int g = (int)(t % G);
+    if (b >= nblk) return;
+    uint64_t lo = gscan[(uint64_t)g * (nblk + 1) + b];
+    const uint64_t hi = gscan[(uint64_t)g * (nblk + 1) + b + 1];
+    if (lo >= hi) return;
+    uint32_t c = compat_chunk_at(cs, nch, G, g, lo);
+    while (lo < hi) {
+        const uint64_t ce = c + 1 < nch ? cs[(uint64_t)(c + 1) * G + g] : ~0ull;
+        const uint64_t e = ce < hi ? ce : hi;
+        if (e > lo) atomicAdd(&cnt[(uint64_t)c * (nblk + 1) + b], (uint32_t)(e - lo));
+        lo = e > lo ? e : lo;
+        ++c;
+    }
+}
+
 template <bool kWrite>
 __global__ __launch_bounds__(kBlock) void cr_chunk_part_kernel(CrStream s, GenomeTable gt,
                                                                const uint32_t* __restrict__ gscan, uint64_t nblk,
@@ -170,8 +229,36 @@ __global__ __launch_bounds__(kBlock) void cr_chunk_part_kernel(CrStream s, Genom
     __shared__ uint32_t gw[kBlock / 64][kMaxG];
     __shared__ uint32_t cbase[kCpChunks];
     __shared__ uint32_t cw[kBlock / 64][kCpChunks];   // stamp << 16 | count (no per-round zeroing)
+    __shared__ uint32_t sd[2], s_cmin, s_cmax;
     const uint64_t b = blockIdx.x;
     const int tid = threadIdx.x, wv = tid >> 6, G = gt.G;
+    if (kWrite) {   // one chunk for the whole block (the common case): its records keep their order
+        if (tid == 0) {
+            s_cmin = 0xFFFFFFFFu;
+            s_cmax = 0;
+        }
+        cr_block_digits(s, b, sd);
+        __syncthreads();
+        if (tid < G) {
+            const uint64_t lo = gscan[(uint64_t)tid * (nblk + 1) + b], hi = gscan[(uint64_t)tid * (nblk + 1) + b + 1];
+            if (lo < hi) {
+                atomicMin(&s_cmin, compat_chunk_at(cs, nch, G, tid, lo));
+                atomicMax(&s_cmax, compat_chunk_at(cs, nch, G, tid, hi - 1));
+            }
+        }
+        __syncthreads();
+        if (s_cmin == s_cmax) {
+            const uint32_t c = s_cmin;
+            const uint64_t base = cnt[(uint64_t)c * (nblk + 1) + b], j0 = b * kCrBlk;
+            for (uint32_t r = tid; r < kCrBlk; r += kBlock) {
+                const uint64_t j = j0 + r;
+                if (j >= s.N) break;
+                key2[base + r] = ((uint64_t)c << kbits) | cr_key_in(s, j, sd[0], sd[1]);
+                idx[base + r] = (uint32_t)cr_idx(s, j);
+            }
+            return;
+        }
+    }
     if (tid < G) gbase[tid] = gscan[(uint64_t)tid * (nblk + 1) + b];
     for (uint32_t c = tid; c < nch; c += kBlock) {
         cbase[c] = kWrite ? cnt[(uint64_t)c * (nblk + 1) + b] : 0u;
@@ -208,7 +295,7 @@ __global__ __launch_bounds__(kBlock) void cr_chunk_part_kernel(CrStream s, Genom
                 const uint32_t x = cw[w][c];
                 d += (x >> 16) == (stamp & 0xFFFFu) ? (x & 0xFFFFu) : 0u;
             }
-            key2[d] = ((uint64_t)c << kbits) | cr_key(s, j);
+            key2[d] = ((uint64_t)c << kbits) | cr_key_in(s, j, sd[0], sd[1]);
             idx[d] = (uint32_t)cr_idx(s, j);
         }
         __syncthreads();
@@ -524,8 +611,9 @@ hipError_t launch_cr_chunk_part(const CrStream& s, const GenomeTable& gt, const 
     const size_t words = cr_chunk_part_cnt_words(s.N, nch);
     hipError_t e = hipMemsetAsync(cnt, 0, words * 4, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(cr_chunk_part_kernel<false>, dim3((unsigned)nblk), dim3(kBlock), 0, st, s, gt, gscan, nblk, cs,
-                       nch, kbits, cnt, (uint64_t*)nullptr, (uint32_t*)nullptr);
+    const uint64_t pairs = nblk * (uint64_t)gt.G;
+    hipLaunchKernelGGL(cr_chunk_count_kernel, dim3((unsigned)((pairs + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, gt,
+                       gscan, nblk, cs, nch, cnt);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = exclusive_scan_u32(cnt, words, d_scan_tmp, nullptr, st)) != hipSuccess) return e;
     hipLaunchKernelGGL(cr_chunk_part_kernel<true>, dim3((unsigned)nblk), dim3(kBlock), 0, st, s, gt, gscan, nblk, cs,

@@ -373,6 +373,22 @@ __global__ __launch_bounds__(kBlk) void compat_merge_fix_kernel(uint32_t* __rest
     }
 }
 
+// Does a chunk start split a run of equal keys of its genome (sk: the genome-major SMLs)?
+// Only such runs' SML order is observable by the chunked search under the default
+// tolerances (which side of the start a copy falls on); without any, the tie replay is skipped.
+__global__ void compat_split_kernel(const uint64_t* __restrict__ sk, GenomeTable gt, const uint64_t* __restrict__ cs,
+                                    uint32_t nch, uint32_t* __restrict__ out) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int G = gt.G;
+    const uint64_t c = t / G;
+    const int g = (int)(t % G);
+    if (c >= nch) return;
+    const uint64_t p = cs[c * G + g];
+    if (p == 0 || p >= gt.m[g]) return;
+    const uint64_t* k = sk + gt.base[g];
+    if (k[p - 1] == k[p]) atomicOr(out, 1u);
+}
+
 // SetMatchLog in compat mode: the chunk of every probe is nondecreasing in AddHashEntry call
 // order (the chunk-major stream), so the chunks are ranges of probes: pfirst[c] = first probe
 // of chunk c (nch + 1 entries, pfirst[nch] = P).  probe_info low word = the group's first
@@ -390,6 +406,15 @@ __global__ void compat_probe_chunk_kernel(const uint64_t* __restrict__ probe_inf
 }
 
 }  // namespace
+
+hipError_t launch_compat_split(const uint64_t* sk, const GenomeTable& gt, const uint64_t* cs, uint32_t nch,
+                               uint32_t* out, hipStream_t st) {
+    hipError_t e = hipMemsetAsync(out, 0, 4, st);
+    if (e != hipSuccess) return e;
+    const uint64_t n = (uint64_t)nch * gt.G;
+    hipLaunchKernelGGL(compat_split_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, sk, gt, cs, nch, out);
+    return hipGetLastError();
+}
 
 hipError_t launch_compat_probe_chunks(const uint64_t* probe_info, uint64_t P, const uint64_t* key2, int kbits,
                                       uint32_t nch, uint32_t* pfirst, hipStream_t st) {

@@ -1682,9 +1682,19 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
         TieWs tw{};
         uint64_t flagged = 0;
         const bool all = wants_tie_order(ctx);
-        rc = tie_order(ctx, N, sk, sk, nullptr, sv, all ? nullptr : sps, all ? nullptr : rws, all ? 0 : 1, &tw,
-                       &flagged, st);
-        if (rc) return rc;
+        bool split = true;   // a chunk start inside a run of equal keys: its SML order matters
+        if (!all) {
+            HIPCHK(launch_compat_split(sk, gt, cs, nch, &dc->scratch32, st));
+            uint32_t h = 0;
+            HIPCHK(hipMemcpyAsync(&h, &dc->scratch32, 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            split = h != 0;
+        }
+        if (split) {
+            rc = tie_order(ctx, N, sk, sk, nullptr, sv, all ? nullptr : sps, all ? nullptr : rws, all ? 0 : 1, &tw,
+                           &flagged, st);
+            if (rc) return rc;
+        }
         if (flagged) HIPCHK(tie_slots_out(tw, const_cast<uint32_t*>(sv), st));
         reordered = flagged != 0;
         ctx->ties_fixed = all;

@@ -117,7 +117,7 @@ struct DevCounters {
     uint32_t ngroups;                 // distinct masked keys (scan total of per-tile counts)
     uint32_t nchains;                 // seed chains among the probes (chains.hip)
     uint32_t max_bucket;              // probes in the fullest hash bucket
-    uint32_t pad;
+    uint32_t scratch32;               // one-word device results read back by the host (compat_split)
     unsigned long long walk_words;    // 64-column hit words evaluated by chain_walk_kernel
     unsigned long long walk_items;    // walks chain_walk_kernel finished
     unsigned long long walk_wins;     // 28-B packed windows those words loaded (present components)
@@ -426,6 +426,8 @@ hipError_t launch_compat_cands(const uint64_t* key2, uint64_t N, uint64_t* list,
 hipError_t launch_compat_fire(const restart::PlanData& d, const uint64_t* key2, uint64_t N, int kbits,
                               const uint64_t* cand, uint64_t C, const uint64_t* cs, uint32_t nch, uint32_t* out,
                               uint64_t* cend, uint64_t* cons, hipStream_t st);
+hipError_t launch_compat_split(const uint64_t* sk, const GenomeTable& gt, const uint64_t* cs, uint32_t nch,
+                               uint32_t* out, hipStream_t st);
 hipError_t launch_compat_probe_chunks(const uint64_t* probe_info, uint64_t P, const uint64_t* key2, int kbits,
                                       uint32_t nch, uint32_t* pfirst, hipStream_t st);
 hipError_t launch_compat_drop(const uint64_t* k_in, const uint32_t* v_in, uint64_t N, const uint64_t* rlo,
