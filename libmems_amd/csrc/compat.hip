@@ -389,6 +389,53 @@ __global__ void compat_split_kernel(const uint64_t* __restrict__ sk, GenomeTable
     if (k[p - 1] == k[p]) atomicOr(out, 1u);
 }
 
+// The chunk-major stream as packed records for the packed-record probe and materialize
+// kernels (RecView): group key = masked-ckey bits 1-30 and the chunk's parity (a group cut
+// by a chunk start, A.12, meets its other part across the boundary), parity, 32-bit index.
+// Those kernels compare group keys of neighbours for equality only, so these bits serve
+// wherever two different neighbouring masked keys differ in them; a boundary where they do
+// not sets *clash and the caller numbers the groups by a scan of group heads instead (exact
+// either way).
+__device__ __forceinline__ uint64_t compat_gid(uint64_t k, int kbits) {   // masked ckey bits 1-30, chunk parity
+    return ((k >> 1) & 0x3FFFFFFFull) | (((k >> kbits) & 1ull) << 30);
+}
+
+// list / cnt (optional): compat_cand_kernel's candidates, collected in the same pass
+__global__ void compat_recs_kernel(const uint64_t* __restrict__ key2, const uint32_t* __restrict__ idx, uint64_t n,
+                                   int kbits, uint64_t* __restrict__ rec, uint32_t* __restrict__ clash,
+                                   uint64_t* __restrict__ list, unsigned long long* __restrict__ cnt, uint64_t cap) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const uint64_t k = key2[j], g = compat_gid(k, kbits);
+    const uint64_t kp = j > 0 ? key2[j - 1] : ~k;
+    if (j > 0 && (kp >> 1) != (k >> 1) && compat_gid(kp, kbits) == g) atomicOr(clash, 1u);
+    if (list && (kp >> 1) != (k >> 1)) {   // a group head: more than MER_REPEAT_LIMIT records?
+        const uint64_t e = j + restart::kRepeatLimit;
+        if (e < n && (key2[e] >> 1) == (k >> 1)) {
+            const unsigned long long q = atomicAdd(cnt, 1ull);
+            if (q < cap) list[q] = j;
+        }
+    }
+    rec[j] = (g << 33) | ((k & 1ull) << 32) | idx[j];
+}
+
+__global__ void compat_heads_kernel(const uint64_t* __restrict__ key2, uint64_t n, uint32_t* __restrict__ head) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    head[j] = (j == 0 || (key2[j] >> 1) != (key2[j - 1] >> 1)) ? 1u : 0u;
+}
+
+// group key = the group's ordinal (exclusive scan of the heads + own head) mod 2^31
+__global__ void compat_recs_scan_kernel(const uint64_t* __restrict__ key2, const uint32_t* __restrict__ idx,
+                                        const uint32_t* __restrict__ hscan, uint64_t n, uint64_t* __restrict__ rec) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const uint64_t k = key2[j];
+    const uint32_t head = (j == 0 || (k >> 1) != (key2[j - 1] >> 1)) ? 1u : 0u;
+    const uint64_t g = (uint64_t)(hscan[j] + head) & 0x7FFFFFFFull;
+    rec[j] = (g << 33) | ((k & 1ull) << 32) | idx[j];
+}
+
 // SetMatchLog in compat mode: the chunk of every probe is nondecreasing in AddHashEntry call
 // order (the chunk-major stream), so the chunks are ranges of probes: pfirst[c] = first probe
 // of chunk c (nch + 1 entries, pfirst[nch] = P).  probe_info low word = the group's first
@@ -406,6 +453,30 @@ __global__ void compat_probe_chunk_kernel(const uint64_t* __restrict__ probe_inf
 }
 
 }  // namespace
+
+// scratch: n + 1 u32 (the scan fallback's heads), scan_tmp for exclusive_scan_u32 over n
+hipError_t launch_compat_recs(const uint64_t* key2, const uint32_t* idx, uint64_t n, int kbits, uint64_t* rec,
+                              uint32_t* clash, uint32_t* scratch, void* scan_tmp, bool force_scan, uint64_t* list,
+                              unsigned long long* cnt, uint64_t cap, hipStream_t st) {
+    hipError_t e;
+    if (list && (e = hipMemsetAsync(cnt, 0, 8, st)) != hipSuccess) return e;
+    if (n == 0) return hipSuccess;
+    const dim3 grid((unsigned)((n + 255) / 256)), blk(256);
+    if (!force_scan || list) {   // (the candidates come from this pass either way)
+        if ((e = hipMemsetAsync(clash, 0, 4, st)) != hipSuccess) return e;
+        hipLaunchKernelGGL(compat_recs_kernel, grid, blk, 0, st, key2, idx, n, kbits, rec, clash, list, cnt, cap);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        uint32_t h = 0;
+        if ((e = hipMemcpyAsync(&h, clash, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+        if (!h && !force_scan) return hipSuccess;
+    }
+    hipLaunchKernelGGL(compat_heads_kernel, grid, blk, 0, st, key2, n, scratch);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = exclusive_scan_u32(scratch, n, scan_tmp, nullptr, st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(compat_recs_scan_kernel, grid, blk, 0, st, key2, idx, (const uint32_t*)scratch, n, rec);
+    return hipGetLastError();
+}
 
 hipError_t launch_compat_split(const uint64_t* sk, const GenomeTable& gt, const uint64_t* cs, uint32_t nch,
                                uint32_t* out, hipStream_t st) {

@@ -101,6 +101,7 @@ struct mums_ctx {
     bool use_onesweep = true;
     // ParallelMemHash chunk-compat mode (compat.hip): chunk = CHUNK_SIZE, ParallelMemHash.cpp:51
     bool pcompat = false;
+    bool compat_rec = false;   // compat: the chunk-major stream as packed records (run_pipeline_compat)
     bool prelabelled = false;   // find_tail: chain_of / pool_loc / fkloc hold the ranks' chain labels
     uint64_t prelab_n = 0;      // entries in pool_loc
     const int64_t* lab_rows = nullptr;   // sharded: the rank's own probe rows the labels refer to
@@ -624,6 +625,7 @@ int materialize_dispatch(mums_ctx* ctx, View sv, const MatchParams& mp, hipStrea
 }
 
 int materialize_seeds(mums_ctx* ctx, const MatchParams& mp, hipStream_t st) {
+    if (ctx->compat_rec) return materialize_dispatch<RecView>(ctx, RecView{ctx->sorted_rec}, mp, st);
     if (ctx->packed_path && ctx->rec_ib == 33)
         return materialize_dispatch<RecViewT<33>>(ctx, RecViewT<33>{ctx->sorted_rec}, mp, st);
     if (ctx->packed_path) return materialize_dispatch<RecView>(ctx, RecView{ctx->sorted_rec}, mp, st);
@@ -1410,6 +1412,7 @@ int run_pipeline(mums_ctx* ctx, int stage) {
 int prepare_run(mums_ctx* ctx, const std::vector<uint64_t>& lens) {
     records_live(ctx);
     ctx->stage_done = 0;
+    ctx->compat_rec = false;
     ctx->ties_fixed = false;
     ctx->tie_slots = 0;
     ctx->restarts = 0;
@@ -1468,26 +1471,40 @@ int prepare_run(mums_ctx* ctx, const std::vector<uint64_t>& lens) {
 // ctx->crall holds the genome-major SML keys.  *n_live = records kept.
 int progress_compat(mums_ctx* ctx, uint32_t nch, const std::vector<uint64_t>& hcs, hipStream_t st);
 
-int compat_truncate(mums_ctx* ctx, uint32_t nch, const uint64_t* cs, int kbits, uint64_t* n_live, hipStream_t st) {
+// the candidate list of compat_truncate in ctx->rsplan: list (cap words) and its counter
+int compat_cand_slots(mums_ctx* ctx, uint32_t nch, uint64_t** list, unsigned long long** cnt, uint64_t* cap_out) {
+    const int G = ctx->gt.G;
+    const uint64_t cap = ctx->N / (restart::kRepeatLimit + 1) + 16;
+    const uint64_t words = cap * (4 + (uint64_t)G) + 2 * (uint64_t)(G + 1) + 16 + 3 * ((uint64_t)nch + 1);
+    HIPCHK(ctx->rsplan.ensure(words * 8 + 256));
+    *list = ctx->rsplan.as<uint64_t>();
+    *cnt = (unsigned long long*)(*list + 3 * cap + 2 * (uint64_t)(G + 1));
+    *cap_out = cap;
+    return MUMS_OK;
+}
+
+// cands_ready: the candidates were collected with the packed records (launch_compat_recs)
+int compat_truncate(mums_ctx* ctx, uint32_t nch, const uint64_t* cs, int kbits, uint64_t* n_live, hipStream_t st,
+                    bool cands_ready = false) {
     const GenomeTable& gt = ctx->gt;
     const int G = gt.G;
     const uint64_t N = ctx->N;
     *n_live = N;
     ctx->restarts = 0;
-    const uint64_t cap = N / (restart::kRepeatLimit + 1) + 16;
-    const uint64_t words = cap * (4 + (uint64_t)G) + 2 * (uint64_t)(G + 1) + 16 + 3 * ((uint64_t)nch + 1);
-    HIPCHK(ctx->rsplan.ensure(words * 8 + 256));
-    uint64_t* d_list = ctx->rsplan.as<uint64_t>();
+    uint64_t* d_list = nullptr;
+    unsigned long long* d_cnt = nullptr;
+    uint64_t cap = 0;
+    int rc0 = compat_cand_slots(ctx, nch, &d_list, &d_cnt, &cap);
+    if (rc0) return rc0;
     uint64_t* d_cend = d_list + cap;
     uint32_t* d_fire = (uint32_t*)(d_cend + cap);
     uint64_t* d_dm = d_list + 3 * cap;   // (d_fire takes cap/2 words of that third block)
     uint64_t* d_db = d_dm + G + 1;
-    unsigned long long* d_cnt = (unsigned long long*)(d_db + G + 1);
     uint64_t* d_rng = d_db + G + 1 + 16;
     uint64_t* d_cons = d_rng + 3 * ((uint64_t)nch + 1);   // cap x (G + 1)
     ctx->compat_cons.clear();
     const uint64_t* key2 = (const uint64_t*)ctx->sorted_key;
-    HIPCHK(launch_compat_cands(key2, N, d_list, d_cnt, cap, st));
+    if (!cands_ready) HIPCHK(launch_compat_cands(key2, N, d_list, d_cnt, cap, st));
     unsigned long long C = 0;
     HIPCHK(hipMemcpyAsync(&C, d_cnt, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -1724,15 +1741,42 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
     ctx->sorted_idx = buf ? ctx->vB.as<uint32_t>() : ctx->vA.as<uint32_t>();
     ctx->sort_passes = (kbits + cbits + 7) / 8;
     uint64_t n_live = N;
-    rc = compat_truncate(ctx, nch, cs, kbits, &n_live, st);
+    // the chunk-major stream as packed records for the packed-record probe / materialize
+    // kernels (group keys compared for equality only: launch_compat_recs), built in the same
+    // pass as MER_REPEAT_LIMIT's candidate list, again after a chunk was cut;
+    // MUMS_DEV_COMPAT_PAIRS (read per call): the (key2, index) pair kernels,
+    // MUMS_DEV_COMPAT_GID_SCAN: group keys numbered by the scan
+    ctx->compat_rec = N < (1ull << 32) && !getenv("MUMS_DEV_COMPAT_PAIRS");
+    const bool gid_scan = getenv("MUMS_DEV_COMPAT_GID_SCAN") != nullptr;
+    if (ctx->compat_rec) {
+        HIPCHK(ctx->recA.ensure(N * 8 + 64));
+        HIPCHK(ctx->tmp.ensure(std::max(ctx->tmp.cap, scan_tmp_bytes(N + 1))));
+        uint64_t* d_list = nullptr;
+        unsigned long long* d_cnt = nullptr;
+        uint64_t cap = 0;
+        if ((rc = compat_cand_slots(ctx, nch, &d_list, &d_cnt, &cap))) return rc;
+        HIPCHK(launch_compat_recs((const uint64_t*)ctx->sorted_key, ctx->sorted_idx, N, kbits, ctx->recA.as<uint64_t>(),
+                                  &dc->scratch32, ctx->ckey.as<uint32_t>(), ctx->tmp.p, gid_scan, d_list, d_cnt, cap,
+                                  st));
+        ctx->sorted_rec = ctx->recA.as<uint64_t>();
+    }
+    rc = compat_truncate(ctx, nch, cs, kbits, &n_live, st, ctx->compat_rec);
     if (rc) return rc;
+    if (ctx->compat_rec && n_live != N)   // records of the cut stream
+        HIPCHK(launch_compat_recs((const uint64_t*)ctx->sorted_key, ctx->sorted_idx, n_live, kbits,
+                                  ctx->recA.as<uint64_t>(), &dc->scratch32, ctx->ckey.as<uint32_t>(), ctx->tmp.p,
+                                  gid_scan, nullptr, nullptr, 0, st));
     if (ctx->progress_on && (rc = progress_compat(ctx, nch, hcs, st))) return rc;
     HIPCHK(hipEventRecord(ctx->ev[EV_SORT], st));
     SegTile* tiles = ctx->tiles.as<SegTile>();
     HIPCHK(launch_flat_tiles(n_live, tiles, st));
-    rc = groups_dispatch<PairView<uint64_t>>(
-        ctx, PairView<uint64_t>{(const uint64_t*)ctx->sorted_key, ctx->sorted_idx}, tiles,
-        (n_live + kSegTile - 1) / kSegTile, mp, ps.probe_info, ps.probe_bucket, ps.slot_info, ps.slot_bucket, st);
+    if (ctx->compat_rec)
+        rc = groups_dispatch<RecView>(ctx, RecView{ctx->sorted_rec}, tiles, (n_live + kSegTile - 1) / kSegTile, mp,
+                                      ps.probe_info, ps.probe_bucket, ps.slot_info, ps.slot_bucket, st);
+    else
+        rc = groups_dispatch<PairView<uint64_t>>(
+            ctx, PairView<uint64_t>{(const uint64_t*)ctx->sorted_key, ctx->sorted_idx}, tiles,
+            (n_live + kSegTile - 1) / kSegTile, mp, ps.probe_info, ps.probe_bucket, ps.slot_info, ps.slot_bucket, st);
     if (rc) return rc;
     rc = finish_seeds(ctx, ps, st);
     if (rc) return rc;

@@ -426,6 +426,9 @@ hipError_t launch_compat_cands(const uint64_t* key2, uint64_t N, uint64_t* list,
 hipError_t launch_compat_fire(const restart::PlanData& d, const uint64_t* key2, uint64_t N, int kbits,
                               const uint64_t* cand, uint64_t C, const uint64_t* cs, uint32_t nch, uint32_t* out,
                               uint64_t* cend, uint64_t* cons, hipStream_t st);
+hipError_t launch_compat_recs(const uint64_t* key2, const uint32_t* idx, uint64_t n, int kbits, uint64_t* rec,
+                              uint32_t* clash, uint32_t* scratch, void* scan_tmp, bool force_scan, uint64_t* list,
+                              unsigned long long* cnt, uint64_t cap, hipStream_t st);
 hipError_t launch_compat_split(const uint64_t* sk, const GenomeTable& gt, const uint64_t* cs, uint32_t nch,
                                uint32_t* out, hipStream_t st);
 hipError_t launch_compat_probe_chunks(const uint64_t* probe_info, uint64_t P, const uint64_t* key2, int kbits,

@@ -171,3 +171,19 @@ def test_parallel_many_chunks(gpu_lib, oracle_mod, n, chunk):
     ml, st = gpu_parallel(gpu_lib, seqs, seed, chunk)
     assert st["chunks"] == ost["chunks"] > 1500
     assert len(ml) == len(lengths) and (ml.lengths == lengths).all() and (ml.starts == starts).all()
+
+
+@pytest.mark.parametrize("env", [{"MUMS_DEV_COMPAT_PAIRS": "1"}, {"MUMS_DEV_COMPAT_GID_SCAN": "1"}])
+def test_parallel_probe_views_agree(gpu_lib, oracle_mod, monkeypatch, env):
+    """The chunk-major stream as packed records (default; group keys = the masked key's low
+    bits, or numbered by a scan) and as (key2, index) pairs give the oracle's list."""
+    for idx in (1, 4, 7):
+        G, n, p, w, chunk, gseed = COMPAT_SMALL[idx]
+        seqs = oracle_mod.generate(G, n, p, gseed)
+        seed = oracle_mod.get_seed(w)
+        lengths, starts, ost = oracle_mod.find_matches(seqs, seed, parallel_compat=True, chunk_size=chunk)
+        with monkeypatch.context() as m:
+            for k, v in env.items():
+                m.setenv(k, v)
+            ml, st = gpu_parallel(gpu_lib, seqs, seed, chunk)
+        assert len(ml) == len(lengths) and (ml.lengths == lengths).all() and (ml.starts == starts).all(), env
