@@ -425,15 +425,21 @@ __global__ __launch_bounds__(kBlock) void chain_link_kernel(View v, const uint64
     for (int i = 0; i < kLinkIPT; ++i) {
         const uint64_t j = (uint64_t)blockIdx.x * (kBlock * kLinkIPT) + (uint64_t)i * kBlock + threadIdx.x;
         it[i] = WalkItem{(uint32_t)j, 1, 0, INT64_MAX};
-        if (j >= P) continue;
+        // probe j + 1 is the next lane's probe j: taken by a shuffle (one row load per probe,
+        // the rows may be random reads through the line order), loaded only by a wave's last lane
         Mhe<MG> A, B;
-        probe_of<MG, View>(v, probe_info, j, gt, mp, L, A);
+        if (j < P) probe_of<MG, View>(v, probe_info, j, gt, mp, L, A);
+        else A = Mhe<MG>{};
+        B.len = __shfl_down(A.len, 1, 64);
+        B.offset = __shfl_down(A.offset, 1, 64);
+        B.mersize = __shfl_down(A.mersize, 1, 64);
+        #pragma unroll
+        for (int g = 0; g < MG; ++g) B.s[g] = __shfl_down(A.s[g], 1, 64);
+        if (j >= P) continue;
+        if ((threadIdx.x & 63) == 63 && j + 1 < P) probe_of<MG, View>(v, probe_info, j + 1, gt, mp, L, B);
         if (fsl) fsl[j] = (uint32_t)start_at(A, first_start(A));
         bool same = false;
-        if (j + 1 < P) {
-            probe_of<MG, View>(v, probe_info, j + 1, gt, mp, L, B);
-            same = same_line<MG>(A, B);
-        }
+        if (j + 1 < P) same = same_line<MG>(A, B);
         uint8_t lk = 0;
         if (same) {
             const int64_t stop = start_at(B, first_start(B)) - start_at(A, first_start(A)) - L;
@@ -1407,6 +1413,15 @@ hipError_t launch_chains(View v, const uint64_t* probe_info, uint64_t P, const G
         hipError_t r;
         if ((r = hipMemsetAsync(flags, 0, 8, st)) != hipSuccess) return r;
         if constexpr (MG % 4 == 0 && MG <= 16) {
+            // the int32 rows are read through the line order (chain_link shares each row with its
+            // neighbour lane): 1.3 ms less than gathering them at C3;
+            // MUMS_DEV_LINE_GATHER=1 (read per call) gathers them first
+            const char* lg = getenv("MUMS_DEV_LINE_GATHER");
+            if (v.rows32 && !(lg && lg[0] == '1')) {
+                LineRows vl{v.rows32, v.stride32, v.L32, o};
+                return chains_core<MG>(vl, w, o, P, gt, mp, ss, packed, d_scan_tmp, d_radix_tmp, chain_of, pool,
+                                       d_nchains, st, ctr, ev_walk, fk, kbase, jl);
+            }
             if (v.rows32) {   // int32 rows in key order (materialize_dispatch): copied in line order
                 hipLaunchKernelGGL(gather_rows32_kernel, dim3(grid_of(P)), dim3(kBlock), 0, st, v.rows32, o, P,
                                    v.stride32, (int32_t*)w.rows_line);

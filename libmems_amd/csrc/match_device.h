@@ -575,12 +575,14 @@ __device__ __forceinline__ void load_probe(const MatProbes& m, uint64_t k, int G
 struct LineRows {
     const int32_t* rows;
     uint32_t stride;
-    int L;   // seed length of the offset sum
+    int L;                           // seed length of the offset sum
+    const uint32_t* ord = nullptr;   // set: rows in key order, read through the line order
 };
 
 template <int MG>
 __device__ __forceinline__ void load_probe(const LineRows& m, uint64_t k, int G, int L, Mhe<MG>& P) {
-    load_probe32<MG>(m.rows + k * (uint64_t)m.stride, G, L, m.L, P);
+    const uint64_t r = m.ord ? (uint64_t)m.ord[k] : k;
+    load_probe32<MG>(m.rows + r * (uint64_t)m.stride, G, L, m.L, P);
 }
 
 __device__ __forceinline__ uint32_t bucket_of(int64_t offset, uint32_t table_size) {

@@ -17,6 +17,8 @@ VARIANTS = [
     {"MUMS_DEV_FIND_CHUNK": "40000", "MUMS_DEV_WIDE_LINE_ROWS": "retry"},
     {"MUMS_DEV_RS_NOAGG": "1"},
     {"MUMS_DEV_LINE_NORUNS": "1"},
+    {"MUMS_DEV_LINE_GATHER": "1"},
+    {"MUMS_DEV_LINE_GATHER": "1", "MUMS_DEV_FIND_CHUNK": "40000"},
 ]
 
 
