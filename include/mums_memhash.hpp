@@ -492,6 +492,10 @@ public:
     // every rank
     void SetRepeatTolerance(uint32_t t) { repeat_tol_ = t; }
     void SetEnumerationTolerance(uint32_t t) { enum_tol_ = t; }
+    // ParallelMemHash's MatchList (ParallelMemHash.cpp:42-121, CHUNK_SIZE = chunk_size): every
+    // rank searches a contiguous range of the chunks, the bucket owners re-add the ranks' tables
+    // rank after rank (genome blocks only)
+    void SetParallelCompat(bool enable, uint64_t chunk_size = 200000) { compat_chunk_ = enable ? chunk_size : 0; }
     bool AddSequence(const std::string& seq) {
         seqs_.push_back(seq);
         return true;
@@ -549,6 +553,10 @@ public:
             ranks_.push_back(std::move(mh));
             g0 += cnt;
         }
+        if (compat_chunk_)
+            for (auto& mh : ranks_)
+                if (mums_set_parallel_compat(mh->handle(), 1, compat_chunk_) != MUMS_OK)
+                    throw InvalidData(mums_last_error(mh->handle()));
         if (!start_points_.empty())
             for (auto& mh : ranks_)
                 if (mums_set_start_points(mh->handle(), start_points_.data(), (uint32_t)start_points_.size()) != MUMS_OK)
@@ -580,6 +588,7 @@ private:
     uint64_t seed_ = 0;
     uint32_t table_size_ = 40000;
     uint32_t repeat_tol_ = 0, enum_tol_ = 1;
+    uint64_t compat_chunk_ = 0;   // ParallelMemHash compat: CHUNK_SIZE (0: MemHash)
     std::vector<uint64_t> start_points_;
 };
 

@@ -590,12 +590,18 @@ class ShardedMemHash:
     comm="local"), one host thread per rank.  The ranks' MatchLists in rank order are the
     bucket-major MatchList of MemHash::FindMatches (DESIGN.md §6)."""
 
-    def __init__(self, devices: Sequence[int], comm: str = "rccl", table_size: int = 40000, layout: str = "blocks"):
+    def __init__(self, devices: Sequence[int], comm: str = "rccl", table_size: int = 40000, layout: str = "blocks",
+                 parallel_compat: bool = False, chunk_size: int = 200000):
         """layout "blocks": a contiguous genome block per rank; "slices": every genome cut into
-        world / G position slices (BASELINE config 5: two 3 Gbp genomes over 8 GPUs)."""
+        world / G position slices (BASELINE config 5: two 3 Gbp genomes over 8 GPUs).
+        parallel_compat: ParallelMemHash's MatchList (ParallelMemHash.cpp:42-121, CHUNK_SIZE =
+        chunk_size): every rank searches a contiguous range of the chunks, the bucket owners
+        re-add the ranks' tables rank after rank (compat_ranks.hip)."""
         if layout not in ("blocks", "slices"):
             raise ValueError("layout: 'blocks' or 'slices'")
         self.layout = layout
+        self.parallel_compat = bool(parallel_compat)
+        self.chunk_size = int(chunk_size)
         self._lib = load_library()
         self.devices = list(devices)
         self.world = len(self.devices)
@@ -697,6 +703,8 @@ class ShardedMemHash:
             g0 += cnt
         for mh in self.ranks:
             mh.LogProgress(self.progress)
+            if self.parallel_compat:
+                mh._check(self._lib.mums_set_parallel_compat(mh._ctx, 1, self.chunk_size))
         sp = getattr(self, "_start_points", None)
         if sp is not None:
             for mh in self.ranks:

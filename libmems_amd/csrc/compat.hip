@@ -241,6 +241,22 @@ __global__ void compat_drop_kernel(const uint64_t* __restrict__ k_in, const uint
     v_out[j - drop] = v_in[j];
 }
 
+// records of chunks [c0, c1) in the chunk-major stream: lower_bound of c0 << kbits and of
+// c1 << kbits over key2 (sorted ascending), one lane each
+__global__ void compat_chunk_span_kernel(const uint64_t* __restrict__ key2, uint64_t n, int kbits, uint32_t c0,
+                                         uint32_t c1, uint64_t* __restrict__ out) {
+    const int t = threadIdx.x;
+    if (t >= 2) return;
+    const uint64_t want = (uint64_t)(t ? c1 : c0) << kbits;
+    uint64_t lo = 0, len = n;
+    while (len > 0) {
+        const uint64_t h = len >> 1;
+        if (key2[lo + h] < want) { lo += h + 1; len -= h + 1; }
+        else len = h;
+    }
+    out[t] = lo;
+}
+
 // MergeTable (ParallelMemHash.cpp:105-121): every entry of the thread table is re-added
 // with AddHashEntry (MemHash.cpp:209-251) into the global table: lower_bound, a
 // collision when equivalent (MheCompare both ways false), else inserted at the
@@ -576,6 +592,29 @@ hipError_t launch_compat_merge(uint32_t* tsize, const uint32_t* bstart, uint32_t
     else if (G <= 32) MUMS_COMPAT_MERGE(32, 256);
     else MUMS_COMPAT_MERGE(64, 256);
 #undef MUMS_COMPAT_MERGE
+    return hipGetLastError();
+}
+
+hipError_t launch_compat_chunk_span(const uint64_t* key2, uint64_t n, int kbits, uint32_t c0, uint32_t c1,
+                                    uint64_t* out, hipStream_t st) {
+    hipLaunchKernelGGL(compat_chunk_span_kernel, dim3(1), dim3(64), 0, st, key2, n, kbits, c0, c1, out);
+    return hipGetLastError();
+}
+
+// the exact merge alone, from first_fail[b] (~0: bucket skipped) in each of nb buckets
+hipError_t launch_compat_merge_from(uint32_t* tsize, const uint32_t* bstart, uint32_t* tbl, const int64_t* pool, int G,
+                                    uint32_t nb, const uint32_t* first_fail, unsigned long long* collisions,
+                                    hipStream_t st) {
+    if (nb == 0) return hipSuccess;
+#define MUMS_COMPAT_FIX(MGV, BLK)                                                                                     \
+    hipLaunchKernelGGL((compat_merge_fix_kernel<MGV, BLK>), dim3(nb), dim3(BLK), 0, st, tsize, bstart, tbl, pool, G,  \
+                       first_fail, collisions)
+    if (G <= 4) MUMS_COMPAT_FIX(4, 1024);
+    else if (G <= 8) MUMS_COMPAT_FIX(8, 1024);
+    else if (G <= 16) MUMS_COMPAT_FIX(16, 512);
+    else if (G <= 32) MUMS_COMPAT_FIX(32, 256);
+    else MUMS_COMPAT_FIX(64, 256);
+#undef MUMS_COMPAT_FIX
     return hipGetLastError();
 }
 

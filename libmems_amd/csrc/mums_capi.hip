@@ -102,6 +102,11 @@ struct mums_ctx {
     // ParallelMemHash chunk-compat mode (compat.hip): chunk = CHUNK_SIZE, ParallelMemHash.cpp:51
     bool pcompat = false;
     bool compat_rec = false;   // compat: the chunk-major stream as packed records (run_pipeline_compat)
+    // compat over ranks (compat_ranks.hip): this context searches chunks [nch * compat_rank /
+    // compat_ranks, nch * (compat_rank + 1) / compat_ranks) with tables of its own
+    uint32_t compat_rank = 0, compat_ranks = 1;
+    mums_ctx* compat_sub = nullptr;   // sharded compat: the rank's search over all genomes
+    DevBuf rkpool0, rkpool1, rku32, ascii_all;   // sharded compat: the owner's merge (ctx_compat_rank_merge)
     bool prelabelled = false;   // find_tail: chain_of / pool_loc / fkloc hold the ranks' chain labels
     uint64_t prelab_n = 0;      // entries in pool_loc
     const int64_t* lab_rows = nullptr;   // sharded: the rank's own probe rows the labels refer to
@@ -981,6 +986,9 @@ int finish_seeds(mums_ctx* ctx, const ProbeSpace& ps, hipStream_t st) {
 
 // per-run statistics (mums_stats) of the last seed stage [+ replay] over n records
 void fill_stats(mums_ctx* ctx, uint64_t n) {
+    struct ClearLast {   // the elapsed times below ignore their status: leave no sticky error behind
+        ~ClearLast() { (void)hipGetLastError(); }
+    } clear_last;
     mums_stats& s = ctx->st;
     s = mums_stats{};
     s.seedmers = n;
@@ -1559,6 +1567,42 @@ int compat_truncate(mums_ctx* ctx, uint32_t nch, const uint64_t* cs, int kbits, 
     return MUMS_OK;
 }
 
+// compat over ranks: keep only this rank's chunks [nch * r / R, nch * (r + 1) / R) of the live
+// chunk-major stream (the oracle's rank model, oracle/mums_oracle.c parallel_compat_search):
+// its search then starts from empty tables at its first chunk.  The MER_REPEAT_LIMIT cuts were
+// decided per chunk before (compat_truncate), so they are unchanged.
+int compat_keep_chunks(mums_ctx* ctx, uint32_t nch, int kbits, uint64_t* n_live, hipStream_t st) {
+    const uint32_t c0 = (uint32_t)((uint64_t)nch * ctx->compat_rank / ctx->compat_ranks);
+    const uint32_t c1 = (uint32_t)((uint64_t)nch * (ctx->compat_rank + 1) / ctx->compat_ranks);
+    const uint64_t n = *n_live;
+    const uint64_t* key2 = (const uint64_t*)ctx->sorted_key;
+    uint64_t* d_rng = nullptr;
+    {
+        uint64_t* d_list = nullptr;
+        unsigned long long* d_cnt = nullptr;
+        uint64_t cap = 0;
+        int rc = compat_cand_slots(ctx, nch, &d_list, &d_cnt, &cap);
+        if (rc) return rc;
+        d_rng = (uint64_t*)(d_cnt + 2);   // 8 words behind the candidate counter
+    }
+    HIPCHK(launch_compat_chunk_span(key2, n, kbits, c0, c1, d_rng, st));
+    uint64_t span[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(span, d_rng, 16, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (span[0] == 0 && span[1] == n) return MUMS_OK;
+    const uint64_t rng[6] = {0, span[1], span[0], n, 0, span[0]};   // rlo[2], rhi[2], rpre[2]
+    HIPCHK(hipMemcpyAsync(d_rng + 2, rng, sizeof(rng), hipMemcpyHostToDevice, st));
+    uint64_t* k_out = ctx->sorted_buf ? ctx->kA.as<uint64_t>() : ctx->kB.as<uint64_t>();
+    uint32_t* v_out = ctx->sorted_buf ? ctx->vA.as<uint32_t>() : ctx->vB.as<uint32_t>();
+    HIPCHK(launch_compat_drop(key2, ctx->sorted_idx, n, d_rng + 2, d_rng + 4, d_rng + 6, 2, k_out, v_out, st));
+    HIPCHK(hipStreamSynchronize(st));   // (rng is a host temporary)
+    ctx->sorted_buf ^= 1;
+    ctx->sorted_key = k_out;
+    ctx->sorted_idx = v_out;
+    *n_live = span[1] - span[0];
+    return MUMS_OK;
+}
+
 int run_pipeline_compat(mums_ctx* ctx, int stage) {
     hipStream_t st = ctx->stream;
     const int G = (int)ctx->genomes.size();
@@ -1762,6 +1806,17 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
     }
     rc = compat_truncate(ctx, nch, cs, kbits, &n_live, st, ctx->compat_rec);
     if (rc) return rc;
+    if (ctx->compat_ranks > 1 && (rc = compat_keep_chunks(ctx, nch, kbits, &n_live, st))) return rc;
+    if (ctx->compat_ranks > 1 && n_live == 0) {   // no chunk (or no live record) in this rank's range
+        ctx->P = 0;
+        ctx->M = 0;
+        ctx->stage_done = stage >= MUMS_STAGE_ALL ? MUMS_STAGE_ALL : MUMS_STAGE_SEEDS;
+        for (int e = EV_SORT; e <= EV_OUTPUT; ++e) HIPCHK(hipEventRecord(ctx->ev[e], st));
+        HIPCHK(hipStreamSynchronize(st));
+        HIPCHK(hipMemcpy(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost));
+        fill_stats(ctx, N);
+        return MUMS_OK;
+    }
     if (ctx->compat_rec && n_live != N)   // records of the cut stream
         HIPCHK(launch_compat_recs((const uint64_t*)ctx->sorted_key, ctx->sorted_idx, n_live, kbits,
                                   ctx->recA.as<uint64_t>(), &dc->scratch32, ctx->ckey.as<uint32_t>(), ctx->tmp.p,
@@ -1929,7 +1984,8 @@ int mums_ctx_destroy(mums_ctx* ctx) {
                       &ctx->rsplan, &ctx->rsbst, &ctx->pool_loc, &ctx->cbuf, &ctx->sids,
                       &ctx->logA, &ctx->logB, &ctx->logvA, &ctx->logvB, &ctx->tiebuf, &ctx->fk, &ctx->fkloc,
                       &ctx->crbuf, &ctx->crcnt, &ctx->crlive, &ctx->crruns, &ctx->crall, &ctx->fsk, &ctx->bst2,
-                      &ctx->side, &ctx->bst8, &ctx->cbst, &ctx->dsarr, &ctx->labx};
+                      &ctx->side, &ctx->bst8, &ctx->cbst, &ctx->dsarr, &ctx->labx, &ctx->rkpool0, &ctx->rkpool1,
+                      &ctx->rku32, &ctx->ascii_all};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i < EV_COUNT; ++i)
         if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
@@ -1937,6 +1993,7 @@ int mums_ctx_destroy(mums_ctx* ctx) {
         if (ctx->ev_ds[i]) (void)hipEventDestroy(ctx->ev_ds[i]);
     for (int i = 0; i < 6; ++i)
         if (ctx->ev_walk[i]) (void)hipEventDestroy(ctx->ev_walk[i]);
+    if (ctx->compat_sub) (void)mums_ctx_destroy(ctx->compat_sub);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return MUMS_OK;
@@ -2397,6 +2454,172 @@ int mums::ctx_table_genomes(mums_ctx* ctx, uint32_t* table_size, uint32_t* genom
     if (check_ctx(ctx)) return MUMS_E_INVALID;
     *table_size = ctx->table_size;
     *genomes = (uint32_t)ctx->gt.G;
+    return MUMS_OK;
+}
+
+// ---- ParallelMemHash compat over ranks (shard_comm.hip compat_shard_run) ----------------
+bool mums::ctx_pcompat(mums_ctx* ctx) { return ctx && ctx->pcompat; }
+
+int mums::ctx_compat_layout(mums_ctx* ctx, uint32_t* first, uint32_t* nown, std::vector<uint64_t>* lens) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    if (!ctx->shard) return fail(ctx, MUMS_E_INVALID, "no shard layout (mums_shard_layout)");
+    if (ctx->slice)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "sharded ParallelMemHash compat: genome blocks only (no position slices)");
+    if (ctx->pairwise || ctx->enum_tol > 1)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "ParallelMemHash compat with PairwiseMatchFinder / enumeration tolerance > 1");
+    if (ctx->match_log)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "sharded ParallelMemHash compat: no match log (the ranks' merge order "
+                                             "is not the one-thread schedule's)");
+    if (!ctx->start_points.empty())
+        return fail(ctx, MUMS_E_UNSUPPORTED, "start points (FindMatchesFromPosition) in the ParallelMemHash compat mode");
+    const uint32_t nl = (uint32_t)ctx->genomes.size();
+    if (ctx->shard_first + nl > ctx->shard_len.size())
+        return fail(ctx, MUMS_E_INVALID, "owned genomes exceed the shard layout");
+    for (uint32_t i = 0; i < nl; ++i)
+        if (ctx->genomes[i].n != ctx->shard_len[ctx->shard_first + i])
+            return fail(ctx, MUMS_E_INVALID, "owned genome length differs from the shard layout");
+    *first = ctx->shard_first;
+    *nown = nl;
+    *lens = ctx->shard_len;
+    return MUMS_OK;
+}
+
+int mums::ctx_compat_rank_find(mums_ctx* ctx, const char* const* d_ascii, const uint64_t* lens, int G, uint32_t rank,
+                               uint32_t ranks, int stage) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    HIPCHK(hipSetDevice(ctx->device));
+    if (!ctx->compat_sub) {
+        mums_ctx* sub = nullptr;
+        const int rc = mums_ctx_create(ctx->device, &sub);
+        if (rc) return fail(ctx, rc, "compat rank context");
+        ctx->compat_sub = sub;
+    }
+    mums_ctx* sub = ctx->compat_sub;
+    (void)mums_clear(sub);
+    if (mums_set_stream(sub, ctx->stream)) return fail(ctx, MUMS_E_HIP, "compat rank context stream");
+    sub->seed = ctx->seed;
+    sub->repeat_tol = ctx->repeat_tol;
+    sub->enum_tol = ctx->enum_tol;
+    sub->table_size = ctx->table_size;
+    sub->masked = ctx->masked;
+    sub->seq_mask = ctx->seq_mask;
+    sub->pcompat = true;
+    sub->chunk_size = ctx->chunk_size;
+    sub->progress_on = ctx->progress_on;
+    sub->profiling = ctx->profiling;
+    sub->match_log = false;
+    sub->compat_rank = rank;
+    sub->compat_ranks = ranks;
+    for (int g = 0; g < G; ++g)
+        if (mums_add_genome_device(sub, d_ascii[g], lens[g])) return fail(ctx, MUMS_E_INVALID, sub->err);
+    const int rc = mums_find_stage(sub, stage);
+    if (rc) return fail(ctx, rc, sub->err);
+    ctx->gt = sub->gt;
+    ctx->st = sub->st;
+    ctx->progress = sub->progress;
+    ctx->nchunks = sub->nchunks;
+    ctx->M = 0;
+    ctx->stage_done = MUMS_STAGE_SEEDS;   // the MatchList: after the owners' merge
+    return MUMS_OK;
+}
+
+int mums::ctx_compat_rank_export(mums_ctx* ctx, uint64_t* bucket_counts, int64_t* d_rows, uint64_t* M) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    mums_ctx* sub = ctx->compat_sub;
+    if (!sub || sub->stage_done < MUMS_STAGE_ALL) return fail(ctx, MUMS_E_INVALID, "no compat rank search");
+    const uint32_t Tb = sub->table_size;
+    *M = sub->M;
+    if (sub->M == 0) {
+        std::fill(bucket_counts, bucket_counts + Tb, 0ull);
+        return MUMS_OK;
+    }
+    HIPCHK(hipSetDevice(ctx->device));
+    std::vector<uint32_t> ts(Tb);
+    HIPCHK(hipMemcpy(ts.data(), sub->tsize.p, (size_t)Tb * 4, hipMemcpyDeviceToHost));
+    for (uint32_t b = 0; b < Tb; ++b) bucket_counts[b] = ts[b];
+    if (d_rows)
+        HIPCHK(launch_rank_rows(sub->obase.as<uint32_t>(), sub->emit_base, sub->emit_tbl, sub->pool.as<int64_t>(),
+                                sub->gt.G, Tb, sub->M, d_rows, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return MUMS_OK;
+}
+
+// MergeTable of the W sources' tables into one, source after source (compat_ranks.hip): the
+// union kernels per step, the exact sequential merge for the buckets whose union fails a check
+int mums::ctx_compat_rank_merge(mums_ctx* ctx, const int64_t* d_rows, uint32_t W, const uint64_t* counts, uint32_t nb) {
+    if (check_ctx(ctx)) return MUMS_E_INVALID;
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    const int G = ctx->gt.G;
+    const uint64_t rowb = 8ull * (G + 2);
+    uint64_t total = 0;
+    std::vector<uint64_t> src_n(W, 0);
+    for (uint32_t s = 0; s < W; ++s)
+        for (uint32_t j = 0; j < nb; ++j) src_n[s] += counts[(uint64_t)s * nb + j];
+    for (uint32_t s = 0; s < W; ++s) total += src_n[s];
+    if (total >= 0xFFFFFFF0ull) return fail(ctx, MUMS_E_UNSUPPORTED, "compat rank merge: more than 2^32 entries per owner");
+    // test hook (read per call): every bucket through the exact sequential merge
+    const bool all_exact = getenv("MUMS_DEV_COMPAT_RANK_EXACT") != nullptr;
+    HIPCHK(ctx->rkpool0.ensure((total + 1) * rowb));
+    HIPCHK(ctx->rkpool1.ensure((total + 1) * rowb));
+    const uint64_t words = 3 * (total + 1) + 8 * ((uint64_t)nb + 2) + 64;
+    HIPCHK(ctx->rku32.ensure(words * 4));
+    HIPCHK(ctx->tmp.ensure(std::max({ctx->tmp.cap, scan_tmp_bytes(total + 2), scan_tmp_bytes((uint64_t)nb + 2)})));
+    HIPCHK(ctx->counters.ensure(sizeof(DevCounters)));
+    DevCounters* dc = ctx->counters.as<DevCounters>();
+    uint32_t* u = ctx->rku32.as<uint32_t>();
+    uint32_t* lbA = u;
+    uint32_t* nd = lbA + (total + 1);
+    uint32_t* tblcat = nd + (total + 1);
+    uint32_t* offA = tblcat + (total + 1);
+    uint32_t* offB = offA + (nb + 2);
+    uint32_t* catoff = offB + (nb + 2);
+    uint32_t* tsz = catoff + (nb + 2);
+    uint32_t* ff = tsz + (nb + 2);
+    uint32_t* bad = ff + (nb + 2);
+    uint32_t* newoff = bad + (nb + 2);
+    int64_t* cur = ctx->rkpool0.as<int64_t>();
+    int64_t* nxt = ctx->rkpool1.as<int64_t>();
+    uint64_t nA = 0, src_off = 0, coll = 0;
+    HIPCHK(hipMemsetAsync(offA, 0, (size_t)(nb + 1) * 4, st));
+    std::vector<uint32_t> hoff(nb + 1);
+    for (uint32_t s = 0; s < W; ++s) {
+        const uint64_t nB = src_n[s];
+        hoff[0] = 0;
+        for (uint32_t j = 0; j < nb; ++j) hoff[j + 1] = hoff[j] + (uint32_t)counts[(uint64_t)s * nb + j];
+        HIPCHK(hipMemcpyAsync(offB, hoff.data(), (size_t)(nb + 1) * 4, hipMemcpyHostToDevice, st));
+        if (nB)   // pool = [A rows | B rows]
+            HIPCHK(hipMemcpyAsync(cur + nA * (G + 2), d_rows + src_off * (G + 2), nB * rowb, hipMemcpyDeviceToDevice, st));
+        src_off += nB;
+        HIPCHK(hipMemsetAsync(bad, all_exact ? 0x01 : 0x00, (size_t)(nb + 1) * 4, st));
+        HIPCHK(hipMemsetAsync(nd + nB, 0, 4, st));
+        HIPCHK(launch_rank_lb(cur, G, (uint32_t)nA, offA, offB, nb, (uint32_t)nB, lbA, nd, bad, st));
+        HIPCHK(exclusive_scan_u32(nd, nB + 1, ctx->tmp.p, &dc->scratch32, st));   // nd -> prefix (nB + 1 words)
+        HIPCHK(launch_rank_place(cur, G, (uint32_t)nA, offA, offB, nb, (uint32_t)nB, lbA, nd, catoff, tsz, tblcat, st));
+        const uint32_t ncat = (uint32_t)(nA + nB);
+        HIPCHK(launch_rank_check(cur, G, catoff, tsz, nb, ncat, tblcat, bad, st));
+        HIPCHK(launch_rank_exact_init((uint32_t)nA, offA, offB, catoff, nb, ncat, bad, tblcat, tsz, ff, st));
+        HIPCHK(launch_compat_merge_from(tsz, catoff, tblcat, cur, G, nb, ff, &dc->collisions, st));
+        HIPCHK(hipMemcpyAsync(newoff, tsz, (size_t)nb * 4, hipMemcpyDeviceToDevice, st));
+        HIPCHK(hipMemsetAsync(newoff + nb, 0, 4, st));
+        HIPCHK(exclusive_scan_u32(newoff, (uint64_t)nb + 1, ctx->tmp.p, &dc->scratch32, st));
+        uint32_t nF = 0;
+        HIPCHK(hipMemcpyAsync(&nF, newoff + nb, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(launch_rank_gather(cur, G, catoff, tsz, nb, ncat, tblcat, newoff, nxt, st));
+        HIPCHK(hipMemcpyAsync(offA, newoff, (size_t)(nb + 1) * 4, hipMemcpyDeviceToDevice, st));
+        HIPCHK(hipStreamSynchronize(st));
+        coll += nA + nB - nF;
+        nA = nF;
+        std::swap(cur, nxt);
+    }
+    ctx->M = nA;
+    HIPCHK(ctx->out_len.ensure((ctx->M + 1) * 8));
+    HIPCHK(ctx->out_s.ensure((ctx->M + 1) * (size_t)G * 8));
+    HIPCHK(launch_rank_list(cur, G, ctx->M, ctx->out_len.as<uint64_t>(), ctx->out_s.as<int64_t>(), st));
+    HIPCHK(hipStreamSynchronize(st));
+    ctx->st.mem_count = ctx->M;
+    ctx->st.collision_count += coll;   // the rank's own search + this owner's re-adds
+    ctx->stage_done = MUMS_STAGE_ALL;
     return MUMS_OK;
 }
 }

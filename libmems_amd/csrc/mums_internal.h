@@ -21,6 +21,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <vector>
+
 #include "restart_plan.h"
 
 namespace mums {
@@ -327,6 +329,19 @@ int ctx_table_genomes(mums_ctx* ctx, uint32_t* table_size, uint32_t* genomes);
 uint32_t ctx_repeat_tol(mums_ctx* ctx);
 bool ctx_merge_chunked(mums_ctx* ctx);   // the last shard merge ran in key chunks
 bool ctx_tie_all(mums_ctx* ctx);         // every run of equal keys in std::sort order (repeat / enum tol)
+// ParallelMemHash compat over ranks (shard_comm.hip compat_shard_run; mums_capi.hip)
+bool ctx_pcompat(mums_ctx* ctx);
+// the shard layout of a compat context: owned genomes [*first, *first + *nown) of lens
+int ctx_compat_layout(mums_ctx* ctx, uint32_t* first, uint32_t* nown, std::vector<uint64_t>* lens);
+// the compat search of chunk range rank / ranks over all genomes (device ASCII) on the
+// context's rank sub-context
+int ctx_compat_rank_find(mums_ctx* ctx, const char* const* d_ascii, const uint64_t* lens, int G, uint32_t rank,
+                         uint32_t ranks, int stage);
+// the rank's table: per-bucket counts (table_size words) and, with d_rows, its rows in bucket order
+int ctx_compat_rank_export(mums_ctx* ctx, uint64_t* bucket_counts, int64_t* d_rows, uint64_t* M);
+// re-add W sources' rows (rank order; source s holds counts[s * nb + j] rows of bucket j of this
+// owner's nb buckets, in bucket order) into this context's MatchList
+int ctx_compat_rank_merge(mums_ctx* ctx, const int64_t* d_rows, uint32_t W, const uint64_t* counts, uint32_t nb);
 
 // overlaps.hip: EliminateOverlaps (Aligner.cpp:62-176) on a device MatchList
 struct EoWork {
@@ -439,6 +454,31 @@ hipError_t launch_compat_drop(const uint64_t* k_in, const uint32_t* v_in, uint64
 hipError_t launch_compat_merge(uint32_t* tsize, const uint32_t* bstart, uint32_t* tbl, const int64_t* pool, int G,
                                uint32_t Tb, unsigned long long* collisions, const uint32_t* tscan, uint64_t total,
                                uint32_t* first_fail, hipStream_t st);
+hipError_t launch_compat_merge_from(uint32_t* tsize, const uint32_t* bstart, uint32_t* tbl, const int64_t* pool, int G,
+                                    uint32_t nb, const uint32_t* first_fail, unsigned long long* collisions,
+                                    hipStream_t st);
+// [first, last) records of the chunk-major stream (key2 sorted) in chunks [c0, c1): out[0..1]
+hipError_t launch_compat_chunk_span(const uint64_t* key2, uint64_t n, int kbits, uint32_t c0, uint32_t c1,
+                                    uint64_t* out, hipStream_t st);
+
+// compat_ranks.hip: the ranks' compat tables re-added rank after rank at the bucket owners
+// (pool rows int64 [len, offset, s_0 .. s_{G-1}]; per-bucket offsets nb + 1 words)
+hipError_t launch_rank_rows(const uint32_t* obase, const uint32_t* bstart, const uint32_t* tbl, const int64_t* pool,
+                            int G, uint32_t Tb, uint64_t M, int64_t* rows, hipStream_t st);
+hipError_t launch_rank_lb(const int64_t* pool, int G, uint32_t nA, const uint32_t* offA, const uint32_t* offB,
+                          uint32_t nb, uint32_t nB, uint32_t* lbA, uint32_t* nd, uint32_t* bad, hipStream_t st);
+hipError_t launch_rank_place(const int64_t* pool, int G, uint32_t nA, const uint32_t* offA, const uint32_t* offB,
+                             uint32_t nb, uint32_t nB, const uint32_t* lbA, const uint32_t* ndp, uint32_t* catoff,
+                             uint32_t* tsize, uint32_t* tblcat, hipStream_t st);
+hipError_t launch_rank_check(const int64_t* pool, int G, const uint32_t* catoff, const uint32_t* tsize, uint32_t nb,
+                             uint32_t ncat, const uint32_t* tblcat, uint32_t* bad, hipStream_t st);
+hipError_t launch_rank_exact_init(uint32_t nA, const uint32_t* offA, const uint32_t* offB, const uint32_t* catoff,
+                                  uint32_t nb, uint32_t ncat, const uint32_t* bad, uint32_t* tblcat, uint32_t* tsize,
+                                  uint32_t* first_fail, hipStream_t st);
+hipError_t launch_rank_gather(const int64_t* pool, int G, const uint32_t* catoff, const uint32_t* tsize, uint32_t nb,
+                              uint32_t ncat, const uint32_t* tblcat, const uint32_t* newoff, int64_t* out,
+                              hipStream_t st);
+hipError_t launch_rank_list(const int64_t* rows, int G, uint64_t M, uint64_t* out_len, int64_t* out_s, hipStream_t st);
 
 // restart.hip: MER_REPEAT_LIMIT restart (MatchFinder.cpp:253-277) / start points
 // (MemHash.cpp:117-127) as a fix-up of the merged stream

@@ -63,7 +63,7 @@ struct mums_comm {
         ~Buf() {
             if (p) (void)hipFree(p);
         }
-    } rec, recv, rows, rrows, packed, packed_all, tags, rtags, ents, rents, efk, refk;
+    } rec, recv, rows, rrows, packed, packed_all, tags, rtags, ents, rents, efk, refk, ascii;
     bool packed_done = false;   // packed_all holds this run's genomes (gather_packed)
 };
 
@@ -304,6 +304,101 @@ int gather_packed(mums_ctx* ctx, mums_comm* comm, hipStream_t st) {
     }
     comm->packed_done = true;
     return MUMS_OK;
+}
+
+// ParallelMemHash compat over the ranks (compat_ranks.hip): every rank holds
+// the whole input (an all-gather of the genomes' ASCII) and searches its contiguous range of
+// the chunks with tables of its own (ParallelMemHash.cpp:42-103 on chunks [nch r / W,
+// nch (r + 1) / W)); the tables' buckets go to their owners (balanced hash-bucket ranges, as
+// in MemHash's sharded find), which re-add the ranks' tables rank after rank (MergeTable,
+// :105-121).  The ranks' lists in rank order are the one-thread MatchList (the oracle's rank
+// model, tests/test_compat_logs_cpu.py::test_chunk_range_ranks_model).
+int compat_shard_run(mums_ctx* ctx, mums_comm* comm, int stage, hipStream_t st) {
+    const int W = comm->world, R = comm->rank;
+    uint32_t first = 0, nown = 0;
+    std::vector<uint64_t> lens;
+    AGREE(mums::ctx_compat_layout(ctx, &first, &nown, &lens));
+    const int G = (int)lens.size();
+    std::vector<uint64_t> gofs((size_t)G + 1, 0);
+    for (int g = 0; g < G; ++g) gofs[g + 1] = gofs[g] + lens[g];
+    std::vector<const char*> ptrs((size_t)G, nullptr), own(nown, nullptr);
+    int rc = MUMS_OK;
+    for (uint32_t i = 0; i < nown && rc == MUMS_OK; ++i) {
+        const void* p = nullptr;
+        uint64_t n = 0;
+        rc = mums_genome_device(ctx, i, &p, &n);
+        own[i] = (const char*)p;
+    }
+    AGREE(rc);
+    if (W == 1) {
+        if (first != 0 || nown != (uint32_t)G) return comm_fail(comm, "one rank must own every genome");
+        for (int g = 0; g < G; ++g) ptrs[g] = own[g];
+    } else {   // all-gather(v) of the owned genome blocks (blocks ascend with the rank)
+        std::vector<uint64_t> meta{first, nown}, MT((size_t)2 * W);
+        RC(comm->allgather_u64(meta.data(), 2, MT.data(), st));
+        uint64_t next = 0;
+        for (int p = 0; p < W; ++p) {
+            if (MT[(size_t)2 * p] != next && MT[(size_t)2 * p + 1] != 0)
+                return comm_fail(comm, "genome blocks are not in rank order");
+            next = std::max<uint64_t>(next, MT[(size_t)2 * p] + MT[(size_t)2 * p + 1]);
+        }
+        if (next != (uint64_t)G) return comm_fail(comm, "the ranks' genome blocks do not cover the layout");
+        const uint64_t mine = gofs[first + nown] - gofs[first];
+        rc = (comm->rec.ensure((size_t)W * mine + 64) || comm->ascii.ensure(gofs[G] + 64)) ? MUMS_E_NOMEM : MUMS_OK;
+        for (int p = 0; p < W && rc == MUMS_OK; ++p)
+            for (uint32_t i = 0; i < nown && rc == MUMS_OK; ++i)
+                if (lens[first + i] &&
+                    hipMemcpyAsync((char*)comm->rec.p + (size_t)p * mine + (gofs[first + i] - gofs[first]), own[i],
+                                   lens[first + i], hipMemcpyDeviceToDevice, st) != hipSuccess)
+                    rc = MUMS_E_HIP;
+        AGREE(rc);
+        std::vector<uint64_t> sb(W, mine), rb(W, 0);
+        for (int p = 0; p < W; ++p) {
+            const uint64_t f = MT[(size_t)2 * p], n = MT[(size_t)2 * p + 1];
+            rb[p] = n ? gofs[f + n] - gofs[f] : 0;
+        }
+        RC(comm->alltoallv(comm->rec.p, sb.data(), comm->ascii.p, rb.data(), st));
+        for (int g = 0; g < G; ++g) ptrs[g] = (const char*)comm->ascii.p + gofs[g];
+    }
+    rc = hipStreamSynchronize(st) != hipSuccess ? MUMS_E_HIP : MUMS_OK;
+    if (rc == MUMS_OK) rc = mums::ctx_compat_rank_find(ctx, ptrs.data(), lens.data(), G, (uint32_t)R, (uint32_t)W, stage);
+    AGREE(rc);
+    if (stage != MUMS_STAGE_ALL) return MUMS_OK;
+    uint32_t T = 0, Gt = 0;
+    RC(mums::ctx_table_genomes(ctx, &T, &Gt));
+    std::vector<uint64_t> bc(T, 0), BC((size_t)W * T);
+    uint64_t M = 0;
+    AGREE(mums::ctx_compat_rank_export(ctx, bc.data(), nullptr, &M));
+    RC(comm->allgather_u64(bc.data(), T, BC.data(), st));
+    std::vector<uint64_t> btot(T, 0);
+    for (int r = 0; r < W; ++r)
+        for (uint32_t b = 0; b < T; ++b) btot[b] += BC[(size_t)r * T + b];
+    std::vector<uint32_t> bf, bn;
+    key_ranges(btot, W, bf, bn);
+    const uint64_t rowb = 8ull * (G + 2);
+    rc = comm->ents.ensure((M + 1) * rowb) ? MUMS_E_NOMEM : MUMS_OK;
+    if (rc == MUMS_OK) rc = mums::ctx_compat_rank_export(ctx, bc.data(), (int64_t*)comm->ents.p, &M);
+    AGREE(rc);
+    const uint32_t nb = bn[R];
+    std::vector<uint64_t> cnt((size_t)W * nb), sb(W, 0), rb(W, 0);
+    uint64_t nrecv = 0;
+    for (int p = 0; p < W; ++p)
+        for (uint32_t b = bf[p]; b < bf[p] + bn[p]; ++b) sb[p] += bc[b] * rowb;
+    for (int s2 = 0; s2 < W; ++s2)
+        for (uint32_t j = 0; j < nb; ++j) {
+            cnt[(size_t)s2 * nb + j] = BC[(size_t)s2 * T + bf[R] + j];
+            rb[s2] += cnt[(size_t)s2 * nb + j] * rowb;
+            nrecv += cnt[(size_t)s2 * nb + j];
+        }
+    const void* rows = comm->ents.p;
+    if (W > 1) {
+        AGREE(comm->rents.ensure((nrecv + 1) * rowb) ? MUMS_E_NOMEM : MUMS_OK);
+        RC(comm->alltoallv(comm->ents.p, sb.data(), comm->rents.p, rb.data(), st));
+        rows = comm->rents.p;
+    }
+    rc = hipStreamSynchronize(st) != hipSuccess ? MUMS_E_HIP : MUMS_OK;
+    if (rc == MUMS_OK) rc = mums::ctx_compat_rank_merge(ctx, (const int64_t*)rows, (uint32_t)W, cnt.data(), nb);
+    return agree(comm, rc, st);
 }
 
 // 4b (default). The restart planned where the records are (mums_shard_restart_counts ..
@@ -644,6 +739,10 @@ int mums_shard_run(mums_ctx* ctx, mums_comm* comm, int stage) {
     hipStream_t st = mums::ctx_stream(ctx);
     int rc = hipSetDevice(mums::ctx_device(ctx)) != hipSuccess ? MUMS_E_NODEVICE : MUMS_OK;
     comm->packed_done = false;
+    if (mums::ctx_pcompat(ctx)) {
+        AGREE(rc);
+        return compat_shard_run(ctx, comm, stage, st);
+    }
     // 1-4: sharded seed stage.  Every local step's status is agreed on before the next
     // collective (agree), so one rank's failure never leaves the others waiting in it.
     uint32_t B = 0;

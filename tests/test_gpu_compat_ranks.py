@@ -1,0 +1,103 @@
+"""ParallelMemHash compat over several ranks through the C ABI (mums_shard_run on a compat
+context; compat_ranks.hip): every rank searches a contiguous range of the chunks
+with tables of its own, the bucket owners re-add the ranks' tables rank after rank (MergeTable,
+ParallelMemHash.cpp:105-121).  The ranks' lists in rank order = the one-thread reference's
+MatchList (the oracle restatement, and the reference's own md5 of SURVEY.md Appendix C), bit for
+bit.  Ranks are threads of one process sharing device 0 (the host-staged in-process
+communicator), RCCL (ncclCommInitAll) for one rank."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+PCOMPAT = json.load(open(os.path.join(GOLDEN, "appendix_c.json")))["parallel_compat"]
+
+
+def sharded(lm, seqs, seed, chunk, world, comm="local", table_size=40000):
+    with lm.ShardedMemHash([0] * world, comm=comm, table_size=table_size, parallel_compat=True,
+                           chunk_size=chunk) as sh:
+        sh.SetSeed(seed)
+        ml = sh.FindMatches(seqs)
+        return ml, sh.stats_per_rank
+
+
+def check(gpu_lib, oracle_mod, seqs, w, chunk, world, comm="local", table_size=40000):
+    seed = oracle_mod.get_seed(w)
+    lengths, starts, ost = oracle_mod.find_matches(seqs, seed, parallel_compat=True, chunk_size=chunk,
+                                                   table_size=table_size)
+    ml, st = sharded(gpu_lib, seqs, seed, chunk, world, comm, table_size)
+    assert all(s["chunks"] == ost["chunks"] for s in st)
+    assert len(ml) == len(lengths)
+    assert np.array_equal(ml.lengths, lengths) and np.array_equal(ml.starts, starts)
+    return ost
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4])
+@pytest.mark.parametrize("G,n,p,w,chunk,gseed", [(3, 300_000, 0.03, 15, 3000, 2), (4, 200_000, 0.01, 15, 2000, 3),
+                                                 (3, 200_000, 1.0, 11, 1003, 6), (5, 300_000, 0.02, 17, 4000, 9)])
+def test_compat_ranks_vs_oracle(gpu_lib, oracle_mod, world, G, n, p, w, chunk, gseed):
+    check(gpu_lib, oracle_mod, oracle_mod.generate(G, n, p, gseed), w, chunk, world)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_compat_ranks_exact_merge(gpu_lib, oracle_mod, monkeypatch, world):
+    """MUMS_DEV_COMPAT_RANK_EXACT: every bucket of every owner through the exact sequential
+    merge (compat_merge_fix_kernel from the accumulated prefix) -- the same list as the union
+    path."""
+    monkeypatch.setenv("MUMS_DEV_COMPAT_RANK_EXACT", "1")
+    check(gpu_lib, oracle_mod, oracle_mod.generate(3, 300_000, 0.03, 2), 15, 3000, world)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_compat_ranks_small_table(gpu_lib, oracle_mod, world):
+    """7 hash buckets: few, long bucket vectors per owner (every rank's table interleaves)."""
+    check(gpu_lib, oracle_mod, oracle_mod.generate(4, 200_000, 0.03, 21), 15, 2500, world, table_size=7)
+
+
+def test_compat_ranks_more_ranks_than_chunks(gpu_lib, oracle_mod):
+    """3 chunks over 4 ranks: a rank with an empty chunk range holds an empty table."""
+    seqs = oracle_mod.generate(3, 60_000, 0.02, 4)
+    ost = check(gpu_lib, oracle_mod, seqs, 15, 25_000, 4)
+    assert ost["chunks"] < 4
+
+
+@pytest.mark.parametrize("copies,tandem,chunk,w,world", [(1500, False, 7000, 15, 2), (2000, True, 50_000, 15, 3),
+                                                         (1200, False, 3000, 11, 4)])
+def test_compat_ranks_repeat_limit_cuts(gpu_lib, oracle_mod, copies, tandem, chunk, w, world):
+    """Chunks cut at their first group above MER_REPEAT_LIMIT (decided per chunk before the
+    ranks take their ranges)."""
+    from tests import repeat_inputs
+    seqs = repeat_inputs.high_copy(G=4, n=300_000, copies=copies, tandem=tandem, seed=copies + chunk)
+    ost = check(gpu_lib, oracle_mod, seqs, w, chunk, world)
+    assert ost["restarts"] > 0
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_compat_ranks_known_answer(gpu_lib, oracle_mod, world):
+    """4 x 10 Mbp related: the patched OpenMP reference's MatchList (md5 of its text)."""
+    case = PCOMPAT[0]
+    seqs = oracle_mod.generate(case["G"], case["n"], case["p"], 12345)
+    ml, st = sharded(gpu_lib, seqs, oracle_mod.get_seed(case["w"]), case["chunk_size"], world)
+    assert all(s["chunks"] == case["chunks"] for s in st)
+    assert len(ml) == case["matches"]
+    assert hashlib.md5(ml.text().encode()).hexdigest() == case["md5"]
+
+
+def test_compat_ranks_rccl_one_rank(gpu_lib, oracle_mod):
+    check(gpu_lib, oracle_mod, oracle_mod.generate(3, 300_000, 0.03, 2), 15, 3000, 1, comm="rccl")
+
+
+def test_compat_ranks_refuse_slices(gpu_lib, oracle_mod):
+    """Position slices (the > 2^32 layout) are not a compat layout: refused on every rank."""
+    seqs = oracle_mod.generate(2, 100_000, 0.02, 3)
+    with gpu_lib.ShardedMemHash([0] * 2, comm="local", layout="slices", parallel_compat=True, chunk_size=3000) as sh:
+        sh.SetSeed(oracle_mod.get_seed(15))
+        with pytest.raises(gpu_lib.MumsError):
+            sh.FindMatches(seqs)
+        assert sh.rank_status == [gpu_lib.MUMS_E_UNSUPPORTED] * 2, sh.rank_status

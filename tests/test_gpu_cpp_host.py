@@ -44,6 +44,19 @@ def test_cpp_sharded_known_answers(tool, case, ranks):
     assert hashlib.md5(out).hexdigest() == case["md5"]
 
 
+@pytest.mark.parametrize("ranks", ["", "--gpus 1", "--local 2", "--local 4"])
+def test_cpp_parallel_compat_known_answer(tool, ranks):
+    """ParallelMemHash through the C++ host (mums_set_parallel_compat; sharded:
+    ShardedMemHash::SetParallelCompat, the chunk-range ranks of DESIGN.md §6b) = the patched
+    OpenMP reference's MatchList of SURVEY.md Appendix C (md5 of the text)."""
+    case = json.load(open(os.path.join(GOLDEN, "appendix_c.json")))["parallel_compat"][0]
+    args = [tool] + ranks.split() + ["--compat", str(case["chunk_size"]), "gen", str(case["G"]), str(case["n"]),
+                                     str(case["w"]), str(case["p"])]
+    out = subprocess.run(args, check=True, capture_output=True, timeout=300).stdout
+    assert out.count(b"\n") == case["matches"]
+    assert hashlib.md5(out).hexdigest() == case["md5"]
+
+
 @pytest.mark.parametrize("case", CASES, ids=lambda c: f"G{c['G']}_n{c['n']}_p{c['p']}_{c['mode']}")
 def test_cpp_deferred_sml_known_answers(tool, case):
     """The drop-in SML path (Aligner.cpp:1181-1184, CreateMemorySMLs MatchList.h:409-435):

@@ -78,11 +78,11 @@ def test_shard_run_ib33_wide_seeds(gpu_lib, oracle_mod, G, n, w, p, world, layou
     run(gpu_lib, oracle_mod, G, n, w, p, world, "local", layout=layout)
 
 
-@pytest.mark.parametrize("mode", ["parallel_compat", "pairwise"])
+@pytest.mark.parametrize("mode", ["pairwise"])
 def test_shard_run_refuses_single_gpu_modes(gpu_lib, oracle_mod, mode):
-    """mums_shard_run builds MemHash's MatchParams: a ParallelMemHash compat or a
-    PairwiseMatchFinder context is refused (MUMS_E_UNSUPPORTED), never answered with
-    MemHash's MatchList."""
+    """mums_shard_run builds MemHash's MatchParams: a PairwiseMatchFinder context is refused
+    (MUMS_E_UNSUPPORTED), never answered with MemHash's MatchList.  (ParallelMemHash compat
+    contexts run the chunk-range ranks: tests/test_gpu_compat_ranks.py.)"""
     import ctypes
     lib = gpu_lib.load_library()
     seqs = oracle_mod.generate(2, 20_000, 0.02, 5)

@@ -66,8 +66,15 @@ int main(int argc, char** argv) {
             --argc;
         }
     }
+    uint64_t compat_chunk = 0;   // --compat CHUNK: ParallelMemHash (CHUNK_SIZE = CHUNK)
+    if (argc > 2 && std::string(argv[1]) == "--compat") {
+        compat_chunk = strtoull(argv[2], nullptr, 10);
+        argv += 2;
+        argc -= 2;
+    }
     if (argc < 3) {
-        std::cerr << "usage: mums_find [--gpus N | --local N] [--slices] gen G n weight p [mask] | files weight f1 f2 ...\n";
+        std::cerr << "usage: mums_find [--gpus N | --local N] [--slices] [--compat CHUNK] gen G n weight p [mask] | "
+                     "files weight f1 f2 ...\n";
         return 2;
     }
     std::string mode = argv[1];
@@ -151,6 +158,7 @@ int main(int argc, char** argv) {
             dup2(saved, 1);
             close(saved);
             sh.SetSeed(weight ? (uint64_t)mums_get_seed(weight, 0) : 0);
+            if (compat_chunk) sh.SetParallelCompat(true, compat_chunk);
             for (const auto& s : seqs) sh.AddSequence(s);
             mums::MatchList ml;
             auto t0 = std::chrono::steady_clock::now();
@@ -169,6 +177,8 @@ int main(int argc, char** argv) {
     }
     try {
         mums::MaskedMemHash mh(0);   // mask 0 behaves exactly like MemHash
+        if (compat_chunk && mums_set_parallel_compat(mh.handle(), 1, compat_chunk) != MUMS_OK)
+            throw mums::InvalidData(mums_last_error(mh.handle()));
         if (mask) mh.SetMask(mask);
         else mums_set_mask(mh.handle(), 0, 0);
         mh.SetSeed(weight ? (uint64_t)mums_get_seed(weight, 0) : 0);
