@@ -2560,6 +2560,8 @@ int mums::ctx_compat_rank_merge(mums_ctx* ctx, const int64_t* d_rows, uint32_t W
     if (total >= 0xFFFFFFF0ull) return fail(ctx, MUMS_E_UNSUPPORTED, "compat rank merge: more than 2^32 entries per owner");
     // test hook (read per call): every bucket through the exact sequential merge
     const bool all_exact = getenv("MUMS_DEV_COMPAT_RANK_EXACT") != nullptr;
+    const bool dbg = getenv("MUMS_DEV_COMPAT_RANK_DEBUG") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
     HIPCHK(ctx->rkpool0.ensure((total + 1) * rowb));
     HIPCHK(ctx->rkpool1.ensure((total + 1) * rowb));
     const uint64_t words = 3 * (total + 1) + 8 * ((uint64_t)nb + 2) + 64;
@@ -2608,6 +2610,15 @@ int mums::ctx_compat_rank_merge(mums_ctx* ctx, const int64_t* d_rows, uint32_t W
         HIPCHK(launch_rank_gather(cur, G, catoff, tsz, nb, ncat, tblcat, newoff, nxt, st));
         HIPCHK(hipMemcpyAsync(offA, newoff, (size_t)(nb + 1) * 4, hipMemcpyDeviceToDevice, st));
         HIPCHK(hipStreamSynchronize(st));
+        if (dbg) {   // development: per source, the buckets that took the exact merge
+            std::vector<uint32_t> hb(nb);
+            HIPCHK(hipMemcpy(hb.data(), bad, (size_t)nb * 4, hipMemcpyDeviceToHost));
+            uint64_t nbad = 0;
+            for (uint32_t v : hb) nbad += v != 0;
+            fprintf(stderr, "compat rank merge: source %u A %lu B %lu -> %u entries, %lu of %u buckets exact, %.2f ms\n", s,
+                    (unsigned long)nA, (unsigned long)nB, nF, (unsigned long)nbad, nb,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+        }
         coll += nA + nB - nF;
         nA = nF;
         std::swap(cur, nxt);
