@@ -1004,10 +1004,16 @@ static int parallel_compat_search(memhash_t* h, const oracle_params* prm, int G,
     /* parallel_compat >= 16: R = parallel_compat - 16 ranks, each searching a contiguous chunk
        range into tables of its own (thread table and G start empty, never synced), their G
        tables re-added rank after rank into one at the end (a model of chunk-parallel GPUs) */
-    const uint64_t R = prm->parallel_compat >= 16 ? (uint64_t)(prm->parallel_compat - 16) : 1;
-    bucket_t* gf = R > 1 ? (bucket_t*)calloc(T, sizeof(bucket_t)) : NULL;
+    /* parallel_compat >= 4096: one rank's table alone, R = (pc - 4096) >> 8 ranks, rank       */
+    /* (pc - 4096) & 255 (its chunk range from empty tables; oracle_merge_tables re-adds them) */
+    const int rank_only = prm->parallel_compat >= 4096;
+    const uint64_t R = rank_only ? (uint64_t)((prm->parallel_compat - 4096) >> 8)
+                                 : prm->parallel_compat >= 16 ? (uint64_t)(prm->parallel_compat - 16) : 1;
+    const uint64_t ronly = rank_only ? (uint64_t)((prm->parallel_compat - 4096) & 255) : 0;
+    bucket_t* gf = R > 1 && !rank_only ? (bucket_t*)calloc(T, sizeof(bucket_t)) : NULL;
     uint64_t rank = 0;
     for (uint64_t i = 0; i < nch; ++i) {
+        if (rank_only && (i < nch * ronly / R || i >= nch * (ronly + 1) / R)) continue;
         if (gf && i == nch * rank / R) {   /* a new rank's range: fresh tables */
             for (uint32_t bI = 0; bI < T; ++bI) { h->buckets[bI].n = 0; gb[bI].n = 0; }
             ++rank;
@@ -1057,6 +1063,61 @@ static int parallel_compat_search(memhash_t* h, const oracle_params* prm, int G,
     free(gb); free(lo); free(hi); free(cs);
     res->chunks = nch;
     return 0;
+}
+
+/* MergeTable (ParallelMemHash.cpp:105-121) of ntables tables into one empty table, table   */
+/* after table: every row through merge_entry (AddHashEntry's lower_bound insert or         */
+/* collision).  rows (lens, starts: G per row) hold every table in bucket / vector order,    */
+/* tables concatenated, nrows[t] rows in table t.  The bucket owners' step of the chunk-range */
+/* ranks.  Result: the merged MatchList in bucket order (TEST INFRASTRUCTURE). */
+oracle_result* oracle_merge_tables(int G, uint32_t table_size, const uint64_t* lens, const int64_t* starts,
+                                   const uint64_t* nrows, uint32_t ntables) {
+    if (G < 1 || G > 64 || table_size == 0) return NULL;
+    uint64_t n = 0;
+    for (uint32_t t = 0; t < ntables; ++t) n += nrows[t];
+    memhash_t h;
+    memset(&h, 0, sizeof(h));
+    h.x.G = G;
+    h.table_size = table_size;
+    h.pool = (mhe_t*)calloc(n ? n : 1, sizeof(mhe_t));
+    int64_t* sc = (int64_t*)malloc((n ? n : 1) * (size_t)G * sizeof(int64_t));
+    if (n) memcpy(sc, starts, n * (size_t)G * sizeof(int64_t));
+    bucket_t* b = (bucket_t*)calloc(table_size, sizeof(bucket_t));
+    oracle_result tmp;
+    memset(&tmp, 0, sizeof(tmp));
+    for (uint64_t k = 0; k < n; ++k) {
+        mhe_t* e = &h.pool[k];
+        e->len = (int64_t)lens[k];
+        e->mersize = 0;
+        e->s = sc + k * (uint64_t)G;
+        calc_offset(e, G);
+        const int64_t T = (int64_t)table_size;
+        merge_entry(&h, &b[(uint32_t)(((e->offset % T) + T) % T)], (uint32_t)k, &tmp);
+    }
+    free(tmp.mlog_len);
+    free(tmp.mlog_s);
+    oracle_result* res = (oracle_result*)calloc(1, sizeof(oracle_result));
+    res->G = G;
+    uint64_t M = 0;
+    for (uint32_t bI = 0; bI < table_size; ++bI) M += b[bI].n;
+    res->count = M;
+    res->mem_count = M;
+    res->collision_count = h.collisions;
+    res->lengths = (uint64_t*)malloc((M ? M : 1) * sizeof(uint64_t));
+    res->starts = (int64_t*)malloc((M ? M : 1) * (size_t)G * sizeof(int64_t));
+    uint64_t o = 0;
+    for (uint32_t bI = 0; bI < table_size; ++bI) {
+        for (uint32_t k = 0; k < b[bI].n; ++k, ++o) {
+            const mhe_t* e = &h.pool[b[bI].v[k]];
+            res->lengths[o] = (uint64_t)e->len;
+            memcpy(res->starts + o * (uint64_t)G, e->s, (size_t)G * sizeof(int64_t));
+        }
+        free(b[bI].v);
+    }
+    free(b);
+    free(sc);
+    free(h.pool);
+    return res;
 }
 
 oracle_result* oracle_find_matches(int G, const char* const* seqs, const uint64_t* lens,

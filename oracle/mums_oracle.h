@@ -68,6 +68,9 @@ typedef struct oracle_result oracle_result;
 
 oracle_result* oracle_find_matches(int G, const char* const* seqs, const uint64_t* lens,
                                    const oracle_params* prm);
+/* MergeTable of tables given as rows in bucket order, table after table */
+oracle_result* oracle_merge_tables(int G, uint32_t table_size, const uint64_t* lens, const int64_t* starts,
+                                   const uint64_t* nrows, uint32_t ntables);
 uint64_t oracle_result_count(const oracle_result* r);
 int      oracle_result_seqcount(const oracle_result* r);
 /* lengths[count], starts[count*G] (row-major, signed 1-based, 0 = NO_MATCH) */

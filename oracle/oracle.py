@@ -298,3 +298,56 @@ def std_sort_ids(keys: np.ndarray, depth: int = -1) -> np.ndarray:
     finally:
         L.oracle_std_sort_depth_override(-1)
     return ids
+
+
+def compat_rank_table(seqs: Sequence[bytes], seed: int, chunk_size: int, rank: int, ranks: int,
+                      table_size: int = 40000) -> Tuple[np.ndarray, np.ndarray, dict]:
+    """One rank of the chunk-range model (DESIGN.md §6b): ParallelMemHash::FindMatches on the
+    chunks [nch * rank / ranks, nch * (rank + 1) / ranks) from empty tables; its table in
+    bucket order (oracle parallel_compat = 4096 + (ranks << 8) + rank)."""
+    assert 1 <= ranks < 256 and 0 <= rank < ranks
+    return find_matches(seqs, seed, table_size=table_size, parallel_compat=4096 + (ranks << 8) + rank,
+                        chunk_size=chunk_size)
+
+
+def merge_tables(tables: Sequence[Tuple[np.ndarray, np.ndarray]], G: int,
+                 table_size: int = 40000) -> Tuple[np.ndarray, np.ndarray, dict]:
+    """MergeTable (ParallelMemHash.cpp:105-121) of the given tables (lengths, starts; each in
+    bucket / vector order) into one empty table, table after table (oracle_merge_tables)."""
+    L = lib()
+    L.oracle_merge_tables.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_uint32]
+    L.oracle_merge_tables.restype = ctypes.c_void_p
+    lens = np.ascontiguousarray(np.concatenate([np.asarray(t[0], dtype=np.uint64) for t in tables] or
+                                               [np.zeros(0, np.uint64)]))
+    sts = np.ascontiguousarray(np.concatenate([np.asarray(t[1], dtype=np.int64).reshape(-1, G) for t in tables] or
+                                              [np.zeros((0, G), np.int64)]))
+    nrows = np.array([len(t[0]) for t in tables] or [0], dtype=np.uint64)
+    r = L.oracle_merge_tables(G, table_size, lens.ctypes.data, sts.ctypes.data, nrows.ctypes.data, len(tables))
+    if not r:
+        raise ValueError("oracle rejected input")
+    try:
+        c = L.oracle_result_count(r)
+        lengths = np.zeros(c, dtype=np.uint64)
+        starts = np.zeros((c, G), dtype=np.int64)
+        if c:
+            L.oracle_result_copy(r, lengths.ctypes.data, starts.ctypes.data)
+        stats = dict(mem_count=L.oracle_result_mem_count(r), collision_count=L.oracle_result_collision_count(r))
+    finally:
+        L.oracle_result_free(r)
+    return lengths, starts, stats
+
+
+def entry_buckets(lengths: np.ndarray, starts: np.ndarray, table_size: int = 40000) -> np.ndarray:
+    """Hash bucket of stored entries: CalculateOffset (MatchHashEntry.cpp:141-160) relative to
+    the first start, mod table_size (MemHash.cpp:213)."""
+    s = np.asarray(starts, dtype=np.int64)
+    if s.size == 0:
+        return np.zeros(0, dtype=np.int64)
+    ln = np.asarray(lengths, dtype=np.int64)
+    first = np.argmax(s != 0, axis=1)
+    ref = s[np.arange(len(s)), first]
+    cols = np.arange(s.shape[1])[None, :]
+    t = s - ref[:, None] - np.where(s < 0, ln[:, None], 0)
+    off = np.where((s != 0) & (cols > first[:, None]), t, 0).sum(axis=1)
+    return ((off % table_size) + table_size) % table_size

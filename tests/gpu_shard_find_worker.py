@@ -6,7 +6,8 @@ Every rank runs its genome block (or, with flag "slices", its genome position sl
 (one GPU on the test box; exchanges over gloo) and saves its part of the MatchList (its
 hash-bucket range, bucket-major).  Flag "abi": the whole pipeline runs inside the C ABI
 (mums_shard_run, shard_comm.hip) with the gloo group as its transport (mums_comm_init_host);
-flag "gapped": N-gapped genomes (MER_REPEAT_LIMIT restarts across the ranks).
+flag "gapped": N-gapped genomes (MER_REPEAT_LIMIT restarts across the ranks); flag "compatC":
+ParallelMemHash with CHUNK_SIZE C (with "abi").
 """
 import os
 import sys
@@ -51,6 +52,9 @@ def main():
         first, count = genome_blocks(G, world)[rank]
         local = [torch.frombuffer(bytearray(s), dtype=torch.uint8).to(dev) for s in seqs[first:first + count]]
         eng = HipShardEngine(0, seed, lens, first, local, table_size=T)
+    compat = [int(f[6:]) for f in flags if f.startswith("compat")]
+    if compat:   # ParallelMemHash over the ranks (chunk-range searches)
+        eng.mh._check(eng.mh._lib.mums_set_parallel_compat(eng.mh._ctx, 1, compat[0]))
     if "abi" in flags:
         stage = AbiShardStage(eng, 0, stage=2, comm="host")
         stage.run_find()

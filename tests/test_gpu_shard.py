@@ -139,20 +139,26 @@ def test_sharded_find_matches_gpu(oracle_mod, G, n, p, w, world, T, slices):
                                                      (3, 200_000, 0.05, 19, 3, 7, ("abi",)),
                                                      (2, 300_000, 0.02, 19, 4, 40000, ("abi", "slices")),
                                                      (3, 200_000, 0.01, 15, 2, 40000, ("abi", "gapped")),
-                                                     (2, 240_000, 0.01, 19, 4, 40000, ("abi", "slices", "gapped"))])
+                                                     (2, 240_000, 0.01, 19, 4, 40000, ("abi", "slices", "gapped")),
+                                                     (3, 300_000, 0.03, 15, 2, 40000, ("abi", "compat3000")),
+                                                     (4, 200_000, 0.01, 15, 3, 40000, ("abi", "compat2000"))])
 def test_sharded_abi_multiprocess_gpu(oracle_mod, G, n, p, w, world, T, flags):
     """mums_shard_run (the C++ orchestration of shard_comm.hip: agreement on every rank's
     status, record and row all-to-allv, packed all-gather, restart planning on rank 0) with
     ranks that are separate processes sharing cuda:0, their collectives carried by a gloo
     process group through mums_comm_init_host.  RCCL refuses two ranks on one GPU, so this
     is the multi-process path the one-GPU box can run; the ranks' MatchLists in rank order
-    = the oracle's, bit for bit (N-gapped inputs: restarts planned over all ranks)."""
+    = the oracle's, bit for bit (N-gapped inputs: restarts planned over all ranks; "compatC":
+    ParallelMemHash over the ranks)."""
     import importlib.util
     spec = importlib.util.spec_from_file_location("gsfw", os.path.join(ROOT, "tests", "gpu_shard_find_worker.py"))
     gsfw = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(gsfw)
     seqs = gsfw.genomes(G, n, p, flags)
-    ref_len, ref_st, ref_stats = oracle_mod.find_matches(seqs, oracle_mod.get_seed(w), table_size=T)
+    compat = [int(f[6:]) for f in flags if f.startswith("compat")]
+    ref_len, ref_st, ref_stats = oracle_mod.find_matches(seqs, oracle_mod.get_seed(w), table_size=T,
+                                                         parallel_compat=bool(compat),
+                                                         chunk_size=compat[0] if compat else 0)
     with tempfile.TemporaryDirectory() as d:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
                "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
@@ -168,4 +174,6 @@ def test_sharded_abi_multiprocess_gpu(oracle_mod, G, n, p, w, world, T, flags):
         assert ref_stats["restarts"] > 0
     assert len(lens) == len(ref_len)
     assert (lens == ref_len).all() and (sts == ref_st).all()
-    assert int(stats[0]) == ref_stats["mem_count"] and int(stats[1]) == ref_stats["collision_count"]
+    assert int(stats[0]) == ref_stats["mem_count"]
+    if not compat:   # (compat: the ranks' own collisions plus the owners' re-adds)
+        assert int(stats[1]) == ref_stats["collision_count"]
