@@ -55,6 +55,16 @@ __device__ __forceinline__ unsigned walk_block() {
     return blockIdx.x;
 #endif
 }
+// waves per SIMD the walk kernels are compiled for (0: the compiler's choice, 3 at MG = 8 --
+// ~150 VGPRs); more waves keep more of the walks' dependent loads in flight
+#ifndef MUMS_WALK_WPE
+#define MUMS_WALK_WPE 0
+#endif
+#if MUMS_WALK_WPE
+#define MUMS_WALK_ATTR __attribute__((amdgpu_waves_per_eu(MUMS_WALK_WPE)))
+#else
+#define MUMS_WALK_ATTR
+#endif
 #ifndef MUMS_HIT_BATCH
 #define MUMS_HIT_BATCH 2   // components whose window loads are in flight together (hit_word; A/B round 4: 1 / 2 / 4 / 8)
 #endif   // 64-column hit words per lane before a walk goes to a workgroup
@@ -521,7 +531,7 @@ __global__ __launch_bounds__(kBlock) void walk_line_key_kernel(const WalkItem* _
 // Queued walks, one lane per item, up to kWalkBudget 64-column words each (most chain ends
 // lie within a few words); the rest go on to chain_walk_kernel's lane groups.
 template <int MG, typename View>
-__global__ __launch_bounds__(kBlock) void chain_walk_short_kernel(View v, const uint64_t* __restrict__ probe_info,
+__global__ __launch_bounds__(kBlock) MUMS_WALK_ATTR void chain_walk_short_kernel(View v, const uint64_t* __restrict__ probe_info,
                                                                   GenomeTable gt, MatchParams mp, SeedSpec ss,
                                                                   const uint32_t* __restrict__ packed,
                                                                   const WalkItem* __restrict__ queue,
@@ -714,7 +724,7 @@ constexpr unsigned kWalkHandoff = MUMS_WALK_HANDOFF;
 // xq for the next launch with wider groups -- the few walks of hundreds of steps otherwise
 // set the kernel's duration one step at a time.
 template <int MG, typename View, int GS>
-__global__ __launch_bounds__(kBlock) void chain_walk_kernel(View v, const uint64_t* __restrict__ probe_info,
+__global__ __launch_bounds__(kBlock) MUMS_WALK_ATTR void chain_walk_kernel(View v, const uint64_t* __restrict__ probe_info,
                                                             GenomeTable gt, MatchParams mp, SeedSpec ss,
                                                             const uint32_t* __restrict__ ord,
                                                             const uint32_t* __restrict__ packed,
