@@ -65,6 +65,9 @@ __device__ __forceinline__ unsigned walk_block() {
 #else
 #define MUMS_WALK_ATTR
 #endif
+#ifndef MUMS_HIT_VEC
+#define MUMS_HIT_VEC 1   // hit_word's window loads as one 16-B + one 12-B load (0: one load per word)
+#endif
 #ifndef MUMS_HIT_BATCH
 #define MUMS_HIT_BATCH 2   // components whose window loads are in flight together (hit_word; A/B round 4: 1 / 2 / 4 / 8)
 #endif   // 64-column hit words per lane before a walk goes to a workgroup
@@ -216,6 +219,10 @@ __device__ __forceinline__ LineSpec line_spec(const SeedSpec& ss, const GenomeTa
     return ls;
 }
 
+// 4 / 3 packed words at a dword-aligned address (global_load_dwordx4 / _dwordx3)
+struct __attribute__((aligned(4))) Words4 { uint32_t x, y, z, w; };
+struct __attribute__((aligned(4))) Words3 { uint32_t x, y, z; };
+
 // hit bits of columns c0 .. c0+63 (bit i = column c0 + i) of the line of P
 template <int MG>
 __device__ uint64_t hit_word(int64_t c0, const Mhe<MG>& P, const GenomeTable& gt, int64_t clo, int64_t chi,
@@ -238,6 +245,11 @@ __device__ uint64_t hit_word(int64_t c0, const Mhe<MG>& P, const GenomeTable& gt
     uint64_t acc0 = 0, acc1 = 0, acc2 = 0;
     bool rev = false;
     constexpr int kBatch = MG < MUMS_HIT_BATCH ? MG : MUMS_HIT_BATCH;
+    // wide loads: a window's 7 words as one 16-B and one 12-B load (dword-aligned; the
+    // walks' divergent loads are bound by vector memory instructions -- one address-unit pass
+    // per cache line touched -- not by bytes); the edges of the packed array take the guarded
+    // word loads
+    const bool vec = MUMS_HIT_VEC != 0;
     #pragma unroll
     for (int g0 = 0; g0 < MG; g0 += kBatch) {
         uint32_t w[kBatch][7];
@@ -251,10 +263,22 @@ __device__ uint64_t hit_word(int64_t c0, const Mhe<MG>& P, const GenomeTable& gt
                 const int64_t p = s > 0 ? s - 1 + c0 : -s + ls.L - 2 - c0 - 95;
                 const int64_t wi = (int64_t)gt.woff[g] + (p >> 4);
                 sh[k] = 2 * (int)(p & 15);
-                #pragma unroll
-                for (int i = 0; i < 7; ++i) {
-                    const int64_t q = wi + i;
-                    w[k][i] = (q >= 0 && (uint64_t)q < ls.nwords) ? packed[q] : 0u;
+                if (vec && wi >= 0 && (uint64_t)wi + 7 <= ls.nwords) {
+                    const Words4 a = *reinterpret_cast<const Words4*>(packed + wi);
+                    const Words3 b = *reinterpret_cast<const Words3*>(packed + wi + 4);
+                    w[k][0] = a.x;
+                    w[k][1] = a.y;
+                    w[k][2] = a.z;
+                    w[k][3] = a.w;
+                    w[k][4] = b.x;
+                    w[k][5] = b.y;
+                    w[k][6] = b.z;
+                } else {
+                    #pragma unroll
+                    for (int i = 0; i < 7; ++i) {
+                        const int64_t q = wi + i;
+                        w[k][i] = (q >= 0 && (uint64_t)q < ls.nwords) ? packed[q] : 0u;
+                    }
                 }
             }
         }
@@ -545,7 +569,7 @@ __global__ __launch_bounds__(kBlock) MUMS_WALK_ATTR void chain_walk_short_kernel
     const LineSpec ls = line_spec(ss, gt);
     const unsigned nq = *qcount;
     const unsigned stride = gridDim.x * kBlock;
-    unsigned long long my_words = 0, my_items = 0, my_wins = 0;
+    uint32_t my_words = 0, my_items = 0, my_wins = 0;   // (a lane's walks: a few, <= kWalkBudget words each)
     // block-uniform trip count: block_push synchronises the workgroup
     for (unsigned q0 = walk_block() * kBlock; q0 < nq; q0 += stride) {
         const unsigned q = q0 + threadIdx.x;
@@ -567,7 +591,7 @@ __global__ __launch_bounds__(kBlock) MUMS_WALK_ATTR void chain_walk_short_kernel
             #pragma unroll
             for (int g = 0; g < MG; ++g) npres += (g < gt.G && A.s[g] != 0) ? 1 : 0;
             my_words += nw;
-            my_wins += (unsigned long long)nw * npres;
+            my_wins += nw * (uint32_t)npres;
             ++my_items;
             if (state == 2) {
                 nx[0] = WalkItem{it.j, it.kind, c, it.stop};
@@ -591,9 +615,9 @@ __global__ __launch_bounds__(kBlock) MUMS_WALK_ATTR void chain_walk_short_kernel
             my_wins += __shfl_xor(my_wins, d, 64);
         }
         if ((threadIdx.x & 63) == 0 && my_items) {
-            atomicAdd(&ctr->short_words, my_words);
-            atomicAdd(&ctr->short_items, my_items);
-            atomicAdd(&ctr->short_wins, my_wins);
+            atomicAdd(&ctr->short_words, (unsigned long long)my_words);
+            atomicAdd(&ctr->short_items, (unsigned long long)my_items);
+            atomicAdd(&ctr->short_wins, (unsigned long long)my_wins);
         }
     }
 }

@@ -4,4 +4,4 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r05w
-bash tools/rounds/ab_c3mums.sh default libmems_amd/var/libmums_b1.so libmems_amd/var/libmums_b1w4.so libmems_amd/var/libmums_b2w4.so 2>&1 | tee gpurun_out/r05w/ab.txt
+bash tools/rounds/ab_c3mums.sh default libmems_amd/var/libmums_b4.so libmems_amd/var/libmums_b2w4.so libmems_amd/var/libmums_b1.so 2>&1 | tee gpurun_out/r05w/ab3.txt
