@@ -181,11 +181,16 @@ __global__ __launch_bounds__(kBlock) void chain_keys_kernel(const int64_t* __res
     key_b[c] = ((uint64_t)bucket_of_fast(e[1], table_size, inv_t) << 32) | (bkey ? bkey[c] : __builtin_bitreverse32(m));
 }
 
-__global__ __launch_bounds__(kBlock) void gather_u64_kernel(const uint64_t* __restrict__ src,
-                                                            const uint32_t* __restrict__ idx, uint32_t n,
-                                                            uint64_t* __restrict__ dst) {
+// (bucket, block key) of chain idx[i] packed on kb + bucket bits: the block key's kb
+// significant bits (the bit-reversed G-genome mask sits in the top G of its 32 bits; dense
+// block ranks are < 2^kb) under the bucket, so the sort that follows needs few passes
+__global__ __launch_bounds__(kBlock) void gather_gkey_kernel(const uint64_t* __restrict__ key_b,
+                                                             const uint32_t* __restrict__ idx, uint32_t n,
+                                                             int low_shift, int kb, uint64_t* __restrict__ dst) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i < n) dst[i] = src[idx[i]];
+    if (i >= n) return;
+    const uint64_t b = key_b[idx[i]];
+    dst[i] = ((b >> 32) << kb) | (uint64_t)((uint32_t)b >> low_shift);
 }
 
 // next_s[c] = smallest first-genome start >= c's among the OTHER chains of c's bucket
@@ -1627,11 +1632,21 @@ hipError_t launch_replay_kept(View v, const GenomeTable& gt, const MatchParams& 
     if ((e = radix_sort<uint64_t>(key_s, nullptr, nch, 32, kA, vA, kB, vB, d_radix_tmp, &buf, st)) != hipSuccess)
         return e;
     const uint32_t* ord1 = buf ? vB : vA;
-    hipLaunchKernelGGL(gather_u64_kernel, dim3(cgrid), dim3(kBlock), 0, st, key_b, ord1, nch, key_g);
+    int tb = 1;   // bucket bits
+    while (tb < 32 && ((uint64_t)1 << tb) < (uint64_t)mp.table_size) ++tb;
+    int kb = 32, low_shift = 0;   // block key bits
+    if (!bkey) {
+        kb = gt.G;
+        low_shift = 32 - gt.G;
+    } else {
+        kb = 1;
+        while (kb < 32 && ((uint64_t)1 << kb) < (uint64_t)nch) ++kb;
+    }
+    hipLaunchKernelGGL(gather_gkey_kernel, dim3(cgrid), dim3(kBlock), 0, st, key_b, ord1, nch, low_shift, kb, key_g);
     uint32_t* vin = buf ? vB : vA;
     uint32_t* vout = buf ? vA : vB;
     int buf2 = 0;
-    if ((e = radix_sort<uint64_t>(key_g, vin, nch, 64, kA, vout, kB, vin, d_radix_tmp, &buf2, st)) != hipSuccess)
+    if ((e = radix_sort<uint64_t>(key_g, vin, nch, kb + tb, kA, vout, kB, vin, d_radix_tmp, &buf2, st)) != hipSuccess)
         return e;
     const uint32_t* ord = buf2 ? vin : vout;
     hipLaunchKernelGGL(chain_next_kernel, dim3(cgrid), dim3(kBlock), 0, st, ord, key_s, key_b, nch, next_s, rank);
