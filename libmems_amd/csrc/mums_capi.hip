@@ -673,12 +673,17 @@ int find_tail(mums_ctx* ctx, const MatchParams& mp, const uint32_t* packed, Rows
     HIPCHK(ctx->radix_tmp.ensure(std::max(radix_tmp_bytes(ctx->P + 1),
                                           chain_radix_tmp_bytes(std::min<uint64_t>(ctx->P, find_chunk()) + 1))));
     HIPCHK(ctx->tmp.ensure(std::max(scan_tmp_bytes(ctx->P + 1), scan_tmp_bytes(Tb))));
-    HIPCHK(hipMemsetAsync(&dc->max_bucket, 0, 4, st));
     HIPCHK(hipMemsetAsync(ctx->bstart.p, 0, (size_t)Tb * 4, st));
     HIPCHK(hipMemsetAsync(ctx->bend.p, 0, (size_t)Tb * 4, st));
     HIPCHK(hipMemsetAsync(ctx->tsize.p, 0, (size_t)Tb * 4, st));
-    HIPCHK(launch_bucket_ranges(ctx->sorted_buckets, ctx->P, ctx->bstart.as<uint32_t>(), ctx->bend.as<uint32_t>(),
-                                &dc->max_bucket, st));
+    if (ctx->sorted_buckets || ctx->P == 0) {
+        HIPCHK(hipMemsetAsync(&dc->max_bucket, 0, 4, st));
+        HIPCHK(launch_bucket_ranges(ctx->sorted_buckets, ctx->P, ctx->bstart.as<uint32_t>(),
+                                    ctx->bend.as<uint32_t>(), &dc->max_bucket, st));
+    } else {   // no bucket order (finish_seeds): the replay sizes its LDS vectors from the kept probes
+        if (chunked) return fail(ctx, MUMS_E_HIP, "sliced FindMatches without the probes' bucket order (internal error)");
+        HIPCHK(hipMemsetAsync(&dc->max_bucket, 0xFF, 4, st));
+    }
     ctx->emit_tbl = ctx->tbl.as<uint32_t>();
     ctx->emit_base = ctx->bstart.as<uint32_t>();
     if (ctx->P == 0) HIPCHK(hipEventRecord(ctx->ev[EV_CHAINS], st));
@@ -941,7 +946,10 @@ int merge_stage(mums_ctx* ctx, uint64_t n, int mb, int key_bits, const MatchPara
 
 // After the groups stage: counters to the host, error flags, then the probes grouped
 // by hash bucket (stable: key order kept inside a bucket; values = probe ids) (A10).
-int finish_seeds(mums_ctx* ctx, const ProbeSpace& ps, hipStream_t st) {
+// find_follows: FindMatches runs next on this context; its one-pass replay (launch_replay_kept)
+// orders only the kept probes by bucket, so the bucket order of all probes is skipped there
+// (MUMS_DEV_KEEP_BUCKET_ORDER, read per call: sort them anyway)
+int finish_seeds(mums_ctx* ctx, const ProbeSpace& ps, hipStream_t st, bool find_follows = false) {
     DevCounters* dc = ctx->counters.as<DevCounters>();
     HIPCHK(hipMemcpyAsync(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -954,6 +962,12 @@ int finish_seeds(mums_ctx* ctx, const ProbeSpace& ps, hipStream_t st) {
     int tbits = 1;
     while (tbits < 32 && ((uint64_t)1 << tbits) < (uint64_t)ctx->table_size) ++tbits;
     const uint64_t P = ctx->P;
+    if (find_follows && P > 0 && P <= find_chunk() && !ctx->shard && !getenv("MUMS_DEV_KEEP_BUCKET_ORDER")) {
+        ctx->sorted_buckets = nullptr;
+        ctx->sorted_ids = nullptr;
+        HIPCHK(hipEventRecord(ctx->ev[EV_BUCKETS], st));
+        return MUMS_OK;
+    }
     // the onesweep variant (MUMS_DEV_BUCKET_ONESWEEP) moves packed 8-B records: 2.36 vs 1.56 ms
     // on C3's 1e8 probes (u32 keys and ids in the radix passes move fewer bytes)
     const bool radix = getenv("MUMS_DEV_BUCKET_ONESWEEP") == nullptr;
@@ -1394,7 +1408,7 @@ int run_pipeline(mums_ctx* ctx, int stage) {
                                                      ps.slot_info, ps.slot_bucket, st);
     }
     if (rc) return rc;
-    rc = finish_seeds(ctx, ps, st);
+    rc = finish_seeds(ctx, ps, st, stage >= MUMS_STAGE_ALL);
     if (rc) return rc;
     rc = restart_stage(ctx, mp, ps, st);
     if (rc) return rc;
@@ -1833,7 +1847,7 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
             ctx, PairView<uint64_t>{(const uint64_t*)ctx->sorted_key, ctx->sorted_idx}, tiles,
             (n_live + kSegTile - 1) / kSegTile, mp, ps.probe_info, ps.probe_bucket, ps.slot_info, ps.slot_bucket, st);
     if (rc) return rc;
-    rc = finish_seeds(ctx, ps, st);
+    rc = finish_seeds(ctx, ps, st, stage >= MUMS_STAGE_ALL);
     if (rc) return rc;
     ctx->compat_pfirst.clear();
     if (ctx->match_log) {   // the probes of every chunk (the match log's per-chunk order)

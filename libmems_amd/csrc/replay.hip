@@ -1262,6 +1262,11 @@ hipError_t replay_tail(View v, const GenomeTable& gt, const MatchParams& mp, int
         if ((e = hipMemcpyAsync(hb.data(), cbeg, mp.table_size * 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
         if ((e = hipMemcpyAsync(he.data(), cend, mp.table_size * 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+        // the LDS vector of the big-bucket kernel: at most the fullest bucket's kept probes (a
+        // bucket's vector holds <= its kept probes; a larger one would spill, correctly)
+        uint32_t kmax = 0;
+        for (uint32_t b = 0; b < mp.table_size; ++b) kmax = std::max(kmax, he[b] - hb[b]);
+        lds_cap = std::min(lds_cap, kmax);
         for (uint32_t b = 0; b < mp.table_size; ++b) {
             const uint32_t beg = hb[b], K = he[b] - hb[b];
             if (K <= big_min) continue;
