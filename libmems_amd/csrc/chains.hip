@@ -926,11 +926,40 @@ __global__ __launch_bounds__(kBlock) void chain_entry_kernel(View v, const uint6
 // of packed 8-B records (radix_seg.hip): first (x << 32 | k) by x (written by the probe
 // producer, chain_line_slots), then (hash << 32 | position after the first sort) by hash;
 // ord[j] = the probe at line position j
+// The records carry the hash sort's keys, so its four digit histograms are counted here
+// (hh: 4 x 256, zeroed) instead of by a histogram read of the records (seg_onesweep_sort
+// hist_in).  Grid-stride; in x order most hashes repeat (a line's probes, the main diagonal
+// above all): a wave adds the lanes equal to its first lane's hash with one LDS add per digit.
 __global__ __launch_bounds__(kBlock) void line_rec2_kernel(const uint32_t* __restrict__ lhash,
                                                            const uint64_t* __restrict__ s1, uint64_t P,
-                                                           uint64_t* __restrict__ rec) {
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < P) rec[i] = ((uint64_t)lhash[(uint32_t)s1[i]] << 32) | i;
+                                                           uint64_t* __restrict__ rec, uint32_t* __restrict__ hh) {
+    __shared__ uint32_t h[4][256];
+    for (int i = threadIdx.x; i < 4 * 256; i += kBlock) (&h[0][0])[i] = 0;
+    __syncthreads();
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    const uint64_t Pr = (P + kBlock - 1) / kBlock * kBlock;   // uniform trip count (ballots)
+    const int lane = threadIdx.x & 63;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < Pr; i += stride) {
+        const bool valid = i < P;
+        const uint32_t hv = valid ? lhash[(uint32_t)s1[i]] : 0u;
+        if (valid) rec[i] = ((uint64_t)hv << 32) | i;
+        const uint32_t v0 = __builtin_amdgcn_readfirstlane(hv);
+        const uint64_t m = __ballot(valid && hv == v0);
+        if (m && lane == __builtin_ctzll(m)) {
+            const uint32_t c = (uint32_t)__popcll(m);
+            #pragma unroll
+            for (int d = 0; d < 4; ++d) atomicAdd(&h[d][(v0 >> (8 * d)) & 0xFFu], c);
+        }
+        if (valid && hv != v0) {
+            #pragma unroll
+            for (int d = 0; d < 4; ++d) atomicAdd(&h[d][(hv >> (8 * d)) & 0xFFu], 1u);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 4 * 256; i += kBlock) {
+        const uint32_t c = (&h[0][0])[i];
+        if (c) atomicAdd(&hh[i], c);
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void line_ord_kernel(const uint64_t* __restrict__ s1,
@@ -1141,7 +1170,8 @@ size_t chain_tmp_bytes(uint64_t P, uint32_t Tb, int G) {
     // + seg (4) + queues (2 x 24) + padding.  The replay reuses it: per chain <= 76 B, then the
     // big-bucket scratch (count 4 + scan 4 + slot 16 per probe, + 4 per bucket)
     // + the probe rows in line order ((G + 1) x 8)
-    return P * (24 + 8 + 1 + 24 + 4 + 2 * sizeof(WalkItem) + 32 + 24 + 8 * (uint64_t)(G + 1)) + (uint64_t)Tb * 4 + 64 * 64;
+    return P * (24 + 8 + 1 + 24 + 4 + 2 * sizeof(WalkItem) + 32 + 24 + 8 * (uint64_t)(G + 1)) + (uint64_t)Tb * 4 + 64 * 64 +
+           4 * 256 * 4 + 256;   // + the line hashes' digit histograms (line_rec2_kernel)
 }
 
 namespace {
@@ -1157,6 +1187,7 @@ struct ChainWs {
     unsigned int* qcount;
     int64_t* rows_line;
     uint32_t* bst;   // {0, P}: the one bucket of the line sort
+    uint32_t* hh;    // 4 x 256: the line hashes' digit histograms (the hash sort's passes)
 };
 
 ChainWs chain_ws(void* d_chain_tmp, uint64_t P, int G, bool with_rows) {
@@ -1181,6 +1212,7 @@ ChainWs chain_ws(void* d_chain_tmp, uint64_t P, int G, bool with_rows) {
     w.queue_long = (WalkItem*)carve(P * sizeof(WalkItem));
     w.qcount = (unsigned int*)carve(64);
     w.bst = (uint32_t*)carve(64);
+    w.hh = (uint32_t*)carve(4 * 256 * 4);
     w.rows_line = with_rows ? (int64_t*)carve(P * (uint64_t)(G + 1) * 8) : nullptr;
     return w;
 }
@@ -1197,13 +1229,16 @@ hipError_t line_sort(const ChainWs& w, uint64_t P, int xbits, void* d_tmp, uint3
     if ((e = seg_onesweep_sort(w.kA, w.kB, P, xbits, 0, w.bst, d_tmp, d_err, &b1, st)) != hipSuccess) return e;
     const uint64_t* s1 = b1 ? w.kB : w.kA;
     uint64_t* r2 = b1 ? w.kA : w.kB;
-    hipLaunchKernelGGL(line_rec2_kernel, dim3(grid_of(P)), dim3(kBlock), 0, st, (const uint32_t*)w.vB, s1, P, r2);
+    const bool fused_hist = kLineHashBits == 32 && !getenv("MUMS_DEV_LINE_GHIST");   // read per call
+    if ((e = hipMemsetAsync(w.hh, 0, 4 * 256 * 4, st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(line_rec2_kernel, dim3((unsigned)std::min<uint64_t>(grid_of(P), 4096)), dim3(kBlock), 0, st,
+                       (const uint32_t*)w.vB, s1, P, r2, w.hh);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     int b2 = 0;
     // the hashes in x order come in runs (a line's probes): run-aware histogram, late publish
     const bool runs = !getenv("MUMS_DEV_LINE_NORUNS");   // read per call (tests toggle it)
     if ((e = seg_onesweep_sort(r2, w.lkey, P, kLineHashBits, 0, w.bst, d_tmp, d_err, &b2, st, nullptr, 32, false,
-                               runs)) != hipSuccess)
+                               runs, fused_hist ? w.hh : nullptr)) != hipSuccess)
         return e;
     const uint64_t* s2 = b2 ? w.lkey : r2;
     hipLaunchKernelGGL(line_ord_kernel, dim3(grid_of(P)), dim3(kBlock), 0, st, s1, s2, P, w.vA);

@@ -237,7 +237,9 @@ size_t onesweep_tmp_bytes(uint64_t n, int msd_bits, int key_bits);
 hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key_bits, int msd_bits,
                              const uint32_t* d_bstart, void* d_tmp, uint32_t* d_err, int* out_buf, hipStream_t st,
                              hipEvent_t* ev_ds = nullptr, int key_shift = 32, bool mask_parity = false,
-                             bool key_runs = false);
+                             bool key_runs = false, const uint32_t* hist_in = nullptr);
+// hist_in: one bucket's digit histograms of every pass (npass x 256), counted by the records'
+// producer: no histogram read of the records
 // key_runs: the keys come in runs of equal digits (the line sort's hashes in x order): the
 // histogram adds once per run and the passes publish their counts after the ranking
 // mask_parity: the segment fix-up leaves key bit 0 (the parity / orientation bit) out of

@@ -1322,7 +1322,8 @@ hipError_t seg_parity_fix(uint64_t* rec, uint64_t* scratch, uint64_t n, int key_
 
 hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key_bits, int msd_bits,
                              const uint32_t* d_bstart, void* d_tmp, uint32_t* d_err, int* out_buf, hipStream_t st,
-                             hipEvent_t* ev_ds, int key_shift, bool mask_parity, bool key_runs) {
+                             hipEvent_t* ev_ds, int key_shift, bool mask_parity, bool key_runs,
+                             const uint32_t* hist_in) {
     const int nkd = (key_bits + 7) / 8;                  // key digits
     const bool segfix = nkd >= 2 && seg_segfix_enabled();
     const int npass = segfix ? nkd - 1 : nkd;            // onesweep launches (digits above the lowest)
@@ -1363,8 +1364,13 @@ hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key
     // the histogram read counts digit 0 only when every later pass's digits are
     // counted by the pass before it (MUMS_OS_NEXTHIST, plain onesweep kernel)
     const bool nexthist = MUMS_OS_NEXTHIST && !MUMS_SORT_PERSIST;
-    hipLaunchKernelGGL(seg_ghist_kernel, dim3(gblocks), dim3(kBlock), 0, st, recA, stiles, ub, npass, ghist,
-                       key_shift, nexthist ? 1 : npass, key_runs ? 1 : 0);
+    if (hist_in && nb == 1 && !segfix && !nexthist) {   // the producer counted every pass's digits
+        e = hipMemcpyAsync(ghist, hist_in, (size_t)npass * kDigits * 4, hipMemcpyDeviceToDevice, st);
+        if (e != hipSuccess) return e;
+    } else {
+        hipLaunchKernelGGL(seg_ghist_kernel, dim3(gblocks), dim3(kBlock), 0, st, recA, stiles, ub, npass, ghist,
+                           key_shift, nexthist ? 1 : npass, key_runs ? 1 : 0);
+    }
     if (nexthist)
         hipLaunchKernelGGL(seg_dbase_kernel, dim3((unsigned)nb), dim3(kBlock), 0, st, ghist, d_bstart, npass, dbase,
                            0);
