@@ -509,17 +509,24 @@ __global__ __launch_bounds__(kBlock) void chain_link_kernel(View v, const uint64
     block_push<kLinkIPT>(want, it, queue, qcount);
 }
 
-// segment starts (first probe, or the previous probe not linked) walk left to the chain start
+// segment starts (first probe, or the previous probe not linked) walk left to the chain start;
+// seg[j] = 1 at segment starts (scanned to segment ids after the walks: the links are final
+// after pass 0, the left walks only find where each chain begins)
 __global__ __launch_bounds__(kBlock) void chain_left_kernel(uint64_t P, const uint8_t* __restrict__ link,
                                                             WalkItem* __restrict__ queue,
-                                                            unsigned int* __restrict__ qcount) {
+                                                            unsigned int* __restrict__ qcount,
+                                                            uint32_t* __restrict__ seg) {
     uint32_t want = 0;
     WalkItem it[kLinkIPT];
     #pragma unroll
     for (int i = 0; i < kLinkIPT; ++i) {
         const uint64_t j = (uint64_t)blockIdx.x * (kBlock * kLinkIPT) + (uint64_t)i * kBlock + threadIdx.x;
         it[i] = WalkItem{(uint32_t)j, 2, 0, INT64_MIN};
-        if (j < P && (j == 0 || !link[j - 1])) want |= 1u << i;
+        if (j < P) {
+            const bool start = j == 0 || !link[j - 1];
+            seg[j] = start ? 1u : 0u;
+            if (start) want |= 1u << i;
+        }
     }
     block_push<kLinkIPT>(want, it, queue, qcount);
 }
@@ -851,14 +858,6 @@ __global__ __launch_bounds__(kBlock) MUMS_WALK_ATTR void chain_walk_kernel(View 
     }
 }
 
-// seg[j] = 1 at segment starts (scanned to segment ids afterwards)
-__global__ __launch_bounds__(kBlock) void chain_flag_kernel(const uint8_t* __restrict__ link, uint64_t P,
-                                                            uint32_t* __restrict__ seg) {
-    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (j >= P) return;
-    seg[j] = (j == 0 || !link[j - 1]) ? 1u : 0u;
-}
-
 // chain of every probe; fk[chain] = its first probe in key order (kbase + the least ord[j]
 // of the segment: a segmented min over the wave, one atomicMin per segment and wave)
 __global__ __launch_bounds__(kBlock) void chain_seg_kernel(const uint8_t* __restrict__ link,
@@ -911,14 +910,23 @@ __global__ __launch_bounds__(kBlock) void chain_entry_kernel(View v, const uint6
     const int64_t xa = start_at(A, first_start(A));
     const int64_t cmin = lcol[j] - xa, cmax = seg_r[s] - xa;
     int64_t* e = pool + (uint64_t)s * (uint64_t)(gt.G + 2);
-    e[0] = cmax - cmin + L;
-    e[1] = A.offset;
+    int64_t w[MG + 2];
+    w[0] = cmax - cmin + L;
+    w[1] = A.offset;
     #pragma unroll
     for (int g = 0; g < MG; ++g) {
-        if (g < gt.G) {
-            const int64_t sg = A.s[g];
-            e[2 + g] = sg > 0 ? sg + cmin : (sg < 0 ? -((-sg) - cmax) : 0);
-        }
+        const int64_t sg = A.s[g];
+        w[2 + g] = sg > 0 ? sg + cmin : (sg < 0 ? -((-sg) - cmax) : 0);
+    }
+    if ((gt.G & 1) == 0) {   // 16-B stores (the entry is (G + 2) x 8 B, 16-B aligned for even G)
+        #pragma unroll
+        for (int q = 0; q < MG + 2; q += 2)
+            if (q < gt.G + 2) *reinterpret_cast<int4*>(e + q) = make_int4((int)w[q], (int)(w[q] >> 32), (int)w[q + 1],
+                                                                          (int)(w[q + 1] >> 32));
+    } else {
+        #pragma unroll
+        for (int q = 0; q < MG + 2; ++q)
+            if (q < gt.G + 2) e[q] = w[q];
     }
 }
 
@@ -1237,11 +1245,17 @@ hipError_t line_sort(const ChainWs& w, uint64_t P, int xbits, void* d_tmp, uint3
     int b2 = 0;
     // the hashes in x order come in runs (a line's probes): run-aware histogram, late publish
     const bool runs = !getenv("MUMS_DEV_LINE_NORUNS");   // read per call (tests toggle it)
+    // the last hash pass stores ord[o] = probe of s1[j] directly (MUMS_DEV_LINE_ORD=1, read per
+    // call: the records, then line_ord_kernel's gather)
+    const bool fused_ord = runs && !getenv("MUMS_DEV_LINE_ORD");
     if ((e = seg_onesweep_sort(r2, w.lkey, P, kLineHashBits, 0, w.bst, d_tmp, d_err, &b2, st, nullptr, 32, false,
-                               runs, fused_hist ? w.hh : nullptr)) != hipSuccess)
+                               runs, fused_hist ? w.hh : nullptr, fused_ord ? s1 : nullptr,
+                               fused_ord ? w.vA : nullptr)) != hipSuccess)
         return e;
-    const uint64_t* s2 = b2 ? w.lkey : r2;
-    hipLaunchKernelGGL(line_ord_kernel, dim3(grid_of(P)), dim3(kBlock), 0, st, s1, s2, P, w.vA);
+    if (!fused_ord) {
+        const uint64_t* s2 = b2 ? w.lkey : r2;
+        hipLaunchKernelGGL(line_ord_kernel, dim3(grid_of(P)), dim3(kBlock), 0, st, s1, s2, P, w.vA);
+    }
     *ord_out = w.vA;
     return hipGetLastError();
 }
@@ -1288,7 +1302,7 @@ hipError_t chains_core(LV vl, const ChainWs& w, const uint32_t* ord, uint64_t P,
                                mp, ss, w.link, w.queue, qshort, qcount + 12, jl ? jl + 2 * P : nullptr);
         else
             hipLaunchKernelGGL(chain_left_kernel, dim3(lgrid), dim3(kBlock), 0, st, P, (const uint8_t*)w.link, w.queue,
-                               qshort);
+                               qshort, w.seg);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         const uint64_t* order = nullptr;
         if (wsort) {   // the queue length sizes the sort: read back (one small sync per pass)
@@ -1360,8 +1374,7 @@ hipError_t chains_core(LV vl, const ChainWs& w, const uint32_t* ord, uint64_t P,
                     hq[8]);
         }
     }
-    hipLaunchKernelGGL(chain_flag_kernel, dim3(grid), dim3(kBlock), 0, st, w.link, P, w.seg);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // (the segment-start flags in w.seg: chain_left_kernel)
     if ((e = exclusive_scan_u32(w.seg, P, d_scan_tmp, d_nchains, st)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(fk, 0xFF, P * 4, st)) != hipSuccess) return e;
     hipLaunchKernelGGL(chain_seg_kernel, dim3(grid), dim3(kBlock), 0, st, w.link, ord, w.seg, P, w.rcol, chain_of,

@@ -382,6 +382,12 @@ __global__ void flat_tiles_kernel(uint64_t N, uint64_t nt, SegTile* __restrict__
 // probe_info) as one batch of independent loads (probe_row_fast).  lkey / fsk (optional):
 // the chain labelling's line key (chains.hip) and the first-genome start of probe k, so
 // neither re-reads the rows.
+#ifndef MUMS_MAT_WIDE
+#define MUMS_MAT_WIDE 1   // materialize: a group's records as 16-B loads (0: one 8-B load each)
+#endif
+constexpr bool kMatWide = MUMS_MAT_WIDE != 0;
+struct __attribute__((aligned(8))) Rec2 { uint64_t a, b; };
+
 template <int MG, typename View, bool kGl = false>
 __global__ __launch_bounds__(kBlock) void probe_materialize_kernel(View v, const uint64_t* __restrict__ probe_info,
                                                                    uint64_t P, GenomeTable gt, MatchParams mp, int L,
@@ -409,8 +415,21 @@ __global__ __launch_bounds__(kBlock) void probe_materialize_kernel(View v, const
         if constexpr (RecIB<View>::value > 0) {
             if (mp.repeat_tol == 0 && mp.enum_tol == 1 && gsz <= (uint32_t)MG) {
                 uint64_t x[MG];
-                #pragma unroll
-                for (int q = 0; q < MG; ++q) x[q] = (uint32_t)q < gsz ? v.rec[h + q] : ~0ull;
+                if constexpr (MG % 2 == 0 && kMatWide) {
+                    // two records per 16-B load: the lanes' groups lie apart, so each load
+                    // instruction is an address-unit pass over up to 64 cache lines; the record
+                    // after a group's last is read and dropped (the buffers end in >= 8 spare)
+                    #pragma unroll
+                    for (int q = 0; q < MG; q += 2) {
+                        Rec2 t{~0ull, ~0ull};
+                        if ((uint32_t)q < gsz) t = *reinterpret_cast<const Rec2*>(v.rec + h + q);
+                        x[q] = t.a;
+                        x[q + 1] = (uint32_t)(q + 1) < gsz ? t.b : ~0ull;
+                    }
+                } else {
+                    #pragma unroll
+                    for (int q = 0; q < MG; ++q) x[q] = (uint32_t)q < gsz ? v.rec[h + q] : ~0ull;
+                }
                 probe_row_fast<MG, RecIB<View>::value, use_gl>(x, gsz, gt, L, Q, &glk);
                 done = true;
             }

@@ -237,7 +237,11 @@ size_t onesweep_tmp_bytes(uint64_t n, int msd_bits, int key_bits);
 hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key_bits, int msd_bits,
                              const uint32_t* d_bstart, void* d_tmp, uint32_t* d_err, int* out_buf, hipStream_t st,
                              hipEvent_t* ev_ds = nullptr, int key_shift = 32, bool mask_parity = false,
-                             bool key_runs = false, const uint32_t* hist_in = nullptr);
+                             bool key_runs = false, const uint32_t* hist_in = nullptr,
+                             const uint64_t* gsrc = nullptr, uint32_t* gout = nullptr);
+// gsrc / gout (key_runs only): the last pass writes gout[o] = low 32 bits of gsrc[low 32 bits of
+// the record] instead of the record (a permutation gather at the store; the records of that
+// pass are not written)
 // hist_in: one bucket's digit histograms of every pass (npass x 256), counted by the records'
 // producer: no histogram read of the records
 // key_runs: the keys come in runs of equal digits (the line sort's hashes in x order): the

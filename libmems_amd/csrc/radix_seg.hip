@@ -434,7 +434,9 @@ __device__ __forceinline__ void onesweep_load(const uint64_t* __restrict__ rin, 
 // 256 threads also own one digit each for the look-back and the digit starts.
 // kAlias: the per-wave digit counts live in the record exchange buffer (every lane folds
 // its slot base into its ranks before the exchange), so a tile costs kT * 8 B + 4 KB of LDS.
-template <int OB, int kIPT, bool kAlias = false, bool kLate = false>
+// kGath (the line sort's last pass): instead of record k, gout[o] = low 32 bits of
+// gsrc[low 32 bits of k] -- the permutation gather of the caller, done at the store
+template <int OB, int kIPT, bool kAlias = false, bool kLate = false, bool kGath = false>
 __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __restrict__ rin,
                                                           uint64_t* __restrict__ rout,
                                                           const SegTile* __restrict__ tiles, uint32_t nclaims,
@@ -442,7 +444,9 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
                                                           const uint32_t* __restrict__ dbase, uint32_t* status,
                                                           uint32_t* tile_counter, uint32_t* err,
                                                           uint32_t* __restrict__ ghist_next,
-                                                          const uint32_t* __restrict__ xq) {
+                                                          const uint32_t* __restrict__ xq,
+                                                          const uint64_t* __restrict__ gsrc = nullptr,
+                                                          uint32_t* __restrict__ gout = nullptr) {
     constexpr int kT = kIPT * OB;
     constexpr bool late = MUMS_OS_LATEPUB || kLate;
     constexpr int kW = OB / 64;
@@ -649,11 +653,15 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
 #else
             const uint64_t o = (uint64_t)gofs[dg] + (sidx - lstart[dg]);
 #endif
+            if constexpr (kGath) {
+                gout[o] = (uint32_t)gsrc[(uint32_t)k];
+            } else {
 #if MUMS_SORT_NT & 2
-            __builtin_nontemporal_store(k, rout + o);
+                __builtin_nontemporal_store(k, rout + o);
 #else
-            rout[o] = k;
+                rout[o] = k;
 #endif
+            }
         }
     }
     if (ghist_next && tid < kDigits) {   // hnext complete: barriers since its atomics
@@ -1323,7 +1331,7 @@ hipError_t seg_parity_fix(uint64_t* rec, uint64_t* scratch, uint64_t n, int key_
 hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key_bits, int msd_bits,
                              const uint32_t* d_bstart, void* d_tmp, uint32_t* d_err, int* out_buf, hipStream_t st,
                              hipEvent_t* ev_ds, int key_shift, bool mask_parity, bool key_runs,
-                             const uint32_t* hist_in) {
+                             const uint32_t* hist_in, const uint64_t* gsrc, uint32_t* gout) {
     const int nkd = (key_bits + 7) / 8;                  // key digits
     const bool segfix = nkd >= 2 && seg_segfix_enabled();
     const int npass = segfix ? nkd - 1 : nkd;            // onesweep launches (digits above the lowest)
@@ -1406,11 +1414,15 @@ hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key
             uint32_t* tc = xq ? counters + 128 + 8 * p : counters + p;
 #define MUMS_OS_LAUNCH(OB, IPT, AL)                                                                               \
     hipLaunchKernelGGL((seg_onesweep_kernel<OB, IPT, AL>), dim3((unsigned)ub), dim3(OB), 0, st, src, dst, otiles, \
-                       (uint32_t)ub, sh, p, npass, dbase, sp, tc, d_err, gn, xq)
-            if (key_runs) {   // equal-digit runs: publish after the ranking (no per-record LDS atomics)
+                       (uint32_t)ub, sh, p, npass, dbase, sp, tc, d_err, gn, xq, nullptr, nullptr)
+            if (key_runs && gout && p + 1 == npass) {   // the last pass stores gout[o] = gsrc[k]
+                hipLaunchKernelGGL((seg_onesweep_kernel<kSortBlock, kSortTile / kSortBlock, true, true, true>),
+                                   dim3((unsigned)ub), dim3(kSortBlock), 0, st, src, dst, otiles, (uint32_t)ub, sh, p,
+                                   npass, dbase, sp, tc, d_err, gn, xq, gsrc, gout);
+            } else if (key_runs) {   // equal-digit runs: publish after the ranking (no per-record LDS atomics)
                 hipLaunchKernelGGL((seg_onesweep_kernel<kSortBlock, kSortTile / kSortBlock, true, true>),
                                    dim3((unsigned)ub), dim3(kSortBlock), 0, st, src, dst, otiles, (uint32_t)ub, sh, p,
-                                   npass, dbase, sp, tc, d_err, gn, xq);
+                                   npass, dbase, sp, tc, d_err, gn, xq, nullptr, nullptr);
             } else
             switch (os_variant()) {
             case 1: MUMS_OS_LAUNCH(512, 16, true); break;
