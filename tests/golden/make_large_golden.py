@@ -10,6 +10,8 @@ box checks the HIP path against them without re-running the oracle for minutes):
       w15, with 20 N runs of 900-3200 bases per genome (tests/tie_inputs.multi_gap, seed
       4246): every chunk holding an N run meets the all-A seed group above MER_REPEAT_LIMIT
       and is cut there (ParallelMemHash.cpp:97) -> matches, md5, chunks, cut chunks.
+  pc_c3shape: ParallelMemHash (chunk 200 000) at BASELINE config 3's shape scaled to
+      8 x 10 Mbp (w19, G = 8), the one-thread schedule with a MergeTable after every chunk.
 
     python tests/golden/make_large_golden.py [c3] [c5s]   (c3: about 15 minutes, ~25 GB RAM)
 """
@@ -29,6 +31,10 @@ CASES = {
     # BASELINE config 5 scaled to 2 x 50 Mbp: the GPU runs it in the chunked mode (forced)
     "c5s": dict(G=2, n=50_000_000, p=0.01, gen_seed=12345, w=19),
     "pc_ngaps": dict(G=4, n=10_000_000, p=0.01, gen_seed=4246, w=15, ngaps=20, chunk_size=200_000),
+    # ParallelMemHash at BASELINE config 3's shape (G = 8, w19 0x7b974ef, related p = 0.01 with
+    # genome 2 reverse-complemented) at 10 Mbp per genome: 50 chunks of the literal per-chunk
+    # MergeTable restatement (ParallelMemHash.cpp:42-121)
+    "pc_c3shape": dict(G=8, n=10_000_000, p=0.01, gen_seed=12345, w=19, chunk_size=200_000),
 }
 OUT = os.path.join(HERE, "large_cases.json")
 

@@ -187,3 +187,18 @@ def test_parallel_probe_views_agree(gpu_lib, oracle_mod, monkeypatch, env):
                 m.setenv(k, v)
             ml, st = gpu_parallel(gpu_lib, seqs, seed, chunk)
         assert len(ml) == len(lengths) and (ml.lengths == lengths).all() and (ml.starts == starts).all(), env
+
+
+def test_parallel_c3shape_known_answer(gpu_lib, oracle_mod):
+    """ParallelMemHash at BASELINE config 3's shape -- G = 8, the default w19 seed (0x7b974ef),
+    related p = 0.01 with genome 2 reverse-complemented -- at 8 x 10 Mbp: the oracle's literal
+    one-thread schedule (a MergeTable after each of the 50 chunks, ParallelMemHash.cpp:42-121)
+    recorded in tests/golden/large_cases.json (make_large_golden.py pc_c3shape)."""
+    c = LARGE["pc_c3shape"]
+    seqs = oracle_mod.generate(c["G"], c["n"], c["p"], c["gen_seed"])
+    assert oracle_mod.get_seed(c["w"]) == c["seed"]
+    ml, st = gpu_parallel(gpu_lib, seqs, c["seed"], c["chunk_size"])
+    assert st["chunks"] == c["chunks"]
+    assert len(ml) == c["matches"] and st["mem_count"] == c["mem_count"]
+    assert ml.text().split("\n", 1)[0] == c["first_line"]
+    assert hashlib.md5(ml.text().encode()).hexdigest() == c["md5"]

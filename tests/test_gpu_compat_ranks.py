@@ -101,3 +101,15 @@ def test_compat_ranks_refuse_slices(gpu_lib, oracle_mod):
         with pytest.raises(gpu_lib.MumsError):
             sh.FindMatches(seqs)
         assert sh.rank_status == [gpu_lib.MUMS_E_UNSUPPORTED] * 2, sh.rank_status
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_compat_ranks_c3shape_known_answer(gpu_lib, oracle_mod, world):
+    """BASELINE config 3's shape (G = 8, w19) at 8 x 10 Mbp over 2 and 4 chunk-range ranks: the
+    oracle's one-thread ParallelMemHash list (tests/golden/large_cases.json pc_c3shape)."""
+    c = json.load(open(os.path.join(GOLDEN, "large_cases.json")))["pc_c3shape"]
+    seqs = oracle_mod.generate(c["G"], c["n"], c["p"], c["gen_seed"])
+    ml, st = sharded(gpu_lib, seqs, c["seed"], c["chunk_size"], world)
+    assert all(s["chunks"] == c["chunks"] for s in st)
+    assert len(ml) == c["matches"]
+    assert hashlib.md5(ml.text().encode()).hexdigest() == c["md5"]
