@@ -188,9 +188,13 @@ __global__ __launch_bounds__(256) void claim_tiles_kernel(const SegTile* __restr
 // output -- run on one XCD and their partial cache lines can merge in its L2.  A block whose
 // queue is empty takes from the next queue: a tile's predecessors precede it in its queue, so
 // they were claimed by running blocks (forward progress as in claim_order_kernel).
-// xq[0..7] queue lengths, xq[8..16] queue offsets, xq[32 + off + i] the i-th tile of a queue.
+// xq[0..7] queue lengths, xq[8..16] queue offsets, xq[32 + off + i] the i-th tile of a queue;
+// xd[off + i] its claim descriptor {tile, first record, count | bucket << 16, tile in bucket}: a
+// claiming block reads its tile with ONE load after the claim's atomic (not the tile id, then
+// the tile's SegTile: two dependent round trips at the start of every tile)
 __global__ __launch_bounds__(256) void xcd_order_kernel(const uint32_t* __restrict__ tfirst, int nb, uint64_t ub,
-                                                        const SegTile* __restrict__ tiles, uint32_t* __restrict__ xq) {
+                                                        const SegTile* __restrict__ tiles, uint32_t* __restrict__ xq,
+                                                        uint4* __restrict__ xd) {
     __shared__ uint32_t s_n[1 << kMaxSegBucketBits];
     __shared__ uint32_t s_off[9];
     for (int b = threadIdx.x; b < nb; b += blockDim.x) s_n[b] = tfirst[b + 1] - tfirst[b];
@@ -222,6 +226,7 @@ __global__ __launch_bounds__(256) void xcd_order_kernel(const uint32_t* __restri
         pos += (n < k ? n : k) + ((uint32_t)b < d.bucket && n > k ? 1u : 0u);
     }
     xq[32 + s_off[x] + pos] = (uint32_t)t;
+    xd[s_off[x] + pos] = make_uint4((uint32_t)t, (uint32_t)d.start, d.count | (d.bucket << 16), d.tb);
 }
 
 __global__ __launch_bounds__(kBlock) void seg_upsweep(const uint64_t* __restrict__ rec, const SegTile* __restrict__ tiles,
@@ -465,7 +470,8 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
                                                           uint32_t* __restrict__ ghist_next,
                                                           const uint32_t* __restrict__ xq,
                                                           const uint64_t* __restrict__ gsrc = nullptr,
-                                                          uint32_t* __restrict__ gout = nullptr) {
+                                                          uint32_t* __restrict__ gout = nullptr,
+                                                          const uint4* __restrict__ xd = nullptr) {
     constexpr int kT = kIPT * OB;
     constexpr bool late = MUMS_OS_LATEPUB || kLate;
     constexpr int kW = OB / 64;
@@ -480,6 +486,7 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
     __shared__ uint32_t s_tile;
     __shared__ uint32_t hcnt[kDigits];
     __shared__ uint32_t hnext[kDigits];   // next pass's digit counts (ghist_next != null)
+    __shared__ uint4 s_desc;              // the claimed tile's descriptor (xd)
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
 #if MUMS_OS_STATS
     unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -491,9 +498,16 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
             const uint32_t x = blockIdx.x & 7u;
             for (uint32_t a = 0; a < 8; ++a) {
                 const uint32_t q = (x + a) & 7u;
+                const uint32_t qo = xq[8 + q], ql = xq[q];   // issued with the atomic
                 const uint32_t cc = atomicAdd(tile_counter + q, 1u);
-                if (cc < xq[q]) {
-                    tt = xq[32 + xq[8 + q] + cc];
+                if (cc < ql) {
+                    if (xd) {
+                        const uint4 dd = xd[qo + cc];
+                        s_desc = dd;
+                        tt = dd.x;
+                    } else {
+                        tt = xq[32 + qo + cc];
+                    }
                     break;
                 }
             }
@@ -512,7 +526,16 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
     const uint32_t t = __builtin_amdgcn_readfirstlane(d.order);
 #else
     const uint32_t t = xq ? c : __builtin_amdgcn_readfirstlane(tiles[c].order);
-    const SegTile d = tiles[t];
+    SegTile d{};
+    if (xd) {   // uniform: the descriptor the claim loaded
+        const uint4 dd = s_desc;
+        d.start = __builtin_amdgcn_readfirstlane(dd.y);
+        d.count = __builtin_amdgcn_readfirstlane(dd.z & 0xFFFFu);
+        d.bucket = __builtin_amdgcn_readfirstlane(dd.z >> 16);
+        d.tb = __builtin_amdgcn_readfirstlane(dd.w);
+    } else {
+        d = tiles[t];
+    }
 #endif
     if (d.count == 0) return;
     OS_STAMP(1);
@@ -708,225 +731,6 @@ __global__ __launch_bounds__(OB) void seg_onesweep_kernel(const uint64_t* __rest
     }
 #endif
 }
-
-#ifndef MUMS_OS_PREFETCH
-#define MUMS_OS_PREFETCH 0        // records per lane of the next tile loaded during the stores
-#endif
-#ifndef MUMS_OS_PSTORE_UNROLL
-#define MUMS_OS_PSTORE_UNROLL 4   // stores per lane in flight while the next tile's records load
-#endif
-// one claim: the block's XCD queue first, then the others (xq, xcd_order_kernel), or the
-// single counter in claim order; ~0 when no tile is left
-__device__ __forceinline__ uint32_t os_claim(const uint32_t* __restrict__ xq, uint32_t* tile_counter, uint32_t nclaims,
-                                             const SegTile* __restrict__ tiles) {
-    if (xq) {
-        const uint32_t x = blockIdx.x & 7u;
-        for (uint32_t a = 0; a < 8; ++a) {
-            const uint32_t q = (x + a) & 7u;
-            const uint32_t cc = atomicAdd(tile_counter + q, 1u);
-            if (cc < xq[q]) return xq[32 + xq[8 + q] + cc];
-        }
-        return 0xFFFFFFFFu;
-    }
-    const uint32_t c = atomicAdd(tile_counter, 1u);
-    return c < nclaims ? tiles[c].order : 0xFFFFFFFFu;
-}
-
-// Persistent onesweep pass (MUMS_DEV_OS_PERSIST=1): a resident grid (two 76-KB blocks per CU)
-// whose blocks claim tile after tile.  A block claims its next tile when it starts the current
-// one and loads the next tile's records while it stores the current one, so the claim's atomic
-// round trip, the descriptor load and the record loads -- three dependent memory latencies at
-// the start of every tile of seg_onesweep_kernel -- overlap the previous tile's work, and no
-// block slot waits for a workgroup launch.  Same ranking / look-back / exchange as the
-// kAlias form.  Forward progress: a block claims its next tile only after its current one, so
-// the unfinished current tile with the earliest claim has every predecessor in its queue
-// finished (an unfinished "next" tile would have been claimed after its block's unfinished
-// current tile, which was claimed earlier still).
-template <int OB, int kIPT, int kTPB>
-__global__ __launch_bounds__(OB) void seg_onesweep_persist2_kernel(const uint64_t* __restrict__ rin,
-                                                                   uint64_t* __restrict__ rout,
-                                                                   const SegTile* __restrict__ tiles, uint32_t nclaims,
-                                                                   int shift, int pass, int npass,
-                                                                   const uint32_t* __restrict__ dbase, uint32_t* status,
-                                                                   uint32_t* tile_counter, uint32_t* err,
-                                                                   const uint32_t* __restrict__ xq) {
-    constexpr int kT = kIPT * OB;
-    constexpr int kW = OB / 64;
-    constexpr int kPre = MUMS_OS_PREFETCH < kIPT ? MUMS_OS_PREFETCH : kIPT;   // records per lane loaded ahead
-    static_assert(OB >= kDigits, "one thread per digit");
-    static_assert(kW * kDigits * 4 <= kT * 8, "counts fit in the exchange buffer");
-    __shared__ uint64_t srec[kT];
-    uint32_t (*wcnt)[kDigits] = reinterpret_cast<uint32_t (*)[kDigits]>(srec);
-    __shared__ uint32_t lstart[kDigits];
-    __shared__ uint32_t gofs[kDigits];
-    __shared__ uint32_t s_w[kDigits / 64];
-    __shared__ uint32_t s_tile[2];
-    __shared__ uint32_t hcnt[kDigits];
-    // the thread index and everything derived from it (record offsets, LDS addresses) are
-    // re-derived every tile from an opaque copy: kept from one tile to the next they would hold
-    // ~13 registers across the loop (two blocks per CU need <= 80)
-    int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    uint32_t qb = wv * (kT / kW) + lane;
-    auto qof = [&](int r) -> uint32_t { return qb + (uint32_t)r * 64u; };
-#if MUMS_OS_STATS
-    unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#endif
-    if (tid == 0) s_tile[0] = os_claim(xq, tile_counter, nclaims, tiles);
-    __syncthreads();
-    uint32_t t = __builtin_amdgcn_readfirstlane(s_tile[0]);
-    uint64_t key[kIPT];
-    uint32_t rank[kIPT];
-    SegTile d{};
-    if (t != 0xFFFFFFFFu) {
-        d = tiles[t];
-        #pragma unroll
-        for (int r = 0; r < kPre; ++r) key[r] = qof(r) < d.count ? rin[d.start + qof(r)] : 0ull;
-    }
-    int par = 0;
-    // kTPB > 0: a fixed number of tiles per block, the loop unrolled (straight-line code as in
-    // seg_onesweep_kernel); 0: persistent
-    #pragma unroll
-    for (int it = 0; kTPB == 0 || it < kTPB; ++it) {
-        if (t == 0xFFFFFFFFu) break;
-        asm volatile("" : "+v"(tid) : : "memory");
-        lane = tid & 63;
-        wv = tid >> 6;
-        qb = wv * (kT / kW) + lane;
-        OS_STAMP(0);
-        if (tid == 0)   // the next tile
-            s_tile[par ^ 1] = (kTPB == 0 || it + 1 < kTPB) ? os_claim(xq, tile_counter, nclaims, tiles) : 0xFFFFFFFFu;
-        #pragma unroll
-        for (int r = kPre; r < kIPT; ++r) key[r] = qof(r) < d.count ? rin[d.start + qof(r)] : 0ull;
-        for (int i = tid; i < kW * kDigits; i += OB) (&wcnt[0][0])[i] = 0;
-        if (tid < kDigits) hcnt[tid] = 0;
-        __syncthreads();
-        OS_STAMP(1);
-        #pragma unroll
-        for (int r = 0; r < kIPT; ++r)
-            if (qof(r) < d.count) atomicAdd(&hcnt[(uint32_t)(key[r] >> shift) & 0xFFu], 1u);
-        __syncthreads();
-        OS_STAMP(2);
-        if (d.tb != 0 && tid < kDigits)
-            __hip_atomic_store(status + (uint64_t)t * kDigits + tid, kFlagAgg | hcnt[tid], __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        #pragma unroll
-        for (int r = 0; r < kIPT; ++r) {
-            const bool valid = qof(r) < d.count;
-            const uint32_t dg = (uint32_t)(key[r] >> shift) & 0xFFu;
-            uint32_t tot;
-            const uint32_t rk = wave_match_rank<8>(dg, valid, &tot);
-            uint32_t old = 0;
-            if (valid) old = wcnt[wv][dg];
-            if (valid && rk == 0) wcnt[wv][dg] = old + tot;
-            rank[r] = old + rk;
-        }
-        __syncthreads();
-        OS_STAMP(3);
-        uint32_t v = 0, acc = 0;
-        if (tid < kDigits) {
-            const int dg = tid;
-            #pragma unroll
-            for (int w = 0; w < kW; ++w) { const uint32_t x = wcnt[w][dg]; wcnt[w][dg] = acc; acc += x; }
-            uint32_t* st = status + (uint64_t)t * kDigits + dg;
-            uint32_t prefix = 0;
-            if (d.tb == 0) {
-                __hip_atomic_store(st, kFlagInc | acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else {
-                const int64_t tfirst = (int64_t)t - (int64_t)d.tb;
-                int64_t j = (int64_t)t - 1;
-                uint32_t spins = 0;
-                bool done = false;
-                while (!done) {
-                    uint32_t sv[kLookback];
-                    #pragma unroll
-                    for (int k = 0; k < kLookback; ++k)
-                        sv[k] = (j - k >= tfirst) ? __hip_atomic_load(status + (uint64_t)(j - k) * kDigits + dg,
-                                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                                  : kFlagInc;
-                    int used = 0;
-                    bool stall = false;
-                    #pragma unroll
-                    for (int k = 0; k < kLookback; ++k) {
-                        if (done || stall) continue;
-                        const uint32_t sx = sv[k];
-                        if ((sx >> 30) == 0u) { stall = true; continue; }
-                        prefix += sx & kValMask;
-                        ++used;
-                        if ((sx & kFlagInc) != 0u) done = true;
-                    }
-                    j -= used;
-                    if (stall && !done) {
-                        if (++spins > (1u << 24)) { atomicOr(err, 2u); break; }
-                        if (spins < 8) __builtin_amdgcn_s_sleep(1);
-                        else __builtin_amdgcn_s_sleep(8);
-                    }
-                }
-                __hip_atomic_store(st, kFlagInc | ((prefix + acc) & kValMask), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            }
-            gofs[dg] = dbase[((uint64_t)d.bucket * npass + pass) * kDigits + dg] + prefix;
-            v = acc;
-            #pragma unroll
-            for (int dd = 1; dd < 64; dd <<= 1) {
-                const uint32_t x = __shfl_up(v, dd, 64);
-                if (lane >= dd) v += x;
-            }
-            if (lane == 63) s_w[wv] = v;
-        }
-        __syncthreads();
-        OS_STAMP(4);
-        if (tid < kDigits) {
-            uint32_t wpre = 0;
-            #pragma unroll
-            for (int w = 0; w < kDigits / 64; ++w) wpre += (w < wv) ? s_w[w] : 0u;
-            lstart[tid] = wpre + v - acc;
-        }
-        __syncthreads();
-        #pragma unroll
-        for (int r = 0; r < kIPT; ++r) {
-            const uint32_t dg = (uint32_t)(key[r] >> shift) & 0xFFu;
-            rank[r] += lstart[dg] + wcnt[wv][dg];
-        }
-        __syncthreads();   // the exchange overwrites the counts
-        #pragma unroll
-        for (int r = 0; r < kIPT; ++r)
-            if (qof(r) < d.count) srec[rank[r]] = key[r];
-        __syncthreads();
-        OS_STAMP(5);
-        // the next tile's records into the key registers while this tile's are stored
-        const uint32_t tn = __builtin_amdgcn_readfirstlane(s_tile[par ^ 1]);
-        SegTile dn{};
-        if (tn != 0xFFFFFFFFu) {
-            dn = tiles[tn];
-            #pragma unroll
-            for (int r = 0; r < kPre; ++r) key[r] = qof(r) < dn.count ? rin[dn.start + qof(r)] : 0ull;
-        }
-        #pragma unroll MUMS_OS_PSTORE_UNROLL
-        for (int r = 0; r < kIPT; ++r) {
-            const uint32_t sidx = tid + r * OB;
-            if (sidx < d.count) {
-                const uint64_t k = srec[sidx];
-                const uint32_t dg = (uint32_t)(k >> shift) & 0xFFu;
-                rout[(uint64_t)gofs[dg] + (sidx - lstart[dg])] = k;
-            }
-        }
-        OS_STAMP(6);
-        __syncthreads();   // srec / gofs / lstart are rewritten by the next tile
-#if MUMS_OS_STATS
-        OS_STAMP(7);
-        if (tid == 0) {
-            unsigned long long* o = g_os_stats + (uint64_t)t * 10;
-            for (int k = 0; k < 8; ++k) o[k] = ts[k];
-            o[8] = blockIdx.x;
-            o[9] = 1;
-        }
-#endif
-        t = tn;
-        d = dn;
-        par ^= 1;
-    }
-}
-
 
 // Persistent onesweep pass: a resident grid of blocks, each claiming tiles in claim
 // order from the counter until none is left.  The next tile's records are loaded
@@ -1525,20 +1329,11 @@ static bool os_xcd() {
     const char* e = getenv("MUMS_DEV_OS_XCD");
     return !(e && e[0] == '0');
 }
-// multi-tile onesweep blocks (seg_onesweep_persist2_kernel), MUMS_DEV_OS_PERSIST read per call:
-// 1 persistent grid, 2 / 3 two / four tiles per block; 0 (unset) the one-tile kernel
-static int os_persist() {
-    const char* e = getenv("MUMS_DEV_OS_PERSIST");
-    return (e && e[0] >= '1' && e[0] <= '4') ? e[0] - '0' : 0;
-}
-// its grid: resident blocks per CU x CUs of the current device
-static uint64_t os_persist_grid() {
-    int dev = 0, cus = 0, per = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per, (const void*)seg_onesweep_persist2_kernel<kSortBlock, kSortTile / kSortBlock, 0>, kSortBlock, 0);
-    return (uint64_t)std::max(cus, 1) * (uint64_t)std::max(per, 1);
+// claim descriptors in the XCD queues (one dependent load per claim, default);
+// MUMS_DEV_OS_XD=0 (read per call) reads the tile id, then its SegTile
+static bool os_xd() {
+    const char* e = getenv("MUMS_DEV_OS_XD");
+    return !(e && e[0] == '0');
 }
 static int os_tile() {
     static const int t[9] = {kSortTile, 8192, 6144, 6144, 4096, 4096, 8192, 8192, 8960};
@@ -1636,9 +1431,12 @@ hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key
     // XCD-grouped claim queues (development A/B): the unused claim-ordered copy's room
     // (fewer than 8 MSD buckets: one queue is all there is)
     uint32_t* xq = (os_xcd() && nb >= 8 && !MUMS_SORT_PERSIST) ? (uint32_t*)ctiles : nullptr;
+    // the queues' claim descriptors behind them (the claim-ordered copy's room: 48 B per tile)
+    uint4* xqd = xq ? (uint4*)(((uintptr_t)(xq + 32 + ub) + 15) & ~(uintptr_t)15) : nullptr;
+    const uint4* xd = os_xd() ? xqd : nullptr;
     if (xq)
         hipLaunchKernelGGL(xcd_order_kernel, dim3((unsigned)((ub + 255) / 256)), dim3(256), 0, st,
-                           (const uint32_t*)btmp, (int)nb, ub, stiles, xq);
+                           (const uint32_t*)btmp, (int)nb, ub, stiles, xq, xqd);
 #endif
     const unsigned gblocks = (unsigned)((ub + kGhistTilesPerBlock - 1) / kGhistTilesPerBlock);
     // the histogram read counts digit 0 only when every later pass's digits are
@@ -1692,26 +1490,15 @@ hipError_t seg_onesweep_sort(uint64_t* recA, uint64_t* recB, uint64_t n, int key
             uint32_t* tc = xq ? counters + 128 + 8 * p : counters + p;
 #define MUMS_OS_LAUNCH(OB, IPT, AL)                                                                               \
     hipLaunchKernelGGL((seg_onesweep_kernel<OB, IPT, AL>), dim3((unsigned)ub), dim3(OB), 0, st, src, dst, otiles, \
-                       (uint32_t)ub, sh, p, npass, dbase, sp, tc, d_err, gn, xq, nullptr, nullptr)
+                       (uint32_t)ub, sh, p, npass, dbase, sp, tc, d_err, gn, xq, nullptr, nullptr, xd)
             if (key_runs && gout && p + 1 == npass) {   // the last pass stores gout[o] = gsrc[k]
                 hipLaunchKernelGGL((seg_onesweep_kernel<kSortBlock, kSortTile / kSortBlock, true, true, true>),
                                    dim3((unsigned)ub), dim3(kSortBlock), 0, st, src, dst, otiles, (uint32_t)ub, sh, p,
-                                   npass, dbase, sp, tc, d_err, gn, xq, gsrc, gout);
+                                   npass, dbase, sp, tc, d_err, gn, xq, gsrc, gout, xd);
             } else if (key_runs) {   // equal-digit runs: publish after the ranking (no per-record LDS atomics)
                 hipLaunchKernelGGL((seg_onesweep_kernel<kSortBlock, kSortTile / kSortBlock, true, true>),
                                    dim3((unsigned)ub), dim3(kSortBlock), 0, st, src, dst, otiles, (uint32_t)ub, sh, p,
-                                   npass, dbase, sp, tc, d_err, gn, xq, nullptr, nullptr);
-            } else if (os_persist()) {   // development A/B: a resident grid claiming tiles
-#define MUMS_OS_PLAUNCH(TPB, GRID)                                                                             \
-    hipLaunchKernelGGL((seg_onesweep_persist2_kernel<kSortBlock, kSortTile / kSortBlock, TPB>), dim3((unsigned)(GRID)), \
-                       dim3(kSortBlock), 0, st, src, dst, otiles, (uint32_t)ub, sh, p, npass, dbase, sp, tc, d_err, xq)
-                switch (os_persist()) {
-                case 2: MUMS_OS_PLAUNCH(2, (ub + 1) / 2); break;
-                case 4: MUMS_OS_PLAUNCH(1, ub); break;
-                case 3: MUMS_OS_PLAUNCH(4, (ub + 3) / 4); break;
-                default: MUMS_OS_PLAUNCH(0, std::min<uint64_t>(ub, os_persist_grid())); break;
-                }
-#undef MUMS_OS_PLAUNCH
+                                   npass, dbase, sp, tc, d_err, gn, xq, nullptr, nullptr, xd);
             } else
             switch (os_variant()) {
             case 1: MUMS_OS_LAUNCH(512, 16, true); break;
