@@ -18,6 +18,7 @@
 //      (a group needs >= 2 records, so <= 2048 probes per tile).
 // A second kernel concatenates the tiles' slots using the scanned tile counts, so
 // the probes end up in ascending key order = the reference's AddHashEntry order.
+#include <cstdlib>
 #include <type_traits>
 
 #include "match_device.h"
@@ -184,14 +185,17 @@ struct TileRecViewT {
     }
 };
 
-template <int MG, int IB, bool kGl = false>
+// kFastOnly: default tolerances only (repeat_tol 0, enum_tol 1) -- the general build_probe path
+// is not compiled in, so its registers do not weigh on the branch-free probe
+template <int MG, int IB, bool kGl = false, bool kFastOnly = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGl ? 6 : 1))) void probe_tile_rec_kernel(const uint64_t* __restrict__ rec,
                                                                 const SegTile* __restrict__ tiles, GenomeTable gt,
                                                                 MatchParams mp, int L,
                                                                 uint32_t* __restrict__ tile_count,
                                                                 uint64_t* __restrict__ slot_info,
                                                                 uint32_t* __restrict__ slot_bucket,
-                                                                DevCounters* __restrict__ ctr) {
+                                                                DevCounters* __restrict__ ctr,
+                                                                double inv_table) {
     constexpr int kGRounds = kGSubRounds;   // this block's part of the tile
     __shared__ uint64_t srec[kGSub];
     __shared__ uint16_t heads[kSubSlots];  // heads of groups of >= 2 records (<= kGSub / 2)
@@ -235,9 +239,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGl ? 6 
     if (threadIdx.x == 64) s_next = (tile0 + cnt < td.bend) ? rec[tile0 + cnt] : ~0ull;
     // the coarse genome lookup in LDS (GenomeTable gl_*; 32-bit indices)
     constexpr bool use_gl = kGl && IB == 32;   // (the launcher checks gt.gl_n)
-    if constexpr (use_gl) {
-        for (uint32_t i = threadIdx.x; i < gt.gl_n; i += kBlock) s_gl[i] = gt.gl[i];
-        for (int i = threadIdx.x; i <= kMaxG; i += kBlock) s_gb[i] = (uint32_t)gt.base[i];
+    if constexpr (use_gl) {   // gl_n <= 256 = kBlock, kMaxG + 1 <= kBlock: one element a thread
+        static_assert(kBlock >= 256 && kBlock > kMaxG, "one lookup entry per thread");
+        if (threadIdx.x < gt.gl_n) s_gl[threadIdx.x] = gt.gl[threadIdx.x];
+        if (threadIdx.x <= kMaxG) s_gb[threadIdx.x] = (uint32_t)gt.base[threadIdx.x];
     }
     const GLook glk{(lds_u8c*)s_gl, (lds_u32c*)s_gb, gt.gl_shift, gt.gl_n ? gt.gl_n - 1 : 0};
     __syncthreads();
@@ -287,8 +292,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGl ? 6 
 
     // 3) one probe per lane, compacted in head order into this tile's slots
     const TileRecViewT<IB> v{(lds_u64*)srec, rec, tile0, cnt};
-    const bool fast = mp.repeat_tol == 0 && mp.enum_tol == 1;
-    const double inv_t = 1.0 / (double)mp.table_size;
+    const bool fast = kFastOnly || (mp.repeat_tol == 0 && mp.enum_tol == 1);
+    const double inv_t = inv_table;   // 1 / table_size from the host (a double division per block otherwise)
     const uint64_t sb = (uint64_t)blockIdx.x * kSubSlots;
     uint32_t nrep = 0, base = 0;
     for (uint32_t c = 0; c < H; c += kBlock) {
@@ -321,7 +326,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kGl ? 6 
                     const uint32_t k0 = (uint32_t)(xb[0] >> (IB + 1));
                     while (i < td.bend && gsz <= (uint32_t)kRepeatLimit && (uint32_t)v.gkey(i) == k0) { ++gsz; ++i; }
                 }
-            } else {
+            } else if constexpr (!kFastOnly) {
                 Mhe<MG> P;
                 ok = build_probe<MG, TileRecViewT<IB>>(v, h, td.bend, gt, mp, L, P, &gsz);
                 off = P.offset;
@@ -715,14 +720,20 @@ hipError_t launch_probe_tiles(View v, const SegTile* tiles, uint64_t ntiles, uin
                               uint32_t* slot_bucket, void* counters, hipStream_t st) {
     if (ntiles == 0) return hipSuccess;
     if constexpr (RecIB<View>::value > 0) {
-        if (RecIB<View>::value == 32 && gt.gl_n > 0)   // the coarse genome lookup (GenomeTable gl_*)
+        const bool fast = mp.repeat_tol == 0 && mp.enum_tol == 1;
+        const double inv_t = 1.0 / (double)mp.table_size;
+        if (RecIB<View>::value == 32 && gt.gl_n > 0 && fast && !getenv("MUMS_DEV_PROBE_GENERAL"))
+            hipLaunchKernelGGL((probe_tile_rec_kernel<MG, RecIB<View>::value, true, true>),
+                               dim3((unsigned)(ntiles * kGSplit)), dim3(kBlock), 0, st, v.rec, tiles, gt, mp, L,
+                               tile_count, slot_info, slot_bucket, (DevCounters*)counters, inv_t);
+        else if (RecIB<View>::value == 32 && gt.gl_n > 0)   // the coarse genome lookup (GenomeTable gl_*)
             hipLaunchKernelGGL((probe_tile_rec_kernel<MG, RecIB<View>::value, true>), dim3((unsigned)(ntiles * kGSplit)),
                                dim3(kBlock), 0, st, v.rec, tiles, gt, mp, L, tile_count, slot_info, slot_bucket,
-                               (DevCounters*)counters);
+                               (DevCounters*)counters, inv_t);
         else
             hipLaunchKernelGGL((probe_tile_rec_kernel<MG, RecIB<View>::value>), dim3((unsigned)(ntiles * kGSplit)),
                                dim3(kBlock), 0, st, v.rec, tiles, gt, mp, L, tile_count, slot_info, slot_bucket,
-                               (DevCounters*)counters);
+                               (DevCounters*)counters, inv_t);
     } else
         hipLaunchKernelGGL((probe_tile_kernel<MG, View>), dim3((unsigned)ntiles), dim3(kBlock), 0, st, v, tiles, N, gt,
                            mp, L, tile_count, slot_info, slot_bucket, (DevCounters*)counters);
