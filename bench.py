@@ -514,13 +514,19 @@ def main():
             matches = int(red[1].item())
             # every rank's chain stage: the probes it labelled (its key range) and the time
             ci = stage.chain_info() if hasattr(stage, "chain_info") else {"probes": 0, "ms": 0.0}
-            per = torch.tensor([[float(ci["probes"]), ci["ms"], float(sm["probes"]), float(sm["ms_replay"])]],
-                               dtype=torch.float64)
+            per = torch.tensor([[float(ci["probes"]), ci["ms"], float(sm["probes"]), float(sm["ms_replay"]),
+                                 float(ci.get("recv_rows", 0)), float(ci.get("recv_bytes", 0)),
+                                 float(ci.get("sent_rows", 0)), float(ci.get("sent_bytes", 0))]], dtype=torch.float64)
             allr = [torch.zeros_like(per) for _ in range(world)] if world > 1 else [per]
             if world > 1:
                 dist.all_gather(allr, per)
+            # per rank: the probes it labelled, the AddHashEntry calls of its buckets (kept rows
+            # received + the collisions the sources counted instead of sending), what it received
+            # and sent in the FindMatches exchange (mums_comm_exchange_info)
             ranks_chain = [{"labelled_probes": int(a[0, 0].item()), "ms_label": round(float(a[0, 1].item()), 3),
-                            "replayed_rows": int(a[0, 2].item()), "ms_replay": round(float(a[0, 3].item()), 3)}
+                            "owned_calls": int(a[0, 2].item()), "ms_replay": round(float(a[0, 3].item()), 3),
+                            "recv_rows": int(a[0, 4].item()), "recv_bytes": int(a[0, 5].item()),
+                            "sent_rows": int(a[0, 6].item()), "sent_bytes": int(a[0, 7].item())}
                            for a in allr]
             mums_c3 = {"mums_per_s": matches / best, "matches": matches, "ms": best * 1e3,
                        "probes": int(red[2].item()), "collisions": int(red[3].item()),

@@ -370,7 +370,29 @@ int  mums_shard_find(mums_ctx* ctx, const int64_t* d_rows, uint64_t nrows, const
  *   mums_shard_find_labelled: on the bucket owner, the received blocks in source-rank order
  *     (src_rows / src_entries: the blocks' sizes); equal entries from several ranks merge, then
  *     the replay and the MatchList of the owned buckets.
- *   mums_shard_chain_info: info[4] = {probes labelled, chains, label time in us, 0}. */
+ *   mums_shard_chain_info: info[4] = {probes labelled, chains, label time in us, rows the rank
+ *     replayed as bucket owner in its last sharded FindMatches}.
+ *
+ * Kept-probe export (what mums_shard_run does by default; MUMS_DEV_SHARD_ALL_ROWS=1 sends every
+ * row as above).  The owner's replay needs only each chain's first AddHashEntry call and the
+ * suspicious calls (first-genome start at or past the chain's next_s: the only ones whose
+ * lower_bound over the bucket vector can miss their chain entry, MemHash.cpp:209-251,
+ * MatchHashEntry.h:121-143); every other call collides with its chain entry.
+ *   mums_shard_chain_entries: after mums_shard_chain_label, the rank's chain entries (G + 2 int64)
+ *     grouped by the rank owning their hash bucket (bounds as above; entry_counts per rank).
+ *   mums_shard_entry_thresholds: on the bucket owner, the received entries in source-rank order:
+ *     equal entries merge; d_thr[2e] = next_s of entry e's chain (the smallest first-genome start
+ *     >= its own among the other chains of its bucket and genome set, ~0 when none), d_thr[2e+1]
+ *     = 1 when e is the chain's first entry in source order (that rank holds the chain's first
+ *     AddHashEntry call).  The answers go back to the sources in the same order.
+ *   mums_shard_kept_export: with the owner's answers for the rank's own entries (the order of
+ *     mums_shard_chain_entries), the rows the replay needs (grouped by destination, key order,
+ *     with tags as mums_shard_chain_export), per entry its first sent row inside its
+ *     destination's row block (d_first; the block's end when none), and per destination the
+ *     probes not sent (dropped_counts: collisions).
+ *   mums_shard_find_kept: mums_shard_find_labelled on the kept rows (the entries of
+ *     mums_shard_chain_entries, d_first of mums_shard_kept_export); dropped = the calls of the
+ *     owned buckets the sources did not send, counted as collisions (MemCollisionCount). */
 int  mums_shard_chain_label(mums_ctx* ctx, const uint32_t* d_packed_all, uint64_t* nchains);
 int  mums_shard_chain_export(mums_ctx* ctx, uint32_t nranks, const uint32_t* bounds, int64_t* d_rows, uint32_t* d_tags,
                              uint64_t capacity_rows, int64_t* d_entries, uint32_t* d_first, uint64_t capacity_entries,
@@ -379,6 +401,15 @@ int  mums_shard_find_labelled(mums_ctx* ctx, const int64_t* d_rows, const uint32
                               const int64_t* d_entries, const uint32_t* d_first, uint64_t nentries, uint32_t nsrc,
                               const uint64_t* src_rows, const uint64_t* src_entries, const uint32_t* d_packed_all);
 int  mums_shard_chain_info(mums_ctx* ctx, uint64_t* info);
+int  mums_shard_chain_entries(mums_ctx* ctx, uint32_t nranks, const uint32_t* bounds, int64_t* d_entries,
+                              uint64_t capacity_entries, uint64_t* entry_counts);
+int  mums_shard_entry_thresholds(mums_ctx* ctx, const int64_t* d_entries, uint64_t nentries, uint32_t* d_thr);
+int  mums_shard_kept_export(mums_ctx* ctx, uint32_t nranks, const uint32_t* d_thr, int64_t* d_rows, uint32_t* d_tags,
+                            uint64_t capacity_rows, uint32_t* d_first, uint64_t* row_counts, uint64_t* dropped_counts);
+int  mums_shard_find_kept(mums_ctx* ctx, const int64_t* d_rows, const uint32_t* d_tags, uint64_t nrows,
+                          const int64_t* d_entries, const uint32_t* d_first, uint64_t nentries, uint32_t nsrc,
+                          const uint64_t* src_rows, const uint64_t* src_entries, uint64_t dropped,
+                          const uint32_t* d_packed_all);
 int  mums_probe_copy(mums_ctx* ctx, uint32_t* buckets, uint64_t* ref_index, uint64_t capacity);
 
 /* ---- multi-GPU MemHash through the ABI ----------
@@ -412,6 +443,9 @@ typedef struct mums_comm_ops {
 int  mums_comm_init_host(mums_comm** comm, int device, int world, int rank, const mums_comm_ops* ops, void* user);
 void mums_comm_destroy(mums_comm* comm);
 const char* mums_comm_last_error(mums_comm* comm);
+/* info[4] = {probe rows sent, bytes sent, probe rows received, bytes received} by this rank in
+ * its last sharded FindMatches (rows, tags, chain entries, thresholds and first-row indices). */
+int mums_comm_exchange_info(mums_comm* comm, uint64_t* info);
 /* the balanced contiguous key (or hash-bucket) ranges of the exchange: rank r gets
  * [first[r], first[r] + count[r]) (host only, no device needed) */
 int  mums_shard_key_ranges(const uint64_t* totals, uint32_t nbuckets, uint32_t world, uint32_t* first,

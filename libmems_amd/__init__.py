@@ -109,7 +109,8 @@ EXPORTED_SYMBOLS = [
     "mums_shard_restart_log", "mums_shard_restart_runs", "mums_shard_restart_ties", "mums_shard_restart_finish",
     "mums_shard_restart_info", "mums_shard_tie_flags", "mums_shard_tie_replay", "mums_shard_tie_apply",
     "mums_genome_device", "mums_shard_chain_label", "mums_shard_chain_export", "mums_shard_find_labelled",
-    "mums_shard_chain_info",
+    "mums_shard_chain_info", "mums_shard_chain_entries", "mums_shard_entry_thresholds", "mums_shard_kept_export",
+    "mums_shard_find_kept", "mums_comm_exchange_info",
 ]
 
 # mums_comm_ops (include/mums.h): the caller's transport as two host callbacks
@@ -155,6 +156,11 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mums_shard_chain_export.argtypes = [vp, u32, vp, vp, vp, u64, vp, vp, u64, vp, vp]
     lib.mums_shard_find_labelled.argtypes = [vp, vp, vp, u64, vp, vp, u64, u32, vp, vp, vp]
     lib.mums_shard_chain_info.argtypes = [vp, vp]
+    lib.mums_shard_chain_entries.argtypes = [vp, u32, vp, vp, u64, vp]
+    lib.mums_shard_entry_thresholds.argtypes = [vp, vp, u64, vp]
+    lib.mums_shard_kept_export.argtypes = [vp, u32, vp, vp, vp, u64, vp, vp, vp]
+    lib.mums_shard_find_kept.argtypes = [vp, vp, vp, u64, vp, vp, u64, u32, vp, vp, u64, vp]
+    lib.mums_comm_exchange_info.argtypes = [vp, vp]
     lib.mums_clear.argtypes = [vp]
     lib.mums_find.argtypes = [vp]
     lib.mums_find_stage.argtypes = [vp, i32]
@@ -744,7 +750,15 @@ class ShardedMemHash:
         for mh in self.ranks:
             ci = np.zeros(4, dtype=np.uint64)
             mh._check(self._lib.mums_shard_chain_info(mh._ctx, ci.ctypes.data))
-            self.chain_info.append({"probes": int(ci[0]), "chains": int(ci[1]), "ms": int(ci[2]) / 1000.0})
+            self.chain_info.append({"probes": int(ci[0]), "chains": int(ci[1]), "ms": int(ci[2]) / 1000.0,
+                                    "owned_rows": int(ci[3])})
+        # per rank: what its communicator moved in the FindMatches exchange (mums_comm_exchange_info)
+        self.exchange_info = []
+        for c in self._comms:
+            xi = np.zeros(4, dtype=np.uint64)
+            if self._lib.mums_comm_exchange_info(c, xi.ctypes.data) == MUMS_OK:
+                self.exchange_info.append({"sent_rows": int(xi[0]), "sent_bytes": int(xi[1]),
+                                           "recv_rows": int(xi[2]), "recv_bytes": int(xi[3])})
         if stage != STAGE_ALL:
             return MatchList(np.zeros(0, dtype=np.uint64), np.zeros((0, G), dtype=np.int64))
         parts = [mh.GetMatchList() for mh in self.ranks]

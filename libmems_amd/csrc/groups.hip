@@ -595,7 +595,61 @@ __global__ __launch_bounds__(kBlock) void chain_entry_out_kernel(const int64_t* 
     const uint32_t c = cperm[k];
     const uint64_t W = (uint64_t)(G + 2);
     for (uint64_t w = 0; w < W; ++w) eout[k * W + w] = pool[(uint64_t)c * W + w];
-    fout[k] = pinv[fk[c]] - rstart[scdest[k]];
+    if (fout) fout[k] = pinv[fk[c]] - rstart[scdest[k]];   // (null: the entries alone, mums_shard_chain_entries)
+}
+
+// ---- the sharded kept-probe export (mums_shard_kept_export) ----------
+// probe k of chain c (export position x = cinv[c], owner's answer thr[x] = {next_s, first}) is
+// sent when the owner's replay needs it -- the chain's first AddHashEntry call (the first probe of
+// a chain whose first call sits on this rank) or a probe starting at or past next_s (suspicious:
+// another chain of the bucket and genome set starts in [chain start, probe start]); every other
+// probe collides with its chain entry.  dest = pdest (sent) or nranks + pdest (dropped), so one
+// stable sort by dest groups the sent rows by rank in key order and counts the dropped ones.
+__global__ __launch_bounds__(kBlock) void kept_dest_kernel(const int64_t* __restrict__ rows, uint64_t P, int G,
+                                                           const uint32_t* __restrict__ chain_of,
+                                                           const uint32_t* __restrict__ cinv,
+                                                           const uint2* __restrict__ thr,
+                                                           const uint32_t* __restrict__ fk,
+                                                           const uint32_t* __restrict__ pdest, uint32_t nranks,
+                                                           uint32_t* __restrict__ dest) {
+    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= P) return;
+    const uint32_t c = chain_of[k];
+    const uint2 t = thr[cinv[c]];
+    bool keep = t.y != 0u && fk[c] == (uint32_t)k;
+    if (!keep) {
+        const int64_t* r = rows + k * (uint64_t)(G + 1);
+        int64_t fs = 0;   // the first present genome's start (forward by SetDirection: > 0)
+        for (int g = 0; g < G && fs == 0; ++g) fs = r[g];
+        keep = (uint64_t)fs >= (uint64_t)t.x;
+    }
+    dest[k] = keep ? pdest[k] : nranks + pdest[k];
+}
+
+// first[d] = the first sorted position holding dest d (P when none)
+__global__ __launch_bounds__(kBlock) void dest_first_kernel(const uint32_t* __restrict__ sdest, uint64_t P,
+                                                            uint32_t* __restrict__ first) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < P && (i == 0 || sdest[i - 1] != sdest[i])) first[sdest[i]] = (uint32_t)i;
+}
+
+// per exported entry: its first sent row inside its destination's row block (the block's end when
+// none of the chain's probes on this rank was sent)
+__global__ __launch_bounds__(kBlock) void entry_first_init_kernel(const uint32_t* __restrict__ scdest, uint64_t nch,
+                                                                  const uint32_t* __restrict__ rcount,
+                                                                  uint32_t* __restrict__ efirst) {
+    const uint64_t x = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (x < nch) efirst[x] = rcount[scdest[x]];
+}
+
+__global__ __launch_bounds__(kBlock) void entry_first_kernel(const uint32_t* __restrict__ perm,
+                                                             const uint32_t* __restrict__ sdest, uint64_t K,
+                                                             const uint32_t* __restrict__ chain_of,
+                                                             const uint32_t* __restrict__ cinv,
+                                                             const uint32_t* __restrict__ rstart,
+                                                             uint32_t* __restrict__ efirst) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < K) atomicMin(&efirst[cinv[chain_of[perm[i]]]], (uint32_t)i - rstart[sdest[i]]);
 }
 
 // A sharded rank's merged packed records (its MSD buckets [kfirst, kfirst + nb), starts
@@ -656,6 +710,34 @@ hipError_t launch_chain_entries_out(const int64_t* pool, const uint32_t* fk, con
     if (nch == 0) return hipSuccess;
     hipLaunchKernelGGL(chain_entry_out_kernel, dim3((unsigned)((nch + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
                        pool, fk, cperm, scdest, nch, G, pinv, rstart, eout, fout);
+    return hipGetLastError();
+}
+
+hipError_t launch_kept_dest(const int64_t* rows, uint64_t P, int G, const uint32_t* chain_of, const uint32_t* cinv,
+                            const uint2* thr, const uint32_t* fk, const uint32_t* pdest, uint32_t nranks, uint32_t* dest,
+                            hipStream_t st) {
+    if (P == 0) return hipSuccess;
+    hipLaunchKernelGGL(kept_dest_kernel, dim3((unsigned)((P + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, rows, P, G,
+                       chain_of, cinv, thr, fk, pdest, nranks, dest);
+    return hipGetLastError();
+}
+
+hipError_t launch_dest_first(const uint32_t* sdest, uint64_t P, uint32_t* first, hipStream_t st) {
+    if (P == 0) return hipSuccess;
+    hipLaunchKernelGGL(dest_first_kernel, dim3((unsigned)((P + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, sdest, P,
+                       first);
+    return hipGetLastError();
+}
+
+hipError_t launch_entry_first(const uint32_t* scdest, uint64_t nch, const uint32_t* rcount, const uint32_t* perm,
+                              const uint32_t* sdest, uint64_t K, const uint32_t* chain_of, const uint32_t* cinv,
+                              const uint32_t* rstart, uint32_t* efirst, hipStream_t st) {
+    if (nch == 0) return hipSuccess;
+    hipLaunchKernelGGL(entry_first_init_kernel, dim3((unsigned)((nch + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+                       scdest, nch, rcount, efirst);
+    if (K)
+        hipLaunchKernelGGL(entry_first_kernel, dim3((unsigned)((K + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, perm,
+                           sdest, K, chain_of, cinv, rstart, efirst);
     return hipGetLastError();
 }
 

@@ -113,6 +113,13 @@ struct mums_ctx {
     uint64_t lab_nch = 0;                // sharded: chains labelled among them
     uint64_t lab_p = 0;                  // sharded: probes labelled (the rank's own)
     double lab_ms = 0;                   // sharded: device time of the labelling
+    // sharded kept-probe export (mums_shard_chain_entries -> mums_shard_kept_export): the
+    // destinations computed for the entries, kept in labx; rows received as bucket owner
+    uint32_t kx_nranks = 0;              // 0: no entry export pending
+    std::vector<uint32_t> kx_estart;     // per destination: its first entry in the export order
+    uint64_t own_rows = 0;               // rows the last sharded FindMatches replayed on this rank
+    uint64_t own_dropped = 0;            // AddHashEntry calls of the owned buckets not sent (collisions)
+    bool kept_rows = false;              // mums_shard_find_kept: entries may outnumber the rows
     bool pairwise = false;   // PairwiseMatchFinder (pairwise.hip)
     uint64_t chunk_size = 200000;
     uint32_t nchunks = 0;
@@ -5205,18 +5212,68 @@ int mums_shard_chain_label(mums_ctx* ctx, const uint32_t* d_packed_all, uint64_t
     return MUMS_OK;
 }
 
-int mums_shard_chain_export(mums_ctx* ctx, uint32_t nranks, const uint32_t* bounds, int64_t* d_rows, uint32_t* d_tags,
-                            uint64_t capacity_rows, int64_t* d_entries, uint32_t* d_first, uint64_t capacity_entries,
-                            uint64_t* row_counts, uint64_t* entry_counts) {
-    int rc = shard_seeds_done(ctx);
-    if (rc) return rc;
-    if (nranks == 0 || nranks > 1024 || !bounds || !row_counts || !entry_counts)
-        return fail(ctx, MUMS_E_INVALID, "bad rank bounds");
+// The rank's probes' and chains' destination ranks (bucket ranges bounds[0..nranks]) in
+// ctx->labx: pdest per probe, the chains stably sorted by destination (cperm, scdest, cinv) and
+// the per-destination entry counts.  Layout of labx: pdest, pinv [P + 64]; cdest, ckB, ciA, ciB,
+// cinv, ckA2 [nch + 64]; rstart [nranks + 1]; cstart [nranks + 1]; scratch [2 nranks + 64].
+struct ChainDests {
+    uint32_t *pdest, *pinv, *cdest, *ckB, *ciA, *ciB, *cinv, *ckA2, *rstart, *cstart, *scratch;
+    const uint32_t* scdest = nullptr;
+    const uint32_t* cperm = nullptr;
+};
+static int chain_dests(mums_ctx* ctx, uint32_t nranks, const uint32_t* bounds, ChainDests* cd,
+                       uint64_t* entry_counts, hipStream_t st) {
+    if (nranks == 0 || nranks > 1024 || !bounds || !entry_counts) return fail(ctx, MUMS_E_INVALID, "bad rank bounds");
     if (bounds[0] != 0 || bounds[nranks] != ctx->table_size)
         return fail(ctx, MUMS_E_INVALID, "bucket bounds must cover [0, table_size)");
     for (uint32_t r = 0; r < nranks; ++r)
         if (bounds[r] > bounds[r + 1]) return fail(ctx, MUMS_E_INVALID, "bucket bounds must not decrease");
     const uint64_t P = ctx->P, nch = ctx->lab_nch;
+    const int G = ctx->gt.G;
+    const int bits = std::max(1, ceil_log2(nranks));
+    HIPCHK(ctx->labx.ensure((P + 64) * 8 + (nch + 64) * 24 + (size_t)(nranks + 1) * 8 + (size_t)(2 * nranks + 64) * 4 +
+                            4096));
+    cd->pdest = ctx->labx.as<uint32_t>();
+    cd->pinv = cd->pdest + (P + 64);
+    cd->cdest = cd->pinv + (P + 64);
+    cd->ckB = cd->cdest + (nch + 64);
+    cd->ciA = cd->ckB + (nch + 64);
+    cd->ciB = cd->ciA + (nch + 64);
+    cd->cinv = cd->ciB + (nch + 64);
+    cd->ckA2 = cd->cinv + (nch + 64);
+    cd->rstart = cd->ckA2 + (nch + 64);
+    cd->cstart = cd->rstart + (nranks + 1);
+    cd->scratch = cd->cstart + (nranks + 1);
+    HIPCHK(ctx->keybuf.ensure((size_t)(nranks + 1) * 8 + 64));
+    HIPCHK(hipMemcpyAsync(ctx->keybuf.p, bounds, (size_t)(nranks + 1) * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(launch_row_buckets(ctx->lab_rows, P, G, ctx->table_size, ctx->keybuf.as<uint32_t>(), nranks, cd->pdest, st));
+    std::fill(entry_counts, entry_counts + nranks, 0ull);
+    if (nch) {   // chains: destination of the first probe (all probes of a chain share its bucket), stable
+        HIPCHK(launch_chain_dest(ctx->fkloc.as<uint32_t>(), nch, cd->pdest, cd->cdest, st));
+        HIPCHK(hipMemcpyAsync(cd->ckA2, cd->cdest, nch * 4, hipMemcpyDeviceToDevice, st));
+        HIPCHK(ctx->radix_tmp.ensure(radix_tmp_bytes(std::max(P, nch) + 1)));
+        int out = 0;
+        HIPCHK(radix_sort<uint32_t>(cd->ckA2, nullptr, nch, bits, cd->ckB, cd->ciA, cd->ckA2, cd->ciB,
+                                    ctx->radix_tmp.p, &out, st));
+        cd->scdest = out ? cd->ckA2 : cd->ckB;
+        cd->cperm = out ? cd->ciB : cd->ciA;
+        HIPCHK(launch_inverse_perm(cd->cperm, nch, cd->cinv, st));
+        std::vector<uint32_t> scd(nch);
+        HIPCHK(hipMemcpyAsync(scd.data(), cd->scdest, nch * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        for (uint64_t i = 0; i < nch; ++i) ++entry_counts[scd[i]];
+    }
+    return MUMS_OK;
+}
+
+int mums_shard_chain_export(mums_ctx* ctx, uint32_t nranks, const uint32_t* bounds, int64_t* d_rows, uint32_t* d_tags,
+                            uint64_t capacity_rows, int64_t* d_entries, uint32_t* d_first, uint64_t capacity_entries,
+                            uint64_t* row_counts, uint64_t* entry_counts) {
+    int rc = shard_seeds_done(ctx);
+    if (rc) return rc;
+    if (!row_counts || !entry_counts) return fail(ctx, MUMS_E_INVALID, "bad rank bounds");
+    const uint64_t P = ctx->P, nch = ctx->lab_nch;
+    if (nranks == 0 || nranks > 1024) return fail(ctx, MUMS_E_INVALID, "bad rank bounds");
     std::fill(row_counts, row_counts + nranks, 0ull);
     std::fill(entry_counts, entry_counts + nranks, 0ull);
     if (P == 0) return MUMS_OK;
@@ -5227,61 +5284,178 @@ int mums_shard_chain_export(mums_ctx* ctx, uint32_t nranks, const uint32_t* boun
     hipStream_t st = ctx->stream;
     const int G = ctx->gt.G;
     const int bits = std::max(1, ceil_log2(nranks));
-    // scratch: per probe its destination (4), the inverse row permutation (4); per chain its
-    // destination, the sort's key / id ping-pong and the inverse (6 x 4); rank starts
     HIPCHK(ctx->rowtmp.ensure((P + 64) * 16 + 8192));
-    HIPCHK(ctx->labx.ensure((P + 64) * 8 + (nch + 64) * 24 + (size_t)(nranks + 1) * 8 + 4096));
-    uint32_t* pdest = ctx->labx.as<uint32_t>();
-    uint32_t* pinv = pdest + (P + 64);
-    uint32_t* cdest = pinv + (P + 64);
-    uint32_t* ckB = cdest + (nch + 64);
-    uint32_t* ciA = ckB + (nch + 64);
-    uint32_t* ciB = ciA + (nch + 64);
-    uint32_t* cinv = ciB + (nch + 64);
-    uint32_t* ckA2 = cinv + (nch + 64);
-    uint32_t* rstart = ckA2 + (nch + 64);
-    uint32_t* cstart = rstart + (nranks + 1);
-    HIPCHK(ctx->keybuf.ensure((size_t)(nranks + 1) * 8 + 64));
-    HIPCHK(hipMemcpyAsync(ctx->keybuf.p, bounds, (size_t)(nranks + 1) * 4, hipMemcpyHostToDevice, st));
-    HIPCHK(launch_row_buckets(ctx->lab_rows, P, G, ctx->table_size, ctx->keybuf.as<uint32_t>(), nranks, pdest, st));
-    // chains: destination of the first probe, stable by destination
-    const uint32_t* scdest = nullptr;
-    const uint32_t* cperm = nullptr;
-    if (nch) {
-        HIPCHK(launch_chain_dest(ctx->fkloc.as<uint32_t>(), nch, pdest, cdest, st));
-        HIPCHK(hipMemcpyAsync(ckA2, cdest, nch * 4, hipMemcpyDeviceToDevice, st));
-        HIPCHK(ctx->radix_tmp.ensure(radix_tmp_bytes(std::max(P, nch) + 1)));
-        int out = 0;
-        HIPCHK(radix_sort<uint32_t>(ckA2, nullptr, nch, bits, ckB, ciA, ckA2, ciB, ctx->radix_tmp.p, &out, st));
-        scdest = out ? ckA2 : ckB;
-        cperm = out ? ciB : ciA;
-        HIPCHK(launch_inverse_perm(cperm, nch, cinv, st));
-    }
+    ChainDests cd{};
+    if ((rc = chain_dests(ctx, nranks, bounds, &cd, entry_counts, st))) return rc;
     // rows: stable by destination (key order per destination)
     uint32_t* dest = (uint32_t*)ctx->rowtmp.p;
-    HIPCHK(hipMemcpyAsync(dest, pdest, P * 4, hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(dest, cd.pdest, P * 4, hipMemcpyDeviceToDevice, st));
     rc = sort_row_keys(ctx, dest, P, bits, st);
     if (rc) return rc;
     const uint32_t* perm = ctx->sorted_ids;
     const uint32_t* sdest = ctx->sorted_buckets;
-    HIPCHK(launch_inverse_perm(perm, P, pinv, st));
+    HIPCHK(launch_inverse_perm(perm, P, cd.pinv, st));
     HIPCHK(launch_gather_rows(ctx->lab_rows, perm, P, G, d_rows, st));
-    std::vector<uint32_t> sd(P), scd(nch);
+    std::vector<uint32_t> sd(P);
     HIPCHK(hipMemcpyAsync(sd.data(), sdest, P * 4, hipMemcpyDeviceToHost, st));
-    if (nch) HIPCHK(hipMemcpyAsync(scd.data(), scdest, nch * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     for (uint64_t i = 0; i < P; ++i) ++row_counts[sd[i]];
-    for (uint64_t i = 0; i < nch; ++i) ++entry_counts[scd[i]];
     std::vector<uint32_t> starts(2 * (nranks + 1), 0);
     for (uint32_t r = 0; r < nranks; ++r) {
         starts[r + 1] = starts[r] + (uint32_t)row_counts[r];
         starts[nranks + 1 + r + 1] = starts[nranks + 1 + r] + (uint32_t)entry_counts[r];
     }
-    HIPCHK(hipMemcpyAsync(rstart, starts.data(), starts.size() * 4, hipMemcpyHostToDevice, st));
-    HIPCHK(launch_chain_tags(ctx->chain_of.as<uint32_t>(), perm, sdest, P, cinv, cstart, d_tags, st));
-    HIPCHK(launch_chain_entries_out(ctx->pool_loc.as<int64_t>(), ctx->fkloc.as<uint32_t>(), cperm, scdest, nch, G,
-                                    pinv, rstart, d_entries, d_first, st));
+    HIPCHK(hipMemcpyAsync(cd.rstart, starts.data(), starts.size() * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(launch_chain_tags(ctx->chain_of.as<uint32_t>(), perm, sdest, P, cd.cinv, cd.cstart, d_tags, st));
+    HIPCHK(launch_chain_entries_out(ctx->pool_loc.as<int64_t>(), ctx->fkloc.as<uint32_t>(), cd.cperm, cd.scdest, nch, G,
+                                    cd.pinv, cd.rstart, d_entries, d_first, st));
     HIPCHK(hipStreamSynchronize(st));   // (starts is a host vector)
+    return MUMS_OK;
+}
+
+// ---- sharded FindMatches, kept-probe export (default in mums_shard_run) ----------------
+// Only two kinds of AddHashEntry call can touch a bucket vector (the replay from kept probes,
+// replay.hip): a chain's first call, and a suspicious one (its first-genome start at or past
+// the chain's next_s).  Whether a probe is either depends on the chains of the whole bucket,
+// which only its owner sees: so the entries go first (mums_shard_chain_entries), the owner
+// answers per entry {next_s, first} (mums_shard_entry_thresholds), and the ranks then send only
+// those probes (mums_shard_kept_export; on related genomes ~5 % of them) -- every other one
+// collides with its chain entry and is counted (dropped_counts) instead of sent.
+int mums_shard_chain_entries(mums_ctx* ctx, uint32_t nranks, const uint32_t* bounds, int64_t* d_entries,
+                             uint64_t capacity_entries, uint64_t* entry_counts) {
+    int rc = shard_seeds_done(ctx);
+    if (rc) return rc;
+    ctx->kx_nranks = 0;
+    if (nranks == 0 || nranks > 1024 || !entry_counts) return fail(ctx, MUMS_E_INVALID, "bad rank bounds");
+    std::fill(entry_counts, entry_counts + nranks, 0ull);
+    const uint64_t P = ctx->P, nch = ctx->lab_nch;
+    if (P && !ctx->lab_rows) return fail(ctx, MUMS_E_INVALID, "mums_shard_chain_label first");
+    if (capacity_entries < nch) return fail(ctx, MUMS_E_INVALID, "export buffer too small");
+    if (nch && !d_entries) return fail(ctx, MUMS_E_INVALID, "null export buffer");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    ChainDests cd{};
+    if (P && (rc = chain_dests(ctx, nranks, bounds, &cd, entry_counts, st))) return rc;
+    ctx->kx_estart.assign(nranks + 1, 0);
+    for (uint32_t r = 0; r < nranks; ++r) ctx->kx_estart[r + 1] = ctx->kx_estart[r] + (uint32_t)entry_counts[r];
+    if (nch)
+        HIPCHK(launch_chain_entries_out(ctx->pool_loc.as<int64_t>(), ctx->fkloc.as<uint32_t>(), cd.cperm, cd.scdest,
+                                        nch, ctx->gt.G, nullptr, nullptr, d_entries, nullptr, st));
+    HIPCHK(hipStreamSynchronize(st));
+    ctx->kx_nranks = nranks;
+    return MUMS_OK;
+}
+
+int mums_shard_entry_thresholds(mums_ctx* ctx, const int64_t* d_entries, uint64_t nentries, uint32_t* d_thr) {
+    int rc = shard_seeds_done(ctx);
+    if (rc) return rc;
+    if (nentries == 0) return MUMS_OK;
+    if (!d_entries || !d_thr) return fail(ctx, MUMS_E_INVALID, "null entries / thresholds");
+    if (nentries >= (1ull << 32) - 64) return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 chain entries on one rank");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    const MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, ctx->masked, ctx->seq_mask};
+    HIPCHK(ctx->counters.ensure(sizeof(DevCounters)));
+    DevCounters* dc = ctx->counters.as<DevCounters>();
+    HIPCHK(ctx->pool.ensure((nentries + 1) * (size_t)(ctx->gt.G + 2) * 8));
+    HIPCHK(ctx->chain_tmp.ensure(chain_thr_tmp_bytes(nentries + 1)));
+    HIPCHK(ctx->radix_tmp.ensure(radix_tmp_bytes(nentries + 1)));
+    HIPCHK(ctx->tmp.ensure(scan_tmp_bytes(nentries + 1)));
+    uint32_t nm = 0;
+    HIPCHK(launch_chain_thresholds(d_entries, nentries, ctx->gt, mp, ctx->pool.as<int64_t>(), ctx->chain_tmp.p,
+                                   ctx->radix_tmp.p, ctx->tmp.p, &dc->nchains, &nm, (uint2*)d_thr, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return MUMS_OK;
+}
+
+int mums_shard_kept_export(mums_ctx* ctx, uint32_t nranks, const uint32_t* d_thr, int64_t* d_rows, uint32_t* d_tags,
+                           uint64_t capacity_rows, uint32_t* d_first, uint64_t* row_counts, uint64_t* dropped_counts) {
+    int rc = shard_seeds_done(ctx);
+    if (rc) return rc;
+    if (!row_counts || !dropped_counts || nranks == 0 || nranks > 1024)
+        return fail(ctx, MUMS_E_INVALID, "bad rank count");
+    if (ctx->kx_nranks != nranks) return fail(ctx, MUMS_E_INVALID, "mums_shard_chain_entries first (same ranks)");
+    std::fill(row_counts, row_counts + nranks, 0ull);
+    std::fill(dropped_counts, dropped_counts + nranks, 0ull);
+    const uint64_t P = ctx->P, nch = ctx->lab_nch;
+    if (P == 0) return MUMS_OK;
+    if (nch && (!d_thr || !d_first)) return fail(ctx, MUMS_E_INVALID, "null thresholds / first rows");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    const int G = ctx->gt.G;
+    ChainDests cd{};   // the layout chain_dests left in labx
+    cd.pdest = ctx->labx.as<uint32_t>();
+    cd.pinv = cd.pdest + (P + 64);
+    cd.cdest = cd.pinv + (P + 64);
+    cd.ckB = cd.cdest + (nch + 64);
+    cd.ciA = cd.ckB + (nch + 64);
+    cd.ciB = cd.ciA + (nch + 64);
+    cd.cinv = cd.ciB + (nch + 64);
+    cd.ckA2 = cd.cinv + (nch + 64);
+    cd.rstart = cd.ckA2 + (nch + 64);
+    cd.cstart = cd.rstart + (nranks + 1);
+    cd.scratch = cd.cstart + (nranks + 1);
+    HIPCHK(ctx->rowtmp.ensure((P + 64) * 16 + 8192));
+    uint32_t* dest = (uint32_t*)ctx->rowtmp.p;
+    HIPCHK(launch_kept_dest(ctx->lab_rows, P, G, ctx->chain_of.as<uint32_t>(), cd.cinv, (const uint2*)d_thr,
+                            ctx->fkloc.as<uint32_t>(), cd.pdest, nranks, dest, st));
+    rc = sort_row_keys(ctx, dest, P, std::max(1, ceil_log2(2ull * nranks)), st);   // stable: key order per destination
+    if (rc) return rc;
+    const uint32_t* perm = ctx->sorted_ids;
+    const uint32_t* sdest = ctx->sorted_buckets;
+    std::vector<uint32_t> first(2 * nranks, (uint32_t)P);
+    HIPCHK(hipMemcpyAsync(cd.scratch, first.data(), first.size() * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(launch_dest_first(sdest, P, cd.scratch, st));
+    HIPCHK(hipMemcpyAsync(first.data(), cd.scratch, first.size() * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    uint64_t end = P;
+    for (int64_t d = 2 * (int64_t)nranks - 1; d >= 0; --d) {
+        const uint64_t c = first[d] == (uint32_t)P ? 0 : end - first[d];
+        if (c) end = first[d];
+        if (d < (int64_t)nranks) row_counts[d] = c;
+        else dropped_counts[d - nranks] = c;
+    }
+    uint64_t K = 0;
+    std::vector<uint32_t> starts(2 * (nranks + 1), 0);
+    for (uint32_t r = 0; r < nranks; ++r) {
+        starts[r + 1] = starts[r] + (uint32_t)row_counts[r];
+        starts[nranks + 1 + r + 1] = ctx->kx_estart[r + 1];
+        K += row_counts[r];
+    }
+    if (capacity_rows < K) return fail(ctx, MUMS_E_INVALID, "export buffer too small");
+    if (K && (!d_rows || !d_tags)) return fail(ctx, MUMS_E_INVALID, "null export buffer");
+    std::vector<uint32_t> rcount(nranks);
+    for (uint32_t r = 0; r < nranks; ++r) rcount[r] = (uint32_t)row_counts[r];
+    HIPCHK(hipMemcpyAsync(cd.rstart, starts.data(), starts.size() * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(cd.scratch, rcount.data(), nranks * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(launch_gather_rows(ctx->lab_rows, perm, K, G, d_rows, st));
+    HIPCHK(launch_chain_tags(ctx->chain_of.as<uint32_t>(), perm, sdest, K, cd.cinv, cd.cstart, d_tags, st));
+    // the chains in export order: their destinations are kx_estart's blocks
+    if (nch) {
+        std::vector<uint32_t> xd(nch);
+        for (uint32_t r = 0; r < nranks; ++r)
+            for (uint32_t x = ctx->kx_estart[r]; x < ctx->kx_estart[r + 1]; ++x) xd[x] = r;
+        HIPCHK(hipMemcpyAsync(cd.ckB, xd.data(), nch * 4, hipMemcpyHostToDevice, st));
+        HIPCHK(launch_entry_first(cd.ckB, nch, cd.scratch, perm, sdest, K, ctx->chain_of.as<uint32_t>(), cd.cinv,
+                                  cd.rstart, d_first, st));
+        HIPCHK(hipStreamSynchronize(st));   // (xd is a host vector)
+    }
+    HIPCHK(hipStreamSynchronize(st));   // (starts / rcount are host vectors)
+    return MUMS_OK;
+}
+
+int mums_shard_find_kept(mums_ctx* ctx, const int64_t* d_rows, const uint32_t* d_tags, uint64_t nrows,
+                         const int64_t* d_entries, const uint32_t* d_first, uint64_t nentries, uint32_t nsrc,
+                         const uint64_t* src_rows, const uint64_t* src_entries, uint64_t dropped,
+                         const uint32_t* d_packed_all) {
+    ctx->kept_rows = true;
+    const int rc = mums_shard_find_labelled(ctx, d_rows, d_tags, nrows, d_entries, d_first, nentries, nsrc, src_rows,
+                                            src_entries, d_packed_all);
+    ctx->kept_rows = false;
+    if (rc) return rc;
+    ctx->own_dropped = dropped;
+    ctx->st.collision_count += dropped;   // every probe not sent collides with its chain entry
+    ctx->st.probes = nrows + dropped;     // the AddHashEntry calls of the owned buckets
     return MUMS_OK;
 }
 
@@ -5290,7 +5464,7 @@ int mums_shard_chain_info(mums_ctx* ctx, uint64_t* info) {
     info[0] = ctx->lab_p;
     info[1] = ctx->lab_nch;
     info[2] = (uint64_t)(ctx->lab_ms * 1000.0 + 0.5);
-    info[3] = 0;
+    info[3] = ctx->own_rows;   // rows this rank replayed as bucket owner (kept or all)
     return MUMS_OK;
 }
 
@@ -5353,7 +5527,9 @@ int mums_shard_find_labelled(mums_ctx* ctx, const int64_t* d_rows, const uint32_
         se += src_entries[s];
     }
     if (sr != nrows || se != nentries) return fail(ctx, MUMS_E_INVALID, "source blocks do not add up");
-    if (nentries > nrows) return fail(ctx, MUMS_E_INVALID, "more chains than probes");
+    if (nentries > nrows && !ctx->kept_rows) return fail(ctx, MUMS_E_INVALID, "more chains than probes");
+    ctx->own_rows = nrows;
+    ctx->own_dropped = 0;
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
     const int G = ctx->gt.G;

@@ -308,6 +308,16 @@ hipError_t launch_chain_tags(const uint32_t* chain_of, const uint32_t* perm, con
 hipError_t launch_chain_entries_out(const int64_t* pool, const uint32_t* fk, const uint32_t* cperm,
                                     const uint32_t* scdest, uint64_t nch, int G, const uint32_t* pinv,
                                     const uint32_t* rstart, int64_t* eout, uint32_t* fout, hipStream_t st);
+// the kept-probe export (groups.hip): per probe its destination (pdest when the owner's replay
+// needs it, nranks + pdest when it collides), the first sorted position of every destination,
+// and per exported entry its first sent row inside its destination's row block
+hipError_t launch_kept_dest(const int64_t* rows, uint64_t P, int G, const uint32_t* chain_of, const uint32_t* cinv,
+                            const uint2* thr, const uint32_t* fk, const uint32_t* pdest, uint32_t nranks, uint32_t* dest,
+                            hipStream_t st);
+hipError_t launch_dest_first(const uint32_t* sdest, uint64_t P, uint32_t* first, hipStream_t st);
+hipError_t launch_entry_first(const uint32_t* scdest, uint64_t nch, const uint32_t* rcount, const uint32_t* perm,
+                              const uint32_t* sdest, uint64_t K, const uint32_t* chain_of, const uint32_t* cinv,
+                              const uint32_t* rstart, uint32_t* efirst, hipStream_t st);
 // flat tiles over [0, N) for the pair path (one bucket)
 hipError_t launch_flat_tiles(uint64_t N, SegTile* d_tiles, hipStream_t st);
 
@@ -377,6 +387,14 @@ size_t chain_tmp_bytes(uint64_t P, uint32_t Tb, int G);
 // per-slice chain entries merged by content (chain_of remapped, *d_nchains = merged count)
 hipError_t launch_add_offset(uint32_t* a, uint64_t n, uint32_t off, hipStream_t st);
 size_t chain_merge_tmp_bytes(uint64_t n);
+// the bucket owner's answer to the sharded kept-probe export (replay.hip): the n received chain
+// entries merged into pool_out (*h_nchains chains), thr[e] = {next_s of entry e's chain, 1 when e
+// is the chain's first received entry}; d_tmp: chain_thr_tmp_bytes(n), d_radix_tmp:
+// radix_tmp_bytes(n + 1), d_scan_tmp: scan_tmp_bytes(n)
+size_t chain_thr_tmp_bytes(uint64_t n);
+hipError_t launch_chain_thresholds(const int64_t* entries, uint64_t n, const GenomeTable& gt, const MatchParams& mp,
+                                   int64_t* pool_out, void* d_tmp, void* d_radix_tmp, void* d_scan_tmp,
+                                   uint32_t* d_nchains, uint32_t* h_nchains, uint2* thr, hipStream_t st);
 // fk_out[merged chain] = min of fk_loc over its per-slice chains
 hipError_t launch_chain_merge(const int64_t* pool_loc, uint64_t n, int G, uint32_t* chain_of, uint64_t P,
                               int64_t* pool_out, void* d_tmp, void* d_radix_tmp, void* d_scan_tmp, uint32_t* d_nchains,

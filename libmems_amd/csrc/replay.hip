@@ -1597,6 +1597,49 @@ __global__ __launch_bounds__(kBlock) void kept_ranges_kernel(const uint64_t* __r
     if (i + 1 == Kc || (uint32_t)(skey[i + 1] >> 32) != b) cend[b] = i + 1;
 }
 
+// The nch chains of a merged pool in (hash bucket, block, first-genome start) order =
+// MheCompare's order inside a bucket: rank[c] and next_s[c] (chain_next_kernel); key_b[c] =
+// bucket << 32 | block key.  Buffers of nch entries: key_s, key_b, key_g, kA, kB (8 B), vA, vB,
+// step, bkey_buf (4 B; step may alias next_s).  *bkey_out: the dense block keys (G > 32) or null.
+static hipError_t chain_order(const int64_t* pool, uint32_t nch, const GenomeTable& gt, const MatchParams& mp,
+                              uint64_t* key_s, uint64_t* key_b, uint64_t* key_g, uint64_t* kA, uint64_t* kB,
+                              uint32_t* vA, uint32_t* vB, uint32_t* step, uint32_t* bkey_buf, void* d_radix_tmp,
+                              void* d_scan_tmp, uint32_t* next_s, uint32_t* rank, const uint32_t** bkey_out,
+                              hipStream_t st) {
+    const unsigned cgrid = (nch + kBlock - 1) / kBlock;
+    hipError_t e = hipSuccess;
+    const uint32_t* bkey = block_keys(pool, nch, gt.G, key_g, kA, vA, kB, vB, step, bkey_buf, d_radix_tmp,
+                                      d_scan_tmp, st, &e);
+    if (e != hipSuccess) return e;
+    *bkey_out = bkey;
+    hipLaunchKernelGGL(chain_keys_kernel, dim3(cgrid), dim3(kBlock), 0, st, pool, nch, gt.G, mp.table_size,
+                       1.0 / (double)mp.table_size, bkey, key_s, key_b);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    int buf = 0;
+    if ((e = radix_sort<uint64_t>(key_s, nullptr, nch, 32, kA, vA, kB, vB, d_radix_tmp, &buf, st)) != hipSuccess)
+        return e;
+    const uint32_t* ord1 = buf ? vB : vA;
+    int tb = 1;   // bucket bits
+    while (tb < 32 && ((uint64_t)1 << tb) < (uint64_t)mp.table_size) ++tb;
+    int kb = 32, low_shift = 0;   // block key bits
+    if (!bkey) {
+        kb = gt.G;
+        low_shift = 32 - gt.G;
+    } else {
+        kb = 1;
+        while (kb < 32 && ((uint64_t)1 << kb) < (uint64_t)nch) ++kb;
+    }
+    hipLaunchKernelGGL(gather_gkey_kernel, dim3(cgrid), dim3(kBlock), 0, st, key_b, ord1, nch, low_shift, kb, key_g);
+    uint32_t* vin = buf ? vB : vA;
+    uint32_t* vout = buf ? vA : vB;
+    int buf2 = 0;
+    if ((e = radix_sort<uint64_t>(key_g, vin, nch, kb + tb, kA, vout, kB, vin, d_radix_tmp, &buf2, st)) != hipSuccess)
+        return e;
+    const uint32_t* ord = buf2 ? vin : vout;
+    hipLaunchKernelGGL(chain_next_kernel, dim3(cgrid), dim3(kBlock), 0, st, ord, key_s, key_b, nch, next_s, rank);
+    return hipGetLastError();
+}
+
 template <int MG, typename View>
 hipError_t launch_replay_kept(View v, const GenomeTable& gt, const MatchParams& mp, int L, uint64_t P,
                               const int64_t* pool, const uint32_t* chain_of, const uint32_t* fk, uint32_t nch,
@@ -1626,35 +1669,10 @@ hipError_t launch_replay_kept(View v, const GenomeTable& gt, const MatchParams& 
     uint4* ckeep = (uint4*)carve((size_t)nch * 16);
     const unsigned cgrid = (nch + kBlock - 1) / kBlock;
     hipError_t e = hipSuccess;
-    const uint32_t* bkey = block_keys(pool, nch, gt.G, key_g, kA, vA, kB, vB, next_s, bkey_buf, d_radix_tmp,
-                                      d_scan_tmp, st, &e);
-    if (e != hipSuccess) return e;
-    // chains in (bucket, block, first start) order -> rank, next_s per chain
-    hipLaunchKernelGGL(chain_keys_kernel, dim3(cgrid), dim3(kBlock), 0, st, pool, nch, gt.G, mp.table_size,
-                       1.0 / (double)mp.table_size, bkey, key_s, key_b);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    int buf = 0;
-    if ((e = radix_sort<uint64_t>(key_s, nullptr, nch, 32, kA, vA, kB, vB, d_radix_tmp, &buf, st)) != hipSuccess)
+    const uint32_t* bkey = nullptr;
+    if ((e = chain_order(pool, nch, gt, mp, key_s, key_b, key_g, kA, kB, vA, vB, next_s, bkey_buf, d_radix_tmp,
+                         d_scan_tmp, next_s, rank, &bkey, st)) != hipSuccess)
         return e;
-    const uint32_t* ord1 = buf ? vB : vA;
-    int tb = 1;   // bucket bits
-    while (tb < 32 && ((uint64_t)1 << tb) < (uint64_t)mp.table_size) ++tb;
-    int kb = 32, low_shift = 0;   // block key bits
-    if (!bkey) {
-        kb = gt.G;
-        low_shift = 32 - gt.G;
-    } else {
-        kb = 1;
-        while (kb < 32 && ((uint64_t)1 << kb) < (uint64_t)nch) ++kb;
-    }
-    hipLaunchKernelGGL(gather_gkey_kernel, dim3(cgrid), dim3(kBlock), 0, st, key_b, ord1, nch, low_shift, kb, key_g);
-    uint32_t* vin = buf ? vB : vA;
-    uint32_t* vout = buf ? vA : vB;
-    int buf2 = 0;
-    if ((e = radix_sort<uint64_t>(key_g, vin, nch, kb + tb, kA, vout, kB, vin, d_radix_tmp, &buf2, st)) != hipSuccess)
-        return e;
-    const uint32_t* ord = buf2 ? vin : vout;
-    hipLaunchKernelGGL(chain_next_kernel, dim3(cgrid), dim3(kBlock), 0, st, ord, key_s, key_b, nch, next_s, rank);
     hipLaunchKernelGGL(chain_sb_kernel, dim3(cgrid), dim3(kBlock), 0, st, pool, nch, gt.G, rank, next_s, chain_sb);
     hipLaunchKernelGGL(chain_keep_kernel, dim3(cgrid), dim3(kBlock), 0, st, fk, (const uint32_t*)next_s,
                        (const uint64_t*)key_b, nch, ckeep);
@@ -1728,6 +1746,80 @@ hipError_t launch_replay_kept(View v, const GenomeTable& gt, const MatchParams& 
     if ((e = hipGetLastError()) != hipSuccess) return e;
     return replay_tail<MG, View>(v, gt, mp, L, nullptr, summ_c, summ_bc, cbeg, cend, cbeg, tbl, spill, pool, chain_sb,
                                  Kc, scr, d_scan_tmp, lds_cap, tsize, ctr, dbg, st, mlog);
+}
+
+// ---- the sharded kept-probe export -------------------------------
+// The bucket owner receives every rank's chain entries (source-rank order; a chain whose probes
+// sit on several ranks arrives once per rank), merges equal ones (launch_chain_merge) and
+// answers per received entry what the source needs to pick the probes the replay keeps: the
+// chain's next_s and whether this entry is the chain's first in source order (its rank holds
+// the chain's first AddHashEntry call).
+size_t chain_thr_tmp_bytes(uint64_t n) {
+    return chain_merge_tmp_bytes(n) + (n + 64) * (8 * 5 + 4 * 9) + 32 * 256;
+}
+
+namespace {
+
+__global__ __launch_bounds__(kBlock) void iota_kernel(uint32_t* __restrict__ a, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) a[i] = (uint32_t)i;
+}
+
+__global__ __launch_bounds__(kBlock) void entry_thr_kernel(const uint32_t* __restrict__ gmap,
+                                                           const uint32_t* __restrict__ first,
+                                                           const uint32_t* __restrict__ next_s, uint64_t n,
+                                                           uint2* __restrict__ thr) {
+    const uint64_t e = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= n) return;
+    const uint32_t m = gmap[e];
+    thr[e] = make_uint2(next_s[m], first[m] == (uint32_t)e ? 1u : 0u);
+}
+
+}  // namespace
+
+hipError_t launch_chain_thresholds(const int64_t* entries, uint64_t n, const GenomeTable& gt, const MatchParams& mp,
+                                   int64_t* pool_out, void* d_tmp, void* d_radix_tmp, void* d_scan_tmp,
+                                   uint32_t* d_nchains, uint32_t* h_nchains, uint2* thr, hipStream_t st) {
+    *h_nchains = 0;
+    if (n == 0) return hipSuccess;
+    char* p = (char*)d_tmp;
+    auto carve = [&](size_t bytes) {
+        char* r = p;
+        p += (bytes + 255) & ~(size_t)255;
+        return (void*)r;
+    };
+    void* mtmp = carve(chain_merge_tmp_bytes(n));
+    uint32_t* gmap = (uint32_t*)carve(n * 4);    // received entry -> merged chain (chain_remap of an iota)
+    uint32_t* ident = (uint32_t*)carve(n * 4);   // first-probe stand-ins: the received entry's own index
+    uint32_t* first = (uint32_t*)carve(n * 4);   // per merged chain: its first received entry
+    const unsigned grid = (unsigned)((n + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(iota_kernel, dim3(grid), dim3(kBlock), 0, st, gmap, n);
+    hipLaunchKernelGGL(iota_kernel, dim3(grid), dim3(kBlock), 0, st, ident, n);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if ((e = launch_chain_merge(entries, n, gt.G, gmap, n, pool_out, mtmp, d_radix_tmp, d_scan_tmp, d_nchains, st,
+                                ident, first)) != hipSuccess)
+        return e;
+    if ((e = hipMemcpyAsync(h_nchains, d_nchains, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+    const uint32_t nch = *h_nchains;
+    uint64_t* key_s = (uint64_t*)carve((size_t)nch * 8);
+    uint64_t* key_b = (uint64_t*)carve((size_t)nch * 8);
+    uint64_t* key_g = (uint64_t*)carve((size_t)nch * 8);
+    uint64_t* kA = (uint64_t*)carve((size_t)nch * 8);
+    uint64_t* kB = (uint64_t*)carve((size_t)nch * 8);
+    uint32_t* vA = (uint32_t*)carve((size_t)nch * 4);
+    uint32_t* vB = (uint32_t*)carve((size_t)nch * 4);
+    uint32_t* next_s = (uint32_t*)carve((size_t)nch * 4);
+    uint32_t* rank = (uint32_t*)carve((size_t)nch * 4);
+    uint32_t* bkey_buf = (uint32_t*)carve((size_t)nch * 4);
+    const uint32_t* bkey = nullptr;
+    if ((e = chain_order(pool_out, nch, gt, mp, key_s, key_b, key_g, kA, kB, vA, vB, next_s, bkey_buf, d_radix_tmp,
+                         d_scan_tmp, next_s, rank, &bkey, st)) != hipSuccess)
+        return e;
+    hipLaunchKernelGGL(entry_thr_kernel, dim3(grid), dim3(kBlock), 0, st, (const uint32_t*)gmap,
+                       (const uint32_t*)first, (const uint32_t*)next_s, n, thr);
+    return hipGetLastError();
 }
 
 hipError_t launch_emit(const uint32_t* obase, const uint32_t* bstart, const uint32_t* tbl, const int64_t* pool, int G,

@@ -63,7 +63,8 @@ struct mums_comm {
         ~Buf() {
             if (p) (void)hipFree(p);
         }
-    } rec, recv, rows, rrows, packed, packed_all, tags, rtags, ents, rents, efk, refk, ascii;
+    } rec, recv, rows, rrows, packed, packed_all, tags, rtags, ents, rents, efk, refk, ascii, thr, rthr;
+    uint64_t sent_rows = 0, sent_bytes = 0, recv_rows = 0, recv_bytes = 0;   // last FindMatches exchange
     bool packed_done = false;   // packed_all holds this run's genomes (gather_packed)
 };
 
@@ -723,6 +724,15 @@ void mums_comm_destroy(mums_comm* c) { delete c; }
 
 const char* mums_comm_last_error(mums_comm* c) { return c ? c->err.c_str() : "null communicator"; }
 
+int mums_comm_exchange_info(mums_comm* c, uint64_t* info) {
+    if (!c || !info) return MUMS_E_INVALID;
+    info[0] = c->sent_rows;
+    info[1] = c->sent_bytes;
+    info[2] = c->recv_rows;
+    info[3] = c->recv_bytes;
+    return MUMS_OK;
+}
+
 int mums_shard_key_ranges(const uint64_t* totals, uint32_t nbuckets, uint32_t world, uint32_t* first,
                           uint32_t* count) {
     if (!totals || !first || !count || world < 1) return MUMS_E_INVALID;
@@ -821,6 +831,106 @@ int mums_shard_run(mums_ctx* ctx, mums_comm* comm, int stage) {
     // default: chains labelled on the probes' own rank (key ranges balance the line sort and
     // the walks); MUMS_DEV_SHARD_BUCKET_CHAINS: labelled by the bucket owner (rows only)
     const bool labelled = getenv("MUMS_DEV_SHARD_BUCKET_CHAINS") == nullptr;
+    // default: only the probes the owners' replay needs travel;
+    // MUMS_DEV_SHARD_ALL_ROWS: every probe row (the round-5 layout)
+    const bool kept = labelled && getenv("MUMS_DEV_SHARD_ALL_ROWS") == nullptr;
+    comm->sent_rows = comm->sent_bytes = comm->recv_rows = comm->recv_bytes = 0;
+    if (kept) {
+        if (!comm->packed_done) RC(gather_packed(ctx, comm, st));
+        uint64_t nch = 0;
+        rc = mums_shard_chain_label(ctx, (const uint32_t*)comm->packed_all.p, &nch);
+        if (rc == MUMS_OK) rc = mums_probe_count(ctx, &P);
+        const uint64_t entb = 8ull * (G + 2);
+        if (rc == MUMS_OK && (comm->ents.ensure((nch + 1) * entb) || comm->efk.ensure((nch + 1) * 4) ||
+                              comm->thr.ensure((nch + 1) * 8)))
+            rc = MUMS_E_NOMEM;
+        // 7a. every chain entry to the owner of its bucket
+        std::vector<uint64_t> ce(W, 0), CE((size_t)W * W);
+        if (rc == MUMS_OK) rc = mums_shard_chain_entries(ctx, (uint32_t)W, bounds.data(), (int64_t*)comm->ents.p, nch + 1,
+                                                         ce.data());
+        AGREE(rc);
+        RC(comm->allgather_u64(ce.data(), W, CE.data(), st));
+        std::vector<uint64_t> src_ents(W);
+        uint64_t nents = 0;
+        for (int s2 = 0; s2 < W; ++s2) {
+            src_ents[s2] = CE[(size_t)s2 * W + R];
+            nents += src_ents[s2];
+        }
+        std::vector<uint64_t> sb(W), rb(W);
+        const void* rents = comm->ents.p;
+        void* rthr = comm->thr.p;
+        if (W > 1) {
+            AGREE(comm->rents.ensure((nents + 1) * entb) || comm->rthr.ensure((nents + 1) * 8) ? MUMS_E_NOMEM : MUMS_OK);
+            for (int q = 0; q < W; ++q) {
+                sb[q] = ce[q] * entb;
+                rb[q] = src_ents[q] * entb;
+            }
+            RC(comm->alltoallv(comm->ents.p, sb.data(), comm->rents.p, rb.data(), st));
+            rents = comm->rents.p;
+            rthr = comm->rthr.p;
+        }
+        rc = hipStreamSynchronize(st) != hipSuccess ? MUMS_E_HIP : MUMS_OK;
+        // 7b. the owners' answers {next_s, first} back to the entries' sources
+        if (rc == MUMS_OK) rc = mums_shard_entry_thresholds(ctx, (const int64_t*)rents, nents, (uint32_t*)rthr);
+        AGREE(rc);
+        if (W > 1) {
+            for (int q = 0; q < W; ++q) {
+                sb[q] = src_ents[q] * 8;
+                rb[q] = ce[q] * 8;
+            }
+            RC(comm->alltoallv(comm->rthr.p, sb.data(), comm->thr.p, rb.data(), st));
+        }
+        rc = hipStreamSynchronize(st) != hipSuccess ? MUMS_E_HIP : MUMS_OK;
+        // 7c. the kept rows, their tags and each entry's first sent row
+        if (rc == MUMS_OK && (comm->rows.ensure((P + 1) * rowb) || comm->tags.ensure((P + 1) * 4))) rc = MUMS_E_NOMEM;
+        std::vector<uint64_t> cnt(2 * (size_t)W, 0), CNT((size_t)W * 2 * W);
+        if (rc == MUMS_OK)
+            rc = mums_shard_kept_export(ctx, (uint32_t)W, (const uint32_t*)comm->thr.p, (int64_t*)comm->rows.p,
+                                        (uint32_t*)comm->tags.p, P + 1, (uint32_t*)comm->efk.p, cnt.data(),
+                                        cnt.data() + W);
+        AGREE(rc);
+        RC(comm->allgather_u64(cnt.data(), 2 * (size_t)W, CNT.data(), st));
+        std::vector<uint64_t> src_rows(W);
+        uint64_t nrows = 0, dropped = 0;
+        for (int s2 = 0; s2 < W; ++s2) {
+            src_rows[s2] = CNT[(size_t)s2 * 2 * W + R];
+            dropped += CNT[(size_t)s2 * 2 * W + W + R];
+            nrows += src_rows[s2];
+        }
+        for (int q = 0; q < W; ++q) comm->sent_rows += cnt[q];
+        comm->recv_rows = nrows;
+        comm->sent_bytes = comm->sent_rows * (rowb + 4);
+        comm->recv_bytes = nrows * (rowb + 4);
+        for (int q = 0; q < W; ++q) comm->sent_bytes += ce[q] * (entb + 8 + 4);
+        comm->recv_bytes += nents * (entb + 8 + 4);
+        const void *rrows = comm->rows.p, *rtags = comm->tags.p, *refk = comm->efk.p;
+        if (W > 1) {
+            AGREE(comm->rrows.ensure((nrows + 1) * rowb) || comm->rtags.ensure((nrows + 1) * 4) ||
+                          comm->refk.ensure((nents + 1) * 4)
+                      ? MUMS_E_NOMEM
+                      : MUMS_OK);
+            auto xchg = [&](const uint64_t* sendn, const uint64_t* recvn, uint64_t unit, const void* sendp,
+                            void* recvp) -> int {
+                for (int q = 0; q < W; ++q) {
+                    sb[q] = sendn[q] * unit;
+                    rb[q] = recvn[q] * unit;
+                }
+                return comm->alltoallv(sendp, sb.data(), recvp, rb.data(), st);
+            };
+            RC(xchg(cnt.data(), src_rows.data(), rowb, comm->rows.p, comm->rrows.p));
+            RC(xchg(cnt.data(), src_rows.data(), 4, comm->tags.p, comm->rtags.p));
+            RC(xchg(ce.data(), src_ents.data(), 4, comm->efk.p, comm->refk.p));
+            rrows = comm->rrows.p;
+            rtags = comm->rtags.p;
+            refk = comm->refk.p;
+        }
+        rc = hipStreamSynchronize(st) != hipSuccess ? MUMS_E_HIP : MUMS_OK;
+        if (rc == MUMS_OK)
+            rc = mums_shard_find_kept(ctx, (const int64_t*)rrows, (const uint32_t*)rtags, nrows, (const int64_t*)rents,
+                                      (const uint32_t*)refk, nents, (uint32_t)W, src_rows.data(), src_ents.data(),
+                                      dropped, (const uint32_t*)comm->packed_all.p);
+        return agree(comm, rc, st);
+    }
     if (labelled) {
         if (!comm->packed_done) RC(gather_packed(ctx, comm, st));
         uint64_t nch = 0;
@@ -846,6 +956,11 @@ int mums_shard_run(mums_ctx* ctx, mums_comm* comm, int stage) {
             nrows += src_rows[s2];
             nents += src_ents[s2];
         }
+        for (int q = 0; q < W; ++q) comm->sent_rows += cnt[q];
+        comm->recv_rows = nrows;
+        comm->sent_bytes = comm->sent_rows * (rowb + 4);
+        comm->recv_bytes = nrows * (rowb + 4) + nents * (entb + 4);
+        for (int q = 0; q < W; ++q) comm->sent_bytes += cnt[(size_t)W + q] * (entb + 4);
         const void *rrows = comm->rows.p, *rtags = comm->tags.p, *rents = comm->ents.p, *refk = comm->efk.p;
         if (W > 1) {
             AGREE(comm->rrows.ensure((nrows + 1) * rowb) || comm->rtags.ensure((nrows + 1) * 4) ||

@@ -396,7 +396,10 @@ class AbiShardStage:
         import numpy as np
         ci = np.zeros(4, dtype=np.uint64)
         self.engine.mh._check(self.engine.mh._lib.mums_shard_chain_info(self.engine.mh._ctx, ci.ctypes.data))
-        return {"probes": int(ci[0]), "chains": int(ci[1]), "ms": int(ci[2]) / 1000.0}
+        xi = np.zeros(4, dtype=np.uint64)
+        self.engine.mh._lib.mums_comm_exchange_info(self.comm, xi.ctypes.data)
+        return {"probes": int(ci[0]), "chains": int(ci[1]), "ms": int(ci[2]) / 1000.0, "owned_rows": int(ci[3]),
+                "sent_rows": int(xi[0]), "sent_bytes": int(xi[1]), "recv_rows": int(xi[2]), "recv_bytes": int(xi[3])}
 
     def close(self) -> None:
         if self.comm:

@@ -112,7 +112,11 @@ def test_shard_chains_labelled_where_the_probes_are(gpu_lib, oracle_mod):
     rank labels the chains of its own probes (mums_shard_chain_label), the bucket owners merge
     the entries and replay.  MatchList = the oracle's; the chain stage divides like the seed
     stage: the largest rank labels <= 1.5 x the mean probe count (by bucket owner one rank
-    would label ~95 %: the related genomes' main diagonal is one hash bucket)."""
+    would label ~95 %: the related genomes' main diagonal is one hash bucket).  Only the probes
+    the owners' replay needs travel (mums_shard_kept_export: chain-first and suspicious calls),
+    so the owner of the main diagonal's bucket receives <= 10 % of all probes; the others are
+    counted as collisions, and every owner still accounts for all AddHashEntry calls of its
+    buckets."""
     G, n, w, p, world = 8, 10_000_000, 15, 0.01, 4
     seqs = oracle_mod.generate(G, n, p, 12345)
     seed = oracle_mod.get_seed(w)
@@ -130,7 +134,40 @@ def test_shard_chains_labelled_where_the_probes_are(gpu_lib, oracle_mod):
     assert sum(lab) == sum(owned)
     mean = sum(lab) / world
     assert max(lab) <= 1.5 * mean, lab
-    assert max(owned) > 1.5 * mean, owned   # (the bucket owners' rows are as skewed as ever)
+    assert max(owned) > 1.5 * mean, owned   # (the bucket owners' AddHashEntry calls stay skewed ...)
+    rows = [i["owned_rows"] for i in info]   # (... but not the rows they receive)
+    assert max(rows) <= max(1.5 * sum(rows) / world, 0.10 * sum(lab)), (rows, sum(lab))
+    xi = sh.exchange_info
+    assert sum(x["recv_rows"] for x in xi) == sum(rows) == sum(x["sent_rows"] for x in xi)
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_shard_kept_rows_equal_all_rows(gpu_lib, oracle_mod, monkeypatch, world):
+    """The kept-probe export and the every-row export (MUMS_DEV_SHARD_ALL_ROWS) give the oracle's
+    MatchList and collision count; the kept export sends fewer rows."""
+    G, n, w, p = 5, 400_000, 15, 0.02
+    seqs = oracle_mod.generate(G, n, p, 77 + world)
+    seed = oracle_mod.get_seed(w)
+    lengths, starts, st = oracle_mod.find_matches(seqs, seed)
+    sent = {}
+    for all_rows in (False, True):
+        with monkeypatch.context() as m:
+            if all_rows:
+                m.setenv("MUMS_DEV_SHARD_ALL_ROWS", "1")
+            with gpu_lib.ShardedMemHash([0] * world, comm="local", table_size=7 if world == 3 else 40000) as sh:
+                sh.SetSeed(seed)
+                ml = sh.FindMatches(seqs)
+                coll = sum(s["collision_count"] for s in sh.stats_per_rank)
+                sent[all_rows] = sum(x["sent_rows"] for x in sh.exchange_info)
+        if world != 3:
+            assert len(ml) == len(lengths), all_rows
+            assert np.array_equal(ml.lengths, lengths) and np.array_equal(ml.starts, starts), all_rows
+            assert coll == st["collision_count"], all_rows
+        else:   # 7 hash buckets: the oracle with the same table size
+            l7, s7, st7 = oracle_mod.find_matches(seqs, seed, table_size=7)
+            assert np.array_equal(ml.lengths, l7) and np.array_equal(ml.starts, s7), all_rows
+            assert coll == st7["collision_count"], all_rows
+    assert sent[False] < sent[True], sent
 
 
 @pytest.mark.parametrize("world", [2, 3])
