@@ -5365,6 +5365,18 @@ int mums_shard_entry_thresholds(mums_ctx* ctx, const int64_t* d_entries, uint64_
     HIPCHK(launch_chain_thresholds(d_entries, nentries, ctx->gt, mp, ctx->pool.as<int64_t>(), ctx->chain_tmp.p,
                                    ctx->radix_tmp.p, ctx->tmp.p, &dc->nchains, &nm, (uint2*)d_thr, st));
     HIPCHK(hipStreamSynchronize(st));
+    if (getenv("MUMS_DEV_SHARD_DEBUG")) {   // development: what the owner answers
+        std::vector<uint32_t> h(2 * nentries);
+        HIPCHK(hipMemcpy(h.data(), d_thr, nentries * 8, hipMemcpyDeviceToHost));
+        uint64_t nfirst = 0, nnone = 0;
+        for (uint64_t e = 0; e < nentries; ++e) {
+            nfirst += h[2 * e + 1];
+            nnone += h[2 * e] == 0xFFFFFFFFu;
+        }
+        fprintf(stderr, "entry_thresholds: %llu entries -> %u chains, first %llu, next_s none %llu, e0 {%u,%u} e1 {%u,%u}\n",
+                (unsigned long long)nentries, nm, (unsigned long long)nfirst, (unsigned long long)nnone, h[0], h[1],
+                nentries > 1 ? h[2] : 0u, nentries > 1 ? h[3] : 0u);
+    }
     return MUMS_OK;
 }
 
@@ -5441,6 +5453,12 @@ int mums_shard_kept_export(mums_ctx* ctx, uint32_t nranks, const uint32_t* d_thr
         HIPCHK(hipStreamSynchronize(st));   // (xd is a host vector)
     }
     HIPCHK(hipStreamSynchronize(st));   // (starts / rcount are host vectors)
+    if (getenv("MUMS_DEV_SHARD_DEBUG")) {
+        uint64_t dr = 0;
+        for (uint32_t r = 0; r < nranks; ++r) dr += dropped_counts[r];
+        fprintf(stderr, "kept_export: P %llu chains %llu kept %llu dropped %llu\n", (unsigned long long)P,
+                (unsigned long long)nch, (unsigned long long)K, (unsigned long long)dr);
+    }
     return MUMS_OK;
 }
 

@@ -94,7 +94,9 @@ struct RcclComm : mums_comm {
     int allgather_u64(const uint64_t* send, size_t n, uint64_t* recv, hipStream_t st) override {
         if (scratch.ensure((world + 1) * n * 8 + 64)) return comm_fail(this, "allgather buffer");
         uint64_t* d = (uint64_t*)scratch.p;
-        if (hipMemcpy(d + (size_t)world * n, send, n * 8, hipMemcpyHostToDevice) != hipSuccess)
+        // on the collective's stream: a pageable host-to-device hipMemcpy may return before its
+        // DMA is done, and the rank's stream is not ordered after the null stream
+        if (hipMemcpyAsync(d + (size_t)world * n, send, n * 8, hipMemcpyHostToDevice, st) != hipSuccess)
             return comm_fail(this, "allgather H2D");
         ncclResult_t r = ncclAllGather(d + (size_t)world * n, d, n, ncclUint64, nc, st);
         if (r != ncclSuccess) return comm_fail(this, std::string("ncclAllGather: ") + ncclGetErrorString(r));
@@ -173,10 +175,13 @@ struct LocalComm : mums_comm {
             const uint64_t so = block_offsets(sh->sbytes[s].data(), world)[rank];
             const uint64_t nb = sh->sbytes[s][rank];
             if (nb != rb[s]) rc = comm_fail(this, "alltoallv: counts differ");
-            else if (nb && hipMemcpy((char*)d_recv + roff[s], (const char*)sh->dsend[s] + so, nb, hipMemcpyDefault) !=
-                               hipSuccess)
+            else if (nb && hipMemcpyAsync((char*)d_recv + roff[s], (const char*)sh->dsend[s] + so, nb, hipMemcpyDefault,
+                                          st) != hipSuccess)
                 rc = comm_fail(this, "alltoallv copy");
         }
+        // the copies complete before anything reads them: a device-to-device hipMemcpy may return
+        // before its copy is done, and the rank's kernels run on its own (non-blocking) stream
+        if (hipStreamSynchronize(st) != hipSuccess) rc = comm_fail(this, "alltoallv copy sync");
         sh->barrier();   // sources stay valid until every rank has copied
         return rc;
     }
@@ -208,7 +213,9 @@ struct HostComm : mums_comm {
             (soff[world] && hipMemcpy(hs.data(), d_send, soff[world], hipMemcpyDeviceToHost) != hipSuccess))
             return comm_fail(this, "alltoallv D2H");
         if (ops.alltoallv(user, hs.data(), sb, hr.data(), rb) != 0) return comm_fail(this, "host alltoallv callback failed");
-        if (roff[world] && hipMemcpy(d_recv, hr.data(), roff[world], hipMemcpyHostToDevice) != hipSuccess)
+        // on the rank's stream, waited for: the kernels that read d_recv run there
+        if (roff[world] && (hipMemcpyAsync(d_recv, hr.data(), roff[world], hipMemcpyHostToDevice, st) != hipSuccess ||
+                            hipStreamSynchronize(st) != hipSuccess))
             return comm_fail(this, "alltoallv H2D");
         return MUMS_OK;
     }
