@@ -68,6 +68,13 @@ struct DevBuf {
     template <typename T> T* as() const { return (T*)p; }
 };
 
+// host -> device on the context's stream, waited for: the context's kernels run on a
+// non-blocking stream, which a null-stream hipMemcpy does not order itself against
+static hipError_t h2d_sync(void* d, const void* h, size_t bytes, hipStream_t st) {
+    const hipError_t e = hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st);
+    return e != hipSuccess ? e : hipStreamSynchronize(st);
+}
+
 struct GenomeIn {
     const char* d_ptr;
     uint64_t n;
@@ -1301,7 +1308,7 @@ int restart_stage(mums_ctx* ctx, const MatchParams& mp, const ProbeSpace& ps, hi
     rc = finish_seeds(ctx, ps, st);
     if (rc) return rc;
     // the report counts the groups above MER_REPEAT_LIMIT of the whole stream
-    HIPCHK(hipMemcpy(&dc->repeat_limit, &rep, 8, hipMemcpyHostToDevice));
+    HIPCHK(h2d_sync(&dc->repeat_limit, &rep, 8, ctx->stream));
     ctx->hc.repeat_limit = rep;
     return MUMS_OK;
 }
@@ -2060,7 +2067,7 @@ int mums_add_genome(mums_ctx* ctx, const char* ascii, uint64_t n) {
     HIPCHK(hipSetDevice(ctx->device));
     char* d = nullptr;
     HIPCHK(hipMalloc(&d, n + 16));
-    if (n) HIPCHK(hipMemcpy(d, ascii, n, hipMemcpyHostToDevice));
+    if (n) HIPCHK(h2d_sync(d, ascii, n, ctx->stream));
     ctx->genomes.push_back({d, n, true});
     ctx->stage_done = 0;
     return MUMS_OK;
@@ -2424,7 +2431,7 @@ int mums_add_genome_sml(mums_ctx* ctx, const char* path, uint64_t* seed_out) {
     uint32_t* dw = nullptr;
     HIPCHK(hipMalloc(&d, n + 16));
     HIPCHK(hipMalloc(&dw, words * 4 + 16));
-    HIPCHK(hipMemcpy(dw, w.data(), words * 4, hipMemcpyHostToDevice));
+    HIPCHK(h2d_sync(dw, w.data(), words * 4, ctx->stream));
     HIPCHK(launch_unpack(dw, n, d, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     HIPCHK(hipFree(dw));
@@ -2741,8 +2748,8 @@ int mums_load_matches(mums_ctx* ctx, uint32_t seq_count, uint64_t count, const u
     HIPCHK(ctx->out_len.ensure((count + 1) * 8));
     HIPCHK(ctx->out_s.ensure((count + 1) * (size_t)seq_count * 8 + 8));
     if (count) {
-        HIPCHK(hipMemcpy(ctx->out_len.p, lengths, count * 8, hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(ctx->out_s.p, starts, count * (size_t)seq_count * 8, hipMemcpyHostToDevice));
+        HIPCHK(h2d_sync(ctx->out_len.p, lengths, count * 8, ctx->stream));
+        HIPCHK(h2d_sync(ctx->out_s.p, starts, count * (size_t)seq_count * 8, ctx->stream));
     }
     ctx->gt.G = (int)seq_count;
     ctx->M = count;
@@ -2759,7 +2766,7 @@ int mums_debug_std_sort(mums_ctx* ctx, const uint64_t* keys, uint64_t n, int dep
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(ctx->flen.ensure(n * 8 + 8));
     HIPCHK(ctx->fs.ensure(n * 4 + 8));
-    HIPCHK(hipMemcpy(ctx->flen.p, keys, n * 8, hipMemcpyHostToDevice));
+    HIPCHK(h2d_sync(ctx->flen.p, keys, n * 8, ctx->stream));
     HIPCHK(eo_sort_ids(ctx->eo, ctx->flen.as<uint64_t>(), (uint32_t)n, depth_override, ctx->fs.as<uint32_t>(),
                        ctx->stream));
     HIPCHK(hipMemcpy(ids, ctx->fs.p, n * 4, hipMemcpyDeviceToHost));
@@ -3067,7 +3074,7 @@ int shard_regroup(mums_ctx* ctx, uint64_t* dst, uint64_t nl, const std::vector<u
     if (rc) return rc;
     rc = finish_seeds(ctx, ps, st);
     if (rc) return rc;
-    HIPCHK(hipMemcpy(&dc->repeat_limit, &rep, 8, hipMemcpyHostToDevice));   // the report: the whole range's groups
+    HIPCHK(h2d_sync(&dc->repeat_limit, &rep, 8, ctx->stream));   // the report: the whole range's groups
     ctx->hc.repeat_limit = rep;
     ctx->restarts = restarts;
     ctx->offset_log.assign(offset_log, offset_log + restarts * (uint64_t)ctx->gt.G);
@@ -3135,8 +3142,8 @@ int mums_shard_merge(mums_ctx* ctx, const uint64_t* d_records, uint32_t nsources
     DevCounters* dc = ctx->counters.as<DevCounters>();
     if (ctx->profiling && !ctx->ev_ds[0])
         for (int i = 0; i < 16; ++i) HIPCHK(hipEventCreate(&ctx->ev_ds[i]));
-    HIPCHK(hipMemcpy(ctx->keybuf.p, chunks.data(), chunks.size() * 8, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(ctx->mstart.p, bst.data(), bst.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(h2d_sync(ctx->keybuf.p, chunks.data(), chunks.size() * 8, ctx->stream));
+    HIPCHK(h2d_sync(ctx->mstart.p, bst.data(), bst.size() * 4, ctx->stream));
     HIPCHK(hipEventRecord(ctx->ev[EV_START], st));
     HIPCHK(hipMemsetAsync(dc, 0, sizeof(DevCounters), st));
     HIPCHK(launch_regroup(d_records, ctx->recA.as<uint64_t>(), ctx->keybuf.as<uint64_t>(),
@@ -3166,7 +3173,7 @@ int mums_shard_merge(mums_ctx* ctx, const uint64_t* d_records, uint32_t nsources
             std::vector<uint32_t> sub(nbk + 1);
             for (uint32_t b = 0; b <= nbk; ++b)
                 sub[b] = b < b0 ? 0u : (b < b1 ? (uint32_t)(bst[b] - o) : (uint32_t)nc);
-            HIPCHK(hipMemcpy(ctx->mstart.p, sub.data(), sub.size() * 4, hipMemcpyHostToDevice));
+            HIPCHK(h2d_sync(ctx->mstart.p, sub.data(), sub.size() * 4, ctx->stream));
             rc = merge_stage(ctx, nc, mb, 2 * ctx->w + 1 - B, mp, ps, st, ctx->rec_ib, ctx->recA.as<uint64_t>() + o,
                              ctx->recB.as<uint64_t>() + o);
             if (rc) return rc;
@@ -3274,7 +3281,7 @@ int mums_shard_restart_plan(mums_ctx* ctx, uint64_t* d_stream, uint32_t nranks, 
                             [&](uint32_t r, uint32_t* d) -> int {
         hb.assign(segs[r].nb + 1, (uint32_t)(segs[r].hi - segs[r].lo));
         for (uint32_t b = 0; b < nbuckets[r]; ++b) hb[b] = (uint32_t)(dstart[first_bucket[r] + b] - segs[r].lo);
-        HIPCHK(hipMemcpy(d, hb.data(), hb.size() * 4, hipMemcpyHostToDevice));
+        HIPCHK(h2d_sync(d, hb.data(), hb.size() * 4, ctx->stream));
         return MUMS_OK;
     }, ctx->rsbst.as<uint32_t>(), n_live, &live, st);
     ctx->N = n_own;
@@ -3297,7 +3304,7 @@ int mums_shard_restart_plan(mums_ctx* ctx, uint64_t* d_stream, uint32_t nranks, 
             head[2 + b] = v;
         }
         bo += segs[r].nb + 1;
-        HIPCHK(hipMemcpy(out + o, head.data(), head.size() * 8, hipMemcpyHostToDevice));
+        HIPCHK(h2d_sync(out + o, head.data(), head.size() * 8, ctx->stream));
         o += head.size() * 8;
         if (nl) HIPCHK(hipMemcpyAsync(out + o, src + segs[r].lo, nl * 8, hipMemcpyDeviceToDevice, st));
         o += nl * 8;
@@ -3400,7 +3407,7 @@ int mums_shard_restart_counts(mums_ctx* ctx, uint64_t* info) {
         std::vector<uint64_t> cand(C);
         HIPCHK(hipMemcpy(cand.data(), d_list, C * 8, hipMemcpyDeviceToHost));
         std::sort(cand.begin(), cand.end());
-        HIPCHK(hipMemcpy(d_list, cand.data(), C * 8, hipMemcpyHostToDevice));
+        HIPCHK(h2d_sync(d_list, cand.data(), C * 8, ctx->stream));
     }
     ctx->ds_C = C;
     // per-genome block counts, this rank's part of every SML (full keys, genome-major)
@@ -4047,7 +4054,7 @@ int run_pipeline_pairwise(mums_ctx* ctx, int stage) {
             ctx->sorted_idx = dv;
             rc = ctx->key64 ? pairwise_rows<uint64_t>(ctx, nl, st) : pairwise_rows<uint32_t>(ctx, nl, st);
             if (rc) return rc;
-            HIPCHK(hipMemcpy(&dc->repeat_limit, &rep, 8, hipMemcpyHostToDevice));
+            HIPCHK(h2d_sync(&dc->repeat_limit, &rep, 8, ctx->stream));
             HIPCHK(hipMemcpy(&ctx->hc, dc, sizeof(DevCounters), hipMemcpyDeviceToHost));
         }
     } else if (ctx->progress_on) {   // LogProgress without a restart (MatchFinder.cpp:296-309)
@@ -5006,7 +5013,7 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
     ctx->stage_done = MUMS_STAGE_SEEDS;
     if (live_rec) {   // the report counts the groups above MER_REPEAT_LIMIT of the whole stream
         ctx->hc.repeat_limit = ctx->cr_cands;
-        HIPCHK(hipMemcpy(&dc->repeat_limit, &ctx->cr_cands, 8, hipMemcpyHostToDevice));
+        HIPCHK(h2d_sync(&dc->repeat_limit, &ctx->cr_cands, 8, ctx->stream));
     }
     if (stage >= MUMS_STAGE_ALL) {
         int tbits = 1;
