@@ -65,6 +65,17 @@ __device__ __forceinline__ unsigned walk_block() {
 #else
 #define MUMS_WALK_ATTR
 #endif
+// the lean lane-group walks (chain_walk_kernel, kGen = false) at four waves per SIMD (<= 128 VGPRs:
+// C3 long walks 5.8 -> 5.0 ms; the short walks spill at that target and stay at three);
+// MUMS_WALK_LEAN_WPE=0: no target
+#ifndef MUMS_WALK_LEAN_WPE
+#define MUMS_WALK_LEAN_WPE 4
+#endif
+#if MUMS_WALK_LEAN_WPE
+#define MUMS_WALK_LEAN_ATTR __attribute__((amdgpu_waves_per_eu(kGen ? 1 : MUMS_WALK_LEAN_WPE)))
+#else
+#define MUMS_WALK_LEAN_ATTR
+#endif
 #ifndef MUMS_HIT_VEC
 #define MUMS_HIT_VEC 1   // hit_word's window loads as one 16-B + one 12-B load (0: one load per word)
 #endif
@@ -223,8 +234,11 @@ __device__ __forceinline__ LineSpec line_spec(const SeedSpec& ss, const GenomeTa
 struct __attribute__((aligned(4))) Words4 { uint32_t x, y, z, w; };
 struct __attribute__((aligned(4))) Words3 { uint32_t x, y, z; };
 
-// hit bits of columns c0 .. c0+63 (bit i = column c0 + i) of the line of P
-template <int MG>
+// hit bits of columns c0 .. c0+63 (bit i = column c0 + i) of the line of P.
+// kGen = false: palindromic care set and odd weight only (every default seed, getSeed rank 0):
+// the column-by-column canonical-key fallback and the self-reverse-complement test are not
+// compiled in, so their registers do not weigh on the walks (the caller checks the seed)
+template <int MG, bool kGen = true>
 __device__ uint64_t hit_word(int64_t c0, const Mhe<MG>& P, const GenomeTable& gt, int64_t clo, int64_t chi,
                              const uint32_t* __restrict__ packed, const SeedSpec& ss, const LineSpec& ls) {
     if (c0 > chi || c0 + 63 < clo) return 0;
@@ -233,11 +247,13 @@ __device__ uint64_t hit_word(int64_t c0, const Mhe<MG>& P, const GenomeTable& gt
     if (c0 + 63 > chi) valid &= ~0ull >> (c0 + 63 - chi);
     const int ref = first_start(P);
     const int64_t sref = start_at(P, ref);
-    if (!ls.bitpar || sref <= 0) {   // generic: canonical keys column by column
-        uint64_t h = 0;
-        for (int i = 0; i < 64; ++i)
-            if ((valid >> i) & 1) h |= (uint64_t)hit_lane<MG>(c0 + i, P, gt, clo, chi, packed, ss) << i;
-        return h;
+    if constexpr (kGen) {
+        if (!ls.bitpar || sref <= 0) {   // generic: canonical keys column by column
+            uint64_t h = 0;
+            for (int i = 0; i < 64; ++i)
+                if ((valid >> i) & 1) h |= (uint64_t)hit_lane<MG>(c0 + i, P, gt, clo, chi, packed, ss) << i;
+            return h;
+        }
     }
     // per batch of (up to) 8 components: every window load is issued before the first
     // use, so a word costs one memory round trip per batch, not one per genome
@@ -318,22 +334,24 @@ __device__ uint64_t hit_word(int64_t c0, const Mhe<MG>& P, const GenomeTable& gt
         any |= k ? ((lo >> k) | (hi << (64 - k))) : lo;
     }
     uint64_t h = ~any & valid;
-    if (rev && ls.even_w) {   // drop self-reverse-complement windows (exact test)
-        for (uint64_t t = h; t; t &= t - 1) {
-            const int i = __builtin_ctzll(t);
-            if (!hit_lane<MG>(c0 + i, P, gt, clo, chi, packed, ss)) h &= ~(1ull << i);
+    if constexpr (kGen) {
+        if (rev && ls.even_w) {   // drop self-reverse-complement windows (exact test)
+            for (uint64_t t = h; t; t &= t - 1) {
+                const int i = __builtin_ctzll(t);
+                if (!hit_lane<MG>(c0 + i, P, gt, clo, chi, packed, ss)) h &= ~(1ull << i);
+            }
         }
     }
     return h;
 }
 
 // 64 hit bits in walk order: bit i = column from + dir * i
-template <int MG>
+template <int MG, bool kGen = true>
 __device__ __forceinline__ uint64_t hit_word_dir(int dir, int64_t from, const Mhe<MG>& P, const GenomeTable& gt,
                                                  int64_t clo, int64_t chi, const uint32_t* __restrict__ packed,
                                                  const SeedSpec& ss, const LineSpec& ls) {
-    if (dir > 0) return hit_word<MG>(from, P, gt, clo, chi, packed, ss, ls);
-    return __builtin_bitreverse64(hit_word<MG>(from - 63, P, gt, clo, chi, packed, ss, ls));
+    if (dir > 0) return hit_word<MG, kGen>(from, P, gt, clo, chi, packed, ss, ls);
+    return __builtin_bitreverse64(hit_word<MG, kGen>(from - 63, P, gt, clo, chi, packed, ss, ls));
 }
 
 // One 64-column word of a chain walk.  Walk offsets u >= 0 (column = start + dir * u);
@@ -364,7 +382,7 @@ __device__ __forceinline__ bool scan_word(uint64_t H, int64_t u0, int64_t* last,
 // Chain walk from hit column cur in direction dir, one word (64 columns) per step.
 // state 0: the chain ends at the returned column; 1: the chain reaches `stop` (returned:
 // a chain hit at or past it); 2: budget spent (returned: the last hit reached).
-template <int MG>
+template <int MG, bool kGen = true>
 __device__ int64_t walk_lane(int dir, int64_t cur, int64_t stop, int budget, const Mhe<MG>& P, const GenomeTable& gt,
                              int64_t clo, int64_t chi, const uint32_t* __restrict__ packed, const SeedSpec& ss,
                              const LineSpec& ls, int* state, unsigned* words) {
@@ -374,7 +392,7 @@ __device__ int64_t walk_lane(int dir, int64_t cur, int64_t stop, int budget, con
         if (dir > 0 ? col >= stop : col <= stop) { *state = 1; return col; }
         if (budget-- <= 0) { *state = 2; return col; }
         ++*words;
-        const uint64_t H = hit_word_dir<MG>(dir, cur + dir * u0, P, gt, clo, chi, packed, ss, ls);
+        const uint64_t H = hit_word_dir<MG, kGen>(dir, cur + dir * u0, P, gt, clo, chi, packed, ss, ls);
         const bool broke = scan_word(H, u0, &last, ls.L);
         u0 += 64;
         if (broke) {
@@ -561,7 +579,7 @@ __global__ __launch_bounds__(kBlock) void walk_line_key_kernel(const WalkItem* _
 
 // Queued walks, one lane per item, up to kWalkBudget 64-column words each (most chain ends
 // lie within a few words); the rest go on to chain_walk_kernel's lane groups.
-template <int MG, typename View>
+template <int MG, typename View, bool kGen = true>
 __global__ __launch_bounds__(kBlock) MUMS_WALK_ATTR void chain_walk_short_kernel(View v, const uint64_t* __restrict__ probe_info,
                                                                   GenomeTable gt, MatchParams mp, SeedSpec ss,
                                                                   const uint32_t* __restrict__ packed,
@@ -592,7 +610,7 @@ __global__ __launch_bounds__(kBlock) MUMS_WALK_ATTR void chain_walk_short_kernel
             const int dir = it.kind == 2 ? -1 : +1;
             int state;
             unsigned nw = 0;
-            const int64_t c = walk_lane<MG>(dir, it.cur, it.stop, kWalkBudget, A, gt, clo, chi, packed, ss, ls, &state,
+            const int64_t c = walk_lane<MG, kGen>(dir, it.cur, it.stop, kWalkBudget, A, gt, clo, chi, packed, ss, ls, &state,
                                             &nw);
             int npres = 0;
             #pragma unroll
@@ -754,8 +772,8 @@ constexpr unsigned kWalkHandoff = MUMS_WALK_HANDOFF;
 // maxsteps > 0: a walk still going after maxsteps steps is handed on (from its last hit) to
 // xq for the next launch with wider groups -- the few walks of hundreds of steps otherwise
 // set the kernel's duration one step at a time.
-template <int MG, typename View, int GS>
-__global__ __launch_bounds__(kBlock) MUMS_WALK_ATTR void chain_walk_kernel(View v, const uint64_t* __restrict__ probe_info,
+template <int MG, typename View, int GS, bool kGen = true>
+__global__ __launch_bounds__(kBlock) MUMS_WALK_ATTR MUMS_WALK_LEAN_ATTR void chain_walk_kernel(View v, const uint64_t* __restrict__ probe_info,
                                                             GenomeTable gt, MatchParams mp, SeedSpec ss,
                                                             const uint32_t* __restrict__ ord,
                                                             const uint32_t* __restrict__ packed,
@@ -796,7 +814,7 @@ __global__ __launch_bounds__(kBlock) MUMS_WALK_ATTR void chain_walk_kernel(View 
                 break;
             }
             ++steps;
-            const uint64_t H = hit_word_dir<MG>(dir, cur + dir * (u0 + 64 * (int64_t)gl), A, gt, clo, chi, packed,
+            const uint64_t H = hit_word_dir<MG, kGen>(dir, cur + dir * (u0 + 64 * (int64_t)gl), A, gt, clo, chi, packed,
                                                 ss, ls);
             const int f = H ? __builtin_ctzll(H) : 64;
             const int hb = H ? 63 - __builtin_clzll(H) : -1;
@@ -1050,6 +1068,16 @@ __global__ __launch_bounds__(kBlock) void gather_rows32_kernel(const int32_t* __
 
 inline unsigned grid_of(uint64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
+// host: the seed's care set is palindromic and its weight odd (line_spec's bitpar and !even_w)
+inline bool seed_bitpar_odd(const SeedSpec& ss) {
+    if (ss.pattern == 0 || ss.L <= 0 || ss.L > 64) return false;
+    const uint64_t pat = ss.pattern >> __builtin_ctzll(ss.pattern);
+    uint64_t rev = 0;
+    for (int i = 0; i < 64; ++i) rev |= ((pat >> i) & 1ull) << (63 - i);
+    rev >>= (64 - ss.L);
+    return rev == pat && (ss.w & 1);
+}
+
 // --- chunked FindMatches: chains labelled per slice of the probes ---------------------
 // launch_chains on a slice of the probes gives every probe its true chain entry (walks
 // read the genomes, not the other probes), but a chain whose probes fall into several
@@ -1284,6 +1312,9 @@ hipError_t chains_core(LV vl, const ChainWs& w, const uint32_t* ord, uint64_t P,
     const bool cdbg = getenv("MUMS_DEV_CHAIN_DEBUG") != nullptr;
     // refilled short-walk lanes (read per call: tests and A/B runs toggle it)
     const bool refill = getenv("MUMS_DEV_WALK_REFILL") && getenv("MUMS_DEV_WALK_REFILL")[0] == '1';
+    // the walks without the generic hit-word path when every window is tested by base comparison
+    // (palindromic care set, odd weight: hit_word<MG, false>); MUMS_DEV_WALK_GEN=1 keeps it
+    const bool lean = seed_bitpar_odd(ss) && !(getenv("MUMS_DEV_WALK_GEN") && getenv("MUMS_DEV_WALK_GEN")[0] == '1');
     // short walks in genome-position order (walk_key_kernel), MUMS_DEV_WALK_SORT=1: measured
     // slower at C3 than the queue's line order, kept for A/B runs
     const char* wsort_env = getenv("MUMS_DEV_WALK_SORT");
@@ -1326,6 +1357,10 @@ hipError_t chains_core(LV vl, const ChainWs& w, const uint32_t* ord, uint64_t P,
             hipLaunchKernelGGL((chain_walk_refill_kernel<MG, LV>), dim3(short_grid), dim3(kBlock), 0, st, vl, gt, mp,
                                ss, packed, (const WalkItem*)w.queue, (const unsigned int*)qshort, w.link, w.rcol,
                                w.lcol, w.queue_long, qlong);
+        else if (lean)
+            hipLaunchKernelGGL((chain_walk_short_kernel<MG, LV, false>), dim3(short_grid), dim3(kBlock), 0, st, vl,
+                               nullptr, gt, mp, ss, packed, (const WalkItem*)w.queue, (const unsigned int*)qshort,
+                               w.link, w.rcol, w.lcol, w.queue_long, qlong, order, (DevCounters*)ctr);
         else
             hipLaunchKernelGGL((chain_walk_short_kernel<MG, LV>), dim3(short_grid), dim3(kBlock), 0, st, vl, nullptr,
                                gt, mp, ss, packed, (const WalkItem*)w.queue, (const unsigned int*)qshort, w.link,
@@ -1353,16 +1388,22 @@ hipError_t chains_core(LV vl, const ChainWs& w, const uint32_t* ord, uint64_t P,
             }
         }
         // the queue of chain_link / chain_left is consumed: it takes the handed-on walks
-        hipLaunchKernelGGL((chain_walk_kernel<MG, LV, kWalkGroup>), dim3(walk_grid), dim3(kBlock), 0, st, vl, nullptr,
-                           gt, mp, ss, ord, packed, (const WalkItem*)w.queue_long, (const unsigned int*)qlong, w.link,
-                           w.rcol, w.lcol, cdbg ? qcount + 4 : nullptr, (DevCounters*)ctr, kWalkHandoff, w.queue,
-                           qcount + 2, lorder);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        if (kWalkHandoff)
-            hipLaunchKernelGGL((chain_walk_kernel<MG, LV, 64>), dim3(walk_grid), dim3(kBlock), 0, st, vl, nullptr, gt,
-                               mp, ss, ord, packed, (const WalkItem*)w.queue, (const unsigned int*)(qcount + 2),
-                               w.link, w.rcol, w.lcol, cdbg ? qcount + 4 : nullptr, (DevCounters*)ctr, 0u,
-                               (WalkItem*)nullptr, (unsigned int*)nullptr, (const uint64_t*)nullptr);
+#define MUMS_WALK_LAUNCH(GEN)                                                                                     \
+    do {                                                                                                             \
+        hipLaunchKernelGGL((chain_walk_kernel<MG, LV, kWalkGroup, GEN>), dim3(walk_grid), dim3(kBlock), 0, st, vl,  \
+                           nullptr, gt, mp, ss, ord, packed, (const WalkItem*)w.queue_long, (const unsigned int*)qlong, \
+                           w.link, w.rcol, w.lcol, cdbg ? qcount + 4 : nullptr, (DevCounters*)ctr, kWalkHandoff,     \
+                           w.queue, qcount + 2, lorder);                                                             \
+        if ((e = hipGetLastError()) != hipSuccess) return e;                                                         \
+        if (kWalkHandoff)                                                                                            \
+            hipLaunchKernelGGL((chain_walk_kernel<MG, LV, 64, GEN>), dim3(walk_grid), dim3(kBlock), 0, st, vl, nullptr, \
+                               gt, mp, ss, ord, packed, (const WalkItem*)w.queue, (const unsigned int*)(qcount + 2), \
+                               w.link, w.rcol, w.lcol, cdbg ? qcount + 4 : nullptr, (DevCounters*)ctr, 0u,           \
+                               (WalkItem*)nullptr, (unsigned int*)nullptr, (const uint64_t*)nullptr);               \
+    } while (0)
+        if (lean) MUMS_WALK_LAUNCH(false);
+        else MUMS_WALK_LAUNCH(true);
+#undef MUMS_WALK_LAUNCH
         if (ev_walk) (void)hipEventRecord(ev_walk[3 * pass + 2], st);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (cdbg) {   // development: walk queue sizes and the long walks' step histogram
