@@ -161,7 +161,9 @@ __global__ __launch_bounds__(kBlock) void cr_ck_kernel(CrStream s, GenomeTable g
 }
 
 // the G SortedMerLists as (genome << kbits | ckey, global index) pairs, genome-major
-// (ParallelMemHash compat: the SMLs its chunking walks, from the MemHash path's sorted stream)
+// (ParallelMemHash compat: the SMLs its chunking walks, from the MemHash path's sorted stream);
+// sv / ck optional (the chunking reads the keys only; the tie replay and the MER_REPEAT_LIMIT
+// plan need the rest)
 __global__ __launch_bounds__(kBlock) void cr_partition_kernel(CrStream s, GenomeTable gt,
                                                               const uint32_t* __restrict__ gscan, uint64_t nblk,
                                                               int kbits, uint64_t* __restrict__ sk,
@@ -171,7 +173,7 @@ __global__ __launch_bounds__(kBlock) void cr_partition_kernel(CrStream s, Genome
     cr_block_ranks(s, gt, blockIdx.x, gscan, nblk, [&](uint64_t j, int g, uint64_t i) {
         const uint64_t o = gt.base[g] + i, k = cr_key_in(s, j, sd[0], sd[1]);
         sk[o] = ((uint64_t)g << kbits) | k;
-        sv[o] = (uint32_t)cr_idx(s, j);
+        if (sv) sv[o] = (uint32_t)cr_idx(s, j);
         if (ck) ck[o] = k;
     });
 }
@@ -347,6 +349,214 @@ __global__ __launch_bounds__(kBlock) void cr_cand_kernel(CrStream s, uint64_t* _
     if (b - a + 1 <= restart::kRepeatLimit) return;
     const unsigned long long k = atomicAdd(cnt, 1ull);
     if (k < cap) list[k] = v;
+}
+
+// ---- ParallelMemHash compat: the chunk-major records straight from the sorted stream -----
+// The chunk-major stream is the stable partition of the sorted stream by chunk (above).  A
+// block boundary of the stream, R_g records of every genome g before it, is closed when no
+// record before it has a higher chunk than one after it: max_g chunk(R_g - 1) <= min_g
+// chunk(R_g).  Between two closed boundaries the records fill exactly their own position
+// range.  Nearly every block has both boundaries closed and one chunk: its records stay in
+// stream order.  The rest form units -- a block holding a chunk start, or a run of blocks
+// whose inner boundaries are open (a chunk start's equal-key records split by a block edge:
+// the longest genome's record opens chunk k, the others' close chunk k - 1) -- partitioned by
+// chunk inside the unit.  compat_recs_kernel's packed records then come out of one pass over
+// the stream, without the key2 / index arrays of the partition.  A unit above kCdUnit blocks
+// or kCdSpan chunks, a group-key clash or a masked-key run above MER_REPEAT_LIMIT (a chunk
+// might be cut: compat_truncate needs key2) set a flag bit; the caller then takes the
+// partition + compat_recs path.
+constexpr uint32_t kCdSpan = 32;   // chunks inside one unit
+constexpr uint32_t kCdUnit = 64;   // blocks per unit
+
+struct CdWs {   // workspace, nblk = cr_blocks(N)
+    uint64_t* bedge;    // 2 nblk: key2 of block b's first and last output record
+    uint32_t* pmax1;    // nblk + 1: 1 + highest chunk before boundary b (0: none)
+    uint32_t* qmin;     // nblk + 1: lowest chunk after boundary b (~0: none)
+    uint32_t* cfirst;   // nblk: block b's chunk range over its own records
+    uint32_t* clast;
+    uint32_t* units;    // 2 nblk: (first block, end block) of every unit
+};
+
+__host__ __device__ inline CdWs cd_ws(void* p, uint64_t nblk) {
+    CdWs w;
+    uint64_t* e = (uint64_t*)p;
+    w.bedge = e;
+    uint32_t* u = (uint32_t*)(e + 2 * nblk);
+    w.pmax1 = u;
+    w.qmin = u + (nblk + 1);
+    w.cfirst = u + 2 * (nblk + 1);
+    w.clast = w.cfirst + nblk;
+    w.units = w.clast + nblk;
+    return w;
+}
+
+// thread (b, g), b <= nblk: genome g's side of boundary b and of block b's chunk range
+__global__ __launch_bounds__(kBlock) void cd_bounds_kernel(GenomeTable gt, const uint32_t* __restrict__ gscan,
+                                                           uint64_t nblk, const uint64_t* __restrict__ cs, uint32_t nch,
+                                                           CdWs w) {
+    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int G = gt.G;
+    const uint64_t b = t / G;
+    const int g = (int)(t % G);
+    if (b > nblk) return;
+    const uint32_t* gs = gscan + (uint64_t)g * (nblk + 1);
+    const uint64_t R = gs[b], m = gs[nblk];
+    if (R > 0) atomicMax(&w.pmax1[b], compat_chunk_at(cs, nch, G, g, R - 1) + 1u);
+    if (R < m) {
+        const uint32_t q = compat_chunk_at(cs, nch, G, g, R);
+        atomicMin(&w.qmin[b], q);
+        if (b < nblk && gs[b + 1] > R) {   // genome g has records in block b
+            atomicMin(&w.cfirst[b], q);
+            atomicMax(&w.clast[b], compat_chunk_at(cs, nch, G, g, gs[b + 1] - 1));
+        }
+    }
+}
+
+__device__ __forceinline__ bool cd_open(const CdWs& w, uint64_t b) {
+    const uint32_t p1 = w.pmax1[b], q = w.qmin[b];
+    return p1 != 0u && q != 0xFFFFFFFFu && p1 - 1u > q;
+}
+
+__device__ __forceinline__ uint64_t cd_rec(uint64_t k, int kbits, uint64_t idx) {
+    return (compat_gid(k, kbits) << 33) | ((k & 1ull) << 32) | idx;
+}
+
+__device__ __forceinline__ bool cd_clash(uint64_t kp, uint64_t k, int kbits) {
+    return (kp >> 1) != (k >> 1) && compat_gid(kp, kbits) == compat_gid(k, kbits);
+}
+
+// one workgroup per stream block: single-chunk blocks between closed boundaries written in
+// stream order; a unit's first block lists the unit (flags[1] of them) for cd_unit_kernel
+__global__ __launch_bounds__(kBlock) void cd_direct_kernel(CrStream s, uint64_t nblk, int kbits, CdWs w,
+                                                           uint64_t* __restrict__ rec, uint32_t* __restrict__ flags) {
+    __shared__ uint32_t sd[2];
+    const uint64_t b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const uint64_t j0 = b * kCrBlk, j1 = s.N < j0 + kCrBlk ? s.N : j0 + kCrBlk;
+    // a masked-key run above MER_REPEAT_LIMIT holds a multiple of 1000 (cr_cand_kernel)
+    const uint64_t m = ((j0 + restart::kRepeatLimit - 1) / restart::kRepeatLimit + tid) * restart::kRepeatLimit;
+    if (m < j1) {
+        const uint64_t v = cr_key(s, m) >> 1;
+        const uint64_t a = cr_run_edge(s, m, v, -1), e = cr_run_edge(s, m, v, +1);
+        if (e - a + 1 > restart::kRepeatLimit) atomicOr(&flags[0], 4u);
+    }
+    if (cd_open(w, b)) return;   // inside a unit an earlier block heads
+    const uint32_t c0 = w.cfirst[b], c1 = w.clast[b];
+    if (c0 != c1 || cd_open(w, b + 1)) {
+        if (tid == 0) {
+            uint64_t e = b + 1;
+            uint32_t lo = c0, hi = c1;
+            while (e < nblk && cd_open(w, e) && e - b < kCdUnit) {
+                lo = min(lo, w.cfirst[e]);
+                hi = max(hi, w.clast[e]);
+                ++e;
+            }
+            if (e < nblk && cd_open(w, e)) atomicOr(&flags[0], 1u);
+            else if (hi - lo >= kCdSpan) atomicOr(&flags[0], 8u);
+            else {
+                const uint32_t u = atomicAdd(&flags[1], 1u);
+                w.units[2 * u] = (uint32_t)b;
+                w.units[2 * u + 1] = (uint32_t)e;
+            }
+        }
+        return;
+    }
+    cr_block_digits(s, b, sd);
+    __syncthreads();
+    const uint64_t ch = (uint64_t)c0 << kbits;
+    bool clash = false;
+    for (uint64_t j = j0 + tid; j < j1; j += kBlock) {
+        const uint64_t k = ch | cr_key_in(s, j, sd[0], sd[1]);
+        rec[j] = cd_rec(k, kbits, cr_idx(s, j));
+        if (j > j0) clash |= cd_clash(ch | cr_key_in(s, j - 1, sd[0], sd[1]), k, kbits);
+        if (j == j0) w.bedge[2 * b] = k;
+        if (j + 1 == j1) w.bedge[2 * b + 1] = k;
+    }
+    if (clash) atomicOr(&flags[0], 2u);
+}
+
+// the listed units (grid-stride): chunks from the genome ranks (kept per record in sc), a
+// stable partition by chunk over the unit, key2 by output position in k2 for the clash check
+__global__ __launch_bounds__(kBlock) void cd_unit_kernel(CrStream s, GenomeTable gt, const uint32_t* __restrict__ gscan,
+                                                         uint64_t nblk, const uint64_t* __restrict__ cs, uint32_t nch,
+                                                         int kbits, CdWs w, uint64_t* __restrict__ rec,
+                                                         uint64_t* __restrict__ k2, uint8_t* __restrict__ sc,
+                                                         uint32_t* __restrict__ flags) {
+    __shared__ uint32_t cpre[kCdSpan];
+    __shared__ uint32_t wc[kBlock / 64][kCdSpan];
+    __shared__ uint32_t sd[2], s_c0;
+    const int tid = threadIdx.x, wv = tid >> 6, G = gt.G;
+    const uint32_t nu = flags[1];
+    for (uint32_t li = blockIdx.x; li < nu; li += gridDim.x) {
+        const uint64_t b0 = w.units[2 * li], b1 = w.units[2 * li + 1];
+        const uint64_t u0 = b0 * kCrBlk, u1 = s.N < b1 * kCrBlk ? s.N : b1 * kCrBlk;
+        __syncthreads();   // the previous unit's LDS reads are done
+        if (tid < (int)kCdSpan) cpre[tid] = 0;
+        if (tid == 0) {
+            uint32_t c0 = w.cfirst[b0];
+            for (uint64_t b = b0 + 1; b < b1; ++b) c0 = min(c0, w.cfirst[b]);
+            s_c0 = c0;
+        }
+        __syncthreads();
+        const uint32_t c0 = s_c0;
+        for (uint64_t b = b0; b < b1; ++b)
+            cr_block_ranks(s, gt, b, gscan, nblk, [&](uint64_t j, int g, uint64_t o) {
+                const uint32_t c = compat_chunk_at(cs, nch, G, g, o) - c0;
+                sc[j] = (uint8_t)c;
+                atomicAdd(&cpre[c], 1u);
+            });
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t a = 0;
+            for (uint32_t c = 0; c < kCdSpan; ++c) {
+                const uint32_t x = cpre[c];
+                cpre[c] = a;
+                a += x;
+            }
+        }
+        for (uint64_t b = b0; b < b1; ++b) {
+            __syncthreads();   // (sd of the previous block read)
+            cr_block_digits(s, b, sd);
+            const uint64_t j0 = b * kCrBlk, j1 = s.N < j0 + kCrBlk ? s.N : j0 + kCrBlk;
+            for (uint64_t r0 = j0; r0 < j1; r0 += kBlock) {
+                for (int i = tid; i < (kBlock / 64) * (int)kCdSpan; i += kBlock) (&wc[0][0])[i] = 0;
+                __syncthreads();
+                const uint64_t j = r0 + tid;
+                const bool valid = j < j1;
+                const uint32_t c = valid ? sc[j] : 0u;
+                uint32_t tot;
+                const uint32_t rk = wave_match_rank<5>(c, valid, &tot);
+                if (valid && rk == 0) wc[wv][c] = tot;
+                __syncthreads();
+                if (valid) {
+                    uint32_t d = cpre[c] + rk;
+                    for (int x = 0; x < wv; ++x) d += wc[x][c];
+                    const uint64_t k = ((uint64_t)(c0 + c) << kbits) | cr_key_in(s, j, sd[0], sd[1]);
+                    k2[u0 + d] = k;
+                    rec[u0 + d] = cd_rec(k, kbits, cr_idx(s, j));
+                }
+                __syncthreads();
+                if (valid && rk == 0) atomicAdd(&cpre[c], tot);
+            }
+        }
+        __syncthreads();   // (k2 of the whole unit written: same workgroup, global memory)
+        bool clash = false;
+        for (uint64_t p = u0 + 1 + tid; p < u1; p += kBlock) clash |= cd_clash(k2[p - 1], k2[p], kbits);
+        if (clash) atomicOr(&flags[0], 2u);
+        for (uint64_t b = b0 + tid; b < b1; b += kBlock) {
+            const uint64_t j0 = b * kCrBlk, j1 = s.N < j0 + kCrBlk ? s.N : j0 + kCrBlk;
+            w.bedge[2 * b] = k2[j0];
+            w.bedge[2 * b + 1] = k2[j1 - 1];
+        }
+    }
+}
+
+// the clash check across block edges
+__global__ __launch_bounds__(kBlock) void cd_edges_kernel(uint64_t nblk, int kbits, CdWs w,
+                                                          uint32_t* __restrict__ flags) {
+    const uint64_t b = (uint64_t)blockIdx.x * kBlock + threadIdx.x + 1;
+    if (b >= nblk) return;
+    if (cd_clash(w.bedge[2 * b - 1], w.bedge[2 * b], kbits)) atomicOr(&flags[0], 2u);
 }
 
 // live[j - lo] for the records [lo, hi) of one chunk: SML index >= its phase's start point
@@ -618,6 +828,38 @@ hipError_t launch_cr_chunk_part(const CrStream& s, const GenomeTable& gt, const 
     if ((e = exclusive_scan_u32(cnt, words, d_scan_tmp, nullptr, st)) != hipSuccess) return e;
     hipLaunchKernelGGL(cr_chunk_part_kernel<true>, dim3((unsigned)nblk), dim3(kBlock), 0, st, s, gt, gscan, nblk, cs,
                        nch, kbits, cnt, key2, idx);
+    return hipGetLastError();
+}
+
+size_t cr_direct_ws_bytes(uint64_t N) {
+    const uint64_t nblk = cr_blocks(N);
+    return (size_t)nblk * 16 + (size_t)(6 * nblk + 2) * 4 + 64;
+}
+
+hipError_t launch_cr_compat_direct(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, const uint64_t* cs,
+                                   uint32_t nch, int kbits, uint64_t* rec, uint64_t* k2, uint8_t* sc, void* ws,
+                                   uint32_t* flags, hipStream_t st) {
+    const uint64_t nblk = cr_blocks(s.N);
+    hipError_t e = hipMemsetAsync(flags, 0, 8, st);
+    if (e != hipSuccess || nblk == 0) return e;
+    const CdWs w = cd_ws(ws, nblk);
+    // pmax1 = 0, qmin = ~0, cfirst = ~0, clast = 0
+    if ((e = hipMemsetAsync(w.pmax1, 0, (nblk + 1) * 4, st)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(w.qmin, 0xFF, (2 * nblk + 1) * 4, st)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(w.clast, 0, nblk * 4, st)) != hipSuccess) return e;
+    const uint64_t pairs = (nblk + 1) * (uint64_t)gt.G;
+    hipLaunchKernelGGL(cd_bounds_kernel, dim3((unsigned)((pairs + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, gt, gscan,
+                       nblk, cs, nch, w);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(cd_direct_kernel, dim3((unsigned)nblk), dim3(kBlock), 0, st, s, nblk, kbits, w, rec, flags);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const unsigned ugrid = (unsigned)std::min<uint64_t>(nblk, 1024);
+    hipLaunchKernelGGL(cd_unit_kernel, dim3(ugrid), dim3(kBlock), 0, st, s, gt, gscan, nblk, cs, nch, kbits, w, rec,
+                       k2, sc, flags);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (nblk > 1)
+        hipLaunchKernelGGL(cd_edges_kernel, dim3((unsigned)((nblk - 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, nblk,
+                           kbits, w, flags);
     return hipGetLastError();
 }
 

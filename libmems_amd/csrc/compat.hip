@@ -411,10 +411,7 @@ __global__ void compat_split_kernel(const uint64_t* __restrict__ sk, GenomeTable
 // Those kernels compare group keys of neighbours for equality only, so these bits serve
 // wherever two different neighbouring masked keys differ in them; a boundary where they do
 // not sets *clash and the caller numbers the groups by a scan of group heads instead (exact
-// either way).
-__device__ __forceinline__ uint64_t compat_gid(uint64_t k, int kbits) {   // masked ckey bits 1-30, chunk parity
-    return ((k >> 1) & 0x3FFFFFFFull) | (((k >> kbits) & 1ull) << 30);
-}
+// either way).  (compat_gid: mums_internal.h, shared with chunked.hip's direct records.)
 
 // list / cnt (optional): compat_cand_kernel's candidates, collected in the same pass
 __global__ void compat_recs_kernel(const uint64_t* __restrict__ key2, const uint32_t* __restrict__ idx, uint64_t n,
@@ -468,7 +465,19 @@ __global__ void compat_probe_chunk_kernel(const uint64_t* __restrict__ probe_inf
         for (uint64_t x = c + 1; x <= nch; ++x) pfirst[x] = (uint32_t)P;
 }
 
+__global__ void compat_strip_kernel(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uint64_t n,
+                                    uint64_t mask) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n) out[j] = in[j] & mask;
+}
+
 }  // namespace
+
+hipError_t launch_compat_strip(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t mask, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(compat_strip_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in, out, n, mask);
+    return hipGetLastError();
+}
 
 // scratch: n + 1 u32 (the scan fallback's heads), scan_tmp for exclusive_scan_u32 over n
 hipError_t launch_compat_recs(const uint64_t* key2, const uint32_t* idx, uint64_t n, int kbits, uint64_t* rec,

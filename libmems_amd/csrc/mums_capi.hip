@@ -182,6 +182,8 @@ struct mums_ctx {
     std::vector<uint32_t> compat_pfirst;  // compat + match log: first probe of every chunk (nch + 1)
     std::vector<uint32_t> log_ids;        // compat + match log: the logged entries (pool ids) in log order
     std::vector<uint64_t> compat_cons;    // compat: consumed SML positions of every chunk cut by MER_REPEAT_LIMIT
+    const uint64_t* compat_ck_src = nullptr;   // compat: crall not built yet, derive it from these SML keys
+    uint64_t compat_ck_mask = 0;
                                           // (nch x G, ~0 = not cut), compat_truncate
     bool progress_on = false;             // MatchFinder::LogProgress: restate the progress text
     std::string progress;                 // its text for the last seed stage
@@ -1507,6 +1509,15 @@ int prepare_run(mums_ctx* ctx, const std::vector<uint64_t>& lens) {
 // ctx->crall holds the genome-major SML keys.  *n_live = records kept.
 int progress_compat(mums_ctx* ctx, uint32_t nch, const std::vector<uint64_t>& hcs, hipStream_t st);
 
+// ctx->crall (the genome-major SML keys without the genome bits) on first use: the packed
+// path's partition leaves it out unless the tie replay or the MER_REPEAT_LIMIT plan needs it
+int compat_ck_ready(mums_ctx* ctx, hipStream_t st) {
+    if (!ctx->compat_ck_src) return MUMS_OK;
+    HIPCHK(launch_compat_strip(ctx->compat_ck_src, ctx->crall.as<uint64_t>(), ctx->N, ctx->compat_ck_mask, st));
+    ctx->compat_ck_src = nullptr;
+    return MUMS_OK;
+}
+
 // the candidate list of compat_truncate in ctx->rsplan: list (cap words) and its counter
 int compat_cand_slots(mums_ctx* ctx, uint32_t nch, uint64_t** list, unsigned long long** cnt, uint64_t* cap_out) {
     const int G = ctx->gt.G;
@@ -1554,6 +1565,7 @@ int compat_truncate(mums_ctx* ctx, uint32_t nch, const uint64_t* cs, int kbits, 
     HIPCHK(hipMemcpyAsync(d_list, cand.data(), C * 8, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(d_dm, hm.data(), (G + 1) * 8, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(d_db, hb.data(), (G + 1) * 8, hipMemcpyHostToDevice, st));
+    if ((rc0 = compat_ck_ready(ctx, st))) return rc0;
     const restart::PlanData d{G, d_dm, d_db, ctx->crall.as<uint64_t>()};
     HIPCHK(launch_compat_fire(d, key2, N, kbits, d_list, C, cs, nch, d_fire, d_cend, d_cons, st));
     std::vector<uint32_t> fire(C);
@@ -1690,6 +1702,8 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
     // radix sort always.
     const int B = std::max(0, kbits - 32);
     const bool packed_sml = B <= 7 && N > 0 && N < (1ull << 30) && !getenv("MUMS_DEV_COMPAT_RADIX");
+    const bool all_ties = wants_tie_order(ctx);
+    ctx->compat_ck_src = nullptr;
     DevBuf dst;            // the sorted stream's bucket starts (packed_sml)
     CrStream pstream{};    // the sorted stream (packed_sml): also the source of the chunk-major order
     HIPCHK(ctx->crall.ensure(N * 8 + 64));
@@ -1720,8 +1734,15 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
         pstream.kb = (uint32_t)(kbits - B);
         pstream.ib = 32;
         HIPCHK(launch_cr_counts(pstream, gt, ctx->crcnt.as<uint32_t>(), ctx->tmp.p, st));
+        // the chunking reads the SML keys only: the indices (tie replay) and crall (the
+        // MER_REPEAT_LIMIT plan, LogProgress) are written when a later step needs them
         HIPCHK(launch_cr_partition(pstream, gt, ctx->crcnt.as<uint32_t>(), kbits, ctx->kA.as<uint64_t>(),
-                                   ctx->vA.as<uint32_t>(), ctx->crall.as<uint64_t>(), st));
+                                   all_ties ? ctx->vA.as<uint32_t>() : nullptr,
+                                   all_ties ? ctx->crall.as<uint64_t>() : nullptr, st));
+        if (!all_ties) {
+            ctx->compat_ck_src = ctx->kA.as<uint64_t>();
+            ctx->compat_ck_mask = kmask;
+        }
         sk = ctx->kA.as<uint64_t>();
         sv = ctx->vA.as<uint32_t>();
     } else {
@@ -1770,7 +1791,7 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
         const uint64_t rws[1] = {nch};
         TieWs tw{};
         uint64_t flagged = 0;
-        const bool all = wants_tie_order(ctx);
+        const bool all = all_ties;
         bool split = true;   // a chunk start inside a run of equal keys: its SML order matters
         if (!all) {
             HIPCHK(launch_compat_split(sk, gt, cs, nch, &dc->scratch32, st));
@@ -1779,6 +1800,9 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
             HIPCHK(hipStreamSynchronize(st));
             split = h != 0;
         }
+        if (split && packed_sml && !all)   // the SMLs' indices for the replay
+            HIPCHK(launch_cr_partition(pstream, gt, ctx->crcnt.as<uint32_t>(), kbits, ctx->kA.as<uint64_t>(),
+                                       ctx->vA.as<uint32_t>(), nullptr, st));
         if (split) {
             rc = tie_order(ctx, N, sk, sk, nullptr, sv, all ? nullptr : sps, all ? nullptr : rws, all ? 0 : 1, &tw,
                            &flagged, st);
@@ -1795,7 +1819,32 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
     // order inside equal keys is the SMLs' (no run reordered), else a (chunk, ckey) radix sort
     // of the SMLs.  The genome-major SMLs' keys (genome bits off, ctx->crall) survive for the
     // MER_REPEAT_LIMIT plan below.
-    if (packed_sml && !reordered && cr_chunk_part_fits(N, nch)) {
+    // Direct form (the common case): compat_recs' packed records straight from the sorted
+    // stream when every block boundary is closed under the chunk order (chunked.hip); any flag
+    // falls back to the partition below.  It needs no key2 / index arrays, so it is taken only
+    // where no later step reads them: no chunk cut (flag 4 screens runs above
+    // MER_REPEAT_LIMIT), no rank split, match log or LogProgress.  MUMS_DEV_COMPAT_PART (read
+    // per call): the partition always.
+    uint64_t* drec = nullptr;
+    if (packed_sml && !reordered && N < (1ull << 32) && ctx->compat_ranks <= 1 && !ctx->match_log &&
+        !ctx->progress_on && !getenv("MUMS_DEV_COMPAT_PAIRS") && !getenv("MUMS_DEV_COMPAT_GID_SCAN") &&
+        !getenv("MUMS_DEV_COMPAT_PART")) {
+        uint64_t* out = pstream.rec == ctx->recA.as<uint64_t>() ? ctx->recB.as<uint64_t>() : ctx->recA.as<uint64_t>();
+        const size_t wsb = (cr_direct_ws_bytes(N) + 255) & ~(size_t)255;
+        HIPCHK(ctx->ckey.ensure(std::max<size_t>(N * 8 + 64, wsb + 64)));
+        uint32_t* d_flags = (uint32_t*)((char*)ctx->ckey.p + wsb);
+        HIPCHK(launch_cr_compat_direct(pstream, gt, ctx->crcnt.as<uint32_t>(), cs, nch, kbits, out, ctx->kB.as<uint64_t>(),
+                                       (uint8_t*)ctx->vB.p, ctx->ckey.p, d_flags, st));
+        uint32_t hf[2] = {0, 0};
+        HIPCHK(hipMemcpyAsync(hf, d_flags, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        if (getenv("MUMS_DEV_COMPAT_DEBUG"))
+            fprintf(stderr, "compat direct: flags %u, %u units, %u chunks\n", hf[0], hf[1], nch);
+        if (hf[0] == 0) drec = out;
+    }
+    if (drec) {
+        buf = 1;   // (key2 / index arrays not built: nothing below reads them)
+    } else if (packed_sml && !reordered && cr_chunk_part_fits(N, nch)) {
         HIPCHK(ctx->ckey.ensure(cr_chunk_part_cnt_words(N, nch) * 4 + 64));   // the (chunk, block) counts
         HIPCHK(ctx->tmp.ensure(std::max(ctx->tmp.cap, scan_tmp_bytes(cr_chunk_part_cnt_words(N, nch)))));
         HIPCHK(launch_cr_chunk_part(pstream, gt, ctx->crcnt.as<uint32_t>(), cs, nch, kbits, ctx->ckey.as<uint32_t>(),
@@ -1804,6 +1853,7 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
     } else {
         HIPCHK(launch_compat_chunk_keys(sk, sv, N, gt, kbits, cs, nch, ctx->ckey.as<uint64_t>(),
                                         ctx->cval.as<uint32_t>(), ctx->crall.as<uint64_t>(), st));
+        ctx->compat_ck_src = nullptr;   // crall written here; the radix sort below reuses kA
         HIPCHK(radix_sort<uint64_t>(ctx->ckey.as<uint64_t>(), ctx->cval.as<uint32_t>(), N, kbits + cbits,
                                     ctx->kA.as<uint64_t>(), ctx->vA.as<uint32_t>(), ctx->kB.as<uint64_t>(),
                                     ctx->vB.as<uint32_t>(), ctx->tmp.p, &buf, st));
@@ -1827,10 +1877,15 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
         unsigned long long* d_cnt = nullptr;
         uint64_t cap = 0;
         if ((rc = compat_cand_slots(ctx, nch, &d_list, &d_cnt, &cap))) return rc;
-        HIPCHK(launch_compat_recs((const uint64_t*)ctx->sorted_key, ctx->sorted_idx, N, kbits, ctx->recA.as<uint64_t>(),
-                                  &dc->scratch32, ctx->ckey.as<uint32_t>(), ctx->tmp.p, gid_scan, d_list, d_cnt, cap,
-                                  st));
-        ctx->sorted_rec = ctx->recA.as<uint64_t>();
+        if (drec) {   // no candidates: the direct form screened every masked-key run
+            HIPCHK(hipMemsetAsync(d_cnt, 0, 8, st));
+            ctx->sorted_rec = drec;
+        } else {
+            HIPCHK(launch_compat_recs((const uint64_t*)ctx->sorted_key, ctx->sorted_idx, N, kbits,
+                                      ctx->recA.as<uint64_t>(), &dc->scratch32, ctx->ckey.as<uint32_t>(), ctx->tmp.p,
+                                      gid_scan, d_list, d_cnt, cap, st));
+            ctx->sorted_rec = ctx->recA.as<uint64_t>();
+        }
     }
     rc = compat_truncate(ctx, nch, cs, kbits, &n_live, st, ctx->compat_rec);
     if (rc) return rc;
@@ -4344,6 +4399,7 @@ int progress_compat(mums_ctx* ctx, uint32_t nch, const std::vector<uint64_t>& hc
     const uint64_t Gu = (uint64_t)G;
     constexpr uint64_t kBuf = restart::kMerBuffer;
     if (hcs.size() < (uint64_t)nch * Gu) return fail(ctx, MUMS_E_HIP, "progress: chunk starts missing (internal error)");
+    if (int rc0 = compat_ck_ready(ctx, st)) return rc0;
     std::vector<ProgressEv> ev;
     std::vector<uint64_t> q, Sall((uint64_t)nch * Gu, 0);
     for (uint32_t c = 0; c < nch; ++c) {

@@ -163,6 +163,12 @@ __device__ __forceinline__ uint32_t wave_match_rank(uint32_t dg, bool valid, uin
     return __builtin_amdgcn_mbcnt_hi(ph, __builtin_amdgcn_mbcnt_lo(pl, 0u));
 }
 
+// ParallelMemHash compat records' group key (compat.hip, chunked.hip): masked-ckey bits 1-30
+// and the chunk's parity, from key2 = chunk << kbits | ckey
+__device__ __forceinline__ uint64_t compat_gid(uint64_t k, int kbits) {
+    return ((k >> 1) & 0x3FFFFFFFull) | (((k >> kbits) & 1ull) << 30);
+}
+
 // genome of a global seed-mer index (G <= 64: a linear scan is cheapest)
 __device__ __forceinline__ int genome_of(const GenomeTable& gt, uint64_t i) {
     int g = 0;
@@ -465,6 +471,8 @@ hipError_t launch_compat_cands(const uint64_t* key2, uint64_t N, uint64_t* list,
 hipError_t launch_compat_fire(const restart::PlanData& d, const uint64_t* key2, uint64_t N, int kbits,
                               const uint64_t* cand, uint64_t C, const uint64_t* cs, uint32_t nch, uint32_t* out,
                               uint64_t* cend, uint64_t* cons, hipStream_t st);
+// out[j] = in[j] & mask (the genome-major SML keys without the genome bits)
+hipError_t launch_compat_strip(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t mask, hipStream_t st);
 hipError_t launch_compat_recs(const uint64_t* key2, const uint32_t* idx, uint64_t n, int kbits, uint64_t* rec,
                               uint32_t* clash, uint32_t* scratch, void* scan_tmp, bool force_scan, uint64_t* list,
                               unsigned long long* cnt, uint64_t cap, hipStream_t st);
@@ -574,6 +582,16 @@ bool cr_chunk_part_fits(uint64_t N, uint32_t nch);
 hipError_t launch_cr_chunk_part(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, const uint64_t* cs,
                                 uint32_t nch, int kbits, uint32_t* cnt, void* d_scan_tmp, uint64_t* key2, uint32_t* idx,
                                 hipStream_t st);
+// The same stream as compat_recs' packed records in one pass (no key2 / index arrays) when every
+// block boundary of the sorted stream is closed under the chunk-major order; ws: cr_direct_ws_bytes.
+// *flags (host, after a stream sync) = 0: rec holds all N records; else the reason the caller
+// takes the partition + compat_recs path (1 open boundary, 2 group-key clash, 4 a masked-key run
+// above MER_REPEAT_LIMIT, 8 too many chunks in one unit).
+// k2 (N u64) and sc (N bytes): scratch of the units that hold chunk starts or open boundaries.
+size_t cr_direct_ws_bytes(uint64_t N);
+hipError_t launch_cr_compat_direct(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, const uint64_t* cs,
+                                   uint32_t nch, int kbits, uint64_t* rec, uint64_t* k2, uint8_t* sc, void* ws,
+                                   uint32_t* flags, hipStream_t st);
 hipError_t launch_cr_ck(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, uint64_t* ck, hipStream_t st,
                         const uint64_t* lbase = nullptr);
 // masked key of genome g's SML index e for every query g << 56 | e (gscan from launch_cr_counts)

@@ -202,3 +202,37 @@ def test_parallel_c3shape_known_answer(gpu_lib, oracle_mod):
     assert len(ml) == c["matches"] and st["mem_count"] == c["mem_count"]
     assert ml.text().split("\n", 1)[0] == c["first_line"]
     assert hashlib.md5(ml.text().encode()).hexdigest() == c["md5"]
+
+
+@pytest.mark.parametrize("idx", [0, 1, 2, 3, 4, 5, 7, "ragged", "many"])
+def test_parallel_direct_records_agree(gpu_lib, oracle_mod, monkeypatch, capfd, idx):
+    """The chunk-major records straight from the sorted stream (chunked.hip cd_*: every block
+    boundary closed, single-chunk blocks in stream order, blocks holding a chunk start
+    partitioned inside) and the partition + compat_recs path (MUMS_DEV_COMPAT_PART) give the
+    oracle's list, genomes of different lengths and 2000 chunks included; the direct form is
+    taken on all of them but the one whose runs the tie replay reorders."""
+    if idx == "ragged":
+        seqs = oracle_mod.generate(3, 400000, 0.02, 77)
+        seqs, w, chunk = [seqs[0], seqs[1][:250000], seqs[2][50000:]], 15, 3000
+    elif idx == "many":
+        seqs, w, chunk = oracle_mod.generate(3, 300_000, 0.02, 41), 15, 150
+    else:
+        G, n, p, w, chunk, gseed = COMPAT_SMALL[idx]
+        seqs = oracle_mod.generate(G, n, p, gseed)
+    seed = oracle_mod.get_seed(w)
+    lengths, starts, ost = oracle_mod.find_matches(seqs, seed, parallel_compat=True, chunk_size=chunk)
+    flags = []
+    for part in (False, True):
+        with monkeypatch.context() as m:
+            m.setenv("MUMS_DEV_COMPAT_DEBUG", "1")
+            if part:
+                m.setenv("MUMS_DEV_COMPAT_PART", "1")
+            ml, st = gpu_parallel(gpu_lib, seqs, seed, chunk)
+        lines = [l for l in capfd.readouterr().err.splitlines() if l.startswith("compat direct:")]
+        flags.append(lines)
+        assert st["chunks"] == ost["chunks"], part
+        assert len(ml) == len(lengths) and (ml.lengths == lengths).all() and (ml.starts == starts).all(), part
+    assert flags[1] == []   # the partition path never tries the direct form
+    if idx == 5:   # (w12 over 999-mer chunks: chunk starts inside equal-key runs, the tie replay
+        return     # reorders them and the partition path runs)
+    assert len(flags[0]) == 1 and flags[0][0].startswith("compat direct: flags 0,"), flags[0]
