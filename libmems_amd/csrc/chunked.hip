@@ -92,12 +92,29 @@ __device__ __forceinline__ uint64_t cr_key_in(const CrStream& s, uint64_t j, uin
     return ((uint64_t)d << s.kb) | ((s.rec[j] >> s.ib) & ((1ull << s.kb) - 1));
 }
 
-// the digits of block b's first and last records into LDS (thread 0; callers barrier first)
+// cr_key_in from a record already loaded (v = s.rec[j])
+__device__ __forceinline__ uint64_t cr_key_val(const CrStream& s, uint64_t v, uint64_t j, uint32_t d0, uint32_t d1) {
+    uint32_t d = d0;
+    if (d1 != d0) {
+        uint32_t lo = d0, n = d1 - d0;
+        while (n > 0) {
+            const uint32_t h = n >> 1;
+            if (s.dstart[lo + h + 1] <= j) { lo += h + 1; n -= h + 1; } else n = h;
+        }
+        d = lo;
+    }
+    return ((uint64_t)d << s.kb) | ((v >> s.ib) & ((1ull << s.kb) - 1));
+}
+
+// the digits of block b's first and last records into LDS (all threads call it; callers
+// barrier before reading sd): thread t tests digit t's range, so the block pays one load
+// latency instead of two dependent binary searches over dstart
 __device__ __forceinline__ void cr_block_digits(const CrStream& s, uint64_t b, uint32_t* sd) {
-    if (threadIdx.x == 0) {
-        const uint64_t j0 = b * kCrBlk, j1 = (s.N < j0 + kCrBlk ? s.N : j0 + kCrBlk) - 1;
-        sd[0] = cr_digit(s, j0);
-        sd[1] = cr_digit(s, j1);
+    const uint64_t j0 = b * kCrBlk, j1 = (s.N < j0 + kCrBlk ? s.N : j0 + kCrBlk) - 1;
+    for (uint32_t t = threadIdx.x; t < s.nd; t += blockDim.x) {
+        const uint64_t a = s.dstart[t], e = s.dstart[t + 1];
+        if (a <= j0 && j0 < e) sd[0] = t;
+        if (a <= j1 && j1 < e) sd[1] = t;
     }
 }
 
@@ -433,12 +450,20 @@ __global__ __launch_bounds__(kBlock) void cd_direct_kernel(CrStream s, uint64_t 
     const uint64_t b = blockIdx.x;
     const int tid = threadIdx.x;
     const uint64_t j0 = b * kCrBlk, j1 = s.N < j0 + kCrBlk ? s.N : j0 + kCrBlk;
-    // a masked-key run above MER_REPEAT_LIMIT holds a multiple of 1000 (cr_cand_kernel)
-    const uint64_t m = ((j0 + restart::kRepeatLimit - 1) / restart::kRepeatLimit + tid) * restart::kRepeatLimit;
-    if (m < j1) {
-        const uint64_t v = cr_key(s, m) >> 1;
-        const uint64_t a = cr_run_edge(s, m, v, -1), e = cr_run_edge(s, m, v, +1);
-        if (e - a + 1 > restart::kRepeatLimit) atomicOr(&flags[0], 4u);
+    cr_block_digits(s, b, sd);
+    __syncthreads();
+    // MER_REPEAT_LIMIT screen, inside the block: a masked-key run of more than 1000 records
+    // holds two positions 500 apart of one block -- two multiples of 500, or the block's first
+    // record and the one 500 on, or its last and the one 500 before (of a run crossing a block
+    // edge, 501 or more records lie on one side).  Runs of 501-1000 may flag too (fallback).
+    if (tid < 16) {
+        uint64_t x = ~0ull;
+        if (tid == 0) x = j0;
+        else if (tid == 1) x = j1 >= j0 + 501 ? j1 - 501 : ~0ull;
+        else x = ((j0 + 499) / 500 + (uint64_t)(tid - 2)) * 500;
+        if (x >= j0 && x + 500 < j1 &&
+            (cr_key_in(s, x, sd[0], sd[1]) >> 1) == (cr_key_in(s, x + 500, sd[0], sd[1]) >> 1))
+            atomicOr(&flags[0], 4u);
     }
     if (cd_open(w, b)) return;   // inside a unit an earlier block heads
     const uint32_t c0 = w.cfirst[b], c1 = w.clast[b];
@@ -461,16 +486,33 @@ __global__ __launch_bounds__(kBlock) void cd_direct_kernel(CrStream s, uint64_t 
         }
         return;
     }
-    cr_block_digits(s, b, sd);
-    __syncthreads();
     const uint64_t ch = (uint64_t)c0 << kbits;
+    const uint32_t d0 = sd[0], d1 = sd[1];
+    const uint64_t* __restrict__ src = s.rec;
     bool clash = false;
-    for (uint64_t j = j0 + tid; j < j1; j += kBlock) {
-        const uint64_t k = ch | cr_key_in(s, j, sd[0], sd[1]);
-        rec[j] = cd_rec(k, kbits, cr_idx(s, j));
-        if (j > j0) clash |= cd_clash(ch | cr_key_in(s, j - 1, sd[0], sd[1]), k, kbits);
-        if (j == j0) w.bedge[2 * b] = k;
-        if (j + 1 == j1) w.bedge[2 * b + 1] = k;
+    // 4 records per thread per batch, loaded before any is stored; the predecessor of a
+    // record (the clash check) from the lane below, lane 0 loads it
+    constexpr int kU = 4;
+    const int lane = tid & 63;
+    for (uint64_t r0 = j0; r0 < j1; r0 += kU * kBlock) {
+        uint64_t v[kU], vp[kU];
+        #pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const uint64_t j = r0 + (uint64_t)u * kBlock + tid;
+            v[u] = j < j1 ? src[j] : 0ull;
+            vp[u] = (lane == 0 && j > j0 && j < j1) ? src[j - 1] : 0ull;
+        }
+        #pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const uint64_t j = r0 + (uint64_t)u * kBlock + tid;
+            const uint64_t up = (uint64_t)__shfl_up((unsigned long long)v[u], 1, 64);
+            if (j >= j1) continue;
+            const uint64_t k = ch | cr_key_val(s, v[u], j, d0, d1);
+            rec[j] = cd_rec(k, kbits, v[u] & ((1ull << s.ib) - 1));
+            if (j > j0) clash |= cd_clash(ch | cr_key_val(s, lane ? up : vp[u], j - 1, d0, d1), k, kbits);
+            if (j == j0) w.bedge[2 * b] = k;
+            if (j + 1 == j1) w.bedge[2 * b + 1] = k;
+        }
     }
     if (clash) atomicOr(&flags[0], 2u);
 }
