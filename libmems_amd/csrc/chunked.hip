@@ -368,6 +368,169 @@ __global__ __launch_bounds__(kBlock) void cr_cand_kernel(CrStream s, uint64_t* _
     if (k < cap) list[k] = v;
 }
 
+// ---- ParallelMemHash compat: chunk starts from the sorted stream (no genome-major SMLs) ----
+// compat_breaks_kernel / compat_find_kernel / compat_split_kernel (compat.hip) read the SMLs
+// genome-major.  When no break walks back (the longest SML's record at k * CHUNK_SIZE starts
+// its masked-key group, the common case), chunk k starts at k * CHUNK_SIZE there, and the rest
+// needs few SML reads: the break mer b_k = SML_mx[k * CHUNK], the check on SML_mx[k * CHUNK - 1],
+// and for FindMer in SML g only lb = #records of g with key < b_k and ub = #records <= b_k --
+// a bsearch over a sorted list compares SML_g[mid] with b_k, i.e. mid with lb and ub.  An SML
+// element is a select (gscan's blocks, then a block scan); lb / ub are stream bounds of b_k
+// and the genomes' ranks there.  One workgroup per chunk start.  flags[0]: 1 a break walks
+// back, 2 a split the bounds cannot decide; the caller then builds the SMLs.
+
+// records of genome g in [j0, j) of block b, for every genome (cnt[kMaxG] in LDS, zeroed by
+// the caller, barrier after)
+__device__ __forceinline__ void cf_block_counts(const CrStream& s, const GenomeTable& gt, uint64_t j0, uint64_t j,
+                                                uint32_t* cnt) {
+    for (uint64_t x = j0 + threadIdx.x; x < j; x += kBlock) atomicAdd(&cnt[genome_of(gt, cr_idx(s, x))], 1u);
+}
+
+// stream position of SML_g[r] (all threads; result in *out after the last barrier)
+__device__ __forceinline__ void cf_select(const CrStream& s, const GenomeTable& gt, const uint32_t* __restrict__ gscan,
+                                          uint64_t nblk, int g, uint64_t r, uint32_t* s_cnt, uint64_t* s_b,
+                                          uint64_t* out) {
+    const uint32_t* gs = gscan + (uint64_t)g * (nblk + 1);
+    if (threadIdx.x == 0) {   // last block b with gs[b] <= r
+        uint64_t lo = 0, n = nblk;
+        while (n > 0) {
+            const uint64_t h = n >> 1;
+            if (gs[lo + h + 1] <= r) { lo += h + 1; n -= h + 1; } else n = h;
+        }
+        *s_b = lo;
+    }
+    __syncthreads();
+    const uint64_t b = *s_b;
+    const uint64_t j0 = b * kCrBlk, j1 = s.N < j0 + kCrBlk ? s.N : j0 + kCrBlk;
+    const uint32_t want = (uint32_t)(r - gs[b]);
+    // thread t's 16 consecutive records: count, block scan, the owner finds the record
+    constexpr uint32_t kPer = kCrBlk / kBlock;
+    const uint64_t a = j0 + (uint64_t)threadIdx.x * kPer;
+    uint32_t c = 0;
+    for (uint32_t u = 0; u < kPer; ++u)
+        if (a + u < j1) c += genome_of(gt, cr_idx(s, a + u)) == g ? 1u : 0u;
+    s_cnt[threadIdx.x] = c;
+    __syncthreads();
+    if (threadIdx.x < 64) {   // exclusive scan of the 256 counts by one wave, 4 per lane
+        uint32_t v0 = s_cnt[4 * threadIdx.x], v1 = s_cnt[4 * threadIdx.x + 1], v2 = s_cnt[4 * threadIdx.x + 2],
+                 v3 = s_cnt[4 * threadIdx.x + 3];
+        const uint32_t t4 = v0 + v1 + v2 + v3;
+        uint32_t inc = t4;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t t = __shfl_up(inc, d, 64);
+            if ((int)threadIdx.x >= d) inc += t;
+        }
+        const uint32_t ex = inc - t4;
+        s_cnt[4 * threadIdx.x] = ex;
+        s_cnt[4 * threadIdx.x + 1] = ex + v0;
+        s_cnt[4 * threadIdx.x + 2] = ex + v0 + v1;
+        s_cnt[4 * threadIdx.x + 3] = ex + v0 + v1 + v2;
+    }
+    __syncthreads();
+    const uint32_t e0 = s_cnt[threadIdx.x];
+    if (want >= e0 && want < e0 + c) {
+        uint32_t k = e0;
+        for (uint32_t u = 0; u < kPer; ++u)
+            if (a + u < j1 && genome_of(gt, cr_idx(s, a + u)) == g) {
+                if (k == want) { *out = a + u; break; }
+                ++k;
+            }
+    }
+    __syncthreads();
+}
+
+// first stream position whose key is >= q
+__device__ __forceinline__ uint64_t cf_lower(const CrStream& s, uint64_t q) {
+    const uint64_t d = q >> s.kb;
+    if (d >= s.nd) return s.N;
+    const uint64_t kq = q & ((1ull << s.kb) - 1);
+    uint64_t lo = s.dstart[d], n = s.dstart[d + 1] - lo;
+    while (n > 0) {
+        const uint64_t h = n >> 1;
+        if (((s.rec[lo + h] >> s.ib) & ((1ull << s.kb) - 1)) < kq) { lo += h + 1; n -= h + 1; } else n = h;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(kBlock) void compat_fast_chunks_kernel(CrStream s, GenomeTable gt,
+                                                                    const uint32_t* __restrict__ gscan, uint64_t nblk,
+                                                                    int mx, uint64_t chunk, int L,
+                                                                    uint64_t* __restrict__ cs,
+                                                                    uint32_t* __restrict__ flags) {
+    __shared__ uint32_t s_cnt[kBlock];
+    __shared__ uint32_t c_lo[kMaxG], c_hi[kMaxG];
+    __shared__ uint64_t s_b, s_pos[2], s_P[2], s_und[kMaxG];
+    __shared__ uint32_t s_nund;
+    const uint32_t k = blockIdx.x + 1;
+    const int G = gt.G;
+    const uint64_t i = (uint64_t)k * chunk;
+    cf_select(s, gt, gscan, nblk, mx, i, s_cnt, &s_b, &s_pos[0]);
+    cf_select(s, gt, gscan, nblk, mx, i - 1, s_cnt, &s_b, &s_pos[1]);
+    const uint64_t q = cr_key(s, s_pos[0]);
+    if ((cr_key(s, s_pos[1]) >> 1) == (q >> 1)) {   // the break walks back: the caller's SML path
+        if (threadIdx.x == 0) atomicOr(&flags[0], 1u);
+        return;
+    }
+    if (threadIdx.x == 0) {
+        s_P[0] = cf_lower(s, q);
+        s_P[1] = cf_lower(s, q + 1);
+    }
+    if (threadIdx.x < kMaxG) {
+        c_lo[threadIdx.x] = 0;
+        c_hi[threadIdx.x] = 0;
+    }
+    if (threadIdx.x == 0) s_nund = 0;
+    __syncthreads();
+    const uint64_t P0 = s_P[0], P1 = s_P[1];
+    const uint64_t b0 = P0 / kCrBlk, b1 = P1 / kCrBlk;
+    cf_block_counts(s, gt, b0 * kCrBlk, P0, c_lo);
+    cf_block_counts(s, gt, b1 * kCrBlk, P1, c_hi);
+    __syncthreads();
+    const int g = threadIdx.x;
+    if (g < G && g != mx) {
+    const uint64_t lb = (b0 < nblk ? gscan[(uint64_t)g * (nblk + 1) + b0] : gscan[(uint64_t)g * (nblk + 1) + nblk]) + c_lo[g];
+    const uint64_t ub = (b1 < nblk ? gscan[(uint64_t)g * (nblk + 1) + b1] : gscan[(uint64_t)g * (nblk + 1) + nblk]) + c_hi[g];
+    // compat_find_kernel's bsearch with SML_g[mid] <, ==, > q read as mid < lb, < ub, >= ub
+    const uint64_t n = gt.n[g];
+    uint64_t cur = 0;
+    bool found = false;
+    if (n != 0 && n >= (uint64_t)L) {
+        uint64_t start = 0, end = n - (uint64_t)L;
+        for (;;) {
+            const uint64_t mid = (start + end) / 2;
+            cur = mid;
+            if (mid >= lb && mid < ub) break;
+            if (mid < lb && mid < end) start = mid + 1;
+            else if (mid >= ub && start < mid) end = mid - 1;
+            else break;
+        }
+        found = cur >= lb && cur < ub;
+        if (found) cur = (q == 0) ? 0 : cur + 1;
+    }
+    cs[(uint64_t)k * G + g] = cur;
+    // compat_split_kernel's check SML_g[p - 1] == SML_g[p] at p = cur
+    const uint64_t p = cur;
+    if (p != 0 && p < gt.m[g]) {
+        if (found) {
+            if (p < ub) atomicOr(&flags[0], 2u);   // SML_g[p - 1] == q; SML_g[p] == q iff p < ub
+        } else if (p != lb) {                      // (p == lb: SML_g[p - 1] < q < SML_g[p])
+            s_und[atomicAdd(&s_nund, 1u)] = ((uint64_t)g << 56) | p;   // both on one side of q
+        }
+    }
+    }
+    if (g == mx) cs[(uint64_t)k * G + g] = i;
+    __syncthreads();
+    // the undecided ones: read both SML elements
+    const uint32_t nu = s_nund;
+    for (uint32_t u = 0; u < nu; ++u) {
+        const int gu = (int)(s_und[u] >> 56);
+        const uint64_t pu = s_und[u] & ((1ull << 56) - 1);
+        cf_select(s, gt, gscan, nblk, gu, pu - 1, s_cnt, &s_b, &s_pos[0]);
+        cf_select(s, gt, gscan, nblk, gu, pu, s_cnt, &s_b, &s_pos[1]);
+        if (threadIdx.x == 0 && cr_key(s, s_pos[0]) == cr_key(s, s_pos[1])) atomicOr(&flags[0], 2u);
+    }
+}
+
 // ---- ParallelMemHash compat: the chunk-major records straight from the sorted stream -----
 // The chunk-major stream is the stable partition of the sorted stream by chunk (above).  A
 // block boundary of the stream, R_g records of every genome g before it, is closed when no
@@ -870,6 +1033,15 @@ hipError_t launch_cr_chunk_part(const CrStream& s, const GenomeTable& gt, const 
     if ((e = exclusive_scan_u32(cnt, words, d_scan_tmp, nullptr, st)) != hipSuccess) return e;
     hipLaunchKernelGGL(cr_chunk_part_kernel<true>, dim3((unsigned)nblk), dim3(kBlock), 0, st, s, gt, gscan, nblk, cs,
                        nch, kbits, cnt, key2, idx);
+    return hipGetLastError();
+}
+
+hipError_t launch_compat_fast_chunks(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, int mx,
+                                    uint64_t chunk, int L, uint32_t nch, uint64_t* cs, uint32_t* flags, hipStream_t st) {
+    hipError_t e = hipMemsetAsync(flags, 0, 4, st);
+    if (e != hipSuccess || nch <= 1) return e;
+    hipLaunchKernelGGL(compat_fast_chunks_kernel, dim3(nch - 1), dim3(kBlock), 0, st, s, gt, gscan, cr_blocks(s.N), mx,
+                       chunk, L, cs, flags);
     return hipGetLastError();
 }
 

@@ -1706,6 +1706,23 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
     ctx->compat_ck_src = nullptr;
     DevBuf dst;            // the sorted stream's bucket starts (packed_sml)
     CrStream pstream{};    // the sorted stream (packed_sml): also the source of the chunk-major order
+    // lean: the chunk starts and the chunk-major records come from the sorted stream alone
+    // (compat_fast_chunks, cr_compat_direct) where no later step reads the SMLs or key2 arrays;
+    // the genome-major SMLs are built only when one of them declines.  MUMS_DEV_COMPAT_SML /
+    // MUMS_DEV_COMPAT_PART (read per call): the SML chunking / the partition path always.
+    const bool lean = packed_sml && !all_ties && N < (1ull << 32) && ctx->compat_ranks <= 1 && !ctx->match_log &&
+                      !ctx->progress_on && !getenv("MUMS_DEV_COMPAT_PAIRS") && !getenv("MUMS_DEV_COMPAT_GID_SCAN") &&
+                      !getenv("MUMS_DEV_COMPAT_PART");
+    bool have_sml = !packed_sml, sml_idx = !packed_sml;   // genome-major keys (kA) / indices (vA) written
+    auto build_sml = [&](bool idx) -> hipError_t {   // from the sorted stream (packed_sml)
+        hipError_t e = launch_cr_partition(pstream, gt, ctx->crcnt.as<uint32_t>(), kbits, ctx->kA.as<uint64_t>(),
+                                           idx ? ctx->vA.as<uint32_t>() : nullptr, nullptr, st);
+        have_sml = true;
+        sml_idx = sml_idx || idx;
+        ctx->compat_ck_src = ctx->kA.as<uint64_t>();
+        ctx->compat_ck_mask = kmask;
+        return e;
+    };
     HIPCHK(ctx->crall.ensure(N * 8 + 64));
     if (packed_sml) {
         HIPCHK(ctx->hist.ensure(((uint64_t)T << B) * 4 + 64));
@@ -1736,12 +1753,12 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
         HIPCHK(launch_cr_counts(pstream, gt, ctx->crcnt.as<uint32_t>(), ctx->tmp.p, st));
         // the chunking reads the SML keys only: the indices (tie replay) and crall (the
         // MER_REPEAT_LIMIT plan, LogProgress) are written when a later step needs them
-        HIPCHK(launch_cr_partition(pstream, gt, ctx->crcnt.as<uint32_t>(), kbits, ctx->kA.as<uint64_t>(),
-                                   all_ties ? ctx->vA.as<uint32_t>() : nullptr,
-                                   all_ties ? ctx->crall.as<uint64_t>() : nullptr, st));
-        if (!all_ties) {
-            ctx->compat_ck_src = ctx->kA.as<uint64_t>();
-            ctx->compat_ck_mask = kmask;
+        if (all_ties) {
+            HIPCHK(launch_cr_partition(pstream, gt, ctx->crcnt.as<uint32_t>(), kbits, ctx->kA.as<uint64_t>(),
+                                       ctx->vA.as<uint32_t>(), ctx->crall.as<uint64_t>(), st));
+            have_sml = sml_idx = true;
+        } else if (!lean) {
+            HIPCHK(build_sml(false));
         }
         sk = ctx->kA.as<uint64_t>();
         sv = ctx->vA.as<uint32_t>();
@@ -1760,7 +1777,37 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
     }
     uint32_t nch = 1;
     std::vector<uint64_t> hcs((size_t)G, 0);   // chunk starts (nch x G)
-    if (mx >= 0) {
+    bool fast_chunks = false;   // chunk starts from the sorted stream, no split (compat_fast_chunks)
+    if (mx >= 0 && !have_sml) {
+        const uint64_t nmx = gt.n[mx], kmax = nmx ? (nmx - 1) / chunk : 0;
+        if (kmax + 1 <= cap && (kmax == 0 || kmax * chunk < gt.m[mx]) && !getenv("MUMS_DEV_COMPAT_SML")) {
+            HIPCHK(launch_compat_fast_chunks(pstream, gt, ctx->crcnt.as<uint32_t>(), mx, chunk, ctx->L,
+                                             (uint32_t)(kmax + 1), cs, &dc->scratch32, st));
+            uint32_t h[2] = {0, 0};
+            HIPCHK(hipMemcpyAsync(&h[0], &dc->scratch32, 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(&h[1], &dc->err, 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            if (h[1] & 1u) return fail(ctx, MUMS_E_GAP, "Gap in genome sequence ('-' encountered)");
+            if (getenv("MUMS_DEV_COMPAT_DEBUG")) fprintf(stderr, "compat fast chunks: flags %u\n", h[0]);
+            if (h[0] == 0) {
+                fast_chunks = true;
+                nch = (uint32_t)(kmax + 1);
+                hcs.assign((size_t)nch * G, 0);
+                HIPCHK(hipMemcpyAsync(hcs.data(), cs, hcs.size() * 8, hipMemcpyDeviceToHost, st));
+                HIPCHK(hipStreamSynchronize(st));
+                for (uint32_t k = 1; k < nch; ++k)
+                    for (int g = 0; g < G; ++g)
+                        if (hcs[(size_t)k * G + g] < hcs[(size_t)(k - 1) * G + g])
+                            return fail(ctx, MUMS_E_UNSUPPORTED, "ParallelMemHash compat: decreasing chunk starts "
+                                                                 "(overlapping chunk ranges) not reproduced");
+            }
+        }
+        if (!fast_chunks) {
+            HIPCHK(hipMemsetAsync(cs, 0, (size_t)cap * G * 8, st));
+            HIPCHK(build_sml(false));
+        }
+    }
+    if (mx >= 0 && !fast_chunks) {
         HIPCHK(launch_compat_breaks(sk, gt, kmask, mx, chunk, cs, bm, cap, d_nch, &dc->err, st));
         uint32_t h[2] = {0, 0};
         HIPCHK(hipMemcpyAsync(&h[0], d_nch, 4, hipMemcpyDeviceToHost, st));
@@ -1792,17 +1839,15 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
         TieWs tw{};
         uint64_t flagged = 0;
         const bool all = all_ties;
-        bool split = true;   // a chunk start inside a run of equal keys: its SML order matters
-        if (!all) {
+        bool split = !fast_chunks;   // a chunk start inside a run of equal keys: its SML order matters
+        if (!all && !fast_chunks) {
             HIPCHK(launch_compat_split(sk, gt, cs, nch, &dc->scratch32, st));
             uint32_t h = 0;
             HIPCHK(hipMemcpyAsync(&h, &dc->scratch32, 4, hipMemcpyDeviceToHost, st));
             HIPCHK(hipStreamSynchronize(st));
             split = h != 0;
         }
-        if (split && packed_sml && !all)   // the SMLs' indices for the replay
-            HIPCHK(launch_cr_partition(pstream, gt, ctx->crcnt.as<uint32_t>(), kbits, ctx->kA.as<uint64_t>(),
-                                       ctx->vA.as<uint32_t>(), nullptr, st));
+        if (split && packed_sml && !sml_idx) HIPCHK(build_sml(true));   // the SMLs' indices for the replay
         if (split) {
             rc = tie_order(ctx, N, sk, sk, nullptr, sv, all ? nullptr : sps, all ? nullptr : rws, all ? 0 : 1, &tw,
                            &flagged, st);
@@ -1842,6 +1887,7 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
             fprintf(stderr, "compat direct: flags %u, %u units, %u chunks\n", hf[0], hf[1], nch);
         if (hf[0] == 0) drec = out;
     }
+    if (!drec && !have_sml) HIPCHK(build_sml(false));   // (the MER_REPEAT_LIMIT plan may read them)
     if (drec) {
         buf = 1;   // (key2 / index arrays not built: nothing below reads them)
     } else if (packed_sml && !reordered && cr_chunk_part_fits(N, nch)) {
@@ -1851,6 +1897,7 @@ int run_pipeline_compat(mums_ctx* ctx, int stage) {
                                     ctx->tmp.p, ctx->kB.as<uint64_t>(), ctx->vB.as<uint32_t>(), st));
         buf = 1;
     } else {
+        if (!sml_idx) HIPCHK(build_sml(true));
         HIPCHK(launch_compat_chunk_keys(sk, sv, N, gt, kbits, cs, nch, ctx->ckey.as<uint64_t>(),
                                         ctx->cval.as<uint32_t>(), ctx->crall.as<uint64_t>(), st));
         ctx->compat_ck_src = nullptr;   // crall written here; the radix sort below reuses kA

@@ -587,6 +587,11 @@ hipError_t launch_cr_chunk_part(const CrStream& s, const GenomeTable& gt, const 
 // *flags (host, after a stream sync) = 0: rec holds all N records; else the reason the caller
 // takes the partition + compat_recs path (1 open boundary, 2 group-key clash, 4 a masked-key run
 // above MER_REPEAT_LIMIT, 8 too many chunks in one unit).
+// ParallelMemHash chunk starts cs[k * G + g] (k = 1 .. nch - 1; row 0 the caller's) from the
+// sorted stream when no break walks back; *flags (4 B device) 0 = cs complete and no chunk start
+// splits an equal-key run, else the caller builds the genome-major SMLs (compat.hip kernels)
+hipError_t launch_compat_fast_chunks(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, int mx,
+                                    uint64_t chunk, int L, uint32_t nch, uint64_t* cs, uint32_t* flags, hipStream_t st);
 // k2 (N u64) and sc (N bytes): scratch of the units that hold chunk starts or open boundaries.
 size_t cr_direct_ws_bytes(uint64_t N);
 hipError_t launch_cr_compat_direct(const CrStream& s, const GenomeTable& gt, const uint32_t* gscan, const uint64_t* cs,

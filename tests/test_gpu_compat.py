@@ -208,7 +208,9 @@ def test_parallel_c3shape_known_answer(gpu_lib, oracle_mod):
 def test_parallel_direct_records_agree(gpu_lib, oracle_mod, monkeypatch, capfd, idx):
     """The chunk-major records straight from the sorted stream (chunked.hip cd_*: every block
     boundary closed, single-chunk blocks in stream order, blocks holding a chunk start
-    partitioned inside) and the partition + compat_recs path (MUMS_DEV_COMPAT_PART) give the
+    partitioned inside), with the chunk starts from the stream too (compat_fast_chunks) or from
+    the genome-major SMLs (MUMS_DEV_COMPAT_SML), and the partition + compat_recs path
+    (MUMS_DEV_COMPAT_PART) give the
     oracle's list, genomes of different lengths and 2000 chunks included; the direct form is
     taken on all of them but the one whose runs the tie replay reorders."""
     if idx == "ragged":
@@ -222,16 +224,19 @@ def test_parallel_direct_records_agree(gpu_lib, oracle_mod, monkeypatch, capfd, 
     seed = oracle_mod.get_seed(w)
     lengths, starts, ost = oracle_mod.find_matches(seqs, seed, parallel_compat=True, chunk_size=chunk)
     flags = []
-    for part in (False, True):
+    for env in (None, "MUMS_DEV_COMPAT_PART", "MUMS_DEV_COMPAT_SML"):
         with monkeypatch.context() as m:
             m.setenv("MUMS_DEV_COMPAT_DEBUG", "1")
-            if part:
-                m.setenv("MUMS_DEV_COMPAT_PART", "1")
+            if env:
+                m.setenv(env, "1")
             ml, st = gpu_parallel(gpu_lib, seqs, seed, chunk)
-        lines = [l for l in capfd.readouterr().err.splitlines() if l.startswith("compat direct:")]
-        flags.append(lines)
-        assert st["chunks"] == ost["chunks"], part
-        assert len(ml) == len(lengths) and (ml.lengths == lengths).all() and (ml.starts == starts).all(), part
+        err = capfd.readouterr().err.splitlines()
+        flags.append([l for l in err if l.startswith("compat direct:")])
+        if env is None:
+            fast = [l for l in err if l.startswith("compat fast chunks:")]
+            print(idx, fast)
+        assert st["chunks"] == ost["chunks"], env
+        assert len(ml) == len(lengths) and (ml.lengths == lengths).all() and (ml.starts == starts).all(), env
     assert flags[1] == []   # the partition path never tries the direct form
     if idx == 5:   # (w12 over 999-mer chunks: chunk starts inside equal-key runs, the tie replay
         return     # reorders them and the partition path runs)
