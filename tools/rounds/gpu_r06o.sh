@@ -2,7 +2,7 @@
 # Compat C3 kernel trace (where the 20 ms over MemHash's sort goes)
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/r06o
+OUT=gpurun_out/${1:-r06o}
 mkdir -p $OUT
 timeout -k 10 300 python3 -u tools/dev/compat_c3.py 3 > $OUT/plain.log 2>&1 || { tail -20 $OUT/plain.log; exit 10; }
 cat $OUT/plain.log
