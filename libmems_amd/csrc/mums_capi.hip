@@ -1457,8 +1457,6 @@ int prepare_run(mums_ctx* ctx, const std::vector<uint64_t>& lens) {
     ctx->offset_log.clear();
     ctx->M = ctx->P = 0;
     const int G = (int)lens.size();
-    if (ctx->enum_tol > 8)
-        return fail(ctx, MUMS_E_UNSUPPORTED, "enumeration tolerance above 8 (odometer slots of the GPU path)");
     uint64_t total = 0;
     for (uint64_t n : lens) total += n;
     uint64_t pat = ctx->seed;
@@ -2025,8 +2023,6 @@ int prepare_shard(mums_ctx* ctx) {
     }
     int rc = prepare_run(ctx, ctx->shard_len);
     if (rc) return rc;
-    if (ctx->enum_tol > 8)   // pairwise.hip kEnumMax
-        return fail(ctx, MUMS_E_UNSUPPORTED, "enumeration tolerance > 8");
     // the sharded merge / find build MemHash's MatchParams: a ParallelMemHash compat or
     // PairwiseMatchFinder context would silently get MemHash's MatchList
     if (ctx->pcompat)
@@ -2221,8 +2217,8 @@ int mums_find_stage(mums_ctx* ctx, int stage) {
         return MUMS_OK;
     }
     const bool big = ctx->N >= 0xFFFFFFF0ull || getenv("MUMS_DEV_CHUNK_RECORDS") != nullptr;
-    if (big && (ctx->pairwise || ctx->pcompat || ctx->enum_tol > 1))
-        return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed-mers: only MemHash / MaskedMemHash, enum_tol <= 1");
+    if (big && ctx->pcompat)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed-mers: ParallelMemHash compat not supported");
     if (ctx->pcompat && ctx->enum_tol > 1)
         return fail(ctx, MUMS_E_UNSUPPORTED, "ParallelMemHash compat with enumeration tolerance > 1");
     if (!ctx->start_points.empty() && ctx->start_points.size() != ctx->genomes.size())   // MatchFinder.cpp:197-199
@@ -2237,7 +2233,7 @@ int mums_find_stage(mums_ctx* ctx, int stage) {
     // the chunked mode may keep its (config-5-sized) tie workspace between seed-stage-only
     // calls; any other pipeline sizes its own
     if (!big && ctx->tiebuf_kept) release_tiebuf(ctx);
-    if (ctx->pairwise || ctx->enum_tol > 1) return run_pipeline_pairwise(ctx, stage);
+    if ((ctx->pairwise || ctx->enum_tol > 1) && !big) return run_pipeline_pairwise(ctx, stage);
     if (ctx->pcompat) return run_pipeline_compat(ctx, stage);
     return big ? run_pipeline_chunked(ctx, stage) : run_pipeline(ctx, stage);
 }
@@ -4801,7 +4797,12 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
     hipStream_t st = ctx->stream;
     const int G = (int)ctx->genomes.size();
     const uint64_t N = ctx->N;
-    MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, ctx->masked, ctx->seq_mask};
+    // PairwiseMatchFinder / enumeration tolerance > 1: every chunk's groups enumerated into
+    // rows (pairwise.hip over launch_chunk_pairs' 64-bit-index pairs) instead of the probe
+    // stage; the rows' order is the AddHashEntry call order as in run_pipeline_pairwise
+    const bool enum_rows = ctx->pairwise || ctx->enum_tol > 1;
+    MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, ctx->pairwise ? 0 : ctx->masked,
+                   ctx->pairwise ? 0 : ctx->seq_mask};
     GenomeTable& gt = ctx->gt;
     const int kbits = 2 * ctx->w + 1;
     // implicit digit bits: the record keeps 31 key bits + 33 index bits.  Above 8 of them
@@ -4899,6 +4900,14 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
             return fail(ctx, MUMS_E_NOMEM, "seed weight 20-21 in the chunked mode: records and side bytes do not fit");
         if (wants_tie_order(ctx) && !resident)
             return fail(ctx, MUMS_E_NOMEM, "repeat tolerance in the chunked mode: the records do not fit resident");
+    }
+    if (enum_rows && !resident)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "PairwiseMatchFinder / enumeration tolerance > 1 in the chunked mode "
+                                             "needs the resident layout");
+    DevBuf epair;   // enum_rows: one chunk's (full ckey, index) pairs + per-head call counts and offsets
+    if (enum_rows) {
+        HIPCHK(epair.ensure((nmax + 64) * 24 + 256));
+        HIPCHK(ctx->tmp.ensure(std::max(ctx->tmp.cap, scan_tmp_bytes(nmax + 1))));
     }
     if (resident) {
         HIPCHK(ctx->recA.ensure((N + 64) * 8));
@@ -5011,6 +5020,42 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
     const size_t Wrow = (size_t)(G + 1) * 8;
     const size_t chain_need = chain_tmp_bytes(find_chunk() + 1, ctx->table_size, G) + 4096;
     if (stage == MUMS_STAGE_ALL && ctx->tiebuf.p && ctx->tiebuf.cap < chain_need + (N / 4) * Wrow) release_tiebuf(ctx);
+    // rows of chunk c's Pc probes / calls appended behind the P_total so far (grown, kept)
+    auto grow_rows = [&](uint64_t Pc, uint32_t c) -> int {
+        if (P_total + Pc >= (1ull << 32) - 64)   // probe ids are 32-bit (bucket order, chains)
+            return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed probes in one FindMatches");
+        const size_t W = Wrow;
+        if (ctx->rowsall.cap < (P_total + Pc + 1) * W) {   // grow, keeping the rows so far
+            // sized for the chunks to come at this chunk's rate (+10 %): one growth
+            // at 2 x 3 Gbp instead of a doubling that would not fit next to the records
+            const uint64_t est = (uint64_t)((double)(P_total + Pc) * nch / (c + 1) * 1.1) + 1;
+            const size_t want = std::max(P_total + Pc + 1, est) * W;
+            DevBuf nb;
+            // (inside the kept workspace: all the room the chain scratch leaves, whatever the
+            // skewed first-chunk estimate says; outgrowing it moves the rows out below)
+            const bool in_tie = !ctx->rowsall.borrowed && ctx->tiebuf.p &&
+                                ctx->tiebuf.cap > chain_need + (P_total + Pc + 1) * W &&
+                                nb.borrow(ctx->tiebuf, 0, ctx->tiebuf.cap - chain_need);
+            if (!in_tie && ctx->tiebuf.p) {   // the rows outgrow the kept workspace: give it up
+                HIPCHK(hipStreamSynchronize(st));
+                if (ctx->rowsall.borrowed) {   // (rows so far inside it: moved out first)
+                    DevBuf keep;
+                    HIPCHK(keep.ensure(P_total * W + 64));
+                    if (P_total) HIPCHK(hipMemcpyAsync(keep.p, ctx->rowsall.p, P_total * W, hipMemcpyDeviceToDevice, st));
+                    HIPCHK(hipStreamSynchronize(st));
+                    ctx->rowsall.release();
+                    ctx->rowsall = keep;
+                }
+                release_tiebuf(ctx);
+            }
+            if (!in_tie) HIPCHK(nb.ensure(want));
+            if (P_total) HIPCHK(hipMemcpyAsync(nb.p, ctx->rowsall.p, P_total * W, hipMemcpyDeviceToDevice, st));
+            HIPCHK(hipStreamSynchronize(st));
+            ctx->rowsall.release();
+            ctx->rowsall = nb;
+        }
+        return MUMS_OK;
+    };
     for (uint32_t c = 0; c < nch; ++c) {
         const uint32_t dlo = c * nbc8;
         uint64_t n_c = 0;
@@ -5054,6 +5099,37 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
             ctx->sorted_rec = live_rec ? live_rec + o : (sbuf ? rB : rA);
         }
         HIPCHK(hipEventRecord(ctx->ev[EV_SORT], st));
+        if (enum_rows) {   // the chunk's AddHashEntry calls as rows (no probe stage)
+            uint64_t* ek = epair.as<uint64_t>();
+            uint64_t* ei = ek + (n_c + 32);
+            uint32_t* ncalls = (uint32_t*)(ei + (n_c + 32));
+            uint32_t* off = ncalls + (n_c + 32);
+            const PairView<uint64_t, uint64_t> pv{ek, ei};
+            uint32_t pc32 = 0;
+            if (n_c) {
+                HIPCHK(launch_chunk_pairs(ctx->sorted_rec, n_c, bstart, nbc + 1, (uint64_t)c * nbc, ek, ei, st));
+                if (ctx->pairwise) HIPCHK(launch_pairwise_count(pv, n_c, gt, ncalls, dc, st));
+                else HIPCHK(launch_enum_count(pv, n_c, gt, mp, ncalls, dc, st));
+                HIPCHK(hipMemcpyAsync(off, ncalls, n_c * 4, hipMemcpyDeviceToDevice, st));
+                HIPCHK(exclusive_scan_u32(off, n_c, ctx->tmp.p, &dc->nprobes, st));
+                HIPCHK(hipMemcpyAsync(&pc32, &dc->nprobes, 4, hipMemcpyDeviceToHost, st));
+                HIPCHK(hipStreamSynchronize(st));
+            }
+            const uint64_t Pc = pc32;
+            if (stage >= MUMS_STAGE_ALL && Pc) {
+                rc = grow_rows(Pc, c);
+                if (rc) return rc;
+                int64_t* rows = (int64_t*)((char*)ctx->rowsall.p + P_total * Wrow);
+                if (ctx->pairwise) HIPCHK(launch_pairwise_emit(pv, n_c, gt, ctx->L, ncalls, off, rows, st));
+                else HIPCHK(launch_enum_emit(pv, n_c, gt, mp, ctx->L, ncalls, off, rows, st));
+            }
+            HIPCHK(hipEventRecord(ctx->ev[EV_GROUPS], st));
+            HIPCHK(hipEventRecord(ctx->ev[EV_BUCKETS], st));
+            HIPCHK(hipEventSynchronize(ctx->ev[EV_BUCKETS]));
+            ms_groups += el(EV_SORT, EV_GROUPS);
+            P_total += Pc;
+            continue;
+        }
         if (n_c) {
             rc = groups_dispatch<RecViewT<33>>(ctx, RecViewT<33>{ctx->sorted_rec}, tiles, ub, mp, ps.probe_info,
                                                ps.probe_bucket, ps.slot_info, ps.slot_bucket, st);
@@ -5074,40 +5150,10 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
         groups += ctx->hc.ngroups;
         const uint64_t Pc = ctx->P;
         if (stage >= MUMS_STAGE_ALL && Pc) {
-            if (P_total + Pc >= (1ull << 32) - 64)   // probe ids are 32-bit (bucket order, chains)
-                return fail(ctx, MUMS_E_UNSUPPORTED, "more than 2^32 seed probes in one FindMatches");
-            const size_t W = (size_t)(G + 1) * 8;
-            if (ctx->rowsall.cap < (P_total + Pc + 1) * W) {   // grow, keeping the rows so far
-                // sized for the chunks to come at this chunk's rate (+10 %): one growth
-                // at 2 x 3 Gbp instead of a doubling that would not fit next to the records
-                const uint64_t est = (uint64_t)((double)(P_total + Pc) * nch / (c + 1) * 1.1) + 1;
-                const size_t want = std::max(P_total + Pc + 1, est) * W;
-                DevBuf nb;
-                // (inside the kept workspace: all the room the chain scratch leaves, whatever the
-                // skewed first-chunk estimate says; outgrowing it moves the rows out below)
-                const bool in_tie = !ctx->rowsall.borrowed && ctx->tiebuf.p &&
-                                    ctx->tiebuf.cap > chain_need + (P_total + Pc + 1) * W &&
-                                    nb.borrow(ctx->tiebuf, 0, ctx->tiebuf.cap - chain_need);
-                if (!in_tie && ctx->tiebuf.p) {   // the rows outgrow the kept workspace: give it up
-                    HIPCHK(hipStreamSynchronize(st));
-                    if (ctx->rowsall.borrowed) {   // (rows so far inside it: moved out first)
-                        DevBuf keep;
-                        HIPCHK(keep.ensure(P_total * W + 64));
-                        if (P_total) HIPCHK(hipMemcpyAsync(keep.p, ctx->rowsall.p, P_total * W, hipMemcpyDeviceToDevice, st));
-                        HIPCHK(hipStreamSynchronize(st));
-                        ctx->rowsall.release();
-                        ctx->rowsall = keep;
-                    }
-                    release_tiebuf(ctx);
-                }
-                if (!in_tie) HIPCHK(nb.ensure(want));
-                if (P_total) HIPCHK(hipMemcpyAsync(nb.p, ctx->rowsall.p, P_total * W, hipMemcpyDeviceToDevice, st));
-                HIPCHK(hipStreamSynchronize(st));
-                ctx->rowsall.release();
-                ctx->rowsall = nb;
-            }
+            rc = grow_rows(Pc, c);
+            if (rc) return rc;
             rc = materialize_dispatch<RecViewT<33>>(ctx, RecViewT<33>{ctx->sorted_rec}, mp, st,
-                                                    (int64_t*)((char*)ctx->rowsall.p + P_total * W));
+                                                    (int64_t*)((char*)ctx->rowsall.p + P_total * Wrow));
             if (rc) return rc;
         }
         P_total += Pc;

@@ -448,13 +448,19 @@ hipError_t launch_pairwise_emit(View v, uint64_t N, const GenomeTable& gt, int L
 hipError_t launch_digit_totals(const uint32_t* hist, uint32_t ndigits, uint32_t T, unsigned long long* out,
                                hipStream_t st);
 
-// MemHash with enumeration tolerance > 1 (<= 8): AddHashEntry calls per group, their rows
+// MemHash with enumeration tolerance > 1 (any: slot kernels up to 8, group walks above):
+// AddHashEntry calls per group, their rows
 template <typename View>
 hipError_t launch_enum_count(View v, uint64_t N, const GenomeTable& gt, const MatchParams& mp, uint32_t* ncalls,
                              void* ctr, hipStream_t st);
 template <typename View>
 hipError_t launch_enum_emit(View v, uint64_t N, const GenomeTable& gt, const MatchParams& mp, int L,
                             const uint32_t* ncalls, const uint32_t* off, int64_t* rows, hipStream_t st);
+
+// pairwise.hip: a chunked-mode chunk (RecViewT<33>, nb + 1 bucket starts, bucket j = implicit
+// digit digit0 + j) as (full ckey, 64-bit index) pairs for the enumeration kernels
+hipError_t launch_chunk_pairs(const uint64_t* rec, uint64_t n, const uint32_t* bstart, uint32_t nb, uint64_t digit0,
+                              uint64_t* key, uint64_t* idx, hipStream_t st);
 
 // compat.hip: ParallelMemHash chunk-compat mode (ParallelMemHash.cpp:42-121)
 hipError_t launch_genome_keys(uint64_t* ckey, uint64_t N, const GenomeTable& gt, int kbits, hipStream_t st);

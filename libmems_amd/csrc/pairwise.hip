@@ -106,7 +106,7 @@ __global__ void pw_emit_kernel(View v, uint64_t N, GenomeTable gt, int L, const 
 }
 
 // ---- enumeration tolerance > 1 -------------------------------------------------------
-constexpr int kEnumMax = 8;   // enum_tol bound of the GPU path (per-genome record slots)
+constexpr int kEnumMax = 8;   // enum_tol bound of the slot kernels (per-genome record slots); above: the walk kernels
 
 // MemHash::EnumerateMatches over the group at head h (per genome in SML order): per genome the
 // first min(count, enum_tol) records; rejected (false) when a genome has more than
@@ -223,6 +223,102 @@ __global__ void en_emit_kernel(View v, uint64_t N, GenomeTable gt, MatchParams m
     }
 }
 
+// ---- enumeration tolerance above kEnumMax ---------------------------------------------
+// Same AddHashEntry calls as en_count / en_emit, without per-genome record slots: the count
+// keeps c[g] = min(count, enum_tol) only, and each odometer combination re-walks the group,
+// taking the q[g]-th record of genome g (a genome's records in the group are in its
+// SortedMerList order, so its first c[g] records are the ones MemHash::EnumerateMatches
+// lists, MemHash.cpp:146-152).  O(group size) per AddHashEntry call: the rare large
+// tolerances pay for the walk, enum_tol <= kEnumMax keeps the slot kernels above.
+template <int MG, typename View>
+__device__ bool en_tally(const View& v, uint64_t h, uint64_t N, const GenomeTable& gt, const MatchParams& mp,
+                         uint32_t (&c)[MG], uint32_t* size) {
+    const uint64_t k0 = v.gkey(h);
+    uint32_t tally[MG];
+    for (int g = 0; g < MG; ++g) { tally[g] = 0; c[g] = 0; }
+    uint32_t n = 0;
+    bool ok = true;
+    for (uint64_t j = h; j < N && v.gkey(j) == k0; ++j) {
+        ++n;
+        const int g = genome_of(gt, v.gidx(j));
+        if (tally[g] < mp.enum_tol) ++c[g];
+        if (tally[g] > mp.repeat_tol) ok = false;
+        ++tally[g];
+    }
+    *size = n;
+    return ok;
+}
+
+template <int MG, typename View>
+__global__ void en_count_walk_kernel(View v, uint64_t N, GenomeTable gt, MatchParams mp, uint32_t* __restrict__ ncalls,
+                                     DevCounters* __restrict__ ctr) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    uint32_t k = 0;
+    if (pw_head(v, i)) {
+        uint32_t c[MG], size = 0;
+        const bool ok = en_tally<MG>(v, i, N, gt, mp, c, &size);
+        if (size > (uint32_t)kRepeatLimit) atomicAdd(&ctr->repeat_limit, 1ull);
+        bool two;
+        if (ok && size >= 2) k = en_calls<MG>(c, gt.G, mp, &two);
+    }
+    ncalls[i] = k;
+}
+
+template <int MG, typename View>
+__global__ void en_emit_walk_kernel(View v, uint64_t N, GenomeTable gt, MatchParams mp, int L,
+                                    const uint32_t* __restrict__ ncalls, const uint32_t* __restrict__ off,
+                                    int64_t* __restrict__ rows) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N || ncalls[i] == 0) return;
+    const int G = gt.G;
+    uint32_t c[MG], size = 0;
+    (void)en_tally<MG>(v, i, N, gt, mp, c, &size);
+    bool two;
+    const uint32_t K = en_calls<MG>(c, G, mp, &two);
+    const uint64_t k0 = v.gkey(i);
+    uint64_t o = off[i];
+    for (uint32_t t = 0; t < K; ++t) {
+        uint32_t q[MG];   // the record of each genome this combination takes (two: every kept one)
+        int64_t sv[MG];
+        uint32_t pv[MG];
+        for (int g = 0; g < G; ++g) { sv[g] = 0; pv[g] = 0; q[g] = 0; }
+        if (!two) {   // odometer: the last genome varies fastest (MatchFinder.cpp:371-390)
+            uint32_t rem = t;
+            for (int g = G - 1; g >= 0; --g) {
+                if (!c[g]) continue;
+                q[g] = rem % c[g];
+                rem /= c[g];
+            }
+        }
+        uint32_t seen[MG];
+        for (int g = 0; g < G; ++g) seen[g] = 0;
+        for (uint64_t j = i; j < N && v.gkey(j) == k0; ++j) {
+            const RecFields r = v.get(j);
+            const int g = genome_of(gt, r.idx);
+            const uint32_t s = seen[g]++;
+            if (s >= c[g]) continue;   // past the genome's first enum_tol records
+            if (two || s == q[g]) {    // (two: the list's records, the later one of a genome wins as in en_emit)
+                sv[g] = (int64_t)(r.idx - gt.base[g]) + 1;
+                pv[g] = r.par;
+            }
+        }
+        // SetDirection (MemHash.cpp:189-203) + CalculateOffset (MatchHashEntry.cpp:141-160)
+        int ref = -1;
+        for (int g = 0; g < G && ref < 0; ++g)
+            if (sv[g] != 0) ref = g;
+        int64_t offset = 0;
+        for (int g = ref + 1; g < G; ++g) {
+            if (sv[g] == 0) continue;
+            if (pv[g] != pv[ref]) sv[g] = -sv[g];
+            offset += sv[g] - sv[ref] - (sv[g] < 0 ? (int64_t)L : 0);
+        }
+        int64_t* row = rows + (o + t) * (uint64_t)(G + 1);
+        for (int g = 0; g < G; ++g) row[g] = sv[g];
+        row[G] = offset;
+    }
+}
+
 inline dim3 grid_of(uint64_t n) { return dim3((unsigned)((n + 255) / 256)); }
 
 }  // namespace
@@ -253,7 +349,12 @@ template <typename View>
 hipError_t launch_enum_count(View v, uint64_t N, const GenomeTable& gt, const MatchParams& mp, uint32_t* ncalls,
                              void* ctr, hipStream_t st) {
     if (N == 0) return hipSuccess;
-    if (gt.G > 32)
+    const bool walk = mp.enum_tol > (uint32_t)kEnumMax;
+    if (gt.G > 32 && walk)
+        hipLaunchKernelGGL((en_count_walk_kernel<64, View>), grid_of(N), dim3(256), 0, st, v, N, gt, mp, ncalls, (DevCounters*)ctr);
+    else if (walk)
+        hipLaunchKernelGGL((en_count_walk_kernel<32, View>), grid_of(N), dim3(256), 0, st, v, N, gt, mp, ncalls, (DevCounters*)ctr);
+    else if (gt.G > 32)
         hipLaunchKernelGGL((en_count_kernel<64, View>), grid_of(N), dim3(256), 0, st, v, N, gt, mp, ncalls, (DevCounters*)ctr);
     else
         hipLaunchKernelGGL((en_count_kernel<32, View>), grid_of(N), dim3(256), 0, st, v, N, gt, mp, ncalls, (DevCounters*)ctr);
@@ -264,7 +365,12 @@ template <typename View>
 hipError_t launch_enum_emit(View v, uint64_t N, const GenomeTable& gt, const MatchParams& mp, int L,
                             const uint32_t* ncalls, const uint32_t* off, int64_t* rows, hipStream_t st) {
     if (N == 0) return hipSuccess;
-    if (gt.G > 32)
+    const bool walk = mp.enum_tol > (uint32_t)kEnumMax;
+    if (gt.G > 32 && walk)
+        hipLaunchKernelGGL((en_emit_walk_kernel<64, View>), grid_of(N), dim3(256), 0, st, v, N, gt, mp, L, ncalls, off, rows);
+    else if (walk)
+        hipLaunchKernelGGL((en_emit_walk_kernel<32, View>), grid_of(N), dim3(256), 0, st, v, N, gt, mp, L, ncalls, off, rows);
+    else if (gt.G > 32)
         hipLaunchKernelGGL((en_emit_kernel<64, View>), grid_of(N), dim3(256), 0, st, v, N, gt, mp, L, ncalls, off, rows);
     else
         hipLaunchKernelGGL((en_emit_kernel<32, View>), grid_of(N), dim3(256), 0, st, v, N, gt, mp, L, ncalls, off, rows);
@@ -281,5 +387,33 @@ hipError_t launch_enum_emit(View v, uint64_t N, const GenomeTable& gt, const Mat
                                             const uint32_t*, const uint32_t*, int64_t*, hipStream_t);
 MUMS_INST_PW(PairView<uint32_t>)
 MUMS_INST_PW(PairView<uint64_t>)
+typedef PairView<uint64_t, uint64_t> PairView64;
+MUMS_INST_PW(PairView64)
+
+namespace {
+// chunk of the chunked mode (records key_low(31) << 33 | index, the 2w+1-31 top key bits
+// implicit: bucket j of the chunk is digit digit0 + j) as (full ckey, 64-bit index) pairs
+__global__ void chunk_pairs_kernel(const uint64_t* __restrict__ rec, uint64_t n, const uint32_t* __restrict__ bstart,
+                                   uint32_t nb, uint64_t digit0, uint64_t* __restrict__ key, uint64_t* __restrict__ idx) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t lo = 0, hi = nb;   // bucket of i: the last start <= i
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((uint64_t)bstart[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+    const uint64_t r = rec[i];
+    key[i] = ((digit0 + lo) << 31) | (r >> 33);
+    idx[i] = r & ((1ull << 33) - 1);
+}
+}  // namespace
+
+hipError_t launch_chunk_pairs(const uint64_t* rec, uint64_t n, const uint32_t* bstart, uint32_t nb, uint64_t digit0,
+                              uint64_t* key, uint64_t* idx, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(chunk_pairs_kernel, grid_of(n), dim3(256), 0, st, rec, n, bstart, nb, digit0, key, idx);
+    return hipGetLastError();
+}
 
 }  // namespace mums

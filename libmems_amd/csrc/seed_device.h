@@ -145,11 +145,12 @@ struct RecFields {
     uint64_t idx;   // global seed-mer index
 };
 
-// PairView: (ckey, global index) pairs (generic path, any weight).
-template <typename K>
+// PairView: (ckey, global index) pairs (generic path, any weight); 64-bit indices (I =
+// uint64_t) for the chunked mode's enumerations above 2^32 seed-mers.
+template <typename K, typename I = uint32_t>
 struct PairView {
     const K* key;
-    const uint32_t* idx;
+    const I* idx;
     __device__ __forceinline__ uint64_t gkey(uint64_t i) const { return (uint64_t)key[i] >> 1; }
     __device__ __forceinline__ uint32_t par(uint64_t i) const { return (uint32_t)(key[i] & 1); }
     __device__ __forceinline__ uint64_t gidx(uint64_t i) const { return idx[i]; }

@@ -4,6 +4,8 @@ against the oracle's restatement, bit for bit.  Parity for enum_tol > 1 rests on
 (no reference fixture covers it; its MemHash core is pinned by SURVEY Appendix C)."""
 import pytest
 
+from tests import repeat_inputs
+
 pytestmark = pytest.mark.gpu
 
 
@@ -38,10 +40,26 @@ def test_enumeration_tolerance_vs_oracle(gpu_lib, oracle_mod, G, n, p, w, rt, et
     assert st["collision_count"] == ost["collision_count"]
 
 
-def test_enumeration_tolerance_above_gpu_bound(gpu_lib, oracle_mod):
-    seqs = oracle_mod.generate(2, 10000, 0.01, 1)
-    with gpu_lib.MemHash(0) as mh:
-        mh.SetSeed(oracle_mod.get_seed(15))
-        mh.SetEnumerationTolerance(9)
-        with pytest.raises(gpu_lib.MumsError):
-            mh.FindMatches(seqs)
+@pytest.mark.parametrize("et,rt,G,masked,mask", [(9, 8, 3, 0, 0), (12, 39, 3, 0, 0), (16, 15, 4, 0, 0),
+                                                   (10, 39, 3, 1, 5), (11, 39, 3, 1, 0)])
+def test_enumeration_tolerance_above_slot_bound(gpu_lib, oracle_mod, et, rt, G, masked, mask):
+    """enum_tol above the slot kernels' 8 per-genome records (pairwise.hip en_*_walk_kernel):
+    40 copies of one element per genome, so groups hold up to 40 records of a genome and the
+    odometer runs up to et^G combinations per group."""
+    seqs = repeat_inputs.high_copy(G=G, n=60_000, copies=40, tandem=False, seed=et)
+    seed = oracle_mod.get_seed(15)
+    lengths, starts, ost = oracle_mod.find_matches(seqs, seed, repeat_tol=rt, enum_tol=et, masked=bool(masked),
+                                                   seq_mask=mask)
+    cls = gpu_lib.MaskedMemHash if masked else gpu_lib.MemHash
+    with cls(0) as mh:
+        mh.SetSeed(seed)
+        mh.SetRepeatTolerance(rt)
+        mh.SetEnumerationTolerance(et)
+        if masked:
+            mh.SetMask(mask)
+        ml = mh.FindMatches(seqs)
+        st = mh.stats()
+    assert st["probes"] == ost["probes"] > 0
+    assert st["collision_count"] == ost["collision_count"]
+    assert len(ml) == len(lengths)
+    assert (ml.lengths == lengths).all() and (ml.starts == starts).all()

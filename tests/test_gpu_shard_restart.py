@@ -281,7 +281,7 @@ def test_enumeration_tolerance(gpu_lib, oracle_mod, name, world, layout):
           enum_tol=o["enum_tol"], start_points=o.get("start_points"))
 
 
-@pytest.mark.parametrize("etol,rtol", [(2, 1), (3, 2), (8, 7)])
+@pytest.mark.parametrize("etol,rtol", [(2, 1), (3, 2), (8, 7), (12, 39)])
 def test_enumeration_tolerance_repeats(gpu_lib, oracle_mod, etol, rtol):
     seqs = repeat_inputs.high_copy(G=3, n=60_000, copies=40, tandem=False, seed=etol)
     check(gpu_lib, oracle_mod, seqs, 3, repeat_tol=rtol, enum_tol=etol)
