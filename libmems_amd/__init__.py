@@ -597,16 +597,19 @@ class ShardedMemHash:
     bucket-major MatchList of MemHash::FindMatches (DESIGN.md §6)."""
 
     def __init__(self, devices: Sequence[int], comm: str = "rccl", table_size: int = 40000, layout: str = "blocks",
-                 parallel_compat: bool = False, chunk_size: int = 200000):
+                 parallel_compat: bool = False, chunk_size: int = 200000, pairwise: bool = False):
         """layout "blocks": a contiguous genome block per rank; "slices": every genome cut into
         world / G position slices (BASELINE config 5: two 3 Gbp genomes over 8 GPUs).
         parallel_compat: ParallelMemHash's MatchList (ParallelMemHash.cpp:42-121, CHUNK_SIZE =
         chunk_size): every rank searches a contiguous range of the chunks, the bucket owners
-        re-add the ranks' tables rank after rank (compat_ranks.hip)."""
+        re-add the ranks' tables rank after rank (compat_ranks.hip).
+        pairwise: PairwiseMatchFinder's MatchList (PairwiseMatchFinder.cpp:37-73): every rank
+        writes the pair rows of its key range's groups (mums_capi.hip shard_enum_rows)."""
         if layout not in ("blocks", "slices"):
             raise ValueError("layout: 'blocks' or 'slices'")
         self.layout = layout
         self.parallel_compat = bool(parallel_compat)
+        self.pairwise = bool(pairwise)
         self.chunk_size = int(chunk_size)
         self._lib = load_library()
         self.devices = list(devices)
@@ -711,6 +714,8 @@ class ShardedMemHash:
             mh.LogProgress(self.progress)
             if self.parallel_compat:
                 mh._check(self._lib.mums_set_parallel_compat(mh._ctx, 1, self.chunk_size))
+            if self.pairwise:
+                mh._check(self._lib.mums_set_pairwise(mh._ctx, 1))
         sp = getattr(self, "_start_points", None)
         if sp is not None:
             for mh in self.ranks:

@@ -655,10 +655,11 @@ __global__ __launch_bounds__(kBlock) void entry_first_kernel(const uint32_t* __r
 // A sharded rank's merged packed records (its MSD buckets [kfirst, kfirst + nb), starts
 // bst[0..nb]) as (full ckey, 32-bit global index) pairs: the group scans that need a
 // group's whole key (enumeration tolerance, pairwise.hip) then never merge two buckets.
+template <typename I, int IB>
 __global__ __launch_bounds__(kBlock) void rec_pairs_kernel(const uint64_t* __restrict__ rec, uint64_t n,
                                                            const uint32_t* __restrict__ bst, uint32_t nb,
                                                            uint32_t kfirst, int kb_rec, uint64_t* __restrict__ key,
-                                                           uint32_t* __restrict__ idx) {
+                                                           I* __restrict__ idx) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     uint32_t lo = 0, hi = nb;   // last bucket j with bst[j] <= i (empty buckets skipped)
@@ -668,8 +669,8 @@ __global__ __launch_bounds__(kBlock) void rec_pairs_kernel(const uint64_t* __res
         else hi = mid - 1;
     }
     const uint64_t r = rec[i];
-    key[i] = ((uint64_t)(kfirst + lo) << kb_rec) | (r >> 32);
-    idx[i] = (uint32_t)r;
+    key[i] = ((uint64_t)(kfirst + lo) << kb_rec) | (r >> IB);
+    idx[i] = (I)(r & ((1ull << IB) - 1));
 }
 
 }  // namespace
@@ -677,8 +678,16 @@ __global__ __launch_bounds__(kBlock) void rec_pairs_kernel(const uint64_t* __res
 hipError_t launch_rec_pairs(const uint64_t* rec, uint64_t n, const uint32_t* d_bst, uint32_t nb, uint32_t kfirst,
                             int kb_rec, uint64_t* key, uint32_t* idx, hipStream_t st) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(rec_pairs_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, rec, n,
-                       d_bst, nb, kfirst, kb_rec, key, idx);
+    hipLaunchKernelGGL((rec_pairs_kernel<uint32_t, 32>), dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+                       rec, n, d_bst, nb, kfirst, kb_rec, key, idx);
+    return hipGetLastError();
+}
+
+hipError_t launch_rec_pairs33(const uint64_t* rec, uint64_t n, const uint32_t* d_bst, uint32_t nb, uint32_t kfirst,
+                              int kb_rec, uint64_t* key, uint64_t* idx, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL((rec_pairs_kernel<uint64_t, 33>), dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+                       rec, n, d_bst, nb, kfirst, kb_rec, key, idx);
     return hipGetLastError();
 }
 

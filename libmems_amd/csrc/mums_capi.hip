@@ -2027,8 +2027,6 @@ int prepare_shard(mums_ctx* ctx) {
     // PairwiseMatchFinder context would silently get MemHash's MatchList
     if (ctx->pcompat)
         return fail(ctx, MUMS_E_UNSUPPORTED, "sharded mode: ParallelMemHash compat runs single-GPU only");
-    if (ctx->pairwise)
-        return fail(ctx, MUMS_E_UNSUPPORTED, "sharded mode: PairwiseMatchFinder runs single-GPU only");
     if (2 * ctx->w + 1 > 32 + kMaxMsdBits)
         return fail(ctx, MUMS_E_UNSUPPORTED, "sharded mode needs 2w+1 <= 43 (packed records)");
     GenomeTable& l = ctx->lgt;
@@ -3067,32 +3065,41 @@ int shard_groups_chunked(mums_ctx* ctx, uint64_t* rec, const std::vector<uint32_
 
 // the sharded FindMatches reads its probe rows from ctx->rowsall (built once per merge /
 // restart) for a chunked merge and under enumeration tolerance > 1
-bool shard_rows_from_all(const mums_ctx* ctx) { return ctx->merge_chunked || ctx->enum_tol > 1; }
+bool shard_rows_from_all(const mums_ctx* ctx) { return ctx->merge_chunked || ctx->enum_tol > 1 || ctx->pairwise; }
 
-// Enumeration tolerance > 1 on a sharded rank (MemHash::EnumerateMatches, MemHash.cpp:139-162 ->
+// Enumeration tolerance > 1 (and PairwiseMatchFinder's pairs) on a sharded rank (MemHash::EnumerateMatches, MemHash.cpp:139-162 ->
 // MatchFinder::EnumerateMatches' odometer, MatchFinder.cpp:342-393): one probe row per
 // AddHashEntry call of every group of the rank's key range, in key order (pairwise.hip
 // en_count / en_emit over the records as full-key pairs, the run order already the std::sort
 // order: mums_shard_tie_*).  ctx->P = the rows.
 int shard_enum_rows(mums_ctx* ctx, hipStream_t st) {
-    if (ctx->rec_ib != 32)
-        return fail(ctx, MUMS_E_UNSUPPORTED, "sharded enumeration tolerance > 1 above 2^32 seed-mers (33-bit records)");
     const uint64_t n = ctx->live_n;   // the live stream (after a restart: its live records)
     const int G = ctx->gt.G;
-    const MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, ctx->masked, ctx->seq_mask};
+    const bool pw = ctx->pairwise;    // PairwiseMatchFinder (PairwiseMatchFinder.cpp:37-73): pair rows
+    const MatchParams mp{ctx->repeat_tol, ctx->enum_tol, ctx->table_size, pw ? 0 : ctx->masked, pw ? 0 : ctx->seq_mask};
     DevCounters* dc = ctx->counters.as<DevCounters>();
     const uint32_t nb = (uint32_t)ctx->live_bst.size() - 1;
+    const bool ib33 = ctx->rec_ib == 33;   // above 2^32 seed-mers: 64-bit indices
     HIPCHK(ctx->ckey.ensure(n * 8 + 64));
-    HIPCHK(ctx->cval.ensure(2 * (n + 64) * 4 + (uint64_t)(nb + 1) * 4));
+    HIPCHK(ctx->cval.ensure((ib33 ? 3 : 2) * (n + 64) * 4 + (uint64_t)(nb + 1) * 4));
     uint32_t* idx = ctx->cval.as<uint32_t>();
-    uint32_t* ncalls = idx + n + 64;
+    uint32_t* ncalls = idx + (ib33 ? 2 : 1) * (n + 64);
     uint32_t* d_bst = ncalls + n + 64;
     HIPCHK(hipMemcpyAsync(d_bst, ctx->live_bst.data(), (uint64_t)(nb + 1) * 4, hipMemcpyHostToDevice, st));
-    HIPCHK(launch_rec_pairs(ctx->sorted_rec, n, d_bst, nb, ctx->shard_kfirst, 2 * ctx->w + 1 - ctx->msd_bits,
-                            ctx->ckey.as<uint64_t>(), idx, st));
+    const int kb_rec = 2 * ctx->w + 1 - ctx->msd_bits;
+    if (ib33)
+        HIPCHK(launch_rec_pairs33(ctx->sorted_rec, n, d_bst, nb, ctx->shard_kfirst, kb_rec, ctx->ckey.as<uint64_t>(),
+                                  (uint64_t*)idx, st));
+    else
+        HIPCHK(launch_rec_pairs(ctx->sorted_rec, n, d_bst, nb, ctx->shard_kfirst, kb_rec, ctx->ckey.as<uint64_t>(), idx,
+                                st));
     const PairView<uint64_t> v{ctx->ckey.as<uint64_t>(), idx};
+    const PairView<uint64_t, uint64_t> v64{ctx->ckey.as<uint64_t>(), (const uint64_t*)idx};
     HIPCHK(hipMemsetAsync(&dc->repeat_limit, 0, 8, st));
-    HIPCHK(launch_enum_count<PairView<uint64_t>>(v, n, ctx->gt, mp, ncalls, dc, st));
+    if (pw && ib33) HIPCHK(launch_pairwise_count(v64, n, ctx->gt, ncalls, dc, st));
+    else if (pw) HIPCHK(launch_pairwise_count(v, n, ctx->gt, ncalls, dc, st));
+    else if (ib33) HIPCHK(launch_enum_count(v64, n, ctx->gt, mp, ncalls, dc, st));
+    else HIPCHK(launch_enum_count(v, n, ctx->gt, mp, ncalls, dc, st));
     HIPCHK(ctx->tmp.ensure(std::max(ctx->tmp.cap, scan_tmp_bytes(n + 1))));
     uint32_t* total = &dc->nprobes;
     HIPCHK(ctx->rowtmp.ensure((n + 64) * 4 + 4096));
@@ -3103,7 +3110,11 @@ int shard_enum_rows(mums_ctx* ctx, hipStream_t st) {
     HIPCHK(hipMemcpyAsync(&P, total, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     HIPCHK(ctx->rowsall.ensure(((uint64_t)P + 1) * (G + 1) * 8));
-    HIPCHK(launch_enum_emit<PairView<uint64_t>>(v, n, ctx->gt, mp, ctx->L, ncalls, off, ctx->rowsall.as<int64_t>(), st));
+    int64_t* rows = ctx->rowsall.as<int64_t>();
+    if (pw && ib33) HIPCHK(launch_pairwise_emit(v64, n, ctx->gt, ctx->L, ncalls, off, rows, st));
+    else if (pw) HIPCHK(launch_pairwise_emit(v, n, ctx->gt, ctx->L, ncalls, off, rows, st));
+    else if (ib33) HIPCHK(launch_enum_emit(v64, n, ctx->gt, mp, ctx->L, ncalls, off, rows, st));
+    else HIPCHK(launch_enum_emit(v, n, ctx->gt, mp, ctx->L, ncalls, off, rows, st));
     HIPCHK(hipStreamSynchronize(st));
     ctx->P = P;
     ctx->st.probes = P;
@@ -3114,7 +3125,7 @@ int shard_enum_rows(mums_ctx* ctx, hipStream_t st) {
 // a chunked merge's probe rows for the sharded FindMatches (once per merge / restart)
 int shard_chunk_rows(mums_ctx* ctx, hipStream_t st) {
     if (!shard_rows_from_all(ctx) || ctx->shard_rows_built) return MUMS_OK;
-    if (ctx->enum_tol > 1) return shard_enum_rows(ctx, st);
+    if (ctx->enum_tol > 1 || ctx->pairwise) return shard_enum_rows(ctx, st);
     ProbeSpace ps{};
     int rc = ensure_probe_space(ctx, ctx->shard_n, seg_tiles_upper(ctx->shard_n, ctx->shard_mb), &ps);
     if (rc) return rc;

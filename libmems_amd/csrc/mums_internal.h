@@ -307,6 +307,9 @@ hipError_t launch_gather_rows(const int64_t* src, const uint32_t* perm, uint64_t
 // 32-bit index) pairs for the group scans of pairwise.hip
 hipError_t launch_rec_pairs(const uint64_t* rec, uint64_t n, const uint32_t* d_bst, uint32_t nb, uint32_t kfirst,
                             int kb_rec, uint64_t* key, uint32_t* idx, hipStream_t st);
+// the same for 33-bit records (above 2^32 seed-mers): 64-bit indices
+hipError_t launch_rec_pairs33(const uint64_t* rec, uint64_t n, const uint32_t* d_bst, uint32_t nb, uint32_t kfirst,
+                              int kb_rec, uint64_t* key, uint64_t* idx, hipStream_t st);
 hipError_t launch_chain_dest(const uint32_t* fk, uint64_t nch, const uint32_t* pdest, uint32_t* cdest, hipStream_t st);
 hipError_t launch_inverse_perm(const uint32_t* perm, uint64_t n, uint32_t* inv, hipStream_t st);
 hipError_t launch_chain_tags(const uint32_t* chain_of, const uint32_t* perm, const uint32_t* sdest, uint64_t P,

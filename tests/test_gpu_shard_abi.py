@@ -78,33 +78,41 @@ def test_shard_run_ib33_wide_seeds(gpu_lib, oracle_mod, G, n, w, p, world, layou
     run(gpu_lib, oracle_mod, G, n, w, p, world, "local", layout=layout)
 
 
-@pytest.mark.parametrize("mode", ["pairwise"])
-def test_shard_run_refuses_single_gpu_modes(gpu_lib, oracle_mod, mode):
-    """mums_shard_run builds MemHash's MatchParams: a PairwiseMatchFinder context is refused
-    (MUMS_E_UNSUPPORTED), never answered with MemHash's MatchList.  (ParallelMemHash compat
-    contexts run the chunk-range ranks: tests/test_gpu_compat_ranks.py.)"""
-    import ctypes
-    lib = gpu_lib.load_library()
-    seqs = oracle_mod.generate(2, 20_000, 0.02, 5)
-    comms = (ctypes.c_void_p * 1)()
-    devs = (ctypes.c_int * 1)(0)
-    assert lib.mums_comm_init_local(comms, 1, devs) == gpu_lib.MUMS_OK
-    try:
-        with gpu_lib.MemHash(0) as mh:
-            mh.SetSeed(oracle_mod.get_seed(15))
-            for s in seqs:
-                mh.AddSequence(s)
-            if mode == "parallel_compat":
-                mh._check(lib.mums_set_parallel_compat(mh._ctx, 1, 3000))
-            else:
-                mh._check(lib.mums_set_pairwise(mh._ctx, 1))
-            lens = (ctypes.c_uint64 * 2)(*[len(s) for s in seqs])
-            mh._check(lib.mums_shard_layout(mh._ctx, 2, 0, lens))
-            rc = lib.mums_shard_run(mh._ctx, comms[0], gpu_lib.STAGE_ALL)
-            assert rc == gpu_lib.MUMS_E_UNSUPPORTED
-            assert "single-GPU" in lib.mums_last_error(mh._ctx).decode()
-    finally:
-        lib.mums_comm_destroy(comms[0])
+@pytest.mark.parametrize("G,n,w,p,world,layout,ib33", [(4, 200_000, 15, 0.03, 2, "blocks", False),
+                                                       (5, 120_000, 17, 0.02, 3, "blocks", False),
+                                                       (2, 200_000, 19, 0.02, 4, "slices", False),
+                                                       (3, 150_000, 21, 0.02, 3, "slices", True),
+                                                       (4, 100_000, 20, 0.03, 2, "blocks", True)])
+def test_shard_run_pairwise(gpu_lib, oracle_mod, G, n, w, p, world, layout, ib33, monkeypatch):
+    """PairwiseMatchFinder over ranks (PairwiseMatchFinder.cpp:37-73): every rank writes the pair
+    rows of its key range's groups (mums_capi.hip shard_enum_rows), the owners replay them as for
+    MemHash.  33-bit records forced small with MUMS_DEV_SHARD_IB33.  MatchList and collisions =
+    the oracle's PairwiseMatchFinder."""
+    if ib33:
+        monkeypatch.setenv("MUMS_DEV_SHARD_IB33", "1")
+    seqs = oracle_mod.generate(G, n, p, 700 + G * 13 + world)
+    seed = oracle_mod.get_seed(w)
+    lengths, starts, st = oracle_mod.find_matches(seqs, seed, pairwise=True)
+    with gpu_lib.ShardedMemHash([0] * world, comm="local", layout=layout, pairwise=True) as sh:
+        sh.SetSeed(seed)
+        ml = sh.FindMatches(seqs)
+        coll = sum(s["collision_count"] for s in sh.stats_per_rank)
+    assert len(ml) == len(lengths)
+    assert np.array_equal(ml.lengths, lengths) and np.array_equal(ml.starts, starts)
+    assert coll == st["collision_count"]
+
+
+def test_shard_run_pairwise_repeats(gpu_lib, oracle_mod):
+    from tests import repeat_inputs
+    seqs = repeat_inputs.high_copy(G=4, n=50_000, copies=30, tandem=False, seed=7)
+    seed = oracle_mod.get_seed(15)
+    lengths, starts, st = oracle_mod.find_matches(seqs, seed, pairwise=True)
+    with gpu_lib.ShardedMemHash([0] * 3, comm="local", pairwise=True) as sh:
+        sh.SetSeed(seed)
+        ml = sh.FindMatches(seqs)
+        coll = sum(s["collision_count"] for s in sh.stats_per_rank)
+    assert np.array_equal(ml.lengths, lengths) and np.array_equal(ml.starts, starts)
+    assert coll == st["collision_count"]
 
 
 def test_shard_chains_labelled_where_the_probes_are(gpu_lib, oracle_mod):

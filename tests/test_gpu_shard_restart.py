@@ -287,6 +287,17 @@ def test_enumeration_tolerance_repeats(gpu_lib, oracle_mod, etol, rtol):
     check(gpu_lib, oracle_mod, seqs, 3, repeat_tol=rtol, enum_tol=etol)
 
 
+@pytest.mark.parametrize("etol,rtol,w,layout", [(2, 1, 19, "blocks"), (3, 39, 19, "slices"), (12, 39, 21, "slices"),
+                                                (2, 2, 20, "blocks")])
+def test_enumeration_tolerance_ib33(gpu_lib, oracle_mod, monkeypatch, etol, rtol, w, layout):
+    """Above 2^32 seed-mers (forced small: MUMS_DEV_SHARD_IB33) the ranks' merged records carry
+    33-bit indices: the enumeration rows come from (full key, 64-bit index) pairs
+    (groups.hip launch_rec_pairs33, mums_capi.hip shard_enum_rows)."""
+    monkeypatch.setenv("MUMS_DEV_SHARD_IB33", "1")
+    seqs = repeat_inputs.high_copy(G=3, n=60_000, copies=40, tandem=False, seed=etol + w)
+    check(gpu_lib, oracle_mod, seqs, 3, w=w, layout=layout, repeat_tol=rtol, enum_tol=etol)
+
+
 def test_enumeration_tolerance_with_restarts(gpu_lib, oracle_mod):
     seqs = repeat_inputs.n_gapped(G=3, n=200_000, gaps=((40_000, 3000), (120_000, 3000)), shift=500, seed=1)
     ref = check(gpu_lib, oracle_mod, seqs, 2, repeat_tol=1, enum_tol=2)
