@@ -496,6 +496,9 @@ public:
     // rank searches a contiguous range of the chunks, the bucket owners re-add the ranks' tables
     // rank after rank (genome blocks only)
     void SetParallelCompat(bool enable, uint64_t chunk_size = 200000) { compat_chunk_ = enable ? chunk_size : 0; }
+    // PairwiseMatchFinder's MatchList (PairwiseMatchFinder.cpp:37-73): every rank writes the pair
+    // rows of its key range's groups (shard_enum_rows)
+    void SetPairwise(bool enable) { pairwise_ = enable; }
     bool AddSequence(const std::string& seq) {
         seqs_.push_back(seq);
         return true;
@@ -557,6 +560,9 @@ public:
             for (auto& mh : ranks_)
                 if (mums_set_parallel_compat(mh->handle(), 1, compat_chunk_) != MUMS_OK)
                     throw InvalidData(mums_last_error(mh->handle()));
+        if (pairwise_)
+            for (auto& mh : ranks_)
+                if (mums_set_pairwise(mh->handle(), 1) != MUMS_OK) throw InvalidData(mums_last_error(mh->handle()));
         if (!start_points_.empty())
             for (auto& mh : ranks_)
                 if (mums_set_start_points(mh->handle(), start_points_.data(), (uint32_t)start_points_.size()) != MUMS_OK)
@@ -589,6 +595,7 @@ private:
     uint32_t table_size_ = 40000;
     uint32_t repeat_tol_ = 0, enum_tol_ = 1;
     uint64_t compat_chunk_ = 0;   // ParallelMemHash compat: CHUNK_SIZE (0: MemHash)
+    bool pairwise_ = false;
     std::vector<uint64_t> start_points_;
 };
 

@@ -620,6 +620,7 @@ class ShardedMemHash:
         self.repeat_tol = 0
         self.enum_tol = 1
         self.progress = False
+        self.match_log = False
         self.seqs: List[bytes] = []
         self.ranks: List[MemHash] = []
         self.stats_per_rank: List[dict] = []
@@ -650,6 +651,23 @@ class ShardedMemHash:
         """MatchFinder::LogProgress (MatchFinder.cpp:55-56) over the ranks: the text of the whole
         merge, restated on rank 0 (the restart is then planned on the gathered streams)."""
         self.progress = bool(enable)
+
+    def SetMatchLog(self, enable: bool = True) -> None:
+        """MemHash::SetMatchLog (MemHash.h:149; written at MemHash.cpp:238-241) under ParallelMemHash
+        compat over the ranks: rank 0 restates the one-thread log with the one-context compat
+        search (each chunk's thread inserts depend on every earlier chunk's entries,
+        ParallelMemHash.cpp:117); MatchLog() joins the ranks' parts in rank order."""
+        if enable and not self.parallel_compat:
+            raise ValueError("ShardedMemHash: the match log needs parallel_compat=True")
+        self.match_log = bool(enable)
+
+    def MatchLog(self) -> MatchList:
+        parts = [mh.MatchLog() for mh in self.ranks]
+        G = len(self.seqs)
+        if not parts:
+            return MatchList(np.zeros(0, dtype=np.uint64), np.zeros((0, G), dtype=np.int64))
+        return MatchList(np.concatenate([p.lengths for p in parts]),
+                         np.concatenate([p.starts.reshape(-1, G) for p in parts]))
 
     def ProgressLog(self) -> str:
         return self.ranks[0].ProgressLog() if self.ranks else ""
@@ -716,6 +734,8 @@ class ShardedMemHash:
                 mh._check(self._lib.mums_set_parallel_compat(mh._ctx, 1, self.chunk_size))
             if self.pairwise:
                 mh._check(self._lib.mums_set_pairwise(mh._ctx, 1))
+            if self.match_log:
+                mh.SetMatchLog(True)
         sp = getattr(self, "_start_points", None)
         if sp is not None:
             for mh in self.ranks:

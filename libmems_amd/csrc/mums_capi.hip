@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -181,6 +182,11 @@ struct mums_ctx {
     std::vector<uint64_t> consumed_log;   // consumed SML positions at every restart (R x G, restart plan)
     std::vector<uint32_t> compat_pfirst;  // compat + match log: first probe of every chunk (nch + 1)
     std::vector<uint32_t> log_ids;        // compat + match log: the logged entries (pool ids) in log order
+    // compat ranks: the one-thread log made on rank 0 (ctx_compat_rank_find); mums_match_log_copy
+    // reads these when log_host is set
+    bool log_host = false;
+    std::vector<uint64_t> log_hlen;
+    std::vector<int64_t> log_hs;
     std::vector<uint64_t> compat_cons;    // compat: consumed SML positions of every chunk cut by MER_REPEAT_LIMIT
     const uint64_t* compat_ck_src = nullptr;   // compat: crall not built yet, derive it from these SML keys
     uint64_t compat_ck_mask = 0;
@@ -1455,6 +1461,7 @@ int prepare_run(mums_ctx* ctx, const std::vector<uint64_t>& lens) {
     ctx->tie_slots = 0;
     ctx->restarts = 0;
     ctx->offset_log.clear();
+    ctx->log_host = false;
     ctx->M = ctx->P = 0;
     const int G = (int)lens.size();
     uint64_t total = 0;
@@ -2027,6 +2034,8 @@ int prepare_shard(mums_ctx* ctx) {
     // PairwiseMatchFinder context would silently get MemHash's MatchList
     if (ctx->pcompat)
         return fail(ctx, MUMS_E_UNSUPPORTED, "sharded mode: ParallelMemHash compat runs single-GPU only");
+    if (ctx->match_log)   // (compat contexts: ctx_compat_rank_find)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "sharded MemHash: no match log (ParallelMemHash compat ranks only)");
     if (2 * ctx->w + 1 > 32 + kMaxMsdBits)
         return fail(ctx, MUMS_E_UNSUPPORTED, "sharded mode needs 2w+1 <= 43 (packed records)");
     GenomeTable& l = ctx->lgt;
@@ -2591,9 +2600,6 @@ int mums::ctx_compat_layout(mums_ctx* ctx, uint32_t* first, uint32_t* nown, std:
         return fail(ctx, MUMS_E_UNSUPPORTED, "sharded ParallelMemHash compat: genome blocks only (no position slices)");
     if (ctx->pairwise || ctx->enum_tol > 1)
         return fail(ctx, MUMS_E_UNSUPPORTED, "ParallelMemHash compat with PairwiseMatchFinder / enumeration tolerance > 1");
-    if (ctx->match_log)
-        return fail(ctx, MUMS_E_UNSUPPORTED, "sharded ParallelMemHash compat: no match log (the ranks' merge order "
-                                             "is not the one-thread schedule's)");
     if (!ctx->start_points.empty())
         return fail(ctx, MUMS_E_UNSUPPORTED, "start points (FindMatchesFromPosition) in the ParallelMemHash compat mode");
     const uint32_t nl = (uint32_t)ctx->genomes.size();
@@ -2644,6 +2650,43 @@ int mums::ctx_compat_rank_find(mums_ctx* ctx, const char* const* d_ascii, const 
     ctx->nchunks = sub->nchunks;
     ctx->M = 0;
     ctx->stage_done = MUMS_STAGE_SEEDS;   // the MatchList: after the owners' merge
+    ctx->log_host = ctx->match_log;
+    ctx->log_n = 0;
+    ctx->log_hlen.clear();
+    ctx->log_hs.clear();
+    // SetMatchLog (MemHash.cpp:238-241) over the ranks: the log is the one-thread schedule's --
+    // each chunk's thread-table inserts against the WHOLE global table before it (the thread table
+    // is a copy of it after every MergeTable, ParallelMemHash.cpp:117) -- which a rank that
+    // searched its chunks from its own earlier chunks only does not have (with long bucket vectors
+    // a seed finds, or misses, an earlier rank's entry around its lower_bound).  Rank 0 holds
+    // every genome (the all-gather above), so it restates the log with the one-context compat
+    // search; the other ranks' parts are empty and the ranks' MatchList is unchanged.
+    if (ctx->match_log && rank == 0 && stage >= MUMS_STAGE_ALL) {
+        mums_ctx* lc = nullptr;
+        int r2 = mums_ctx_create(ctx->device, &lc);
+        if (r2) return fail(ctx, r2, "compat match log context");
+        std::unique_ptr<mums_ctx, int (*)(mums_ctx*)> hold(lc, mums_ctx_destroy);
+        if (mums_set_stream(lc, ctx->stream)) return fail(ctx, MUMS_E_HIP, "compat match log context stream");
+        lc->seed = ctx->seed;
+        lc->repeat_tol = ctx->repeat_tol;
+        lc->enum_tol = ctx->enum_tol;
+        lc->table_size = ctx->table_size;
+        lc->masked = ctx->masked;
+        lc->seq_mask = ctx->seq_mask;
+        lc->pcompat = true;
+        lc->chunk_size = ctx->chunk_size;
+        lc->match_log = true;
+        for (int g = 0; g < G; ++g)
+            if (mums_add_genome_device(lc, d_ascii[g], lens[g])) return fail(ctx, MUMS_E_INVALID, lc->err);
+        if ((r2 = mums_find_stage(lc, MUMS_STAGE_ALL))) return fail(ctx, r2, lc->err);
+        uint64_t n = 0;
+        if ((r2 = mums_match_log_copy(lc, nullptr, nullptr, 0, &n))) return fail(ctx, r2, lc->err);
+        ctx->log_hlen.resize(n);
+        ctx->log_hs.resize(n * (uint64_t)G);
+        if (n && (r2 = mums_match_log_copy(lc, ctx->log_hlen.data(), ctx->log_hs.data(), n, &n)))
+            return fail(ctx, r2, lc->err);
+        ctx->log_n = n;
+    }
     return MUMS_OK;
 }
 
@@ -2793,8 +2836,15 @@ int mums_match_log_copy(mums_ctx* ctx, uint64_t* lengths, int64_t* starts, uint6
     if (!lengths && !starts) return MUMS_OK;
     if (capacity < ctx->log_n) return fail(ctx, MUMS_E_INVALID, "match log capacity too small");
     if (ctx->log_n == 0) return MUMS_OK;
-    HIPCHK(hipSetDevice(ctx->device));
     const int G = ctx->gt.G;
+    if (ctx->log_host) {   // a compat rank's log (ctx_compat_rank_find)
+        for (uint64_t i = 0; i < ctx->log_n; ++i) {
+            if (lengths) lengths[i] = ctx->log_hlen[i];
+            if (starts) std::copy(&ctx->log_hs[i * (uint64_t)G], &ctx->log_hs[(i + 1) * (uint64_t)G], starts + i * (uint64_t)G);
+        }
+        return MUMS_OK;
+    }
+    HIPCHK(hipSetDevice(ctx->device));
     std::vector<uint32_t> ids(ctx->log_n);   // pool entries of the inserted chains, in log order
     if (ctx->pcompat) {
         ids = ctx->log_ids;
