@@ -3115,6 +3115,8 @@ int shard_groups_chunked(mums_ctx* ctx, uint64_t* rec, const std::vector<uint32_
 
 // the sharded FindMatches reads its probe rows from ctx->rowsall (built once per merge /
 // restart) for a chunked merge and under enumeration tolerance > 1
+int enum_count_check(mums_ctx* ctx, hipStream_t st);   // (after sort_row_keys below)
+
 bool shard_rows_from_all(const mums_ctx* ctx) { return ctx->merge_chunked || ctx->enum_tol > 1 || ctx->pairwise; }
 
 // Enumeration tolerance > 1 (and PairwiseMatchFinder's pairs) on a sharded rank (MemHash::EnumerateMatches, MemHash.cpp:139-162 ->
@@ -3159,6 +3161,7 @@ int shard_enum_rows(mums_ctx* ctx, hipStream_t st) {
     uint32_t P = 0;
     HIPCHK(hipMemcpyAsync(&P, total, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    if (int rc = enum_count_check(ctx, st)) return rc;
     HIPCHK(ctx->rowsall.ensure(((uint64_t)P + 1) * (G + 1) * 8));
     int64_t* rows = ctx->rowsall.as<int64_t>();
     if (pw && ib33) HIPCHK(launch_pairwise_emit(v64, n, ctx->gt, ctx->L, ncalls, off, rows, st));
@@ -4108,6 +4111,17 @@ int sort_row_keys(mums_ctx* ctx, uint32_t* keys, uint64_t P, int bits, hipStream
     return MUMS_OK;
 }
 
+// after an enumeration count (pairwise.hip en_rows32): a group with more than 2^31
+// AddHashEntry calls (enum_tol^genomes) does not fit the row stream
+int enum_count_check(mums_ctx* ctx, hipStream_t st) {
+    uint32_t err = 0;
+    HIPCHK(hipMemcpyAsync(&err, &ctx->counters.as<DevCounters>()->err, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (err & 64u)
+        return fail(ctx, MUMS_E_UNSUPPORTED, "enumeration tolerance: a seed group with more than 2^31 AddHashEntry calls");
+    return MUMS_OK;
+}
+
 // PairwiseMatchFinder::FindMatches (PairwiseMatchFinder.cpp:37-73 over MemHash): pair
 // path keys + sort, one probe row per single-copy genome pair of every group
 // (pairwise.hip), then the rows' buckets and the FindMatches tail.
@@ -4126,6 +4140,7 @@ int pairwise_rows(mums_ctx* ctx, uint64_t N, hipStream_t st) {
     uint32_t P = 0;
     HIPCHK(hipMemcpyAsync(&P, &dc->nprobes, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    if (int rc = enum_count_check(ctx, st)) return rc;
     ctx->P = P;
     HIPCHK(ctx->mprobe.ensure(((uint64_t)P + 1) * (size_t)(ctx->gt.G + 1) * 8));
     if (ctx->pairwise)
@@ -5175,6 +5190,7 @@ int run_pipeline_chunked(mums_ctx* ctx, int stage) {
                 HIPCHK(exclusive_scan_u32(off, n_c, ctx->tmp.p, &dc->nprobes, st));
                 HIPCHK(hipMemcpyAsync(&pc32, &dc->nprobes, 4, hipMemcpyDeviceToHost, st));
                 HIPCHK(hipStreamSynchronize(st));
+                if ((rc = enum_count_check(ctx, st))) return rc;
             }
             const uint64_t Pc = pc32;
             if (stage >= MUMS_STAGE_ALL && Pc) {

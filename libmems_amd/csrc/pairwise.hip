@@ -144,13 +144,13 @@ __device__ bool en_collect(const View& v, uint64_t h, uint64_t N, const GenomeTa
 // genome), or the single HashMatch of a two-record list; HashMatch / MaskedMemHash::
 // HashMatch decide whether each combination is added (same genome set for all of them).
 template <int MG>
-__device__ __forceinline__ uint32_t en_calls(const uint32_t (&c)[MG], int G, const MatchParams& mp, bool* two) {
-    uint32_t total = 0, nid = 0, combos = 1;
+__device__ __forceinline__ uint64_t en_calls(const uint32_t (&c)[MG], int G, const MatchParams& mp, bool* two) {
+    uint64_t total = 0, nid = 0, combos = 1;
     uint64_t mn = 0;
     for (int g = 0; g < G; ++g) {
         total += c[g];
         mn <<= 1;
-        if (c[g]) { ++nid; combos *= c[g]; mn |= 1; }
+        if (c[g]) { ++nid; combos = combos > (1ull << 32) ? combos : combos * c[g]; mn |= 1; }
     }
     *two = total == 2;
     if (total < 2) return 0;
@@ -158,6 +158,14 @@ __device__ __forceinline__ uint32_t en_calls(const uint32_t (&c)[MG], int G, con
     const bool add = mp.masked ? (mp.seq_mask == 0 || mn == mp.seq_mask) : nid >= 2;
     if (!add) return 0;
     return (total == 2) ? 1u : combos;
+}
+
+// a group's AddHashEntry calls as a 32-bit row count; above 2^31 (enum_tol^genomes) the row
+// stream cannot hold them: DevCounters::err bit 64, the host refuses the find
+__device__ __forceinline__ uint32_t en_rows32(uint64_t k, DevCounters* ctr) {
+    if (k <= 0x7FFFFFFFull) return (uint32_t)k;
+    atomicOr(&ctr->err, 64u);
+    return 0;
 }
 
 template <int MG, typename View>
@@ -172,7 +180,7 @@ __global__ void en_count_kernel(View v, uint64_t N, GenomeTable gt, MatchParams 
         const bool ok = en_collect<MG>(v, i, N, gt, mp, c, pos, par, &size);
         if (size > (uint32_t)kRepeatLimit) atomicAdd(&ctr->repeat_limit, 1ull);
         bool two;
-        if (ok && size >= 2) k = en_calls<MG>(c, gt.G, mp, &two);
+        if (ok && size >= 2) k = en_rows32(en_calls<MG>(c, gt.G, mp, &two), ctr);
     }
     ncalls[i] = k;
 }
@@ -188,9 +196,9 @@ __global__ void en_emit_kernel(View v, uint64_t N, GenomeTable gt, MatchParams m
     uint8_t par[MG][kEnumMax];
     (void)en_collect<MG>(v, i, N, gt, mp, c, pos, par, &size);
     bool two;
-    const uint32_t K = en_calls<MG>(c, G, mp, &two);
+    const uint64_t K = en_calls<MG>(c, G, mp, &two);
     uint64_t o = off[i];
-    for (uint32_t t = 0; t < K; ++t) {
+    for (uint64_t t = 0; t < K; ++t) {
         int64_t sv[MG];
         uint32_t pv[MG];
         for (int g = 0; g < G; ++g) { sv[g] = 0; pv[g] = 0; }
@@ -198,10 +206,10 @@ __global__ void en_emit_kernel(View v, uint64_t N, GenomeTable gt, MatchParams m
             for (int g = 0; g < G; ++g)
                 for (uint32_t q = 0; q < c[g]; ++q) { sv[g] = (int64_t)pos[g][q] + 1; pv[g] = par[g][q]; }
         } else {     // odometer: the last genome varies fastest (MatchFinder.cpp:371-390)
-            uint32_t rem = t;
+            uint64_t rem = t;
             for (int g = G - 1; g >= 0; --g) {
                 if (!c[g]) continue;
-                const uint32_t q = rem % c[g];
+                const uint32_t q = (uint32_t)(rem % c[g]);
                 rem /= c[g];
                 sv[g] = (int64_t)pos[g][q] + 1;
                 pv[g] = par[g][q];
@@ -260,7 +268,7 @@ __global__ void en_count_walk_kernel(View v, uint64_t N, GenomeTable gt, MatchPa
         const bool ok = en_tally<MG>(v, i, N, gt, mp, c, &size);
         if (size > (uint32_t)kRepeatLimit) atomicAdd(&ctr->repeat_limit, 1ull);
         bool two;
-        if (ok && size >= 2) k = en_calls<MG>(c, gt.G, mp, &two);
+        if (ok && size >= 2) k = en_rows32(en_calls<MG>(c, gt.G, mp, &two), ctr);
     }
     ncalls[i] = k;
 }
@@ -275,19 +283,19 @@ __global__ void en_emit_walk_kernel(View v, uint64_t N, GenomeTable gt, MatchPar
     uint32_t c[MG], size = 0;
     (void)en_tally<MG>(v, i, N, gt, mp, c, &size);
     bool two;
-    const uint32_t K = en_calls<MG>(c, G, mp, &two);
+    const uint64_t K = en_calls<MG>(c, G, mp, &two);
     const uint64_t k0 = v.gkey(i);
     uint64_t o = off[i];
-    for (uint32_t t = 0; t < K; ++t) {
+    for (uint64_t t = 0; t < K; ++t) {
         uint32_t q[MG];   // the record of each genome this combination takes (two: every kept one)
         int64_t sv[MG];
         uint32_t pv[MG];
         for (int g = 0; g < G; ++g) { sv[g] = 0; pv[g] = 0; q[g] = 0; }
         if (!two) {   // odometer: the last genome varies fastest (MatchFinder.cpp:371-390)
-            uint32_t rem = t;
+            uint64_t rem = t;
             for (int g = G - 1; g >= 0; --g) {
                 if (!c[g]) continue;
-                q[g] = rem % c[g];
+                q[g] = (uint32_t)(rem % c[g]);
                 rem /= c[g];
             }
         }

@@ -63,3 +63,16 @@ def test_enumeration_tolerance_above_slot_bound(gpu_lib, oracle_mod, et, rt, G, 
     assert st["collision_count"] == ost["collision_count"]
     assert len(ml) == len(lengths)
     assert (ml.lengths == lengths).all() and (ml.starts == starts).all()
+
+
+def test_enumeration_calls_above_row_stream_refused(gpu_lib, oracle_mod):
+    """8 genomes with ~20 copies of one element each under enum_tol 20: a group's odometer has
+    ~20^8 > 2^31 AddHashEntry calls, more than the row stream holds -- refused
+    (MUMS_E_UNSUPPORTED, pairwise.hip en_rows32), never a wrapped row count."""
+    seqs = repeat_inputs.high_copy(G=8, n=30_000, copies=20, tandem=False, seed=3)
+    with gpu_lib.MemHash(0) as mh:
+        mh.SetSeed(oracle_mod.get_seed(15))
+        mh.SetRepeatTolerance(40)
+        mh.SetEnumerationTolerance(20)
+        with pytest.raises(gpu_lib.MumsError, match="2\\^31"):
+            mh.FindMatches(seqs)
