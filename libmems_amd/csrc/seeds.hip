@@ -18,6 +18,7 @@
 //                        wave64 ballot match-any, reorders through LDS and writes
 //                        (ckey_low << 32 | index) records into their buckets.
 // HBM bytes per seed-mer: pack 1 + 0.25 (packed path) ; scatter 0.25 + 8.
+#include <cstdlib>
 #include <type_traits>
 
 #include "seed_device.h"
@@ -59,11 +60,14 @@ template <int kMode, typename K, uint64_t PAT = 0>
 __global__ __launch_bounds__(kBlock) void seed_pack_kernel(SeedSpec ss, GenomeTable gt, AsciiPtrs ap,
                                                            uint32_t* __restrict__ packed, K* __restrict__ ckey,
                                                            int msd_bits, uint32_t* __restrict__ hist, uint32_t T,
-                                                           uint32_t* __restrict__ err) {
+                                                           uint32_t* __restrict__ err, int swz) {
     __shared__ uint8_t bytes[kTileBytes + 16];
     __shared__ uint32_t words[kTileWords];
     __shared__ uint32_t bh[1 << kMaxMsdBits];
-    const uint32_t t = blockIdx.x;
+    // XCD-grouped tiles (as the scatter below): the digit-major histogram columns hist[i * T + t]
+    // of neighbouring tiles share cache lines, which merge in one XCD's L2 instead of reaching
+    // HBM as 4-B partial lines from eight L2s
+    const uint32_t t = swz ? xcd_grouped_block(blockIdx.x, gridDim.x) : blockIdx.x;
     const int g = tile_genome(gt, t);
     const uint32_t x = t - gt.tfirst[g];
     const uint64_t n = gt.n[g];
@@ -414,18 +418,19 @@ hipError_t launch_seed_pack(const SeedSpec& ss, const GenomeTable& gt, const cha
     AsciiPtrs ap{};
     for (int g = 0; g < gt.G; ++g) ap.p[g] = d_ascii[g];
     if (ntiles == 0) return hipSuccess;
+    const int swz = getenv("MUMS_DEV_PACK_LINEAR") ? 0 : 1;   // (development A/B, read per call)
     if (mode == 0) {
         if (key64)
             hipLaunchKernelGGL((seed_pack_kernel<0, uint64_t>), dim3(ntiles), dim3(kBlock), 0, st, ss, gt, ap,
-                               d_packed, (uint64_t*)d_ckey, 0, d_hist, ntiles, d_err);
+                               d_packed, (uint64_t*)d_ckey, 0, d_hist, ntiles, d_err, swz);
         else
             hipLaunchKernelGGL((seed_pack_kernel<0, uint32_t>), dim3(ntiles), dim3(kBlock), 0, st, ss, gt, ap,
-                               d_packed, (uint32_t*)d_ckey, 0, d_hist, ntiles, d_err);
+                               d_packed, (uint32_t*)d_ckey, 0, d_hist, ntiles, d_err, swz);
     } else {
         with_static_seed(ss.pattern, [&](auto pc) {
             constexpr uint64_t PAT = decltype(pc)::value;
             hipLaunchKernelGGL((seed_pack_kernel<1, uint64_t, PAT>), dim3(ntiles), dim3(kBlock), 0, st, ss, gt, ap,
-                               d_packed, (uint64_t*)nullptr, msd_bits, d_hist, ntiles, d_err);
+                               d_packed, (uint64_t*)nullptr, msd_bits, d_hist, ntiles, d_err, swz);
         });
     }
     return hipGetLastError();
