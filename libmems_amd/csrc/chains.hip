@@ -1322,7 +1322,9 @@ hipError_t chains_core(LV vl, const ChainWs& w, const uint32_t* ord, uint64_t P,
     const bool wsort_long = wsort && wsort_env[0] == '2';   // and the handed-on walks back in line order
     int pbits = 1;
     while (pbits < 32 && (1ull << pbits) < P) ++pbits;
-    const int wshift = kWalkSortShift;
+    // (MUMS_DEV_WALK_SHIFT, read per call: the granule of that order, development A/B)
+    const char* wsh_env = getenv("MUMS_DEV_WALK_SHIFT");
+    const int wshift = wsh_env ? std::max(0, std::min(31, atoi(wsh_env))) : kWalkSortShift;
     const int wbits = std::max(1, x_bits(gt) - wshift);
     uint32_t* d_err = ctr ? &((DevCounters*)ctr)->err : w.qcount + 14;
     for (int pass = 0; pass < 2; ++pass) {
